@@ -1,0 +1,158 @@
+"""TEST INFRASTRUCTURE ONLY — numpy restatement of the WaveNet MoL vocoder's synthesis path
+(fast-WaveNet incremental generation) of mwhitehill/Tacotron-2 (see ``oracle/__init__.py``:
+parity unpinned, never imported by the product).
+
+Weights are keyed by the canonical TF names from ``tt2.weights.wavenet_weight_specs``
+(prefix ``WaveNet_model/inference/``).
+"""
+import numpy as np
+
+P = "WaveNet_model/inference/"
+SQRT_HALF = np.float32(np.sqrt(0.5))
+
+
+def _w(W, name, dt=np.float32):
+    return np.asarray(W[P + name], dtype=dt)
+
+
+def receptive_field_size(total_layers, num_cycles, kernel_size):
+    """wavenet.py:54-71."""
+    per = total_layers // num_cycles
+    return (kernel_size - 1) * sum(2 ** (i % per) for i in range(total_layers)) + 1
+
+
+def interp_condition(mel, max_abs_value=4.0):
+    """Host-side conditioning prep of wavenet_vocoder/synthesizer.py:63-70: clip to
+    [-max, max] then wavenet_vocoder/feeder.py:426-428 _interp to [0, 1]."""
+    m = np.clip(np.asarray(mel, np.float32), -max_abs_value, max_abs_value)
+    return ((m + np.float32(max_abs_value)) / np.float32(2 * max_abs_value)).astype(np.float32)
+
+
+def upsample_2d(c, W, scales, freq_kernel=3):
+    """ConvTranspose2D stack + ReLU (wavenet.py:171-203, 782-803; modules.py:736-770).
+
+    c [B, F, T_f] (channels_first, expanded to [B,1,F,T]); per scale s a 1→1 channel
+    conv2d_transpose with kernel (freq_kernel, s), strides (1, s), 'same':
+        out[f, i·s + j] = Σ_d in[f + pad − d, i] · K[d, j] + b,  pad = (freq_kernel−1)//2
+    (the adjoint of TF's 'same' correlation), then ReLU.  Returns [B, F, T_f·Πs]."""
+    x = np.asarray(c, np.float32)
+    B, F, _ = x.shape
+    pad = (freq_kernel - 1) // 2
+    for i, s in enumerate(scales):
+        scope = "local_conditioning_upsampling_{}/ConvTranspose2D_layer_{}/".format(i + 1, i)
+        K = _w(W, scope + "kernel")[:, :, 0, 0]   # [freq_kernel, s]
+        b = _w(W, scope + "bias")[0]
+        T = x.shape[-1]
+        out = np.zeros((B, F, T, s), np.float32)
+        for d in range(freq_kernel):
+            sh = pad - d                          # out[f] += in[f + sh] * K[d]
+            src = np.zeros_like(x)
+            if sh >= 0:
+                src[:, :F - sh] = x[:, sh:]
+            else:
+                src[:, -sh:] = x[:, :F + sh]
+            out += src[..., None] * K[d][None, None, None, :]
+        x = np.maximum(out.reshape(B, F, T * s) + b, np.float32(0))
+    return x
+
+
+def mol_sample(logits, u_mix, u_log, log_scale_min):
+    """sample_from_discretized_mix_logistic (mixture.py:76-107) with injected uniforms.
+
+    logits [N, 3·nr_mix]; u_mix [N, nr_mix]; u_log [N].  The Gumbel term log(−log u) and the
+    logistic noise log u − log(1−u) are evaluated in float64 and rounded to float32 (documented
+    build convention, identical on the HIP path) so that the mixture index k is reproducible
+    bit-for-bit across devices.  Returns (x float32 [N], k int32 [N])."""
+    logits = np.asarray(logits, np.float32)
+    nr = logits.shape[1] // 3
+    u_mix = np.asarray(u_mix, np.float32).astype(np.float64)   # the ABI carries fp32 uniforms
+    u_log = np.asarray(u_log, np.float32).astype(np.float64)
+    gl = np.log(-np.log(u_mix)).astype(np.float32)
+    temp = logits[:, :nr] - gl                                  # :92
+    k = np.argmax(temp, axis=1).astype(np.int32)                # :93 (first max)
+    rows = np.arange(logits.shape[0])
+    means = logits[rows, nr + k]                                # :98
+    log_scales = np.maximum(logits[rows, 2 * nr + k], np.float32(log_scale_min))   # :99-100
+    noise = (np.log(u_log) - np.log(1.0 - u_log)).astype(np.float32)
+    x = means + np.exp(log_scales) * noise                      # :105
+    return np.minimum(np.maximum(x, np.float32(-1)), np.float32(1)).astype(np.float32), k
+
+
+def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False):
+    """WaveNet.incremental (wavenet.py:724-911) for scalar ('raw') input and the MoL head.
+
+    c_up: upsampled conditioning [B, T, cin]; u_mix [T, B, nr_mix]; u_log [T, B];
+    test_inputs [B, T] overrides next_input (wavenet.py:876-878).  Returns y [B, T] (float32),
+    k [B, T] (int32) and, optionally, logits [B, T, out_channels]."""
+    c_up = np.asarray(c_up, np.float32)
+    B, T, _ = c_up.shape
+    L, stacks = hp["layers"], hp["stacks"]
+    per = L // stacks
+    R = hp["residual_channels"]
+    legacy, res_legacy = hp.get("legacy", False), hp.get("residual_legacy", False)
+    kw = hp.get("kernel_size", 3)
+    first_k = _w(W, "input_convolution/kernel").reshape(1, R)
+    first_b = _w(W, "input_convolution/bias")
+    layers = []
+    for l in range(L):
+        s = "ResidualConv1DGLU_{}/".format(l)
+        cs = s + "residual_block_causal_conv_ResidualConv1DGLU_{}/".format(l)
+        layers.append(dict(
+            d=2 ** (l % per),
+            k=_w(W, cs + "kernel").reshape(kw * R, -1), b=_w(W, cs + "bias"),
+            kc=_w(W, s + "residual_block_cin_conv_ResidualConv1DGLU_{}/kernel".format(l))[0],
+            bc=_w(W, s + "residual_block_cin_conv_ResidualConv1DGLU_{}/bias".format(l)),
+            ks=_w(W, s + "residual_block_skip_conv_ResidualConv1DGLU_{}/kernel".format(l))[0],
+            bs=_w(W, s + "residual_block_skip_conv_ResidualConv1DGLU_{}/bias".format(l)),
+            ko=_w(W, s + "residual_block_out_conv_ResidualConv1DGLU_{}/kernel".format(l))[0],
+            bo=_w(W, s + "residual_block_out_conv_ResidualConv1DGLU_{}/bias".format(l))))
+    f1k = _w(W, "skip_convolutions/final_convolution_1/kernel")[0]
+    f1b = _w(W, "skip_convolutions/final_convolution_1/bias")
+    f2k = _w(W, "skip_convolutions/final_convolution_2/kernel")[0]
+    f2b = _w(W, "skip_convolutions/final_convolution_2/bias")
+    queues = [np.zeros((B, kw + (kw - 1) * (ly["d"] - 1), R), np.float32) for ly in layers]  # :815
+    cur = np.zeros((B, 1), np.float32)   # initial_input = 0 ('raw'), wavenet.py:437-445
+    ys = np.zeros((B, T), np.float32)
+    ks = np.zeros((B, T), np.int32)
+    lg = np.zeros((B, T, f2b.shape[0]), np.float32) if return_logits else None
+    zero = np.float32(0)
+    for t in range(T):
+        ct = c_up[:, t]
+        x = cur @ first_k + first_b                       # first_conv.incremental_step :826
+        skips = None
+        for ly, q in zip(layers, queues):                 # :830-837
+            residual = x
+            q[:, :-1] = q[:, 1:].copy()                   # modules.py:285-288 shift + append
+            q[:, -1] = x
+            taps = q[:, ::ly["d"]]                        # modules.py:291-292
+            h = taps.reshape(B, -1) @ ly["k"] + ly["b"]   # modules.py:295-297
+            G2 = h.shape[1] // 2
+            cc = ct @ ly["kc"] + ly["bc"]                 # modules.py:497-501
+            a = h[:, :G2] + cc[:, :G2]
+            bgate = h[:, G2:] + cc[:, G2:]
+            z = np.tanh(a) * (1.0 / (1.0 + np.exp(-bgate))).astype(np.float32)   # :510
+            sk = z @ ly["ks"] + ly["bs"]                  # :512
+            x = z @ ly["ko"] + ly["bo"]                   # :515
+            x = (x + residual) * SQRT_HALF if res_legacy else x + residual    # :517-520
+            if skips is None:
+                skips = sk
+            else:
+                skips = (skips + sk) * SQRT_HALF if legacy else skips + sk   # wavenet.py:833-836
+        x = np.maximum(skips, zero) @ f1k + f1b          # :840-844
+        x = np.maximum(x, zero) @ f2k + f2b
+        if lg is not None:
+            lg[:, t] = x
+        y, k = mol_sample(x, u_mix[t], u_log[t], hp["log_scale_min"])
+        ys[:, t] = y
+        ks[:, t] = k
+        cur = y[:, None] if test_inputs is None else np.asarray(test_inputs, np.float32)[:, t:t + 1]
+    return (ys, ks, lg) if return_logits else (ys, ks)
+
+
+def synthesize(mel, W, hp, u_mix, u_log, test_inputs=None, return_logits=False):
+    """wavenet_vocoder/synthesizer.py:46-103 for one batch of equal-length mels [B, T_f, 80]:
+    clip + interp, upsample, incremental generation of T_f·hop samples."""
+    c = interp_condition(mel, hp.get("max_abs_value", 4.0))       # [B, T_f, 80]
+    c_up = upsample_2d(c.transpose(0, 2, 1), W, hp["upsample_scales"],
+                       hp.get("freq_axis_kernel_size", 3))        # [B, 80, T]
+    return incremental(c_up.transpose(0, 2, 1), W, hp, u_mix, u_log, test_inputs, return_logits)

@@ -1,0 +1,166 @@
+// Shared device/host helpers for libtt2 (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/tt2.h"
+
+namespace tt2 {
+
+// ------------------------------------------------------------------------------------------
+// Errors: HIP failures become exceptions inside the library and a status at the ABI.
+// ------------------------------------------------------------------------------------------
+struct Error : std::runtime_error {
+  int status;
+  Error(int s, const std::string& m) : std::runtime_error(m), status(s) {}
+};
+
+void set_last_error(const std::string& msg);
+
+#define TT2_HIP(call)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      throw ::tt2::Error(e_ == hipErrorOutOfMemory ? TT2_ERR_OOM : TT2_ERR_HIP,            \
+                         std::string(#call) + ": " + hipGetErrorString(e_));               \
+  } while (0)
+
+#define TT2_CHECK(cond, status, msg)                                                       \
+  do {                                                                                     \
+    if (!(cond)) throw ::tt2::Error(status, msg);                                          \
+  } while (0)
+
+template <class F>
+tt2_status guard(F&& f) {
+  try {
+    f();
+    return TT2_OK;
+  } catch (const Error& e) {
+    set_last_error(e.what());
+    return e.status;
+  } catch (const std::exception& e) {
+    set_last_error(e.what());
+    return TT2_ERR_INVALID_ARG;
+  }
+}
+
+// Device buffer owned by a context.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { free(); }
+  void alloc(size_t n) {
+    if (n == bytes && p) return;
+    free();
+    if (n) TT2_HIP(hipMalloc(&p, n));
+    bytes = n;
+  }
+  void free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// Host-side store of loaded weights, keyed by TF variable name.
+struct HostTensor {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+};
+using WeightMap = std::map<std::string, HostTensor>;
+
+void put_tensor(WeightMap& wm, const char* name, const float* host, const int64_t* shape, int ndim);
+const HostTensor& need(const WeightMap& wm, const std::string& name, std::vector<int64_t> shape);
+
+// ------------------------------------------------------------------------------------------
+// MFMA f32 fragment layouts (v_mfma_f32_16x16x4_f32).
+//
+// Lane l of a 64-lane wave supplies A[i=l&15][k=l>>4] and B[k=l>>4][j=l&15]; the 4 accumulator
+// registers hold D[row=(l>>4)*4+r][col=l&15].
+//
+// "AF" activation layout of a 32-row block with K columns (K % 16 == 0): lane l of the wave that
+// processes k-group sg (16 k's) and row-half h loads one float4 holding A[h*16+(l&15)]
+// [16*sg + 4*j + (l>>4)] for j = 0..3 -> one 1 KiB coalesced load per (sg, h).
+// "WF" weight layout of a 16-column tile: lane l loads float4 W[16*sg + 4*j + (l>>4)][l&15].
+// ------------------------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline int af_idx(int m, int k) {
+  const int s = k >> 2, kk = k & 3, h = m >> 4, i = m & 15;
+  return ((((s >> 2) * 2 + h) * 64 + (kk * 16 + i)) << 2) + (s & 3);
+}
+__host__ __device__ inline int wf_idx(int k, int j) {  // within one 16-column tile
+  const int s = k >> 2, kk = k & 3;
+  return ((((s >> 2) * 64) + (kk * 16 + j)) << 2) + (s & 3);
+}
+
+// acc[h] += A(rows h*16..h*16+15, k in [16*sg0, 16*sg1)) * Wtile(k, 0..15)
+__device__ __forceinline__ void skinny_mfma(const float* __restrict__ X, const float* __restrict__ Wt,
+                                            int sg0, int sg1, f32x4& acc0, f32x4& acc1, int lane) {
+  const f32x4* Xv = reinterpret_cast<const f32x4*>(X);
+  const f32x4* Wv = reinterpret_cast<const f32x4*>(Wt);
+#pragma unroll 4
+  for (int sg = sg0; sg < sg1; ++sg) {
+    const f32x4 a0 = Xv[(sg * 2 + 0) * 64 + lane];
+    const f32x4 a1 = Xv[(sg * 2 + 1) * 64 + lane];
+    const f32x4 b = Wv[sg * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], b[j], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], b[j], acc1, 0, 0, 0);
+    }
+  }
+}
+
+// Reduce the (acc0, acc1) of NW waves (each covering a K slice) through LDS into
+// out[m*16 + n] (32 x 16), summing waves in index order (deterministic).
+template <int NW>
+__device__ __forceinline__ void reduce_waves_32x16(const f32x4& acc0, const f32x4& acc1, float* lds,
+                                                   float* out, int wave, int lane, int tid) {
+  // lds: NW * 512 floats
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int n = lane & 15, m = (lane >> 4) * 4 + r;
+    lds[wave * 512 + m * 16 + n] = acc0[r];
+    lds[wave * 512 + (m + 16) * 16 + n] = acc1[r];
+  }
+  __syncthreads();
+  for (int e = tid; e < 512; e += NW * 64) {
+    float s = lds[e];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) s += lds[w * 512 + e];
+    out[e] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// Accurate variants used where parity matters (expf is correctly-rounded-ish ocml).
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// counter-based RNG (splitmix64 finaliser) used when the caller injects no noise
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ inline double u01_open(uint64_t h) {  // in [1e-5, 1-1e-5)
+  const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+  return 1e-5 + u * (1.0 - 2e-5);
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace tt2

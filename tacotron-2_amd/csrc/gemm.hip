@@ -1,0 +1,196 @@
+// fp32 GEMM on the CDNA4 f32-input matrix cores (v_mfma_f32_32x32x2_f32, exact fp32 fma chain).
+//
+// C[M,N] = epilogue(A[M,K] · B[K,N]).  A is read through an implicit-im2col loader (dense rows,
+// 'same' conv1d, NHWC conv2d) so the encoder/postnet/refnet convolutions never materialise their
+// column matrices in HBM.  Block tile (64·WMB)×(64·WNB)×16, 4 waves in a 2×2 grid, each wave owns
+// WMB×WNB 32×32 accumulators; LDS double-buffered, next tile prefetched into registers while the
+// current one is multiplied.
+#include "gemm.h"
+
+namespace tt2 {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <bool VA>
+__device__ __forceinline__ void load_a4(const GemmArgs& g, int m, int k, float* v) {
+  v[0] = v[1] = v[2] = v[3] = 0.f;
+  if (m >= g.M || k >= g.K) return;
+  if (g.a_mode == A_DENSE) {
+    const float* p = g.A + (long)m * g.lda + k;
+    if (VA && k + 3 < g.K) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(p);
+      v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+    } else {
+      for (int i = 0; i < 4; ++i)
+        if (k + i < g.K) v[i] = p[i];
+    }
+    return;
+  }
+  if (g.a_mode == A_CONV1D) {
+    const int b = m / g.T, t = m - b * g.T;
+    if (VA && k + 3 < g.K) {  // C % 4 == 0: the 4 k's share one tap
+      const int tap = k / g.C, c = k - tap * g.C;
+      const int tt = t + tap - g.pad;
+      if (tt >= 0 && tt < g.T) {
+        const f32x4 q = *reinterpret_cast<const f32x4*>(g.A + b * g.xs_b + (long)tt * g.xs_t + c);
+        v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+      }
+    } else {
+      for (int i = 0; i < 4; ++i) {
+        const int kk = k + i;
+        if (kk >= g.K) break;
+        const int tap = kk / g.C, c = kk - tap * g.C;
+        const int tt = t + tap - g.pad;
+        if (tt >= 0 && tt < g.T) v[i] = g.A[b * g.xs_b + (long)tt * g.xs_t + c];
+      }
+    }
+    return;
+  }
+  // A_CONV2D (NHWC)
+  const int hw = g.Ho * g.Wo;
+  const int n = m / hw, r = m - n * hw, ho = r / g.Wo, wo = r - ho * g.Wo;
+  if (VA && k + 3 < g.K) {
+    const int ij = k / g.C, c = k - ij * g.C, i = ij / g.kw2, j = ij - i * g.kw2;
+    const int h = ho * g.sh + i - g.pt, w = wo * g.sw + j - g.pl;
+    if (h >= 0 && h < g.H && w >= 0 && w < g.Wd) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(g.A + (((long)n * g.H + h) * g.Wd + w) * g.C + c);
+      v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+    }
+  } else {
+    for (int e = 0; e < 4; ++e) {
+      const int kk = k + e;
+      if (kk >= g.K) break;
+      const int ij = kk / g.C, c = kk - ij * g.C, i = ij / g.kw2, j = ij - i * g.kw2;
+      const int h = ho * g.sh + i - g.pt, w = wo * g.sw + j - g.pl;
+      if (h >= 0 && h < g.H && w >= 0 && w < g.Wd) v[e] = g.A[(((long)n * g.H + h) * g.Wd + w) * g.C + c];
+    }
+  }
+}
+
+template <bool VB>
+__device__ __forceinline__ void load_b4(const GemmArgs& g, int k, int n, float* v) {
+  v[0] = v[1] = v[2] = v[3] = 0.f;
+  if (k >= g.K || n >= g.N) return;
+  const float* p = g.Bw + (long)k * g.ldb + n;
+  if (VB && n + 3 < g.N) {
+    const f32x4 q = *reinterpret_cast<const f32x4*>(p);
+    v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+  } else {
+    for (int i = 0; i < 4; ++i)
+      if (n + i < g.N) v[i] = p[i];
+  }
+}
+
+template <int WMB, int WNB, bool VA, bool VB>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  constexpr int BM = 64 * WMB, BN = 64 * WNB, BK = 16;
+  constexpr int EA = BM * BK / 256, TPR_A = BK / EA;
+  constexpr int EB = BN * BK / 256, TPR_B = BN / EB;
+  __shared__ float As[2][BK][BM + 4];
+  __shared__ float Bs[2][BK][BN + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int am = tid / TPR_A, ak = (tid % TPR_A) * EA;
+  const int bk = tid / TPR_B, bn = (tid % TPR_B) * EB;
+  float ra[EA], rb[EB];
+  f32x16 acc[WMB][WNB];
+#pragma unroll
+  for (int i = 0; i < WMB; ++i)
+#pragma unroll
+    for (int j = 0; j < WNB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < EA; e += 4) load_a4<VA>(g, m0 + am, k0 + ak + e, &ra[e]);
+#pragma unroll
+    for (int e = 0; e < EB; e += 4) load_b4<VB>(g, k0 + bk, n0 + bn + e, &rb[e]);
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) As[buf][ak + e][am] = ra[e];
+#pragma unroll
+    for (int e = 0; e < EB; ++e) Bs[buf][bk][bn + e] = rb[e];
+  };
+
+  const int nk = (g.K + BK - 1) / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      float a[WMB], b[WNB];
+#pragma unroll
+      for (int i = 0; i < WMB; ++i) a[i] = As[cur][kk + (lane >> 5)][wm * 32 * WMB + i * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < WNB; ++j) b[j] = Bs[cur][kk + (lane >> 5)][wn * 32 * WNB + j * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < WMB; ++i)
+#pragma unroll
+        for (int j = 0; j < WNB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < WMB; ++i)
+#pragma unroll
+    for (int j = 0; j < WNB; ++j) {
+      const int col = n0 + wn * 32 * WNB + j * 32 + (lane & 31);
+      if (col >= g.N) continue;
+      const float bias = g.bias ? g.bias[col] : 0.f;
+      const float sc = g.bn_scale ? g.bn_scale[col] : 1.f;
+      const float sh = g.bn_shift ? g.bn_shift[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 32 * WMB + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= g.M) continue;
+        float y = acc[i][j][r] + bias;
+        if (g.act == ACT_RELU) y = fmaxf(y, 0.f);
+        else if (g.act == ACT_TANH) y = tanhf(y);
+        if (g.bn_scale) y = y * sc + sh;
+        if (g.act == ACT_BN_RELU) y = fmaxf(y, 0.f);  // BN then ReLU (conv2d(), modules.py:507-510)
+        if (g.residual) y = g.residual[(long)row * g.ldr + col] + y;
+        if (g.clip) y = fminf(fmaxf(y, g.clip_lo), g.clip_hi);
+        g.Cout[(long)row * g.ldc + col] = y;
+      }
+    }
+}
+
+template <int WMB, int WNB>
+static void launch(const GemmArgs& a, bool va, bool vb, hipStream_t s) {
+  dim3 grid(cdiv(a.N, 64 * WNB), cdiv(a.M, 64 * WMB));
+  if (va && vb) hipLaunchKernelGGL((gemm_kernel<WMB, WNB, true, true>), grid, dim3(256), 0, s, a);
+  else if (va) hipLaunchKernelGGL((gemm_kernel<WMB, WNB, true, false>), grid, dim3(256), 0, s, a);
+  else if (vb) hipLaunchKernelGGL((gemm_kernel<WMB, WNB, false, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((gemm_kernel<WMB, WNB, false, false>), grid, dim3(256), 0, s, a);
+  TT2_HIP(hipGetLastError());
+}
+
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+void gemm(const GemmArgs& a, hipStream_t s) {
+  TT2_CHECK(a.M > 0 && a.N > 0 && a.K > 0, TT2_ERR_SHAPE_MISMATCH, "gemm: empty problem");
+  bool va = al16(a.A);
+  if (a.a_mode == A_DENSE) va = va && (a.lda % 4 == 0);
+  else if (a.a_mode == A_CONV1D) va = va && (a.C % 4 == 0) && (a.xs_t % 4 == 0) && (a.xs_b % 4 == 0);
+  else va = va && (a.C % 4 == 0);
+  const bool vb = al16(a.Bw) && (a.ldb % 4 == 0);
+  const int wnb = a.N <= 64 ? 1 : 2;
+  const long tiles22 = (long)cdiv(a.M, 128) * cdiv(a.N, 64 * wnb);
+  const int wmb = tiles22 >= 512 ? 2 : 1;
+  if (wmb == 2 && wnb == 2) launch<2, 2>(a, va, vb, s);
+  else if (wmb == 2) launch<2, 1>(a, va, vb, s);
+  else if (wnb == 2) launch<1, 2>(a, va, vb, s);
+  else launch<1, 1>(a, va, vb, s);
+}
+
+}  // namespace tt2

@@ -1,0 +1,1351 @@
+// Tacotron-2 synthesis path on MI355X (gfx950): encoder, reference encoders + GST, attention
+// memory, the autoregressive decoder (prenet → 2×Zoneout-LSTM → location-sensitive attention →
+// frame/stop projection) and the Postnet.  See DESIGN.md for the data layout and roofline.
+//
+// Reference: code/tacotron/models/{tacotron.py, modules.py, attention.py,
+// Architecture_wrappers.py, helpers.py, custom_decoder.py, multihead_attention.py}.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <tuple>
+
+#include "common.h"
+#include "gemm.h"
+
+namespace tt2 {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& m) { g_last_error = m; }
+
+void put_tensor(WeightMap& wm, const char* name, const float* host, const int64_t* shape, int ndim) {
+  TT2_CHECK(name && host && ndim >= 0 && (ndim == 0 || shape), TT2_ERR_INVALID_ARG,
+            "load_tensor: null argument");
+  HostTensor t;
+  int64_t n = 1;
+  for (int i = 0; i < ndim; ++i) {
+    TT2_CHECK(shape[i] >= 0, TT2_ERR_INVALID_ARG, "load_tensor: negative dim");
+    t.shape.push_back(shape[i]);
+    n *= shape[i];
+  }
+  t.data.assign(host, host + n);
+  wm[name] = std::move(t);
+}
+
+const HostTensor& need(const WeightMap& wm, const std::string& name, std::vector<int64_t> shape) {
+  auto it = wm.find(name);
+  TT2_CHECK(it != wm.end(), TT2_ERR_NOT_LOADED, "missing weight: " + name);
+  std::vector<int64_t> got = it->second.shape;
+  // scalars may come as () or (1,)
+  auto squeeze = [](std::vector<int64_t> v) {
+    std::vector<int64_t> r;
+    for (auto d : v)
+      if (d != 1) r.push_back(d);
+    return r;
+  };
+  if (squeeze(got) != squeeze(shape)) {
+    std::string s = "shape mismatch for " + name + ": got (";
+    for (auto d : got) s += std::to_string(d) + ",";
+    s += ") want (";
+    for (auto d : shape) s += std::to_string(d) + ",";
+    throw Error(TT2_ERR_SHAPE_MISMATCH, s + ")");
+  }
+  return it->second;
+}
+
+static const char* TP = "Tacotron_model/inference/";
+
+// ==========================================================================================
+// Device kernels
+// ==========================================================================================
+
+// ---- encoder -----------------------------------------------------------------------------
+
+// embedding_lookup (tacotron.py:215-217): x[b,t,:] = table[ids[b,t], :]
+__global__ void k_embed(const int* __restrict__ ids, const float* __restrict__ table, float* __restrict__ x,
+                        int BT, int E, int n_sym) {
+  const int row = blockIdx.x;
+  if (row >= BT) return;
+  int id = ids[row];
+  id = id < 0 ? 0 : (id >= n_sym ? n_sym - 1 : id);
+  for (int e = threadIdx.x; e < E; e += blockDim.x) x[(long)row * E + e] = table[(long)id * E + e];
+}
+
+// One time step of both directions of the encoder Zoneout-BiLSTM (modules.py:313-323) with
+// tf.nn.bidirectional_dynamic_rnn sequence_length semantics.  Block = (dir, 4 hidden units).
+// gates = xproj[b, pos, dir] (x·Wx + b, precomputed for every t by one GEMM) + h_prev·Wh.
+struct EncLstmArgs {
+  const float* xproj;   // [B*T][2*4U]
+  const float* wh;      // [2][U/4][U x 16 WF tile]
+  float* hs;            // [2 dirs][2 parity][32 x U AF]
+  float* cs;            // [2][32][U]
+  float* out;           // [B][T][2U]
+  const int* lengths;
+  int B, T, U, t;
+  float zo, one_m_zo;
+};
+
+__global__ __launch_bounds__(256) void k_enc_lstm_step(EncLstmArgs a) {
+  __shared__ float red[4 * 512];
+  __shared__ float G[512];
+  const int ng = a.U / 4;
+  const int dir = blockIdx.x / ng, g = blockIdx.x % ng;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int par = a.t & 1;
+  const float* X = a.hs + ((long)(dir * 2 + par) * 32 * a.U);
+  float* Xn = a.hs + ((long)(dir * 2 + (par ^ 1)) * 32 * a.U);
+  const float* Wt = a.wh + ((long)(dir * ng + g) * a.U * 16);
+  const int nsg = a.U / 16;
+  const int sg0 = wave * nsg / 4, sg1 = (wave + 1) * nsg / 4;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  skinny_mfma(X, Wt, sg0, sg1, acc0, acc1, lane);
+  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
+  if (tid < 128) {
+    const int m = tid >> 2, uu = tid & 3, u = 4 * g + uu;
+    const int U = a.U;
+    const float hprev = X[af_idx(m, u)];
+    float* cp = a.cs + ((long)dir * 32 + m) * U + u;
+    bool act = false;
+    int pos = 0;
+    if (m < a.B) {
+      const int L = a.lengths[m];
+      act = a.t < L;
+      pos = dir == 0 ? a.t : L - 1 - a.t;
+    }
+    if (act) {
+      const float* xp = a.xproj + ((long)m * a.T + pos) * (8 * U) + dir * 4 * U;
+      const float zi = G[m * 16 + 0 * 4 + uu] + xp[0 * U + u];
+      const float zj = G[m * 16 + 1 * 4 + uu] + xp[1 * U + u];
+      const float zf = G[m * 16 + 2 * 4 + uu] + xp[2 * U + u];
+      const float zz = G[m * 16 + 3 * 4 + uu] + xp[3 * U + u];
+      const float cprev = *cp;
+      const float cn = sigm(zf + 1.0f) * cprev + sigm(zi) * tanhf(zj);
+      const float hn = sigm(zz) * tanhf(cn);
+      *cp = a.one_m_zo * cn + a.zo * cprev;
+      Xn[af_idx(m, u)] = a.one_m_zo * hn + a.zo * hprev;
+      a.out[((long)m * a.T + pos) * (2 * U) + dir * U + u] = hn;
+    } else {
+      Xn[af_idx(m, u)] = hprev;  // state copied through past the row's length
+    }
+  }
+}
+
+// ReferenceEncoder GRU + dense(tanh) (modules.py:57-64) and GST MultiheadAttention
+// (multihead_attention.py:35-132, tacotron.py:276-282) for one batch row.
+struct RefGstArgs {
+  const float* x;        // conv stack output [B][T2][gin]
+  int T2, gin, D;        // D = reference_depth (GRU units)
+  const float* kg; const float* bg;  // [(gin+D)][2D], [2D]
+  const float* kc; const float* bc;  // [(gin+D)][D], [D]
+  const float* kd; const float* bd;  // [D][128], [128]
+  const float* tokens;               // [ntok][tokd]
+  const float* kq; const float* bq;  // [128][A], [A]
+  const float* kk; const float* bk;  // [tokd][A], [A]
+  const float* av; const float* ag; const float* ab;  // [A/heads], scalar, [A/heads]
+  int ntok, tokd, A, heads;
+  float* ref_out;  // [B][128]
+  float* style;    // [B][style_w] (writes at style_off)
+  int style_w, style_off;
+};
+
+__global__ __launch_bounds__(256) void k_ref_gru_gst(RefGstArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int D = a.D, gin = a.gin, In = gin + D;
+  float* xh = sm;                 // [In]   concat(x, h) / concat(x, r*h)
+  float* h = xh + In;             // [D]
+  float* gates = h + D;           // [2D]
+  float* ref = gates + 2 * D;     // [128]
+  float* q = ref + 128;           // [A]
+  float* keys = q + a.A;          // [ntok][A]
+  float* vals = keys + a.ntok * a.A;  // [ntok][tokd]
+  float* sc = vals + a.ntok * a.tokd; // [heads][ntok]
+  for (int i = tid; i < D; i += blockDim.x) h[i] = 0.f;
+  __syncthreads();
+  for (int t = 0; t < a.T2; ++t) {
+    const float* xt = a.x + ((long)b * a.T2 + t) * gin;
+    for (int i = tid; i < gin; i += blockDim.x) xh[i] = xt[i];
+    for (int i = tid; i < D; i += blockDim.x) xh[gin + i] = h[i];
+    __syncthreads();
+    for (int j = tid; j < 2 * D; j += blockDim.x) {
+      float s = 0.f;
+      for (int k = 0; k < In; ++k) s += xh[k] * a.kg[(long)k * 2 * D + j];
+      gates[j] = sigm(s + a.bg[j]);
+    }
+    __syncthreads();
+    for (int i = tid; i < D; i += blockDim.x) xh[gin + i] = gates[i] * h[i];  // r * h
+    __syncthreads();
+    float hn = 0.f;
+    if (tid < D) {
+      float s = 0.f;
+      for (int k = 0; k < In; ++k) s += xh[k] * a.kc[(long)k * D + tid];
+      const float c = tanhf(s + a.bc[tid]);
+      const float u = gates[D + tid];
+      hn = u * h[tid] + (1.f - u) * c;
+    }
+    __syncthreads();
+    if (tid < D) h[tid] = hn;
+    __syncthreads();
+  }
+  // dense(128, tanh) on the last GRU output
+  if (tid < 128) {
+    float s = 0.f;
+    for (int k = 0; k < D; ++k) s += h[k] * a.kd[k * 128 + tid];
+    ref[tid] = tanhf(s + a.bd[tid]);
+    a.ref_out[b * 128 + tid] = ref[tid];
+  }
+  // GST values = tanh(tokens)
+  for (int i = tid; i < a.ntok * a.tokd; i += blockDim.x) vals[i] = tanhf(a.tokens[i]);
+  __syncthreads();
+  for (int j = tid; j < a.A; j += blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < 128; ++k) s += ref[k] * a.kq[k * a.A + j];
+    q[j] = s + a.bq[j];
+  }
+  for (int e = tid; e < a.ntok * a.A; e += blockDim.x) {
+    const int tok = e / a.A, j = e % a.A;
+    float s = 0.f;
+    for (int d = 0; d < a.tokd; ++d) s += vals[tok * a.tokd + d] * a.kk[d * a.A + j];
+    keys[e] = s + a.bk[j];
+  }
+  __syncthreads();
+  const int dh = a.A / a.heads;
+  // normed_v = g * v * rsqrt(sum(v^2))
+  float vn = 0.f;
+  for (int d = 0; d < dh; ++d) vn += a.av[d] * a.av[d];
+  const float scale = a.ag[0] * (1.0f / sqrtf(vn));
+  for (int e = tid; e < a.heads * a.ntok; e += blockDim.x) {
+    const int hh = e / a.ntok, tok = e % a.ntok;
+    float s = 0.f;
+    for (int d = 0; d < dh; ++d)
+      s += (scale * a.av[d]) * tanhf(keys[tok * a.A + hh * dh + d] + q[hh * dh + d] + a.ab[d]);
+    sc[e] = s;
+  }
+  __syncthreads();
+  if (tid < a.heads) {
+    float mx = -INFINITY;
+    for (int tok = 0; tok < a.ntok; ++tok) mx = fmaxf(mx, sc[tid * a.ntok + tok]);
+    float sum = 0.f;
+    for (int tok = 0; tok < a.ntok; ++tok) {
+      const float e = expf(sc[tid * a.ntok + tok] - mx);
+      sc[tid * a.ntok + tok] = e;
+      sum += e;
+    }
+    for (int tok = 0; tok < a.ntok; ++tok) sc[tid * a.ntok + tok] /= sum;
+  }
+  __syncthreads();
+  for (int e = tid; e < a.heads * a.tokd; e += blockDim.x) {
+    const int hh = e / a.tokd, d = e % a.tokd;
+    float s = 0.f;
+    for (int tok = 0; tok < a.ntok; ++tok) s += sc[hh * a.ntok + tok] * vals[tok * a.tokd + d];
+    a.style[(long)b * a.style_w + a.style_off + e] = s;
+  }
+}
+
+// values = concat(encoder_outputs, tile(style)) · seq_mask (tacotron.py:307-308 + TF
+// BahdanauAttention._prepare_memory)
+__global__ void k_memory(const float* __restrict__ enc, const float* __restrict__ style,
+                         const int* __restrict__ lengths, float* __restrict__ values, int B, int T, int E2,
+                         int SW) {
+  const int row = blockIdx.x;  // b*T + t
+  const int b = row / T, t = row % T;
+  const int D = E2 + SW;
+  const bool valid = t < lengths[b];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float v = 0.f;
+    if (valid) v = d < E2 ? enc[(long)row * E2 + d] : style[(long)b * SW + d - E2];
+    values[(long)row * D + d] = v;
+  }
+}
+
+// ---- decoder -------------------------------------------------------------------------------
+
+struct DecCtl {
+  int done;
+  int n_steps;
+  int tbase;
+  int pad;
+};
+
+struct DecArgs {
+  DecCtl* ctl;
+  int B, T_in, max_iters, T_lim;   // T_lim: GTA target length (0 = free running)
+  int nm, P, H, Dm, A, F, KL;
+  int K1, K2, Kp;                  // LSTM1 / LSTM2 / projection input widths
+  float zo, one_m_zo;
+  int stop_at_any, mask_encoder, cumulative, constraint, monotonic, win;
+  // weights
+  const float* pre_w1; const float* pre_b1; const float* pre_w2; const float* pre_b2;
+  const float* l1_w; const float* l1_b; const float* l2_w; const float* l2_b;
+  const float* q_w; const float* loc_cw; const float* loc_cb; const float* loc_w;
+  const float* va; const float* ba; const float* proj_w; const float* proj_b;
+  // attention memory
+  const float* keys;    // [B][T_in][A]
+  const float* values;  // [B][T_in][Dm]
+  const int* lengths;
+  // state / activations
+  float* X1[2]; float* X2[2]; float* Xp;
+  float* c1; float* c2;
+  float* Qp;      // [KSQ][32][A]
+  float* energy;  // [B][T_in]
+  float* cum;     // [B][T_in]
+  int* max_att;   // [B]
+  float* PP;      // [KSP][32][NPJ]
+  int KSQ, KSP, NPJ;
+  // noise / teacher
+  const uint8_t* masks;  // [max_iters][2][B][P] or null
+  uint64_t seed;
+  const float* targets;  // [B][T_lim][nm] or null
+  // outputs
+  float* frames;  // [B][max_iters][nm]
+  float* stop;    // [B][max_iters]
+  float* align;   // [B][T_in][max_iters] or null
+};
+
+__device__ __forceinline__ float prenet_keep(const DecArgs& a, int t, int layer, int b, int j) {
+  if (b >= a.B) return 0.f;
+  if (a.masks) return (float)a.masks[(((long)t * 2 + layer) * a.B + b) * a.P + j];
+  const uint64_t h = mix64(a.seed ^ mix64(((((uint64_t)t * 2 + layer) * 4096u + b) << 16) + j));
+  return (h >> 63) ? 1.f : 0.f;
+}
+
+// Prenet (modules.py:346-357) of step t, preceded by the TacoTestHelper/dynamic_decode
+// bookkeeping of step t-1 (helpers.py:36-59): reduce the frame/stop projection partials,
+// write frames/stop[t-1], decide `finished`, select next input (frame or GTA target).
+// Grid: P/16 blocks (layer-2 column tiles); every block recomputes layer 1 (K = num_mels).
+__global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep) {
+  __shared__ __attribute__((aligned(16))) float fin[32 * 80 + 32 * 16];   // AF [32][nm<=80(+pad)]
+  __shared__ __attribute__((aligned(16))) float h1[32 * 256];             // AF [32][P<=256]
+  __shared__ float red[4 * 512];
+  __shared__ float G[512];
+  __shared__ float stopv[32];
+  __shared__ int s_done;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (a.ctl->done) return;
+  const int t = a.ctl->tbase + istep;
+  const int nm = a.nm, nmp = (nm + 15) & ~15;
+  // ---- finish step t-1 ----
+  for (int i = tid; i < 32 * nmp; i += blockDim.x) fin[i] = 0.f;
+  if (tid == 0) s_done = 0;
+  __syncthreads();
+  if (t > 0) {
+    for (int e = tid; e < 32 * (nm + 1); e += blockDim.x) {
+      const int m = e / (nm + 1), n = e % (nm + 1);
+      float s = 0.f;
+      for (int ks = 0; ks < a.KSP; ++ks) s += a.PP[((long)ks * 32 + m) * a.NPJ + n];
+      s += a.proj_b[n];
+      if (n == nm) {
+        stopv[m] = sigm(s);
+      } else {
+        float v = s;
+        if (a.targets) v = (m < a.B) ? a.targets[((long)m * a.T_lim + (t - 1)) * nm + n] : 0.f;
+        fin[af_idx(m, n)] = (m < a.B) ? v : 0.f;
+        if (blockIdx.x == 0 && m < a.B) a.frames[((long)m * a.max_iters + (t - 1)) * nm + n] = s;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int fin_all = 1, fin_any = 0;
+      for (int m = 0; m < a.B; ++m) {
+        const int f = rintf(stopv[m]) == 1.0f;
+        fin_all &= f;
+        fin_any |= f;
+        if (blockIdx.x == 0) a.stop[(long)m * a.max_iters + (t - 1)] = stopv[m];
+      }
+      int done = a.stop_at_any ? fin_any : fin_all;
+      if (a.T_lim > 0) done = t >= a.T_lim;   // TacoTrainingHelper: time + 1 >= T_targets
+      if (t >= a.max_iters) done = 1;         // dynamic_decode maximum_iterations
+      s_done = done;
+      if (done && blockIdx.x == 0) {
+        a.ctl->n_steps = t;
+        a.ctl->done = 1;
+      }
+    }
+    __syncthreads();
+    if (s_done) return;
+  }
+  // ---- layer 1: relu(fin·W1 + b1) * keep / 0.5  (all 16-col tiles, K = nm) ----
+  const int P = a.P, ntile = P / 16, nsg1 = nmp / 16;
+  for (int tile = wave; tile < ntile; tile += 4) {
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    skinny_mfma(fin, a.pre_w1 + (long)tile * nmp * 16, 0, nsg1, acc0, acc1, lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = tile * 16 + (lane & 15);
+      const int m0 = (lane >> 4) * 4 + r;
+      float v0 = fmaxf(acc0[r] + a.pre_b1[n], 0.f);
+      float v1 = fmaxf(acc1[r] + a.pre_b1[n], 0.f);
+      v0 = (v0 / 0.5f) * prenet_keep(a, t, 0, m0, n);
+      v1 = (v1 / 0.5f) * prenet_keep(a, t, 0, m0 + 16, n);
+      h1[af_idx(m0, n)] = v0;
+      h1[af_idx(m0 + 16, n)] = v1;
+    }
+  }
+  __syncthreads();
+  // ---- layer 2: this block's 16 columns, K = P split over 4 waves ----
+  const int tile = blockIdx.x, nsg2 = P / 16;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  skinny_mfma(h1, a.pre_w2 + (long)tile * P * 16, wave * nsg2 / 4, (wave + 1) * nsg2 / 4, acc0, acc1, lane);
+  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
+  float* X1 = a.X1[istep & 1];
+  for (int e = tid; e < 512; e += blockDim.x) {
+    const int m = e >> 4, n = tile * 16 + (e & 15);
+    float v = fmaxf(G[e] + a.pre_b2[n], 0.f);
+    v = (v / 0.5f) * prenet_keep(a, t, 1, m, n);
+    X1[af_idx(m, n)] = v;
+  }
+}
+
+// Zoneout-LSTM layer (modules.py:220-248 on TF LSTMCell): block g owns hidden units [4g, 4g+4)
+// = 16 gate columns (i,j,f,o × 4), K split over 4 waves, fused cell/zoneout epilogue.
+//   X [32 x K AF] input (h_prev at column hprev_off); writes h_new (raw LSTM output) into
+//   Xo at column ho_off, the zoned h into Xz at column hz_off, c in place.
+struct LstmArgs {
+  const DecCtl* ctl;
+  const float* X; int K; int hprev_off;
+  const float* W; const float* b;
+  float* c; int H;
+  float* Xo; int ho_off;
+  float* Xz; int hz_off;
+  float zo, one_m_zo;
+};
+
+__global__ __launch_bounds__(256) void k_lstm(LstmArgs a) {
+  __shared__ float red[4 * 512];
+  __shared__ float G[512];
+  if (a.ctl->done) return;
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nsg = a.K / 16;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  skinny_mfma(a.X, a.W + (long)g * a.K * 16, wave * nsg / 4, (wave + 1) * nsg / 4, acc0, acc1, lane);
+  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
+  if (tid < 128) {
+    const int m = tid >> 2, uu = tid & 3, u = 4 * g + uu;
+    const float* bb = a.b + g * 16;
+    const float zi = G[m * 16 + 0 + uu] + bb[0 + uu];
+    const float zj = G[m * 16 + 4 + uu] + bb[4 + uu];
+    const float zf = G[m * 16 + 8 + uu] + bb[8 + uu];
+    const float zz = G[m * 16 + 12 + uu] + bb[12 + uu];
+    float* cp = a.c + (long)m * a.H + u;
+    const float cprev = *cp;
+    const float hprev = a.X[af_idx(m, a.hprev_off + u)];
+    const float cn = sigm(zf + 1.0f) * cprev + sigm(zi) * tanhf(zj);
+    const float hn = sigm(zz) * tanhf(cn);
+    *cp = a.one_m_zo * cn + a.zo * cprev;
+    a.Xo[af_idx(m, a.ho_off + u)] = hn;
+    a.Xz[af_idx(m, a.hz_off + u)] = a.one_m_zo * hn + a.zo * hprev;
+  }
+}
+
+// Split-K skinny GEMM writing partial sums: out[ks][m][ldo] (cols tile*16..) for the query layer
+// (attention.py:187) and the frame/stop projections (Architecture_wrappers.py:243-247).
+struct PartArgs {
+  const DecCtl* ctl;
+  const float* X; int K;     // AF input
+  const float* W;            // [ntile][K x 16 WF]
+  float* out; int ldo; int ntile; int KS;
+};
+
+__global__ __launch_bounds__(256) void k_partial(PartArgs a) {
+  __shared__ float red[4 * 512];
+  __shared__ float G[512];
+  if (a.ctl->done) return;
+  const int tile = blockIdx.x % a.ntile, ks = blockIdx.x / a.ntile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nsg = a.K / 16;
+  const int s0 = ks * nsg / a.KS, s1 = (ks + 1) * nsg / a.KS;
+  const int n = s1 - s0;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  skinny_mfma(a.X, a.W + (long)tile * a.K * 16, s0 + wave * n / 4, s0 + (wave + 1) * n / 4, acc0, acc1, lane);
+  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
+  for (int e = tid; e < 512; e += blockDim.x) {
+    const int m = e >> 4, c = tile * 16 + (e & 15);
+    a.out[((long)ks * 32 + m) * a.ldo + c] = G[e];
+  }
+}
+
+// Location-sensitive energies (attention.py:37-69, 186-215) for 32 encoder steps of one row:
+// q = Σ query partials; f = conv1d(cum, 31 taps) + b; loc = f·W_loc;
+// e_t = Σ_k v_a[k]·tanh(keys + q + loc + b_a); window constraint; -inf past the row's length.
+__global__ __launch_bounds__(256) void k_energy(DecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (a.ctl->done) return;
+  const int b = blockIdx.x, t0 = blockIdx.y * 32, tid = threadIdx.x;
+  const int A = a.A, F = a.F, KL = a.KL, padl = (KL - 1) / 2;
+  float* q = sm;                       // [A]
+  float* win = q + A;                  // [32 + KL - 1]
+  float* f = win + 32 + KL;            // [32][F+1]
+  float* wl = f + 32 * (F + 1);        // [F][A]
+  for (int k = tid; k < A; k += blockDim.x) {
+    float s = 0.f;
+    for (int ks = 0; ks < a.KSQ; ++ks) s += a.Qp[((long)ks * 32 + b) * A + k];
+    q[k] = s;
+  }
+  for (int i = tid; i < 32 + KL - 1; i += blockDim.x) {
+    const int t = t0 - padl + i;
+    win[i] = (t >= 0 && t < a.T_in) ? a.cum[(long)b * a.T_in + t] : 0.f;
+  }
+  for (int i = tid; i < F * A; i += blockDim.x) wl[i] = a.loc_w[i];
+  __syncthreads();
+  for (int e = tid; e < 32 * F; e += blockDim.x) {
+    const int tt = e / F, fl = e % F;
+    float s = 0.f;
+    for (int tap = 0; tap < KL; ++tap) s += win[tt + tap] * a.loc_cw[tap * F + fl];
+    f[tt * (F + 1) + fl] = s + a.loc_cb[fl];
+  }
+  __syncthreads();
+  // thread -> (tt = tid>>3, 16-wide k slice kq)
+  const int tt = tid >> 3, kq = tid & 7;
+  const int t = t0 + tt;
+  float e = 0.f;
+  if (t < a.T_in) {
+    const float* kr = a.keys + ((long)b * a.T_in + t) * A;
+    for (int k = kq * (A / 8); k < (kq + 1) * (A / 8); ++k) {
+      float loc = 0.f;
+      for (int fl = 0; fl < F; ++fl) loc += f[tt * (F + 1) + fl] * wl[fl * A + k];
+      e += a.va[k] * tanhf(kr[k] + q[k] + loc + a.ba[k]);
+    }
+  }
+  e += __shfl_xor(e, 1);
+  e += __shfl_xor(e, 2);
+  e += __shfl_xor(e, 4);
+  if (kq == 0 && t < a.T_in) {
+    if (a.constraint) {
+      const int pm = a.max_att[b], w = a.win;
+      bool masked;
+      if (a.monotonic) masked = (t < pm) || (t >= pm + w);
+      else masked = (t < pm - (w / 2 + (w % 2 != 0 ? 1 : 0))) || (t >= pm + w / 2);
+      if (masked) e = -4294967296.0f;  // -2**32 + 1 in fp32
+    }
+    if (a.mask_encoder && t >= a.lengths[b]) e = -INFINITY;
+    a.energy[(long)b * a.T_in + t] = e;
+  }
+}
+
+// softmax → alignments, context = alignments · values for 64 memory channels of one row
+// (attention.py:10-35, 217-225); the dc==0 block also updates cum/max_att and writes alignments.
+__global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (a.ctl->done) return;
+  const int b = blockIdx.x, dc = blockIdx.y, tid = threadIdx.x;
+  const int T = a.T_in;
+  float* al = sm;               // [T]
+  float* red = al + ((T + 3) & ~3);   // [256*4]
+  __shared__ float s_max, s_sum;
+  for (int i = tid; i < T; i += blockDim.x) al[i] = a.energy[(long)b * T + i];
+  __syncthreads();
+  if (tid < 64) {
+    float mx = -INFINITY;
+    for (int i = tid; i < T; i += 64) mx = fmaxf(mx, al[i]);
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (tid == 0) s_max = mx;
+  }
+  __syncthreads();
+  for (int i = tid; i < T; i += blockDim.x) al[i] = expf(al[i] - s_max);
+  __syncthreads();
+  if (tid < 64) {
+    float s = 0.f;
+    for (int i = tid; i < T; i += 64) s += al[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (tid == 0) s_sum = s;
+  }
+  __syncthreads();
+  for (int i = tid; i < T; i += blockDim.x) al[i] = al[i] / s_sum;
+  __syncthreads();
+  // context for channels [dc*64, dc*64+64)
+  const int tq = tid >> 4, dq = tid & 15;
+  const int d = dc * 64 + dq * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (d < a.Dm) {
+    const float* vr = a.values + (long)b * T * a.Dm + d;
+    for (int t = tq; t < T; t += 16) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(vr + (long)t * a.Dm);
+      const float w = al[t];
+      acc[0] += w * v[0]; acc[1] += w * v[1]; acc[2] += w * v[2]; acc[3] += w * v[3];
+    }
+  }
+  for (int j = 0; j < 4; ++j) red[(j * 16 + dq) * 16 + tq] = acc[j];
+  __syncthreads();
+  if (tid < 64) {
+    const int j = tid >> 4, dq2 = tid & 15;
+    float s = 0.f;
+    for (int i = 0; i < 16; ++i) s += red[(j * 16 + dq2) * 16 + i];
+    const int dd = dc * 64 + dq2 * 4 + j;
+    if (dd < a.Dm) {
+      a.X1[(istep + 1) & 1][af_idx(b, a.P + dd)] = s;
+      a.Xp[af_idx(b, a.H + dd)] = s;
+    }
+  }
+  if (dc == 0) {
+    const int t_step = a.ctl->tbase + istep;
+    for (int i = tid; i < T; i += blockDim.x) {
+      float* c = a.cum + (long)b * T + i;
+      *c = a.cumulative ? al[i] + *c : al[i];
+      if (a.align && t_step < a.max_iters) a.align[((long)b * T + i) * a.max_iters + t_step] = al[i];
+    }
+    if (tid < 64) {
+      float best = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int i = tid; i < T; i += 64)
+        if (al[i] > best) { best = al[i]; bi = i; }
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      if (tid == 0) a.max_att[b] = bi;
+    }
+  }
+}
+
+__global__ void k_advance(DecCtl* ctl, int S) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) ctl->tbase += S;
+}
+
+// decoder_output clip (tacotron.py:362-363): dst[b][t][n] = clip(src[b][t][n])
+__global__ void k_clip_frames(const float* __restrict__ src, long src_bstride, float* __restrict__ dst, int B,
+                              int T, int nm, float lo, float hi, int do_clip) {
+  const long n = (long)B * T * nm;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = i / ((long)T * nm);
+    const long r = i - (long)b * T * nm;
+    float v = src[b * src_bstride + r];
+    if (do_clip) v = fminf(fmaxf(v, lo), hi);
+    dst[i] = v;
+  }
+}
+
+// ==========================================================================================
+// Host side
+// ==========================================================================================
+
+struct RefNetDev {
+  DevBuf cw[6], cb[6], bs[6], bh[6];
+  DevBuf kg, bg, kc, bc, kd, bd, tok, kq, bq, kk, bk, av, ag, ab;
+};
+
+struct Graph {
+  hipGraphExec_t exec = nullptr;
+  std::tuple<int, int, int, int, const void*, const void*, uint64_t, const void*, const void*, const void*> key;
+};
+
+}  // namespace tt2
+
+struct tt2_ctx {
+  tt2_config cfg;
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  tt2::WeightMap host;
+  bool finalized = false;
+  int nm, E, Cenc, U, Dm, A, F, KL, P, H, PC, SW, K1, K2, Kp, NPJ, KSQ = 4, KSP = 8;
+  int nref;
+  // weights
+  tt2::DevBuf emb;
+  tt2::DevBuf enc_cw[8], enc_cb[8], enc_bs[8], enc_bh[8];
+  tt2::DevBuf enc_wx, enc_bx, enc_wh;
+  tt2::RefNetDev ref[2];
+  tt2::DevBuf mem_k;
+  tt2::DevBuf pre_w1, pre_b1, pre_w2, pre_b2, l1_w, l1_b, l2_w, l2_b, q_w;
+  tt2::DevBuf loc_cw, loc_cb, loc_w, va, ba, proj_w, proj_b;
+  tt2::DevBuf post_cw[8], post_cb[8], post_bs[8], post_bh[8], post_pw, post_pb;
+  // activations
+  tt2::DevBuf ids, lens, refm[2], x_a, x_b, xproj, enc_out, enc_h, enc_c, conv_a, conv_b, ref_out, style,
+      values, keys;
+  tt2::DevBuf X1[2], X2[2], Xp, c1, c2, Qp, energy, cum, max_att, PP, ctl, masks, targets;
+  tt2::DevBuf frames, stop, align, dec, post_a, post_b, mel;
+  int* ctl_host = nullptr;  // pinned [2 slots]
+  int B = 0, T_in = 0, n_steps = 0, last_max_iters = 0;
+  bool encoded = false, decoded = false;
+  tt2::Graph graph;
+  static constexpr int S = 16;  // decoder steps per captured graph chunk
+};
+
+namespace tt2 {
+
+static void upload(DevBuf& d, const std::vector<float>& h) {
+  d.alloc(h.size() * sizeof(float));
+  TT2_HIP(hipMemcpy(d.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+}
+static void upload(DevBuf& d, const HostTensor& t) { upload(d, t.data); }
+
+// BN inference constants: y*scale + shift with scale = gamma·rsqrt(var+eps), shift = beta − mean·scale
+static void bn_consts(const WeightMap& wm, const std::string& scope, int c, DevBuf& sc, DevBuf& sh) {
+  const auto& g = need(wm, scope + "batch_normalization/gamma", {c});
+  const auto& be = need(wm, scope + "batch_normalization/beta", {c});
+  const auto& m = need(wm, scope + "batch_normalization/moving_mean", {c});
+  const auto& v = need(wm, scope + "batch_normalization/moving_variance", {c});
+  std::vector<float> s(c), h(c);
+  for (int i = 0; i < c; ++i) {
+    s[i] = g.data[i] / sqrtf(v.data[i] + 1e-3f);
+    h[i] = be.data[i] - m.data[i] * s[i];
+  }
+  upload(sc, s);
+  upload(sh, h);
+}
+
+// Repack W[K][N] columns `cols` (16 per tile) into WF tiles, K padded to Kp (zeros)
+static std::vector<float> pack_wf(const float* W, int K, int N, const std::vector<int>& cols, int Kp) {
+  const int nt = (int)cols.size() / 16;
+  std::vector<float> out((size_t)nt * Kp * 16, 0.f);
+  for (int tile = 0; tile < nt; ++tile)
+    for (int j = 0; j < 16; ++j) {
+      const int c = cols[tile * 16 + j];
+      if (c < 0) continue;
+      for (int k = 0; k < K; ++k) out[(size_t)tile * Kp * 16 + wf_idx(k, j)] = W[(size_t)k * N + c];
+    }
+  return out;
+}
+
+// LSTM gate column order per block g: [i u0..u3, j u0..u3, f u0..u3, o u0..u3]
+static std::vector<int> lstm_cols(int H) {
+  std::vector<int> cols;
+  for (int g = 0; g < H / 4; ++g)
+    for (int gate = 0; gate < 4; ++gate)
+      for (int uu = 0; uu < 4; ++uu) cols.push_back(gate * H + 4 * g + uu);
+  return cols;
+}
+
+static void finalize(tt2_ctx* c) {
+  const auto& cfg = c->cfg;
+  const WeightMap& wm = c->host;
+  const std::string P(TP);
+  TT2_HIP(hipSetDevice(c->dev));
+  upload(c->emb, need(wm, P + "inputs_embedding", {cfg.n_symbols, c->E}));
+  int cin = c->E;
+  for (int i = 1; i <= cfg.enc_conv_num_layers; ++i) {
+    const std::string s = P + "encoder_convolutions/conv_layer_" + std::to_string(i) + "_encoder_convolutions/";
+    upload(c->enc_cw[i - 1], need(wm, s + "conv1d/kernel", {cfg.enc_conv_kernel_size, cin, c->Cenc}));
+    upload(c->enc_cb[i - 1], need(wm, s + "conv1d/bias", {c->Cenc}));
+    bn_consts(wm, s, c->Cenc, c->enc_bs[i - 1], c->enc_bh[i - 1]);
+    cin = c->Cenc;
+  }
+  {
+    const int U = c->U;
+    std::vector<float> wx((size_t)cin * 8 * U), bx(8 * U);
+    std::vector<float> wh;
+    for (int d = 0; d < 2; ++d) {
+      const std::string s = P + "encoder_LSTM/bidirectional_rnn/" + (d ? "bw" : "fw") + "/lstm_cell/";
+      const auto& k = need(wm, s + "kernel", {cin + U, 4 * U});
+      const auto& b = need(wm, s + "bias", {4 * U});
+      for (int r = 0; r < cin; ++r)
+        for (int col = 0; col < 4 * U; ++col) wx[(size_t)r * 8 * U + d * 4 * U + col] = k.data[(size_t)r * 4 * U + col];
+      for (int col = 0; col < 4 * U; ++col) bx[d * 4 * U + col] = b.data[col];
+      auto p = pack_wf(k.data.data() + (size_t)cin * 4 * U, U, 4 * U, lstm_cols(U), U);
+      wh.insert(wh.end(), p.begin(), p.end());
+    }
+    upload(c->enc_wx, wx);
+    upload(c->enc_bx, bx);
+    upload(c->enc_wh, wh);
+  }
+  // reference encoders + GST
+  const char* tags[2] = {"emt", "spk"};
+  for (int r = 0; r < c->nref; ++r) {
+    auto& R = c->ref[r];
+    const std::string s = P + "refnet_" + tags[r] + "/";
+    int ci = 1, F = cfg.num_mels;
+    for (int i = 0; i < 6; ++i) {
+      const std::string s2 = s + "conv2d_" + std::to_string(i) + "/";
+      const int f = cfg.reference_filters[i];
+      upload(R.cw[i], need(wm, s2 + "conv2d/kernel", {3, 3, ci, f}));
+      upload(R.cb[i], need(wm, s2 + "conv2d/bias", {f}));
+      bn_consts(wm, s2, f, R.bs[i], R.bh[i]);
+      ci = f;
+      F = (F + 1) / 2;
+    }
+    const int gin = F * ci, D = cfg.reference_depth;
+    upload(R.kg, need(wm, s + "rnn/gru_cell/gates/kernel", {gin + D, 2 * D}));
+    upload(R.bg, need(wm, s + "rnn/gru_cell/gates/bias", {2 * D}));
+    upload(R.kc, need(wm, s + "rnn/gru_cell/candidate/kernel", {gin + D, D}));
+    upload(R.bc, need(wm, s + "rnn/gru_cell/candidate/bias", {D}));
+    upload(R.kd, need(wm, s + "dense/kernel", {D, 128}));
+    upload(R.bd, need(wm, s + "dense/bias", {128}));
+    const int tokd = cfg.style_embed_depth / cfg.num_heads, Aa = cfg.style_att_dim;
+    upload(R.tok, need(wm, P + "style_tokens_" + tags[r], {cfg.num_gst, tokd}));
+    const std::string mh = P + "Multihead-attention-" + tags[r] + "/";
+    upload(R.kq, need(wm, mh + "conv1d/kernel", {1, 128, Aa}));
+    upload(R.bq, need(wm, mh + "conv1d/bias", {Aa}));
+    upload(R.kk, need(wm, mh + "conv1d_1/kernel", {1, tokd, Aa}));
+    upload(R.bk, need(wm, mh + "conv1d_1/bias", {Aa}));
+    upload(R.av, need(wm, mh + "attention_v", {Aa / cfg.num_heads}));
+    upload(R.ag, need(wm, mh + "attention_g", {}));
+    upload(R.ab, need(wm, mh + "attention_b", {Aa / cfg.num_heads}));
+  }
+  upload(c->mem_k, need(wm, P + "memory_layer/kernel", {c->Dm, c->A}));
+  // decoder
+  {
+    const int nmp = (c->nm + 15) & ~15;
+    std::vector<int> cols;
+    for (int j = 0; j < c->P; ++j) cols.push_back(j);
+    const auto& w1 = need(wm, P + "decoder/decoder_prenet/dense_1/kernel", {c->nm, c->P});
+    upload(c->pre_w1, pack_wf(w1.data.data(), c->nm, c->P, cols, nmp));
+    upload(c->pre_b1, need(wm, P + "decoder/decoder_prenet/dense_1/bias", {c->P}));
+    const auto& w2 = need(wm, P + "decoder/decoder_prenet/dense_2/kernel", {c->P, c->P});
+    upload(c->pre_w2, pack_wf(w2.data.data(), c->P, c->P, cols, c->P));
+    upload(c->pre_b2, need(wm, P + "decoder/decoder_prenet/dense_2/bias", {c->P}));
+  }
+  for (int l = 0; l < 2; ++l) {
+    const std::string s = P + "decoder/decoder_LSTM/multi_rnn_cell/cell_" + std::to_string(l) + "/lstm_cell/";
+    const int K = l == 0 ? c->K1 : c->K2, H = c->H;
+    const auto& k = need(wm, s + "kernel", {K, 4 * H});
+    const auto& b = need(wm, s + "bias", {4 * H});
+    auto cols = lstm_cols(H);
+    std::vector<float> bt(cols.size());
+    for (size_t i = 0; i < cols.size(); ++i) bt[i] = b.data[cols[i]];
+    upload(l == 0 ? c->l1_w : c->l2_w, pack_wf(k.data.data(), K, 4 * H, cols, K));
+    upload(l == 0 ? c->l1_b : c->l2_b, bt);
+  }
+  {
+    std::vector<int> cols;
+    for (int j = 0; j < c->A; ++j) cols.push_back(j);
+    const auto& q = need(wm, P + "decoder/query_layer/kernel", {c->H, c->A});
+    upload(c->q_w, pack_wf(q.data.data(), c->H, c->A, cols, c->H));
+  }
+  const std::string la = P + "decoder/Location_Sensitive_Attention/";
+  upload(c->loc_cw, need(wm, la + "location_features_convolution/kernel", {c->KL, 1, c->F}));
+  upload(c->loc_cb, need(wm, la + "location_features_convolution/bias", {c->F}));
+  upload(c->loc_w, need(wm, la + "location_features_layer/kernel", {c->F, c->A}));
+  upload(c->va, need(wm, la + "attention_variable_projection", {c->A}));
+  upload(c->ba, need(wm, la + "attention_bias", {c->A}));
+  {
+    const std::string fp = P + "decoder/linear_transform_projection/projection_linear_transform_projection/";
+    const std::string sp = P + "decoder/stop_token_projection/projection_stop_token_projection/";
+    const auto& fk = need(wm, fp + "kernel", {c->Kp, c->nm});
+    const auto& fb = need(wm, fp + "bias", {c->nm});
+    const auto& sk = need(wm, sp + "kernel", {c->Kp, 1});
+    const auto& sb = need(wm, sp + "bias", {1});
+    const int N = c->nm + 1;
+    std::vector<float> W((size_t)c->Kp * N);
+    for (int k = 0; k < c->Kp; ++k) {
+      for (int n = 0; n < c->nm; ++n) W[(size_t)k * N + n] = fk.data[(size_t)k * c->nm + n];
+      W[(size_t)k * N + c->nm] = sk.data[k];
+    }
+    std::vector<int> cols;
+    for (int j = 0; j < c->NPJ; ++j) cols.push_back(j < N ? j : -1);
+    upload(c->proj_w, pack_wf(W.data(), c->Kp, N, cols, c->Kp));
+    std::vector<float> pb(c->NPJ, 0.f);
+    for (int n = 0; n < c->nm; ++n) pb[n] = fb.data[n];
+    pb[c->nm] = sb.data[0];
+    upload(c->proj_b, pb);
+  }
+  cin = c->nm;
+  for (int i = 1; i <= cfg.postnet_num_layers; ++i) {
+    const std::string s = P + "postnet_convolutions/conv_layer_" + std::to_string(i) + "_postnet_convolutions/";
+    upload(c->post_cw[i - 1], need(wm, s + "conv1d/kernel", {cfg.postnet_kernel_size, cin, c->PC}));
+    upload(c->post_cb[i - 1], need(wm, s + "conv1d/bias", {c->PC}));
+    bn_consts(wm, s, c->PC, c->post_bs[i - 1], c->post_bh[i - 1]);
+    cin = c->PC;
+  }
+  upload(c->post_pw, need(wm, P + "postnet_projection/projection_postnet_projection/kernel", {c->PC, c->nm}));
+  upload(c->post_pb, need(wm, P + "postnet_projection/projection_postnet_projection/bias", {c->nm}));
+  c->finalized = true;
+}
+
+static void alloc_acts(tt2_ctx* c) {
+  const auto& cfg = c->cfg;
+  const long B = cfg.max_batch, T = cfg.max_T_in, TR = std::max(cfg.max_T_ref, 1), MI = cfg.max_iters;
+  const long W = std::max<long>({(long)c->E, (long)c->Cenc});
+  c->ids.alloc(B * T * 4);
+  c->lens.alloc(64 * 4);
+  for (int r = 0; r < 2; ++r) c->refm[r].alloc(B * TR * c->nm * 4);
+  c->x_a.alloc(B * T * W * 4);
+  c->x_b.alloc(B * T * W * 4);
+  c->xproj.alloc(B * T * 8 * c->U * 4);
+  c->enc_out.alloc(B * T * 2 * c->U * 4);
+  c->enc_h.alloc(4L * 32 * c->U * 4);
+  c->enc_c.alloc(2L * 32 * c->U * 4);
+  // refnet conv scratch: largest layer output = B * ceil(T/2) * ceil(80/2) * filters[0..1]
+  long mx = 0;
+  {
+    long t = TR, f = c->nm;
+    for (int i = 0; i < 6; ++i) {
+      t = (t + 1) / 2;
+      f = (f + 1) / 2;
+      mx = std::max(mx, B * t * f * cfg.reference_filters[i]);
+    }
+  }
+  c->conv_a.alloc(std::max(mx, 16L) * 4);
+  c->conv_b.alloc(std::max(mx, 16L) * 4);
+  c->ref_out.alloc(2 * B * 128 * 4);
+  c->style.alloc(B * std::max(c->SW, 1) * 4);
+  c->values.alloc(B * T * c->Dm * 4);
+  c->keys.alloc(B * T * c->A * 4);
+  for (int p = 0; p < 2; ++p) {
+    c->X1[p].alloc(32L * c->K1 * 4);
+    c->X2[p].alloc(32L * c->K2 * 4);
+  }
+  c->Xp.alloc(32L * c->Kp * 4);
+  c->c1.alloc(32L * c->H * 4);
+  c->c2.alloc(32L * c->H * 4);
+  c->Qp.alloc((long)c->KSQ * 32 * c->A * 4);
+  c->energy.alloc(B * T * 4);
+  c->cum.alloc(B * T * 4);
+  c->max_att.alloc(64 * 4);
+  c->PP.alloc((long)c->KSP * 32 * c->NPJ * 4);
+  c->ctl.alloc(sizeof(DecCtl));
+  c->frames.alloc(B * MI * c->nm * 4);
+  c->stop.alloc(B * MI * 4);
+  c->align.alloc(B * T * MI * 4);
+  c->dec.alloc(B * MI * c->nm * 4);
+  c->post_a.alloc(B * MI * c->PC * 4);
+  c->post_b.alloc(B * MI * c->PC * 4);
+  c->mel.alloc(B * MI * c->nm * 4);
+  TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ctl_host), 4 * sizeof(int)));
+}
+
+// ---------------------------------------------------------------- encode
+static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const int* lens_h, int B, int T,
+                       const float* ref_d[2], const int T_ref[2], hipStream_t s) {
+  const auto& cfg = c->cfg;
+  TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_finalize_weights not called");
+  TT2_CHECK(B >= 1 && B <= cfg.max_batch && B <= 32, TT2_ERR_SHAPE_MISMATCH, "batch exceeds capacity (<=32)");
+  TT2_CHECK(T >= 1 && T <= cfg.max_T_in, TT2_ERR_SHAPE_MISMATCH, "T_in exceeds capacity");
+  for (int b = 0; b < B; ++b)
+    TT2_CHECK(lens_h[b] >= 1 && lens_h[b] <= T, TT2_ERR_INVALID_ARG, "input_lengths must be in [1, T_in]");
+  const int BT = B * T;
+  hipLaunchKernelGGL(k_embed, dim3(BT), dim3(128), 0, s, ids_d, c->emb.as<float>(), c->x_a.as<float>(), BT, c->E,
+                     cfg.n_symbols);
+  TT2_HIP(hipGetLastError());
+  // encoder convolutions: relu inside conv, then BN (modules.py:485-497, bnorm='after')
+  float* xin = c->x_a.as<float>();
+  float* xout = c->x_b.as<float>();
+  int cin = c->E;
+  for (int i = 0; i < cfg.enc_conv_num_layers; ++i) {
+    GemmArgs g;
+    g.M = BT; g.N = c->Cenc; g.K = cfg.enc_conv_kernel_size * cin;
+    g.a_mode = A_CONV1D; g.A = xin; g.T = T; g.C = cin; g.kw = cfg.enc_conv_kernel_size;
+    g.pad = (cfg.enc_conv_kernel_size - 1) / 2; g.xs_b = (long)T * cin; g.xs_t = cin;
+    g.Bw = c->enc_cw[i].as<float>(); g.ldb = c->Cenc; g.Cout = xout; g.ldc = c->Cenc;
+    g.bias = c->enc_cb[i].as<float>(); g.act = ACT_RELU;
+    g.bn_scale = c->enc_bs[i].as<float>(); g.bn_shift = c->enc_bh[i].as<float>();
+    gemm(g, s);
+    std::swap(xin, xout);
+    cin = c->Cenc;
+  }
+  // BiLSTM: x·Wx + b for all t and both directions in one GEMM, then T recurrent steps
+  {
+    GemmArgs g;
+    g.M = BT; g.N = 8 * c->U; g.K = cin; g.A = xin; g.lda = cin;
+    g.Bw = c->enc_wx.as<float>(); g.ldb = 8 * c->U; g.Cout = c->xproj.as<float>(); g.ldc = 8 * c->U;
+    g.bias = c->enc_bx.as<float>();
+    gemm(g, s);
+  }
+  TT2_HIP(hipMemsetAsync(c->enc_h.p, 0, c->enc_h.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->enc_c.p, 0, c->enc_c.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->enc_out.p, 0, (size_t)BT * 2 * c->U * 4, s));
+  int Tmax = 0;
+  for (int b = 0; b < B; ++b) Tmax = std::max(Tmax, lens_h[b]);
+  for (int t = 0; t < Tmax; ++t) {
+    EncLstmArgs a;
+    a.xproj = c->xproj.as<float>(); a.wh = c->enc_wh.as<float>(); a.hs = c->enc_h.as<float>();
+    a.cs = c->enc_c.as<float>(); a.out = c->enc_out.as<float>(); a.lengths = lens_d;
+    a.B = B; a.T = T; a.U = c->U; a.t = t; a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
+    hipLaunchKernelGGL(k_enc_lstm_step, dim3(2 * c->U / 4), dim3(256), 0, s, a);
+  }
+  TT2_HIP(hipGetLastError());
+  // reference encoders + GST
+  if (cfg.use_gst) {
+    for (int r = 0; r < c->nref; ++r) {
+      auto& R = c->ref[r];
+      const int TR = T_ref[r];
+      TT2_CHECK(TR >= 1 && TR <= cfg.max_T_ref, TT2_ERR_SHAPE_MISMATCH, "T_ref exceeds capacity");
+      const float* x = ref_d[r];
+      int H = TR, Wd = c->nm, C = 1;
+      float* bufs[2] = {c->conv_a.as<float>(), c->conv_b.as<float>()};
+      for (int i = 0; i < 6; ++i) {
+        const int f = cfg.reference_filters[i];
+        const int Ho = (H + 1) / 2, Wo = (Wd + 1) / 2;
+        GemmArgs g;
+        g.M = B * Ho * Wo; g.N = f; g.K = 9 * C; g.a_mode = A_CONV2D; g.A = x;
+        g.H = H; g.Wd = Wd; g.C = C; g.Ho = Ho; g.Wo = Wo; g.kh = 3; g.kw2 = 3; g.sh = 2; g.sw = 2;
+        g.pt = std::max((Ho - 1) * 2 + 3 - H, 0) / 2; g.pl = std::max((Wo - 1) * 2 + 3 - Wd, 0) / 2;
+        g.Bw = R.cw[i].as<float>(); g.ldb = f; g.Cout = bufs[i & 1]; g.ldc = f;
+        g.bias = R.cb[i].as<float>(); g.act = ACT_BN_RELU;
+        g.bn_scale = R.bs[i].as<float>(); g.bn_shift = R.bh[i].as<float>();
+        gemm(g, s);
+        x = bufs[i & 1];
+        H = Ho; Wd = Wo; C = f;
+      }
+      RefGstArgs a;
+      a.x = x; a.T2 = H; a.gin = Wd * C; a.D = cfg.reference_depth;
+      a.kg = R.kg.as<float>(); a.bg = R.bg.as<float>(); a.kc = R.kc.as<float>(); a.bc = R.bc.as<float>();
+      a.kd = R.kd.as<float>(); a.bd = R.bd.as<float>(); a.tokens = R.tok.as<float>();
+      a.kq = R.kq.as<float>(); a.bq = R.bq.as<float>(); a.kk = R.kk.as<float>(); a.bk = R.bk.as<float>();
+      a.av = R.av.as<float>(); a.ag = R.ag.as<float>(); a.ab = R.ab.as<float>();
+      a.ntok = cfg.num_gst; a.tokd = cfg.style_embed_depth / cfg.num_heads; a.A = cfg.style_att_dim;
+      a.heads = cfg.num_heads; a.ref_out = c->ref_out.as<float>() + r * cfg.max_batch * 128;
+      a.style = c->style.as<float>(); a.style_w = c->SW; a.style_off = r * cfg.style_embed_depth;
+      const int In = a.gin + a.D;
+      const size_t shm = sizeof(float) * (In + a.D + 2 * a.D + 128 + a.A + a.ntok * a.A + a.ntok * a.tokd +
+                                          a.heads * a.ntok + 16);
+      hipLaunchKernelGGL(k_ref_gru_gst, dim3(B), dim3(256), shm, s, a);
+      TT2_HIP(hipGetLastError());
+    }
+  }
+  hipLaunchKernelGGL(k_memory, dim3(BT), dim3(256), 0, s, c->enc_out.as<float>(), c->style.as<float>(), lens_d,
+                     c->values.as<float>(), B, T, 2 * c->U, c->SW);
+  TT2_HIP(hipGetLastError());
+  {
+    GemmArgs g;
+    g.M = BT; g.N = c->A; g.K = c->Dm; g.A = c->values.as<float>(); g.lda = c->Dm;
+    g.Bw = c->mem_k.as<float>(); g.ldb = c->A; g.Cout = c->keys.as<float>(); g.ldc = c->A;
+    gemm(g, s);
+  }
+  c->B = B;
+  c->T_in = T;
+  c->encoded = true;
+  c->decoded = false;
+}
+
+// ---------------------------------------------------------------- decode
+static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64_t seed,
+                             const float* targets_d, int T_lim, float* frames_d, float* stop_d, float* align_d) {
+  const auto& cfg = c->cfg;
+  DecArgs a;
+  a.ctl = c->ctl.as<DecCtl>();
+  a.B = c->B; a.T_in = c->T_in; a.max_iters = max_iters; a.T_lim = targets_d ? T_lim : 0;
+  a.nm = c->nm; a.P = c->P; a.H = c->H; a.Dm = c->Dm; a.A = c->A; a.F = c->F; a.KL = c->KL;
+  a.K1 = c->K1; a.K2 = c->K2; a.Kp = c->Kp;
+  a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
+  a.stop_at_any = cfg.stop_at_any; a.mask_encoder = cfg.mask_encoder; a.cumulative = cfg.cumulative_weights;
+  a.constraint = cfg.synthesis_constraint; a.monotonic = cfg.constraint_monotonic; a.win = cfg.attention_win_size;
+  a.pre_w1 = c->pre_w1.as<float>(); a.pre_b1 = c->pre_b1.as<float>();
+  a.pre_w2 = c->pre_w2.as<float>(); a.pre_b2 = c->pre_b2.as<float>();
+  a.l1_w = c->l1_w.as<float>(); a.l1_b = c->l1_b.as<float>(); a.l2_w = c->l2_w.as<float>(); a.l2_b = c->l2_b.as<float>();
+  a.q_w = c->q_w.as<float>(); a.loc_cw = c->loc_cw.as<float>(); a.loc_cb = c->loc_cb.as<float>();
+  a.loc_w = c->loc_w.as<float>(); a.va = c->va.as<float>(); a.ba = c->ba.as<float>();
+  a.proj_w = c->proj_w.as<float>(); a.proj_b = c->proj_b.as<float>();
+  a.keys = c->keys.as<float>(); a.values = c->values.as<float>(); a.lengths = c->lens.as<int>();
+  for (int p = 0; p < 2; ++p) { a.X1[p] = c->X1[p].as<float>(); a.X2[p] = c->X2[p].as<float>(); }
+  a.Xp = c->Xp.as<float>(); a.c1 = c->c1.as<float>(); a.c2 = c->c2.as<float>();
+  a.Qp = c->Qp.as<float>(); a.energy = c->energy.as<float>(); a.cum = c->cum.as<float>();
+  a.max_att = c->max_att.as<int>(); a.PP = c->PP.as<float>();
+  a.KSQ = c->KSQ; a.KSP = c->KSP; a.NPJ = c->NPJ;
+  a.masks = masks_d; a.seed = seed; a.targets = targets_d;
+  a.frames = frames_d; a.stop = stop_d; a.align = align_d;
+  return a;
+}
+
+static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, hipStream_t s) {
+  const int par = i & 1;
+  hipLaunchKernelGGL(k_prenet, dim3(c->P / 16), dim3(256), 0, s, a, i);
+  LstmArgs l1;
+  l1.ctl = a.ctl; l1.X = a.X1[par]; l1.K = c->K1; l1.hprev_off = c->P + c->Dm; l1.W = a.l1_w; l1.b = a.l1_b;
+  l1.c = a.c1; l1.H = c->H; l1.Xo = a.X2[par]; l1.ho_off = 0; l1.Xz = a.X1[par ^ 1]; l1.hz_off = c->P + c->Dm;
+  l1.zo = a.zo; l1.one_m_zo = a.one_m_zo;
+  hipLaunchKernelGGL(k_lstm, dim3(c->H / 4), dim3(256), 0, s, l1);
+  LstmArgs l2 = l1;
+  l2.X = a.X2[par]; l2.K = c->K2; l2.hprev_off = c->H; l2.W = a.l2_w; l2.b = a.l2_b; l2.c = a.c2;
+  l2.Xo = a.Xp; l2.ho_off = 0; l2.Xz = a.X2[par ^ 1]; l2.hz_off = c->H;
+  hipLaunchKernelGGL(k_lstm, dim3(c->H / 4), dim3(256), 0, s, l2);
+  PartArgs q;
+  q.ctl = a.ctl; q.X = a.Xp; q.K = c->H; q.W = a.q_w; q.out = a.Qp; q.ldo = c->A; q.ntile = c->A / 16; q.KS = c->KSQ;
+  hipLaunchKernelGGL(k_partial, dim3(q.ntile * q.KS), dim3(256), 0, s, q);
+  const size_t shm_e = sizeof(float) * (c->A + 32 + c->KL + 32 * (c->F + 1) + c->F * c->A);
+  hipLaunchKernelGGL(k_energy, dim3(a.B, cdiv(a.T_in, 32)), dim3(256), shm_e, s, a);
+  const size_t shm_s = sizeof(float) * (((a.T_in + 3) & ~3) + 256 * 4);
+  hipLaunchKernelGGL(k_softmax_ctx, dim3(a.B, cdiv(c->Dm, 64)), dim3(256), shm_s, s, a, i);
+  PartArgs p;
+  p.ctl = a.ctl; p.X = a.Xp; p.K = c->Kp; p.W = a.proj_w; p.out = a.PP; p.ldo = c->NPJ; p.ntile = c->NPJ / 16;
+  p.KS = c->KSP;
+  hipLaunchKernelGGL(k_partial, dim3(p.ntile * p.KS), dim3(256), 0, s, p);
+}
+
+static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64_t seed, const float* targets_d,
+                       int T_lim, float* frames_d, float* stop_d, float* align_d, hipStream_t s) {
+  TT2_CHECK(c->encoded, TT2_ERR_STATE, "tt2_decode called before tt2_encode");
+  TT2_CHECK(max_iters >= 1 && max_iters <= c->cfg.max_iters, TT2_ERR_SHAPE_MISMATCH, "max_iters exceeds capacity");
+  TT2_CHECK(!targets_d || T_lim >= 1, TT2_ERR_INVALID_ARG, "targets given with T_targets < 1");
+  // zero decoder state (zero_state, Architecture_wrappers.py:158-195; _go_frames helpers.py:136)
+  for (int p = 0; p < 2; ++p) {
+    TT2_HIP(hipMemsetAsync(c->X1[p].p, 0, c->X1[p].bytes, s));
+    TT2_HIP(hipMemsetAsync(c->X2[p].p, 0, c->X2[p].bytes, s));
+  }
+  TT2_HIP(hipMemsetAsync(c->Xp.p, 0, c->Xp.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->c1.p, 0, c->c1.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->c2.p, 0, c->c2.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->cum.p, 0, c->cum.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->max_att.p, 0, c->max_att.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->ctl.p, 0, sizeof(DecCtl), s));
+  const DecArgs a = make_dec_args(c, max_iters, masks_d, seed, targets_d, T_lim, frames_d, stop_d, align_d);
+  auto key = std::make_tuple(c->B, c->T_in, max_iters, T_lim, (const void*)masks_d, (const void*)targets_d, seed,
+                             (const void*)frames_d, (const void*)stop_d, (const void*)align_d);
+  if (!c->graph.exec || c->graph.key != key) {
+    if (c->graph.exec) (void)hipGraphExecDestroy(c->graph.exec);
+    c->graph.exec = nullptr;
+    hipStream_t cs;
+    TT2_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraph_t gr;
+    TT2_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < tt2_ctx::S; ++i) enqueue_step(c, a, i, cs);
+    hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, cs, a.ctl, tt2_ctx::S);
+    TT2_HIP(hipStreamEndCapture(cs, &gr));
+    TT2_HIP(hipGraphInstantiate(&c->graph.exec, gr, nullptr, nullptr, 0));
+    TT2_HIP(hipGraphDestroy(gr));
+    TT2_HIP(hipStreamDestroy(cs));
+    c->graph.key = key;
+  }
+  // launch chunks; watch the device `done` flag one chunk behind so the GPU never idles
+  const int max_chunks = (max_iters + 1 + tt2_ctx::S - 1) / tt2_ctx::S;
+  hipEvent_t ev[2];
+  TT2_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+  TT2_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  for (int ch = 0; ch < max_chunks; ++ch) {
+    TT2_HIP(hipGraphLaunch(c->graph.exec, s));
+    TT2_HIP(hipMemcpyAsync(&c->ctl_host[ch & 1], &c->ctl.as<DecCtl>()->done, sizeof(int), hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipEventRecord(ev[ch & 1], s));
+    if (ch >= 1) {
+      TT2_HIP(hipEventSynchronize(ev[(ch - 1) & 1]));
+      if (c->ctl_host[(ch - 1) & 1]) break;
+    }
+  }
+  TT2_HIP(hipEventDestroy(ev[0]));
+  TT2_HIP(hipEventDestroy(ev[1]));
+  DecCtl h;
+  TT2_HIP(hipMemcpyAsync(&h, c->ctl.p, sizeof(DecCtl), hipMemcpyDeviceToHost, s));
+  TT2_HIP(hipStreamSynchronize(s));
+  TT2_CHECK(h.done, TT2_ERR_STATE, "decoder did not terminate");
+  c->n_steps = h.n_steps;
+  c->last_max_iters = max_iters;
+  c->decoded = true;
+}
+
+// ---------------------------------------------------------------- postnet
+static void postnet_dev(tt2_ctx* c, const float* frames_d, long frames_bstride, int B, int T, float* dec_d,
+                        float* mel_d, hipStream_t s) {
+  const auto& cfg = c->cfg;
+  const float lo = cfg.symmetric_mels ? -cfg.max_abs_value - cfg.lower_bound_decay : 0.f - cfg.lower_bound_decay;
+  const float hi = cfg.max_abs_value;
+  const long n = (long)B * T * c->nm;
+  hipLaunchKernelGGL(k_clip_frames, dim3((unsigned)std::min<long>(cdiv((int)std::min<long>(n, 1L << 30), 256), 4096)),
+                     dim3(256), 0, s, frames_d, frames_bstride, dec_d, B, T, c->nm, lo, hi, cfg.clip_outputs);
+  TT2_HIP(hipGetLastError());
+  const float* xin = dec_d;
+  float* bufs[2] = {c->post_a.as<float>(), c->post_b.as<float>()};
+  int cin = c->nm;
+  for (int i = 0; i < cfg.postnet_num_layers; ++i) {
+    GemmArgs g;
+    g.M = B * T; g.N = c->PC; g.K = cfg.postnet_kernel_size * cin; g.a_mode = A_CONV1D; g.A = xin;
+    g.T = T; g.C = cin; g.kw = cfg.postnet_kernel_size; g.pad = (cfg.postnet_kernel_size - 1) / 2;
+    g.xs_b = (long)T * cin; g.xs_t = cin;
+    g.Bw = c->post_cw[i].as<float>(); g.ldb = c->PC; g.Cout = bufs[i & 1]; g.ldc = c->PC;
+    g.bias = c->post_cb[i].as<float>(); g.act = (i < cfg.postnet_num_layers - 1) ? ACT_TANH : ACT_NONE;
+    g.bn_scale = c->post_bs[i].as<float>(); g.bn_shift = c->post_bh[i].as<float>();
+    gemm(g, s);
+    xin = bufs[i & 1];
+    cin = c->PC;
+  }
+  GemmArgs g;
+  g.M = B * T; g.N = c->nm; g.K = c->PC; g.A = xin; g.lda = c->PC;
+  g.Bw = c->post_pw.as<float>(); g.ldb = c->nm; g.Cout = mel_d; g.ldc = c->nm; g.bias = c->post_pb.as<float>();
+  g.residual = dec_d; g.ldr = c->nm; g.clip = cfg.clip_outputs; g.clip_lo = lo; g.clip_hi = hi;
+  gemm(g, s);
+}
+
+}  // namespace tt2
+
+using namespace tt2;
+
+extern "C" {
+
+const char* tt2_last_error(void) { return g_last_error.c_str(); }
+const char* tt2_version(void) { return "libtt2 0.1 gfx950 fp32 (MFMA f32)"; }
+
+void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_ref, int max_iters) {
+  std::memset(c, 0, sizeof(*c));
+  c->num_mels = 80; c->n_symbols = 66; c->embedding_dim = 512; c->enc_conv_num_layers = 3;
+  c->enc_conv_kernel_size = 5; c->enc_conv_channels = 512; c->encoder_lstm_units = 256;
+  c->attention_dim = 128; c->attention_filters = 32; c->attention_kernel = 31; c->prenet_units = 256;
+  c->decoder_lstm_units = 1024; c->postnet_num_layers = 5; c->postnet_kernel_size = 5; c->postnet_channels = 512;
+  c->use_gst = 1; c->emt_only = 0; c->num_gst = 10; c->num_heads = 4; c->style_embed_depth = 256;
+  c->style_att_dim = 128; c->reference_depth = 128;
+  const int rf[6] = {32, 32, 64, 64, 128, 128};
+  for (int i = 0; i < 6; ++i) c->reference_filters[i] = rf[i];
+  c->zoneout = 0.1f; c->max_abs_value = 4.f; c->lower_bound_decay = 0.1f; c->symmetric_mels = 1;
+  c->clip_outputs = 1; c->stop_at_any = 0; c->mask_encoder = 1; c->cumulative_weights = 1;
+  c->synthesis_constraint = 0; c->constraint_monotonic = 0; c->attention_win_size = 7;
+  c->max_batch = max_batch; c->max_T_in = max_T_in; c->max_T_ref = max_T_ref; c->max_iters = max_iters;
+}
+
+tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
+  return guard([&] {
+    TT2_CHECK(cfg && out, TT2_ERR_INVALID_ARG, "tt2_create: null argument");
+    *out = nullptr;
+    int ndev = 0;
+    TT2_HIP(hipGetDeviceCount(&ndev));
+    TT2_CHECK(hip_device >= 0 && hip_device < ndev, TT2_ERR_INVALID_ARG, "tt2_create: bad device index");
+    TT2_CHECK(cfg->max_batch >= 1 && cfg->max_batch <= 32, TT2_ERR_INVALID_ARG, "max_batch must be in [1, 32]");
+    TT2_CHECK(cfg->max_T_in >= 1 && cfg->max_iters >= 1, TT2_ERR_INVALID_ARG, "capacities must be >= 1");
+    TT2_CHECK(cfg->num_mels <= 80 && cfg->num_mels >= 1, TT2_ERR_INVALID_ARG, "num_mels must be <= 80");
+    TT2_CHECK(cfg->prenet_units % 16 == 0 && cfg->prenet_units <= 256, TT2_ERR_INVALID_ARG,
+              "prenet_units must be a multiple of 16, <= 256");
+    TT2_CHECK(cfg->decoder_lstm_units % 16 == 0, TT2_ERR_INVALID_ARG, "decoder_lstm_units % 16 != 0");
+    TT2_CHECK(cfg->encoder_lstm_units % 16 == 0, TT2_ERR_INVALID_ARG, "encoder_lstm_units % 16 != 0");
+    TT2_CHECK(cfg->attention_dim % 16 == 0 && cfg->attention_dim >= 16, TT2_ERR_INVALID_ARG, "attention_dim % 16 != 0");
+    TT2_CHECK(cfg->attention_kernel % 2 == 1, TT2_ERR_INVALID_ARG, "attention_kernel must be odd");
+    auto c = std::make_unique<tt2_ctx>();
+    c->cfg = *cfg;
+    c->dev = hip_device;
+    TT2_HIP(hipSetDevice(hip_device));
+    TT2_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->nm = cfg->num_mels; c->E = cfg->embedding_dim; c->Cenc = cfg->enc_conv_channels; c->U = cfg->encoder_lstm_units;
+    c->A = cfg->attention_dim; c->F = cfg->attention_filters; c->KL = cfg->attention_kernel; c->P = cfg->prenet_units;
+    c->H = cfg->decoder_lstm_units; c->PC = cfg->postnet_channels;
+    c->nref = cfg->use_gst ? (cfg->emt_only ? 1 : 2) : 0;
+    c->SW = cfg->use_gst ? c->nref * cfg->style_embed_depth : 0;
+    c->Dm = 2 * c->U + c->SW;
+    TT2_CHECK(c->Dm % 64 == 0, TT2_ERR_INVALID_ARG, "memory width must be a multiple of 64");
+    TT2_CHECK(cfg->use_gst, TT2_ERR_INVALID_ARG, "use_gst=False (paper Tacotron-2 memory) is not built yet");
+    c->K1 = c->P + c->Dm + c->H; c->K2 = 2 * c->H; c->Kp = c->H + c->Dm;
+    c->NPJ = ((c->nm + 1 + 15) / 16) * 16;
+    alloc_acts(c.get());
+    *out = c.release();
+  });
+}
+
+void tt2_destroy(tt2_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->dev);
+  if (c->graph.exec) (void)hipGraphExecDestroy(c->graph.exec);
+  if (c->ctl_host) (void)hipHostFree(c->ctl_host);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;  // DevBuf destructors release the device buffers
+}
+
+tt2_status tt2_load_tensor(tt2_ctx* c, const char* name, const float* host, const int64_t* shape, int ndim) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    put_tensor(c->host, name, host, shape, ndim);
+    c->finalized = false;
+  });
+}
+
+tt2_status tt2_finalize_weights(tt2_ctx* c) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    finalize(c);
+  });
+}
+
+tt2_status tt2_encode(tt2_ctx* c, const int32_t* ids, const int32_t* lengths, int B, int T_in, const float* ref_emt,
+                      int T_ref_emt, const float* ref_spk, int T_ref_spk, float* memory_out, float* style_out) {
+  return guard([&] {
+    TT2_CHECK(c && ids && lengths, TT2_ERR_INVALID_ARG, "tt2_encode: null argument");
+    TT2_CHECK(B >= 1 && B <= c->cfg.max_batch, TT2_ERR_SHAPE_MISMATCH, "batch exceeds capacity");
+    TT2_CHECK(T_in >= 1 && T_in <= c->cfg.max_T_in, TT2_ERR_SHAPE_MISMATCH, "T_in exceeds capacity");
+    TT2_CHECK(!c->cfg.use_gst || (ref_emt && (c->nref < 2 || ref_spk)), TT2_ERR_INVALID_ARG,
+              "must provide references");  // tacotron.py:66-67
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = c->stream;
+    TT2_HIP(hipMemcpyAsync(c->ids.p, ids, sizeof(int) * B * T_in, hipMemcpyHostToDevice, s));
+    TT2_HIP(hipMemcpyAsync(c->lens.p, lengths, sizeof(int) * B, hipMemcpyHostToDevice, s));
+    const float* refs[2] = {ref_emt, ref_spk};
+    const int trs[2] = {T_ref_emt, T_ref_spk};
+    const float* ref_d[2] = {nullptr, nullptr};
+    for (int r = 0; r < c->nref; ++r) {
+      TT2_CHECK(trs[r] >= 1 && trs[r] <= c->cfg.max_T_ref, TT2_ERR_SHAPE_MISMATCH, "T_ref exceeds capacity");
+      TT2_HIP(hipMemcpyAsync(c->refm[r].p, refs[r], sizeof(float) * B * trs[r] * c->nm, hipMemcpyHostToDevice, s));
+      ref_d[r] = c->refm[r].as<float>();
+    }
+    encode_dev(c, c->ids.as<int>(), c->lens.as<int>(), lengths, B, T_in, ref_d, trs, s);
+    if (memory_out)
+      TT2_HIP(hipMemcpyAsync(memory_out, c->values.p, sizeof(float) * B * T_in * c->Dm, hipMemcpyDeviceToHost, s));
+    if (style_out && c->SW)
+      for (int b = 0; b < B; ++b)
+        TT2_HIP(hipMemcpyAsync(style_out + (size_t)b * c->SW, c->style.as<float>() + (size_t)b * c->SW,
+                               sizeof(float) * c->SW, hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipStreamSynchronize(s));
+  });
+}
+
+tt2_status tt2_decode(tt2_ctx* c, int max_iters, const uint8_t* prenet_masks, uint64_t seed, const float* targets,
+                      int T_targets, float* frames, float* stop, float* align, int32_t* n_steps) {
+  return guard([&] {
+    TT2_CHECK(c && frames && stop && n_steps, TT2_ERR_INVALID_ARG, "tt2_decode: null argument");
+    TT2_CHECK(c->encoded, TT2_ERR_STATE, "tt2_decode called before tt2_encode");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = c->stream;
+    const int B = c->B;
+    const uint8_t* masks_d = nullptr;
+    if (prenet_masks) {
+      const size_t n = (size_t)max_iters * 2 * B * c->P;
+      c->masks.alloc(n);
+      TT2_HIP(hipMemcpyAsync(c->masks.p, prenet_masks, n, hipMemcpyHostToDevice, s));
+      masks_d = c->masks.as<uint8_t>();
+    }
+    const float* tg_d = nullptr;
+    if (targets) {
+      TT2_CHECK(T_targets >= 1, TT2_ERR_INVALID_ARG, "T_targets must be >= 1");
+      const size_t n = (size_t)B * T_targets * c->nm * sizeof(float);
+      c->targets.alloc(n);
+      TT2_HIP(hipMemcpyAsync(c->targets.p, targets, n, hipMemcpyHostToDevice, s));
+      tg_d = c->targets.as<float>();
+    }
+    decode_dev(c, max_iters, masks_d, seed, tg_d, T_targets, c->frames.as<float>(), c->stop.as<float>(),
+               align ? c->align.as<float>() : nullptr, s);
+    const int n = c->n_steps;
+    *n_steps = n;
+    for (int b = 0; b < B; ++b) {
+      TT2_HIP(hipMemcpyAsync(frames + (size_t)b * max_iters * c->nm, c->frames.as<float>() + (size_t)b * max_iters * c->nm,
+                             sizeof(float) * n * c->nm, hipMemcpyDeviceToHost, s));
+      TT2_HIP(hipMemcpyAsync(stop + (size_t)b * max_iters, c->stop.as<float>() + (size_t)b * max_iters,
+                             sizeof(float) * n, hipMemcpyDeviceToHost, s));
+    }
+    if (align)
+      TT2_HIP(hipMemcpyAsync(align, c->align.p, sizeof(float) * B * c->T_in * max_iters, hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipStreamSynchronize(s));
+  });
+}
+
+tt2_status tt2_postnet(tt2_ctx* c, const float* frames_in, int B, int T, float* decoder_output, float* mel_out) {
+  return guard([&] {
+    TT2_CHECK(c && mel_out, TT2_ERR_INVALID_ARG, "tt2_postnet: null argument");
+    TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_finalize_weights not called");
+    TT2_CHECK(B >= 1 && B <= c->cfg.max_batch && T >= 1 && T <= c->cfg.max_iters, TT2_ERR_SHAPE_MISMATCH,
+              "postnet: shape exceeds capacity");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = c->stream;
+    const float* src;
+    long bstride;
+    if (frames_in) {
+      // stage caller frames in post_a: the clip kernel moves them to `dec` before conv 1 reuses post_a
+      TT2_CHECK((size_t)B * T * c->nm * 4 <= c->post_a.bytes, TT2_ERR_SHAPE_MISMATCH, "postnet staging too small");
+      TT2_HIP(hipMemcpyAsync(c->post_a.p, frames_in, sizeof(float) * B * T * c->nm, hipMemcpyHostToDevice, s));
+      src = c->post_a.as<float>();
+      bstride = (long)T * c->nm;
+    } else {
+      TT2_CHECK(c->decoded, TT2_ERR_STATE, "tt2_postnet(NULL) called before tt2_decode");
+      TT2_CHECK(B == c->B && T == c->n_steps, TT2_ERR_SHAPE_MISMATCH, "postnet shape differs from last decode");
+      src = c->frames.as<float>();
+      bstride = (long)c->last_max_iters * c->nm;
+    }
+    postnet_dev(c, src, bstride, B, T, c->dec.as<float>(), c->mel.as<float>(), s);
+    if (decoder_output)
+      TT2_HIP(hipMemcpyAsync(decoder_output, c->dec.p, sizeof(float) * B * T * c->nm, hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipMemcpyAsync(mel_out, c->mel.p, sizeof(float) * B * T * c->nm, hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipStreamSynchronize(s));
+  });
+}
+
+tt2_status tt2_synthesize_dev(tt2_ctx* c, const int32_t* ids_d, const int32_t* lengths_d, const int32_t* lengths_host,
+                              int B, int T_in, const float* ref_emt_d, int T_ref_emt, const float* ref_spk_d,
+                              int T_ref_spk, int max_iters, const uint8_t* prenet_masks_d, uint64_t seed,
+                              float* mel_d, float* stop_d, int32_t* n_steps_host, void* stream) {
+  return guard([&] {
+    TT2_CHECK(c && ids_d && lengths_d && lengths_host && mel_d && n_steps_host, TT2_ERR_INVALID_ARG,
+              "tt2_synthesize_dev: null argument");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    TT2_HIP(hipMemcpyAsync(c->lens.p, lengths_d, sizeof(int) * B, hipMemcpyDeviceToDevice, s));
+    const float* ref_d[2] = {ref_emt_d, ref_spk_d};
+    const int trs[2] = {T_ref_emt, T_ref_spk};
+    encode_dev(c, ids_d, c->lens.as<int>(), lengths_host, B, T_in, ref_d, trs, s);
+    decode_dev(c, max_iters, prenet_masks_d, seed, nullptr, 0, c->frames.as<float>(),
+               stop_d ? stop_d : c->stop.as<float>(), nullptr, s);
+    postnet_dev(c, c->frames.as<float>(), (long)max_iters * c->nm, B, c->n_steps, c->dec.as<float>(), mel_d, s);
+    *n_steps_host = c->n_steps;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,167 @@
+"""Tacotron (code/tacotron/models/tacotron.py:25-680), synthesis path on MI355X.
+
+``Tacotron.initialize`` keeps the reference's signature and argument validation but runs eagerly:
+instead of building a TF graph it executes encoder → decoder loop → Postnet through libtt2.so and
+stores numpy arrays in the reference's ``tower_*`` attributes (one list entry per tower).
+Training (is_training=True, losses, optimizer) is not on this path.
+"""
+import os
+
+import numpy as np
+
+from tt2.engine import TacotronEngine
+from tt2.weights import init_tacotron_weights
+
+
+def split_func(x, split_pos):
+    """tacotron.py:16-23: un-concatenate the time-axis-packed multi-tower batch."""
+    rst = []
+    start = 0
+    for i in range(split_pos.shape[0]):
+        rst.append(x[:, start:start + split_pos[i]])
+        start += split_pos[i]
+    return rst
+
+
+class Tacotron():
+    """Tacotron-2 Feature prediction Model."""
+
+    def __init__(self, hparams):
+        self._hparams = hparams
+        self._weights = None
+        self._engine = None
+        self.device = int(os.environ.get("LOCAL_RANK", "0")) if "TT2_DEVICE" not in os.environ \
+            else int(os.environ["TT2_DEVICE"])
+
+    # -- weights (replaces tf.train.Saver.restore, tacotron/synthesizer.py:93-94) -------------
+    def load_weights(self, weights):
+        """weights: dict {TF variable name: array} or path to a .npz with those keys."""
+        if isinstance(weights, str):
+            with np.load(weights, allow_pickle=False) as z:
+                weights = {k: z[k] for k in z.files}
+        self._weights = dict(weights)
+        self._engine = None
+
+    def init_random_weights(self, seed=None, emt_only=False):
+        hp = self._hparams
+        self.load_weights(init_tacotron_weights(
+            hp, hp.tacotron_random_seed if seed is None else seed, emt_only))
+
+    def _get_engine(self, B, T_in, T_ref, max_iters, emt_only, constraint):
+        if self._weights is None:
+            raise RuntimeError("Tacotron weights not loaded: call load_weights() (checkpoint) or "
+                               "init_random_weights()")
+        e = self._engine
+        if (e is None or not e.fits(B, T_in, T_ref, max_iters) or e.emt_only != emt_only
+                or e.cfg.synthesis_constraint != int(constraint)):
+            if e is not None:
+                e.close()
+            self._engine = None
+            e = TacotronEngine(self._hparams, self._weights, max(B, 1), T_in, max(T_ref, 1),
+                               max_iters, self.device, emt_only, constraint)
+            self._engine = e
+        return e
+
+    def initialize(self, args, inputs, input_lengths, mel_targets=None, stop_token_targets=None,
+                   linear_targets=None, targets_lengths=None, gta=False, global_step=None,
+                   is_training=False, is_evaluating=False, split_infos=None, emt_labels=None,
+                   spk_labels=None, emt_up_labels=None, spk_up_labels=None, spk_emb=None,
+                   ref_mel_emt=None, ref_mel_spk=None, ref_mel_up_emt=None, ref_mel_up_spk=None,
+                   use_emt_disc=False, use_spk_disc=False, use_intercross=False,
+                   use_unpaired=False, n_emt=None, n_spk=None, synth=False,
+                   prenet_masks=None, seed=0):
+        """Same arguments as the reference (tacotron.py:31-35) plus the injected prenet dropout
+        keep-masks ``prenet_masks`` [max_iters, 2, B, 256] (None = device RNG keyed by ``seed``)."""
+        hp = self._hparams
+        # argument validation, tacotron.py:48-71
+        if mel_targets is None and stop_token_targets is not None:
+            raise ValueError('no multi targets were provided but token_targets were given')
+        if mel_targets is not None and stop_token_targets is None and not gta:
+            raise ValueError('Mel targets are provided without corresponding token_targets')
+        if not gta and hp.predict_linear == True and linear_targets is None and is_training:
+            raise ValueError('Model is set to use post processing to predict linear spectrograms '
+                             'in training but no linear targets given!')
+        if gta and linear_targets is not None:
+            raise ValueError('Linear spectrogram prediction is not supported in GTA mode!')
+        if is_training and hp.mask_decoder and targets_lengths is None:
+            raise RuntimeError('Model set to mask paddings but no targets lengths provided for the mask!')
+        if is_training and is_evaluating:
+            raise RuntimeError('Model can not be in training and evaluation modes at the same time!')
+        if hp.tacotron_use_style_emb_disc and (n_emt == None or n_spk == None):
+            raise ValueError('must specify number of emotions and number of speakers!')
+        if use_unpaired and not (hp.tacotron_use_style_emb_disc):
+            raise ValueError('trying to use unpaired ')
+        if getattr(args, "nat_gan", False) and not (getattr(args, "unpaired", False)):
+            print("USING NATURALNESS GAN WITHOUT UNPAIRED SAMPLES")
+        if ref_mel_emt is None and ref_mel_spk is None:
+            raise ValueError("must provide references")
+        adain = getattr(args, "adain", False)
+        emt_only = bool(getattr(args, "emt_only", False))
+        if adain and (emt_only or getattr(args, "unpaired", False)):
+            raise ValueError("must provide speaker reference to use AdaIn and Unpaired with AddIn "
+                             "not implemented")
+        if use_unpaired and not (getattr(args, "pretrained_emb_disc_all", False)):
+            raise ValueError('must use unpaired with pretrained_emb_disc_all')
+        # scope of the MI355X path
+        if is_training or is_evaluating:
+            raise NotImplementedError("training / eval-loss graphs are not on the synthesis path "
+                                      "(SURVEY.md §8f rank 1)")
+        if adain or getattr(args, "pretrained_emb_disc_all", False) or use_unpaired:
+            raise NotImplementedError("adain / pretrained_emb_disc_all / unpaired style paths are "
+                                      "not built; the fork default GST path is")
+        if not hp.use_gst:
+            raise NotImplementedError("use_gst=False is not built")
+        if ref_mel_spk is None and not emt_only:
+            raise ValueError("must provide references")
+        constraint = bool(getattr(args, "synth_constraint", False))
+
+        inputs = np.asarray(inputs, np.int32)
+        input_lengths = np.asarray(input_lengths, np.int32).reshape(-1)
+        ntow = hp.tacotron_num_gpus
+        # split towers exactly as the reference packs them (tacotron.py:83-138)
+        if split_infos is not None and ntow > 1:
+            split_infos = np.asarray(split_infos, np.int32)
+            tower_inputs = split_func(inputs, split_infos[:, 0])
+            tower_ref_emt = split_func(np.asarray(ref_mel_emt, np.float32), split_infos[:, 5])
+            tower_ref_spk = (split_func(np.asarray(ref_mel_spk, np.float32), split_infos[:, 6])
+                             if ref_mel_spk is not None else [None] * ntow)
+            tower_targets = (split_func(np.asarray(mel_targets, np.float32), split_infos[:, 1])
+                             if mel_targets is not None else [None] * ntow)
+            tower_lengths = np.split(input_lengths, ntow)
+        else:
+            tower_inputs, tower_lengths = [inputs], [input_lengths]
+            tower_ref_emt = [np.asarray(ref_mel_emt, np.float32)]
+            tower_ref_spk = [np.asarray(ref_mel_spk, np.float32) if ref_mel_spk is not None else None]
+            tower_targets = [np.asarray(mel_targets, np.float32) if mel_targets is not None else None]
+
+        self.tower_decoder_output = []
+        self.tower_alignments = []
+        self.tower_stop_token_prediction = []
+        self.tower_mel_outputs = []
+        self.tower_encoder_outputs = []
+        self.tower_style_embeddings = []
+        self.tower_inputs = tower_inputs
+        self.tower_input_lengths = tower_lengths
+        self.tower_mel_targets = [t for t in tower_targets if t is not None]
+        self.tower_ref_mel_emt = tower_ref_emt
+        self.tower_ref_mel_spk = tower_ref_spk
+        max_iters = hp.max_iters
+        for i in range(len(tower_inputs)):
+            ids = np.ascontiguousarray(tower_inputs[i].reshape(tower_lengths[i].shape[0], -1))
+            B, T_in = ids.shape
+            ref_e = tower_ref_emt[i].reshape(B, -1, hp.num_mels)
+            ref_s = None if tower_ref_spk[i] is None else tower_ref_spk[i].reshape(B, -1, hp.num_mels)
+            T_ref = max(ref_e.shape[1], ref_s.shape[1] if ref_s is not None else 0)
+            tg = None
+            if gta and tower_targets[i] is not None:
+                tg = tower_targets[i].reshape(B, -1, hp.num_mels)[:, hp.outputs_per_step - 1::hp.outputs_per_step]
+            eng = self._get_engine(B, T_in, T_ref, max_iters, emt_only, constraint)
+            masks = prenet_masks if i == 0 or prenet_masks is None else prenet_masks
+            out = eng.synthesize(ids, tower_lengths[i], ref_e, ref_s, max_iters, masks, seed, tg)
+            self.tower_decoder_output.append(out["decoder_output"])
+            self.tower_alignments.append(out["alignments"])
+            self.tower_stop_token_prediction.append(out["stop_token_prediction"])
+            self.tower_mel_outputs.append(out["mel_outputs"])
+            self.tower_encoder_outputs.append(out["encoder_outputs"])
+            self.tower_style_embeddings.append(out["style"][:, None, :])
+        self.all_vars = list(self._weights.keys())

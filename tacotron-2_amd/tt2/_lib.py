@@ -1,0 +1,134 @@
+"""ctypes binding of libtt2.so (include/tt2.h).
+
+There is no CPU fallback: if the HIP library is missing or fails to load, every model call raises
+``TT2NotBuilt``.  Build it with ``make -C tacotron-2_amd`` (or ``__graft_entry__.build()``).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libtt2.so")
+
+TT2_OK = 0
+_STATUS = {-1: "INVALID_ARG", -2: "SHAPE_MISMATCH", -3: "OOM", -4: "HIP_ERROR", -5: "NOT_LOADED",
+           -6: "STATE"}
+
+
+class TT2Error(RuntimeError):
+    """A libtt2 call failed; ``status`` is the tt2_status code."""
+
+    def __init__(self, status, msg):
+        super().__init__("{} ({}): {}".format(_STATUS.get(status, "ERROR"), status, msg))
+        self.status = status
+
+
+class TT2NotBuilt(RuntimeError):
+    pass
+
+
+class Config(ctypes.Structure):
+    """tt2_config (include/tt2.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "num_mels", "n_symbols", "embedding_dim", "enc_conv_num_layers", "enc_conv_kernel_size",
+        "enc_conv_channels", "encoder_lstm_units", "attention_dim", "attention_filters",
+        "attention_kernel", "prenet_units", "decoder_lstm_units", "postnet_num_layers",
+        "postnet_kernel_size", "postnet_channels", "use_gst", "emt_only", "num_gst", "num_heads",
+        "style_embed_depth", "style_att_dim", "reference_depth")] + [
+        ("reference_filters", ctypes.c_int * 6),
+        ("zoneout", ctypes.c_float), ("max_abs_value", ctypes.c_float),
+        ("lower_bound_decay", ctypes.c_float)] + [(n, ctypes.c_int) for n in (
+            "symmetric_mels", "clip_outputs", "stop_at_any", "mask_encoder", "cumulative_weights",
+            "synthesis_constraint", "constraint_monotonic", "attention_win_size", "max_batch",
+            "max_T_in", "max_T_ref", "max_iters")]
+
+
+class WnConfig(ctypes.Structure):
+    """tt2_wn_config (include/tt2.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "layers", "stacks", "residual_channels", "gate_channels", "skip_out_channels",
+        "kernel_size", "cin_channels", "out_channels", "legacy", "residual_legacy")] + [
+        ("log_scale_min", ctypes.c_float), ("n_upsample", ctypes.c_int),
+        ("upsample_scales", ctypes.c_int * 8), ("freq_axis_kernel_size", ctypes.c_int),
+        ("max_batch", ctypes.c_int), ("max_samples", ctypes.c_int64)]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_U64 = ctypes.c_uint64
+_F = ctypes.c_float
+
+#: every symbol include/tt2.h declares, with (restype, argtypes)
+SIGNATURES = {
+    "tt2_last_error": (ctypes.c_char_p, []),
+    "tt2_version": (ctypes.c_char_p, []),
+    "tt2_default_config": (None, [ctypes.POINTER(Config), _I, _I, _I, _I]),
+    "tt2_create": (_I, [ctypes.POINTER(Config), _I, ctypes.POINTER(_P)]),
+    "tt2_destroy": (None, [_P]),
+    "tt2_load_tensor": (_I, [_P, ctypes.c_char_p, _P, _P, _I]),
+    "tt2_finalize_weights": (_I, [_P]),
+    "tt2_encode": (_I, [_P, _P, _P, _I, _I, _P, _I, _P, _I, _P, _P]),
+    "tt2_decode": (_I, [_P, _I, _P, _U64, _P, _I, _P, _P, _P, _P]),
+    "tt2_postnet": (_I, [_P, _P, _I, _I, _P, _P]),
+    "tt2_synthesize_dev": (_I, [_P, _P, _P, _P, _I, _I, _P, _I, _P, _I, _I, _P, _U64, _P, _P, _P,
+                                _P]),
+    "tt2_wn_default_config": (None, [ctypes.POINTER(WnConfig), _I, ctypes.c_int64]),
+    "tt2_wn_create": (_I, [ctypes.POINTER(WnConfig), _I, ctypes.POINTER(_P)]),
+    "tt2_wn_destroy": (None, [_P]),
+    "tt2_wn_load_tensor": (_I, [_P, ctypes.c_char_p, _P, _P, _I]),
+    "tt2_wn_finalize": (_I, [_P]),
+    "tt2_wn_generate": (_I, [_P, _P, _I, _I, _P, _P, _U64, _P, _P, _P, _P, _P]),
+    "tt2_wn_generate_dev": (_I, [_P, _P, _I, _I, _P, _P, _U64, _P, _P, _P, _P, _P]),
+    "tt2_mol_sample": (_I, [_P, _P, _P, _I, _I, _F, _P, _P]),
+}
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libtt2.so (once).  Raises TT2NotBuilt if it is absent or unloadable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise TT2NotBuilt("HIP library not built: {} is missing (run `make -C tacotron-2_amd`)"
+                          .format(path))
+    try:
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:
+        raise TT2NotBuilt("failed to load {}: {}".format(path, e))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status):
+    if status != TT2_OK:
+        msg = load_library().tt2_last_error()
+        raise TT2Error(status, msg.decode() if msg else "")
+
+
+def ptr(a):
+    """Pointer of a C-contiguous numpy array (or None)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def f32(a):
+    return None if a is None else np.ascontiguousarray(a, dtype=np.float32)
+
+
+def i32(a):
+    return None if a is None else np.ascontiguousarray(a, dtype=np.int32)
+
+
+def load_tensor(fn, handle, name, arr):
+    arr = np.ascontiguousarray(arr, dtype=np.float32)
+    shape = (ctypes.c_int64 * max(arr.ndim, 1))(*arr.shape)
+    check(fn(handle, name.encode(), ptr(arr), ctypes.cast(shape, ctypes.c_void_p), arr.ndim))

@@ -1,0 +1,243 @@
+"""Host engines over libtt2.so: one context per (process, device), weights uploaded once.
+
+``TacotronEngine`` / ``WaveNetEngine`` hold the C-ABI handles; the reference-named classes in
+``tacotron.models`` / ``wavenet_vocoder.models`` are thin eager front-ends over them.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, f32, i32, ptr
+from .hparams import get_hop_size
+from .weights import memory_width
+
+
+def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=False,
+                    synthesis_constraint=False):
+    """tt2_config from hparams (names mirror code/hparams.py)."""
+    lib = _lib.load_library()
+    cfg = _lib.Config()
+    lib.tt2_default_config(ctypes.byref(cfg), max_batch, max_T_in, max_T_ref, max_iters)
+    cfg.num_mels = hp.num_mels
+    cfg.embedding_dim = hp.embedding_dim
+    cfg.enc_conv_num_layers = hp.enc_conv_num_layers
+    cfg.enc_conv_kernel_size = hp.enc_conv_kernel_size[0]
+    cfg.enc_conv_channels = hp.enc_conv_channels
+    cfg.encoder_lstm_units = hp.encoder_lstm_units
+    cfg.attention_dim = hp.attention_dim
+    cfg.attention_filters = hp.attention_filters
+    cfg.attention_kernel = hp.attention_kernel[0]
+    if len(hp.prenet_layers) != 2 or hp.prenet_layers[0] != hp.prenet_layers[1]:
+        raise NotImplementedError("prenet_layers must be two equal widths on this build")
+    cfg.prenet_units = hp.prenet_layers[0]
+    if hp.decoder_layers != 2:
+        raise NotImplementedError("decoder_layers must be 2 on this build")
+    cfg.decoder_lstm_units = hp.decoder_lstm_units
+    cfg.postnet_num_layers = hp.postnet_num_layers
+    cfg.postnet_kernel_size = hp.postnet_kernel_size[0]
+    cfg.postnet_channels = hp.postnet_channels
+    cfg.use_gst = 1 if hp.use_gst else 0
+    cfg.emt_only = 1 if emt_only else 0
+    cfg.num_gst = hp.num_gst
+    cfg.num_heads = hp.num_heads
+    cfg.style_embed_depth = hp.style_embed_depth
+    cfg.style_att_dim = hp.style_att_dim
+    cfg.reference_depth = hp.reference_depth
+    for i, f in enumerate(hp.reference_filters):
+        cfg.reference_filters[i] = f
+    cfg.zoneout = hp.tacotron_zoneout_rate
+    cfg.max_abs_value = hp.max_abs_value
+    cfg.lower_bound_decay = hp.lower_bound_decay
+    cfg.symmetric_mels = 1 if hp.symmetric_mels else 0
+    cfg.clip_outputs = 1 if hp.clip_outputs else 0
+    cfg.stop_at_any = 1 if hp.stop_at_any else 0
+    cfg.mask_encoder = 1 if hp.mask_encoder else 0
+    cfg.cumulative_weights = 1 if hp.cumulative_weights else 0
+    cfg.synthesis_constraint = 1 if synthesis_constraint else 0
+    cfg.constraint_monotonic = 1 if hp.synthesis_constraint_type == "monotonic" else 0
+    cfg.attention_win_size = hp.attention_win_size
+    if hp.outputs_per_step != 1:
+        raise NotImplementedError("outputs_per_step (r) must be 1 on this build (hparams.py:140)")
+    if hp.smoothing:
+        raise NotImplementedError("smoothing attention normalisation is not built")
+    return cfg
+
+
+class TacotronEngine(object):
+    """Owns one tt2_ctx."""
+
+    def __init__(self, hp, weights, max_batch, max_T_in, max_T_ref, max_iters, device=0,
+                 emt_only=False, synthesis_constraint=False):
+        self.lib = _lib.load_library()
+        self.hp = hp
+        self.emt_only = emt_only
+        self.cfg = tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only,
+                                   synthesis_constraint)
+        self.caps = (max_batch, max_T_in, max_T_ref, max_iters)
+        self.D = memory_width(hp, emt_only)
+        h = ctypes.c_void_p()
+        check(self.lib.tt2_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
+        self.h = h
+        for name, arr in weights.items():
+            if name.startswith("Tacotron_model/"):
+                _lib.load_tensor(self.lib.tt2_load_tensor, self.h, name, arr)
+        check(self.lib.tt2_finalize_weights(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tt2_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def fits(self, B, T_in, T_ref, max_iters):
+        c = self.caps
+        return B <= c[0] and T_in <= c[1] and T_ref <= c[2] and max_iters <= c[3]
+
+    def encode(self, ids, lengths, ref_emt, ref_spk):
+        ids = i32(ids)
+        lengths = i32(lengths)
+        B, T = ids.shape
+        ref_emt = f32(ref_emt)
+        ref_spk = f32(ref_spk) if ref_spk is not None else None
+        mem = np.zeros((B, T, self.D), np.float32)
+        sw = self.D - 2 * self.hp.encoder_lstm_units
+        style = np.zeros((B, max(sw, 1)), np.float32)
+        check(self.lib.tt2_encode(self.h, ptr(ids), ptr(lengths), B, T, ptr(ref_emt),
+                                  ref_emt.shape[1], ptr(ref_spk),
+                                  ref_spk.shape[1] if ref_spk is not None else 0, ptr(mem),
+                                  ptr(style)))
+        return mem, style[:, :sw]
+
+    def decode(self, max_iters, prenet_masks=None, seed=0, targets=None):
+        B = self._B
+        masks = None if prenet_masks is None else np.ascontiguousarray(prenet_masks, np.uint8)
+        if masks is not None and masks.shape[0] < max_iters:
+            raise ValueError("prenet_masks must cover max_iters steps")
+        if masks is not None:
+            masks = np.ascontiguousarray(masks[:max_iters])
+        tg = f32(targets)
+        frames = np.zeros((B, max_iters, self.hp.num_mels), np.float32)
+        stop = np.zeros((B, max_iters), np.float32)
+        align = np.zeros((B, self._T_in, max_iters), np.float32)
+        n = ctypes.c_int32()
+        check(self.lib.tt2_decode(self.h, max_iters, ptr(masks), seed, ptr(tg),
+                                  tg.shape[1] if tg is not None else 0, ptr(frames), ptr(stop),
+                                  ptr(align), ctypes.byref(n)))
+        n = n.value
+        return frames[:, :n], stop[:, :n], align[:, :, :n]
+
+    def postnet(self, frames=None, B=None, T=None):
+        if frames is not None:
+            frames = f32(frames)
+            B, T = frames.shape[:2]
+        dec = np.zeros((B, T, self.hp.num_mels), np.float32)
+        mel = np.zeros((B, T, self.hp.num_mels), np.float32)
+        check(self.lib.tt2_postnet(self.h, ptr(frames), B, T, ptr(dec), ptr(mel)))
+        return dec, mel
+
+    def synthesize(self, ids, lengths, ref_emt, ref_spk, max_iters, prenet_masks=None, seed=0,
+                   targets=None):
+        """encode → decode → postnet; returns the tower_* outputs of one tower."""
+        ids = i32(ids)
+        self._B, self._T_in = ids.shape
+        mem, style = self.encode(ids, lengths, ref_emt, ref_spk)
+        frames, stop, align = self.decode(max_iters, prenet_masks, seed, targets)
+        dec, mel = self.postnet(None, self._B, frames.shape[1])
+        return dict(encoder_outputs=mem, style=style, decoder_output=dec, mel_outputs=mel,
+                    stop_token_prediction=stop, alignments=align, frames=frames)
+
+
+def wavenet_config(hp, max_batch, max_samples):
+    lib = _lib.load_library()
+    cfg = _lib.WnConfig()
+    lib.tt2_wn_default_config(ctypes.byref(cfg), max_batch, max_samples)
+    cfg.layers = hp.layers
+    cfg.stacks = hp.stacks
+    cfg.residual_channels = hp.residual_channels
+    cfg.gate_channels = hp.gate_channels
+    cfg.skip_out_channels = hp.skip_out_channels
+    cfg.kernel_size = hp.kernel_size
+    cfg.cin_channels = hp.cin_channels
+    cfg.out_channels = hp.out_channels
+    cfg.legacy = 1 if hp.legacy else 0
+    cfg.residual_legacy = 1 if hp.residual_legacy else 0
+    cfg.log_scale_min = hp.log_scale_min
+    if hp.upsample_type != "2D":
+        raise NotImplementedError("upsample_type {!r} is not built (only '2D', paper_hparams)"
+                                  .format(hp.upsample_type))
+    cfg.n_upsample = len(hp.upsample_scales)
+    for i, s in enumerate(hp.upsample_scales):
+        cfg.upsample_scales[i] = s
+    cfg.freq_axis_kernel_size = hp.freq_axis_kernel_size
+    prod = int(np.prod(hp.upsample_scales))
+    if prod != get_hop_size(hp):
+        raise ValueError("prod(upsample_scales)={} != hop_size={} (hparams.py:241 asserts this)"
+                         .format(prod, get_hop_size(hp)))
+    return cfg
+
+
+class WaveNetEngine(object):
+    """Owns one tt2_wn_ctx."""
+
+    def __init__(self, hp, weights, max_batch, max_samples, device=0):
+        self.lib = _lib.load_library()
+        self.hp = hp
+        self.cfg = wavenet_config(hp, max_batch, max_samples)
+        self.caps = (max_batch, max_samples)
+        self.hop = int(np.prod(hp.upsample_scales))
+        h = ctypes.c_void_p()
+        check(self.lib.tt2_wn_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
+        self.h = h
+        for name, arr in weights.items():
+            if name.startswith("WaveNet_model/"):
+                _lib.load_tensor(self.lib.tt2_wn_load_tensor, self.h, name, arr)
+        check(self.lib.tt2_wn_finalize(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tt2_wn_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def fits(self, B, T):
+        return B <= self.caps[0] and T <= self.caps[1]
+
+    def generate(self, cond, u_mix=None, u_log=None, seed=0, teacher=None, want_logits=False,
+                 want_upsampled=False):
+        """cond [B, T_f, cin] (clipped + interp'd).  Returns dict(y [B,T], k [B,T], logits?,
+        upsampled? [B, cin, T])."""
+        cond = f32(cond)
+        B, T_f, F = cond.shape
+        T = T_f * self.hop
+        nr = self.hp.out_channels // 3
+        um, ul, tg = f32(u_mix), f32(u_log), f32(teacher)
+        if um is not None and um.shape != (T, B, nr):
+            raise ValueError("u_mix must be [T, B, nr_mix] = {}".format((T, B, nr)))
+        if ul is not None and ul.shape != (T, B):
+            raise ValueError("u_log must be [T, B]")
+        if tg is not None and tg.shape != (B, T):
+            raise ValueError("teacher (test_inputs) must be [B, T]")
+        y = np.zeros((B, T), np.float32)
+        k = np.zeros((B, T), np.int32)
+        lg = np.zeros((B, T, self.hp.out_channels), np.float32) if want_logits else None
+        up = np.zeros((B, F, T), np.float32) if want_upsampled else None
+        check(self.lib.tt2_wn_generate(self.h, ptr(cond), B, T_f, ptr(um), ptr(ul), seed, ptr(tg),
+                                       ptr(y), ptr(k), ptr(lg), ptr(up)))
+        return dict(y=y, k=k, logits=lg, upsampled=up)
+
+
+def mol_sample(logits, u_mix, u_log, log_scale_min):
+    """tt2_mol_sample: logits [n, 3*nr], u_mix [n, nr], u_log [n] -> (x [n], k [n])."""
+    lib = _lib.load_library()
+    logits = f32(logits)
+    u_mix = f32(u_mix)
+    u_log = f32(u_log)
+    n, C = logits.shape
+    x = np.zeros((n,), np.float32)
+    k = np.zeros((n,), np.int32)
+    check(lib.tt2_mol_sample(ptr(logits), ptr(u_mix), ptr(u_log), n, C // 3, log_scale_min,
+                             ptr(x), ptr(k)))
+    return x, k

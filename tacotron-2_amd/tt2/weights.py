@@ -1,0 +1,207 @@
+"""Canonical weight key space (the reference's TF variable names) and seeded random init.
+
+The reference ships no trained Tacotron/WaveNet checkpoints, so benchmarks and
+parity tests run on random-init weights of the reference architecture.  Names follow the TF
+variable scopes the reference builds (``Tacotron_model/inference/...`` from
+``code/tacotron/synthesizer.py:38`` + ``tacotron.py:201``; ``WaveNet_model/inference/...`` from
+``code/wavenet_vocoder/synthesizer.py:27`` + ``wavenet.py:269``).  Scope names inside TF
+library cells (``lstm_cell``, ``gru_cell``, ``bidirectional_rnn``) follow TF 1.x conventions and
+are unverified without TensorFlow (no real checkpoint for these layers exists in the reference).
+"""
+import numpy as np
+
+TP = "Tacotron_model/inference/"
+WP = "WaveNet_model/inference/"
+
+
+def _bn(scope, c):
+    s = scope + "batch_normalization/"
+    return [(s + "gamma", (c,), "bn_gamma"), (s + "beta", (c,), "bn_beta"),
+            (s + "moving_mean", (c,), "bn_mean"), (s + "moving_variance", (c,), "bn_var")]
+
+
+def tacotron_weight_specs(hp, emt_only=False):
+    """(name, shape, init) for every variable on the synthesis path (tacotron.py:215-381)."""
+    S = []
+    n_sym = 66  # tacotron/utils/symbols.py:9-17
+    E = hp.embedding_dim
+    S.append((TP + "inputs_embedding", (n_sym, E), "glorot"))
+    cin = E
+    kw = hp.enc_conv_kernel_size[0]
+    for i in range(1, hp.enc_conv_num_layers + 1):
+        sc = TP + "encoder_convolutions/conv_layer_{}_encoder_convolutions/".format(i)
+        S.append((sc + "conv1d/kernel", (kw, cin, hp.enc_conv_channels), "glorot"))
+        S.append((sc + "conv1d/bias", (hp.enc_conv_channels,), "bias"))
+        S += _bn(sc, hp.enc_conv_channels)
+        cin = hp.enc_conv_channels
+    U = hp.encoder_lstm_units
+    for d in ("fw", "bw"):
+        sc = TP + "encoder_LSTM/bidirectional_rnn/{}/lstm_cell/".format(d)
+        S.append((sc + "kernel", (cin + U, 4 * U), "glorot"))
+        S.append((sc + "bias", (4 * U,), "bias"))
+    # reference encoders (modules.py:9-64) and GST (tacotron.py:219-282)
+    tags = ["emt"] if emt_only else ["emt", "spk"]
+    for tag in tags:
+        sc = TP + "refnet_{}/".format(tag)
+        c_in, F = 1, hp.num_mels
+        for i, f in enumerate(hp.reference_filters):
+            s2 = sc + "conv2d_{}/".format(i)
+            S.append((s2 + "conv2d/kernel", (3, 3, c_in, f), "glorot"))
+            S.append((s2 + "conv2d/bias", (f,), "bias"))
+            S += _bn(s2, f)
+            c_in = f
+            F = -(-F // 2)
+        gin = F * c_in
+        D = hp.reference_depth
+        S.append((sc + "rnn/gru_cell/gates/kernel", (gin + D, 2 * D), "glorot"))
+        S.append((sc + "rnn/gru_cell/gates/bias", (2 * D,), "gru_gate_bias"))
+        S.append((sc + "rnn/gru_cell/candidate/kernel", (gin + D, D), "glorot"))
+        S.append((sc + "rnn/gru_cell/candidate/bias", (D,), "bias"))
+        S.append((sc + "dense/kernel", (D, 128), "glorot"))
+        S.append((sc + "dense/bias", (128,), "bias"))
+        tok_d = hp.style_embed_depth // hp.num_heads
+        S.append((TP + "style_tokens_{}".format(tag), (hp.num_gst, tok_d), "gst_tokens"))
+        mh = TP + "Multihead-attention-{}/".format(tag)
+        A = hp.style_att_dim
+        S.append((mh + "conv1d/kernel", (1, 128, A), "glorot"))
+        S.append((mh + "conv1d/bias", (A,), "bias"))
+        S.append((mh + "conv1d_1/kernel", (1, tok_d, A), "glorot"))
+        S.append((mh + "conv1d_1/bias", (A,), "bias"))
+        S.append((mh + "attention_v", (A // hp.num_heads,), "glorot"))
+        S.append((mh + "attention_g", (), "mha_g"))
+        S.append((mh + "attention_b", (A // hp.num_heads,), "bias"))
+    Dm = memory_width(hp, emt_only)
+    Ad = hp.attention_dim
+    S.append((TP + "memory_layer/kernel", (Dm, Ad), "glorot"))
+    S.append((TP + "decoder/query_layer/kernel", (hp.decoder_lstm_units, Ad), "glorot"))
+    la = TP + "decoder/Location_Sensitive_Attention/"
+    S.append((la + "location_features_convolution/kernel",
+              (hp.attention_kernel[0], 1, hp.attention_filters), "glorot"))
+    S.append((la + "location_features_convolution/bias", (hp.attention_filters,), "bias"))
+    S.append((la + "location_features_layer/kernel", (hp.attention_filters, Ad), "glorot"))
+    S.append((la + "attention_variable_projection", (Ad,), "glorot"))
+    S.append((la + "attention_bias", (Ad,), "bias"))
+    p_in = hp.num_mels
+    for i, n in enumerate(hp.prenet_layers):
+        sc = TP + "decoder/decoder_prenet/dense_{}/".format(i + 1)
+        S.append((sc + "kernel", (p_in, n), "glorot"))
+        S.append((sc + "bias", (n,), "bias"))
+        p_in = n
+    H = hp.decoder_lstm_units
+    x_in = p_in + Dm
+    for l in range(hp.decoder_layers):
+        sc = TP + "decoder/decoder_LSTM/multi_rnn_cell/cell_{}/lstm_cell/".format(l)
+        S.append((sc + "kernel", (x_in + H, 4 * H), "glorot"))
+        S.append((sc + "bias", (4 * H,), "bias"))
+        x_in = H
+    fp = TP + "decoder/linear_transform_projection/projection_linear_transform_projection/"
+    S.append((fp + "kernel", (H + Dm, hp.num_mels * hp.outputs_per_step), "glorot"))
+    S.append((fp + "bias", (hp.num_mels * hp.outputs_per_step,), "bias"))
+    sp = TP + "decoder/stop_token_projection/projection_stop_token_projection/"
+    S.append((sp + "kernel", (H + Dm, hp.outputs_per_step), "glorot"))
+    S.append((sp + "bias", (hp.outputs_per_step,), "stop_bias"))
+    cin = hp.num_mels
+    kw = hp.postnet_kernel_size[0]
+    for i in range(1, hp.postnet_num_layers + 1):
+        sc = TP + "postnet_convolutions/conv_layer_{}_postnet_convolutions/".format(i)
+        S.append((sc + "conv1d/kernel", (kw, cin, hp.postnet_channels), "glorot"))
+        S.append((sc + "conv1d/bias", (hp.postnet_channels,), "bias"))
+        S += _bn(sc, hp.postnet_channels)
+        cin = hp.postnet_channels
+    pp = TP + "postnet_projection/projection_postnet_projection/"
+    S.append((pp + "kernel", (cin, hp.num_mels), "glorot"))
+    S.append((pp + "bias", (hp.num_mels,), "bias"))
+    return S
+
+
+def memory_width(hp, emt_only=False):
+    """D_mem = 2·encoder_lstm_units + style width (tacotron.py:297-308)."""
+    style = hp.style_embed_depth if hp.use_gst else 128
+    return 2 * hp.encoder_lstm_units + (style if emt_only else 2 * style)
+
+
+def wavenet_weight_specs(hp):
+    """(name, shape, init) of the WaveNet synthesis graph (wavenet.py:89-208)."""
+    S = []
+    R, G, Sk = hp.residual_channels, hp.gate_channels, hp.skip_out_channels
+    S.append((WP + "input_convolution/kernel", (1, 1, R), "glorot"))
+    S.append((WP + "input_convolution/bias", (R,), "bias"))
+    for l in range(hp.layers):
+        s = WP + "ResidualConv1DGLU_{}/".format(l)
+        for kind, shape in (("causal", (hp.kernel_size, R, G)), ("cin", (1, hp.cin_channels, G)),
+                            ("skip", (1, G // 2, Sk)), ("out", (1, G // 2, R))):
+            sc = s + "residual_block_{}_conv_ResidualConv1DGLU_{}/".format(kind, l)
+            S.append((sc + "kernel", shape, "glorot"))
+            S.append((sc + "bias", (shape[-1],), "bias"))
+    S.append((WP + "skip_convolutions/final_convolution_1/kernel", (1, Sk, Sk), "glorot"))
+    S.append((WP + "skip_convolutions/final_convolution_1/bias", (Sk,), "bias"))
+    S.append((WP + "skip_convolutions/final_convolution_2/kernel", (1, Sk, hp.out_channels), "glorot"))
+    S.append((WP + "skip_convolutions/final_convolution_2/bias", (hp.out_channels,), "bias"))
+    if hp.upsample_type != "2D":
+        raise NotImplementedError("upsample_type {!r}: only '2D' (paper_hparams) is on the MI355X "
+                                  "path (SURVEY.md §8f lists the others as next)".format(hp.upsample_type))
+    for i, s in enumerate(hp.upsample_scales):
+        sc = WP + "local_conditioning_upsampling_{}/ConvTranspose2D_layer_{}/".format(i + 1, i)
+        S.append((sc + "kernel", (hp.freq_axis_kernel_size, s, 1, 1), "nn_upsample:{}".format(
+            len(hp.upsample_scales))))
+        S.append((sc + "bias", (1,), "bias"))
+    return S
+
+
+def _init(rng, shape, kind, hp):
+    shape = tuple(shape)
+    if kind == "glorot":
+        if len(shape) == 0:
+            return np.float32(rng.uniform(-1, 1))
+        if len(shape) == 1:
+            fi = fo = shape[0]
+        else:
+            rf = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+            fi, fo = shape[-2] * rf, shape[-1] * rf
+        lim = np.sqrt(6.0 / (fi + fo))
+        return rng.uniform(-lim, lim, shape).astype(np.float32)
+    if kind == "bias":
+        return rng.uniform(-0.1, 0.1, shape).astype(np.float32)
+    if kind == "stop_bias":
+        # negative so that an untrained (random) model decodes to max_iters instead of stopping on
+        # a coin flip; tests that exercise the stop rule override this bias explicitly
+        return rng.uniform(-3.5, -2.5, shape).astype(np.float32)
+    if kind == "gru_gate_bias":
+        return (1.0 + rng.uniform(-0.1, 0.1, shape)).astype(np.float32)  # TF GRUCell bias init 1.0
+    if kind == "bn_gamma":
+        return rng.uniform(0.8, 1.2, shape).astype(np.float32)
+    if kind in ("bn_beta", "bn_mean"):
+        return rng.uniform(-0.1, 0.1, shape).astype(np.float32)
+    if kind == "bn_var":
+        return rng.uniform(0.8, 1.2, shape).astype(np.float32)
+    if kind == "gst_tokens":  # truncated_normal(stddev=0.5), tacotron.py:221-224
+        v = rng.normal(0, 0.5, shape)
+        return np.clip(v, -1.0, 1.0).astype(np.float32)
+    if kind == "mha_g":  # sqrt(1/num_units), multihead_attention.py:103-105
+        return np.float32(np.sqrt(1.0 / (hp.style_att_dim // hp.num_heads)))
+    if kind.startswith("nn_upsample"):
+        # ConvTranspose2D._init_kernel (modules.py:761-770) + a small perturbation so every tap
+        # is exercised by the parity tests.
+        up_layers = int(kind.split(":")[1])
+        kh, kw = shape[0], shape[1]
+        k = np.zeros((kh, kw), np.float64)
+        ov = kw // kw
+        k[kh // 2, :] = 1.0 / max(ov, 1) if kw % 2 == 0 else 1.0
+        k = k * (hp.NN_scaler ** (1.0 / up_layers)) + rng.uniform(-0.05, 0.05, (kh, kw))
+        return k.reshape(shape).astype(np.float32)
+    raise ValueError(kind)
+
+
+def init_weights(specs, hp, seed=5339):
+    """Seeded random init (seed defaults to tacotron_random_seed/wavenet_random_seed = 5339)."""
+    rng = np.random.default_rng(seed)
+    return {name: np.asarray(_init(rng, shape, kind, hp), np.float32).reshape(shape)
+            for name, shape, kind in specs}
+
+
+def init_tacotron_weights(hp, seed=5339, emt_only=False):
+    return init_weights(tacotron_weight_specs(hp, emt_only), hp, seed)
+
+
+def init_wavenet_weights(hp, seed=5339):
+    return init_weights(wavenet_weight_specs(hp), hp, seed)

@@ -1,0 +1,142 @@
+"""WaveNet (code/wavenet_vocoder/models/wavenet.py:86-923), synthesis path on MI355X.
+
+``initialize`` / ``incremental`` keep the reference signatures and run eagerly through libtt2.so
+(upsampling network + fast-WaveNet incremental generation + MoL sampler); the results land in
+``tower_y_hat`` / ``tower_synth_upsampled_local_features`` like the reference's graph outputs.
+"""
+import os
+
+import numpy as np
+
+from tt2.engine import WaveNetEngine
+from tt2.hparams import get_hop_size
+from tt2.weights import init_wavenet_weights
+from wavenet_vocoder.util import is_mulaw, is_mulaw_quantize, is_scalar_input
+
+
+def receptive_field_size(total_layers, num_cycles, kernel_size, dilation=lambda x: 2 ** x):
+    """wavenet.py:54-71."""
+    assert total_layers % num_cycles == 0
+    layers_per_cycle = total_layers // num_cycles
+    dilations = [dilation(i % layers_per_cycle) for i in range(total_layers)]
+    return (kernel_size - 1) * sum(dilations) + 1
+
+
+class WaveNet():
+    """Tacotron-2 Wavenet Vocoder model."""
+
+    def __init__(self, hparams, init):
+        self._hparams = hparams
+        if self.local_conditioning_enabled():
+            assert hparams.num_mels == hparams.cin_channels
+        assert hparams.layers % hparams.stacks == 0
+        self.scalar_input = is_scalar_input(hparams.input_type)
+        self.receptive_field = receptive_field_size(hparams.layers, hparams.stacks,
+                                                    hparams.kernel_size)
+        self._weights = None
+        self._engine = None
+        self.device = int(os.environ.get("TT2_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+    def local_conditioning_enabled(self):
+        return self._hparams.cin_channels > 0
+
+    def global_conditioning_enabled(self):
+        return self._hparams.gin_channels > 0
+
+    def has_speaker_embedding(self):
+        return False
+
+    # -- weights (replaces create_shadow_saver/load_averaged_model, wavenet_vocoder/train.py:67-86)
+    def load_weights(self, weights):
+        if isinstance(weights, str):
+            with np.load(weights, allow_pickle=False) as z:
+                weights = {k: z[k] for k in z.files}
+        self._weights = dict(weights)
+        self._engine = None
+
+    def init_random_weights(self, seed=None):
+        hp = self._hparams
+        self.load_weights(init_wavenet_weights(hp, hp.wavenet_random_seed if seed is None else seed))
+
+    def _check_path(self):
+        hp = self._hparams
+        if not is_scalar_input(hp.input_type) or is_mulaw(hp.input_type):
+            raise NotImplementedError("only input_type='raw' is on the MI355X path")
+        if hp.out_channels == 2:
+            raise NotImplementedError("Gaussian output head (out_channels=2) is not built; the MoL "
+                                      "head (paper_hparams out_channels=30) is (SURVEY.md §8f)")
+        if self.global_conditioning_enabled():
+            raise NotImplementedError("global conditioning (gin_channels > 0) is not built")
+        if not self.local_conditioning_enabled():
+            raise NotImplementedError("unconditional synthesis (cin_channels <= 0) is not built")
+
+    def _get_engine(self, B, T):
+        if self._weights is None:
+            raise RuntimeError("WaveNet weights not loaded: call load_weights() or "
+                               "init_random_weights()")
+        e = self._engine
+        if e is None or not e.fits(B, T):
+            if e is not None:
+                e.close()
+            self._engine = None
+            e = WaveNetEngine(self._hparams, self._weights, max(B, 1), T, self.device)
+            self._engine = e
+        return e
+
+    def initialize(self, y, c, g, input_lengths, x=None, synthesis_length=None, test_inputs=None,
+                   split_infos=None, u_mix=None, u_log=None, seed=0):
+        """wavenet.py:218-473 (synthesis branch :408-465).  c: [B, T_frames, cin] conditioning,
+        already clipped + _interp'd by the caller (wavenet_vocoder/synthesizer.py:63-70).
+        u_mix [T,B,10] / u_log [T,B] inject the MoL sampler's uniforms (None = device RNG)."""
+        hp = self._hparams
+        self.is_training = x is not None
+        self.is_evaluating = not self.is_training and y is not None
+        if self.is_training or self.is_evaluating:
+            raise NotImplementedError("WaveNet training / eval-loss graphs are not on the synthesis "
+                                      "path")
+        self._check_path()
+        if c is None:
+            raise NotImplementedError("synthesis without local conditioning is not built")
+        c = np.asarray(c, np.float32)
+        if c.ndim != 3 or c.shape[2] != hp.cin_channels:
+            raise ValueError('Expected 3 dimension shape [batch_size(1), time_length, {}] for local '
+                             'condition features but found {}'.format(hp.cin_channels, c.shape))
+        ntow = hp.wavenet_num_gpus
+        cs = np.split(c, ntow, axis=0) if ntow > 1 else [c]
+        tis = ([None] * ntow if test_inputs is None else
+               np.split(np.asarray(test_inputs, np.float32).reshape(c.shape[0], -1), ntow, axis=0))
+        self.tower_y_hat = []
+        self.tower_synth_upsampled_local_features = []
+        self.tower_mix_indices = []
+        hop = get_hop_size(hp)
+        for i, ci in enumerate(cs):
+            B, T_f, _ = ci.shape
+            T = T_f * hop
+            um = ul = None
+            if u_mix is not None:
+                um = np.asarray(u_mix, np.float32)[:, i * B:(i + 1) * B]
+                ul = np.asarray(u_log, np.float32)[:, i * B:(i + 1) * B]
+            out = self._get_engine(B, T).generate(ci, um, ul, seed, tis[i], want_upsampled=True)
+            self.tower_y_hat.append(out["y"])
+            self.tower_synth_upsampled_local_features.append(out["upsampled"])
+            self.tower_mix_indices.append(out["k"])
+
+    def incremental(self, initial_input, c=None, g=None, time_length=100, test_inputs=None,
+                    softmax=True, quantize=True, log_scale_min=-7.0, log_scale_min_gauss=-7.0,
+                    u_mix=None, u_log=None, seed=0, return_logits=False):
+        """wavenet.py:724-911: returns generated samples [B, 1, T] (the reference returns
+        [batch_size, channels, time_length]).  c: [B, cin, T_frames] (channels first, as the
+        reference passes it at wavenet.py:427) — upsampled inside, like the reference."""
+        self._check_path()
+        if initial_input is not None and np.any(np.asarray(initial_input) != 0):
+            raise NotImplementedError("initial_input must be the 'raw' silence value 0")
+        if abs(log_scale_min - self._hparams.log_scale_min) > 1e-6:
+            raise ValueError("log_scale_min must equal hparams.log_scale_min on this build")
+        c = np.asarray(c, np.float32).transpose(0, 2, 1)
+        out = self._get_engine(c.shape[0], c.shape[1] * get_hop_size(self._hparams)).generate(
+            c, u_mix, u_log, seed,
+            None if test_inputs is None else np.asarray(test_inputs, np.float32).reshape(c.shape[0], -1),
+            want_logits=return_logits, want_upsampled=True)
+        self.upsampled_local_features = out["upsampled"]
+        y = out["y"][:, None, :]
+        return (y, out["logits"]) if return_logits else y

@@ -1,0 +1,266 @@
+"""GPU parity: libtt2.so (HIP, gfx950) vs the numpy oracle on identical seeded inputs.
+
+Tolerances (BASELINE.json north_star): mel frames within 1e-4; MoL mixture indices bit-exact given
+injected uniforms.  Intermediate tensors use the same 1e-4 absolute bound unless noted.
+"""
+import numpy as np
+import pytest
+
+from _common import (full_hparams, mol_uniforms, oracle_hp, prenet_masks, small_hparams,
+                     small_wavenet_hparams, tacotron_inputs, wavenet_oracle_hp)
+from oracle import tacotron_ref as TR
+from oracle import wavenet_ref as WR
+
+pytestmark = pytest.mark.gpu
+
+MEL_TOL = 1e-4
+
+
+def _engine(hp, W, B, T, T_ref, max_iters, constraint=False):
+    from tt2.engine import TacotronEngine
+    return TacotronEngine(hp, W, B, T, T_ref, max_iters, 0, False, constraint)
+
+
+@pytest.fixture(scope="module")
+def small_setup():
+    from tt2.weights import init_tacotron_weights
+    hp = small_hparams()
+    W = init_tacotron_weights(hp, seed=5339)
+    return hp, W
+
+
+@pytest.fixture(scope="module")
+def full_setup():
+    from tt2.weights import init_tacotron_weights
+    hp = full_hparams()
+    W = init_tacotron_weights(hp, seed=5339)
+    return hp, W
+
+
+def test_library_loads_native():
+    from tt2 import _lib
+    lib = _lib.load_library()
+    assert b"gfx950" in lib.tt2_version()
+
+
+def test_mol_sampler_bit_exact():
+    from tt2.engine import mol_sample
+    rng = np.random.default_rng(0)
+    n, nr = 4096, 10
+    logits = rng.normal(0, 2, (n, 3 * nr)).astype(np.float32)
+    # adversarial near-ties: duplicate logits on some rows
+    logits[:256, 1] = logits[:256, 0]
+    um = rng.uniform(1e-5, 1 - 1e-5, (n, nr)).astype(np.float32)
+    um[:128, 1] = um[:128, 0]  # exact tie of (logit, uniform) -> first index wins
+    ul = rng.uniform(1e-5, 1 - 1e-5, (n,)).astype(np.float32)
+    lsm = float(np.log(1e-14))
+    x, k = mol_sample(logits, um, ul, lsm)
+    xr, kr = WR.mol_sample(logits, um, ul, lsm)
+    np.testing.assert_array_equal(k, kr)
+    np.testing.assert_allclose(x, xr, atol=2e-6, rtol=1e-5)
+
+
+def test_mixture_shim_shapes():
+    from wavenet_vocoder.models.mixture import sample_with_index
+    rng = np.random.default_rng(1)
+    y = rng.normal(0, 1, (2, 30, 17)).astype(np.float32)
+    um = rng.uniform(1e-5, 1 - 1e-5, (2, 17, 10))
+    ul = rng.uniform(1e-5, 1 - 1e-5, (2, 17))
+    x, k = sample_with_index(y, -32.0, um, ul)
+    xr, kr = WR.mol_sample(y.transpose(0, 2, 1).reshape(-1, 30), um.reshape(-1, 10),
+                           ul.reshape(-1), -32.0)
+    assert x.shape == (2, 17)
+    np.testing.assert_array_equal(k.reshape(-1), kr)
+    np.testing.assert_allclose(x.reshape(-1), xr, atol=2e-6)
+
+
+@pytest.mark.parametrize("B,T", [(3, 11), (1, 5)])
+def test_encoder_memory_small(small_setup, B, T):
+    hp, W = small_setup
+    ids, lens, re, rs = tacotron_inputs(B, T, 70, seed=7)
+    eng = _engine(hp, W, B, T, 70, 8)
+    mem, style = eng.encode(ids, lens, re, rs)
+    oh = oracle_hp(hp)
+    enc = TR.encoder(ids, lens, W, oh)
+    st = TR.style_embedding(re, rs, W, oh)
+    vals, _ = TR.memory_and_keys(enc, st, lens, W)
+    np.testing.assert_allclose(style, st, atol=1e-5)
+    np.testing.assert_allclose(mem, vals, atol=1e-5)
+    eng.close()
+
+
+def _decode_compare(hp, W, B, T, T_ref, n, targets=None, seed=11, constraint=False, tol=MEL_TOL):
+    ids, lens, re, rs = tacotron_inputs(B, T, T_ref, seed=seed)
+    P = hp.prenet_layers[0]
+    masks = prenet_masks(n, B, P, seed=seed)
+    eng = _engine(hp, W, B, T, T_ref, n, constraint)
+    out = eng.synthesize(ids, lens, re, rs, n, masks, 0, targets)
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp, constraint), masks, n, targets)
+    assert out["frames"].shape == ref["decoder_output"].shape
+    np.testing.assert_allclose(out["stop_token_prediction"], ref["stop_token_prediction"], atol=tol)
+    np.testing.assert_allclose(out["alignments"], ref["alignments"], atol=tol)
+    np.testing.assert_allclose(out["decoder_output"], ref["decoder_output"], atol=tol)
+    np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], atol=tol)
+    eng.close()
+    return out, ref
+
+
+def test_decoder_free_run_small(small_setup):
+    hp, W = small_setup
+    _decode_compare(hp, W, B=4, T=13, T_ref=64, n=30)
+
+
+def test_decoder_window_constraint_small(small_setup):
+    hp, W = small_setup
+    _decode_compare(hp, W, B=2, T=17, T_ref=64, n=20, constraint=True)
+
+
+def test_decoder_gta_small(small_setup):
+    hp, W = small_setup
+    B, n = 3, 60
+    tg = np.random.default_rng(3).uniform(-4, 4, (B, 45, hp.num_mels)).astype(np.float32)
+    out, ref = _decode_compare(hp, W, B=B, T=9, T_ref=64, n=n, targets=tg)
+    assert out["frames"].shape[1] == 45  # TacoTrainingHelper stops at T_targets
+
+
+def test_stop_rule_small(small_setup):
+    """Batch-level stop (helpers.py:40-54): all rows stop together at the first step where every
+    row rounds to 1; with a large positive stop bias that is step 0 -> 1 frame."""
+    hp, W = small_setup
+    W2 = dict(W)
+    key = "Tacotron_model/inference/decoder/stop_token_projection/projection_stop_token_projection/bias"
+    W2[key] = np.array([8.0], np.float32)
+    out, ref = _decode_compare(hp, W2, B=3, T=7, T_ref=64, n=25)
+    assert out["frames"].shape[1] == 1 == ref["decoder_output"].shape[1]
+
+
+def test_stop_rule_mid_sequence(small_setup):
+    """A stop bias near the decision boundary stops at an intermediate step; GPU and oracle must
+    agree on the step (the stop probabilities themselves are compared at 1e-4)."""
+    hp, W = small_setup
+    W2 = dict(W)
+    key = "Tacotron_model/inference/decoder/stop_token_projection/projection_stop_token_projection/bias"
+    for bias in (0.6, 1.0, 1.5):
+        W2[key] = np.array([bias], np.float32)
+        out, ref = _decode_compare(hp, W2, B=2, T=7, T_ref=64, n=40, seed=5)
+        assert out["frames"].shape[1] == ref["decoder_output"].shape[1]
+
+
+def test_postnet_standalone(small_setup):
+    hp, W = small_setup
+    rng = np.random.default_rng(4)
+    frames = rng.uniform(-5, 5, (2, 37, hp.num_mels)).astype(np.float32)
+    eng = _engine(hp, W, 2, 8, 64, 40)
+    dec, mel = eng.postnet(frames)
+    rd, rm = TR.postnet_and_clip(frames, W, oracle_hp(hp))
+    np.testing.assert_allclose(dec, rd, atol=1e-6)
+    np.testing.assert_allclose(mel, rm, atol=MEL_TOL)
+    eng.close()
+
+
+def test_full_dims_free_run(full_setup):
+    """Fork-default dimensions (D_mem 1024, 2x1024 LSTM, 512-ch postnet), short horizon."""
+    hp, W = full_setup
+    _decode_compare(hp, W, B=4, T=23, T_ref=96, n=12)
+
+
+def test_full_dims_gta(full_setup):
+    hp, W = full_setup
+    B = 2
+    tg = np.random.default_rng(9).uniform(-4, 4, (B, 40, hp.num_mels)).astype(np.float32)
+    _decode_compare(hp, W, B=B, T=15, T_ref=64, n=40, targets=tg)
+
+
+def test_tacotron_shim_initialize(small_setup):
+    """tacotron.models.create_model('Tacotron', hp).initialize(...) fills tower_* like the
+    reference (tacotron.py:573-632)."""
+    from types import SimpleNamespace
+
+    from tacotron.models import create_model
+    hp, W = small_setup
+    hp = hp.copy()
+    hp.max_iters = 15
+    B, T = 2, 9
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=2)
+    masks = prenet_masks(15, B, hp.prenet_layers[0], seed=2)
+    m = create_model("Tacotron", hp)
+    m.load_weights(W)
+    args = SimpleNamespace(emt_only=False, adain=False, unpaired=False, nat_gan=False,
+                           pretrained_emb_disc_all=False, synth_constraint=False)
+    m.initialize(args, ids, lens, ref_mel_emt=re, ref_mel_spk=rs, n_emt=4, n_spk=2, synth=True,
+                 prenet_masks=masks)
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, 15)
+    assert len(m.tower_mel_outputs) == 1
+    np.testing.assert_allclose(m.tower_mel_outputs[0], ref["mel_outputs"], atol=MEL_TOL)
+    assert m.tower_alignments[0].shape == ref["alignments"].shape
+
+
+# ------------------------------------------------------------------------------------ WaveNet
+
+def _wn(hp, W, maxB, maxT):
+    from tt2.engine import WaveNetEngine
+    return WaveNetEngine(hp, W, maxB, maxT, 0)
+
+
+@pytest.mark.parametrize("layers,stacks", [(6, 2), (24, 4)])
+def test_wavenet_teacher_forced(layers, stacks):
+    from tt2.weights import init_wavenet_weights
+    hp = small_wavenet_hparams(layers, stacks)
+    W = init_wavenet_weights(hp, seed=5339)
+    rng = np.random.default_rng(21)
+    B, T_f = 2, 2
+    T = T_f * 275
+    mel = rng.uniform(-4, 4, (B, T_f, 80)).astype(np.float32)
+    cond = WR.interp_condition(mel)
+    um, ul = mol_uniforms(T, B, seed=3)
+    teacher = rng.uniform(-0.9, 0.9, (B, T)).astype(np.float32)
+    eng = _wn(hp, W, B, T)
+    out = eng.generate(cond, um, ul, 0, teacher, want_logits=True, want_upsampled=True)
+    c_up = WR.upsample_2d(cond.transpose(0, 2, 1), W, hp.upsample_scales)
+    np.testing.assert_allclose(out["upsampled"], c_up, atol=1e-5)
+    y, k, lg = WR.incremental(c_up.transpose(0, 2, 1), W, wavenet_oracle_hp(hp), um, ul, teacher,
+                              return_logits=True)
+    np.testing.assert_allclose(out["logits"], lg, atol=1e-4, rtol=1e-4)
+    # bit-exact mixture indices unless the oracle's own Gumbel margin is below fp32 resolution
+    gl = np.log(-np.log(um.astype(np.float64))).astype(np.float32)
+    temp = lg[..., :10] - gl.transpose(1, 0, 2)
+    srt = np.sort(temp, -1)
+    margin = srt[..., -1] - srt[..., -2]
+    safe = margin > 1e-4
+    assert safe.mean() > 0.99
+    np.testing.assert_array_equal(out["k"][safe], k[safe])
+    np.testing.assert_allclose(out["y"][safe], y[safe], atol=1e-4)
+    eng.close()
+
+
+def test_wavenet_free_run_short():
+    from tt2.weights import init_wavenet_weights
+    hp = small_wavenet_hparams(24, 4)
+    W = init_wavenet_weights(hp, seed=5339)
+    rng = np.random.default_rng(5)
+    B, T_f = 1, 1
+    T = 275
+    cond = WR.interp_condition(rng.uniform(-4, 4, (B, T_f, 80)).astype(np.float32))
+    um, ul = mol_uniforms(T, B, seed=8)
+    out = _wn(hp, W, B, T).generate(cond, um, ul, 0, None)
+    c_up = WR.upsample_2d(cond.transpose(0, 2, 1), W, hp.upsample_scales)
+    y, k = WR.incremental(c_up.transpose(0, 2, 1), W, wavenet_oracle_hp(hp), um, ul)
+    # free running: identical until a (rare) near-tie diverges; require a long identical prefix
+    same = out["k"][0] == k[0]
+    first_diff = int(np.argmin(same)) if not same.all() else T
+    assert first_diff >= 200
+    np.testing.assert_allclose(out["y"][0, :first_diff], y[0, :first_diff], atol=1e-4)
+
+
+def test_wavenet_shim_initialize():
+    from wavenet_vocoder.models import create_model
+    hp = small_wavenet_hparams(6, 2)
+    m = create_model("WaveNet", hp)
+    m.init_random_weights()
+    rng = np.random.default_rng(6)
+    c = WR.interp_condition(rng.uniform(-4, 4, (2, 1, 80)).astype(np.float32))
+    um, ul = mol_uniforms(275, 2, seed=1)
+    m.initialize(None, c, None, None, u_mix=um, u_log=ul)
+    assert m.tower_y_hat[0].shape == (2, 275)
+    assert m.tower_synth_upsampled_local_features[0].shape == (2, 80, 275)
+    assert np.all(np.abs(m.tower_y_hat[0]) <= 1.0)
