@@ -888,8 +888,8 @@ static void alloc_acts(tt2_ctx* c) {
   c->stop.alloc(B * MI * 4);
   c->align.alloc(B * T * MI * 4);
   c->dec.alloc(B * MI * c->nm * 4);
-  c->post_a.alloc(B * MI * c->PC * 4);
-  c->post_b.alloc(B * MI * c->PC * 4);
+  c->post_a.alloc(B * MI * std::max(c->PC, c->nm) * 4);
+  c->post_b.alloc(B * MI * std::max(c->PC, c->nm) * 4);
   c->mel.alloc(B * MI * c->nm * 4);
   TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ctl_host), 4 * sizeof(int)));
 }
