@@ -1,0 +1,290 @@
+#!/usr/bin/env python
+"""bench.py — MI355X throughput of the Tacotron-2 synthesis path (BASELINE.json).
+
+Headline (``value``): mel-frames/s of Tacotron-2 encoder + decoder loop + Postnet inference on
+configs[1] ("decoder+Postnet inference, batch=32x200-char synthetic, 1xMI355X"): one step = one full
+synthesis of a 32-utterance batch (200 chars + EOS, T_out = 1000 decoder frames, random-init fp32
+weights of the fork-default architecture, D_mem = 1024).  The ``wavenet`` object carries
+configs[2] (24-layer R=64 MoL WaveNet, batch 1, 22.05 kHz): audio-samples/s.
+
+Multi-GPU (``--gpus N`` under torch.distributed.run): one rank per GPU, each rank synthesises its
+own batch (utterance-batch sharding) — weak scaling, no collective in the timed
+region; the timed region is bracketed by barrier + synchronize and the max over ranks is reported.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "tacotron-2_amd"), ROOT]
+
+METRIC = "mel-frames/sec (decoder) + audio-samples/sec (WaveNet) @1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--chars", type=int, default=200)
+    p.add_argument("--ref-frames", type=int, default=400)
+    p.add_argument("--t-out", type=int, default=1000)
+    p.add_argument("--wavenet-frames", type=int, default=80, help="mel frames per WaveNet utterance")
+    p.add_argument("--wavenet-steps", type=int, default=1)
+    p.add_argument("--no-wavenet", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-steps", type=int, default=100)
+    p.add_argument("--profile-iters", type=int, default=50)
+    return p.parse_args()
+
+
+def lstm_bytes(K, H, M=32):
+    """Algorithmic HBM bytes of one k_lstm launch: weights + bias + input activations + c r/w +
+    h outputs (raw + zoneout) — every byte the step must touch once."""
+    return 4 * (K * 4 * H + 4 * H + M * K + 2 * M * H + 2 * M * H)
+
+
+def cpu_baseline_tacotron(hp, W, B, T, T_ref, t_out, steps):
+    """Oracle (numpy) on this host: encoder + `steps` decoder steps + Postnet over `steps` frames,
+    extrapolated linearly to T_out frames."""
+    from oracle.hp import oracle_hp
+    from tt2.synthetic import tacotron_inputs
+    from oracle import tacotron_ref as TR
+    ids, lens, re, rs = tacotron_inputs(B, T, T_ref, seed=1234, ragged=False)
+    oh = oracle_hp(hp)
+    masks = (np.random.default_rng(5339).random((steps, 2, B, hp.prenet_layers[0])) < 0.5)
+    t0 = time.perf_counter()
+    enc = TR.encoder(ids, lens, W, oh)
+    st = TR.style_embedding(re, rs, W, oh)
+    vals, keys = TR.memory_and_keys(enc, st, lens, W)
+    t1 = time.perf_counter()
+    frames, _, _ = TR.dynamic_decode(keys, vals, lens, W, oh, masks.astype(np.uint8), steps)
+    t2 = time.perf_counter()
+    TR.postnet_and_clip(frames, W, oh)
+    t3 = time.perf_counter()
+    scale = t_out / float(frames.shape[1])
+    t_full = (t1 - t0) + scale * ((t2 - t1) + (t3 - t2))
+    return dict(value=B * t_out / t_full, t_encoder_s=t1 - t0, t_decoder_s=t2 - t1,
+                t_postnet_s=t3 - t2, decoded=int(frames.shape[1]))
+
+
+def cpu_baseline_wavenet(hp, W, samples):
+    from oracle import wavenet_ref as WR
+    from oracle.hp import wavenet_oracle_hp
+    rng = np.random.default_rng(5339)
+    T = samples
+    c_up = rng.uniform(0, 1, (1, T, 80)).astype(np.float32)
+    um = rng.uniform(1e-5, 1 - 1e-5, (T, 1, 10)).astype(np.float32)
+    ul = rng.uniform(1e-5, 1 - 1e-5, (T, 1)).astype(np.float32)
+    t0 = time.perf_counter()
+    WR.incremental(c_up, W, wavenet_oracle_hp(hp), um, ul)
+    return T / (time.perf_counter() - t0)
+
+
+def threads_used():
+    try:
+        from threadpoolctl import threadpool_info
+        n = [i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"]
+        return max(n) if n else 1
+    except Exception:
+        return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def load_traffic(kernel):
+    """HBM bytes/launch from the committed rocprofv3 PMC summary (profiles/), FETCH_SIZE x2 +
+    WRITE_SIZE per MI355X_MICROARCH.md §HBM, or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
+                                device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    import ctypes
+    from tt2 import _lib
+    from tt2.engine import TacotronEngine, WaveNetEngine
+    from tt2.hparams import bench_wavenet_hparams, hparams
+    from tt2.weights import init_tacotron_weights, init_wavenet_weights
+    from tt2.synthetic import tacotron_inputs
+
+    lib = _lib.load_library()
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1, max_iters=a.t_out))
+    B, T = a.batch, a.chars + 1
+    W = init_tacotron_weights(hp, seed=hp.tacotron_random_seed)
+    eng = TacotronEngine(hp, W, B, T, a.ref_frames, a.t_out, local)
+    ids, lens, re, rs = tacotron_inputs(B, T, a.ref_frames, seed=1234 + rank, ragged=False)
+    dev = torch.device("cuda", local)
+    ids_d = torch.from_numpy(ids).to(dev)
+    lens_d = torch.from_numpy(lens).to(dev)
+    re_d = torch.from_numpy(re).to(dev)
+    rs_d = torch.from_numpy(rs).to(dev)
+    mel_d = torch.empty((B, a.t_out, hp.num_mels), dtype=torch.float32, device=dev)
+    stop_d = torch.empty((B, a.t_out), dtype=torch.float32, device=dev)
+    lens_h = np.ascontiguousarray(lens, np.int32)
+    n_steps = ctypes.c_int32()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        _lib.check(lib.tt2_synthesize_dev(
+            eng.h, ids_d.data_ptr(), lens_d.data_ptr(), _lib.ptr(lens_h), B, T, re_d.data_ptr(),
+            a.ref_frames, rs_d.data_ptr(), a.ref_frames, a.t_out, None, 5339 + rank,
+            mel_d.data_ptr(), stop_d.data_ptr(), ctypes.byref(n_steps), ctypes.c_void_p(stream)))
+        return n_steps.value
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    frames = 0
+    for _ in range(a.steps):
+        frames += B * step()
+    torch.cuda.synchronize()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    total_frames = frames * world
+    value = total_frames / el
+    ms3 = (ctypes.c_float * 3)()
+    _lib.check(lib.tt2_last_timings(eng.h, ms3))
+    phases = dict(encode_ms=round(ms3[0], 3), decode_ms=round(ms3[1], 3), postnet_ms=round(ms3[2], 3),
+                  decode_us_per_step=round(1000.0 * ms3[1] / max(n_steps.value, 1), 3))
+
+    # --- dominant kernel roofline: the decoder Zoneout-LSTM layers (k_lstm) ---
+    us7 = (ctypes.c_float * 7)()
+    _lib.check(lib.tt2_profile_decoder_kernels(eng.h, a.profile_iters, us7))
+    st64 = (ctypes.c_longlong * 64)()
+    _lib.check(lib.tt2_debug_stamps(eng.h, st64))
+    stamps = {"prenet": [st64[i] - st64[0] for i in range(6)],
+              "energy": [st64[i] - st64[8] for i in range(8, 13)],
+              "lstm": [st64[i] - st64[16] for i in range(16, 20)]}
+    H, P = hp.decoder_lstm_units, hp.prenet_layers[0]
+    D = eng.D
+    by = 0.5 * (lstm_bytes(P + D + H, H) + lstm_bytes(2 * H, H))
+    lstm_us = us7[1]
+    achieved = by / (lstm_us * 1e-6) / 1e9
+    traffic = load_traffic("k_lstm")
+    roofline = dict(kernel="k_lstm (decoder Zoneout-LSTM, layers 1/2 alternating)", bound="hbm",
+                    achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                    algorithmic_bytes_per_launch=int(by), avg_launch_us=round(lstm_us, 3),
+                    per_kernel_us=dict(zip(["prenet", "lstm_avg", "query", "energy",
+                                            "softmax_context", "projection", "lstm2"],
+                                           [round(v, 3) for v in us7])))
+
+    # --- WaveNet (configs[2]) ---
+    wn = None
+    if not a.no_wavenet:
+        whp = bench_wavenet_hparams()
+        WW = init_wavenet_weights(whp, seed=whp.wavenet_random_seed)
+        hop = 275
+        Tn = a.wavenet_frames * hop
+        weng = WaveNetEngine(whp, WW, 1, Tn, local)
+        rng = np.random.default_rng(5339 + rank)
+        cond = ((np.clip(rng.uniform(-4, 4, (1, 80, a.wavenet_frames)), -4, 4) + 4) / 8).astype(np.float32)
+        cond_d = torch.from_numpy(cond).to(dev)
+        wav_d = torch.empty((1, Tn), dtype=torch.float32, device=dev)
+
+        def wstep():
+            _lib.check(lib.tt2_wn_generate_dev(weng.h, cond_d.data_ptr(), 1, a.wavenet_frames, None,
+                                               None, 5339 + rank, None, wav_d.data_ptr(), None,
+                                               None, ctypes.c_void_p(stream)))
+
+        wstep()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.wavenet_steps):
+            wstep()
+        torch.cuda.synchronize()
+        barrier()
+        wel = max_over_ranks(time.perf_counter() - t0)
+        wms = (ctypes.c_float * 3)()
+        _lib.check(lib.tt2_wn_last_timings(weng.h, wms))
+        gen_s = wms[2] / 1000.0
+        # algorithmic bytes per sample: dilated conv + skip/out weights + head + conditioning row
+        R, G, S_, L = whp.residual_channels, whp.gate_channels, whp.skip_out_channels, whp.layers
+        wbytes = 4 * (L * (3 * R * G + G + (G // 2) * (S_ + R) + S_ + R) + S_ * S_ + S_ * 30 + L * G)
+        wach = wbytes * Tn / gen_s / 1e9
+        wn = dict(metric="audio-samples/sec", value=round(world * Tn * a.wavenet_steps / wel, 1),
+                  unit="audio-samples/s", per_gpu_batch=1, samples_per_utterance=Tn,
+                  realtime_factor=round((Tn * a.wavenet_steps / wel) / 22050.0, 3),
+                  phases_ms=dict(upsample=round(wms[0], 3), cond_gemm=round(wms[1], 3),
+                                 generate=round(wms[2], 3)),
+                  us_per_sample=round(1e6 * gen_s / Tn, 3),
+                  roofline=dict(kernel="k_generate64", bound="latency (one CU per utterance)",
+                                achieved=round(wach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                                frac=round(wach / HBM_PEAK_GBS, 5),
+                                algorithmic_bytes_per_sample=int(wbytes)))
+        weng.close()
+
+    # --- CPU baseline (rank 0, N = 1 only) ---
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        c = cpu_baseline_tacotron(hp, W, B, T, a.ref_frames, a.t_out, a.cpu_steps)
+        cores = threads_used()
+        cpu = dict(value=round(c["value"], 2), unit="mel-frames/s", cores=cores, kind="port",
+                   sample="numpy oracle (oracle/tacotron_ref.py), B=32x201 chars: encoder + {} of {} "
+                          "decoder steps + Postnet on {} frames, extrapolated linearly to T_out={} "
+                          "(enc {:.2f}s, dec {:.2f}s, postnet {:.2f}s)".format(
+                              c["decoded"], a.t_out, c["decoded"], a.t_out, c["t_encoder_s"],
+                              c["t_decoder_s"], c["t_postnet_s"]),
+                   label="CPU restatement of the reference path (not TF)")
+        if wn is not None:
+            whp = bench_wavenet_hparams()
+            WW = init_wavenet_weights(whp, seed=whp.wavenet_random_seed)
+            wn["cpu_baseline"] = dict(value=round(cpu_baseline_wavenet(whp, WW, 2000), 1),
+                                      unit="audio-samples/s", cores=cores, kind="port",
+                                      sample="numpy oracle incremental(), 2000 samples, B=1")
+
+    if rank == 0:
+        out = dict(metric=METRIC, value=round(value, 1), unit="mel-frames/s", n_gpus=world,
+                   steps=a.steps, warmup=a.warmup, ms_per_step=round(1000.0 * el / a.steps, 3),
+                   higher_is_better=True, scaling="weak", vs_baseline=None, dtype="f32",
+                   data="synthetic (seeded ids/ref mels, random-init weights)",
+                   config=dict(workload="configs[1]: Tacotron-2 encoder+decoder+Postnet inference, "
+                                        "batch=32x200-char synthetic, T_out=1000, 1 batch per GPU",
+                               global_batch=B * world, chars=a.chars, t_out=a.t_out,
+                               decoded_steps=n_steps.value, ref_frames=a.ref_frames,
+                               parallelism="utterance-batch sharding x{}".format(world)),
+                   phases=phases, roofline=roofline, cpu_baseline=cpu, wavenet=wn,
+                   diag_stamps_cycles=stamps)
+        print(json.dumps(out))
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

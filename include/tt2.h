@@ -138,6 +138,19 @@ tt2_status tt2_synthesize_dev(tt2_ctx* ctx, const int32_t* ids_d, const int32_t*
                               uint64_t seed, float* mel_d, float* stop_d, int32_t* n_steps_host,
                               void* stream);
 
+/* Measurement hooks (not part of the reference surface; used by bench.py for the roofline).
+ * tt2_last_timings: HIP-event times (ms) of the last tt2_synthesize_dev phases
+ *   [encode, decode loop, postnet].
+ * tt2_profile_decoder_kernels: after a decode, re-launch each per-step decoder kernel `iters`
+ *   times back-to-back on the context stream between one HIP event pair; avg_us[7] = time per
+ *   launch of [prenet, lstm(layer1/layer2 alternating), query, energy, softmax+context,
+ *   frame/stop projection, lstm layer 2 only].  Leaves the decoder state undefined. */
+tt2_status tt2_last_timings(tt2_ctx* ctx, float* ms3);
+tt2_status tt2_profile_decoder_kernels(tt2_ctx* ctx, int iters, float* avg_us7);
+/* s_memtime phase stamps (block 0) recorded during the last tt2_profile_decoder_kernels call:
+ * [0..5] prenet, [8..12] energy, [16..19] lstm; diagnostic only. */
+tt2_status tt2_debug_stamps(tt2_ctx* ctx, long long* out64);
+
 /* ------------------------------------------------------------------------------------------ */
 /* WaveNet MoL vocoder (replaces wavenet_vocoder/models/wavenet.py WaveNet.initialize synthesis */
 /* branch :408-465 and WaveNet.incremental :724-911)                                           */
@@ -189,6 +202,9 @@ tt2_status tt2_wn_generate_dev(tt2_wn_ctx* ctx, const float* cond_d, int B, int 
                                const float* u_mix_d, const float* u_log_d, uint64_t seed,
                                const float* teacher_d, float* wav_d, int32_t* mix_idx_d,
                                float* logits_d, void* stream);
+
+/* HIP-event times (ms) of the last generate call: [upsample, conditioning GEMM, generation]. */
+tt2_status tt2_wn_last_timings(tt2_wn_ctx* ctx, float* ms3);
 
 /* Standalone sample_from_discretized_mix_logistic (mixture.py:76-107) on the current HIP device:
  * logits [n, 3*nr_mix], u_mix [n, nr_mix], u_log [n] (host) -> x [n], k [n] (host). */

@@ -123,6 +123,48 @@ __device__ __forceinline__ void skinny_mfma(const float* __restrict__ X, const f
   }
 }
 
+// Same product with every load of the wave's NPW k-groups issued before the first MFMA, so the
+// whole K-slice (3 KiB per k-group per wave) is in flight at once; hipcc emits counted vmcnt waits.
+template <int NPW>
+__device__ __forceinline__ void skinny_mfma_all(const float* __restrict__ X, const float* __restrict__ Wt,
+                                                int sg0, f32x4& acc0, f32x4& acc1, int lane) {
+  const f32x4* Xv = reinterpret_cast<const f32x4*>(X);
+  const f32x4* Wv = reinterpret_cast<const f32x4*>(Wt);
+  f32x4 a0[NPW], a1[NPW], b[NPW];
+#pragma unroll
+  for (int j = 0; j < NPW; ++j) {
+    b[j] = Wv[(sg0 + j) * 64 + lane];
+    a0[j] = Xv[((sg0 + j) * 2 + 0) * 64 + lane];
+    a1[j] = Xv[((sg0 + j) * 2 + 1) * 64 + lane];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep every load ahead of the first MFMA
+#pragma unroll
+  for (int j = 0; j < NPW; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][e], b[j][e], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][e], b[j][e], acc1, 0, 0, 0);
+    }
+}
+
+// acc += X (LDS/global AF, k-groups [0, nsg)) * pre-loaded weight fragments w[0..nsg)
+template <int MAXK>
+__device__ __forceinline__ void skinny_mfma_w(const float* __restrict__ X, const f32x4* w, int nsg,
+                                              f32x4& acc0, f32x4& acc1, int lane) {
+  const f32x4* Xv = reinterpret_cast<const f32x4*>(X);
+#pragma unroll
+  for (int j = 0; j < MAXK; ++j) {
+    if (j >= nsg) break;
+    const f32x4 a0 = Xv[(j * 2 + 0) * 64 + lane];
+    const f32x4 a1 = Xv[(j * 2 + 1) * 64 + lane];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[e], w[j][e], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[e], w[j][e], acc1, 0, 0, 0);
+    }
+  }
+}
+
 // Reduce the (acc0, acc1) of NW waves (each covering a K slice) through LDS into
 // out[m*16 + n] (32 x 16), summing waves in index order (deterministic).
 template <int NW>
@@ -146,6 +188,12 @@ __device__ __forceinline__ void reduce_waves_32x16(const f32x4& acc0, const f32x
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// tanh from one v_exp_f32 + one division: |abs err| < 2e-7 over the whole range (the location-
+// sensitive energy evaluates 32x128 of these per 32 encoder steps; libm tanhf costs ~10x more)
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __expf(2.0f * x);
+  return 1.0f - 2.0f / (e + 1.0f);
+}
 // Accurate variants used where parity matters (expf is correctly-rounded-ish ocml).
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
@@ -155,6 +203,10 @@ __host__ __device__ inline uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
+}
+__host__ __device__ inline uint32_t hash32(uint32_t x) {  // murmur3 fmix32
+  x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
+  return x;
 }
 __host__ __device__ inline double u01_open(uint64_t h) {  // in [1e-5, 1-1e-5)
   const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);

@@ -279,7 +279,8 @@ struct DecArgs {
   // weights
   const float* pre_w1; const float* pre_b1; const float* pre_w2; const float* pre_b2;
   const float* l1_w; const float* l1_b; const float* l2_w; const float* l2_b;
-  const float* q_w; const float* loc_cw; const float* loc_cb; const float* loc_w;
+  const float* q_w; const float* loc_cw; const float* loc_cb; const float* loc_w;  // WF-packed
+  int KLp, Fp;  // location conv taps / filters padded to 16
   const float* va; const float* ba; const float* proj_w; const float* proj_b;
   // attention memory
   const float* keys;    // [B][T_in][A]
@@ -298,51 +299,129 @@ struct DecArgs {
   const uint8_t* masks;  // [max_iters][2][B][P] or null
   uint64_t seed;
   const float* targets;  // [B][T_lim][nm] or null
+  long long* stamps;  // diagnostic s_memtime stamps (profiling only; no output depends on them)
   // outputs
   float* frames;  // [B][max_iters][nm]
   float* stop;    // [B][max_iters]
   float* align;   // [B][T_in][max_iters] or null
 };
 
-__device__ __forceinline__ float prenet_keep(const DecArgs& a, int t, int layer, int b, int j) {
-  if (b >= a.B) return 0.f;
-  if (a.masks) return (float)a.masks[(((long)t * 2 + layer) * a.B + b) * a.P + j];
-  const uint64_t h = mix64(a.seed ^ mix64(((((uint64_t)t * 2 + layer) * 4096u + b) << 16) + j));
-  return (h >> 63) ? 1.f : 0.f;
+// Keep bits of the always-on prenet dropout when the caller injects none: counter-based hash of
+// (seed, flat index) -> Bernoulli(0.5), generated for the whole decode in one launch.
+__global__ void k_gen_masks(uint8_t* __restrict__ m, long n, uint32_t s0, uint32_t s1) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    m[i] = (uint8_t)(hash32(hash32((uint32_t)i ^ s0) + s1) >> 31);
 }
 
 // Prenet (modules.py:346-357) of step t, preceded by the TacoTestHelper/dynamic_decode
 // bookkeeping of step t-1 (helpers.py:36-59): reduce the frame/stop projection partials,
 // write frames/stop[t-1], decide `finished`, select next input (frame or GTA target).
 // Grid: P/16 blocks (layer-2 column tiles); every block recomputes layer 1 (K = num_mels).
-__global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep) {
-  __shared__ __attribute__((aligned(16))) float fin[32 * 80 + 32 * 16];   // AF [32][nm<=80(+pad)]
-  __shared__ __attribute__((aligned(16))) float h1[32 * 256];             // AF [32][P<=256]
+// Every global load the block needs (partials, keep masks) is issued before the first use.
+constexpr int KSQ_C = 4;  // query split-K
+constexpr int KSP_C = 4;  // projection split-K
+#define STAMP(i)                                                                         \
+  do {                                                                                   \
+    if (a.stamps && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)              \
+      a.stamps[i] = __builtin_amdgcn_s_memtime();                                        \
+  } while (0)
+
+__global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep, int t) {
+  __shared__ __attribute__((aligned(16))) float fin[32 * 80];   // AF [32][nm<=80]
+  __shared__ __attribute__((aligned(16))) float h1[32 * 256];   // AF [32][P<=256]
   __shared__ float red[4 * 512];
   __shared__ float G[512];
   __shared__ float stopv[32];
+  __shared__ __attribute__((aligned(16))) uint8_t mk1[32 * 256];
+  __shared__ uint8_t mk2[32 * 16];
   __shared__ int s_done;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (a.ctl->done) return;
-  const int t = a.ctl->tbase + istep;
-  const int nm = a.nm, nmp = (nm + 15) & ~15;
-  // ---- finish step t-1 ----
+  STAMP(0);
+  const int done0 = a.ctl->done;
+  const int nm = a.nm, nmp = (nm + 15) & ~15, P = a.P, tile = blockIdx.x;
+  // ---- issue loads: projection partials (row m, 12 columns), keep masks of step t ----
+  const int pm = tid >> 3, pq = tid & 7;  // NPJ = 96 = 8 x 12
+  f32x4 pp[KSP_C][3];
+  if (t > 0 && a.NPJ == 96) {
+#pragma unroll
+    for (int ks = 0; ks < KSP_C; ++ks)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        pp[ks][j] = *reinterpret_cast<const f32x4*>(a.PP + ((long)ks * 32 + pm) * 96 + pq * 12 + 4 * j);
+  }
+  const int ntile = P / 16, nsg1 = nmp / 16, nsg2 = P / 16;
+  const f32x4* W1v = reinterpret_cast<const f32x4*>(a.pre_w1);
+  const f32x4* W2v = reinterpret_cast<const f32x4*>(a.pre_w2);
+  f32x4 w1[4][5], w2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int tl = wave + 4 * i;
+      if (tl < ntile && j < nsg1) w1[i][j] = W1v[(tl * nsg1 + j) * 64 + lane];
+    }
+  const int s2a = wave * nsg2 / 4, s2b = (wave + 1) * nsg2 / 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (s2a + j < s2b) w2[j] = W2v[((long)tile * nsg2 + s2a + j) * 64 + lane];
+  const long mrow = (long)t * 2 * a.B * P;
+  if (t < a.max_iters) {
+    for (int i = tid; i < 32 * P / 16; i += blockDim.x) {  // 16-byte chunks of layer-1 masks
+      const int m = (i * 16) / P;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (m < a.B) v = *reinterpret_cast<const uint4*>(a.masks + mrow + (long)i * 16);
+      reinterpret_cast<uint4*>(mk1)[i] = v;
+    }
+    for (int i = tid; i < 32 * 16; i += blockDim.x) {
+      const int m = i >> 4, j = i & 15;
+      mk2[i] = m < a.B ? a.masks[mrow + (long)a.B * P + (long)m * P + tile * 16 + j] : 0;
+    }
+  }
+  if (done0) return;
+  STAMP(1);
   for (int i = tid; i < 32 * nmp; i += blockDim.x) fin[i] = 0.f;
   if (tid == 0) s_done = 0;
   __syncthreads();
+  STAMP(2);
+  // ---- finish step t-1 ----
   if (t > 0) {
-    for (int e = tid; e < 32 * (nm + 1); e += blockDim.x) {
-      const int m = e / (nm + 1), n = e % (nm + 1);
-      float s = 0.f;
-      for (int ks = 0; ks < a.KSP; ++ks) s += a.PP[((long)ks * 32 + m) * a.NPJ + n];
-      s += a.proj_b[n];
-      if (n == nm) {
-        stopv[m] = sigm(s);
-      } else {
-        float v = s;
-        if (a.targets) v = (m < a.B) ? a.targets[((long)m * a.T_lim + (t - 1)) * nm + n] : 0.f;
-        fin[af_idx(m, n)] = (m < a.B) ? v : 0.f;
-        if (blockIdx.x == 0 && m < a.B) a.frames[((long)m * a.max_iters + (t - 1)) * nm + n] = s;
+    if (a.NPJ == 96) {
+      float v[12];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) v[j] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KSP_C; ++ks)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * j + e] += pp[ks][j][e];
+      for (int j = 0; j < 12; ++j) {
+        const int n = pq * 12 + j, m = pm;
+        if (n > nm) continue;
+        const float s = v[j] + a.proj_b[n];
+        if (n == nm) {
+          stopv[m] = sigm(s);
+        } else {
+          float x = s;
+          if (a.targets) x = (m < a.B) ? a.targets[((long)m * a.T_lim + (t - 1)) * nm + n] : 0.f;
+          fin[af_idx(m, n)] = (m < a.B) ? x : 0.f;
+          if (tile == 0 && m < a.B) a.frames[((long)m * a.max_iters + (t - 1)) * nm + n] = s;
+        }
+      }
+    } else {
+      for (int e = tid; e < 32 * (nm + 1); e += blockDim.x) {
+        const int m = e / (nm + 1), n = e % (nm + 1);
+        float s = 0.f;
+        for (int ks = 0; ks < KSP_C; ++ks) s += a.PP[((long)ks * 32 + m) * a.NPJ + n];
+        s += a.proj_b[n];
+        if (n == nm) {
+          stopv[m] = sigm(s);
+        } else {
+          float x = s;
+          if (a.targets) x = (m < a.B) ? a.targets[((long)m * a.T_lim + (t - 1)) * nm + n] : 0.f;
+          fin[af_idx(m, n)] = (m < a.B) ? x : 0.f;
+          if (tile == 0 && m < a.B) a.frames[((long)m * a.max_iters + (t - 1)) * nm + n] = s;
+        }
       }
     }
     __syncthreads();
@@ -352,13 +431,13 @@ __global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep) {
         const int f = rintf(stopv[m]) == 1.0f;
         fin_all &= f;
         fin_any |= f;
-        if (blockIdx.x == 0) a.stop[(long)m * a.max_iters + (t - 1)] = stopv[m];
+        if (tile == 0) a.stop[(long)m * a.max_iters + (t - 1)] = stopv[m];
       }
       int done = a.stop_at_any ? fin_any : fin_all;
       if (a.T_lim > 0) done = t >= a.T_lim;   // TacoTrainingHelper: time + 1 >= T_targets
       if (t >= a.max_iters) done = 1;         // dynamic_decode maximum_iterations
       s_done = done;
-      if (done && blockIdx.x == 0) {
+      if (done && tile == 0) {
         a.ctl->n_steps = t;
         a.ctl->done = 1;
       }
@@ -366,36 +445,38 @@ __global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep) {
     __syncthreads();
     if (s_done) return;
   }
+  STAMP(3);
   // ---- layer 1: relu(fin·W1 + b1) * keep / 0.5  (all 16-col tiles, K = nm) ----
-  const int P = a.P, ntile = P / 16, nsg1 = nmp / 16;
-  for (int tile = wave; tile < ntile; tile += 4) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tl = wave + 4 * i;
+    if (tl >= ntile) break;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    skinny_mfma(fin, a.pre_w1 + (long)tile * nmp * 16, 0, nsg1, acc0, acc1, lane);
+    skinny_mfma_w<5>(fin, w1[i], nsg1, acc0, acc1, lane);
+    const int n = tl * 16 + (lane & 15);
+    const float bn = a.pre_b1[n];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int n = tile * 16 + (lane & 15);
       const int m0 = (lane >> 4) * 4 + r;
-      float v0 = fmaxf(acc0[r] + a.pre_b1[n], 0.f);
-      float v1 = fmaxf(acc1[r] + a.pre_b1[n], 0.f);
-      v0 = (v0 / 0.5f) * prenet_keep(a, t, 0, m0, n);
-      v1 = (v1 / 0.5f) * prenet_keep(a, t, 0, m0 + 16, n);
+      const float v0 = (fmaxf(acc0[r] + bn, 0.f) / 0.5f) * (float)mk1[m0 * P + n];
+      const float v1 = (fmaxf(acc1[r] + bn, 0.f) / 0.5f) * (float)mk1[(m0 + 16) * P + n];
       h1[af_idx(m0, n)] = v0;
       h1[af_idx(m0 + 16, n)] = v1;
     }
   }
   __syncthreads();
+  STAMP(4);
   // ---- layer 2: this block's 16 columns, K = P split over 4 waves ----
-  const int tile = blockIdx.x, nsg2 = P / 16;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  skinny_mfma(h1, a.pre_w2 + (long)tile * P * 16, wave * nsg2 / 4, (wave + 1) * nsg2 / 4, acc0, acc1, lane);
+  skinny_mfma_w<4>(h1 + s2a * 2 * 64 * 4, w2, s2b - s2a, acc0, acc1, lane);
   reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
   float* X1 = a.X1[istep & 1];
   for (int e = tid; e < 512; e += blockDim.x) {
-    const int m = e >> 4, n = tile * 16 + (e & 15);
-    float v = fmaxf(G[e] + a.pre_b2[n], 0.f);
-    v = (v / 0.5f) * prenet_keep(a, t, 1, m, n);
+    const int m = e >> 4, j = e & 15, n = tile * 16 + j;
+    const float v = (fmaxf(G[e] + a.pre_b2[n], 0.f) / 0.5f) * (float)mk2[m * 16 + j];
     X1[af_idx(m, n)] = v;
   }
+  STAMP(5);
 }
 
 // Zoneout-LSTM layer (modules.py:220-248 on TF LSTMCell): block g owns hidden units [4g, 4g+4)
@@ -403,6 +484,7 @@ __global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep) {
 //   X [32 x K AF] input (h_prev at column hprev_off); writes h_new (raw LSTM output) into
 //   Xo at column ho_off, the zoned h into Xz at column hz_off, c in place.
 struct LstmArgs {
+  long long* stamps = nullptr;
   const DecCtl* ctl;
   const float* X; int K; int hprev_off;
   const float* W; const float* b;
@@ -412,15 +494,22 @@ struct LstmArgs {
   float zo, one_m_zo;
 };
 
-__global__ __launch_bounds__(256) void k_lstm(LstmArgs a) {
-  __shared__ float red[4 * 512];
+template <int NPW>
+__global__ __launch_bounds__(512) void k_lstm(LstmArgs a) {
+  __shared__ float red[8 * 512];
   __shared__ float G[512];
-  if (a.ctl->done) return;
+  STAMP(16);
+  const int done = a.ctl->done;  // read early, tested once the weight stream is in flight
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nsg = a.K / 16;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  skinny_mfma(a.X, a.W + (long)g * a.K * 16, wave * nsg / 4, (wave + 1) * nsg / 4, acc0, acc1, lane);
-  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
+  const float* Wg = a.W + (long)g * a.K * 16;
+  if constexpr (NPW > 0) skinny_mfma_all<NPW>(a.X, Wg, wave * NPW, acc0, acc1, lane);
+  else skinny_mfma(a.X, Wg, wave * nsg / 8, (wave + 1) * nsg / 8, acc0, acc1, lane);
+  STAMP(17);
+  if (done) return;
+  reduce_waves_32x16<8>(acc0, acc1, red, G, wave, lane, tid);
+  STAMP(18);
   if (tid < 128) {
     const int m = tid >> 2, uu = tid & 3, u = 4 * g + uu;
     const float* bb = a.b + g * 16;
@@ -437,6 +526,18 @@ __global__ __launch_bounds__(256) void k_lstm(LstmArgs a) {
     a.Xo[af_idx(m, a.ho_off + u)] = hn;
     a.Xz[af_idx(m, a.hz_off + u)] = a.one_m_zo * hn + a.zo * hprev;
   }
+  STAMP(19);
+}
+
+static void launch_lstm(const LstmArgs& l, int H, hipStream_t s) {
+  const int nsg = l.K / 16;
+  const dim3 grid(H / 4), blk(512);
+  if (nsg % 8 == 0 && nsg / 8 == 18) hipLaunchKernelGGL(k_lstm<18>, grid, blk, 0, s, l);
+  else if (nsg % 8 == 0 && nsg / 8 == 16) hipLaunchKernelGGL(k_lstm<16>, grid, blk, 0, s, l);
+  else if (nsg % 8 == 0 && nsg / 8 == 8) hipLaunchKernelGGL(k_lstm<8>, grid, blk, 0, s, l);
+  else if (nsg % 8 == 0 && nsg / 8 == 4) hipLaunchKernelGGL(k_lstm<4>, grid, blk, 0, s, l);
+  else if (nsg % 8 == 0 && nsg / 8 == 2) hipLaunchKernelGGL(k_lstm<2>, grid, blk, 0, s, l);
+  else hipLaunchKernelGGL(k_lstm<0>, grid, blk, 0, s, l);
 }
 
 // Split-K skinny GEMM writing partial sums: out[ks][m][ldo] (cols tile*16..) for the query layer
@@ -448,17 +549,21 @@ struct PartArgs {
   float* out; int ldo; int ntile; int KS;
 };
 
+template <int NPW>
 __global__ __launch_bounds__(256) void k_partial(PartArgs a) {
   __shared__ float red[4 * 512];
   __shared__ float G[512];
-  if (a.ctl->done) return;
+  const int done = a.ctl->done;
   const int tile = blockIdx.x % a.ntile, ks = blockIdx.x / a.ntile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nsg = a.K / 16;
   const int s0 = ks * nsg / a.KS, s1 = (ks + 1) * nsg / a.KS;
   const int n = s1 - s0;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  skinny_mfma(a.X, a.W + (long)tile * a.K * 16, s0 + wave * n / 4, s0 + (wave + 1) * n / 4, acc0, acc1, lane);
+  const float* Wt = a.W + (long)tile * a.K * 16;
+  if constexpr (NPW > 0) skinny_mfma_all<NPW>(a.X, Wt, s0 + wave * NPW, acc0, acc1, lane);
+  else skinny_mfma(a.X, Wt, s0 + wave * n / 4, s0 + (wave + 1) * n / 4, acc0, acc1, lane);
+  if (done) return;
   reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
   for (int e = tid; e < 512; e += blockDim.x) {
     const int m = e >> 4, c = tile * 16 + (e & 15);
@@ -466,106 +571,194 @@ __global__ __launch_bounds__(256) void k_partial(PartArgs a) {
   }
 }
 
+static void launch_partial(const PartArgs& p, hipStream_t s) {
+  const int nsg = p.K / 16;
+  const dim3 grid(p.ntile * p.KS), blk(256);
+  const bool even = nsg % (p.KS * 4) == 0;
+  const int npw = even ? nsg / (p.KS * 4) : 0;
+  if (npw == 4) hipLaunchKernelGGL(k_partial<4>, grid, blk, 0, s, p);
+  else if (npw == 2) hipLaunchKernelGGL(k_partial<2>, grid, blk, 0, s, p);
+  else if (npw == 8) hipLaunchKernelGGL(k_partial<8>, grid, blk, 0, s, p);
+  else hipLaunchKernelGGL(k_partial<0>, grid, blk, 0, s, p);
+}
+
 // Location-sensitive energies (attention.py:37-69, 186-215) for 32 encoder steps of one row:
-// q = Σ query partials; f = conv1d(cum, 31 taps) + b; loc = f·W_loc;
-// e_t = Σ_k v_a[k]·tanh(keys + q + loc + b_a); window constraint; -inf past the row's length.
+//   q = Σ query partials;  f = im2col(cum, 31 taps)·W_conv + b  (MFMA, K = taps);
+//   loc = f·W_loc (MFMA, K = filters);  e_t = Σ_k v_a[k]·tanh(keys + q + loc + b_a)
+// then the synthesis window constraint and -inf past the row's length (TF _maybe_mask_score).
 __global__ __launch_bounds__(256) void k_energy(DecArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  if (a.ctl->done) return;
-  const int b = blockIdx.x, t0 = blockIdx.y * 32, tid = threadIdx.x;
-  const int A = a.A, F = a.F, KL = a.KL, padl = (KL - 1) / 2;
-  float* q = sm;                       // [A]
-  float* win = q + A;                  // [32 + KL - 1]
-  float* f = win + 32 + KL;            // [32][F+1]
-  float* wl = f + 32 * (F + 1);        // [F][A]
+  __shared__ __attribute__((aligned(16))) float A1[32 * 64];  // AF [32 t][KLp taps]
+  __shared__ __attribute__((aligned(16))) float A2[32 * 64];  // AF [32 t][Fp filters]
+  __shared__ float q[256];
+  __shared__ float win[32 + 64];
+  __shared__ float ep[4][32];
+  STAMP(8);
+  const int done = a.ctl->done;
+  const int b = blockIdx.x, t0 = blockIdx.y * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int A = a.A, KL = a.KL, KLp = a.KLp, Fp = a.Fp, padl = (KL - 1) / 2;
+  // prefetch the keys this lane consumes after the location MFMA (<= 4 tiles x 8 rows)
+  float kv[4][8];
+  const int ntl = A / 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tile = wave + 4 * i;
+    const int k = tile * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int t = t0 + (lane >> 4) * 4 + (r & 3) + (r >> 2) * 16;
+      kv[i][r] = (tile < ntl && t < a.T_in) ? a.keys[((long)b * a.T_in + t) * A + k] : 0.f;
+    }
+  }
+  const f32x4* CWv = reinterpret_cast<const f32x4*>(a.loc_cw);
+  const f32x4* LWv = reinterpret_cast<const f32x4*>(a.loc_w);
+  const int nkc = KLp / 16, nkf = Fp / 16;
+  f32x4 wcv[4], wlv[4][4];
+  float vkv[4], bkv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (wave < nkf && j < nkc) wcv[j] = CWv[((long)wave * nkc + j) * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tile = wave + 4 * i;
+    const int k = tile * 16 + (lane & 15);
+    vkv[i] = tile < ntl ? a.va[k] : 0.f;
+    bkv[i] = tile < ntl ? a.ba[k] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (tile < ntl && j < nkf) wlv[i][j] = LWv[((long)tile * nkf + j) * 64 + lane];
+  }
   for (int k = tid; k < A; k += blockDim.x) {
+    float qp[KSQ_C];
+#pragma unroll
+    for (int ks = 0; ks < KSQ_C; ++ks) qp[ks] = a.Qp[((long)ks * 32 + b) * A + k];
     float s = 0.f;
-    for (int ks = 0; ks < a.KSQ; ++ks) s += a.Qp[((long)ks * 32 + b) * A + k];
+#pragma unroll
+    for (int ks = 0; ks < KSQ_C; ++ks) s += qp[ks];
     q[k] = s;
   }
   for (int i = tid; i < 32 + KL - 1; i += blockDim.x) {
     const int t = t0 - padl + i;
     win[i] = (t >= 0 && t < a.T_in) ? a.cum[(long)b * a.T_in + t] : 0.f;
   }
-  for (int i = tid; i < F * A; i += blockDim.x) wl[i] = a.loc_w[i];
+  if (done) return;
   __syncthreads();
-  for (int e = tid; e < 32 * F; e += blockDim.x) {
-    const int tt = e / F, fl = e % F;
-    float s = 0.f;
-    for (int tap = 0; tap < KL; ++tap) s += win[tt + tap] * a.loc_cw[tap * F + fl];
-    f[tt * (F + 1) + fl] = s + a.loc_cb[fl];
+  STAMP(9);
+  for (int e = tid; e < 32 * KLp; e += blockDim.x) {
+    const int t = e / KLp, tap = e - t * KLp;
+    A1[af_idx(t, tap)] = tap < KL ? win[t + tap] : 0.f;
   }
   __syncthreads();
-  // thread -> (tt = tid>>3, 16-wide k slice kq)
-  const int tt = tid >> 3, kq = tid & 7;
-  const int t = t0 + tt;
-  float e = 0.f;
-  if (t < a.T_in) {
-    const float* kr = a.keys + ((long)b * a.T_in + t) * A;
-    for (int k = kq * (A / 8); k < (kq + 1) * (A / 8); ++k) {
-      float loc = 0.f;
-      for (int fl = 0; fl < F; ++fl) loc += f[tt * (F + 1) + fl] * wl[fl * A + k];
-      e += a.va[k] * tanhf(kr[k] + q[k] + loc + a.ba[k]);
+  if (wave < Fp / 16) {  // location convolution, one 16-filter tile per wave
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+    skinny_mfma_w<4>(A1, wcv, nkc, c0, c1, lane);
+    const int n = wave * 16 + (lane & 15);
+    const float cb = n < a.F ? a.loc_cb[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = (lane >> 4) * 4 + r;
+      A2[af_idx(m, n)] = n < a.F ? c0[r] + cb : 0.f;
+      A2[af_idx(m + 16, n)] = n < a.F ? c1[r] + cb : 0.f;
     }
   }
-  e += __shfl_xor(e, 1);
-  e += __shfl_xor(e, 2);
-  e += __shfl_xor(e, 4);
-  if (kq == 0 && t < a.T_in) {
-    if (a.constraint) {
-      const int pm = a.max_att[b], w = a.win;
-      bool masked;
-      if (a.monotonic) masked = (t < pm) || (t >= pm + w);
-      else masked = (t < pm - (w / 2 + (w % 2 != 0 ? 1 : 0))) || (t >= pm + w / 2);
-      if (masked) e = -4294967296.0f;  // -2**32 + 1 in fp32
+  __syncthreads();
+  STAMP(10);
+  float e0[4] = {0.f, 0.f, 0.f, 0.f}, e1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tile = wave + 4 * i;
+    if (tile >= ntl) break;
+    f32x4 l0 = {0.f, 0.f, 0.f, 0.f}, l1 = {0.f, 0.f, 0.f, 0.f};
+    skinny_mfma_w<4>(A2, wlv[i], nkf, l0, l1, lane);
+    const int k = tile * 16 + (lane & 15);
+    const float vk = vkv[i], bk = bkv[i], qk = q[k];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ta = t0 + (lane >> 4) * 4 + r, tb = ta + 16;
+      if (ta < a.T_in) e0[r] += vk * tanh_fast(kv[i][r] + qk + l0[r] + bk);
+      if (tb < a.T_in) e1[r] += vk * tanh_fast(kv[i][4 + r] + qk + l1[r] + bk);
     }
-    if (a.mask_encoder && t >= a.lengths[b]) e = -INFINITY;
-    a.energy[(long)b * a.T_in + t] = e;
   }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      e0[r] += __shfl_xor(e0[r], o);
+      e1[r] += __shfl_xor(e1[r], o);
+    }
+  STAMP(11);
+  if ((lane & 15) == 0)
+    for (int r = 0; r < 4; ++r) {
+      ep[wave][(lane >> 4) * 4 + r] = e0[r];
+      ep[wave][16 + (lane >> 4) * 4 + r] = e1[r];
+    }
+  __syncthreads();
+  if (tid < 32) {
+    const int t = t0 + tid;
+    if (t < a.T_in) {
+      float e = ep[0][tid] + ep[1][tid] + ep[2][tid] + ep[3][tid];
+      if (a.constraint) {
+        const int pm = a.max_att[b], w = a.win;
+        bool masked;
+        if (a.monotonic) masked = (t < pm) || (t >= pm + w);
+        else masked = (t < pm - (w / 2 + (w % 2 != 0 ? 1 : 0))) || (t >= pm + w / 2);
+        if (masked) e = -4294967296.0f;  // -2**32 + 1 in fp32
+      }
+      if (a.mask_encoder && t >= a.lengths[b]) e = -INFINITY;
+      a.energy[(long)b * a.T_in + t] = e;
+    }
+  }
+  STAMP(12);
 }
 
 // softmax → alignments, context = alignments · values for 64 memory channels of one row
 // (attention.py:10-35, 217-225); the dc==0 block also updates cum/max_att and writes alignments.
-__global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep) {
+__global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t_step) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  if (a.ctl->done) return;
+  const int done = a.ctl->done;
   const int b = blockIdx.x, dc = blockIdx.y, tid = threadIdx.x;
   const int T = a.T_in;
-  float* al = sm;               // [T]
-  float* red = al + ((T + 3) & ~3);   // [256*4]
+  float* al = sm;                      // [T]
+  float* red = al + ((T + 3) & ~3);    // [4*16*16]
   __shared__ float s_max, s_sum;
+  // values for this block's 64 channels are independent of the softmax: issue them first
+  const int tq = tid >> 4, dq = tid & 15;
+  const int d = dc * 64 + dq * 4;
+  const float* vr = a.values + (long)b * T * a.Dm + d;
+  f32x4 v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int t = tq + 16 * i;
+    if (t < T && d < a.Dm) v[i] = *reinterpret_cast<const f32x4*>(vr + (long)t * a.Dm);
+    else v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   for (int i = tid; i < T; i += blockDim.x) al[i] = a.energy[(long)b * T + i];
+  if (done) return;
   __syncthreads();
   if (tid < 64) {
     float mx = -INFINITY;
     for (int i = tid; i < T; i += 64) mx = fmaxf(mx, al[i]);
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    if (tid == 0) s_max = mx;
+    float sum = 0.f;
+    for (int i = tid; i < T; i += 64) sum += expf(al[i] - mx);
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if (tid == 0) { s_max = mx; s_sum = sum; }
   }
   __syncthreads();
-  for (int i = tid; i < T; i += blockDim.x) al[i] = expf(al[i] - s_max);
+  for (int i = tid; i < T; i += blockDim.x) al[i] = expf(al[i] - s_max) / s_sum;
   __syncthreads();
-  if (tid < 64) {
-    float s = 0.f;
-    for (int i = tid; i < T; i += 64) s += al[i];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (tid == 0) s_sum = s;
-  }
-  __syncthreads();
-  for (int i = tid; i < T; i += blockDim.x) al[i] = al[i] / s_sum;
-  __syncthreads();
-  // context for channels [dc*64, dc*64+64)
-  const int tq = tid >> 4, dq = tid & 15;
-  const int d = dc * 64 + dq * 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (d < a.Dm) {
-    const float* vr = a.values + (long)b * T * a.Dm + d;
-    for (int t = tq; t < T; t += 16) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(vr + (long)t * a.Dm);
-      const float w = al[t];
-      acc[0] += w * v[0]; acc[1] += w * v[1]; acc[2] += w * v[2]; acc[3] += w * v[3];
-    }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int t = tq + 16 * i;
+    const float w = t < T ? al[t] : 0.f;
+    acc[0] += w * v[i][0]; acc[1] += w * v[i][1]; acc[2] += w * v[i][2]; acc[3] += w * v[i][3];
   }
+  if (d < a.Dm)
+    for (int t = tq + 256; t < T; t += 16) {  // tail for T_in > 256
+      const f32x4 x = *reinterpret_cast<const f32x4*>(vr + (long)t * a.Dm);
+      const float w = al[t];
+      acc[0] += w * x[0]; acc[1] += w * x[1]; acc[2] += w * x[2]; acc[3] += w * x[3];
+    }
   for (int j = 0; j < 4; ++j) red[(j * 16 + dq) * 16 + tq] = acc[j];
   __syncthreads();
   if (tid < 64) {
@@ -579,7 +772,6 @@ __global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep) {
     }
   }
   if (dc == 0) {
-    const int t_step = a.ctl->tbase + istep;
     for (int i = tid; i < T; i += blockDim.x) {
       float* c = a.cum + (long)b * T + i;
       *c = a.cumulative ? al[i] + *c : al[i];
@@ -598,10 +790,6 @@ __global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep) {
       if (tid == 0) a.max_att[b] = bi;
     }
   }
-}
-
-__global__ void k_advance(DecCtl* ctl, int S) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) ctl->tbase += S;
 }
 
 // decoder_output clip (tacotron.py:362-363): dst[b][t][n] = clip(src[b][t][n])
@@ -627,7 +815,7 @@ struct RefNetDev {
 };
 
 struct Graph {
-  hipGraphExec_t exec = nullptr;
+  std::vector<hipGraphExec_t> chunks;  // chunk c covers decoder steps [c*S, c*S+S)
   std::tuple<int, int, int, int, const void*, const void*, uint64_t, const void*, const void*, const void*> key;
 };
 
@@ -639,7 +827,7 @@ struct tt2_ctx {
   hipStream_t stream = nullptr;
   tt2::WeightMap host;
   bool finalized = false;
-  int nm, E, Cenc, U, Dm, A, F, KL, P, H, PC, SW, K1, K2, Kp, NPJ, KSQ = 4, KSP = 8;
+  int nm, E, Cenc, U, Dm, A, F, KL, P, H, PC, SW, K1, K2, Kp, NPJ, KSQ = tt2::KSQ_C, KSP = tt2::KSP_C, KLp, Fp;
   int nref;
   // weights
   tt2::DevBuf emb;
@@ -653,13 +841,18 @@ struct tt2_ctx {
   // activations
   tt2::DevBuf ids, lens, refm[2], x_a, x_b, xproj, enc_out, enc_h, enc_c, conv_a, conv_b, ref_out, style,
       values, keys;
-  tt2::DevBuf X1[2], X2[2], Xp, c1, c2, Qp, energy, cum, max_att, PP, ctl, masks, targets;
+  tt2::DevBuf X1[2], X2[2], Xp, c1, c2, Qp, energy, cum, max_att, PP, ctl, masks, gmasks, targets;
   tt2::DevBuf frames, stop, align, dec, post_a, post_b, mel;
   int* ctl_host = nullptr;  // pinned [2 slots]
   int B = 0, T_in = 0, n_steps = 0, last_max_iters = 0;
   bool encoded = false, decoded = false;
   tt2::Graph graph;
   static constexpr int S = 16;  // decoder steps per captured graph chunk
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // synthesize phase timing
+  bool timed = false;
+  tt2::DecArgs last_args;
+  long long stamps_host[64] = {0};
+  bool have_args = false;
 };
 
 namespace tt2 {
@@ -803,9 +996,18 @@ static void finalize(tt2_ctx* c) {
     upload(c->q_w, pack_wf(q.data.data(), c->H, c->A, cols, c->H));
   }
   const std::string la = P + "decoder/Location_Sensitive_Attention/";
-  upload(c->loc_cw, need(wm, la + "location_features_convolution/kernel", {c->KL, 1, c->F}));
-  upload(c->loc_cb, need(wm, la + "location_features_convolution/bias", {c->F}));
-  upload(c->loc_w, need(wm, la + "location_features_layer/kernel", {c->F, c->A}));
+  {
+    // conv [KL][1][F] -> Fp/16 WF tiles over K = KLp taps; dense [F][A] -> A/16 WF tiles over K = Fp
+    const auto& cw = need(wm, la + "location_features_convolution/kernel", {c->KL, 1, c->F});
+    std::vector<int> fcols;
+    for (int j = 0; j < c->Fp; ++j) fcols.push_back(j < c->F ? j : -1);
+    upload(c->loc_cw, pack_wf(cw.data.data(), c->KL, c->F, fcols, c->KLp));
+    upload(c->loc_cb, need(wm, la + "location_features_convolution/bias", {c->F}));
+    const auto& lw = need(wm, la + "location_features_layer/kernel", {c->F, c->A});
+    std::vector<int> acols;
+    for (int j = 0; j < c->A; ++j) acols.push_back(j);
+    upload(c->loc_w, pack_wf(lw.data.data(), c->F, c->A, acols, c->Fp));
+  }
   upload(c->va, need(wm, la + "attention_variable_projection", {c->A}));
   upload(c->ba, need(wm, la + "attention_bias", {c->A}));
   {
@@ -883,6 +1085,7 @@ static void alloc_acts(tt2_ctx* c) {
   c->cum.alloc(B * T * 4);
   c->max_att.alloc(64 * 4);
   c->PP.alloc((long)c->KSP * 32 * c->NPJ * 4);
+  c->gmasks.alloc((size_t)MI * 2 * B * c->P);
   c->ctl.alloc(sizeof(DecCtl));
   c->frames.alloc(B * MI * c->nm * 4);
   c->stop.alloc(B * MI * 4);
@@ -1013,6 +1216,7 @@ static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, 
   a.pre_w1 = c->pre_w1.as<float>(); a.pre_b1 = c->pre_b1.as<float>();
   a.pre_w2 = c->pre_w2.as<float>(); a.pre_b2 = c->pre_b2.as<float>();
   a.l1_w = c->l1_w.as<float>(); a.l1_b = c->l1_b.as<float>(); a.l2_w = c->l2_w.as<float>(); a.l2_b = c->l2_b.as<float>();
+  a.KLp = c->KLp; a.Fp = c->Fp;
   a.q_w = c->q_w.as<float>(); a.loc_cw = c->loc_cw.as<float>(); a.loc_cb = c->loc_cb.as<float>();
   a.loc_w = c->loc_w.as<float>(); a.va = c->va.as<float>(); a.ba = c->ba.as<float>();
   a.proj_w = c->proj_w.as<float>(); a.proj_b = c->proj_b.as<float>();
@@ -1022,34 +1226,33 @@ static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, 
   a.Qp = c->Qp.as<float>(); a.energy = c->energy.as<float>(); a.cum = c->cum.as<float>();
   a.max_att = c->max_att.as<int>(); a.PP = c->PP.as<float>();
   a.KSQ = c->KSQ; a.KSP = c->KSP; a.NPJ = c->NPJ;
-  a.masks = masks_d; a.seed = seed; a.targets = targets_d;
+  a.masks = masks_d; a.seed = seed; a.targets = targets_d; a.stamps = nullptr;
   a.frames = frames_d; a.stop = stop_d; a.align = align_d;
   return a;
 }
 
-static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, hipStream_t s) {
+static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, int t, hipStream_t s) {
   const int par = i & 1;
-  hipLaunchKernelGGL(k_prenet, dim3(c->P / 16), dim3(256), 0, s, a, i);
+  hipLaunchKernelGGL(k_prenet, dim3(c->P / 16), dim3(256), 0, s, a, i, t);
   LstmArgs l1;
   l1.ctl = a.ctl; l1.X = a.X1[par]; l1.K = c->K1; l1.hprev_off = c->P + c->Dm; l1.W = a.l1_w; l1.b = a.l1_b;
   l1.c = a.c1; l1.H = c->H; l1.Xo = a.X2[par]; l1.ho_off = 0; l1.Xz = a.X1[par ^ 1]; l1.hz_off = c->P + c->Dm;
   l1.zo = a.zo; l1.one_m_zo = a.one_m_zo;
-  hipLaunchKernelGGL(k_lstm, dim3(c->H / 4), dim3(256), 0, s, l1);
+  launch_lstm(l1, c->H, s);
   LstmArgs l2 = l1;
   l2.X = a.X2[par]; l2.K = c->K2; l2.hprev_off = c->H; l2.W = a.l2_w; l2.b = a.l2_b; l2.c = a.c2;
   l2.Xo = a.Xp; l2.ho_off = 0; l2.Xz = a.X2[par ^ 1]; l2.hz_off = c->H;
-  hipLaunchKernelGGL(k_lstm, dim3(c->H / 4), dim3(256), 0, s, l2);
+  launch_lstm(l2, c->H, s);
   PartArgs q;
   q.ctl = a.ctl; q.X = a.Xp; q.K = c->H; q.W = a.q_w; q.out = a.Qp; q.ldo = c->A; q.ntile = c->A / 16; q.KS = c->KSQ;
-  hipLaunchKernelGGL(k_partial, dim3(q.ntile * q.KS), dim3(256), 0, s, q);
-  const size_t shm_e = sizeof(float) * (c->A + 32 + c->KL + 32 * (c->F + 1) + c->F * c->A);
-  hipLaunchKernelGGL(k_energy, dim3(a.B, cdiv(a.T_in, 32)), dim3(256), shm_e, s, a);
-  const size_t shm_s = sizeof(float) * (((a.T_in + 3) & ~3) + 256 * 4);
-  hipLaunchKernelGGL(k_softmax_ctx, dim3(a.B, cdiv(c->Dm, 64)), dim3(256), shm_s, s, a, i);
+  launch_partial(q, s);
+  hipLaunchKernelGGL(k_energy, dim3(a.B, cdiv(a.T_in, 32)), dim3(256), 0, s, a);
+  const size_t shm_s = sizeof(float) * (((a.T_in + 3) & ~3) + 4 * 16 * 16);
+  hipLaunchKernelGGL(k_softmax_ctx, dim3(a.B, cdiv(c->Dm, 64)), dim3(256), shm_s, s, a, i, t);
   PartArgs p;
   p.ctl = a.ctl; p.X = a.Xp; p.K = c->Kp; p.W = a.proj_w; p.out = a.PP; p.ldo = c->NPJ; p.ntile = c->NPJ / 16;
   p.KS = c->KSP;
-  hipLaunchKernelGGL(k_partial, dim3(p.ntile * p.KS), dim3(256), 0, s, p);
+  launch_partial(p, s);
 }
 
 static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64_t seed, const float* targets_d,
@@ -1068,31 +1271,48 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
   TT2_HIP(hipMemsetAsync(c->cum.p, 0, c->cum.bytes, s));
   TT2_HIP(hipMemsetAsync(c->max_att.p, 0, c->max_att.bytes, s));
   TT2_HIP(hipMemsetAsync(c->ctl.p, 0, sizeof(DecCtl), s));
+  if (!masks_d) {  // prenet dropout keep bits from the counter-based device RNG
+    const long n = (long)max_iters * 2 * c->B * c->P;
+    hipLaunchKernelGGL(k_gen_masks, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, s,
+                       c->gmasks.as<uint8_t>(), n, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x9e3779b9u);
+    TT2_HIP(hipGetLastError());
+    masks_d = c->gmasks.as<uint8_t>();
+  }
   const DecArgs a = make_dec_args(c, max_iters, masks_d, seed, targets_d, T_lim, frames_d, stop_d, align_d);
+  c->last_args = a;
+  c->have_args = true;
   auto key = std::make_tuple(c->B, c->T_in, max_iters, T_lim, (const void*)masks_d, (const void*)targets_d, seed,
                              (const void*)frames_d, (const void*)stop_d, (const void*)align_d);
-  if (!c->graph.exec || c->graph.key != key) {
-    if (c->graph.exec) (void)hipGraphExecDestroy(c->graph.exec);
-    c->graph.exec = nullptr;
-    hipStream_t cs;
-    TT2_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-    hipGraph_t gr;
-    TT2_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < tt2_ctx::S; ++i) enqueue_step(c, a, i, cs);
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, cs, a.ctl, tt2_ctx::S);
-    TT2_HIP(hipStreamEndCapture(cs, &gr));
-    TT2_HIP(hipGraphInstantiate(&c->graph.exec, gr, nullptr, nullptr, 0));
-    TT2_HIP(hipGraphDestroy(gr));
-    TT2_HIP(hipStreamDestroy(cs));
+  if (c->graph.key != key) {
+    for (auto g : c->graph.chunks)
+      if (g) (void)hipGraphExecDestroy(g);
+    c->graph.chunks.clear();
     c->graph.key = key;
   }
+  // one captured graph per S-step chunk (step index baked into the kernel arguments),
+  // instantiated on first use and replayed by later calls with the same shapes
+  auto chunk_graph = [&](int ch) -> hipGraphExec_t {
+    if ((int)c->graph.chunks.size() <= ch) c->graph.chunks.resize(ch + 1, nullptr);
+    if (!c->graph.chunks[ch]) {
+      hipStream_t cs;
+      TT2_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+      hipGraph_t gr;
+      TT2_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+      for (int i = 0; i < tt2_ctx::S; ++i) enqueue_step(c, a, i, ch * tt2_ctx::S + i, cs);
+      TT2_HIP(hipStreamEndCapture(cs, &gr));
+      TT2_HIP(hipGraphInstantiate(&c->graph.chunks[ch], gr, nullptr, nullptr, 0));
+      TT2_HIP(hipGraphDestroy(gr));
+      TT2_HIP(hipStreamDestroy(cs));
+    }
+    return c->graph.chunks[ch];
+  };
   // launch chunks; watch the device `done` flag one chunk behind so the GPU never idles
   const int max_chunks = (max_iters + 1 + tt2_ctx::S - 1) / tt2_ctx::S;
   hipEvent_t ev[2];
   TT2_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
   TT2_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
   for (int ch = 0; ch < max_chunks; ++ch) {
-    TT2_HIP(hipGraphLaunch(c->graph.exec, s));
+    TT2_HIP(hipGraphLaunch(chunk_graph(ch), s));
     TT2_HIP(hipMemcpyAsync(&c->ctl_host[ch & 1], &c->ctl.as<DecCtl>()->done, sizeof(int), hipMemcpyDeviceToHost, s));
     TT2_HIP(hipEventRecord(ev[ch & 1], s));
     if (ch >= 1) {
@@ -1192,6 +1412,9 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     c->nm = cfg->num_mels; c->E = cfg->embedding_dim; c->Cenc = cfg->enc_conv_channels; c->U = cfg->encoder_lstm_units;
     c->A = cfg->attention_dim; c->F = cfg->attention_filters; c->KL = cfg->attention_kernel; c->P = cfg->prenet_units;
     c->H = cfg->decoder_lstm_units; c->PC = cfg->postnet_channels;
+    c->KLp = (c->KL + 15) / 16 * 16; c->Fp = (c->F + 15) / 16 * 16;
+    TT2_CHECK(c->KLp <= 64 && c->Fp <= 64, TT2_ERR_INVALID_ARG, "attention_kernel / attention_filters must be <= 64");
+    TT2_CHECK(c->A <= 256, TT2_ERR_INVALID_ARG, "attention_dim must be <= 256");
     c->nref = cfg->use_gst ? (cfg->emt_only ? 1 : 2) : 0;
     c->SW = cfg->use_gst ? c->nref * cfg->style_embed_depth : 0;
     c->Dm = 2 * c->U + c->SW;
@@ -1200,6 +1423,7 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     c->K1 = c->P + c->Dm + c->H; c->K2 = 2 * c->H; c->Kp = c->H + c->Dm;
     c->NPJ = ((c->nm + 1 + 15) / 16) * 16;
     alloc_acts(c.get());
+    for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
     *out = c.release();
   });
 }
@@ -1207,8 +1431,11 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
 void tt2_destroy(tt2_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->dev);
-  if (c->graph.exec) (void)hipGraphExecDestroy(c->graph.exec);
+  for (auto g : c->graph.chunks)
+    if (g) (void)hipGraphExecDestroy(g);
   if (c->ctl_host) (void)hipHostFree(c->ctl_host);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;  // DevBuf destructors release the device buffers
 }
@@ -1340,11 +1567,100 @@ tt2_status tt2_synthesize_dev(tt2_ctx* c, const int32_t* ids_d, const int32_t* l
     TT2_HIP(hipMemcpyAsync(c->lens.p, lengths_d, sizeof(int) * B, hipMemcpyDeviceToDevice, s));
     const float* ref_d[2] = {ref_emt_d, ref_spk_d};
     const int trs[2] = {T_ref_emt, T_ref_spk};
+    TT2_HIP(hipEventRecord(c->ev[0], s));
     encode_dev(c, ids_d, c->lens.as<int>(), lengths_host, B, T_in, ref_d, trs, s);
+    TT2_HIP(hipEventRecord(c->ev[1], s));
     decode_dev(c, max_iters, prenet_masks_d, seed, nullptr, 0, c->frames.as<float>(),
                stop_d ? stop_d : c->stop.as<float>(), nullptr, s);
+    TT2_HIP(hipEventRecord(c->ev[2], s));
     postnet_dev(c, c->frames.as<float>(), (long)max_iters * c->nm, B, c->n_steps, c->dec.as<float>(), mel_d, s);
+    TT2_HIP(hipEventRecord(c->ev[3], s));
+    c->timed = true;
     *n_steps_host = c->n_steps;
+  });
+}
+
+tt2_status tt2_last_timings(tt2_ctx* c, float* ms3) {
+  return guard([&] {
+    TT2_CHECK(c && ms3, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_CHECK(c->timed, TT2_ERR_STATE, "no timed tt2_synthesize_dev call yet");
+    TT2_HIP(hipEventSynchronize(c->ev[3]));
+    for (int i = 0; i < 3; ++i) TT2_HIP(hipEventElapsedTime(&ms3[i], c->ev[i], c->ev[i + 1]));
+  });
+}
+
+static long long* g_stamps_dev = nullptr;
+
+tt2_status tt2_profile_decoder_kernels(tt2_ctx* c, int iters, float* avg_us) {
+  return guard([&] {
+    TT2_CHECK(c && avg_us && iters >= 1, TT2_ERR_INVALID_ARG, "bad argument");
+    TT2_CHECK(c->have_args, TT2_ERR_STATE, "tt2_profile_decoder_kernels needs a prior decode");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = c->stream;
+    DecArgs a = c->last_args;
+    if (!g_stamps_dev) TT2_HIP(hipMalloc(&g_stamps_dev, 64 * sizeof(long long)));
+    TT2_HIP(hipMemsetAsync(g_stamps_dev, 0, 64 * sizeof(long long), s));
+    a.stamps = g_stamps_dev;
+    a.frames = c->frames.as<float>();
+    a.stop = c->stop.as<float>();
+    a.align = nullptr;
+    TT2_HIP(hipMemsetAsync(c->ctl.p, 0, sizeof(DecCtl), s));  // done = 0, tbase = 0
+    hipEvent_t e0, e1;
+    TT2_HIP(hipEventCreate(&e0));
+    TT2_HIP(hipEventCreate(&e1));
+    LstmArgs l1;
+    l1.stamps = a.stamps;
+    l1.ctl = a.ctl; l1.K = c->K1; l1.hprev_off = c->P + c->Dm; l1.W = a.l1_w; l1.b = a.l1_b; l1.c = a.c1;
+    l1.H = c->H; l1.ho_off = 0; l1.hz_off = c->P + c->Dm; l1.zo = a.zo; l1.one_m_zo = a.one_m_zo;
+    LstmArgs l2 = l1;
+    l2.K = c->K2; l2.hprev_off = c->H; l2.W = a.l2_w; l2.b = a.l2_b; l2.c = a.c2; l2.ho_off = 0; l2.hz_off = c->H;
+    PartArgs q;
+    q.ctl = a.ctl; q.X = a.Xp; q.K = c->H; q.W = a.q_w; q.out = a.Qp; q.ldo = c->A; q.ntile = c->A / 16; q.KS = c->KSQ;
+    PartArgs p;
+    p.ctl = a.ctl; p.X = a.Xp; p.K = c->Kp; p.W = a.proj_w; p.out = a.PP; p.ldo = c->NPJ; p.ntile = c->NPJ / 16;
+    p.KS = c->KSP;
+    const size_t shm_s = sizeof(float) * (((a.T_in + 3) & ~3) + 4 * 16 * 16);
+    for (int k = 0; k < 7; ++k) {
+      // `iters` back-to-back launches between one event pair: per-launch time = device
+      // duration + the inter-kernel gap (comparable with rocprofv3 kernel-trace averages)
+      TT2_HIP(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; ++i) {
+        const int par = i & 1;
+        switch (k) {
+          case 0: hipLaunchKernelGGL(k_prenet, dim3(c->P / 16), dim3(256), 0, s, a, 0, 0); break;
+          case 1: {
+            LstmArgs l = par ? l2 : l1;
+            l.X = par ? a.X2[0] : a.X1[0]; l.Xo = par ? a.Xp : a.X2[0]; l.Xz = par ? a.X2[1] : a.X1[1];
+            launch_lstm(l, c->H, s);
+          } break;
+          case 2: launch_partial(q, s); break;
+          case 3: hipLaunchKernelGGL(k_energy, dim3(a.B, cdiv(a.T_in, 32)), dim3(256), 0, s, a); break;
+          case 4: hipLaunchKernelGGL(k_softmax_ctx, dim3(a.B, cdiv(c->Dm, 64)), dim3(256), shm_s, s, a, 0, 0); break;
+          case 5: launch_partial(p, s); break;
+          case 6: {
+            LstmArgs l = l2;
+            l.X = a.X2[0]; l.Xo = a.Xp; l.Xz = a.X2[1];
+            launch_lstm(l, c->H, s);
+          } break;
+        }
+      }
+      TT2_HIP(hipEventRecord(e1, s));
+      TT2_HIP(hipEventSynchronize(e1));
+      float ms = 0.f;
+      TT2_HIP(hipEventElapsedTime(&ms, e0, e1));
+      avg_us[k] = 1000.f * ms / iters;
+    }
+    TT2_HIP(hipEventDestroy(e0));
+    TT2_HIP(hipEventDestroy(e1));
+    TT2_HIP(hipMemcpy(c->stamps_host, g_stamps_dev, 64 * sizeof(long long), hipMemcpyDeviceToHost));
+    c->decoded = false;
+  });
+}
+
+tt2_status tt2_debug_stamps(tt2_ctx* c, long long* out64) {
+  return guard([&] {
+    TT2_CHECK(c && out64, TT2_ERR_INVALID_ARG, "null argument");
+    for (int i = 0; i < 64; ++i) out64[i] = c->stamps_host[i];
   });
 }
 

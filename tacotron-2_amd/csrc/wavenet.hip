@@ -56,15 +56,15 @@ __global__ void k_upsample(const float* __restrict__ in, float* __restrict__ out
 // so the lane that reduces quad q can apply tanh(a)·σ(b) without a cross-lane exchange.
 static inline int gate_col(int R, int q, int e) { return (e < 2 ? 2 * q + e : R + 2 * q + (e - 2)); }
 
-constexpr int WN_THREADS = 512;
+constexpr int WN_THREADS = 256;
 
 struct GenArgs {
   int B, T, L, stacks;
   const float* first_w; const float* first_b;      // [R], [R]
-  const f32x4* conv_w;  // [L][12][512] float4 (R=64: quad q, k-slice ks -> tid = q*16+ks)
+  const f32x4* conv_w;  // [L][24][256] float4 (R=64: quad q, k-slice ks -> tid = q*8+ks)
   const float* conv_b;  // [L][G] permuted
   const float* cond;    // [B][T][L][G] permuted (includes cond bias)
-  const f32x4* so_w;    // [L][4][512] float4: [Ws|Wo][ks*4+k'][4q..4q+3]
+  const f32x4* so_w;    // [L][8][256] float4: [Ws|Wo][ks*8+k'][4q..4q+3]
   const float* so_b;    // [L][2R] = [bs | bo]
   const float* f1_w; const float* f1_b;  // [S][S], [S]
   const float* f2_w; const float* f2_b;  // [S][C], [C]
@@ -79,15 +79,17 @@ struct GenArgs {
 
 __device__ __forceinline__ float gumbel_L(double u) { return (float)log(-log(u)); }
 
-// R = 64, G = 128, S = 64 (BASELINE config 3).  512 threads = 8 waves (2 per SIMD).
-// Dilated conv:  tid = q*16 + ks -> output quad q (gate-permuted columns), k-slice ks of 12.
-// Skip/out 1x1:  tid = q*16 + ks -> output quad q (q<16 skip, q>=16 out), k-slice ks of 4.
-// Cross-slice sums are DPP/shuffle reductions inside a wave; two barriers per layer.
+// R = 64, G = 128, S = 64 (BASELINE config 3).  256 threads = 4 waves, one per SIMD, so each
+// lane may hold 512 VGPRs: the current and the next layer's weights (2 x 128 VGPRs) stay in
+// registers and the next layer's stream is in flight while the current layer computes.
+// Dilated conv:  tid = q*8 + ks -> output quad q (gate-permuted columns), k-slice ks of 24.
+// Skip/out 1x1:  tid = q*8 + ks -> output quad q (q<16 skip, q>=16 out), k-slice ks of 8.
+// Cross-slice sums are shuffle reductions over 8 lanes; two barriers per layer.
 __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
-  constexpr int R = 64, G = 128, S = 64;
+  constexpr int R = 64, G = 128, S = 64, NT = WN_THREADS;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = tid >> 4, ks = tid & 15;
+  const int q = tid >> 3, ks = tid & 7;
   const int L = a.L, per = L / a.stacks, LG = L * G;
   float* in = sm;            // [3R] conv input: taps t-2d, t-d, current x
   float* z = in + 3 * R;     // [R] gated activations
@@ -100,40 +102,42 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
   const f32x4* cond4 = reinterpret_cast<const f32x4*>(a.cond);
   f32x4* cbuf4 = reinterpret_cast<f32x4*>(cbuf);
   // head weights live in registers for the whole utterance
-  const int q2 = tid >> 5, k2 = tid & 31;  // f1: 16 quads x 32 slices of 2 k
-  f32x4 hw1[2];
-  for (int e = 0; e < 2; ++e) hw1[e] = *reinterpret_cast<const f32x4*>(a.f1_w + (2 * k2 + e) * S + 4 * q2);
+  const int q2 = tid >> 4, k2 = tid & 15;  // f1: 16 quads x 16 slices of 4 k
+  f32x4 hw1[4];
+  for (int e = 0; e < 4; ++e) hw1[e] = *reinterpret_cast<const f32x4*>(a.f1_w + (4 * k2 + e) * S + 4 * q2);
   const f32x4 hb1 = *reinterpret_cast<const f32x4*>(a.f1_b + 4 * q2);
-  f32x4 hw2, hb2;  // f2: quad = wave (8 x 4 = 32 >= C columns), k = lane
+  const int q3 = tid >> 5, k3 = tid & 31;  // f2: 8 quads (32 >= C columns) x 32 slices of 2 k
+  float hw2[2][4], hb2[4];
   for (int e = 0; e < 4; ++e) {
-    const int col = 4 * wave + e;
-    hw2[e] = col < a.C ? a.f2_w[lane * a.C + col] : 0.f;
+    const int col = 4 * q3 + e;
+    for (int kk = 0; kk < 2; ++kk) hw2[kk][e] = col < a.C ? a.f2_w[(2 * k3 + kk) * a.C + col] : 0.f;
     hb2[e] = col < a.C ? a.f2_b[col] : 0.f;
   }
   int ring_total = 0;
   for (int l = 0; l < L; ++l) ring_total += (2 * (1 << (l % per)) + 1) * R;
-  for (int i = tid; i < ring_total; i += WN_THREADS) rings[i] = 0.f;
-  for (int i = tid; i < LG / 4; i += WN_THREADS) cbuf4[i] = cond4[((long)b * a.T) * (LG / 4) + i];
+  for (int i = tid; i < ring_total; i += NT) rings[i] = 0.f;
+  for (int i = tid; i < LG / 4; i += NT) cbuf4[i] = cond4[((long)b * a.T) * (LG / 4) + i];
   if (tid == 0) misc[0] = 0.f;  // initial input 0 for 'raw' (wavenet.py:437-445)
   const float SQH = 0.70710677f; // float32(np.sqrt(0.5))
   const f32x4* cw4 = a.conv_w;
   const f32x4* so4 = a.so_w;
   const f32x4* cb4 = reinterpret_cast<const f32x4*>(a.conv_b);
   const f32x4* sb4 = reinterpret_cast<const f32x4*>(a.so_b);
-  f32x4 wc[12], ws[4];
+  f32x4 wc[24], ws[8];
 #pragma unroll
-  for (int kk = 0; kk < 12; ++kk) wc[kk] = cw4[kk * WN_THREADS + tid];
+  for (int kk = 0; kk < 24; ++kk) wc[kk] = cw4[kk * NT + tid];
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) ws[kk] = so4[kk * WN_THREADS + tid];
+  for (int kk = 0; kk < 8; ++kk) ws[kk] = so4[kk * NT + tid];
   __syncthreads();
 
   for (int t = 0; t < a.T; ++t) {
     // ---- prefetch: next sample's conditioning, this sample's MoL uniforms / teacher value ----
-    f32x4 cn[2];
+    constexpr int NCN = 3;  // ceil(L*G/4 / NT) for L <= 24
+    f32x4 cn[NCN];
     const bool has_next = t + 1 < a.T;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = tid + i * WN_THREADS;
+    for (int i = 0; i < NCN; ++i) {
+      const int idx = tid + i * NT;
       if (has_next && idx < LG / 4) cn[i] = cond4[((long)b * a.T + t + 1) * (LG / 4) + idx];
     }
     float um = 0.5f, ul = 0.5f, tv = 0.f;
@@ -149,7 +153,7 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
     if (tid < R) {
       const float x0 = misc[0] * a.first_w[tid] + a.first_b[tid];
       const int Ld = 3;  // d = 1
-      in[0 * R + tid] = rings[((t + 1) % Ld) * R + tid];   // x(t-2d)
+      in[0 * R + tid] = rings[((t + 1) % Ld) * R + tid];      // x(t-2d)
       in[1 * R + tid] = rings[((t + Ld - 1) % Ld) * R + tid];  // x(t-d)
       in[2 * R + tid] = x0;
       rings[(t % Ld) * R + tid] = x0;
@@ -160,11 +164,11 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
     for (int l = 0; l < L; ++l) {
       const int d = 1 << (l % per), Ld = 2 * d + 1;
       const int ln = (l + 1 == L) ? 0 : l + 1;  // prefetch wraps to layer 0 of the next sample
-      f32x4 nwc[12], nws[4];
+      f32x4 nwc[24], nws[8];
 #pragma unroll
-      for (int kk = 0; kk < 12; ++kk) nwc[kk] = cw4[((long)ln * 12 + kk) * WN_THREADS + tid];
+      for (int kk = 0; kk < 24; ++kk) nwc[kk] = cw4[((long)ln * 24 + kk) * NT + tid];
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) nws[kk] = so4[((long)ln * 4 + kk) * WN_THREADS + tid];
+      for (int kk = 0; kk < 8; ++kk) nws[kk] = so4[((long)ln * 8 + kk) * NT + tid];
       f32x4 cb = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
       if (ks == 0) {
         cb = cb4[l * (G / 4) + q];
@@ -172,9 +176,9 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
       }
       // dilated conv GEMV over the 3 queue taps (modules.py:283-297)
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const f32x4* ip4 = reinterpret_cast<const f32x4*>(in + ks * 12);
+      const f32x4* ip4 = reinterpret_cast<const f32x4*>(in + ks * 24);
 #pragma unroll
-      for (int k4 = 0; k4 < 3; ++k4) {
+      for (int k4 = 0; k4 < 6; ++k4) {
         const f32x4 xv = ip4[k4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
         }
       }
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
+      for (int o = 1; o < 8; o <<= 1) {
         acc[0] += __shfl_xor(acc[0], o); acc[1] += __shfl_xor(acc[1], o);
         acc[2] += __shfl_xor(acc[2], o); acc[3] += __shfl_xor(acc[3], o);
       }
@@ -199,24 +203,28 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
       __syncthreads();
       // skip / out 1x1 (modules.py:512-520)
       f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 zv = reinterpret_cast<const f32x4*>(z)[ks];
+      const f32x4* zp4 = reinterpret_cast<const f32x4*>(z + ks * 8);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const f32x4 w = ws[e];
-        acc2[0] += zv[e] * w[0]; acc2[1] += zv[e] * w[1]; acc2[2] += zv[e] * w[2]; acc2[3] += zv[e] * w[3];
+      for (int k4 = 0; k4 < 2; ++k4) {
+        const f32x4 zv = zp4[k4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f32x4 w = ws[k4 * 4 + e];
+          acc2[0] += zv[e] * w[0]; acc2[1] += zv[e] * w[1]; acc2[2] += zv[e] * w[2]; acc2[3] += zv[e] * w[3];
+        }
       }
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
+      for (int o = 1; o < 8; o <<= 1) {
         acc2[0] += __shfl_xor(acc2[0], o); acc2[1] += __shfl_xor(acc2[1], o);
         acc2[2] += __shfl_xor(acc2[2], o); acc2[3] += __shfl_xor(acc2[3], o);
       }
       if (ks == 0) {
         if (q < 16) {  // skip connection sum (wavenet.py:833-836)
-          f32x4 s;
-          for (int e = 0; e < 4; ++e) s[e] = acc2[e] + sb[e];
-          if (l == 0) skips = s;
-          else if (a.legacy) for (int e = 0; e < 4; ++e) skips[e] = (skips[e] + s[e]) * SQH;
-          else for (int e = 0; e < 4; ++e) skips[e] = skips[e] + s[e];
+          f32x4 sv;
+          for (int e = 0; e < 4; ++e) sv[e] = acc2[e] + sb[e];
+          if (l == 0) skips = sv;
+          else if (a.legacy) for (int e = 0; e < 4; ++e) skips[e] = (skips[e] + sv[e]) * SQH;
+          else for (int e = 0; e < 4; ++e) skips[e] = skips[e] + sv[e];
         } else if (l + 1 < L) {  // residual output -> next layer's input and queue
           const int j = 4 * (q - 16);
           const int dn = 1 << ((l + 1) % per), Ln = 2 * dn + 1;
@@ -234,14 +242,14 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
       roff += Ld * R;
       __syncthreads();
 #pragma unroll
-      for (int kk = 0; kk < 12; ++kk) wc[kk] = nwc[kk];
+      for (int kk = 0; kk < 24; ++kk) wc[kk] = nwc[kk];
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) ws[kk] = nws[kk];
+      for (int kk = 0; kk < 8; ++kk) ws[kk] = nws[kk];
     }
     // next sample's conditioning -> LDS (every read of this sample's cbuf is behind a barrier)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = tid + i * WN_THREADS;
+    for (int i = 0; i < NCN; ++i) {
+      const int idx = tid + i * NT;
       if (has_next && idx < LG / 4) cbuf4[idx] = cn[i];
     }
     // ---- head: ReLU -> 1x1 -> ReLU -> 1x1 (wavenet.py:840-844) ----
@@ -250,12 +258,13 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
     __syncthreads();
     {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int e = 0; e < 2; ++e) {
-        const float x = skv[2 * k2 + e];
-        acc[0] += x * hw1[e][0]; acc[1] += x * hw1[e][1]; acc[2] += x * hw1[e][2]; acc[3] += x * hw1[e][3];
+      const f32x4 xv = reinterpret_cast<const f32x4*>(skv)[k2];
+      for (int e = 0; e < 4; ++e) {
+        acc[0] += xv[e] * hw1[e][0]; acc[1] += xv[e] * hw1[e][1];
+        acc[2] += xv[e] * hw1[e][2]; acc[3] += xv[e] * hw1[e][3];
       }
 #pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
+      for (int o = 1; o < 16; o <<= 1) {
         acc[0] += __shfl_xor(acc[0], o); acc[1] += __shfl_xor(acc[1], o);
         acc[2] += __shfl_xor(acc[2], o); acc[3] += __shfl_xor(acc[3], o);
       }
@@ -264,17 +273,15 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
     }
     __syncthreads();
     {
-      f32x4 acc;
-      const float x = h1[lane];
-      for (int e = 0; e < 4; ++e) acc[e] = x * hw2[e];
+      float acc[4];
+      const float x0 = h1[2 * k3], x1 = h1[2 * k3 + 1];
+      for (int e = 0; e < 4; ++e) acc[e] = x0 * hw2[0][e] + x1 * hw2[1][e];
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        acc[0] += __shfl_xor(acc[0], o); acc[1] += __shfl_xor(acc[1], o);
-        acc[2] += __shfl_xor(acc[2], o); acc[3] += __shfl_xor(acc[3], o);
-      }
-      if (lane == 0)
+      for (int o = 1; o < 32; o <<= 1)
+        for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], o);
+      if (k3 == 0)
         for (int e = 0; e < 4; ++e) {
-          const int col = 4 * wave + e;
+          const int col = 4 * q3 + e;
           if (col < a.C) {
             lg[col] = acc[e] + hb2[e];
             if (a.logits) a.logits[((long)b * a.T + t) * a.C + col] = lg[col];
@@ -349,6 +356,8 @@ struct tt2_wn_ctx {
   tt2::DevBuf first_w, first_b, conv_w, conv_b, cond_w, cond_b, so_w, so_b, f1_w, f1_b, f2_w, f2_b;
   tt2::DevBuf up_k[8], up_b[8];
   tt2::DevBuf cin_d, up_a, up_b_buf, c_up_t, cond, umix, ulog, teacher, wav, kout, logits;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool timed = false;
 };
 
 namespace tt2 {
@@ -365,8 +374,10 @@ static void wn_finalize(tt2_wn_ctx* c) {
   TT2_HIP(hipSetDevice(c->dev));
   wupload(c->first_w, need(wm, P + "input_convolution/kernel", {1, 1, R}).data);
   wupload(c->first_b, need(wm, P + "input_convolution/bias", {R}).data);
-  std::vector<float> cw((size_t)L * 12 * WN_THREADS * 4), cb((size_t)L * G), condw((size_t)cin * L * G),
-      condb((size_t)L * G), sow((size_t)L * 4 * WN_THREADS * 4), sob((size_t)L * 2 * R);
+  constexpr int CK = 3 * 64 / (WN_THREADS / 32);  // conv k's per slice (24)
+  constexpr int SK = 64 / (WN_THREADS / 32);      // skip/out k's per slice (8)
+  std::vector<float> cw((size_t)L * CK * WN_THREADS * 4), cb((size_t)L * G), condw((size_t)cin * L * G),
+      condb((size_t)L * G), sow((size_t)L * SK * WN_THREADS * 4), sob((size_t)L * 2 * R);
   for (int l = 0; l < L; ++l) {
     const std::string s = P + "ResidualConv1DGLU_" + std::to_string(l) + "/";
     const std::string ln = "_ResidualConv1DGLU_" + std::to_string(l) + "/";
@@ -379,18 +390,18 @@ static void wn_finalize(tt2_wn_ctx* c) {
     const auto& ko = need(wm, s + "residual_block_out_conv" + ln + "kernel", {1, G / 2, R});
     const auto& bo = need(wm, s + "residual_block_out_conv" + ln + "bias", {R});
     for (int tid = 0; tid < WN_THREADS; ++tid) {
-      const int q = tid >> 4, ks = tid & 15;
-      for (int kk = 0; kk < 12; ++kk) {
-        const int kidx = ks * 12 + kk;  // row of the linearized [kw*R, G] weight
+      const int q = tid / (WN_THREADS / 32), ks = tid % (WN_THREADS / 32);
+      for (int kk = 0; kk < CK; ++kk) {
+        const int kidx = ks * CK + kk;  // row of the linearized [kw*R, G] weight
         for (int e = 0; e < 4; ++e)
-          cw[(((size_t)l * 12 + kk) * WN_THREADS + tid) * 4 + e] = k.data[(size_t)kidx * G + gate_col(R, q, e)];
+          cw[(((size_t)l * CK + kk) * WN_THREADS + tid) * 4 + e] = k.data[(size_t)kidx * G + gate_col(R, q, e)];
       }
-      for (int kk = 0; kk < 4; ++kk) {
-        const int kidx = ks * 4 + kk;
+      for (int kk = 0; kk < SK; ++kk) {
+        const int kidx = ks * SK + kk;
         for (int e = 0; e < 4; ++e) {
           const int col = 4 * q + e;  // 0..127: [skip 0..63 | out 0..63]
           const float v = col < S ? ksk.data[(size_t)kidx * S + col] : ko.data[(size_t)kidx * R + (col - S)];
-          sow[(((size_t)l * 4 + kk) * WN_THREADS + tid) * 4 + e] = v;
+          sow[(((size_t)l * SK + kk) * WN_THREADS + tid) * 4 + e] = v;
         }
       }
     }
@@ -443,6 +454,7 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   c->up_a.alloc(sizeof(float) * B * F * T);
   c->up_b_buf.alloc(sizeof(float) * B * F * T);
   c->c_up_t.alloc(sizeof(float) * B * T * F);
+  TT2_HIP(hipEventRecord(c->ev[0], s));
   const float* src = cond_in;  // [B][F][T_f] channels-first
   long Tcur = T_f;
   float* bufs[2] = {c->up_a.as<float>(), c->up_b_buf.as<float>()};
@@ -459,6 +471,7 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
     src = dst;
     Tcur *= sc;
   }
+  TT2_HIP(hipEventRecord(c->ev[1], s));
   // conditioning 1x1 of every layer for every sample: [B*T, F] x [F, L*G]
   c->cond.alloc(sizeof(float) * B * T * c->L * c->G);
   GemmArgs g;
@@ -466,6 +479,7 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   g.Bw = c->cond_w.as<float>(); g.ldb = c->L * c->G; g.Cout = c->cond.as<float>(); g.ldc = c->L * c->G;
   g.bias = c->cond_b.as<float>();
   gemm(g, s);
+  TT2_HIP(hipEventRecord(c->ev[2], s));
   GenArgs a;
   a.B = B; a.T = (int)T; a.L = c->L; a.stacks = c->cfg.stacks;
   a.first_w = c->first_w.as<float>(); a.first_b = c->first_b.as<float>();
@@ -478,6 +492,8 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   const size_t shm = gen_lds_bytes(c);
   hipLaunchKernelGGL(k_generate64, dim3(B), dim3(WN_THREADS), shm, s, a);
   TT2_HIP(hipGetLastError());
+  TT2_HIP(hipEventRecord(c->ev[3], s));
+  c->timed = true;
 }
 
 }  // namespace tt2
@@ -510,6 +526,8 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
               "MoL head needs out_channels = 3*nr_mix <= 30");
     TT2_CHECK(cfg->layers >= 1 && cfg->stacks >= 1 && cfg->layers % cfg->stacks == 0, TT2_ERR_INVALID_ARG,
               "layers % stacks != 0");
+    TT2_CHECK(cfg->layers * cfg->gate_channels / 4 <= 3 * WN_THREADS, TT2_ERR_INVALID_ARG,
+              "conditioning row of one sample exceeds the prefetch registers (layers*G <= 3072)");
     TT2_CHECK(cfg->cin_channels >= 1 && cfg->cin_channels <= 128, TT2_ERR_INVALID_ARG, "cin_channels out of range");
     TT2_CHECK(cfg->n_upsample >= 1 && cfg->n_upsample <= 8, TT2_ERR_INVALID_ARG, "n_upsample out of range");
     TT2_CHECK(cfg->max_batch >= 1 && cfg->max_samples >= 1, TT2_ERR_INVALID_ARG, "capacities must be >= 1");
@@ -522,6 +540,7 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
     for (int i = 0; i < cfg->n_upsample; ++i) c->hop *= cfg->upsample_scales[i];
     TT2_HIP(hipSetDevice(hip_device));
     TT2_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
     const size_t shm = gen_lds_bytes(c.get());
     TT2_CHECK(shm <= 160 * 1024, TT2_ERR_INVALID_ARG, "queue rings exceed the 160 KiB LDS of a CU");
     TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_generate64),
@@ -534,7 +553,18 @@ void tt2_wn_destroy(tt2_wn_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
+}
+
+tt2_status tt2_wn_last_timings(tt2_wn_ctx* c, float* ms3) {
+  return guard([&] {
+    TT2_CHECK(c && ms3, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_CHECK(c->timed, TT2_ERR_STATE, "no generate call yet");
+    TT2_HIP(hipEventSynchronize(c->ev[3]));
+    for (int i = 0; i < 3; ++i) TT2_HIP(hipEventElapsedTime(&ms3[i], c->ev[i], c->ev[i + 1]));
+  });
 }
 
 tt2_status tt2_wn_load_tensor(tt2_wn_ctx* c, const char* name, const float* host, const int64_t* shape, int ndim) {

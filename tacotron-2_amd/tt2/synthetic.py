@@ -1,0 +1,34 @@
+"""Seeded synthetic inputs of the BASELINE.json configs (no datasets are available offline)."""
+import numpy as np
+
+
+def tacotron_inputs(B, T, T_ref, seed=1234, ragged=True, num_mels=80):
+    """Character ids rng(seed).integers(2,66) followed by EOS (id 1, tacotron/utils/text.py:40-41),
+    pad id 0; lengths (ragged: U[T/2, T], row 0 full); reference mels U[-4, 4] [B, T_ref, 80]."""
+    rng = np.random.default_rng(seed)
+    ids = np.zeros((B, T), np.int32)
+    if ragged:
+        lengths = rng.integers(max(2, T // 2), T + 1, B).astype(np.int32)
+        lengths[0] = T
+    else:
+        lengths = np.full(B, T, np.int32)
+    for b in range(B):
+        L = lengths[b]
+        ids[b, :L - 1] = rng.integers(2, 66, L - 1)
+        ids[b, L - 1] = 1
+    ref_e = rng.uniform(-4, 4, (B, T_ref, num_mels)).astype(np.float32)
+    ref_s = rng.uniform(-4, 4, (B, T_ref, num_mels)).astype(np.float32)
+    return ids, lengths, ref_e, ref_s
+
+
+def prenet_masks(n, B, P, seed=5339):
+    """Keep bits of the always-on prenet dropout (rate 0.5), [n, 2, B, P] uint8."""
+    return (np.random.default_rng(seed).random((n, 2, B, P)) < 0.5).astype(np.uint8)
+
+
+def mol_uniforms(T, B, nr=10, seed=5339):
+    """U[1e-5, 1-1e-5) uniforms of the MoL sampler (mixture.py:91,104): u_mix [T,B,nr], u_log [T,B]."""
+    rng = np.random.default_rng(seed)
+    um = rng.uniform(1e-5, 1 - 1e-5, (T, B, nr)).astype(np.float32)
+    ul = rng.uniform(1e-5, 1 - 1e-5, (T, B)).astype(np.float32)
+    return um, ul
