@@ -1,0 +1,65 @@
+"""Utterance-batch sharding across ranks.
+
+The reference splits a batch into per-GPU towers on the CPU (tacotron.py:83-138,
+wavenet.py:227-239) and concatenates the outputs on the host (tacotron/synthesizer.py:177-179).
+Here each rank (one process per GPU) synthesises a contiguous slice of the utterances with no
+exchange during compute; the only collective is one all_gather of the padded outputs and their
+lengths at the end (RCCL over xGMI with backend "nccl", or gloo on CPU).  The batch-level stop
+rule is per shard, exactly like the reference's per-tower dynamic_decode.
+"""
+import numpy as np
+
+
+def shard_range(n, rank, world):
+    """Contiguous slice [start, end) of n utterances owned by `rank` (remainder spread over the
+    first ranks, as np.array_split does)."""
+    base, rem = divmod(n, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def shard(arrays, rank, world):
+    """Slice every array along axis 0 to this rank's utterances."""
+    n = arrays[0].shape[0]
+    s, e = shard_range(n, rank, world)
+    return [None if a is None else a[s:e] for a in arrays]
+
+
+def gather_padded(local, lengths, group=None, pad_value=0.0):
+    """All-gather per-rank outputs [B_r, T_r, ...] with per-utterance lengths [B_r] (time axis 1).
+
+    Returns (list of per-utterance arrays trimmed to their lengths, in global utterance order).
+    Works with any torch.distributed backend; tensors live on the device the backend expects
+    (CUDA for nccl, CPU for gloo)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) \
+        if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    local = np.asarray(local)
+    lengths = np.asarray(lengths, np.int64)
+    meta = torch.tensor([local.shape[0], local.shape[1] if local.ndim > 1 else 0], dtype=torch.int64,
+                        device=dev)
+    metas = [torch.zeros_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    bmax = int(max(m[0] for m in metas))
+    tmax = int(max(m[1] for m in metas))
+    tail = local.shape[2:]
+    pad = np.full((bmax, tmax) + tail, pad_value, dtype=np.float32)
+    pad[:local.shape[0], :local.shape[1]] = local
+    lpad = np.zeros((bmax,), np.int64)
+    lpad[:lengths.shape[0]] = lengths
+    t = torch.from_numpy(pad).to(dev)
+    lt = torch.from_numpy(lpad).to(dev)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    louts = [torch.empty_like(lt) for _ in range(world)]
+    dist.all_gather(outs, t, group=group)
+    dist.all_gather(louts, lt, group=group)
+    res = []
+    for r in range(world):
+        nb = int(metas[r][0])
+        o = outs[r].cpu().numpy()
+        ls = louts[r].cpu().numpy()
+        for i in range(nb):
+            res.append(o[i, :int(ls[i])])
+    return res

@@ -1,0 +1,94 @@
+"""Multi-process (gloo, world_size 2) tests of utterance-batch sharding (tt2/parallel.py).
+
+The MI355X path shards utterances across ranks with no data-path collective and all-gathers the
+padded outputs once at the end.  Here each rank runs the oracle on its shard
+(stand-in for the device path, which needs a GPU) and the gathered result must equal the
+single-process run over the whole batch, utterance by utterance."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from tt2.parallel import shard, shard_range
+
+
+def test_shard_range_covers_exactly():
+    for n in range(0, 23):
+        for w in range(1, 9):
+            got = [shard_range(n, r, w) for r in range(w)]
+            assert got[0][0] == 0 and got[-1][1] == n
+            assert all(got[i][1] == got[i + 1][0] for i in range(w - 1))
+            sizes = [e - s for s, e in got]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "tacotron-2_amd"), root, os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from _common import small_hparams
+    from oracle import tacotron_ref as TR
+    from oracle.hp import oracle_hp
+    from tt2.parallel import gather_padded, shard, shard_range
+    from tt2.synthetic import prenet_masks, tacotron_inputs
+    from tt2.weights import init_tacotron_weights
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hp = small_hparams()
+        W = init_tacotron_weights(hp, seed=5339)
+        B, n = 5, 9
+        ids, lens, re, rs = tacotron_inputs(B, 12, 40, seed=13)
+        masks = prenet_masks(n, B, hp.prenet_layers[0], seed=13)    # [n, 2, B, P]
+        ids_r, lens_r, re_r, rs_r = shard([ids, lens, re, rs], rank, world)
+        s, e = shard_range(B, rank, world)
+        out = TR.synthesize(ids_r, lens_r, re_r, rs_r, W, oracle_hp(hp), masks[:, :, s:e], n)
+        mel = out["mel_outputs"]
+        lengths = np.full((mel.shape[0],), mel.shape[1], np.int64)
+        got = gather_padded(mel, lengths)
+        if rank == 0:
+            np.savez(os.path.join(out_dir, "gathered.npz"), *got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_synthesis_matches_single_process(tmp_path):
+    from _common import small_hparams
+    from oracle import tacotron_ref as TR
+    from oracle.hp import oracle_hp
+    from tt2.synthetic import prenet_masks, tacotron_inputs
+    from tt2.weights import init_tacotron_weights
+
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    with np.load(str(tmp_path / "gathered.npz"), allow_pickle=False) as z:
+        got = [z["arr_{}".format(i)] for i in range(len(z.files))]
+    hp = small_hparams()
+    W = init_tacotron_weights(hp, seed=5339)
+    B, n = 5, 9
+    ids, lens, re, rs = tacotron_inputs(B, 12, 40, seed=13)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=13)
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, n)["mel_outputs"]
+    assert len(got) == B
+    for b in range(B):
+        np.testing.assert_allclose(got[b], ref[b], rtol=0, atol=1e-5)
+
+
+def test_shard_arrays_none_passthrough():
+    a = np.arange(10).reshape(5, 2)
+    x, y = shard([a, None], 1, 2)
+    np.testing.assert_array_equal(x, a[3:])
+    assert y is None
