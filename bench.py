@@ -233,6 +233,12 @@ def main():
         wms = (ctypes.c_float * 3)()
         _lib.check(lib.tt2_wn_last_timings(weng.h, wms))
         gen_s = wms[2] / 1000.0
+        st = (ctypes.c_longlong * 512)()
+        _lib.check(lib.tt2_wn_debug_stamps(weng.h, st))
+        nst = (whp.layers + 2) // 3
+        base = st[0]
+        wn_stamps = [[round((st[s_ * 8 + k] - base) * 0.01, 2) if st[s_ * 8 + k] else None
+                      for k in range(6)] for s_ in range(nst)]
         # algorithmic bytes per sample: dilated conv + skip/out weights + head + conditioning row
         R, G, S_, L = whp.residual_channels, whp.gate_channels, whp.skip_out_channels, whp.layers
         wbytes = 4 * (L * (3 * R * G + G + (G // 2) * (S_ + R) + S_ + R) + S_ * S_ + S_ * 30 + L * G)
@@ -243,10 +249,12 @@ def main():
                   phases_ms=dict(upsample=round(wms[0], 3), cond_gemm=round(wms[1], 3),
                                  generate=round(wms[2], 3)),
                   us_per_sample=round(1e6 * gen_s / Tn, 3),
-                  roofline=dict(kernel="k_generate64", bound="latency (one CU per utterance)",
+                  roofline=dict(kernel="k_generate_pipe",
+                                bound="latency (serial sample chain; weights register-resident)",
                                 achieved=round(wach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                                 frac=round(wach / HBM_PEAK_GBS, 5),
-                                algorithmic_bytes_per_sample=int(wbytes)))
+                                algorithmic_bytes_per_sample=int(wbytes)),
+                  diag_stage_stamps_us=wn_stamps)
         weng.close()
 
     # --- CPU baseline (rank 0, N = 1 only) ---

@@ -206,6 +206,11 @@ tt2_status tt2_wn_generate_dev(tt2_wn_ctx* ctx, const float* cond_d, int B, int 
 /* HIP-event times (ms) of the last generate call: [upsample, conditioning GEMM, generation]. */
 tt2_status tt2_wn_last_timings(tt2_wn_ctx* ctx, float* ms3);
 
+/* Diagnostic: s_memrealtime (100 MHz, device-wide) stamps of utterance 0 at sample T/2 of the last
+ * generate call, out512[stage*8 + k]: k=0 input received, 1..3 after each layer, 4 head done
+ * (last stage), 5 sample handed to stage 0 (last stage). */
+tt2_status tt2_wn_debug_stamps(tt2_wn_ctx* ctx, long long* out512);
+
 /* Standalone sample_from_discretized_mix_logistic (mixture.py:76-107) on the current HIP device:
  * logits [n, 3*nr_mix], u_mix [n, nr_mix], u_log [n] (host) -> x [n], k [n] (host). */
 tt2_status tt2_mol_sample(const float* logits, const float* u_mix, const float* u_log, int n,

@@ -215,4 +215,48 @@ __host__ __device__ inline double u01_open(uint64_t h) {  // in [1e-5, 1-1e-5)
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// ------------------------------------------------------------------------------------------
+// DPP cross-lane reductions inside one 16-lane row (VALU only, no LDS round trip).  Every step
+// adds a value and its mirror partner, so all 16 lanes end with bitwise-identical sums.
+// ------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
+constexpr int DPP_HALF_MIRROR = 0x141; // row_half_mirror
+constexpr int DPP_MIRROR = 0x140;      // row_mirror
+__device__ __forceinline__ float sum16(float v) {
+  v += dpp_f<DPP_XOR1>(v);
+  v += dpp_f<DPP_XOR2>(v);
+  v += dpp_f<DPP_HALF_MIRROR>(v);
+  v += dpp_f<DPP_MIRROR>(v);
+  return v;
+}
+__device__ __forceinline__ void sum16x4(f32x4& a) {
+#define TT2_STEP(C)                                                                                  \
+  {                                                                                                  \
+    const float t0 = dpp_f<C>(a[0]), t1 = dpp_f<C>(a[1]), t2 = dpp_f<C>(a[2]), t3 = dpp_f<C>(a[3]); \
+    a[0] += t0; a[1] += t1; a[2] += t2; a[3] += t3;                                                  \
+  }
+  TT2_STEP(DPP_XOR1) TT2_STEP(DPP_XOR2) TT2_STEP(DPP_HALF_MIRROR) TT2_STEP(DPP_MIRROR)
+#undef TT2_STEP
+}
+// argmax over a 16-lane row, ties -> lowest index (tf.argmax); result in every lane of the row
+__device__ __forceinline__ void argmax16(float& v, int& i) {
+#define TT2_STEP(C)                                                    \
+  {                                                                    \
+    const float ov = dpp_f<C>(v);                                      \
+    const int oi = dpp_i<C>(i);                                        \
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }             \
+  }
+  TT2_STEP(DPP_XOR1) TT2_STEP(DPP_XOR2) TT2_STEP(DPP_HALF_MIRROR) TT2_STEP(DPP_MIRROR)
+#undef TT2_STEP
+}
+
 }  // namespace tt2

@@ -56,263 +56,359 @@ __global__ void k_upsample(const float* __restrict__ in, float* __restrict__ out
 // so the lane that reduces quad q can apply tanh(a)·σ(b) without a cross-lane exchange.
 static inline int gate_col(int R, int q, int e) { return (e < 2 ? 2 * q + e : R + 2 * q + (e - 2)); }
 
-constexpr int WN_THREADS = 256;
+// ---------------------------------------------------------------------------------------------
+// Layer-pipelined generator.  Generation is a strict serial chain (sample t+1 needs the sample
+// drawn from all 24 layers of sample t), so its speed is the latency of one pass through the
+// stack.  One CU cannot hold the 3.1 MB of per-sample weights, and streaming them from L2 every
+// sample is what bounds a single-CU generator (~43 GB/s per CU -> 75 us/sample).  Here the stack is
+// cut into NST = ceil(L/3) stages of three layers; each stage is one 512-thread workgroup on its
+// own CU that keeps its layers' weights in REGISTERS (64 VGPRs per layer per lane) and its layers'
+// fast-WaveNet queues in LDS for the whole utterance.  Per sample the activations travel
+// stage -> stage as 128 data-tagged 8-byte granules {tag = t+1, fp32 bits} (x and the running skip
+// sum) written with relaxed agent-scope atomic stores and swept by one wave of the consumer
+// (cdna_hip_programming.md §6 Guideline 16, R2: the data is the flag, no fences); the last stage
+// runs the ReLU/1x1/ReLU/1x1 head and the MoL sampler and hands the sample back to stage 0.
+// Every spin is bounded (status word + early exit), every polled word is zeroed before the launch.
+// Stage s of utterance u runs as block ((u/8)*NST + s)*8 + u%8: with round-robin dispatch all
+// stages of one utterance share an XCD (speed only; the protocol is placement-independent).
+// ---------------------------------------------------------------------------------------------
+constexpr int WN_THREADS = 512;   // 8 waves, 2 per SIMD: <= 256 VGPRs per lane
+constexpr int WN_LPS = 3;         // layers per stage
+constexpr int WN_CK = 12;         // conv rows per k-slice (192 / 16)
+constexpr int WN_SK = 4;          // skip/out rows per k-slice (64 / 16)
+constexpr int WN_GR = 128;        // granules per stage edge (x[64] | skip[64])
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
 
 struct GenArgs {
-  int B, T, L, stacks;
-  const float* first_w; const float* first_b;      // [R], [R]
-  const f32x4* conv_w;  // [L][24][256] float4 (R=64: quad q, k-slice ks -> tid = q*8+ks)
-  const float* conv_b;  // [L][G] permuted
-  const float* cond;    // [B][T][L][G] permuted (includes cond bias)
-  const f32x4* so_w;    // [L][8][256] float4: [Ws|Wo][ks*8+k'][4q..4q+3]
+  int B, T, L, per, nst;   // utterances in this launch, samples, layers, layers per stack, stages
+  int b0, Bg;              // first global utterance of this launch, global batch
+  const float* first_w; const float* first_b;  // [R], [R]
+  const f32x4* conv_w;  // [L][12][512] float4: tid = q*16+ks holds rows 12ks.. of quad q
+  const float* conv_b;  // [L][G] gate-permuted
+  const float* cond;    // [Bg][T][L][G] gate-permuted (includes the cin_conv bias)
+  const f32x4* so_w;    // [L][4][512] float4: rows 4ks.. of [Ws|Wo] quad q
   const float* so_b;    // [L][2R] = [bs | bo]
   const float* f1_w; const float* f1_b;  // [S][S], [S]
   const float* f2_w; const float* f2_b;  // [S][C], [C]
-  int C;                // out_channels
+  int C;
   int legacy, res_legacy;
   float log_scale_min;
-  const float* u_mix; const float* u_log;  // [T][B][nr], [T][B] or null
+  const float* u_mix; const float* u_log;  // [T][Bg][nr], [T][Bg] or null
   uint64_t seed;
-  const float* teacher;  // [B][T] or null
-  float* wav; int* kout; float* logits;
+  const float* teacher;  // [Bg][T] or null
+  float* wav; int* kout; float* logits;    // [Bg][T], [Bg][T], [Bg][T][C]
+  unsigned long long* gran;  // [B][nst][128]
+  int* status;               // 0 ok, else spin timeout code
+  long long* stamps;         // [64][8] s_memrealtime stamps of utterance 0 at sample T/2 (diagnostic)
 };
 
 __device__ __forceinline__ float gumbel_L(double u) { return (float)log(-log(u)); }
 
-// R = 64, G = 128, S = 64 (BASELINE config 3).  256 threads = 4 waves, one per SIMD, so each
-// lane may hold 512 VGPRs: the current and the next layer's weights (2 x 128 VGPRs) stay in
-// registers and the next layer's stream is in flight while the current layer computes.
-// Dilated conv:  tid = q*8 + ks -> output quad q (gate-permuted columns), k-slice ks of 24.
-// Skip/out 1x1:  tid = q*8 + ks -> output quad q (q<16 skip, q>=16 out), k-slice ks of 8.
-// Cross-slice sums are shuffle reductions over 8 lanes; two barriers per layer.
-__global__ __launch_bounds__(WN_THREADS) void k_generate64(GenArgs a) {
-  constexpr int R = 64, G = 128, S = 64, NT = WN_THREADS;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = tid >> 3, ks = tid & 7;
-  const int L = a.L, per = L / a.stacks, LG = L * G;
-  float* in = sm;            // [3R] conv input: taps t-2d, t-d, current x
-  float* z = in + 3 * R;     // [R] gated activations
-  float* skv = z + R;        // [S]
-  float* h1 = skv + S;       // [S]
-  float* lg = h1 + S;        // [32] logits
-  float* misc = lg + 32;     // [16] misc[0] = next input sample
-  float* cbuf = misc + 16;   // [L*G] conditioning of the current sample
-  float* rings = cbuf + LG;  // per-layer rings of 2d+1 entries
-  const f32x4* cond4 = reinterpret_cast<const f32x4*>(a.cond);
-  f32x4* cbuf4 = reinterpret_cast<f32x4*>(cbuf);
-  // head weights live in registers for the whole utterance
-  const int q2 = tid >> 4, k2 = tid & 15;  // f1: 16 quads x 16 slices of 4 k
-  f32x4 hw1[4];
-  for (int e = 0; e < 4; ++e) hw1[e] = *reinterpret_cast<const f32x4*>(a.f1_w + (4 * k2 + e) * S + 4 * q2);
-  const f32x4 hb1 = *reinterpret_cast<const f32x4*>(a.f1_b + 4 * q2);
-  const int q3 = tid >> 5, k3 = tid & 31;  // f2: 8 quads (32 >= C columns) x 32 slices of 2 k
-  float hw2[2][4], hb2[4];
-  for (int e = 0; e < 4; ++e) {
-    const int col = 4 * q3 + e;
-    for (int kk = 0; kk < 2; ++kk) hw2[kk][e] = col < a.C ? a.f2_w[(2 * k3 + kk) * a.C + col] : 0.f;
-    hb2[e] = col < a.C ? a.f2_b[col] : 0.f;
+__device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v) {
+  __hip_atomic_store((gu64*)g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave: sweep n (<= 128) granules until every tag == tag.  Lane i returns granules i, i+64.
+// Bounded: gives up after ~4 s (or when another stage reported a failure) and returns false.
+__device__ bool sweep(const unsigned long long* g, int n, unsigned tag, float& v0, float& v1, int* status,
+                      int lane) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  for (unsigned it = 0;; ++it) {
+    bool ok = true;
+    if (lane < n) {
+      const unsigned long long x = __hip_atomic_load((gu64*)(g + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v0 = __uint_as_float((unsigned)x);
+      ok = (unsigned)(x >> 32) == tag;
+    }
+    if (lane + 64 < n) {
+      const unsigned long long x =
+          __hip_atomic_load((gu64*)(g + lane + 64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v1 = __uint_as_float((unsigned)x);
+      ok = ok && (unsigned)(x >> 32) == tag;
+    }
+    if (__all(ok)) return true;
+    if ((it & 255) == 255) {
+      const int st = __hip_atomic_load((gi32*)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (st != 0) return false;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+        if (lane == 0) __hip_atomic_store((gi32*)status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
   }
-  int ring_total = 0;
-  for (int l = 0; l < L; ++l) ring_total += (2 * (1 << (l % per)) + 1) * R;
-  for (int i = tid; i < ring_total; i += NT) rings[i] = 0.f;
-  for (int i = tid; i < LG / 4; i += NT) cbuf4[i] = cond4[((long)b * a.T) * (LG / 4) + i];
-  if (tid == 0) misc[0] = 0.f;  // initial input 0 for 'raw' (wavenet.py:437-445)
-  const float SQH = 0.70710677f; // float32(np.sqrt(0.5))
-  const f32x4* cw4 = a.conv_w;
-  const f32x4* so4 = a.so_w;
-  const f32x4* cb4 = reinterpret_cast<const f32x4*>(a.conv_b);
-  const f32x4* sb4 = reinterpret_cast<const f32x4*>(a.so_b);
-  f32x4 wc[24], ws[8];
+}
+
+template <bool LEGACY, bool RES_LEGACY>
+__global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
+  constexpr int R = 64, G = 128, S = 64, NT = WN_THREADS;
+  const int blk = blockIdx.x, xl = blk & 7, grp = blk >> 3;
+  const int s = grp % a.nst, bl = (grp / a.nst) * 8 + xl;
+  if (bl >= a.B) return;
+  const int b = a.b0 + bl;  // global utterance
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = tid >> 4, ks = tid & 15;
+  const int L = a.L, per = a.per, l0 = s * WN_LPS, nl = min(WN_LPS, L - l0);
+  const bool first = s == 0, last = s + 1 == a.nst;
+  unsigned long long* gin = a.gran + ((long)bl * a.nst + (first ? a.nst - 1 : s - 1)) * WN_GR;
+  unsigned long long* gout = a.gran + ((long)bl * a.nst + s) * WN_GR;
+
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* inb = sm;                   // [192] conv input: x(t-2d) | x(t-d) | x(t)
+  float* z = inb + 3 * R;            // [64]
+  float* skr = z + R;                // [64] received skip sum
+  float* skv = skr + S;              // [64]
+  float* h1 = skv + S;               // [64]
+  float* lg = h1 + S;                // [32]
+  float* gum = lg + 32;              // [2][16] Gumbel terms (+ [15] = logistic noise) by t&1
+  float* cbuf = gum + 32;            // [2][3*128] conditioning by t&1
+  float* cbias = cbuf + 2 * WN_LPS * G;  // [3*128]
+  float* sbias = cbias + WN_LPS * G;     // [3*128]
+  float* hw1 = sbias + WN_LPS * G;       // [64*64]
+  float* hw2 = hw1 + S * S;              // [64*32]
+  float* hb = hw2 + S * 32;              // [64 + 32]
+  int* flag = reinterpret_cast<int*>(hb + 96);  // [4] abort
+  f32x4* wsl = reinterpret_cast<f32x4*>(hb + 100);  // [2][4][512] skip/out weights of layers 1, 2
+  float* rings = hb + 100 + 2 * WN_SK * NT * 4;      // this stage's queues
+
+  // ---- per-stage layer geometry (wave-uniform) ----
+  int dl[WN_LPS], Ll[WN_LPS], ro[WN_LPS], pos[WN_LPS];  // pos[j] = t mod L_j, kept incrementally
+  {
+    int off = 0;
 #pragma unroll
-  for (int kk = 0; kk < 24; ++kk) wc[kk] = cw4[kk * NT + tid];
+    for (int j = 0; j < WN_LPS; ++j) {
+      dl[j] = 1 << ((l0 + j) % per);
+      Ll[j] = 2 * dl[j] + 1;
+      ro[j] = off;
+      pos[j] = 0;
+      off += (j < nl) ? Ll[j] * R : 0;
+    }
+    for (int i = tid; i < off; i += NT) rings[i] = 0.f;
+  }
+  // ---- weights -> registers (dilated convs, first skip/out) and LDS (other skip/outs) for the
+  //      whole utterance: 144 + 16 VGPRs of weights per lane ----
+  f32x4 wc[WN_LPS][WN_CK], ws0[WN_SK];
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) ws[kk] = so4[kk * NT + tid];
+  for (int j = 0; j < WN_LPS; ++j) {
+    const int l = min(l0 + j, L - 1);
+#pragma unroll
+    for (int kk = 0; kk < WN_CK; ++kk) wc[j][kk] = a.conv_w[((long)l * WN_CK + kk) * NT + tid];
+  }
+#pragma unroll
+  for (int kk = 0; kk < WN_SK; ++kk) ws0[kk] = a.so_w[((long)l0 * WN_SK + kk) * NT + tid];
+  for (int j = 1; j < nl; ++j)
+#pragma unroll
+    for (int kk = 0; kk < WN_SK; ++kk) wsl[((j - 1) * WN_SK + kk) * NT + tid] = a.so_w[((long)(l0 + j) * WN_SK + kk) * NT + tid];
+  for (int i = tid; i < nl * G; i += NT) {
+    cbias[i] = a.conv_b[(long)l0 * G + i];
+    sbias[i] = a.so_b[(long)l0 * 2 * R + i];
+  }
+  if (last) {
+    for (int i = tid; i < S * S; i += NT) hw1[i] = a.f1_w[i];
+    for (int i = tid; i < S * 32; i += NT) {
+      const int k = i >> 5, c = i & 31;
+      hw2[i] = c < a.C ? a.f2_w[k * a.C + c] : 0.f;
+    }
+    for (int i = tid; i < 96; i += NT) hb[i] = i < S ? a.f1_b[i] : (i - S < a.C ? a.f2_b[i - S] : 0.f);
+  }
+  const f32x4* cond4 = reinterpret_cast<const f32x4*>(a.cond);
+  const long crow = (long)L * G / 4;  // float4 per sample row
+  if (tid < nl * G / 4) reinterpret_cast<f32x4*>(cbuf)[tid] = cond4[((long)b * a.T) * crow + l0 * G / 4 + tid];
+  float fw = 0.f, fb = 0.f;
+  if (first && tid < R) { fw = a.first_w[tid]; fb = a.first_b[tid]; }
+  if (tid == 0) flag[0] = 0;
+  const float SQH = 0.70710677f;  // float32(np.sqrt(0.5))
+  const int nr = a.C / 3;
+  f32x4 skips = {0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
   for (int t = 0; t < a.T; ++t) {
-    // ---- prefetch: next sample's conditioning, this sample's MoL uniforms / teacher value ----
-    constexpr int NCN = 3;  // ceil(L*G/4 / NT) for L <= 24
-    f32x4 cn[NCN];
+    const int cb_cur = t & 1;
+    // ---- prefetch (latency hidden behind the hand-off wait) ----
+    f32x4 cn = {0.f, 0.f, 0.f, 0.f};
     const bool has_next = t + 1 < a.T;
-#pragma unroll
-    for (int i = 0; i < NCN; ++i) {
-      const int idx = tid + i * NT;
-      if (has_next && idx < LG / 4) cn[i] = cond4[((long)b * a.T + t + 1) * (LG / 4) + idx];
-    }
-    float um = 0.5f, ul = 0.5f, tv = 0.f;
-    if (tid < 10)
-      um = a.u_mix ? a.u_mix[((long)t * a.B + b) * 10 + tid]
-                   : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.B + b) * 16 + tid)));
-    if (tid == 0) {
-      ul = a.u_log ? a.u_log[(long)t * a.B + b]
-                   : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.B + b) * 16 + 15)));
-      if (a.teacher) tv = a.teacher[(long)b * a.T + t];
-    }
-    // ---- first conv (Conv1D1x1, in=1) + layer-0 queue ----
-    if (tid < R) {
-      const float x0 = misc[0] * a.first_w[tid] + a.first_b[tid];
-      const int Ld = 3;  // d = 1
-      in[0 * R + tid] = rings[((t + 1) % Ld) * R + tid];      // x(t-2d)
-      in[1 * R + tid] = rings[((t + Ld - 1) % Ld) * R + tid];  // x(t-d)
-      in[2 * R + tid] = x0;
-      rings[(t % Ld) * R + tid] = x0;
-    }
-    f32x4 skips = {0.f, 0.f, 0.f, 0.f};
-    int roff = 0;
-    __syncthreads();
-    for (int l = 0; l < L; ++l) {
-      const int d = 1 << (l % per), Ld = 2 * d + 1;
-      const int ln = (l + 1 == L) ? 0 : l + 1;  // prefetch wraps to layer 0 of the next sample
-      f32x4 nwc[24], nws[8];
-#pragma unroll
-      for (int kk = 0; kk < 24; ++kk) nwc[kk] = cw4[((long)ln * 24 + kk) * NT + tid];
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) nws[kk] = so4[((long)ln * 8 + kk) * NT + tid];
-      f32x4 cb = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
-      if (ks == 0) {
-        cb = cb4[l * (G / 4) + q];
-        sb = sb4[l * (G / 4) + q];
+    if (has_next && tid < nl * G / 4) cn = cond4[((long)b * a.T + t + 1) * crow + l0 * G / 4 + tid];
+    if (last && wave == 1) {  // this sample's Gumbel terms and logistic noise, off the critical path
+      if (lane < nr) {
+        const float um = a.u_mix ? a.u_mix[((long)t * a.Bg + b) * nr + lane]
+                                 : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.Bg + b) * 16 + lane)));
+        gum[cb_cur * 16 + lane] = gumbel_L((double)um);
+      } else if (lane == 15) {
+        const float ul = a.u_log ? a.u_log[(long)t * a.Bg + b]
+                                 : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.Bg + b) * 16 + 15)));
+        const double uu = (double)ul;
+        gum[cb_cur * 16 + 15] = (float)(log(uu) - log(1.0 - uu));
       }
-      // dilated conv GEMV over the 3 queue taps (modules.py:283-297)
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const f32x4* ip4 = reinterpret_cast<const f32x4*>(in + ks * 24);
+    }
+    // ---- receive this stage's input (wave 0) ----
+    if (wave == 0) {
+      float v0 = 0.f, v1 = 0.f;
+      bool ok = true;
+      if (first) {
+        if (t > 0) ok = sweep(gin, 1, (unsigned)t, v0, v1, a.status, lane);
+        const float xp = __shfl(v0, 0);
+        v0 = xp * fw + fb;  // first_conv 1x1 (wavenet.py:822): x0 = y_{t-1}·w + b
+      } else {
+        ok = sweep(gin, WN_GR, (unsigned)(t + 1), v0, v1, a.status, lane);
+      }
+      if (!ok) {
+        if (lane == 0) flag[0] = 1;
+      } else {
+        float* rg = rings + ro[0];
+        const int p0 = pos[0], L0 = Ll[0];
+        const int po = p0 + 1 == L0 ? 0 : p0 + 1, pm = p0 + dl[0] + 1 >= L0 ? p0 + dl[0] + 1 - L0 : p0 + dl[0] + 1;
+        inb[2 * R + lane] = v0;
+        rg[p0 * R + lane] = v0;
+        inb[lane] = rg[po * R + lane];       // x(t-2d)
+        inb[R + lane] = rg[pm * R + lane];   // x(t-d)
+        skr[lane] = v1;
+      }
+    }
+    __syncthreads();
+    if (flag[0]) return;
+    const bool stamp = a.stamps && bl == 0 && a.b0 == 0 && t == a.T / 2 && tid == 0 && s < 64;
+    if (stamp) a.stamps[s * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (!first && ks == 0 && q < 16) skips = reinterpret_cast<const f32x4*>(skr)[q];
+
 #pragma unroll
-      for (int k4 = 0; k4 < 6; ++k4) {
+    for (int j = 0; j < WN_LPS; ++j) {
+      if (j >= nl) break;
+      const int l = l0 + j;
+      // dilated conv over the 3 queue taps (modules.py:283-297): 12 rows x 4 gate columns per lane
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const f32x4* ip4 = reinterpret_cast<const f32x4*>(inb + ks * WN_CK);
+#pragma unroll
+      for (int k4 = 0; k4 < WN_CK / 4; ++k4) {
         const f32x4 xv = ip4[k4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const f32x4 w = wc[k4 * 4 + e];
+          const f32x4 w = wc[j][k4 * 4 + e];
           acc[0] += xv[e] * w[0]; acc[1] += xv[e] * w[1]; acc[2] += xv[e] * w[2]; acc[3] += xv[e] * w[3];
         }
       }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        acc[0] += __shfl_xor(acc[0], o); acc[1] += __shfl_xor(acc[1], o);
-        acc[2] += __shfl_xor(acc[2], o); acc[3] += __shfl_xor(acc[3], o);
-      }
-      if (ks == 0) {  // (conv + b) + (cond·W + b_c), gated tanh·σ (modules.py:494-510)
-        const f32x4 cd = cbuf4[l * (G / 4) + q];
-        const float av0 = (acc[0] + cb[0]) + cd[0];
-        const float av1 = (acc[1] + cb[1]) + cd[1];
-        const float bv0 = (acc[2] + cb[2]) + cd[2];
-        const float bv1 = (acc[3] + cb[3]) + cd[3];
-        z[2 * q] = tanhf(av0) * sigm(bv0);
-        z[2 * q + 1] = tanhf(av1) * sigm(bv1);
+      const f32x4 cb = reinterpret_cast<const f32x4*>(cbias + j * G)[q];
+      const f32x4 cd = reinterpret_cast<const f32x4*>(cbuf + cb_cur * WN_LPS * G + j * G)[q];
+      sum16x4(acc);
+      if (ks == 0) {  // (conv + b) + (cond·Wc + bc) -> tanh(a)·σ(b) (modules.py:494-510)
+        const float av0 = (acc[0] + cb[0]) + cd[0], av1 = (acc[1] + cb[1]) + cd[1];
+        const float bv0 = (acc[2] + cb[2]) + cd[2], bv1 = (acc[3] + cb[3]) + cd[3];
+        float2 zz;
+        zz.x = tanhf(av0) * sigm(bv0);
+        zz.y = tanhf(av1) * sigm(bv1);
+        reinterpret_cast<float2*>(z)[q] = zz;
       }
       __syncthreads();
-      // skip / out 1x1 (modules.py:512-520)
+      // skip / out 1x1 (modules.py:512-520): 4 rows x 4 columns of [Ws | Wo] per lane
       f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
-      const f32x4* zp4 = reinterpret_cast<const f32x4*>(z + ks * 8);
-#pragma unroll
-      for (int k4 = 0; k4 < 2; ++k4) {
-        const f32x4 zv = zp4[k4];
+      {
+        const f32x4 zv = reinterpret_cast<const f32x4*>(z)[ks];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const f32x4 w = ws[k4 * 4 + e];
+          const f32x4 w = j == 0 ? ws0[e] : wsl[((j - 1) * WN_SK + e) * NT + tid];
           acc2[0] += zv[e] * w[0]; acc2[1] += zv[e] * w[1]; acc2[2] += zv[e] * w[2]; acc2[3] += zv[e] * w[3];
         }
       }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        acc2[0] += __shfl_xor(acc2[0], o); acc2[1] += __shfl_xor(acc2[1], o);
-        acc2[2] += __shfl_xor(acc2[2], o); acc2[3] += __shfl_xor(acc2[3], o);
-      }
+      const f32x4 sb = reinterpret_cast<const f32x4*>(sbias + j * G)[q];
+      sum16x4(acc2);
       if (ks == 0) {
-        if (q < 16) {  // skip connection sum (wavenet.py:833-836)
+        if (q < 16) {  // skip sum (wavenet.py:833-836)
           f32x4 sv;
           for (int e = 0; e < 4; ++e) sv[e] = acc2[e] + sb[e];
           if (l == 0) skips = sv;
-          else if (a.legacy) for (int e = 0; e < 4; ++e) skips[e] = (skips[e] + sv[e]) * SQH;
+          else if (LEGACY) for (int e = 0; e < 4; ++e) skips[e] = (skips[e] + sv[e]) * SQH;
           else for (int e = 0; e < 4; ++e) skips[e] = skips[e] + sv[e];
-        } else if (l + 1 < L) {  // residual output -> next layer's input and queue
-          const int j = 4 * (q - 16);
-          const int dn = 1 << ((l + 1) % per), Ln = 2 * dn + 1;
-          float* ringn = rings + roff + Ld * R;
+          if (j + 1 == nl && !last)
+            for (int e = 0; e < 4; ++e) put_granule(gout + R + 4 * q + e, (unsigned)(t + 1), skips[e]);
+        } else if (l + 1 < L) {  // residual output (modules.py:517-520)
+          const int c4 = q - 16;  // channel quad
+          f32x4 xo = reinterpret_cast<const f32x4*>(inb + 2 * R)[c4];
           for (int e = 0; e < 4; ++e) {
-            float xo = (acc2[e] + sb[e]) + in[2 * R + j + e];
-            if (a.res_legacy) xo = xo * SQH;
-            in[2 * R + j + e] = xo;
-            ringn[(t % Ln) * R + j + e] = xo;
-            in[0 * R + j + e] = ringn[((t + 1) % Ln) * R + j + e];
-            in[1 * R + j + e] = ringn[((t + Ln - dn) % Ln) * R + j + e];
+            xo[e] = (acc2[e] + sb[e]) + xo[e];
+            if (RES_LEGACY) xo[e] = xo[e] * SQH;
+          }
+          if (j + 1 < nl) {  // next layer of this stage: its queue and taps (reads before writes)
+            const int jn = j + 1 < WN_LPS ? j + 1 : 0;
+            const int Ln = Ll[jn], dn = dl[jn], pn = pos[jn];
+            const int po = pn + 1 == Ln ? 0 : pn + 1, pm = pn + dn + 1 >= Ln ? pn + dn + 1 - Ln : pn + dn + 1;
+            f32x4* rg4 = reinterpret_cast<f32x4*>(rings + ro[jn]);
+            const f32x4 xold = rg4[po * (R / 4) + c4], xmid = rg4[pm * (R / 4) + c4];
+            f32x4* in4 = reinterpret_cast<f32x4*>(inb);
+            in4[c4] = xold;
+            in4[R / 4 + c4] = xmid;
+            in4[2 * R / 4 + c4] = xo;
+            rg4[pn * (R / 4) + c4] = xo;
+          } else {
+            for (int e = 0; e < 4; ++e) put_granule(gout + 4 * c4 + e, (unsigned)(t + 1), xo[e]);
           }
         }
       }
-      roff += Ld * R;
       __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < 24; ++kk) wc[kk] = nwc[kk];
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) ws[kk] = nws[kk];
+      if (stamp) a.stamps[s * 8 + 1 + j] = __builtin_amdgcn_s_memrealtime();
     }
-    // next sample's conditioning -> LDS (every read of this sample's cbuf is behind a barrier)
 #pragma unroll
-    for (int i = 0; i < NCN; ++i) {
-      const int idx = tid + i * NT;
-      if (has_next && idx < LG / 4) cbuf4[idx] = cn[i];
-    }
-    // ---- head: ReLU -> 1x1 -> ReLU -> 1x1 (wavenet.py:840-844) ----
+    for (int j = 0; j < WN_LPS; ++j) pos[j] = pos[j] + 1 == Ll[j] ? 0 : pos[j] + 1;
+    // next sample's conditioning -> the other cbuf half (its last reader finished a barrier ago)
+    if (has_next && tid < nl * G / 4) reinterpret_cast<f32x4*>(cbuf + (cb_cur ^ 1) * WN_LPS * G)[tid] = cn;
+    if (!last) continue;
+
+    // ---- head: ReLU -> 1x1 (S->S) -> ReLU -> 1x1 (S->C) (wavenet.py:840-844) ----
     if (ks == 0 && q < 16)
       for (int e = 0; e < 4; ++e) skv[4 * q + e] = fmaxf(skips[e], 0.f);
     __syncthreads();
     {
+      const int q2 = tid >> 5, k2 = tid & 31;  // 16 column quads x 32 slices of 2 rows
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 xv = reinterpret_cast<const f32x4*>(skv)[k2];
-      for (int e = 0; e < 4; ++e) {
-        acc[0] += xv[e] * hw1[e][0]; acc[1] += xv[e] * hw1[e][1];
-        acc[2] += xv[e] * hw1[e][2]; acc[3] += xv[e] * hw1[e][3];
-      }
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        acc[0] += __shfl_xor(acc[0], o); acc[1] += __shfl_xor(acc[1], o);
-        acc[2] += __shfl_xor(acc[2], o); acc[3] += __shfl_xor(acc[3], o);
+      for (int kk = 0; kk < 2; ++kk) {
+        const float xv = skv[2 * k2 + kk];
+        const f32x4 w = reinterpret_cast<const f32x4*>(hw1 + (2 * k2 + kk) * S)[q2];
+        acc[0] += xv * w[0]; acc[1] += xv * w[1]; acc[2] += xv * w[2]; acc[3] += xv * w[3];
       }
+      sum16x4(acc);
+      for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], 16);
       if (k2 == 0)
-        for (int e = 0; e < 4; ++e) h1[4 * q2 + e] = fmaxf(acc[e] + hb1[e], 0.f);
+        for (int e = 0; e < 4; ++e) h1[4 * q2 + e] = fmaxf(acc[e] + hb[4 * q2 + e], 0.f);
     }
     __syncthreads();
     {
-      float acc[4];
-      const float x0 = h1[2 * k3], x1 = h1[2 * k3 + 1];
-      for (int e = 0; e < 4; ++e) acc[e] = x0 * hw2[0][e] + x1 * hw2[1][e];
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1)
-        for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], o);
-      if (k3 == 0)
+      const int q3 = wave;  // 8 column quads (32 >= C) x 64 rows, one row per lane
+      const float xv = h1[lane];
+      const f32x4 w = reinterpret_cast<const f32x4*>(hw2 + lane * 32)[q3];
+      f32x4 acc = {xv * w[0], xv * w[1], xv * w[2], xv * w[3]};
+      sum16x4(acc);
+      for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], 16);
+      for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], 32);
+      if (lane == 0)
         for (int e = 0; e < 4; ++e) {
           const int col = 4 * q3 + e;
           if (col < a.C) {
-            lg[col] = acc[e] + hb2[e];
+            lg[col] = acc[e] + hb[S + col];
             if (a.logits) a.logits[((long)b * a.T + t) * a.C + col] = lg[col];
           }
         }
     }
     __syncthreads();
-    // ---- MoL sampler (mixture.py:76-107), wave 0 ----
-    if (tid < 64) {
-      const int nr = a.C / 3;
+    if (stamp) a.stamps[s * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+    // ---- MoL sampler (mixture.py:76-107), wave 0; hand the sample to stage 0 ----
+    if (wave == 0) {
       float temp = -INFINITY;
       int idx = lane;
-      if (lane < nr) temp = lg[lane] - gumbel_L((double)um);
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ot = __shfl_xor(temp, o);
-        const int oi = __shfl_xor(idx, o);
-        if (ot > temp || (ot == temp && oi < idx)) { temp = ot; idx = oi; }
-      }
+      if (lane < nr) temp = lg[lane] - gum[cb_cur * 16 + lane];
+      argmax16(temp, idx);  // nr <= 10: the mixture logits sit in lanes 0..15
       if (lane == 0) {
         const float mean = lg[nr + idx];
         const float ls = fmaxf(lg[2 * nr + idx], a.log_scale_min);
-        const double uu = (double)ul;
-        const float noise = (float)(log(uu) - log(1.0 - uu));
-        float x = mean + expf(ls) * noise;
+        float x = mean + expf(ls) * gum[cb_cur * 16 + 15];
         x = fminf(fmaxf(x, -1.f), 1.f);
+        const float xn = a.teacher ? a.teacher[(long)b * a.T + t] : x;  // wavenet.py:876-878
+        put_granule(gout, (unsigned)(t + 1), xn);
+        if (stamp) a.stamps[s * 8 + 5] = __builtin_amdgcn_s_memrealtime();
         a.wav[(long)b * a.T + t] = x;
         if (a.kout) a.kout[(long)b * a.T + t] = idx;
-        misc[0] = a.teacher ? tv : x;  // wavenet.py:876-878 test_inputs override
       }
     }
-    __syncthreads();
   }
 }
 
@@ -355,7 +451,9 @@ struct tt2_wn_ctx {
   long hop;
   tt2::DevBuf first_w, first_b, conv_w, conv_b, cond_w, cond_b, so_w, so_b, f1_w, f1_b, f2_w, f2_b;
   tt2::DevBuf up_k[8], up_b[8];
-  tt2::DevBuf cin_d, up_a, up_b_buf, c_up_t, cond, umix, ulog, teacher, wav, kout, logits;
+  tt2::DevBuf cin_d, up_a, up_b_buf, c_up_t, cond, umix, ulog, teacher, wav, kout, logits, gran, stamps;
+  int chunk = 1;                 // utterances per generation launch
+  int* status_host = nullptr;    // pinned: spin-timeout word of the last launch
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool timed = false;
 };
@@ -374,8 +472,7 @@ static void wn_finalize(tt2_wn_ctx* c) {
   TT2_HIP(hipSetDevice(c->dev));
   wupload(c->first_w, need(wm, P + "input_convolution/kernel", {1, 1, R}).data);
   wupload(c->first_b, need(wm, P + "input_convolution/bias", {R}).data);
-  constexpr int CK = 3 * 64 / (WN_THREADS / 32);  // conv k's per slice (24)
-  constexpr int SK = 64 / (WN_THREADS / 32);      // skip/out k's per slice (8)
+  constexpr int CK = WN_CK, SK = WN_SK;
   std::vector<float> cw((size_t)L * CK * WN_THREADS * 4), cb((size_t)L * G), condw((size_t)cin * L * G),
       condb((size_t)L * G), sow((size_t)L * SK * WN_THREADS * 4), sob((size_t)L * 2 * R);
   for (int l = 0; l < L; ++l) {
@@ -390,9 +487,9 @@ static void wn_finalize(tt2_wn_ctx* c) {
     const auto& ko = need(wm, s + "residual_block_out_conv" + ln + "kernel", {1, G / 2, R});
     const auto& bo = need(wm, s + "residual_block_out_conv" + ln + "bias", {R});
     for (int tid = 0; tid < WN_THREADS; ++tid) {
-      const int q = tid / (WN_THREADS / 32), ks = tid % (WN_THREADS / 32);
+      const int q = tid / 16, ks = tid % 16;  // 32 column quads x 16 k-slices
       for (int kk = 0; kk < CK; ++kk) {
-        const int kidx = ks * CK + kk;  // row of the linearized [kw*R, G] weight
+        const int kidx = ks * CK + kk;  // row of the linearized [kw*R, G] kernel (taps oldest first)
         for (int e = 0; e < 4; ++e)
           cw[(((size_t)l * CK + kk) * WN_THREADS + tid) * 4 + e] = k.data[(size_t)kidx * G + gate_col(R, q, e)];
       }
@@ -435,11 +532,31 @@ static void wn_finalize(tt2_wn_ctx* c) {
   c->finalized = true;
 }
 
+typedef void (*PipeKernel)(GenArgs);
+static PipeKernel pipe_kernel(bool legacy, bool res_legacy) {
+  if (legacy) return res_legacy ? k_generate_pipe<true, true> : k_generate_pipe<true, false>;
+  return res_legacy ? k_generate_pipe<false, true> : k_generate_pipe<false, false>;
+}
+
+// the generation kernel's bounded spins report a stalled hand-off through the status word
+static void check_status(tt2_wn_ctx* c) {
+  TT2_CHECK(*c->status_host == 0, TT2_ERR_HIP,
+            "WaveNet generation: a pipeline hand-off timed out (stage workgroups not co-resident?)");
+}
+
+static int wn_stages(const tt2_wn_ctx* c) { return (c->L + WN_LPS - 1) / WN_LPS; }
+
 static size_t gen_lds_bytes(const tt2_wn_ctx* c) {
-  const int per = c->L / c->cfg.stacks;
+  const int per = c->L / c->cfg.stacks, nst = wn_stages(c);
   long ring = 0;
-  for (int l = 0; l < c->L; ++l) ring += (2 * (1 << (l % per)) + 1) * c->R;
-  return sizeof(float) * (3 * c->R + c->R + c->S + c->S + 32 + 16 + (long)c->L * c->G + ring);
+  for (int st = 0; st < nst; ++st) {
+    long r = 0;
+    for (int l = st * WN_LPS; l < std::min(c->L, (st + 1) * WN_LPS); ++l) r += (2 * (1 << (l % per)) + 1) * c->R;
+    ring = std::max(ring, r);
+  }
+  const long fixed = 3 * 64 + 64 * 4 + 32 + 32 + 2 * WN_LPS * 128 + 2 * WN_LPS * 128 + 64 * 64 + 64 * 32 + 100 +
+                     2 * WN_SK * WN_THREADS * 4;
+  return sizeof(float) * (fixed + ring);
 }
 
 static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f, const float* umix_d,
@@ -480,8 +597,12 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   g.bias = c->cond_b.as<float>();
   gemm(g, s);
   TT2_HIP(hipEventRecord(c->ev[2], s));
+  const int nst = wn_stages(c);
+  const int chunk = c->chunk;  // utterances per launch: every stage of every utterance co-resident
+  const size_t gbytes = sizeof(unsigned long long) * (size_t)chunk * nst * WN_GR + 16;
+  c->gran.alloc(gbytes);
   GenArgs a;
-  a.B = B; a.T = (int)T; a.L = c->L; a.stacks = c->cfg.stacks;
+  a.T = (int)T; a.L = c->L; a.per = c->L / c->cfg.stacks; a.nst = nst; a.Bg = B;
   a.first_w = c->first_w.as<float>(); a.first_b = c->first_b.as<float>();
   a.conv_w = c->conv_w.as<f32x4>(); a.conv_b = c->conv_b.as<float>(); a.cond = c->cond.as<float>();
   a.so_w = c->so_w.as<f32x4>(); a.so_b = c->so_b.as<float>();
@@ -489,9 +610,23 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   a.C = c->C; a.legacy = c->cfg.legacy; a.res_legacy = c->cfg.residual_legacy; a.log_scale_min = c->cfg.log_scale_min;
   a.u_mix = umix_d; a.u_log = ulog_d; a.seed = seed; a.teacher = teacher_d;
   a.wav = wav_d; a.kout = k_d; a.logits = logits_d;
+  a.status = c->gran.as<int>();
+  c->stamps.alloc(sizeof(long long) * 64 * 8);
+  TT2_HIP(hipMemsetAsync(c->stamps.p, 0, sizeof(long long) * 64 * 8, s));
+  a.stamps = c->stamps.as<long long>();
+  a.gran = reinterpret_cast<unsigned long long*>(c->gran.as<char>() + 16);
   const size_t shm = gen_lds_bytes(c);
-  hipLaunchKernelGGL(k_generate64, dim3(B), dim3(WN_THREADS), shm, s, a);
-  TT2_HIP(hipGetLastError());
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    a.b0 = b0;
+    a.B = std::min(chunk, B - b0);
+    // every polled word (granule tags, status) starts at 0 for each launch (Guideline 16)
+    TT2_HIP(hipMemsetAsync(c->gran.p, 0, gbytes, s));
+    const int grid = cdiv(a.B, 8) * nst * 8;
+    const auto kern = pipe_kernel(c->cfg.legacy != 0, c->cfg.residual_legacy != 0);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(WN_THREADS), shm, s, a);
+    TT2_HIP(hipGetLastError());
+    TT2_HIP(hipMemcpyAsync(c->status_host, c->gran.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  }
   TT2_HIP(hipEventRecord(c->ev[3], s));
   c->timed = true;
 }
@@ -526,8 +661,6 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
               "MoL head needs out_channels = 3*nr_mix <= 30");
     TT2_CHECK(cfg->layers >= 1 && cfg->stacks >= 1 && cfg->layers % cfg->stacks == 0, TT2_ERR_INVALID_ARG,
               "layers % stacks != 0");
-    TT2_CHECK(cfg->layers * cfg->gate_channels / 4 <= 3 * WN_THREADS, TT2_ERR_INVALID_ARG,
-              "conditioning row of one sample exceeds the prefetch registers (layers*G <= 3072)");
     TT2_CHECK(cfg->cin_channels >= 1 && cfg->cin_channels <= 128, TT2_ERR_INVALID_ARG, "cin_channels out of range");
     TT2_CHECK(cfg->n_upsample >= 1 && cfg->n_upsample <= 8, TT2_ERR_INVALID_ARG, "n_upsample out of range");
     TT2_CHECK(cfg->max_batch >= 1 && cfg->max_samples >= 1, TT2_ERR_INVALID_ARG, "capacities must be >= 1");
@@ -543,8 +676,18 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
     for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
     const size_t shm = gen_lds_bytes(c.get());
     TT2_CHECK(shm <= 160 * 1024, TT2_ERR_INVALID_ARG, "queue rings exceed the 160 KiB LDS of a CU");
-    TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_generate64),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    const void* kern = reinterpret_cast<const void*>(pipe_kernel(cfg->legacy != 0, cfg->residual_legacy != 0));
+    TT2_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    // co-residency: one stage workgroup per CU, every workgroup of a launch resident at once
+    int nb = 0, ncu = 0;
+    TT2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, WN_THREADS, shm));
+    TT2_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
+    TT2_CHECK(nb >= 1, TT2_ERR_INVALID_ARG, "generation kernel does not fit on a CU");
+    const int nst = wn_stages(c.get());
+    TT2_CHECK(nst * 8 <= ncu, TT2_ERR_INVALID_ARG, "too many pipeline stages for this device");
+    c->chunk = 8 * (ncu / (nst * 8));  // grid = ceil(chunk/8)*nst*8 <= ncu
+    TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->status_host), sizeof(int), hipHostMallocDefault));
+    *c->status_host = 0;
     *out = c.release();
   });
 }
@@ -552,9 +695,11 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
 void tt2_wn_destroy(tt2_wn_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->dev);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  if (c->status_host) (void)hipHostFree(c->status_host);
   delete c;
 }
 
@@ -563,7 +708,18 @@ tt2_status tt2_wn_last_timings(tt2_wn_ctx* c, float* ms3) {
     TT2_CHECK(c && ms3, TT2_ERR_INVALID_ARG, "null argument");
     TT2_CHECK(c->timed, TT2_ERR_STATE, "no generate call yet");
     TT2_HIP(hipEventSynchronize(c->ev[3]));
+    TT2_HIP(hipStreamSynchronize(c->stream));
+    check_status(c);
     for (int i = 0; i < 3; ++i) TT2_HIP(hipEventElapsedTime(&ms3[i], c->ev[i], c->ev[i + 1]));
+  });
+}
+
+tt2_status tt2_wn_debug_stamps(tt2_wn_ctx* c, long long* out512) {
+  return guard([&] {
+    TT2_CHECK(c && out512, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_CHECK(c->stamps.p, TT2_ERR_STATE, "no generate call yet");
+    TT2_HIP(hipStreamSynchronize(c->stream));
+    TT2_HIP(hipMemcpy(out512, c->stamps.p, sizeof(long long) * 512, hipMemcpyDeviceToHost));
   });
 }
 
@@ -630,6 +786,7 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* c, const float* cond, int B, int T_f, con
     if (upsampled_out)
       TT2_HIP(hipMemcpyAsync(upsampled_out, upl.p, sizeof(float) * B * F * T, hipMemcpyDeviceToHost, s));
     TT2_HIP(hipStreamSynchronize(s));
+    check_status(c);
   });
 }
 

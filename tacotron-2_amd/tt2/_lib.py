@@ -77,6 +77,7 @@ SIGNATURES = {
     "tt2_profile_decoder_kernels": (_I, [_P, _I, _P]),
     "tt2_debug_stamps": (_I, [_P, _P]),
     "tt2_wn_last_timings": (_I, [_P, _P]),
+    "tt2_wn_debug_stamps": (_I, [_P, _P]),
     "tt2_wn_default_config": (None, [ctypes.POINTER(WnConfig), _I, ctypes.c_int64]),
     "tt2_wn_create": (_I, [ctypes.POINTER(WnConfig), _I, ctypes.POINTER(_P)]),
     "tt2_wn_destroy": (None, [_P]),
