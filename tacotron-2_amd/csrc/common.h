@@ -247,6 +247,22 @@ __device__ __forceinline__ void sum16x4(f32x4& a) {
   TT2_STEP(DPP_XOR1) TT2_STEP(DPP_XOR2) TT2_STEP(DPP_HALF_MIRROR) TT2_STEP(DPP_MIRROR)
 #undef TT2_STEP
 }
+// after sum16: lane 31 of each 32-lane half holds that half's sum (rows 0+1, rows 2+3)
+__device__ __forceinline__ float sum32_to_lane31(float v) {
+  v = sum16(v);
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));  // row_bcast:15
+}
+// full 64-lane sum, valid in lane 63
+__device__ __forceinline__ float sum64_to_lane63(float v) {
+  v = sum32_to_lane31(v);
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));  // row_bcast:31
+}
+// Gate non-linearities from v_exp_f32 + v_rcp_f32 (no branches, no IEEE division): abs error
+// < 3e-7 for tanh, relative error < 4e-7 for the sigmoid over the whole range.
+__device__ __forceinline__ float sigm_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_rcp(float x) {
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);
+}
 // argmax over a 16-lane row, ties -> lowest index (tf.argmax); result in every lane of the row
 __device__ __forceinline__ void argmax16(float& v, int& i) {
 #define TT2_STEP(C)                                                    \

@@ -72,10 +72,12 @@ static inline int gate_col(int R, int q, int e) { return (e < 2 ? 2 * q + e : R 
 // Stage s of utterance u runs as block ((u/8)*NST + s)*8 + u%8: with round-robin dispatch all
 // stages of one utterance share an XCD (speed only; the protocol is placement-independent).
 // ---------------------------------------------------------------------------------------------
-constexpr int WN_THREADS = 512;   // 8 waves, 2 per SIMD: <= 256 VGPRs per lane
+constexpr int WN_THREADS = 256;   // 4 waves, 1 per SIMD: 512 registers per lane (VGPR + AGPR)
 constexpr int WN_LPS = 3;         // layers per stage
-constexpr int WN_CK = 12;         // conv rows per k-slice (192 / 16)
-constexpr int WN_SK = 4;          // skip/out rows per k-slice (64 / 16)
+constexpr int WN_TK = 16;         // conv tap rows per k-slice (128 / 8): x(t-2d) | x(t-d)
+constexpr int WN_XK = 8;          // conv x(t) rows per k-slice (64 / 8)
+constexpr int WN_CK = WN_TK + WN_XK;
+constexpr int WN_SK = 8;          // skip/out rows per k-slice (64 / 8)
 constexpr int WN_GR = 128;        // granules per stage edge (x[64] | skip[64])
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -141,23 +143,50 @@ __device__ bool sweep(const unsigned long long* g, int n, unsigned tag, float& v
   }
 }
 
+// 256 threads: tid = q*8 + ks, q = column quad (32 x 4 gate columns / 32 x 4 skip|out columns),
+// ks = k-slice (8).  Per lane and layer: 16 float4 of tap weights (used off the critical path;
+// the allocator parks them in AGPRs), 8 float4 of x(t) conv weights and 8 float4 of skip/out
+// weights (VGPRs).  Cross-slice sums are 3-level DPP reductions inside 8-lane groups.
+__device__ __forceinline__ void sum8x4(f32x4& a) {
+#define TT2_STEP(C)                                                                                  \
+  {                                                                                                  \
+    const float t0 = dpp_f<C>(a[0]), t1 = dpp_f<C>(a[1]), t2 = dpp_f<C>(a[2]), t3 = dpp_f<C>(a[3]); \
+    a[0] += t0; a[1] += t1; a[2] += t2; a[3] += t3;                                                  \
+  }
+  TT2_STEP(DPP_XOR1) TT2_STEP(DPP_XOR2) TT2_STEP(DPP_HALF_MIRROR)
+#undef TT2_STEP
+}
+
+// Explicit AGPR residency for the off-critical-path tap weights (the allocator otherwise parks the
+// critical-path weights there and pays a v_accvgpr_read per use inside the serial chain).
+__device__ __forceinline__ float agpr_put(float v) {
+  float r;
+  asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(r) : "v"(v));
+  return r;
+}
+__device__ __forceinline__ float agpr_get(float r) {
+  float v;
+  asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(r));
+  return v;
+}
+
 template <bool LEGACY, bool RES_LEGACY>
-__global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
+__global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
   constexpr int R = 64, G = 128, S = 64, NT = WN_THREADS;
   const int blk = blockIdx.x, xl = blk & 7, grp = blk >> 3;
   const int s = grp % a.nst, bl = (grp / a.nst) * 8 + xl;
   if (bl >= a.B) return;
   const int b = a.b0 + bl;  // global utterance
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = tid >> 4, ks = tid & 15;
+  const int q = tid >> 3, ks = tid & 7;
   const int L = a.L, per = a.per, l0 = s * WN_LPS, nl = min(WN_LPS, L - l0);
   const bool first = s == 0, last = s + 1 == a.nst;
   unsigned long long* gin = a.gran + ((long)bl * a.nst + (first ? a.nst - 1 : s - 1)) * WN_GR;
   unsigned long long* gout = a.gran + ((long)bl * a.nst + s) * WN_GR;
 
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* inb = sm;                   // [192] conv input: x(t-2d) | x(t-d) | x(t)
-  float* z = inb + 3 * R;            // [64]
+  float* xcur = sm;                  // [64] input x(t) of the layer being computed
+  float* z = xcur + R;               // [64]
   float* skr = z + R;                // [64] received skip sum
   float* skv = skr + S;              // [64]
   float* h1 = skv + S;               // [64]
@@ -170,8 +199,7 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
   float* hw2 = hw1 + S * S;              // [64*32]
   float* hb = hw2 + S * 32;              // [64 + 32]
   int* flag = reinterpret_cast<int*>(hb + 96);  // [4] abort
-  f32x4* wsl = reinterpret_cast<f32x4*>(hb + 100);  // [2][4][512] skip/out weights of layers 1, 2
-  float* rings = hb + 100 + 2 * WN_SK * NT * 4;      // this stage's queues
+  float* rings = hb + 100;                      // this stage's queues
 
   // ---- per-stage layer geometry (wave-uniform) ----
   int dl[WN_LPS], Ll[WN_LPS], ro[WN_LPS], pos[WN_LPS];  // pos[j] = t mod L_j, kept incrementally
@@ -187,20 +215,23 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
     }
     for (int i = tid; i < off; i += NT) rings[i] = 0.f;
   }
-  // ---- weights -> registers (dilated convs, first skip/out) and LDS (other skip/outs) for the
-  //      whole utterance: 144 + 16 VGPRs of weights per lane ----
-  f32x4 wc[WN_LPS][WN_CK], ws0[WN_SK];
+  // ---- weights for the whole utterance, in registers ----
+  float wt[WN_LPS][WN_TK * 4];  // AGPRs
+  f32x4 wx[WN_LPS][WN_XK], wsr[WN_LPS][WN_SK];
 #pragma unroll
   for (int j = 0; j < WN_LPS; ++j) {
     const int l = min(l0 + j, L - 1);
 #pragma unroll
-    for (int kk = 0; kk < WN_CK; ++kk) wc[j][kk] = a.conv_w[((long)l * WN_CK + kk) * NT + tid];
+    for (int kk = 0; kk < WN_TK; ++kk) {
+      const f32x4 w = a.conv_w[((long)l * WN_CK + kk) * NT + tid];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wt[j][4 * kk + e] = agpr_put(w[e]);
+    }
+#pragma unroll
+    for (int kk = 0; kk < WN_XK; ++kk) wx[j][kk] = a.conv_w[((long)l * WN_CK + WN_TK + kk) * NT + tid];
+#pragma unroll
+    for (int kk = 0; kk < WN_SK; ++kk) wsr[j][kk] = a.so_w[((long)l * WN_SK + kk) * NT + tid];
   }
-#pragma unroll
-  for (int kk = 0; kk < WN_SK; ++kk) ws0[kk] = a.so_w[((long)l0 * WN_SK + kk) * NT + tid];
-  for (int j = 1; j < nl; ++j)
-#pragma unroll
-    for (int kk = 0; kk < WN_SK; ++kk) wsl[((j - 1) * WN_SK + kk) * NT + tid] = a.so_w[((long)(l0 + j) * WN_SK + kk) * NT + tid];
   for (int i = tid; i < nl * G; i += NT) {
     cbias[i] = a.conv_b[(long)l0 * G + i];
     sbias[i] = a.so_b[(long)l0 * 2 * R + i];
@@ -221,16 +252,16 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
   if (tid == 0) flag[0] = 0;
   const float SQH = 0.70710677f;  // float32(np.sqrt(0.5))
   const int nr = a.C / 3;
-  f32x4 skips = {0.f, 0.f, 0.f, 0.f};
+  f32x4 skips = {0.f, 0.f, 0.f, 0.f}, xres = {0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
   for (int t = 0; t < a.T; ++t) {
     const int cb_cur = t & 1;
-    // ---- prefetch (latency hidden behind the hand-off wait) ----
+    // ---- off the critical path (overlaps the hand-off wait) ----
     f32x4 cn = {0.f, 0.f, 0.f, 0.f};
     const bool has_next = t + 1 < a.T;
     if (has_next && tid < nl * G / 4) cn = cond4[((long)b * a.T + t + 1) * crow + l0 * G / 4 + tid];
-    if (last && wave == 1) {  // this sample's Gumbel terms and logistic noise, off the critical path
+    if (last && wave == 1) {  // this sample's Gumbel terms and logistic noise
       if (lane < nr) {
         const float um = a.u_mix ? a.u_mix[((long)t * a.Bg + b) * nr + lane]
                                  : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.Bg + b) * 16 + lane)));
@@ -241,6 +272,36 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
         const double uu = (double)ul;
         gum[cb_cur * 16 + 15] = (float)(log(uu) - log(1.0 - uu));
       }
+    }
+    // dilated-conv taps x(t-2d), x(t-d) of every layer of this stage are already in the queues:
+    // their part of the conv (2/3 of its rows), the conv bias and the conditioning are summed now
+    f32x4 tp[WN_LPS];
+#pragma unroll
+    for (int j = 0; j < WN_LPS; ++j) {
+      tp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (j >= nl) continue;
+      const int p = pos[j], Lj = Ll[j];
+      const int slot = ks < 4 ? (p + 1 == Lj ? 0 : p + 1)                               // x(t-2d)
+                              : (p + dl[j] + 1 >= Lj ? p + dl[j] + 1 - Lj : p + dl[j] + 1);  // x(t-d)
+      const f32x4* tv = reinterpret_cast<const f32x4*>(rings + ro[j] + slot * R + 16 * (ks & 3));
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const f32x4 xv = tv[k4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * (4 * k4 + e);
+          const float w0 = agpr_get(wt[j][r]), w1 = agpr_get(wt[j][r + 1]);
+          const float w2 = agpr_get(wt[j][r + 2]), w3 = agpr_get(wt[j][r + 3]);
+          acc[0] += xv[e] * w0; acc[1] += xv[e] * w1; acc[2] += xv[e] * w2; acc[3] += xv[e] * w3;
+        }
+      }
+      if (ks == 0) {
+        const f32x4 cb = reinterpret_cast<const f32x4*>(cbias + j * G)[q];
+        const f32x4 cd = reinterpret_cast<const f32x4*>(cbuf + cb_cur * WN_LPS * G + j * G)[q];
+        for (int e = 0; e < 4; ++e) acc[e] += cb[e] + cd[e];
+      }
+      tp[j] = acc;
     }
     // ---- receive this stage's input (wave 0) ----
     if (wave == 0) {
@@ -256,13 +317,8 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
       if (!ok) {
         if (lane == 0) flag[0] = 1;
       } else {
-        float* rg = rings + ro[0];
-        const int p0 = pos[0], L0 = Ll[0];
-        const int po = p0 + 1 == L0 ? 0 : p0 + 1, pm = p0 + dl[0] + 1 >= L0 ? p0 + dl[0] + 1 - L0 : p0 + dl[0] + 1;
-        inb[2 * R + lane] = v0;
-        rg[p0 * R + lane] = v0;
-        inb[lane] = rg[po * R + lane];       // x(t-2d)
-        inb[R + lane] = rg[pm * R + lane];   // x(t-d)
+        xcur[lane] = v0;
+        rings[ro[0] + pos[0] * R + lane] = v0;
         skr[lane] = v1;
       }
     }
@@ -270,48 +326,59 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
     if (flag[0]) return;
     const bool stamp = a.stamps && bl == 0 && a.b0 == 0 && t == a.T / 2 && tid == 0 && s < 64;
     if (stamp) a.stamps[s * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-    if (!first && ks == 0 && q < 16) skips = reinterpret_cast<const f32x4*>(skr)[q];
+    if (ks == 0) {
+      if (q < 16) {
+        if (!first) skips = reinterpret_cast<const f32x4*>(skr)[q];
+      } else {
+        xres = reinterpret_cast<const f32x4*>(xcur)[q - 16];
+      }
+    }
 
 #pragma unroll
     for (int j = 0; j < WN_LPS; ++j) {
       if (j >= nl) break;
       const int l = l0 + j;
-      // dilated conv over the 3 queue taps (modules.py:283-297): 12 rows x 4 gate columns per lane
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const f32x4* ip4 = reinterpret_cast<const f32x4*>(inb + ks * WN_CK);
+      // conv rows of x(t) (modules.py:283-297) on top of the precomputed tap part
+      f32x4 acc = tp[j];
+      {
+        const f32x4* xv4 = reinterpret_cast<const f32x4*>(xcur + 8 * ks);
 #pragma unroll
-      for (int k4 = 0; k4 < WN_CK / 4; ++k4) {
-        const f32x4 xv = ip4[k4];
+        for (int k4 = 0; k4 < 2; ++k4) {
+          const f32x4 xv = xv4[k4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const f32x4 w = wc[j][k4 * 4 + e];
-          acc[0] += xv[e] * w[0]; acc[1] += xv[e] * w[1]; acc[2] += xv[e] * w[2]; acc[3] += xv[e] * w[3];
+          for (int e = 0; e < 4; ++e) {
+            const f32x4 w = wx[j][4 * k4 + e];
+            acc[0] += xv[e] * w[0]; acc[1] += xv[e] * w[1]; acc[2] += xv[e] * w[2]; acc[3] += xv[e] * w[3];
+          }
         }
       }
-      const f32x4 cb = reinterpret_cast<const f32x4*>(cbias + j * G)[q];
-      const f32x4 cd = reinterpret_cast<const f32x4*>(cbuf + cb_cur * WN_LPS * G + j * G)[q];
-      sum16x4(acc);
-      if (ks == 0) {  // (conv + b) + (cond·Wc + bc) -> tanh(a)·σ(b) (modules.py:494-510)
-        const float av0 = (acc[0] + cb[0]) + cd[0], av1 = (acc[1] + cb[1]) + cd[1];
-        const float bv0 = (acc[2] + cb[2]) + cd[2], bv1 = (acc[3] + cb[3]) + cd[3];
+      const f32x4 sb = reinterpret_cast<const f32x4*>(sbias + j * G)[q];  // for the skip/out phase
+      sum8x4(acc);
+      if (ks == 0) {  // tanh(a)·σ(b) (modules.py:494-510)
         float2 zz;
-        zz.x = tanhf(av0) * sigm(bv0);
-        zz.y = tanhf(av1) * sigm(bv1);
+        zz.x = tanh_rcp(acc[0]) * sigm_fast(acc[2]);
+        zz.y = tanh_rcp(acc[1]) * sigm_fast(acc[3]);
         reinterpret_cast<float2*>(z)[q] = zz;
       }
+      // next sample's conditioning -> the other cbuf half: its last reader was the previous
+      // sample's tap precompute, and the barrier closing this layer orders it before the next one
+      if (j == 0 && has_next && tid < nl * G / 4) reinterpret_cast<f32x4*>(cbuf + (cb_cur ^ 1) * WN_LPS * G)[tid] = cn;
       __syncthreads();
-      // skip / out 1x1 (modules.py:512-520): 4 rows x 4 columns of [Ws | Wo] per lane
+      // skip / out 1x1 (modules.py:512-520): 8 rows x 4 columns of [Ws | Wo] per lane
       f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
       {
-        const f32x4 zv = reinterpret_cast<const f32x4*>(z)[ks];
+        const f32x4* zv4 = reinterpret_cast<const f32x4*>(z + 8 * ks);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const f32x4 w = j == 0 ? ws0[e] : wsl[((j - 1) * WN_SK + e) * NT + tid];
-          acc2[0] += zv[e] * w[0]; acc2[1] += zv[e] * w[1]; acc2[2] += zv[e] * w[2]; acc2[3] += zv[e] * w[3];
+        for (int k4 = 0; k4 < 2; ++k4) {
+          const f32x4 zv = zv4[k4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f32x4 w = wsr[j][4 * k4 + e];
+            acc2[0] += zv[e] * w[0]; acc2[1] += zv[e] * w[1]; acc2[2] += zv[e] * w[2]; acc2[3] += zv[e] * w[3];
+          }
         }
       }
-      const f32x4 sb = reinterpret_cast<const f32x4*>(sbias + j * G)[q];
-      sum16x4(acc2);
+      sum8x4(acc2);
       if (ks == 0) {
         if (q < 16) {  // skip sum (wavenet.py:833-836)
           f32x4 sv;
@@ -323,24 +390,16 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
             for (int e = 0; e < 4; ++e) put_granule(gout + R + 4 * q + e, (unsigned)(t + 1), skips[e]);
         } else if (l + 1 < L) {  // residual output (modules.py:517-520)
           const int c4 = q - 16;  // channel quad
-          f32x4 xo = reinterpret_cast<const f32x4*>(inb + 2 * R)[c4];
           for (int e = 0; e < 4; ++e) {
-            xo[e] = (acc2[e] + sb[e]) + xo[e];
-            if (RES_LEGACY) xo[e] = xo[e] * SQH;
+            xres[e] = (acc2[e] + sb[e]) + xres[e];
+            if (RES_LEGACY) xres[e] = xres[e] * SQH;
           }
-          if (j + 1 < nl) {  // next layer of this stage: its queue and taps (reads before writes)
+          if (j + 1 < nl) {  // next layer of this stage: its x(t) and its queue
             const int jn = j + 1 < WN_LPS ? j + 1 : 0;
-            const int Ln = Ll[jn], dn = dl[jn], pn = pos[jn];
-            const int po = pn + 1 == Ln ? 0 : pn + 1, pm = pn + dn + 1 >= Ln ? pn + dn + 1 - Ln : pn + dn + 1;
-            f32x4* rg4 = reinterpret_cast<f32x4*>(rings + ro[jn]);
-            const f32x4 xold = rg4[po * (R / 4) + c4], xmid = rg4[pm * (R / 4) + c4];
-            f32x4* in4 = reinterpret_cast<f32x4*>(inb);
-            in4[c4] = xold;
-            in4[R / 4 + c4] = xmid;
-            in4[2 * R / 4 + c4] = xo;
-            rg4[pn * (R / 4) + c4] = xo;
+            reinterpret_cast<f32x4*>(xcur)[c4] = xres;
+            reinterpret_cast<f32x4*>(rings + ro[jn] + pos[jn] * R)[c4] = xres;
           } else {
-            for (int e = 0; e < 4; ++e) put_granule(gout + 4 * c4 + e, (unsigned)(t + 1), xo[e]);
+            for (int e = 0; e < 4; ++e) put_granule(gout + 4 * c4 + e, (unsigned)(t + 1), xres[e]);
           }
         }
       }
@@ -349,42 +408,39 @@ __global__ __launch_bounds__(WN_THREADS) void k_generate_pipe(GenArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < WN_LPS; ++j) pos[j] = pos[j] + 1 == Ll[j] ? 0 : pos[j] + 1;
-    // next sample's conditioning -> the other cbuf half (its last reader finished a barrier ago)
-    if (has_next && tid < nl * G / 4) reinterpret_cast<f32x4*>(cbuf + (cb_cur ^ 1) * WN_LPS * G)[tid] = cn;
     if (!last) continue;
 
     // ---- head: ReLU -> 1x1 (S->S) -> ReLU -> 1x1 (S->C) (wavenet.py:840-844) ----
     if (ks == 0 && q < 16)
       for (int e = 0; e < 4; ++e) skv[4 * q + e] = fmaxf(skips[e], 0.f);
     __syncthreads();
-    {
-      const int q2 = tid >> 5, k2 = tid & 31;  // 16 column quads x 32 slices of 2 rows
+    {  // 16 column quads x 16 slices of 4 rows
+      const int q2 = tid >> 4, k2 = tid & 15;
+      const f32x4 xv = reinterpret_cast<const f32x4*>(skv)[k2];
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const float xv = skv[2 * k2 + kk];
-        const f32x4 w = reinterpret_cast<const f32x4*>(hw1 + (2 * k2 + kk) * S)[q2];
-        acc[0] += xv * w[0]; acc[1] += xv * w[1]; acc[2] += xv * w[2]; acc[3] += xv * w[3];
+      for (int e = 0; e < 4; ++e) {
+        const f32x4 w = reinterpret_cast<const f32x4*>(hw1 + (4 * k2 + e) * S)[q2];
+        acc[0] += xv[e] * w[0]; acc[1] += xv[e] * w[1]; acc[2] += xv[e] * w[2]; acc[3] += xv[e] * w[3];
       }
       sum16x4(acc);
-      for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], 16);
       if (k2 == 0)
         for (int e = 0; e < 4; ++e) h1[4 * q2 + e] = fmaxf(acc[e] + hb[4 * q2 + e], 0.f);
     }
     __syncthreads();
-    {
-      const int q3 = wave;  // 8 column quads (32 >= C) x 64 rows, one row per lane
-      const float xv = h1[lane];
-      const f32x4 w = reinterpret_cast<const f32x4*>(hw2 + lane * 32)[q3];
-      f32x4 acc = {xv * w[0], xv * w[1], xv * w[2], xv * w[3]};
-      sum16x4(acc);
-      for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], 16);
-      for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], 32);
-      if (lane == 0)
+    {  // 8 column quads (32 >= C) x 32 slices of 2 rows
+      const int q3 = tid >> 5, k3 = tid & 31;
+      const float x0 = h1[2 * k3], x1 = h1[2 * k3 + 1];
+      const f32x4 w0 = reinterpret_cast<const f32x4*>(hw2 + (2 * k3) * 32)[q3];
+      const f32x4 w1 = reinterpret_cast<const f32x4*>(hw2 + (2 * k3 + 1) * 32)[q3];
+      float r[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = sum32_to_lane31(x0 * w0[e] + x1 * w1[e]);
+      if (k3 == 31)
         for (int e = 0; e < 4; ++e) {
           const int col = 4 * q3 + e;
           if (col < a.C) {
-            lg[col] = acc[e] + hb[S + col];
+            lg[col] = r[e] + hb[S + col];
             if (a.logits) a.logits[((long)b * a.T + t) * a.C + col] = lg[col];
           }
         }
@@ -487,9 +543,11 @@ static void wn_finalize(tt2_wn_ctx* c) {
     const auto& ko = need(wm, s + "residual_block_out_conv" + ln + "kernel", {1, G / 2, R});
     const auto& bo = need(wm, s + "residual_block_out_conv" + ln + "bias", {R});
     for (int tid = 0; tid < WN_THREADS; ++tid) {
-      const int q = tid / 16, ks = tid % 16;  // 32 column quads x 16 k-slices
+      const int q = tid / 8, ks = tid % 8;  // 32 column quads x 8 k-slices
       for (int kk = 0; kk < CK; ++kk) {
-        const int kidx = ks * CK + kk;  // row of the linearized [kw*R, G] kernel (taps oldest first)
+        // row of the linearized [kw*R, G] kernel (taps oldest first): kk < 16 -> tap row 16ks+kk
+        // of [x(t-2d) | x(t-d)], kk >= 16 -> x(t) row 2R + 8ks + (kk-16)
+        const int kidx = kk < WN_TK ? WN_TK * ks + kk : 2 * R + WN_XK * ks + (kk - WN_TK);
         for (int e = 0; e < 4; ++e)
           cw[(((size_t)l * CK + kk) * WN_THREADS + tid) * 4 + e] = k.data[(size_t)kidx * G + gate_col(R, q, e)];
       }
@@ -554,8 +612,7 @@ static size_t gen_lds_bytes(const tt2_wn_ctx* c) {
     for (int l = st * WN_LPS; l < std::min(c->L, (st + 1) * WN_LPS); ++l) r += (2 * (1 << (l % per)) + 1) * c->R;
     ring = std::max(ring, r);
   }
-  const long fixed = 3 * 64 + 64 * 4 + 32 + 32 + 2 * WN_LPS * 128 + 2 * WN_LPS * 128 + 64 * 64 + 64 * 32 + 100 +
-                     2 * WN_SK * WN_THREADS * 4;
+  const long fixed = 64 + 64 * 4 + 32 + 32 + 2 * WN_LPS * 128 + 2 * WN_LPS * 128 + 64 * 64 + 64 * 32 + 100;
   return sizeof(float) * (fixed + ring);
 }
 
