@@ -238,7 +238,9 @@ def main():
         nst = (whp.layers + 2) // 3
         base = st[0]
         wn_stamps = [[round((st[s_ * 8 + k] - base) * 0.01, 2) if st[s_ * 8 + k] else None
-                      for k in range(6)] for s_ in range(nst)]
+                      for k in range(8)] for s_ in range(nst)]
+        wn_clock_mhz = [round((st[448 + 2 * s_ + 1] - st[448 + 2 * s_]) /
+                              max(1e-9, (st[s_ * 8 + 3] - st[s_ * 8 + 0]) * 0.01), 1) for s_ in range(nst)]
         # algorithmic bytes per sample: dilated conv + skip/out weights + head + conditioning row
         R, G, S_, L = whp.residual_channels, whp.gate_channels, whp.skip_out_channels, whp.layers
         wbytes = 4 * (L * (3 * R * G + G + (G // 2) * (S_ + R) + S_ + R) + S_ * S_ + S_ * 30 + L * G)
@@ -254,7 +256,7 @@ def main():
                                 achieved=round(wach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                                 frac=round(wach / HBM_PEAK_GBS, 5),
                                 algorithmic_bytes_per_sample=int(wbytes)),
-                  diag_stage_stamps_us=wn_stamps)
+                  diag_stage_stamps_us=wn_stamps, diag_shader_clock_mhz=wn_clock_mhz)
         weng.close()
 
     # --- CPU baseline (rank 0, N = 1 only) ---

@@ -108,6 +108,12 @@ struct GenArgs {
 
 __device__ __forceinline__ float gumbel_L(double u) { return (float)log(-log(u)); }
 
+// keeps a loop-invariant per-lane offset from being hoisted (and then spilled) out of the sample loop
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v) {
   __hip_atomic_store((gu64*)g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
@@ -187,7 +193,8 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* xcur = sm;                  // [64] input x(t) of the layer being computed
   float* z = xcur + R;               // [64]
-  float* skr = z + R;                // [64] received skip sum
+  float* fwb = z + R;                // [128] first_conv weight | bias (stage 0)
+  float* skr = fwb + 2 * R;          // [64] received skip sum
   float* skv = skr + S;              // [64]
   float* h1 = skv + S;               // [64]
   float* lg = h1 + S;                // [32]
@@ -247,8 +254,7 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
   const f32x4* cond4 = reinterpret_cast<const f32x4*>(a.cond);
   const long crow = (long)L * G / 4;  // float4 per sample row
   if (tid < nl * G / 4) reinterpret_cast<f32x4*>(cbuf)[tid] = cond4[((long)b * a.T) * crow + l0 * G / 4 + tid];
-  float fw = 0.f, fb = 0.f;
-  if (first && tid < R) { fw = a.first_w[tid]; fb = a.first_b[tid]; }
+  if (first && tid < R) { fwb[tid] = a.first_w[tid]; fwb[R + tid] = a.first_b[tid]; }
   if (tid == 0) flag[0] = 0;
   const float SQH = 0.70710677f;  // float32(np.sqrt(0.5))
   const int nr = a.C / 3;
@@ -303,17 +309,19 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
       }
       tp[j] = acc;
     }
-    // ---- receive this stage's input (wave 0) ----
+    // ---- receive this stage's input (wave 0 sweeps; one barrier publishes it to the stage) ----
     if (wave == 0) {
       float v0 = 0.f, v1 = 0.f;
       bool ok = true;
       if (first) {
         if (t > 0) ok = sweep(gin, 1, (unsigned)t, v0, v1, a.status, lane);
         const float xp = __shfl(v0, 0);
-        v0 = xp * fw + fb;  // first_conv 1x1 (wavenet.py:822): x0 = y_{t-1}·w + b
+        v0 = xp * fwb[lane] + fwb[R + lane];  // first_conv 1x1 (wavenet.py:822): x0 = y_{t-1}·w + b
       } else {
         ok = sweep(gin, WN_GR, (unsigned)(t + 1), v0, v1, a.status, lane);
       }
+      if (a.stamps && lane == 0 && bl == 0 && a.b0 == 0 && t == a.T / 2)
+        a.stamps[s * 8 + 7] = __builtin_amdgcn_s_memrealtime();
       if (!ok) {
         if (lane == 0) flag[0] = 1;
       } else {
@@ -326,6 +334,7 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
     if (flag[0]) return;
     const bool stamp = a.stamps && bl == 0 && a.b0 == 0 && t == a.T / 2 && tid == 0 && s < 64;
     if (stamp) a.stamps[s * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (stamp) a.stamps[448 + 2 * s] = __builtin_amdgcn_s_memtime();
     if (ks == 0) {
       if (q < 16) {
         if (!first) skips = reinterpret_cast<const f32x4*>(skr)[q];
@@ -341,15 +350,16 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
       // conv rows of x(t) (modules.py:283-297) on top of the precomputed tap part
       f32x4 acc = tp[j];
       {
-        const f32x4* xv4 = reinterpret_cast<const f32x4*>(xcur + 8 * ks);
+        float xv[8];
+        {
+          const f32x4* xv4 = reinterpret_cast<const f32x4*>(xcur + 8 * ks);
+          const f32x4 x0 = xv4[0], x1 = xv4[1];
+          for (int e = 0; e < 4; ++e) { xv[e] = x0[e]; xv[4 + e] = x1[e]; }
+        }
 #pragma unroll
-        for (int k4 = 0; k4 < 2; ++k4) {
-          const f32x4 xv = xv4[k4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const f32x4 w = wx[j][4 * k4 + e];
-            acc[0] += xv[e] * w[0]; acc[1] += xv[e] * w[1]; acc[2] += xv[e] * w[2]; acc[3] += xv[e] * w[3];
-          }
+        for (int i = 0; i < 8; ++i) {
+          const f32x4 w = wx[j][i];
+          acc[0] += xv[i] * w[0]; acc[1] += xv[i] * w[1]; acc[2] += xv[i] * w[2]; acc[3] += xv[i] * w[3];
         }
       }
       const f32x4 sb = reinterpret_cast<const f32x4*>(sbias + j * G)[q];  // for the skip/out phase
@@ -386,10 +396,14 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
           if (l == 0) skips = sv;
           else if (LEGACY) for (int e = 0; e < 4; ++e) skips[e] = (skips[e] + sv[e]) * SQH;
           else for (int e = 0; e < 4; ++e) skips[e] = skips[e] + sv[e];
-          if (j + 1 == nl && !last)
-            for (int e = 0; e < 4; ++e) put_granule(gout + R + 4 * q + e, (unsigned)(t + 1), skips[e]);
+          if (j + 1 == nl && !last) {
+            const int go = opaque(R + 4 * q);
+            for (int e = 0; e < 4; ++e) put_granule(gout + go + e, (unsigned)(t + 1), skips[e]);
+            if (a.stamps && tid == 0 && bl == 0 && a.b0 == 0 && t == a.T / 2)
+              a.stamps[s * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+          }
         } else if (l + 1 < L) {  // residual output (modules.py:517-520)
-          const int c4 = q - 16;  // channel quad
+          const int c4 = opaque(q - 16);  // channel quad
           for (int e = 0; e < 4; ++e) {
             xres[e] = (acc2[e] + sb[e]) + xres[e];
             if (RES_LEGACY) xres[e] = xres[e] * SQH;
@@ -405,50 +419,71 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
       }
       __syncthreads();
       if (stamp) a.stamps[s * 8 + 1 + j] = __builtin_amdgcn_s_memrealtime();
+      if (stamp && j + 1 == nl) a.stamps[448 + 2 * s + 1] = __builtin_amdgcn_s_memtime();
     }
 #pragma unroll
     for (int j = 0; j < WN_LPS; ++j) pos[j] = pos[j] + 1 == Ll[j] ? 0 : pos[j] + 1;
     if (!last) continue;
 
-    // ---- head: ReLU -> 1x1 (S->S) -> ReLU -> 1x1 (S->C) (wavenet.py:840-844) ----
+    // ---- head: ReLU -> 1x1 (S->S) -> ReLU -> 1x1 (S->C) (wavenet.py:840-844) and the MoL
+    //      sampler (mixture.py:76-107), all in wave 0 after one barrier ----
     if (ks == 0 && q < 16)
       for (int e = 0; e < 4; ++e) skv[4 * q + e] = fmaxf(skips[e], 0.f);
     __syncthreads();
-    {  // 16 column quads x 16 slices of 4 rows
-      const int q2 = tid >> 4, k2 = tid & 15;
-      const f32x4 xv = reinterpret_cast<const f32x4*>(skv)[k2];
+    if (wave != 0) continue;
+    {  // f1: 16 column quads x 4 slices of 16 rows per lane
+      const int q2 = lane >> 2, k2 = lane & 3;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const f32x4* xv4 = reinterpret_cast<const f32x4*>(skv + 16 * k2);
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const f32x4 xv = xv4[k4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f32x4 w = reinterpret_cast<const f32x4*>(hw1 + (16 * k2 + 4 * k4 + e) * S)[q2];
+          acc[0] += xv[e] * w[0]; acc[1] += xv[e] * w[1]; acc[2] += xv[e] * w[2]; acc[3] += xv[e] * w[3];
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const f32x4 w = reinterpret_cast<const f32x4*>(hw1 + (4 * k2 + e) * S)[q2];
-        acc[0] += xv[e] * w[0]; acc[1] += xv[e] * w[1]; acc[2] += xv[e] * w[2]; acc[3] += xv[e] * w[3];
+        acc[e] += dpp_f<DPP_XOR1>(acc[e]);
+        acc[e] += dpp_f<DPP_XOR2>(acc[e]);
       }
-      sum16x4(acc);
-      if (k2 == 0)
-        for (int e = 0; e < 4; ++e) h1[4 * q2 + e] = fmaxf(acc[e] + hb[4 * q2 + e], 0.f);
+      if (k2 == 0) {
+        const f32x4 bb = reinterpret_cast<const f32x4*>(hb)[q2];
+        f32x4 hv;
+        for (int e = 0; e < 4; ++e) hv[e] = fmaxf(acc[e] + bb[e], 0.f);
+        reinterpret_cast<f32x4*>(h1)[q2] = hv;
+      }
     }
-    __syncthreads();
-    {  // 8 column quads (32 >= C) x 32 slices of 2 rows
-      const int q3 = tid >> 5, k3 = tid & 31;
-      const float x0 = h1[2 * k3], x1 = h1[2 * k3 + 1];
-      const f32x4 w0 = reinterpret_cast<const f32x4*>(hw2 + (2 * k3) * 32)[q3];
-      const f32x4 w1 = reinterpret_cast<const f32x4*>(hw2 + (2 * k3 + 1) * 32)[q3];
-      float r[4];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's h1 stores before its loads
+    {  // f2: 8 column quads (32 >= C) x 8 slices of 8 rows per lane
+      const int q3 = lane >> 3, k3 = lane & 7;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const f32x4* xv4 = reinterpret_cast<const f32x4*>(h1 + 8 * k3);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) r[e] = sum32_to_lane31(x0 * w0[e] + x1 * w1[e]);
-      if (k3 == 31)
+      for (int k4 = 0; k4 < 2; ++k4) {
+        const f32x4 xv = xv4[k4];
+#pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int col = 4 * q3 + e;
-          if (col < a.C) {
-            lg[col] = r[e] + hb[S + col];
-            if (a.logits) a.logits[((long)b * a.T + t) * a.C + col] = lg[col];
-          }
+          const f32x4 w = reinterpret_cast<const f32x4*>(hw2 + (8 * k3 + 4 * k4 + e) * 32)[q3];
+          acc[0] += xv[e] * w[0]; acc[1] += xv[e] * w[1]; acc[2] += xv[e] * w[2]; acc[3] += xv[e] * w[3];
         }
+      }
+      sum8x4(acc);
+      if (k3 == 0) {
+        const f32x4 bb = reinterpret_cast<const f32x4*>(hb + S)[q3];
+        f32x4 lv;
+        for (int e = 0; e < 4; ++e) lv[e] = acc[e] + bb[e];
+        reinterpret_cast<f32x4*>(lg)[q3] = lv;
+        if (a.logits)
+          for (int e = 0; e < 4; ++e)
+            if (4 * q3 + e < a.C) a.logits[((long)b * a.T + t) * a.C + 4 * q3 + e] = lv[e];
+      }
     }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
     if (stamp) a.stamps[s * 8 + 4] = __builtin_amdgcn_s_memrealtime();
-    // ---- MoL sampler (mixture.py:76-107), wave 0; hand the sample to stage 0 ----
-    if (wave == 0) {
+    {
       float temp = -INFINITY;
       int idx = lane;
       if (lane < nr) temp = lg[lane] - gum[cb_cur * 16 + lane];
@@ -612,7 +647,7 @@ static size_t gen_lds_bytes(const tt2_wn_ctx* c) {
     for (int l = st * WN_LPS; l < std::min(c->L, (st + 1) * WN_LPS); ++l) r += (2 * (1 << (l % per)) + 1) * c->R;
     ring = std::max(ring, r);
   }
-  const long fixed = 64 + 64 * 4 + 32 + 32 + 2 * WN_LPS * 128 + 2 * WN_LPS * 128 + 64 * 64 + 64 * 32 + 100;
+  const long fixed = 64 + 64 * 6 + 32 + 32 + 2 * WN_LPS * 128 + 2 * WN_LPS * 128 + 64 * 64 + 64 * 32 + 100;
   return sizeof(float) * (fixed + ring);
 }
 
