@@ -45,9 +45,9 @@ def parse():
 
 
 def lstm_bytes(K, H, M=32):
-    """Algorithmic HBM bytes of one k_lstm launch: weights + bias + input activations + c r/w +
-    h outputs (raw + zoneout) — every byte the step must touch once."""
-    return 4 * (K * 4 * H + 4 * H + M * K + 2 * M * H + 2 * M * H)
+    """Algorithmic HBM bytes of one k_lstm launch: critical-path weights (K rows) + bias + input
+    activations + recurrent/style gate terms + c r/w + h_prev + h outputs (raw + zoneout)."""
+    return 4 * (K * 4 * H + 4 * H + M * K + M * 4 * H + 2 * M * H + 3 * M * H)
 
 
 def cpu_baseline_tacotron(hp, W, B, T, T_ref, t_out, steps):
@@ -182,7 +182,12 @@ def main():
                   decode_us_per_step=round(1000.0 * ms3[1] / max(n_steps.value, 1), 3))
 
     # --- dominant kernel roofline: the decoder Zoneout-LSTM layers (k_lstm) ---
-    us7 = (ctypes.c_float * 7)()
+    dec_stamps = None
+    if os.environ.get("TT2_STAMP_STEP"):
+        st64 = (ctypes.c_longlong * 64)()
+        _lib.check(lib.tt2_debug_stamps(eng.h, st64))
+        dec_stamps = [st64[i] - st64[0] for i in range(6)]
+    us7 = (ctypes.c_float * 10)()
     _lib.check(lib.tt2_profile_decoder_kernels(eng.h, a.profile_iters, us7))
     st64 = (ctypes.c_longlong * 64)()
     _lib.check(lib.tt2_debug_stamps(eng.h, st64))
@@ -190,8 +195,8 @@ def main():
               "energy": [st64[i] - st64[8] for i in range(8, 13)],
               "lstm": [st64[i] - st64[16] for i in range(16, 20)]}
     H, P = hp.decoder_lstm_units, hp.prenet_layers[0]
-    D = eng.D
-    by = 0.5 * (lstm_bytes(P + D + H, H) + lstm_bytes(2 * H, H))
+    E2 = 2 * hp.encoder_lstm_units
+    by = 0.5 * (lstm_bytes(P + E2, H) + lstm_bytes(H, H))
     lstm_us = us7[1]
     achieved = by / (lstm_us * 1e-6) / 1e9
     traffic = load_traffic("k_lstm")
@@ -199,8 +204,10 @@ def main():
                     achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
                     algorithmic_bytes_per_launch=int(by), avg_launch_us=round(lstm_us, 3),
+                    decode_step_prenet_stamps=dec_stamps,
                     per_kernel_us=dict(zip(["prenet", "lstm_avg", "query", "energy",
-                                            "softmax_context", "projection", "lstm2"],
+                                            "softmax_context", "projection", "lstm2", "side_job_only",
+                                            "energy_only", "softmax_only"],
                                            [round(v, 3) for v in us7])))
 
     # --- WaveNet (configs[2]) ---

@@ -142,11 +142,12 @@ tt2_status tt2_synthesize_dev(tt2_ctx* ctx, const int32_t* ids_d, const int32_t*
  * tt2_last_timings: HIP-event times (ms) of the last tt2_synthesize_dev phases
  *   [encode, decode loop, postnet].
  * tt2_profile_decoder_kernels: after a decode, re-launch each per-step decoder kernel `iters`
- *   times back-to-back on the context stream between one HIP event pair; avg_us[7] = time per
- *   launch of [prenet, lstm(layer1/layer2 alternating), query, energy, softmax+context,
- *   frame/stop projection, lstm layer 2 only].  Leaves the decoder state undefined. */
+ *   times back-to-back on the context stream between one HIP event pair; avg_us[10] = time per
+ *   launch of [prenet, lstm(layer1/layer2 alternating), query, energy(+side job), softmax+context
+ *   (+side job), frame/stop projection, lstm layer 2 only, side job alone, energy alone,
+ *   softmax+context alone].  Leaves the decoder state undefined. */
 tt2_status tt2_last_timings(tt2_ctx* ctx, float* ms3);
-tt2_status tt2_profile_decoder_kernels(tt2_ctx* ctx, int iters, float* avg_us7);
+tt2_status tt2_profile_decoder_kernels(tt2_ctx* ctx, int iters, float* avg_us10);
 /* s_memtime phase stamps (block 0) recorded during the last tt2_profile_decoder_kernels call:
  * [0..5] prenet, [8..12] energy, [16..19] lstm; diagnostic only. */
 tt2_status tt2_debug_stamps(tt2_ctx* ctx, long long* out64);

@@ -261,6 +261,23 @@ __global__ void k_memory(const float* __restrict__ enc, const float* __restrict_
 }
 
 // ---- decoder -------------------------------------------------------------------------------
+//
+// One decoder step = 7 dependent launches (captured per 16-step chunk in a hipGraph):
+//   k_prenet   finish step t-1 (frame/stop projection reduce, stop rule) + prenet of step t
+//   k_lstm     LSTM layer 1 on [prenet | context_enc] (+ precomputed recurrent/style gate terms)
+//   k_lstm     LSTM layer 2 on h1_new (+ precomputed recurrent gate term)
+//   k_partial  query layer (split-K partials)
+//   k_energy   location-sensitive energies          + side job: W_hh2·h2(t)  for step t+1
+//   k_softmax  softmax, alignments, context_enc     + side job: W_hh1·h1(t)  for step t+1
+//   k_partial  frame/stop projection (split-K partials)
+// Two algebraic identities keep bytes off the per-step critical path:
+//  * memory = [encoder outputs | tiled style] masked past each row's length (tacotron.py:297-308),
+//    so context_style = (Σ_{t<len} align_t)·style: the softmax kernel reads only the encoder half of
+//    the values, and the style rows of the LSTM-1 and projection kernels become per-utterance
+//    vectors GS = style·W_style scaled by that per-row sum each step;
+//  * [x | h]·W = x·W_x + h·W_h: the recurrent halves h(t-1)·W_h do not depend on step t's chain,
+//    so they are computed as extra workgroups ("side jobs") of two latency-bound launches of the
+//    previous step and added in the LSTM epilogues.
 
 struct DecCtl {
   int done;
@@ -269,35 +286,47 @@ struct DecCtl {
   int pad;
 };
 
+// A skinny GEMM [32 x K] · [K x 16·ntile] run as extra workgroups of a host launch:
+// block j of the job computes 16 columns, output tile-major out[tile][32][16].
+struct SideJob {
+  const float* X;   // AF [32 x K]
+  const float* W;   // WF tiles [ntile][K x 16]
+  float* out;       // [ntile][32][16]
+  int K, ntile;
+};
+
 struct DecArgs {
   DecCtl* ctl;
   int B, T_in, max_iters, T_lim;   // T_lim: GTA target length (0 = free running)
-  int nm, P, H, Dm, A, F, KL;
-  int K1, K2, Kp;                  // LSTM1 / LSTM2 / projection input widths
+  int nm, P, H, Dm, E2, A, F, KL;  // E2: encoder-output width of the memory (2 x encoder_lstm_units)
+  int K1, Kp;                      // LSTM-1 / projection critical input widths
   float zo, one_m_zo;
   int stop_at_any, mask_encoder, cumulative, constraint, monotonic, win;
   // weights
-  const float* pre_w1; const float* pre_b1; const float* pre_w2; const float* pre_b2;
-  const float* l1_w; const float* l1_b; const float* l2_w; const float* l2_b;
+  const float* pre_b1; const float* pre_w2; const float* pre_b2;
   const float* q_w; const float* loc_cw; const float* loc_cb; const float* loc_w;  // WF-packed
   int KLp, Fp;  // location conv taps / filters padded to 16
   const float* va; const float* ba; const float* proj_w; const float* proj_b;
+  const float* PS;      // [32][NPF] style·W_proj_style (per utterance), incl. the folded prenet-L1 columns
+  const float* TP1;     // [B][T_lim][P] targets·W1 + b1 (GTA) or null
   // attention memory
   const float* keys;    // [B][T_in][A]
-  const float* values;  // [B][T_in][Dm]
+  const float* values;  // [B][T_in][Dm] (only the first E2 channels are read per step)
   const int* lengths;
   // state / activations
-  float* X1[2]; float* X2[2]; float* Xp;
-  float* c1; float* c2;
+  float* X1[2];   // AF [32 x K1] = [prenet | context_enc], by step parity
+  float* Xp;      // AF [32 x Kp] = [h2_new | context_enc]
+  float* ssum;    // [32] Σ_{t<len} alignments of the last step
   float* Qp;      // [KSQ][32][A]
   float* energy;  // [B][T_in]
   float* cum;     // [B][T_in]
   int* max_att;   // [B]
-  float* PP;      // [KSP][32][NPJ]
-  int KSQ, KSP, NPJ;
+  float* PP;      // [KSP][32][NPF]: frame/stop columns [0, NPJ), prenet-L1 columns [NPJ, NPJ+P)
+  int KSQ, KSP, NPJ, NPF;
   // noise / teacher
-  const uint8_t* masks;  // [max_iters][2][B][P] or null
+  const uint8_t* masks;  // [max_iters][2][B][P] keep bits (injected, or k_gen_masks from the seed)
   uint64_t seed;
+  int stamp_step;        // prenet stamps recorded at this decoder step (diagnostic)
   const float* targets;  // [B][T_lim][nm] or null
   long long* stamps;  // diagnostic s_memtime stamps (profiling only; no output depends on them)
   // outputs
@@ -308,28 +337,65 @@ struct DecArgs {
 
 // Keep bits of the always-on prenet dropout when the caller injects none: counter-based hash of
 // (seed, flat index) -> Bernoulli(0.5), generated for the whole decode in one launch.
+// Keep bits of the always-on prenet dropout when the caller injects none: counter-based hash of
+// (seed, flat index) -> Bernoulli(0.5), generated for the whole decode in one launch.
 __global__ void k_gen_masks(uint8_t* __restrict__ m, long n, uint32_t s0, uint32_t s1) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     m[i] = (uint8_t)(hash32(hash32((uint32_t)i ^ s0) + s1) >> 31);
 }
 
-// Prenet (modules.py:346-357) of step t, preceded by the TacoTestHelper/dynamic_decode
-// bookkeeping of step t-1 (helpers.py:36-59): reduce the frame/stop projection partials,
-// write frames/stop[t-1], decide `finished`, select next input (frame or GTA target).
-// Grid: P/16 blocks (layer-2 column tiles); every block recomputes layer 1 (K = num_mels).
-// Every global load the block needs (partials, keep masks) is issued before the first use.
 constexpr int KSQ_C = 4;  // query split-K
 constexpr int KSP_C = 4;  // projection split-K
 #define STAMP(i)                                                                         \
   do {                                                                                   \
-    if (a.stamps && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)              \
+    if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0)                                 \
       a.stamps[i] = __builtin_amdgcn_s_memtime();                                        \
   } while (0)
 
-__global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep, int t) {
-  __shared__ __attribute__((aligned(16))) float fin[32 * 80];   // AF [32][nm<=80]
-  __shared__ __attribute__((aligned(16))) float h1[32 * 256];   // AF [32][P<=256]
+// One side-job tile with a 256-thread block: K split over 4 waves (every weight load in flight
+// before the first MFMA when K/64 k-groups fit the template), LDS reduce, tile-major store.
+template <int NPW>
+__device__ __forceinline__ void side_tile(const SideJob& j, int tile, float* red, float* G, int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nsg = j.K / 16;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const float* Wt = j.W + (long)tile * j.K * 16;
+  if constexpr (NPW > 0) skinny_mfma_all<NPW>(j.X, Wt, wave * NPW, acc0, acc1, lane);
+  else skinny_mfma(j.X, Wt, wave * nsg / 4, (wave + 1) * nsg / 4, acc0, acc1, lane);
+  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
+  for (int e = tid; e < 512; e += 256) j.out[(long)tile * 512 + e] = G[e];
+}
+__device__ __forceinline__ void side_job(const SideJob& j, int blk, float* red, float* G, int tid) {
+  if (j.K == 1024) side_tile<16>(j, blk, red, G, tid);
+  else side_tile<0>(j, blk, red, G, tid);
+}
+
+// Side job as its own launch (parallel graph branch).
+__global__ __launch_bounds__(256) void k_side(const DecCtl* ctl, SideJob sj) {
   __shared__ float red[4 * 512];
+  __shared__ float G[512];
+  if (ctl->done) return;
+  side_job(sj, blockIdx.x, red, G, threadIdx.x);
+}
+
+// Prenet (modules.py:346-357) of step t, preceded by the TacoTestHelper/dynamic_decode
+// bookkeeping of step t-1 (helpers.py:36-59): reduce the frame/stop projection partials (+ style
+// term), write frames/stop[t-1], decide `finished`.  Layer 1 is never recomputed here: its
+// pre-activation frame_in·W1 + b1 arrives ready — free running, frame·W1 = [h2|ctx]·(W_f·W1) +
+// b_f·W1 is folded into the projection launch (its columns NPJ.. of the partials); with GTA
+// targets it was computed for all steps at decode start (TP1); at t = 0 (GO frame) it is b1.
+// Grid: P/16 blocks (layer-2 column tiles) of 16 waves.
+constexpr int PRE_T = 1024;
+__global__ __launch_bounds__(PRE_T) void k_prenet(DecArgs a, int istep, int t) {
+  // (never assign to a field of `a`: a modified by-value kernel argument is copied to scratch)
+  long long* const stp = (a.stamp_step < 0 || t == a.stamp_step) ? a.stamps : nullptr;
+#undef STAMP
+#define STAMP(i)                                                                         \
+  do {                                                                                   \
+    if (stp && blockIdx.x == 0 && threadIdx.x == 0) stp[i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  __shared__ __attribute__((aligned(16))) float h1[32 * 256];   // AF [32][P<=256]
+  __shared__ float red[16 * 512];
   __shared__ float G[512];
   __shared__ float stopv[32];
   __shared__ __attribute__((aligned(16))) uint8_t mk1[32 * 256];
@@ -338,138 +404,153 @@ __global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep, int t) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   STAMP(0);
   const int done0 = a.ctl->done;
-  const int nm = a.nm, nmp = (nm + 15) & ~15, P = a.P, tile = blockIdx.x;
-  // ---- issue loads: projection partials (row m, 12 columns), keep masks of step t ----
-  const int pm = tid >> 3, pq = tid & 7;  // NPJ = 96 = 8 x 12
-  f32x4 pp[KSP_C][3];
-  if (t > 0 && a.NPJ == 96) {
+  const int nm = a.nm, P = a.P, tile = blockIdx.x, NPF = a.NPF;
+  // ---- issue loads: frame/stop partials (row pm, 3 columns), layer-1 pre-activation sources
+  //      (row pm, 8 columns), style sums, keep masks, this block's layer-2 weights ----
+  const int pm = tid >> 5, pq = tid & 31;  // 32 rows x 32 lanes
+  // every load below is unconditional (clamped index, value selected later) so that all of them
+  // are in flight together; a conditional load becomes a branch that waits for it
+  float pp[KSP_C][3], pps[3], ppb[3];
+  const float ssum_m = a.ssum[pm];  // frame/stop phase row
+  const float* PPr = a.PP + (long)pm * NPF;
 #pragma unroll
-    for (int ks = 0; ks < KSP_C; ++ks)
+  for (int j = 0; j < 3; ++j) {
+    const int n = min(pq * 3 + j, a.NPJ - 1);
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        pp[ks][j] = *reinterpret_cast<const f32x4*>(a.PP + ((long)ks * 32 + pm) * 96 + pq * 12 + 4 * j);
+    for (int ks = 0; ks < KSP_C; ++ks) pp[ks][j] = PPr[(long)ks * 32 * NPF + n];
+    pps[j] = a.PS[(long)pm * NPF + n];
+    ppb[j] = a.proj_b[n];
   }
-  const int ntile = P / 16, nsg1 = nmp / 16, nsg2 = P / 16;
-  const f32x4* W1v = reinterpret_cast<const f32x4*>(a.pre_w1);
+  // next step's keep masks -> this XCD's L2 (the same block id runs next step's prenet on it);
+  // asm loads into a never-read register: the compiler neither drops nor waits for them
+  // (the destination register is kept live to the kernel's end so nothing reuses it while the
+  // untracked load is in flight)
+  unsigned pf_dummy = 0u;
+  if (t + 1 < a.max_iters && tid < 160) {
+    // layer-1 masks (all rows, one load per 64-byte line) and this tile's layer-2 mask rows
+    const long nrow = (long)(t + 1) * 2 * a.B * P;
+    const long bp = (long)a.B * P;
+    long off = -1;
+    if (tid < 128) off = (long)tid * 64 < bp ? (long)tid * 64 : -1;
+    else if (tid - 128 < a.B) off = bp + (long)(tid - 128) * P + tile * 16;
+    if (off >= 0) asm volatile("global_load_dword %0, %1, off" : "=v"(pf_dummy) : "v"(a.masks + nrow + off) : "memory");
+  }
+  // layer-1 pre-activations arrive in "AF-group" column order: position 4g + j holds column
+  const int G4 = P / 4, nit = (32 * G4 + PRE_T - 1) / PRE_T;  // nit <= 2
+  const int mode1 = t == 0 ? 0 : (a.targets ? 1 : 2);  // GO frame / GTA teacher / folded projection
+  const int im = tid & 31;
+  const float ssum_i = a.ssum[im];
+  f32x4 l1v[2], l1p[2][KSP_C], l1s[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int g = min((tid >> 5) + it * (PRE_T / 32), G4 - 1);
+    if (mode1 == 2) {
+#pragma unroll
+      for (int ks = 0; ks < KSP_C; ++ks)
+        l1p[it][ks] = *reinterpret_cast<const f32x4*>(a.PP + ((long)ks * 32 + im) * NPF + a.NPJ + 4 * g);
+      l1s[it] = *reinterpret_cast<const f32x4*>(a.PS + (long)im * NPF + a.NPJ + 4 * g);
+      l1v[it] = *reinterpret_cast<const f32x4*>(a.proj_b + a.NPJ + 4 * g);
+    } else if (mode1 == 1) {
+      const int mm = min(im, a.B - 1), tt = min(t - 1, a.T_lim - 1);
+      l1v[it] = *reinterpret_cast<const f32x4*>(a.TP1 + ((long)mm * a.T_lim + tt) * P + 4 * g);
+    } else {
+      l1v[it] = *reinterpret_cast<const f32x4*>(a.pre_b1 + 4 * g);
+    }
+  }
+  const int nsg2 = P / 16;
   const f32x4* W2v = reinterpret_cast<const f32x4*>(a.pre_w2);
-  f32x4 w1[4][5], w2[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int tl = wave + 4 * i;
-      if (tl < ntile && j < nsg1) w1[i][j] = W1v[(tl * nsg1 + j) * 64 + lane];
-    }
-  const int s2a = wave * nsg2 / 4, s2b = (wave + 1) * nsg2 / 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (s2a + j < s2b) w2[j] = W2v[((long)tile * nsg2 + s2a + j) * 64 + lane];
+  f32x4 w2 = {0.f, 0.f, 0.f, 0.f};
+  if (wave < nsg2) w2 = W2v[((long)tile * nsg2 + wave) * 64 + lane];
   const long mrow = (long)t * 2 * a.B * P;
-  if (t < a.max_iters) {
-    for (int i = tid; i < 32 * P / 16; i += blockDim.x) {  // 16-byte chunks of layer-1 masks
-      const int m = (i * 16) / P;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (m < a.B) v = *reinterpret_cast<const uint4*>(a.masks + mrow + (long)i * 16);
-      reinterpret_cast<uint4*>(mk1)[i] = v;
-    }
-    for (int i = tid; i < 32 * 16; i += blockDim.x) {
-      const int m = i >> 4, j = i & 15;
-      mk2[i] = m < a.B ? a.masks[mrow + (long)a.B * P + (long)m * P + tile * 16 + j] : 0;
-    }
+  // keep masks into registers now, into LDS after the stop decision (loads complete in issue
+  // order: anything consumed earlier must not wait behind them)
+  const bool has_mask = t < a.max_iters;
+  const int nch = 32 * P / 16;  // 16-column chunks of layer-1 masks (<= PRE_T)
+  uint4 mv = {0u, 0u, 0u, 0u};
+  uint8_t m2v = 0;
+  if (has_mask && tid < nch) {
+    const int m = (tid * 16) / P;
+    if (m < a.B) mv = *reinterpret_cast<const uint4*>(a.masks + mrow + (long)tid * 16);
+  }
+  if (has_mask && tid < 32 * 16) {
+    const int m = tid >> 4, j = tid & 15;
+    if (m < a.B) m2v = a.masks[mrow + (long)a.B * P + (long)m * P + tile * 16 + j];
   }
   if (done0) return;
   STAMP(1);
-  for (int i = tid; i < 32 * nmp; i += blockDim.x) fin[i] = 0.f;
-  if (tid == 0) s_done = 0;
-  __syncthreads();
-  STAMP(2);
   // ---- finish step t-1 ----
   if (t > 0) {
-    if (a.NPJ == 96) {
-      float v[12];
+    for (int jj = 0; jj < 3; ++jj) {
+      const int n = pq * 3 + jj, m = pm;
+      if (n > nm) continue;
+      float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 12; ++j) v[j] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < KSP_C; ++ks)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[4 * j + e] += pp[ks][j][e];
-      for (int j = 0; j < 12; ++j) {
-        const int n = pq * 12 + j, m = pm;
-        if (n > nm) continue;
-        const float s = v[j] + a.proj_b[n];
-        if (n == nm) {
-          stopv[m] = sigm(s);
-        } else {
-          float x = s;
-          if (a.targets) x = (m < a.B) ? a.targets[((long)m * a.T_lim + (t - 1)) * nm + n] : 0.f;
-          fin[af_idx(m, n)] = (m < a.B) ? x : 0.f;
-          if (tile == 0 && m < a.B) a.frames[((long)m * a.max_iters + (t - 1)) * nm + n] = s;
-        }
-      }
-    } else {
-      for (int e = tid; e < 32 * (nm + 1); e += blockDim.x) {
-        const int m = e / (nm + 1), n = e % (nm + 1);
-        float s = 0.f;
-        for (int ks = 0; ks < KSP_C; ++ks) s += a.PP[((long)ks * 32 + m) * a.NPJ + n];
-        s += a.proj_b[n];
-        if (n == nm) {
-          stopv[m] = sigm(s);
-        } else {
-          float x = s;
-          if (a.targets) x = (m < a.B) ? a.targets[((long)m * a.T_lim + (t - 1)) * nm + n] : 0.f;
-          fin[af_idx(m, n)] = (m < a.B) ? x : 0.f;
-          if (tile == 0 && m < a.B) a.frames[((long)m * a.max_iters + (t - 1)) * nm + n] = s;
-        }
+      for (int ks = 0; ks < KSP_C; ++ks) s += pp[ks][jj];
+      s = (s + ssum_m * pps[jj]) + ppb[jj];
+      if (n == nm) {
+        stopv[m] = sigm(s);
+      } else if (tile == 0 && m < a.B) {
+        a.frames[((long)m * a.max_iters + (t - 1)) * nm + n] = s;
       }
     }
     __syncthreads();
-    if (tid == 0) {
-      int fin_all = 1, fin_any = 0;
-      for (int m = 0; m < a.B; ++m) {
-        const int f = rintf(stopv[m]) == 1.0f;
-        fin_all &= f;
-        fin_any |= f;
-        if (tile == 0) a.stop[(long)m * a.max_iters + (t - 1)] = stopv[m];
-      }
-      int done = a.stop_at_any ? fin_any : fin_all;
+    STAMP(2);
+    if (wave == 0) {  // batch-level stop rule (helpers.py:40-48): one lane per row
+      const bool valid = lane < a.B;
+      const float sv = valid ? stopv[lane] : 0.f;
+      const bool f = valid && rintf(sv) == 1.0f;
+      const unsigned long long fb = __ballot(f), vb = __ballot(valid);
+      if (valid && tile == 0) a.stop[(long)lane * a.max_iters + (t - 1)] = sv;
+      int done = a.stop_at_any ? (fb != 0ull) : (fb == vb);
       if (a.T_lim > 0) done = t >= a.T_lim;   // TacoTrainingHelper: time + 1 >= T_targets
       if (t >= a.max_iters) done = 1;         // dynamic_decode maximum_iterations
-      s_done = done;
-      if (done && tile == 0) {
-        a.ctl->n_steps = t;
-        a.ctl->done = 1;
+      if (lane == 0) {
+        s_done = done;
+        if (done && tile == 0) {
+          a.ctl->n_steps = t;
+          a.ctl->done = 1;
+        }
       }
     }
     __syncthreads();
     if (s_done) return;
   }
   STAMP(3);
-  // ---- layer 1: relu(fin·W1 + b1) * keep / 0.5  (all 16-col tiles, K = nm) ----
+  // ---- keep masks -> LDS: layer 1 in AF-group byte order (4x4 byte transpose of each chunk:
+  //      byte 4kk + j <- column kk + 4j), layer 2 as loaded ----
+  if (tid < nch) {
+    const unsigned w[4] = {mv.x, mv.y, mv.z, mv.w};
+    unsigned o[4];
+    for (int kk = 0; kk < 4; ++kk)
+      o[kk] = ((w[0] >> (8 * kk)) & 0xffu) | (((w[1] >> (8 * kk)) & 0xffu) << 8) |
+              (((w[2] >> (8 * kk)) & 0xffu) << 16) | (((w[3] >> (8 * kk)) & 0xffu) << 24);
+    reinterpret_cast<uint4*>(mk1)[tid] = uint4{o[0], o[1], o[2], o[3]};
+  }
+  if (tid < 32 * 16) mk2[tid] = m2v;
+  __syncthreads();
+  // ---- layer 1: relu(pre-activation) * keep / 0.5 ----
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int tl = wave + 4 * i;
-    if (tl >= ntile) break;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    skinny_mfma_w<5>(fin, w1[i], nsg1, acc0, acc1, lane);
-    const int n = tl * 16 + (lane & 15);
-    const float bn = a.pre_b1[n];
+  for (int it = 0; it < 2; ++it) {
+    const int g = (tid >> 5) + it * (PRE_T / 32);
+    if (it >= nit || g >= G4) break;
+    f32x4 x = l1v[it];
+    if (mode1 == 2) {
+      f32x4 sacc = l1p[it][0];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m0 = (lane >> 4) * 4 + r;
-      const float v0 = (fmaxf(acc0[r] + bn, 0.f) / 0.5f) * (float)mk1[m0 * P + n];
-      const float v1 = (fmaxf(acc1[r] + bn, 0.f) / 0.5f) * (float)mk1[(m0 + 16) * P + n];
-      h1[af_idx(m0, n)] = v0;
-      h1[af_idx(m0 + 16, n)] = v1;
+      for (int ks = 1; ks < KSP_C; ++ks) sacc += l1p[it][ks];
+      for (int e = 0; e < 4; ++e) x[e] = (sacc[e] + ssum_i * l1s[it][e]) + x[e];  // (Σ partials + style) + (b_f·W1 + b1)
     }
+    const unsigned mw = reinterpret_cast<const unsigned*>(mk1)[(im * P + 4 * g) >> 2];
+    f32x4 hv;
+    for (int e = 0; e < 4; ++e) hv[e] = (fmaxf(x[e], 0.f) / 0.5f) * (float)((mw >> (8 * e)) & 0xffu);
+    *reinterpret_cast<f32x4*>(h1 + af_idx(im, 16 * (g >> 2) + (g & 3))) = hv;
   }
   __syncthreads();
   STAMP(4);
-  // ---- layer 2: this block's 16 columns, K = P split over 4 waves ----
+  // ---- layer 2: this block's 16 columns, one k-group of 16 per wave ----
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  skinny_mfma_w<4>(h1 + s2a * 2 * 64 * 4, w2, s2b - s2a, acc0, acc1, lane);
-  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
+  if (wave < nsg2) skinny_mfma_w<1>(h1 + wave * 2 * 64 * 4, &w2, 1, acc0, acc1, lane);
+  reduce_waves_32x16<16>(acc0, acc1, red, G, wave, lane, tid);
   float* X1 = a.X1[istep & 1];
   for (int e = tid; e < 512; e += blockDim.x) {
     const int m = e >> 4, j = e & 15, n = tile * 16 + j;
@@ -477,20 +558,30 @@ __global__ __launch_bounds__(256) void k_prenet(DecArgs a, int istep, int t) {
     X1[af_idx(m, n)] = v;
   }
   STAMP(5);
+  asm volatile("" ::"v"(pf_dummy));
 }
+#undef STAMP
+#define STAMP(i)                                                                         \
+  do {                                                                                   \
+    if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0)                                 \
+      a.stamps[i] = __builtin_amdgcn_s_memtime();                                        \
+  } while (0)
 
 // Zoneout-LSTM layer (modules.py:220-248 on TF LSTMCell): block g owns hidden units [4g, 4g+4)
-// = 16 gate columns (i,j,f,o × 4), K split over 4 waves, fused cell/zoneout epilogue.
-//   X [32 x K AF] input (h_prev at column hprev_off); writes h_new (raw LSTM output) into
-//   Xo at column ho_off, the zoned h into Xz at column hz_off, c in place.
+// = 16 gate columns (i,j,f,o × 4).  gates = X·W (K split over 8 waves, all weight loads in flight
+// first) + RG (recurrent h(t-1)·W_h, a side job of the previous step) + ssum·GS (style term) + b;
+// fused cell/zoneout epilogue.  Writes h_new (the raw LSTM output, the layer's output) into Xo at
+// column ho_off and the zoned state into Hz; c in place.
 struct LstmArgs {
   long long* stamps = nullptr;
   const DecCtl* ctl;
-  const float* X; int K; int hprev_off;
+  const float* X; int K;
   const float* W; const float* b;
+  const float* RG;                    // [H/4][32][16] or null
+  const float* GS; const float* ssum; // [32][4H] (lstm column order) + [32], or null
+  const float* Hprev; float* Hz;      // AF [32 x H] zoned states t-1 / t
   float* c; int H;
   float* Xo; int ho_off;
-  float* Xz; int hz_off;
   float zo, one_m_zo;
 };
 
@@ -506,25 +597,32 @@ __global__ __launch_bounds__(512) void k_lstm(LstmArgs a) {
   const float* Wg = a.W + (long)g * a.K * 16;
   if constexpr (NPW > 0) skinny_mfma_all<NPW>(a.X, Wg, wave * NPW, acc0, acc1, lane);
   else skinny_mfma(a.X, Wg, wave * nsg / 8, (wave + 1) * nsg / 8, acc0, acc1, lane);
+  // epilogue operands (independent of the GEMM): issue before the reduction
+  float rg[4] = {0.f, 0.f, 0.f, 0.f}, gs[4] = {0.f, 0.f, 0.f, 0.f}, cprev = 0.f, hprev = 0.f, sm = 0.f;
+  const int m = tid >> 2, uu = tid & 3, u = 4 * g + uu;
+  if (tid < 128) {
+    if (a.RG)
+      for (int q = 0; q < 4; ++q) rg[q] = a.RG[((long)g * 32 + m) * 16 + 4 * q + uu];
+    if (a.GS) {
+      for (int q = 0; q < 4; ++q) gs[q] = a.GS[(long)m * 4 * a.H + g * 16 + 4 * q + uu];
+      sm = a.ssum[m];
+    }
+    cprev = a.c[(long)m * a.H + u];
+    hprev = a.Hprev[af_idx(m, u)];
+  }
   STAMP(17);
   if (done) return;
   reduce_waves_32x16<8>(acc0, acc1, red, G, wave, lane, tid);
   STAMP(18);
   if (tid < 128) {
-    const int m = tid >> 2, uu = tid & 3, u = 4 * g + uu;
     const float* bb = a.b + g * 16;
-    const float zi = G[m * 16 + 0 + uu] + bb[0 + uu];
-    const float zj = G[m * 16 + 4 + uu] + bb[4 + uu];
-    const float zf = G[m * 16 + 8 + uu] + bb[8 + uu];
-    const float zz = G[m * 16 + 12 + uu] + bb[12 + uu];
-    float* cp = a.c + (long)m * a.H + u;
-    const float cprev = *cp;
-    const float hprev = a.X[af_idx(m, a.hprev_off + u)];
-    const float cn = sigm(zf + 1.0f) * cprev + sigm(zi) * tanhf(zj);
-    const float hn = sigm(zz) * tanhf(cn);
-    *cp = a.one_m_zo * cn + a.zo * cprev;
+    float z[4];
+    for (int q = 0; q < 4; ++q) z[q] = ((G[m * 16 + 4 * q + uu] + rg[q]) + sm * gs[q]) + bb[4 * q + uu];
+    const float cn = sigm(z[2] + 1.0f) * cprev + sigm(z[0]) * tanhf(z[1]);
+    const float hn = sigm(z[3]) * tanhf(cn);
+    a.c[(long)m * a.H + u] = a.one_m_zo * cn + a.zo * cprev;
     a.Xo[af_idx(m, a.ho_off + u)] = hn;
-    a.Xz[af_idx(m, a.hz_off + u)] = a.one_m_zo * hn + a.zo * hprev;
+    a.Hz[af_idx(m, u)] = a.one_m_zo * hn + a.zo * hprev;
   }
   STAMP(19);
 }
@@ -532,11 +630,12 @@ __global__ __launch_bounds__(512) void k_lstm(LstmArgs a) {
 static void launch_lstm(const LstmArgs& l, int H, hipStream_t s) {
   const int nsg = l.K / 16;
   const dim3 grid(H / 4), blk(512);
-  if (nsg % 8 == 0 && nsg / 8 == 18) hipLaunchKernelGGL(k_lstm<18>, grid, blk, 0, s, l);
-  else if (nsg % 8 == 0 && nsg / 8 == 16) hipLaunchKernelGGL(k_lstm<16>, grid, blk, 0, s, l);
-  else if (nsg % 8 == 0 && nsg / 8 == 8) hipLaunchKernelGGL(k_lstm<8>, grid, blk, 0, s, l);
-  else if (nsg % 8 == 0 && nsg / 8 == 4) hipLaunchKernelGGL(k_lstm<4>, grid, blk, 0, s, l);
-  else if (nsg % 8 == 0 && nsg / 8 == 2) hipLaunchKernelGGL(k_lstm<2>, grid, blk, 0, s, l);
+  const int npw = nsg % 8 == 0 ? nsg / 8 : 0;
+  if (npw == 18) hipLaunchKernelGGL(k_lstm<18>, grid, blk, 0, s, l);
+  else if (npw == 8) hipLaunchKernelGGL(k_lstm<8>, grid, blk, 0, s, l);
+  else if (npw == 6) hipLaunchKernelGGL(k_lstm<6>, grid, blk, 0, s, l);
+  else if (npw == 4) hipLaunchKernelGGL(k_lstm<4>, grid, blk, 0, s, l);
+  else if (npw == 2) hipLaunchKernelGGL(k_lstm<2>, grid, blk, 0, s, l);
   else hipLaunchKernelGGL(k_lstm<0>, grid, blk, 0, s, l);
 }
 
@@ -550,9 +649,14 @@ struct PartArgs {
 };
 
 template <int NPW>
-__global__ __launch_bounds__(256) void k_partial(PartArgs a) {
+__global__ __launch_bounds__(256) void k_partial(PartArgs a, SideJob sj) {
   __shared__ float red[4 * 512];
   __shared__ float G[512];
+  if ((int)blockIdx.x >= a.ntile * a.KS) {  // extra blocks: side job
+    if (a.ctl->done) return;
+    side_job(sj, blockIdx.x - a.ntile * a.KS, red, G, threadIdx.x);
+    return;
+  }
   const int done = a.ctl->done;
   const int tile = blockIdx.x % a.ntile, ks = blockIdx.x / a.ntile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -571,30 +675,38 @@ __global__ __launch_bounds__(256) void k_partial(PartArgs a) {
   }
 }
 
-static void launch_partial(const PartArgs& p, hipStream_t s) {
+static void launch_partial(const PartArgs& p, const SideJob& sj, hipStream_t s) {
   const int nsg = p.K / 16;
-  const dim3 grid(p.ntile * p.KS), blk(256);
+  const dim3 grid(p.ntile * p.KS + sj.ntile), blk(256);
   const bool even = nsg % (p.KS * 4) == 0;
   const int npw = even ? nsg / (p.KS * 4) : 0;
-  if (npw == 4) hipLaunchKernelGGL(k_partial<4>, grid, blk, 0, s, p);
-  else if (npw == 2) hipLaunchKernelGGL(k_partial<2>, grid, blk, 0, s, p);
-  else if (npw == 8) hipLaunchKernelGGL(k_partial<8>, grid, blk, 0, s, p);
-  else hipLaunchKernelGGL(k_partial<0>, grid, blk, 0, s, p);
+  if (npw == 4) hipLaunchKernelGGL(k_partial<4>, grid, blk, 0, s, p, sj);
+  else if (npw == 6) hipLaunchKernelGGL(k_partial<6>, grid, blk, 0, s, p, sj);
+  else if (npw == 2) hipLaunchKernelGGL(k_partial<2>, grid, blk, 0, s, p, sj);
+  else if (npw == 8) hipLaunchKernelGGL(k_partial<8>, grid, blk, 0, s, p, sj);
+  else hipLaunchKernelGGL(k_partial<0>, grid, blk, 0, s, p, sj);
 }
 
 // Location-sensitive energies (attention.py:37-69, 186-215) for 32 encoder steps of one row:
 //   q = Σ query partials;  f = im2col(cum, 31 taps)·W_conv + b  (MFMA, K = taps);
 //   loc = f·W_loc (MFMA, K = filters);  e_t = Σ_k v_a[k]·tanh(keys + q + loc + b_a)
 // then the synthesis window constraint and -inf past the row's length (TF _maybe_mask_score).
-__global__ __launch_bounds__(256) void k_energy(DecArgs a) {
+// Blocks past B·ceil(T_in/32) run the side job.
+__global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
   __shared__ __attribute__((aligned(16))) float A1[32 * 64];  // AF [32 t][KLp taps]
   __shared__ __attribute__((aligned(16))) float A2[32 * 64];  // AF [32 t][Fp filters]
   __shared__ float q[256];
   __shared__ float win[32 + 64];
   __shared__ float ep[4][32];
+  const int ntt = (a.T_in + 31) / 32, nE = a.B * ntt;
+  if ((int)blockIdx.x >= nE) {
+    if (a.ctl->done) return;
+    side_job(sj, blockIdx.x - nE, A1, A2 + 1536, threadIdx.x);  // red: A1+A2[0..1535] (2048 floats)
+    return;
+  }
   STAMP(8);
   const int done = a.ctl->done;
-  const int b = blockIdx.x, t0 = blockIdx.y * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int A = a.A, KL = a.KL, KLp = a.KLp, Fp = a.Fp, padl = (KL - 1) / 2;
   // prefetch the keys this lane consumes after the location MFMA (<= 4 tiles x 8 rows)
   float kv[4][8];
@@ -710,12 +822,21 @@ __global__ __launch_bounds__(256) void k_energy(DecArgs a) {
   STAMP(12);
 }
 
-// softmax → alignments, context = alignments · values for 64 memory channels of one row
-// (attention.py:10-35, 217-225); the dc==0 block also updates cum/max_att and writes alignments.
-__global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t_step) {
+
+// softmax → alignments, context_enc = alignments · values[:, :, 0:E2] for 64 channels of one row
+// (attention.py:10-35, 217-225); the dc==0 block also updates cum/max_att, writes alignments and
+// the row's Σ_{t<len} alignments (the scale of the style half of the context).
+// Blocks past B·E2/64 run the side job.
+__global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t_step, SideJob sj) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int ndc = a.E2 / 64, nS = a.B * ndc;
+  if ((int)blockIdx.x >= nS) {
+    if (a.ctl->done) return;
+    side_job(sj, blockIdx.x - nS, sm, sm + 2048, threadIdx.x);
+    return;
+  }
   const int done = a.ctl->done;
-  const int b = blockIdx.x, dc = blockIdx.y, tid = threadIdx.x;
+  const int b = blockIdx.x / ndc, dc = blockIdx.x % ndc, tid = threadIdx.x;
   const int T = a.T_in;
   float* al = sm;                      // [T]
   float* red = al + ((T + 3) & ~3);    // [4*16*16]
@@ -728,7 +849,7 @@ __global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int t = tq + 16 * i;
-    if (t < T && d < a.Dm) v[i] = *reinterpret_cast<const f32x4*>(vr + (long)t * a.Dm);
+    if (t < T) v[i] = *reinterpret_cast<const f32x4*>(vr + (long)t * a.Dm);
     else v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   for (int i = tid; i < T; i += blockDim.x) al[i] = a.energy[(long)b * T + i];
@@ -753,12 +874,11 @@ __global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t
     const float w = t < T ? al[t] : 0.f;
     acc[0] += w * v[i][0]; acc[1] += w * v[i][1]; acc[2] += w * v[i][2]; acc[3] += w * v[i][3];
   }
-  if (d < a.Dm)
-    for (int t = tq + 256; t < T; t += 16) {  // tail for T_in > 256
-      const f32x4 x = *reinterpret_cast<const f32x4*>(vr + (long)t * a.Dm);
-      const float w = al[t];
-      acc[0] += w * x[0]; acc[1] += w * x[1]; acc[2] += w * x[2]; acc[3] += w * x[3];
-    }
+  for (int t = tq + 256; t < T; t += 16) {  // tail for T_in > 256
+    const f32x4 x = *reinterpret_cast<const f32x4*>(vr + (long)t * a.Dm);
+    const float w = al[t];
+    acc[0] += w * x[0]; acc[1] += w * x[1]; acc[2] += w * x[2]; acc[3] += w * x[3];
+  }
   for (int j = 0; j < 4; ++j) red[(j * 16 + dq) * 16 + tq] = acc[j];
   __syncthreads();
   if (tid < 64) {
@@ -766,28 +886,33 @@ __global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t
     float s = 0.f;
     for (int i = 0; i < 16; ++i) s += red[(j * 16 + dq2) * 16 + i];
     const int dd = dc * 64 + dq2 * 4 + j;
-    if (dd < a.Dm) {
-      a.X1[(istep + 1) & 1][af_idx(b, a.P + dd)] = s;
-      a.Xp[af_idx(b, a.H + dd)] = s;
-    }
+    a.X1[(istep + 1) & 1][af_idx(b, a.P + dd)] = s;
+    a.Xp[af_idx(b, a.H + dd)] = s;
   }
   if (dc == 0) {
+    const int len = a.lengths[b];
     for (int i = tid; i < T; i += blockDim.x) {
       float* c = a.cum + (long)b * T + i;
       *c = a.cumulative ? al[i] + *c : al[i];
       if (a.align && t_step < a.max_iters) a.align[((long)b * T + i) * a.max_iters + t_step] = al[i];
     }
     if (tid < 64) {
-      float best = -INFINITY;
+      float best = -INFINITY, ss = 0.f;
       int bi = 0x7fffffff;
-      for (int i = tid; i < T; i += 64)
+      for (int i = tid; i < T; i += 64) {
         if (al[i] > best) { best = al[i]; bi = i; }
+        if (i < len) ss += al[i];
+      }
       for (int o = 32; o > 0; o >>= 1) {
         const float ob = __shfl_xor(best, o);
         const int oi = __shfl_xor(bi, o);
         if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        ss += __shfl_xor(ss, o);
       }
-      if (tid == 0) a.max_att[b] = bi;
+      if (tid == 0) {
+        a.max_att[b] = bi;
+        a.ssum[b] = ss;
+      }
     }
   }
 }
@@ -808,7 +933,6 @@ __global__ void k_clip_frames(const float* __restrict__ src, long src_bstride, f
 // ==========================================================================================
 // Host side
 // ==========================================================================================
-
 struct RefNetDev {
   DevBuf cw[6], cb[6], bs[6], bh[6];
   DevBuf kg, bg, kc, bc, kd, bd, tok, kq, bq, kk, bk, av, ag, ab;
@@ -827,7 +951,7 @@ struct tt2_ctx {
   hipStream_t stream = nullptr;
   tt2::WeightMap host;
   bool finalized = false;
-  int nm, E, Cenc, U, Dm, A, F, KL, P, H, PC, SW, K1, K2, Kp, NPJ, KSQ = tt2::KSQ_C, KSP = tt2::KSP_C, KLp, Fp;
+  int nm, E, Cenc, U, Dm, E2, A, F, KL, P, H, PC, SW, K1, Kp, NPJ, NPF, KSQ = tt2::KSQ_C, KSP = tt2::KSP_C, KLp, Fp;
   int nref;
   // weights
   tt2::DevBuf emb;
@@ -835,13 +959,15 @@ struct tt2_ctx {
   tt2::DevBuf enc_wx, enc_bx, enc_wh;
   tt2::RefNetDev ref[2];
   tt2::DevBuf mem_k;
-  tt2::DevBuf pre_w1, pre_b1, pre_w2, pre_b2, l1_w, l1_b, l2_w, l2_b, q_w;
-  tt2::DevBuf loc_cw, loc_cb, loc_w, va, ba, proj_w, proj_b;
+  tt2::DevBuf pre_w1r, pre_b1, pre_w2, pre_b2, q_w;  // pre_w1r: row-major [nm][P] (GTA TP1 GEMM)
+  tt2::DevBuf l1_w, l1_wh, l1_ws, l1_b, l2_w, l2_wh, l2_b;  // critical rows / recurrent rows / style rows
+  tt2::DevBuf loc_cw, loc_cb, loc_w, va, ba, proj_w, proj_ws, proj_b;
   tt2::DevBuf post_cw[8], post_cb[8], post_bs[8], post_bh[8], post_pw, post_pb;
   // activations
   tt2::DevBuf ids, lens, refm[2], x_a, x_b, xproj, enc_out, enc_h, enc_c, conv_a, conv_b, ref_out, style,
       values, keys;
-  tt2::DevBuf X1[2], X2[2], Xp, c1, c2, Qp, energy, cum, max_att, PP, ctl, masks, gmasks, targets;
+  tt2::DevBuf X1[2], X2, Xp, H0s[2], H1s[2], RG0, RG1, GS0, PS, ssum, TP1, c1, c2, Qp, energy, cum, max_att, PP, ctl,
+      masks, gmasks, targets;
   tt2::DevBuf frames, stop, align, dec, post_a, post_b, mel;
   int* ctl_host = nullptr;  // pinned [2 slots]
   int B = 0, T_in = 0, n_steps = 0, last_max_iters = 0;
@@ -852,6 +978,8 @@ struct tt2_ctx {
   bool timed = false;
   tt2::DecArgs last_args;
   long long stamps_host[64] = {0};
+  int side_mode = 0;                 // TT2_SIDE_MODE env: 0 hosted side jobs, 1 parallel branch
+  hipEvent_t sev[8] = {nullptr};     // capture-time fork/join events
   bool have_args = false;
 };
 
@@ -889,6 +1017,13 @@ static std::vector<float> pack_wf(const float* W, int K, int N, const std::vecto
       for (int k = 0; k < K; ++k) out[(size_t)tile * Kp * 16 + wf_idx(k, j)] = W[(size_t)k * N + c];
     }
   return out;
+}
+
+// AF-group column order of the prenet layer-1 pre-activations: position p = 4g + j holds column
+// 16(g/4) + g%4 + 4j, so a float4 at 4g is the AF float4 of group g (k_prenet)
+static int af_group_col(int p) {
+  const int g = p >> 2, j = p & 3;
+  return 16 * (g >> 2) + (g & 3) + 4 * j;
 }
 
 // LSTM gate column order per block g: [i u0..u3, j u0..u3, f u0..u3, o u0..u3]
@@ -968,26 +1103,44 @@ static void finalize(tt2_ctx* c) {
   upload(c->mem_k, need(wm, P + "memory_layer/kernel", {c->Dm, c->A}));
   // decoder
   {
-    const int nmp = (c->nm + 15) & ~15;
     std::vector<int> cols;
     for (int j = 0; j < c->P; ++j) cols.push_back(j);
+    // layer 1 in AF-group column order (see k_prenet): used for the GTA TP1 GEMM and the GO frame
     const auto& w1 = need(wm, P + "decoder/decoder_prenet/dense_1/kernel", {c->nm, c->P});
-    upload(c->pre_w1, pack_wf(w1.data.data(), c->nm, c->P, cols, nmp));
-    upload(c->pre_b1, need(wm, P + "decoder/decoder_prenet/dense_1/bias", {c->P}));
+    const auto& b1 = need(wm, P + "decoder/decoder_prenet/dense_1/bias", {c->P});
+    std::vector<float> w1p((size_t)c->nm * c->P), b1p(c->P);
+    for (int p = 0; p < c->P; ++p) {
+      const int j = af_group_col(p);
+      b1p[p] = b1.data[j];
+      for (int n = 0; n < c->nm; ++n) w1p[(size_t)n * c->P + p] = w1.data[(size_t)n * c->P + j];
+    }
+    upload(c->pre_w1r, w1p);
+    upload(c->pre_b1, b1p);
     const auto& w2 = need(wm, P + "decoder/decoder_prenet/dense_2/kernel", {c->P, c->P});
     upload(c->pre_w2, pack_wf(w2.data.data(), c->P, c->P, cols, c->P));
     upload(c->pre_b2, need(wm, P + "decoder/decoder_prenet/dense_2/bias", {c->P}));
   }
   for (int l = 0; l < 2; ++l) {
+    // layer 1 rows: [prenet P | context_enc E2 | context_style SW | h H]; layer 2 rows: [h1_new H | h H]
     const std::string s = P + "decoder/decoder_LSTM/multi_rnn_cell/cell_" + std::to_string(l) + "/lstm_cell/";
-    const int K = l == 0 ? c->K1 : c->K2, H = c->H;
-    const auto& k = need(wm, s + "kernel", {K, 4 * H});
-    const auto& b = need(wm, s + "bias", {4 * H});
+    const int H = c->H, N = 4 * H;
+    const int Kfull = l == 0 ? c->P + c->Dm + H : 2 * H;
+    const int Kc = l == 0 ? c->K1 : H;   // critical rows
+    const int Kh0 = l == 0 ? c->P + c->Dm : H;  // first recurrent row
+    const auto& k = need(wm, s + "kernel", {Kfull, N});
+    const auto& b = need(wm, s + "bias", {N});
     auto cols = lstm_cols(H);
     std::vector<float> bt(cols.size());
     for (size_t i = 0; i < cols.size(); ++i) bt[i] = b.data[cols[i]];
-    upload(l == 0 ? c->l1_w : c->l2_w, pack_wf(k.data.data(), K, 4 * H, cols, K));
+    upload(l == 0 ? c->l1_w : c->l2_w, pack_wf(k.data.data(), Kc, N, cols, Kc));
+    upload(l == 0 ? c->l1_wh : c->l2_wh, pack_wf(k.data.data() + (size_t)Kh0 * N, H, N, cols, H));
     upload(l == 0 ? c->l1_b : c->l2_b, bt);
+    if (l == 0) {  // style rows, lstm column order, row-major [SW][4H] (B operand of the GS GEMM)
+      std::vector<float> ws((size_t)c->SW * N);
+      for (int r = 0; r < c->SW; ++r)
+        for (int i = 0; i < N; ++i) ws[(size_t)r * N + i] = k.data[(size_t)(c->P + c->E2 + r) * N + cols[i]];
+      upload(c->l1_ws, ws);
+    }
   }
   {
     std::vector<int> cols;
@@ -1013,23 +1166,44 @@ static void finalize(tt2_ctx* c) {
   {
     const std::string fp = P + "decoder/linear_transform_projection/projection_linear_transform_projection/";
     const std::string sp = P + "decoder/stop_token_projection/projection_stop_token_projection/";
-    const auto& fk = need(wm, fp + "kernel", {c->Kp, c->nm});
+    const auto& fk = need(wm, fp + "kernel", {c->H + c->Dm, c->nm});
     const auto& fb = need(wm, fp + "bias", {c->nm});
-    const auto& sk = need(wm, sp + "kernel", {c->Kp, 1});
+    const auto& sk = need(wm, sp + "kernel", {c->H + c->Dm, 1});
     const auto& sb = need(wm, sp + "bias", {1});
-    const int N = c->nm + 1;
-    std::vector<float> W((size_t)c->Kp * N);
-    for (int k = 0; k < c->Kp; ++k) {
-      for (int n = 0; n < c->nm; ++n) W[(size_t)k * N + n] = fk.data[(size_t)k * c->nm + n];
-      W[(size_t)k * N + c->nm] = sk.data[k];
+    // columns [0, NPJ): frame (nm) | stop | 0-pad; [NPJ, NPF): prenet layer 1 folded through the
+    // frame projection, W_f·W1 (free-running decoding feeds the frame back: helpers.py:57)
+    const int N = c->nm + 1, Kfull = c->H + c->Dm, NPF = c->NPF, Pn = c->P;
+    const auto& w1 = need(wm, P + "decoder/decoder_prenet/dense_1/kernel", {c->nm, Pn});
+    const auto& b1 = need(wm, P + "decoder/decoder_prenet/dense_1/bias", {Pn});
+    std::vector<float> W((size_t)Kfull * NPF, 0.f);
+    for (int k = 0; k < Kfull; ++k) {
+      for (int n = 0; n < c->nm; ++n) W[(size_t)k * NPF + n] = fk.data[(size_t)k * c->nm + n];
+      W[(size_t)k * NPF + c->nm] = sk.data[k];
+      for (int p = 0; p < Pn; ++p) {
+        const int j = af_group_col(p);
+        double acc = 0.0;
+        for (int n = 0; n < c->nm; ++n) acc += (double)fk.data[(size_t)k * c->nm + n] * w1.data[(size_t)n * Pn + j];
+        W[(size_t)k * NPF + c->NPJ + p] = (float)acc;
+      }
     }
     std::vector<int> cols;
-    for (int j = 0; j < c->NPJ; ++j) cols.push_back(j < N ? j : -1);
-    upload(c->proj_w, pack_wf(W.data(), c->Kp, N, cols, c->Kp));
-    std::vector<float> pb(c->NPJ, 0.f);
+    for (int j = 0; j < NPF; ++j) cols.push_back(j);
+    upload(c->proj_w, pack_wf(W.data(), c->Kp, NPF, cols, c->Kp));  // rows [h2 | context_enc]
+    std::vector<float> ws((size_t)c->SW * NPF, 0.f);                // context_style rows
+    for (int r = 0; r < c->SW; ++r)
+      for (int n = 0; n < NPF; ++n) ws[(size_t)r * NPF + n] = W[(size_t)(c->Kp + r) * NPF + n];
+    upload(c->proj_ws, ws);
+    std::vector<float> pb(NPF, 0.f);
     for (int n = 0; n < c->nm; ++n) pb[n] = fb.data[n];
     pb[c->nm] = sb.data[0];
+    for (int p = 0; p < Pn; ++p) {  // b_f·W1 + b1
+      const int j = af_group_col(p);
+      double acc = 0.0;
+      for (int n = 0; n < c->nm; ++n) acc += (double)fb.data[n] * w1.data[(size_t)n * Pn + j];
+      pb[c->NPJ + p] = (float)(acc + b1.data[j]);
+    }
     upload(c->proj_b, pb);
+    (void)N;
   }
   cin = c->nm;
   for (int i = 1; i <= cfg.postnet_num_layers; ++i) {
@@ -1075,17 +1249,25 @@ static void alloc_acts(tt2_ctx* c) {
   c->keys.alloc(B * T * c->A * 4);
   for (int p = 0; p < 2; ++p) {
     c->X1[p].alloc(32L * c->K1 * 4);
-    c->X2[p].alloc(32L * c->K2 * 4);
+    c->H0s[p].alloc(32L * c->H * 4);
+    c->H1s[p].alloc(32L * c->H * 4);
   }
+  c->X2.alloc(32L * c->H * 4);
   c->Xp.alloc(32L * c->Kp * 4);
+  c->RG0.alloc(32L * 4 * c->H * 4);
+  c->RG1.alloc(32L * 4 * c->H * 4);
+  c->GS0.alloc(32L * 4 * c->H * 4);
+  c->PS.alloc(32L * c->NPF * 4);
+  c->ssum.alloc(32 * 4);
+  TT2_HIP(hipMemset(c->GS0.p, 0, c->GS0.bytes));  // rows >= B stay zero
+  TT2_HIP(hipMemset(c->PS.p, 0, c->PS.bytes));
   c->c1.alloc(32L * c->H * 4);
   c->c2.alloc(32L * c->H * 4);
   c->Qp.alloc((long)c->KSQ * 32 * c->A * 4);
   c->energy.alloc(B * T * 4);
   c->cum.alloc(B * T * 4);
   c->max_att.alloc(64 * 4);
-  c->PP.alloc((long)c->KSP * 32 * c->NPJ * 4);
-  c->gmasks.alloc((size_t)MI * 2 * B * c->P);
+  c->PP.alloc((long)c->KSP * 32 * c->NPF * 4);
   c->ctl.alloc(sizeof(DecCtl));
   c->frames.alloc(B * MI * c->nm * 4);
   c->stop.alloc(B * MI * 4);
@@ -1195,6 +1377,16 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.Bw = c->mem_k.as<float>(); g.ldb = c->A; g.Cout = c->keys.as<float>(); g.ldc = c->A;
     gemm(g, s);
   }
+  {  // per-utterance style terms of the decoder: GS = style·W_lstm1[style rows], PS = style·W_proj[style rows]
+    GemmArgs g;
+    g.M = B; g.N = 4 * c->H; g.K = c->SW; g.A = c->style.as<float>(); g.lda = c->SW;
+    g.Bw = c->l1_ws.as<float>(); g.ldb = 4 * c->H; g.Cout = c->GS0.as<float>(); g.ldc = 4 * c->H;
+    gemm(g, s);
+    GemmArgs p;
+    p.M = B; p.N = c->NPF; p.K = c->SW; p.A = c->style.as<float>(); p.lda = c->SW;
+    p.Bw = c->proj_ws.as<float>(); p.ldb = c->NPF; p.Cout = c->PS.as<float>(); p.ldc = c->NPF;
+    gemm(p, s);
+  }
   c->B = B;
   c->T_in = T;
   c->encoded = true;
@@ -1202,57 +1394,129 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
 }
 
 // ---------------------------------------------------------------- decode
+static long long* g_stamps_dev = nullptr;  // diagnostic s_memtime stamps (profiling only)
+
 static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64_t seed,
                              const float* targets_d, int T_lim, float* frames_d, float* stop_d, float* align_d) {
   const auto& cfg = c->cfg;
   DecArgs a;
   a.ctl = c->ctl.as<DecCtl>();
   a.B = c->B; a.T_in = c->T_in; a.max_iters = max_iters; a.T_lim = targets_d ? T_lim : 0;
-  a.nm = c->nm; a.P = c->P; a.H = c->H; a.Dm = c->Dm; a.A = c->A; a.F = c->F; a.KL = c->KL;
-  a.K1 = c->K1; a.K2 = c->K2; a.Kp = c->Kp;
+  a.nm = c->nm; a.P = c->P; a.H = c->H; a.Dm = c->Dm; a.E2 = c->E2; a.A = c->A; a.F = c->F; a.KL = c->KL;
+  a.K1 = c->K1; a.Kp = c->Kp;
   a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
   a.stop_at_any = cfg.stop_at_any; a.mask_encoder = cfg.mask_encoder; a.cumulative = cfg.cumulative_weights;
   a.constraint = cfg.synthesis_constraint; a.monotonic = cfg.constraint_monotonic; a.win = cfg.attention_win_size;
-  a.pre_w1 = c->pre_w1.as<float>(); a.pre_b1 = c->pre_b1.as<float>();
+  a.pre_b1 = c->pre_b1.as<float>();
   a.pre_w2 = c->pre_w2.as<float>(); a.pre_b2 = c->pre_b2.as<float>();
-  a.l1_w = c->l1_w.as<float>(); a.l1_b = c->l1_b.as<float>(); a.l2_w = c->l2_w.as<float>(); a.l2_b = c->l2_b.as<float>();
   a.KLp = c->KLp; a.Fp = c->Fp;
   a.q_w = c->q_w.as<float>(); a.loc_cw = c->loc_cw.as<float>(); a.loc_cb = c->loc_cb.as<float>();
   a.loc_w = c->loc_w.as<float>(); a.va = c->va.as<float>(); a.ba = c->ba.as<float>();
-  a.proj_w = c->proj_w.as<float>(); a.proj_b = c->proj_b.as<float>();
+  a.proj_w = c->proj_w.as<float>(); a.proj_b = c->proj_b.as<float>(); a.PS = c->PS.as<float>();
   a.keys = c->keys.as<float>(); a.values = c->values.as<float>(); a.lengths = c->lens.as<int>();
-  for (int p = 0; p < 2; ++p) { a.X1[p] = c->X1[p].as<float>(); a.X2[p] = c->X2[p].as<float>(); }
-  a.Xp = c->Xp.as<float>(); a.c1 = c->c1.as<float>(); a.c2 = c->c2.as<float>();
+  for (int p = 0; p < 2; ++p) a.X1[p] = c->X1[p].as<float>();
+  a.Xp = c->Xp.as<float>(); a.ssum = c->ssum.as<float>();
   a.Qp = c->Qp.as<float>(); a.energy = c->energy.as<float>(); a.cum = c->cum.as<float>();
   a.max_att = c->max_att.as<int>(); a.PP = c->PP.as<float>();
-  a.KSQ = c->KSQ; a.KSP = c->KSP; a.NPJ = c->NPJ;
+  a.KSQ = c->KSQ; a.KSP = c->KSP; a.NPJ = c->NPJ; a.NPF = c->NPF;
+  a.TP1 = targets_d ? c->TP1.as<float>() : nullptr;
   a.masks = masks_d; a.seed = seed; a.targets = targets_d; a.stamps = nullptr;
+  a.stamp_step = -1;
+  if (const char* st = getenv("TT2_STAMP_STEP")) {  // diagnostic: prenet stamps of one decode step
+    if (!g_stamps_dev) TT2_HIP(hipMalloc(&g_stamps_dev, 64 * sizeof(long long)));
+    a.stamps = g_stamps_dev;
+    a.stamp_step = atoi(st);
+  }
   a.frames = frames_d; a.stop = stop_d; a.align = align_d;
   return a;
 }
 
-static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, int t, hipStream_t s) {
-  const int par = i & 1;
-  hipLaunchKernelGGL(k_prenet, dim3(c->P / 16), dim3(256), 0, s, a, i, t);
-  LstmArgs l1;
-  l1.ctl = a.ctl; l1.X = a.X1[par]; l1.K = c->K1; l1.hprev_off = c->P + c->Dm; l1.W = a.l1_w; l1.b = a.l1_b;
-  l1.c = a.c1; l1.H = c->H; l1.Xo = a.X2[par]; l1.ho_off = 0; l1.Xz = a.X1[par ^ 1]; l1.hz_off = c->P + c->Dm;
-  l1.zo = a.zo; l1.one_m_zo = a.one_m_zo;
-  launch_lstm(l1, c->H, s);
-  LstmArgs l2 = l1;
-  l2.X = a.X2[par]; l2.K = c->K2; l2.hprev_off = c->H; l2.W = a.l2_w; l2.b = a.l2_b; l2.c = a.c2;
-  l2.Xo = a.Xp; l2.ho_off = 0; l2.Xz = a.X2[par ^ 1]; l2.hz_off = c->H;
-  launch_lstm(l2, c->H, s);
+// The per-step launches (shared by the captured decode graph and the profiler).  `par` = step
+// parity selecting the ping-pong state buffers.
+static void launch_prenet(tt2_ctx* c, const DecArgs& a, int i, int t, hipStream_t s) {
+  hipLaunchKernelGGL(k_prenet, dim3(c->P / 16), dim3(PRE_T), 0, s, a, i, t);
+}
+static LstmArgs lstm_args(tt2_ctx* c, const DecArgs& a, int layer, int par) {
+  LstmArgs l;
+  l.stamps = a.stamps;
+  l.ctl = a.ctl; l.H = c->H; l.zo = a.zo; l.one_m_zo = a.one_m_zo; l.ho_off = 0;
+  if (layer == 0) {
+    l.X = a.X1[par]; l.K = c->K1; l.W = c->l1_w.as<float>(); l.b = c->l1_b.as<float>();
+    l.RG = c->RG0.as<float>(); l.GS = c->GS0.as<float>(); l.ssum = c->ssum.as<float>();
+    l.Hprev = c->H0s[par].as<float>(); l.Hz = c->H0s[par ^ 1].as<float>(); l.c = c->c1.as<float>();
+    l.Xo = c->X2.as<float>();
+  } else {
+    l.X = c->X2.as<float>(); l.K = c->H; l.W = c->l2_w.as<float>(); l.b = c->l2_b.as<float>();
+    l.RG = c->RG1.as<float>(); l.GS = nullptr; l.ssum = nullptr;
+    l.Hprev = c->H1s[par].as<float>(); l.Hz = c->H1s[par ^ 1].as<float>(); l.c = c->c2.as<float>();
+    l.Xo = c->Xp.as<float>();
+  }
+  return l;
+}
+static void launch_query(tt2_ctx* c, const DecArgs& a, const SideJob& sj, hipStream_t s) {
   PartArgs q;
   q.ctl = a.ctl; q.X = a.Xp; q.K = c->H; q.W = a.q_w; q.out = a.Qp; q.ldo = c->A; q.ntile = c->A / 16; q.KS = c->KSQ;
-  launch_partial(q, s);
-  hipLaunchKernelGGL(k_energy, dim3(a.B, cdiv(a.T_in, 32)), dim3(256), 0, s, a);
-  const size_t shm_s = sizeof(float) * (((a.T_in + 3) & ~3) + 4 * 16 * 16);
-  hipLaunchKernelGGL(k_softmax_ctx, dim3(a.B, cdiv(c->Dm, 64)), dim3(256), shm_s, s, a, i, t);
+  launch_partial(q, sj, s);
+}
+static void launch_proj(tt2_ctx* c, const DecArgs& a, const SideJob& sj, hipStream_t s) {
   PartArgs p;
-  p.ctl = a.ctl; p.X = a.Xp; p.K = c->Kp; p.W = a.proj_w; p.out = a.PP; p.ldo = c->NPJ; p.ntile = c->NPJ / 16;
+  // GTA feeds targets, not frames, to the prenet: the folded prenet-L1 columns are not needed
+  p.ctl = a.ctl; p.X = a.Xp; p.K = c->Kp; p.W = a.proj_w; p.out = a.PP; p.ldo = c->NPF;
+  p.ntile = (a.targets ? c->NPJ : c->NPF) / 16;
   p.KS = c->KSP;
-  launch_partial(p, s);
+  launch_partial(p, sj, s);
+}
+// recurrent gate terms of step i+1 from the zoned states written at step i
+static SideJob side_rec(tt2_ctx* c, int layer, int par) {
+  SideJob j;
+  j.X = (layer == 0 ? c->H0s[par ^ 1] : c->H1s[par ^ 1]).as<float>();
+  j.W = (layer == 0 ? c->l1_wh : c->l2_wh).as<float>();
+  j.out = (layer == 0 ? c->RG0 : c->RG1).as<float>();
+  j.K = c->H;
+  j.ntile = 4 * c->H / 16;
+  return j;
+}
+static void launch_energy(tt2_ctx* c, const DecArgs& a, const SideJob& sj, hipStream_t s) {
+  const int nE = a.B * cdiv(a.T_in, 32);
+  hipLaunchKernelGGL(k_energy, dim3(nE + sj.ntile), dim3(256), 0, s, a, sj);
+}
+static void launch_softmax(tt2_ctx* c, const DecArgs& a, int i, int t, const SideJob& sj, hipStream_t s) {
+  const size_t shm = sizeof(float) * std::max<size_t>(((a.T_in + 3) & ~3) + 4 * 16 * 16, 2048 + 512);
+  hipLaunchKernelGGL(k_softmax_ctx, dim3(a.B * (c->E2 / 64) + sj.ntile), dim3(256), shm, s, a, i, t, sj);
+}
+
+static void launch_side(tt2_ctx* c, const DecArgs& a, const SideJob& sj, hipStream_t s) {
+  hipLaunchKernelGGL(k_side, dim3(sj.ntile), dim3(256), 0, s, a.ctl, sj);
+}
+
+// side_mode 0: recurrent terms as extra blocks of the energy / softmax launches;
+// side_mode 1: as launches on a second captured stream (parallel graph branches);
+// side_mode 2: as extra blocks of the query / projection launches
+static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, int t, hipStream_t s, hipStream_t s2) {
+  const int par = i & 1;
+  SideJob none = side_rec(c, 0, par);
+  none.ntile = 0;
+  launch_prenet(c, a, i, t, s);
+  if (c->side_mode == 1 && i > 0) TT2_HIP(hipStreamWaitEvent(s, c->sev[2 * ((i - 1) & 1)], 0));
+  launch_lstm(lstm_args(c, a, 0, par), c->H, s);
+  if (c->side_mode == 1) {  // RG0 for step i+1 from h0(i)
+    TT2_HIP(hipEventRecord(c->sev[4], s));
+    TT2_HIP(hipStreamWaitEvent(s2, c->sev[4], 0));
+    launch_side(c, a, side_rec(c, 0, par), s2);
+    TT2_HIP(hipEventRecord(c->sev[2 * (i & 1)], s2));
+  }
+  if (c->side_mode == 1 && i > 0) TT2_HIP(hipStreamWaitEvent(s, c->sev[2 * ((i - 1) & 1) + 1], 0));
+  launch_lstm(lstm_args(c, a, 1, par), c->H, s);
+  if (c->side_mode == 1) {  // RG1 for step i+1 from h1(i)
+    TT2_HIP(hipEventRecord(c->sev[5], s));
+    TT2_HIP(hipStreamWaitEvent(s2, c->sev[5], 0));
+    launch_side(c, a, side_rec(c, 1, par), s2);
+    TT2_HIP(hipEventRecord(c->sev[2 * (i & 1) + 1], s2));
+  }
+  launch_query(c, a, c->side_mode == 2 ? side_rec(c, 1, par) : none, s);
+  launch_energy(c, a, c->side_mode == 0 ? side_rec(c, 1, par) : none, s);
+  launch_softmax(c, a, i, t, c->side_mode == 0 ? side_rec(c, 0, par) : none, s);
+  launch_proj(c, a, c->side_mode == 2 ? side_rec(c, 0, par) : none, s);
 }
 
 static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64_t seed, const float* targets_d,
@@ -1263,9 +1527,14 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
   // zero decoder state (zero_state, Architecture_wrappers.py:158-195; _go_frames helpers.py:136)
   for (int p = 0; p < 2; ++p) {
     TT2_HIP(hipMemsetAsync(c->X1[p].p, 0, c->X1[p].bytes, s));
-    TT2_HIP(hipMemsetAsync(c->X2[p].p, 0, c->X2[p].bytes, s));
+    TT2_HIP(hipMemsetAsync(c->H0s[p].p, 0, c->H0s[p].bytes, s));
+    TT2_HIP(hipMemsetAsync(c->H1s[p].p, 0, c->H1s[p].bytes, s));
   }
+  TT2_HIP(hipMemsetAsync(c->X2.p, 0, c->X2.bytes, s));
   TT2_HIP(hipMemsetAsync(c->Xp.p, 0, c->Xp.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->RG0.p, 0, c->RG0.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->RG1.p, 0, c->RG1.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->ssum.p, 0, c->ssum.bytes, s));
   TT2_HIP(hipMemsetAsync(c->c1.p, 0, c->c1.bytes, s));
   TT2_HIP(hipMemsetAsync(c->c2.p, 0, c->c2.bytes, s));
   TT2_HIP(hipMemsetAsync(c->cum.p, 0, c->cum.bytes, s));
@@ -1273,10 +1542,19 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
   TT2_HIP(hipMemsetAsync(c->ctl.p, 0, sizeof(DecCtl), s));
   if (!masks_d) {  // prenet dropout keep bits from the counter-based device RNG
     const long n = (long)max_iters * 2 * c->B * c->P;
+    c->gmasks.alloc((size_t)n);
     hipLaunchKernelGGL(k_gen_masks, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, s,
                        c->gmasks.as<uint8_t>(), n, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x9e3779b9u);
     TT2_HIP(hipGetLastError());
     masks_d = c->gmasks.as<uint8_t>();
+  }
+  if (targets_d) {  // GTA: prenet layer-1 pre-activations of every teacher frame, TP1 = targets·W1 + b1
+    c->TP1.alloc(sizeof(float) * (size_t)c->B * T_lim * c->P);
+    GemmArgs g;
+    g.M = c->B * T_lim; g.N = c->P; g.K = c->nm; g.A = targets_d; g.lda = c->nm;
+    g.Bw = c->pre_w1r.as<float>(); g.ldb = c->P; g.Cout = c->TP1.as<float>(); g.ldc = c->P;
+    g.bias = c->pre_b1.as<float>();
+    gemm(g, s);
   }
   const DecArgs a = make_dec_args(c, max_iters, masks_d, seed, targets_d, T_lim, frames_d, stop_d, align_d);
   c->last_args = a;
@@ -1294,15 +1572,25 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
   auto chunk_graph = [&](int ch) -> hipGraphExec_t {
     if ((int)c->graph.chunks.size() <= ch) c->graph.chunks.resize(ch + 1, nullptr);
     if (!c->graph.chunks[ch]) {
-      hipStream_t cs;
+      hipStream_t cs, cs2;
       TT2_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+      TT2_HIP(hipStreamCreateWithFlags(&cs2, hipStreamNonBlocking));
       hipGraph_t gr;
       TT2_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-      for (int i = 0; i < tt2_ctx::S; ++i) enqueue_step(c, a, i, ch * tt2_ctx::S + i, cs);
+      if (c->side_mode == 1) {  // fork the side stream into the capture
+        TT2_HIP(hipEventRecord(c->sev[6], cs));
+        TT2_HIP(hipStreamWaitEvent(cs2, c->sev[6], 0));
+      }
+      for (int i = 0; i < tt2_ctx::S; ++i) enqueue_step(c, a, i, ch * tt2_ctx::S + i, cs, cs2);
+      if (c->side_mode == 1) {  // join: the chunk's last side jobs before the next chunk
+        TT2_HIP(hipEventRecord(c->sev[7], cs2));
+        TT2_HIP(hipStreamWaitEvent(cs, c->sev[7], 0));
+      }
       TT2_HIP(hipStreamEndCapture(cs, &gr));
       TT2_HIP(hipGraphInstantiate(&c->graph.chunks[ch], gr, nullptr, nullptr, 0));
       TT2_HIP(hipGraphDestroy(gr));
       TT2_HIP(hipStreamDestroy(cs));
+      TT2_HIP(hipStreamDestroy(cs2));
     }
     return c->graph.chunks[ch];
   };
@@ -1420,10 +1708,15 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     c->Dm = 2 * c->U + c->SW;
     TT2_CHECK(c->Dm % 64 == 0, TT2_ERR_INVALID_ARG, "memory width must be a multiple of 64");
     TT2_CHECK(cfg->use_gst, TT2_ERR_INVALID_ARG, "use_gst=False (paper Tacotron-2 memory) is not built yet");
-    c->K1 = c->P + c->Dm + c->H; c->K2 = 2 * c->H; c->Kp = c->H + c->Dm;
+    c->E2 = 2 * c->U;
+    c->K1 = c->P + c->E2; c->Kp = c->H + c->E2;
+    TT2_CHECK(c->E2 % 64 == 0, TT2_ERR_INVALID_ARG, "2*encoder_lstm_units must be a multiple of 64");
     c->NPJ = ((c->nm + 1 + 15) / 16) * 16;
+    c->NPF = c->NPJ + c->P;
     alloc_acts(c.get());
     for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
+    for (auto& e : c->sev) TT2_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (const char* m = getenv("TT2_SIDE_MODE")) c->side_mode = atoi(m);
     *out = c.release();
   });
 }
@@ -1435,6 +1728,8 @@ void tt2_destroy(tt2_ctx* c) {
     if (g) (void)hipGraphExecDestroy(g);
   if (c->ctl_host) (void)hipHostFree(c->ctl_host);
   for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->sev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;  // DevBuf destructors release the device buffers
@@ -1589,7 +1884,7 @@ tt2_status tt2_last_timings(tt2_ctx* c, float* ms3) {
   });
 }
 
-static long long* g_stamps_dev = nullptr;
+#define TT2_NPROF 10
 
 tt2_status tt2_profile_decoder_kernels(tt2_ctx* c, int iters, float* avg_us) {
   return guard([&] {
@@ -1608,40 +1903,27 @@ tt2_status tt2_profile_decoder_kernels(tt2_ctx* c, int iters, float* avg_us) {
     hipEvent_t e0, e1;
     TT2_HIP(hipEventCreate(&e0));
     TT2_HIP(hipEventCreate(&e1));
-    LstmArgs l1;
-    l1.stamps = a.stamps;
-    l1.ctl = a.ctl; l1.K = c->K1; l1.hprev_off = c->P + c->Dm; l1.W = a.l1_w; l1.b = a.l1_b; l1.c = a.c1;
-    l1.H = c->H; l1.ho_off = 0; l1.hz_off = c->P + c->Dm; l1.zo = a.zo; l1.one_m_zo = a.one_m_zo;
-    LstmArgs l2 = l1;
-    l2.K = c->K2; l2.hprev_off = c->H; l2.W = a.l2_w; l2.b = a.l2_b; l2.c = a.c2; l2.ho_off = 0; l2.hz_off = c->H;
-    PartArgs q;
-    q.ctl = a.ctl; q.X = a.Xp; q.K = c->H; q.W = a.q_w; q.out = a.Qp; q.ldo = c->A; q.ntile = c->A / 16; q.KS = c->KSQ;
-    PartArgs p;
-    p.ctl = a.ctl; p.X = a.Xp; p.K = c->Kp; p.W = a.proj_w; p.out = a.PP; p.ldo = c->NPJ; p.ntile = c->NPJ / 16;
-    p.KS = c->KSP;
-    const size_t shm_s = sizeof(float) * (((a.T_in + 3) & ~3) + 4 * 16 * 16);
-    for (int k = 0; k < 7; ++k) {
+    DecArgs a0 = a;
+    a0.B = 0;  // energy launch with only its side-job blocks
+    SideJob none = side_rec(c, 1, 0);
+    none.ntile = 0;
+    for (int k = 0; k < TT2_NPROF; ++k) {
       // `iters` back-to-back launches between one event pair: per-launch time = device
       // duration + the inter-kernel gap (comparable with rocprofv3 kernel-trace averages)
       TT2_HIP(hipEventRecord(e0, s));
       for (int i = 0; i < iters; ++i) {
         const int par = i & 1;
         switch (k) {
-          case 0: hipLaunchKernelGGL(k_prenet, dim3(c->P / 16), dim3(256), 0, s, a, 0, 0); break;
-          case 1: {
-            LstmArgs l = par ? l2 : l1;
-            l.X = par ? a.X2[0] : a.X1[0]; l.Xo = par ? a.Xp : a.X2[0]; l.Xz = par ? a.X2[1] : a.X1[1];
-            launch_lstm(l, c->H, s);
-          } break;
-          case 2: launch_partial(q, s); break;
-          case 3: hipLaunchKernelGGL(k_energy, dim3(a.B, cdiv(a.T_in, 32)), dim3(256), 0, s, a); break;
-          case 4: hipLaunchKernelGGL(k_softmax_ctx, dim3(a.B, cdiv(c->Dm, 64)), dim3(256), shm_s, s, a, 0, 0); break;
-          case 5: launch_partial(p, s); break;
-          case 6: {
-            LstmArgs l = l2;
-            l.X = a.X2[0]; l.Xo = a.Xp; l.Xz = a.X2[1];
-            launch_lstm(l, c->H, s);
-          } break;
+          case 0: launch_prenet(c, a, 0, 0, s); break;
+          case 1: launch_lstm(lstm_args(c, a, par, 0), c->H, s); break;  // layers 1/2 alternating
+          case 2: launch_query(c, a, none, s); break;
+          case 3: launch_energy(c, a, side_rec(c, 1, 0), s); break;
+          case 4: launch_softmax(c, a, 0, 0, side_rec(c, 0, 0), s); break;
+          case 5: launch_proj(c, a, none, s); break;
+          case 6: launch_lstm(lstm_args(c, a, 1, 0), c->H, s); break;
+          case 7: launch_energy(c, a0, side_rec(c, 1, 0), s); break;   // side job alone
+          case 8: launch_energy(c, a, none, s); break;                 // energy alone
+          case 9: launch_softmax(c, a, 0, 0, none, s); break;          // softmax alone
         }
       }
       TT2_HIP(hipEventRecord(e1, s));
@@ -1660,6 +1942,10 @@ tt2_status tt2_profile_decoder_kernels(tt2_ctx* c, int iters, float* avg_us) {
 tt2_status tt2_debug_stamps(tt2_ctx* c, long long* out64) {
   return guard([&] {
     TT2_CHECK(c && out64, TT2_ERR_INVALID_ARG, "null argument");
+    if (g_stamps_dev) {
+      TT2_HIP(hipDeviceSynchronize());
+      TT2_HIP(hipMemcpy(c->stamps_host, g_stamps_dev, 64 * sizeof(long long), hipMemcpyDeviceToHost));
+    }
     for (int i = 0; i < 64; ++i) out64[i] = c->stamps_host[i];
   });
 }
