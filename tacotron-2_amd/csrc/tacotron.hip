@@ -293,6 +293,7 @@ struct SideJob {
   const float* W;   // WF tiles [ntile][K x 16]
   float* out;       // [ntile][32][16]
   int K, ntile;
+  int delay;        // s_sleep(64) repetitions before the side blocks start (~1.7 us each)
 };
 
 struct DecArgs {
@@ -309,6 +310,7 @@ struct DecArgs {
   const float* va; const float* ba; const float* proj_w; const float* proj_b;
   const float* PS;      // [32][NPF] style·W_proj_style (per utterance), incl. the folded prenet-L1 columns
   const float* TP1;     // [B][T_lim][P] targets·W1 + b1 (GTA) or null
+  const float* pre1;    // [32][P] prenet-L1 pre-activations of the last projection (AF-group order)
   // attention memory
   const float* keys;    // [B][T_in][A]
   const float* values;  // [B][T_in][Dm] (only the first E2 channels are read per step)
@@ -366,6 +368,8 @@ __device__ __forceinline__ void side_tile(const SideJob& j, int tile, float* red
   for (int e = tid; e < 512; e += 256) j.out[(long)tile * 512 + e] = G[e];
 }
 __device__ __forceinline__ void side_job(const SideJob& j, int blk, float* red, float* G, int tid) {
+  // let the host launch's own (latency-critical) loads reach the memory system first
+  if (j.delay > 0) for (int i = 0; i < j.delay; ++i) __builtin_amdgcn_s_sleep(64);
   if (j.K == 1024) side_tile<16>(j, blk, red, G, tid);
   else side_tile<0>(j, blk, red, G, tid);
 }
@@ -378,15 +382,19 @@ __global__ __launch_bounds__(256) void k_side(const DecCtl* ctl, SideJob sj) {
   side_job(sj, blockIdx.x, red, G, threadIdx.x);
 }
 
-// Prenet (modules.py:346-357) of step t, preceded by the TacoTestHelper/dynamic_decode
-// bookkeeping of step t-1 (helpers.py:36-59): reduce the frame/stop projection partials (+ style
-// term), write frames/stop[t-1], decide `finished`.  Layer 1 is never recomputed here: its
-// pre-activation frame_in·W1 + b1 arrives ready — free running, frame·W1 = [h2|ctx]·(W_f·W1) +
-// b_f·W1 is folded into the projection launch (its columns NPJ.. of the partials); with GTA
-// targets it was computed for all steps at decode start (TP1); at t = 0 (GO frame) it is b1.
+// Prenet (modules.py:346-357) of step t.  Layer 1 is never recomputed here: its pre-activation
+// frame_in·W1 + b1 arrives ready — free running, frame·W1 = [h2|ctx]·(W_f·W1) + b_f·W1 was folded
+// into the previous step's projection launch, which also reduced it (pre1); with GTA targets it
+// was computed for all steps at decode start (TP1); at t = 0 (GO frame) it is b1.  Frames, stop
+// tokens and the stop decision of step t-1 were written by that projection launch too.
 // Grid: P/16 blocks (layer-2 column tiles) of 16 waves.
 constexpr int PRE_T = 1024;
 __global__ __launch_bounds__(PRE_T) void k_prenet(DecArgs a, int istep, int t) {
+  __shared__ __attribute__((aligned(16))) float h1[32 * 256];   // AF [32][P<=256]
+  __shared__ float red[16 * 512];
+  __shared__ float G[512];
+  __shared__ __attribute__((aligned(16))) uint8_t mk1[32 * 256];
+  __shared__ uint8_t mk2[32 * 16];
   // (never assign to a field of `a`: a modified by-value kernel argument is copied to scratch)
   long long* const stp = (a.stamp_step < 0 || t == a.stamp_step) ? a.stamps : nullptr;
 #undef STAMP
@@ -394,62 +402,23 @@ __global__ __launch_bounds__(PRE_T) void k_prenet(DecArgs a, int istep, int t) {
   do {                                                                                   \
     if (stp && blockIdx.x == 0 && threadIdx.x == 0) stp[i] = __builtin_amdgcn_s_memtime(); \
   } while (0)
-  __shared__ __attribute__((aligned(16))) float h1[32 * 256];   // AF [32][P<=256]
-  __shared__ float red[16 * 512];
-  __shared__ float G[512];
-  __shared__ float stopv[32];
-  __shared__ __attribute__((aligned(16))) uint8_t mk1[32 * 256];
-  __shared__ uint8_t mk2[32 * 16];
-  __shared__ int s_done;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   STAMP(0);
   const int done0 = a.ctl->done;
-  const int nm = a.nm, P = a.P, tile = blockIdx.x, NPF = a.NPF;
-  // ---- issue loads: frame/stop partials (row pm, 3 columns), layer-1 pre-activation sources
-  //      (row pm, 8 columns), style sums, keep masks, this block's layer-2 weights ----
-  const int pm = tid >> 5, pq = tid & 31;  // 32 rows x 32 lanes
-  // every load below is unconditional (clamped index, value selected later) so that all of them
-  // are in flight together; a conditional load becomes a branch that waits for it
-  float pp[KSP_C][3], pps[3], ppb[3];
-  const float ssum_m = a.ssum[pm];  // frame/stop phase row
-  const float* PPr = a.PP + (long)pm * NPF;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int n = min(pq * 3 + j, a.NPJ - 1);
-#pragma unroll
-    for (int ks = 0; ks < KSP_C; ++ks) pp[ks][j] = PPr[(long)ks * 32 * NPF + n];
-    pps[j] = a.PS[(long)pm * NPF + n];
-    ppb[j] = a.proj_b[n];
-  }
-  // next step's keep masks -> this XCD's L2 (the same block id runs next step's prenet on it);
-  // asm loads into a never-read register: the compiler neither drops nor waits for them
-  // (the destination register is kept live to the kernel's end so nothing reuses it while the
-  // untracked load is in flight)
-  unsigned pf_dummy = 0u;
-  if (t + 1 < a.max_iters && tid < 160) {
-    // layer-1 masks (all rows, one load per 64-byte line) and this tile's layer-2 mask rows
-    const long nrow = (long)(t + 1) * 2 * a.B * P;
-    const long bp = (long)a.B * P;
-    long off = -1;
-    if (tid < 128) off = (long)tid * 64 < bp ? (long)tid * 64 : -1;
-    else if (tid - 128 < a.B) off = bp + (long)(tid - 128) * P + tile * 16;
-    if (off >= 0) asm volatile("global_load_dword %0, %1, off" : "=v"(pf_dummy) : "v"(a.masks + nrow + off) : "memory");
-  }
-  // layer-1 pre-activations arrive in "AF-group" column order: position 4g + j holds column
-  const int G4 = P / 4, nit = (32 * G4 + PRE_T - 1) / PRE_T;  // nit <= 2
+  const int P = a.P, tile = blockIdx.x;
+  // ---- issue every load up front (unconditional, clamped indices: a conditional load becomes
+  //      a branch that waits for it).  Layer-1 pre-activations come in "AF-group" column order:
+  //      position 4g + j holds column 16(g/4) + g%4 + 4j, so one float4 is the AF float4 of
+  //      (row m, group g) in h1.  Items (m, g): lanes run over rows (conflict-free AF stores).
+  const int G4 = P / 4;
   const int mode1 = t == 0 ? 0 : (a.targets ? 1 : 2);  // GO frame / GTA teacher / folded projection
   const int im = tid & 31;
-  const float ssum_i = a.ssum[im];
-  f32x4 l1v[2], l1p[2][KSP_C], l1s[2];
+  f32x4 l1v[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int g = min((tid >> 5) + it * (PRE_T / 32), G4 - 1);
     if (mode1 == 2) {
-#pragma unroll
-      for (int ks = 0; ks < KSP_C; ++ks)
-        l1p[it][ks] = *reinterpret_cast<const f32x4*>(a.PP + ((long)ks * 32 + im) * NPF + a.NPJ + 4 * g);
-      l1s[it] = *reinterpret_cast<const f32x4*>(a.PS + (long)im * NPF + a.NPJ + 4 * g);
-      l1v[it] = *reinterpret_cast<const f32x4*>(a.proj_b + a.NPJ + 4 * g);
+      l1v[it] = *reinterpret_cast<const f32x4*>(a.pre1 + (long)im * P + 4 * g);
     } else if (mode1 == 1) {
       const int mm = min(im, a.B - 1), tt = min(t - 1, a.T_lim - 1);
       l1v[it] = *reinterpret_cast<const f32x4*>(a.TP1 + ((long)mm * a.T_lim + tt) * P + 4 * g);
@@ -462,8 +431,6 @@ __global__ __launch_bounds__(PRE_T) void k_prenet(DecArgs a, int istep, int t) {
   f32x4 w2 = {0.f, 0.f, 0.f, 0.f};
   if (wave < nsg2) w2 = W2v[((long)tile * nsg2 + wave) * 64 + lane];
   const long mrow = (long)t * 2 * a.B * P;
-  // keep masks into registers now, into LDS after the stop decision (loads complete in issue
-  // order: anything consumed earlier must not wait behind them)
   const bool has_mask = t < a.max_iters;
   const int nch = 32 * P / 16;  // 16-column chunks of layer-1 masks (<= PRE_T)
   uint4 mv = {0u, 0u, 0u, 0u};
@@ -478,44 +445,6 @@ __global__ __launch_bounds__(PRE_T) void k_prenet(DecArgs a, int istep, int t) {
   }
   if (done0) return;
   STAMP(1);
-  // ---- finish step t-1 ----
-  if (t > 0) {
-    for (int jj = 0; jj < 3; ++jj) {
-      const int n = pq * 3 + jj, m = pm;
-      if (n > nm) continue;
-      float s = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < KSP_C; ++ks) s += pp[ks][jj];
-      s = (s + ssum_m * pps[jj]) + ppb[jj];
-      if (n == nm) {
-        stopv[m] = sigm(s);
-      } else if (tile == 0 && m < a.B) {
-        a.frames[((long)m * a.max_iters + (t - 1)) * nm + n] = s;
-      }
-    }
-    __syncthreads();
-    STAMP(2);
-    if (wave == 0) {  // batch-level stop rule (helpers.py:40-48): one lane per row
-      const bool valid = lane < a.B;
-      const float sv = valid ? stopv[lane] : 0.f;
-      const bool f = valid && rintf(sv) == 1.0f;
-      const unsigned long long fb = __ballot(f), vb = __ballot(valid);
-      if (valid && tile == 0) a.stop[(long)lane * a.max_iters + (t - 1)] = sv;
-      int done = a.stop_at_any ? (fb != 0ull) : (fb == vb);
-      if (a.T_lim > 0) done = t >= a.T_lim;   // TacoTrainingHelper: time + 1 >= T_targets
-      if (t >= a.max_iters) done = 1;         // dynamic_decode maximum_iterations
-      if (lane == 0) {
-        s_done = done;
-        if (done && tile == 0) {
-          a.ctl->n_steps = t;
-          a.ctl->done = 1;
-        }
-      }
-    }
-    __syncthreads();
-    if (s_done) return;
-  }
-  STAMP(3);
   // ---- keep masks -> LDS: layer 1 in AF-group byte order (4x4 byte transpose of each chunk:
   //      byte 4kk + j <- column kk + 4j), layer 2 as loaded ----
   if (tid < nch) {
@@ -528,18 +457,13 @@ __global__ __launch_bounds__(PRE_T) void k_prenet(DecArgs a, int istep, int t) {
   }
   if (tid < 32 * 16) mk2[tid] = m2v;
   __syncthreads();
+  STAMP(2);
   // ---- layer 1: relu(pre-activation) * keep / 0.5 ----
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int g = (tid >> 5) + it * (PRE_T / 32);
-    if (it >= nit || g >= G4) break;
-    f32x4 x = l1v[it];
-    if (mode1 == 2) {
-      f32x4 sacc = l1p[it][0];
-#pragma unroll
-      for (int ks = 1; ks < KSP_C; ++ks) sacc += l1p[it][ks];
-      for (int e = 0; e < 4; ++e) x[e] = (sacc[e] + ssum_i * l1s[it][e]) + x[e];  // (Σ partials + style) + (b_f·W1 + b1)
-    }
+    if (g >= G4) break;
+    const f32x4 x = l1v[it];
     const unsigned mw = reinterpret_cast<const unsigned*>(mk1)[(im * P + 4 * g) >> 2];
     f32x4 hv;
     for (int e = 0; e < 4; ++e) hv[e] = (fmaxf(x[e], 0.f) / 0.5f) * (float)((mw >> (8 * e)) & 0xffu);
@@ -558,7 +482,6 @@ __global__ __launch_bounds__(PRE_T) void k_prenet(DecArgs a, int istep, int t) {
     X1[af_idx(m, n)] = v;
   }
   STAMP(5);
-  asm volatile("" ::"v"(pf_dummy));
 }
 #undef STAMP
 #define STAMP(i)                                                                         \
@@ -685,6 +608,99 @@ static void launch_partial(const PartArgs& p, const SideJob& sj, hipStream_t s) 
   else if (npw == 2) hipLaunchKernelGGL(k_partial<2>, grid, blk, 0, s, p, sj);
   else if (npw == 8) hipLaunchKernelGGL(k_partial<8>, grid, blk, 0, s, p, sj);
   else hipLaunchKernelGGL(k_partial<0>, grid, blk, 0, s, p, sj);
+}
+
+// Frame/stop projection (Architecture_wrappers.py:243-247, modules.py:392-448) with the folded
+// prenet layer 1 of the next step, split-K over KS blocks per 16-column tile.  Each block stores
+// its partial tile; the last of a tile's KS blocks (arrival ticket, agent-scope release/acquire,
+// cdna_hip_programming.md §6 Guideline 16 counter form) reduces the tile, adds the style term
+// and bias, and writes frames[t] / stop[t] / pre1; the stop tile's last arriver also applies the
+// batch-level stop rule of TacoTestHelper / dynamic_decode (helpers.py:36-59) and sets `done`.
+typedef __attribute__((address_space(1))) float gf32;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+struct ProjArgs {
+  DecCtl* ctl;
+  const float* X; int K;          // AF [32 x Kp] = [h2 | context_enc]
+  const float* W;                 // WF tiles [ntile][K x 16]
+  float* PP; int ldo; int ntile; int KS;
+  unsigned* cnt;                  // [ntile] arrival tickets (zeroed per decode, reset by the last arriver)
+  const float* PS; const float* bias; const float* ssum;
+  float* pre1;                    // [32][P] prenet-L1 pre-activations (AF-group column order)
+  float* frames; float* stop;
+  int B, nm, NPJ, P, max_iters, T_lim, stop_at_any;
+};
+
+template <int NPW>
+__global__ __launch_bounds__(256) void k_proj(ProjArgs a, SideJob sj, int t) {
+  __shared__ float red[4 * 512];
+  __shared__ float G[512];
+  __shared__ float stopv[32];
+  __shared__ int s_last;
+  if ((int)blockIdx.x >= a.ntile * a.KS) {  // extra blocks: side job
+    if (a.ctl->done) return;
+    side_job(sj, blockIdx.x - a.ntile * a.KS, red, G, threadIdx.x);
+    return;
+  }
+  const int done = a.ctl->done;
+  const int tile = blockIdx.x % a.ntile, ks = blockIdx.x / a.ntile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nsg = a.K / 16;
+  const int s0 = ks * nsg / a.KS, s1 = (ks + 1) * nsg / a.KS;
+  const int n = s1 - s0;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const float* Wt = a.W + (long)tile * a.K * 16;
+  if constexpr (NPW > 0) skinny_mfma_all<NPW>(a.X, Wt, s0 + wave * NPW, acc0, acc1, lane);
+  else skinny_mfma(a.X, Wt, s0 + wave * n / 4, s0 + (wave + 1) * n / 4, acc0, acc1, lane);
+  if (done) return;
+  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
+  // ---- arrival ticket (write-through form, Guideline 16 R1): partials stored sc1 and drained,
+  //      one ticket add per block, the last arriver reads the partials with sc1 loads ----
+  for (int e = tid; e < 512; e += 256) {
+    const int m = e >> 4, c = tile * 16 + (e & 15);
+    __hip_atomic_store((gf32*)(a.PP + ((long)ks * 32 + m) * a.ldo + c), G[e], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned tk = __hip_atomic_fetch_add((gu32*)(a.cnt + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = tk == (unsigned)a.KS - 1;
+    if (last) __hip_atomic_store((gu32*)(a.cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (int e = tid; e < 512; e += 256) {
+    const int m = e >> 4, c = tile * 16 + (e & 15);
+    float v = 0.f;
+    for (int k2 = 0; k2 < a.KS; ++k2)
+      v += __hip_atomic_load((gf32*)(a.PP + ((long)k2 * 32 + m) * a.ldo + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v = (v + a.ssum[m] * a.PS[(long)m * a.ldo + c]) + a.bias[c];
+    if (c >= a.NPJ) {
+      a.pre1[(long)m * a.P + (c - a.NPJ)] = v;
+    } else if (c < a.nm) {
+      if (m < a.B) a.frames[((long)m * a.max_iters + t) * a.nm + c] = v;
+    } else if (c == a.nm) {
+      stopv[m] = sigm(v);
+    }
+  }
+  if (a.nm / 16 != tile) return;  // the tile holding the stop column decides `done`
+  __syncthreads();
+  if (wave == 0) {
+    const bool valid = lane < a.B;
+    const float sv = valid ? stopv[lane] : 0.f;
+    const bool f = valid && rintf(sv) == 1.0f;
+    const unsigned long long fb = __ballot(f), vb = __ballot(valid);
+    if (valid) a.stop[(long)lane * a.max_iters + t] = sv;
+    int dn = a.stop_at_any ? (fb != 0ull) : (fb == vb);
+    if (a.T_lim > 0) dn = t + 1 >= a.T_lim;  // TacoTrainingHelper: time + 1 >= T_targets
+    if (t + 1 >= a.max_iters) dn = 1;         // dynamic_decode maximum_iterations
+    if (lane == 0 && dn) {
+      a.ctl->n_steps = t + 1;
+      a.ctl->done = 1;
+    }
+  }
 }
 
 // Location-sensitive energies (attention.py:37-69, 186-215) for 32 encoder steps of one row:
@@ -966,7 +982,7 @@ struct tt2_ctx {
   // activations
   tt2::DevBuf ids, lens, refm[2], x_a, x_b, xproj, enc_out, enc_h, enc_c, conv_a, conv_b, ref_out, style,
       values, keys;
-  tt2::DevBuf X1[2], X2, Xp, H0s[2], H1s[2], RG0, RG1, GS0, PS, ssum, TP1, c1, c2, Qp, energy, cum, max_att, PP, ctl,
+  tt2::DevBuf X1[2], X2, Xp, H0s[2], H1s[2], RG0, RG1, GS0, PS, ssum, TP1, pre1, pcnt, c1, c2, Qp, energy, cum, max_att, PP, ctl,
       masks, gmasks, targets;
   tt2::DevBuf frames, stop, align, dec, post_a, post_b, mel;
   int* ctl_host = nullptr;  // pinned [2 slots]
@@ -979,6 +995,7 @@ struct tt2_ctx {
   tt2::DecArgs last_args;
   long long stamps_host[64] = {0};
   int side_mode = 0;                 // TT2_SIDE_MODE env: 0 hosted side jobs, 1 parallel branch
+  int side_delay = 2, side_delay2 = 0;  // TT2_SIDE_DELAY / TT2_SIDE_DELAY2 env (energy / softmax host)
   hipEvent_t sev[8] = {nullptr};     // capture-time fork/join events
   bool have_args = false;
 };
@@ -1259,6 +1276,8 @@ static void alloc_acts(tt2_ctx* c) {
   c->GS0.alloc(32L * 4 * c->H * 4);
   c->PS.alloc(32L * c->NPF * 4);
   c->ssum.alloc(32 * 4);
+  c->pre1.alloc(32L * c->P * 4);
+  c->pcnt.alloc(64 * 4);
   TT2_HIP(hipMemset(c->GS0.p, 0, c->GS0.bytes));  // rows >= B stay zero
   TT2_HIP(hipMemset(c->PS.p, 0, c->PS.bytes));
   c->c1.alloc(32L * c->H * 4);
@@ -1420,6 +1439,7 @@ static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, 
   a.max_att = c->max_att.as<int>(); a.PP = c->PP.as<float>();
   a.KSQ = c->KSQ; a.KSP = c->KSP; a.NPJ = c->NPJ; a.NPF = c->NPF;
   a.TP1 = targets_d ? c->TP1.as<float>() : nullptr;
+  a.pre1 = c->pre1.as<float>();
   a.masks = masks_d; a.seed = seed; a.targets = targets_d; a.stamps = nullptr;
   a.stamp_step = -1;
   if (const char* st = getenv("TT2_STAMP_STEP")) {  // diagnostic: prenet stamps of one decode step
@@ -1458,13 +1478,25 @@ static void launch_query(tt2_ctx* c, const DecArgs& a, const SideJob& sj, hipStr
   q.ctl = a.ctl; q.X = a.Xp; q.K = c->H; q.W = a.q_w; q.out = a.Qp; q.ldo = c->A; q.ntile = c->A / 16; q.KS = c->KSQ;
   launch_partial(q, sj, s);
 }
-static void launch_proj(tt2_ctx* c, const DecArgs& a, const SideJob& sj, hipStream_t s) {
-  PartArgs p;
+static void launch_proj(tt2_ctx* c, const DecArgs& a, int t, const SideJob& sj, hipStream_t s) {
+  ProjArgs p;
   // GTA feeds targets, not frames, to the prenet: the folded prenet-L1 columns are not needed
-  p.ctl = a.ctl; p.X = a.Xp; p.K = c->Kp; p.W = a.proj_w; p.out = a.PP; p.ldo = c->NPF;
+  p.ctl = a.ctl; p.X = a.Xp; p.K = c->Kp; p.W = a.proj_w; p.PP = a.PP; p.ldo = c->NPF;
   p.ntile = (a.targets ? c->NPJ : c->NPF) / 16;
   p.KS = c->KSP;
-  launch_partial(p, sj, s);
+  p.cnt = c->pcnt.as<unsigned>();
+  p.PS = a.PS; p.bias = a.proj_b; p.ssum = a.ssum; p.pre1 = c->pre1.as<float>();
+  p.frames = a.frames; p.stop = a.stop;
+  p.B = a.B; p.nm = a.nm; p.NPJ = c->NPJ; p.P = c->P; p.max_iters = a.max_iters; p.T_lim = a.T_lim;
+  p.stop_at_any = a.stop_at_any;
+  const int nsg = p.K / 16;
+  const dim3 grid(p.ntile * p.KS + sj.ntile), blk(256);
+  const int npw = nsg % (p.KS * 4) == 0 ? nsg / (p.KS * 4) : 0;
+  if (npw == 6) hipLaunchKernelGGL(k_proj<6>, grid, blk, 0, s, p, sj, t);
+  else if (npw == 4) hipLaunchKernelGGL(k_proj<4>, grid, blk, 0, s, p, sj, t);
+  else if (npw == 8) hipLaunchKernelGGL(k_proj<8>, grid, blk, 0, s, p, sj, t);
+  else if (npw == 2) hipLaunchKernelGGL(k_proj<2>, grid, blk, 0, s, p, sj, t);
+  else hipLaunchKernelGGL(k_proj<0>, grid, blk, 0, s, p, sj, t);
 }
 // recurrent gate terms of step i+1 from the zoned states written at step i
 static SideJob side_rec(tt2_ctx* c, int layer, int par) {
@@ -1474,6 +1506,7 @@ static SideJob side_rec(tt2_ctx* c, int layer, int par) {
   j.out = (layer == 0 ? c->RG0 : c->RG1).as<float>();
   j.K = c->H;
   j.ntile = 4 * c->H / 16;
+  j.delay = layer == 1 ? c->side_delay : c->side_delay2;  // RG1 runs in the energy launch, RG0 in softmax
   return j;
 }
 static void launch_energy(tt2_ctx* c, const DecArgs& a, const SideJob& sj, hipStream_t s) {
@@ -1516,7 +1549,7 @@ static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, int t, hipStream_t
   launch_query(c, a, c->side_mode == 2 ? side_rec(c, 1, par) : none, s);
   launch_energy(c, a, c->side_mode == 0 ? side_rec(c, 1, par) : none, s);
   launch_softmax(c, a, i, t, c->side_mode == 0 ? side_rec(c, 0, par) : none, s);
-  launch_proj(c, a, c->side_mode == 2 ? side_rec(c, 0, par) : none, s);
+  launch_proj(c, a, t, c->side_mode == 2 ? side_rec(c, 0, par) : none, s);
 }
 
 static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64_t seed, const float* targets_d,
@@ -1535,6 +1568,7 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
   TT2_HIP(hipMemsetAsync(c->RG0.p, 0, c->RG0.bytes, s));
   TT2_HIP(hipMemsetAsync(c->RG1.p, 0, c->RG1.bytes, s));
   TT2_HIP(hipMemsetAsync(c->ssum.p, 0, c->ssum.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->pcnt.p, 0, c->pcnt.bytes, s));
   TT2_HIP(hipMemsetAsync(c->c1.p, 0, c->c1.bytes, s));
   TT2_HIP(hipMemsetAsync(c->c2.p, 0, c->c2.bytes, s));
   TT2_HIP(hipMemsetAsync(c->cum.p, 0, c->cum.bytes, s));
@@ -1717,6 +1751,8 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
     for (auto& e : c->sev) TT2_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (const char* m = getenv("TT2_SIDE_MODE")) c->side_mode = atoi(m);
+    if (const char* m = getenv("TT2_SIDE_DELAY")) c->side_delay = atoi(m);
+    if (const char* m = getenv("TT2_SIDE_DELAY2")) c->side_delay2 = atoi(m);
     *out = c.release();
   });
 }
@@ -1910,6 +1946,7 @@ tt2_status tt2_profile_decoder_kernels(tt2_ctx* c, int iters, float* avg_us) {
     for (int k = 0; k < TT2_NPROF; ++k) {
       // `iters` back-to-back launches between one event pair: per-launch time = device
       // duration + the inter-kernel gap (comparable with rocprofv3 kernel-trace averages)
+      TT2_HIP(hipMemsetAsync(c->ctl.p, 0, sizeof(DecCtl), s));
       TT2_HIP(hipEventRecord(e0, s));
       for (int i = 0; i < iters; ++i) {
         const int par = i & 1;
@@ -1919,7 +1956,7 @@ tt2_status tt2_profile_decoder_kernels(tt2_ctx* c, int iters, float* avg_us) {
           case 2: launch_query(c, a, none, s); break;
           case 3: launch_energy(c, a, side_rec(c, 1, 0), s); break;
           case 4: launch_softmax(c, a, 0, 0, side_rec(c, 0, 0), s); break;
-          case 5: launch_proj(c, a, none, s); break;
+          case 5: launch_proj(c, a, 0, none, s); break;
           case 6: launch_lstm(lstm_args(c, a, 1, 0), c->H, s); break;
           case 7: launch_energy(c, a0, side_rec(c, 1, 0), s); break;   // side job alone
           case 8: launch_energy(c, a, none, s); break;                 // energy alone
