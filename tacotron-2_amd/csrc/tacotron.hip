@@ -305,9 +305,9 @@ struct DecArgs {
   int stop_at_any, mask_encoder, cumulative, constraint, monotonic, win;
   // weights
   const float* pre_b1; const float* pre_w2; const float* pre_b2;
-  const float* q_w; const float* loc_cw; const float* loc_cb; const float* loc_w;  // WF-packed
+  const float* q_w; const float* loc_cw;  // WF-packed; loc_cw = W_conv·W_loc [KLp taps x A]
   int KLp, Fp;  // location conv taps / filters padded to 16
-  const float* va; const float* ba; const float* proj_w; const float* proj_b;
+  const float* va; const float* proj_w; const float* proj_b;
   const float* PS;      // [32][NPF] style·W_proj_style (per utterance), incl. the folded prenet-L1 columns
   const float* TP1;     // [B][T_lim][P] targets·W1 + b1 (GTA) or null
   const float* pre1;    // [32][P] prenet-L1 pre-activations of the last projection (AF-group order)
@@ -710,7 +710,7 @@ __global__ __launch_bounds__(256) void k_proj(ProjArgs a, SideJob sj, int t) {
 // Blocks past B·ceil(T_in/32) run the side job.
 __global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
   __shared__ __attribute__((aligned(16))) float A1[32 * 64];  // AF [32 t][KLp taps]
-  __shared__ __attribute__((aligned(16))) float A2[32 * 64];  // AF [32 t][Fp filters]
+  __shared__ __attribute__((aligned(16))) float A2[32 * 64];  // side-job scratch
   __shared__ float q[256];
   __shared__ float win[32 + 64];
   __shared__ float ep[4][32];
@@ -724,36 +724,33 @@ __global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
   const int done = a.ctl->done;
   const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int A = a.A, KL = a.KL, KLp = a.KLp, Fp = a.Fp, padl = (KL - 1) / 2;
-  // prefetch the keys this lane consumes after the location MFMA (<= 4 tiles x 8 rows)
+  // location features folded: loc = im2col(cum, KL taps)·(W_conv·W_loc), one MFMA GEMM with
+  // K = taps (the conv bias·W_loc and the attention bias b_a were added to the keys at encode)
+  // prefetch (unconditional, clamped): the keys this lane consumes (<= 4 tiles x 8 rows)
   float kv[4][8];
   const int ntl = A / 16;
+  const int tmax = a.T_in - 1;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int tile = wave + 4 * i;
+    const int tile = min(wave + 4 * i, ntl - 1);
     const int k = tile * 16 + (lane & 15);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const int t = t0 + (lane >> 4) * 4 + (r & 3) + (r >> 2) * 16;
-      kv[i][r] = (tile < ntl && t < a.T_in) ? a.keys[((long)b * a.T_in + t) * A + k] : 0.f;
+      const int t = min(t0 + (lane >> 4) * 4 + (r & 3) + (r >> 2) * 16, tmax);
+      kv[i][r] = a.keys[((long)b * a.T_in + t) * A + k];
     }
   }
   const f32x4* CWv = reinterpret_cast<const f32x4*>(a.loc_cw);
-  const f32x4* LWv = reinterpret_cast<const f32x4*>(a.loc_w);
-  const int nkc = KLp / 16, nkf = Fp / 16;
-  f32x4 wcv[4], wlv[4][4];
-  float vkv[4], bkv[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (wave < nkf && j < nkc) wcv[j] = CWv[((long)wave * nkc + j) * 64 + lane];
+  const int nkc = KLp / 16;
+  f32x4 wcv[4][4];
+  float vkv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int tile = wave + 4 * i;
+    const int tile = min(wave + 4 * i, ntl - 1);
     const int k = tile * 16 + (lane & 15);
-    vkv[i] = tile < ntl ? a.va[k] : 0.f;
-    bkv[i] = tile < ntl ? a.ba[k] : 0.f;
+    vkv[i] = a.va[k];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (tile < ntl && j < nkf) wlv[i][j] = LWv[((long)tile * nkf + j) * 64 + lane];
+    for (int j = 0; j < 4; ++j) wcv[i][j] = CWv[((long)tile * nkc + min(j, nkc - 1)) * 64 + lane];
   }
   for (int k = tid; k < A; k += blockDim.x) {
     float qp[KSQ_C];
@@ -766,7 +763,8 @@ __global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
   }
   for (int i = tid; i < 32 + KL - 1; i += blockDim.x) {
     const int t = t0 - padl + i;
-    win[i] = (t >= 0 && t < a.T_in) ? a.cum[(long)b * a.T_in + t] : 0.f;
+    const float v = a.cum[(long)b * a.T_in + min(max(t, 0), tmax)];
+    win[i] = (t >= 0 && t < a.T_in) ? v : 0.f;
   }
   if (done) return;
   __syncthreads();
@@ -776,19 +774,6 @@ __global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
     A1[af_idx(t, tap)] = tap < KL ? win[t + tap] : 0.f;
   }
   __syncthreads();
-  if (wave < Fp / 16) {  // location convolution, one 16-filter tile per wave
-    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-    skinny_mfma_w<4>(A1, wcv, nkc, c0, c1, lane);
-    const int n = wave * 16 + (lane & 15);
-    const float cb = n < a.F ? a.loc_cb[n] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = (lane >> 4) * 4 + r;
-      A2[af_idx(m, n)] = n < a.F ? c0[r] + cb : 0.f;
-      A2[af_idx(m + 16, n)] = n < a.F ? c1[r] + cb : 0.f;
-    }
-  }
-  __syncthreads();
   STAMP(10);
   float e0[4] = {0.f, 0.f, 0.f, 0.f}, e1[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -796,23 +781,21 @@ __global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
     const int tile = wave + 4 * i;
     if (tile >= ntl) break;
     f32x4 l0 = {0.f, 0.f, 0.f, 0.f}, l1 = {0.f, 0.f, 0.f, 0.f};
-    skinny_mfma_w<4>(A2, wlv[i], nkf, l0, l1, lane);
+    skinny_mfma_w<4>(A1, wcv[i], nkc, l0, l1, lane);
     const int k = tile * 16 + (lane & 15);
-    const float vk = vkv[i], bk = bkv[i], qk = q[k];
+    const float vk = vkv[i], qk = q[k];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int ta = t0 + (lane >> 4) * 4 + r, tb = ta + 16;
-      if (ta < a.T_in) e0[r] += vk * tanh_fast(kv[i][r] + qk + l0[r] + bk);
-      if (tb < a.T_in) e1[r] += vk * tanh_fast(kv[i][4 + r] + qk + l1[r] + bk);
+      if (ta < a.T_in) e0[r] += vk * tanh_fast(kv[i][r] + qk + l0[r]);
+      if (tb < a.T_in) e1[r] += vk * tanh_fast(kv[i][4 + r] + qk + l1[r]);
     }
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      e0[r] += __shfl_xor(e0[r], o);
-      e1[r] += __shfl_xor(e1[r], o);
-    }
+  for (int r = 0; r < 4; ++r) {
+    e0[r] = sum16(e0[r]);
+    e1[r] = sum16(e1[r]);
+  }
   STAMP(11);
   if ((lane & 15) == 0)
     for (int r = 0; r < 4; ++r) {
@@ -977,7 +960,7 @@ struct tt2_ctx {
   tt2::DevBuf mem_k;
   tt2::DevBuf pre_w1r, pre_b1, pre_w2, pre_b2, q_w;  // pre_w1r: row-major [nm][P] (GTA TP1 GEMM)
   tt2::DevBuf l1_w, l1_wh, l1_ws, l1_b, l2_w, l2_wh, l2_b;  // critical rows / recurrent rows / style rows
-  tt2::DevBuf loc_cw, loc_cb, loc_w, va, ba, proj_w, proj_ws, proj_b;
+  tt2::DevBuf loc_cw, keys_b, va, proj_w, proj_ws, proj_b;
   tt2::DevBuf post_cw[8], post_cb[8], post_bs[8], post_bh[8], post_pw, post_pb;
   // activations
   tt2::DevBuf ids, lens, refm[2], x_a, x_b, xproj, enc_out, enc_h, enc_c, conv_a, conv_b, ref_out, style,
@@ -1167,19 +1150,30 @@ static void finalize(tt2_ctx* c) {
   }
   const std::string la = P + "decoder/Location_Sensitive_Attention/";
   {
-    // conv [KL][1][F] -> Fp/16 WF tiles over K = KLp taps; dense [F][A] -> A/16 WF tiles over K = Fp
+    // location features (attention.py:37-69): conv [KL][1][F] then dense [F][A], both linear, are
+    // folded into one [KL x A] filter (A/16 WF tiles over K = KLp taps); the conv bias·W_loc and
+    // the attention bias b_a join the keys (memory_layer output) as one per-dim bias
     const auto& cw = need(wm, la + "location_features_convolution/kernel", {c->KL, 1, c->F});
-    std::vector<int> fcols;
-    for (int j = 0; j < c->Fp; ++j) fcols.push_back(j < c->F ? j : -1);
-    upload(c->loc_cw, pack_wf(cw.data.data(), c->KL, c->F, fcols, c->KLp));
-    upload(c->loc_cb, need(wm, la + "location_features_convolution/bias", {c->F}));
+    const auto& cb = need(wm, la + "location_features_convolution/bias", {c->F});
     const auto& lw = need(wm, la + "location_features_layer/kernel", {c->F, c->A});
+    const auto& ba = need(wm, la + "attention_bias", {c->A});
+    std::vector<float> wc((size_t)c->KL * c->A), kb(c->A);
+    for (int k = 0; k < c->A; ++k) {
+      for (int tap = 0; tap < c->KL; ++tap) {
+        double acc = 0.0;
+        for (int f = 0; f < c->F; ++f) acc += (double)cw.data[(size_t)tap * c->F + f] * lw.data[(size_t)f * c->A + k];
+        wc[(size_t)tap * c->A + k] = (float)acc;
+      }
+      double bacc = 0.0;
+      for (int f = 0; f < c->F; ++f) bacc += (double)cb.data[f] * lw.data[(size_t)f * c->A + k];
+      kb[k] = (float)(bacc + ba.data[k]);
+    }
     std::vector<int> acols;
     for (int j = 0; j < c->A; ++j) acols.push_back(j);
-    upload(c->loc_w, pack_wf(lw.data.data(), c->F, c->A, acols, c->Fp));
+    upload(c->loc_cw, pack_wf(wc.data(), c->KL, c->A, acols, c->KLp));
+    upload(c->keys_b, kb);
   }
   upload(c->va, need(wm, la + "attention_variable_projection", {c->A}));
-  upload(c->ba, need(wm, la + "attention_bias", {c->A}));
   {
     const std::string fp = P + "decoder/linear_transform_projection/projection_linear_transform_projection/";
     const std::string sp = P + "decoder/stop_token_projection/projection_stop_token_projection/";
@@ -1394,6 +1388,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     GemmArgs g;
     g.M = BT; g.N = c->A; g.K = c->Dm; g.A = c->values.as<float>(); g.lda = c->Dm;
     g.Bw = c->mem_k.as<float>(); g.ldb = c->A; g.Cout = c->keys.as<float>(); g.ldc = c->A;
+    g.bias = c->keys_b.as<float>();  // b_a + b_conv·W_loc (folded location-feature bias)
     gemm(g, s);
   }
   {  // per-utterance style terms of the decoder: GS = style·W_lstm1[style rows], PS = style·W_proj[style rows]
@@ -1429,8 +1424,7 @@ static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, 
   a.pre_b1 = c->pre_b1.as<float>();
   a.pre_w2 = c->pre_w2.as<float>(); a.pre_b2 = c->pre_b2.as<float>();
   a.KLp = c->KLp; a.Fp = c->Fp;
-  a.q_w = c->q_w.as<float>(); a.loc_cw = c->loc_cw.as<float>(); a.loc_cb = c->loc_cb.as<float>();
-  a.loc_w = c->loc_w.as<float>(); a.va = c->va.as<float>(); a.ba = c->ba.as<float>();
+  a.q_w = c->q_w.as<float>(); a.loc_cw = c->loc_cw.as<float>(); a.va = c->va.as<float>();
   a.proj_w = c->proj_w.as<float>(); a.proj_b = c->proj_b.as<float>(); a.PS = c->PS.as<float>();
   a.keys = c->keys.as<float>(); a.values = c->values.as<float>(); a.lengths = c->lens.as<int>();
   for (int p = 0; p < 2; ++p) a.X1[p] = c->X1[p].as<float>();
