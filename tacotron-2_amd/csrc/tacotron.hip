@@ -354,24 +354,26 @@ constexpr int KSP_C = 4;  // projection split-K
       a.stamps[i] = __builtin_amdgcn_s_memtime();                                        \
   } while (0)
 
-// One side-job tile with a 256-thread block: K split over 4 waves (every weight load in flight
-// before the first MFMA when K/64 k-groups fit the template), LDS reduce, tile-major store.
-template <int NPW>
+// One side-job tile with an NW-wave block: K split over the waves (every weight load in flight
+// before the first MFMA when K/(16·NW) k-groups fit the template), LDS reduce (red: NW·512
+// floats), tile-major store.
+template <int NW, int NPW>
 __device__ __forceinline__ void side_tile(const SideJob& j, int tile, float* red, float* G, int tid) {
   const int lane = tid & 63, wave = tid >> 6;
   const int nsg = j.K / 16;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const float* Wt = j.W + (long)tile * j.K * 16;
   if constexpr (NPW > 0) skinny_mfma_all<NPW>(j.X, Wt, wave * NPW, acc0, acc1, lane);
-  else skinny_mfma(j.X, Wt, wave * nsg / 4, (wave + 1) * nsg / 4, acc0, acc1, lane);
-  reduce_waves_32x16<4>(acc0, acc1, red, G, wave, lane, tid);
-  for (int e = tid; e < 512; e += 256) j.out[(long)tile * 512 + e] = G[e];
+  else skinny_mfma(j.X, Wt, wave * nsg / NW, (wave + 1) * nsg / NW, acc0, acc1, lane);
+  reduce_waves_32x16<NW>(acc0, acc1, red, G, wave, lane, tid);
+  for (int e = tid; e < 512; e += NW * 64) j.out[(long)tile * 512 + e] = G[e];
 }
+template <int NW = 4>
 __device__ __forceinline__ void side_job(const SideJob& j, int blk, float* red, float* G, int tid) {
   // let the host launch's own (latency-critical) loads reach the memory system first
   if (j.delay > 0) for (int i = 0; i < j.delay; ++i) __builtin_amdgcn_s_sleep(64);
-  if (j.K == 1024) side_tile<16>(j, blk, red, G, tid);
-  else side_tile<0>(j, blk, red, G, tid);
+  if (j.K == 1024) side_tile<NW, 64 / NW>(j, blk, red, G, tid);
+  else side_tile<NW, 0>(j, blk, red, G, tid);
 }
 
 // Side job as its own launch (parallel graph branch).
@@ -704,35 +706,35 @@ __global__ __launch_bounds__(256) void k_proj(ProjArgs a, SideJob sj, int t) {
 }
 
 // Location-sensitive energies (attention.py:37-69, 186-215) for 32 encoder steps of one row:
-//   q = Σ query partials;  f = im2col(cum, 31 taps)·W_conv + b  (MFMA, K = taps);
-//   loc = f·W_loc (MFMA, K = filters);  e_t = Σ_k v_a[k]·tanh(keys + q + loc + b_a)
+//   q = Σ query partials;  loc = im2col(cum, KL taps)·(W_conv·W_loc) (MFMA, K = taps);
+//   e_t = Σ_k v_a[k]·tanh(keys' + q + loc)  (keys' = keys + b_a + b_conv·W_loc, built at encode)
 // then the synthesis window constraint and -inf past the row's length (TF _maybe_mask_score).
-// Blocks past B·ceil(T_in/32) run the side job.
-__global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
-  __shared__ __attribute__((aligned(16))) float A1[32 * 64];  // AF [32 t][KLp taps]
-  __shared__ __attribute__((aligned(16))) float A2[32 * 64];  // side-job scratch
+// 8 waves, one 16-dim attention tile each (A <= 256).  Blocks past B·ceil(T_in/32) run the
+// side job.
+constexpr int NWE = 8;
+__global__ __launch_bounds__(NWE * 64) void k_energy(DecArgs a, SideJob sj) {
+  __shared__ __attribute__((aligned(16))) float smE[NWE * 512 + 512];  // A1 | side-job scratch
   __shared__ float q[256];
   __shared__ float win[32 + 64];
-  __shared__ float ep[4][32];
+  __shared__ float ep[NWE][32];
+  float* A1 = smE;  // AF [32 t][KLp taps]
   const int ntt = (a.T_in + 31) / 32, nE = a.B * ntt;
   if ((int)blockIdx.x >= nE) {
     if (a.ctl->done) return;
-    side_job(sj, blockIdx.x - nE, A1, A2 + 1536, threadIdx.x);  // red: A1+A2[0..1535] (2048 floats)
+    side_job<NWE>(sj, blockIdx.x - nE, smE, smE + NWE * 512, threadIdx.x);
     return;
   }
   STAMP(8);
   const int done = a.ctl->done;
   const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int A = a.A, KL = a.KL, KLp = a.KLp, Fp = a.Fp, padl = (KL - 1) / 2;
-  // location features folded: loc = im2col(cum, KL taps)·(W_conv·W_loc), one MFMA GEMM with
-  // K = taps (the conv bias·W_loc and the attention bias b_a were added to the keys at encode)
-  // prefetch (unconditional, clamped): the keys this lane consumes (<= 4 tiles x 8 rows)
-  float kv[4][8];
+  const int A = a.A, KL = a.KL, KLp = a.KLp, padl = (KL - 1) / 2;
+  // prefetch (unconditional, clamped): the keys this lane consumes (<= 2 tiles x 8 rows)
+  float kv[2][8];
   const int ntl = A / 16;
   const int tmax = a.T_in - 1;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int tile = min(wave + 4 * i, ntl - 1);
+  for (int i = 0; i < 2; ++i) {
+    const int tile = min(wave + NWE * i, ntl - 1);
     const int k = tile * 16 + (lane & 15);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -742,11 +744,11 @@ __global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
   }
   const f32x4* CWv = reinterpret_cast<const f32x4*>(a.loc_cw);
   const int nkc = KLp / 16;
-  f32x4 wcv[4][4];
-  float vkv[4];
+  f32x4 wcv[2][4];
+  float vkv[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int tile = min(wave + 4 * i, ntl - 1);
+  for (int i = 0; i < 2; ++i) {
+    const int tile = min(wave + NWE * i, ntl - 1);
     const int k = tile * 16 + (lane & 15);
     vkv[i] = a.va[k];
 #pragma unroll
@@ -777,8 +779,8 @@ __global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
   STAMP(10);
   float e0[4] = {0.f, 0.f, 0.f, 0.f}, e1[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int tile = wave + 4 * i;
+  for (int i = 0; i < 2; ++i) {
+    const int tile = wave + NWE * i;
     if (tile >= ntl) break;
     f32x4 l0 = {0.f, 0.f, 0.f, 0.f}, l1 = {0.f, 0.f, 0.f, 0.f};
     skinny_mfma_w<4>(A1, wcv[i], nkc, l0, l1, lane);
@@ -806,7 +808,8 @@ __global__ __launch_bounds__(256) void k_energy(DecArgs a, SideJob sj) {
   if (tid < 32) {
     const int t = t0 + tid;
     if (t < a.T_in) {
-      float e = ep[0][tid] + ep[1][tid] + ep[2][tid] + ep[3][tid];
+      float e = 0.f;
+      for (int w = 0; w < NWE; ++w) e += ep[w][tid];
       if (a.constraint) {
         const int pm = a.max_att[b], w = a.win;
         bool masked;
@@ -978,7 +981,7 @@ struct tt2_ctx {
   tt2::DecArgs last_args;
   long long stamps_host[64] = {0};
   int side_mode = 0;                 // TT2_SIDE_MODE env: 0 hosted side jobs, 1 parallel branch
-  int side_delay = 2, side_delay2 = 0;  // TT2_SIDE_DELAY / TT2_SIDE_DELAY2 env (energy / softmax host)
+  int side_delay = 1, side_delay2 = 0;  // TT2_SIDE_DELAY / TT2_SIDE_DELAY2 env (energy / softmax host)
   hipEvent_t sev[8] = {nullptr};     // capture-time fork/join events
   bool have_args = false;
 };
@@ -1505,7 +1508,7 @@ static SideJob side_rec(tt2_ctx* c, int layer, int par) {
 }
 static void launch_energy(tt2_ctx* c, const DecArgs& a, const SideJob& sj, hipStream_t s) {
   const int nE = a.B * cdiv(a.T_in, 32);
-  hipLaunchKernelGGL(k_energy, dim3(nE + sj.ntile), dim3(256), 0, s, a, sj);
+  hipLaunchKernelGGL(k_energy, dim3(nE + sj.ntile), dim3(NWE * 64), 0, s, a, sj);
 }
 static void launch_softmax(tt2_ctx* c, const DecArgs& a, int i, int t, const SideJob& sj, hipStream_t s) {
   const size_t shm = sizeof(float) * std::max<size_t>(((a.T_in + 3) & ~3) + 4 * 16 * 16, 2048 + 512);
