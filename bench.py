@@ -50,6 +50,22 @@ def lstm_bytes(K, H, M=32):
     return 4 * (K * 4 * H + 4 * H + M * K + M * 4 * H + 2 * M * H + 3 * M * H)
 
 
+DECODER_STEP_SCOPES = ("decoder/decoder_prenet/", "decoder/decoder_LSTM/", "decoder/query_layer/",
+                       "decoder/Location_Sensitive_Attention/", "decoder/linear_transform_projection/",
+                       "decoder/stop_token_projection/")
+
+
+def decoder_step_bytes(W, hp, B, T):
+    """Algorithmic HBM bytes of one decoder step: every weight the step touches
+    (prenet, 2 LSTM layers, query/location/attention weights, frame + stop projections), the
+    attention keys [B,T,A] and values [B,T,D_mem], and the cumulative alignments read + written."""
+    P = "Tacotron_model/inference/"
+    params = sum(v.size for k, v in W.items()
+                 if k.startswith(P) and any(k[len(P):].startswith(sc) for sc in DECODER_STEP_SCOPES))
+    D = 2 * hp.encoder_lstm_units + 2 * hp.style_embed_depth
+    return 4 * (params + B * T * hp.attention_dim + B * T * D + 2 * B * T)
+
+
 def cpu_baseline_tacotron(hp, W, B, T, T_ref, t_out, steps):
     """Oracle (numpy) on this host: encoder + `steps` decoder steps + Postnet over `steps` frames,
     extrapolated linearly to T_out frames."""
@@ -181,34 +197,57 @@ def main():
     phases = dict(encode_ms=round(ms3[0], 3), decode_ms=round(ms3[1], 3), postnet_ms=round(ms3[2], 3),
                   decode_us_per_step=round(1000.0 * ms3[1] / max(n_steps.value, 1), 3))
 
-    # --- dominant kernel roofline: the decoder Zoneout-LSTM layers (k_lstm) ---
-    dec_stamps = None
-    if os.environ.get("TT2_STAMP_STEP"):
+    # --- dominant kernel roofline ---
+    persist, pd_ms = eng.decoder_path()
+    stamps = None
+    if persist:
+        # k_decode_persist runs the whole decode loop in one launch; algorithmic bytes per step =
+        # every decoder-step weight + keys + values + cum-align r/w (fp32)
+        n = n_steps.value
+        step_bytes = decoder_step_bytes(W, hp, B, T)
+        achieved = step_bytes * n / (pd_ms * 1e-3) / 1e9
+        traffic = load_traffic("k_decode_persist")
+        roofline = dict(kernel="k_decode_persist (whole dynamic_decode loop, one launch)", bound="hbm",
+                        achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        algorithmic_bytes_per_launch=int(step_bytes * n),
+                        algorithmic_bytes_per_step=int(step_bytes), steps_per_launch=n,
+                        avg_launch_us=round(pd_ms * 1000.0, 1),
+                        us_per_step=round(pd_ms * 1000.0 / max(n, 1), 3),
+                        traffic_per_step=(round(traffic / n) if traffic else None))
+        if os.environ.get("TT2_STAMP_STEP"):
+            st = (ctypes.c_longlong * 8192)()
+            _lib.check(lib.tt2_debug_pd_stamps(eng.h, st))
+            arr = np.array(st[:], dtype=np.int64).reshape(256, 32)
+            t0 = arr[:, 0][arr[:, 0] > 0].min()
+            rel = np.where(arr > 0, (arr - t0) * 0.01, np.nan)
+            stamps = {"persist_stage_us_wg0": [round(float(v), 2) for v in rel[0]],
+                      "persist_stage_us_min": [round(float(v), 2) for v in np.nanmin(rel, 0)],
+                      "persist_stage_us_max": [round(float(v), 2) for v in np.nanmax(rel, 0)],
+                      "persist_stage_argmax_wg": [int(v) for v in np.nanargmax(np.nan_to_num(rel, nan=-1), 0)]}
+            np.save(os.path.join(ROOT, "gpurun_out", "pd_stamps.npy"), arr)
+    else:
+        us7 = (ctypes.c_float * 10)()
+        _lib.check(lib.tt2_profile_decoder_kernels(eng.h, a.profile_iters, us7))
         st64 = (ctypes.c_longlong * 64)()
         _lib.check(lib.tt2_debug_stamps(eng.h, st64))
-        dec_stamps = [st64[i] - st64[0] for i in range(6)]
-    us7 = (ctypes.c_float * 10)()
-    _lib.check(lib.tt2_profile_decoder_kernels(eng.h, a.profile_iters, us7))
-    st64 = (ctypes.c_longlong * 64)()
-    _lib.check(lib.tt2_debug_stamps(eng.h, st64))
-    stamps = {"prenet": [st64[i] - st64[0] for i in range(6)],
-              "energy": [st64[i] - st64[8] for i in range(8, 13)],
-              "lstm": [st64[i] - st64[16] for i in range(16, 20)]}
-    H, P = hp.decoder_lstm_units, hp.prenet_layers[0]
-    E2 = 2 * hp.encoder_lstm_units
-    by = 0.5 * (lstm_bytes(P + E2, H) + lstm_bytes(H, H))
-    lstm_us = us7[1]
-    achieved = by / (lstm_us * 1e-6) / 1e9
-    traffic = load_traffic("k_lstm")
-    roofline = dict(kernel="k_lstm (decoder Zoneout-LSTM, layers 1/2 alternating)", bound="hbm",
-                    achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                    algorithmic_bytes_per_launch=int(by), avg_launch_us=round(lstm_us, 3),
-                    decode_step_prenet_stamps=dec_stamps,
-                    per_kernel_us=dict(zip(["prenet", "lstm_avg", "query", "energy",
-                                            "softmax_context", "projection", "lstm2", "side_job_only",
-                                            "energy_only", "softmax_only"],
-                                           [round(v, 3) for v in us7])))
+        stamps = {"prenet": [st64[i] - st64[0] for i in range(6)],
+                  "energy": [st64[i] - st64[8] for i in range(8, 13)],
+                  "lstm": [st64[i] - st64[16] for i in range(16, 20)]}
+        H, P = hp.decoder_lstm_units, hp.prenet_layers[0]
+        E2 = 2 * hp.encoder_lstm_units
+        by = 0.5 * (lstm_bytes(P + E2, H) + lstm_bytes(H, H))
+        lstm_us = us7[1]
+        achieved = by / (lstm_us * 1e-6) / 1e9
+        traffic = load_traffic("k_lstm")
+        roofline = dict(kernel="k_lstm (decoder Zoneout-LSTM, layers 1/2 alternating)", bound="hbm",
+                        achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        algorithmic_bytes_per_launch=int(by), avg_launch_us=round(lstm_us, 3),
+                        per_kernel_us=dict(zip(["prenet", "lstm_avg", "query", "energy",
+                                                "softmax_context", "projection", "lstm2", "side_job_only",
+                                                "energy_only", "softmax_only"],
+                                               [round(v, 3) for v in us7])))
 
     # --- WaveNet (configs[2]) ---
     wn = None
@@ -296,7 +335,7 @@ def main():
                                decoded_steps=n_steps.value, ref_frames=a.ref_frames,
                                parallelism="utterance-batch sharding x{}".format(world)),
                    phases=phases, roofline=roofline, cpu_baseline=cpu, wavenet=wn,
-                   diag_stamps_cycles=stamps)
+                   diag_stamps=stamps)
         print(json.dumps(out))
     eng.close()
     if world > 1:

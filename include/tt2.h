@@ -149,8 +149,18 @@ tt2_status tt2_synthesize_dev(tt2_ctx* ctx, const int32_t* ids_d, const int32_t*
 tt2_status tt2_last_timings(tt2_ctx* ctx, float* ms3);
 tt2_status tt2_profile_decoder_kernels(tt2_ctx* ctx, int iters, float* avg_us10);
 /* s_memtime phase stamps (block 0) recorded during the last tt2_profile_decoder_kernels call:
- * [0..5] prenet, [8..12] energy, [16..19] lstm; diagnostic only. */
+ * [0..5] prenet, [8..12] energy, [16..19] lstm; or, after a persistent decode run with env
+ * TT2_STAMP_STEP=k, s_memrealtime (100 MHz) stamps [0..15] of work-group 0's stages at step k.
+ * Diagnostic only. */
 tt2_status tt2_debug_stamps(tt2_ctx* ctx, long long* out64);
+/* Which decoder implementation the context uses for its current shapes: *persistent = 1 for the
+ * single-launch persistent kernel (k_decode_persist: fork-default widths, B <= 32, T_in <= 256,
+ * a device with >= 256 CUs; env TT2_DECODER=launch forces 0), 0 for the per-step launch path;
+ * *kernel_ms = HIP-event duration of the last persistent decode launch (0 otherwise). */
+tt2_status tt2_decoder_path(tt2_ctx* ctx, int* persistent, float* kernel_ms);
+/* Persistent decode run with env TT2_STAMP_STEP=k: s_memrealtime (100 MHz) stamps [256 work-groups]
+ * [32 stage points] of step k (k_decode_persist PD_STAMP sites).  Diagnostic only. */
+tt2_status tt2_debug_pd_stamps(tt2_ctx* ctx, long long* out8192);
 
 /* ------------------------------------------------------------------------------------------ */
 /* WaveNet MoL vocoder (replaces wavenet_vocoder/models/wavenet.py WaveNet.initialize synthesis */

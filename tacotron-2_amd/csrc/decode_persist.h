@@ -1,0 +1,75 @@
+// Persistent Tacotron-2 decoder (gfx950): the whole dynamic_decode loop as ONE launch of 256
+// work-groups (one per CU) with the recurrent weights resident in registers and LDS.  See
+// decode_persist.hip for the schedule and DESIGN.md §5 for the roofline.
+#pragma once
+#include "common.h"
+
+namespace tt2 {
+
+// Fixed geometry of the persistent path (fork-default hparams, hparams.py:147-178).  Other shapes
+// run the per-step launch path in tacotron.hip.
+constexpr int PD_NB = 256;    // work-groups = LSTM column tiles (4 hidden units x 4 gates each)
+constexpr int PD_NT = 512;    // threads per work-group (8 waves, 2 per SIMD)
+constexpr int PD_H = 1024;    // decoder_lstm_units
+constexpr int PD_P = 256;     // prenet_units
+constexpr int PD_E2 = 512;    // encoder-output half of the attention memory
+constexpr int PD_A = 128;     // attention_dim
+constexpr int PD_NPJ = 96;    // frame (80) + stop (1) columns, padded to 16
+constexpr int PD_NPF = 352;   // + the prenet-L1 columns folded into the projection
+constexpr int PD_NTILE = 22;  // projection column tiles
+constexpr int PD_KSP = 8;     // projection K split (128 h2 rows + 64 context rows per split)
+constexpr int PD_TMAX = 256;  // max encoder steps (T_in)
+constexpr int PD_KLP = 32;    // location-conv taps padded to 16
+enum { PD_F_PRE = 0, PD_F_H1, PD_F_H2, PD_F_E, PD_F_CTX, PD_F_PP, PD_NPH };
+
+struct PdArgs {
+  unsigned* flags;  // [PD_NPH][PD_NB] hand-off tags (zeroed before every launch)
+  unsigned* flags2; // [PD_NPH][8 groups][32] group-level tags of the all-producer waits
+  int* ctl;         // [4]: done, n_steps, err, pad (zeroed before every launch)
+  int B, T_in, max_iters, T_lim, nm;
+  int stop_at_any, mask_encoder, cumulative, constraint, monotonic, win;
+  float zo, one_m_zo;
+  // weights (tacotron.hip finalize layouts)
+  const float* l1_w;    // [256 tiles][768 x 16] WF, rows [prenet | context_enc]
+  const float* l1_wh;   // [256][1024 x 16] recurrent rows
+  const float* l1_b;    // [4096] lstm column order
+  const float* l2_w;    // [256][1024 x 16] input rows (h1_new)
+  const float* l2_wh;   // [256][1024 x 16] recurrent rows
+  const float* l2_b;
+  const float* GS;      // [32][4096] style·W1[style rows] per utterance
+  const float* q_wt;    // [128][1024] query_layer kernel, transposed
+  const float* loc_cw;  // [8 tiles][32 x 16] WF (location conv folded through the location dense)
+  const float* va;      // [128] attention_variable_projection
+  const float* proj_w;  // [22 tiles][1536 x 16] WF, rows [h2 | context_enc]
+  const float* proj_b;  // [352]
+  const float* PS;      // [32][352] style·W_proj[style rows]
+  const float* pre_b1;  // [256] prenet L1 bias, AF-group column order
+  const float* pre_w2t; // [256 out][256 in] prenet layer-2 kernel, transposed
+  const float* pre_b2;  // [256]
+  const float* TP1;     // GTA: [B][T_lim][256] targets·W1 + b1 (AF-group order), or null
+  const float* keysT;   // [B][128][256] keys (+ b_a + b_conv·W_loc), encoder step fastest
+  const float* valuesT; // [B][512][256] encoder half of the values, encoder step fastest, 0 past T_in
+  const int* lengths;   // [B]
+  const uint8_t* masks; // [max_iters][2][B][256] prenet keep bits
+  // exchange buffers, two step parities each
+  float* H1x;   // [2][32 x 1024] AF: h1_new
+  float* H2x;   // [2][32 x 1024] AF: h2_new
+  float* Ex;    // [2][32 rows][8 slices][256 t]: partial energies
+  float* CTXx;  // [2][32 x 512] AF: context_enc
+  float* SSx;   // [2][32]: Σ_{t<len} alignments (style-context scale)
+  float* PPx;   // [2][8 splits][32 rows][352]: projection partials
+  float* PREx;  // [2][32 x 256] AF: prenet output of the next step
+  // outputs
+  float* frames;  // [B][max_iters][nm]
+  float* stop;    // [B][max_iters]
+  float* align;   // [B][T_in][max_iters] or null
+  long long* stamps;  // diagnostic s_memrealtime stamps of one step (null = off)
+  int stamp_step;
+};
+
+size_t pd_lds_bytes();
+// True when this device can keep all PD_NB work-groups resident at once.
+bool pd_device_ok(int dev);
+void pd_launch(const PdArgs& a, hipStream_t s);
+
+}  // namespace tt2

@@ -1,0 +1,757 @@
+// Persistent Tacotron-2 decoder for MI355X (gfx950): the whole dynamic_decode loop
+// (tacotron.py:349-354 over TacotronDecoderCell.__call__, Architecture_wrappers.py:197-267) as ONE
+// launch of 256 work-groups, one per CU.
+//
+// Why: at batch 32 the decoder step is a chain of small dependent GEMVs.  Streaming the 73 MB of
+// step weights from HBM every step bounds a per-launch design at ~13 us/step plus ~1.5 us per
+// kernel boundary.  The chip holds 256 x (512 KB VGPR + 160 KB LDS): every step weight fits
+// on-chip, so each work-group keeps its LSTM column tile resident (input rows in registers,
+// recurrent rows in LDS) and the per-step HBM traffic drops to the activations exchanged between
+// work-groups.
+//
+// Roles of work-group g (every work-group has all three):
+//   LSTM   hidden units [4g, 4g+4) of both layers = one 16-column gate tile (lstm_cols order)
+//   row    attention row b = (g&7)*4 + ((g>>3)&3), slice j = g>>5: attention dims [16j, 16j+16),
+//          context channels [64j, 64j+64), prenet-L2 outputs [32j, 32j+32).  The 8 siblings of a
+//          row have equal g%8 (one XCD under round-robin placement: faster, never required).
+//   proj   g < 176: frame/stop/prenet-L1 projection tile g%22, K split g/22
+//
+// One step t (tag = t+1, buffers by parity t&1).  "wait X" = poll the producers' X flags; every
+// payload byte is stored write-through (sc1) and drained before the flag, every read of it is an
+// sc1 load (MI355X_MICROARCH.md § visibility, Valid forms row 1).
+//   A  wait PRE(all)  [stop rule of t-1 from the flags' low bits]  L1 gates += prenet rows
+//      (context, style and recurrent terms were accumulated earlier) -> h1_new -> H1, flag H1
+//      tail: RG2 = (1-z)·h2_new(t-1)·W2h + z·RG2      (zoned-state recurrence, linear)
+//   B  wait H1(all)   L2 gates = h1_new·W2i + RG2 -> h2_new -> H2, flag H2
+//      tail: RG1 = (1-z)·h1_new(t)·W1h + z·RG1
+//   C  wait H2(all)   q_j = h2_new[b]·Wq[:, j-slice]; partial energies over all encoder steps -> E
+//      tail (proj blocks): projection partial += h2 rows of its K split
+//   D  wait E(row)    Σ_j energies, masks, softmax, cum/max_att, context slice -> CTX, flag CTX
+//      tail: location features of step t+1 (cum is local to the row's siblings)
+//   E  proj blocks: wait CTX(slice) -> projection partial += context rows -> PP, flag PP
+//   F  wait PP(all)   frame/stop (row), stop bit, prenet of step t+1 -> PRE, flag PRE|stop
+//      tail: wait CTX(all): L1 context rows for step t+1; Σ_{t<len} align of every row
+// Spins are bounded (2 s): a timeout or a peer's error makes every work-group exit and the host
+// reports TT2_ERR_HIP.
+#include "decode_persist.h"
+
+namespace tt2 {
+
+typedef __attribute__((address_space(1))) float pd_gf32;
+typedef __attribute__((address_space(1))) unsigned pd_gu32;
+typedef __attribute__((address_space(1))) int pd_gi32;
+#define PD_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+constexpr long long PD_TIMEOUT = 200000000LL;  // 2 s of s_memrealtime (100 MHz)
+constexpr int PD_LDS_FLOATS = 16384 * 2 + 4096 + 512 * 5 + 288 + 256 * 2 + 32 + 16 + 16 + 16;  // 157.6 KB
+
+// write-through (sc1) stores and L1-bypassing (sc1) loads of hand-off data
+__device__ __forceinline__ float pd_ld(const float* p) {
+  return __hip_atomic_load((pd_gf32*)const_cast<float*>(p), PD_RLX);
+}
+__device__ __forceinline__ void pd_st(float* p, float v) { __hip_atomic_store((pd_gf32*)p, v, PD_RLX); }
+__device__ __forceinline__ f32x4 pd_ld4(const float* base, int i4) {
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, i4 * 16, 0, 16));
+}
+
+// Wave-uniform bounded spin: poll until cond() holds on every lane.  false on timeout (2 s) or
+// when a peer reported a failure in ctl[2]; the failing phase is recorded there.
+template <class F>
+__device__ __forceinline__ bool pd_spin(const PdArgs& a, int ph, int lane, F cond) {
+  long long t0 = 0;
+  for (unsigned spin = 0;; ++spin) {
+    if (__all(cond())) return true;
+    if ((spin & 63) == 0) {
+      const long long now = __builtin_amdgcn_s_memrealtime();
+      if (spin == 0) {
+        t0 = now;
+      } else if (__hip_atomic_load((pd_gi32*)(a.ctl + 2), PD_RLX) != 0 || now - t0 > PD_TIMEOUT) {
+        if (lane == 0) __hip_atomic_store((pd_gi32*)(a.ctl + 2), 1 + ph, PD_RLX);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ unsigned pd_flag(const unsigned* f) {
+  return __hip_atomic_load((pd_gu32*)const_cast<unsigned*>(f), PD_RLX);
+}
+
+// Wave-level poll: every flag f[base + i*stride] (i < n <= 64) of phase ph has (v >> shift) >= need.
+__device__ __forceinline__ bool pd_poll(const PdArgs& a, int ph, int base, int stride, int n, unsigned need, int shift,
+                                        int lane) {
+  const unsigned* f = a.flags + ph * PD_NB + base;
+  return pd_spin(a, ph, lane, [&] { return lane >= n || (pd_flag(f + lane * stride) >> shift) >= need; });
+}
+
+// Wave-level poll for ALL producers g < nprod of phase ph, two-level so that no flag line has more
+// than 32 pollers (256 pollers on one line serialise at its memory channel, ~3 us per hop): group
+// x = g%8, slot s = g/8 first waits for producers [8s, 8s+8) and raises its group flag
+// flags2[ph][x][s]; then it waits for the 32 group flags of its own group x.
+__device__ __forceinline__ bool pd_poll_all(const PdArgs& a, int ph, int nprod, unsigned need, int shift, int lane) {
+  const int g = blockIdx.x, x = g & 7, s = g >> 3;
+  const unsigned* f = a.flags + ph * PD_NB + 8 * s;
+  unsigned* f2 = a.flags2 + ph * PD_NB + 32 * x;
+  if (!pd_spin(a, ph, lane, [&] { return lane >= 8 || 8 * s + lane >= nprod || (pd_flag(f + lane) >> shift) >= need; }))
+    return false;
+  if (lane == 0) __hip_atomic_store((pd_gu32*)(f2 + s), need, PD_RLX);
+  return pd_spin(a, ph, lane, [&] { return lane >= 32 || pd_flag(f2 + lane) >= need; });
+}
+
+// Every storing wave drains its sc1 stores, then one lane raises this work-group's flag.
+__device__ __forceinline__ void pd_publish(const PdArgs& a, int ph, unsigned val, int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store((pd_gu32*)(a.flags + ph * PD_NB + blockIdx.x), val, PD_RLX);
+}
+
+// acc(rows 0..15 | 16..31) += A(k-group) · W(k-group, 16 columns)
+__device__ __forceinline__ void kg_mfma(const f32x4& a0, const f32x4& a1, const f32x4& bw, f32x4& c0, f32x4& c1) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[e], bw[e], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[e], bw[e], c1, 0, 0, 0);
+  }
+}
+
+// Partial tile of wave w -> red[w][32][16] (the MFMA D layout transposed to row-major).
+__device__ __forceinline__ void put_partials(const f32x4& acc0, const f32x4& acc1, float* red, int w, int lane) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int n = lane & 15, m = (lane >> 4) * 4 + r;
+    red[w * 512 + m * 16 + n] = acc0[r];
+    red[w * 512 + (m + 16) * 16 + n] = acc1[r];
+  }
+}
+template <int NW>
+__device__ __forceinline__ float sum_partials(const float* red, int idx) {
+  float v = red[idx];
+#pragma unroll
+  for (int ww = 1; ww < NW; ++ww) v += red[ww * 512 + idx];
+  return v;
+}
+
+// Barrier of the 4 tail waves (4..7) through an LDS counter: the chain waves never take part, so
+// a tail job can finish its reduction while wave 0 is still polling.
+__device__ __forceinline__ void tail_bar(int* ctr, unsigned& gen, int lane) {
+  gen += 4;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while ((unsigned)__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen)
+    __builtin_amdgcn_s_sleep(0);
+}
+
+#define PD_STAMP(i)                                                                   \
+  do {                                                                                \
+    if (stp && tid == 0) stp[g * 32 + (i)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+
+__global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* const sW1h = sm;              // [64 kg][64 lanes] f32x4: W1 recurrent rows of this tile
+  float* const sW2h = sm + 16384;      // same for W2
+  float* const red = sm + 32768;       // [8][512] partial tiles / stage scratch (tail jobs: during waits)
+  float* const G = red + 4096;         // [32][16] spare tile
+  float* const RG1 = G + 512;          // [32][16] zoned-h1 recurrent gate terms of the next L1
+  float* const RG2 = RG1 + 512;        // same for L2
+  float* const RGc = RG2 + 512;        // [32][16] context rows of the next L1
+  float* const PPh = RGc + 512;        // [32][16] projection partial, h2 rows (proj blocks)
+  float* const cw = PPh + 512;         // [15 + T + 16] cumulative alignments, zero padded (location conv)
+  float* const al = cw + 288;          // [256] alignments of the step
+  float* const x1 = al + 256;          // [256] prenet layer-1 output of the row
+  float* const ssa = x1 + 256;         // [32] Σ_{t<len} align of every row (last step)
+  float* const qv = ssa + 32;          // [16] query slice
+  float* const sc = qv + 16;           // softmax max / sum, Σ_{t<len} align of this row
+  int* const si = reinterpret_cast<int*>(sc + 16);  // [0] max_att [1] done [2] wait result [3] tail ok [4] tail ctr
+  const int g = blockIdx.x, tid_ = threadIdx.x;
+  const int b = (g & 7) * 4 + ((g >> 3) & 3), j = g >> 5;
+  const bool rowv = b < a.B;
+  const bool isproj = g < PD_NTILE * PD_KSP;
+  const int pn = g % PD_NTILE, pks = g / PD_NTILE;
+  const int T = a.T_in;
+  const int sib0 = (b >> 2) + 8 * (b & 3);  // siblings of row b: sib0 + 32*jj
+  long long* const stp0 = a.stamps;
+
+  // ---------------- prologue: resident weights and per-row constants ----------------
+  const int tid = tid_, lane = tid & 63, w = tid >> 6;
+  const int tw = (w - 4) & 3;                    // tail-wave index (waves 4..7)
+  const int em = (tid >> 2) & 31, eu = tid & 3;  // LSTM epilogue thread (tid < 128) -> row, unit
+  f32x4 w1p[2], w2i[8];                          // chain: L1 prenet rows, L2 input rows (8 waves)
+  {
+    const f32x4* L1 = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * (PD_P + PD_E2) * 16);
+    const f32x4* L2 = reinterpret_cast<const f32x4*>(a.l2_w + (long)g * PD_H * 16);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) w1p[i] = L1[(2 * w + i) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w2i[i] = L2[(8 * w + i) * 64 + lane];
+    const f32x4* L1h = reinterpret_cast<const f32x4*>(a.l1_wh + (long)g * PD_H * 16);
+    const f32x4* L2h = reinterpret_cast<const f32x4*>(a.l2_wh + (long)g * PD_H * 16);
+    f32x4* d1 = reinterpret_cast<f32x4*>(sW1h);
+    f32x4* d2 = reinterpret_cast<f32x4*>(sW2h);
+    for (int e = tid; e < PD_H * 4; e += PD_NT) {
+      d1[e] = L1h[e];
+      d2[e] = L2h[e];
+    }
+  }
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 wpc = zero4;
+  if (isproj && w < 4) {
+    const f32x4* PW = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16);
+    wpc = PW[(PD_H / 16 + 4 * pks + w) * 64 + lane];
+  }
+  // tail-job weights streamed from L2 each step (1.25 MB per XCD, L2-resident): L1 context rows
+  // (k-groups [8 tw, 8 tw + 8) of the tile's context block) and projection h2 rows
+  const f32x4* const W1C = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * (PD_P + PD_E2) * 16) + (PD_P / 16 + 8 * tw) * 64;
+  const f32x4* const WPH = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16) + (8 * pks + 2 * tw) * 64;
+  f32x4 wl[2];
+  {
+    const f32x4* LW = reinterpret_cast<const f32x4*>(a.loc_cw + (long)j * PD_KLP * 16);
+    wl[0] = LW[lane];
+    wl[1] = LW[64 + lane];
+  }
+  float b1v[4], b2v[4], gsv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int col = g * 16 + 4 * q + eu;
+    b1v[q] = a.l1_b[col];
+    b2v[q] = a.l2_b[col];
+    gsv[q] = a.GS[(long)em * 4 * PD_H + col];
+  }
+  float c1 = 0.f, c2 = 0.f;  // cell states of (em, unit 4g+eu), threads < 128
+  const int len = rowv ? a.lengths[b] : 0;
+  const float va_k = a.va[16 * j + (lane & 15)];
+  const float b2p = a.pre_b2[32 * j + (tid & 31)];
+  for (int e = tid; e < 512; e += PD_NT) {
+    RG1[e] = 0.f;
+    RG2[e] = 0.f;
+    RGc[e] = 0.f;  // context(-1) = 0
+  }
+  for (int e = tid; e < 288; e += PD_NT) cw[e] = 0.f;
+  if (tid < 256) al[tid] = 0.f;
+  if (tid < 32) ssa[tid] = 0.f;
+  if (tid == 0) {
+    si[0] = 0;
+    si[4] = 0;
+    sc[2] = 0.f;
+  }
+  unsigned tgen = 0;  // tail-barrier generation (waves 4..7)
+  f32x4 vals[8];  // values[b][32*(tid/64) + 4i + e][64j + tid%64]: valuesT is [B][E2][256], 0 past T_in
+  {
+    const f32x4* V = reinterpret_cast<const f32x4*>(a.valuesT + ((long)(rowv ? b : 0) * PD_E2 + 64 * j + (tid & 63)) * PD_TMAX +
+                                                    32 * (tid >> 6));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vals[i] = V[i];
+  }
+  f32x4 loc[2] = {zero4, zero4};  // location features of the next step (cum = 0)
+  const long BP = (long)a.B * PD_P;
+
+  // Prenet (modules.py:346-357, dropout always on) of decoder step ts for row b, outputs
+  // [32j, 32j+32).  Layer-1 work runs on threads 256..511 (position tid-256, AF-group column order
+  // of the folded pre-activations) so wave 0 -- the poller -- never waits on the keep-bit loads.
+  struct PrenetOps {
+    float keep1, keep2;
+    f32x4 w2p[4];  // W2[16*(tid/32) + 4i + e][32j + tid%32] (pre_w2t is [P][P] transposed; L2-resident)
+  };
+  auto prenet_keep = [&](int ts, int tid, float& k1, float& k2) {
+    k1 = k2 = 0.f;
+    if (rowv && ts < a.max_iters && tid >= 256) {
+      const int pos = tid - 256;
+      const int col = 16 * (pos >> 4) + ((pos >> 2) & 3) + 4 * (pos & 3);
+      k1 = (float)a.masks[(long)ts * 2 * BP + (long)b * PD_P + col];
+      if (pos < 32) k2 = (float)a.masks[((long)ts * 2 + 1) * BP + (long)b * PD_P + 32 * j + pos];
+    }
+  };
+  auto prenet_ops = [&](float k1, float k2, int tid) {
+    PrenetOps o;
+    o.keep1 = k1;
+    o.keep2 = k2;
+    const f32x4* W2 = reinterpret_cast<const f32x4*>(a.pre_w2t + (long)(32 * j + (tid & 31)) * PD_P + 16 * (tid >> 5));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o.w2p[i] = W2[i];
+    return o;
+  };
+  auto prenet = [&](const PrenetOps& o, auto pre1, int par, int tid) {
+    if (tid >= 256) {
+      const int pos = tid - 256;
+      const int col = 16 * (pos >> 4) + ((pos >> 2) & 3) + 4 * (pos & 3);  // af_group_col(pos)
+      x1[col] = rowv ? (fmaxf(pre1(pos), 0.f) / 0.5f) * o.keep1 : 0.f;
+      if (pos < 32) red[3072 + pos] = o.keep2;  // layer-2 keep bits -> the 32 output threads
+    }
+    __syncthreads();
+    {
+      const int k16 = tid >> 5;
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s += x1[16 * k16 + i] * o.w2p[i >> 2][i & 3];
+      red[k16 * 32 + (tid & 31)] = s;
+    }
+    __syncthreads();
+    if (tid < 32) {
+      float v = 0.f;
+#pragma unroll
+      for (int k16 = 0; k16 < 16; ++k16) v += red[k16 * 32 + tid];
+      const int n = 32 * j + tid;
+      const float out = rowv ? (fmaxf(v + b2p, 0.f) / 0.5f) * red[3072 + tid] : 0.f;
+      pd_st(a.PREx + par * 32 * PD_P + af_idx(b, n), out);
+    }
+  };
+
+  // One wait window: wave 0 polls (block-uniform result), tail waves 4..7 run `tail`, then the
+  // whole work-group meets at a barrier.
+  auto window = [&](int w_, auto poll, auto tail) -> bool {
+    if (w_ == 0) {
+      const bool ok = poll();
+      if ((threadIdx.x & 63) == 0) si[2] = ok;
+    } else if (w_ >= 4) {
+      tail();
+    }
+    __syncthreads();
+    const bool ok = si[2] != 0;
+    return ok;
+  };
+  auto no_tail = [] {};
+
+  // Tail reduction of the 4 tail waves' tiles: RG = (1-z)·Σ + z·RG (zoned-state recurrence) or a
+  // plain store (mix = false).
+  auto tail_reduce = [&](const f32x4& t0, const f32x4& t1, float* dst, bool mix, int tid) {
+    put_partials(t0, t1, red, tw, tid & 63);
+    tail_bar(si + 4, tgen, tid & 63);
+    for (int idx = tid - 256; idx < 512; idx += 256) {
+      const float v = sum_partials<4>(red, idx);
+      dst[idx] = mix ? a.one_m_zo * v + a.zo * dst[idx] : v;
+    }
+  };
+
+  // Tail job: X rows (AF, k-groups [16 tw, 16 tw + 16)) · W (LDS tiles) of one tail wave.
+  auto rec_job = [&](const float* X, const float* Wl, f32x4& t0, f32x4& t1, int lane) {
+    const f32x4* Wv = reinterpret_cast<const f32x4*>(Wl);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      f32x4 x0[4], x1v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int sg = 16 * tw + 4 * h + i;
+        x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
+        x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int sg = 16 * tw + 4 * h + i;
+        kg_mfma(x0[i], x1v[i], Wv[sg * 64 + lane], t0, t1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // Tail job: L1 context rows of step t (context(t-1) of every row, once all slices landed) and
+  // the rows' style scales.
+  auto ctx_job = [&](int pprev, unsigned tgprev, int lane, int tid) {
+    f32x4 w1c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w1c[i] = W1C[i * 64 + lane];
+    if (tw == 0) {
+      const bool ok = pd_poll_all(a, PD_F_CTX, PD_NB, tgprev, 0, lane);
+      if (lane == 0) si[3] = ok;
+    }
+    tail_bar(si + 4, tgen, lane);
+    if (!si[3]) return;
+    const float* X = a.CTXx + pprev * 32 * PD_E2;
+    f32x4 s0 = zero4, s1 = zero4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4 x0[4], x1v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int sg = 8 * tw + 4 * h + i;
+        x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
+        x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) kg_mfma(x0[i], x1v[i], w1c[4 * h + i], s0, s1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    tail_reduce(s0, s1, RGc, false, tid);
+    if (tid - 256 < 32) ssa[tid - 256] = pd_ld(a.SSx + pprev * 32 + (tid - 256));
+  };
+  __syncthreads();
+  // GO frame (helpers.py:136-138): frame 0 -> layer-1 pre-activation = b1
+  {
+    float k1, k2;
+    prenet_keep(0, tid, k1, k2);
+    prenet(prenet_ops(k1, k2, tid), [&](int pos) { return a.pre_b1[pos]; }, 0, tid);
+  }
+  pd_publish(a, PD_F_PRE, 1u << 1, tid);
+
+  for (int t = 0; t < a.max_iters; ++t) {
+    const unsigned tg = t + 1;
+    const int p = t & 1;
+    long long* const stp = (stp0 && t == a.stamp_step) ? stp0 : nullptr;
+    // Thread indices re-derived from an opaque copy every step: otherwise every loop-invariant
+    // LDS/global address of the body is hoisted out of the step loop and spilled.
+    int tid = tid_, lane, w, em, eu;
+    asm volatile("" : "+v"(tid));
+    lane = tid & 63;
+    w = tid >> 6;
+    em = (tid >> 2) & 31;
+    eu = tid & 3;
+    PD_STAMP(0);
+    float keep1n, keep2n;  // prenet keep bits of step t+1, in flight during the whole step
+    prenet_keep(t + 1, tid, keep1n, keep2n);
+    // ================= A: LSTM layer 1 =================
+    // tail: L1 context rows of this step (context(t-1)), style scales
+    if (!window(w, [&] { return pd_poll_all(a, PD_F_PRE, PD_NB, tg, 1, lane); },
+                [&] {
+                  if (t > 0) ctx_job(p ^ 1, tg - 1, lane, tid);
+                }))
+      return;
+    PD_STAMP(1);
+    if (t > 0 && w == 0) {
+      // stop rule of step t-1 (TacoTestHelper.next_inputs, helpers.py:40-59 + dynamic_decode):
+      // every valid row rounds to 1 (stop_at_any: any row); GTA stops at T_targets instead
+      int dn;
+      if (a.T_lim > 0) {
+        dn = t >= a.T_lim;
+      } else {
+        const int gg = lane & 31, bb = (gg & 7) * 4 + ((gg >> 3) & 3);
+        const unsigned v = pd_flag(a.flags + PD_F_PRE * PD_NB + gg);
+        const bool valid = lane < 32 && bb < a.B;
+        const unsigned long long fb = __ballot(valid && (v & 1u)), vb = __ballot(valid);
+        dn = a.stop_at_any ? (fb != 0ull) : (fb == vb);
+      }
+      if (lane == 0) si[1] = dn;
+    }
+    __syncthreads();
+    if (t > 0 && si[1]) {
+      if (g == 0 && tid == 0) {
+        a.ctl[1] = t;
+        a.ctl[0] = 1;
+      }
+      return;
+    }
+    {
+      const float* X = a.PREx + p * 32 * PD_P;
+      f32x4 a0[2], a1[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int sg = 2 * w + i;
+        a0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
+        a1[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
+      }
+      f32x4 s0 = zero4, s1 = zero4;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) kg_mfma(a0[i], a1[i], w1p[i], s0, s1);
+      PD_STAMP(18);
+      put_partials(s0, s1, red, w, lane);
+      __syncthreads();
+      PD_STAMP(19);
+    }
+    if (tid < 128) {
+      float z[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int idx = em * 16 + 4 * q + eu;
+        z[q] = (((sum_partials<8>(red, idx) + RGc[idx]) + RG1[idx]) + ssa[em] * gsv[q]) + b1v[q];
+      }
+      const float cn = sigm(z[2] + 1.0f) * c1 + sigm(z[0]) * tanhf(z[1]);
+      const float hn = sigm(z[3]) * tanhf(cn);
+      c1 = a.one_m_zo * cn + a.zo * c1;
+      pd_st(a.H1x + p * 32 * PD_H + af_idx(em, 4 * g + eu), hn);
+    }
+    pd_publish(a, PD_F_H1, tg, tid);
+    PD_STAMP(2);
+    // ================= B: LSTM layer 2 =================
+    // tail: RG2(t) = (1-z)·h2_new(t-1)·W2h + z·RG2(t-1)
+    if (!window(w, [&] { return pd_poll_all(a, PD_F_H1, PD_NB, tg, 0, lane); },
+                [&] {
+                  if (t > 0) {
+                    f32x4 s0 = zero4, s1 = zero4;
+                    rec_job(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, s0, s1, lane);
+                    tail_reduce(s0, s1, RG2, true, tid);
+                  }
+                }))
+      return;
+    PD_STAMP(4);
+    {
+      const float* X = a.H1x + p * 32 * PD_H;
+      f32x4 s0 = zero4, s1 = zero4;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 x0[4], x1v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int sg = 8 * w + 4 * h + i;
+          x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
+          x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) kg_mfma(x0[i], x1v[i], w2i[4 * h + i], s0, s1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      PD_STAMP(16);
+      put_partials(s0, s1, red, w, lane);
+      __syncthreads();
+      PD_STAMP(17);
+    }
+    if (tid < 128) {
+      float z[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int idx = em * 16 + 4 * q + eu;
+        z[q] = (sum_partials<8>(red, idx) + RG2[idx]) + b2v[q];
+      }
+      const float cn = sigm(z[2] + 1.0f) * c2 + sigm(z[0]) * tanhf(z[1]);
+      const float hn = sigm(z[3]) * tanhf(cn);
+      c2 = a.one_m_zo * cn + a.zo * c2;
+      pd_st(a.H2x + p * 32 * PD_H + af_idx(em, 4 * g + eu), hn);
+    }
+    pd_publish(a, PD_F_H2, tg, tid);
+    PD_STAMP(5);
+    // ================= C: query slice + partial energies (attention.py:37-69, 186-201) =================
+    // issued ahead of the H2 wait (L2-resident: shared by the 32 rows of slice j):
+    f32x4 wq[8];  // W_q[32*(tid/16) + 4i + e][16j + tid%16] (q_wt is [A][H])
+    {
+      const f32x4* Q = reinterpret_cast<const f32x4*>(a.q_wt + (long)(16 * j + (tid & 15)) * PD_H + 32 * (tid >> 4));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) wq[i] = Q[i];
+    }
+    f32x4 kv[2];  // keys[b][t0 + r][16j + lane%16], t0 = 16(w + 8i) + 4(lane/16): keysT is [B][A][256]
+    {
+      const f32x4* K = reinterpret_cast<const f32x4*>(a.keysT + ((long)(rowv ? b : 0) * PD_A + 16 * j + (lane & 15)) * PD_TMAX);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) kv[i] = K[(w + 8 * i) * 4 + (lane >> 4)];
+    }
+    // tail: RG1(t+1) = (1-z)·h1_new(t)·W1h + z·RG1(t)
+    if (!window(w, [&] { return pd_poll_all(a, PD_F_H2, PD_NB, tg, 0, lane); },
+                [&] {
+                  f32x4 s0 = zero4, s1 = zero4;
+                  rec_job(a.H1x + p * 32 * PD_H, sW1h, s0, s1, lane);
+                  tail_reduce(s0, s1, RG1, true, tid);
+                }))
+      return;
+    PD_STAMP(7);
+    if (rowv) {
+      const float* X = a.H2x + p * 32 * PD_H;
+      red[tid] = pd_ld(X + af_idx(b, tid));
+      red[tid + 512] = pd_ld(X + af_idx(b, tid + 512));
+      __syncthreads();
+      {
+        const int k = tid & 15, seg = tid >> 4;
+        float s = 0.f;
+#pragma unroll
+        for (int ii = 0; ii < 32; ++ii) s += red[seg * 32 + ii] * wq[ii >> 2][ii & 3];
+        red[1024 + seg * 16 + k] = s;
+      }
+      __syncthreads();
+      if (tid < 16) {
+        float q = 0.f;
+        for (int s2 = 0; s2 < 32; ++s2) q += red[1024 + s2 * 16 + tid];
+        qv[tid] = q;
+      }
+      __syncthreads();
+      const float qk = qv[lane & 15];
+      float* E = a.Ex + (((long)p * 32 + b) * 8 + j) * PD_TMAX;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = sum16(va_k * tanh_fast(kv[i][r] + qk + loc[i][r]));
+          if ((lane & 15) == 0) pd_st(E + (w + 8 * i) * 16 + (lane >> 4) * 4 + r, e);
+        }
+    }
+    pd_publish(a, PD_F_E, tg, tid);
+    PD_STAMP(8);
+    // ================= D: softmax, cumulative alignments, context (attention.py:10-35, 202-227) ==========
+    // tail: projection partial of this split's h2_new rows (proj blocks, Architecture_wrappers.py:243-247)
+    if (!window(w, [&] { return pd_poll(a, PD_F_E, sib0, 32, 8, tg, 0, lane); },
+                [&] {
+                  if (isproj) {
+                    const float* X = a.H2x + p * 32 * PD_H;
+                    const f32x4 wph[2] = {WPH[lane], WPH[64 + lane]};
+                    f32x4 s0 = zero4, s1 = zero4;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                      const int sg = 8 * pks + 2 * tw + i;
+                      kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wph[i], s0, s1);
+                    }
+                    tail_reduce(s0, s1, PPh, false, tid);
+                  }
+                }))
+      return;
+    PD_STAMP(9);
+    if (rowv) {
+      const float* E = a.Ex + ((long)p * 32 + b) * 8 * PD_TMAX;
+      if (tid < PD_TMAX) {
+        float e = -INFINITY;
+        if (tid < T) {
+          e = 0.f;
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) e += pd_ld(E + jj * PD_TMAX + tid);
+          if (a.constraint) {  // synthesis window (attention.py:202-215)
+            const int pm = si[0], wn = a.win;
+            bool masked;
+            if (a.monotonic) masked = (tid < pm) || (tid >= pm + wn);
+            else masked = (tid < pm - (wn / 2 + (wn % 2 != 0 ? 1 : 0))) || (tid >= pm + wn / 2);
+            if (masked) e = -4294967296.0f;  // -2**32 + 1 in fp32
+          }
+          if (a.mask_encoder && tid >= len) e = -INFINITY;
+        }
+        red[tid] = e;
+      }
+      __syncthreads();
+      if (w == 0) {
+        float mx = -INFINITY;
+        for (int i = lane; i < T; i += 64) mx = fmaxf(mx, red[i]);
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        float sum = 0.f;
+        for (int i = lane; i < T; i += 64) sum += expf(red[i] - mx);
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        if (lane == 0) {
+          sc[0] = mx;
+          sc[1] = sum;
+        }
+      }
+      __syncthreads();
+      PD_STAMP(21);
+      if (tid < PD_TMAX) al[tid] = tid < T ? expf(red[tid] - sc[0]) / sc[1] : 0.f;
+      __syncthreads();
+      if (tid < T) {
+        const float cp = cw[15 + tid];
+        cw[15 + tid] = a.cumulative ? al[tid] + cp : al[tid];
+        if (j == 0 && a.align) a.align[((long)b * T + tid) * a.max_iters + t] = al[tid];
+      }
+      if (w == 1) {  // max_att = argmax (ties -> first), Σ_{t<len} alignments
+        float best = -INFINITY, ss = 0.f;
+        int bi = 0x7fffffff;
+        for (int i = lane; i < T; i += 64) {
+          if (al[i] > best) {
+            best = al[i];
+            bi = i;
+          }
+          if (i < len) ss += al[i];
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          const float ob = __shfl_xor(best, o);
+          const int oi = __shfl_xor(bi, o);
+          if (ob > best || (ob == best && oi < bi)) {
+            best = ob;
+            bi = oi;
+          }
+          ss += __shfl_xor(ss, o);
+        }
+        if (lane == 0) {
+          si[0] = bi;
+          sc[2] = ss;
+        }
+      }
+      {
+        const int c = tid & 63, ts = tid >> 6;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) s += al[ts * 32 + i] * vals[i >> 2][i & 3];
+        red[ts * 64 + c] = s;
+      }
+      __syncthreads();
+      if (tid < 64) {
+        float s = 0.f;
+#pragma unroll
+        for (int ts = 0; ts < 8; ++ts) s += red[ts * 64 + tid];
+        pd_st(a.CTXx + p * 32 * PD_E2 + af_idx(b, 64 * j + tid), s);
+      }
+      if (tid == 64 && j == 0) pd_st(a.SSx + p * 32 + b, sc[2]);
+    } else {
+      if (tid < 64) pd_st(a.CTXx + p * 32 * PD_E2 + af_idx(b, 64 * j + tid), 0.f);
+      if (tid == 64 && j == 0) pd_st(a.SSx + p * 32 + b, 0.f);
+    }
+    pd_publish(a, PD_F_CTX, tg, tid);
+    PD_STAMP(10);
+    // location features of step t+1: im2col(cum) · (W_conv·W_loc) on MFMA (attention.py:59-62)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int t0 = (w + 8 * i) * 16 + (lane & 15) + (lane >> 4);
+      f32x4 l = zero4;
+#pragma unroll
+      for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          l = __builtin_amdgcn_mfma_f32_16x16x4f32(cw[t0 + 16 * sg + 4 * e], wl[sg][e], l, 0, 0, 0);
+      loc[i] = l;
+    }
+    // ================= E: projection partial, context rows =================
+    if (isproj) {
+      if (!window(w, [&] { return pd_poll(a, PD_F_CTX, 32 * pks, 1, 32, tg, 0, lane); }, no_tail)) return;
+      PD_STAMP(11);
+      f32x4 s0 = zero4, s1 = zero4;
+      if (w < 4) {
+        const float* X = a.CTXx + p * 32 * PD_E2;
+        const int sg = 4 * pks + w;
+        kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wpc, s0, s1);
+        put_partials(s0, s1, red, w, lane);
+      }
+      __syncthreads();
+      {
+        const int m = tid >> 4, col = tid & 15;
+        pd_st(a.PPx + (((long)p * PD_KSP + pks) * 32 + m) * PD_NPF + 16 * pn + col, sum_partials<4>(red, tid) + PPh[tid]);
+      }
+      pd_publish(a, PD_F_PP, tg, tid);
+      PD_STAMP(12);
+    }
+    // ================= F: frame / stop (modules.py:392-448), prenet of step t+1 =================
+    const PrenetOps pops = prenet_ops(keep1n, keep2n, tid);
+    if (!window(w, [&] { return pd_poll_all(a, PD_F_PP, PD_NTILE * PD_KSP, tg, 0, lane); }, no_tail)) return;
+    PD_STAMP(13);
+    int stopbit = 0;
+    if (rowv) {
+      if (tid < PD_NPF) {
+        float v = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < PD_KSP; ++ks) v += pd_ld(a.PPx + (((long)p * PD_KSP + ks) * 32 + b) * PD_NPF + tid);
+        red[tid] = (v + sc[2] * a.PS[(long)b * PD_NPF + tid]) + a.proj_b[tid];
+      }
+      __syncthreads();
+      PD_STAMP(20);
+      const float sv = sigm(red[a.nm]);
+      if (j == 0) {
+        if (tid < a.nm) a.frames[((long)b * a.max_iters + t) * a.nm + tid] = red[tid];
+        if (tid == a.nm) a.stop[(long)b * a.max_iters + t] = sv;
+      }
+      stopbit = rintf(sv) == 1.0f;
+    }
+    if (t + 1 < a.max_iters) {
+      if (a.TP1) {  // GTA (TacoTrainingHelper): the next input is the teacher frame t
+        const float* tp = a.TP1 + ((long)b * a.T_lim + min(t, a.T_lim - 1)) * PD_P;
+        prenet(pops, [&](int pos) { return tp[pos]; }, p ^ 1, tid);
+      } else {  // free running: frame t through the folded layer-1 columns of the projection
+        prenet(pops, [&](int pos) { return red[PD_NPJ + pos]; }, p ^ 1, tid);
+      }
+    }
+    pd_publish(a, PD_F_PRE, ((tg + 1) << 1) | (unsigned)stopbit, tid);
+    PD_STAMP(14);
+  }
+  if (g == 0 && tid == 0) {
+    a.ctl[1] = a.max_iters;
+    a.ctl[0] = 1;
+  }
+}
+
+size_t pd_lds_bytes() { return sizeof(float) * (size_t)PD_LDS_FLOATS; }
+
+bool pd_device_ok(int dev) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+  if (prop.multiProcessorCount < PD_NB) return false;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_decode_persist),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)pd_lds_bytes()) != hipSuccess)
+    return false;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_persist, PD_NT, pd_lds_bytes()) != hipSuccess)
+    return false;
+  return nb >= 1;
+}
+
+void pd_launch(const PdArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_decode_persist, dim3(PD_NB), dim3(PD_NT), pd_lds_bytes(), s, a);
+  TT2_HIP(hipGetLastError());
+}
+
+}  // namespace tt2

@@ -13,6 +13,7 @@
 #include <tuple>
 
 #include "common.h"
+#include "decode_persist.h"
 #include "gemm.h"
 
 namespace tt2 {
@@ -919,6 +920,20 @@ __global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t
   }
 }
 
+// Encoder-step-fastest copies of keys / values for the persistent decoder:
+// dst[b][c][t] = src[b][t][c] (t < T, c < C; row stride ld), 0 for T <= t < 256.
+__global__ void k_transpose_bt(const float* __restrict__ src, long ld, float* __restrict__ dst, int T, int C) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z, c0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int r = ty; r < 32; r += 8) {
+    const int t = t0 + r;
+    tile[r][tx] = t < T ? src[((long)b * T + t) * ld + c0 + tx] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) dst[((long)b * C + c0 + r) * 256 + t0 + tx] = tile[tx][r];
+}
+
 // decoder_output clip (tacotron.py:362-363): dst[b][t][n] = clip(src[b][t][n])
 __global__ void k_clip_frames(const float* __restrict__ src, long src_bstride, float* __restrict__ dst, int B,
                               int T, int nm, float lo, float hi, int do_clip) {
@@ -984,6 +999,13 @@ struct tt2_ctx {
   int side_delay = 1, side_delay2 = 0;  // TT2_SIDE_DELAY / TT2_SIDE_DELAY2 env (energy / softmax host)
   hipEvent_t sev[8] = {nullptr};     // capture-time fork/join events
   bool have_args = false;
+  // persistent decoder (decode_persist.hip)
+  int pd_mode = 1;        // TT2_DECODER env: 1 persistent when the shapes fit, 0 launch path only
+  bool pd_dev_ok = false; // all PD_NB work-groups can be resident on this device
+  bool last_pd = false;   // the last decode ran the persistent kernel
+  tt2::DevBuf q_wt, pre_w2t, keysT, valuesT, pd_ctl, H1x, H2x, Ex, CTXx, SSx, PPx, PREx;
+  hipEvent_t pd_ev[2] = {nullptr, nullptr};
+  float pd_kernel_ms = 0.f;
 };
 
 namespace tt2 {
@@ -1122,6 +1144,10 @@ static void finalize(tt2_ctx* c) {
     const auto& w2 = need(wm, P + "decoder/decoder_prenet/dense_2/kernel", {c->P, c->P});
     upload(c->pre_w2, pack_wf(w2.data.data(), c->P, c->P, cols, c->P));
     upload(c->pre_b2, need(wm, P + "decoder/decoder_prenet/dense_2/bias", {c->P}));
+    std::vector<float> w2t((size_t)c->P * c->P);  // [out][in] for the persistent decoder
+    for (int k = 0; k < c->P; ++k)
+      for (int n = 0; n < c->P; ++n) w2t[(size_t)n * c->P + k] = w2.data[(size_t)k * c->P + n];
+    upload(c->pre_w2t, w2t);
   }
   for (int l = 0; l < 2; ++l) {
     // layer 1 rows: [prenet P | context_enc E2 | context_style SW | h H]; layer 2 rows: [h1_new H | h H]
@@ -1150,6 +1176,10 @@ static void finalize(tt2_ctx* c) {
     for (int j = 0; j < c->A; ++j) cols.push_back(j);
     const auto& q = need(wm, P + "decoder/query_layer/kernel", {c->H, c->A});
     upload(c->q_w, pack_wf(q.data.data(), c->H, c->A, cols, c->H));
+    std::vector<float> qt((size_t)c->A * c->H);  // [A][H]: the persistent decoder's per-row query slices
+    for (int k = 0; k < c->H; ++k)
+      for (int n = 0; n < c->A; ++n) qt[(size_t)n * c->H + k] = q.data[(size_t)k * c->A + n];
+    upload(c->q_wt, qt);
   }
   const std::string la = P + "decoder/Location_Sensitive_Attention/";
   {
@@ -1412,6 +1442,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
 
 // ---------------------------------------------------------------- decode
 static long long* g_stamps_dev = nullptr;  // diagnostic s_memtime stamps (profiling only)
+static long long* g_pd_stamps_dev = nullptr;  // [PD_NB][16] persistent-decoder stage stamps
 
 static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64_t seed,
                              const float* targets_d, int T_lim, float* frames_d, float* stop_d, float* align_d) {
@@ -1549,6 +1580,79 @@ static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, int t, hipStream_t
   launch_proj(c, a, t, c->side_mode == 2 ? side_rec(c, 0, par) : none, s);
 }
 
+// ---- persistent decoder (decode_persist.hip) ----
+static bool pd_fits(tt2_ctx* c) {
+  return c->pd_mode == 1 && c->pd_dev_ok && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
+         c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= PD_TMAX && c->B <= 32;
+}
+
+static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, const float* targets_d, int T_lim,
+                               float* frames_d, float* stop_d, float* align_d, hipStream_t s) {
+  if (!c->H1x.p) {
+    c->pd_ctl.alloc(sizeof(unsigned) * (2 * PD_NPH * PD_NB + 16));
+    c->H1x.alloc(2L * 32 * PD_H * 4);
+    c->H2x.alloc(2L * 32 * PD_H * 4);
+    c->Ex.alloc(2L * 32 * 8 * PD_TMAX * 4);
+    c->CTXx.alloc(2L * 32 * PD_E2 * 4);
+    c->SSx.alloc(2L * 32 * 4);
+    c->PPx.alloc(2L * PD_KSP * 32 * PD_NPF * 4);
+    c->PREx.alloc(2L * 32 * PD_P * 4);
+    for (auto& e : c->pd_ev) TT2_HIP(hipEventCreate(&e));
+  }
+  const auto& cfg = c->cfg;
+  c->keysT.alloc(sizeof(float) * (size_t)cfg.max_batch * PD_A * PD_TMAX);
+  c->valuesT.alloc(sizeof(float) * (size_t)cfg.max_batch * PD_E2 * PD_TMAX);
+  hipLaunchKernelGGL(k_transpose_bt, dim3(PD_TMAX / 32, PD_A / 32, c->B), dim3(256), 0, s, c->keys.as<float>(),
+                     (long)PD_A, c->keysT.as<float>(), c->T_in, PD_A);
+  hipLaunchKernelGGL(k_transpose_bt, dim3(PD_TMAX / 32, PD_E2 / 32, c->B), dim3(256), 0, s, c->values.as<float>(),
+                     (long)c->Dm, c->valuesT.as<float>(), c->T_in, PD_E2);
+  TT2_HIP(hipGetLastError());
+  TT2_HIP(hipMemsetAsync(c->pd_ctl.p, 0, c->pd_ctl.bytes, s));  // flags + ctl words, every launch
+  PdArgs a;
+  a.flags = c->pd_ctl.as<unsigned>();
+  a.flags2 = a.flags + PD_NPH * PD_NB;
+  a.ctl = reinterpret_cast<int*>(a.flags + 2 * PD_NPH * PD_NB);
+  a.B = c->B; a.T_in = c->T_in; a.max_iters = max_iters; a.T_lim = targets_d ? T_lim : 0; a.nm = c->nm;
+  a.stop_at_any = cfg.stop_at_any; a.mask_encoder = cfg.mask_encoder; a.cumulative = cfg.cumulative_weights;
+  a.constraint = cfg.synthesis_constraint; a.monotonic = cfg.constraint_monotonic; a.win = cfg.attention_win_size;
+  a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
+  a.l1_w = c->l1_w.as<float>(); a.l1_wh = c->l1_wh.as<float>(); a.l1_b = c->l1_b.as<float>();
+  a.l2_w = c->l2_w.as<float>(); a.l2_wh = c->l2_wh.as<float>(); a.l2_b = c->l2_b.as<float>();
+  a.GS = c->GS0.as<float>(); a.q_wt = c->q_wt.as<float>(); a.loc_cw = c->loc_cw.as<float>(); a.va = c->va.as<float>();
+  a.proj_w = c->proj_w.as<float>(); a.proj_b = c->proj_b.as<float>(); a.PS = c->PS.as<float>();
+  a.pre_b1 = c->pre_b1.as<float>(); a.pre_w2t = c->pre_w2t.as<float>(); a.pre_b2 = c->pre_b2.as<float>();
+  a.TP1 = targets_d ? c->TP1.as<float>() : nullptr;
+  a.keysT = c->keysT.as<float>(); a.valuesT = c->valuesT.as<float>(); a.lengths = c->lens.as<int>();
+  a.masks = masks_d;
+  a.H1x = c->H1x.as<float>(); a.H2x = c->H2x.as<float>(); a.Ex = c->Ex.as<float>(); a.CTXx = c->CTXx.as<float>();
+  a.SSx = c->SSx.as<float>(); a.PPx = c->PPx.as<float>(); a.PREx = c->PREx.as<float>();
+  a.frames = frames_d; a.stop = stop_d; a.align = align_d;
+  a.stamps = nullptr;
+  a.stamp_step = -1;
+  if (const char* st = getenv("TT2_STAMP_STEP")) {  // diagnostic: stage stamps of one decode step
+    if (!g_pd_stamps_dev) TT2_HIP(hipMalloc(&g_pd_stamps_dev, PD_NB * 32 * sizeof(long long)));
+    TT2_HIP(hipMemsetAsync(g_pd_stamps_dev, 0, PD_NB * 32 * sizeof(long long), s));
+    a.stamps = g_pd_stamps_dev;
+    a.stamp_step = atoi(st);
+  }
+  TT2_HIP(hipEventRecord(c->pd_ev[0], s));
+  pd_launch(a, s);
+  TT2_HIP(hipEventRecord(c->pd_ev[1], s));
+  int h[4];
+  TT2_HIP(hipMemcpyAsync(h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
+  TT2_HIP(hipStreamSynchronize(s));
+  TT2_HIP(hipEventElapsedTime(&c->pd_kernel_ms, c->pd_ev[0], c->pd_ev[1]));
+  TT2_CHECK(h[2] == 0, TT2_ERR_HIP,
+            "persistent decoder: a hand-off wait timed out (phase " + std::to_string(h[2] - 1) +
+                "); set TT2_DECODER=launch to use the per-step launch path");
+  TT2_CHECK(h[0] == 1, TT2_ERR_STATE, "persistent decoder did not terminate");
+  c->n_steps = h[1];
+  c->last_max_iters = max_iters;
+  c->last_pd = true;
+  c->have_args = false;
+  c->decoded = true;
+}
+
 static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64_t seed, const float* targets_d,
                        int T_lim, float* frames_d, float* stop_d, float* align_d, hipStream_t s) {
   TT2_CHECK(c->encoded, TT2_ERR_STATE, "tt2_decode called before tt2_encode");
@@ -1587,6 +1691,11 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
     g.bias = c->pre_b1.as<float>();
     gemm(g, s);
   }
+  if (pd_fits(c)) {
+    decode_persist_dev(c, max_iters, masks_d, targets_d, T_lim, frames_d, stop_d, align_d, s);
+    return;
+  }
+  c->last_pd = false;
   const DecArgs a = make_dec_args(c, max_iters, masks_d, seed, targets_d, T_lim, frames_d, stop_d, align_d);
   c->last_args = a;
   c->have_args = true;
@@ -1747,6 +1856,8 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     alloc_acts(c.get());
     for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
     for (auto& e : c->sev) TT2_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (const char* m = getenv("TT2_DECODER")) c->pd_mode = std::string(m) == "launch" ? 0 : 1;
+    c->pd_dev_ok = pd_device_ok(hip_device);
     if (const char* m = getenv("TT2_SIDE_MODE")) c->side_mode = atoi(m);
     if (const char* m = getenv("TT2_SIDE_DELAY")) c->side_delay = atoi(m);
     if (const char* m = getenv("TT2_SIDE_DELAY2")) c->side_delay2 = atoi(m);
@@ -1760,6 +1871,8 @@ void tt2_destroy(tt2_ctx* c) {
   for (auto g : c->graph.chunks)
     if (g) (void)hipGraphExecDestroy(g);
   if (c->ctl_host) (void)hipHostFree(c->ctl_host);
+  for (auto& e : c->pd_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->sev)
@@ -1970,6 +2083,23 @@ tt2_status tt2_profile_decoder_kernels(tt2_ctx* c, int iters, float* avg_us) {
     TT2_HIP(hipEventDestroy(e1));
     TT2_HIP(hipMemcpy(c->stamps_host, g_stamps_dev, 64 * sizeof(long long), hipMemcpyDeviceToHost));
     c->decoded = false;
+  });
+}
+
+tt2_status tt2_decoder_path(tt2_ctx* c, int* persistent, float* kernel_ms) {
+  return guard([&] {
+    TT2_CHECK(c && persistent && kernel_ms, TT2_ERR_INVALID_ARG, "null argument");
+    *persistent = c->last_pd ? 1 : (pd_fits(c) ? 1 : 0);
+    *kernel_ms = c->last_pd ? c->pd_kernel_ms : 0.f;
+  });
+}
+
+tt2_status tt2_debug_pd_stamps(tt2_ctx* c, long long* out8192) {
+  return guard([&] {
+    TT2_CHECK(c && out8192, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_CHECK(g_pd_stamps_dev, TT2_ERR_STATE, "no persistent decode ran with TT2_STAMP_STEP set");
+    TT2_HIP(hipDeviceSynchronize());
+    TT2_HIP(hipMemcpy(out8192, g_pd_stamps_dev, PD_NB * 32 * sizeof(long long), hipMemcpyDeviceToHost));
   });
 }
 

@@ -76,6 +76,8 @@ SIGNATURES = {
     "tt2_last_timings": (_I, [_P, _P]),
     "tt2_profile_decoder_kernels": (_I, [_P, _I, _P]),
     "tt2_debug_stamps": (_I, [_P, _P]),
+    "tt2_decoder_path": (_I, [_P, _P, _P]),
+    "tt2_debug_pd_stamps": (_I, [_P, _P]),
     "tt2_wn_last_timings": (_I, [_P, _P]),
     "tt2_wn_debug_stamps": (_I, [_P, _P]),
     "tt2_wn_default_config": (None, [ctypes.POINTER(WnConfig), _I, ctypes.c_int64]),

@@ -128,6 +128,15 @@ class TacotronEngine(object):
         n = n.value
         return frames[:, :n], stop[:, :n], align[:, :, :n]
 
+    def decoder_path(self):
+        """(persistent, kernel_ms): 1 when the single-launch persistent decoder serves the current
+        shapes (k_decode_persist), 0 for the per-step launch path; HIP-event time of the last
+        persistent decode launch."""
+        p = ctypes.c_int()
+        ms = ctypes.c_float()
+        check(self.lib.tt2_decoder_path(self.h, ctypes.byref(p), ctypes.byref(ms)))
+        return p.value, ms.value
+
     def postnet(self, frames=None, B=None, T=None):
         if frames is not None:
             frames = f32(frames)

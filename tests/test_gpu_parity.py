@@ -171,6 +171,79 @@ def test_full_dims_gta(full_setup):
     _decode_compare(hp, W, B=B, T=15, T_ref=64, n=40, targets=tg)
 
 
+# ---- persistent decoder (k_decode_persist: one launch, weights resident on-chip) ----
+
+def _persistent(eng):
+    return eng.decoder_path()[0] == 1
+
+
+def test_persistent_full_batch_free_run(full_setup):
+    """configs[1] shape (B=32, 200 chars + EOS, ragged lengths) through the persistent decoder,
+    free running with injected prenet masks, against the oracle over 50 steps."""
+    hp, W = full_setup
+    out, ref = _decode_compare(hp, W, B=32, T=201, T_ref=96, n=50, seed=21)
+
+
+def test_persistent_selected_for_bench_shape(full_setup):
+    hp, W = full_setup
+    ids, lens, re, rs = tacotron_inputs(32, 201, 64, seed=4)
+    eng = _engine(hp, W, 32, 201, 64, 4)
+    eng.synthesize(ids, lens, re, rs, 4, prenet_masks(4, 32, hp.prenet_layers[0], seed=4))
+    assert _persistent(eng), "k_decode_persist not used at configs[1] shapes on this device"
+    eng.close()
+
+
+def test_persistent_partial_batch_window(full_setup):
+    """Padding rows (B=5 < 32) and the synthesis window constraint (attention.py:202-215)."""
+    hp, W = full_setup
+    _decode_compare(hp, W, B=5, T=57, T_ref=64, n=30, seed=8, constraint=True)
+
+
+def test_persistent_gta_full_batch(full_setup):
+    hp, W = full_setup
+    B = 32
+    tg = np.random.default_rng(12).uniform(-4, 4, (B, 33, hp.num_mels)).astype(np.float32)
+    out, ref = _decode_compare(hp, W, B=B, T=120, T_ref=64, n=40, targets=tg, seed=12)
+    assert out["frames"].shape[1] == 33
+
+
+def test_persistent_stop_rule(full_setup):
+    """Batch-level stop decided from the flags' stop bits: GPU and oracle stop at the same step."""
+    hp, W = full_setup
+    W2 = dict(W)
+    key = "Tacotron_model/inference/decoder/stop_token_projection/projection_stop_token_projection/bias"
+    for bias in (0.3, 0.8, 8.0):
+        W2[key] = np.array([bias], np.float32)
+        out, ref = _decode_compare(hp, W2, B=6, T=31, T_ref=64, n=40, seed=6)
+        assert out["frames"].shape[1] == ref["decoder_output"].shape[1]
+
+
+def test_persistent_matches_launch_path_long(full_setup):
+    """1000-step horizon at configs[1] shapes: persistent decoder vs the per-step launch path
+    (both HIP; the oracle is too slow for 1000 steps x 32 rows in a unit test)."""
+    import os
+    hp, W = full_setup
+    B, T, n = 32, 201, 1000
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=31)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=31)
+    eng = _engine(hp, W, B, T, 64, n)
+    a = eng.synthesize(ids, lens, re, rs, n, masks)
+    assert _persistent(eng)
+    eng.close()
+    os.environ["TT2_DECODER"] = "launch"
+    try:
+        eng2 = _engine(hp, W, B, T, 64, n)
+    finally:
+        del os.environ["TT2_DECODER"]
+    b = eng2.synthesize(ids, lens, re, rs, n, masks)
+    assert not _persistent(eng2)
+    eng2.close()
+    assert a["frames"].shape == b["frames"].shape
+    np.testing.assert_allclose(a["stop_token_prediction"], b["stop_token_prediction"], atol=1e-4)
+    np.testing.assert_allclose(a["alignments"], b["alignments"], atol=1e-4)
+    np.testing.assert_allclose(a["decoder_output"], b["decoder_output"], atol=1e-4)
+
+
 def test_tacotron_shim_initialize(small_setup):
     """tacotron.models.create_model('Tacotron', hp).initialize(...) fills tower_* like the
     reference (tacotron.py:573-632)."""
