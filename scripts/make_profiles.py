@@ -27,7 +27,7 @@ def main():
     bench = os.path.join(os.path.dirname(src), os.path.basename(src) + ".bench.json")
     hdr = ("# rocprofv3 --kernel-trace --stats + separate --pmc passes (FETCH_SIZE | WRITE_SIZE |\n"
            "# TCC_HIT_sum TCC_MISS_sum | GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES) of\n"
-           "#   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-wavenet --t-out 200\n"
+           "#   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-wavenet\n"
            "# (scripts/gpu_prof.sh).  FETCH_KB/WRITE_KB are raw counter values per launch (KiB);\n"
            "# HBM bytes = 2*FETCH + WRITE on gfx950.  clk_GHz column is not meaningful.\n")
     with open(os.path.join(out, tag + "_summary.txt"), "w") as f:

@@ -29,6 +29,7 @@ struct PdArgs {
   int B, T_in, max_iters, T_lim, nm;
   int stop_at_any, mask_encoder, cumulative, constraint, monotonic, win;
   float zo, one_m_zo;
+  int poll_sleep;       // s_sleep(1) repetitions between flag polls (env TT2_PD_SLEEP)
   // weights (tacotron.hip finalize layouts)
   const float* l1_w;    // [256 tiles][768 x 16] WF, rows [prenet | context_enc]
   const float* l1_wh;   // [256][1024 x 16] recurrent rows

@@ -71,7 +71,7 @@ __device__ __forceinline__ bool pd_spin(const PdArgs& a, int ph, int lane, F con
         return false;
       }
     }
-    __builtin_amdgcn_s_sleep(1);
+    for (int z = 0; z < a.poll_sleep; ++z) __builtin_amdgcn_s_sleep(1);  // back off: pollers load the memory system
   }
 }
 
@@ -87,17 +87,28 @@ __device__ __forceinline__ bool pd_poll(const PdArgs& a, int ph, int base, int s
 }
 
 // Wave-level poll for ALL producers g < nprod of phase ph, two-level so that no flag line has more
-// than 32 pollers (256 pollers on one line serialise at its memory channel, ~3 us per hop): group
-// x = g%8, slot s = g/8 first waits for producers [8s, 8s+8) and raises its group flag
-// flags2[ph][x][s]; then it waits for the 32 group flags of its own group x.
+// than 32 pollers (256 pollers on one line serialise at its memory channel, ~3 us per hop): the
+// consumers form groups of 8 (x = g/8, member s = g%8); member s waits for producers
+// [32s, 32s+32) (one 128-B line) and raises flags2[ph][x][s], then waits for its group's 8 flags.
 __device__ __forceinline__ bool pd_poll_all(const PdArgs& a, int ph, int nprod, unsigned need, int shift, int lane) {
-  const int g = blockIdx.x, x = g & 7, s = g >> 3;
-  const unsigned* f = a.flags + ph * PD_NB + 8 * s;
-  unsigned* f2 = a.flags2 + ph * PD_NB + 32 * x;
-  if (!pd_spin(a, ph, lane, [&] { return lane >= 8 || 8 * s + lane >= nprod || (pd_flag(f + lane) >> shift) >= need; }))
+  const int g = blockIdx.x, x = g >> 3, s = g & 7;
+  const unsigned* f = a.flags + ph * PD_NB + 32 * s;
+  unsigned* f2 = a.flags2 + ph * PD_NB + 8 * x;
+  if (!pd_spin(a, ph, lane, [&] { return lane >= 32 || 32 * s + lane >= nprod || (pd_flag(f + lane) >> shift) >= need; }))
     return false;
   if (lane == 0) __hip_atomic_store((pd_gu32*)(f2 + s), need, PD_RLX);
-  return pd_spin(a, ph, lane, [&] { return lane >= 32 || pd_flag(f2 + lane) >= need; });
+  return pd_spin(a, ph, lane, [&] { return lane >= 8 || pd_flag(f2 + lane) >= need; });
+}
+
+// Block-level waits: wave 0 polls, the work-group joins at a barrier (result via LDS slot).
+template <class F>
+__device__ __forceinline__ bool pd_block_wait(int* slot, F poll) {
+  if (threadIdx.x < 64) {
+    const bool ok = poll();
+    if (threadIdx.x == 0) *slot = ok;
+  }
+  __syncthreads();
+  return *slot != 0;
 }
 
 // Every storing wave drains its sc1 stores, then one lane raises this work-group's flag.
@@ -176,7 +187,6 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 
   // ---------------- prologue: resident weights and per-row constants ----------------
   const int tid = tid_, lane = tid & 63, w = tid >> 6;
-  const int tw = (w - 4) & 3;                    // tail-wave index (waves 4..7)
   const int em = (tid >> 2) & 31, eu = tid & 3;  // LSTM epilogue thread (tid < 128) -> row, unit
   f32x4 w1p[2], w2i[8];                          // chain: L1 prenet rows, L2 input rows (8 waves)
   {
@@ -201,10 +211,14 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     const f32x4* PW = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16);
     wpc = PW[(PD_H / 16 + 4 * pks + w) * 64 + lane];
   }
-  // tail-job weights streamed from L2 each step (1.25 MB per XCD, L2-resident): L1 context rows
-  // (k-groups [8 tw, 8 tw + 8) of the tile's context block) and projection h2 rows
-  const f32x4* const W1C = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * (PD_P + PD_E2) * 16) + (PD_P / 16 + 8 * tw) * 64;
-  const f32x4* const WPH = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16) + (8 * pks + 2 * tw) * 64;
+  f32x4 wph = zero4;  // projection h2 rows of this split, k-group 8 pks + w
+  if (isproj) wph = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16)[(8 * pks + w) * 64 + lane];
+  f32x4 w1c[4];  // L1 context rows, k-groups 16 + 4w + i of the tile
+  {
+    const f32x4* W1C = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * (PD_P + PD_E2) * 16) + (PD_P / 16 + 4 * w) * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w1c[i] = W1C[i * 64 + lane];
+  }
   f32x4 wl[2];
   {
     const f32x4* LW = reinterpret_cast<const f32x4*>(a.loc_cw + (long)j * PD_KLP * 16);
@@ -236,7 +250,6 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     si[4] = 0;
     sc[2] = 0.f;
   }
-  unsigned tgen = 0;  // tail-barrier generation (waves 4..7)
   f32x4 vals[8];  // values[b][32*(tid/64) + 4i + e][64j + tid%64]: valuesT is [B][E2][256], 0 past T_in
   {
     const f32x4* V = reinterpret_cast<const f32x4*>(a.valuesT + ((long)(rowv ? b : 0) * PD_E2 + 64 * j + (tid & 63)) * PD_TMAX +
@@ -298,81 +311,29 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
   };
 
-  // One wait window: wave 0 polls (block-uniform result), tail waves 4..7 run `tail`, then the
-  // whole work-group meets at a barrier.
-  auto window = [&](int w_, auto poll, auto tail) -> bool {
-    if (w_ == 0) {
-      const bool ok = poll();
-      if ((threadIdx.x & 63) == 0) si[2] = ok;
-    } else if (w_ >= 4) {
-      tail();
-    }
-    __syncthreads();
-    const bool ok = si[2] != 0;
-    return ok;
-  };
-  auto no_tail = [] {};
-
-  // Tail reduction of the 4 tail waves' tiles: RG = (1-z)·Σ + z·RG (zoned-state recurrence) or a
-  // plain store (mix = false).
-  auto tail_reduce = [&](const f32x4& t0, const f32x4& t1, float* dst, bool mix, int tid) {
-    put_partials(t0, t1, red, tw, tid & 63);
-    tail_bar(si + 4, tgen, tid & 63);
-    for (int idx = tid - 256; idx < 512; idx += 256) {
-      const float v = sum_partials<4>(red, idx);
-      dst[idx] = mix ? a.one_m_zo * v + a.zo * dst[idx] : v;
-    }
-  };
-
-  // Tail job: X rows (AF, k-groups [16 tw, 16 tw + 16)) · W (LDS tiles) of one tail wave.
-  auto rec_job = [&](const float* X, const float* Wl, f32x4& t0, f32x4& t1, int lane) {
+  // Recurrent tail (all 8 waves, K split 8 ways, 2 batches of 4 k-groups):
+  //   dst = (1-z)·(X·W) + z·dst   -- the zoned-state recurrence RG(t+1) = h_z(t)·W_h, linear in h_new
+  auto rec8 = [&](const float* X, const float* Wl, float* dst, int w, int lane, int tid) {
     const f32x4* Wv = reinterpret_cast<const f32x4*>(Wl);
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      f32x4 x0[4], x1v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int sg = 16 * tw + 4 * h + i;
-        x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
-        x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int sg = 16 * tw + 4 * h + i;
-        kg_mfma(x0[i], x1v[i], Wv[sg * 64 + lane], t0, t1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // Tail job: L1 context rows of step t (context(t-1) of every row, once all slices landed) and
-  // the rows' style scales.
-  auto ctx_job = [&](int pprev, unsigned tgprev, int lane, int tid) {
-    f32x4 w1c[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w1c[i] = W1C[i * 64 + lane];
-    if (tw == 0) {
-      const bool ok = pd_poll_all(a, PD_F_CTX, PD_NB, tgprev, 0, lane);
-      if (lane == 0) si[3] = ok;
-    }
-    tail_bar(si + 4, tgen, lane);
-    if (!si[3]) return;
-    const float* X = a.CTXx + pprev * 32 * PD_E2;
     f32x4 s0 = zero4, s1 = zero4;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f32x4 x0[4], x1v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int sg = 8 * tw + 4 * h + i;
+        const int sg = 8 * w + 4 * h + i;
         x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
         x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) kg_mfma(x0[i], x1v[i], w1c[4 * h + i], s0, s1);
+      for (int i = 0; i < 4; ++i) {
+        const int sg = 8 * w + 4 * h + i;
+        kg_mfma(x0[i], x1v[i], Wv[sg * 64 + lane], s0, s1);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
-    tail_reduce(s0, s1, RGc, false, tid);
-    if (tid - 256 < 32) ssa[tid - 256] = pd_ld(a.SSx + pprev * 32 + (tid - 256));
+    reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
+    dst[tid] = a.one_m_zo * G[tid] + a.zo * dst[tid];
   };
   __syncthreads();
   // GO frame (helpers.py:136-138): frame 0 -> layer-1 pre-activation = b1
@@ -399,12 +360,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     float keep1n, keep2n;  // prenet keep bits of step t+1, in flight during the whole step
     prenet_keep(t + 1, tid, keep1n, keep2n);
     // ================= A: LSTM layer 1 =================
-    // tail: L1 context rows of this step (context(t-1)), style scales
-    if (!window(w, [&] { return pd_poll_all(a, PD_F_PRE, PD_NB, tg, 1, lane); },
-                [&] {
-                  if (t > 0) ctx_job(p ^ 1, tg - 1, lane, tid);
-                }))
-      return;
+    if (!pd_block_wait(si + 2, [&] { return pd_poll_all(a, PD_F_PRE, PD_NB, tg, 1, lane); })) return;
     PD_STAMP(1);
     if (t > 0 && w == 0) {
       // stop rule of step t-1 (TacoTestHelper.next_inputs, helpers.py:40-59 + dynamic_decode):
@@ -460,17 +416,10 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_H1, tg, tid);
     PD_STAMP(2);
+    if (t > 0) rec8(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, RG2, w, lane, tid);  // RG2(t) from h2_new(t-1)
+    PD_STAMP(3);
     // ================= B: LSTM layer 2 =================
-    // tail: RG2(t) = (1-z)·h2_new(t-1)·W2h + z·RG2(t-1)
-    if (!window(w, [&] { return pd_poll_all(a, PD_F_H1, PD_NB, tg, 0, lane); },
-                [&] {
-                  if (t > 0) {
-                    f32x4 s0 = zero4, s1 = zero4;
-                    rec_job(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, s0, s1, lane);
-                    tail_reduce(s0, s1, RG2, true, tid);
-                  }
-                }))
-      return;
+    if (!pd_block_wait(si + 3, [&] { return pd_poll_all(a, PD_F_H1, PD_NB, tg, 0, lane); })) return;
     PD_STAMP(4);
     {
       const float* X = a.H1x + p * 32 * PD_H;
@@ -507,8 +456,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_H2, tg, tid);
     PD_STAMP(5);
-    // ================= C: query slice + partial energies (attention.py:37-69, 186-201) =================
-    // issued ahead of the H2 wait (L2-resident: shared by the 32 rows of slice j):
+    // issued ahead of the RG1 tail and the H2 wait (L2-resident: shared by the 32 rows of slice j):
     f32x4 wq[8];  // W_q[32*(tid/16) + 4i + e][16j + tid%16] (q_wt is [A][H])
     {
       const f32x4* Q = reinterpret_cast<const f32x4*>(a.q_wt + (long)(16 * j + (tid & 15)) * PD_H + 32 * (tid >> 4));
@@ -521,15 +469,12 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) kv[i] = K[(w + 8 * i) * 4 + (lane >> 4)];
     }
-    // tail: RG1(t+1) = (1-z)·h1_new(t)·W1h + z·RG1(t)
-    if (!window(w, [&] { return pd_poll_all(a, PD_F_H2, PD_NB, tg, 0, lane); },
-                [&] {
-                  f32x4 s0 = zero4, s1 = zero4;
-                  rec_job(a.H1x + p * 32 * PD_H, sW1h, s0, s1, lane);
-                  tail_reduce(s0, s1, RG1, true, tid);
-                }))
-      return;
+    rec8(a.H1x + p * 32 * PD_H, sW1h, RG1, w, lane, tid);  // RG1(t+1) from h1_new(t)
+    PD_STAMP(6);
+    // ================= C: query slice + partial energies (attention.py:37-69, 186-201) =================
+    if (!pd_block_wait(si + 4, [&] { return pd_poll_all(a, PD_F_H2, PD_NB, tg, 0, lane); })) return;
     PD_STAMP(7);
+
     if (rowv) {
       const float* X = a.H2x + p * 32 * PD_H;
       red[tid] = pd_ld(X + af_idx(b, tid));
@@ -561,23 +506,16 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_E, tg, tid);
     PD_STAMP(8);
+    if (isproj) {  // projection partial, h2_new rows of this split (Architecture_wrappers.py:243-247)
+      const float* X = a.H2x + p * 32 * PD_H;
+      const int sg = 8 * pks + w;
+      f32x4 s0 = zero4, s1 = zero4;
+      kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wph, s0, s1);
+      reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
+      PPh[tid] = G[tid];
+    }
     // ================= D: softmax, cumulative alignments, context (attention.py:10-35, 202-227) ==========
-    // tail: projection partial of this split's h2_new rows (proj blocks, Architecture_wrappers.py:243-247)
-    if (!window(w, [&] { return pd_poll(a, PD_F_E, sib0, 32, 8, tg, 0, lane); },
-                [&] {
-                  if (isproj) {
-                    const float* X = a.H2x + p * 32 * PD_H;
-                    const f32x4 wph[2] = {WPH[lane], WPH[64 + lane]};
-                    f32x4 s0 = zero4, s1 = zero4;
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                      const int sg = 8 * pks + 2 * tw + i;
-                      kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wph[i], s0, s1);
-                    }
-                    tail_reduce(s0, s1, PPh, false, tid);
-                  }
-                }))
-      return;
+    if (!pd_block_wait(si + 5, [&] { return pd_poll(a, PD_F_E, sib0, 32, 8, tg, 0, lane); })) return;
     PD_STAMP(9);
     if (rowv) {
       const float* E = a.Ex + ((long)p * 32 + b) * 8 * PD_TMAX;
@@ -679,12 +617,12 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     // ================= E: projection partial, context rows =================
     if (isproj) {
-      if (!window(w, [&] { return pd_poll(a, PD_F_CTX, 32 * pks, 1, 32, tg, 0, lane); }, no_tail)) return;
+      if (!pd_block_wait(si + 6, [&] { return pd_poll(a, PD_F_CTX, 32 * pks, 1, 32, tg, 0, lane); })) return;
       PD_STAMP(11);
-      f32x4 s0 = zero4, s1 = zero4;
       if (w < 4) {
         const float* X = a.CTXx + p * 32 * PD_E2;
         const int sg = 4 * pks + w;
+        f32x4 s0 = zero4, s1 = zero4;
         kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wpc, s0, s1);
         put_partials(s0, s1, red, w, lane);
       }
@@ -698,7 +636,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     // ================= F: frame / stop (modules.py:392-448), prenet of step t+1 =================
     const PrenetOps pops = prenet_ops(keep1n, keep2n, tid);
-    if (!window(w, [&] { return pd_poll_all(a, PD_F_PP, PD_NTILE * PD_KSP, tg, 0, lane); }, no_tail)) return;
+    if (!pd_block_wait(si + 7, [&] { return pd_poll_all(a, PD_F_PP, PD_NTILE * PD_KSP, tg, 0, lane); })) return;
     PD_STAMP(13);
     int stopbit = 0;
     if (rowv) {
@@ -727,6 +665,21 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_PRE, ((tg + 1) << 1) | (unsigned)stopbit, tid);
     PD_STAMP(14);
+    // L1 context rows of step t+1 once every context slice landed, and the rows' style scales
+    {
+      if (!pd_block_wait(si + 8, [&] { return pd_poll_all(a, PD_F_CTX, PD_NB, tg, 0, lane); })) return;
+      const float* X = a.CTXx + p * 32 * PD_E2;
+      f32x4 s0 = zero4, s1 = zero4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int sg = 4 * w + i;
+        kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), w1c[i], s0, s1);
+      }
+      reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
+      RGc[tid] = G[tid];
+      if (tid < 32) ssa[tid] = pd_ld(a.SSx + p * 32 + tid);
+    }
+    PD_STAMP(15);
   }
   if (g == 0 && tid == 0) {
     a.ctl[1] = a.max_iters;

@@ -1616,6 +1616,8 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   a.stop_at_any = cfg.stop_at_any; a.mask_encoder = cfg.mask_encoder; a.cumulative = cfg.cumulative_weights;
   a.constraint = cfg.synthesis_constraint; a.monotonic = cfg.constraint_monotonic; a.win = cfg.attention_win_size;
   a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
+  a.poll_sleep = 4;
+  if (const char* e = getenv("TT2_PD_SLEEP")) a.poll_sleep = atoi(e);
   a.l1_w = c->l1_w.as<float>(); a.l1_wh = c->l1_wh.as<float>(); a.l1_b = c->l1_b.as<float>();
   a.l2_w = c->l2_w.as<float>(); a.l2_wh = c->l2_wh.as<float>(); a.l2_b = c->l2_b.as<float>();
   a.GS = c->GS0.as<float>(); a.q_wt = c->q_wt.as<float>(); a.loc_cw = c->loc_cw.as<float>(); a.va = c->va.as<float>();
