@@ -90,10 +90,25 @@ __device__ __forceinline__ bool pd_poll(const PdArgs& a, int ph, int base, int s
 // than 32 pollers (256 pollers on one line serialise at its memory channel, ~3 us per hop): the
 // consumers form groups of 8 (x = g/8, member s = g%8); member s waits for producers
 // [32s, 32s+32) (one 128-B line) and raises flags2[ph][x][s], then waits for its group's 8 flags.
-__device__ __forceinline__ bool pd_poll_all(const PdArgs& a, int ph, int nprod, unsigned need, int shift, int lane) {
+__device__ __forceinline__ bool pd_poll_all(const PdArgs& a, int ph, int nprod, unsigned need, int shift, int lane,
+                                            bool sweep_first) {
   const int g = blockIdx.x, x = g >> 3, s = g & 7;
   const unsigned* f = a.flags + ph * PD_NB + 32 * s;
   unsigned* f2 = a.flags2 + ph * PD_NB + 8 * x;
+  if (sweep_first) {  // one sweep of all producers first: one round trip when the hand-off already
+                      // landed (waits behind a long tail); not where all 256 arrive at once
+    const unsigned* fa = a.flags + ph * PD_NB;
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pidx = lane + 64 * i;
+      ok = ok && (pidx >= nprod || (pd_flag(fa + pidx) >> shift) >= need);
+    }
+    if (__all(ok)) {
+      if (lane == 0) __hip_atomic_store((pd_gu32*)(f2 + s), need, PD_RLX);  // members may be polling it
+      return true;
+    }
+  }
   if (!pd_spin(a, ph, lane, [&] { return lane >= 32 || 32 * s + lane >= nprod || (pd_flag(f + lane) >> shift) >= need; }))
     return false;
   if (lane == 0) __hip_atomic_store((pd_gu32*)(f2 + s), need, PD_RLX);
@@ -360,7 +375,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     float keep1n, keep2n;  // prenet keep bits of step t+1, in flight during the whole step
     prenet_keep(t + 1, tid, keep1n, keep2n);
     // ================= A: LSTM layer 1 =================
-    if (!pd_block_wait(si + 2, [&] { return pd_poll_all(a, PD_F_PRE, PD_NB, tg, 1, lane); })) return;
+    if (!pd_block_wait(si + 2, [&] { return pd_poll_all(a, PD_F_PRE, PD_NB, tg, 1, lane, false); })) return;
     PD_STAMP(1);
     if (t > 0 && w == 0) {
       // stop rule of step t-1 (TacoTestHelper.next_inputs, helpers.py:40-59 + dynamic_decode):
@@ -386,17 +401,31 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       return;
     }
     {
+      // L1 input rows [prenet(t) | context(t-1)]: every PRE flag implies every context slice of
+      // t-1 was published (PRE <- PP <- CTX slices of all 8 splits), so no separate wait
       const float* X = a.PREx + p * 32 * PD_P;
-      f32x4 a0[2], a1[2];
+      const float* XC = a.CTXx + (p ^ 1) * 32 * PD_E2;
+      f32x4 a0[2], a1[2], c0[4], c1v[4];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int sg = 2 * w + i;
         a0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
         a1[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
       }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int sg = 4 * w + i;
+        c0[i] = pd_ld4(XC, (sg * 2) * 64 + lane);
+        c1v[i] = pd_ld4(XC, (sg * 2 + 1) * 64 + lane);
+      }
+      if (tid < 32) ssa[tid] = t > 0 ? pd_ld(a.SSx + (p ^ 1) * 32 + tid) : 0.f;
       f32x4 s0 = zero4, s1 = zero4;
 #pragma unroll
       for (int i = 0; i < 2; ++i) kg_mfma(a0[i], a1[i], w1p[i], s0, s1);
+      if (t > 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) kg_mfma(c0[i], c1v[i], w1c[i], s0, s1);
+      }
       PD_STAMP(18);
       put_partials(s0, s1, red, w, lane);
       __syncthreads();
@@ -407,7 +436,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = em * 16 + 4 * q + eu;
-        z[q] = (((sum_partials<8>(red, idx) + RGc[idx]) + RG1[idx]) + ssa[em] * gsv[q]) + b1v[q];
+        z[q] = ((sum_partials<8>(red, idx) + RG1[idx]) + ssa[em] * gsv[q]) + b1v[q];
       }
       const float cn = sigm(z[2] + 1.0f) * c1 + sigm(z[0]) * tanhf(z[1]);
       const float hn = sigm(z[3]) * tanhf(cn);
@@ -419,7 +448,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     if (t > 0) rec8(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, RG2, w, lane, tid);  // RG2(t) from h2_new(t-1)
     PD_STAMP(3);
     // ================= B: LSTM layer 2 =================
-    if (!pd_block_wait(si + 3, [&] { return pd_poll_all(a, PD_F_H1, PD_NB, tg, 0, lane); })) return;
+    if (!pd_block_wait(si + 3, [&] { return pd_poll_all(a, PD_F_H1, PD_NB, tg, 0, lane, true); })) return;
     PD_STAMP(4);
     {
       const float* X = a.H1x + p * 32 * PD_H;
@@ -472,7 +501,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     rec8(a.H1x + p * 32 * PD_H, sW1h, RG1, w, lane, tid);  // RG1(t+1) from h1_new(t)
     PD_STAMP(6);
     // ================= C: query slice + partial energies (attention.py:37-69, 186-201) =================
-    if (!pd_block_wait(si + 4, [&] { return pd_poll_all(a, PD_F_H2, PD_NB, tg, 0, lane); })) return;
+    if (!pd_block_wait(si + 4, [&] { return pd_poll_all(a, PD_F_H2, PD_NB, tg, 0, lane, true); })) return;
     PD_STAMP(7);
 
     if (rowv) {
@@ -636,7 +665,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     // ================= F: frame / stop (modules.py:392-448), prenet of step t+1 =================
     const PrenetOps pops = prenet_ops(keep1n, keep2n, tid);
-    if (!pd_block_wait(si + 7, [&] { return pd_poll_all(a, PD_F_PP, PD_NTILE * PD_KSP, tg, 0, lane); })) return;
+    if (!pd_block_wait(si + 7, [&] { return pd_poll_all(a, PD_F_PP, PD_NTILE * PD_KSP, tg, 0, lane, false); })) return;
     PD_STAMP(13);
     int stopbit = 0;
     if (rowv) {
@@ -665,20 +694,6 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_PRE, ((tg + 1) << 1) | (unsigned)stopbit, tid);
     PD_STAMP(14);
-    // L1 context rows of step t+1 once every context slice landed, and the rows' style scales
-    {
-      if (!pd_block_wait(si + 8, [&] { return pd_poll_all(a, PD_F_CTX, PD_NB, tg, 0, lane); })) return;
-      const float* X = a.CTXx + p * 32 * PD_E2;
-      f32x4 s0 = zero4, s1 = zero4;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int sg = 4 * w + i;
-        kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), w1c[i], s0, s1);
-      }
-      reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
-      RGc[tid] = G[tid];
-      if (tid < 32) ssa[tid] = pd_ld(a.SSx + p * 32 + tid);
-    }
     PD_STAMP(15);
   }
   if (g == 0 && tid == 0) {
