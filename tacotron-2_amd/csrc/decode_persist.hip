@@ -326,29 +326,27 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
   };
 
-  // Recurrent tail (all 8 waves, K split 8 ways, 2 batches of 4 k-groups):
-  //   dst = (1-z)·(X·W) + z·dst   -- the zoned-state recurrence RG(t+1) = h_z(t)·W_h, linear in h_new
-  auto rec8 = [&](const float* X, const float* Wl, float* dst, int w, int lane, int tid) {
+  // Recurrent tail half h (all 8 waves, K split 8 ways, k-groups 8w + 4h .. +4): the zoned-state
+  // recurrence RG(t+1) = h_z(t)·W_h = (1-z)·h_new(t)·W_h + z·RG(t) is linear in h_new, so it is
+  // computed in two halves placed in two hand-off windows: half 0 -> tmp, half 1 -> dst mixed.
+  auto rec_half = [&](const float* X, const float* Wl, int h, float* tmp, float* dst, int w, int lane, int tid) {
     const f32x4* Wv = reinterpret_cast<const f32x4*>(Wl);
     f32x4 s0 = zero4, s1 = zero4;
+    f32x4 x0[4], x1v[4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      f32x4 x0[4], x1v[4];
+    for (int i = 0; i < 4; ++i) {
+      const int sg = 8 * w + 4 * h + i;
+      x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
+      x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
+    }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int sg = 8 * w + 4 * h + i;
-        x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
-        x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int sg = 8 * w + 4 * h + i;
-        kg_mfma(x0[i], x1v[i], Wv[sg * 64 + lane], s0, s1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < 4; ++i) {
+      const int sg = 8 * w + 4 * h + i;
+      kg_mfma(x0[i], x1v[i], Wv[sg * 64 + lane], s0, s1);
     }
     reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
-    dst[tid] = a.one_m_zo * G[tid] + a.zo * dst[tid];
+    if (h == 0) tmp[tid] = G[tid];
+    else dst[tid] = a.one_m_zo * (tmp[tid] + G[tid]) + a.zo * dst[tid];
   };
   __syncthreads();
   // GO frame (helpers.py:136-138): frame 0 -> layer-1 pre-activation = b1
@@ -445,7 +443,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_H1, tg, tid);
     PD_STAMP(2);
-    if (t > 0) rec8(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, RG2, w, lane, tid);  // RG2(t) from h2_new(t-1)
+    if (t > 0) rec_half(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, 1, PPh, RG2, w, lane, tid);  // RG2(t), 2nd half
     PD_STAMP(3);
     // ================= B: LSTM layer 2 =================
     if (!pd_block_wait(si + 3, [&] { return pd_poll_all(a, PD_F_H1, PD_NB, tg, 0, lane, true); })) return;
@@ -498,7 +496,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) kv[i] = K[(w + 8 * i) * 4 + (lane >> 4)];
     }
-    rec8(a.H1x + p * 32 * PD_H, sW1h, RG1, w, lane, tid);  // RG1(t+1) from h1_new(t)
+    rec_half(a.H1x + p * 32 * PD_H, sW1h, 0, RGc, RG1, w, lane, tid);  // RG1(t+1) from h1_new(t), 1st half
     PD_STAMP(6);
     // ================= C: query slice + partial energies (attention.py:37-69, 186-201) =================
     if (!pd_block_wait(si + 4, [&] { return pd_poll_all(a, PD_F_H2, PD_NB, tg, 0, lane, true); })) return;
@@ -632,6 +630,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_CTX, tg, tid);
     PD_STAMP(10);
+    rec_half(a.H1x + p * 32 * PD_H, sW1h, 1, RGc, RG1, w, lane, tid);  // RG1(t+1), 2nd half
     // location features of step t+1: im2col(cum) · (W_conv·W_loc) on MFMA (attention.py:59-62)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -694,6 +693,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_PRE, ((tg + 1) << 1) | (unsigned)stopbit, tid);
     PD_STAMP(14);
+    rec_half(a.H2x + p * 32 * PD_H, sW2h, 0, PPh, RG2, w, lane, tid);  // RG2(t+1) from h2_new(t), 1st half
     PD_STAMP(15);
   }
   if (g == 0 && tid == 0) {
