@@ -226,8 +226,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     const f32x4* PW = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16);
     wpc = PW[(PD_H / 16 + 4 * pks + w) * 64 + lane];
   }
-  f32x4 wph = zero4;  // projection h2 rows of this split, k-group 8 pks + w
-  if (isproj) wph = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16)[(8 * pks + w) * 64 + lane];
+  // projection h2 rows of this split, k-group 8 pks + w (read in the C tail; L2-resident)
+  const f32x4* const WPH = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16) + (8 * pks) * 64;
   f32x4 w1c[4];  // L1 context rows, k-groups 16 + 4w + i of the tile
   {
     const f32x4* W1C = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * (PD_P + PD_E2) * 16) + (PD_P / 16 + 4 * w) * 64;
@@ -273,6 +273,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     for (int i = 0; i < 8; ++i) vals[i] = V[i];
   }
   f32x4 loc[2] = {zero4, zero4};  // location features of the next step (cum = 0)
+  f32x4 accC0 = zero4, accC1 = zero4;  // L1 context rows of the next step (context(-1) = 0)
   const long BP = (long)a.B * PD_P;
 
   // Prenet (modules.py:346-357, dropout always on) of decoder step ts for row b, outputs
@@ -399,31 +400,19 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       return;
     }
     {
-      // L1 input rows [prenet(t) | context(t-1)]: every PRE flag implies every context slice of
-      // t-1 was published (PRE <- PP <- CTX slices of all 8 splits), so no separate wait
+      // L1 input rows [prenet(t) | context(t-1)]: the context rows were accumulated into accC
+      // while the prenet hand-off was in flight
       const float* X = a.PREx + p * 32 * PD_P;
-      const float* XC = a.CTXx + (p ^ 1) * 32 * PD_E2;
-      f32x4 a0[2], a1[2], c0[4], c1v[4];
+      f32x4 a0[2], a1[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int sg = 2 * w + i;
         a0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
         a1[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int sg = 4 * w + i;
-        c0[i] = pd_ld4(XC, (sg * 2) * 64 + lane);
-        c1v[i] = pd_ld4(XC, (sg * 2 + 1) * 64 + lane);
-      }
-      if (tid < 32) ssa[tid] = t > 0 ? pd_ld(a.SSx + (p ^ 1) * 32 + tid) : 0.f;
-      f32x4 s0 = zero4, s1 = zero4;
+      f32x4 s0 = accC0, s1 = accC1;
 #pragma unroll
       for (int i = 0; i < 2; ++i) kg_mfma(a0[i], a1[i], w1p[i], s0, s1);
-      if (t > 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) kg_mfma(c0[i], c1v[i], w1c[i], s0, s1);
-      }
       PD_STAMP(18);
       put_partials(s0, s1, red, w, lane);
       __syncthreads();
@@ -537,7 +526,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       const float* X = a.H2x + p * 32 * PD_H;
       const int sg = 8 * pks + w;
       f32x4 s0 = zero4, s1 = zero4;
-      kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wph, s0, s1);
+      kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), WPH[w * 64 + lane], s0, s1);
       reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
       PPh[tid] = G[tid];
     }
@@ -663,6 +652,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       PD_STAMP(12);
     }
     // ================= F: frame / stop (modules.py:392-448), prenet of step t+1 =================
+    rec_half(a.H2x + p * 32 * PD_H, sW2h, 0, PPh, RG2, w, lane, tid);  // RG2(t+1) from h2_new(t), 1st half
     const PrenetOps pops = prenet_ops(keep1n, keep2n, tid);
     if (!pd_block_wait(si + 7, [&] { return pd_poll_all(a, PD_F_PP, PD_NTILE * PD_KSP, tg, 0, lane, false); })) return;
     PD_STAMP(13);
@@ -693,7 +683,18 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_PRE, ((tg + 1) << 1) | (unsigned)stopbit, tid);
     PD_STAMP(14);
-    rec_half(a.H2x + p * 32 * PD_H, sW2h, 0, PPh, RG2, w, lane, tid);  // RG2(t+1) from h2_new(t), 1st half
+    {  // L1 context rows of step t+1 and the style scales: every context slice of t landed before
+       // any PP flag (PP <- CTX slices of all 8 splits), and this work-group has seen all PP flags
+      const float* XC = a.CTXx + p * 32 * PD_E2;
+      accC0 = zero4;
+      accC1 = zero4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int sg = 4 * w + i;
+        kg_mfma(pd_ld4(XC, (sg * 2) * 64 + lane), pd_ld4(XC, (sg * 2 + 1) * 64 + lane), w1c[i], accC0, accC1);
+      }
+      if (tid < 32) ssa[tid] = pd_ld(a.SSx + p * 32 + tid);
+    }
     PD_STAMP(15);
   }
   if (g == 0 && tid == 0) {
