@@ -55,10 +55,10 @@ struct PdArgs {
   // exchange buffers, two step parities each
   float* H1x;   // [2][32 x 1024] AF: h1_new
   float* H2x;   // [2][32 x 1024] AF: h2_new
-  float* Ex;    // [2][32 rows][8 slices][256 t]: partial energies
+  unsigned long long* Eg;  // [2][32 rows][8 slices][256 t] {tag, partial energy} granules
   float* CTXx;  // [2][32 x 512] AF: context_enc
   float* SSx;   // [2][32]: Σ_{t<len} alignments (style-context scale)
-  float* PPx;   // [2][8 splits][32 rows][352]: projection partials
+  unsigned long long* PPg; // [2][8 splits][32 rows][352] {tag, projection partial} granules
   float* PREx;  // [2][32 x 256] AF: prenet output of the next step
   // outputs
   float* frames;  // [B][max_iters][nm]

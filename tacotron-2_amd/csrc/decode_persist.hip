@@ -40,6 +40,7 @@ namespace tt2 {
 typedef __attribute__((address_space(1))) float pd_gf32;
 typedef __attribute__((address_space(1))) unsigned pd_gu32;
 typedef __attribute__((address_space(1))) int pd_gi32;
+typedef __attribute__((address_space(1))) unsigned long long pd_gu64;
 #define PD_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 
 constexpr long long PD_TIMEOUT = 200000000LL;  // 2 s of s_memrealtime (100 MHz)
@@ -124,6 +125,42 @@ __device__ __forceinline__ bool pd_block_wait(int* slot, F poll) {
   }
   __syncthreads();
   return *slot != 0;
+}
+
+// Data-tagged 8-byte granule {tag, fp32 bits}: the data is the flag (Guideline 16 R2) -- no drain,
+// no separate flag round trip.  For the small intra-row exchanges (energies, projection partials).
+__device__ __forceinline__ void pd_put(unsigned long long* g, unsigned tag, float v) {
+  __hip_atomic_store((pd_gu64*)g, ((unsigned long long)tag << 32) | __float_as_uint(v), PD_RLX);
+}
+// Each active lane fetches N granules base[off + i*stride] (base wave-uniform) until every tag ==
+// tag (wave-uniform bounded spin).  false: timeout or a peer failed.
+template <int N>
+__device__ __forceinline__ bool pd_take(const PdArgs& a, int ph, const unsigned long long* base, int off, int stride,
+                                        unsigned tag, bool active, float (&v)[N]) {
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned long long*>(base), (short)0, 0x7fffffff, 0x00020000);
+  long long t0 = 0;
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off * 8, i * stride * 8, 16);  // sc1
+        v[i] = __uint_as_float(x[0]);
+        ok = ok && x[1] == tag;
+      }
+    }
+    if (__all(ok)) return true;
+    if ((spin & 31) == 0) {
+      const long long now = __builtin_amdgcn_s_memrealtime();
+      if (spin == 0) {
+        t0 = now;
+      } else if (__hip_atomic_load((pd_gi32*)(a.ctl + 2), PD_RLX) != 0 || now - t0 > PD_TIMEOUT) {
+        if ((threadIdx.x & 63) == 0) __hip_atomic_store((pd_gi32*)(a.ctl + 2), 1 + ph, PD_RLX);
+        return false;
+      }
+    }
+    for (int z = 0; z < a.poll_sleep; ++z) __builtin_amdgcn_s_sleep(1);
+  }
 }
 
 // Every storing wave drains its sc1 stores, then one lane raises this work-group's flag.
@@ -511,16 +548,16 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       }
       __syncthreads();
       const float qk = qv[lane & 15];
-      float* E = a.Ex + (((long)p * 32 + b) * 8 + j) * PD_TMAX;
+      unsigned long long* E = a.Eg + (((long)p * 32 + b) * 8 + j) * PD_TMAX;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = sum16(va_k * tanh_fast(kv[i][r] + qk + loc[i][r]));
-          if ((lane & 15) == 0) pd_st(E + (w + 8 * i) * 16 + (lane >> 4) * 4 + r, e);
+          if ((lane & 15) == 0) pd_put(E + (w + 8 * i) * 16 + (lane >> 4) * 4 + r, tg, e);
         }
     }
-    pd_publish(a, PD_F_E, tg, tid);
+    __syncthreads();  // red / qv reuse below
     PD_STAMP(8);
     if (isproj) {  // projection partial, h2_new rows of this split (Architecture_wrappers.py:243-247)
       const float* X = a.H2x + p * 32 * PD_H;
@@ -531,16 +568,19 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       PPh[tid] = G[tid];
     }
     // ================= D: softmax, cumulative alignments, context (attention.py:10-35, 202-227) ==========
-    if (!pd_block_wait(si + 5, [&] { return pd_poll(a, PD_F_E, sib0, 32, 8, tg, 0, lane); })) return;
     PD_STAMP(9);
     if (rowv) {
-      const float* E = a.Ex + ((long)p * 32 + b) * 8 * PD_TMAX;
+      const unsigned long long* E = a.Eg + ((long)p * 32 + b) * 8 * PD_TMAX;
+      if (tid == 0) si[5] = 1;
+      __syncthreads();
       if (tid < PD_TMAX) {
+        float ev[8];
+        if (!pd_take<8>(a, PD_F_E, E, tid, PD_TMAX, tg, tid < T, ev)) si[5] = 0;
         float e = -INFINITY;
         if (tid < T) {
           e = 0.f;
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) e += pd_ld(E + jj * PD_TMAX + tid);
+          for (int jj = 0; jj < 8; ++jj) e += ev[jj];
           if (a.constraint) {  // synthesis window (attention.py:202-215)
             const int pm = si[0], wn = a.win;
             bool masked;
@@ -553,6 +593,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         red[tid] = e;
       }
       __syncthreads();
+      if (!si[5]) return;
       if (w == 0) {
         float mx = -INFINITY;
         for (int i = lane; i < T; i += 64) mx = fmaxf(mx, red[i]);
@@ -646,26 +687,38 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       __syncthreads();
       {
         const int m = tid >> 4, col = tid & 15;
-        pd_st(a.PPx + (((long)p * PD_KSP + pks) * 32 + m) * PD_NPF + 16 * pn + col, sum_partials<4>(red, tid) + PPh[tid]);
+        pd_put(a.PPg + (((long)p * PD_KSP + pks) * 32 + m) * PD_NPF + 16 * pn + col, tg, sum_partials<4>(red, tid) + PPh[tid]);
       }
-      pd_publish(a, PD_F_PP, tg, tid);
+      __syncthreads();  // red / PPh are reused by the next tail
       PD_STAMP(12);
     }
     // ================= F: frame / stop (modules.py:392-448), prenet of step t+1 =================
     rec_half(a.H2x + p * 32 * PD_H, sW2h, 0, PPh, RG2, w, lane, tid);  // RG2(t+1) from h2_new(t), 1st half
-    const PrenetOps pops = prenet_ops(keep1n, keep2n, tid);
-    if (!pd_block_wait(si + 7, [&] { return pd_poll_all(a, PD_F_PP, PD_NTILE * PD_KSP, tg, 0, lane, false); })) return;
     PD_STAMP(13);
     int stopbit = 0;
-    if (rowv) {
-      if (tid < PD_NPF) {
-        float v = 0.f;
+    if (tid == 0) si[5] = 1;
+    __syncthreads();  // also: every proj work-group's PPh / red reads of stage E are done
+    {
+      // Every work-group -- padding rows too -- takes its row's partials: seeing all 176 producers
+      // is what orders the context slices of step t before the L1 context rows read after F.
+      if (tid < 384) {  // waves 0..5: the 352 projection columns of row b, 8 K-split partials each
+        float pv[PD_KSP];
+        const bool act = tid < PD_NPF;
+        if (!pd_take<PD_KSP>(a, PD_F_PP, a.PPg + ((long)p * PD_KSP * 32 + b) * PD_NPF, act ? tid : 0, 32 * PD_NPF,
+                             tg, act, pv))
+          si[5] = 0;
+        if (act && rowv) {
+          float v = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < PD_KSP; ++ks) v += pd_ld(a.PPx + (((long)p * PD_KSP + ks) * 32 + b) * PD_NPF + tid);
-        red[tid] = (v + sc[2] * a.PS[(long)b * PD_NPF + tid]) + a.proj_b[tid];
+          for (int ks = 0; ks < PD_KSP; ++ks) v += pv[ks];
+          red[tid] = (v + sc[2] * a.PS[(long)b * PD_NPF + tid]) + a.proj_b[tid];
+        }
       }
       __syncthreads();
+      if (!si[5]) return;
       PD_STAMP(20);
+    }
+    if (rowv) {
       const float sv = sigm(red[a.nm]);
       if (j == 0) {
         if (tid < a.nm) a.frames[((long)b * a.max_iters + t) * a.nm + tid] = red[tid];
@@ -673,6 +726,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       }
       stopbit = rintf(sv) == 1.0f;
     }
+    const PrenetOps pops = prenet_ops(keep1n, keep2n, tid);  // W2 slice: L2-resident
     if (t + 1 < a.max_iters) {
       if (a.TP1) {  // GTA (TacoTrainingHelper): the next input is the teacher frame t
         const float* tp = a.TP1 + ((long)b * a.T_lim + min(t, a.T_lim - 1)) * PD_P;

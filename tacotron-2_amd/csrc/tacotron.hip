@@ -1592,10 +1592,10 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     c->pd_ctl.alloc(sizeof(unsigned) * (2 * PD_NPH * PD_NB + 16));
     c->H1x.alloc(2L * 32 * PD_H * 4);
     c->H2x.alloc(2L * 32 * PD_H * 4);
-    c->Ex.alloc(2L * 32 * 8 * PD_TMAX * 4);
+    c->Ex.alloc(2L * 32 * 8 * PD_TMAX * 8);
     c->CTXx.alloc(2L * 32 * PD_E2 * 4);
     c->SSx.alloc(2L * 32 * 4);
-    c->PPx.alloc(2L * PD_KSP * 32 * PD_NPF * 4);
+    c->PPx.alloc(2L * PD_KSP * 32 * PD_NPF * 8);
     c->PREx.alloc(2L * 32 * PD_P * 4);
     for (auto& e : c->pd_ev) TT2_HIP(hipEventCreate(&e));
   }
@@ -1626,8 +1626,8 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   a.TP1 = targets_d ? c->TP1.as<float>() : nullptr;
   a.keysT = c->keysT.as<float>(); a.valuesT = c->valuesT.as<float>(); a.lengths = c->lens.as<int>();
   a.masks = masks_d;
-  a.H1x = c->H1x.as<float>(); a.H2x = c->H2x.as<float>(); a.Ex = c->Ex.as<float>(); a.CTXx = c->CTXx.as<float>();
-  a.SSx = c->SSx.as<float>(); a.PPx = c->PPx.as<float>(); a.PREx = c->PREx.as<float>();
+  a.H1x = c->H1x.as<float>(); a.H2x = c->H2x.as<float>(); a.Eg = c->Ex.as<unsigned long long>(); a.CTXx = c->CTXx.as<float>();
+  a.SSx = c->SSx.as<float>(); a.PPg = c->PPx.as<unsigned long long>(); a.PREx = c->PREx.as<float>();
   a.frames = frames_d; a.stop = stop_d; a.align = align_d;
   a.stamps = nullptr;
   a.stamp_step = -1;
