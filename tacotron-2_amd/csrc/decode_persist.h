@@ -59,7 +59,7 @@ struct PdArgs {
   float* CTXx;  // [2][32 x 512] AF: context_enc
   float* SSx;   // [2][32]: Σ_{t<len} alignments (style-context scale)
   unsigned long long* PPg; // [2][8 splits][32 rows][352] {tag, projection partial} granules
-  float* PREx;  // [2][32 x 256] AF: prenet output of the next step
+  unsigned long long* PREg;  // [2][32 x 256] AF-ordered {tag = step<<1 | stop bit, prenet output} granules
   // outputs
   float* frames;  // [B][max_iters][nm]
   float* stop;    // [B][max_iters]

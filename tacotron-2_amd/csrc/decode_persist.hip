@@ -338,7 +338,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     for (int i = 0; i < 4; ++i) o.w2p[i] = W2[i];
     return o;
   };
-  auto prenet = [&](const PrenetOps& o, auto pre1, int par, int tid) {
+  auto prenet = [&](const PrenetOps& o, auto pre1, int par, unsigned tag, int tid) {
     if (tid >= 256) {
       const int pos = tid - 256;
       const int col = 16 * (pos >> 4) + ((pos >> 2) & 3) + 4 * (pos & 3);  // af_group_col(pos)
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       for (int k16 = 0; k16 < 16; ++k16) v += red[k16 * 32 + tid];
       const int n = 32 * j + tid;
       const float out = rowv ? (fmaxf(v + b2p, 0.f) / 0.5f) * red[3072 + tid] : 0.f;
-      pd_st(a.PREx + par * 32 * PD_P + af_idx(b, n), out);
+      pd_put(a.PREg + par * 32 * PD_P + af_idx(b, n), tag, out);
     }
   };
 
@@ -391,9 +391,10 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   {
     float k1, k2;
     prenet_keep(0, tid, k1, k2);
-    prenet(prenet_ops(k1, k2, tid), [&](int pos) { return a.pre_b1[pos]; }, 0, tid);
+    prenet(prenet_ops(k1, k2, tid), [&](int pos) { return a.pre_b1[pos]; }, 0, 1u << 1, tid);
   }
-  pd_publish(a, PD_F_PRE, 1u << 1, tid);
+  if (tid == 0) si[1] = 0;
+  __syncthreads();
 
   for (int t = 0; t < a.max_iters; ++t) {
     const unsigned tg = t + 1;
@@ -411,49 +412,76 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     float keep1n, keep2n;  // prenet keep bits of step t+1, in flight during the whole step
     prenet_keep(t + 1, tid, keep1n, keep2n);
     // ================= A: LSTM layer 1 =================
-    if (!pd_block_wait(si + 2, [&] { return pd_poll_all(a, PD_F_PRE, PD_NB, tg, 1, lane, false); })) return;
-    PD_STAMP(1);
-    if (t > 0 && w == 0) {
-      // stop rule of step t-1 (TacoTestHelper.next_inputs, helpers.py:40-59 + dynamic_decode):
-      // every valid row rounds to 1 (stop_at_any: any row); GTA stops at T_targets instead
-      int dn;
-      if (a.T_lim > 0) {
-        dn = t >= a.T_lim;
-      } else {
-        const int gg = lane & 31, bb = (gg & 7) * 4 + ((gg >> 3) & 3);
-        const unsigned v = pd_flag(a.flags + PD_F_PRE * PD_NB + gg);
-        const bool valid = lane < 32 && bb < a.B;
-        const unsigned long long fb = __ballot(valid && (v & 1u)), vb = __ballot(valid);
-        dn = a.stop_at_any ? (fb != 0ull) : (fb == vb);
-      }
-      if (lane == 0) si[1] = dn;
-    }
-    __syncthreads();
-    if (t > 0 && si[1]) {
-      if (g == 0 && tid == 0) {
-        a.ctl[1] = t;
-        a.ctl[0] = 1;
-      }
-      return;
-    }
+    // prenet(t) of every row arrives as AF-ordered granules {tag = (t+1)<<1 | stop bit of the
+    // producing row at t-1, value}; wave w takes k-groups 2w, 2w+1 = columns [32w, 32w+32), written
+    // by the 32 work-groups of slice j = w, so the 8 waves together hear from all 256.
+    f32x4 a0[2], a1[2];
     {
-      // L1 input rows [prenet(t) | context(t-1)]: the context rows were accumulated into accC
-      // while the prenet hand-off was in flight
-      const float* X = a.PREx + p * 32 * PD_P;
-      f32x4 a0[2], a1[2];
+      const auto rp = __builtin_amdgcn_make_buffer_rsrc(a.PREg + p * 32 * PD_P, (short)0, 0x7fffffff, 0x00020000);
+      unsigned sb[2] = {0u, 0u};  // stop bits of rows lane%16 and 16 + lane%16
+      long long t0 = 0;
+      for (unsigned spin = 0;; ++spin) {
+        bool ok = true;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int sg = 2 * w + i;
-        a0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
-        a1[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int fo = (((2 * w + i) * 2 + h) * 64 + lane) * 4;  // AF float index of the lane's float4
+            const auto q0 = __builtin_amdgcn_raw_buffer_load_b128(rp, fo * 8, 0, 16);       // granules 0, 1
+            const auto q1 = __builtin_amdgcn_raw_buffer_load_b128(rp, fo * 8 + 16, 0, 16);  // granules 2, 3
+            f32x4 v = {__uint_as_float(q0[0]), __uint_as_float(q0[2]), __uint_as_float(q1[0]), __uint_as_float(q1[2])};
+            ok = ok && (q0[1] >> 1) == tg && (q0[3] >> 1) == tg && (q1[1] >> 1) == tg && (q1[3] >> 1) == tg;
+            if (h == 0) a0[i] = v;
+            else a1[i] = v;
+            if (i == 0) sb[h] = q0[1] & 1u;
+          }
+        if (__all(ok)) break;
+        if ((spin & 31) == 0) {
+          const long long now = __builtin_amdgcn_s_memrealtime();
+          if (spin == 0) {
+            t0 = now;
+          } else if (__hip_atomic_load((pd_gi32*)(a.ctl + 2), PD_RLX) != 0 || now - t0 > PD_TIMEOUT) {
+            if (lane == 0) {
+              __hip_atomic_store((pd_gi32*)(a.ctl + 2), 1 + PD_F_PRE, PD_RLX);
+              atomicMax(si + 1, 2);
+            }
+            break;
+          }
+        }
+        for (int z = 0; z < a.poll_sleep; ++z) __builtin_amdgcn_s_sleep(1);
       }
-      f32x4 s0 = accC0, s1 = accC1;
+      if (t > 0 && w == 0) {
+        // stop rule of step t-1 (TacoTestHelper.next_inputs, helpers.py:40-59 + dynamic_decode):
+        // every valid row rounds to 1 (stop_at_any: any row); GTA stops at T_targets instead
+        int dn;
+        if (a.T_lim > 0) {
+          dn = t >= a.T_lim;
+        } else {
+          const int r0 = lane & 15;
+          const bool v0 = lane < 16 && r0 < a.B, v1 = lane < 16 && r0 + 16 < a.B;
+          const unsigned long long f0 = __ballot(v0 && sb[0]), f1 = __ballot(v1 && sb[1]);
+          const unsigned long long m0 = __ballot(v0), m1 = __ballot(v1);
+          dn = a.stop_at_any ? ((f0 | f1) != 0ull) : (f0 == m0 && f1 == m1);
+        }
+        if (lane == 0 && dn) atomicMax(si + 1, 1);
+      }
+    }
+    PD_STAMP(1);
+    {
+      f32x4 s0 = accC0, s1 = accC1;  // L1 context rows of t-1, accumulated during the prenet hand-off
 #pragma unroll
       for (int i = 0; i < 2; ++i) kg_mfma(a0[i], a1[i], w1p[i], s0, s1);
       PD_STAMP(18);
       put_partials(s0, s1, red, w, lane);
       __syncthreads();
       PD_STAMP(19);
+    }
+    if (si[1]) {  // 1: the batch stopped at t-1 (every work-group decides alike); 2: a hand-off failed
+      if (si[1] == 1 && g == 0 && tid == 0) {
+        a.ctl[1] = t;
+        a.ctl[0] = 1;
+      }
+      return;
     }
     if (tid < 128) {
       float z[4];
@@ -730,12 +758,12 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     if (t + 1 < a.max_iters) {
       if (a.TP1) {  // GTA (TacoTrainingHelper): the next input is the teacher frame t
         const float* tp = a.TP1 + ((long)b * a.T_lim + min(t, a.T_lim - 1)) * PD_P;
-        prenet(pops, [&](int pos) { return tp[pos]; }, p ^ 1, tid);
+        prenet(pops, [&](int pos) { return tp[pos]; }, p ^ 1, ((tg + 1) << 1) | (unsigned)stopbit, tid);
       } else {  // free running: frame t through the folded layer-1 columns of the projection
-        prenet(pops, [&](int pos) { return red[PD_NPJ + pos]; }, p ^ 1, tid);
+        prenet(pops, [&](int pos) { return red[PD_NPJ + pos]; }, p ^ 1, ((tg + 1) << 1) | (unsigned)stopbit, tid);
       }
     }
-    pd_publish(a, PD_F_PRE, ((tg + 1) << 1) | (unsigned)stopbit, tid);
+    __syncthreads();  // red reuse by stage A
     PD_STAMP(14);
     {  // L1 context rows of step t+1 and the style scales: every context slice of t landed before
        // any PP flag (PP <- CTX slices of all 8 splits), and this work-group has seen all PP flags

@@ -1596,7 +1596,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     c->CTXx.alloc(2L * 32 * PD_E2 * 4);
     c->SSx.alloc(2L * 32 * 4);
     c->PPx.alloc(2L * PD_KSP * 32 * PD_NPF * 8);
-    c->PREx.alloc(2L * 32 * PD_P * 4);
+    c->PREx.alloc(2L * 32 * PD_P * 8);
     for (auto& e : c->pd_ev) TT2_HIP(hipEventCreate(&e));
   }
   const auto& cfg = c->cfg;
@@ -1627,7 +1627,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   a.keysT = c->keysT.as<float>(); a.valuesT = c->valuesT.as<float>(); a.lengths = c->lens.as<int>();
   a.masks = masks_d;
   a.H1x = c->H1x.as<float>(); a.H2x = c->H2x.as<float>(); a.Eg = c->Ex.as<unsigned long long>(); a.CTXx = c->CTXx.as<float>();
-  a.SSx = c->SSx.as<float>(); a.PPg = c->PPx.as<unsigned long long>(); a.PREx = c->PREx.as<float>();
+  a.SSx = c->SSx.as<float>(); a.PPg = c->PPx.as<unsigned long long>(); a.PREg = c->PREx.as<unsigned long long>();
   a.frames = frames_d; a.stop = stop_d; a.align = align_d;
   a.stamps = nullptr;
   a.stamp_step = -1;
