@@ -490,8 +490,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         const int idx = em * 16 + 4 * q + eu;
         z[q] = ((sum_partials<8>(red, idx) + RG1[idx]) + ssa[em] * gsv[q]) + b1v[q];
       }
-      const float cn = sigm(z[2] + 1.0f) * c1 + sigm(z[0]) * tanhf(z[1]);
-      const float hn = sigm(z[3]) * tanhf(cn);
+      const float cn = sigm_fast(z[2] + 1.0f) * c1 + sigm_fast(z[0]) * tanh_rcp(z[1]);
+      const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
       c1 = a.one_m_zo * cn + a.zo * c1;
       pd_st(a.H1x + p * 32 * PD_H + af_idx(em, 4 * g + eu), hn);
     }
@@ -530,8 +530,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         const int idx = em * 16 + 4 * q + eu;
         z[q] = (sum_partials<8>(red, idx) + RG2[idx]) + b2v[q];
       }
-      const float cn = sigm(z[2] + 1.0f) * c2 + sigm(z[0]) * tanhf(z[1]);
-      const float hn = sigm(z[3]) * tanhf(cn);
+      const float cn = sigm_fast(z[2] + 1.0f) * c2 + sigm_fast(z[0]) * tanh_rcp(z[1]);
+      const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
       c2 = a.one_m_zo * cn + a.zo * c2;
       pd_st(a.H2x + p * 32 * PD_H + af_idx(em, 4 * g + eu), hn);
     }
