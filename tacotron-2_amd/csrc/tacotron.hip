@@ -136,10 +136,10 @@ __global__ __launch_bounds__(256) void k_enc_lstm_step(EncLstmArgs a) {
 // ReferenceEncoder GRU + dense(tanh) (modules.py:57-64) and GST MultiheadAttention
 // (multihead_attention.py:35-132, tacotron.py:276-282) for one batch row.
 struct RefGstArgs {
-  const float* x;        // conv stack output [B][T2][gin]
-  int T2, gin, D;        // D = reference_depth (GRU units)
-  const float* kg; const float* bg;  // [(gin+D)][2D], [2D]
-  const float* kc; const float* bc;  // [(gin+D)][D], [D]
+  const float* xg;       // [B][T2][3D]: x_t·[Wg_x | Wc_x] + [bg | bc] for every frame (one GEMM)
+  int T2, D;             // D = reference_depth (GRU units)
+  const float* whg;      // [D][2D] recurrent rows of the gates kernel
+  const float* whc;      // [D][D]  recurrent rows of the candidate kernel
   const float* kd; const float* bd;  // [D][128], [128]
   const float* tokens;               // [ntok][tokd]
   const float* kq; const float* bq;  // [128][A], [A]
@@ -154,9 +154,9 @@ struct RefGstArgs {
 __global__ __launch_bounds__(256) void k_ref_gru_gst(RefGstArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int D = a.D, gin = a.gin, In = gin + D;
-  float* xh = sm;                 // [In]   concat(x, h) / concat(x, r*h)
-  float* h = xh + In;             // [D]
+  const int D = a.D;
+  float* rh = sm;                 // [D] r * h
+  float* h = rh + D;              // [D]
   float* gates = h + D;           // [2D]
   float* ref = gates + 2 * D;     // [128]
   float* q = ref + 128;           // [A]
@@ -165,24 +165,36 @@ __global__ __launch_bounds__(256) void k_ref_gru_gst(RefGstArgs a) {
   float* sc = vals + a.ntok * a.tokd; // [heads][ntok]
   for (int i = tid; i < D; i += blockDim.x) h[i] = 0.f;
   __syncthreads();
+  // TF GRUCell over every padded frame: [r, u] = σ([x, h]·Wg + bg), c = tanh([x, r⊙h]·Wc + bc),
+  // h' = u⊙h + (1-u)⊙c.  The x rows of both kernels (+ biases) were applied to all frames by one
+  // GEMM before this kernel; each step only does the D recurrent rows.
   for (int t = 0; t < a.T2; ++t) {
-    const float* xt = a.x + ((long)b * a.T2 + t) * gin;
-    for (int i = tid; i < gin; i += blockDim.x) xh[i] = xt[i];
-    for (int i = tid; i < D; i += blockDim.x) xh[gin + i] = h[i];
-    __syncthreads();
+    const float* xg = a.xg + ((long)b * a.T2 + t) * 3 * D;
     for (int j = tid; j < 2 * D; j += blockDim.x) {
-      float s = 0.f;
-      for (int k = 0; k < In; ++k) s += xh[k] * a.kg[(long)k * 2 * D + j];
-      gates[j] = sigm(s + a.bg[j]);
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < D; k += 4) {
+        s0 += h[k] * a.whg[(long)k * 2 * D + j];
+        s1 += h[k + 1] * a.whg[(long)(k + 1) * 2 * D + j];
+        s2 += h[k + 2] * a.whg[(long)(k + 2) * 2 * D + j];
+        s3 += h[k + 3] * a.whg[(long)(k + 3) * 2 * D + j];
+      }
+      gates[j] = sigm(xg[j] + ((s0 + s1) + (s2 + s3)));
     }
     __syncthreads();
-    for (int i = tid; i < D; i += blockDim.x) xh[gin + i] = gates[i] * h[i];  // r * h
+    for (int i = tid; i < D; i += blockDim.x) rh[i] = gates[i] * h[i];
     __syncthreads();
     float hn = 0.f;
     if (tid < D) {
-      float s = 0.f;
-      for (int k = 0; k < In; ++k) s += xh[k] * a.kc[(long)k * D + tid];
-      const float c = tanhf(s + a.bc[tid]);
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < D; k += 4) {
+        s0 += rh[k] * a.whc[(long)k * D + tid];
+        s1 += rh[k + 1] * a.whc[(long)(k + 1) * D + tid];
+        s2 += rh[k + 2] * a.whc[(long)(k + 2) * D + tid];
+        s3 += rh[k + 3] * a.whc[(long)(k + 3) * D + tid];
+      }
+      const float c = tanhf(xg[2 * D + tid] + ((s0 + s1) + (s2 + s3)));
       const float u = gates[D + tid];
       hn = u * h[tid] + (1.f - u) * c;
     }
@@ -952,7 +964,8 @@ __global__ void k_clip_frames(const float* __restrict__ src, long src_bstride, f
 // ==========================================================================================
 struct RefNetDev {
   DevBuf cw[6], cb[6], bs[6], bh[6];
-  DevBuf kg, bg, kc, bc, kd, bd, tok, kq, bq, kk, bk, av, ag, ab;
+  DevBuf wx, bx, whg, whc, kd, bd, tok, kq, bq, kk, bk, av, ag, ab;  // wx = [Wg_x | Wc_x], bx = [bg | bc]
+  int gin = 0;
 };
 
 struct Graph {
@@ -981,6 +994,7 @@ struct tt2_ctx {
   tt2::DevBuf loc_cw, keys_b, va, proj_w, proj_ws, proj_b;
   tt2::DevBuf post_cw[8], post_cb[8], post_bs[8], post_bh[8], post_pw, post_pb;
   // activations
+  tt2::DevBuf refxg;  // reference-encoder GRU input projections [B][T2][3D]
   tt2::DevBuf ids, lens, refm[2], x_a, x_b, xproj, enc_out, enc_h, enc_c, conv_a, conv_b, ref_out, style,
       values, keys;
   tt2::DevBuf X1[2], X2, Xp, H0s[2], H1s[2], RG0, RG1, GS0, PS, ssum, TP1, pre1, pcnt, c1, c2, Qp, energy, cum, max_att, PP, ctl,
@@ -1108,10 +1122,24 @@ static void finalize(tt2_ctx* c) {
       F = (F + 1) / 2;
     }
     const int gin = F * ci, D = cfg.reference_depth;
-    upload(R.kg, need(wm, s + "rnn/gru_cell/gates/kernel", {gin + D, 2 * D}));
-    upload(R.bg, need(wm, s + "rnn/gru_cell/gates/bias", {2 * D}));
-    upload(R.kc, need(wm, s + "rnn/gru_cell/candidate/kernel", {gin + D, D}));
-    upload(R.bc, need(wm, s + "rnn/gru_cell/candidate/bias", {D}));
+    {
+      const auto& kg = need(wm, s + "rnn/gru_cell/gates/kernel", {gin + D, 2 * D});
+      const auto& bg = need(wm, s + "rnn/gru_cell/gates/bias", {2 * D});
+      const auto& kc = need(wm, s + "rnn/gru_cell/candidate/kernel", {gin + D, D});
+      const auto& bc = need(wm, s + "rnn/gru_cell/candidate/bias", {D});
+      std::vector<float> wx((size_t)gin * 3 * D), bx(3 * D);
+      for (int k = 0; k < gin; ++k) {
+        for (int j = 0; j < 2 * D; ++j) wx[(size_t)k * 3 * D + j] = kg.data[(size_t)k * 2 * D + j];
+        for (int j = 0; j < D; ++j) wx[(size_t)k * 3 * D + 2 * D + j] = kc.data[(size_t)k * D + j];
+      }
+      for (int j = 0; j < 2 * D; ++j) bx[j] = bg.data[j];
+      for (int j = 0; j < D; ++j) bx[2 * D + j] = bc.data[j];
+      upload(R.wx, wx);
+      upload(R.bx, bx);
+      upload(R.whg, std::vector<float>(kg.data.begin() + (size_t)gin * 2 * D, kg.data.end()));
+      upload(R.whc, std::vector<float>(kc.data.begin() + (size_t)gin * D, kc.data.end()));
+      R.gin = gin;
+    }
     upload(R.kd, need(wm, s + "dense/kernel", {D, 128}));
     upload(R.bd, need(wm, s + "dense/bias", {128}));
     const int tokd = cfg.style_embed_depth / cfg.num_heads, Aa = cfg.style_att_dim;
@@ -1398,17 +1426,26 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
         x = bufs[i & 1];
         H = Ho; Wd = Wo; C = f;
       }
+      const int D = cfg.reference_depth;
+      TT2_CHECK(Wd * C == R.gin, TT2_ERR_SHAPE_MISMATCH, "reference encoder: GRU input width mismatch");
+      c->refxg.alloc(sizeof(float) * (size_t)B * H * 3 * D);
+      {  // x rows of the GRU gates + candidate kernels for every frame at once
+        GemmArgs g;
+        g.M = B * H; g.N = 3 * D; g.K = R.gin; g.A = x; g.lda = R.gin;
+        g.Bw = R.wx.as<float>(); g.ldb = 3 * D; g.Cout = c->refxg.as<float>(); g.ldc = 3 * D;
+        g.bias = R.bx.as<float>();
+        gemm(g, s);
+      }
       RefGstArgs a;
-      a.x = x; a.T2 = H; a.gin = Wd * C; a.D = cfg.reference_depth;
-      a.kg = R.kg.as<float>(); a.bg = R.bg.as<float>(); a.kc = R.kc.as<float>(); a.bc = R.bc.as<float>();
+      a.xg = c->refxg.as<float>(); a.T2 = H; a.D = D;
+      a.whg = R.whg.as<float>(); a.whc = R.whc.as<float>();
       a.kd = R.kd.as<float>(); a.bd = R.bd.as<float>(); a.tokens = R.tok.as<float>();
       a.kq = R.kq.as<float>(); a.bq = R.bq.as<float>(); a.kk = R.kk.as<float>(); a.bk = R.bk.as<float>();
       a.av = R.av.as<float>(); a.ag = R.ag.as<float>(); a.ab = R.ab.as<float>();
       a.ntok = cfg.num_gst; a.tokd = cfg.style_embed_depth / cfg.num_heads; a.A = cfg.style_att_dim;
       a.heads = cfg.num_heads; a.ref_out = c->ref_out.as<float>() + r * cfg.max_batch * 128;
       a.style = c->style.as<float>(); a.style_w = c->SW; a.style_off = r * cfg.style_embed_depth;
-      const int In = a.gin + a.D;
-      const size_t shm = sizeof(float) * (In + a.D + 2 * a.D + 128 + a.A + a.ntok * a.A + a.ntok * a.tokd +
+      const size_t shm = sizeof(float) * (a.D + a.D + 2 * a.D + 128 + a.A + a.ntok * a.A + a.ntok * a.tokd +
                                           a.heads * a.ntok + 16);
       hipLaunchKernelGGL(k_ref_gru_gst, dim3(B), dim3(256), shm, s, a);
       TT2_HIP(hipGetLastError());
