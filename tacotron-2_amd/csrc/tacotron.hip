@@ -133,6 +133,135 @@ __global__ __launch_bounds__(256) void k_enc_lstm_step(EncLstmArgs a) {
   }
 }
 
+// Persistent BiLSTM (fork-default U = 256): the whole recurrence as ONE launch of 2 x U/4
+// work-groups, work-group (dir, g) owning units [4g, 4g+4) of one direction with its recurrent
+// weight tile in registers.  h of step t travels to the direction's U/4 work-groups as AF-ordered
+// data-tagged 8-byte granules {tag = t+1, zoned h} (the data is the flag: one round trip per step,
+// cdna_hip_programming.md §6 Guideline 16 R2); every spin is bounded.  Same arithmetic as
+// k_enc_lstm_step.
+typedef __attribute__((address_space(1))) unsigned long long enc_gu64;
+typedef __attribute__((address_space(1))) int enc_gi32;
+constexpr int ENC_U = 256;
+struct EncPArgs {
+  const float* xproj;  // [B][T][8U]: x·W_x + b for both directions
+  const float* wh;     // [2][U/4 tiles][U x 16] WF
+  unsigned long long* Hg;  // [2 dirs][2 parities][32 x U] AF granules (zeroed before the launch)
+  float* out;          // [B][T][2U]
+  const int* lengths;
+  int B, T, Tmax;
+  float zo, one_m_zo;
+  int* err;            // timeout flag
+};
+
+__global__ __launch_bounds__(256) void k_enc_bilstm_persist(EncPArgs a) {
+  __shared__ float red[4 * 512];
+  __shared__ float G[512];
+  constexpr int U = ENC_U, ng = U / 4, NKG = U / 64;  // k-groups per wave
+  const int dir = blockIdx.x / ng, g = blockIdx.x % ng;
+  const int tid0 = threadIdx.x;
+  f32x4 wt[NKG];
+  {
+    const f32x4* Wt = reinterpret_cast<const f32x4*>(a.wh + ((long)(dir * ng + g) * U * 16));
+    const int w = tid0 >> 6, lane = tid0 & 63;
+#pragma unroll
+    for (int i = 0; i < NKG; ++i) wt[i] = Wt[(NKG * w + i) * 64 + lane];
+  }
+  const int m = (tid0 >> 2) & 31, uu = tid0 & 3, u = 4 * g + uu;
+  const int L = (tid0 < 128 && m < a.B) ? a.lengths[m] : 0;
+  float c = 0.f, hz = 0.f;  // cell and zoned hidden state of (m, u), threads < 128
+  unsigned long long* const Hd = a.Hg + (long)dir * 2 * 32 * U;
+  const auto r0 = __builtin_amdgcn_make_buffer_rsrc(Hd, (short)0, 0x7fffffff, 0x00020000);
+  const auto r1 = __builtin_amdgcn_make_buffer_rsrc(Hd + 32 * U, (short)0, 0x7fffffff, 0x00020000);
+  for (int t = 0; t < a.Tmax; ++t) {
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, w = tid >> 6;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    if (t > 0) {  // h(t-1): parity (t-1)&1, tag t
+      const auto rp = (t & 1) ? r0 : r1;
+      f32x4 x0[NKG], x1[NKG];
+      long long t0 = 0;
+      // cheap poll first: one sentinel granule (row 0 of the producer's first unit) per producer
+      // work-group of this wave's k-slice (units [U/4·w, U/4·(w+1)) = producers [16w, 16w+16))
+      for (unsigned spin = 0;; ++spin) {
+        bool ok = true;
+        if (lane < U / 16) {
+          const unsigned long long* sp = Hd + ((t - 1) & 1) * 32 * U + af_idx(0, 4 * (U / 16 * w + lane));
+          ok = (unsigned)(__hip_atomic_load((enc_gu64*)sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) ==
+               (unsigned)t;
+        }
+        if (__all(ok)) break;
+        if ((spin & 31) == 0) {
+          const long long now = __builtin_amdgcn_s_memrealtime();
+          if (spin == 0) {
+            t0 = now;
+          } else if (__hip_atomic_load((enc_gi32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                     now - t0 > 200000000LL) {
+            if (lane == 0) __hip_atomic_store((enc_gi32*)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+          }
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      for (unsigned spin = 0;; ++spin) {  // then every granule, verified (rarely re-read)
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < NKG; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int fo = (((NKG * w + i) * 2 + h) * 64 + lane) * 4;
+            const auto q0 = __builtin_amdgcn_raw_buffer_load_b128(rp, fo * 8, 0, 16);
+            const auto q1 = __builtin_amdgcn_raw_buffer_load_b128(rp, fo * 8 + 16, 0, 16);
+            const f32x4 v = {__uint_as_float(q0[0]), __uint_as_float(q0[2]), __uint_as_float(q1[0]),
+                             __uint_as_float(q1[2])};
+            ok = ok && q0[1] == (unsigned)t && q0[3] == (unsigned)t && q1[1] == (unsigned)t && q1[3] == (unsigned)t;
+            if (h == 0) x0[i] = v;
+            else x1[i] = v;
+          }
+        if (__all(ok)) break;
+        if ((spin & 31) == 0) {
+          const long long now = __builtin_amdgcn_s_memrealtime();
+          if (spin == 0) {
+            t0 = now;
+          } else if (__hip_atomic_load((enc_gi32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                     now - t0 > 200000000LL) {
+            if (lane == 0) __hip_atomic_store((enc_gi32*)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;  // whole wave; the others time out or see err the same way
+          }
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+#pragma unroll
+      for (int i = 0; i < NKG; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[i][e], wt[i][e], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[i][e], wt[i][e], acc1, 0, 0, 0);
+        }
+    }
+    reduce_waves_32x16<4>(acc0, acc1, red, G, w, lane, tid);
+    if (tid < 128) {
+      const bool act = t < L;
+      if (act) {
+        const int pos = dir == 0 ? t : L - 1 - t;
+        const float* xp = a.xproj + ((long)m * a.T + pos) * (8 * U) + dir * 4 * U;
+        const float zi = G[m * 16 + 0 * 4 + uu] + xp[0 * U + u];
+        const float zj = G[m * 16 + 1 * 4 + uu] + xp[1 * U + u];
+        const float zf = G[m * 16 + 2 * 4 + uu] + xp[2 * U + u];
+        const float zz = G[m * 16 + 3 * 4 + uu] + xp[3 * U + u];
+        const float cn = sigm(zf + 1.0f) * c + sigm(zi) * tanhf(zj);
+        const float hn = sigm(zz) * tanhf(cn);
+        c = a.one_m_zo * cn + a.zo * c;
+        hz = a.one_m_zo * hn + a.zo * hz;
+        a.out[((long)m * a.T + pos) * (2 * U) + dir * U + u] = hn;
+      }  // past the row's length the state is carried through unchanged
+      __hip_atomic_store((enc_gu64*)(Hd + (t & 1) * 32 * U + af_idx(m, u)),
+                         ((unsigned long long)(t + 1) << 32) | __float_as_uint(hz), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ReferenceEncoder GRU + dense(tanh) (modules.py:57-64) and GST MultiheadAttention
 // (multihead_attention.py:35-132, tacotron.py:276-282) for one batch row.
 struct RefGstArgs {
@@ -995,6 +1124,8 @@ struct tt2_ctx {
   tt2::DevBuf post_cw[8], post_cb[8], post_bs[8], post_bh[8], post_pw, post_pb;
   // activations
   tt2::DevBuf refxg;  // reference-encoder GRU input projections [B][T2][3D]
+  tt2::DevBuf enc_hg;  // persistent BiLSTM h granules [2][2][32 x U] + timeout word
+  bool enc_err_check = false;
   tt2::DevBuf ids, lens, refm[2], x_a, x_b, xproj, enc_out, enc_h, enc_c, conv_a, conv_b, ref_out, style,
       values, keys;
   tt2::DevBuf X1[2], X2, Xp, H0s[2], H1s[2], RG0, RG1, GS0, PS, ssum, TP1, pre1, pcnt, c1, c2, Qp, energy, cum, max_att, PP, ctl,
@@ -1395,6 +1526,19 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
   TT2_HIP(hipMemsetAsync(c->enc_out.p, 0, (size_t)BT * 2 * c->U * 4, s));
   int Tmax = 0;
   for (int b = 0; b < B; ++b) Tmax = std::max(Tmax, lens_h[b]);
+  if (c->U == ENC_U && c->pd_dev_ok && c->pd_mode == 1) {  // persistent recurrence (128 work-groups)
+    c->enc_hg.alloc(sizeof(unsigned long long) * 2 * 2 * 32 * ENC_U + 64);
+    TT2_HIP(hipMemsetAsync(c->enc_hg.p, 0, c->enc_hg.bytes, s));
+    EncPArgs a;
+    a.xproj = c->xproj.as<float>(); a.wh = c->enc_wh.as<float>(); a.Hg = c->enc_hg.as<unsigned long long>();
+    a.out = c->enc_out.as<float>(); a.lengths = lens_d; a.B = B; a.T = T; a.Tmax = Tmax;
+    a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
+    a.err = reinterpret_cast<int*>(a.Hg + 2 * 2 * 32 * ENC_U);
+    hipLaunchKernelGGL(k_enc_bilstm_persist, dim3(2 * ENC_U / 4), dim3(256), 0, s, a);
+    TT2_HIP(hipGetLastError());
+    TT2_HIP(hipMemcpyAsync(&c->ctl_host[2], a.err, sizeof(int), hipMemcpyDeviceToHost, s));
+    c->enc_err_check = true;
+  } else
   for (int t = 0; t < Tmax; ++t) {
     EncLstmArgs a;
     a.xproj = c->xproj.as<float>(); a.wh = c->enc_wh.as<float>(); a.hs = c->enc_h.as<float>();
@@ -1618,6 +1762,13 @@ static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, int t, hipStream_t
 }
 
 // ---- persistent decoder (decode_persist.hip) ----
+// the persistent BiLSTM's timeout word, copied to host behind the launch; read after a sync
+static void check_encoder(tt2_ctx* c) {
+  if (!c->enc_err_check) return;
+  c->enc_err_check = false;
+  TT2_CHECK(c->ctl_host[2] == 0, TT2_ERR_HIP, "persistent BiLSTM encoder: a hand-off wait timed out");
+}
+
 static bool pd_fits(tt2_ctx* c) {
   return c->pd_mode == 1 && c->pd_dev_ok && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
          c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= PD_TMAX && c->B <= 32;
@@ -1645,6 +1796,10 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
                      (long)c->Dm, c->valuesT.as<float>(), c->T_in, PD_E2);
   TT2_HIP(hipGetLastError());
   TT2_HIP(hipMemsetAsync(c->pd_ctl.p, 0, c->pd_ctl.bytes, s));  // flags + ctl words, every launch
+  // granule tags restart at 1 every launch: a stale tag of an earlier decode must never match
+  TT2_HIP(hipMemsetAsync(c->Ex.p, 0, c->Ex.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->PPx.p, 0, c->PPx.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->PREx.p, 0, c->PREx.bytes, s));
   PdArgs a;
   a.flags = c->pd_ctl.as<unsigned>();
   a.flags2 = a.flags + PD_NPH * PD_NB;
@@ -1681,6 +1836,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   TT2_HIP(hipMemcpyAsync(h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
   TT2_HIP(hipStreamSynchronize(s));
   TT2_HIP(hipEventElapsedTime(&c->pd_kernel_ms, c->pd_ev[0], c->pd_ev[1]));
+  check_encoder(c);
   TT2_CHECK(h[2] == 0, TT2_ERR_HIP,
             "persistent decoder: a hand-off wait timed out (phase " + std::to_string(h[2] - 1) +
                 "); set TT2_DECODER=launch to use the per-step launch path");
@@ -1956,6 +2112,8 @@ tt2_status tt2_encode(tt2_ctx* c, const int32_t* ids, const int32_t* lengths, in
       ref_d[r] = c->refm[r].as<float>();
     }
     encode_dev(c, c->ids.as<int>(), c->lens.as<int>(), lengths, B, T_in, ref_d, trs, s);
+    TT2_HIP(hipStreamSynchronize(s));
+    check_encoder(c);
     if (memory_out)
       TT2_HIP(hipMemcpyAsync(memory_out, c->values.p, sizeof(float) * B * T_in * c->Dm, hipMemcpyDeviceToHost, s));
     if (style_out && c->SW)

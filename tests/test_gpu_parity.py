@@ -218,6 +218,24 @@ def test_persistent_stop_rule(full_setup):
         assert out["frames"].shape[1] == ref["decoder_output"].shape[1]
 
 
+def test_persistent_repeat_calls_after_early_stop(full_setup):
+    """Granule tags restart every launch: a decode that stopped after 2 steps must not leave tags
+    that a second decode on the same context accepts as fresh."""
+    hp, W = full_setup
+    B, T, n = 4, 19, 20
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=17)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=17)
+    eng = _engine(hp, W, B, T, 64, n)
+    ids0, lens0, re0, rs0 = tacotron_inputs(B, T, 64, seed=99)  # different first call
+    first = eng.synthesize(ids0, lens0, re0, rs0, 2, prenet_masks(2, B, hp.prenet_layers[0], seed=99))
+    assert first["frames"].shape[1] == 2
+    again = eng.synthesize(ids, lens, re, rs, n, masks)      # same context, full horizon
+    eng.close()
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, n)
+    np.testing.assert_allclose(again["decoder_output"], ref["decoder_output"], atol=MEL_TOL)
+    np.testing.assert_allclose(again["alignments"], ref["alignments"], atol=MEL_TOL)
+
+
 def test_persistent_matches_launch_path_long(full_setup):
     """1000-step horizon at configs[1] shapes: persistent decoder vs the per-step launch path
     (both HIP; the oracle is too slow for 1000 steps x 32 rows in a unit test)."""
