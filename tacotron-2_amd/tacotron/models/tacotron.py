@@ -42,6 +42,29 @@ class Tacotron():
         self._weights = dict(weights)
         self._engine = None
 
+    def load_checkpoint(self, checkpoint, scopes=None):
+        """tf.train.Saver(var_list).restore(sess, checkpoint) without TensorFlow: read the TF
+        tensor bundle ``checkpoint`` (a prefix, or a directory holding a ``checkpoint`` state file
+        as tf.train.get_checkpoint_state reads it) with tt2.ckpt and overwrite the matching
+        variables; ``scopes`` restricts the restore to names containing one of the substrings,
+        like the reference's refnet restore (tacotron/train.py:284-285, 330-338:
+        ``load_checkpoint('spk_disc/pretrained_model_emt_disc', scopes=['refnet_emt'])``).
+        Returns the restored names."""
+        from tt2 import ckpt
+        prefix = ckpt.latest_checkpoint(checkpoint) if os.path.isdir(checkpoint) else checkpoint
+        names = [n for n, _ in ckpt.list_variables(prefix) if n.startswith("Tacotron_model/")
+                 and (scopes is None or any(sc in n for sc in scopes))]
+        values = ckpt.read_checkpoint(prefix, set(names))
+        if self._weights is None:
+            self._weights = {}
+        for n, v in values.items():
+            if n in self._weights and self._weights[n].shape != v.shape:
+                raise ValueError("checkpoint variable {} has shape {}, model expects {}".format(
+                    n, v.shape, self._weights[n].shape))
+            self._weights[n] = v.astype(np.float32)
+        self._engine = None
+        return sorted(values)
+
     def init_random_weights(self, seed=None, emt_only=False):
         hp = self._hparams
         self.load_weights(init_tacotron_weights(
