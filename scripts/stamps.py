@@ -1,0 +1,21 @@
+"""Summarise gpurun_out/pd_stamps.npy (TT2_STAMP_STEP stage stamps of k_decode_persist, 256 x 32
+s_memrealtime values at 100 MHz) per stage: median / max over work-groups, proj vs other."""
+import sys
+
+import numpy as np
+
+NAMES = {0: "start", 1: "A pre taken", 18: "A mfma", 19: "A red", 2: "H1 pub", 3: "after H1 pub", 4: "H1 wait",
+         16: "B mfma", 17: "B red", 5: "H2 pub", 6: "prefetch", 7: "C start", 8: "energies", 9: "projh+RG1a",
+         21: "softmax", 10: "CTX pub", 11: "CTX wait(proj)", 12: "PP put", 13: "RG2 tail0", 20: "PP take",
+         14: "prenet", 15: "end"}
+ORDER = [0, 1, 18, 19, 2, 3, 4, 16, 17, 5, 6, 7, 8, 9, 21, 10, 11, 12, 13, 20, 14, 15]
+s = np.load(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pd_stamps.npy").astype(np.int64)
+r = (s - s[:, 0].min()) * 0.01
+g = np.arange(256)
+for i in ORDER:
+    line = f"{i:2d} {NAMES[i]:16s}"
+    for k, m in (("all", g >= 0), ("proj", g < 176), ("other", g >= 176)):
+        v = r[m, i][s[m, i] != 0]
+        if len(v):
+            line += f"  {k}: {np.median(v):6.2f} / {v.max():6.2f}"
+    print(line)

@@ -184,6 +184,21 @@ def test_persistent_full_batch_free_run(full_setup):
     out, ref = _decode_compare(hp, W, B=32, T=201, T_ref=96, n=50, seed=21)
 
 
+def test_trained_refnet_weights_persistent(full_setup):
+    """The reference's own trained emotion reference encoder (refnet_emt, ckpt-5200, restored
+    the way tacotron/train.py:284 does; committed as tests/golden/refnet_emt_ckpt5200.npz) in
+    place of the random refnet_emt weights: encoder + style path + persistent decoder vs oracle."""
+    import os
+    hp, W = full_setup
+    fx = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "refnet_emt_ckpt5200.npz")
+    W2 = dict(W)
+    with np.load(fx) as z:
+        for k in z.files:
+            assert W2[k].shape == z[k].shape, k
+            W2[k] = z[k]
+    _decode_compare(hp, W2, B=32, T=121, T_ref=96, n=30, seed=31)
+
+
 def test_persistent_selected_for_bench_shape(full_setup):
     hp, W = full_setup
     ids, lens, re, rs = tacotron_inputs(32, 201, 64, seed=4)
