@@ -20,12 +20,14 @@ constexpr int PD_NTILE = 22;  // projection column tiles
 constexpr int PD_KSP = 8;     // projection K split (128 h2 rows + 64 context rows per split)
 constexpr int PD_TMAX = 256;  // max encoder steps (T_in)
 constexpr int PD_KLP = 32;    // location-conv taps padded to 16
+constexpr int PD_NREP = 8;    // replicas of the H1/H2 flag lines (32 pollers per line)
 enum { PD_F_PRE = 0, PD_F_H1, PD_F_H2, PD_F_E, PD_F_CTX, PD_F_PP, PD_NPH };
 
 struct PdArgs {
   unsigned* flags;  // [PD_NPH][PD_NB] hand-off tags (zeroed before every launch)
   unsigned* flags2; // [PD_NPH][8 groups][32] group-level tags of the all-producer waits
   int* ctl;         // [4]: done, n_steps, err, pad (zeroed before every launch)
+  unsigned* rflags; // [2: H1, H2][PD_NREP replicas][PD_NB] hand-off tags, one replica per consumer XCD group
   int B, T_in, max_iters, T_lim, nm;
   int stop_at_any, mask_encoder, cumulative, constraint, monotonic, win;
   float zo, one_m_zo;

@@ -116,6 +116,14 @@ __device__ __forceinline__ bool pd_poll_all(const PdArgs& a, int ph, int nprod, 
   return pd_spin(a, ph, lane, [&] { return lane >= 8 || pd_flag(f2 + lane) >= need; });
 }
 
+// Wave-level poll of the 32 producers [base, base+32) of h-phase r (0: H1, 1: H2) on this work-group's
+// replica of their flag line (replica g%8: 32 pollers per line).  Each wave waits only for the
+// producers of the rows it loads, so early waves start their MFMAs while late producers finish.
+__device__ __forceinline__ bool pd_poll_rep(const PdArgs& a, int ph, int r, int base, unsigned need, int lane) {
+  const unsigned* f = a.rflags + (r * PD_NREP + (blockIdx.x & (PD_NREP - 1))) * PD_NB + base;
+  return pd_spin(a, ph, lane, [&] { return lane >= 32 || pd_flag(f + lane) >= need; });
+}
+
 // Block-level waits: wave 0 polls, the work-group joins at a barrier (result via LDS slot).
 template <class F>
 __device__ __forceinline__ bool pd_block_wait(int* slot, F poll) {
@@ -168,6 +176,13 @@ __device__ __forceinline__ void pd_publish(const PdArgs& a, int ph, unsigned val
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) __hip_atomic_store((pd_gu32*)(a.flags + ph * PD_NB + blockIdx.x), val, PD_RLX);
+}
+
+// pd_publish to every replica of h-phase r's flag line.
+__device__ __forceinline__ void pd_publish_rep(const PdArgs& a, int r, unsigned val, int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid < PD_NREP) __hip_atomic_store((pd_gu32*)(a.rflags + (r * PD_NREP + tid) * PD_NB + blockIdx.x), val, PD_RLX);
 }
 
 // acc(rows 0..15 | 16..31) += A(k-group) · W(k-group, 16 columns)
@@ -300,6 +315,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   if (tid == 0) {
     si[0] = 0;
     si[4] = 0;
+    si[8] = 0;
     sc[2] = 0.f;
   }
   f32x4 vals[8];  // values[b][32*(tid/64) + 4i + e][64j + tid%64]: valuesT is [B][E2][256], 0 past T_in
@@ -495,12 +511,13 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       c1 = a.one_m_zo * cn + a.zo * c1;
       pd_st(a.H1x + p * 32 * PD_H + af_idx(em, 4 * g + eu), hn);
     }
-    pd_publish(a, PD_F_H1, tg, tid);
+    pd_publish_rep(a, 0, tg, tid);
     PD_STAMP(2);
     if (t > 0) rec_half(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, 1, PPh, RG2, w, lane, tid);  // RG2(t), 2nd half
     PD_STAMP(3);
     // ================= B: LSTM layer 2 =================
-    if (!pd_block_wait(si + 3, [&] { return pd_poll_all(a, PD_F_H1, PD_NB, tg, 0, lane, true); })) return;
+    // wave w multiplies h1 units [128w, 128w+128) = the rows of producers [32w, 32w+32)
+    if (!pd_poll_rep(a, PD_F_H1, 0, 32 * w, tg, lane)) si[8] = 1;
     PD_STAMP(4);
     {
       const float* X = a.H1x + p * 32 * PD_H;
@@ -522,6 +539,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       put_partials(s0, s1, red, w, lane);
       __syncthreads();
       PD_STAMP(17);
+      if (si[8]) return;
     }
     if (tid < 128) {
       float z[4];
@@ -535,7 +553,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       c2 = a.one_m_zo * cn + a.zo * c2;
       pd_st(a.H2x + p * 32 * PD_H + af_idx(em, 4 * g + eu), hn);
     }
-    pd_publish(a, PD_F_H2, tg, tid);
+    pd_publish_rep(a, 1, tg, tid);
     PD_STAMP(5);
     // issued ahead of the RG1 tail and the H2 wait (L2-resident: shared by the 32 rows of slice j):
     f32x4 wq[8];  // W_q[32*(tid/16) + 4i + e][16j + tid%16] (q_wt is [A][H])
@@ -553,13 +571,15 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     rec_half(a.H1x + p * 32 * PD_H, sW1h, 0, RGc, RG1, w, lane, tid);  // RG1(t+1) from h1_new(t), 1st half
     PD_STAMP(6);
     // ================= C: query slice + partial energies (attention.py:37-69, 186-201) =================
-    if (!pd_block_wait(si + 4, [&] { return pd_poll_all(a, PD_F_H2, PD_NB, tg, 0, lane, true); })) return;
+    // wave w: producers [32w, 32w+32) = h2 units [128w, 128w+128), the units its RG2 tails read
+    // too; after the next barrier every wave may read all of h2_new (projection h2 rows)
+    if (!pd_poll_rep(a, PD_F_H2, 1, 32 * w, tg, lane)) si[8] = 1;
     PD_STAMP(7);
 
     if (rowv) {
       const float* X = a.H2x + p * 32 * PD_H;
-      red[tid] = pd_ld(X + af_idx(b, tid));
-      red[tid + 512] = pd_ld(X + af_idx(b, tid + 512));
+      red[128 * w + lane] = pd_ld(X + af_idx(b, 128 * w + lane));
+      red[128 * w + 64 + lane] = pd_ld(X + af_idx(b, 128 * w + 64 + lane));
       __syncthreads();
       {
         const int k = tid & 15, seg = tid >> 4;
@@ -586,6 +606,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         }
     }
     __syncthreads();  // red / qv reuse below
+    if (si[8]) return;
     PD_STAMP(8);
     if (isproj) {  // projection partial, h2_new rows of this split (Architecture_wrappers.py:243-247)
       const float* X = a.H2x + p * 32 * PD_H;

@@ -1777,7 +1777,7 @@ static bool pd_fits(tt2_ctx* c) {
 static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, const float* targets_d, int T_lim,
                                float* frames_d, float* stop_d, float* align_d, hipStream_t s) {
   if (!c->H1x.p) {
-    c->pd_ctl.alloc(sizeof(unsigned) * (2 * PD_NPH * PD_NB + 16));
+    c->pd_ctl.alloc(sizeof(unsigned) * (2 * PD_NPH * PD_NB + 32 + 2 * PD_NREP * PD_NB));
     c->H1x.alloc(2L * 32 * PD_H * 4);
     c->H2x.alloc(2L * 32 * PD_H * 4);
     c->Ex.alloc(2L * 32 * 8 * PD_TMAX * 8);
@@ -1804,6 +1804,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   a.flags = c->pd_ctl.as<unsigned>();
   a.flags2 = a.flags + PD_NPH * PD_NB;
   a.ctl = reinterpret_cast<int*>(a.flags + 2 * PD_NPH * PD_NB);
+  a.rflags = a.flags + 2 * PD_NPH * PD_NB + 32;
   a.B = c->B; a.T_in = c->T_in; a.max_iters = max_iters; a.T_lim = targets_d ? T_lim : 0; a.nm = c->nm;
   a.stop_at_any = cfg.stop_at_any; a.mask_encoder = cfg.mask_encoder; a.cumulative = cfg.cumulative_weights;
   a.constraint = cfg.synthesis_constraint; a.monotonic = cfg.constraint_monotonic; a.win = cfg.attention_win_size;
