@@ -304,11 +304,6 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   const int len = rowv ? a.lengths[b] : 0;
   const float va_k = a.va[16 * j + (lane & 15)];
   const float b2p = a.pre_b2[32 * j + (tid & 31)];
-  for (int e = tid; e < 512; e += PD_NT) {
-    RG1[e] = 0.f;
-    RG2[e] = 0.f;
-    RGc[e] = 0.f;  // context(-1) = 0
-  }
   for (int e = tid; e < 288; e += PD_NT) cw[e] = 0.f;
   if (tid < 256) al[tid] = 0.f;
   if (tid < 32) ssa[tid] = 0.f;
@@ -327,6 +322,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   }
   f32x4 loc[2] = {zero4, zero4};  // location features of the next step (cum = 0)
   f32x4 accC0 = zero4, accC1 = zero4;  // L1 context rows of the next step (context(-1) = 0)
+  f32x4 q1a = zero4, q1b = zero4, q2a = zero4, q2b = zero4;  // this wave's Q partials of RG1, RG2
   const long BP = (long)a.B * PD_P;
 
   // Prenet (modules.py:346-357, dropout always on) of decoder step ts for row b, outputs
@@ -380,12 +376,13 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
   };
 
-  // Recurrent tail half h (all 8 waves, K split 8 ways, k-groups 8w + 4h .. +4): the zoned-state
-  // recurrence RG(t+1) = h_z(t)·W_h = (1-z)·h_new(t)·W_h + z·RG(t) is linear in h_new, so it is
-  // computed in two halves placed in two hand-off windows: half 0 -> tmp, half 1 -> dst mixed.
-  auto rec_half = [&](const float* X, const float* Wl, int h, float* tmp, float* dst, int w, int lane, int tid) {
+  // Recurrent tail half h (all 8 waves, K split 8 ways, k-groups 8w + 4h .. +4).  The zoned-state
+  // recurrence RG(t+1) = h_z(t)·W_h = (1-z)·h_new(t)·W_h + z·RG(t) is linear in h_new, so every wave
+  // keeps its own K-slice partial Q_w with RG = (1-z)·Σ_w Q_w:  Q_w(t+1) = z·Q_w(t) + h_new(t)·W_h
+  // (its slice), in registers.  No reduction: the partials join the gate accumulators of stage A/B,
+  // whose cross-wave reduction runs anyway.  The two halves sit in two hand-off windows.
+  auto rec_half = [&](const float* X, const float* Wl, int h, f32x4& Qa, f32x4& Qb, int w, int lane) {
     const f32x4* Wv = reinterpret_cast<const f32x4*>(Wl);
-    f32x4 s0 = zero4, s1 = zero4;
     f32x4 x0[4], x1v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -393,14 +390,15 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
       x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
     }
+    if (h == 0) {
+      Qa = a.zo * Qa;
+      Qb = a.zo * Qb;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int sg = 8 * w + 4 * h + i;
-      kg_mfma(x0[i], x1v[i], Wv[sg * 64 + lane], s0, s1);
+      kg_mfma(x0[i], x1v[i], Wv[sg * 64 + lane], Qa, Qb);
     }
-    reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
-    if (h == 0) tmp[tid] = G[tid];
-    else dst[tid] = a.one_m_zo * (tmp[tid] + G[tid]) + a.zo * dst[tid];
   };
   __syncthreads();
   // GO frame (helpers.py:136-138): frame 0 -> layer-1 pre-activation = b1
@@ -484,7 +482,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     PD_STAMP(1);
     {
-      f32x4 s0 = accC0, s1 = accC1;  // L1 context rows of t-1, accumulated during the prenet hand-off
+      // L1 context rows of t-1 (accumulated during the prenet hand-off) + this wave's RG1 partial
+      f32x4 s0 = accC0 + a.one_m_zo * q1a, s1 = accC1 + a.one_m_zo * q1b;
 #pragma unroll
       for (int i = 0; i < 2; ++i) kg_mfma(a0[i], a1[i], w1p[i], s0, s1);
       PD_STAMP(18);
@@ -504,7 +503,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = em * 16 + 4 * q + eu;
-        z[q] = ((sum_partials<8>(red, idx) + RG1[idx]) + ssa[em] * gsv[q]) + b1v[q];
+        z[q] = (sum_partials<8>(red, idx) + ssa[em] * gsv[q]) + b1v[q];
       }
       const float cn = sigm_fast(z[2] + 1.0f) * c1 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
@@ -513,7 +512,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish_rep(a, 0, tg, tid);
     PD_STAMP(2);
-    if (t > 0) rec_half(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, 1, PPh, RG2, w, lane, tid);  // RG2(t), 2nd half
+    if (t > 0) rec_half(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, 1, q2a, q2b, w, lane);  // RG2(t), 2nd half
     PD_STAMP(3);
     // ================= B: LSTM layer 2 =================
     // wave w multiplies h1 units [128w, 128w+128) = the rows of producers [32w, 32w+32)
@@ -521,7 +520,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     PD_STAMP(4);
     {
       const float* X = a.H1x + p * 32 * PD_H;
-      f32x4 s0 = zero4, s1 = zero4;
+      f32x4 s0 = a.one_m_zo * q2a, s1 = a.one_m_zo * q2b;  // + this wave's RG2 partial
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         f32x4 x0[4], x1v[4];
@@ -546,7 +545,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = em * 16 + 4 * q + eu;
-        z[q] = (sum_partials<8>(red, idx) + RG2[idx]) + b2v[q];
+        z[q] = sum_partials<8>(red, idx) + b2v[q];
       }
       const float cn = sigm_fast(z[2] + 1.0f) * c2 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
@@ -568,7 +567,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) kv[i] = K[(w + 8 * i) * 4 + (lane >> 4)];
     }
-    rec_half(a.H1x + p * 32 * PD_H, sW1h, 0, RGc, RG1, w, lane, tid);  // RG1(t+1) from h1_new(t), 1st half
+    rec_half(a.H1x + p * 32 * PD_H, sW1h, 0, q1a, q1b, w, lane);  // RG1(t+1) from h1_new(t), 1st half
     PD_STAMP(6);
     // ================= C: query slice + partial energies (attention.py:37-69, 186-201) =================
     // wave w: producers [32w, 32w+32) = h2 units [128w, 128w+128), the units its RG2 tails read
@@ -709,7 +708,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     pd_publish(a, PD_F_CTX, tg, tid);
     PD_STAMP(10);
-    rec_half(a.H1x + p * 32 * PD_H, sW1h, 1, RGc, RG1, w, lane, tid);  // RG1(t+1), 2nd half
+    rec_half(a.H1x + p * 32 * PD_H, sW1h, 1, q1a, q1b, w, lane);  // RG1(t+1), 2nd half
     // location features of step t+1: im2col(cum) · (W_conv·W_loc) on MFMA (attention.py:59-62)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -742,7 +741,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       PD_STAMP(12);
     }
     // ================= F: frame / stop (modules.py:392-448), prenet of step t+1 =================
-    rec_half(a.H2x + p * 32 * PD_H, sW2h, 0, PPh, RG2, w, lane, tid);  // RG2(t+1) from h2_new(t), 1st half
+    rec_half(a.H2x + p * 32 * PD_H, sW2h, 0, q2a, q2b, w, lane);  // RG2(t+1) from h2_new(t), 1st half
     PD_STAMP(13);
     int stopbit = 0;
     if (tid == 0) si[5] = 1;
