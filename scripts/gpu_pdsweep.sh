@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-sw}
-for S in 1 4 10 20; do
-  TT2_PD_SLEEP=$S TT2_STAMP_STEP=500 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-wavenet > gpurun_out/sw_${TAG}_$S.json 2> gpurun_out/sw_${TAG}_$S.err || { echo "bench failed $S"; tail -5 gpurun_out/sw_${TAG}_$S.err; exit 1; }
-  python -c "import json; d=json.load(open('gpurun_out/sw_${TAG}_$S.json')); print($S, d['roofline']['us_per_step'], d['diag_stamps']['persist_stage_us_min'][:16])"
+for S in ${SWEEP:-0 1 2 4 8}; do
+  env ${SWVAR:-TT2_PD_SLEEP}=$S timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-wavenet > gpurun_out/sw_${TAG}_$S.json 2> gpurun_out/sw_${TAG}_$S.err || { echo "bench failed $S"; tail -5 gpurun_out/sw_${TAG}_$S.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/sw_${TAG}_$S.json')); print($S, d['roofline']['us_per_step'])"
 done
