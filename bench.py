@@ -17,10 +17,14 @@ import os
 import sys
 import time
 
+import ctypes
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "tacotron-2_amd"), ROOT]
+
+from tt2 import _lib  # noqa: E402
 
 METRIC = "mel-frames/sec (decoder) + audio-samples/sec (WaveNet) @1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
@@ -38,6 +42,9 @@ def parse():
     p.add_argument("--wavenet-frames", type=int, default=80, help="mel frames per WaveNet utterance")
     p.add_argument("--wavenet-steps", type=int, default=1)
     p.add_argument("--no-wavenet", action="store_true")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--e2e-frames", type=int, default=1000,
+                   help="decoder frames per utterance of the end-to-end leg (configs[3])")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=100)
     p.add_argument("--profile-iters", type=int, default=50)
@@ -123,6 +130,67 @@ def load_traffic(kernel):
     except Exception:
         return None
 
+E2E_TEXT = ("Scientists at the CERN laboratory say they have discovered a new particle. "
+            "The buses aren't the problem, they actually provide a solution. Does the quick "
+            "brown fox jump over the lazy dog? He thought it was time to present the present.")
+
+
+def bench_e2e(a, rank, world, local, barrier, max_over_ranks):
+    """configs[3]: end-to-end text -> mel -> wav, batch = world utterances sharded one per rank
+    (8 over 8 GPUs in the config), each a 200-character text through the text frontend,
+    Tacotron-2 (T_out = a.e2e_frames decoder frames, stop ignored by the random-init stop bias) and
+    the 24-layer R=64 MoL WaveNet (T_out x 275 samples); one all_gather of the trimmed waveforms
+    (RCCL) closes the timed region.  Weak scaling: utterances/s = world / max-over-ranks time."""
+    import torch
+    from tacotron.utils.text import text_to_sequence
+    from tt2.e2e import TextToSpeech, e2e_hparams, synthesize_sharded
+    from tt2.weights import init_tacotron_weights, init_wavenet_weights
+    hp = e2e_hparams(a.e2e_frames)
+    text = E2E_TEXT[:200]
+    seq = text_to_sequence(text, [c.strip() for c in hp.cleaners.split(",")])
+    ids = np.asarray([seq] * world, np.int32)
+    lens = np.full((world,), len(seq), np.int32)
+    rng = np.random.default_rng(1234)
+    re = rng.uniform(-4, 4, (world, a.ref_frames, hp.num_mels)).astype(np.float32)
+    rs = rng.uniform(-4, 4, (world, a.ref_frames, hp.num_mels)).astype(np.float32)
+    W = init_tacotron_weights(hp, seed=hp.tacotron_random_seed)
+    WW = init_wavenet_weights(hp, seed=hp.wavenet_random_seed)
+    tts = TextToSpeech(hp, W, WW, 1, ids.shape[1], a.ref_frames, a.e2e_frames, local)
+
+    def run():
+        if world > 1:
+            return synthesize_sharded(tts, ids, lens, re, rs, seed=5339)
+        return tts.synthesize(ids, lens, re, rs, seed=5339)["wavs"]
+
+    # warm-up: every kernel once on a short decode (same shapes except the step count)
+    dev = torch.device("cuda", local)
+    tts.synthesize_dev(torch.from_numpy(ids[:1]).to(dev), torch.from_numpy(lens[:1]).to(dev),
+                       lens[:1], torch.from_numpy(re[:1]).to(dev), torch.from_numpy(rs[:1]).to(dev),
+                       seed=1, max_iters=8)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    wavs = run()
+    torch.cuda.synchronize()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    ms3 = (ctypes.c_float * 3)()
+    _lib.check(tts.lib.tt2_last_timings(tts.taco.h, ms3))
+    wms = (ctypes.c_float * 3)()
+    _lib.check(tts.lib.tt2_wn_last_timings(tts.wn.h, wms))
+    samples = int(sum(w.shape[0] for w in wavs))
+    tts.close()
+    return dict(metric="utterances/sec (text->mel->wav)", value=round(world / el, 4),
+                unit="utterances/s", audio_samples_per_s=round(samples / el, 1),
+                realtime_factor=round(samples / el / hp.sample_rate / world, 3),
+                seconds=round(el, 3), utterances=world, per_rank_utterances=1,
+                chars=len(seq) - 1, decoder_frames=a.e2e_frames, samples_per_utterance=samples // world,
+                rank0_phases_ms=dict(encode=round(ms3[0], 2), decode=round(ms3[1], 2),
+                                     postnet=round(ms3[2], 2), upsample=round(wms[0], 2),
+                                     cond_gemm=round(wms[1], 2), generate=round(wms[2], 2)),
+                config="configs[3]: end-to-end text->mel->wav, {} utterance(s) sharded one per "
+                       "GPU, waveforms all-gathered{}".format(world, " over RCCL" if world > 1 else ""))
+
 
 def main():
     a = parse()
@@ -147,8 +215,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    import ctypes
-    from tt2 import _lib
     from tt2.engine import TacotronEngine, WaveNetEngine
     from tt2.hparams import bench_wavenet_hparams, hparams
     from tt2.weights import init_tacotron_weights, init_wavenet_weights
@@ -305,6 +371,11 @@ def main():
                   diag_stage_stamps_us=wn_stamps, diag_shader_clock_mhz=wn_clock_mhz)
         weng.close()
 
+    # --- end-to-end text -> mel -> wav (configs[3]): one utterance per rank, RCCL gather ---
+    e2e = None
+    if not a.no_e2e:
+        e2e = bench_e2e(a, rank, world, local, barrier, max_over_ranks)
+
     # --- CPU baseline (rank 0, N = 1 only) ---
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -334,7 +405,7 @@ def main():
                                global_batch=B * world, chars=a.chars, t_out=a.t_out,
                                decoded_steps=n_steps.value, ref_frames=a.ref_frames,
                                parallelism="utterance-batch sharding x{}".format(world)),
-                   phases=phases, roofline=roofline, cpu_baseline=cpu, wavenet=wn,
+                   phases=phases, roofline=roofline, cpu_baseline=cpu, wavenet=wn, e2e=e2e,
                    diag_stamps=stamps)
         print(json.dumps(out))
     eng.close()

@@ -138,6 +138,13 @@ tt2_status tt2_synthesize_dev(tt2_ctx* ctx, const int32_t* ids_d, const int32_t*
                               uint64_t seed, float* mel_d, float* stop_d, int32_t* n_steps_host,
                               void* stream);
 
+/* get_output_lengths (tacotron/synthesizer.py:384-387) on device: lengths_d[b] = first step
+ * t < n_steps whose stop probability rounds to 1 (np.round: half-to-even), else n_steps.
+ * stop_d is [B, ld] (row stride ld >= n_steps, e.g. the stop_d of tt2_synthesize_dev with
+ * ld = max_iters).  Enqueued on `stream`. */
+tt2_status tt2_output_lengths_dev(const float* stop_d, int B, int n_steps, int ld,
+                                  int32_t* lengths_d, void* stream);
+
 /* Measurement hooks (not part of the reference surface; used by bench.py for the roofline).
  * tt2_last_timings: HIP-event times (ms) of the last tt2_synthesize_dev phases
  *   [encode, decode loop, postnet].
@@ -208,11 +215,22 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* ctx, const float* cond, int B, int T_f,
                            const float* teacher, float* wav_out, int32_t* mix_idx_out,
                            float* logits_out, float* upsampled_out);
 
-/* Same on DEVICE pointers, enqueued on `stream` (hipStream_t as void*). */
+/* Same on DEVICE pointers, enqueued on `stream` (hipStream_t as void*).  cond_d is
+ * CHANNELS-FIRST [B, cin, T_f] (the layout tt2_wn_cond_from_mels_dev writes; the reference
+ * transposes to it before upsampling, wavenet.py:427). */
 tt2_status tt2_wn_generate_dev(tt2_wn_ctx* ctx, const float* cond_d, int B, int T_f,
                                const float* u_mix_d, const float* u_log_d, uint64_t seed,
                                const float* teacher_d, float* wav_d, int32_t* mix_idx_d,
                                float* logits_d, void* stream);
+
+/* WaveNet conditioning from Tacotron mels, the device half of wavenet_vocoder/synthesizer.py:56-70
+ * (+ feeder.py _interp :426-428): row b of mels_d [B, ld_t, num_mels] keeps its first
+ * lengths_d[b] frames, clipped to [lo, hi] if clip (clip_for_wavenet), padded with lo to T_f
+ * frames (_pad_inputs with T2_output_range[0]), rescaled (x-lo)/(hi-lo) if normalize
+ * (normalize_for_wavenet), written channels-first to cond_d [B, num_mels, T_f]. */
+tt2_status tt2_wn_cond_from_mels_dev(const float* mels_d, int ld_t, const int32_t* lengths_d,
+                                     int B, int T_f, int num_mels, float lo, float hi, int clip,
+                                     int normalize, float* cond_d, void* stream);
 
 /* HIP-event times (ms) of the last generate call: [upsample, conditioning GEMM, generation]. */
 tt2_status tt2_wn_last_timings(tt2_wn_ctx* ctx, float* ms3);

@@ -404,3 +404,9 @@ def get_output_lengths(stop_tokens):
     for row in np.round(stop_tokens).tolist():
         out.append(row.index(1) if 1 in row else len(row))
     return out
+
+
+def get_output_lengths(stop_tokens):
+    """tacotron/synthesizer.py:384-387: per row, the index of the first 1 in np.round(stop)
+    (round half to even), else the row length."""
+    return [row.index(1) if 1 in row else len(row) for row in np.round(stop_tokens).tolist()]

@@ -28,6 +28,21 @@ def interp_condition(mel, max_abs_value=4.0):
     return ((m + np.float32(max_abs_value)) / np.float32(2 * max_abs_value)).astype(np.float32)
 
 
+def condition_batch(mels, max_abs_value=4.0, symmetric=True, clip=True, normalize=True):
+    """wavenet_vocoder/synthesizer.py:52-70 for a list of ragged mels [T_i, 80]: clip to
+    T2_output_range (clip_for_wavenet), _pad_inputs with T2_output_range[0] to maxlen (:117-118),
+    _interp to [0, 1] (normalize_for_wavenet, feeder.py:426-428).  Returns [B, maxlen, 80] f32."""
+    lo, hi = (-max_abs_value, max_abs_value) if symmetric else (0.0, max_abs_value)
+    maxlen = max(len(m) for m in mels)
+    if clip:
+        mels = [np.clip(m, lo, hi) for m in mels]
+    c = np.stack([np.pad(m, [(0, maxlen - len(m)), (0, 0)], mode='constant', constant_values=lo)
+                  for m in mels]).astype(np.float32)
+    if normalize:
+        c = ((c - np.float32(lo)) / np.float32(hi - lo)).astype(np.float32)
+    return c
+
+
 def upsample_2d(c, W, scales, freq_kernel=3):
     """ConvTranspose2D stack + ReLU (wavenet.py:171-203, 782-803; modules.py:736-770).
 

@@ -1076,6 +1076,24 @@ __global__ void k_transpose_bt(const float* __restrict__ src, long ld, float* __
 }
 
 // decoder_output clip (tacotron.py:362-363): dst[b][t][n] = clip(src[b][t][n])
+// get_output_lengths (tacotron/synthesizer.py:384-387): per row, the first step whose stop
+// probability rounds to 1 (np.round = round-half-even = rintf), else n_steps.  One wave per row,
+// 64 steps per ballot.
+__global__ __launch_bounds__(64) void k_output_lengths(const float* __restrict__ stop, int n_steps, long ld,
+                                                       int* __restrict__ lengths) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  int found = n_steps;
+  for (int t0 = 0; t0 < n_steps; t0 += 64) {
+    const int t = t0 + lane;
+    const unsigned long long m = __ballot(t < n_steps && rintf(stop[(long)b * ld + t]) == 1.0f);
+    if (m) {
+      found = t0 + __builtin_ctzll(m);
+      break;
+    }
+  }
+  if (lane == 0) lengths[b] = found;
+}
+
 __global__ void k_clip_frames(const float* __restrict__ src, long src_bstride, float* __restrict__ dst, int B,
                               int T, int nm, float lo, float hi, int do_clip) {
   const long n = (long)B * T * nm;
@@ -2309,6 +2327,16 @@ tt2_status tt2_debug_stamps(tt2_ctx* c, long long* out64) {
       TT2_HIP(hipMemcpy(c->stamps_host, g_stamps_dev, 64 * sizeof(long long), hipMemcpyDeviceToHost));
     }
     for (int i = 0; i < 64; ++i) out64[i] = c->stamps_host[i];
+  });
+}
+
+tt2_status tt2_output_lengths_dev(const float* stop_d, int B, int n_steps, int ld, int32_t* lengths_d, void* stream) {
+  return guard([&] {
+    TT2_CHECK(stop_d && lengths_d, TT2_ERR_INVALID_ARG, "tt2_output_lengths_dev: null argument");
+    TT2_CHECK(B >= 1 && n_steps >= 0 && ld >= n_steps, TT2_ERR_SHAPE_MISMATCH, "tt2_output_lengths_dev: bad sizes");
+    hipLaunchKernelGGL(k_output_lengths, dim3(B), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), stop_d, n_steps,
+                       (long)ld, lengths_d);
+    TT2_HIP(hipGetLastError());
   });
 }
 

@@ -52,6 +52,37 @@ __global__ void k_upsample(const float* __restrict__ in, float* __restrict__ out
   }
 }
 
+// WaveNet conditioning from Tacotron mels (wavenet_vocoder/synthesizer.py:56-70 +
+// feeder.py:426-428): row b of mels [B][ld_t][F] keeps its first len[b] frames, clipped to
+// [lo, hi] (clip_for_wavenet), padded with lo up to T_f, rescaled (x - lo)/(hi - lo) to [0, 1]
+// (normalize_for_wavenet) and written channels-first [B][F][T_f], the layout the upsampler
+// reads.  32x32 tiles transposed through LDS so both the [t][f] reads and the [f][t] writes
+// are coalesced.
+__global__ __launch_bounds__(256) void k_cond_from_mels(const float* __restrict__ mels, long ld_t,
+                                                        const int* __restrict__ len, int F, int T_f, float lo,
+                                                        float hi, int clip, int normalize, float* __restrict__ cond) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z, t0 = blockIdx.x * 32, f0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int L = min(len[b], T_f);
+  const float scale = normalize ? 1.f / (hi - lo) : 1.f;
+  const float off = normalize ? lo : 0.f;
+  for (int r = ty; r < 32; r += 8) {
+    const int t = t0 + r, f = f0 + tx;
+    float v = lo;
+    if (t < L && f < F) {
+      v = mels[((long)b * ld_t + t) * F + f];
+      if (clip) v = fminf(fmaxf(v, lo), hi);
+    }
+    tile[r][tx] = (v - off) * scale;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int f = f0 + r, t = t0 + tx;
+    if (f < F && t < T_f) cond[((long)b * F + f) * T_f + t] = tile[tx][r];
+  }
+}
+
 // Column order of the gated conv / cond outputs per quad q: {a_2q, a_2q+1, b_2q, b_2q+1}
 // so the lane that reduces quad q can apply tanh(a)·σ(b) without a cross-lane exchange.
 static inline int gate_col(int R, int q, int e) { return (e < 2 ? 2 * q + e : R + 2 * q + (e - 2)); }
@@ -890,6 +921,21 @@ tt2_status tt2_wn_generate_dev(tt2_wn_ctx* c, const float* cond_d, int B, int T_
     TT2_HIP(hipSetDevice(c->dev));
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     wn_generate_dev(c, cond_d, B, T_f, u_mix_d, u_log_d, seed, teacher_d, wav_d, mix_idx_d, logits_d, nullptr, s);
+  });
+}
+
+tt2_status tt2_wn_cond_from_mels_dev(const float* mels_d, int ld_t, const int32_t* lengths_d, int B, int T_f,
+                                     int num_mels, float lo, float hi, int clip, int normalize, float* cond_d,
+                                     void* stream) {
+  return guard([&] {
+    TT2_CHECK(mels_d && lengths_d && cond_d, TT2_ERR_INVALID_ARG, "tt2_wn_cond_from_mels_dev: null argument");
+    TT2_CHECK(B >= 1 && T_f >= 1 && num_mels >= 1 && ld_t >= 1, TT2_ERR_SHAPE_MISMATCH,
+              "tt2_wn_cond_from_mels_dev: bad sizes");
+    TT2_CHECK(hi > lo, TT2_ERR_INVALID_ARG, "tt2_wn_cond_from_mels_dev: empty output range");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_cond_from_mels, dim3(cdiv(T_f, 32), cdiv(num_mels, 32), B), dim3(256), 0, s, mels_d,
+                       (long)ld_t, lengths_d, num_mels, T_f, lo, hi, clip, normalize, cond_d);
+    TT2_HIP(hipGetLastError());
   });
 }
 

@@ -73,6 +73,7 @@ SIGNATURES = {
     "tt2_postnet": (_I, [_P, _P, _I, _I, _P, _P]),
     "tt2_synthesize_dev": (_I, [_P, _P, _P, _P, _I, _I, _P, _I, _P, _I, _I, _P, _U64, _P, _P, _P,
                                 _P]),
+    "tt2_output_lengths_dev": (_I, [_P, _I, _I, _I, _P, _P]),
     "tt2_last_timings": (_I, [_P, _P]),
     "tt2_profile_decoder_kernels": (_I, [_P, _I, _P]),
     "tt2_debug_stamps": (_I, [_P, _P]),
@@ -87,6 +88,7 @@ SIGNATURES = {
     "tt2_wn_finalize": (_I, [_P]),
     "tt2_wn_generate": (_I, [_P, _P, _I, _I, _P, _P, _U64, _P, _P, _P, _P, _P]),
     "tt2_wn_generate_dev": (_I, [_P, _P, _I, _I, _P, _P, _U64, _P, _P, _P, _P, _P]),
+    "tt2_wn_cond_from_mels_dev": (_I, [_P, _I, _P, _I, _I, _I, _F, _F, _I, _I, _P, _P]),
     "tt2_mol_sample": (_I, [_P, _P, _P, _I, _I, _F, _P, _P]),
 }
 

@@ -54,6 +54,33 @@ class WaveNet():
         self._weights = dict(weights)
         self._engine = None
 
+    def load_checkpoint(self, checkpoint):
+        """create_shadow_saver + load_averaged_model (wavenet_vocoder/train.py:67-86) without
+        TensorFlow: every model variable <v> is restored from the bundle's EMA shadow
+        ``<v>/ExponentialMovingAverage`` (falling back to <v> itself when the bundle holds no
+        shadow, e.g. a plain Saver checkpoint).  Returns the restored model names."""
+        from tt2 import ckpt
+        prefix = ckpt.latest_checkpoint(checkpoint) if os.path.isdir(checkpoint) else checkpoint
+        avail = dict(ckpt.list_variables(prefix))
+        if self._weights is None:
+            self.init_random_weights()
+        want = {}
+        for n in self._weights:
+            sh = n + "/ExponentialMovingAverage"
+            if sh in avail:
+                want[sh] = n
+            elif n in avail:
+                want[n] = n
+        values = ckpt.read_checkpoint(prefix, set(want))
+        for src, v in values.items():
+            n = want[src]
+            if self._weights[n].shape != v.shape:
+                raise ValueError("checkpoint variable {} has shape {}, model expects {}".format(
+                    src, v.shape, self._weights[n].shape))
+            self._weights[n] = v.astype(np.float32)
+        self._engine = None
+        return sorted(want.values())
+
     def init_random_weights(self, seed=None):
         hp = self._hparams
         self.load_weights(init_wavenet_weights(hp, hp.wavenet_random_seed if seed is None else seed))

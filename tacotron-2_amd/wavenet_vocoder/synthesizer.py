@@ -1,0 +1,83 @@
+"""Synthesizer of code/wavenet_vocoder/synthesizer.py:13-131 on the MI355X path.
+
+``load`` builds the eager ``WaveNet`` and restores weights: a TF tensor bundle holding the EMA
+shadow variables the reference restores (``create_shadow_saver`` / ``load_averaged_model``,
+wavenet_vocoder/train.py:67-86: ``<var>/ExponentialMovingAverage`` mapped onto ``<var>``), a
+``.npz`` of TF-named arrays, or ``None`` for the seeded random initialisation.  ``synthesize``
+keeps the reference's host-side batch preparation (audio lengths = mel frames x hop, clip to
+T2_output_range, pad with its lower end to the longest mel, ``_interp`` to [0, 1]) and writes
+``wavenet-audio-<basename>.wav`` per utterance (datasets/audio.py save_wavenet_wav).  Not
+reproduced (off the hot path): the debug-wav mode, the reconstructed-mel / upsampled-feature /
+waveform plots.
+"""
+import os
+
+import numpy as np
+
+from tt2.audio import save_wavenet_wav
+from tt2.hparams import get_hop_size
+from wavenet_vocoder.models import create_model
+
+
+def _interp(feats, in_range):
+    """wavenet_vocoder/feeder.py:426-428: rescale [-max, max] (or [0, max]) to [0, 1]."""
+    return (feats - in_range[0]) / (in_range[1] - in_range[0])
+
+
+def _pad_inputs(x, maxlen, _pad=0):
+    return np.pad(x, [(0, maxlen - len(x)), (0, 0)], mode='constant', constant_values=_pad)
+
+
+class Synthesizer:
+    def load(self, checkpoint_path, hparams, model_name='WaveNet'):
+        self._hparams = hparams
+        local_cond, global_cond = self._check_conditions()
+        if not local_cond or global_cond:
+            raise NotImplementedError('only local (mel) conditioning without global conditioning '
+                                      'is on the MI355X path')
+        self.model = create_model(model_name, hparams)
+        if checkpoint_path is None:
+            self.model.init_random_weights()
+        elif str(checkpoint_path).endswith('.npz'):
+            self.model.load_weights(checkpoint_path)
+        else:
+            self.model.init_random_weights()
+            self.model.load_checkpoint(checkpoint_path)
+
+    def synthesize(self, mel_spectrograms, speaker_ids, basenames, out_dir, log_dir, u_mix=None,
+                   u_log=None, seed=0):
+        """mel_spectrograms: list of [T_i, num_mels] arrays.  Returns the wav paths (or, with
+        ``out_dir=None``, the trimmed waveforms)."""
+        hp = self._hparams
+        if speaker_ids is not None and any(s != '<no_g>' for s in speaker_ids):
+            raise NotImplementedError('global conditioning (speaker ids) is not on the MI355X path')
+        mel_spectrograms = [np.asarray(m, np.float32) for m in mel_spectrograms]
+        audio_lengths = [len(x) * get_hop_size(hp) for x in mel_spectrograms]
+        maxlen = max([len(x) for x in mel_spectrograms])
+        T2_output_range = (-hp.max_abs_value, hp.max_abs_value) if hp.symmetric_mels \
+            else (0, hp.max_abs_value)
+        if hp.clip_for_wavenet:
+            mel_spectrograms = [np.clip(x, T2_output_range[0], T2_output_range[1])
+                                for x in mel_spectrograms]
+        c_batch = np.stack([_pad_inputs(x, maxlen, _pad=T2_output_range[0])
+                            for x in mel_spectrograms]).astype(np.float32)
+        if hp.normalize_for_wavenet:
+            c_batch = _interp(c_batch, T2_output_range).astype(np.float32)
+        self.model.initialize(None, c_batch, None, None, u_mix=u_mix, u_log=u_log, seed=seed)
+        generated_wavs = [w for tower in self.model.tower_y_hat for w in tower]
+        upsampled = [f for tower in self.model.tower_synth_upsampled_local_features for f in tower]
+        generated_wavs = [w[:n] for w, n in zip(generated_wavs, audio_lengths)]
+        self.upsampled_features = [f[:, :n] for f, n in zip(upsampled, audio_lengths)]
+        if out_dir is None:
+            return generated_wavs
+        os.makedirs(out_dir, exist_ok=True)
+        audio_filenames = []
+        for i, wav in enumerate(generated_wavs):
+            audio_filename = os.path.join(out_dir, 'wavenet-audio-{}.wav'.format(basenames[i]))
+            save_wavenet_wav(wav.copy(), audio_filename, sr=hp.sample_rate,
+                             inv_preemphasize=hp.preemphasize, k=hp.preemphasis)
+            audio_filenames.append(audio_filename)
+        return audio_filenames
+
+    def _check_conditions(self):
+        return self._hparams.cin_channels > 0, self._hparams.gin_channels > 0

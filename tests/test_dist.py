@@ -92,3 +92,52 @@ def test_shard_arrays_none_passthrough():
     x, y = shard([a, None], 1, 2)
     np.testing.assert_array_equal(x, a[3:])
     assert y is None
+
+
+class _StubTTS(object):
+    """CPU stand-in for tt2.e2e.TextToSpeech (the device path needs a GPU): utterance i gets a
+    waveform of length 3 * (sum of its ids) % 17 + 1 whose samples encode its ids."""
+
+    def synthesize(self, ids, lengths, ref_emt, ref_spk, seed=0):
+        wavs = []
+        for b in range(ids.shape[0]):
+            n = 3 * int(ids[b, :lengths[b]].sum()) % 17 + 1
+            wavs.append(np.arange(n, dtype=np.float32) + float(ids[b, 0]))
+        return dict(wavs=wavs)
+
+
+def _e2e_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "tacotron-2_amd"), root, os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from test_dist import _StubTTS
+    from tt2.e2e import synthesize_sharded
+    from tt2.synthetic import tacotron_inputs
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ids, lens, re, rs = tacotron_inputs(5, 9, 4, seed=21)
+        got = synthesize_sharded(_StubTTS(), ids, lens, re, rs)
+        np.savez(os.path.join(out_dir, "r{}.npz".format(rank)), *got)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_e2e_gathers_in_global_order(tmp_path, world):
+    """tt2.e2e.synthesize_sharded: every rank ends with the trimmed waveforms of ALL utterances in
+    global order (ragged lengths, uneven shards: 5 utterances over 2 or 3 ranks)."""
+    from tt2.synthetic import tacotron_inputs
+    mp.start_processes(_e2e_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    ids, lens, re, rs = tacotron_inputs(5, 9, 4, seed=21)
+    ref = _StubTTS().synthesize(ids, lens, re, rs)["wavs"]
+    for r in range(world):
+        with np.load(str(tmp_path / "r{}.npz".format(r)), allow_pickle=False) as z:
+            got = [z["arr_{}".format(i)] for i in range(len(z.files))]
+        assert len(got) == 5
+        for g, w in zip(got, ref):
+            np.testing.assert_array_equal(g, w)

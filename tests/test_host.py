@@ -256,3 +256,44 @@ def test_product_does_not_import_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dp, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f
+
+
+def test_oracle_output_lengths_and_condition_batch():
+    from oracle import tacotron_ref as TR
+    from oracle import wavenet_ref as WR
+    stop = np.array([[0.1, 0.5, 0.51, 0.9], [0.2, 0.2, 0.3, 0.4], [0.7, 0.1, 0.1, 0.1]], np.float32)
+    assert TR.get_output_lengths(stop) == [2, 4, 0]
+    m = [np.full((3, 80), 5.0, np.float32), np.full((1, 80), -1.0, np.float32)]
+    c = WR.condition_batch(m)
+    assert c.shape == (2, 3, 80)
+    np.testing.assert_array_equal(c[0], 1.0)                 # clipped to 4 -> 1
+    np.testing.assert_array_equal(c[1, 0], 3.0 / 8.0)        # (-1 + 4) / 8
+    np.testing.assert_array_equal(c[1, 1:], 0.0)             # padded with -4 -> 0
+
+
+def test_synthesizer_filenames_to_inputs_pads_per_tower(tmp_path):
+    """tacotron/synthesizer.py:296-371: ids padded with 0 per tower and concatenated on the time
+    axis, reference mels padded with -max_abs_value, split_infos [max_seq_len,0,0,0,0,T_e,T_s]."""
+    from tacotron.synthesizer import filenames_to_inputs, get_output_lengths
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=2, tacotron_synthesis_batch_size=2))
+    refs = [np.ones((5 + i, 80), np.float32) for i in range(4)]
+    out = filenames_to_inputs(hp, ["ab", "abcd", "a", "abc"], ["b0", "b1", "b2", "b3"], None,
+                              ["r"] * 4, refs, refs[::-1])
+    _, _, seqs, lens, split, re, rs, _, _ = out
+    np.testing.assert_array_equal(lens, [3, 5, 2, 4])
+    assert seqs.shape == (2, 5 + 4)
+    np.testing.assert_array_equal(split[:, 0], [5, 4])
+    np.testing.assert_array_equal(split[:, 5], [6, 8])
+    assert re.shape == (2, 6 + 8, 80) and rs.shape == (2, 8 + 6, 80)
+    assert re[0, 5, 0] == -4.0 and re[1, 6 + 7, 0] == 1.0
+    assert get_output_lengths(np.array([[0.2, 0.7], [0.1, 0.1]])) == [1, 2]
+
+
+def test_wavenet_synthesizer_host_prep_rejects_global_conditioning():
+    from wavenet_vocoder.synthesizer import Synthesizer, _interp
+    np.testing.assert_allclose(_interp(np.array([-4.0, 0.0, 4.0]), (-4, 4)), [0, 0.5, 1])
+    hp = bench_wavenet_hparams()
+    hp.gin_channels = 4
+    with pytest.raises(NotImplementedError):
+        Synthesizer().load(None, hp)
