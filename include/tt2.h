@@ -182,7 +182,7 @@ typedef struct tt2_wn_config {
   int skip_out_channels;   /* S */
   int kernel_size;         /* 3 */
   int cin_channels;        /* 80 */
-  int out_channels;        /* 30 = 3 * nr_mix (MoL head) */
+  int out_channels;        /* 30 = 3 * nr_mix (MoL head) or 2 (Gaussian head, gaussian.py:39-52) */
   int legacy;              /* skip-sum sqrt(1/2) scaling (wavenet.py:833-836) */
   int residual_legacy;     /* residual sqrt(1/2) scaling (modules.py:517-520) */
   float log_scale_min;     /* log(1e-14) */
@@ -191,6 +191,13 @@ typedef struct tt2_wn_config {
   int freq_axis_kernel_size; /* 3 */
   int max_batch;
   int64_t max_samples;     /* capacity in audio samples per utterance */
+  int upsample_type;       /* 0 '2D' (paper), 1 '1D', 2 'Resize', 3 'SubPixel' (fork default),
+                              4 'NearestNeighbor' (wavenet.py:163-203) */
+  int upsample_activation; /* 0 None, 1 'Relu', 2 'LeakyRelu' (wavenet.py:195-201) */
+  float leaky_alpha;       /* 0.4 */
+  int NN_init;             /* SubPixel: 0 = every output channel uses channel 0's kernel
+                              (SubPixelConvolution.build, modules.py:585-593) */
+  float log_scale_min_gauss; /* Gaussian head (out_channels == 2): log(1e-7) fork / paper value */
 } tt2_wn_config;
 
 typedef struct tt2_wn_ctx tt2_wn_ctx;
@@ -206,7 +213,8 @@ tt2_status tt2_wn_finalize(tt2_wn_ctx* ctx);
  *   cond     [B,T_f,cin] conditioning ALREADY clipped + _interp'd to [0,1]
  *            (wavenet_vocoder/synthesizer.py:63-70 is host-side, done by the shim).
  *   u_mix    [T,B,nr_mix], u_log [T,B]: injected uniforms of the MoL sampler (mixture.py:91,104)
- *            in [1e-5, 1-1e-5); NULL = counter-based device RNG keyed by seed.
+ *            in [1e-5, 1-1e-5); NULL = counter-based device RNG keyed by seed.  Gaussian head:
+ *            u_mix unused, u_log [T,B] = the N(0,1) draws of Normal.sample (gaussian.py:50).
  *   teacher  [B,T] or NULL: test_inputs override of the next input (wavenet.py:876-878).
  *   wav_out  [B,T]; mix_idx_out [B,T] (nullable); logits_out [B,T,out_channels] (nullable);
  *   upsampled_out [B,cin,T] (nullable, = tower_synth_upsampled_local_features). */

@@ -16,4 +16,6 @@ def wavenet_oracle_hp(hp):
                 legacy=hp.legacy, residual_legacy=hp.residual_legacy,
                 log_scale_min=hp.log_scale_min, upsample_scales=list(hp.upsample_scales),
                 freq_axis_kernel_size=hp.freq_axis_kernel_size, max_abs_value=hp.max_abs_value,
-                kernel_size=hp.kernel_size)
+                kernel_size=hp.kernel_size, upsample_type=hp.upsample_type,
+                upsample_activation=hp.upsample_activation, leaky_alpha=hp.leaky_alpha,
+                NN_init=hp.NN_init, log_scale_min_gauss=hp.log_scale_min_gauss)

@@ -43,7 +43,7 @@ def condition_batch(mels, max_abs_value=4.0, symmetric=True, clip=True, normaliz
     return c
 
 
-def upsample_2d(c, W, scales, freq_kernel=3):
+def upsample_2d(c, W, scales, freq_kernel=3, act="Relu", alpha=0.4):
     """ConvTranspose2D stack + ReLU (wavenet.py:171-203, 782-803; modules.py:736-770).
 
     c [B, F, T_f] (channels_first, expanded to [B,1,F,T]); per scale s a 1→1 channel
@@ -67,7 +67,97 @@ def upsample_2d(c, W, scales, freq_kernel=3):
             else:
                 src[:, -sh:] = x[:, :F + sh]
             out += src[..., None] * K[d][None, None, None, :]
-        x = np.maximum(out.reshape(B, F, T * s) + b, np.float32(0))
+        x = _act(out.reshape(B, F, T * s) + b, act, alpha)
+    return x
+
+
+def _act(x, act, alpha):
+    """upsample activation (modules.py:23-41): None / 'Relu' / 'LeakyRelu' = max(x, alpha·x)."""
+    if act == "Relu":
+        return np.maximum(x, np.float32(0))
+    if act == "LeakyRelu":
+        return np.maximum(x, np.float32(alpha) * x)
+    return x
+
+
+def _shift_freq(x, sh):
+    """src[:, f] = x[:, f + sh] (zero outside), x [B, F, T]."""
+    F = x.shape[1]
+    src = np.zeros_like(x)
+    if sh >= 0:
+        src[:, :F - sh] = x[:, sh:]
+    else:
+        src[:, -sh:] = x[:, :F + sh]
+    return src
+
+
+def _shift_time(x, sh):
+    """src[..., t] = x[..., t + sh] (zero outside)."""
+    T = x.shape[-1]
+    src = np.zeros_like(x)
+    if sh >= 0:
+        src[..., :T - sh] = x[..., sh:]
+    else:
+        src[..., -sh:] = x[..., :T + sh]
+    return src
+
+
+def upsample_network(c, W, hp):
+    """The conditioning upsampling network of wavenet.py:163-203 applied as at :782-803, for every
+    upsample_type.  c [B, F, T_f] channels-first; returns [B, F, T_f·hop].
+
+    '2D'       ConvTranspose2D 1→1, kernel (KF, s), stride (1, s), 'same' (modules.py:736-770)
+    '1D'       ConvTranspose1D F→F, kernel (1, s), stride (1, s), 'same' (modules.py:697-733):
+               out[o, i·s+j] = Σ_c in[c, i] · K[0, j, o, c] + b[o]  (kernel == stride: no overlap)
+    'Resize'   NN resize ×s on time, then Conv2D 1→1 kernel (KF, s) 'same' (modules.py:657-694)
+    'SubPixel' Conv2D 1→s kernel (KF, 3) 'same', then periodic shuffle out[f, w·s+k] = conv[f, w, k]
+               (modules.py:539-654); NN_init=False tiles output channel 0 (:585-593)
+    'NearestNeighbor'  tf.image.resize NEAREST ×hop (modules.py:524-536), no activation
+    TF 'same' for stride 1: pad_before = (k−1)//2.  Activation upsample_activation after every
+    learnable layer."""
+    ut = hp.get("upsample_type", "2D")
+    act, alpha = hp.get("upsample_activation", "Relu"), hp.get("leaky_alpha", 0.4)
+    KF = hp.get("freq_axis_kernel_size", 3)
+    scales = hp["upsample_scales"]
+    x = np.asarray(c, np.float32)
+    if ut == "2D":
+        up = upsample_2d(x, W, scales, KF, act=act, alpha=alpha)
+        return up
+    if ut == "NearestNeighbor":
+        return np.repeat(x, int(np.prod(scales)), axis=-1)
+    name = {"1D": "ConvTranspose1D", "Resize": "ResizeConvolution",
+            "SubPixel": "SubPixelConvolution"}[ut]
+    B, F, _ = x.shape
+    pf = (KF - 1) // 2
+    for i, s in enumerate(scales):
+        scope = "local_conditioning_upsampling_{}/{}_layer_{}/".format(i + 1, name, i)
+        K = _w(W, scope + "kernel")
+        b = _w(W, scope + "bias")
+        T = x.shape[-1]
+        if ut == "1D":
+            # [B, c, T] x K[0, j, o, c] -> [B, o, T, j]
+            out = np.einsum("bct,joc->botj", x, K[0]).astype(np.float32) + b[None, :, None, None]
+            x = out.reshape(B, F, T * s)
+        elif ut == "Resize":
+            nn = np.repeat(x, s, axis=-1)
+            pt = (s - 1) // 2
+            out = np.zeros_like(nn)
+            for d in range(KF):
+                src_f = _shift_freq(nn, d - pf)
+                for q in range(s):
+                    out += _shift_time(src_f, q - pt) * K[d, q, 0, 0]
+            x = out + b[0]
+        else:  # SubPixel
+            K = K[:, :, 0, :]                                   # [KF, 3, s]
+            if not hp.get("NN_init", True):
+                K = np.broadcast_to(K[:, :, :1], K.shape)
+            conv = np.zeros((B, F, T, s), np.float32)
+            for d in range(KF):
+                src_f = _shift_freq(x, d - pf)
+                for q in range(3):
+                    conv += _shift_time(src_f, q - 1)[..., None] * K[d, q][None, None, None, :]
+            x = (conv + b[None, None, None, :]).reshape(B, F, T * s)
+        x = _act(x.astype(np.float32), act, alpha)
     return x
 
 
@@ -94,7 +184,8 @@ def mol_sample(logits, u_mix, u_log, log_scale_min):
 
 
 def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False):
-    """WaveNet.incremental (wavenet.py:724-911) for scalar ('raw') input and the MoL head.
+    """WaveNet.incremental (wavenet.py:724-911) for scalar ('raw') input, MoL or Gaussian head
+    (out_channels == 2: u_log carries the N(0,1) draws, u_mix is unused).
 
     c_up: upsampled conditioning [B, T, cin]; u_mix [T, B, nr_mix]; u_log [T, B];
     test_inputs [B, T] overrides next_input (wavenet.py:876-878).  Returns y [B, T] (float32),
@@ -157,7 +248,12 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
         x = np.maximum(x, zero) @ f2k + f2b
         if lg is not None:
             lg[:, t] = x
-        y, k = mol_sample(x, u_mix[t], u_log[t], hp["log_scale_min"])
+        if x.shape[1] == 2:   # Gaussian head: sample_from_gaussian (gaussian.py:39-52), u_log = N(0,1)
+            ls = np.maximum(x[:, 1], np.float32(hp["log_scale_min_gauss"]))
+            y = np.clip(x[:, 0] + np.exp(ls) * np.asarray(u_log[t], np.float32), -1, 1).astype(np.float32)
+            k = np.zeros((B,), np.int32)
+        else:
+            y, k = mol_sample(x, u_mix[t], u_log[t], hp["log_scale_min"])
         ys[:, t] = y
         ks[:, t] = k
         cur = y[:, None] if test_inputs is None else np.asarray(test_inputs, np.float32)[:, t:t + 1]
@@ -168,6 +264,5 @@ def synthesize(mel, W, hp, u_mix, u_log, test_inputs=None, return_logits=False):
     """wavenet_vocoder/synthesizer.py:46-103 for one batch of equal-length mels [B, T_f, 80]:
     clip + interp, upsample, incremental generation of T_f·hop samples."""
     c = interp_condition(mel, hp.get("max_abs_value", 4.0))       # [B, T_f, 80]
-    c_up = upsample_2d(c.transpose(0, 2, 1), W, hp["upsample_scales"],
-                       hp.get("freq_axis_kernel_size", 3))        # [B, 80, T]
+    c_up = upsample_network(c.transpose(0, 2, 1), W, hp)         # [B, 80, T]
     return incremental(c_up.transpose(0, 2, 1), W, hp, u_mix, u_log, test_inputs, return_logits)

@@ -5,7 +5,7 @@
 // ConvTranspose2D :736-770), mixture.py (sample_from_discretized_mix_logistic :76-107).
 //
 // Pipeline per call:
-//   1. k_upsample × n_upsample   ConvTranspose2D(kernel (3,s), stride (1,s), 'same') + ReLU
+//   1. k_upsample × n_upsample   upsampling network (2D / 1D / Resize / SubPixel / NN) + activation
 //   2. gemm                      cond[t][l][·] = c_t·Wc_l + bc_l for ALL t and layers at once
 //                                (the conditioning 1×1 never depends on generated samples)
 //   3. k_generate                one persistent workgroup per utterance walks t = 0..T-1:
@@ -27,26 +27,73 @@ namespace tt2 {
 
 static const char* WP = "WaveNet_model/inference/";
 
-// ConvTranspose2D 1→1 channel, kernel (KF, s), stride (1, s), 'same' (modules.py:736-770):
-//   out[b][f][i*s+j] = relu(Σ_d in[b][f+pad-d][i] · K[d][j] + bias),  pad = (KF-1)/2
+// Upsampling network, one launch per layer (wavenet.py:163-203 builds it, :782-803 applies it), on
+// channels-first [B][F][T] conditioning (F = cin "frequency" rows).  mode (tt2_wn_config
+// upsample_type) and the reference layer each restates:
+//   WN_UP_2D        ConvTranspose2D 1->1, kernel (KF, s), stride (1, s), 'same' (modules.py:736-770):
+//                   out[f][i*s+j] = Σ_d in[f+pad-d][i] · K[d][j] + b           K [KF][s][1][1]
+//   WN_UP_1D        ConvTranspose1D F->F, kernel (1, s), stride (1, s), 'same' (modules.py:697-733):
+//                   out[o][i*s+j] = Σ_c in[c][i] · K[0][j][o][c] + b[o]         K [1][s][F][F]
+//   WN_UP_RESIZE    nearest-neighbour x s along time, then Conv2D 1->1 kernel (KF, s) 'same'
+//                   (modules.py:657-694): out[f][u] = Σ_{d,e} nn[f+d-pf][u+e-pt] · K[d][e] + b
+//   WN_UP_SUBPIXEL  Conv2D 1->s kernel (KF, 3) 'same' + periodic shuffle along time
+//                   (modules.py:539-654): out[f][w*s+k] = Σ_{d,e} in[f+d-pf][w+e-1] · K[d][e][0][k] + b[k]
+//   WN_UP_NN        tf.image.resize NEAREST x hop (modules.py:524-536): out[f][u] = in[f][u/s], no act
+// pf = (KF-1)/2, pt = (s-1)/2 (TF 'same': the odd pad goes after).  Activation (upsample_activation):
+// none / ReLU / LeakyReLU max(x, alpha·x) (modules.py:23-41).  out_t (nullable) receives the last
+// layer transposed to [B][T][F] for the conditioning GEMM.
+enum { WN_UP_2D = 0, WN_UP_1D = 1, WN_UP_RESIZE = 2, WN_UP_SUBPIXEL = 3, WN_UP_NN = 4 };
+enum { WN_ACT_NONE = 0, WN_ACT_RELU = 1, WN_ACT_LEAKY = 2 };
+
 __global__ void k_upsample(const float* __restrict__ in, float* __restrict__ out, float* __restrict__ out_t,
                            const float* __restrict__ K, const float* __restrict__ bias, int B, int F, int Tin,
-                           int s, int KF) {
+                           int s, int KF, int mode, int act, float alpha) {
   const long Tout = (long)Tin * s;
   const long n = (long)B * F * Tout;
-  const int pad = (KF - 1) / 2;
+  const int pf = (KF - 1) / 2;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
     const int b = e / ((long)F * Tout);
     const long r = e - (long)b * F * Tout;
     const int f = r / Tout;
     const long to = r - (long)f * Tout;
     const int i = to / s, j = to - (long)i * s;
+    const float* x = in + (long)b * F * Tin;
     float acc = 0.f;
-    for (int d = 0; d < KF; ++d) {
-      const int ff = f + pad - d;
-      if (ff >= 0 && ff < F) acc += in[((long)b * F + ff) * Tin + i] * K[d * s + j];
+    if (mode == WN_UP_2D) {
+      for (int d = 0; d < KF; ++d) {
+        const int ff = f + pf - d;
+        if (ff >= 0 && ff < F) acc += x[(long)ff * Tin + i] * K[d * s + j];
+      }
+      acc += bias[0];
+    } else if (mode == WN_UP_1D) {
+      const float* kr = K + ((long)j * F + f) * F;
+      for (int c = 0; c < F; ++c) acc += x[(long)c * Tin + i] * kr[c];
+      acc += bias[f];
+    } else if (mode == WN_UP_RESIZE) {
+      const int pt = (s - 1) / 2;
+      for (int d = 0; d < KF; ++d) {
+        const int ff = f + d - pf;
+        if (ff < 0 || ff >= F) continue;
+        for (int q = 0; q < s; ++q) {
+          const long u = to + q - pt;
+          if (u >= 0 && u < Tout) acc += x[(long)ff * Tin + u / s] * K[d * s + q];
+        }
+      }
+      acc += bias[0];
+    } else if (mode == WN_UP_SUBPIXEL) {
+      for (int d = 0; d < KF; ++d) {
+        const int ff = f + d - pf;
+        if (ff < 0 || ff >= F) continue;
+        for (int q = 0; q < 3; ++q) {
+          const int w = i + q - 1;
+          if (w >= 0 && w < Tin) acc += x[(long)ff * Tin + w] * K[(d * 3 + q) * s + j];
+        }
+      }
+      acc += bias[j];
+    } else {  // WN_UP_NN
+      acc = x[(long)f * Tin + i];
     }
-    const float y = fmaxf(acc + bias[0], 0.f);
+    const float y = act == WN_ACT_RELU ? fmaxf(acc, 0.f) : (act == WN_ACT_LEAKY ? fmaxf(acc, alpha * acc) : acc);
     out[e] = y;
     if (out_t) out_t[((long)b * Tout + to) * F + f] = y;
   }
@@ -127,8 +174,9 @@ struct GenArgs {
   const float* f2_w; const float* f2_b;  // [S][C], [C]
   int C;
   int legacy, res_legacy;
-  float log_scale_min;
-  const float* u_mix; const float* u_log;  // [T][Bg][nr], [T][Bg] or null
+  float log_scale_min, log_scale_min_gauss;
+  int gauss;                               // out_channels == 2: Gaussian head
+  const float* u_mix; const float* u_log;  // [T][Bg][nr], [T][Bg] or null (Gaussian: u_log = N(0,1) draws)
   uint64_t seed;
   const float* teacher;  // [Bg][T] or null
   float* wav; int* kout; float* logits;    // [Bg][T], [Bg][T], [Bg][T][C]
@@ -298,7 +346,19 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
     f32x4 cn = {0.f, 0.f, 0.f, 0.f};
     const bool has_next = t + 1 < a.T;
     if (has_next && tid < nl * G / 4) cn = cond4[((long)b * a.T + t + 1) * crow + l0 * G / 4 + tid];
-    if (last && wave == 1) {  // this sample's Gumbel terms and logistic noise
+    if (last && wave == 1 && a.gauss) {  // this sample's N(0,1) draw (injected in u_log, or Box-Muller)
+      if (lane == 15) {
+        float nz;
+        if (a.u_log) {
+          nz = a.u_log[(long)t * a.Bg + b];
+        } else {
+          const uint64_t k0 = ((uint64_t)t * a.Bg + b) * 16;
+          const double u1 = u01_open(mix64(a.seed ^ mix64(k0 + 14))), u2 = u01_open(mix64(a.seed ^ mix64(k0 + 15)));
+          nz = (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+        }
+        gum[cb_cur * 16 + 15] = nz;
+      }
+    } else if (last && wave == 1) {  // this sample's Gumbel terms and logistic noise
       if (lane < nr) {
         const float um = a.u_mix ? a.u_mix[((long)t * a.Bg + b) * nr + lane]
                                  : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.Bg + b) * 16 + lane)));
@@ -517,11 +577,13 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
     {
       float temp = -INFINITY;
       int idx = lane;
-      if (lane < nr) temp = lg[lane] - gum[cb_cur * 16 + lane];
+      if (!a.gauss && lane < nr) temp = lg[lane] - gum[cb_cur * 16 + lane];
       argmax16(temp, idx);  // nr <= 10: the mixture logits sit in lanes 0..15
       if (lane == 0) {
-        const float mean = lg[nr + idx];
-        const float ls = fmaxf(lg[2 * nr + idx], a.log_scale_min);
+        // MoL: mixture idx (mixture.py:92-105); Gaussian: out = [mean, log_scale] (gaussian.py:39-52)
+        if (a.gauss) idx = 0;
+        const float mean = a.gauss ? lg[0] : lg[nr + idx];
+        const float ls = a.gauss ? fmaxf(lg[1], a.log_scale_min_gauss) : fmaxf(lg[2 * nr + idx], a.log_scale_min);
         float x = mean + expf(ls) * gum[cb_cur * 16 + 15];
         x = fminf(fmaxf(x, -1.f), 1.f);
         const float xn = a.teacher ? a.teacher[(long)b * a.T + t] : x;  // wavenet.py:876-878
@@ -646,12 +708,27 @@ static void wn_finalize(tt2_wn_ctx* c) {
   wupload(c->f1_b, need(wm, P + "skip_convolutions/final_convolution_1/bias", {S}).data);
   wupload(c->f2_w, need(wm, P + "skip_convolutions/final_convolution_2/kernel", {1, S, C}).data);
   wupload(c->f2_b, need(wm, P + "skip_convolutions/final_convolution_2/bias", {C}).data);
-  for (int i = 0; i < c->cfg.n_upsample; ++i) {
-    const std::string sc = P + "local_conditioning_upsampling_" + std::to_string(i + 1) + "/ConvTranspose2D_layer_" +
+  static const char* kUpName[4] = {"ConvTranspose2D_layer_", "ConvTranspose1D_layer_", "ResizeConvolution_layer_",
+                                   "SubPixelConvolution_layer_"};
+  const int ut = c->cfg.upsample_type;
+  for (int i = 0; ut != WN_UP_NN && i < c->cfg.n_upsample; ++i) {
+    const std::string sc = P + "local_conditioning_upsampling_" + std::to_string(i + 1) + "/" + kUpName[ut] +
                            std::to_string(i) + "/";
     const int s = c->cfg.upsample_scales[i], kf = c->cfg.freq_axis_kernel_size;
-    wupload(c->up_k[i], need(wm, sc + "kernel", {kf, s, 1, 1}).data);
-    wupload(c->up_b[i], need(wm, sc + "bias", {1}).data);
+    if (ut == WN_UP_1D) {
+      wupload(c->up_k[i], need(wm, sc + "kernel", {1, s, cin, cin}).data);
+      wupload(c->up_b[i], need(wm, sc + "bias", {cin}).data);
+    } else if (ut == WN_UP_SUBPIXEL) {
+      std::vector<float> k = need(wm, sc + "kernel", {kf, 3, 1, s}).data;
+      if (!c->cfg.NN_init)  // SubPixelConvolution.build (modules.py:585-593): every channel = channel 0
+        for (int q = 0; q < kf * 3; ++q)
+          for (int o = 1; o < s; ++o) k[(size_t)q * s + o] = k[(size_t)q * s];
+      wupload(c->up_k[i], k);
+      wupload(c->up_b[i], need(wm, sc + "bias", {s}).data);
+    } else {
+      wupload(c->up_k[i], need(wm, sc + "kernel", {kf, s, 1, 1}).data);
+      wupload(c->up_b[i], need(wm, sc + "bias", {1}).data);
+    }
   }
   c->finalized = true;
 }
@@ -698,15 +775,18 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   const float* src = cond_in;  // [B][F][T_f] channels-first
   long Tcur = T_f;
   float* bufs[2] = {c->up_a.as<float>(), c->up_b_buf.as<float>()};
-  for (int i = 0; i < c->cfg.n_upsample; ++i) {
-    const int sc = c->cfg.upsample_scales[i];
-    const bool last = i + 1 == c->cfg.n_upsample;
+  const int ut = c->cfg.upsample_type;
+  const int nup = ut == WN_UP_NN ? 1 : c->cfg.n_upsample;  // NearestNeighborUpsample: one x hop layer
+  const int act = ut == WN_UP_NN ? WN_ACT_NONE : c->cfg.upsample_activation;
+  for (int i = 0; i < nup; ++i) {
+    const int sc = ut == WN_UP_NN ? (int)c->hop : c->cfg.upsample_scales[i];
+    const bool last = i + 1 == nup;
     float* dst = (last && upsampled_d) ? upsampled_d : bufs[i & 1];
     const long n = (long)B * F * Tcur * sc;
     const int grid = (int)std::min<long>((n + 255) / 256, 65536);
     hipLaunchKernelGGL(k_upsample, dim3(grid), dim3(256), 0, s, src, dst, last ? c->c_up_t.as<float>() : nullptr,
-                       c->up_k[i].as<float>(), c->up_b[i].as<float>(), B, F, (int)Tcur, sc,
-                       c->cfg.freq_axis_kernel_size);
+                       ut == WN_UP_NN ? nullptr : c->up_k[i].as<float>(), ut == WN_UP_NN ? nullptr : c->up_b[i].as<float>(),
+                       B, F, (int)Tcur, sc, c->cfg.freq_axis_kernel_size, ut, act, c->cfg.leaky_alpha);
     TT2_HIP(hipGetLastError());
     src = dst;
     Tcur *= sc;
@@ -731,6 +811,8 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   a.so_w = c->so_w.as<f32x4>(); a.so_b = c->so_b.as<float>();
   a.f1_w = c->f1_w.as<float>(); a.f1_b = c->f1_b.as<float>(); a.f2_w = c->f2_w.as<float>(); a.f2_b = c->f2_b.as<float>();
   a.C = c->C; a.legacy = c->cfg.legacy; a.res_legacy = c->cfg.residual_legacy; a.log_scale_min = c->cfg.log_scale_min;
+  a.log_scale_min_gauss = c->cfg.log_scale_min_gauss;
+  a.gauss = c->C == 2;
   a.u_mix = umix_d; a.u_log = ulog_d; a.seed = seed; a.teacher = teacher_d;
   a.wav = wav_d; a.kout = k_d; a.logits = logits_d;
   a.status = c->gran.as<int>();
@@ -767,6 +849,8 @@ void tt2_wn_default_config(tt2_wn_config* c, int max_batch, int64_t max_samples)
   c->log_scale_min = (float)std::log(1e-14); c->n_upsample = 3;
   c->upsample_scales[0] = 5; c->upsample_scales[1] = 5; c->upsample_scales[2] = 11;
   c->freq_axis_kernel_size = 3; c->max_batch = max_batch; c->max_samples = max_samples;
+  c->upsample_type = 0; c->upsample_activation = 1; c->leaky_alpha = 0.4f; c->NN_init = 1;
+  c->log_scale_min_gauss = (float)std::log(1e-7);
 }
 
 tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** out) {
@@ -780,8 +864,12 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
               TT2_ERR_INVALID_ARG,
               "this build's generation kernel is specialised for R=64, G=128, S=64 (BASELINE config 3)");
     TT2_CHECK(cfg->kernel_size == 3, TT2_ERR_INVALID_ARG, "kernel_size must be 3");
-    TT2_CHECK(cfg->out_channels % 3 == 0 && cfg->out_channels <= 30 && cfg->out_channels >= 3, TT2_ERR_INVALID_ARG,
-              "MoL head needs out_channels = 3*nr_mix <= 30");
+    TT2_CHECK(cfg->out_channels == 2 || (cfg->out_channels % 3 == 0 && cfg->out_channels <= 30 && cfg->out_channels >= 3),
+              TT2_ERR_INVALID_ARG, "head needs out_channels = 2 (Gaussian) or 3*nr_mix <= 30 (MoL)");
+    TT2_CHECK(cfg->upsample_type >= WN_UP_2D && cfg->upsample_type <= WN_UP_NN, TT2_ERR_INVALID_ARG,
+              "upsample_type out of range");
+    TT2_CHECK(cfg->upsample_activation >= WN_ACT_NONE && cfg->upsample_activation <= WN_ACT_LEAKY,
+              TT2_ERR_INVALID_ARG, "upsample_activation out of range");
     TT2_CHECK(cfg->layers >= 1 && cfg->stacks >= 1 && cfg->layers % cfg->stacks == 0, TT2_ERR_INVALID_ARG,
               "layers % stacks != 0");
     TT2_CHECK(cfg->cin_channels >= 1 && cfg->cin_channels <= 128, TT2_ERR_INVALID_ARG, "cin_channels out of range");
@@ -880,7 +968,7 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* c, const float* cond, int B, int T_f, con
     c->cin_d.alloc(cf.size() * sizeof(float));
     TT2_HIP(hipMemcpyAsync(c->cin_d.p, cf.data(), cf.size() * sizeof(float), hipMemcpyHostToDevice, s));
     const float *um = nullptr, *ul = nullptr, *tg = nullptr;
-    if (u_mix) {
+    if (u_mix && nr > 0) {
       c->umix.alloc(sizeof(float) * T * B * nr);
       TT2_HIP(hipMemcpyAsync(c->umix.p, u_mix, sizeof(float) * T * B * nr, hipMemcpyHostToDevice, s));
       um = c->umix.as<float>();

@@ -51,7 +51,10 @@ class WnConfig(ctypes.Structure):
         "kernel_size", "cin_channels", "out_channels", "legacy", "residual_legacy")] + [
         ("log_scale_min", ctypes.c_float), ("n_upsample", ctypes.c_int),
         ("upsample_scales", ctypes.c_int * 8), ("freq_axis_kernel_size", ctypes.c_int),
-        ("max_batch", ctypes.c_int), ("max_samples", ctypes.c_int64)]
+        ("max_batch", ctypes.c_int), ("max_samples", ctypes.c_int64),
+        ("upsample_type", ctypes.c_int), ("upsample_activation", ctypes.c_int),
+        ("leaky_alpha", ctypes.c_float), ("NN_init", ctypes.c_int),
+        ("log_scale_min_gauss", ctypes.c_float)]
 
 
 _P = ctypes.c_void_p

@@ -158,6 +158,10 @@ class TacotronEngine(object):
                     stop_token_prediction=stop, alignments=align, frames=frames)
 
 
+#: tt2_wn_config.upsample_type codes (wavenet.py:163-203)
+UPSAMPLE_TYPES = ("2D", "1D", "Resize", "SubPixel", "NearestNeighbor")
+
+
 def wavenet_config(hp, max_batch, max_samples):
     lib = _lib.load_library()
     cfg = _lib.WnConfig()
@@ -173,9 +177,16 @@ def wavenet_config(hp, max_batch, max_samples):
     cfg.legacy = 1 if hp.legacy else 0
     cfg.residual_legacy = 1 if hp.residual_legacy else 0
     cfg.log_scale_min = hp.log_scale_min
-    if hp.upsample_type != "2D":
-        raise NotImplementedError("upsample_type {!r} is not built (only '2D', paper_hparams)"
-                                  .format(hp.upsample_type))
+    if hp.upsample_type not in UPSAMPLE_TYPES:
+        raise ValueError("upsample_type {!r} not in {}".format(hp.upsample_type, UPSAMPLE_TYPES))
+    cfg.upsample_type = UPSAMPLE_TYPES.index(hp.upsample_type)
+    acts = (None, "Relu", "LeakyRelu")
+    if hp.upsample_activation not in acts:
+        raise ValueError("upsample_activation {!r} not in {}".format(hp.upsample_activation, acts))
+    cfg.upsample_activation = acts.index(hp.upsample_activation)
+    cfg.leaky_alpha = hp.leaky_alpha
+    cfg.NN_init = 1 if hp.NN_init else 0
+    cfg.log_scale_min_gauss = hp.log_scale_min_gauss
     cfg.n_upsample = len(hp.upsample_scales)
     for i, s in enumerate(hp.upsample_scales):
         cfg.upsample_scales[i] = s
@@ -223,6 +234,8 @@ class WaveNetEngine(object):
         T = T_f * self.hop
         nr = self.hp.out_channels // 3
         um, ul, tg = f32(u_mix), f32(u_log), f32(teacher)
+        if self.hp.out_channels == 2:
+            um = None  # Gaussian head: only the N(0,1) draws in u_log
         if um is not None and um.shape != (T, B, nr):
             raise ValueError("u_mix must be [T, B, nr_mix] = {}".format((T, B, nr)))
         if ul is not None and ul.shape != (T, B):

@@ -137,14 +137,24 @@ def wavenet_weight_specs(hp):
     S.append((WP + "skip_convolutions/final_convolution_1/bias", (Sk,), "bias"))
     S.append((WP + "skip_convolutions/final_convolution_2/kernel", (1, Sk, hp.out_channels), "glorot"))
     S.append((WP + "skip_convolutions/final_convolution_2/bias", (hp.out_channels,), "bias"))
-    if hp.upsample_type != "2D":
-        raise NotImplementedError("upsample_type {!r}: only '2D' (paper_hparams) is on the MI355X "
-                                  "path (SURVEY.md §8f lists the others as next)".format(hp.upsample_type))
+    ut = hp.upsample_type
+    if ut == "NearestNeighbor":  # NearestNeighborUpsample: no variables (modules.py:524-536)
+        return S
+    name = {"2D": "ConvTranspose2D", "1D": "ConvTranspose1D", "Resize": "ResizeConvolution",
+            "SubPixel": "SubPixelConvolution"}[ut]
+    kf, nl = hp.freq_axis_kernel_size, len(hp.upsample_scales)
     for i, s in enumerate(hp.upsample_scales):
-        sc = WP + "local_conditioning_upsampling_{}/ConvTranspose2D_layer_{}/".format(i + 1, i)
-        S.append((sc + "kernel", (hp.freq_axis_kernel_size, s, 1, 1), "nn_upsample:{}".format(
-            len(hp.upsample_scales))))
-        S.append((sc + "bias", (1,), "bias"))
+        sc = WP + "local_conditioning_upsampling_{}/{}_layer_{}/".format(i + 1, name, i)
+        if ut == "1D":     # Conv2DTranspose kernel [1, s, out=cin, in=cin], bias [cin]
+            S.append((sc + "kernel", (1, s, hp.cin_channels, hp.cin_channels),
+                      "nn_up1d:{}".format(nl)))
+            S.append((sc + "bias", (hp.cin_channels,), "bias"))
+        elif ut == "SubPixel":  # Conv2D (kf, 3), 1 -> s filters
+            S.append((sc + "kernel", (kf, 3, 1, s), "nn_subpixel:{}".format(nl)))
+            S.append((sc + "bias", (s,), "bias"))
+        else:              # 2D / Resize: (kf, s) 1 -> 1
+            S.append((sc + "kernel", (kf, s, 1, 1), "nn_{}:{}".format(ut.lower(), nl)))
+            S.append((sc + "bias", (1,), "bias"))
     return S
 
 
@@ -179,16 +189,27 @@ def _init(rng, shape, kind, hp):
         return np.clip(v, -1.0, 1.0).astype(np.float32)
     if kind == "mha_g":  # sqrt(1/num_units), multihead_attention.py:103-105
         return np.float32(np.sqrt(1.0 / (hp.style_att_dim // hp.num_heads)))
-    if kind.startswith("nn_upsample"):
-        # ConvTranspose2D._init_kernel (modules.py:761-770) + a small perturbation so every tap
-        # is exercised by the parity tests.
-        up_layers = int(kind.split(":")[1])
+    if kind.startswith("nn_"):
+        # the reference's NN_init kernels (modules.py:645-654, 686-694, 723-733, 761-770) scaled by
+        # NN_scaler^(1/up_layers), plus a small perturbation so every tap is exercised by the
+        # parity tests
+        kind, up_layers = kind.split(":")
+        scale = hp.NN_scaler ** (1.0 / int(up_layers))
+        if kind == "nn_up1d":
+            _, kw, co, ci = shape
+            k = np.tile(np.eye(co, ci)[None, None], (1, kw, 1, 1))
+            return (k * scale + rng.uniform(-0.05, 0.05, shape)).astype(np.float32)
         kh, kw = shape[0], shape[1]
         k = np.zeros((kh, kw), np.float64)
-        ov = kw // kw
-        k[kh // 2, :] = 1.0 / max(ov, 1) if kw % 2 == 0 else 1.0
-        k = k * (hp.NN_scaler ** (1.0 / up_layers)) + rng.uniform(-0.05, 0.05, (kh, kw))
-        return k.reshape(shape).astype(np.float32)
+        if kind == "nn_2d":
+            k[kh // 2, :] = 1.0
+        else:  # resize / subpixel: centre tap(s)
+            js = [kw // 2 - 1, kw // 2] if kw % 2 == 0 else [kw // 2]
+            for j in js:
+                k[kh // 2, j] = 0.5 if kw % 2 == 0 else 1.0
+        k = k.reshape(kh, kw, 1, 1) * scale
+        k = np.broadcast_to(k, shape) + rng.uniform(-0.05, 0.05, shape)
+        return k.astype(np.float32)
     raise ValueError(kind)
 
 

@@ -89,9 +89,6 @@ class WaveNet():
         hp = self._hparams
         if not is_scalar_input(hp.input_type) or is_mulaw(hp.input_type):
             raise NotImplementedError("only input_type='raw' is on the MI355X path")
-        if hp.out_channels == 2:
-            raise NotImplementedError("Gaussian output head (out_channels=2) is not built; the MoL "
-                                      "head (paper_hparams out_channels=30) is (SURVEY.md §8f)")
         if self.global_conditioning_enabled():
             raise NotImplementedError("global conditioning (gin_channels > 0) is not built")
         if not self.local_conditioning_enabled():
