@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-frames", type=int, default=1000,
                    help="decoder frames per utterance of the end-to-end leg (configs[3])")
+    p.add_argument("--no-griffin-lim", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=100)
     p.add_argument("--profile-iters", type=int, default=50)
@@ -129,6 +130,45 @@ def load_traffic(kernel):
         return d["kernels"][kernel]["hbm_bytes_per_launch"]
     except Exception:
         return None
+
+def bench_griffin_lim(local, frames=1000):
+    """tt2_gl_synthesize_dev on a synthetic normalised mel [1000, 80] (paper_hparams audio: n_fft
+    2048, win 1100, hop 275; 60 iterations), HIP-event timed; audio-samples/s of the output."""
+    import torch
+    from tt2.audio import GriffinLim
+    from tt2.hparams import paper_hparams
+    hp = paper_hparams.copy()
+    gl = GriffinLim(hp, local)
+    rng = np.random.default_rng(7)
+    mel = np.clip(rng.uniform(-4, 2, (1, 80)) + np.cumsum(rng.normal(0, 0.3, (frames, 80)), 0),
+                  -4, 4).astype(np.float32)
+    dev = torch.device("cuda", local)
+    mel_d = torch.from_numpy(mel).to(dev)
+    L = (frames - 1) * hp.hop_size + hp.win_size
+    wav_d = torch.empty((L,), dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    def run():
+        _lib.check(gl.lib.tt2_gl_synthesize_dev(gl.h, mel_d.data_ptr(), frames, 1, -1, wav_d.data_ptr(),
+                                                ctypes.c_void_p(st.cuda_stream)))
+
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(3):
+        run()
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / 3
+    gl.close()
+    n = hp.n_fft
+    # algorithmic bytes per iteration: spec read + angle write/read + frame buffer write/read
+    it_bytes = frames * (4 * (n // 2 + 1) * 3 + 4 * 2 * hp.win_size * 2)
+    return dict(metric="audio-samples/sec (Griffin-Lim, 60 iterations)", value=round(L / (ms * 1e-3), 1),
+                unit="audio-samples/s", ms_per_utterance=round(ms, 3), frames=frames, samples=L,
+                iters=hp.griffin_lim_iters, n_fft=n, win=hp.win_size, hop=hp.hop_size,
+                algorithmic_gb_per_s=round(it_bytes * hp.griffin_lim_iters / (ms * 1e-3) / 1e9, 1))
+
 
 E2E_TEXT = ("Scientists at the CERN laboratory say they have discovered a new particle. "
             "The buses aren't the problem, they actually provide a solution. Does the quick "
@@ -376,6 +416,11 @@ def main():
     if not a.no_e2e:
         e2e = bench_e2e(a, rank, world, local, barrier, max_over_ranks)
 
+    # --- Griffin-Lim vocoder (GL_on_GPU path, 60 iterations) on a 1000-frame mel ---
+    glr = None
+    if not a.no_griffin_lim:
+        glr = bench_griffin_lim(local)
+
     # --- CPU baseline (rank 0, N = 1 only) ---
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -406,6 +451,7 @@ def main():
                                decoded_steps=n_steps.value, ref_frames=a.ref_frames,
                                parallelism="utterance-batch sharding x{}".format(world)),
                    phases=phases, roofline=roofline, cpu_baseline=cpu, wavenet=wn, e2e=e2e,
+                   griffin_lim=glr,
                    diag_stamps=stamps)
         print(json.dumps(out))
     eng.close()

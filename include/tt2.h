@@ -253,6 +253,45 @@ tt2_status tt2_wn_debug_stamps(tt2_wn_ctx* ctx, long long* out512);
 tt2_status tt2_mol_sample(const float* logits, const float* u_mix, const float* u_log, int n,
                           int nr_mix, float log_scale_min, float* x, int32_t* k);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Griffin-Lim vocoder, TF GPU variant (GL_on_GPU = True, hparams.py:135): replaces             */
+/* datasets/audio.py inv_mel_spectrogram_tensorflow / inv_linear_spectrogram_tensorflow         */
+/* (:131-143) + _griffin_lim_tensorflow (:163-176), called by tacotron/synthesizer.py:152-160    */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct tt2_gl_config {
+  int n_fft;               /* 2048 (fft_length; power of two <= 4096) */
+  int hop_size;            /* 275 paper / 200 fork (frame_step) */
+  int win_size;            /* 1100 paper / 800 fork (frame_length, periodic Hann window) */
+  int num_mels;            /* 80 */
+  float magnitude_power;   /* 2 */
+  float power;             /* 1.5 (S^power before G&L) */
+  float ref_level_db;      /* 20 */
+  float min_level_db;      /* -100 */
+  float max_abs_value;     /* 4 */
+  int symmetric_mels;      /* 1 */
+  int allow_clipping_in_normalization; /* 1 */
+  int griffin_lim_iters;   /* 60 */
+} tt2_gl_config;
+
+typedef struct tt2_gl_ctx tt2_gl_ctx;
+
+void tt2_gl_default_config(tt2_gl_config* cfg);
+tt2_status tt2_gl_create(const tt2_gl_config* cfg, int hip_device, tt2_gl_ctx** out);
+void tt2_gl_destroy(tt2_gl_ctx* ctx);
+/* pinv(mel_basis) [n_fft/2+1, num_mels] row-major (_mel_to_linear_tensorflow, audio.py:237-241;
+ * the mel basis is librosa.filters.mel(sr, n_fft, num_mels, fmin, fmax), audio.py:243-246). */
+tt2_status tt2_gl_set_inv_mel_basis(tt2_gl_ctx* ctx, const float* inv_basis);
+/* spec [T, num_mels] (is_mel = 1, normalised mel as the Tacotron emits it) or [T, n_fft/2+1]
+ * (is_mel = 0, normalised linear spectrogram) -> wav_out [(T-1)*hop + win] (no inverse
+ * pre-emphasis: the reference applies it on the host afterwards, synthesizer.py:153-154).
+ * iters < 0 = cfg.griffin_lim_iters. */
+tt2_status tt2_gl_synthesize(tt2_gl_ctx* ctx, const float* spec, int T, int is_mel, int iters,
+                             float* wav_out);
+/* Same on DEVICE pointers, enqueued on `stream` (hipStream_t as void*). */
+tt2_status tt2_gl_synthesize_dev(tt2_gl_ctx* ctx, const float* spec_d, int T, int is_mel,
+                                 int iters, float* wav_d, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

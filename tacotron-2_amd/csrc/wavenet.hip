@@ -175,7 +175,6 @@ struct GenArgs {
   int C;
   int legacy, res_legacy;
   float log_scale_min, log_scale_min_gauss;
-  int gauss;                               // out_channels == 2: Gaussian head
   const float* u_mix; const float* u_log;  // [T][Bg][nr], [T][Bg] or null (Gaussian: u_log = N(0,1) draws)
   uint64_t seed;
   const float* teacher;  // [Bg][T] or null
@@ -255,7 +254,9 @@ __device__ __forceinline__ float agpr_get(float r) {
   return v;
 }
 
-template <bool LEGACY, bool RES_LEGACY>
+// GAUSS: out_channels == 2 Gaussian head (a template parameter so the MoL instantiation keeps
+// its register allocation: a runtime flag costs the register-resident generator spills)
+template <bool LEGACY, bool RES_LEGACY, bool GAUSS>
 __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
   constexpr int R = 64, G = 128, S = 64, NT = WN_THREADS;
   const int blk = blockIdx.x, xl = blk & 7, grp = blk >> 3;
@@ -346,19 +347,20 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
     f32x4 cn = {0.f, 0.f, 0.f, 0.f};
     const bool has_next = t + 1 < a.T;
     if (has_next && tid < nl * G / 4) cn = cond4[((long)b * a.T + t + 1) * crow + l0 * G / 4 + tid];
-    if (last && wave == 1 && a.gauss) {  // this sample's N(0,1) draw (injected in u_log, or Box-Muller)
+    if (GAUSS && last && wave == 1) {  // this sample's N(0,1) draw (injected in u_log, or Box-Muller)
       if (lane == 15) {
         float nz;
         if (a.u_log) {
           nz = a.u_log[(long)t * a.Bg + b];
         } else {
           const uint64_t k0 = ((uint64_t)t * a.Bg + b) * 16;
-          const double u1 = u01_open(mix64(a.seed ^ mix64(k0 + 14))), u2 = u01_open(mix64(a.seed ^ mix64(k0 + 15)));
-          nz = (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+          const float u1 = (float)u01_open(mix64(a.seed ^ mix64(k0 + 14)));
+          const float u2 = (float)u01_open(mix64(a.seed ^ mix64(k0 + 15)));
+          nz = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
         }
         gum[cb_cur * 16 + 15] = nz;
       }
-    } else if (last && wave == 1) {  // this sample's Gumbel terms and logistic noise
+    } else if (!GAUSS && last && wave == 1) {  // this sample's Gumbel terms and logistic noise
       if (lane < nr) {
         const float um = a.u_mix ? a.u_mix[((long)t * a.Bg + b) * nr + lane]
                                  : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.Bg + b) * 16 + lane)));
@@ -577,13 +579,13 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
     {
       float temp = -INFINITY;
       int idx = lane;
-      if (!a.gauss && lane < nr) temp = lg[lane] - gum[cb_cur * 16 + lane];
+      if (!GAUSS && lane < nr) temp = lg[lane] - gum[cb_cur * 16 + lane];
       argmax16(temp, idx);  // nr <= 10: the mixture logits sit in lanes 0..15
       if (lane == 0) {
         // MoL: mixture idx (mixture.py:92-105); Gaussian: out = [mean, log_scale] (gaussian.py:39-52)
-        if (a.gauss) idx = 0;
-        const float mean = a.gauss ? lg[0] : lg[nr + idx];
-        const float ls = a.gauss ? fmaxf(lg[1], a.log_scale_min_gauss) : fmaxf(lg[2 * nr + idx], a.log_scale_min);
+        if (GAUSS) idx = 0;
+        const float mean = GAUSS ? lg[0] : lg[nr + idx];
+        const float ls = GAUSS ? fmaxf(lg[1], a.log_scale_min_gauss) : fmaxf(lg[2 * nr + idx], a.log_scale_min);
         float x = mean + expf(ls) * gum[cb_cur * 16 + 15];
         x = fminf(fmaxf(x, -1.f), 1.f);
         const float xn = a.teacher ? a.teacher[(long)b * a.T + t] : x;  // wavenet.py:876-878
@@ -734,9 +736,13 @@ static void wn_finalize(tt2_wn_ctx* c) {
 }
 
 typedef void (*PipeKernel)(GenArgs);
-static PipeKernel pipe_kernel(bool legacy, bool res_legacy) {
-  if (legacy) return res_legacy ? k_generate_pipe<true, true> : k_generate_pipe<true, false>;
-  return res_legacy ? k_generate_pipe<false, true> : k_generate_pipe<false, false>;
+static PipeKernel pipe_kernel(bool legacy, bool res_legacy, bool gauss) {
+  if (gauss) {
+    if (legacy) return res_legacy ? k_generate_pipe<true, true, true> : k_generate_pipe<true, false, true>;
+    return res_legacy ? k_generate_pipe<false, true, true> : k_generate_pipe<false, false, true>;
+  }
+  if (legacy) return res_legacy ? k_generate_pipe<true, true, false> : k_generate_pipe<true, false, false>;
+  return res_legacy ? k_generate_pipe<false, true, false> : k_generate_pipe<false, false, false>;
 }
 
 // the generation kernel's bounded spins report a stalled hand-off through the status word
@@ -812,7 +818,6 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   a.f1_w = c->f1_w.as<float>(); a.f1_b = c->f1_b.as<float>(); a.f2_w = c->f2_w.as<float>(); a.f2_b = c->f2_b.as<float>();
   a.C = c->C; a.legacy = c->cfg.legacy; a.res_legacy = c->cfg.residual_legacy; a.log_scale_min = c->cfg.log_scale_min;
   a.log_scale_min_gauss = c->cfg.log_scale_min_gauss;
-  a.gauss = c->C == 2;
   a.u_mix = umix_d; a.u_log = ulog_d; a.seed = seed; a.teacher = teacher_d;
   a.wav = wav_d; a.kout = k_d; a.logits = logits_d;
   a.status = c->gran.as<int>();
@@ -827,7 +832,7 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
     // every polled word (granule tags, status) starts at 0 for each launch (Guideline 16)
     TT2_HIP(hipMemsetAsync(c->gran.p, 0, gbytes, s));
     const int grid = cdiv(a.B, 8) * nst * 8;
-    const auto kern = pipe_kernel(c->cfg.legacy != 0, c->cfg.residual_legacy != 0);
+    const auto kern = pipe_kernel(c->cfg.legacy != 0, c->cfg.residual_legacy != 0, c->C == 2);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WN_THREADS), shm, s, a);
     TT2_HIP(hipGetLastError());
     TT2_HIP(hipMemcpyAsync(c->status_host, c->gran.p, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -887,7 +892,7 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
     for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
     const size_t shm = gen_lds_bytes(c.get());
     TT2_CHECK(shm <= 160 * 1024, TT2_ERR_INVALID_ARG, "queue rings exceed the 160 KiB LDS of a CU");
-    const void* kern = reinterpret_cast<const void*>(pipe_kernel(cfg->legacy != 0, cfg->residual_legacy != 0));
+    const void* kern = reinterpret_cast<const void*>(pipe_kernel(cfg->legacy != 0, cfg->residual_legacy != 0, cfg->out_channels == 2));
     TT2_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     // co-residency: one stage workgroup per CU, every workgroup of a launch resident at once
     int nb = 0, ncu = 0;

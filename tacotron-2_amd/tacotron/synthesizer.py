@@ -6,9 +6,10 @@ seeded random initialisation.  ``synthesize`` keeps the reference's arguments an
 ``filenames_to_inputs`` pads ids per tower and reference mels with -max_abs_value, the stop
 tokens give each row's length (``get_output_lengths``), mels are trimmed and clipped to
 T2_output_range and written as ``<out_dir>/mels/mel-<basename>_<basename_ref>.npy`` (float32,
-[T, 80]).  Differences, each because the piece is off the hot path: no Griffin-Lim wav, no
-alignment/spectrogram plots, no live playback (``basenames=None`` returns the mels instead of
-playing them).  The reference returns an always-empty ``saved_mels_paths`` (it never appends,
+[T, 80]); with a ``log_dir`` each mel is also vocoded by the GPU Griffin-Lim
+(``tt2.audio.inv_mel_spectrogram``) into ``<log_dir>/wavs/wav-<basename>_<ref>.wav`` like the
+reference.  Not reproduced (off the hot path): alignment/spectrogram plots, live playback
+(``basenames=None`` returns the mels instead of playing them).  The reference returns an always-empty ``saved_mels_paths`` (it never appends,
 synthesizer.py:221); here it lists the files written, so ``run_eval``'s map.txt gets its rows.
 """
 import os
@@ -92,6 +93,16 @@ class Synthesizer:
                                                                                basenames_refs[i]))
             np.save(mel_filename, mel.astype(np.float32), allow_pickle=False)
             saved_mels_paths.append(mel_filename)
+            if log_dir is not None and len(mel):
+                # mel -> wav through the GPU Griffin-Lim (GL_on_GPU, synthesizer.py:199-206),
+                # 0.5 s of silence on both sides
+                from tt2.audio import inv_mel_spectrogram, save_wav
+                os.makedirs(os.path.join(log_dir, 'wavs'), exist_ok=True)
+                wav = inv_mel_spectrogram(mel, hparams)
+                pad = np.zeros(int(.5 * hparams.sample_rate))
+                save_wav(np.concatenate([pad, wav, pad]),
+                         os.path.join(log_dir, 'wavs/wav-{}_{}.wav'.format(basenames[i], basenames_refs[i])),
+                         sr=hparams.sample_rate)
         return saved_mels_paths, speaker_ids
 
 

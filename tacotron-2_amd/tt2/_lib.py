@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libtt2.so")
+# TT2_LIB: an alternative build of the same ABI (A/B kernel experiments); default = in-tree
+LIB_PATH = os.environ.get("TT2_LIB") or os.path.join(os.path.dirname(_HERE), "libtt2.so")
 
 TT2_OK = 0
 _STATUS = {-1: "INVALID_ARG", -2: "SHAPE_MISMATCH", -3: "OOM", -4: "HIP_ERROR", -5: "NOT_LOADED",
@@ -57,6 +58,15 @@ class WnConfig(ctypes.Structure):
         ("log_scale_min_gauss", ctypes.c_float)]
 
 
+class GlConfig(ctypes.Structure):
+    """tt2_gl_config (include/tt2.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in ("n_fft", "hop_size", "win_size", "num_mels")] + [
+        (n, ctypes.c_float) for n in ("magnitude_power", "power", "ref_level_db", "min_level_db",
+                                      "max_abs_value")] + [
+        (n, ctypes.c_int) for n in ("symmetric_mels", "allow_clipping_in_normalization",
+                                    "griffin_lim_iters")]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _U64 = ctypes.c_uint64
@@ -92,6 +102,12 @@ SIGNATURES = {
     "tt2_wn_generate": (_I, [_P, _P, _I, _I, _P, _P, _U64, _P, _P, _P, _P, _P]),
     "tt2_wn_generate_dev": (_I, [_P, _P, _I, _I, _P, _P, _U64, _P, _P, _P, _P, _P]),
     "tt2_wn_cond_from_mels_dev": (_I, [_P, _I, _P, _I, _I, _I, _F, _F, _I, _I, _P, _P]),
+    "tt2_gl_default_config": (None, [ctypes.POINTER(GlConfig)]),
+    "tt2_gl_create": (_I, [ctypes.POINTER(GlConfig), _I, ctypes.POINTER(_P)]),
+    "tt2_gl_destroy": (None, [_P]),
+    "tt2_gl_set_inv_mel_basis": (_I, [_P, _P]),
+    "tt2_gl_synthesize": (_I, [_P, _P, _I, _I, _I, _P]),
+    "tt2_gl_synthesize_dev": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "tt2_mol_sample": (_I, [_P, _P, _P, _I, _I, _F, _P, _P]),
 }
 

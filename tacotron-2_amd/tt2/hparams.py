@@ -96,6 +96,7 @@ _FORK = dict(
     signal_normalization=True, allow_clipping_in_normalization=True, symmetric_mels=True,
     max_abs_value=4.0, normalize_for_wavenet=True, clip_for_wavenet=True, wavenet_pad_sides=1,
     min_level_db=-100, ref_level_db=20, fmin=55, fmax=7600, power=1.5, griffin_lim_iters=60,
+    magnitude_power=2.0, use_lws=False,
     GL_on_GPU=True,
     # GST (hparams.py:108-115)
     use_gst=True, num_gst=10, num_heads=4, style_embed_depth=256,

@@ -154,6 +154,9 @@ def test_synthesizer_file_contract(tmp_path):
                                mel_ref_filenames_spk=refs[::-1],
                                prenet_masks=prenet_masks(n, 2, hp.prenet_layers[0], seed=1))
     assert [p.split("/")[-1] for p in paths] == ["mel-a_r0.npy", "mel-b_r1.npy"]
+    for b, r in (("a", "r0"), ("b", "r1")):   # Griffin-Lim wavs of the eval log dir
+        sr, gl = wavfile.read(str(tmp_path / "wavs" / "wav-{}_{}.wav".format(b, r)))
+        assert sr == hp.sample_rate and gl.dtype == np.int16
     assert spk == ["<no_g>", "<no_g>"]
     mels = [np.load(p, allow_pickle=False) for p in paths]
     for m, tl in zip(mels, ts.target_lengths):
