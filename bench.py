@@ -153,13 +153,14 @@ def bench_griffin_lim(local, frames=1000):
                                                 ctypes.c_void_p(st.cuda_stream)))
 
     run()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
+    # wall clock between device-wide synchronizes: torch's default stream is the NULL handle, so
+    # the library runs on its own stream and torch events would not bracket it
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
     for _ in range(3):
         run()
-    e1.record(st)
     torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / 3
+    ms = (time.perf_counter() - t0) * 1e3 / 3
     gl.close()
     n = hp.n_fft
     # algorithmic bytes per iteration: spec read + angle write/read + frame buffer write/read

@@ -75,12 +75,24 @@ class TextToSpeech(object):
         u_log_d [>=T,B] MoL uniforms for T = max(lengths)*hop samples (t-major, so a buffer sized
         for max_iters*hop serves any decoded length).  None = the device RNGs keyed by ``seed``."""
         import torch
-        hp = self.hp
         dev = ids_d.device
+        if stream is None:
+            # one explicit stream for the whole chain: torch's default stream is the NULL handle,
+            # which the library maps to each context's OWN non-blocking stream -- two contexts
+            # (Tacotron, WaveNet) plus the hand-off kernels would then run unordered
+            if getattr(self, "_stream", None) is None:
+                self._stream = torch.cuda.Stream(dev)
+            self._stream.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(self._stream):
+                out = self.synthesize_dev(ids_d, lens_d, lens_h, ref_emt_d, ref_spk_d, seed,
+                                          self._stream.cuda_stream, max_iters, u_mix_d, u_log_d,
+                                          prenet_masks_d)
+            torch.cuda.current_stream(dev).wait_stream(self._stream)
+            return out
+        hp = self.hp
         B, T_in = ids_d.shape
         mi = self.max_iters if max_iters is None else max_iters
-        st = ctypes.c_void_p(stream if stream is not None else
-                             torch.cuda.current_stream(dev).cuda_stream)
+        st = ctypes.c_void_p(stream)
         lens_h = np.ascontiguousarray(lens_h, np.int32)
         mel = torch.empty((B, mi, hp.num_mels), dtype=torch.float32, device=dev)
         stop = torch.empty((B, mi), dtype=torch.float32, device=dev)
@@ -95,7 +107,7 @@ class TextToSpeech(object):
         n = n.value
         lengths_d = torch.empty((B,), dtype=torch.int32, device=dev)
         check(self.lib.tt2_output_lengths_dev(stop.data_ptr(), B, n, mi, lengths_d.data_ptr(), st))
-        lengths = lengths_d.cpu().numpy()  # the one host round trip: sizes the WaveNet run
+        lengths = lengths_d.cpu().numpy()  # the one host round trip (on this stream): sizes WaveNet
         T_f = int(lengths.max()) if B else 0
         wav = torch.zeros((B, max(T_f, 0) * self.hop), dtype=torch.float32, device=dev)
         if T_f > 0:
