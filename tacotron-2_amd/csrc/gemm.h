@@ -30,7 +30,12 @@ struct GemmArgs {
   long ldr = 0;
   int clip = 0;
   float clip_lo = 0.f, clip_hi = 0.f;
-  // optional second output of the pre-residual value (unused = nullptr)
+  // arithmetic: 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 products); 1 = split fp16x3:
+  // every operand x = hi + lo (two fp16, after an exact power-of-two pre-scale A·2^4, B·2^10 that
+  // keeps lo out of fp16 subnormals), A·B = Ah·Bh + Ah·Bl + Al·Bh on v_mfma_f32_32x32x16_f16 with
+  // fp32 accumulation (the dropped lo·lo term is ~2^-22 relative; fp16 products are exact in
+  // fp32) -- 3/16 of the fp32 MFMA cost, ~1e-7 relative error.  Needs |A| < 4e3, |B| < 64.
+  int split16 = 0;
 };
 
 void gemm(const GemmArgs& a, hipStream_t s);

@@ -1,4 +1,5 @@
-// fp32 GEMM on the CDNA4 f32-input matrix cores (v_mfma_f32_32x32x2_f32, exact fp32 fma chain).
+// fp32 GEMM on the CDNA4 matrix cores: exact fp32 (v_mfma_f32_32x32x2_f32) or split fp16x3
+// (v_mfma_f32_32x32x16_f16 on hi/lo halves, GemmArgs::split16).
 //
 // C[M,N] = epilogue(A[M,K] · B[K,N]).  A is read through an implicit-im2col loader (dense rows,
 // 'same' conv1d, NHWC conv2d) so the encoder/postnet/refnet convolutions never materialise their
@@ -81,6 +82,29 @@ __device__ __forceinline__ void load_b4(const GemmArgs& g, int k, int n, float* 
   }
 }
 
+// Fused epilogue of one 32x32 accumulator tile (C/D layout: col = lane&31,
+// row = (r&3) + 8*(r>>2) + 4*(lane>>5), identical for the f32 and f16 MFMA shapes on gfx950).
+__device__ __forceinline__ void epilogue_tile(const GemmArgs& g, const f32x16& acc, int row0, int col0, int lane) {
+  const int col = col0 + (lane & 31);
+  if (col >= g.N) return;
+  const float bias = g.bias ? g.bias[col] : 0.f;
+  const float sc = g.bn_scale ? g.bn_scale[col] : 1.f;
+  const float sh = g.bn_shift ? g.bn_shift[col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row >= g.M) continue;
+    float y = acc[r] + bias;
+    if (g.act == ACT_RELU) y = fmaxf(y, 0.f);
+    else if (g.act == ACT_TANH) y = tanhf(y);
+    if (g.bn_scale) y = y * sc + sh;
+    if (g.act == ACT_BN_RELU) y = fmaxf(y, 0.f);  // BN then ReLU (conv2d(), modules.py:507-510)
+    if (g.residual) y = g.residual[(long)row * g.ldr + col] + y;
+    if (g.clip) y = fminf(fmaxf(y, g.clip_lo), g.clip_hi);
+    g.Cout[(long)row * g.ldc + col] = y;
+  }
+}
+
 template <int WMB, int WNB, bool VA, bool VB>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   constexpr int BM = 64 * WMB, BN = 64 * WNB, BK = 16;
@@ -139,29 +163,115 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
   for (int i = 0; i < WMB; ++i)
 #pragma unroll
-    for (int j = 0; j < WNB; ++j) {
-      const int col = n0 + wn * 32 * WNB + j * 32 + (lane & 31);
-      if (col >= g.N) continue;
-      const float bias = g.bias ? g.bias[col] : 0.f;
-      const float sc = g.bn_scale ? g.bn_scale[col] : 1.f;
-      const float sh = g.bn_shift ? g.bn_shift[col] : 0.f;
+    for (int j = 0; j < WNB; ++j)
+      epilogue_tile(g, acc[i][j], m0 + wm * 32 * WMB + i * 32, n0 + wn * 32 * WNB + j * 32, lane);
+}
+
+
+// ---- split fp16x3 GEMM (GemmArgs::split16) -------------------------------------------------
+// Block 128x128x32, 4 waves in a 2x2 grid, each wave 2x2 tiles of 32x32 (v_mfma_f32_32x32x16_f16:
+// lane l holds A[row l&31][k = 8(l>>5) + j] and B[k = 8(l>>5) + j][col l&31], j < 8).  Operands are
+// split into fp16 hi/lo planes when staged into LDS ([row][k] for A, [col][k] for B, k contiguous:
+// one ds_read_b128 per fragment), LDS double-buffered, next tile prefetched into registers.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int X3_BK = 32, X3_LD = X3_BK + 8;  // padded k stride (halfs)
+// Operands are pre-scaled by powers of two before the split (A x2^4, B x2^10, result x2^-14,
+// exact): an unscaled lo of a 1e-3 weight is an fp16 subnormal with ~1% precision, which cost up
+// to 3e-5 relative error; scaled, the split is ~1e-7 relative for |A| < 4e3, |B| < 64.
+constexpr float X3_SA = 16.f, X3_SB = 1024.f, X3_UNSCALE = 1.f / (16.f * 1024.f);
+
+__device__ __forceinline__ void split8(const float* v, float scale, f16x8& hi, f16x8& lo) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 32 * WMB + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= g.M) continue;
-        float y = acc[i][j][r] + bias;
-        if (g.act == ACT_RELU) y = fmaxf(y, 0.f);
-        else if (g.act == ACT_TANH) y = tanhf(y);
-        if (g.bn_scale) y = y * sc + sh;
-        if (g.act == ACT_BN_RELU) y = fmaxf(y, 0.f);  // BN then ReLU (conv2d(), modules.py:507-510)
-        if (g.residual) y = g.residual[(long)row * g.ldr + col] + y;
-        if (g.clip) y = fminf(fmaxf(y, g.clip_lo), g.clip_hi);
-        g.Cout[(long)row * g.ldc + col] = y;
+  for (int e = 0; e < 8; ++e) {
+    const float x = v[e] * scale;
+    const _Float16 h = (_Float16)x;
+    hi[e] = h;
+    lo[e] = (_Float16)(x - (float)h);
+  }
+}
+
+template <bool VA>
+__global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
+  constexpr int BM = 128, BN = 128, BK = X3_BK;
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[2][BM][X3_LD], Al[2][BM][X3_LD];
+  __shared__ __attribute__((aligned(16))) _Float16 Bh[2][BN][X3_LD], Bl[2][BN][X3_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int am = tid >> 1, ak = (tid & 1) * 16;    // A: row am, k [ak, ak+16)
+  const int bn = tid & 127, bk = (tid >> 7) * 16;  // B: col bn, k [bk, bk+16) (coalesced over n)
+  float ra[16], rb[16];
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 16; e += 4) load_a4<VA>(g, m0 + am, k0 + ak + e, &ra[e]);
+    const int n = n0 + bn;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int k = k0 + bk + e;
+      rb[e] = (n < g.N && k < g.K) ? g.Bw[(long)k * g.ldb + n] : 0.f;
+    }
+  };
+  auto sstore = [&](int buf) {
+    f16x8 h, l;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      split8(&ra[8 * q], X3_SA, h, l);
+      *reinterpret_cast<f16x8*>(&Ah[buf][am][ak + 8 * q]) = h;
+      *reinterpret_cast<f16x8*>(&Al[buf][am][ak + 8 * q]) = l;
+      split8(&rb[8 * q], X3_SB, h, l);
+      *reinterpret_cast<f16x8*>(&Bh[buf][bn][bk + 8 * q]) = h;
+      *reinterpret_cast<f16x8*>(&Bl[buf][bn][bk + 8 * q]) = l;
+    }
+  };
+
+  const int nk = (g.K + BK - 1) / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int r = lane & 31, h8 = (lane >> 5) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+    for (int s16 = 0; s16 < BK; s16 += 16) {
+      f16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = *reinterpret_cast<const f16x8*>(&Ah[cur][wm * 64 + i * 32 + r][s16 + h8]);
+        al[i] = *reinterpret_cast<const f16x8*>(&Al[cur][wm * 64 + i * 32 + r][s16 + h8]);
+        bh[i] = *reinterpret_cast<const f16x8*>(&Bh[cur][wn * 64 + i * 32 + r][s16 + h8]);
+        bl[i] = *reinterpret_cast<const f16x8*>(&Bl[cur][wn * 64 + i * 32 + r][s16 + h8]);
       }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] *= X3_UNSCALE;
+      epilogue_tile(g, acc[i][j], m0 + wm * 64 + i * 32, n0 + wn * 64 + j * 32, lane);
     }
 }
 
@@ -183,6 +293,13 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   if (a.a_mode == A_DENSE) va = va && (a.lda % 4 == 0);
   else if (a.a_mode == A_CONV1D) va = va && (a.C % 4 == 0) && (a.xs_t % 4 == 0) && (a.xs_b % 4 == 0);
   else va = va && (a.C % 4 == 0);
+  if (a.split16) {
+    dim3 grid(cdiv(a.N, 128), cdiv(a.M, 128));
+    if (va) hipLaunchKernelGGL(gemm_x3_kernel<true>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(gemm_x3_kernel<false>, grid, dim3(256), 0, s, a);
+    TT2_HIP(hipGetLastError());
+    return;
+  }
   const bool vb = al16(a.Bw) && (a.ldb % 4 == 0);
   const int wnb = a.N <= 64 ? 1 : 2;
   const long tiles22 = (long)cdiv(a.M, 128) * cdiv(a.N, 64 * wnb);

@@ -1527,6 +1527,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.Bw = c->enc_cw[i].as<float>(); g.ldb = c->Cenc; g.Cout = xout; g.ldc = c->Cenc;
     g.bias = c->enc_cb[i].as<float>(); g.act = ACT_RELU;
     g.bn_scale = c->enc_bs[i].as<float>(); g.bn_shift = c->enc_bh[i].as<float>();
+    g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
     std::swap(xin, xout);
     cin = c->Cenc;
@@ -1537,6 +1538,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.M = BT; g.N = 8 * c->U; g.K = cin; g.A = xin; g.lda = cin;
     g.Bw = c->enc_wx.as<float>(); g.ldb = 8 * c->U; g.Cout = c->xproj.as<float>(); g.ldc = 8 * c->U;
     g.bias = c->enc_bx.as<float>();
+    g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
   }
   TT2_HIP(hipMemsetAsync(c->enc_h.p, 0, c->enc_h.bytes, s));
@@ -1584,6 +1586,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
         g.Bw = R.cw[i].as<float>(); g.ldb = f; g.Cout = bufs[i & 1]; g.ldc = f;
         g.bias = R.cb[i].as<float>(); g.act = ACT_BN_RELU;
         g.bn_scale = R.bs[i].as<float>(); g.bn_shift = R.bh[i].as<float>();
+        g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
         gemm(g, s);
         x = bufs[i & 1];
         H = Ho; Wd = Wo; C = f;
@@ -1596,6 +1599,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
         g.M = B * H; g.N = 3 * D; g.K = R.gin; g.A = x; g.lda = R.gin;
         g.Bw = R.wx.as<float>(); g.ldb = 3 * D; g.Cout = c->refxg.as<float>(); g.ldc = 3 * D;
         g.bias = R.bx.as<float>();
+        g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
         gemm(g, s);
       }
       RefGstArgs a;
@@ -1621,6 +1625,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.M = BT; g.N = c->A; g.K = c->Dm; g.A = c->values.as<float>(); g.lda = c->Dm;
     g.Bw = c->mem_k.as<float>(); g.ldb = c->A; g.Cout = c->keys.as<float>(); g.ldc = c->A;
     g.bias = c->keys_b.as<float>();  // b_a + b_conv·W_loc (folded location-feature bias)
+    g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
   }
   {  // per-utterance style terms of the decoder: GS = style·W_lstm1[style rows], PS = style·W_proj[style rows]
@@ -1994,6 +1999,7 @@ static void postnet_dev(tt2_ctx* c, const float* frames_d, long frames_bstride, 
     g.Bw = c->post_cw[i].as<float>(); g.ldb = c->PC; g.Cout = bufs[i & 1]; g.ldc = c->PC;
     g.bias = c->post_cb[i].as<float>(); g.act = (i < cfg.postnet_num_layers - 1) ? ACT_TANH : ACT_NONE;
     g.bn_scale = c->post_bs[i].as<float>(); g.bn_shift = c->post_bh[i].as<float>();
+    g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
     xin = bufs[i & 1];
     cin = c->PC;
@@ -2002,6 +2008,7 @@ static void postnet_dev(tt2_ctx* c, const float* frames_d, long frames_bstride, 
   g.M = B * T; g.N = c->nm; g.K = c->PC; g.A = xin; g.lda = c->PC;
   g.Bw = c->post_pw.as<float>(); g.ldb = c->nm; g.Cout = mel_d; g.ldc = c->nm; g.bias = c->post_pb.as<float>();
   g.residual = dec_d; g.ldr = c->nm; g.clip = cfg.clip_outputs; g.clip_lo = lo; g.clip_hi = hi;
+  g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
   gemm(g, s);
 }
 

@@ -804,6 +804,7 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   g.M = (int)(B * T); g.N = c->L * c->G; g.K = F; g.A = c->c_up_t.as<float>(); g.lda = F;
   g.Bw = c->cond_w.as<float>(); g.ldb = c->L * c->G; g.Cout = c->cond.as<float>(); g.ldc = c->L * c->G;
   g.bias = c->cond_b.as<float>();
+  g.split16 = 1;  // conditioning in [0, 1] after the upsampler: fp16x3 split MFMA (gemm.h)
   gemm(g, s);
   TT2_HIP(hipEventRecord(c->ev[2], s));
   const int nst = wn_stages(c);
