@@ -1,0 +1,167 @@
+"""TEST INFRASTRUCTURE ONLY — torch (CPU, float64 autograd) restatement of the teacher-forced
+Tacotron-2 decoder training step of mwhitehill/Tacotron-2 (SURVEY.md §8f rank 1, configs[4]).
+
+Only ``tests/`` and ``bench.py``'s ``cpu_baseline`` leg may import this module, as the checker;
+the product path (``tacotron-2_amd``) never does.  Parity status: **parity unpinned** (TensorFlow
+is absent, the reference has no training fixtures); the forward half is pinned to the numpy
+inference oracle (``oracle/tacotron_ref.py``) by running it with inference zoneout, and the
+gradients are torch autograd of this restatement.
+
+Scope of the slice ("decoder training step"): memory (encoder outputs ⊕ style, as the decoder
+receives it) → memory_layer keys → teacher-forced ``dynamic_decode`` with TacoTrainingHelper
+(ratio 1, constant mode: hparams.py:300-301, helpers.py:118-129) → frame/stop projections →
+losses ``before`` (MSE, mask_decoder=False: tacotron.py:774) + stop sigmoid cross-entropy
+(tacotron.py:778-779) + L2 regularisation of the decoder-slice kernels (tacotron.py:865-867) →
+gradients → tower mean + clip_by_global_norm(1.0) (tacotron.py:1194-1221) → TF AdamOptimizer
+(tacotron.py:1029) with the exponential learning-rate decay (tacotron.py:1227-1251;
+hparams.py:272-282).  The Postnet
+``after`` loss and the encoder backward are outside this slice.
+
+Training-mode zoneout (modules.py:236-240): ``c = (1-z)·dropout(c_new - c_prev, 1-z) + c_prev``,
+i.e. ``c = c_prev + m·(c_new - c_prev)`` with keep bits m ~ Bernoulli(1-z) (injected).
+"""
+import numpy as np
+import torch
+
+P = "Tacotron_model/inference/"
+LA = P + "decoder/Location_Sensitive_Attention/"
+L1 = P + "decoder/decoder_LSTM/multi_rnn_cell/cell_0/lstm_cell/"
+L2 = P + "decoder/decoder_LSTM/multi_rnn_cell/cell_1/lstm_cell/"
+FP = P + "decoder/linear_transform_projection/projection_linear_transform_projection/"
+SP = P + "decoder/stop_token_projection/projection_stop_token_projection/"
+
+
+def train_var_names(n_prenet=2):
+    """The decoder-slice trainable variables, in the order of the library's flat buffers."""
+    names = [P + "memory_layer/kernel", P + "decoder/query_layer/kernel",
+             LA + "location_features_convolution/kernel", LA + "location_features_convolution/bias",
+             LA + "location_features_layer/kernel", LA + "attention_variable_projection",
+             LA + "attention_bias"]
+    for i in range(n_prenet):
+        s = P + "decoder/decoder_prenet/dense_{}/".format(i + 1)
+        names += [s + "kernel", s + "bias"]
+    names += [L1 + "kernel", L1 + "bias", L2 + "kernel", L2 + "bias",
+              FP + "kernel", FP + "bias", SP + "kernel", SP + "bias"]
+    return names
+
+
+def regularized(name):
+    """tacotron.py:865-867: every variable except biases, '_projection', embeddings, RNN/LSTM."""
+    return not ("bias" in name or "Bias" in name or "_projection" in name
+                or "inputs_embedding" in name or "RNN" in name or "LSTM" in name)
+
+
+def _conv_same(cum, k, b):
+    """tf.layers.conv1d 'same', 1 input channel (attention.py:193-195): cum [B,T], k [kw,1,F]."""
+    kw = k.shape[0]
+    pad = (kw - 1) // 2
+    x = torch.nn.functional.pad(cum, (pad, kw - 1 - pad))
+    cols = x.unfold(1, kw, 1)                          # [B,T,kw]
+    return cols @ k[:, 0, :] + b                       # [B,T,F]
+
+
+def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneout=0.1):
+    """Teacher-forced decoder forward.  W: dict name -> torch tensor (requires_grad as wanted);
+    memory [B,T_in,D]; lengths [B]; targets [B,T,80]; prenet_masks [T,2,B,P] keep bits;
+    zoneout_masks [T,4,B,H] keep bits (c1,h1,c2,h2; training zoneout) or None (inference mix).
+    Returns frames [B,T,80], stop logits [B,T], alignments [B,T_in,T]."""
+    B, T_in, D = memory.shape
+    T = targets.shape[1]
+    dt = memory.dtype
+    mask = (torch.arange(T_in)[None, :] < torch.as_tensor(lengths)[:, None]).to(dt)
+    values = memory * mask[:, :, None]                                  # BahdanauAttention memory
+    keys = values @ W[P + "memory_layer/kernel"]                        # memory_layer, no bias
+    H = W[L1 + "bias"].shape[0] // 4
+    c1 = h1 = c2 = h2 = torch.zeros(B, H, dtype=dt)
+    ctx = torch.zeros(B, D, dtype=dt)
+    cum = torch.zeros(B, T_in, dtype=dt)
+    frame_in = torch.zeros(B, targets.shape[2], dtype=dt)               # _go_frames helpers.py:136
+    big_neg = torch.tensor(float("-inf"), dtype=dt)
+    frames, stops, aligns = [], [], []
+
+    def cell(x, c, h, k, b, mc, mh):
+        z = torch.cat([x, h], 1) @ k + b
+        i, j, f, o = z.chunk(4, 1)
+        cn = torch.sigmoid(f + 1.0) * c + torch.sigmoid(i) * torch.tanh(j)
+        hn = torch.sigmoid(o) * torch.tanh(cn)
+        if mc is None:
+            return hn, (1 - zoneout) * cn + zoneout * c, (1 - zoneout) * hn + zoneout * h
+        return hn, c + mc * (cn - c), h + mh * (hn - h)
+
+    for t in range(T):
+        x = frame_in
+        for i in range(2):
+            s = P + "decoder/decoder_prenet/dense_{}/".format(i + 1)
+            x = torch.relu(x @ W[s + "kernel"] + W[s + "bias"]) / 0.5 * prenet_masks[t, i]
+        zm = [None] * 4 if zoneout_masks is None else [zoneout_masks[t, q] for q in range(4)]
+        o1, c1, h1 = cell(torch.cat([x, ctx], 1), c1, h1, W[L1 + "kernel"], W[L1 + "bias"],
+                          zm[0], zm[1])
+        o2, c2, h2 = cell(o1, c2, h2, W[L2 + "kernel"], W[L2 + "bias"], zm[2], zm[3])
+        q = o2 @ W[P + "decoder/query_layer/kernel"]
+        f = _conv_same(cum, W[LA + "location_features_convolution/kernel"],
+                       W[LA + "location_features_convolution/bias"])
+        loc = f @ W[LA + "location_features_layer/kernel"]
+        e = (W[LA + "attention_variable_projection"]
+             * torch.tanh(keys + q[:, None, :] + loc + W[LA + "attention_bias"])).sum(2)
+        e = torch.where(mask > 0, e, big_neg)
+        a = torch.softmax(e, 1)
+        cum = cum + a
+        ctx = (a[:, :, None] * values).sum(1)
+        pin = torch.cat([o2, ctx], 1)
+        frames.append(pin @ W[FP + "kernel"] + W[FP + "bias"])
+        stops.append((pin @ W[SP + "kernel"] + W[SP + "bias"])[:, 0])
+        aligns.append(a)
+        frame_in = targets[:, t]
+    return torch.stack(frames, 1), torch.stack(stops, 1), torch.stack(aligns, 2)
+
+
+def losses(frames, stop_logits, targets, stop_targets, W, reg_weight):
+    """before (tf.losses.mean_squared_error), stop (mean sigmoid CE, pos_weight 1), reg."""
+    before = ((frames - targets) ** 2).mean()
+    x, z = stop_logits, stop_targets
+    stop = (torch.clamp(x, min=0) - x * z + torch.log1p(torch.exp(-x.abs()))).mean()
+    reg = sum((v ** 2).sum() / 2 for n, v in W.items() if regularized(n)) * reg_weight
+    return before, stop, reg
+
+
+def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,
+                reg_weight=1e-6, dtype=torch.float64):
+    """One forward + backward; returns (outputs dict, losses tuple, grads dict incl. 'memory')."""
+    names = train_var_names()
+    W = {n: torch.tensor(np.asarray(Wnp[n]), dtype=dtype, requires_grad=True) for n in names}
+    mem = torch.tensor(np.asarray(memory), dtype=dtype, requires_grad=True)
+    tg = torch.tensor(np.asarray(targets), dtype=dtype)
+    st = torch.tensor(np.asarray(stop_targets), dtype=dtype)
+    pm = torch.tensor(np.asarray(prenet_masks), dtype=dtype)
+    zm = None if zoneout_masks is None else torch.tensor(np.asarray(zoneout_masks), dtype=dtype)
+    fr, sl, al = forward(W, mem, lengths, tg, pm, zm)
+    b, s, r = losses(fr, sl, tg, st, W, reg_weight)
+    (b + s + r).backward()
+    g = {n: W[n].grad.numpy() for n in names}
+    g["memory"] = mem.grad.numpy()
+    out = dict(frames=fr.detach().numpy(), stop_logits=sl.detach().numpy(),
+               alignments=al.detach().numpy())
+    return out, (b.item(), s.item(), r.item()), g
+
+
+def learning_rate(step, hp):
+    """Tacotron._learning_rate_decay (tacotron.py:1227-1251): exponential_decay from
+    tacotron_start_decay, clipped to [final, initial]."""
+    init = hp.tacotron_initial_learning_rate
+    lr = init * hp.tacotron_decay_rate ** ((step - hp.tacotron_start_decay) / hp.tacotron_decay_steps)
+    return min(max(lr, hp.tacotron_final_learning_rate), init)
+
+
+def clip_and_adam(params, grads, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-6, clip=1.0):
+    """tf.clip_by_global_norm(grads, 1.) then tf.train.AdamOptimizer.apply_gradients (step =
+    the post-increment count t >= 1): lr_t = lr·sqrt(1-b2^t)/(1-b1^t); m,v moments; w -= lr_t·m/
+    (sqrt(v)+eps).  Mutates params/m/v (dicts of float64 numpy arrays); returns the global norm."""
+    gn = float(np.sqrt(sum(float((np.asarray(g, np.float64) ** 2).sum()) for g in grads.values())))
+    scale = clip / max(gn, clip)
+    lr_t = lr * np.sqrt(1 - beta2 ** step) / (1 - beta1 ** step)
+    for n in params:
+        g = np.asarray(grads[n], np.float64) * scale
+        m[n] = beta1 * m[n] + (1 - beta1) * g
+        v[n] = beta2 * v[n] + (1 - beta2) * g * g
+        params[n] = params[n] - lr_t * m[n] / (np.sqrt(v[n]) + eps)
+    return gn

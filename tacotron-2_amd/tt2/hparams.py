@@ -116,6 +116,13 @@ _FORK = dict(
     tacotron_synthesis_batch_size=1, tacotron_spk_emb_dim=1024, tacotron_se_concat=True,
     tacotron_use_style_emb_disc=True, tacotron_style_emb_disc_refnet=True,
     tacotron_use_orthog_loss=True,
+    # Tacotron training (hparams.py:44,272-302)
+    tacotron_decay_learning_rate=True, tacotron_start_decay=15000,
+    tacotron_decay_steps=10000, tacotron_decay_rate=0.5, tacotron_initial_learning_rate=1e-3,
+    tacotron_final_learning_rate=1e-4, tacotron_adam_beta1=0.9, tacotron_adam_beta2=0.999,
+    tacotron_adam_epsilon=1e-6, tacotron_reg_weight=1e-6, tacotron_scale_regularization=False,
+    tacotron_clip_gradients=True, tacotron_teacher_forcing_mode="constant",
+    tacotron_teacher_forcing_ratio=1.0, cross_entropy_pos_weight=1,
     # WaveNet (hparams.py:207-253)
     input_type="raw", quantize_channels=2 ** 16, use_bias=True, legacy=True, residual_legacy=True,
     log_scale_min=float(np.log(1e-14)), log_scale_min_gauss=float(np.log(1e-7)), cdf_loss=False,

@@ -32,3 +32,26 @@ def mol_uniforms(T, B, nr=10, seed=5339):
     um = rng.uniform(1e-5, 1 - 1e-5, (T, B, nr)).astype(np.float32)
     ul = rng.uniform(1e-5, 1 - 1e-5, (T, B)).astype(np.float32)
     return um, ul
+
+
+def train_batch(B, T_in, T_out, D, num_mels=80, seed=1234, ragged=True):
+    """configs[4]-shaped synthetic teacher-forced batch: decoder memory N(0, 0.5) [B,T_in,D],
+    input lengths (ragged U[T_in/2, T_in], row 0 full), mel targets U[-4, 4] [B,T_out,80] and
+    stop-token targets (0 before each row's target length, 1 from it on; tacotron/feeder.py pads
+    with 1), target lengths U[T_out/2, T_out] (row 0 full)."""
+    rng = np.random.default_rng(seed)
+    memory = (rng.standard_normal((B, T_in, D)) * 0.5).astype(np.float32)
+    lengths = np.full(B, T_in, np.int32)
+    tlen = np.full(B, T_out, np.int32)
+    if ragged and B > 1:
+        lengths[1:] = rng.integers(max(1, T_in // 2), T_in + 1, B - 1)
+        tlen[1:] = rng.integers(max(1, T_out // 2), T_out + 1, B - 1)
+    targets = rng.uniform(-4, 4, (B, T_out, num_mels)).astype(np.float32)
+    stop = (np.arange(T_out)[None, :] >= tlen[:, None] - 1).astype(np.float32)
+    return memory, lengths, targets, stop
+
+
+def zoneout_masks(n, B, H, rate=0.1, seed=5339):
+    """Training-mode zoneout keep bits (modules.py:236-240: dropout(new - prev, 1 - rate)) of the
+    two decoder LSTMs: [n, 4, B, H] uint8 (c1, h1, c2, h2)."""
+    return (np.random.default_rng(seed + 1).random((n, 4, B, H)) >= rate).astype(np.uint8)

@@ -1,0 +1,98 @@
+"""Teacher-forced decoder training step (SURVEY.md §8f rank 1, configs[4]).
+
+CPU: the torch-autograd oracle (oracle/train_ref.py) is pinned to the numpy inference oracle's
+teacher-forced decode, its gradients to finite differences, its Adam/clip step to the TF formulas.
+GPU (-m gpu): libtt2's training kernels (csrc/train.hip) through the C ABI against that oracle.
+Parity unpinned against TF itself.
+"""
+import numpy as np
+import pytest
+import torch
+
+from _common import small_hparams
+from oracle import tacotron_ref as TR
+from oracle import train_ref as TRN
+from oracle.hp import oracle_hp
+from tt2.synthetic import prenet_masks, train_batch, zoneout_masks
+from tt2.weights import init_tacotron_weights, memory_width
+
+MEM_K = "Tacotron_model/inference/memory_layer/kernel"
+
+
+def _case(hp, B=3, T_in=9, T_out=7, seed=11):
+    W = init_tacotron_weights(hp, seed=5339)
+    D = memory_width(hp)
+    mem, lens, tg, st = train_batch(B, T_in, T_out, D, seed=seed)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=seed)
+    zm = zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=seed)
+    return W, mem, lens, tg, st, pm, zm
+
+
+def test_forward_matches_numpy_inference_oracle():
+    """With inference zoneout the torch restatement is the numpy oracle's GTA decode."""
+    hp = small_hparams()
+    W, mem, lens, tg, st, pm, _ = _case(hp)
+    Wt = {n: torch.tensor(np.asarray(W[n]), dtype=torch.float64) for n in TRN.train_var_names()}
+    fr, sl, al = TRN.forward(Wt, torch.tensor(mem, dtype=torch.float64), lens,
+                             torch.tensor(tg, dtype=torch.float64),
+                             torch.tensor(pm, dtype=torch.float64), None,
+                             zoneout=hp.tacotron_zoneout_rate)
+    mask = (np.arange(mem.shape[1])[None, :] < lens[:, None])
+    values = mem.astype(np.float64) * mask[:, :, None]
+    keys = values @ np.asarray(W[MEM_K], np.float64)
+    ohp = oracle_hp(hp)
+    f2, s2, a2 = TR.dynamic_decode(keys, values, lens, W, ohp, pm, tg.shape[1], targets=tg,
+                                   dt=np.float64)
+    np.testing.assert_allclose(fr.numpy(), f2, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(torch.sigmoid(sl).numpy(), s2, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(al.numpy(), a2, rtol=1e-10, atol=1e-10)
+
+
+def test_oracle_gradients_match_finite_differences():
+    hp = small_hparams()
+    W, mem, lens, tg, st, pm, zm = _case(hp, B=2, T_in=6, T_out=4)
+    _, _, g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, reg_weight=1e-3)
+    rng = np.random.default_rng(0)
+
+    def loss_of(W2, mem2):
+        Wt = {n: torch.tensor(np.asarray(W2[n]), dtype=torch.float64) for n in TRN.train_var_names()}
+        tg_t = torch.tensor(tg, dtype=torch.float64)
+        fr, sl, _ = TRN.forward(Wt, torch.tensor(mem2, dtype=torch.float64), lens, tg_t,
+                                torch.tensor(pm, dtype=torch.float64),
+                                torch.tensor(zm, dtype=torch.float64))
+        b, s, r = TRN.losses(fr, sl, tg_t, torch.tensor(st, dtype=torch.float64), Wt, 1e-3)
+        return float(b + s + r)
+
+    eps = 1e-6
+    for name in (MEM_K, TRN.L1 + "kernel", TRN.LA + "location_features_convolution/kernel",
+                 TRN.LA + "attention_variable_projection", TRN.FP + "bias"):
+        arr = np.asarray(W[name], np.float64)
+        for _ in range(3):
+            idx = tuple(rng.integers(0, s) for s in arr.shape)
+            Wp, Wm = dict(W), dict(W)
+            ap, am = arr.copy(), arr.copy()
+            ap[idx] += eps
+            am[idx] -= eps
+            Wp[name], Wm[name] = ap, am
+            fd = (loss_of(Wp, mem.astype(np.float64)) - loss_of(Wm, mem.astype(np.float64))) / (2 * eps)
+            assert abs(fd - g[name][idx]) < 1e-6 + 1e-5 * abs(fd), (name, idx, fd, g[name][idx])
+    # memory gradient is zero past each row's length (values = memory · mask)
+    for b in range(mem.shape[0]):
+        assert np.all(g["memory"][b, lens[b]:] == 0)
+
+
+def test_learning_rate_and_adam_formulas():
+    hp = small_hparams()
+    assert TRN.learning_rate(0, hp) == hp.tacotron_initial_learning_rate
+    lr = TRN.learning_rate(hp.tacotron_start_decay + hp.tacotron_decay_steps, hp)
+    assert abs(lr - max(hp.tacotron_initial_learning_rate * hp.tacotron_decay_rate,
+                        hp.tacotron_final_learning_rate)) < 1e-15
+    assert TRN.learning_rate(10 ** 7, hp) == hp.tacotron_final_learning_rate
+    p = {"w": np.array([1.0, -2.0])}
+    g = {"w": np.array([3.0, 4.0])}                     # global norm 5 -> clipped to 1
+    m = {"w": np.zeros(2)}
+    v = {"w": np.zeros(2)}
+    gn = TRN.clip_and_adam(p, g, m, v, 1, 1e-3)
+    assert gn == 5.0
+    # first Adam step moves each weight by ~lr·sign(g)
+    np.testing.assert_allclose(p["w"], [1.0 - 1e-3, -2.0 - 1e-3], rtol=0, atol=1e-7)
