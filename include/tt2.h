@@ -292,6 +292,68 @@ tt2_status tt2_gl_synthesize(tt2_gl_ctx* ctx, const float* spec, int T, int is_m
 tt2_status tt2_gl_synthesize_dev(tt2_gl_ctx* ctx, const float* spec_d, int T, int is_mel,
                                  int iters, float* wav_d, void* stream);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Teacher-forced decoder training step (BASELINE configs[4]): replaces    */
+/* Tacotron.initialize(is_training=True) + add_loss() + add_optimizer() (tacotron.py:31-35,      */
+/* 683-986, 1002-1251) for the decoder slice: TacoTrainingHelper dynamic_decode (helpers.py:      */
+/* 62-133) -> before-MSE + stop CE + L2 (tacotron.py:774,778-779,865-867) -> BPTT gradients ->   */
+/* clip_by_global_norm(1.0) + AdamOptimizer (tacotron.py:1029,1219-1221).                        */
+/* Trainable variables are the decoder's TF names (memory_layer, query_layer, location conv /    */
+/* layer, v_a, b_a, prenet, both LSTM cells, frame and stop projections).                        */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct tt2_train_config {
+  int batch;               /* rows per step on this device (configs[4]: 64) */
+  int max_T_in;            /* <= 384 (attention-kernel LDS budget) */
+  int max_T_out;           /* decoder steps (r = 1) */
+  int memory_dim;          /* D_mem (1024 fork default) */
+  int num_mels;            /* 80 */
+  int prenet_units;        /* 256 (both prenet layers) */
+  int decoder_lstm_units;  /* 1024 */
+  int attention_dim;       /* 128 (must divide 256) */
+  int attention_filters;   /* 32 (<= 32) */
+  int attention_kernel;    /* 31 */
+  float zoneout;           /* 0.1: used only when no zoneout masks are passed (inference mix) */
+  float reg_weight;        /* tacotron_reg_weight 1e-6 */
+  float adam_beta1, adam_beta2, adam_epsilon;  /* 0.9, 0.999, 1e-6 */
+  float clip_norm;         /* 1.0 (tacotron_clip_gradients); <= 0 disables */
+} tt2_train_config;
+
+typedef struct tt2_train_ctx tt2_train_ctx;
+
+void tt2_train_default_config(tt2_train_config* cfg, int batch, int max_T_in, int max_T_out);
+tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_train_ctx** out);
+void tt2_train_destroy(tt2_train_ctx* ctx);
+/* Same names/shapes as tt2_load_tensor; names outside the decoder slice are ignored. */
+tt2_status tt2_train_load_tensor(tt2_train_ctx* ctx, const char* tf_name, const float* host,
+                                 const int64_t* shape, int ndim);
+/* All slice variables loaded -> zero the Adam moments. */
+tt2_status tt2_train_finalize(tt2_train_ctx* ctx);
+/* Use a caller-owned device buffer (e.g. a torch tensor RCCL all-reduces) as the flat gradient
+ * buffer; NULL restores the internal one.  *n_out = its length in floats. */
+tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* ctx, float* grads_d, int64_t* n_out);
+/* Forward + losses + backward on DEVICE inputs: memory [B,T_in,D] (encoder outputs ⊕ style),
+ * lengths int32 [B], mel targets [B,T_out,80], stop targets [B,T_out], prenet keep bits u8
+ * [T_out,2,B,P], zoneout keep bits u8 [T_out,4,B,H] (c1,h1,c2,h2) or NULL (inference mix).
+ * Gradients (incl. L2) land in the flat gradient buffer; enqueued on `stream`. */
+tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* ctx, const float* memory_d,
+                                          const int32_t* lengths_d, const float* targets_d,
+                                          const float* stop_targets_d,
+                                          const uint8_t* prenet_masks_d,
+                                          const uint8_t* zoneout_masks_d, int T_in, int T_out,
+                                          void* stream);
+/* clip_by_global_norm + Adam with learning rate lr at update count global_step (>= 1). */
+tt2_status tt2_train_apply_dev(tt2_train_ctx* ctx, float lr, int global_step, void* stream);
+/* Synchronise; out4 = {before_loss, stop_loss, reg_loss, grad_global_norm (after apply)};
+ * fb_ms (nullable) = device time of the last forward_backward. */
+tt2_status tt2_train_losses(tt2_train_ctx* ctx, float* out4, float* fb_ms);
+/* which: 0 = parameter, 1 = gradient, 2 = Adam m, 3 = Adam v; name "memory" (which ignored) =
+ * d loss / d memory [B,T_in,D] of the last forward_backward. */
+tt2_status tt2_train_get_tensor(tt2_train_ctx* ctx, const char* tf_name, int which, float* host);
+/* Last forward's decoder frames [B,T,80], stop logits [B,T], alignments [B,T_in,T] (nullable). */
+tt2_status tt2_train_outputs(tt2_train_ctx* ctx, float* frames, float* stop_logits,
+                             float* alignments);
+
 #ifdef __cplusplus
 }
 #endif

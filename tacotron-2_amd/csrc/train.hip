@@ -1,0 +1,1075 @@
+// Teacher-forced Tacotron-2 decoder training step (BASELINE configs[4]).
+//
+// One call = TacoTrainingHelper(ratio 1) dynamic_decode forward (helpers.py:62-133,
+// Architecture_wrappers.py:197-267) with every activation kept resident in HBM, the losses of the
+// slice (before-MSE tacotron.py:774, stop sigmoid CE :778-779, L2 :865-867), backpropagation
+// through time, and (separately) clip_by_global_norm(1.0) + Adam (tacotron.py:1029,1219-1221).
+//
+// Layout (time-major, t = decoder step, b = row; one slot per step, slot T is the carry-out):
+//   X1[t]  [B, P + D + H]   LSTM-1 input  [prenet(target_{t-1}) | ctx_{t-1} | hz1_{t-1}]
+//   X2[t]  [B, 2H]          LSTM-2 input  [h1_new_t | hz2_{t-1}]
+//   PIN[t] [B, H + D]       projection input [h2_new_t | ctx_t]
+//   G*[t]  [B, 4H]          gate activations (σi, tanh j, σ(f+1), σo) after the forward
+//   ALIGN  [B, T_in, T]     alignments (row-major per utterance: the d_values GEMM reads it as A)
+// Every matrix product is the fp32 MFMA GEMM (gemm.hip): per-step products at M = B, the weight
+// gradients as one GEMM over all T·B rows after the loop (activations transposed once).  The
+// recurrences' elementwise parts (LSTM cells, location-sensitive attention, softmax, context) are
+// the kernels below.  Backward mirrors the forward slot layout: dX1[t], dX2[t] hold the gradients
+// of the step-t inputs, so a step's carry-ins are read from slot t+1.
+#include <cmath>
+#include <cstring>
+
+#include "common.h"
+#include "gemm.h"
+
+namespace tt2 {
+
+struct TrVar {
+  std::string name;
+  std::vector<int64_t> shape;
+  long off = 0, n = 0;
+  bool reg = false;
+};
+
+}  // namespace tt2
+
+using namespace tt2;
+
+struct tt2_train_ctx {
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  tt2_train_config cfg{};
+  int B = 0, Tm = 0, Tin = 0, D = 0, NM = 0, P = 0, H = 0, A = 0, F = 0, KW = 0;
+  int LX1 = 0;  // P + D + H
+  std::vector<TrVar> vars;
+  std::map<std::string, int> index;
+  long total = 0;
+  WeightMap host;
+  bool finalized = false;
+  long step_count = 0;
+  // flat parameter / gradient / Adam buffers
+  DevBuf params, grads_own, adam_m, adam_v;
+  float* grads = nullptr;  // grads_own or a caller-bound buffer
+  // transposed weights (refreshed every step)
+  DevBuf K1T, K2T, WqT, WfT, WsT, WmT, Wp2T;
+  // activations
+  DevBuf values, keys, X1, X2, PIN, G1, G2, C1, C2, CN1, CN2, Q, ALIGN, CUM, P1, XIN, FR, ST;
+  // backward
+  DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DH2, DCTX, DKEYS, DCUM;
+  DevBuf dV, dBA, dWL, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red;
+  int T_last = 0, Tin_last = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float last_ms = 0.f;
+};
+
+namespace tt2 {
+
+constexpr int TR_MAX_TIN = 384;  // LDS budget of the attention kernels
+constexpr int TR_JC = 32;        // j-chunk of the attention backward
+
+__device__ __forceinline__ float sigm_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// block (256 threads = 4 waves) reductions through a 4-float LDS scratch
+__device__ __forceinline__ float block_sum(float v, float* s4) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s4[w] = v;
+  __syncthreads();
+  return s4[0] + s4[1] + s4[2] + s4[3];
+}
+__device__ __forceinline__ float block_max(float v, float* s4) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s4[w] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3]));
+}
+
+// ---- generic helpers ---------------------------------------------------------------------
+// dst[c * ldd + r] = src[r * lds + c]  (32x32 LDS tiles)
+__global__ __launch_bounds__(256) void k_tr_transpose(const float* __restrict__ src, long rows, long cols, long lds,
+                                                      float* __restrict__ dst, long ldd) {
+  __shared__ float tile[32][33];
+  const long r0 = (long)blockIdx.y * 32, c0 = (long)blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
+  for (int i = ty; i < 32; i += 8) {
+    const long r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < rows && c < cols) ? src[r * lds + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const long c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows) dst[c * ldd + r] = tile[tx][i];
+  }
+}
+
+// partial column sums: part[s][n] = sum over rows m = s, s+S, ... of in[m*ld + n]
+__global__ __launch_bounds__(256) void k_tr_colsum_part(const float* __restrict__ in, long M, int N, long ld,
+                                                        float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const int S = gridDim.y, s = blockIdx.y;
+  float acc = 0.f;
+  if (n < N)
+    for (long m = (long)s * 4 + r; m < M; m += (long)S * 4) acc += in[m * ld + n];
+  red[r][c] = acc;
+  __syncthreads();
+  if (r == 0 && n < N) part[(long)s * N + n] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+__global__ void k_tr_colsum_final(const float* __restrict__ part, int S, int N, float* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (int s = 0; s < S; ++s) acc += part[(long)s * N + n];
+  out[n] = acc;
+}
+
+// ---- forward -------------------------------------------------------------------------------
+// XIN[t][b] = t == 0 ? GO (zeros, helpers.py:136-138) : targets[b][t-1]  (helpers.py:126-129)
+__global__ void k_tr_inputs(const float* __restrict__ tg, int B, int T, int NM, float* __restrict__ xin) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)T * B * NM;
+  if (i >= n) return;
+  const int c = (int)(i % NM);
+  const int b = (int)((i / NM) % B);
+  const int t = (int)(i / ((long)NM * B));
+  xin[i] = t == 0 ? 0.f : tg[((long)b * T + (t - 1)) * NM + c];
+}
+// values = memory · seq_mask (BahdanauAttention memory masking)
+__global__ void k_tr_values(const float* __restrict__ mem, const int* __restrict__ lens, int B, int Tin, int D,
+                            float* __restrict__ val) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * Tin * D) return;
+  const int j = (int)((i / D) % Tin), b = (int)(i / ((long)D * Tin));
+  val[i] = j < lens[b] ? mem[i] : 0.f;
+}
+// prenet dropout (modules.py:355, rate .5, always on): x = x / 0.5 · keep, in place on a strided
+// [T·B, P] view; masks [T][2][B][P]
+__global__ void k_tr_prenet_mask(float* __restrict__ x, long ld, const uint8_t* __restrict__ m, int layer, int T,
+                                 int B, int P) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)T * B * P) return;
+  const int p = (int)(i % P);
+  const long tb = i / P;
+  const int b = (int)(tb % B), t = (int)(tb / B);
+  const float keep = (float)m[(((long)t * 2 + layer) * B + b) * P + p];
+  x[tb * ld + p] = (x[tb * ld + p] / 0.5f) * keep;
+}
+
+// TF LSTMCell (modules.py:206) + training zoneout (modules.py:236-240) for one step.
+// G [B,4H] pre-activations (bias added) -> overwritten with (σi, tanh j, σ(f+1), σo).
+struct TrLstmFwd {
+  float* G;
+  const float* c_prev;   // [B,H]
+  const float* hz_prev;  // strided
+  long ld_hz_prev;
+  const uint8_t* zm;     // [T][4][B][H] or null (inference mix)
+  int t, layer, B, H;
+  float z;
+  float* cn;       // [B,H] c_new
+  float* c_out;    // [B,H] zoned c
+  float* h_out;    // strided h_new
+  long ld_h;
+  float* hz_out;   // strided zoned h
+  long ld_hz;
+};
+__global__ void k_tr_lstm_fwd(TrLstmFwd a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.B * a.H) return;
+  const int b = i / a.H, n = i % a.H;
+  float* g = a.G + (long)b * 4 * a.H;
+  const float si = sigm_acc(g[n]), tj = tanhf(g[a.H + n]), sf = sigm_acc(g[2 * a.H + n] + 1.0f),
+              so = sigm_acc(g[3 * a.H + n]);
+  g[n] = si;
+  g[a.H + n] = tj;
+  g[2 * a.H + n] = sf;
+  g[3 * a.H + n] = so;
+  const float cp = a.c_prev[i];
+  const float hp = a.hz_prev[(long)b * a.ld_hz_prev + n];
+  const float cnew = sf * cp + si * tj;
+  const float hnew = so * tanhf(cnew);
+  float c, h;
+  if (a.zm) {
+    const long base = (((long)a.t * 4 + 2 * a.layer) * a.B + b) * a.H + n;
+    const float mc = (float)a.zm[base], mh = (float)a.zm[base + (long)a.B * a.H];
+    c = cp + mc * (cnew - cp);
+    h = hp + mh * (hnew - hp);
+  } else {
+    c = (1.f - a.z) * cnew + a.z * cp;
+    h = (1.f - a.z) * hnew + a.z * hp;
+  }
+  a.cn[i] = cnew;
+  a.c_out[i] = c;
+  a.h_out[(long)b * a.ld_h + n] = hnew;
+  a.hz_out[(long)b * a.ld_hz + n] = h;
+}
+
+struct TrAtt {
+  int B, Tin, T, A, F, KW, D, H, P, t;
+  const int* lens;
+  const float* keys;    // [B,Tin,A]
+  const float* values;  // [B,Tin,D]
+  const float* Q;       // [T][B][A]
+  const float* Kc;      // [KW][F] location conv kernel
+  const float* bc;      // [F]
+  const float* Wl;      // [F][A]
+  const float* va;      // [A]
+  const float* ba;      // [A]
+  float* ALIGN;         // [B][Tin][T]
+  float* CUM;           // [(T+1)][B][Tin]
+  // forward outputs of the context
+  float* PIN;
+  float* X1;
+  // backward
+  const float* dPIN;
+  const float* dX1;
+  float* DCTX;   // [T][B][D]
+  float* DQ;     // [T][B][A]
+  float* DKEYS;  // [B][Tin][A]
+  float* DCUM;   // [B][Tin]
+  float* dV;     // [B][A]
+  float* dBA;    // [B][A]
+  float* dWL;    // [B][F][A]
+  float* dKC;    // [B][KW][F]
+  float* dBC;    // [B][F]
+};
+
+// location features f[j][c] = bc[c] + Σ_tap cum[j + tap - pad]·Kc[tap][c]  (attention.py:193-195)
+__device__ __forceinline__ void tr_loc_features(const TrAtt& a, const float* cum_pad, float* f) {
+  for (int i = threadIdx.x; i < a.Tin * a.F; i += blockDim.x) {
+    const int j = i / a.F, c = i % a.F;
+    float acc = a.bc[c];
+    for (int tap = 0; tap < a.KW; ++tap) acc += cum_pad[j + tap] * a.Kc[tap * a.F + c];
+    f[i] = acc;
+  }
+}
+
+// One block (256 threads) per row b: location-sensitive energies (attention.py:37-69), masked
+// softmax, cumulative alignments (:222-225).  Dynamic LDS: cum_pad, f, Wl, e.
+__global__ __launch_bounds__(256) void k_tr_att_fwd(TrAtt a) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x;
+  const int pad = (a.KW - 1) / 2;
+  float* cum_pad = lds;                          // Tin + KW
+  float* f = cum_pad + a.Tin + a.KW;             // Tin * F
+  float* Wl = f + a.Tin * a.F;                   // F * A
+  float* e = Wl + a.F * a.A;                     // Tin
+  float* s4 = e + a.Tin;                         // 4
+  const float* cum_prev = a.CUM + ((long)a.t * a.B + b) * a.Tin;
+  for (int i = threadIdx.x; i < a.Tin + a.KW; i += blockDim.x) {
+    const int j = i - pad;
+    cum_pad[i] = (j >= 0 && j < a.Tin) ? cum_prev[j] : 0.f;
+  }
+  for (int i = threadIdx.x; i < a.F * a.A; i += blockDim.x) Wl[i] = a.Wl[i];
+  __syncthreads();
+  tr_loc_features(a, cum_pad, f);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* q = a.Q + ((long)a.t * a.B + b) * a.A;
+  const int len = a.lens[b];
+  for (int j = wave; j < a.Tin; j += 4) {
+    float acc = 0.f;
+    for (int k = lane; k < a.A; k += 64) {
+      float u = a.keys[((long)b * a.Tin + j) * a.A + k] + q[k] + a.ba[k];
+      for (int c = 0; c < a.F; ++c) u += f[j * a.F + c] * Wl[c * a.A + k];
+      acc += a.va[k] * tanhf(u);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) e[j] = j < len ? acc : -INFINITY;
+  }
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) mx = fmaxf(mx, e[j]);
+  mx = block_max(mx, s4);
+  float sm = 0.f;
+  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) sm += j < len ? expf(e[j] - mx) : 0.f;
+  sm = block_sum(sm, s4);
+  float* cum_next = a.CUM + ((long)(a.t + 1) * a.B + b) * a.Tin;
+  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) {
+    const float al = j < len ? expf(e[j] - mx) / sm : 0.f;
+    a.ALIGN[((long)b * a.Tin + j) * a.T + a.t] = al;
+    cum_next[j] = cum_prev[j] + al;
+  }
+}
+
+// context_t = align_t · values  (attention.py:27) -> PIN[t][b][H:], X1[t+1][b][P:P+D]
+__global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
+  extern __shared__ float al[];
+  const int b = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) al[j] = a.ALIGN[((long)b * a.Tin + j) * a.T + a.t];
+  __syncthreads();
+  if (n >= a.D) return;
+  const float* v = a.values + (long)b * a.Tin * a.D + n;
+  float acc = 0.f;
+  for (int j = 0; j < a.Tin; ++j) acc += al[j] * v[(long)j * a.D];
+  a.PIN[((long)a.t * a.B + b) * (a.H + a.D) + a.H + n] = acc;
+  a.X1[((long)(a.t + 1) * a.B + b) * (a.P + a.D + a.H) + a.P + n] = acc;
+}
+
+// frame MSE + stop sigmoid CE (tacotron.py:774,778-779) and their output gradients.  Frames are
+// time-major [T][B][NM]; targets [B][T][NM].  Deterministic per-block partials.
+__global__ __launch_bounds__(256) void k_tr_loss(const float* __restrict__ FR, const float* __restrict__ ST,
+                                                 const float* __restrict__ tg, const float* __restrict__ stg, int B,
+                                                 int T, int NM, float* __restrict__ dFR, float* __restrict__ dST,
+                                                 float* __restrict__ part) {
+  __shared__ float s4[4];
+  const long nf = (long)T * B * NM;
+  const float inv_f = 1.0f / (float)nf, inv_s = 1.0f / (float)((long)T * B);
+  float sq = 0.f, ce = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % NM);
+    const int b = (int)((i / NM) % B);
+    const int t = (int)(i / ((long)NM * B));
+    const float d = FR[i] - tg[((long)b * T + t) * NM + c];
+    sq += d * d;
+    dFR[i] = 2.f * d * inv_f;
+  }
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < (long)T * B; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i % B), t = (int)(i / B);
+    const float x = ST[i], z = stg[(long)b * T + t];
+    ce += fmaxf(x, 0.f) - x * z + log1pf(expf(-fabsf(x)));
+    dST[i] = (sigm_acc(x) - z) * inv_s;
+  }
+  sq = block_sum(sq, s4);
+  ce = block_sum(ce, s4);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 2] = sq;
+    part[blockIdx.x * 2 + 1] = ce;
+  }
+}
+__global__ void k_tr_loss_final(const float* __restrict__ part, int nb, long nf, long ns, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double sq = 0, ce = 0;
+  for (int i = 0; i < nb; ++i) {
+    sq += part[2 * i];
+    ce += part[2 * i + 1];
+  }
+  out[0] = (float)(sq / (double)nf);
+  out[1] = (float)(ce / (double)ns);
+}
+
+// ---- backward ------------------------------------------------------------------------------
+struct TrLstmBwd {
+  const float* dh_ext;  // strided d h_new from the layer's consumers
+  long ld_dh;
+  const float* dhz;     // strided d(zoned h_t) from step t+1
+  long ld_dhz;
+  float* DC;            // [B,H] in: d(zoned c_t); out: d(zoned c_{t-1})
+  const float* G;       // [B,4H] activations
+  const float* cn;      // [B,H]
+  const float* c_prev;  // [B,H]
+  const uint8_t* zm;
+  int t, layer, B, H;
+  float z;
+  float* dG;            // [B,4H]
+  float* R;             // [B, ldr]: (1-kh)·dhz at column off_r + n
+  long ldr;
+  int off_r;
+};
+__global__ void k_tr_lstm_bwd(TrLstmBwd a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.B * a.H) return;
+  const int b = i / a.H, n = i % a.H;
+  const float* g = a.G + (long)b * 4 * a.H;
+  const float si = g[n], tj = g[a.H + n], sf = g[2 * a.H + n], so = g[3 * a.H + n];
+  float kc, kh;
+  if (a.zm) {
+    const long base = (((long)a.t * 4 + 2 * a.layer) * a.B + b) * a.H + n;
+    kc = (float)a.zm[base];
+    kh = (float)a.zm[base + (long)a.B * a.H];
+  } else {
+    kc = kh = 1.f - a.z;
+  }
+  const float dhz = a.dhz[(long)b * a.ld_dhz + n];
+  const float dcz = a.DC[i];
+  const float dhn = a.dh_ext[(long)b * a.ld_dh + n] + kh * dhz;
+  const float cnew = a.cn[i];
+  const float tc = tanhf(cnew);
+  const float dcn = kc * dcz + dhn * so * (1.f - tc * tc);
+  const float dso = dhn * tc, dsf = dcn * a.c_prev[i], dsi = dcn * tj, dtj = dcn * si;
+  float* dg = a.dG + (long)b * 4 * a.H;
+  dg[n] = dsi * si * (1.f - si);
+  dg[a.H + n] = dtj * (1.f - tj * tj);
+  dg[2 * a.H + n] = dsf * sf * (1.f - sf);
+  dg[3 * a.H + n] = dso * so * (1.f - so);
+  a.DC[i] = (1.f - kc) * dcz + dcn * sf;
+  a.R[(long)b * a.ldr + a.off_r + n] = (1.f - kh) * dhz;
+}
+
+// Attention backward for one step, one block per row b.  Recomputes the location features and
+// tanh terms from CUM[t] and Q[t] instead of storing [T,B,Tin,A] of them.
+__global__ __launch_bounds__(256) void k_tr_att_bwd(TrAtt a) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int pad = (a.KW - 1) / 2;
+  float* dctx = lds;                          // D
+  float* cum_pad = dctx + a.D;                // Tin + KW
+  float* al = cum_pad + a.Tin + a.KW;         // Tin
+  float* da = al + a.Tin;                     // Tin (d align -> d energy)
+  float* f = da + a.Tin;                      // Tin*F
+  float* df = f + a.Tin * a.F;                // Tin*F
+  float* Wl = df + a.Tin * a.F;               // F*A
+  float* dU = Wl + a.F * a.A;                 // JC*A
+  float* racc = dU + TR_JC * a.A;             // 3 * 256 (dv, dba, dq partials)
+  float* s4 = racc + 3 * 256;                 // 4
+  const long tb = (long)a.t * a.B + b;
+  const int len = a.lens[b];
+  for (int n = tid; n < a.D; n += blockDim.x) {
+    const float v = a.dPIN[tb * (a.H + a.D) + a.H + n] + a.dX1[(tb + a.B) * (a.P + a.D + a.H) + a.P + n];
+    dctx[n] = v;
+    a.DCTX[tb * a.D + n] = v;
+  }
+  const float* cum_prev = a.CUM + tb * a.Tin;
+  for (int i = tid; i < a.Tin + a.KW; i += blockDim.x) {
+    const int j = i - pad;
+    cum_pad[i] = (j >= 0 && j < a.Tin) ? cum_prev[j] : 0.f;
+  }
+  for (int j = tid; j < a.Tin; j += blockDim.x) al[j] = a.ALIGN[((long)b * a.Tin + j) * a.T + a.t];
+  for (int i = tid; i < a.F * a.A; i += blockDim.x) Wl[i] = a.Wl[i];
+  __syncthreads();
+  // d align_j = dctx · values_j + d cum_t[j]   (cum_t = cum_{t-1} + align_t)
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int j = wave; j < a.Tin; j += 4) {
+    const float* v = a.values + ((long)b * a.Tin + j) * a.D;
+    float acc = 0.f;
+    for (int n = lane; n < a.D; n += 64) acc += dctx[n] * v[n];
+    acc = wave_sum(acc);
+    if (lane == 0) da[j] = acc + a.DCUM[(long)b * a.Tin + j];
+  }
+  tr_loc_features(a, cum_pad, f);
+  __syncthreads();
+  // softmax backward: de_j = a_j (da_j - Σ a·da)
+  float s = 0.f;
+  for (int j = tid; j < a.Tin; j += blockDim.x) s += al[j] * da[j];
+  s = block_sum(s, s4);
+  for (int j = tid; j < a.Tin; j += blockDim.x) da[j] = j < len ? al[j] * (da[j] - s) : 0.f;
+  __syncthreads();
+  // energies backward over j-chunks
+  const int NJ = blockDim.x / a.A;  // A divides 256
+  const int k = tid % a.A, js = tid / a.A;
+  const float* q = a.Q + tb * a.A;
+  const float vak = a.va[k], qk = q[k], bak = a.ba[k];
+  float dv = 0.f, dba = 0.f, wl_acc[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) wl_acc[c] = 0.f;
+  for (int j0 = 0; j0 < a.Tin; j0 += TR_JC) {
+    const int jn = min(TR_JC, a.Tin - j0);
+    for (int jj = js; jj < jn; jj += NJ) {
+      const int j = j0 + jj;
+      const long kidx = ((long)b * a.Tin + j) * a.A + k;
+      float u = a.keys[kidx] + qk + bak;
+      for (int c = 0; c < a.F; ++c) u += f[j * a.F + c] * Wl[c * a.A + k];
+      const float th = tanhf(u);
+      const float de = da[j];
+      const float du = de * vak * (1.f - th * th);
+      dv += de * th;
+      dba += du;
+#pragma unroll
+      for (int c = 0; c < 32; ++c)
+        if (c < a.F) wl_acc[c] += f[j * a.F + c] * du;
+      a.DKEYS[kidx] += du;
+      dU[jj * a.A + k] = du;
+    }
+    __syncthreads();
+    for (int i = tid; i < jn * a.F; i += blockDim.x) {
+      const int jj = i / a.F, c = i % a.F;
+      float acc = 0.f;
+      for (int kk = 0; kk < a.A; ++kk) acc += dU[jj * a.A + kk] * Wl[c * a.A + kk];
+      df[(j0 + jj) * a.F + c] = acc;
+    }
+    __syncthreads();
+  }
+  // dq_k = Σ_j dU[j][k] = dba (same sum); combine the NJ sub-rows
+  racc[tid] = dv;
+  racc[256 + tid] = dba;
+  __syncthreads();
+  if (tid < a.A) {
+    float sv = 0.f, sb = 0.f;
+    for (int g = 0; g < NJ; ++g) {
+      sv += racc[g * a.A + tid];
+      sb += racc[256 + g * a.A + tid];
+    }
+    a.DQ[tb * a.A + tid] = sb;
+    a.dV[(long)b * a.A + tid] += sv;
+    a.dBA[(long)b * a.A + tid] += sb;
+  }
+  for (int g = 0; g < NJ; ++g) {
+    if (js == g)
+      for (int c = 0; c < a.F; ++c) a.dWL[((long)b * a.F + c) * a.A + k] += wl_acc[c];
+    __syncthreads();
+  }
+  // location conv backward: dKc, dbc, and d cum_{t-1} = d cum_t + convT(df)
+  for (int i = tid; i < a.KW * a.F; i += blockDim.x) {
+    const int tap = i / a.F, c = i % a.F;
+    float acc = 0.f;
+    for (int j = 0; j < a.Tin; ++j) acc += df[j * a.F + c] * cum_pad[j + tap];
+    a.dKC[(long)b * a.KW * a.F + i] += acc;
+  }
+  for (int c = tid; c < a.F; c += blockDim.x) {
+    float acc = 0.f;
+    for (int j = 0; j < a.Tin; ++j) acc += df[j * a.F + c];
+    a.dBC[(long)b * a.F + c] += acc;
+  }
+  for (int i = tid; i < a.Tin; i += blockDim.x) {
+    float acc = a.DCUM[(long)b * a.Tin + i];
+    for (int tap = 0; tap < a.KW; ++tap) {
+      const int j = i - tap + pad;
+      if (j < 0 || j >= a.Tin) continue;
+      for (int c = 0; c < a.F; ++c) acc += df[j * a.F + c] * a.Kc[tap * a.F + c];
+    }
+    a.DCUM[(long)b * a.Tin + i] = acc;  // each i owned by one thread; da already consumed it
+  }
+}
+
+// prenet backward through dropout + ReLU: dz = (p > 0) ? 2·dp : 0   (p = relu(z)/0.5·keep)
+__global__ void k_tr_prenet_bwd(const float* __restrict__ dp, long ld_dp, const float* __restrict__ p, long ld_p,
+                                long M, int N, float* __restrict__ dz) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * N) return;
+  const long m = i / N;
+  const int n = (int)(i % N);
+  dz[i] = p[m * ld_p + n] > 0.f ? 2.f * dp[m * ld_dp + n] : 0.f;
+}
+
+__global__ void k_tr_mask_rows(const float* __restrict__ x, const int* __restrict__ lens, int B, int Tin, int D,
+                               float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * Tin * D) return;
+  const int j = (int)((i / D) % Tin), b = (int)(i / ((long)D * Tin));
+  y[i] = j < lens[b] ? x[i] : 0.f;
+}
+
+// L2 regularisation (tacotron.py:865-867): g += reg·w over [off, off+n); partial Σ w²/2
+__global__ __launch_bounds__(256) void k_tr_reg(const float* __restrict__ w, float* __restrict__ g, long n, float reg,
+                                                float* __restrict__ part) {
+  __shared__ float s4[4];
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = w[i];
+    g[i] += reg * v;
+    acc += 0.5f * v * v;
+  }
+  acc = block_sum(acc, s4);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_tr_sumsq(const float* __restrict__ g, long n, float* __restrict__ part) {
+  __shared__ float s4[4];
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) acc += g[i] * g[i];
+  acc = block_sum(acc, s4);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+__global__ void k_tr_sum_final(const float* __restrict__ part, int nb, float scale, float* __restrict__ out, int sq) {
+  if (threadIdx.x != 0) return;
+  double s = 0;
+  for (int i = 0; i < nb; ++i) s += part[i];
+  out[0] = sq ? (float)sqrt(s) : (float)(s * scale);
+}
+
+// clip_by_global_norm(clip) + TF Adam (lr_t folded on the host)
+__global__ void k_tr_adam(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
+                          float* __restrict__ v, long n, const float* __restrict__ norm, float clip, float b1, float b2,
+                          float eps, float lr_t) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float scale = clip > 0.f ? clip / fmaxf(norm[0], clip) : 1.f;
+  const float gi = g[i] * scale;
+  const float mi = b1 * m[i] + (1.f - b1) * gi;
+  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  w[i] -= lr_t * mi / (sqrtf(vi) + eps);
+}
+
+// ---- host orchestration ----------------------------------------------------------------------
+static inline unsigned nblk(long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+static void tr_transpose(const float* src, long rows, long cols, long lds, float* dst, long ldd, hipStream_t s) {
+  dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));
+  hipLaunchKernelGGL(k_tr_transpose, grid, dim3(256), 0, s, src, rows, cols, lds, dst, ldd);
+}
+
+static void tr_colsum(tt2_train_ctx* c, const float* in, long M, int N, long ld, float* out, hipStream_t s) {
+  const int S = (int)std::min<long>(64, std::max<long>(1, M / 64));
+  hipLaunchKernelGGL(k_tr_colsum_part, dim3((N + 63) / 64, S), dim3(256), 0, s, in, M, N, ld, c->part.as<float>());
+  hipLaunchKernelGGL(k_tr_colsum_final, dim3((N + 255) / 256), dim3(256), 0, s, c->part.as<float>(), S, N, out);
+}
+
+static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
+                    hipStream_t s, const float* bias = nullptr, const float* residual = nullptr, long ldr = 0,
+                    int act = ACT_NONE) {
+  GemmArgs g;
+  g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.Bw = Bw; g.ldb = ldb; g.Cout = C; g.ldc = ldc;
+  g.bias = bias; g.residual = residual; g.ldr = ldr; g.act = act;
+  gemm(g, s);
+}
+
+static float* pvar(tt2_train_ctx* c, const std::string& n) { return c->params.as<float>() + c->vars[c->index.at(n)].off; }
+static float* gvar(tt2_train_ctx* c, const std::string& n) { return c->grads + c->vars[c->index.at(n)].off; }
+
+static const char* TP = "Tacotron_model/inference/";
+static std::string vn(const char* s) { return std::string(TP) + s; }
+#define LAV(x) vn("decoder/Location_Sensitive_Attention/" x)
+#define L1V(x) vn("decoder/decoder_LSTM/multi_rnn_cell/cell_0/lstm_cell/" x)
+#define L2V(x) vn("decoder/decoder_LSTM/multi_rnn_cell/cell_1/lstm_cell/" x)
+#define FPV(x) vn("decoder/linear_transform_projection/projection_linear_transform_projection/" x)
+#define SPV(x) vn("decoder/stop_token_projection/projection_stop_token_projection/" x)
+#define PRV(i, x) vn((std::string("decoder/decoder_prenet/dense_") + std::to_string(i) + "/" x).c_str())
+
+static void tr_build_vars(tt2_train_ctx* c) {
+  const int D = c->D, A = c->A, F = c->F, KW = c->KW, P = c->P, H = c->H, NM = c->NM;
+  auto add = [&](const std::string& n, std::vector<int64_t> sh, bool reg) {
+    TrVar v;
+    v.name = n;
+    v.shape = sh;
+    v.n = 1;
+    for (auto d : sh) v.n *= d;
+    v.off = c->total;
+    v.reg = reg;
+    c->total += (v.n + 63) / 64 * 64;  // 256-byte aligned segments
+    c->index[n] = (int)c->vars.size();
+    c->vars.push_back(v);
+  };
+  // order and regularisation mask: oracle/train_ref.py train_var_names() / regularized()
+  add(vn("memory_layer/kernel"), {D, A}, true);
+  add(vn("decoder/query_layer/kernel"), {H, A}, true);
+  add(LAV("location_features_convolution/kernel"), {KW, 1, F}, true);
+  add(LAV("location_features_convolution/bias"), {F}, false);
+  add(LAV("location_features_layer/kernel"), {F, A}, true);
+  add(LAV("attention_variable_projection"), {A}, false);
+  add(LAV("attention_bias"), {A}, false);
+  add(PRV(1, "kernel"), {NM, P}, true);
+  add(PRV(1, "bias"), {P}, false);
+  add(PRV(2, "kernel"), {P, P}, true);
+  add(PRV(2, "bias"), {P}, false);
+  add(L1V("kernel"), {P + D + H, 4 * H}, false);
+  add(L1V("bias"), {4 * H}, false);
+  add(L2V("kernel"), {2 * H, 4 * H}, false);
+  add(L2V("bias"), {4 * H}, false);
+  add(FPV("kernel"), {H + D, NM}, false);
+  add(FPV("bias"), {NM}, false);
+  add(SPV("kernel"), {H + D, 1}, false);
+  add(SPV("bias"), {1}, false);
+}
+
+static void tr_alloc(tt2_train_ctx* c) {
+  const long B = c->B, T = c->Tm, Tin = c->Tin, D = c->D, H = c->H, P = c->P, A = c->A, F = c->F, KW = c->KW,
+             NM = c->NM, LX1 = c->LX1;
+  const long TB = T * B;
+  auto f = [](DevBuf& d, long n) { d.alloc(sizeof(float) * (size_t)std::max<long>(n, 1)); };
+  f(c->params, c->total); f(c->grads_own, c->total); f(c->adam_m, c->total); f(c->adam_v, c->total);
+  c->grads = c->grads_own.as<float>();
+  f(c->K1T, 4 * H * LX1); f(c->K2T, 4 * H * 2 * H); f(c->WqT, A * H); f(c->WfT, NM * (H + D)); f(c->WsT, H + D);
+  f(c->WmT, A * D); f(c->Wp2T, P * P);
+  f(c->values, B * Tin * D); f(c->keys, B * Tin * A);
+  f(c->X1, (T + 1) * B * LX1); f(c->X2, (T + 1) * B * 2 * H); f(c->PIN, TB * (H + D));
+  f(c->G1, TB * 4 * H); f(c->G2, TB * 4 * H); f(c->C1, (T + 1) * B * H); f(c->C2, (T + 1) * B * H);
+  f(c->CN1, TB * H); f(c->CN2, TB * H); f(c->Q, TB * A); f(c->ALIGN, B * Tin * T); f(c->CUM, (T + 1) * B * Tin);
+  f(c->P1, TB * P); f(c->XIN, TB * NM); f(c->FR, TB * NM); f(c->ST, TB);
+  f(c->dFR, TB * NM); f(c->dST, TB); f(c->dPIN, TB * (H + D)); f(c->dX1, (T + 1) * B * LX1);
+  f(c->dX2, (T + 1) * B * 2 * H); f(c->dG1, TB * 4 * H); f(c->dG2, TB * 4 * H); f(c->DC1, B * H); f(c->DC2, B * H);
+  f(c->R1, B * LX1); f(c->R2, B * 2 * H); f(c->DQ, TB * A); f(c->DH2, B * H); f(c->DCTX, TB * D);
+  f(c->DKEYS, B * Tin * A); f(c->DCUM, B * Tin); f(c->dV, B * A); f(c->dBA, B * A); f(c->dWL, B * F * A);
+  f(c->dKC, B * KW * F); f(c->dBC, B * F); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
+  f(c->dZ, TB * P); f(c->dPre, TB * P);
+  const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM});
+  f(c->TBUF, tmax);
+  f(c->part, 64 * std::max<long>(4 * H, LX1) + 4096);
+  f(c->red, 64);
+}
+
+static size_t att_fwd_lds(const tt2_train_ctx* c, int Tin) {
+  return sizeof(float) * ((size_t)Tin + c->KW + (size_t)Tin * c->F + (size_t)c->F * c->A + Tin + 4);
+}
+static size_t att_bwd_lds(const tt2_train_ctx* c, int Tin) {
+  return sizeof(float) * ((size_t)c->D + Tin + c->KW + 2 * (size_t)Tin + 2 * (size_t)Tin * c->F +
+                          (size_t)c->F * c->A + (size_t)TR_JC * c->A + 3 * 256 + 4);
+}
+
+// forward + losses + backward for one batch; grads complete (incl. L2) on return (stream order)
+static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* lens, const float* tg, const float* stg,
+                                const uint8_t* pm, const uint8_t* zm, int Tin, int T, hipStream_t s) {
+  const int B = c->B, D = c->D, H = c->H, P = c->P, A = c->A, F = c->F, KW = c->KW, NM = c->NM, LX1 = c->LX1;
+  const long TB = (long)T * B;
+  const float z = c->cfg.zoneout;
+  c->T_last = T;
+  c->Tin_last = Tin;
+  // weight transposes for the backward products
+  tr_transpose(pvar(c, L1V("kernel")), LX1, 4 * H, 4 * H, c->K1T.as<float>(), LX1, s);
+  tr_transpose(pvar(c, L2V("kernel")), 2 * H, 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, s);
+  tr_transpose(pvar(c, vn("decoder/query_layer/kernel")), H, A, A, c->WqT.as<float>(), H, s);
+  tr_transpose(pvar(c, FPV("kernel")), H + D, NM, NM, c->WfT.as<float>(), H + D, s);
+  tr_transpose(pvar(c, SPV("kernel")), H + D, 1, 1, c->WsT.as<float>(), H + D, s);
+  tr_transpose(pvar(c, vn("memory_layer/kernel")), D, A, A, c->WmT.as<float>(), D, s);
+  tr_transpose(pvar(c, PRV(2, "kernel")), P, P, P, c->Wp2T.as<float>(), P, s);
+  TT2_HIP(hipMemsetAsync(c->grads, 0, sizeof(float) * c->total, s));
+
+  // ---- forward ----
+  float* X1 = c->X1.as<float>();
+  float* X2 = c->X2.as<float>();
+  float* PIN = c->PIN.as<float>();
+  TT2_HIP(hipMemsetAsync(X1, 0, sizeof(float) * (size_t)B * LX1, s));  // slot 0: ctx_{-1} = h_{-1} = 0
+  TT2_HIP(hipMemsetAsync(X2, 0, sizeof(float) * (size_t)B * 2 * H, s));
+  TT2_HIP(hipMemsetAsync(c->C1.p, 0, sizeof(float) * (size_t)B * H, s));
+  TT2_HIP(hipMemsetAsync(c->C2.p, 0, sizeof(float) * (size_t)B * H, s));
+  TT2_HIP(hipMemsetAsync(c->CUM.p, 0, sizeof(float) * (size_t)B * Tin, s));
+  hipLaunchKernelGGL(k_tr_inputs, dim3(nblk(TB * NM)), dim3(256), 0, s, tg, B, T, NM, c->XIN.as<float>());
+  hipLaunchKernelGGL(k_tr_values, dim3(nblk((long)B * Tin * D)), dim3(256), 0, s, mem, lens, B, Tin, D,
+                     c->values.as<float>());
+  tr_gemm(B * Tin, A, D, c->values.as<float>(), D, pvar(c, vn("memory_layer/kernel")), A, c->keys.as<float>(), A, s);
+  // prenet over all steps at once (teacher-forced inputs are known up front)
+  tr_gemm((int)TB, P, NM, c->XIN.as<float>(), NM, pvar(c, PRV(1, "kernel")), P, c->P1.as<float>(), P, s,
+          pvar(c, PRV(1, "bias")), nullptr, 0, ACT_RELU);
+  hipLaunchKernelGGL(k_tr_prenet_mask, dim3(nblk(TB * P)), dim3(256), 0, s, c->P1.as<float>(), (long)P, pm, 0, T, B, P);
+  tr_gemm((int)TB, P, P, c->P1.as<float>(), P, pvar(c, PRV(2, "kernel")), P, X1, LX1, s, pvar(c, PRV(2, "bias")),
+          nullptr, 0, ACT_RELU);
+  hipLaunchKernelGGL(k_tr_prenet_mask, dim3(nblk(TB * P)), dim3(256), 0, s, X1, (long)LX1, pm, 1, T, B, P);
+
+  TrAtt at{};
+  at.B = B; at.Tin = Tin; at.T = T; at.A = A; at.F = F; at.KW = KW; at.D = D; at.H = H; at.P = P;
+  at.lens = lens; at.keys = c->keys.as<float>(); at.values = c->values.as<float>(); at.Q = c->Q.as<float>();
+  at.Kc = pvar(c, LAV("location_features_convolution/kernel"));
+  at.bc = pvar(c, LAV("location_features_convolution/bias"));
+  at.Wl = pvar(c, LAV("location_features_layer/kernel"));
+  at.va = pvar(c, LAV("attention_variable_projection"));
+  at.ba = pvar(c, LAV("attention_bias"));
+  at.ALIGN = c->ALIGN.as<float>(); at.CUM = c->CUM.as<float>(); at.PIN = PIN; at.X1 = X1;
+  at.dPIN = c->dPIN.as<float>(); at.dX1 = c->dX1.as<float>(); at.DCTX = c->DCTX.as<float>(); at.DQ = c->DQ.as<float>();
+  at.DKEYS = c->DKEYS.as<float>(); at.DCUM = c->DCUM.as<float>(); at.dV = c->dV.as<float>(); at.dBA = c->dBA.as<float>();
+  at.dWL = c->dWL.as<float>(); at.dKC = c->dKC.as<float>(); at.dBC = c->dBC.as<float>();
+  const size_t lf = att_fwd_lds(c, Tin), lb = att_bwd_lds(c, Tin);
+  const unsigned bh = nblk((long)B * H);
+
+  for (int t = 0; t < T; ++t) {
+    const long s1 = (long)t * B;
+    tr_gemm(B, 4 * H, LX1, X1 + s1 * LX1, LX1, pvar(c, L1V("kernel")), 4 * H, c->G1.as<float>() + s1 * 4 * H, 4 * H, s,
+            pvar(c, L1V("bias")));
+    TrLstmFwd l1{c->G1.as<float>() + s1 * 4 * H, c->C1.as<float>() + s1 * H, X1 + s1 * LX1 + P + D, LX1, zm, t, 0, B, H,
+                 z, c->CN1.as<float>() + s1 * H, c->C1.as<float>() + (s1 + B) * H, X2 + s1 * 2 * H, 2 * H,
+                 X1 + (s1 + B) * LX1 + P + D, LX1};
+    hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l1);
+    tr_gemm(B, 4 * H, 2 * H, X2 + s1 * 2 * H, 2 * H, pvar(c, L2V("kernel")), 4 * H, c->G2.as<float>() + s1 * 4 * H,
+            4 * H, s, pvar(c, L2V("bias")));
+    TrLstmFwd l2{c->G2.as<float>() + s1 * 4 * H, c->C2.as<float>() + s1 * H, X2 + s1 * 2 * H + H, 2 * H, zm, t, 1, B,
+                 H, z, c->CN2.as<float>() + s1 * H, c->C2.as<float>() + (s1 + B) * H, PIN + s1 * (H + D), H + D,
+                 X2 + (s1 + B) * 2 * H + H, 2 * H};
+    hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l2);
+    tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
+            c->Q.as<float>() + s1 * A, A, s);
+    at.t = t;
+    hipLaunchKernelGGL(k_tr_att_fwd, dim3(B), dim3(256), lf, s, at);
+    hipLaunchKernelGGL(k_tr_ctx, dim3((D + 255) / 256, B), dim3(256), sizeof(float) * Tin, s, at);
+  }
+  tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
+  tr_gemm((int)TB, 1, H + D, PIN, H + D, pvar(c, SPV("kernel")), 1, c->ST.as<float>(), 1, s, pvar(c, SPV("bias")));
+  float* red = c->red.as<float>();
+  hipLaunchKernelGGL(k_tr_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->ST.as<float>(), tg, stg, B, T, NM,
+                     c->dFR.as<float>(), c->dST.as<float>(), c->part.as<float>());
+  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, TB * NM, TB, red);
+
+  // ---- backward ----
+  float* dPIN = c->dPIN.as<float>();
+  float* dX1 = c->dX1.as<float>();
+  float* dX2 = c->dX2.as<float>();
+  tr_gemm((int)TB, H + D, NM, c->dFR.as<float>(), NM, c->WfT.as<float>(), H + D, dPIN, H + D, s);
+  tr_gemm((int)TB, H + D, 1, c->dST.as<float>(), 1, c->WsT.as<float>(), H + D, dPIN, H + D, s, nullptr, dPIN, H + D);
+  TT2_HIP(hipMemsetAsync(dX1 + TB * LX1, 0, sizeof(float) * (size_t)B * LX1, s));
+  TT2_HIP(hipMemsetAsync(dX2 + TB * 2 * H, 0, sizeof(float) * (size_t)B * 2 * H, s));
+  for (DevBuf* d : {&c->DC1, &c->DC2, &c->R1, &c->R2, &c->DKEYS, &c->DCUM, &c->dV, &c->dBA, &c->dWL, &c->dKC, &c->dBC})
+    TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+  for (int t = T - 1; t >= 0; --t) {
+    const long s1 = (long)t * B;
+    at.t = t;
+    hipLaunchKernelGGL(k_tr_att_bwd, dim3(B), dim3(256), lb, s, at);
+    tr_gemm(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, c->DH2.as<float>(), H, s, nullptr,
+            dPIN + s1 * (H + D), H + D);
+    TrLstmBwd b2{c->DH2.as<float>(), H, dX2 + (s1 + B) * 2 * H + H, 2 * H, c->DC2.as<float>(),
+                 c->G2.as<float>() + s1 * 4 * H, c->CN2.as<float>() + s1 * H, c->C2.as<float>() + s1 * H, zm, t, 1, B,
+                 H, z, c->dG2.as<float>() + s1 * 4 * H, c->R2.as<float>(), 2 * H, H};
+    hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b2);
+    tr_gemm(B, 2 * H, 4 * H, c->dG2.as<float>() + s1 * 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, dX2 + s1 * 2 * H,
+            2 * H, s, nullptr, c->R2.as<float>(), 2 * H);
+    TrLstmBwd b1{dX2 + s1 * 2 * H, 2 * H, dX1 + (s1 + B) * LX1 + P + D, LX1, c->DC1.as<float>(),
+                 c->G1.as<float>() + s1 * 4 * H, c->CN1.as<float>() + s1 * H, c->C1.as<float>() + s1 * H, zm, t, 0, B,
+                 H, z, c->dG1.as<float>() + s1 * 4 * H, c->R1.as<float>(), LX1, P + D};
+    hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b1);
+    tr_gemm(B, LX1, 4 * H, c->dG1.as<float>() + s1 * 4 * H, 4 * H, c->K1T.as<float>(), LX1, dX1 + s1 * LX1, LX1, s,
+            nullptr, c->R1.as<float>(), LX1);
+  }
+
+  // ---- weight gradients over all T·B rows ----
+  float* TBUF = c->TBUF.as<float>();
+  const int TBi = (int)TB;
+  tr_transpose(X1, TB, LX1, LX1, TBUF, TB, s);
+  tr_gemm(LX1, 4 * H, TBi, TBUF, TB, c->dG1.as<float>(), 4 * H, gvar(c, L1V("kernel")), 4 * H, s);
+  tr_colsum(c, c->dG1.as<float>(), TB, 4 * H, 4 * H, gvar(c, L1V("bias")), s);
+  tr_transpose(X2, TB, 2 * H, 2 * H, TBUF, TB, s);
+  tr_gemm(2 * H, 4 * H, TBi, TBUF, TB, c->dG2.as<float>(), 4 * H, gvar(c, L2V("kernel")), 4 * H, s);
+  tr_colsum(c, c->dG2.as<float>(), TB, 4 * H, 4 * H, gvar(c, L2V("bias")), s);
+  tr_transpose(PIN, TB, H + D, H + D, TBUF, TB, s);
+  tr_gemm(H, A, TBi, TBUF, TB, c->DQ.as<float>(), A, gvar(c, vn("decoder/query_layer/kernel")), A, s);
+  tr_gemm(H + D, NM, TBi, TBUF, TB, c->dFR.as<float>(), NM, gvar(c, FPV("kernel")), NM, s);
+  tr_gemm(H + D, 1, TBi, TBUF, TB, c->dST.as<float>(), 1, gvar(c, SPV("kernel")), 1, s);
+  tr_colsum(c, c->dFR.as<float>(), TB, NM, NM, gvar(c, FPV("bias")), s);
+  tr_colsum(c, c->dST.as<float>(), TB, 1, 1, gvar(c, SPV("bias")), s);
+  // prenet
+  hipLaunchKernelGGL(k_tr_prenet_bwd, dim3(nblk(TB * P)), dim3(256), 0, s, dX1, (long)LX1, X1, (long)LX1, TB, P,
+                     c->dZ.as<float>());
+  tr_transpose(c->P1.as<float>(), TB, P, P, TBUF, TB, s);
+  tr_gemm(P, P, TBi, TBUF, TB, c->dZ.as<float>(), P, gvar(c, PRV(2, "kernel")), P, s);
+  tr_colsum(c, c->dZ.as<float>(), TB, P, P, gvar(c, PRV(2, "bias")), s);
+  tr_gemm(TBi, P, P, c->dZ.as<float>(), P, c->Wp2T.as<float>(), P, c->dPre.as<float>(), P, s);
+  hipLaunchKernelGGL(k_tr_prenet_bwd, dim3(nblk(TB * P)), dim3(256), 0, s, c->dPre.as<float>(), (long)P,
+                     c->P1.as<float>(), (long)P, TB, P, c->dZ.as<float>());
+  tr_transpose(c->XIN.as<float>(), TB, NM, NM, TBUF, TB, s);
+  tr_gemm(NM, P, TBi, TBUF, TB, c->dZ.as<float>(), P, gvar(c, PRV(1, "kernel")), P, s);
+  tr_colsum(c, c->dZ.as<float>(), TB, P, P, gvar(c, PRV(1, "bias")), s);
+  // attention parameters: sums of the per-row partials
+  tr_colsum(c, c->dV.as<float>(), B, A, A, gvar(c, LAV("attention_variable_projection")), s);
+  tr_colsum(c, c->dBA.as<float>(), B, A, A, gvar(c, LAV("attention_bias")), s);
+  tr_colsum(c, c->dWL.as<float>(), B, F * A, (long)F * A, gvar(c, LAV("location_features_layer/kernel")), s);
+  tr_colsum(c, c->dKC.as<float>(), B, KW * F, (long)KW * F, gvar(c, LAV("location_features_convolution/kernel")), s);
+  tr_colsum(c, c->dBC.as<float>(), B, F, F, gvar(c, LAV("location_features_convolution/bias")), s);
+  // memory: d values = Σ_t align_t^T · dctx_t (+ keys path), memory_layer kernel
+  for (int b = 0; b < B; ++b)
+    tr_gemm(Tin, D, T, c->ALIGN.as<float>() + (long)b * Tin * T, T, c->DCTX.as<float>() + (long)b * D, (long)B * D,
+            c->DVAL.as<float>() + (long)b * Tin * D, D, s);
+  tr_transpose(c->values.as<float>(), (long)B * Tin, D, D, TBUF, (long)B * Tin, s);
+  tr_gemm(D, A, B * Tin, TBUF, (long)B * Tin, c->DKEYS.as<float>(), A, gvar(c, vn("memory_layer/kernel")), A, s);
+  tr_gemm(B * Tin, D, A, c->DKEYS.as<float>(), A, c->WmT.as<float>(), D, c->DVAL.as<float>(), D, s, nullptr,
+          c->DVAL.as<float>(), D);
+  hipLaunchKernelGGL(k_tr_mask_rows, dim3(nblk((long)B * Tin * D)), dim3(256), 0, s, c->DVAL.as<float>(), lens, B, Tin,
+                     D, c->DMEM.as<float>());
+  // L2 regularisation of the regularised kernels
+  int nreg = 0;
+  for (const auto& v : c->vars) {
+    if (!v.reg) continue;
+    hipLaunchKernelGGL(k_tr_reg, dim3(64), dim3(256), 0, s, c->params.as<float>() + v.off, c->grads + v.off, v.n,
+                       c->cfg.reg_weight, c->part.as<float>() + 64 * nreg);
+    ++nreg;
+  }
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 64 * nreg, c->cfg.reg_weight,
+                     red + 2, 0);
+}
+
+static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s) {
+  float* red = c->red.as<float>();
+  hipLaunchKernelGGL(k_tr_sumsq, dim3(256), dim3(256), 0, s, c->grads, c->total, c->part.as<float>());
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, 1.f, red + 3, 1);
+  const double b1 = c->cfg.adam_beta1, b2 = c->cfg.adam_beta2;
+  const int t = std::max(1, global_step);
+  const float lr_t = (float)(lr * std::sqrt(1.0 - std::pow(b2, t)) / (1.0 - std::pow(b1, t)));
+  hipLaunchKernelGGL(k_tr_adam, dim3(nblk(c->total)), dim3(256), 0, s, c->params.as<float>(), c->grads,
+                     c->adam_m.as<float>(), c->adam_v.as<float>(), c->total, red + 3, c->cfg.clip_norm,
+                     c->cfg.adam_beta1, c->cfg.adam_beta2, c->cfg.adam_epsilon, lr_t);
+}
+
+}  // namespace tt2
+
+// ---- C ABI -------------------------------------------------------------------------------------
+extern "C" {
+
+void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int max_T_out) {
+  std::memset(c, 0, sizeof(*c));
+  c->batch = batch;
+  c->max_T_in = max_T_in;
+  c->max_T_out = max_T_out;
+  c->memory_dim = 1024;
+  c->num_mels = 80;
+  c->prenet_units = 256;
+  c->decoder_lstm_units = 1024;
+  c->attention_dim = 128;
+  c->attention_filters = 32;
+  c->attention_kernel = 31;
+  c->zoneout = 0.1f;
+  c->reg_weight = 1e-6f;
+  c->adam_beta1 = 0.9f;
+  c->adam_beta2 = 0.999f;
+  c->adam_epsilon = 1e-6f;
+  c->clip_norm = 1.0f;
+}
+
+tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_train_ctx** out) {
+  return guard([&] {
+    TT2_CHECK(cfg && out, TT2_ERR_INVALID_ARG, "tt2_train_create: null argument");
+    *out = nullptr;
+    TT2_CHECK(cfg->batch >= 1 && cfg->max_T_in >= 1 && cfg->max_T_out >= 1, TT2_ERR_INVALID_ARG, "bad capacity");
+    TT2_CHECK(cfg->max_T_in <= TR_MAX_TIN, TT2_ERR_INVALID_ARG, "max_T_in exceeds the attention kernels' LDS budget");
+    TT2_CHECK(cfg->attention_dim >= 1 && cfg->attention_dim <= 256 && 256 % cfg->attention_dim == 0,
+              TT2_ERR_INVALID_ARG, "attention_dim must divide 256");
+    TT2_CHECK(cfg->attention_filters >= 1 && cfg->attention_filters <= 32, TT2_ERR_INVALID_ARG,
+              "attention_filters must be <= 32");
+    int n = 0;
+    TT2_HIP(hipGetDeviceCount(&n));
+    TT2_CHECK(hip_device >= 0 && hip_device < n, TT2_ERR_HIP, "no such HIP device");
+    TT2_HIP(hipSetDevice(hip_device));
+    auto* c = new tt2_train_ctx();
+    try {
+      c->dev = hip_device;
+      c->cfg = *cfg;
+      c->B = cfg->batch; c->Tm = cfg->max_T_out; c->Tin = cfg->max_T_in; c->D = cfg->memory_dim;
+      c->NM = cfg->num_mels; c->P = cfg->prenet_units; c->H = cfg->decoder_lstm_units; c->A = cfg->attention_dim;
+      c->F = cfg->attention_filters; c->KW = cfg->attention_kernel; c->LX1 = c->P + c->D + c->H;
+      TT2_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      TT2_HIP(hipEventCreate(&c->ev0));
+      TT2_HIP(hipEventCreate(&c->ev1));
+      tr_build_vars(c);
+      tr_alloc(c);
+      const size_t lb = att_bwd_lds(c, c->Tin);
+      TT2_CHECK(lb <= 160 * 1024, TT2_ERR_INVALID_ARG, "attention backward LDS exceeds 160 KiB");
+      TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tr_att_bwd),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
+      TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tr_att_fwd),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)att_fwd_lds(c, c->Tin)));
+    } catch (...) {
+      delete c;
+      throw;
+    }
+    *out = c;
+  });
+}
+
+void tt2_train_destroy(tt2_train_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->dev);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+tt2_status tt2_train_load_tensor(tt2_train_ctx* c, const char* name, const float* host, const int64_t* shape, int ndim) {
+  return guard([&] {
+    TT2_CHECK(c && name && host && (shape || ndim == 0), TT2_ERR_INVALID_ARG, "tt2_train_load_tensor: null argument");
+    auto it = c->index.find(name);
+    if (it == c->index.end()) return;  // not a decoder-slice variable: ignored (full checkpoints load as-is)
+    const TrVar& v = c->vars[it->second];
+    long n = 1;
+    for (int i = 0; i < ndim; ++i) n *= shape[i];
+    TT2_CHECK(n == v.n, TT2_ERR_SHAPE_MISMATCH, std::string("shape mismatch for ") + name);
+    TT2_HIP(hipSetDevice(c->dev));
+    TT2_HIP(hipMemcpy(c->params.as<float>() + v.off, host, sizeof(float) * n, hipMemcpyHostToDevice));
+    c->host[name].shape.assign(shape, shape + ndim);
+  });
+}
+
+tt2_status tt2_train_finalize(tt2_train_ctx* c) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    for (const auto& v : c->vars)
+      TT2_CHECK(c->host.count(v.name), TT2_ERR_NOT_LOADED, "missing variable " + v.name);
+    TT2_HIP(hipSetDevice(c->dev));
+    TT2_HIP(hipMemset(c->adam_m.p, 0, c->adam_m.bytes));
+    TT2_HIP(hipMemset(c->adam_v.p, 0, c->adam_v.bytes));
+    c->finalized = true;
+  });
+}
+
+tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* c, float* grads_d, int64_t* n_out) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    if (n_out) *n_out = c->total;
+    c->grads = grads_d ? grads_d : c->grads_own.as<float>();
+  });
+}
+
+tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* c, const float* memory_d, const int32_t* lengths_d,
+                                          const float* targets_d, const float* stop_targets_d,
+                                          const uint8_t* prenet_masks_d, const uint8_t* zoneout_masks_d, int T_in,
+                                          int T_out, void* stream) {
+  return guard([&] {
+    TT2_CHECK(c && memory_d && lengths_d && targets_d && stop_targets_d && prenet_masks_d, TT2_ERR_INVALID_ARG,
+              "tt2_train_forward_backward_dev: null argument");
+    TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_train_finalize not called");
+    TT2_CHECK(T_in >= 1 && T_in <= c->Tin && T_out >= 1 && T_out <= c->Tm, TT2_ERR_SHAPE_MISMATCH,
+              "T_in/T_out exceed capacity");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    TT2_HIP(hipEventRecord(c->ev0, s));
+    tr_forward_backward(c, memory_d, lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d, T_in, T_out,
+                        s);
+    TT2_HIP(hipEventRecord(c->ev1, s));
+    TT2_HIP(hipGetLastError());
+  });
+}
+
+tt2_status tt2_train_apply_dev(tt2_train_ctx* c, float lr, int global_step, void* stream) {
+  return guard([&] {
+    TT2_CHECK(c && c->finalized, TT2_ERR_NOT_LOADED, "tt2_train_apply_dev: not finalized");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    tr_apply(c, lr, global_step, s);
+    TT2_HIP(hipGetLastError());
+  });
+}
+
+tt2_status tt2_train_losses(tt2_train_ctx* c, float* out4, float* fb_ms) {
+  return guard([&] {
+    TT2_CHECK(c && out4, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_HIP(hipSetDevice(c->dev));
+    TT2_HIP(hipDeviceSynchronize());
+    TT2_HIP(hipMemcpy(out4, c->red.p, sizeof(float) * 4, hipMemcpyDeviceToHost));
+    if (fb_ms) TT2_HIP(hipEventElapsedTime(fb_ms, c->ev0, c->ev1));
+  });
+}
+
+tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, float* host) {
+  return guard([&] {
+    TT2_CHECK(c && name && host, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_HIP(hipSetDevice(c->dev));
+    TT2_HIP(hipDeviceSynchronize());
+    if (std::string(name) == "memory") {  // d loss / d memory of the last forward_backward
+      TT2_HIP(hipMemcpy(host, c->DMEM.p, sizeof(float) * (size_t)c->B * c->Tin_last * c->D, hipMemcpyDeviceToHost));
+      return;
+    }
+    auto it = c->index.find(name);
+    TT2_CHECK(it != c->index.end(), TT2_ERR_INVALID_ARG, std::string("unknown variable ") + name);
+    const TrVar& v = c->vars[it->second];
+    const float* base = which == 0 ? c->params.as<float>() : which == 1 ? c->grads
+                      : which == 2 ? c->adam_m.as<float>() : c->adam_v.as<float>();
+    TT2_CHECK(which >= 0 && which <= 3, TT2_ERR_INVALID_ARG, "which must be 0..3");
+    TT2_HIP(hipMemcpy(host, base + v.off, sizeof(float) * v.n, hipMemcpyDeviceToHost));
+  });
+}
+
+tt2_status tt2_train_outputs(tt2_train_ctx* c, float* frames, float* stop_logits, float* alignments) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    TT2_HIP(hipSetDevice(c->dev));
+    TT2_HIP(hipDeviceSynchronize());
+    const int B = c->B, T = c->T_last, NM = c->NM, Tin = c->Tin_last;
+    // device layouts are time-major [T][B][..]; the ABI returns [B][T][..] like tower_decoder_output
+    if (frames) {
+      std::vector<float> tmp((size_t)T * B * NM);
+      TT2_HIP(hipMemcpy(tmp.data(), c->FR.p, sizeof(float) * tmp.size(), hipMemcpyDeviceToHost));
+      for (int t = 0; t < T; ++t)
+        for (int b = 0; b < B; ++b)
+          std::memcpy(frames + ((size_t)b * T + t) * NM, tmp.data() + ((size_t)t * B + b) * NM, sizeof(float) * NM);
+    }
+    if (stop_logits) {
+      std::vector<float> tmp((size_t)T * B);
+      TT2_HIP(hipMemcpy(tmp.data(), c->ST.p, sizeof(float) * tmp.size(), hipMemcpyDeviceToHost));
+      for (int t = 0; t < T; ++t)
+        for (int b = 0; b < B; ++b) stop_logits[(size_t)b * T + t] = tmp[(size_t)t * B + b];
+    }
+    if (alignments)  // [B][Tin][T] already
+      TT2_HIP(hipMemcpy(alignments, c->ALIGN.p, sizeof(float) * (size_t)B * Tin * T, hipMemcpyDeviceToHost));
+  });
+}
+
+}  // extern "C"

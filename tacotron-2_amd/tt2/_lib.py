@@ -67,6 +67,15 @@ class GlConfig(ctypes.Structure):
                                     "griffin_lim_iters")]
 
 
+class TrainConfig(ctypes.Structure):
+    """tt2_train_config (include/tt2.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "batch", "max_T_in", "max_T_out", "memory_dim", "num_mels", "prenet_units",
+        "decoder_lstm_units", "attention_dim", "attention_filters", "attention_kernel")] + [
+        (n, ctypes.c_float) for n in ("zoneout", "reg_weight", "adam_beta1", "adam_beta2",
+                                      "adam_epsilon", "clip_norm")]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _U64 = ctypes.c_uint64
@@ -109,6 +118,17 @@ SIGNATURES = {
     "tt2_gl_synthesize": (_I, [_P, _P, _I, _I, _I, _P]),
     "tt2_gl_synthesize_dev": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "tt2_mol_sample": (_I, [_P, _P, _P, _I, _I, _F, _P, _P]),
+    "tt2_train_default_config": (None, [ctypes.POINTER(TrainConfig), _I, _I, _I]),
+    "tt2_train_create": (_I, [ctypes.POINTER(TrainConfig), _I, ctypes.POINTER(_P)]),
+    "tt2_train_destroy": (None, [_P]),
+    "tt2_train_load_tensor": (_I, [_P, ctypes.c_char_p, _P, _P, _I]),
+    "tt2_train_finalize": (_I, [_P]),
+    "tt2_train_bind_grads_dev": (_I, [_P, _P, ctypes.POINTER(ctypes.c_int64)]),
+    "tt2_train_forward_backward_dev": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "tt2_train_apply_dev": (_I, [_P, _F, _I, _P]),
+    "tt2_train_losses": (_I, [_P, _P, _P]),
+    "tt2_train_get_tensor": (_I, [_P, ctypes.c_char_p, _I, _P]),
+    "tt2_train_outputs": (_I, [_P, _P, _P, _P]),
 }
 
 _lib = None

@@ -1,0 +1,193 @@
+"""Teacher-forced Tacotron-2 decoder training step on libtt2 (SURVEY.md §8f rank 1, configs[4]).
+
+``TacotronTrainer`` mirrors what the reference's training graph does per step for the decoder
+slice — ``Tacotron.initialize(is_training=True)`` with TacoTrainingHelper, ``add_loss()`` and
+``add_optimizer()`` (tacotron/models/tacotron.py:31-35, 683-986, 1002-1251), driven by
+``tacotron/train.py``'s ``sess.run([step, loss, optimize])`` — on the C ABI's training context
+(csrc/train.hip).  Data-parallel training keeps one process per GPU; the reference's CPU tower
+mean of the gradients (tacotron.py:1194-1208) becomes one RCCL all-reduce of the flat gradient
+buffer between backward and the clipped Adam update.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+from .weights import memory_width
+
+
+def learning_rate(step, hp):
+    """Tacotron._learning_rate_decay (tacotron.py:1227-1251): exponential decay from
+    tacotron_start_decay every tacotron_decay_steps by tacotron_decay_rate, clipped to
+    [tacotron_final_learning_rate, tacotron_initial_learning_rate]."""
+    init = hp.tacotron_initial_learning_rate
+    if not hp.tacotron_decay_learning_rate:
+        return init
+    lr = init * hp.tacotron_decay_rate ** ((step - hp.tacotron_start_decay) / hp.tacotron_decay_steps)
+    return min(max(lr, hp.tacotron_final_learning_rate), init)
+
+
+def train_config(hp, batch, max_T_in, max_T_out, emt_only=False):
+    lib = _lib.load_library()
+    cfg = _lib.TrainConfig()
+    lib.tt2_train_default_config(ctypes.byref(cfg), batch, max_T_in, max_T_out)
+    if len(hp.prenet_layers) != 2 or hp.prenet_layers[0] != hp.prenet_layers[1]:
+        raise NotImplementedError("prenet_layers must be two equal widths on this build")
+    if hp.decoder_layers != 2 or hp.outputs_per_step != 1:
+        raise NotImplementedError("decoder_layers = 2 and outputs_per_step = 1 on this build")
+    if hp.tacotron_teacher_forcing_mode != "constant" or hp.tacotron_teacher_forcing_ratio != 1.0:
+        raise NotImplementedError("only constant teacher forcing with ratio 1 is built "
+                                  "(hparams.py:300-301 defaults)")
+    if hp.mask_decoder or hp.predict_linear or hp.cross_entropy_pos_weight != 1:
+        raise NotImplementedError("mask_decoder / predict_linear / pos_weight != 1 are not built")
+    cfg.memory_dim = memory_width(hp, emt_only)
+    cfg.num_mels = hp.num_mels
+    cfg.prenet_units = hp.prenet_layers[0]
+    cfg.decoder_lstm_units = hp.decoder_lstm_units
+    cfg.attention_dim = hp.attention_dim
+    cfg.attention_filters = hp.attention_filters
+    cfg.attention_kernel = hp.attention_kernel[0]
+    cfg.zoneout = hp.tacotron_zoneout_rate
+    reg = hp.tacotron_reg_weight
+    if hp.tacotron_scale_regularization:                      # tacotron.py:857-861
+        reg *= 1.0 / (2 * hp.max_abs_value) if hp.symmetric_mels else 1.0 / hp.max_abs_value
+    cfg.reg_weight = reg
+    cfg.adam_beta1 = hp.tacotron_adam_beta1
+    cfg.adam_beta2 = hp.tacotron_adam_beta2
+    cfg.adam_epsilon = hp.tacotron_adam_epsilon
+    cfg.clip_norm = 1.0 if hp.tacotron_clip_gradients else 0.0
+    return cfg
+
+
+class TacotronTrainer(object):
+    """One tt2_train_ctx on one GPU.  Inputs may be numpy arrays or torch tensors; everything
+    runs on the trainer's own torch stream (passed to the library explicitly)."""
+
+    def __init__(self, hp, weights, batch, max_T_in, max_T_out, device=0, emt_only=False):
+        import torch
+        self.torch = torch
+        self.lib = _lib.load_library()
+        self.hp = hp
+        self.device = torch.device("cuda", device)
+        self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only)
+        self.B = batch
+        h = ctypes.c_void_p()
+        check(self.lib.tt2_train_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
+        self.h = h
+        for name, arr in weights.items():
+            if name.startswith("Tacotron_model/"):
+                _lib.load_tensor(self.lib.tt2_train_load_tensor, self.h, name, arr)
+        check(self.lib.tt2_train_finalize(self.h))
+        self.stream = torch.cuda.Stream(device=self.device)
+        n = ctypes.c_int64()
+        check(self.lib.tt2_train_bind_grads_dev(self.h, None, ctypes.byref(n)))
+        self.n_params = n.value
+        self.grad_buf = None
+        self.global_step = 0
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tt2_train_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def bind_grad_buffer(self):
+        """Flat gradient buffer as a torch tensor (for RCCL all-reduce); returned view."""
+        if self.grad_buf is None:
+            self.grad_buf = self.torch.zeros(self.n_params, dtype=self.torch.float32,
+                                             device=self.device)
+            check(self.lib.tt2_train_bind_grads_dev(self.h, ctypes.c_void_p(self.grad_buf.data_ptr()),
+                                                    None))
+        return self.grad_buf
+
+    def _dev(self, a, dtype):
+        t = self.torch
+        if a is None:
+            return None
+        if isinstance(a, t.Tensor):
+            return a.to(self.device, dtype).contiguous()
+        return t.from_numpy(np.ascontiguousarray(a)).to(self.device, dtype, non_blocking=False)
+
+    def forward_backward(self, memory, lengths, targets, stop_targets, prenet_masks,
+                         zoneout_masks=None):
+        """Teacher-forced forward + losses + backward; gradients land in the flat buffer."""
+        t = self.torch
+        with t.cuda.stream(self.stream):
+            mem = self._dev(memory, t.float32)
+            lens = self._dev(lengths, t.int32)
+            tg = self._dev(targets, t.float32)
+            st = self._dev(stop_targets, t.float32)
+            pm = self._dev(prenet_masks, t.uint8)
+            zm = self._dev(zoneout_masks, t.uint8)
+            B, T_in, _ = mem.shape
+            T_out = tg.shape[1]
+            if B != self.B:
+                raise ValueError("batch {} != trainer batch {}".format(B, self.B))
+            if tuple(pm.shape) != (T_out, 2, B, self.cfg.prenet_units):
+                raise ValueError("prenet_masks must be [T_out, 2, B, prenet_units]")
+            if zm is not None and tuple(zm.shape) != (T_out, 4, B, self.cfg.decoder_lstm_units):
+                raise ValueError("zoneout_masks must be [T_out, 4, B, decoder_lstm_units]")
+            self._keep = (mem, lens, tg, st, pm, zm)      # alive until the stream has used them
+            ptr = (lambda x: None if x is None else ctypes.c_void_p(x.data_ptr()))
+            check(self.lib.tt2_train_forward_backward_dev(
+                self.h, ptr(mem), ptr(lens), ptr(tg), ptr(st), ptr(pm), ptr(zm), T_in, T_out,
+                ctypes.c_void_p(self.stream.cuda_stream)))
+
+    def allreduce_grads(self, group=None):
+        """Tower mean (tacotron.py:1194-1208) as one all-reduce over the flat gradient buffer."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        buf = self.bind_grad_buffer()
+        with self.torch.cuda.stream(self.stream):
+            dist.all_reduce(buf, group=group)
+            buf.div_(dist.get_world_size(group))
+
+    def apply(self, global_step=None, lr=None):
+        """clip_by_global_norm(1.0) + Adam at update count ``global_step`` (1-based)."""
+        if global_step is None:
+            global_step = self.global_step + 1
+        self.global_step = global_step
+        if lr is None:
+            lr = learning_rate(global_step, self.hp)
+        check(self.lib.tt2_train_apply_dev(self.h, float(lr), int(global_step),
+                                           ctypes.c_void_p(self.stream.cuda_stream)))
+        return lr
+
+    def step(self, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks=None):
+        """One training step (forward, backward, DP all-reduce when initialised, clipped Adam);
+        returns the losses dict."""
+        self.forward_backward(memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks)
+        self.allreduce_grads()
+        self.apply()
+        return self.losses()
+
+    def losses(self):
+        out = np.zeros(4, np.float32)
+        ms = ctypes.c_float()
+        check(self.lib.tt2_train_losses(self.h, out.ctypes.data_as(ctypes.c_void_p),
+                                        ctypes.byref(ms)))
+        return dict(before=float(out[0]), stop_token=float(out[1]), regularization=float(out[2]),
+                    loss=float(out[0] + out[1] + out[2]), grad_norm=float(out[3]),
+                    forward_backward_ms=float(ms.value))
+
+    def get(self, name, which=0, shape=None):
+        """which: 0 param, 1 gradient, 2 Adam m, 3 Adam v; name 'memory' = d loss / d memory."""
+        if shape is None:
+            raise ValueError("shape required")
+        out = np.zeros(shape, np.float32)
+        check(self.lib.tt2_train_get_tensor(self.h, name.encode(), which,
+                                            out.ctypes.data_as(ctypes.c_void_p)))
+        return out
+
+    def outputs(self, T_in, T_out):
+        fr = np.zeros((self.B, T_out, self.cfg.num_mels), np.float32)
+        st = np.zeros((self.B, T_out), np.float32)
+        al = np.zeros((self.B, T_in, T_out), np.float32)
+        check(self.lib.tt2_train_outputs(self.h, fr.ctypes.data_as(ctypes.c_void_p),
+                                         st.ctypes.data_as(ctypes.c_void_p),
+                                         al.ctypes.data_as(ctypes.c_void_p)))
+        return fr, st, al

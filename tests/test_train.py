@@ -96,3 +96,99 @@ def test_learning_rate_and_adam_formulas():
     assert gn == 5.0
     # first Adam step moves each weight by ~lr·sign(g)
     np.testing.assert_allclose(p["w"], [1.0 - 1e-3, -2.0 - 1e-3], rtol=0, atol=1e-7)
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU parity (C ABI) against the float64 oracle
+# ---------------------------------------------------------------------------------------------
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _gpu_vs_oracle(hp, B, T_in, T_out, use_zoneout_masks=True, seed=11):
+    from tt2.train import TacotronTrainer
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out, seed)
+    if not use_zoneout_masks:
+        zm = None
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0)
+    try:
+        tr.forward_backward(mem, lens, tg, st, pm, zm)
+        L = tr.losses()
+        fr, sl, al = tr.outputs(T_in, T_out)
+        grads = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in TRN.train_var_names()}
+        gmem = tr.get("memory", 1, mem.shape)
+    finally:
+        tr.close()
+    out, (b, s, r), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight)
+    return (fr, sl, al, L, grads, gmem), (out, (b, s, r), g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zoneout_masks", [True, False])
+def test_gpu_train_forward_backward_small(zoneout_masks):
+    """Small widths, ragged lengths: outputs 1e-4 (north_star's mel tolerance), losses 1e-5
+    relative, every gradient within 1e-4 of the float64 oracle relative to its max."""
+    hp = small_hparams()
+    (fr, sl, al, L, grads, gmem), (out, (b, s, r), g) = _gpu_vs_oracle(hp, 3, 9, 12, zoneout_masks)
+    assert np.abs(fr - out["frames"]).max() < 1e-4
+    assert np.abs(sl - out["stop_logits"]).max() < 1e-4
+    assert np.abs(al - out["alignments"]).max() < 1e-5
+    assert abs(L["before"] - b) < 1e-5 * abs(b) + 1e-7
+    assert abs(L["stop_token"] - s) < 1e-5 * abs(s) + 1e-7
+    assert abs(L["regularization"] - r) < 1e-4 * abs(r) + 1e-9
+    for n in TRN.train_var_names():
+        assert _rel(grads[n], g[n]) < 1e-4, (n, _rel(grads[n], g[n]))
+    assert _rel(gmem, g["memory"]) < 1e-4
+    for bb in range(3):
+        assert np.all(gmem[bb, _case(hp, 3, 9, 12)[2][bb]:] == 0)
+
+
+@pytest.mark.gpu
+def test_gpu_train_forward_backward_full_widths():
+    """Fork-default widths (D_mem 1024, LSTM 1024, attention 128/32/31, prenet 256) on a short
+    ragged batch: the production kernel shapes (A = 128 → 2 sub-rows per attention block)."""
+    hp = small_hparams()
+    hp.override_from_dict(dict(attention_dim=128, attention_filters=32, prenet_layers=[256, 256],
+                               decoder_lstm_units=1024, embedding_dim=512, enc_conv_channels=512,
+                               encoder_lstm_units=256, style_embed_depth=256, style_att_dim=128,
+                               reference_filters=[32, 32, 64, 64, 128, 128], reference_depth=128))
+    (fr, sl, al, L, grads, gmem), (out, (b, s, r), g) = _gpu_vs_oracle(hp, 4, 37, 10)
+    assert np.abs(fr - out["frames"]).max() < 1e-4
+    assert np.abs(al - out["alignments"]).max() < 1e-5
+    assert abs(L["before"] - b) < 1e-5 * abs(b)
+    for n in TRN.train_var_names():
+        assert _rel(grads[n], g[n]) < 2e-4, (n, _rel(grads[n], g[n]))
+    assert _rel(gmem, g["memory"]) < 2e-4
+
+
+@pytest.mark.gpu
+def test_gpu_train_adam_updates_match_oracle():
+    """Two steps of clip_by_global_norm + Adam against oracle/train_ref.clip_and_adam."""
+    from tt2.train import TacotronTrainer, learning_rate
+    hp = small_hparams()
+    B, T_in, T_out = 2, 8, 6
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
+    names = TRN.train_var_names()
+    p = {n: np.asarray(W[n], np.float64) for n in names}
+    m = {n: np.zeros_like(p[n]) for n in names}
+    v = {n: np.zeros_like(p[n]) for n in names}
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0)
+    try:
+        for step in (1, 2):
+            tr.forward_backward(mem, lens, tg, st, pm, zm)
+            lr = tr.apply(step)
+            L = tr.losses()
+            Wcur = dict(W)
+            Wcur.update(p)
+            _, _, g = TRN.train_grads(Wcur, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight)
+            g.pop("memory")
+            gn = TRN.clip_and_adam(p, g, m, v, step, learning_rate(step, hp))
+            assert abs(L["grad_norm"] - gn) < 1e-4 * gn
+            assert lr == learning_rate(step, hp)
+            for n in names:
+                got = tr.get(n, 0, p[n].shape)
+                assert np.abs(got - p[n]).max() < 1e-6 + 1e-5 * np.abs(p[n]).max(), n
+    finally:
+        tr.close()
