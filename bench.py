@@ -46,6 +46,11 @@ def parse():
     p.add_argument("--e2e-frames", type=int, default=1000,
                    help="decoder frames per utterance of the end-to-end leg (configs[3])")
     p.add_argument("--no-griffin-lim", action="store_true")
+    p.add_argument("--no-train", action="store_true")
+    p.add_argument("--train-batch", type=int, default=64)
+    p.add_argument("--train-t-in", type=int, default=150)
+    p.add_argument("--train-t-out", type=int, default=800)
+    p.add_argument("--train-steps", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=100)
     p.add_argument("--profile-iters", type=int, default=50)
@@ -169,6 +174,77 @@ def bench_griffin_lim(local, frames=1000):
                 unit="audio-samples/s", ms_per_utterance=round(ms, 3), frames=frames, samples=L,
                 iters=hp.griffin_lim_iters, n_fft=n, win=hp.win_size, hop=hp.hop_size,
                 algorithmic_gb_per_s=round(it_bytes * hp.griffin_lim_iters / (ms * 1e-3) / 1e9, 1))
+
+
+def train_step_flops(B, T_in, T, hp, D):
+    """Algorithmic FLOPs of one teacher-forced decoder training step (forward + backward): the
+    matrix products (per step-row: LSTM-1 [P+D+H]x4H, LSTM-2 2Hx4H, query HxA, projections
+    (H+D)x81; prenet once over all rows; keys once per batch) counted 3x (forward, input
+    gradient, weight gradient) plus the attention's location/energy/context terms (2x)."""
+    H, A, F, KW, P, NM = (hp.decoder_lstm_units, hp.attention_dim, hp.attention_filters,
+                          hp.attention_kernel[0], hp.prenet_layers[0], hp.num_mels)
+    row = 2 * ((P + D + H) * 4 * H + 2 * H * 4 * H + H * A + (H + D) * (NM + 1) + NM * P + P * P)
+    att = 2 * T_in * (F * KW + F * A + 2 * A + D)
+    return B * T * (3 * row + 2 * att) + 3 * 2 * B * T_in * D * A
+
+
+def bench_train(a, rank, world, local, barrier, max_over_ranks):
+    """configs[4]: teacher-forced decoder training step (fork-default widths, D_mem 1024) at
+    B = 64 rows per GPU, T_in = 150, T_out = 800 (LJSpeech-shaped); data-parallel over ranks with
+    one RCCL all-reduce of the flat gradient buffer; K timed steps of forward + backward +
+    all-reduce + clipped Adam, max over ranks."""
+    import torch
+    from tt2.hparams import hparams
+    from tt2.synthetic import prenet_masks, train_batch, zoneout_masks
+    from tt2.train import TacotronTrainer
+    from tt2.weights import init_tacotron_weights, memory_width
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    B, Ti, T = a.train_batch, a.train_t_in, a.train_t_out
+    D = memory_width(hp)
+    W = init_tacotron_weights(hp, seed=hp.tacotron_random_seed)
+    tr = TacotronTrainer(hp, W, B, Ti, T, local)
+    if world > 1:
+        tr.bind_grad_buffer()
+    dev = torch.device("cuda", local)
+    mem, lens, tg, st = train_batch(B, Ti, T, D, seed=1234 + rank)
+    batch = [torch.from_numpy(x).to(dev) for x in (mem, lens, tg, st)]
+    batch.append(torch.from_numpy(prenet_masks(T, B, hp.prenet_layers[0], seed=7 + rank)).to(dev))
+    batch.append(torch.from_numpy(zoneout_masks(T, B, hp.decoder_lstm_units, seed=7 + rank)).to(dev))
+    losses = []
+
+    def step():
+        tr.forward_backward(*batch)
+        tr.allreduce_grads()
+        tr.apply()
+
+    step()
+    losses.append(tr.losses())
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.train_steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    L = tr.losses()
+    tr.close()
+    ms = 1e3 * el / a.train_steps
+    fl = train_step_flops(B, Ti, T, hp, D)
+    tf = fl / (ms * 1e-3) / 1e12
+    return dict(metric="mel-frames/sec (teacher-forced training step)",
+                value=round(world * B * T / (ms * 1e-3), 1), unit="mel-frames/s",
+                ms_per_step=round(ms, 2), steps=a.train_steps, warmup=1,
+                forward_backward_ms=round(L["forward_backward_ms"], 2),
+                loss_first=round(losses[0]["loss"], 5), loss_last=round(L["loss"], 5),
+                grad_norm=round(L["grad_norm"], 5), dtype="f32",
+                config=dict(workload="configs[4]: Tacotron-2 decoder training step (teacher-forced), "
+                                     "B={} rows/GPU, T_in={}, T_out={}, D_mem={}".format(B, Ti, T, D),
+                            global_batch=B * world, parallelism="dp{} (RCCL grad all-reduce)".format(world)),
+                roofline=dict(bound="mfma", achieved=round(tf, 2), peak=157.3, unit="TFLOP/s",
+                              frac=round(tf / 157.3, 4), algorithmic_flops_per_step=int(fl),
+                              note="fp32 MFMA peak (v_mfma_f32_32x32x2_f32); whole-step average"))
 
 
 E2E_TEXT = ("Scientists at the CERN laboratory say they have discovered a new particle. "
@@ -422,6 +498,11 @@ def main():
     if not a.no_griffin_lim:
         glr = bench_griffin_lim(local)
 
+    # --- teacher-forced decoder training step (configs[4]) ---
+    trn = None
+    if not a.no_train:
+        trn = bench_train(a, rank, world, local, barrier, max_over_ranks)
+
     # --- CPU baseline (rank 0, N = 1 only) ---
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -452,7 +533,7 @@ def main():
                                decoded_steps=n_steps.value, ref_frames=a.ref_frames,
                                parallelism="utterance-batch sharding x{}".format(world)),
                    phases=phases, roofline=roofline, cpu_baseline=cpu, wavenet=wn, e2e=e2e,
-                   griffin_lim=glr,
+                   griffin_lim=glr, train=trn,
                    diag_stamps=stamps)
         print(json.dumps(out))
     eng.close()

@@ -304,7 +304,7 @@ tt2_status tt2_gl_synthesize_dev(tt2_gl_ctx* ctx, const float* spec_d, int T, in
 
 typedef struct tt2_train_config {
   int batch;               /* rows per step on this device (configs[4]: 64) */
-  int max_T_in;            /* <= 384 (attention-kernel LDS budget) */
+  int max_T_in;            /* <= 320 (attention-kernel LDS budget) */
   int max_T_out;           /* decoder steps (r = 1) */
   int memory_dim;          /* D_mem (1024 fork default) */
   int num_mels;            /* 80 */

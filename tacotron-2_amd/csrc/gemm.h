@@ -36,6 +36,12 @@ struct GemmArgs {
   // fp32 accumulation (the dropped lo·lo term is ~2^-22 relative; fp16 products are exact in
   // fp32) -- 3/16 of the fp32 MFMA cost, ~1e-7 relative error.  Needs |A| < 4e3, |B| < 64.
   int split16 = 0;
+  // split-K for skinny products (fp32 path): when kpart != nullptr the dispatcher may split K over
+  // blockIdx.z so a 64-row GEMM fills the chip; raw partials go to kpart (>= kpart_floats floats,
+  // caller-owned, stream-ordered) and one reduce launch applies the epilogue.
+  float* kpart = nullptr;
+  long kpart_floats = 0;
+  int ksplit = 1;  // set by the dispatcher
 };
 
 void gemm(const GemmArgs& a, hipStream_t s);

@@ -8,6 +8,8 @@
 // current one is multiplied.
 #include "gemm.h"
 
+#include <algorithm>
+
 namespace tt2 {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -139,13 +141,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     for (int e = 0; e < EB; ++e) Bs[buf][bk][bn + e] = rb[e];
   };
 
-  const int nk = (g.K + BK - 1) / BK;
-  gload(0);
+  // split-K: this block covers k tiles [kt0, kt1) (g.K clipped so the loaders zero-fill past it)
+  const int nkt = (g.K + BK - 1) / BK;
+  const int per = (nkt + g.ksplit - 1) / g.ksplit;
+  const int kt0 = blockIdx.z * per, kt1 = min(nkt, kt0 + per);
+  if (g.ksplit > 1) g.K = min(g.K, kt1 * BK);
+  const int nk = kt1 - kt0;
+  if (nk > 0) {
+  gload(kt0 * BK);
   sstore(0);
   __syncthreads();
+  }
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+    if (kt + 1 < nk) gload((kt0 + kt + 1) * BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       float a[WMB], b[WNB];
@@ -163,11 +172,44 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
 
+  if (g.ksplit > 1) {  // raw partial tile -> kpart[z][M][N]
+    float* P = g.kpart + (long)blockIdx.z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < WMB; ++i)
+#pragma unroll
+      for (int j = 0; j < WNB; ++j) {
+        const int col = n0 + wn * 32 * WNB + j * 32 + (lane & 31);
+        if (col >= g.N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * 32 * WMB + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < g.M) P[(long)row * g.N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < WMB; ++i)
 #pragma unroll
     for (int j = 0; j < WNB; ++j)
       epilogue_tile(g, acc[i][j], m0 + wm * 32 * WMB + i * 32, n0 + wn * 32 * WNB + j * 32, lane);
+}
+
+// split-K combine: C = epilogue(sum_z kpart[z]) (same epilogue as epilogue_tile)
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)g.M * g.N) return;
+  const int row = (int)(i / g.N), col = (int)(i % g.N);
+  float y = 0.f;
+  for (int z = 0; z < g.ksplit; ++z) y += g.kpart[(long)z * g.M * g.N + i];
+  if (g.bias) y += g.bias[col];
+  if (g.act == ACT_RELU) y = fmaxf(y, 0.f);
+  else if (g.act == ACT_TANH) y = tanhf(y);
+  if (g.bn_scale) y = y * g.bn_scale[col] + g.bn_shift[col];
+  if (g.act == ACT_BN_RELU) y = fmaxf(y, 0.f);
+  if (g.residual) y = g.residual[(long)row * g.ldr + col] + y;
+  if (g.clip) y = fminf(fmaxf(y, g.clip_lo), g.clip_hi);
+  g.Cout[(long)row * g.ldc + col] = y;
 }
 
 
@@ -277,7 +319,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
 
 template <int WMB, int WNB>
 static void launch(const GemmArgs& a, bool va, bool vb, hipStream_t s) {
-  dim3 grid(cdiv(a.N, 64 * WNB), cdiv(a.M, 64 * WMB));
+  dim3 grid(cdiv(a.N, 64 * WNB), cdiv(a.M, 64 * WMB), a.ksplit);
   if (va && vb) hipLaunchKernelGGL((gemm_kernel<WMB, WNB, true, true>), grid, dim3(256), 0, s, a);
   else if (va) hipLaunchKernelGGL((gemm_kernel<WMB, WNB, true, false>), grid, dim3(256), 0, s, a);
   else if (vb) hipLaunchKernelGGL((gemm_kernel<WMB, WNB, false, true>), grid, dim3(256), 0, s, a);
@@ -304,10 +346,24 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   const int wnb = a.N <= 64 ? 1 : 2;
   const long tiles22 = (long)cdiv(a.M, 128) * cdiv(a.N, 64 * wnb);
   const int wmb = tiles22 >= 512 ? 2 : 1;
-  if (wmb == 2 && wnb == 2) launch<2, 2>(a, va, vb, s);
-  else if (wmb == 2) launch<2, 1>(a, va, vb, s);
-  else if (wnb == 2) launch<1, 2>(a, va, vb, s);
-  else launch<1, 1>(a, va, vb, s);
+  GemmArgs g = a;
+  g.ksplit = 1;
+  if (a.kpart) {  // split K until ~256 work-groups, >= 8 k tiles (128 k) per split
+    const long tiles = (long)cdiv(a.M, 64 * wmb) * cdiv(a.N, 64 * wnb);
+    const int nkt = cdiv(a.K, 16);
+    int ks = (int)std::min<long>(256 / std::max<long>(tiles, 1), nkt / 8);
+    ks = std::max(1, std::min(ks, 32));
+    while (ks > 1 && (long)ks * a.M * a.N > a.kpart_floats) --ks;
+    g.ksplit = ks;
+  }
+  if (wmb == 2 && wnb == 2) launch<2, 2>(g, va, vb, s);
+  else if (wmb == 2) launch<2, 1>(g, va, vb, s);
+  else if (wnb == 2) launch<1, 2>(g, va, vb, s);
+  else launch<1, 1>(g, va, vb, s);
+  if (g.ksplit > 1) {
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256)), dim3(256), 0, s, g);
+    TT2_HIP(hipGetLastError());
+  }
 }
 
 }  // namespace tt2

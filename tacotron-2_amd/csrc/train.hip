@@ -56,7 +56,7 @@ struct tt2_train_ctx {
   DevBuf values, keys, X1, X2, PIN, G1, G2, C1, C2, CN1, CN2, Q, ALIGN, CUM, P1, XIN, FR, ST;
   // backward
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DH2, DCTX, DKEYS, DCUM;
-  DevBuf dV, dBA, dWL, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red;
+  DevBuf dV, dBA, dWL, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
   int T_last = 0, Tin_last = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
@@ -64,8 +64,9 @@ struct tt2_train_ctx {
 
 namespace tt2 {
 
-constexpr int TR_MAX_TIN = 384;  // LDS budget of the attention kernels
+constexpr int TR_MAX_TIN = 320;  // LDS budget of the attention kernels
 constexpr int TR_JC = 32;        // j-chunk of the attention backward
+constexpr int TR_AT = 1024;      // threads per attention block (one block per utterance row)
 
 __device__ __forceinline__ float sigm_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
 
@@ -79,22 +80,26 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
-// block (256 threads = 4 waves) reductions through a 4-float LDS scratch
-__device__ __forceinline__ float block_sum(float v, float* s4) {
+// block reductions (any multiple of 64 threads, <= 1024) through a 16-float LDS scratch
+__device__ __forceinline__ float block_sum(float v, float* s16) {
   v = wave_sum(v);
-  const int w = threadIdx.x >> 6;
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) s4[w] = v;
+  if ((threadIdx.x & 63) == 0) s16[w] = v;
   __syncthreads();
-  return s4[0] + s4[1] + s4[2] + s4[3];
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += s16[i];
+  return r;
 }
-__device__ __forceinline__ float block_max(float v, float* s4) {
+__device__ __forceinline__ float block_max(float v, float* s16) {
   v = wave_max(v);
-  const int w = threadIdx.x >> 6;
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) s4[w] = v;
+  if ((threadIdx.x & 63) == 0) s16[w] = v;
   __syncthreads();
-  return fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3]));
+  float r = -INFINITY;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, s16[i]);
+  return r;
 }
 
 // ---- generic helpers ---------------------------------------------------------------------
@@ -259,7 +264,7 @@ __device__ __forceinline__ void tr_loc_features(const TrAtt& a, const float* cum
 
 // One block (256 threads) per row b: location-sensitive energies (attention.py:37-69), masked
 // softmax, cumulative alignments (:222-225).  Dynamic LDS: cum_pad, f, Wl, e.
-__global__ __launch_bounds__(256) void k_tr_att_fwd(TrAtt a) {
+__global__ __launch_bounds__(TR_AT) void k_tr_att_fwd(TrAtt a) {
   extern __shared__ float lds[];
   const int b = blockIdx.x;
   const int pad = (a.KW - 1) / 2;
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(256) void k_tr_att_fwd(TrAtt a) {
   float* f = cum_pad + a.Tin + a.KW;             // Tin * F
   float* Wl = f + a.Tin * a.F;                   // F * A
   float* e = Wl + a.F * a.A;                     // Tin
-  float* s4 = e + a.Tin;                         // 4
+  float* s4 = e + a.Tin;                         // 16
   const float* cum_prev = a.CUM + ((long)a.t * a.B + b) * a.Tin;
   for (int i = threadIdx.x; i < a.Tin + a.KW; i += blockDim.x) {
     const int j = i - pad;
@@ -277,10 +282,10 @@ __global__ __launch_bounds__(256) void k_tr_att_fwd(TrAtt a) {
   __syncthreads();
   tr_loc_features(a, cum_pad, f);
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const float* q = a.Q + ((long)a.t * a.B + b) * a.A;
   const int len = a.lens[b];
-  for (int j = wave; j < a.Tin; j += 4) {
+  for (int j = wave; j < a.Tin; j += nw) {
     float acc = 0.f;
     for (int k = lane; k < a.A; k += 64) {
       float u = a.keys[((long)b * a.Tin + j) * a.A + k] + q[k] + a.ba[k];
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(256) void k_tr_loss(const float* __restrict__ FR, c
                                                  const float* __restrict__ tg, const float* __restrict__ stg, int B,
                                                  int T, int NM, float* __restrict__ dFR, float* __restrict__ dST,
                                                  float* __restrict__ part) {
-  __shared__ float s4[4];
+  __shared__ float s4[16];
   const long nf = (long)T * B * NM;
   const float inv_f = 1.0f / (float)nf, inv_s = 1.0f / (float)((long)T * B);
   float sq = 0.f, ce = 0.f;
@@ -411,7 +416,7 @@ __global__ void k_tr_lstm_bwd(TrLstmBwd a) {
 
 // Attention backward for one step, one block per row b.  Recomputes the location features and
 // tanh terms from CUM[t] and Q[t] instead of storing [T,B,Tin,A] of them.
-__global__ __launch_bounds__(256) void k_tr_att_bwd(TrAtt a) {
+__global__ __launch_bounds__(TR_AT) void k_tr_att_bwd(TrAtt a) {
   extern __shared__ float lds[];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int pad = (a.KW - 1) / 2;
@@ -422,9 +427,10 @@ __global__ __launch_bounds__(256) void k_tr_att_bwd(TrAtt a) {
   float* f = da + a.Tin;                      // Tin*F
   float* df = f + a.Tin * a.F;                // Tin*F
   float* Wl = df + a.Tin * a.F;               // F*A
-  float* dU = Wl + a.F * a.A;                 // JC*A
-  float* racc = dU + TR_JC * a.A;             // 3 * 256 (dv, dba, dq partials)
-  float* s4 = racc + 3 * 256;                 // 4
+  float* WlT = Wl + a.F * a.A;                // A*F (transposed copy: conflict-free d f reads)
+  float* dU = WlT + a.F * a.A;                // JC*A
+  float* racc = dU + TR_JC * a.A;             // 2 * TR_AT (dv, dba partials)
+  float* s4 = racc + 2 * TR_AT;               // 16
   const long tb = (long)a.t * a.B + b;
   const int len = a.lens[b];
   for (int n = tid; n < a.D; n += blockDim.x) {
@@ -438,11 +444,15 @@ __global__ __launch_bounds__(256) void k_tr_att_bwd(TrAtt a) {
     cum_pad[i] = (j >= 0 && j < a.Tin) ? cum_prev[j] : 0.f;
   }
   for (int j = tid; j < a.Tin; j += blockDim.x) al[j] = a.ALIGN[((long)b * a.Tin + j) * a.T + a.t];
-  for (int i = tid; i < a.F * a.A; i += blockDim.x) Wl[i] = a.Wl[i];
+  for (int i = tid; i < a.F * a.A; i += blockDim.x) {
+    const float w = a.Wl[i];
+    Wl[i] = w;
+    WlT[(i % a.A) * a.F + i / a.A] = w;
+  }
   __syncthreads();
   // d align_j = dctx · values_j + d cum_t[j]   (cum_t = cum_{t-1} + align_t)
-  const int lane = tid & 63, wave = tid >> 6;
-  for (int j = wave; j < a.Tin; j += 4) {
+  const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  for (int j = wave; j < a.Tin; j += nw) {
     const float* v = a.values + ((long)b * a.Tin + j) * a.D;
     float acc = 0.f;
     for (int n = lane; n < a.D; n += 64) acc += dctx[n] * v[n];
@@ -458,7 +468,7 @@ __global__ __launch_bounds__(256) void k_tr_att_bwd(TrAtt a) {
   for (int j = tid; j < a.Tin; j += blockDim.x) da[j] = j < len ? al[j] * (da[j] - s) : 0.f;
   __syncthreads();
   // energies backward over j-chunks
-  const int NJ = blockDim.x / a.A;  // A divides 256
+  const int NJ = blockDim.x / a.A;  // A divides 256 (so also TR_AT)
   const int k = tid % a.A, js = tid / a.A;
   const float* q = a.Q + tb * a.A;
   const float vak = a.va[k], qk = q[k], bak = a.ba[k];
@@ -487,20 +497,20 @@ __global__ __launch_bounds__(256) void k_tr_att_bwd(TrAtt a) {
     for (int i = tid; i < jn * a.F; i += blockDim.x) {
       const int jj = i / a.F, c = i % a.F;
       float acc = 0.f;
-      for (int kk = 0; kk < a.A; ++kk) acc += dU[jj * a.A + kk] * Wl[c * a.A + kk];
+      for (int kk = 0; kk < a.A; ++kk) acc += dU[jj * a.A + kk] * WlT[kk * a.F + c];
       df[(j0 + jj) * a.F + c] = acc;
     }
     __syncthreads();
   }
   // dq_k = Σ_j dU[j][k] = dba (same sum); combine the NJ sub-rows
   racc[tid] = dv;
-  racc[256 + tid] = dba;
+  racc[TR_AT + tid] = dba;
   __syncthreads();
   if (tid < a.A) {
     float sv = 0.f, sb = 0.f;
     for (int g = 0; g < NJ; ++g) {
       sv += racc[g * a.A + tid];
-      sb += racc[256 + g * a.A + tid];
+      sb += racc[TR_AT + g * a.A + tid];
     }
     a.DQ[tb * a.A + tid] = sb;
     a.dV[(long)b * a.A + tid] += sv;
@@ -523,14 +533,21 @@ __global__ __launch_bounds__(256) void k_tr_att_bwd(TrAtt a) {
     for (int j = 0; j < a.Tin; ++j) acc += df[j * a.F + c];
     a.dBC[(long)b * a.F + c] += acc;
   }
-  for (int i = tid; i < a.Tin; i += blockDim.x) {
-    float acc = a.DCUM[(long)b * a.Tin + i];
-    for (int tap = 0; tap < a.KW; ++tap) {
-      const int j = i - tap + pad;
-      if (j < 0 || j >= a.Tin) continue;
-      for (int c = 0; c < a.F; ++c) acc += df[j * a.F + c] * a.Kc[tap * a.F + c];
+  {  // 32 lanes per position i (lane = filter c), reduced with xor shuffles inside the half-wave
+    const int c = tid & 31;
+    for (int i0 = 0; i0 < a.Tin; i0 += blockDim.x / 32) {
+      const int i = i0 + tid / 32;
+      float acc = 0.f;
+      if (i < a.Tin && c < a.F)
+        for (int tap = 0; tap < a.KW; ++tap) {
+          const int j = i - tap + pad;
+          if (j >= 0 && j < a.Tin) acc += df[j * a.F + c] * a.Kc[tap * a.F + c];
+        }
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      // each i owned by one half-wave; da already consumed d cum_t
+      if (c == 0 && i < a.Tin) a.DCUM[(long)b * a.Tin + i] += acc;
     }
-    a.DCUM[(long)b * a.Tin + i] = acc;  // each i owned by one thread; da already consumed it
   }
 }
 
@@ -555,7 +572,7 @@ __global__ void k_tr_mask_rows(const float* __restrict__ x, const int* __restric
 // L2 regularisation (tacotron.py:865-867): g += reg·w over [off, off+n); partial Σ w²/2
 __global__ __launch_bounds__(256) void k_tr_reg(const float* __restrict__ w, float* __restrict__ g, long n, float reg,
                                                 float* __restrict__ part) {
-  __shared__ float s4[4];
+  __shared__ float s4[16];
   float acc = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float v = w[i];
@@ -567,7 +584,7 @@ __global__ __launch_bounds__(256) void k_tr_reg(const float* __restrict__ w, flo
 }
 
 __global__ __launch_bounds__(256) void k_tr_sumsq(const float* __restrict__ g, long n, float* __restrict__ part) {
-  __shared__ float s4[4];
+  __shared__ float s4[16];
   float acc = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) acc += g[i] * g[i];
   acc = block_sum(acc, s4);
@@ -609,10 +626,16 @@ static void tr_colsum(tt2_train_ctx* c, const float* in, long M, int N, long ld,
   hipLaunchKernelGGL(k_tr_colsum_final, dim3((N + 255) / 256), dim3(256), 0, s, c->part.as<float>(), S, N, out);
 }
 
+static DevBuf* g_tr_kpart = nullptr;  // split-K scratch of the context being driven (stream-ordered)
+
 static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
                     hipStream_t s, const float* bias = nullptr, const float* residual = nullptr, long ldr = 0,
                     int act = ACT_NONE) {
   GemmArgs g;
+  if (g_tr_kpart) {
+    g.kpart = g_tr_kpart->as<float>();
+    g.kpart_floats = (long)(g_tr_kpart->bytes / sizeof(float));
+  }
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.Bw = Bw; g.ldb = ldb; g.Cout = C; g.ldc = ldc;
   g.bias = bias; g.residual = residual; g.ldr = ldr; g.act = act;
   gemm(g, s);
@@ -690,14 +713,15 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->TBUF, tmax);
   f(c->part, 64 * std::max<long>(4 * H, LX1) + 4096);
   f(c->red, 64);
+  f(c->kpart, 4L << 20);
 }
 
 static size_t att_fwd_lds(const tt2_train_ctx* c, int Tin) {
-  return sizeof(float) * ((size_t)Tin + c->KW + (size_t)Tin * c->F + (size_t)c->F * c->A + Tin + 4);
+  return sizeof(float) * ((size_t)Tin + c->KW + (size_t)Tin * c->F + (size_t)c->F * c->A + Tin + 16);
 }
 static size_t att_bwd_lds(const tt2_train_ctx* c, int Tin) {
   return sizeof(float) * ((size_t)c->D + Tin + c->KW + 2 * (size_t)Tin + 2 * (size_t)Tin * c->F +
-                          (size_t)c->F * c->A + (size_t)TR_JC * c->A + 3 * 256 + 4);
+                          2 * (size_t)c->F * c->A + (size_t)TR_JC * c->A + 2 * TR_AT + 16);
 }
 
 // forward + losses + backward for one batch; grads complete (incl. L2) on return (stream order)
@@ -708,6 +732,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   const float z = c->cfg.zoneout;
   c->T_last = T;
   c->Tin_last = Tin;
+  g_tr_kpart = &c->kpart;
   // weight transposes for the backward products
   tr_transpose(pvar(c, L1V("kernel")), LX1, 4 * H, 4 * H, c->K1T.as<float>(), LX1, s);
   tr_transpose(pvar(c, L2V("kernel")), 2 * H, 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, s);
@@ -771,7 +796,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
             c->Q.as<float>() + s1 * A, A, s);
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_fwd, dim3(B), dim3(256), lf, s, at);
+    hipLaunchKernelGGL(k_tr_att_fwd, dim3(B), dim3(TR_AT), lf, s, at);
     hipLaunchKernelGGL(k_tr_ctx, dim3((D + 255) / 256, B), dim3(256), sizeof(float) * Tin, s, at);
   }
   tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
@@ -794,7 +819,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   for (int t = T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_bwd, dim3(B), dim3(256), lb, s, at);
+    hipLaunchKernelGGL(k_tr_att_bwd, dim3(B), dim3(TR_AT), lb, s, at);
     tr_gemm(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, c->DH2.as<float>(), H, s, nullptr,
             dPIN + s1 * (H + D), H + D);
     TrLstmBwd b2{c->DH2.as<float>(), H, dX2 + (s1 + B) * 2 * H + H, 2 * H, c->DC2.as<float>(),
@@ -864,6 +889,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   }
   hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 64 * nreg, c->cfg.reg_weight,
                      red + 2, 0);
+  g_tr_kpart = nullptr;
 }
 
 static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s) {
