@@ -57,6 +57,7 @@ struct tt2_train_ctx {
   // backward
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DH2, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dWL, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
+  DevBuf TH, E, DA, DF, PQ;
   int T_last = 0, Tin_last = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
@@ -65,8 +66,7 @@ struct tt2_train_ctx {
 namespace tt2 {
 
 constexpr int TR_MAX_TIN = 320;  // LDS budget of the attention kernels
-constexpr int TR_JC = 32;        // j-chunk of the attention backward
-constexpr int TR_AT = 1024;      // threads per attention block (one block per utterance row)
+constexpr int TR_JT = 16;        // j rows (encoder positions) per attention work-group
 
 __device__ __forceinline__ float sigm_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
 
@@ -223,7 +223,7 @@ __global__ void k_tr_lstm_fwd(TrLstmFwd a) {
 }
 
 struct TrAtt {
-  int B, Tin, T, A, F, KW, D, H, P, t;
+  int B, Tin, T, A, F, KW, D, H, P, t, nt;  // nt = j-tiles per row (TR_JT rows each)
   const int* lens;
   const float* keys;    // [B,Tin,A]
   const float* values;  // [B,Tin,D]
@@ -235,93 +235,110 @@ struct TrAtt {
   const float* ba;      // [A]
   float* ALIGN;         // [B][Tin][T]
   float* CUM;           // [(T+1)][B][Tin]
+  float* TH;            // [T][B][Tin][A] tanh(keys + q + loc + b_a), kept for the backward
+  float* E;             // [B][Tin] energies of the current step
   // forward outputs of the context
   float* PIN;
   float* X1;
   // backward
   const float* dPIN;
   const float* dX1;
+  float* DA;     // [B][Tin] d align_t (+ d cum_t)
+  float* DF;     // [B][Tin][F] d location features
+  float* PQ;     // [B][nt][A] per-tile d query partials
   float* DCTX;   // [T][B][D]
   float* DQ;     // [T][B][A]
   float* DKEYS;  // [B][Tin][A]
   float* DCUM;   // [B][Tin]
-  float* dV;     // [B][A]
-  float* dBA;    // [B][A]
-  float* dWL;    // [B][F][A]
-  float* dKC;    // [B][KW][F]
-  float* dBC;    // [B][F]
+  float* dV;     // [B][nt][A]   accumulated over steps
+  float* dBA;    // [B][nt][A]
+  float* dWL;    // [B][nt][F][A]
+  float* dKC;    // [B][nt][KW][F]
+  float* dBC;    // [B][nt][F]
 };
 
-// location features f[j][c] = bc[c] + Σ_tap cum[j + tap - pad]·Kc[tap][c]  (attention.py:193-195)
-__device__ __forceinline__ void tr_loc_features(const TrAtt& a, const float* cum_pad, float* f) {
-  for (int i = threadIdx.x; i < a.Tin * a.F; i += blockDim.x) {
-    const int j = i / a.F, c = i % a.F;
+// Location features of rows j0..j0+TR_JT-1 of utterance b (attention.py:193-195):
+// f[jj][c] = bc[c] + Σ_tap cum_{t-1}[j0 + jj + tap - pad]·Kc[tap][c]; cseg = the cum segment.
+__device__ __forceinline__ void tr_locf_tile(const TrAtt& a, int b, int j0, float* cseg, float* f) {
+  const int pad = (a.KW - 1) / 2;
+  const float* cum_prev = a.CUM + ((long)a.t * a.B + b) * a.Tin;
+  for (int i = threadIdx.x; i < TR_JT + a.KW - 1; i += blockDim.x) {
+    const int j = j0 + i - pad;
+    cseg[i] = (j >= 0 && j < a.Tin) ? cum_prev[j] : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TR_JT * a.F; i += blockDim.x) {
+    const int jj = i / a.F, c = i % a.F;
     float acc = a.bc[c];
-    for (int tap = 0; tap < a.KW; ++tap) acc += cum_pad[j + tap] * a.Kc[tap * a.F + c];
+    for (int tap = 0; tap < a.KW; ++tap) acc += cseg[jj + tap] * a.Kc[tap * a.F + c];
     f[i] = acc;
   }
+  __syncthreads();
 }
 
-// One block (256 threads) per row b: location-sensitive energies (attention.py:37-69), masked
-// softmax, cumulative alignments (:222-225).  Dynamic LDS: cum_pad, f, Wl, e.
-__global__ __launch_bounds__(TR_AT) void k_tr_att_fwd(TrAtt a) {
-  extern __shared__ float lds[];
-  const int b = blockIdx.x;
-  const int pad = (a.KW - 1) / 2;
-  float* cum_pad = lds;                          // Tin + KW
-  float* f = cum_pad + a.Tin + a.KW;             // Tin * F
-  float* Wl = f + a.Tin * a.F;                   // F * A
-  float* e = Wl + a.F * a.A;                     // Tin
-  float* s4 = e + a.Tin;                         // 16
-  const float* cum_prev = a.CUM + ((long)a.t * a.B + b) * a.Tin;
-  for (int i = threadIdx.x; i < a.Tin + a.KW; i += blockDim.x) {
-    const int j = i - pad;
-    cum_pad[i] = (j >= 0 && j < a.Tin) ? cum_prev[j] : 0.f;
-  }
+// Energies e_j = Σ_k v_a[k]·tanh(keys_jk + q_k + loc_jk + b_a[k]) (attention.py:37-69) for one
+// tile of TR_JT rows; grid (nt, B) spreads a step over the chip.  Keeps tanh for the backward.
+__global__ __launch_bounds__(256) void k_tr_att_energy(TrAtt a) {
+  __shared__ float cseg[TR_JT + 64];
+  __shared__ float f[TR_JT * 32];
+  __shared__ float Wl[32 * 256];
+  const int b = blockIdx.y, j0 = blockIdx.x * TR_JT;
   for (int i = threadIdx.x; i < a.F * a.A; i += blockDim.x) Wl[i] = a.Wl[i];
-  __syncthreads();
-  tr_loc_features(a, cum_pad, f);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const float* q = a.Q + ((long)a.t * a.B + b) * a.A;
-  const int len = a.lens[b];
-  for (int j = wave; j < a.Tin; j += nw) {
+  tr_locf_tile(a, b, j0, cseg, f);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long tb = (long)a.t * a.B + b;
+  const float* q = a.Q + tb * a.A;
+  for (int jj = wave; jj < TR_JT; jj += 4) {
+    const int j = j0 + jj;
+    if (j >= a.Tin) break;
     float acc = 0.f;
     for (int k = lane; k < a.A; k += 64) {
       float u = a.keys[((long)b * a.Tin + j) * a.A + k] + q[k] + a.ba[k];
-      for (int c = 0; c < a.F; ++c) u += f[j * a.F + c] * Wl[c * a.A + k];
-      acc += a.va[k] * tanhf(u);
+      for (int c = 0; c < a.F; ++c) u += f[jj * a.F + c] * Wl[c * a.A + k];
+      const float th = tanhf(u);
+      a.TH[(tb * a.Tin + j) * a.A + k] = th;
+      acc += a.va[k] * th;
     }
     acc = wave_sum(acc);
-    if (lane == 0) e[j] = j < len ? acc : -INFINITY;
-  }
-  __syncthreads();
-  float mx = -INFINITY;
-  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) mx = fmaxf(mx, e[j]);
-  mx = block_max(mx, s4);
-  float sm = 0.f;
-  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) sm += j < len ? expf(e[j] - mx) : 0.f;
-  sm = block_sum(sm, s4);
-  float* cum_next = a.CUM + ((long)(a.t + 1) * a.B + b) * a.Tin;
-  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) {
-    const float al = j < len ? expf(e[j] - mx) / sm : 0.f;
-    a.ALIGN[((long)b * a.Tin + j) * a.T + a.t] = al;
-    cum_next[j] = cum_prev[j] + al;
+    if (lane == 0) a.E[(long)b * a.Tin + j] = acc;
   }
 }
 
-// context_t = align_t · values  (attention.py:27) -> PIN[t][b][H:], X1[t+1][b][P:P+D]
+// Masked softmax (attention.py:218, TF _maybe_mask_score) recomputed by every block of the row,
+// cumulative alignments (:222-225) by block 0, then context_t = align_t · values (:27)
+// -> PIN[t][b][H:], X1[t+1][b][P:P+D].
 __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
   extern __shared__ float al[];
+  __shared__ float s16[16];
   const int b = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
-  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) al[j] = a.ALIGN[((long)b * a.Tin + j) * a.T + a.t];
+  const int len = a.lens[b];
+  const float* e = a.E + (long)b * a.Tin;
+  float mx = -INFINITY;
+  for (int j = threadIdx.x; j < len; j += blockDim.x) mx = fmaxf(mx, e[j]);
+  mx = block_max(mx, s16);
+  float sm = 0.f;
+  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) {
+    const float x = j < len ? expf(e[j] - mx) : 0.f;
+    al[j] = x;
+    sm += x;
+  }
+  sm = block_sum(sm, s16);
+  const long tb = (long)a.t * a.B + b;
+  for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) {
+    const float x = al[j] / sm;
+    al[j] = x;
+    if (blockIdx.x == 0) {
+      a.ALIGN[((long)b * a.Tin + j) * a.T + a.t] = x;
+      a.CUM[(tb + a.B) * a.Tin + j] = a.CUM[tb * a.Tin + j] + x;
+    }
+  }
   __syncthreads();
   if (n >= a.D) return;
   const float* v = a.values + (long)b * a.Tin * a.D + n;
   float acc = 0.f;
   for (int j = 0; j < a.Tin; ++j) acc += al[j] * v[(long)j * a.D];
-  a.PIN[((long)a.t * a.B + b) * (a.H + a.D) + a.H + n] = acc;
-  a.X1[((long)(a.t + 1) * a.B + b) * (a.P + a.D + a.H) + a.P + n] = acc;
+  a.PIN[tb * (a.H + a.D) + a.H + n] = acc;
+  a.X1[(tb + a.B) * (a.P + a.D + a.H) + a.P + n] = acc;
 }
 
 // frame MSE + stop sigmoid CE (tacotron.py:774,778-779) and their output gradients.  Frames are
@@ -414,140 +431,147 @@ __global__ void k_tr_lstm_bwd(TrLstmBwd a) {
   a.R[(long)b * a.ldr + a.off_r + n] = (1.f - kh) * dhz;
 }
 
-// Attention backward for one step, one block per row b.  Recomputes the location features and
-// tanh terms from CUM[t] and Q[t] instead of storing [T,B,Tin,A] of them.
-__global__ __launch_bounds__(TR_AT) void k_tr_att_bwd(TrAtt a) {
-  extern __shared__ float lds[];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int pad = (a.KW - 1) / 2;
-  float* dctx = lds;                          // D
-  float* cum_pad = dctx + a.D;                // Tin + KW
-  float* al = cum_pad + a.Tin + a.KW;         // Tin
-  float* da = al + a.Tin;                     // Tin (d align -> d energy)
-  float* f = da + a.Tin;                      // Tin*F
-  float* df = f + a.Tin * a.F;                // Tin*F
-  float* Wl = df + a.Tin * a.F;               // F*A
-  float* WlT = Wl + a.F * a.A;                // A*F (transposed copy: conflict-free d f reads)
-  float* dU = WlT + a.F * a.A;                // JC*A
-  float* racc = dU + TR_JC * a.A;             // 2 * TR_AT (dv, dba partials)
-  float* s4 = racc + 2 * TR_AT;               // 16
+// ---- attention backward for one step: three chip-wide launches over (j-tile, row) ----
+// (1) d align_j = dctx_t · values_j + d cum_t[j]  (cum_t = cum_{t-1} + align_t)
+__global__ __launch_bounds__(256) void k_tr_att_dalign(TrAtt a) {
+  __shared__ float dctx[1024];
+  const int b = blockIdx.y, j0 = blockIdx.x * TR_JT;
   const long tb = (long)a.t * a.B + b;
-  const int len = a.lens[b];
-  for (int n = tid; n < a.D; n += blockDim.x) {
+  for (int n = threadIdx.x; n < a.D; n += blockDim.x) {
     const float v = a.dPIN[tb * (a.H + a.D) + a.H + n] + a.dX1[(tb + a.B) * (a.P + a.D + a.H) + a.P + n];
     dctx[n] = v;
-    a.DCTX[tb * a.D + n] = v;
-  }
-  const float* cum_prev = a.CUM + tb * a.Tin;
-  for (int i = tid; i < a.Tin + a.KW; i += blockDim.x) {
-    const int j = i - pad;
-    cum_pad[i] = (j >= 0 && j < a.Tin) ? cum_prev[j] : 0.f;
-  }
-  for (int j = tid; j < a.Tin; j += blockDim.x) al[j] = a.ALIGN[((long)b * a.Tin + j) * a.T + a.t];
-  for (int i = tid; i < a.F * a.A; i += blockDim.x) {
-    const float w = a.Wl[i];
-    Wl[i] = w;
-    WlT[(i % a.A) * a.F + i / a.A] = w;
+    if (blockIdx.x == 0) a.DCTX[tb * a.D + n] = v;
   }
   __syncthreads();
-  // d align_j = dctx · values_j + d cum_t[j]   (cum_t = cum_{t-1} + align_t)
-  const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  for (int j = wave; j < a.Tin; j += nw) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int jj = wave; jj < TR_JT; jj += 4) {
+    const int j = j0 + jj;
+    if (j >= a.Tin) break;
     const float* v = a.values + ((long)b * a.Tin + j) * a.D;
     float acc = 0.f;
     for (int n = lane; n < a.D; n += 64) acc += dctx[n] * v[n];
     acc = wave_sum(acc);
-    if (lane == 0) da[j] = acc + a.DCUM[(long)b * a.Tin + j];
+    if (lane == 0) a.DA[(long)b * a.Tin + j] = acc + a.DCUM[(long)b * a.Tin + j];
   }
-  tr_loc_features(a, cum_pad, f);
-  __syncthreads();
-  // softmax backward: de_j = a_j (da_j - Σ a·da)
+}
+
+// (2) softmax backward de_j = a_j (da_j - Σ a·da), tanh backward du_jk = de_j v_k (1 - th²):
+// d keys (+=), per-tile partials of d v_a, d b_a (= d q), d W_loc = f^T du, and d f = du · W_loc^T
+__global__ __launch_bounds__(256) void k_tr_att_energy_bwd(TrAtt a) {
+  __shared__ float cseg[TR_JT + 64];
+  __shared__ float f[TR_JT * 32];
+  __shared__ float WlT[256 * 33];
+  __shared__ float dU[TR_JT * 256];
+  __shared__ float de[TR_JT];
+  __shared__ float racc[2 * 256];
+  __shared__ float s16[16];
+  const int b = blockIdx.y, tile = blockIdx.x, j0 = tile * TR_JT, tid = threadIdx.x;
+  const long tb = (long)a.t * a.B + b;
+  const int len = a.lens[b];
   float s = 0.f;
-  for (int j = tid; j < a.Tin; j += blockDim.x) s += al[j] * da[j];
-  s = block_sum(s, s4);
-  for (int j = tid; j < a.Tin; j += blockDim.x) da[j] = j < len ? al[j] * (da[j] - s) : 0.f;
-  __syncthreads();
-  // energies backward over j-chunks
-  const int NJ = blockDim.x / a.A;  // A divides 256 (so also TR_AT)
-  const int k = tid % a.A, js = tid / a.A;
-  const float* q = a.Q + tb * a.A;
-  const float vak = a.va[k], qk = q[k], bak = a.ba[k];
-  float dv = 0.f, dba = 0.f, wl_acc[32];
-#pragma unroll
-  for (int c = 0; c < 32; ++c) wl_acc[c] = 0.f;
-  for (int j0 = 0; j0 < a.Tin; j0 += TR_JC) {
-    const int jn = min(TR_JC, a.Tin - j0);
-    for (int jj = js; jj < jn; jj += NJ) {
-      const int j = j0 + jj;
-      const long kidx = ((long)b * a.Tin + j) * a.A + k;
-      float u = a.keys[kidx] + qk + bak;
-      for (int c = 0; c < a.F; ++c) u += f[j * a.F + c] * Wl[c * a.A + k];
-      const float th = tanhf(u);
-      const float de = da[j];
-      const float du = de * vak * (1.f - th * th);
-      dv += de * th;
-      dba += du;
-#pragma unroll
-      for (int c = 0; c < 32; ++c)
-        if (c < a.F) wl_acc[c] += f[j * a.F + c] * du;
-      a.DKEYS[kidx] += du;
-      dU[jj * a.A + k] = du;
-    }
-    __syncthreads();
-    for (int i = tid; i < jn * a.F; i += blockDim.x) {
-      const int jj = i / a.F, c = i % a.F;
-      float acc = 0.f;
-      for (int kk = 0; kk < a.A; ++kk) acc += dU[jj * a.A + kk] * WlT[kk * a.F + c];
-      df[(j0 + jj) * a.F + c] = acc;
-    }
-    __syncthreads();
+  for (int j = tid; j < len; j += blockDim.x)
+    s += a.ALIGN[((long)b * a.Tin + j) * a.T + a.t] * a.DA[(long)b * a.Tin + j];
+  s = block_sum(s, s16);
+  if (tid < TR_JT) {
+    const int j = j0 + tid;
+    de[tid] = j < len ? a.ALIGN[((long)b * a.Tin + j) * a.T + a.t] * (a.DA[(long)b * a.Tin + j] - s) : 0.f;
   }
-  // dq_k = Σ_j dU[j][k] = dba (same sum); combine the NJ sub-rows
+  for (int i = tid; i < a.F * a.A; i += blockDim.x) WlT[(i % a.A) * 33 + i / a.A] = a.Wl[i];
+  tr_locf_tile(a, b, j0, cseg, f);  // syncs
+  const int NJ = blockDim.x / a.A, k = tid % a.A, js = tid / a.A;
+  const float vak = a.va[k];
+  float dv = 0.f, dq = 0.f;
+  for (int jj = js; jj < TR_JT; jj += NJ) {
+    const int j = j0 + jj;
+    float du = 0.f;
+    if (j < a.Tin) {
+      const float th = a.TH[(tb * a.Tin + j) * a.A + k];
+      du = de[jj] * vak * (1.f - th * th);
+      dv += de[jj] * th;
+      dq += du;
+      a.DKEYS[((long)b * a.Tin + j) * a.A + k] += du;
+    }
+    dU[jj * a.A + k] = du;
+  }
   racc[tid] = dv;
-  racc[TR_AT + tid] = dba;
+  racc[256 + tid] = dq;
   __syncthreads();
+  const long pt = (long)b * a.nt + tile;
   if (tid < a.A) {
-    float sv = 0.f, sb = 0.f;
+    float sv = 0.f, sq = 0.f;
     for (int g = 0; g < NJ; ++g) {
       sv += racc[g * a.A + tid];
-      sb += racc[TR_AT + g * a.A + tid];
+      sq += racc[256 + g * a.A + tid];
     }
-    a.DQ[tb * a.A + tid] = sb;
-    a.dV[(long)b * a.A + tid] += sv;
-    a.dBA[(long)b * a.A + tid] += sb;
+    a.PQ[pt * a.A + tid] = sq;
+    a.dV[pt * a.A + tid] += sv;
+    a.dBA[pt * a.A + tid] += sq;
   }
-  for (int g = 0; g < NJ; ++g) {
-    if (js == g)
-      for (int c = 0; c < a.F; ++c) a.dWL[((long)b * a.F + c) * a.A + k] += wl_acc[c];
-    __syncthreads();
+  for (int i = tid; i < a.F * a.A; i += blockDim.x) {
+    const int c = i / a.A, kk = i % a.A;
+    float acc = 0.f;
+#pragma unroll 4
+    for (int jj = 0; jj < TR_JT; ++jj) acc += f[jj * a.F + c] * dU[jj * a.A + kk];
+    a.dWL[pt * a.F * a.A + i] += acc;
   }
-  // location conv backward: dKc, dbc, and d cum_{t-1} = d cum_t + convT(df)
+  for (int i = tid; i < TR_JT * a.F; i += blockDim.x) {
+    const int jj = i / a.F, c = i % a.F, j = j0 + jj;
+    if (j >= a.Tin) continue;
+    float acc = 0.f;
+    for (int kk = 0; kk < a.A; ++kk) acc += dU[jj * a.A + kk] * WlT[kk * 33 + c];
+    a.DF[((long)b * a.Tin + j) * a.F + c] = acc;
+  }
+}
+
+// (3) d query (sum of the tile partials), location-conv backward: per-tile partials of d Kc and
+// d bc, and d cum_{t-1}[i] = d cum_t[i] + Σ_tap,c df[i - tap + pad][c]·Kc[tap][c]
+__global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
+  __shared__ float cseg[TR_JT + 64];
+  __shared__ float dfh[(TR_JT + 64) * 32];
+  const int b = blockIdx.y, tile = blockIdx.x, j0 = tile * TR_JT, tid = threadIdx.x;
+  const int pad = (a.KW - 1) / 2, lo = a.KW - 1 - pad;  // halo below / above
+  const long tb = (long)a.t * a.B + b;
+  if (tile == 0)
+    for (int k = tid; k < a.A; k += blockDim.x) {
+      float acc = 0.f;
+      for (int g = 0; g < a.nt; ++g) acc += a.PQ[((long)b * a.nt + g) * a.A + k];
+      a.DQ[tb * a.A + k] = acc;
+    }
+  const float* cum_prev = a.CUM + tb * a.Tin;
+  for (int i = tid; i < TR_JT + a.KW - 1; i += blockDim.x) {
+    const int j = j0 + i - pad;
+    cseg[i] = (j >= 0 && j < a.Tin) ? cum_prev[j] : 0.f;
+  }
+  // df rows j0 - lo .. j0 + TR_JT - 1 + pad (zero outside [0, Tin))
+  const int nh = TR_JT + a.KW - 1;
+  for (int i = tid; i < nh * a.F; i += blockDim.x) {
+    const int j = j0 - lo + i / a.F, c = i % a.F;
+    dfh[i] = (j >= 0 && j < a.Tin) ? a.DF[((long)b * a.Tin + j) * a.F + c] : 0.f;
+  }
+  __syncthreads();
+  const long pt = (long)b * a.nt + tile;
+  const float* dfs = dfh + lo * a.F;  // the tile's own rows
   for (int i = tid; i < a.KW * a.F; i += blockDim.x) {
     const int tap = i / a.F, c = i % a.F;
     float acc = 0.f;
-    for (int j = 0; j < a.Tin; ++j) acc += df[j * a.F + c] * cum_pad[j + tap];
-    a.dKC[(long)b * a.KW * a.F + i] += acc;
+    for (int jj = 0; jj < TR_JT; ++jj) acc += dfs[jj * a.F + c] * cseg[jj + tap];
+    a.dKC[pt * a.KW * a.F + i] += acc;
   }
   for (int c = tid; c < a.F; c += blockDim.x) {
     float acc = 0.f;
-    for (int j = 0; j < a.Tin; ++j) acc += df[j * a.F + c];
-    a.dBC[(long)b * a.F + c] += acc;
+    for (int jj = 0; jj < TR_JT; ++jj) acc += dfs[jj * a.F + c];
+    a.dBC[pt * a.F + c] += acc;
   }
-  {  // 32 lanes per position i (lane = filter c), reduced with xor shuffles inside the half-wave
-    const int c = tid & 31;
-    for (int i0 = 0; i0 < a.Tin; i0 += blockDim.x / 32) {
-      const int i = i0 + tid / 32;
-      float acc = 0.f;
-      if (i < a.Tin && c < a.F)
-        for (int tap = 0; tap < a.KW; ++tap) {
-          const int j = i - tap + pad;
-          if (j >= 0 && j < a.Tin) acc += df[j * a.F + c] * a.Kc[tap * a.F + c];
-        }
+  // 32 lanes per position (lane = filter), 8 positions per pass
+  const int c = tid & 31;
+  for (int i0 = 0; i0 < TR_JT; i0 += blockDim.x / 32) {
+    const int ii = i0 + tid / 32, i = j0 + ii;
+    float acc = 0.f;
+    if (c < a.F)
+      for (int tap = 0; tap < a.KW; ++tap) acc += dfs[(ii - tap + pad) * a.F + c] * a.Kc[tap * a.F + c];
 #pragma unroll
-      for (int o = 16; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-      // each i owned by one half-wave; da already consumed d cum_t
-      if (c == 0 && i < a.Tin) a.DCUM[(long)b * a.Tin + i] += acc;
-    }
+    for (int o = 16; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (c == 0 && i < a.Tin) a.DCUM[(long)b * a.Tin + i] += acc;
   }
 }
 
@@ -706,22 +730,16 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->dFR, TB * NM); f(c->dST, TB); f(c->dPIN, TB * (H + D)); f(c->dX1, (T + 1) * B * LX1);
   f(c->dX2, (T + 1) * B * 2 * H); f(c->dG1, TB * 4 * H); f(c->dG2, TB * 4 * H); f(c->DC1, B * H); f(c->DC2, B * H);
   f(c->R1, B * LX1); f(c->R2, B * 2 * H); f(c->DQ, TB * A); f(c->DH2, B * H); f(c->DCTX, TB * D);
-  f(c->DKEYS, B * Tin * A); f(c->DCUM, B * Tin); f(c->dV, B * A); f(c->dBA, B * A); f(c->dWL, B * F * A);
-  f(c->dKC, B * KW * F); f(c->dBC, B * F); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
+  const long NT = (Tin + TR_JT - 1) / TR_JT;
+  f(c->DKEYS, B * Tin * A); f(c->DCUM, B * Tin); f(c->dV, B * NT * A); f(c->dBA, B * NT * A);
+  f(c->dWL, B * NT * F * A); f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F);
+  f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DA, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
   f(c->dZ, TB * P); f(c->dPre, TB * P);
   const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM});
   f(c->TBUF, tmax);
   f(c->part, 64 * std::max<long>(4 * H, LX1) + 4096);
   f(c->red, 64);
   f(c->kpart, 4L << 20);
-}
-
-static size_t att_fwd_lds(const tt2_train_ctx* c, int Tin) {
-  return sizeof(float) * ((size_t)Tin + c->KW + (size_t)Tin * c->F + (size_t)c->F * c->A + Tin + 16);
-}
-static size_t att_bwd_lds(const tt2_train_ctx* c, int Tin) {
-  return sizeof(float) * ((size_t)c->D + Tin + c->KW + 2 * (size_t)Tin + 2 * (size_t)Tin * c->F +
-                          2 * (size_t)c->F * c->A + (size_t)TR_JC * c->A + 2 * TR_AT + 16);
 }
 
 // forward + losses + backward for one batch; grads complete (incl. L2) on return (stream order)
@@ -776,7 +794,11 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   at.dPIN = c->dPIN.as<float>(); at.dX1 = c->dX1.as<float>(); at.DCTX = c->DCTX.as<float>(); at.DQ = c->DQ.as<float>();
   at.DKEYS = c->DKEYS.as<float>(); at.DCUM = c->DCUM.as<float>(); at.dV = c->dV.as<float>(); at.dBA = c->dBA.as<float>();
   at.dWL = c->dWL.as<float>(); at.dKC = c->dKC.as<float>(); at.dBC = c->dBC.as<float>();
-  const size_t lf = att_fwd_lds(c, Tin), lb = att_bwd_lds(c, Tin);
+  at.TH = c->TH.as<float>(); at.E = c->E.as<float>(); at.DA = c->DA.as<float>(); at.DF = c->DF.as<float>();
+  at.PQ = c->PQ.as<float>();
+  const int NT = (Tin + TR_JT - 1) / TR_JT;
+  at.nt = NT;
+  const dim3 att_grid(NT, B);
   const unsigned bh = nblk((long)B * H);
 
   for (int t = 0; t < T; ++t) {
@@ -796,7 +818,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
             c->Q.as<float>() + s1 * A, A, s);
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_fwd, dim3(B), dim3(TR_AT), lf, s, at);
+    hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(256), 0, s, at);
     hipLaunchKernelGGL(k_tr_ctx, dim3((D + 255) / 256, B), dim3(256), sizeof(float) * Tin, s, at);
   }
   tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
@@ -819,7 +841,9 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   for (int t = T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_bwd, dim3(B), dim3(TR_AT), lb, s, at);
+    hipLaunchKernelGGL(k_tr_att_dalign, att_grid, dim3(256), 0, s, at);
+    hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(256), 0, s, at);
+    hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
     tr_gemm(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, c->DH2.as<float>(), H, s, nullptr,
             dPIN + s1 * (H + D), H + D);
     TrLstmBwd b2{c->DH2.as<float>(), H, dX2 + (s1 + B) * 2 * H + H, 2 * H, c->DC2.as<float>(),
@@ -864,11 +888,13 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_gemm(NM, P, TBi, TBUF, TB, c->dZ.as<float>(), P, gvar(c, PRV(1, "kernel")), P, s);
   tr_colsum(c, c->dZ.as<float>(), TB, P, P, gvar(c, PRV(1, "bias")), s);
   // attention parameters: sums of the per-row partials
-  tr_colsum(c, c->dV.as<float>(), B, A, A, gvar(c, LAV("attention_variable_projection")), s);
-  tr_colsum(c, c->dBA.as<float>(), B, A, A, gvar(c, LAV("attention_bias")), s);
-  tr_colsum(c, c->dWL.as<float>(), B, F * A, (long)F * A, gvar(c, LAV("location_features_layer/kernel")), s);
-  tr_colsum(c, c->dKC.as<float>(), B, KW * F, (long)KW * F, gvar(c, LAV("location_features_convolution/kernel")), s);
-  tr_colsum(c, c->dBC.as<float>(), B, F, F, gvar(c, LAV("location_features_convolution/bias")), s);
+  const long BNT = (long)B * NT;
+  tr_colsum(c, c->dV.as<float>(), BNT, A, A, gvar(c, LAV("attention_variable_projection")), s);
+  tr_colsum(c, c->dBA.as<float>(), BNT, A, A, gvar(c, LAV("attention_bias")), s);
+  tr_colsum(c, c->dWL.as<float>(), BNT, F * A, (long)F * A, gvar(c, LAV("location_features_layer/kernel")), s);
+  tr_colsum(c, c->dKC.as<float>(), BNT, KW * F, (long)KW * F,
+            gvar(c, LAV("location_features_convolution/kernel")), s);
+  tr_colsum(c, c->dBC.as<float>(), BNT, F, F, gvar(c, LAV("location_features_convolution/bias")), s);
   // memory: d values = Σ_t align_t^T · dctx_t (+ keys path), memory_layer kernel
   for (int b = 0; b < B; ++b)
     tr_gemm(Tin, D, T, c->ALIGN.as<float>() + (long)b * Tin * T, T, c->DCTX.as<float>() + (long)b * D, (long)B * D,
@@ -955,12 +981,7 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
       TT2_HIP(hipEventCreate(&c->ev1));
       tr_build_vars(c);
       tr_alloc(c);
-      const size_t lb = att_bwd_lds(c, c->Tin);
-      TT2_CHECK(lb <= 160 * 1024, TT2_ERR_INVALID_ARG, "attention backward LDS exceeds 160 KiB");
-      TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tr_att_bwd),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
-      TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tr_att_fwd),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)att_fwd_lds(c, c->Tin)));
+
     } catch (...) {
       delete c;
       throw;
