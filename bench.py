@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--train-t-in", type=int, default=150)
     p.add_argument("--train-t-out", type=int, default=800)
     p.add_argument("--train-steps", type=int, default=2)
+    p.add_argument("--train-precision", default="bf16", choices=["bf16", "fp32"],
+                   help="configs[4] names bf16 (GEMM operands; fp32 accumulation and state)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=100)
     p.add_argument("--profile-iters", type=int, default=50)
@@ -203,7 +205,7 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
     B, Ti, T = a.train_batch, a.train_t_in, a.train_t_out
     D = memory_width(hp)
     W = init_tacotron_weights(hp, seed=hp.tacotron_random_seed)
-    tr = TacotronTrainer(hp, W, B, Ti, T, local)
+    tr = TacotronTrainer(hp, W, B, Ti, T, local, precision=a.train_precision)
     if world > 1:
         tr.bind_grad_buffer()
     dev = torch.device("cuda", local)
@@ -233,18 +235,21 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
     ms = 1e3 * el / a.train_steps
     fl = train_step_flops(B, Ti, T, hp, D)
     tf = fl / (ms * 1e-3) / 1e12
+    peak = 2500.0 if a.train_precision == "bf16" else 157.3
     return dict(metric="mel-frames/sec (teacher-forced training step)",
                 value=round(world * B * T / (ms * 1e-3), 1), unit="mel-frames/s",
                 ms_per_step=round(ms, 2), steps=a.train_steps, warmup=1,
                 forward_backward_ms=round(L["forward_backward_ms"], 2),
                 loss_first=round(losses[0]["loss"], 5), loss_last=round(L["loss"], 5),
-                grad_norm=round(L["grad_norm"], 5), dtype="f32",
+                grad_norm=round(L["grad_norm"], 5), dtype=a.train_precision,
                 config=dict(workload="configs[4]: Tacotron-2 decoder training step (teacher-forced), "
                                      "B={} rows/GPU, T_in={}, T_out={}, D_mem={}".format(B, Ti, T, D),
                             global_batch=B * world, parallelism="dp{} (RCCL grad all-reduce)".format(world)),
-                roofline=dict(bound="mfma", achieved=round(tf, 2), peak=157.3, unit="TFLOP/s",
-                              frac=round(tf / 157.3, 4), algorithmic_flops_per_step=int(fl),
-                              note="fp32 MFMA peak (v_mfma_f32_32x32x2_f32); whole-step average"))
+                roofline=dict(bound="mfma", achieved=round(tf, 2), peak=peak, unit="TFLOP/s",
+                              frac=round(tf / peak, 4), algorithmic_flops_per_step=int(fl),
+                              note="dense MFMA peak of the GEMM dtype ({}); whole-step average".format(
+                                  "v_mfma_f32_32x32x16_bf16" if a.train_precision == "bf16"
+                                  else "v_mfma_f32_32x32x2_f32")))
 
 
 E2E_TEXT = ("Scientists at the CERN laboratory say they have discovered a new particle. "

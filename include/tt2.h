@@ -317,6 +317,8 @@ typedef struct tt2_train_config {
   float reg_weight;        /* tacotron_reg_weight 1e-6 */
   float adam_beta1, adam_beta2, adam_epsilon;  /* 0.9, 0.999, 1e-6 */
   float clip_norm;         /* 1.0 (tacotron_clip_gradients); <= 0 disables */
+  int precision;           /* 0 = fp32 GEMMs (parity); 1 = bf16 GEMM operands, fp32 accumulation,
+                              fp32 master weights / cell state / optimizer (configs[4]) */
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;

@@ -35,6 +35,7 @@ struct GemmArgs {
   // keeps lo out of fp16 subnormals), A·B = Ah·Bh + Ah·Bl + Al·Bh on v_mfma_f32_32x32x16_f16 with
   // fp32 accumulation (the dropped lo·lo term is ~2^-22 relative; fp16 products are exact in
   // fp32) -- 3/16 of the fp32 MFMA cost, ~1e-7 relative error.  Needs |A| < 4e3, |B| < 64.
+  // 2 = bf16 operands (round-to-nearest-even), fp32 accumulation: mixed-precision training.
   int split16 = 0;
   // split-K for skinny products (fp32 path): when kpart != nullptr the dispatcher may split K over
   // blockIdx.z so a 64-row GEMM fills the chip; raw partials go to kpart (>= kpart_floats floats,

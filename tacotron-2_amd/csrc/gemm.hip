@@ -9,6 +9,8 @@
 #include "gemm.h"
 
 #include <algorithm>
+#include <type_traits>
+#include <cstdlib>
 
 namespace tt2 {
 
@@ -235,20 +237,36 @@ __device__ __forceinline__ void split8(const float* v, float scale, f16x8& hi, f
   }
 }
 
-template <bool VA>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void to_bf16x8(const float* v, bf16x8& o) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];  // round to nearest even
+}
+
+// MODE 1: split fp16x3 (fp32-accurate); MODE 2: bf16 operands (one v_mfma_f32_32x32x16_bf16 per
+// k-slab, fp32 accumulation -- the mixed-precision training GEMM).  Block (64·WMB) x 128 x 32,
+// 4 waves in a 2x2 grid, each wave WMB x 2 tiles of 32x32; split-K over blockIdx.z as in
+// gemm_kernel (raw partials to kpart, epilogue in gemm_splitk_reduce).
+template <bool VA, int MODE, int WMB>
 __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
-  constexpr int BM = 128, BN = 128, BK = X3_BK;
-  __shared__ __attribute__((aligned(16))) _Float16 Ah[2][BM][X3_LD], Al[2][BM][X3_LD];
-  __shared__ __attribute__((aligned(16))) _Float16 Bh[2][BN][X3_LD], Bl[2][BN][X3_LD];
+  constexpr int BM = 64 * WMB, BN = 128, BK = X3_BK;
+  constexpr int EA = BM * BK / 256;            // A elements per thread (16 or 8)
+  constexpr int TPR_A = BK / EA;               // threads per A row
+  constexpr int NPL = MODE == 1 ? 2 : 1;       // hi/lo planes
+  typedef typename std::conditional<MODE == 1, _Float16, __bf16>::type ET;
+  typedef typename std::conditional<MODE == 1, f16x8, bf16x8>::type V8;
+  __shared__ __attribute__((aligned(16))) ET As[NPL][2][BM][X3_LD];
+  __shared__ __attribute__((aligned(16))) ET Bs[NPL][2][BN][X3_LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int am = tid >> 1, ak = (tid & 1) * 16;    // A: row am, k [ak, ak+16)
-  const int bn = tid & 127, bk = (tid >> 7) * 16;  // B: col bn, k [bk, bk+16) (coalesced over n)
-  float ra[16], rb[16];
-  f32x16 acc[2][2];
+  const int am = tid / TPR_A, ak = (tid % TPR_A) * EA;  // A: row am, k [ak, ak+EA)
+  const int bn = tid & 127, bk = (tid >> 7) * 16;       // B: col bn, k [bk, bk+16) (coalesced over n)
+  float ra[EA], rb[16];
+  f32x16 acc[WMB][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WMB; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -256,7 +274,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
 
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int e = 0; e < 16; e += 4) load_a4<VA>(g, m0 + am, k0 + ak + e, &ra[e]);
+    for (int e = 0; e < EA; e += 4) load_a4<VA>(g, m0 + am, k0 + ak + e, &ra[e]);
     const int n = n0 + bn;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -265,56 +283,110 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
     }
   };
   auto sstore = [&](int buf) {
-    f16x8 h, l;
+    if constexpr (MODE == 1) {
+      f16x8 h, l;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      split8(&ra[8 * q], X3_SA, h, l);
-      *reinterpret_cast<f16x8*>(&Ah[buf][am][ak + 8 * q]) = h;
-      *reinterpret_cast<f16x8*>(&Al[buf][am][ak + 8 * q]) = l;
-      split8(&rb[8 * q], X3_SB, h, l);
-      *reinterpret_cast<f16x8*>(&Bh[buf][bn][bk + 8 * q]) = h;
-      *reinterpret_cast<f16x8*>(&Bl[buf][bn][bk + 8 * q]) = l;
+      for (int q = 0; q < EA / 8; ++q) {
+        split8(&ra[8 * q], X3_SA, h, l);
+        *reinterpret_cast<f16x8*>(&As[0][buf][am][ak + 8 * q]) = h;
+        *reinterpret_cast<f16x8*>(&As[1][buf][am][ak + 8 * q]) = l;
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        split8(&rb[8 * q], X3_SB, h, l);
+        *reinterpret_cast<f16x8*>(&Bs[0][buf][bn][bk + 8 * q]) = h;
+        *reinterpret_cast<f16x8*>(&Bs[1][buf][bn][bk + 8 * q]) = l;
+      }
+    } else {
+      bf16x8 h;
+#pragma unroll
+      for (int q = 0; q < EA / 8; ++q) {
+        to_bf16x8(&ra[8 * q], h);
+        *reinterpret_cast<bf16x8*>(&As[0][buf][am][ak + 8 * q]) = h;
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        to_bf16x8(&rb[8 * q], h);
+        *reinterpret_cast<bf16x8*>(&Bs[0][buf][bn][bk + 8 * q]) = h;
+      }
     }
   };
 
-  const int nk = (g.K + BK - 1) / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
+  const int nkt = (g.K + BK - 1) / BK;
+  const int per = (nkt + g.ksplit - 1) / g.ksplit;
+  const int kt0 = blockIdx.z * per, kt1 = min(nkt, kt0 + per);
+  if (g.ksplit > 1) g.K = min(g.K, kt1 * BK);
+  const int nk = kt1 - kt0;
+  if (nk > 0) {
+    gload(kt0 * BK);
+    sstore(0);
+    __syncthreads();
+  }
   const int r = lane & 31, h8 = (lane >> 5) * 8;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+    if (kt + 1 < nk) gload((kt0 + kt + 1) * BK);
 #pragma unroll
     for (int s16 = 0; s16 < BK; s16 += 16) {
-      f16x8 ah[2], al[2], bh[2], bl[2];
+      V8 ah[WMB], bh[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        ah[i] = *reinterpret_cast<const f16x8*>(&Ah[cur][wm * 64 + i * 32 + r][s16 + h8]);
-        al[i] = *reinterpret_cast<const f16x8*>(&Al[cur][wm * 64 + i * 32 + r][s16 + h8]);
-        bh[i] = *reinterpret_cast<const f16x8*>(&Bh[cur][wn * 64 + i * 32 + r][s16 + h8]);
-        bl[i] = *reinterpret_cast<const f16x8*>(&Bl[cur][wn * 64 + i * 32 + r][s16 + h8]);
+      for (int i = 0; i < WMB; ++i) ah[i] = *reinterpret_cast<const V8*>(&As[0][cur][wm * 32 * WMB + i * 32 + r][s16 + h8]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bh[j] = *reinterpret_cast<const V8*>(&Bs[0][cur][wn * 64 + j * 32 + r][s16 + h8]);
+      if constexpr (MODE == 1) {
+        V8 al[WMB], bl[2];
+#pragma unroll
+        for (int i = 0; i < WMB; ++i)
+          al[i] = *reinterpret_cast<const V8*>(&As[NPL - 1][cur][wm * 32 * WMB + i * 32 + r][s16 + h8]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bl[j] = *reinterpret_cast<const V8*>(&Bs[NPL - 1][cur][wn * 64 + j * 32 + r][s16 + h8]);
+#pragma unroll
+        for (int i = 0; i < WMB; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < WMB; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
     }
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
+  if constexpr (MODE == 1) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WMB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] *= X3_UNSCALE;
-      epilogue_tile(g, acc[i][j], m0 + wm * 64 + i * 32, n0 + wn * 64 + j * 32, lane);
-    }
+        for (int q = 0; q < 16; ++q) acc[i][j][q] *= X3_UNSCALE;
+  }
+  if (g.ksplit > 1) {  // raw partial tile -> kpart[z][M][N]
+    float* P = g.kpart + (long)blockIdx.z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < WMB; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+        if (col >= g.N) continue;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int row = m0 + wm * 32 * WMB + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+          if (row < g.M) P[(long)row * g.N + col] = acc[i][j][q];
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < WMB; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) epilogue_tile(g, acc[i][j], m0 + wm * 32 * WMB + i * 32, n0 + wn * 64 + j * 32, lane);
 }
 
 template <int WMB, int WNB>
@@ -336,10 +408,35 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   else if (a.a_mode == A_CONV1D) va = va && (a.C % 4 == 0) && (a.xs_t % 4 == 0) && (a.xs_b % 4 == 0);
   else va = va && (a.C % 4 == 0);
   if (a.split16) {
-    dim3 grid(cdiv(a.N, 128), cdiv(a.M, 128));
-    if (va) hipLaunchKernelGGL(gemm_x3_kernel<true>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(gemm_x3_kernel<false>, grid, dim3(256), 0, s, a);
+    const int wm16 = a.M <= 64 ? 1 : 2;
+    GemmArgs g = a;
+    g.ksplit = 1;
+    const long tiles = (long)cdiv(a.N, 128) * cdiv(a.M, 64 * wm16);
+    if (a.kpart) {  // split K until ~kTarget work-groups, >= 4 k tiles (128 k) per split
+      static const long kTarget = [] {
+        const char* e = std::getenv("TT2_SPLITK16_TARGET");
+        return e ? std::max(1L, std::atol(e)) : 512L;
+      }();
+      int ks = (int)std::min<long>(kTarget / std::max<long>(tiles, 1), cdiv(a.K, X3_BK) / 4);
+      ks = std::max(1, std::min(ks, 32));
+      while (ks > 1 && (long)ks * a.M * a.N > a.kpart_floats) --ks;
+      g.ksplit = ks;
+    }
+    dim3 grid(cdiv(a.N, 128), cdiv(a.M, 64 * wm16), g.ksplit);
+#define TT2_X3(VA_, MODE_, WMB_) hipLaunchKernelGGL((gemm_x3_kernel<VA_, MODE_, WMB_>), grid, dim3(256), 0, s, g)
+    if (a.split16 == 1) {
+      if (wm16 == 2) { if (va) TT2_X3(true, 1, 2); else TT2_X3(false, 1, 2); }
+      else { if (va) TT2_X3(true, 1, 1); else TT2_X3(false, 1, 1); }
+    } else {
+      if (wm16 == 2) { if (va) TT2_X3(true, 2, 2); else TT2_X3(false, 2, 2); }
+      else { if (va) TT2_X3(true, 2, 1); else TT2_X3(false, 2, 1); }
+    }
+#undef TT2_X3
     TT2_HIP(hipGetLastError());
+    if (g.ksplit > 1) {
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256)), dim3(256), 0, s, g);
+      TT2_HIP(hipGetLastError());
+    }
     return;
   }
   const bool vb = al16(a.Bw) && (a.ldb % 4 == 0);
@@ -348,10 +445,14 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   const int wmb = tiles22 >= 512 ? 2 : 1;
   GemmArgs g = a;
   g.ksplit = 1;
-  if (a.kpart) {  // split K until ~256 work-groups, >= 8 k tiles (128 k) per split
+  if (a.kpart) {  // split K until ~kTarget work-groups, >= 8 k tiles (128 k) per split
+    static const long kTarget = [] {
+      const char* e = std::getenv("TT2_SPLITK_TARGET");
+      return e ? std::max(1L, std::atol(e)) : 512L;
+    }();
     const long tiles = (long)cdiv(a.M, 64 * wmb) * cdiv(a.N, 64 * wnb);
     const int nkt = cdiv(a.K, 16);
-    int ks = (int)std::min<long>(256 / std::max<long>(tiles, 1), nkt / 8);
+    int ks = (int)std::min<long>(kTarget / std::max<long>(tiles, 1), nkt / 8);
     ks = std::max(1, std::min(ks, 32));
     while (ks > 1 && (long)ks * a.M * a.N > a.kpart_floats) --ks;
     g.ksplit = ks;

@@ -651,6 +651,7 @@ static void tr_colsum(tt2_train_ctx* c, const float* in, long M, int N, long ld,
 }
 
 static DevBuf* g_tr_kpart = nullptr;  // split-K scratch of the context being driven (stream-ordered)
+static int g_tr_prec = 0;             // GemmArgs::split16 of the context being driven (0 fp32, 2 bf16)
 
 static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
                     hipStream_t s, const float* bias = nullptr, const float* residual = nullptr, long ldr = 0,
@@ -662,6 +663,7 @@ static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* 
   }
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.Bw = Bw; g.ldb = ldb; g.Cout = C; g.ldc = ldc;
   g.bias = bias; g.residual = residual; g.ldr = ldr; g.act = act;
+  g.split16 = g_tr_prec;
   gemm(g, s);
 }
 
@@ -751,6 +753,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   c->T_last = T;
   c->Tin_last = Tin;
   g_tr_kpart = &c->kpart;
+  g_tr_prec = c->cfg.precision ? 2 : 0;
   // weight transposes for the backward products
   tr_transpose(pvar(c, L1V("kernel")), LX1, 4 * H, 4 * H, c->K1T.as<float>(), LX1, s);
   tr_transpose(pvar(c, L2V("kernel")), 2 * H, 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, s);
@@ -916,6 +919,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 64 * nreg, c->cfg.reg_weight,
                      red + 2, 0);
   g_tr_kpart = nullptr;
+  g_tr_prec = 0;
 }
 
 static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s) {
@@ -953,6 +957,7 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   c->adam_beta2 = 0.999f;
   c->adam_epsilon = 1e-6f;
   c->clip_norm = 1.0f;
+  c->precision = 0;
 }
 
 tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_train_ctx** out) {

@@ -28,7 +28,7 @@ def learning_rate(step, hp):
     return min(max(lr, hp.tacotron_final_learning_rate), init)
 
 
-def train_config(hp, batch, max_T_in, max_T_out, emt_only=False):
+def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32"):
     lib = _lib.load_library()
     cfg = _lib.TrainConfig()
     lib.tt2_train_default_config(ctypes.byref(cfg), batch, max_T_in, max_T_out)
@@ -57,6 +57,9 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False):
     cfg.adam_beta2 = hp.tacotron_adam_beta2
     cfg.adam_epsilon = hp.tacotron_adam_epsilon
     cfg.clip_norm = 1.0 if hp.tacotron_clip_gradients else 0.0
+    if precision not in ("fp32", "bf16"):
+        raise ValueError("precision must be 'fp32' or 'bf16'")
+    cfg.precision = 1 if precision == "bf16" else 0
     return cfg
 
 
@@ -64,13 +67,14 @@ class TacotronTrainer(object):
     """One tt2_train_ctx on one GPU.  Inputs may be numpy arrays or torch tensors; everything
     runs on the trainer's own torch stream (passed to the library explicitly)."""
 
-    def __init__(self, hp, weights, batch, max_T_in, max_T_out, device=0, emt_only=False):
+    def __init__(self, hp, weights, batch, max_T_in, max_T_out, device=0, emt_only=False,
+                 precision="fp32"):
         import torch
         self.torch = torch
         self.lib = _lib.load_library()
         self.hp = hp
         self.device = torch.device("cuda", device)
-        self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only)
+        self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only, precision)
         self.B = batch
         h = ctypes.c_void_p()
         check(self.lib.tt2_train_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))

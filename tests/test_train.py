@@ -192,3 +192,41 @@ def test_gpu_train_adam_updates_match_oracle():
                 assert np.abs(got - p[n]).max() < 1e-6 + 1e-5 * np.abs(p[n]).max(), n
     finally:
         tr.close()
+
+
+@pytest.mark.gpu
+def test_gpu_train_bf16_gemms_close_to_oracle():
+    """configs[4]'s bf16 mode (bf16 GEMM operands, fp32 accumulation / state / optimizer) against
+    the float64 oracle at fork-default widths: a mixed-precision tolerance, not parity."""
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    hp.override_from_dict(dict(attention_dim=128, attention_filters=32, prenet_layers=[256, 256],
+                               decoder_lstm_units=1024))
+    B, T_in, T_out = 4, 37, 10
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16")
+    try:
+        tr.forward_backward(mem, lens, tg, st, pm, zm)
+        L = tr.losses()
+        fr, sl, al = tr.outputs(T_in, T_out)
+        grads = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in TRN.train_var_names()}
+    finally:
+        tr.close()
+    out, (b, s, r), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight)
+    errs = {n: _rel(grads[n], g[n]) for n in TRN.train_var_names()}
+    frob = {n: float(np.linalg.norm(grads[n] - g[n]) / max(np.linalg.norm(g[n]), 1e-30))
+            for n in TRN.train_var_names()}
+    for n in TRN.train_var_names():
+        print("  {:90s} maxrel {:.3e} frob {:.3e}".format(n, errs[n], frob[n]))
+    print("bf16 frames max|err| {:.3e}, loss rel {:.3e}, worst grad {}".format(
+        float(np.abs(fr - out["frames"]).max()), abs(L["before"] - b) / b,
+        max(errs.items(), key=lambda kv: kv[1])))
+    assert np.abs(fr - out["frames"]).max() < 1e-2
+    assert abs(L["before"] - b) < 1e-3 * b
+    for n, e in errs.items():
+        if "prenet" in n:
+            # bf16-rounded prenet pre-activations near 0 flip ReLU/keep decisions; over the 40
+            # rows of this case one flip moves a whole row's contribution (measured 2-6 %)
+            assert frob[n] < 0.1, (n, frob[n])
+        else:
+            assert e < 1e-2, (n, e)  # measured 0.2-0.5 % (bf16 operand rounding)
