@@ -63,3 +63,20 @@ def gather_padded(local, lengths, group=None, pad_value=0.0):
         for i in range(nb):
             res.append(o[i, :int(ls[i])])
     return res
+
+
+def tower_mean_(flat_grads, group=None):
+    """Data-parallel training: the reference averages the per-tower gradients on the CPU
+    (Tacotron.get_clipped_grads, tacotron.py:1194-1208: reduce_mean over the tower axis) before
+    clip_by_global_norm; here each rank is one tower and the mean is one all-reduce (SUM, then
+    divide) over the flat gradient buffer, in place.  RCCL over xGMI for CUDA tensors ("nccl"),
+    gloo for CPU tensors."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return flat_grads
+    world = dist.get_world_size(group)
+    if world == 1:
+        return flat_grads
+    dist.all_reduce(flat_grads, op=dist.ReduceOp.SUM, group=group)
+    flat_grads.div_(world)
+    return flat_grads

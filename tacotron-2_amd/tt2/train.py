@@ -145,10 +145,10 @@ class TacotronTrainer(object):
         import torch.distributed as dist
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return
+        from .parallel import tower_mean_
         buf = self.bind_grad_buffer()
         with self.torch.cuda.stream(self.stream):
-            dist.all_reduce(buf, group=group)
-            buf.div_(dist.get_world_size(group))
+            tower_mean_(buf, group)
 
     def apply(self, global_step=None, lr=None):
         """clip_by_global_norm(1.0) + Adam at update count ``global_step`` (1-based)."""

@@ -141,3 +141,64 @@ def test_gloo_sharded_e2e_gathers_in_global_order(tmp_path, world):
         assert len(got) == 5
         for g, w in zip(got, ref):
             np.testing.assert_array_equal(g, w)
+
+
+def _train_worker(rank, world, port, out_dir):
+    """Each rank = one tower: oracle gradients on its shard of the batch, flattened in the
+    library's variable order, tower-averaged with tt2.parallel.tower_mean_ over gloo."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "tacotron-2_amd"), root, os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from _common import small_hparams
+    from oracle import train_ref as TRN
+    from tt2.parallel import shard, shard_range, tower_mean_
+    from tt2.synthetic import prenet_masks, train_batch, zoneout_masks
+    from tt2.weights import init_tacotron_weights, memory_width
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    hp = small_hparams()
+    W = init_tacotron_weights(hp, seed=5339)
+    B, T_in, T = 4, 7, 5
+    mem, lens, tg, st = train_batch(B, T_in, T, memory_width(hp), seed=3)
+    pm = prenet_masks(T, B, hp.prenet_layers[0], seed=3)
+    zm = zoneout_masks(T, B, hp.decoder_lstm_units, seed=3)
+    m, l, t, s = shard([mem, lens, tg, st], rank, world)
+    sl = slice(*shard_range(B, rank, world))
+    _, _, g = TRN.train_grads(W, m, l, t, s, pm[:, :, sl], zm[:, :, sl], hp.tacotron_reg_weight)
+    flat = torch.from_numpy(np.concatenate([g[n].ravel() for n in TRN.train_var_names()]))
+    tower_mean_(flat)
+    np.save(os.path.join(out_dir, "grads_{}.npy".format(rank)), flat.numpy())
+    dist.destroy_process_group()
+
+
+def test_train_tower_mean_over_two_ranks(tmp_path):
+    """world_size 2 (gloo): the all-reduced flat gradients equal the reference's tower mean —
+    the average of the two towers' gradients computed separately — on every rank."""
+    import sys
+    from _common import small_hparams
+    from oracle import train_ref as TRN
+    from tt2.synthetic import prenet_masks, train_batch, zoneout_masks
+    from tt2.weights import init_tacotron_weights, memory_width
+    world = 2
+    mp.spawn(_train_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    hp = small_hparams()
+    W = init_tacotron_weights(hp, seed=5339)
+    B, T_in, T = 4, 7, 5
+    mem, lens, tg, st = train_batch(B, T_in, T, memory_width(hp), seed=3)
+    pm = prenet_masks(T, B, hp.prenet_layers[0], seed=3)
+    zm = zoneout_masks(T, B, hp.decoder_lstm_units, seed=3)
+    towers = []
+    for r in range(world):
+        s, e = shard_range(B, r, world)
+        _, _, g = TRN.train_grads(W, mem[s:e], lens[s:e], tg[s:e], st[s:e], pm[:, :, s:e],
+                                  zm[:, :, s:e], hp.tacotron_reg_weight)
+        towers.append(np.concatenate([g[n].ravel() for n in TRN.train_var_names()]))
+    want = (towers[0] + towers[1]) / 2
+    for r in range(world):
+        got = np.load(str(tmp_path / "grads_{}.npy".format(r)))
+        np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15)
