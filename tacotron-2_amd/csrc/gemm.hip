@@ -418,7 +418,7 @@ void gemm(const GemmArgs& a, hipStream_t s) {
         return e ? std::max(1L, std::atol(e)) : 512L;
       }();
       int ks = (int)std::min<long>(kTarget / std::max<long>(tiles, 1), cdiv(a.K, X3_BK) / 4);
-      ks = std::max(1, std::min(ks, 32));
+      ks = std::max(1, std::min(ks, 256));
       while (ks > 1 && (long)ks * a.M * a.N > a.kpart_floats) --ks;
       g.ksplit = ks;
     }
@@ -453,7 +453,7 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     const long tiles = (long)cdiv(a.M, 64 * wmb) * cdiv(a.N, 64 * wnb);
     const int nkt = cdiv(a.K, 16);
     int ks = (int)std::min<long>(kTarget / std::max<long>(tiles, 1), nkt / 8);
-    ks = std::max(1, std::min(ks, 32));
+    ks = std::max(1, std::min(ks, 256));
     while (ks > 1 && (long)ks * a.M * a.N > a.kpart_floats) --ks;
     g.ksplit = ks;
   }

@@ -56,8 +56,8 @@ struct tt2_train_ctx {
   DevBuf values, keys, X1, X2, PIN, G1, G2, C1, C2, CN1, CN2, Q, ALIGN, CUM, P1, XIN, FR, ST;
   // backward
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DH2, DCTX, DKEYS, DCUM;
-  DevBuf dV, dBA, dWL, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
-  DevBuf TH, E, DA, DF, PQ;
+  DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
+  DevBuf TH, E, DA, DF, PQ, FALL, ALN;
   int T_last = 0, Tin_last = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
@@ -235,7 +235,9 @@ struct TrAtt {
   const float* ba;      // [A]
   float* ALIGN;         // [B][Tin][T]
   float* CUM;           // [(T+1)][B][Tin]
-  float* TH;            // [T][B][Tin][A] tanh(keys + q + loc + b_a), kept for the backward
+  float* TH;            // [T][B][Tin][A] tanh(keys + q + loc + b_a); the backward overwrites it with du
+  float* FALL;          // [T][B][Tin][F] location features (for d W_loc = Σ f^T du after the loop)
+  float* ALN;           // [T][B][Tin] alignments, time-major copy for coalesced backward reads
   float* E;             // [B][Tin] energies of the current step
   // forward outputs of the context
   float* PIN;
@@ -252,7 +254,6 @@ struct TrAtt {
   float* DCUM;   // [B][Tin]
   float* dV;     // [B][nt][A]   accumulated over steps
   float* dBA;    // [B][nt][A]
-  float* dWL;    // [B][nt][F][A]
   float* dKC;    // [B][nt][KW][F]
   float* dBC;    // [B][nt][F]
 };
@@ -287,6 +288,10 @@ __global__ __launch_bounds__(256) void k_tr_att_energy(TrAtt a) {
   tr_locf_tile(a, b, j0, cseg, f);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long tb = (long)a.t * a.B + b;
+  for (int i = threadIdx.x; i < TR_JT * a.F; i += blockDim.x) {
+    const int j = j0 + i / a.F;
+    if (j < a.Tin) a.FALL[(tb * a.Tin + j0) * a.F + i] = f[i];
+  }
   const float* q = a.Q + tb * a.A;
   for (int jj = wave; jj < TR_JT; jj += 4) {
     const int j = j0 + jj;
@@ -329,6 +334,7 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
     al[j] = x;
     if (blockIdx.x == 0) {
       a.ALIGN[((long)b * a.Tin + j) * a.T + a.t] = x;
+      a.ALN[tb * a.Tin + j] = x;
       a.CUM[(tb + a.B) * a.Tin + j] = a.CUM[tb * a.Tin + j] + x;
     }
   }
@@ -456,10 +462,8 @@ __global__ __launch_bounds__(256) void k_tr_att_dalign(TrAtt a) {
 }
 
 // (2) softmax backward de_j = a_j (da_j - Σ a·da), tanh backward du_jk = de_j v_k (1 - th²):
-// d keys (+=), per-tile partials of d v_a, d b_a (= d q), d W_loc = f^T du, and d f = du · W_loc^T
+// d keys (+=), per-tile partials of d v_a, d b_a (= d q), du kept for d W_loc, d f = du · W_loc^T
 __global__ __launch_bounds__(256) void k_tr_att_energy_bwd(TrAtt a) {
-  __shared__ float cseg[TR_JT + 64];
-  __shared__ float f[TR_JT * 32];
   __shared__ float WlT[256 * 33];
   __shared__ float dU[TR_JT * 256];
   __shared__ float de[TR_JT];
@@ -470,14 +474,14 @@ __global__ __launch_bounds__(256) void k_tr_att_energy_bwd(TrAtt a) {
   const int len = a.lens[b];
   float s = 0.f;
   for (int j = tid; j < len; j += blockDim.x)
-    s += a.ALIGN[((long)b * a.Tin + j) * a.T + a.t] * a.DA[(long)b * a.Tin + j];
+    s += a.ALN[tb * a.Tin + j] * a.DA[(long)b * a.Tin + j];
   s = block_sum(s, s16);
   if (tid < TR_JT) {
     const int j = j0 + tid;
-    de[tid] = j < len ? a.ALIGN[((long)b * a.Tin + j) * a.T + a.t] * (a.DA[(long)b * a.Tin + j] - s) : 0.f;
+    de[tid] = j < len ? a.ALN[tb * a.Tin + j] * (a.DA[(long)b * a.Tin + j] - s) : 0.f;
   }
   for (int i = tid; i < a.F * a.A; i += blockDim.x) WlT[(i % a.A) * 33 + i / a.A] = a.Wl[i];
-  tr_locf_tile(a, b, j0, cseg, f);  // syncs
+  __syncthreads();
   const int NJ = blockDim.x / a.A, k = tid % a.A, js = tid / a.A;
   const float vak = a.va[k];
   float dv = 0.f, dq = 0.f;
@@ -485,11 +489,13 @@ __global__ __launch_bounds__(256) void k_tr_att_energy_bwd(TrAtt a) {
     const int j = j0 + jj;
     float du = 0.f;
     if (j < a.Tin) {
-      const float th = a.TH[(tb * a.Tin + j) * a.A + k];
+      const long hidx = (tb * a.Tin + j) * a.A + k;
+      const float th = a.TH[hidx];
       du = de[jj] * vak * (1.f - th * th);
       dv += de[jj] * th;
       dq += du;
       a.DKEYS[((long)b * a.Tin + j) * a.A + k] += du;
+      a.TH[hidx] = du;  // d W_loc = FALL^T · du as one GEMM after the loop
     }
     dU[jj * a.A + k] = du;
   }
@@ -506,13 +512,6 @@ __global__ __launch_bounds__(256) void k_tr_att_energy_bwd(TrAtt a) {
     a.PQ[pt * a.A + tid] = sq;
     a.dV[pt * a.A + tid] += sv;
     a.dBA[pt * a.A + tid] += sq;
-  }
-  for (int i = tid; i < a.F * a.A; i += blockDim.x) {
-    const int c = i / a.A, kk = i % a.A;
-    float acc = 0.f;
-#pragma unroll 4
-    for (int jj = 0; jj < TR_JT; ++jj) acc += f[jj * a.F + c] * dU[jj * a.A + kk];
-    a.dWL[pt * a.F * a.A + i] += acc;
   }
   for (int i = tid; i < TR_JT * a.F; i += blockDim.x) {
     const int jj = i / a.F, c = i % a.F, j = j0 + jj;
@@ -734,10 +733,10 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->R1, B * LX1); f(c->R2, B * 2 * H); f(c->DQ, TB * A); f(c->DH2, B * H); f(c->DCTX, TB * D);
   const long NT = (Tin + TR_JT - 1) / TR_JT;
   f(c->DKEYS, B * Tin * A); f(c->DCUM, B * Tin); f(c->dV, B * NT * A); f(c->dBA, B * NT * A);
-  f(c->dWL, B * NT * F * A); f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F);
+  f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F); f(c->FALL, TB * Tin * F); f(c->ALN, TB * Tin);
   f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DA, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
   f(c->dZ, TB * P); f(c->dPre, TB * P);
-  const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM});
+  const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM, TB * Tin * F});
   f(c->TBUF, tmax);
   f(c->part, 64 * std::max<long>(4 * H, LX1) + 4096);
   f(c->red, 64);
@@ -796,7 +795,8 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   at.ALIGN = c->ALIGN.as<float>(); at.CUM = c->CUM.as<float>(); at.PIN = PIN; at.X1 = X1;
   at.dPIN = c->dPIN.as<float>(); at.dX1 = c->dX1.as<float>(); at.DCTX = c->DCTX.as<float>(); at.DQ = c->DQ.as<float>();
   at.DKEYS = c->DKEYS.as<float>(); at.DCUM = c->DCUM.as<float>(); at.dV = c->dV.as<float>(); at.dBA = c->dBA.as<float>();
-  at.dWL = c->dWL.as<float>(); at.dKC = c->dKC.as<float>(); at.dBC = c->dBC.as<float>();
+  at.dKC = c->dKC.as<float>(); at.dBC = c->dBC.as<float>();
+  at.FALL = c->FALL.as<float>(); at.ALN = c->ALN.as<float>();
   at.TH = c->TH.as<float>(); at.E = c->E.as<float>(); at.DA = c->DA.as<float>(); at.DF = c->DF.as<float>();
   at.PQ = c->PQ.as<float>();
   const int NT = (Tin + TR_JT - 1) / TR_JT;
@@ -839,7 +839,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_gemm((int)TB, H + D, 1, c->dST.as<float>(), 1, c->WsT.as<float>(), H + D, dPIN, H + D, s, nullptr, dPIN, H + D);
   TT2_HIP(hipMemsetAsync(dX1 + TB * LX1, 0, sizeof(float) * (size_t)B * LX1, s));
   TT2_HIP(hipMemsetAsync(dX2 + TB * 2 * H, 0, sizeof(float) * (size_t)B * 2 * H, s));
-  for (DevBuf* d : {&c->DC1, &c->DC2, &c->R1, &c->R2, &c->DKEYS, &c->DCUM, &c->dV, &c->dBA, &c->dWL, &c->dKC, &c->dBC})
+  for (DevBuf* d : {&c->DC1, &c->DC2, &c->R1, &c->R2, &c->DKEYS, &c->DCUM, &c->dV, &c->dBA, &c->dKC, &c->dBC})
     TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
   for (int t = T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
@@ -894,7 +894,11 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   const long BNT = (long)B * NT;
   tr_colsum(c, c->dV.as<float>(), BNT, A, A, gvar(c, LAV("attention_variable_projection")), s);
   tr_colsum(c, c->dBA.as<float>(), BNT, A, A, gvar(c, LAV("attention_bias")), s);
-  tr_colsum(c, c->dWL.as<float>(), BNT, F * A, (long)F * A, gvar(c, LAV("location_features_layer/kernel")), s);
+  {  // d W_loc = Σ_{t,b,j} f ⊗ du over all T·B·Tin rows
+    const long R = TB * Tin;
+    tr_transpose(c->FALL.as<float>(), R, F, F, TBUF, R, s);
+    tr_gemm(F, A, (int)R, TBUF, R, c->TH.as<float>(), A, gvar(c, LAV("location_features_layer/kernel")), A, s);
+  }
   tr_colsum(c, c->dKC.as<float>(), BNT, KW * F, (long)KW * F,
             gvar(c, LAV("location_features_convolution/kernel")), s);
   tr_colsum(c, c->dBC.as<float>(), BNT, F, F, gvar(c, LAV("location_features_convolution/bias")), s);
