@@ -41,6 +41,11 @@ struct GemmArgs {
   // blockIdx.z so a 64-row GEMM fills the chip; raw partials go to kpart (>= kpart_floats floats,
   // caller-owned, stream-ordered) and one reduce launch applies the epilogue.
   float* kpart = nullptr;
+  // split16 == 2 only: B given pre-transposed in bf16, Bt16[n * ldbt + k] (ldbt % 8 == 0, 16-byte
+  // aligned) -- half the weight bytes and one 16-byte load per 8 k (training weights, converted
+  // once per optimizer step).  Bw is ignored when set.
+  const void* Bt16 = nullptr;
+  long ldbt = 0;
   long kpart_floats = 0;
   int ksplit = 1;  // set by the dispatcher
 };

@@ -248,7 +248,7 @@ __device__ __forceinline__ void to_bf16x8(const float* v, bf16x8& o) {
 // k-slab, fp32 accumulation -- the mixed-precision training GEMM).  Block (64·WMB) x 128 x 32,
 // 4 waves in a 2x2 grid, each wave WMB x 2 tiles of 32x32; split-K over blockIdx.z as in
 // gemm_kernel (raw partials to kpart, epilogue in gemm_splitk_reduce).
-template <bool VA, int MODE, int WMB>
+template <bool VA, int MODE, int WMB, bool BT = false>
 __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
   constexpr int BM = 64 * WMB, BN = 128, BK = X3_BK;
   constexpr int EA = BM * BK / 256;            // A elements per thread (16 or 8)
@@ -264,6 +264,8 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
   const int am = tid / TPR_A, ak = (tid % TPR_A) * EA;  // A: row am, k [ak, ak+EA)
   const int bn = tid & 127, bk = (tid >> 7) * 16;       // B: col bn, k [bk, bk+16) (coalesced over n)
   float ra[EA], rb[16];
+  bf16x8 rbt[2];  // MODE 2 with Bt16: 16 pre-converted k values of column n
+  constexpr bool bt = MODE == 2 && BT;  // B from g.Bt16 (pre-transposed bf16)
   f32x16 acc[WMB][2];
 #pragma unroll
   for (int i = 0; i < WMB; ++i)
@@ -276,6 +278,21 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
 #pragma unroll
     for (int e = 0; e < EA; e += 4) load_a4<VA>(g, m0 + am, k0 + ak + e, &ra[e]);
     const int n = n0 + bn;
+    if constexpr (bt) {
+      const __bf16* src = reinterpret_cast<const __bf16*>(g.Bt16) + (long)n * g.ldbt + k0 + bk;
+      const int k = k0 + bk;
+      if (n < g.N && k + 16 <= g.K) {
+        rbt[0] = *reinterpret_cast<const bf16x8*>(src);
+        rbt[1] = *reinterpret_cast<const bf16x8*>(src + 8);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const __bf16 v = (n < g.N && k + e < g.K) ? src[e] : (__bf16)0.f;
+          if (e < 8) rbt[0][e] = v; else rbt[1][e - 8] = v;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int k = k0 + bk + e;
@@ -306,7 +323,11 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        to_bf16x8(&rb[8 * q], h);
+        if constexpr (bt) {
+          h = rbt[q];
+        } else {
+          to_bf16x8(&rb[8 * q], h);
+        }
         *reinterpret_cast<bf16x8*>(&Bs[0][buf][bn][bk + 8 * q]) = h;
       }
     }
@@ -408,6 +429,8 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   else if (a.a_mode == A_CONV1D) va = va && (a.C % 4 == 0) && (a.xs_t % 4 == 0) && (a.xs_b % 4 == 0);
   else va = va && (a.C % 4 == 0);
   if (a.split16) {
+    TT2_CHECK(!a.Bt16 || (a.split16 == 2 && al16(a.Bt16) && a.ldbt % 8 == 0), TT2_ERR_INVALID_ARG,
+              "gemm: Bt16 needs split16 == 2, 16-byte alignment and ldbt % 8 == 0");
     const int wm16 = a.M <= 64 ? 1 : 2;
     GemmArgs g = a;
     g.ksplit = 1;
@@ -427,6 +450,11 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     if (a.split16 == 1) {
       if (wm16 == 2) { if (va) TT2_X3(true, 1, 2); else TT2_X3(false, 1, 2); }
       else { if (va) TT2_X3(true, 1, 1); else TT2_X3(false, 1, 1); }
+    } else if (a.Bt16) {
+#define TT2_X3B(VA_, WMB_) hipLaunchKernelGGL((gemm_x3_kernel<VA_, 2, WMB_, true>), grid, dim3(256), 0, s, g)
+      if (wm16 == 2) { if (va) TT2_X3B(true, 2); else TT2_X3B(false, 2); }
+      else { if (va) TT2_X3B(true, 1); else TT2_X3B(false, 1); }
+#undef TT2_X3B
     } else {
       if (wm16 == 2) { if (va) TT2_X3(true, 2, 2); else TT2_X3(false, 2, 2); }
       else { if (va) TT2_X3(true, 2, 1); else TT2_X3(false, 2, 1); }

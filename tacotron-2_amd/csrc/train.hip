@@ -58,6 +58,8 @@ struct tt2_train_ctx {
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DH2, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
   DevBuf TH, E, DA, DF, PQ, FALL, ALN;
+  // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
+  DevBuf hK1, hK1T, hK2, hK2T, hWq, hWqT;
   int T_last = 0, Tin_last = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
@@ -140,6 +142,11 @@ __global__ void k_tr_colsum_final(const float* __restrict__ part, int S, int N, 
   float acc = 0.f;
   for (int s = 0; s < S; ++s) acc += part[(long)s * N + n];
   out[n] = acc;
+}
+
+__global__ void k_tr_to_bf16(const float* __restrict__ src, long n, __bf16* __restrict__ dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (__bf16)src[i];
 }
 
 // ---- forward -------------------------------------------------------------------------------
@@ -654,8 +661,12 @@ static int g_tr_prec = 0;             // GemmArgs::split16 of the context being 
 
 static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
                     hipStream_t s, const float* bias = nullptr, const float* residual = nullptr, long ldr = 0,
-                    int act = ACT_NONE) {
+                    int act = ACT_NONE, const DevBuf* bt16 = nullptr, long ldbt = 0) {
   GemmArgs g;
+  if (g_tr_prec == 2 && bt16 && bt16->p && ldbt % 8 == 0) {  // weights pre-converted: B^T in bf16
+    g.Bt16 = bt16->p;
+    g.ldbt = ldbt;
+  }
   if (g_tr_kpart) {
     g.kpart = g_tr_kpart->as<float>();
     g.kpart_floats = (long)(g_tr_kpart->bytes / sizeof(float));
@@ -740,6 +751,11 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->TBUF, tmax);
   f(c->part, 64 * std::max<long>(4 * H, LX1) + 4096);
   f(c->red, 64);
+  if (c->cfg.precision) {
+    auto h = [](DevBuf& d, long n) { d.alloc(2 * (size_t)std::max<long>(n, 1)); };
+    h(c->hK1, LX1 * 4 * H); h(c->hK1T, LX1 * 4 * H); h(c->hK2, 8 * H * H); h(c->hK2T, 8 * H * H);
+    h(c->hWq, H * A); h(c->hWqT, H * A);
+  }
   f(c->kpart, 4L << 20);
 }
 
@@ -761,6 +777,17 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_transpose(pvar(c, SPV("kernel")), H + D, 1, 1, c->WsT.as<float>(), H + D, s);
   tr_transpose(pvar(c, vn("memory_layer/kernel")), D, A, A, c->WmT.as<float>(), D, s);
   tr_transpose(pvar(c, PRV(2, "kernel")), P, P, P, c->Wp2T.as<float>(), P, s);
+  if (c->cfg.precision) {
+    auto cv = [&](const float* src, long n, DevBuf& d) {
+      hipLaunchKernelGGL(k_tr_to_bf16, dim3(nblk(n)), dim3(256), 0, s, src, n, d.as<__bf16>());
+    };
+    cv(pvar(c, L1V("kernel")), (long)LX1 * 4 * H, c->hK1);
+    cv(c->K1T.as<float>(), (long)LX1 * 4 * H, c->hK1T);
+    cv(pvar(c, L2V("kernel")), 8L * H * H, c->hK2);
+    cv(c->K2T.as<float>(), 8L * H * H, c->hK2T);
+    cv(pvar(c, vn("decoder/query_layer/kernel")), (long)H * A, c->hWq);
+    cv(c->WqT.as<float>(), (long)H * A, c->hWqT);
+  }
   TT2_HIP(hipMemsetAsync(c->grads, 0, sizeof(float) * c->total, s));
 
   // ---- forward ----
@@ -807,19 +834,19 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   for (int t = 0; t < T; ++t) {
     const long s1 = (long)t * B;
     tr_gemm(B, 4 * H, LX1, X1 + s1 * LX1, LX1, pvar(c, L1V("kernel")), 4 * H, c->G1.as<float>() + s1 * 4 * H, 4 * H, s,
-            pvar(c, L1V("bias")));
+            pvar(c, L1V("bias")), nullptr, 0, ACT_NONE, &c->hK1T, LX1);
     TrLstmFwd l1{c->G1.as<float>() + s1 * 4 * H, c->C1.as<float>() + s1 * H, X1 + s1 * LX1 + P + D, LX1, zm, t, 0, B, H,
                  z, c->CN1.as<float>() + s1 * H, c->C1.as<float>() + (s1 + B) * H, X2 + s1 * 2 * H, 2 * H,
                  X1 + (s1 + B) * LX1 + P + D, LX1};
     hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l1);
     tr_gemm(B, 4 * H, 2 * H, X2 + s1 * 2 * H, 2 * H, pvar(c, L2V("kernel")), 4 * H, c->G2.as<float>() + s1 * 4 * H,
-            4 * H, s, pvar(c, L2V("bias")));
+            4 * H, s, pvar(c, L2V("bias")), nullptr, 0, ACT_NONE, &c->hK2T, 2 * H);
     TrLstmFwd l2{c->G2.as<float>() + s1 * 4 * H, c->C2.as<float>() + s1 * H, X2 + s1 * 2 * H + H, 2 * H, zm, t, 1, B,
                  H, z, c->CN2.as<float>() + s1 * H, c->C2.as<float>() + (s1 + B) * H, PIN + s1 * (H + D), H + D,
                  X2 + (s1 + B) * 2 * H + H, 2 * H};
     hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l2);
     tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
-            c->Q.as<float>() + s1 * A, A, s);
+            c->Q.as<float>() + s1 * A, A, s, nullptr, nullptr, 0, ACT_NONE, &c->hWqT, H);
     at.t = t;
     hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(256), 0, s, at);
     hipLaunchKernelGGL(k_tr_ctx, dim3((D + 255) / 256, B), dim3(256), sizeof(float) * Tin, s, at);
@@ -848,19 +875,19 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(256), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
     tr_gemm(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, c->DH2.as<float>(), H, s, nullptr,
-            dPIN + s1 * (H + D), H + D);
+            dPIN + s1 * (H + D), H + D, ACT_NONE, &c->hWq, A);
     TrLstmBwd b2{c->DH2.as<float>(), H, dX2 + (s1 + B) * 2 * H + H, 2 * H, c->DC2.as<float>(),
                  c->G2.as<float>() + s1 * 4 * H, c->CN2.as<float>() + s1 * H, c->C2.as<float>() + s1 * H, zm, t, 1, B,
                  H, z, c->dG2.as<float>() + s1 * 4 * H, c->R2.as<float>(), 2 * H, H};
     hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b2);
     tr_gemm(B, 2 * H, 4 * H, c->dG2.as<float>() + s1 * 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, dX2 + s1 * 2 * H,
-            2 * H, s, nullptr, c->R2.as<float>(), 2 * H);
+            2 * H, s, nullptr, c->R2.as<float>(), 2 * H, ACT_NONE, &c->hK2, 4 * H);
     TrLstmBwd b1{dX2 + s1 * 2 * H, 2 * H, dX1 + (s1 + B) * LX1 + P + D, LX1, c->DC1.as<float>(),
                  c->G1.as<float>() + s1 * 4 * H, c->CN1.as<float>() + s1 * H, c->C1.as<float>() + s1 * H, zm, t, 0, B,
                  H, z, c->dG1.as<float>() + s1 * 4 * H, c->R1.as<float>(), LX1, P + D};
     hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b1);
     tr_gemm(B, LX1, 4 * H, c->dG1.as<float>() + s1 * 4 * H, 4 * H, c->K1T.as<float>(), LX1, dX1 + s1 * LX1, LX1, s,
-            nullptr, c->R1.as<float>(), LX1);
+            nullptr, c->R1.as<float>(), LX1, ACT_NONE, &c->hK1, 4 * H);
   }
 
   // ---- weight gradients over all T·B rows ----
