@@ -319,6 +319,8 @@ typedef struct tt2_train_config {
   float clip_norm;         /* 1.0 (tacotron_clip_gradients); <= 0 disables */
   int precision;           /* 0 = fp32 GEMMs (parity); 1 = bf16 GEMM operands, fp32 accumulation,
                               fp32 master weights / cell state / optimizer (configs[4]) */
+  int clip_outputs;        /* 1: decoder_output = clip(frames, clip_lo, clip_hi) before the loss */
+  float clip_lo, clip_hi;  /* -max_abs_value - lower_bound_decay, max_abs_value (-4.1, 4) */
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;

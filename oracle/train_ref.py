@@ -115,9 +115,16 @@ def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneo
     return torch.stack(frames, 1), torch.stack(stops, 1), torch.stack(aligns, 2)
 
 
-def losses(frames, stop_logits, targets, stop_targets, W, reg_weight):
-    """before (tf.losses.mean_squared_error), stop (mean sigmoid CE, pos_weight 1), reg."""
-    before = ((frames - targets) ** 2).mean()
+def clip_decoder_output(frames, clip=(-4.1, 4.0)):
+    """tacotron.py:360-361: decoder_output = min(max(frames, lo - lower_bound_decay), hi) when
+    clip_outputs (T2_output_range = (-max_abs_value, max_abs_value) for symmetric mels)."""
+    return frames if clip is None else torch.clamp(frames, clip[0], clip[1])
+
+
+def losses(frames, stop_logits, targets, stop_targets, W, reg_weight, clip=(-4.1, 4.0)):
+    """before (tf.losses.mean_squared_error on the clipped decoder output), stop (mean sigmoid
+    CE, pos_weight 1), reg."""
+    before = ((clip_decoder_output(frames, clip) - targets) ** 2).mean()
     x, z = stop_logits, stop_targets
     stop = (torch.clamp(x, min=0) - x * z + torch.log1p(torch.exp(-x.abs()))).mean()
     reg = sum((v ** 2).sum() / 2 for n, v in W.items() if regularized(n)) * reg_weight
@@ -125,7 +132,7 @@ def losses(frames, stop_logits, targets, stop_targets, W, reg_weight):
 
 
 def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,
-                reg_weight=1e-6, dtype=torch.float64):
+                reg_weight=1e-6, dtype=torch.float64, clip=(-4.1, 4.0)):
     """One forward + backward; returns (outputs dict, losses tuple, grads dict incl. 'memory')."""
     names = train_var_names()
     W = {n: torch.tensor(np.asarray(Wnp[n]), dtype=dtype, requires_grad=True) for n in names}
@@ -135,11 +142,11 @@ def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneo
     pm = torch.tensor(np.asarray(prenet_masks), dtype=dtype)
     zm = None if zoneout_masks is None else torch.tensor(np.asarray(zoneout_masks), dtype=dtype)
     fr, sl, al = forward(W, mem, lengths, tg, pm, zm)
-    b, s, r = losses(fr, sl, tg, st, W, reg_weight)
+    b, s, r = losses(fr, sl, tg, st, W, reg_weight, clip)
     (b + s + r).backward()
     g = {n: W[n].grad.numpy() for n in names}
     g["memory"] = mem.grad.numpy()
-    out = dict(frames=fr.detach().numpy(), stop_logits=sl.detach().numpy(),
+    out = dict(frames=clip_decoder_output(fr, clip).detach().numpy(), stop_logits=sl.detach().numpy(),
                alignments=al.detach().numpy())
     return out, (b.item(), s.item(), r.item()), g
 

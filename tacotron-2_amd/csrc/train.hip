@@ -356,10 +356,10 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
 
 // frame MSE + stop sigmoid CE (tacotron.py:774,778-779) and their output gradients.  Frames are
 // time-major [T][B][NM]; targets [B][T][NM].  Deterministic per-block partials.
-__global__ __launch_bounds__(256) void k_tr_loss(const float* __restrict__ FR, const float* __restrict__ ST,
+__global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const float* __restrict__ ST,
                                                  const float* __restrict__ tg, const float* __restrict__ stg, int B,
-                                                 int T, int NM, float* __restrict__ dFR, float* __restrict__ dST,
-                                                 float* __restrict__ part) {
+                                                 int T, int NM, int clip, float lo, float hi, float* __restrict__ dFR,
+                                                 float* __restrict__ dST, float* __restrict__ part) {
   __shared__ float s4[16];
   const long nf = (long)T * B * NM;
   const float inv_f = 1.0f / (float)nf, inv_s = 1.0f / (float)((long)T * B);
@@ -368,9 +368,14 @@ __global__ __launch_bounds__(256) void k_tr_loss(const float* __restrict__ FR, c
     const int c = (int)(i % NM);
     const int b = (int)((i / NM) % B);
     const int t = (int)(i / ((long)NM * B));
-    const float d = FR[i] - tg[((long)b * T + t) * NM + c];
+    // decoder_output = clip(frames, lo, hi) when clip_outputs (tacotron.py:360-361); the clip's
+    // gradient passes where lo <= x <= hi (TF maximum/minimum)
+    const float x = FR[i];
+    const float y = clip ? fminf(fmaxf(x, lo), hi) : x;
+    const float d = y - tg[((long)b * T + t) * NM + c];
     sq += d * d;
-    dFR[i] = 2.f * d * inv_f;
+    dFR[i] = (!clip || (x >= lo && x <= hi)) ? 2.f * d * inv_f : 0.f;
+    FR[i] = y;
   }
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < (long)T * B; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i % B), t = (int)(i / B);
@@ -656,8 +661,10 @@ static void tr_colsum(tt2_train_ctx* c, const float* in, long M, int N, long ld,
   hipLaunchKernelGGL(k_tr_colsum_final, dim3((N + 255) / 256), dim3(256), 0, s, c->part.as<float>(), S, N, out);
 }
 
-static DevBuf* g_tr_kpart = nullptr;  // split-K scratch of the context being driven (stream-ordered)
-static int g_tr_prec = 0;             // GemmArgs::split16 of the context being driven (0 fp32, 2 bf16)
+// per calling thread: the context a tt2_train_* call is driving (a call runs on one thread, so
+// distinct contexts driven from different threads stay independent)
+static thread_local DevBuf* g_tr_kpart = nullptr;  // split-K scratch (stream-ordered)
+static thread_local int g_tr_prec = 0;             // GemmArgs::split16 (0 fp32, 2 bf16)
 
 static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
                     hipStream_t s, const float* bias = nullptr, const float* residual = nullptr, long ldr = 0,
@@ -855,7 +862,8 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_gemm((int)TB, 1, H + D, PIN, H + D, pvar(c, SPV("kernel")), 1, c->ST.as<float>(), 1, s, pvar(c, SPV("bias")));
   float* red = c->red.as<float>();
   hipLaunchKernelGGL(k_tr_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->ST.as<float>(), tg, stg, B, T, NM,
-                     c->dFR.as<float>(), c->dST.as<float>(), c->part.as<float>());
+                     c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dFR.as<float>(), c->dST.as<float>(),
+                     c->part.as<float>());
   hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, TB * NM, TB, red);
 
   // ---- backward ----
@@ -989,6 +997,9 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   c->adam_epsilon = 1e-6f;
   c->clip_norm = 1.0f;
   c->precision = 0;
+  c->clip_outputs = 1;
+  c->clip_lo = -4.1f;
+  c->clip_hi = 4.0f;
 }
 
 tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_train_ctx** out) {

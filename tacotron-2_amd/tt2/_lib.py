@@ -73,7 +73,9 @@ class TrainConfig(ctypes.Structure):
         "batch", "max_T_in", "max_T_out", "memory_dim", "num_mels", "prenet_units",
         "decoder_lstm_units", "attention_dim", "attention_filters", "attention_kernel")] + [
         (n, ctypes.c_float) for n in ("zoneout", "reg_weight", "adam_beta1", "adam_beta2",
-                                      "adam_epsilon", "clip_norm")] + [("precision", ctypes.c_int)]
+                                      "adam_epsilon", "clip_norm")] + [
+        ("precision", ctypes.c_int), ("clip_outputs", ctypes.c_int), ("clip_lo", ctypes.c_float),
+        ("clip_hi", ctypes.c_float)]
 
 
 _P = ctypes.c_void_p

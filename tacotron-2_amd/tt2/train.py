@@ -60,6 +60,12 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
     if precision not in ("fp32", "bf16"):
         raise ValueError("precision must be 'fp32' or 'bf16'")
     cfg.precision = 1 if precision == "bf16" else 0
+    # T2_output_range (tacotron.py:360-361): symmetric (-max, max), else (0, max)
+    lo, hi = ((-hp.max_abs_value, hp.max_abs_value) if hp.symmetric_mels
+              else (0.0, hp.max_abs_value))
+    cfg.clip_outputs = 1 if hp.clip_outputs else 0
+    cfg.clip_lo = lo - hp.lower_bound_decay
+    cfg.clip_hi = hi
     return cfg
 
 

@@ -107,6 +107,11 @@ def _rel(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 
+def _clip(hp):
+    lo, hi = (-hp.max_abs_value, hp.max_abs_value) if hp.symmetric_mels else (0.0, hp.max_abs_value)
+    return (lo - hp.lower_bound_decay, hi) if hp.clip_outputs else None
+
+
 def _gpu_vs_oracle(hp, B, T_in, T_out, use_zoneout_masks=True, seed=11):
     from tt2.train import TacotronTrainer
     W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out, seed)
@@ -121,7 +126,8 @@ def _gpu_vs_oracle(hp, B, T_in, T_out, use_zoneout_masks=True, seed=11):
         gmem = tr.get("memory", 1, mem.shape)
     finally:
         tr.close()
-    out, (b, s, r), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight)
+    out, (b, s, r), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight,
+                                        clip=_clip(hp))
     return (fr, sl, al, L, grads, gmem), (out, (b, s, r), g)
 
 
@@ -143,6 +149,20 @@ def test_gpu_train_forward_backward_small(zoneout_masks):
     assert _rel(gmem, g["memory"]) < 1e-4
     for bb in range(3):
         assert np.all(gmem[bb, _case(hp, 3, 9, 12)[2][bb]:] == 0)
+
+
+@pytest.mark.gpu
+def test_gpu_train_clipped_decoder_output():
+    """clip_outputs with a tight range (max_abs_value 0.02): decoder_output is clipped before the
+    before-loss (tacotron.py:360-361) and no gradient flows through clipped frames."""
+    hp = small_hparams()
+    hp.override_from_dict(dict(max_abs_value=0.02, lower_bound_decay=0.01))
+    (fr, sl, al, L, grads, gmem), (out, (b, s, r), g) = _gpu_vs_oracle(hp, 3, 9, 12)
+    assert np.mean(np.abs(fr) >= 0.02 - 1e-7) > 0.1            # the clip is active
+    assert np.abs(fr - out["frames"]).max() < 1e-5
+    assert abs(L["before"] - b) < 1e-5 * abs(b)
+    for n in TRN.train_var_names():
+        assert _rel(grads[n], g[n]) < 1e-4, (n, _rel(grads[n], g[n]))
 
 
 @pytest.mark.gpu
@@ -212,7 +232,8 @@ def test_gpu_train_bf16_gemms_close_to_oracle():
         grads = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in TRN.train_var_names()}
     finally:
         tr.close()
-    out, (b, s, r), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight)
+    out, (b, s, r), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight,
+                                        clip=_clip(hp))
     errs = {n: _rel(grads[n], g[n]) for n in TRN.train_var_names()}
     frob = {n: float(np.linalg.norm(grads[n] - g[n]) / max(np.linalg.norm(g[n]), 1e-30))
             for n in TRN.train_var_names()}
