@@ -181,13 +181,16 @@ def bench_griffin_lim(local, frames=1000):
 def train_step_flops(B, T_in, T, hp, D):
     """Algorithmic FLOPs of one teacher-forced decoder training step (forward + backward): the
     matrix products (per step-row: LSTM-1 [P+D+H]x4H, LSTM-2 2Hx4H, query HxA, projections
-    (H+D)x81; prenet once over all rows; keys once per batch) counted 3x (forward, input
-    gradient, weight gradient) plus the attention's location/energy/context terms (2x)."""
+    (H+D)x81; prenet once over all rows; keys once per batch; Postnet convs + projection) counted
+    3x (forward, input gradient, weight gradient) plus the attention's location/energy/context
+    terms (2x)."""
     H, A, F, KW, P, NM = (hp.decoder_lstm_units, hp.attention_dim, hp.attention_filters,
                           hp.attention_kernel[0], hp.prenet_layers[0], hp.num_mels)
     row = 2 * ((P + D + H) * 4 * H + 2 * H * 4 * H + H * A + (H + D) * (NM + 1) + NM * P + P * P)
     att = 2 * T_in * (F * KW + F * A + 2 * A + D)
-    return B * T * (3 * row + 2 * att) + 3 * 2 * B * T_in * D * A
+    C, kw, L = hp.postnet_channels, hp.postnet_kernel_size[0], hp.postnet_num_layers
+    post = 2 * (kw * NM * C + (L - 1) * kw * C * C + C * NM)
+    return B * T * (3 * row + 2 * att + 3 * post) + 3 * 2 * B * T_in * D * A
 
 
 def bench_train(a, rank, world, local, barrier, max_over_ranks):
@@ -197,7 +200,7 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
     all-reduce + clipped Adam, max over ranks."""
     import torch
     from tt2.hparams import hparams
-    from tt2.synthetic import prenet_masks, train_batch, zoneout_masks
+    from tt2.synthetic import postnet_masks, prenet_masks, train_batch, zoneout_masks
     from tt2.train import TacotronTrainer
     from tt2.weights import init_tacotron_weights, memory_width
     hp = hparams.copy()
@@ -213,6 +216,8 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
     batch = [torch.from_numpy(x).to(dev) for x in (mem, lens, tg, st)]
     batch.append(torch.from_numpy(prenet_masks(T, B, hp.prenet_layers[0], seed=7 + rank)).to(dev))
     batch.append(torch.from_numpy(zoneout_masks(T, B, hp.decoder_lstm_units, seed=7 + rank)).to(dev))
+    batch.append(torch.from_numpy(postnet_masks(hp.postnet_num_layers, B, T, hp.postnet_channels,
+                                                seed=7 + rank)).to(dev))
     losses = []
 
     def step():
@@ -243,7 +248,8 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
                 loss_first=round(losses[0]["loss"], 5), loss_last=round(L["loss"], 5),
                 grad_norm=round(L["grad_norm"], 5), dtype=a.train_precision,
                 config=dict(workload="configs[4]: Tacotron-2 decoder training step (teacher-forced), "
-                                     "B={} rows/GPU, T_in={}, T_out={}, D_mem={}".format(B, Ti, T, D),
+                                     "+ Postnet (training BN/dropout), B={} rows/GPU, T_in={}, T_out={}, "
+                                     "D_mem={}".format(B, Ti, T, D),
                             global_batch=B * world, parallelism="dp{} (RCCL grad all-reduce)".format(world)),
                 roofline=dict(bound="mfma", achieved=round(tf, 2), peak=peak, unit="TFLOP/s",
                               frac=round(tf / peak, 4), algorithmic_flops_per_step=int(fl),

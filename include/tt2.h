@@ -321,6 +321,9 @@ typedef struct tt2_train_config {
                               fp32 master weights / cell state / optimizer (configs[4]) */
   int clip_outputs;        /* 1: decoder_output = clip(frames, clip_lo, clip_hi) before the loss */
   float clip_lo, clip_hi;  /* -max_abs_value - lower_bound_decay, max_abs_value (-4.1, 4) */
+  int postnet;             /* 1: also the Postnet (training-mode BN + dropout) and the after loss */
+  int postnet_layers, postnet_channels, postnet_kernel;  /* 5, 512, 5 */
+  float bn_momentum, bn_eps;                               /* 0.99, 1e-3 (tf.layers defaults) */
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;
@@ -338,19 +341,22 @@ tt2_status tt2_train_finalize(tt2_train_ctx* ctx);
 tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* ctx, float* grads_d, int64_t* n_out);
 /* Forward + losses + backward on DEVICE inputs: memory [B,T_in,D] (encoder outputs ⊕ style),
  * lengths int32 [B], mel targets [B,T_out,80], stop targets [B,T_out], prenet keep bits u8
- * [T_out,2,B,P], zoneout keep bits u8 [T_out,4,B,H] (c1,h1,c2,h2) or NULL (inference mix).
+ * [T_out,2,B,P], zoneout keep bits u8 [T_out,4,B,H] (c1,h1,c2,h2) or NULL (inference mix),
+ * Postnet dropout keep bits u8 [layers,B,T_out,channels] or NULL (no dropout; cfg.postnet only).
  * Gradients (incl. L2) land in the flat gradient buffer; enqueued on `stream`. */
 tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* ctx, const float* memory_d,
                                           const int32_t* lengths_d, const float* targets_d,
                                           const float* stop_targets_d,
                                           const uint8_t* prenet_masks_d,
-                                          const uint8_t* zoneout_masks_d, int T_in, int T_out,
+                                          const uint8_t* zoneout_masks_d,
+                                          const uint8_t* postnet_masks_d, int T_in, int T_out,
                                           void* stream);
 /* clip_by_global_norm + Adam with learning rate lr at update count global_step (>= 1). */
 tt2_status tt2_train_apply_dev(tt2_train_ctx* ctx, float lr, int global_step, void* stream);
-/* Synchronise; out4 = {before_loss, stop_loss, reg_loss, grad_global_norm (after apply)};
- * fb_ms (nullable) = device time of the last forward_backward. */
-tt2_status tt2_train_losses(tt2_train_ctx* ctx, float* out4, float* fb_ms);
+/* Synchronise; out5 = {before_loss, stop_loss, reg_loss, grad_global_norm (after apply),
+ * after_loss (0 without the Postnet)}; fb_ms (nullable) = device time of the last
+ * forward_backward.  apply also runs the Postnet BN moving-average updates. */
+tt2_status tt2_train_losses(tt2_train_ctx* ctx, float* out5, float* fb_ms);
 /* which: 0 = parameter, 1 = gradient, 2 = Adam m, 3 = Adam v; name "memory" (which ignored) =
  * d loss / d memory [B,T_in,D] of the last forward_backward. */
 tt2_status tt2_train_get_tensor(tt2_train_ctx* ctx, const char* tf_name, int which, float* host);

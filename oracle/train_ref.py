@@ -31,6 +31,25 @@ FP = P + "decoder/linear_transform_projection/projection_linear_transform_projec
 SP = P + "decoder/stop_token_projection/projection_stop_token_projection/"
 
 
+PN = P + "postnet_convolutions/conv_layer_{}_postnet_convolutions/"
+PP = P + "postnet_projection/projection_postnet_projection/"
+
+
+def postnet_var_names(layers=5):
+    """Trainable Postnet variables (modules.py:451-497; tacotron.py:362-375), library order."""
+    names = []
+    for i in range(1, layers + 1):
+        s = PN.format(i)
+        names += [s + "conv1d/kernel", s + "conv1d/bias", s + "batch_normalization/gamma",
+                  s + "batch_normalization/beta"]
+    return names + [PP + "kernel", PP + "bias"]
+
+
+def postnet_stat_names(layers=5):
+    return [PN.format(i) + "batch_normalization/" + n for i in range(1, layers + 1)
+            for n in ("moving_mean", "moving_variance")]
+
+
 def train_var_names(n_prenet=2):
     """The decoder-slice trainable variables, in the order of the library's flat buffers."""
     names = [P + "memory_layer/kernel", P + "decoder/query_layer/kernel",
@@ -131,10 +150,39 @@ def losses(frames, stop_logits, targets, stop_targets, W, reg_weight, clip=(-4.1
     return before, stop, reg
 
 
+def postnet_train(W, dec, masks, eps=1e-3, layers=5):
+    """Postnet in training mode (modules.py:474-497, conv1d with bnorm='after'): per layer
+    conv1d 'same' + tanh (identity for the last), batch normalisation with the BATCH statistics
+    over all B·T positions (tf.layers.batch_normalization(training=True); biased variance),
+    dropout(rate 0.5) with keep bits ``masks [layers, B, T, C]`` (None = no dropout); then
+    postnet_projection (tacotron.py:368-372).  Returns (projected residual, [(mean, var)])."""
+    x = dec
+    stats = []
+    for i in range(1, layers + 1):
+        s = PN.format(i)
+        k = W[s + "conv1d/kernel"]                                       # [kw, Cin, C]
+        kw = k.shape[0]
+        pad = (kw - 1) // 2
+        xp = torch.nn.functional.pad(x, (0, 0, pad, kw - 1 - pad))      # [B, T+kw-1, Cin]
+        cols = xp.unfold(1, kw, 1)                                       # [B, T, Cin, kw]
+        z = torch.einsum("btck,kcn->btn", cols, k) + W[s + "conv1d/bias"]
+        a = torch.tanh(z) if i < layers else z
+        mean = a.mean(dim=(0, 1))
+        var = ((a - mean) ** 2).mean(dim=(0, 1))
+        stats.append((mean, var))
+        y = (W[s + "batch_normalization/gamma"] * (a - mean) / torch.sqrt(var + eps)
+             + W[s + "batch_normalization/beta"])
+        x = y if masks is None else y / 0.5 * masks[i - 1]
+    return x @ W[PP + "kernel"] + W[PP + "bias"], stats
+
+
 def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,
-                reg_weight=1e-6, dtype=torch.float64, clip=(-4.1, 4.0)):
-    """One forward + backward; returns (outputs dict, losses tuple, grads dict incl. 'memory')."""
-    names = train_var_names()
+                reg_weight=1e-6, dtype=torch.float64, clip=(-4.1, 4.0), postnet=False,
+                postnet_masks=None):
+    """One forward + backward; returns (outputs dict, losses tuple, grads dict incl. 'memory').
+    postnet=True adds the Postnet and the ``after`` loss (tacotron.py:362-381, 775-776): losses
+    become (before, stop, reg, after) and outputs gain 'mel_outputs' and 'bn_stats'."""
+    names = train_var_names() + (postnet_var_names() if postnet else [])
     W = {n: torch.tensor(np.asarray(Wnp[n]), dtype=dtype, requires_grad=True) for n in names}
     mem = torch.tensor(np.asarray(memory), dtype=dtype, requires_grad=True)
     tg = torch.tensor(np.asarray(targets), dtype=dtype)
@@ -143,12 +191,29 @@ def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneo
     zm = None if zoneout_masks is None else torch.tensor(np.asarray(zoneout_masks), dtype=dtype)
     fr, sl, al = forward(W, mem, lengths, tg, pm, zm)
     b, s, r = losses(fr, sl, tg, st, W, reg_weight, clip)
-    (b + s + r).backward()
-    g = {n: W[n].grad.numpy() for n in names}
-    g["memory"] = mem.grad.numpy()
+    total = b + s + r
     out = dict(frames=clip_decoder_output(fr, clip).detach().numpy(), stop_logits=sl.detach().numpy(),
                alignments=al.detach().numpy())
-    return out, (b.item(), s.item(), r.item()), g
+    if postnet:
+        dec = clip_decoder_output(fr, clip)
+        pmk = None if postnet_masks is None else torch.tensor(np.asarray(postnet_masks), dtype=dtype)
+        proj, stats = postnet_train(W, dec, pmk)
+        mel = clip_decoder_output(dec + proj, clip)                      # tacotron.py:375-378
+        after = ((mel - tg) ** 2).mean()
+        total = total + after
+        out["mel_outputs"] = mel.detach().numpy()
+        out["bn_stats"] = [(m.detach().numpy(), v.detach().numpy()) for m, v in stats]
+    total.backward()
+    g = {n: W[n].grad.numpy() for n in names}
+    g["memory"] = mem.grad.numpy()
+    L = (b.item(), s.item(), r.item()) + ((after.item(),) if postnet else ())
+    return out, L, g
+
+
+def bn_moving_update(moving, batch, momentum=0.99):
+    """tf.layers.batch_normalization UPDATE_OPS (run with the optimizer, tacotron.py:1088-1090):
+    moving -= (moving - batch)·(1 - momentum)."""
+    return moving - (moving - batch) * (1 - momentum)
 
 
 def learning_rate(step, hp):

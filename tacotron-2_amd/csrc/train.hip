@@ -60,7 +60,14 @@ struct tt2_train_ctx {
   DevBuf TH, E, DA, DF, PQ, FALL, ALN;
   // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
   DevBuf hK1, hK1T, hK2, hK2T, hWq, hWqT;
+  // Postnet training (cfg.postnet): PA[i] activations (pre-BN), PX[i] layer inputs (PX[0] unused:
+  // layer 1 reads the clipped frames), batch stats, projection, scratch
+  DevBuf PA[8], PX[9];  // postnet_layers <= 8
+  DevBuf BNM, BNV, PPRJ, dPP, DYb, DZb, dPXa, dPXb, WFLIP, PWT, CLIPM, pn_part;
+  int PL = 0, PC = 0, PK = 0;
+  bool pn_masks = false;
   int T_last = 0, Tin_last = 0;
+  bool pn_ran = false;  // batch stats of the last forward are valid (moving averages in apply)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
 };
@@ -359,7 +366,8 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
 __global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const float* __restrict__ ST,
                                                  const float* __restrict__ tg, const float* __restrict__ stg, int B,
                                                  int T, int NM, int clip, float lo, float hi, float* __restrict__ dFR,
-                                                 float* __restrict__ dST, float* __restrict__ part) {
+                                                 float* __restrict__ dST, float* __restrict__ part,
+                                                 uint8_t* __restrict__ clipm) {
   __shared__ float s4[16];
   const long nf = (long)T * B * NM;
   const float inv_f = 1.0f / (float)nf, inv_s = 1.0f / (float)((long)T * B);
@@ -374,7 +382,9 @@ __global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const f
     const float y = clip ? fminf(fmaxf(x, lo), hi) : x;
     const float d = y - tg[((long)b * T + t) * NM + c];
     sq += d * d;
-    dFR[i] = (!clip || (x >= lo && x <= hi)) ? 2.f * d * inv_f : 0.f;
+    const bool pass = !clip || (x >= lo && x <= hi);
+    dFR[i] = pass ? 2.f * d * inv_f : 0.f;
+    if (clipm) clipm[i] = pass ? 1 : 0;
     FR[i] = y;
   }
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < (long)T * B; i += (long)gridDim.x * blockDim.x) {
@@ -647,6 +657,170 @@ __global__ void k_tr_adam(float* __restrict__ w, const float* __restrict__ g, fl
   w[i] -= lr_t * mi / (sqrtf(vi) + eps);
 }
 
+// ---- Postnet training (modules.py:474-497 in training mode) --------------------------------------
+// column statistics over M rows: mode 0 sum(x); 1 sum((x - c)^2); per-split partials then final
+__global__ __launch_bounds__(256) void k_pn_colstat_part(const float* __restrict__ x, long M, int N,
+                                                         const float* __restrict__ ctr, int mode,
+                                                         float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int cc = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + cc;
+  const int S = gridDim.y, sp = blockIdx.y;
+  float acc = 0.f;
+  if (n < N) {
+    const float c0 = mode ? ctr[n] : 0.f;
+    for (long m = (long)sp * 4 + r; m < M; m += (long)S * 4) {
+      const float v = x[m * N + n] - c0;
+      acc += mode ? v * v : v;
+    }
+  }
+  red[r][cc] = acc;
+  __syncthreads();
+  if (r == 0 && n < N) part[(long)sp * N + n] = red[0][cc] + red[1][cc] + red[2][cc] + red[3][cc];
+}
+__global__ void k_pn_colstat_final(const float* __restrict__ part, int S, int N, float scale, float* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (int sp = 0; sp < S; ++sp) acc += part[(long)sp * N + n];
+  out[n] = acc * scale;
+}
+// y = gamma (a - mean) rsqrt(var + eps) + beta, then dropout(0.5) with keep bits (or identity)
+__global__ void k_pn_bn_fwd(const float* __restrict__ a, long M, int C, const float* __restrict__ mean,
+                            const float* __restrict__ var, const float* __restrict__ gamma,
+                            const float* __restrict__ beta, float eps, const uint8_t* __restrict__ keep,
+                            float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const int c = (int)(i % C);
+  float v = gamma[c] * (a[i] - mean[c]) * rsqrtf(var[c] + eps) + beta[c];
+  if (keep) v = (v / 0.5f) * (float)keep[i];
+  y[i] = v;
+}
+// BN backward sums over rows: S1 = sum dy, S2 = sum dy * xhat, with dy = dx_next * dropout
+__global__ __launch_bounds__(256) void k_pn_bn_bwd_part(const float* __restrict__ dxn, const uint8_t* __restrict__ keep,
+                                                        const float* __restrict__ a, long M, int C,
+                                                        const float* __restrict__ mean, const float* __restrict__ var,
+                                                        float eps, float* __restrict__ dy, float* __restrict__ part) {
+  __shared__ float r1[4][64], r2[4][64];
+  const int cc = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc;
+  const int S = gridDim.y, sp = blockIdx.y;
+  float s1 = 0.f, s2 = 0.f;
+  if (c < C) {
+    const float mu = mean[c], rs = rsqrtf(var[c] + eps);
+    for (long m = (long)sp * 4 + r; m < M; m += (long)S * 4) {
+      const long i = m * C + c;
+      float g = dxn[i];
+      if (keep) g = g * 2.f * (float)keep[i];
+      dy[i] = g;
+      s1 += g;
+      s2 += g * (a[i] - mu) * rs;
+    }
+  }
+  r1[r][cc] = s1;
+  r2[r][cc] = s2;
+  __syncthreads();
+  if (r == 0 && c < C) {
+    part[(long)sp * 2 * C + c] = r1[0][cc] + r1[1][cc] + r1[2][cc] + r1[3][cc];
+    part[(long)sp * 2 * C + C + c] = r2[0][cc] + r2[1][cc] + r2[2][cc] + r2[3][cc];
+  }
+}
+// finalize: d beta = S1, d gamma = S2 (written into the gradient slots)
+__global__ void k_pn_bn_bwd_final(const float* __restrict__ part, int S, int C, float* __restrict__ sums,
+                                  float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int sp = 0; sp < S; ++sp) {
+    s1 += part[(long)sp * 2 * C + c];
+    s2 += part[(long)sp * 2 * C + C + c];
+  }
+  sums[c] = s1;
+  sums[C + c] = s2;
+  dbeta[c] = s1;
+  dgamma[c] = s2;
+}
+// dz = [tanh'] gamma rstd (dy - S1/M - xhat S2/M)
+__global__ void k_pn_bn_bwd_dz(const float* __restrict__ dy, const float* __restrict__ a, long M, int C,
+                               const float* __restrict__ mean, const float* __restrict__ var, float eps,
+                               const float* __restrict__ gamma, const float* __restrict__ sums, int tanh_act,
+                               float* __restrict__ dz) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const int c = (int)(i % C);
+  const float rs = rsqrtf(var[c] + eps);
+  const float av = a[i];
+  const float xh = (av - mean[c]) * rs;
+  const float inv_m = 1.0f / (float)M;
+  float g = gamma[c] * rs * (dy[i] - sums[c] * inv_m - xh * sums[C + c] * inv_m);
+  if (tanh_act) g *= 1.f - av * av;
+  dz[i] = g;
+}
+// im2col^T of a conv1d input x(b, t, c) = x[b*xs_b + t*xs_t + c]:
+// out[(tap*C + c) * ldo + b*T + t] = x(b, t + tap - pad, c) (0 outside [0, T))
+__global__ void k_pn_im2col_t(const float* __restrict__ x, long xs_b, long xs_t, int B, int T, int C, int kw, int pad,
+                              float* __restrict__ out, long ldo) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long M = (long)B * T;
+  if (i >= (long)kw * C * M) return;
+  const long m = i % M;
+  const long kc = i / M;
+  const int c = (int)(kc % C), tap = (int)(kc / C);
+  const int b = (int)(m / T), t = (int)(m % T);
+  const int ts = t + tap - pad;
+  out[kc * ldo + m] = (ts >= 0 && ts < T) ? x[(long)b * xs_b + (long)ts * xs_t + c] : 0.f;
+}
+// Wflip[(tap' * Cout + co) * Cin + ci] = W[((kw-1-tap') * Cin + ci) * Cout + co]  (conv1d input gradient)
+__global__ void k_pn_flip(const float* __restrict__ w, int kw, int cin, int cout, float* __restrict__ wf) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)kw * cin * cout) return;
+  const int ci = (int)(i % cin);
+  const int co = (int)((i / cin) % cout);
+  const int tp = (int)(i / ((long)cin * cout));
+  wf[i] = w[((long)(kw - 1 - tp) * cin + ci) * cout + co];
+}
+// after loss: mel = clip(dec[t][b] + proj[b][t]) (tacotron.py:375-378); MSE partials; d proj
+__global__ __launch_bounds__(256) void k_pn_after_loss(const float* __restrict__ FR, const float* __restrict__ prj,
+                                                       const float* __restrict__ tg, int B, int T, int NM, int clip,
+                                                       float lo, float hi, float* __restrict__ dprj,
+                                                       float* __restrict__ part) {
+  __shared__ float s16[16];
+  const long n = (long)B * T * NM;
+  const float inv = 1.0f / (float)n;
+  float sq = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % NM);
+    const long bt = i / NM;
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    const float x = FR[((long)t * B + b) * NM + c] + prj[i];
+    const float y = clip ? fminf(fmaxf(x, lo), hi) : x;
+    const float d = y - tg[i];
+    sq += d * d;
+    dprj[i] = (!clip || (x >= lo && x <= hi)) ? 2.f * d * inv : 0.f;
+  }
+  sq = block_sum(sq, s16);
+  if (threadIdx.x == 0) part[blockIdx.x] = sq;
+}
+// dFR[t][b] += clipmask(frames) * (d mel + d postnet input)   (dec = clip(frames) feeds both)
+__global__ void k_pn_add_ddec(const float* __restrict__ dprj, const float* __restrict__ dx0, const uint8_t* clipm,
+                              int B, int T, int NM, float* __restrict__ dFR) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * T * NM) return;
+  const int c = (int)(i % NM);
+  const long bt = i / NM;
+  const int t = (int)(bt % T), b = (int)(bt / T);
+  const long j = ((long)t * B + b) * NM + c;
+  if (clipm[j]) dFR[j] += dprj[i] + dx0[i];
+}
+__global__ void k_pn_moving(float* __restrict__ mm, float* __restrict__ mv, const float* __restrict__ mean,
+                            const float* __restrict__ var, int C, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mm[c] -= (mm[c] - mean[c]) * (1.f - momentum);
+  mv[c] -= (mv[c] - var[c]) * (1.f - momentum);
+}
+
 // ---- host orchestration ----------------------------------------------------------------------
 static inline unsigned nblk(long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
@@ -680,6 +854,15 @@ static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* 
   }
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.Bw = Bw; g.ldb = ldb; g.Cout = C; g.ldc = ldc;
   g.bias = bias; g.residual = residual; g.ldr = ldr; g.act = act;
+  g.split16 = g_tr_prec;
+  gemm(g, s);
+}
+
+static void tr_gemm_run(GemmArgs& g, hipStream_t s) {  // conv-mode products: same precision / split-K
+  if (g_tr_kpart) {
+    g.kpart = g_tr_kpart->as<float>();
+    g.kpart_floats = (long)(g_tr_kpart->bytes / sizeof(float));
+  }
   g.split16 = g_tr_prec;
   gemm(g, s);
 }
@@ -730,6 +913,25 @@ static void tr_build_vars(tt2_train_ctx* c) {
   add(FPV("bias"), {NM}, false);
   add(SPV("kernel"), {H + D, 1}, false);
   add(SPV("bias"), {1}, false);
+  if (!c->cfg.postnet) return;
+  // Postnet (oracle/train_ref.py postnet_var_names / postnet_stat_names); moving statistics are
+  // non-trainable slots of the same table (zero gradient -> Adam leaves them alone)
+  for (int i = 1; i <= c->PL; ++i) {
+    const std::string sc = vn("postnet_convolutions/conv_layer_") + std::to_string(i) + "_postnet_convolutions/";
+    const int cin = i == 1 ? NM : c->PC;
+    add(sc + "conv1d/kernel", {c->PK, cin, c->PC}, true);
+    add(sc + "conv1d/bias", {c->PC}, false);
+    add(sc + "batch_normalization/gamma", {c->PC}, true);
+    add(sc + "batch_normalization/beta", {c->PC}, true);
+    add(sc + "batch_normalization/moving_mean", {c->PC}, false);
+    add(sc + "batch_normalization/moving_variance", {c->PC}, false);
+  }
+  add(vn("postnet_projection/projection_postnet_projection/kernel"), {c->PC, NM}, false);
+  add(vn("postnet_projection/projection_postnet_projection/bias"), {NM}, false);
+}
+
+static std::string pn_scope(int i) {
+  return vn("postnet_convolutions/conv_layer_") + std::to_string(i) + "_postnet_convolutions/";
 }
 
 static void tr_alloc(tt2_train_ctx* c) {
@@ -754,7 +956,8 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F); f(c->FALL, TB * Tin * F); f(c->ALN, TB * Tin);
   f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DA, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
   f(c->dZ, TB * P); f(c->dPre, TB * P);
-  const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM, TB * Tin * F});
+  const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM, TB * Tin * F,
+                              c->cfg.postnet ? TB * (long)c->PK * c->PC : 0L});
   f(c->TBUF, tmax);
   f(c->part, 64 * std::max<long>(4 * H, LX1) + 4096);
   f(c->red, 64);
@@ -764,11 +967,111 @@ static void tr_alloc(tt2_train_ctx* c) {
     h(c->hWq, H * A); h(c->hWqT, H * A);
   }
   f(c->kpart, 4L << 20);
+  if (c->cfg.postnet) {
+    const long PC = c->PC, PK = c->PK;
+    for (int i = 0; i < c->PL; ++i) f(c->PA[i], TB * PC);
+    for (int i = 1; i <= c->PL; ++i) f(c->PX[i], TB * PC);
+    f(c->BNM, c->PL * PC); f(c->BNV, c->PL * PC); f(c->PPRJ, TB * NM); f(c->dPP, TB * NM);
+    f(c->DYb, TB * PC); f(c->DZb, TB * PC); f(c->dPXa, TB * PC); f(c->dPXb, TB * PC);
+    f(c->WFLIP, PK * PC * PC); f(c->PWT, NM * PC); f(c->pn_part, 64 * 2 * PC + 1024);
+    c->CLIPM.alloc((size_t)TB * NM);
+  }
+}
+
+// Postnet forward (training-mode BN + dropout) + after loss + backward; adds d decoder_output into
+// dFR (through the frame clip).  Runs between the decoder forward and the decoder backward.
+static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, int T, hipStream_t s) {
+  const int B = c->B, NM = c->NM, C = c->PC, KW = c->PK, L = c->PL;
+  const long M = (long)B * T;
+  const int pad = (KW - 1) / 2;
+  const float eps = c->cfg.bn_eps;
+  float* red = c->red.as<float>();
+  float* part = c->pn_part.as<float>();
+  float* sums = part + 64L * 2 * C;
+  float* TBUF = c->TBUF.as<float>();
+  const int S = (int)std::min<long>(64, std::max<long>(1, M / 64));
+  auto colstat = [&](const float* x, const float* ctr, int mode, float* out) {
+    hipLaunchKernelGGL(k_pn_colstat_part, dim3((C + 63) / 64, S), dim3(256), 0, s, x, M, C, ctr, mode, part);
+    hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, out);
+  };
+  auto conv_in = [&](int i, GemmArgs& g) {  // layer i's input as an implicit-im2col conv1d operand
+    if (i == 0) {  // clipped decoder frames, time-major [T][B][NM]
+      g.A = c->FR.as<float>(); g.C = NM; g.xs_b = NM; g.xs_t = (long)B * NM;
+    } else {
+      g.A = c->PX[i].as<float>(); g.C = C; g.xs_b = (long)T * C; g.xs_t = C;
+    }
+  };
+  for (int i = 0; i < L; ++i) {
+    const std::string sc = pn_scope(i + 1);
+    GemmArgs g;
+    g.a_mode = A_CONV1D; g.M = (int)M; g.N = C; g.T = T; g.kw = KW; g.pad = pad;
+    conv_in(i, g);
+    g.K = KW * g.C;
+    g.Bw = pvar(c, sc + "conv1d/kernel"); g.ldb = C; g.Cout = c->PA[i].as<float>(); g.ldc = C;
+    g.bias = pvar(c, sc + "conv1d/bias"); g.act = i < L - 1 ? ACT_TANH : ACT_NONE;
+    tr_gemm_run(g, s);
+    float* mean = c->BNM.as<float>() + (long)i * C;
+    float* var = c->BNV.as<float>() + (long)i * C;
+    colstat(c->PA[i].as<float>(), nullptr, 0, mean);
+    colstat(c->PA[i].as<float>(), mean, 1, var);
+    hipLaunchKernelGGL(k_pn_bn_fwd, dim3(nblk(M * C)), dim3(256), 0, s, c->PA[i].as<float>(), M, C, mean, var,
+                       pvar(c, sc + "batch_normalization/gamma"), pvar(c, sc + "batch_normalization/beta"), eps,
+                       pnm ? pnm + (long)i * M * C : nullptr, c->PX[i + 1].as<float>());
+  }
+  const std::string pp = vn("postnet_projection/projection_postnet_projection/");
+  tr_gemm((int)M, NM, C, c->PX[L].as<float>(), C, pvar(c, pp + "kernel"), NM, c->PPRJ.as<float>(), NM, s,
+          pvar(c, pp + "bias"));
+  hipLaunchKernelGGL(k_pn_after_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->PPRJ.as<float>(), tg, B, T,
+                     NM, c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dPP.as<float>(), c->part.as<float>());
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, 1.0f / (float)(M * NM),
+                     red + 4, 0);
+  // backward: projection
+  tr_transpose(c->PX[L].as<float>(), M, C, C, TBUF, M, s);
+  tr_gemm(C, NM, (int)M, TBUF, M, c->dPP.as<float>(), NM, gvar(c, pp + "kernel"), NM, s);
+  tr_colsum(c, c->dPP.as<float>(), M, NM, NM, gvar(c, pp + "bias"), s);
+  tr_transpose(pvar(c, pp + "kernel"), C, NM, NM, c->PWT.as<float>(), C, s);
+  float* dxn = c->dPXa.as<float>();
+  float* dxo = c->dPXb.as<float>();
+  tr_gemm((int)M, C, NM, c->dPP.as<float>(), NM, c->PWT.as<float>(), C, dxn, C, s);
+  for (int i = L - 1; i >= 0; --i) {
+    const std::string sc = pn_scope(i + 1);
+    const float* mean = c->BNM.as<float>() + (long)i * C;
+    const float* var = c->BNV.as<float>() + (long)i * C;
+    hipLaunchKernelGGL(k_pn_bn_bwd_part, dim3((C + 63) / 64, S), dim3(256), 0, s, dxn,
+                       pnm ? pnm + (long)i * M * C : nullptr, c->PA[i].as<float>(), M, C, mean, var, eps,
+                       c->DYb.as<float>(), part);
+    hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, sums,
+                       gvar(c, sc + "batch_normalization/gamma"), gvar(c, sc + "batch_normalization/beta"));
+    hipLaunchKernelGGL(k_pn_bn_bwd_dz, dim3(nblk(M * C)), dim3(256), 0, s, c->DYb.as<float>(), c->PA[i].as<float>(),
+                       M, C, mean, var, eps, pvar(c, sc + "batch_normalization/gamma"), sums, i < L - 1 ? 1 : 0,
+                       c->DZb.as<float>());
+    tr_colsum(c, c->DZb.as<float>(), M, C, C, gvar(c, sc + "conv1d/bias"), s);
+    const int cin = i == 0 ? NM : C;
+    {
+      GemmArgs gi;
+      conv_in(i, gi);
+      hipLaunchKernelGGL(k_pn_im2col_t, dim3(nblk((long)KW * cin * M)), dim3(256), 0, s, gi.A, gi.xs_b, gi.xs_t, B,
+                         T, cin, KW, pad, TBUF, M);
+    }
+    tr_gemm(KW * cin, C, (int)M, TBUF, M, c->DZb.as<float>(), C, gvar(c, sc + "conv1d/kernel"), C, s);
+    hipLaunchKernelGGL(k_pn_flip, dim3(nblk((long)KW * cin * C)), dim3(256), 0, s, pvar(c, sc + "conv1d/kernel"), KW,
+                       cin, C, c->WFLIP.as<float>());
+    GemmArgs g;
+    g.a_mode = A_CONV1D; g.M = (int)M; g.N = cin; g.T = T; g.kw = KW; g.pad = KW - 1 - pad;
+    g.A = c->DZb.as<float>(); g.C = C; g.xs_b = (long)T * C; g.xs_t = C; g.K = KW * C;
+    g.Bw = c->WFLIP.as<float>(); g.ldb = cin; g.Cout = dxo; g.ldc = cin;
+    tr_gemm_run(g, s);
+    std::swap(dxn, dxo);
+  }
+  hipLaunchKernelGGL(k_pn_add_ddec, dim3(nblk(M * NM)), dim3(256), 0, s, c->dPP.as<float>(), dxn,
+                     c->CLIPM.as<uint8_t>(), B, T, NM, c->dFR.as<float>());
+  c->pn_ran = true;
 }
 
 // forward + losses + backward for one batch; grads complete (incl. L2) on return (stream order)
 static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* lens, const float* tg, const float* stg,
-                                const uint8_t* pm, const uint8_t* zm, int Tin, int T, hipStream_t s) {
+                                const uint8_t* pm, const uint8_t* zm, const uint8_t* pnm, int Tin, int T,
+                                hipStream_t s) {
   const int B = c->B, D = c->D, H = c->H, P = c->P, A = c->A, F = c->F, KW = c->KW, NM = c->NM, LX1 = c->LX1;
   const long TB = (long)T * B;
   const float z = c->cfg.zoneout;
@@ -863,8 +1166,10 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   float* red = c->red.as<float>();
   hipLaunchKernelGGL(k_tr_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->ST.as<float>(), tg, stg, B, T, NM,
                      c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dFR.as<float>(), c->dST.as<float>(),
-                     c->part.as<float>());
+                     c->part.as<float>(), c->cfg.postnet ? c->CLIPM.as<uint8_t>() : nullptr);
   hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, TB * NM, TB, red);
+  c->pn_ran = false;
+  if (c->cfg.postnet) tr_postnet(c, tg, pnm, T, s);
 
   // ---- backward ----
   float* dPIN = c->dPIN.as<float>();
@@ -963,6 +1268,15 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
 
 static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s) {
   float* red = c->red.as<float>();
+  if (c->cfg.postnet && c->pn_ran) {  // BN UPDATE_OPS run with the optimizer (tacotron.py:1088-1090)
+    for (int i = 0; i < c->PL; ++i) {
+      const std::string sc = pn_scope(i + 1) + "batch_normalization/";
+      hipLaunchKernelGGL(k_pn_moving, dim3((c->PC + 255) / 256), dim3(256), 0, s, pvar(c, sc + "moving_mean"),
+                         pvar(c, sc + "moving_variance"), c->BNM.as<float>() + (long)i * c->PC,
+                         c->BNV.as<float>() + (long)i * c->PC, c->PC, c->cfg.bn_momentum);
+    }
+    c->pn_ran = false;
+  }
   hipLaunchKernelGGL(k_tr_sumsq, dim3(256), dim3(256), 0, s, c->grads, c->total, c->part.as<float>());
   hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, 1.f, red + 3, 1);
   const double b1 = c->cfg.adam_beta1, b2 = c->cfg.adam_beta2;
@@ -1000,6 +1314,12 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   c->clip_outputs = 1;
   c->clip_lo = -4.1f;
   c->clip_hi = 4.0f;
+  c->postnet = 0;
+  c->postnet_layers = 5;
+  c->postnet_channels = 512;
+  c->postnet_kernel = 5;
+  c->bn_momentum = 0.99f;
+  c->bn_eps = 1e-3f;
 }
 
 tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_train_ctx** out) {
@@ -1023,6 +1343,10 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
       c->B = cfg->batch; c->Tm = cfg->max_T_out; c->Tin = cfg->max_T_in; c->D = cfg->memory_dim;
       c->NM = cfg->num_mels; c->P = cfg->prenet_units; c->H = cfg->decoder_lstm_units; c->A = cfg->attention_dim;
       c->F = cfg->attention_filters; c->KW = cfg->attention_kernel; c->LX1 = c->P + c->D + c->H;
+      c->PL = cfg->postnet_layers; c->PC = cfg->postnet_channels; c->PK = cfg->postnet_kernel;
+      TT2_CHECK(!cfg->postnet || (c->PL >= 1 && c->PL <= 8 && c->PC >= 1 && c->PK >= 1 && c->PK <= 64),
+                TT2_ERR_INVALID_ARG,
+                "bad postnet shape");
       TT2_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       TT2_HIP(hipEventCreate(&c->ev0));
       TT2_HIP(hipEventCreate(&c->ev1));
@@ -1084,8 +1408,8 @@ tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* c, float* grads_d, int64_t* n
 
 tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* c, const float* memory_d, const int32_t* lengths_d,
                                           const float* targets_d, const float* stop_targets_d,
-                                          const uint8_t* prenet_masks_d, const uint8_t* zoneout_masks_d, int T_in,
-                                          int T_out, void* stream) {
+                                          const uint8_t* prenet_masks_d, const uint8_t* zoneout_masks_d,
+                                          const uint8_t* postnet_masks_d, int T_in, int T_out, void* stream) {
   return guard([&] {
     TT2_CHECK(c && memory_d && lengths_d && targets_d && stop_targets_d && prenet_masks_d, TT2_ERR_INVALID_ARG,
               "tt2_train_forward_backward_dev: null argument");
@@ -1095,8 +1419,8 @@ tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* c, const float* memory_
     TT2_HIP(hipSetDevice(c->dev));
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     TT2_HIP(hipEventRecord(c->ev0, s));
-    tr_forward_backward(c, memory_d, lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d, T_in, T_out,
-                        s);
+    tr_forward_backward(c, memory_d, lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d,
+                        postnet_masks_d, T_in, T_out, s);
     TT2_HIP(hipEventRecord(c->ev1, s));
     TT2_HIP(hipGetLastError());
   });
@@ -1112,12 +1436,13 @@ tt2_status tt2_train_apply_dev(tt2_train_ctx* c, float lr, int global_step, void
   });
 }
 
-tt2_status tt2_train_losses(tt2_train_ctx* c, float* out4, float* fb_ms) {
+tt2_status tt2_train_losses(tt2_train_ctx* c, float* out4 /* [5] */, float* fb_ms) {
   return guard([&] {
     TT2_CHECK(c && out4, TT2_ERR_INVALID_ARG, "null argument");
     TT2_HIP(hipSetDevice(c->dev));
     TT2_HIP(hipDeviceSynchronize());
-    TT2_HIP(hipMemcpy(out4, c->red.p, sizeof(float) * 4, hipMemcpyDeviceToHost));
+    TT2_HIP(hipMemcpy(out4, c->red.p, sizeof(float) * 5, hipMemcpyDeviceToHost));
+    if (!c->cfg.postnet) out4[4] = 0.f;
     if (fb_ms) TT2_HIP(hipEventElapsedTime(fb_ms, c->ev0, c->ev1));
   });
 }

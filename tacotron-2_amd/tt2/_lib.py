@@ -75,7 +75,9 @@ class TrainConfig(ctypes.Structure):
         (n, ctypes.c_float) for n in ("zoneout", "reg_weight", "adam_beta1", "adam_beta2",
                                       "adam_epsilon", "clip_norm")] + [
         ("precision", ctypes.c_int), ("clip_outputs", ctypes.c_int), ("clip_lo", ctypes.c_float),
-        ("clip_hi", ctypes.c_float)]
+        ("clip_hi", ctypes.c_float)] + [(n, ctypes.c_int) for n in (
+            "postnet", "postnet_layers", "postnet_channels", "postnet_kernel")] + [
+        ("bn_momentum", ctypes.c_float), ("bn_eps", ctypes.c_float)]
 
 
 _P = ctypes.c_void_p
@@ -126,7 +128,7 @@ SIGNATURES = {
     "tt2_train_load_tensor": (_I, [_P, ctypes.c_char_p, _P, _P, _I]),
     "tt2_train_finalize": (_I, [_P]),
     "tt2_train_bind_grads_dev": (_I, [_P, _P, ctypes.POINTER(ctypes.c_int64)]),
-    "tt2_train_forward_backward_dev": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "tt2_train_forward_backward_dev": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "tt2_train_apply_dev": (_I, [_P, _F, _I, _P]),
     "tt2_train_losses": (_I, [_P, _P, _P]),
     "tt2_train_get_tensor": (_I, [_P, ctypes.c_char_p, _I, _P]),

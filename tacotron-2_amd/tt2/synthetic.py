@@ -55,3 +55,9 @@ def zoneout_masks(n, B, H, rate=0.1, seed=5339):
     """Training-mode zoneout keep bits (modules.py:236-240: dropout(new - prev, 1 - rate)) of the
     two decoder LSTMs: [n, 4, B, H] uint8 (c1, h1, c2, h2)."""
     return (np.random.default_rng(seed + 1).random((n, 4, B, H)) >= rate).astype(np.uint8)
+
+
+def postnet_masks(layers, B, T, C, rate=0.5, seed=5339):
+    """Postnet dropout keep bits (modules.py:496-497, tacotron_dropout_rate 0.5, training=True):
+    [layers, B, T, C] uint8."""
+    return (np.random.default_rng(seed + 2).random((layers, B, T, C)) >= rate).astype(np.uint8)

@@ -28,7 +28,7 @@ def learning_rate(step, hp):
     return min(max(lr, hp.tacotron_final_learning_rate), init)
 
 
-def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32"):
+def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32", postnet=True):
     lib = _lib.load_library()
     cfg = _lib.TrainConfig()
     lib.tt2_train_default_config(ctypes.byref(cfg), batch, max_T_in, max_T_out)
@@ -66,6 +66,11 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
     cfg.clip_outputs = 1 if hp.clip_outputs else 0
     cfg.clip_lo = lo - hp.lower_bound_decay
     cfg.clip_hi = hi
+    # Postnet + after loss (tacotron.py:362-381, 775-776)
+    cfg.postnet = 1 if postnet else 0
+    cfg.postnet_layers = hp.postnet_num_layers
+    cfg.postnet_channels = hp.postnet_channels
+    cfg.postnet_kernel = hp.postnet_kernel_size[0]
     return cfg
 
 
@@ -74,13 +79,14 @@ class TacotronTrainer(object):
     runs on the trainer's own torch stream (passed to the library explicitly)."""
 
     def __init__(self, hp, weights, batch, max_T_in, max_T_out, device=0, emt_only=False,
-                 precision="fp32"):
+                 precision="fp32", postnet=True):
         import torch
         self.torch = torch
         self.lib = _lib.load_library()
         self.hp = hp
         self.device = torch.device("cuda", device)
-        self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only, precision)
+        self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only, precision, postnet)
+        self.postnet = postnet
         self.B = batch
         h = ctypes.c_void_p()
         check(self.lib.tt2_train_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
@@ -122,8 +128,10 @@ class TacotronTrainer(object):
         return t.from_numpy(np.ascontiguousarray(a)).to(self.device, dtype, non_blocking=False)
 
     def forward_backward(self, memory, lengths, targets, stop_targets, prenet_masks,
-                         zoneout_masks=None):
-        """Teacher-forced forward + losses + backward; gradients land in the flat buffer."""
+                         zoneout_masks=None, postnet_masks=None):
+        """Teacher-forced forward + losses + backward; gradients land in the flat buffer.
+        postnet_masks: Postnet dropout keep bits [layers, B, T_out, channels] (None = no
+        dropout)."""
         t = self.torch
         with t.cuda.stream(self.stream):
             mem = self._dev(memory, t.float32)
@@ -132,6 +140,7 @@ class TacotronTrainer(object):
             st = self._dev(stop_targets, t.float32)
             pm = self._dev(prenet_masks, t.uint8)
             zm = self._dev(zoneout_masks, t.uint8)
+            pnm = self._dev(postnet_masks, t.uint8) if self.postnet else None
             B, T_in, _ = mem.shape
             T_out = tg.shape[1]
             if B != self.B:
@@ -140,10 +149,13 @@ class TacotronTrainer(object):
                 raise ValueError("prenet_masks must be [T_out, 2, B, prenet_units]")
             if zm is not None and tuple(zm.shape) != (T_out, 4, B, self.cfg.decoder_lstm_units):
                 raise ValueError("zoneout_masks must be [T_out, 4, B, decoder_lstm_units]")
-            self._keep = (mem, lens, tg, st, pm, zm)      # alive until the stream has used them
+            if pnm is not None and tuple(pnm.shape) != (self.cfg.postnet_layers, B, T_out,
+                                                        self.cfg.postnet_channels):
+                raise ValueError("postnet_masks must be [layers, B, T_out, channels]")
+            self._keep = (mem, lens, tg, st, pm, zm, pnm)  # alive until the stream has used them
             ptr = (lambda x: None if x is None else ctypes.c_void_p(x.data_ptr()))
             check(self.lib.tt2_train_forward_backward_dev(
-                self.h, ptr(mem), ptr(lens), ptr(tg), ptr(st), ptr(pm), ptr(zm), T_in, T_out,
+                self.h, ptr(mem), ptr(lens), ptr(tg), ptr(st), ptr(pm), ptr(zm), ptr(pnm), T_in, T_out,
                 ctypes.c_void_p(self.stream.cuda_stream)))
 
     def allreduce_grads(self, group=None):
@@ -167,21 +179,24 @@ class TacotronTrainer(object):
                                            ctypes.c_void_p(self.stream.cuda_stream)))
         return lr
 
-    def step(self, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks=None):
+    def step(self, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks=None,
+             postnet_masks=None):
         """One training step (forward, backward, DP all-reduce when initialised, clipped Adam);
         returns the losses dict."""
-        self.forward_backward(memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks)
+        self.forward_backward(memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,
+                              postnet_masks)
         self.allreduce_grads()
         self.apply()
         return self.losses()
 
     def losses(self):
-        out = np.zeros(4, np.float32)
+        out = np.zeros(5, np.float32)
         ms = ctypes.c_float()
         check(self.lib.tt2_train_losses(self.h, out.ctypes.data_as(ctypes.c_void_p),
                                         ctypes.byref(ms)))
         return dict(before=float(out[0]), stop_token=float(out[1]), regularization=float(out[2]),
-                    loss=float(out[0] + out[1] + out[2]), grad_norm=float(out[3]),
+                    after=float(out[4]), loss=float(out[0] + out[1] + out[2] + out[4]),
+                    grad_norm=float(out[3]),
                     forward_backward_ms=float(ms.value))
 
     def get(self, name, which=0, shape=None):

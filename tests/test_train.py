@@ -13,7 +13,7 @@ from _common import small_hparams
 from oracle import tacotron_ref as TR
 from oracle import train_ref as TRN
 from oracle.hp import oracle_hp
-from tt2.synthetic import prenet_masks, train_batch, zoneout_masks
+from tt2.synthetic import postnet_masks, prenet_masks, train_batch, zoneout_masks
 from tt2.weights import init_tacotron_weights, memory_width
 
 MEM_K = "Tacotron_model/inference/memory_layer/kernel"
@@ -81,6 +81,37 @@ def test_oracle_gradients_match_finite_differences():
         assert np.all(g["memory"][b, lens[b]:] == 0)
 
 
+def test_oracle_postnet_gradients_match_finite_differences():
+    """Postnet in training mode (batch-statistics BN, dropout, clipped after loss): autograd of
+    the restatement vs central differences on conv, BN and projection variables."""
+    hp = small_hparams()
+    W, mem, lens, tg, st, pm, zm = _case(hp, B=2, T_in=6, T_out=5)
+    pnm = postnet_masks(hp.postnet_num_layers, 2, 5, hp.postnet_channels)
+    _, L, g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, 1e-3, postnet=True, postnet_masks=pnm)
+    assert len(L) == 4 and L[3] > 0
+
+    def loss_of(W2):
+        _, L2, _ = TRN.train_grads(W2, mem, lens, tg, st, pm, zm, 1e-3, postnet=True,
+                                   postnet_masks=pnm)
+        return sum(L2)
+
+    rng = np.random.default_rng(1)
+    eps = 1e-6
+    for name in (TRN.PN.format(1) + "conv1d/kernel", TRN.PN.format(3) + "batch_normalization/gamma",
+                 TRN.PN.format(5) + "batch_normalization/beta", TRN.PP + "kernel",
+                 TRN.L2 + "kernel"):
+        arr = np.asarray(W[name], np.float64)
+        for _ in range(2):
+            idx = tuple(rng.integers(0, n) for n in arr.shape)
+            Wp, Wm = dict(W), dict(W)
+            ap, am = arr.copy(), arr.copy()
+            ap[idx] += eps
+            am[idx] -= eps
+            Wp[name], Wm[name] = ap, am
+            fd = (loss_of(Wp) - loss_of(Wm)) / (2 * eps)
+            assert abs(fd - g[name][idx]) < 1e-6 + 1e-5 * abs(fd), (name, idx, fd, g[name][idx])
+
+
 def test_learning_rate_and_adam_formulas():
     hp = small_hparams()
     assert TRN.learning_rate(0, hp) == hp.tacotron_initial_learning_rate
@@ -117,7 +148,7 @@ def _gpu_vs_oracle(hp, B, T_in, T_out, use_zoneout_masks=True, seed=11):
     W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out, seed)
     if not use_zoneout_masks:
         zm = None
-    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0)
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, postnet=False)
     try:
         tr.forward_backward(mem, lens, tg, st, pm, zm)
         L = tr.losses()
@@ -194,7 +225,7 @@ def test_gpu_train_adam_updates_match_oracle():
     p = {n: np.asarray(W[n], np.float64) for n in names}
     m = {n: np.zeros_like(p[n]) for n in names}
     v = {n: np.zeros_like(p[n]) for n in names}
-    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0)
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, postnet=False)
     try:
         for step in (1, 2):
             tr.forward_backward(mem, lens, tg, st, pm, zm)
@@ -224,7 +255,7 @@ def test_gpu_train_bf16_gemms_close_to_oracle():
                                decoder_lstm_units=1024))
     B, T_in, T_out = 4, 37, 10
     W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
-    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16")
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", postnet=False)
     try:
         tr.forward_backward(mem, lens, tg, st, pm, zm)
         L = tr.losses()
@@ -251,3 +282,49 @@ def test_gpu_train_bf16_gemms_close_to_oracle():
             assert frob[n] < 0.1, (n, frob[n])
         else:
             assert e < 1e-2, (n, e)  # measured 0.2-0.5 % (bf16 operand rounding)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dropout", [True, False])
+def test_gpu_train_with_postnet(dropout):
+    """Decoder + Postnet training step (tacotron.py:362-381): training-mode batch norm, Postnet
+    dropout keep bits, after loss on the clipped mel; every gradient (decoder, Postnet convs, BN
+    gamma/beta, projection) and d memory against the float64 oracle, then apply() moves the BN
+    moving averages by (1 - 0.99)·(batch - moving) (UPDATE_OPS)."""
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    B, T_in, T_out = 3, 9, 12
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels) if dropout else None
+    names = TRN.train_var_names() + TRN.postnet_var_names()
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0)
+    try:
+        tr.forward_backward(mem, lens, tg, st, pm, zm, pnm)
+        L = tr.losses()
+        grads = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}
+        gmem = tr.get("memory", 1, mem.shape)
+        tr.apply(1)
+        tr.losses()
+        moving = {n: tr.get(n, 0, np.asarray(W[n]).shape) for n in TRN.postnet_stat_names()}
+    finally:
+        tr.close()
+    out, (b, s, r, after), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm,
+                                               hp.tacotron_reg_weight, clip=_clip(hp),
+                                               postnet=True, postnet_masks=pnm)
+    assert abs(L["before"] - b) < 1e-5 * b
+    assert abs(L["after"] - after) < 1e-5 * after, (L["after"], after)
+    assert abs(L["regularization"] - r) < 1e-4 * r
+    for n in names:
+        if np.abs(g[n]).max() < 1e-12:
+            # the last conv's bias feeds batch-statistics BN directly (no tanh): its gradient is
+            # exactly zero in exact arithmetic, fp32 leaves rounding noise
+            assert np.abs(grads[n]).max() < 1e-6, n
+            continue
+        assert _rel(grads[n], g[n]) < 2e-4, (n, _rel(grads[n], g[n]))
+    assert _rel(gmem, g["memory"]) < 2e-4
+    for i, (bm, bv) in enumerate(out["bn_stats"]):
+        mn, vn = TRN.postnet_stat_names()[2 * i: 2 * i + 2]
+        np.testing.assert_allclose(moving[mn], TRN.bn_moving_update(np.asarray(W[mn], np.float64), bm),
+                                   rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(moving[vn], TRN.bn_moving_update(np.asarray(W[vn], np.float64), bv),
+                                   rtol=1e-5, atol=1e-6)
