@@ -48,8 +48,12 @@ struct GemmArgs {
   long ldbt = 0;
   long kpart_floats = 0;
   int ksplit = 1;  // set by the dispatcher
+  int raw = 0;     // internal: partials only (gemm_raw)
 };
 
 void gemm(const GemmArgs& a, hipStream_t s);
+// Same product, but the raw fp32 partial sums are left in a.kpart as [ks][M][N] (no epilogue, no
+// combine launch; ks >= 1 is returned) for a caller-fused combine.  a.kpart is required.
+int gemm_raw(const GemmArgs& a, hipStream_t s);
 
 }  // namespace tt2

@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  if (g.ksplit > 1) {  // raw partial tile -> kpart[z][M][N]
+  if (g.ksplit > 1 || g.raw) {  // raw partial tile -> kpart[z][M][N]
     float* P = g.kpart + (long)blockIdx.z * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < WMB; ++i)
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[i][j][q] *= X3_UNSCALE;
   }
-  if (g.ksplit > 1) {  // raw partial tile -> kpart[z][M][N]
+  if (g.ksplit > 1 || g.raw) {  // raw partial tile -> kpart[z][M][N]
     float* P = g.kpart + (long)blockIdx.z * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < WMB; ++i)
@@ -422,7 +422,22 @@ static void launch(const GemmArgs& a, bool va, bool vb, hipStream_t s) {
 
 static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+int gemm_impl(const GemmArgs& a, hipStream_t s);
+
+int gemm_raw(const GemmArgs& a, hipStream_t s) {
+  TT2_CHECK(a.kpart, TT2_ERR_INVALID_ARG, "gemm_raw: kpart required");
+  GemmArgs g = a;
+  g.raw = 1;
+  return gemm_impl(g, s);
+}
+
 void gemm(const GemmArgs& a, hipStream_t s) {
+  GemmArgs g = a;
+  g.raw = 0;
+  (void)gemm_impl(g, s);
+}
+
+int gemm_impl(const GemmArgs& a, hipStream_t s) {
   TT2_CHECK(a.M > 0 && a.N > 0 && a.K > 0, TT2_ERR_SHAPE_MISMATCH, "gemm: empty problem");
   bool va = al16(a.A);
   if (a.a_mode == A_DENSE) va = va && (a.lda % 4 == 0);
@@ -461,11 +476,11 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     }
 #undef TT2_X3
     TT2_HIP(hipGetLastError());
-    if (g.ksplit > 1) {
+    if (g.ksplit > 1 && !g.raw) {
       hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256)), dim3(256), 0, s, g);
       TT2_HIP(hipGetLastError());
     }
-    return;
+    return g.ksplit;
   }
   const bool vb = al16(a.Bw) && (a.ldb % 4 == 0);
   const int wnb = a.N <= 64 ? 1 : 2;
@@ -489,10 +504,11 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   else if (wmb == 2) launch<2, 1>(g, va, vb, s);
   else if (wnb == 2) launch<1, 2>(g, va, vb, s);
   else launch<1, 1>(g, va, vb, s);
-  if (g.ksplit > 1) {
+  if (g.ksplit > 1 && !g.raw) {
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256)), dim3(256), 0, s, g);
     TT2_HIP(hipGetLastError());
   }
+  return g.ksplit;
 }
 
 }  // namespace tt2

@@ -192,6 +192,9 @@ __global__ void k_tr_prenet_mask(float* __restrict__ x, long ld, const uint8_t* 
 // G [B,4H] pre-activations (bias added) -> overwritten with (σi, tanh j, σ(f+1), σo).
 struct TrLstmFwd {
   float* G;
+  const float* part;  // non-null: G's pre-activations = sum over ks raw split-K partials [ks][B][4H] + bias
+  int ks;
+  const float* bias;
   const float* c_prev;   // [B,H]
   const float* hz_prev;  // strided
   long ld_hz_prev;
@@ -210,8 +213,23 @@ __global__ void k_tr_lstm_fwd(TrLstmFwd a) {
   if (i >= a.B * a.H) return;
   const int b = i / a.H, n = i % a.H;
   float* g = a.G + (long)b * 4 * a.H;
-  const float si = sigm_acc(g[n]), tj = tanhf(g[a.H + n]), sf = sigm_acc(g[2 * a.H + n] + 1.0f),
-              so = sigm_acc(g[3 * a.H + n]);
+  float pre[4];
+  if (a.part) {  // fused split-K combine (gemm_raw): 4 independent chains, loads unrolled
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pre[q] = a.bias[q * a.H + n];
+    const float* p0 = a.part + (long)b * 4 * a.H + n;
+    const long zs = (long)a.B * 4 * a.H;
+#pragma unroll 4
+    for (int z = 0; z < a.ks; ++z) {
+      const float* pz = p0 + z * zs;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pre[q] += pz[q * a.H];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pre[q] = g[q * a.H + n];
+  }
+  const float si = sigm_acc(pre[0]), tj = tanhf(pre[1]), sf = sigm_acc(pre[2] + 1.0f), so = sigm_acc(pre[3]);
   g[n] = si;
   g[a.H + n] = tj;
   g[2 * a.H + n] = sf;
@@ -413,8 +431,17 @@ __global__ void k_tr_loss_final(const float* __restrict__ part, int nb, long nf,
 
 // ---- backward ------------------------------------------------------------------------------
 struct TrLstmBwd {
-  const float* dh_ext;  // strided d h_new from the layer's consumers
+  const float* dh_ext;  // strided d h_new from the layer's consumers (or residual with part)
   long ld_dh;
+  // non-null: d h_new = sum_z part[z][b][n] (+ dh_ext[b][n] if dh_ext) from a raw split-K GEMM
+  // with pN columns; side != null also combines columns [H, 2H) (+ side_res) into side[b][n]
+  const float* part;
+  int ks;
+  long pN;
+  float* side;
+  long ld_side;
+  const float* side_res;
+  long ld_side_res;
   const float* dhz;     // strided d(zoned h_t) from step t+1
   long ld_dhz;
   float* DC;            // [B,H] in: d(zoned c_t); out: d(zoned c_{t-1})
@@ -445,7 +472,27 @@ __global__ void k_tr_lstm_bwd(TrLstmBwd a) {
   }
   const float dhz = a.dhz[(long)b * a.ld_dhz + n];
   const float dcz = a.DC[i];
-  const float dhn = a.dh_ext[(long)b * a.ld_dh + n] + kh * dhz;
+  float dext;
+  if (a.part) {
+    dext = a.dh_ext ? a.dh_ext[(long)b * a.ld_dh + n] : 0.f;
+    float sd = a.side ? a.side_res[(long)b * a.ld_side_res + a.H + n] : 0.f;
+    const long zs = (long)a.B * a.pN;
+    const float* p0 = a.part + (long)b * a.pN + n;
+    if (a.side) {
+#pragma unroll 4
+      for (int z = 0; z < a.ks; ++z) {
+        dext += p0[z * zs];
+        sd += p0[z * zs + a.H];
+      }
+    } else {
+#pragma unroll 4
+      for (int z = 0; z < a.ks; ++z) dext += p0[z * zs];
+    }
+    if (a.side) a.side[(long)b * a.ld_side + n] = sd;
+  } else {
+    dext = a.dh_ext[(long)b * a.ld_dh + n];
+  }
+  const float dhn = dext + kh * dhz;
   const float cnew = a.cn[i];
   const float tc = tanhf(cnew);
   const float dcn = kc * dcz + dhn * so * (1.f - tc * tc);
@@ -858,6 +905,21 @@ static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* 
   gemm(g, s);
 }
 
+// raw split-K product for a fused combine: partials [ks][M][N] in the context's kpart; returns ks
+static int tr_gemm_raw(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, hipStream_t s,
+                       const DevBuf* bt16 = nullptr, long ldbt = 0) {
+  GemmArgs g;
+  if (g_tr_prec == 2 && bt16 && bt16->p && ldbt % 8 == 0) {
+    g.Bt16 = bt16->p;
+    g.ldbt = ldbt;
+  }
+  g.kpart = g_tr_kpart->as<float>();
+  g.kpart_floats = (long)(g_tr_kpart->bytes / sizeof(float));
+  g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.Bw = Bw; g.ldb = ldb; g.Cout = nullptr; g.ldc = N;
+  g.split16 = g_tr_prec;
+  return gemm_raw(g, s);
+}
+
 static void tr_gemm_run(GemmArgs& g, hipStream_t s) {  // conv-mode products: same precision / split-K
   if (g_tr_kpart) {
     g.kpart = g_tr_kpart->as<float>();
@@ -1143,17 +1205,23 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
 
   for (int t = 0; t < T; ++t) {
     const long s1 = (long)t * B;
-    tr_gemm(B, 4 * H, LX1, X1 + s1 * LX1, LX1, pvar(c, L1V("kernel")), 4 * H, c->G1.as<float>() + s1 * 4 * H, 4 * H, s,
-            pvar(c, L1V("bias")), nullptr, 0, ACT_NONE, &c->hK1T, LX1);
-    TrLstmFwd l1{c->G1.as<float>() + s1 * 4 * H, c->C1.as<float>() + s1 * H, X1 + s1 * LX1 + P + D, LX1, zm, t, 0, B, H,
-                 z, c->CN1.as<float>() + s1 * H, c->C1.as<float>() + (s1 + B) * H, X2 + s1 * 2 * H, 2 * H,
-                 X1 + (s1 + B) * LX1 + P + D, LX1};
+    // LSTM-1: raw split-K product, combine + bias + cell + zoneout fused in k_tr_lstm_fwd
+    const int k1 = tr_gemm_raw(B, 4 * H, LX1, X1 + s1 * LX1, LX1, pvar(c, L1V("kernel")), 4 * H, s, &c->hK1T, LX1);
+    TrLstmFwd l1{};
+    l1.G = c->G1.as<float>() + s1 * 4 * H; l1.part = c->kpart.as<float>(); l1.ks = k1; l1.bias = pvar(c, L1V("bias"));
+    l1.c_prev = c->C1.as<float>() + s1 * H; l1.hz_prev = X1 + s1 * LX1 + P + D; l1.ld_hz_prev = LX1;
+    l1.zm = zm; l1.t = t; l1.layer = 0; l1.B = B; l1.H = H; l1.z = z;
+    l1.cn = c->CN1.as<float>() + s1 * H; l1.c_out = c->C1.as<float>() + (s1 + B) * H;
+    l1.h_out = X2 + s1 * 2 * H; l1.ld_h = 2 * H; l1.hz_out = X1 + (s1 + B) * LX1 + P + D; l1.ld_hz = LX1;
     hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l1);
-    tr_gemm(B, 4 * H, 2 * H, X2 + s1 * 2 * H, 2 * H, pvar(c, L2V("kernel")), 4 * H, c->G2.as<float>() + s1 * 4 * H,
-            4 * H, s, pvar(c, L2V("bias")), nullptr, 0, ACT_NONE, &c->hK2T, 2 * H);
-    TrLstmFwd l2{c->G2.as<float>() + s1 * 4 * H, c->C2.as<float>() + s1 * H, X2 + s1 * 2 * H + H, 2 * H, zm, t, 1, B,
-                 H, z, c->CN2.as<float>() + s1 * H, c->C2.as<float>() + (s1 + B) * H, PIN + s1 * (H + D), H + D,
-                 X2 + (s1 + B) * 2 * H + H, 2 * H};
+    const int k2 = tr_gemm_raw(B, 4 * H, 2 * H, X2 + s1 * 2 * H, 2 * H, pvar(c, L2V("kernel")), 4 * H, s, &c->hK2T,
+                               2 * H);
+    TrLstmFwd l2{};
+    l2.G = c->G2.as<float>() + s1 * 4 * H; l2.part = c->kpart.as<float>(); l2.ks = k2; l2.bias = pvar(c, L2V("bias"));
+    l2.c_prev = c->C2.as<float>() + s1 * H; l2.hz_prev = X2 + s1 * 2 * H + H; l2.ld_hz_prev = 2 * H;
+    l2.zm = zm; l2.t = t; l2.layer = 1; l2.B = B; l2.H = H; l2.z = z;
+    l2.cn = c->CN2.as<float>() + s1 * H; l2.c_out = c->C2.as<float>() + (s1 + B) * H;
+    l2.h_out = PIN + s1 * (H + D); l2.ld_h = H + D; l2.hz_out = X2 + (s1 + B) * 2 * H + H; l2.ld_hz = 2 * H;
     hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l2);
     tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
             c->Q.as<float>() + s1 * A, A, s, nullptr, nullptr, 0, ACT_NONE, &c->hWqT, H);
@@ -1187,17 +1255,26 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     hipLaunchKernelGGL(k_tr_att_dalign, att_grid, dim3(256), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(256), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
-    tr_gemm(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, c->DH2.as<float>(), H, s, nullptr,
-            dPIN + s1 * (H + D), H + D, ACT_NONE, &c->hWq, A);
-    TrLstmBwd b2{c->DH2.as<float>(), H, dX2 + (s1 + B) * 2 * H + H, 2 * H, c->DC2.as<float>(),
-                 c->G2.as<float>() + s1 * 4 * H, c->CN2.as<float>() + s1 * H, c->C2.as<float>() + s1 * H, zm, t, 1, B,
-                 H, z, c->dG2.as<float>() + s1 * 4 * H, c->R2.as<float>(), 2 * H, H};
+    // LSTM-2 backward: d h2 = DQ·Wq^T (raw split-K) + d PIN[t][:, :H], combined in the cell kernel
+    const int kq = tr_gemm_raw(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, s, &c->hWq, A);
+    TrLstmBwd b2{};
+    b2.dh_ext = dPIN + s1 * (H + D); b2.ld_dh = H + D; b2.part = c->kpart.as<float>(); b2.ks = kq; b2.pN = H;
+    b2.dhz = dX2 + (s1 + B) * 2 * H + H; b2.ld_dhz = 2 * H; b2.DC = c->DC2.as<float>();
+    b2.G = c->G2.as<float>() + s1 * 4 * H; b2.cn = c->CN2.as<float>() + s1 * H; b2.c_prev = c->C2.as<float>() + s1 * H;
+    b2.zm = zm; b2.t = t; b2.layer = 1; b2.B = B; b2.H = H; b2.z = z;
+    b2.dG = c->dG2.as<float>() + s1 * 4 * H; b2.R = c->R2.as<float>(); b2.ldr = 2 * H; b2.off_r = H;
     hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b2);
-    tr_gemm(B, 2 * H, 4 * H, c->dG2.as<float>() + s1 * 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, dX2 + s1 * 2 * H,
-            2 * H, s, nullptr, c->R2.as<float>(), 2 * H, ACT_NONE, &c->hK2, 4 * H);
-    TrLstmBwd b1{dX2 + s1 * 2 * H, 2 * H, dX1 + (s1 + B) * LX1 + P + D, LX1, c->DC1.as<float>(),
-                 c->G1.as<float>() + s1 * 4 * H, c->CN1.as<float>() + s1 * H, c->C1.as<float>() + s1 * H, zm, t, 0, B,
-                 H, z, c->dG1.as<float>() + s1 * 4 * H, c->R1.as<float>(), LX1, P + D};
+    // dX2 = dG2·K2^T + R2 (raw split-K): columns [0,H) are d h1_new (consumed by the LSTM-1
+    // backward), columns [H,2H) = d hz2_{t-1} are written to dX2[t] by the same kernel
+    const int kx = tr_gemm_raw(B, 2 * H, 4 * H, c->dG2.as<float>() + s1 * 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, s,
+                               &c->hK2, 4 * H);
+    TrLstmBwd b1{};
+    b1.dh_ext = nullptr; b1.ld_dh = 0; b1.part = c->kpart.as<float>(); b1.ks = kx; b1.pN = 2 * H;
+    b1.side = dX2 + s1 * 2 * H + H; b1.ld_side = 2 * H; b1.side_res = c->R2.as<float>(); b1.ld_side_res = 2 * H;
+    b1.dhz = dX1 + (s1 + B) * LX1 + P + D; b1.ld_dhz = LX1; b1.DC = c->DC1.as<float>();
+    b1.G = c->G1.as<float>() + s1 * 4 * H; b1.cn = c->CN1.as<float>() + s1 * H; b1.c_prev = c->C1.as<float>() + s1 * H;
+    b1.zm = zm; b1.t = t; b1.layer = 0; b1.B = B; b1.H = H; b1.z = z;
+    b1.dG = c->dG1.as<float>() + s1 * 4 * H; b1.R = c->R1.as<float>(); b1.ldr = LX1; b1.off_r = P + D;
     hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b1);
     tr_gemm(B, LX1, 4 * H, c->dG1.as<float>() + s1 * 4 * H, 4 * H, c->K1T.as<float>(), LX1, dX1 + s1 * LX1, LX1, s,
             nullptr, c->R1.as<float>(), LX1, ACT_NONE, &c->hK1, 4 * H);
