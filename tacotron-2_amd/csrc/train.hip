@@ -76,6 +76,7 @@ namespace tt2 {
 
 constexpr int TR_MAX_TIN = 320;  // LDS budget of the attention kernels
 constexpr int TR_JT = 16;        // j rows (encoder positions) per attention work-group
+constexpr int TR_AT = 1024;      // threads of the energy / d-align / energy-backward work-groups
 
 __device__ __forceinline__ float sigm_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
 
@@ -311,21 +312,21 @@ __device__ __forceinline__ void tr_locf_tile(const TrAtt& a, int b, int j0, floa
 
 // Energies e_j = Σ_k v_a[k]·tanh(keys_jk + q_k + loc_jk + b_a[k]) (attention.py:37-69) for one
 // tile of TR_JT rows; grid (nt, B) spreads a step over the chip.  Keeps tanh for the backward.
-__global__ __launch_bounds__(256) void k_tr_att_energy(TrAtt a) {
+__global__ __launch_bounds__(TR_AT) void k_tr_att_energy(TrAtt a) {
   __shared__ float cseg[TR_JT + 64];
   __shared__ float f[TR_JT * 32];
   __shared__ float Wl[32 * 256];
   const int b = blockIdx.y, j0 = blockIdx.x * TR_JT;
   for (int i = threadIdx.x; i < a.F * a.A; i += blockDim.x) Wl[i] = a.Wl[i];
   tr_locf_tile(a, b, j0, cseg, f);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const long tb = (long)a.t * a.B + b;
   for (int i = threadIdx.x; i < TR_JT * a.F; i += blockDim.x) {
     const int j = j0 + i / a.F;
     if (j < a.Tin) a.FALL[(tb * a.Tin + j0) * a.F + i] = f[i];
   }
   const float* q = a.Q + tb * a.A;
-  for (int jj = wave; jj < TR_JT; jj += 4) {
+  for (int jj = wave; jj < TR_JT; jj += nw) {
     const int j = j0 + jj;
     if (j >= a.Tin) break;
     float acc = 0.f;
@@ -508,7 +509,7 @@ __global__ void k_tr_lstm_bwd(TrLstmBwd a) {
 
 // ---- attention backward for one step: three chip-wide launches over (j-tile, row) ----
 // (1) d align_j = dctx_t · values_j + d cum_t[j]  (cum_t = cum_{t-1} + align_t)
-__global__ __launch_bounds__(256) void k_tr_att_dalign(TrAtt a) {
+__global__ __launch_bounds__(TR_AT) void k_tr_att_dalign(TrAtt a) {
   __shared__ float dctx[1024];
   const int b = blockIdx.y, j0 = blockIdx.x * TR_JT;
   const long tb = (long)a.t * a.B + b;
@@ -518,8 +519,8 @@ __global__ __launch_bounds__(256) void k_tr_att_dalign(TrAtt a) {
     if (blockIdx.x == 0) a.DCTX[tb * a.D + n] = v;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int jj = wave; jj < TR_JT; jj += 4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int jj = wave; jj < TR_JT; jj += nw) {
     const int j = j0 + jj;
     if (j >= a.Tin) break;
     const float* v = a.values + ((long)b * a.Tin + j) * a.D;
@@ -532,11 +533,11 @@ __global__ __launch_bounds__(256) void k_tr_att_dalign(TrAtt a) {
 
 // (2) softmax backward de_j = a_j (da_j - Σ a·da), tanh backward du_jk = de_j v_k (1 - th²):
 // d keys (+=), per-tile partials of d v_a, d b_a (= d q), du kept for d W_loc, d f = du · W_loc^T
-__global__ __launch_bounds__(256) void k_tr_att_energy_bwd(TrAtt a) {
+__global__ __launch_bounds__(TR_AT) void k_tr_att_energy_bwd(TrAtt a) {
   __shared__ float WlT[256 * 33];
   __shared__ float dU[TR_JT * 256];
   __shared__ float de[TR_JT];
-  __shared__ float racc[2 * 256];
+  __shared__ float racc[2 * TR_AT];
   __shared__ float s16[16];
   const int b = blockIdx.y, tile = blockIdx.x, j0 = tile * TR_JT, tid = threadIdx.x;
   const long tb = (long)a.t * a.B + b;
@@ -569,14 +570,14 @@ __global__ __launch_bounds__(256) void k_tr_att_energy_bwd(TrAtt a) {
     dU[jj * a.A + k] = du;
   }
   racc[tid] = dv;
-  racc[256 + tid] = dq;
+  racc[TR_AT + tid] = dq;
   __syncthreads();
   const long pt = (long)b * a.nt + tile;
   if (tid < a.A) {
     float sv = 0.f, sq = 0.f;
     for (int g = 0; g < NJ; ++g) {
       sv += racc[g * a.A + tid];
-      sq += racc[256 + g * a.A + tid];
+      sq += racc[TR_AT + g * a.A + tid];
     }
     a.PQ[pt * a.A + tid] = sq;
     a.dV[pt * a.A + tid] += sv;
@@ -1226,7 +1227,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
             c->Q.as<float>() + s1 * A, A, s, nullptr, nullptr, 0, ACT_NONE, &c->hWqT, H);
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(256), 0, s, at);
+    hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(TR_AT), 0, s, at);
     hipLaunchKernelGGL(k_tr_ctx, dim3((D + 255) / 256, B), dim3(256), sizeof(float) * Tin, s, at);
   }
   tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
@@ -1252,8 +1253,8 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   for (int t = T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_dalign, att_grid, dim3(256), 0, s, at);
-    hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(256), 0, s, at);
+    hipLaunchKernelGGL(k_tr_att_dalign, att_grid, dim3(TR_AT), 0, s, at);
+    hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(TR_AT), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
     // LSTM-2 backward: d h2 = DQ·Wq^T (raw split-K) + d PIN[t][:, :H], combined in the cell kernel
     const int kq = tr_gemm_raw(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, s, &c->hWq, A);
