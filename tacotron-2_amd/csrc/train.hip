@@ -348,7 +348,7 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy(TrAtt a) {
 __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
   extern __shared__ float al[];
   __shared__ float s16[16];
-  const int b = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
   const int len = a.lens[b];
   const float* e = a.E + (long)b * a.Tin;
   float mx = -INFINITY;
@@ -372,12 +372,23 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
     }
   }
   __syncthreads();
-  if (n >= a.D) return;
-  const float* v = a.values + (long)b * a.Tin * a.D + n;
+  // 64 channels per work-group, the 4 waves split the encoder rows (j = wave mod 4), LDS combine
+  __shared__ float red[4][64];
+  const int nl = threadIdx.x & 63, wq = threadIdx.x >> 6;
+  const int nc = blockIdx.x * 64 + nl;
   float acc = 0.f;
-  for (int j = 0; j < a.Tin; ++j) acc += al[j] * v[(long)j * a.D];
-  a.PIN[tb * (a.H + a.D) + a.H + n] = acc;
-  a.X1[(tb + a.B) * (a.P + a.D + a.H) + a.P + n] = acc;
+  if (nc < a.D) {
+    const float* v = a.values + (long)b * a.Tin * a.D + nc;
+#pragma unroll 4
+    for (int j = wq; j < a.Tin; j += 4) acc += al[j] * v[(long)j * a.D];
+  }
+  red[wq][nl] = acc;
+  __syncthreads();
+  if (wq == 0 && nc < a.D) {
+    const float r = red[0][nl] + red[1][nl] + red[2][nl] + red[3][nl];
+    a.PIN[tb * (a.H + a.D) + a.H + nc] = r;
+    a.X1[(tb + a.B) * (a.P + a.D + a.H) + a.P + nc] = r;
+  }
 }
 
 // frame MSE + stop sigmoid CE (tacotron.py:774,778-779) and their output gradients.  Frames are
@@ -1228,7 +1239,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
             c->Q.as<float>() + s1 * A, A, s, nullptr, nullptr, 0, ACT_NONE, &c->hWqT, H);
     at.t = t;
     hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(TR_AT), 0, s, at);
-    hipLaunchKernelGGL(k_tr_ctx, dim3((D + 255) / 256, B), dim3(256), sizeof(float) * Tin, s, at);
+    hipLaunchKernelGGL(k_tr_ctx, dim3((D + 63) / 64, B), dim3(256), sizeof(float) * Tin, s, at);
   }
   tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
   tr_gemm((int)TB, 1, H + D, PIN, H + D, pvar(c, SPV("kernel")), 1, c->ST.as<float>(), 1, s, pvar(c, SPV("bias")));
