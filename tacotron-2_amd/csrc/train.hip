@@ -1421,6 +1421,12 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
               TT2_ERR_INVALID_ARG, "attention_dim must divide 256");
     TT2_CHECK(cfg->attention_filters >= 1 && cfg->attention_filters <= 32, TT2_ERR_INVALID_ARG,
               "attention_filters must be <= 32");
+    // LDS tiles of the attention kernels: location-conv window (TR_JT + 64), d context (1024)
+    TT2_CHECK(cfg->attention_kernel >= 1 && cfg->attention_kernel <= 65, TT2_ERR_INVALID_ARG,
+              "attention_kernel must be <= 65");
+    TT2_CHECK(cfg->memory_dim >= 1 && cfg->memory_dim <= 1024, TT2_ERR_INVALID_ARG, "memory_dim must be <= 1024");
+    TT2_CHECK(cfg->prenet_units >= 1 && cfg->decoder_lstm_units >= 1 && cfg->num_mels >= 1, TT2_ERR_INVALID_ARG,
+              "bad widths");
     int n = 0;
     TT2_HIP(hipGetDeviceCount(&n));
     TT2_CHECK(hip_device >= 0 && hip_device < n, TT2_ERR_HIP, "no such HIP device");

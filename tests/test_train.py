@@ -328,3 +328,26 @@ def test_gpu_train_with_postnet(dropout):
                                    rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(moving[vn], TRN.bn_moving_update(np.asarray(W[vn], np.float64), bv),
                                    rtol=1e-5, atol=1e-6)
+
+
+def test_train_config_validation_without_gpu():
+    """The C ABI rejects shapes the training kernels' LDS tiles cannot hold before touching the
+    device (no GPU needed): max_T_in > 320, attention_dim not dividing 256, memory_dim > 1024."""
+    import ctypes
+    from tt2 import _lib
+    from tt2.train import train_config
+    lib = _lib.load_library()
+    hp = small_hparams()
+
+    def create_fails(cfg, msg):
+        h = ctypes.c_void_p()
+        assert lib.tt2_train_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == -1
+        assert msg in lib.tt2_last_error().decode()
+
+    create_fails(train_config(hp, 2, 400, 8), "max_T_in")
+    cfg = train_config(hp, 2, 16, 8)
+    cfg.attention_dim = 48
+    create_fails(cfg, "attention_dim")
+    cfg = train_config(hp, 2, 16, 8)
+    cfg.memory_dim = 2048
+    create_fails(cfg, "memory_dim")
