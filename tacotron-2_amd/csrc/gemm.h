@@ -46,10 +46,26 @@ struct GemmArgs {
   // once per optimizer step).  Bw is ignored when set.
   const void* Bt16 = nullptr;
   long ldbt = 0;
+  // split16 == 1: pre-split planes from split_weights() (Bt16 = hi, Bt16lo = lo, both [N][ldbt])
+  const void* Bt16lo = nullptr;
   long kpart_floats = 0;
   int ksplit = 1;  // set by the dispatcher
   int raw = 0;     // internal: partials only (gemm_raw)
 };
+
+// Pre-split fp16 planes of a static weight for split16 == 1 (see GemmArgs::Bt16lo).
+struct SplitB {
+  DevBuf hi, lo;
+  long ldbt = 0;
+  void set(GemmArgs& g) const {
+    if (hi.p) {
+      g.Bt16 = hi.p;
+      g.Bt16lo = lo.p;
+      g.ldbt = ldbt;
+    }
+  }
+};
+void split_weights(const float* B, int K, int N, long ldb, SplitB& out, hipStream_t s);
 
 void gemm(const GemmArgs& a, hipStream_t s);
 // Same product, but the raw fp32 partial sums are left in a.kpart as [ks][M][N] (no epilogue, no

@@ -86,6 +86,19 @@ __device__ __forceinline__ void load_b4(const GemmArgs& g, int k, int n, float* 
   }
 }
 
+// Static weights for split16 == 1: B [K][N] fp32 -> pre-scaled (x2^10), split fp16 planes
+// transposed to [N][ldbt] (k contiguous): one 16-byte load per 8 k in the GEMM, no per-call split.
+__global__ void k_split_bt(const float* __restrict__ B, int K, int N, long ldb, long ldbt, _Float16* __restrict__ hi,
+                           _Float16* __restrict__ lo) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)N * ldbt) return;
+  const int n = (int)(i / ldbt), k = (int)(i % ldbt);
+  const float x = k < K ? B[(long)k * ldb + n] * 1024.f : 0.f;
+  const _Float16 h = (_Float16)x;
+  hi[i] = h;
+  lo[i] = (_Float16)(x - (float)h);
+}
+
 // Fused epilogue of one 32x32 accumulator tile (C/D layout: col = lane&31,
 // row = (r&3) + 8*(r>>2) + 4*(lane>>5), identical for the f32 and f16 MFMA shapes on gfx950).
 __device__ __forceinline__ void epilogue_tile(const GemmArgs& g, const f32x16& acc, int row0, int col0, int lane) {
@@ -265,7 +278,9 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
   const int bn = tid & 127, bk = (tid >> 7) * 16;       // B: col bn, k [bk, bk+16) (coalesced over n)
   float ra[EA], rb[16];
   bf16x8 rbt[2];  // MODE 2 with Bt16: 16 pre-converted k values of column n
-  constexpr bool bt = MODE == 2 && BT;  // B from g.Bt16 (pre-transposed bf16)
+  f16x8 rbh[2], rbl[2];  // MODE 1 with Bt16/Bt16lo: 16 pre-split (hi, lo) k values of column n
+  constexpr bool bt = MODE == 2 && BT;   // B from g.Bt16 (pre-transposed bf16)
+  constexpr bool bt1 = MODE == 1 && BT;  // B from pre-scaled, pre-split fp16 planes
   f32x16 acc[WMB][2];
 #pragma unroll
   for (int i = 0; i < WMB; ++i)
@@ -278,6 +293,26 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
 #pragma unroll
     for (int e = 0; e < EA; e += 4) load_a4<VA>(g, m0 + am, k0 + ak + e, &ra[e]);
     const int n = n0 + bn;
+    if constexpr (bt1) {
+      const long off = (long)n * g.ldbt + k0 + bk;
+      const _Float16* sh = reinterpret_cast<const _Float16*>(g.Bt16) + off;
+      const _Float16* sl = reinterpret_cast<const _Float16*>(g.Bt16lo) + off;
+      const int k = k0 + bk;
+      if (n < g.N && k + 16 <= g.K) {
+        rbh[0] = *reinterpret_cast<const f16x8*>(sh);
+        rbh[1] = *reinterpret_cast<const f16x8*>(sh + 8);
+        rbl[0] = *reinterpret_cast<const f16x8*>(sl);
+        rbl[1] = *reinterpret_cast<const f16x8*>(sl + 8);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const bool ok = n < g.N && k + e < g.K;
+          const _Float16 vh = ok ? sh[e] : (_Float16)0.f, vl = ok ? sl[e] : (_Float16)0.f;
+          if (e < 8) { rbh[0][e] = vh; rbl[0][e] = vl; } else { rbh[1][e - 8] = vh; rbl[1][e - 8] = vl; }
+        }
+      }
+      return;
+    }
     if constexpr (bt) {
       const __bf16* src = reinterpret_cast<const __bf16*>(g.Bt16) + (long)n * g.ldbt + k0 + bk;
       const int k = k0 + bk;
@@ -310,7 +345,12 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        split8(&rb[8 * q], X3_SB, h, l);
+        if constexpr (bt1) {
+          h = rbh[q];
+          l = rbl[q];
+        } else {
+          split8(&rb[8 * q], X3_SB, h, l);
+        }
         *reinterpret_cast<f16x8*>(&Bs[0][buf][bn][bk + 8 * q]) = h;
         *reinterpret_cast<f16x8*>(&Bs[1][buf][bn][bk + 8 * q]) = l;
       }
@@ -424,6 +464,16 @@ static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 
 int gemm_impl(const GemmArgs& a, hipStream_t s);
 
+void split_weights(const float* B, int K, int N, long ldb, SplitB& out, hipStream_t s) {
+  out.ldbt = (K + 7) / 8 * 8;
+  const size_t n = (size_t)N * out.ldbt;
+  out.hi.alloc(n * sizeof(_Float16));
+  out.lo.alloc(n * sizeof(_Float16));
+  hipLaunchKernelGGL(k_split_bt, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, B, K, N, ldb, out.ldbt,
+                     out.hi.as<_Float16>(), out.lo.as<_Float16>());
+  TT2_HIP(hipGetLastError());
+}
+
 int gemm_raw(const GemmArgs& a, hipStream_t s) {
   TT2_CHECK(a.kpart, TT2_ERR_INVALID_ARG, "gemm_raw: kpart required");
   GemmArgs g = a;
@@ -444,8 +494,8 @@ int gemm_impl(const GemmArgs& a, hipStream_t s) {
   else if (a.a_mode == A_CONV1D) va = va && (a.C % 4 == 0) && (a.xs_t % 4 == 0) && (a.xs_b % 4 == 0);
   else va = va && (a.C % 4 == 0);
   if (a.split16) {
-    TT2_CHECK(!a.Bt16 || (a.split16 == 2 && al16(a.Bt16) && a.ldbt % 8 == 0), TT2_ERR_INVALID_ARG,
-              "gemm: Bt16 needs split16 == 2, 16-byte alignment and ldbt % 8 == 0");
+    TT2_CHECK(!a.Bt16 || (al16(a.Bt16) && a.ldbt % 8 == 0 && (a.split16 == 2 || (a.Bt16lo && al16(a.Bt16lo)))),
+              TT2_ERR_INVALID_ARG, "gemm: Bt16 needs 16-byte alignment, ldbt % 8 == 0 (and Bt16lo for split16 == 1)");
     const int wm16 = a.M <= 64 ? 1 : 2;
     GemmArgs g = a;
     g.ksplit = 1;
@@ -462,7 +512,12 @@ int gemm_impl(const GemmArgs& a, hipStream_t s) {
     }
     dim3 grid(cdiv(a.N, 128), cdiv(a.M, 64 * wm16), g.ksplit);
 #define TT2_X3(VA_, MODE_, WMB_) hipLaunchKernelGGL((gemm_x3_kernel<VA_, MODE_, WMB_>), grid, dim3(256), 0, s, g)
-    if (a.split16 == 1) {
+    if (a.split16 == 1 && a.Bt16) {
+#define TT2_X3P(VA_, WMB_) hipLaunchKernelGGL((gemm_x3_kernel<VA_, 1, WMB_, true>), grid, dim3(256), 0, s, g)
+      if (wm16 == 2) { if (va) TT2_X3P(true, 2); else TT2_X3P(false, 2); }
+      else { if (va) TT2_X3P(true, 1); else TT2_X3P(false, 1); }
+#undef TT2_X3P
+    } else if (a.split16 == 1) {
       if (wm16 == 2) { if (va) TT2_X3(true, 1, 2); else TT2_X3(false, 1, 2); }
       else { if (va) TT2_X3(true, 1, 1); else TT2_X3(false, 1, 1); }
     } else if (a.Bt16) {

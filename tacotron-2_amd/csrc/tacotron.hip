@@ -1140,6 +1140,8 @@ struct tt2_ctx {
   tt2::DevBuf l1_w, l1_wh, l1_ws, l1_b, l2_w, l2_wh, l2_b;  // critical rows / recurrent rows / style rows
   tt2::DevBuf loc_cw, keys_b, va, proj_w, proj_ws, proj_b;
   tt2::DevBuf post_cw[8], post_cb[8], post_bs[8], post_bh[8], post_pw, post_pb;
+  // pre-split fp16 planes of the static conv / projection weights (split16 GEMMs, gemm.h SplitB)
+  tt2::SplitB enc_cw_s[8], post_cw_s[8], post_pw_s, mem_k_s;
   // activations
   tt2::DevBuf refxg;  // reference-encoder GRU input projections [B][T2][3D]
   tt2::DevBuf enc_hg;  // persistent BiLSTM h granules [2][2][32 x U] + timeout word
@@ -1233,6 +1235,8 @@ static void finalize(tt2_ctx* c) {
   for (int i = 1; i <= cfg.enc_conv_num_layers; ++i) {
     const std::string s = P + "encoder_convolutions/conv_layer_" + std::to_string(i) + "_encoder_convolutions/";
     upload(c->enc_cw[i - 1], need(wm, s + "conv1d/kernel", {cfg.enc_conv_kernel_size, cin, c->Cenc}));
+    split_weights(c->enc_cw[i - 1].as<float>(), cfg.enc_conv_kernel_size * cin, c->Cenc, c->Cenc, c->enc_cw_s[i - 1],
+                  nullptr);
     upload(c->enc_cb[i - 1], need(wm, s + "conv1d/bias", {c->Cenc}));
     bn_consts(wm, s, c->Cenc, c->enc_bs[i - 1], c->enc_bh[i - 1]);
     cin = c->Cenc;
@@ -1303,6 +1307,7 @@ static void finalize(tt2_ctx* c) {
     upload(R.ab, need(wm, mh + "attention_b", {Aa / cfg.num_heads}));
   }
   upload(c->mem_k, need(wm, P + "memory_layer/kernel", {c->Dm, c->A}));
+  split_weights(c->mem_k.as<float>(), c->Dm, c->A, c->A, c->mem_k_s, nullptr);
   // decoder
   {
     std::vector<int> cols;
@@ -1430,11 +1435,15 @@ static void finalize(tt2_ctx* c) {
   for (int i = 1; i <= cfg.postnet_num_layers; ++i) {
     const std::string s = P + "postnet_convolutions/conv_layer_" + std::to_string(i) + "_postnet_convolutions/";
     upload(c->post_cw[i - 1], need(wm, s + "conv1d/kernel", {cfg.postnet_kernel_size, cin, c->PC}));
+    split_weights(c->post_cw[i - 1].as<float>(), cfg.postnet_kernel_size * cin, c->PC, c->PC, c->post_cw_s[i - 1],
+                  nullptr);
     upload(c->post_cb[i - 1], need(wm, s + "conv1d/bias", {c->PC}));
     bn_consts(wm, s, c->PC, c->post_bs[i - 1], c->post_bh[i - 1]);
     cin = c->PC;
   }
   upload(c->post_pw, need(wm, P + "postnet_projection/projection_postnet_projection/kernel", {c->PC, c->nm}));
+  split_weights(c->post_pw.as<float>(), c->PC, c->nm, c->nm, c->post_pw_s, nullptr);
+  TT2_HIP(hipDeviceSynchronize());
   upload(c->post_pb, need(wm, P + "postnet_projection/projection_postnet_projection/bias", {c->nm}));
   c->finalized = true;
 }
@@ -1525,6 +1534,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.a_mode = A_CONV1D; g.A = xin; g.T = T; g.C = cin; g.kw = cfg.enc_conv_kernel_size;
     g.pad = (cfg.enc_conv_kernel_size - 1) / 2; g.xs_b = (long)T * cin; g.xs_t = cin;
     g.Bw = c->enc_cw[i].as<float>(); g.ldb = c->Cenc; g.Cout = xout; g.ldc = c->Cenc;
+    c->enc_cw_s[i].set(g);
     g.bias = c->enc_cb[i].as<float>(); g.act = ACT_RELU;
     g.bn_scale = c->enc_bs[i].as<float>(); g.bn_shift = c->enc_bh[i].as<float>();
     g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
@@ -1624,6 +1634,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     GemmArgs g;
     g.M = BT; g.N = c->A; g.K = c->Dm; g.A = c->values.as<float>(); g.lda = c->Dm;
     g.Bw = c->mem_k.as<float>(); g.ldb = c->A; g.Cout = c->keys.as<float>(); g.ldc = c->A;
+    c->mem_k_s.set(g);
     g.bias = c->keys_b.as<float>();  // b_a + b_conv·W_loc (folded location-feature bias)
     g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
@@ -1997,6 +2008,7 @@ static void postnet_dev(tt2_ctx* c, const float* frames_d, long frames_bstride, 
     g.T = T; g.C = cin; g.kw = cfg.postnet_kernel_size; g.pad = (cfg.postnet_kernel_size - 1) / 2;
     g.xs_b = (long)T * cin; g.xs_t = cin;
     g.Bw = c->post_cw[i].as<float>(); g.ldb = c->PC; g.Cout = bufs[i & 1]; g.ldc = c->PC;
+    c->post_cw_s[i].set(g);
     g.bias = c->post_cb[i].as<float>(); g.act = (i < cfg.postnet_num_layers - 1) ? ACT_TANH : ACT_NONE;
     g.bn_scale = c->post_bs[i].as<float>(); g.bn_shift = c->post_bh[i].as<float>();
     g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
@@ -2007,6 +2019,7 @@ static void postnet_dev(tt2_ctx* c, const float* frames_d, long frames_bstride, 
   GemmArgs g;
   g.M = B * T; g.N = c->nm; g.K = c->PC; g.A = xin; g.lda = c->PC;
   g.Bw = c->post_pw.as<float>(); g.ldb = c->nm; g.Cout = mel_d; g.ldc = c->nm; g.bias = c->post_pb.as<float>();
+  c->post_pw_s.set(g);
   g.residual = dec_d; g.ldr = c->nm; g.clip = cfg.clip_outputs; g.clip_lo = lo; g.clip_hi = hi;
   g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
   gemm(g, s);
