@@ -1136,6 +1136,7 @@ struct tt2_ctx {
   tt2::DevBuf enc_wx, enc_bx, enc_wh;
   tt2::RefNetDev ref[2];
   tt2::DevBuf mem_k;
+  tt2::DevBuf kpart;  // split-K partials of the small once-per-utterance GEMMs (this ctx's stream)
   tt2::DevBuf pre_w1r, pre_b1, pre_w2, pre_b2, q_w;  // pre_w1r: row-major [nm][P] (GTA TP1 GEMM)
   tt2::DevBuf l1_w, l1_wh, l1_ws, l1_b, l2_w, l2_wh, l2_b;  // critical rows / recurrent rows / style rows
   tt2::DevBuf loc_cw, keys_b, va, proj_w, proj_ws, proj_b;
@@ -1308,6 +1309,7 @@ static void finalize(tt2_ctx* c) {
   }
   upload(c->mem_k, need(wm, P + "memory_layer/kernel", {c->Dm, c->A}));
   split_weights(c->mem_k.as<float>(), c->Dm, c->A, c->A, c->mem_k_s, nullptr);
+  c->kpart.alloc(sizeof(float) * (8u << 20));
   // decoder
   {
     std::vector<int> cols;
@@ -1597,6 +1599,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
         g.bias = R.cb[i].as<float>(); g.act = ACT_BN_RELU;
         g.bn_scale = R.bs[i].as<float>(); g.bn_shift = R.bh[i].as<float>();
         g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
+        g.kpart = c->kpart.as<float>(); g.kpart_floats = (long)(c->kpart.bytes / sizeof(float));  // deep layers: few tiles
         gemm(g, s);
         x = bufs[i & 1];
         H = Ho; Wd = Wo; C = f;
@@ -1610,6 +1613,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
         g.Bw = R.wx.as<float>(); g.ldb = 3 * D; g.Cout = c->refxg.as<float>(); g.ldc = 3 * D;
         g.bias = R.bx.as<float>();
         g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
+        g.kpart = c->kpart.as<float>(); g.kpart_floats = (long)(c->kpart.bytes / sizeof(float));
         gemm(g, s);
       }
       RefGstArgs a;
@@ -1635,6 +1639,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.M = BT; g.N = c->A; g.K = c->Dm; g.A = c->values.as<float>(); g.lda = c->Dm;
     g.Bw = c->mem_k.as<float>(); g.ldb = c->A; g.Cout = c->keys.as<float>(); g.ldc = c->A;
     c->mem_k_s.set(g);
+    g.kpart = c->kpart.as<float>(); g.kpart_floats = (long)(c->kpart.bytes / sizeof(float));
     g.bias = c->keys_b.as<float>();  // b_a + b_conv·W_loc (folded location-feature bias)
     g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
