@@ -1126,6 +1126,9 @@ struct tt2_ctx {
   tt2_config cfg;
   int dev = 0;
   hipStream_t stream = nullptr;
+  // the reference encoders run beside the text encoder (independent until k_memory): fork/join
+  hipStream_t ref_stream = nullptr;
+  hipEvent_t ref_ev[2] = {nullptr, nullptr};
   tt2::WeightMap host;
   bool finalized = false;
   int nm, E, Cenc, U, Dm, E2, A, F, KL, P, H, PC, SW, K1, Kp, NPJ, NPF, KSQ = tt2::KSQ_C, KSP = tt2::KSP_C, KLp, Fp;
@@ -1523,6 +1526,13 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
   for (int b = 0; b < B; ++b)
     TT2_CHECK(lens_h[b] >= 1 && lens_h[b] <= T, TT2_ERR_INVALID_ARG, "input_lengths must be in [1, T_in]");
   const int BT = B * T;
+  // fork: the reference encoders (GST) depend only on the reference mels -> own stream, joined
+  // before k_memory; they fill the CUs the 128-work-group persistent BiLSTM leaves idle
+  const hipStream_t sr = (cfg.use_gst && c->ref_stream) ? c->ref_stream : s;
+  if (sr != s) {
+    TT2_HIP(hipEventRecord(c->ref_ev[0], s));
+    TT2_HIP(hipStreamWaitEvent(sr, c->ref_ev[0], 0));
+  }
   hipLaunchKernelGGL(k_embed, dim3(BT), dim3(128), 0, s, ids_d, c->emb.as<float>(), c->x_a.as<float>(), BT, c->E,
                      cfg.n_symbols);
   TT2_HIP(hipGetLastError());
@@ -1600,7 +1610,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
         g.bn_scale = R.bs[i].as<float>(); g.bn_shift = R.bh[i].as<float>();
         g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
         g.kpart = c->kpart.as<float>(); g.kpart_floats = (long)(c->kpart.bytes / sizeof(float));  // deep layers: few tiles
-        gemm(g, s);
+        gemm(g, sr);
         x = bufs[i & 1];
         H = Ho; Wd = Wo; C = f;
       }
@@ -1614,7 +1624,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
         g.bias = R.bx.as<float>();
         g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
         g.kpart = c->kpart.as<float>(); g.kpart_floats = (long)(c->kpart.bytes / sizeof(float));
-        gemm(g, s);
+        gemm(g, sr);
       }
       RefGstArgs a;
       a.xg = c->refxg.as<float>(); a.T2 = H; a.D = D;
@@ -1627,9 +1637,13 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
       a.style = c->style.as<float>(); a.style_w = c->SW; a.style_off = r * cfg.style_embed_depth;
       const size_t shm = sizeof(float) * (a.D + a.D + 2 * a.D + 128 + a.A + a.ntok * a.A + a.ntok * a.tokd +
                                           a.heads * a.ntok + 16);
-      hipLaunchKernelGGL(k_ref_gru_gst, dim3(B), dim3(256), shm, s, a);
+      hipLaunchKernelGGL(k_ref_gru_gst, dim3(B), dim3(256), shm, sr, a);
       TT2_HIP(hipGetLastError());
     }
+  }
+  if (sr != s) {  // join
+    TT2_HIP(hipEventRecord(c->ref_ev[1], sr));
+    TT2_HIP(hipStreamWaitEvent(s, c->ref_ev[1], 0));
   }
   hipLaunchKernelGGL(k_memory, dim3(BT), dim3(256), 0, s, c->enc_out.as<float>(), c->style.as<float>(), lens_d,
                      c->values.as<float>(), B, T, 2 * c->U, c->SW);
@@ -2076,6 +2090,8 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     c->dev = hip_device;
     TT2_HIP(hipSetDevice(hip_device));
     TT2_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    TT2_HIP(hipStreamCreateWithFlags(&c->ref_stream, hipStreamNonBlocking));
+    for (auto& e : c->ref_ev) TT2_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->nm = cfg->num_mels; c->E = cfg->embedding_dim; c->Cenc = cfg->enc_conv_channels; c->U = cfg->encoder_lstm_units;
     c->A = cfg->attention_dim; c->F = cfg->attention_filters; c->KL = cfg->attention_kernel; c->P = cfg->prenet_units;
     c->H = cfg->decoder_lstm_units; c->PC = cfg->postnet_channels;
@@ -2116,6 +2132,10 @@ void tt2_destroy(tt2_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->sev)
     if (e) (void)hipEventDestroy(e);
+  if (c->ref_stream) (void)hipStreamSynchronize(c->ref_stream);
+  for (auto& e : c->ref_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ref_stream) (void)hipStreamDestroy(c->ref_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;  // DevBuf destructors release the device buffers
 }

@@ -68,6 +68,7 @@ struct tt2_train_ctx {
   bool pn_masks = false;
   int T_last = 0, Tin_last = 0;
   bool pn_ran = false;  // batch stats of the last forward are valid (moving averages in apply)
+  hipStream_t last_stream = nullptr;  // stream of the last forward_backward / apply (read-backs)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
 };
@@ -1034,7 +1035,10 @@ static void tr_alloc(tt2_train_ctx* c) {
                               c->cfg.postnet ? TB * (long)c->PK * c->PC : 0L});
   f(c->TBUF, tmax);
   f(c->part, 64 * std::max<long>(4 * H, LX1) + 4096);
-  f(c->red, 64);
+  // loss / norm slots in a 64 KiB allocation: with a 256-byte hipMalloc, in a process that had
+  // run the end-to-end tests first, the kernels' writes to it never showed up in read-backs
+  // (observed on ROCm 7.2 / MI355X; gradients in large buffers were correct) -- cause not found
+  f(c->red, 16384);
   if (c->cfg.precision) {
     auto h = [](DevBuf& d, long n) { d.alloc(2 * (size_t)std::max<long>(n, 1)); };
     h(c->hK1, LX1 * 4 * H); h(c->hK1T, LX1 * 4 * H); h(c->hK2, 8 * H * H); h(c->hK2T, 8 * H * H);
@@ -1046,7 +1050,8 @@ static void tr_alloc(tt2_train_ctx* c) {
     for (int i = 0; i < c->PL; ++i) f(c->PA[i], TB * PC);
     for (int i = 1; i <= c->PL; ++i) f(c->PX[i], TB * PC);
     f(c->BNM, c->PL * PC); f(c->BNV, c->PL * PC); f(c->PPRJ, TB * NM); f(c->dPP, TB * NM);
-    f(c->DYb, TB * PC); f(c->DZb, TB * PC); f(c->dPXa, TB * PC); f(c->dPXb, TB * PC);
+    // layer inputs' gradients: PC channels, num_mels for the first layer (may exceed PC)
+    f(c->DYb, TB * PC); f(c->DZb, TB * PC); f(c->dPXa, TB * std::max(PC, NM)); f(c->dPXb, TB * std::max(PC, NM));
     f(c->WFLIP, PK * PC * PC); f(c->PWT, NM * PC); f(c->pn_part, 64 * 2 * PC + 1024);
     c->CLIPM.alloc((size_t)TB * NM);
   }
@@ -1173,6 +1178,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     cv(c->WqT.as<float>(), (long)H * A, c->hWqT);
   }
   TT2_HIP(hipMemsetAsync(c->grads, 0, sizeof(float) * c->total, s));
+  TT2_HIP(hipMemsetAsync(c->red.p, 0xFF, 4 * sizeof(float), s));  // NaN until this call's losses land
 
   // ---- forward ----
   float* X1 = c->X1.as<float>();
@@ -1378,6 +1384,16 @@ static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s)
 
 }  // namespace tt2
 
+// device -> host read-back ordered after the producing stream (see tt2_train_losses)
+static void tr_d2h(tt2_train_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (c->last_stream) {
+    TT2_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->last_stream));
+    TT2_HIP(hipStreamSynchronize(c->last_stream));
+  } else {
+    TT2_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  }
+}
+
 // ---- C ABI -------------------------------------------------------------------------------------
 extern "C" {
 
@@ -1513,6 +1529,7 @@ tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* c, const float* memory_
               "T_in/T_out exceed capacity");
     TT2_HIP(hipSetDevice(c->dev));
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    c->last_stream = s;
     TT2_HIP(hipEventRecord(c->ev0, s));
     tr_forward_backward(c, memory_d, lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d,
                         postnet_masks_d, T_in, T_out, s);
@@ -1526,6 +1543,7 @@ tt2_status tt2_train_apply_dev(tt2_train_ctx* c, float lr, int global_step, void
     TT2_CHECK(c && c->finalized, TT2_ERR_NOT_LOADED, "tt2_train_apply_dev: not finalized");
     TT2_HIP(hipSetDevice(c->dev));
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    c->last_stream = s;
     tr_apply(c, lr, global_step, s);
     TT2_HIP(hipGetLastError());
   });
@@ -1535,8 +1553,11 @@ tt2_status tt2_train_losses(tt2_train_ctx* c, float* out4 /* [5] */, float* fb_m
   return guard([&] {
     TT2_CHECK(c && out4, TT2_ERR_INVALID_ARG, "null argument");
     TT2_HIP(hipSetDevice(c->dev));
-    TT2_HIP(hipDeviceSynchronize());
-    TT2_HIP(hipMemcpy(out4, c->red.p, sizeof(float) * 5, hipMemcpyDeviceToHost));
+    // read back in the order of the stream that produced the values: a synchronous hipMemcpy of a
+    // few bytes after hipDeviceSynchronize() returned stale data here (small D2H copies are served
+    // by the host through the BAR and missed the last kernels' L2-resident writes)
+    TT2_HIP(hipMemcpyAsync(out4, c->red.p, sizeof(float) * 5, hipMemcpyDeviceToHost, c->last_stream));
+    TT2_HIP(hipStreamSynchronize(c->last_stream));
     if (!c->cfg.postnet) out4[4] = 0.f;
     if (fb_ms) TT2_HIP(hipEventElapsedTime(fb_ms, c->ev0, c->ev1));
   });
@@ -1548,7 +1569,7 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
     TT2_HIP(hipSetDevice(c->dev));
     TT2_HIP(hipDeviceSynchronize());
     if (std::string(name) == "memory") {  // d loss / d memory of the last forward_backward
-      TT2_HIP(hipMemcpy(host, c->DMEM.p, sizeof(float) * (size_t)c->B * c->Tin_last * c->D, hipMemcpyDeviceToHost));
+      tr_d2h(c, host, c->DMEM.p, sizeof(float) * (size_t)c->B * c->Tin_last * c->D);
       return;
     }
     auto it = c->index.find(name);
@@ -1557,7 +1578,7 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
     const float* base = which == 0 ? c->params.as<float>() : which == 1 ? c->grads
                       : which == 2 ? c->adam_m.as<float>() : c->adam_v.as<float>();
     TT2_CHECK(which >= 0 && which <= 3, TT2_ERR_INVALID_ARG, "which must be 0..3");
-    TT2_HIP(hipMemcpy(host, base + v.off, sizeof(float) * v.n, hipMemcpyDeviceToHost));
+    tr_d2h(c, host, base + v.off, sizeof(float) * v.n);
   });
 }
 
@@ -1570,19 +1591,19 @@ tt2_status tt2_train_outputs(tt2_train_ctx* c, float* frames, float* stop_logits
     // device layouts are time-major [T][B][..]; the ABI returns [B][T][..] like tower_decoder_output
     if (frames) {
       std::vector<float> tmp((size_t)T * B * NM);
-      TT2_HIP(hipMemcpy(tmp.data(), c->FR.p, sizeof(float) * tmp.size(), hipMemcpyDeviceToHost));
+      tr_d2h(c, tmp.data(), c->FR.p, sizeof(float) * tmp.size());
       for (int t = 0; t < T; ++t)
         for (int b = 0; b < B; ++b)
           std::memcpy(frames + ((size_t)b * T + t) * NM, tmp.data() + ((size_t)t * B + b) * NM, sizeof(float) * NM);
     }
     if (stop_logits) {
       std::vector<float> tmp((size_t)T * B);
-      TT2_HIP(hipMemcpy(tmp.data(), c->ST.p, sizeof(float) * tmp.size(), hipMemcpyDeviceToHost));
+      tr_d2h(c, tmp.data(), c->ST.p, sizeof(float) * tmp.size());
       for (int t = 0; t < T; ++t)
         for (int b = 0; b < B; ++b) stop_logits[(size_t)b * T + t] = tmp[(size_t)t * B + b];
     }
     if (alignments)  // [B][Tin][T] already
-      TT2_HIP(hipMemcpy(alignments, c->ALIGN.p, sizeof(float) * (size_t)B * Tin * T, hipMemcpyDeviceToHost));
+      tr_d2h(c, alignments, c->ALIGN.p, sizeof(float) * (size_t)B * Tin * T);
   });
 }
 
