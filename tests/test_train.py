@@ -351,3 +351,42 @@ def test_train_config_validation_without_gpu():
     cfg = train_config(hp, 2, 16, 8)
     cfg.memory_dim = 2048
     create_fails(cfg, "memory_dim")
+
+
+@pytest.mark.gpu
+def test_gpu_train_full_size_properties():
+    """configs[4] shape (B=64, T_in=150, T_out=800, fork-default widths, Postnet): too large for the
+    float64 oracle, so size-independent properties -- fp32 and bf16 agree on the losses (1e-3
+    relative) and gradient norm (2 %), everything finite, and three clipped-Adam steps on one
+    batch lower the total loss."""
+    from tt2.hparams import hparams
+    from tt2.train import TacotronTrainer
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    B, T_in, T_out = 64, 150, 800
+    W = init_tacotron_weights(hp, seed=5339)
+    mem, lens, tg, st = train_batch(B, T_in, T_out, memory_width(hp), seed=7)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=7)
+    zm = zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=7)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=7)
+    res = {}
+    for prec in ("fp32", "bf16"):
+        tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision=prec)
+        try:
+            losses = []
+            for step in (1, 2, 3):
+                tr.forward_backward(mem, lens, tg, st, pm, zm, pnm)
+                tr.apply(step)
+                losses.append(tr.losses())
+            g = tr.get(TRN.L1 + "kernel", 0, np.asarray(W[TRN.L1 + "kernel"]).shape)
+        finally:
+            tr.close()
+        assert all(np.isfinite([L["loss"], L["grad_norm"]]).all() for L in losses)
+        assert np.isfinite(g).all()
+        assert losses[-1]["loss"] < losses[0]["loss"], [L["loss"] for L in losses]
+        res[prec] = losses
+    for k in ("before", "after", "stop_token"):
+        a, b = res["fp32"][0][k], res["bf16"][0][k]
+        assert abs(a - b) < 1e-3 * abs(a), (k, a, b)
+    a, b = res["fp32"][0]["grad_norm"], res["bf16"][0]["grad_norm"]
+    assert abs(a - b) < 2e-2 * a, (a, b)
