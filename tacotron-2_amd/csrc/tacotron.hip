@@ -1505,7 +1505,7 @@ static void alloc_acts(tt2_ctx* c) {
   c->cum.alloc(B * T * 4);
   c->max_att.alloc(64 * 4);
   c->PP.alloc((long)c->KSP * 32 * c->NPF * 4);
-  c->ctl.alloc(sizeof(DecCtl));
+  c->ctl.alloc(std::max<size_t>(sizeof(DecCtl), 65536));  // >= 64 KiB: see train.hip on 256-byte allocations
   c->frames.alloc(B * MI * c->nm * 4);
   c->stop.alloc(B * MI * 4);
   c->align.alloc(B * T * MI * 4);
