@@ -183,6 +183,36 @@ def test_gpu_train_forward_backward_small(zoneout_masks):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,T_in,T_out", [(1, 5, 1), (1, 17, 9), (5, 16, 3)])
+def test_gpu_train_edge_shapes(B, T_in, T_out):
+    """Single-row batches, a one-step decode, T_in on a 16-row attention-tile boundary, with the
+    Postnet: outputs, losses and every gradient against the oracle."""
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out, seed=23)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=23)
+    names = TRN.train_var_names() + TRN.postnet_var_names()
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0)
+    try:
+        tr.forward_backward(mem, lens, tg, st, pm, zm, pnm)
+        L = tr.losses()
+        fr, sl, al = tr.outputs(T_in, T_out)
+        grads = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}
+    finally:
+        tr.close()
+    out, (b, s, r, after), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight,
+                                               clip=_clip(hp), postnet=True, postnet_masks=pnm)
+    assert np.abs(fr - out["frames"]).max() < 1e-4
+    assert np.abs(al - out["alignments"]).max() < 1e-5
+    assert abs(L["before"] - b) < 1e-5 * b and abs(L["after"] - after) < 1e-5 * after
+    for n in names:
+        if np.abs(g[n]).max() < 1e-12:
+            assert np.abs(grads[n]).max() < 1e-6, n
+            continue
+        assert _rel(grads[n], g[n]) < 2e-4, (n, _rel(grads[n], g[n]))
+
+
+@pytest.mark.gpu
 def test_gpu_train_clipped_decoder_output():
     """clip_outputs with a tight range (max_abs_value 0.02): decoder_output is clipped before the
     before-loss (tacotron.py:360-361) and no gradient flows through clipped frames."""
