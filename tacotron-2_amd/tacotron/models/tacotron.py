@@ -3,7 +3,9 @@
 ``Tacotron.initialize`` keeps the reference's signature and argument validation but runs eagerly:
 instead of building a TF graph it executes encoder → decoder loop → Postnet through libtt2.so and
 stores numpy arrays in the reference's ``tower_*`` attributes (one list entry per tower).
-Training (is_training=True, losses, optimizer) is not on this path.
+Training through this class (is_training=True) would also train the encoder, GST and reference
+encoders, whose backward is not built; the decoder + Postnet training step is
+``tt2.train.TacotronTrainer``.
 """
 import os
 
@@ -127,8 +129,9 @@ class Tacotron():
             raise ValueError('must use unpaired with pretrained_emb_disc_all')
         # scope of the MI355X path
         if is_training or is_evaluating:
-            raise NotImplementedError("training / eval-loss graphs are not on the synthesis path "
-                                      "(SURVEY.md §8f rank 1)")
+            raise NotImplementedError("training / eval-loss graphs of the whole model are not built "
+                                      "(no encoder/GST backward); the decoder + Postnet training "
+                                      "step is tt2.train.TacotronTrainer")
         if adain or getattr(args, "pretrained_emb_disc_all", False) or use_unpaired:
             raise NotImplementedError("adain / pretrained_emb_disc_all / unpaired style paths are "
                                       "not built; the fork default GST path is")
