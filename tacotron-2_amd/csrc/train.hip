@@ -57,7 +57,7 @@ struct tt2_train_ctx {
   // backward
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DH2, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
-  DevBuf TH, E, DA, DF, PQ, FALL, ALN;
+  DevBuf TH, E, DF, PQ, FALL, ALN;
   // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
   DevBuf hK1, hK1T, hK2, hK2T, hWq, hWqT;
   // Postnet training (cfg.postnet): PA[i] activations (pre-BN), PX[i] layer inputs (PX[0] unused:
@@ -279,7 +279,6 @@ struct TrAtt {
   // backward
   const float* dPIN;
   const float* dX1;
-  float* DA;     // [B][Tin] d align_t (+ d cum_t)
   float* DF;     // [B][Tin][F] d location features
   float* PQ;     // [B][nt][A] per-tile d query partials
   float* DCTX;   // [T][B][D]
@@ -519,31 +518,9 @@ __global__ void k_tr_lstm_bwd(TrLstmBwd a) {
   a.R[(long)b * a.ldr + a.off_r + n] = (1.f - kh) * dhz;
 }
 
-// ---- attention backward for one step: three chip-wide launches over (j-tile, row) ----
-// (1) d align_j = dctx_t · values_j + d cum_t[j]  (cum_t = cum_{t-1} + align_t)
-__global__ __launch_bounds__(TR_AT) void k_tr_att_dalign(TrAtt a) {
-  __shared__ float dctx[1024];
-  const int b = blockIdx.y, j0 = blockIdx.x * TR_JT;
-  const long tb = (long)a.t * a.B + b;
-  for (int n = threadIdx.x; n < a.D; n += blockDim.x) {
-    const float v = a.dPIN[tb * (a.H + a.D) + a.H + n] + a.dX1[(tb + a.B) * (a.P + a.D + a.H) + a.P + n];
-    dctx[n] = v;
-    if (blockIdx.x == 0) a.DCTX[tb * a.D + n] = v;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int jj = wave; jj < TR_JT; jj += nw) {
-    const int j = j0 + jj;
-    if (j >= a.Tin) break;
-    const float* v = a.values + ((long)b * a.Tin + j) * a.D;
-    float acc = 0.f;
-    for (int n = lane; n < a.D; n += 64) acc += dctx[n] * v[n];
-    acc = wave_sum(acc);
-    if (lane == 0) a.DA[(long)b * a.Tin + j] = acc + a.DCUM[(long)b * a.Tin + j];
-  }
-}
-
-// (2) softmax backward de_j = a_j (da_j - Σ a·da), tanh backward du_jk = de_j v_k (1 - th²):
+// ---- attention backward for one step: two chip-wide launches over (j-tile, row) ----
+// (1) d align_j = dctx_t · values_j + d cum_t[j] (cum_t = cum_{t-1} + align_t), softmax backward
+// de_j = a_j (da_j - Σ a·da), tanh backward du_jk = de_j v_k (1 - th²):
 // d keys (+=), per-tile partials of d v_a, d b_a (= d q), du kept for d W_loc, d f = du · W_loc^T
 __global__ __launch_bounds__(TR_AT) void k_tr_att_energy_bwd(TrAtt a) {
   __shared__ float WlT[256 * 33];
@@ -551,16 +528,40 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy_bwd(TrAtt a) {
   __shared__ float de[TR_JT];
   __shared__ float racc[2 * TR_AT];
   __shared__ float s16[16];
+  __shared__ float dctx[1024];
+  __shared__ float dat[TR_JT];
   const int b = blockIdx.y, tile = blockIdx.x, j0 = tile * TR_JT, tid = threadIdx.x;
   const long tb = (long)a.t * a.B + b;
   const int len = a.lens[b];
+  // d context_t (block 0 keeps it for the d-values GEMM)
+  for (int n = tid; n < a.D; n += blockDim.x) {
+    const float v = a.dPIN[tb * (a.H + a.D) + a.H + n] + a.dX1[(tb + a.B) * (a.P + a.D + a.H) + a.P + n];
+    dctx[n] = v;
+    if (tile == 0) a.DCTX[tb * a.D + n] = v;
+  }
+  __syncthreads();
+  // softmax backward needs s = Σ_j a_j da_j with da_j = dctx·v_j + dcum_j; since ctx_t = Σ_j a_j v_j,
+  // s = dctx·ctx_t + Σ_j a_j dcum_j -- every tile gets it without the other tiles' da
   float s = 0.f;
-  for (int j = tid; j < len; j += blockDim.x)
-    s += a.ALN[tb * a.Tin + j] * a.DA[(long)b * a.Tin + j];
+  for (int n = tid; n < a.D; n += blockDim.x) s += dctx[n] * a.PIN[tb * (a.H + a.D) + a.H + n];
+  for (int j = tid; j < len; j += blockDim.x) s += a.ALN[tb * a.Tin + j] * a.DCUM[(long)b * a.Tin + j];
   s = block_sum(s, s16);
+  {  // d align of this tile's rows: one encoder row per wave
+    const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    for (int jj = wave; jj < TR_JT; jj += nw) {
+      const int j = j0 + jj;
+      if (j >= a.Tin) break;
+      const float* v = a.values + ((long)b * a.Tin + j) * a.D;
+      float acc = 0.f;
+      for (int n = lane; n < a.D; n += 64) acc += dctx[n] * v[n];
+      acc = wave_sum(acc);
+      if (lane == 0) dat[jj] = acc + a.DCUM[(long)b * a.Tin + j];
+    }
+  }
+  __syncthreads();
   if (tid < TR_JT) {
     const int j = j0 + tid;
-    de[tid] = j < len ? a.ALN[tb * a.Tin + j] * (a.DA[(long)b * a.Tin + j] - s) : 0.f;
+    de[tid] = j < len ? a.ALN[tb * a.Tin + j] * (dat[tid] - s) : 0.f;
   }
   for (int i = tid; i < a.F * a.A; i += blockDim.x) WlT[(i % a.A) * 33 + i / a.A] = a.Wl[i];
   __syncthreads();
@@ -604,7 +605,7 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy_bwd(TrAtt a) {
   }
 }
 
-// (3) d query (sum of the tile partials), location-conv backward: per-tile partials of d Kc and
+// (2) d query (sum of the tile partials), location-conv backward: per-tile partials of d Kc and
 // d bc, and d cum_{t-1}[i] = d cum_t[i] + Σ_tap,c df[i - tap + pad][c]·Kc[tap][c]
 __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
   __shared__ float cseg[TR_JT + 64];
@@ -1029,7 +1030,7 @@ static void tr_alloc(tt2_train_ctx* c) {
   const long NT = (Tin + TR_JT - 1) / TR_JT;
   f(c->DKEYS, B * Tin * A); f(c->DCUM, B * Tin); f(c->dV, B * NT * A); f(c->dBA, B * NT * A);
   f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F); f(c->FALL, TB * Tin * F); f(c->ALN, TB * Tin);
-  f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DA, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
+  f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
   f(c->dZ, TB * P); f(c->dPre, TB * P);
   const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM, TB * Tin * F,
                               c->cfg.postnet ? TB * (long)c->PK * c->PC : 0L});
@@ -1214,7 +1215,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   at.DKEYS = c->DKEYS.as<float>(); at.DCUM = c->DCUM.as<float>(); at.dV = c->dV.as<float>(); at.dBA = c->dBA.as<float>();
   at.dKC = c->dKC.as<float>(); at.dBC = c->dBC.as<float>();
   at.FALL = c->FALL.as<float>(); at.ALN = c->ALN.as<float>();
-  at.TH = c->TH.as<float>(); at.E = c->E.as<float>(); at.DA = c->DA.as<float>(); at.DF = c->DF.as<float>();
+  at.TH = c->TH.as<float>(); at.E = c->E.as<float>(); at.DF = c->DF.as<float>();
   at.PQ = c->PQ.as<float>();
   const int NT = (Tin + TR_JT - 1) / TR_JT;
   at.nt = NT;
@@ -1270,7 +1271,6 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   for (int t = T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_dalign, att_grid, dim3(TR_AT), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(TR_AT), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
     // LSTM-2 backward: d h2 = DQ·Wq^T (raw split-K) + d PIN[t][:, :H], combined in the cell kernel
