@@ -11,9 +11,11 @@
 //   PIN[t] [B, H + D]       projection input [h2_new_t | ctx_t]
 //   G*[t]  [B, 4H]          gate activations (σi, tanh j, σ(f+1), σo) after the forward
 //   ALIGN  [B, T_in, T]     alignments (row-major per utterance: the d_values GEMM reads it as A)
-// Every matrix product is the fp32 MFMA GEMM (gemm.hip): per-step products at M = B, the weight
-// gradients as one GEMM over all T·B rows after the loop (activations transposed once).  The
-// recurrences' elementwise parts (LSTM cells, location-sensitive attention, softmax, context) are
+// Every matrix product is an MFMA GEMM from gemm.hip (fp32 operands, or bf16 operands with fp32
+// accumulation when cfg.precision = 1): per-step products at M = B with split-K (the LSTM cells
+// fused into the split-K combine, gemm_raw), the weight gradients as one GEMM over all T·B rows
+// after the loop (activations transposed once).  The recurrences' elementwise parts (LSTM cells,
+// location-sensitive attention, softmax, context) and the Postnet's training-mode batch norm are
 // the kernels below.  Backward mirrors the forward slot layout: dX1[t], dX2[t] hold the gradients
 // of the step-t inputs, so a step's carry-ins are read from slot t+1.
 #include <cmath>
@@ -55,7 +57,7 @@ struct tt2_train_ctx {
   // activations
   DevBuf values, keys, X1, X2, PIN, G1, G2, C1, C2, CN1, CN2, Q, ALIGN, CUM, P1, XIN, FR, ST;
   // backward
-  DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DH2, DCTX, DKEYS, DCUM;
+  DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
   DevBuf TH, E, DF, PQ, FALL, ALN;
   // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
@@ -1026,7 +1028,7 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->P1, TB * P); f(c->XIN, TB * NM); f(c->FR, TB * NM); f(c->ST, TB);
   f(c->dFR, TB * NM); f(c->dST, TB); f(c->dPIN, TB * (H + D)); f(c->dX1, (T + 1) * B * LX1);
   f(c->dX2, (T + 1) * B * 2 * H); f(c->dG1, TB * 4 * H); f(c->dG2, TB * 4 * H); f(c->DC1, B * H); f(c->DC2, B * H);
-  f(c->R1, B * LX1); f(c->R2, B * 2 * H); f(c->DQ, TB * A); f(c->DH2, B * H); f(c->DCTX, TB * D);
+  f(c->R1, B * LX1); f(c->R2, B * 2 * H); f(c->DQ, TB * A); f(c->DCTX, TB * D);
   const long NT = (Tin + TR_JT - 1) / TR_JT;
   f(c->DKEYS, B * Tin * A); f(c->DCUM, B * Tin); f(c->dV, B * NT * A); f(c->dBA, B * NT * A);
   f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F); f(c->FALL, TB * Tin * F); f(c->ALN, TB * Tin);
