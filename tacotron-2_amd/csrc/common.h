@@ -105,6 +105,33 @@ __host__ __device__ inline int wf_idx(int k, int j) {  // within one 16-column t
   return ((((s >> 2) * 64) + (kk * 16 + j)) << 2) + (s & 3);
 }
 
+// One k-group (16 k) of an AF x WF product as split fp16x3 MFMA: the AF/WF float4 of lane l holds
+// k = 16sg + 4e + (l>>4) for both operands, so the same (l>>4, e) -> k map turns each hi/lo pair
+// of float4s into valid v_mfma_f32_16x16x16_f16 operands; A·B = Ah·Bh + Ah·Bl + Al·Bh (fp32
+// accumulation, fp16 products exact) -- 3 instead of 8 fp32 MFMAs' worth of issue per row half.
+typedef _Float16 kg_f16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void kg_split(const f32x4& v, kg_f16x4& h, kg_f16x4& l) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const _Float16 x = (_Float16)v[e];
+    h[e] = x;
+    l[e] = (_Float16)(v[e] - (float)x);
+  }
+}
+__device__ __forceinline__ void kg_mfma_x3(const f32x4& a0, const f32x4& a1, const f32x4& bw, f32x4& c0,
+                                           f32x4& c1) {
+  kg_f16x4 a0h, a0l, a1h, a1l, bh, bl;
+  kg_split(a0, a0h, a0l);
+  kg_split(a1, a1h, a1l);
+  kg_split(bw, bh, bl);
+  c0 = __builtin_amdgcn_mfma_f32_16x16x16f16(a0l, bh, c0, 0, 0, 0);
+  c1 = __builtin_amdgcn_mfma_f32_16x16x16f16(a1l, bh, c1, 0, 0, 0);
+  c0 = __builtin_amdgcn_mfma_f32_16x16x16f16(a0h, bl, c0, 0, 0, 0);
+  c1 = __builtin_amdgcn_mfma_f32_16x16x16f16(a1h, bl, c1, 0, 0, 0);
+  c0 = __builtin_amdgcn_mfma_f32_16x16x16f16(a0h, bh, c0, 0, 0, 0);
+  c1 = __builtin_amdgcn_mfma_f32_16x16x16f16(a1h, bh, c1, 0, 0, 0);
+}
+
 // acc[h] += A(rows h*16..h*16+15, k in [16*sg0, 16*sg1)) * Wtile(k, 0..15)
 __device__ __forceinline__ void skinny_mfma(const float* __restrict__ X, const float* __restrict__ Wt,
                                             int sg0, int sg1, f32x4& acc0, f32x4& acc1, int lane) {

@@ -185,29 +185,9 @@ __device__ __forceinline__ void pd_publish_rep(const PdArgs& a, int r, unsigned 
   if (tid < PD_NREP) __hip_atomic_store((pd_gu32*)(a.rflags + (r * PD_NREP + tid) * PD_NB + blockIdx.x), val, PD_RLX);
 }
 
-// acc(rows 0..15 | 16..31) += A(k-group) · W(k-group, 16 columns) -- split fp16x3 variant: the
-// AF/WF float4 of lane l holds k = 16sg + 4e + (l>>4), the same (l>>4, e) -> k map for A and B, so
-// the 16 k of a group feed one v_mfma_f32_16x16x16_f16 per hi/lo product.
-typedef _Float16 kg_f16x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void kg_split(const f32x4& v, kg_f16x4& h, kg_f16x4& l) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const _Float16 x = (_Float16)v[e];
-    h[e] = x;
-    l[e] = (_Float16)(v[e] - (float)x);
-  }
-}
+// acc(rows 0..15 | 16..31) += A(k-group) · W(k-group, 16 columns), split fp16x3 (common.h)
 __device__ __forceinline__ void kg_mfma(const f32x4& a0, const f32x4& a1, const f32x4& bw, f32x4& c0, f32x4& c1) {
-  kg_f16x4 a0h, a0l, a1h, a1l, bh, bl;
-  kg_split(a0, a0h, a0l);
-  kg_split(a1, a1h, a1l);
-  kg_split(bw, bh, bl);
-  c0 = __builtin_amdgcn_mfma_f32_16x16x16f16(a0l, bh, c0, 0, 0, 0);
-  c1 = __builtin_amdgcn_mfma_f32_16x16x16f16(a1l, bh, c1, 0, 0, 0);
-  c0 = __builtin_amdgcn_mfma_f32_16x16x16f16(a0h, bl, c0, 0, 0, 0);
-  c1 = __builtin_amdgcn_mfma_f32_16x16x16f16(a1h, bl, c1, 0, 0, 0);
-  c0 = __builtin_amdgcn_mfma_f32_16x16x16f16(a0h, bh, c0, 0, 0, 0);
-  c1 = __builtin_amdgcn_mfma_f32_16x16x16f16(a1h, bh, c1, 0, 0, 0);
+  kg_mfma_x3(a0, a1, bw, c0, c1);
 }
 
 // Partial tile of wave w -> red[w][32][16] (the MFMA D layout transposed to row-major).

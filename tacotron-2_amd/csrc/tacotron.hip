@@ -232,12 +232,7 @@ __global__ __launch_bounds__(256) void k_enc_bilstm_persist(EncPArgs a) {
         __builtin_amdgcn_s_sleep(2);
       }
 #pragma unroll
-      for (int i = 0; i < NKG; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[i][e], wt[i][e], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[i][e], wt[i][e], acc1, 0, 0, 0);
-        }
+      for (int i = 0; i < NKG; ++i) kg_mfma_x3(x0[i], x1[i], wt[i], acc0, acc1);  // split fp16x3 (common.h)
     }
     reduce_waves_32x16<4>(acc0, acc1, red, G, w, lane, tid);
     if (tid < 128) {
