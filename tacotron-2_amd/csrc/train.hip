@@ -530,7 +530,7 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy_bwd(TrAtt a) {
   __shared__ float de[TR_JT];
   __shared__ float racc[2 * TR_AT];
   __shared__ float s16[16];
-  __shared__ float dctx[1024];
+  __shared__ __attribute__((aligned(16))) float dctx[1024];
   __shared__ float dat[TR_JT];
   const int b = blockIdx.y, tile = blockIdx.x, j0 = tile * TR_JT, tid = threadIdx.x;
   const long tb = (long)a.t * a.B + b;
@@ -555,7 +555,17 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy_bwd(TrAtt a) {
       if (j >= a.Tin) break;
       const float* v = a.values + ((long)b * a.Tin + j) * a.D;
       float acc = 0.f;
-      for (int n = lane; n < a.D; n += 64) acc += dctx[n] * v[n];
+      if ((a.D & 3) == 0) {  // 16-byte loads: the values row is the kernel's dominant read
+        const float4* v4 = reinterpret_cast<const float4*>(v);
+        const float4* d4 = reinterpret_cast<const float4*>(dctx);
+#pragma unroll 4
+        for (int n = lane; n < (a.D >> 2); n += 64) {
+          const float4 x = v4[n], y = d4[n];
+          acc += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+        }
+      } else {
+        for (int n = lane; n < a.D; n += 64) acc += dctx[n] * v[n];
+      }
       acc = wave_sum(acc);
       if (lane == 0) dat[jj] = acc + a.DCUM[(long)b * a.Tin + j];
     }
