@@ -295,18 +295,19 @@ struct TrAtt {
 
 // Location features of rows j0..j0+TR_JT-1 of utterance b (attention.py:193-195):
 // f[jj][c] = bc[c] + Σ_tap cum_{t-1}[j0 + jj + tap - pad]·Kc[tap][c]; cseg = the cum segment.
-__device__ __forceinline__ void tr_locf_tile(const TrAtt& a, int b, int j0, float* cseg, float* f) {
+__device__ __forceinline__ void tr_locf_tile(const TrAtt& a, int b, int j0, float* cseg, float* f, float* Kcs) {
   const int pad = (a.KW - 1) / 2;
   const float* cum_prev = a.CUM + ((long)a.t * a.B + b) * a.Tin;
   for (int i = threadIdx.x; i < TR_JT + a.KW - 1; i += blockDim.x) {
     const int j = j0 + i - pad;
     cseg[i] = (j >= 0 && j < a.Tin) ? cum_prev[j] : 0.f;
   }
+  for (int i = threadIdx.x; i < a.KW * a.F; i += blockDim.x) Kcs[i] = a.Kc[i];  // taps from LDS
   __syncthreads();
   for (int i = threadIdx.x; i < TR_JT * a.F; i += blockDim.x) {
     const int jj = i / a.F, c = i % a.F;
     float acc = a.bc[c];
-    for (int tap = 0; tap < a.KW; ++tap) acc += cseg[jj + tap] * a.Kc[tap * a.F + c];
+    for (int tap = 0; tap < a.KW; ++tap) acc += cseg[jj + tap] * Kcs[tap * a.F + c];
     f[i] = acc;
   }
   __syncthreads();
@@ -318,9 +319,10 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy(TrAtt a) {
   __shared__ float cseg[TR_JT + 64];
   __shared__ float f[TR_JT * 32];
   __shared__ float Wl[32 * 256];
+  __shared__ float Kcs[65 * 32];  // attention_kernel <= 65, attention_filters <= 32 (tt2_train_create)
   const int b = blockIdx.y, j0 = blockIdx.x * TR_JT;
   for (int i = threadIdx.x; i < a.F * a.A; i += blockDim.x) Wl[i] = a.Wl[i];
-  tr_locf_tile(a, b, j0, cseg, f);
+  tr_locf_tile(a, b, j0, cseg, f, Kcs);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const long tb = (long)a.t * a.B + b;
   for (int i = threadIdx.x; i < TR_JT * a.F; i += blockDim.x) {
