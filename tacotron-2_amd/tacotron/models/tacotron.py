@@ -96,7 +96,9 @@ class Tacotron():
                    use_unpaired=False, n_emt=None, n_spk=None, synth=False,
                    prenet_masks=None, seed=0):
         """Same arguments as the reference (tacotron.py:31-35) plus the injected prenet dropout
-        keep-masks ``prenet_masks`` [max_iters, 2, B, 256] (None = device RNG keyed by ``seed``)."""
+        keep-masks ``prenet_masks`` [max_iters, 2, B_total, 256] over every tower's utterances in
+        tower order, or a list with one [max_iters, 2, B, 256] array per tower (None = device RNG
+        keyed by ``seed``)."""
         hp = self._hparams
         # argument validation, tacotron.py:48-71
         if mel_targets is None and stop_token_targets is not None:
@@ -153,6 +155,11 @@ class Tacotron():
                              if ref_mel_spk is not None else [None] * ntow)
             tower_targets = (split_func(np.asarray(mel_targets, np.float32), split_infos[:, 1])
                              if mel_targets is not None else [None] * ntow)
+            # tf.split(input_lengths, num_or_size_splits=tacotron_num_gpus) (tacotron.py:89): an
+            # integer split, so the reference itself requires equal tower sizes
+            if input_lengths.shape[0] % ntow:
+                raise ValueError("input_lengths ({}) must split evenly over tacotron_num_gpus={} "
+                                 "(tacotron.py:89 tf.split)".format(input_lengths.shape[0], ntow))
             tower_lengths = np.split(input_lengths, ntow)
         else:
             tower_inputs, tower_lengths = [inputs], [input_lengths]
@@ -172,6 +179,7 @@ class Tacotron():
         self.tower_ref_mel_emt = tower_ref_emt
         self.tower_ref_mel_spk = tower_ref_spk
         max_iters = hp.max_iters
+        row0 = 0  # first utterance of tower i in the global (tower-major) row order
         for i in range(len(tower_inputs)):
             ids = np.ascontiguousarray(tower_inputs[i].reshape(tower_lengths[i].shape[0], -1))
             B, T_in = ids.shape
@@ -182,7 +190,15 @@ class Tacotron():
             if gta and tower_targets[i] is not None:
                 tg = tower_targets[i].reshape(B, -1, hp.num_mels)[:, hp.outputs_per_step - 1::hp.outputs_per_step]
             eng = self._get_engine(B, T_in, T_ref, max_iters, emt_only, constraint)
-            masks = prenet_masks if i == 0 or prenet_masks is None else prenet_masks
+            # prenet_masks covers every utterance of every tower, [max_iters, 2, ntow*B, P] in
+            # tower-major row order (or a list with one [max_iters, 2, B, P] array per tower)
+            if prenet_masks is None:
+                masks = None
+            elif isinstance(prenet_masks, (list, tuple)):
+                masks = prenet_masks[i]
+            else:
+                masks = np.asarray(prenet_masks)[:, :, row0:row0 + B]
+            row0 += B
             out = eng.synthesize(ids, tower_lengths[i], ref_e, ref_s, max_iters, masks, seed, tg)
             self.tower_decoder_output.append(out["decoder_output"])
             self.tower_alignments.append(out["alignments"])

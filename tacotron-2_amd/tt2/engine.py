@@ -115,6 +115,10 @@ class TacotronEngine(object):
         masks = None if prenet_masks is None else np.ascontiguousarray(prenet_masks, np.uint8)
         if masks is not None and masks.shape[0] < max_iters:
             raise ValueError("prenet_masks must cover max_iters steps")
+        if masks is not None and masks.shape[1:] != (2, B, self.hp.prenet_layers[0]):
+            raise ValueError("prenet_masks must be [max_iters, 2, B, prenet_units] = [{}, 2, {}, {}]"
+                             ", got {}".format(max_iters, B, self.hp.prenet_layers[0],
+                                               masks.shape))
         if masks is not None:
             masks = np.ascontiguousarray(masks[:max_iters])
         tg = f32(targets)

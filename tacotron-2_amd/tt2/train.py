@@ -100,6 +100,10 @@ class TacotronTrainer(object):
         check(self.lib.tt2_train_bind_grads_dev(self.h, None, ctypes.byref(n)))
         self.n_params = n.value
         self.grad_buf = None
+        # Bind the flat gradient buffer before any backward pass: forward_backward() writes the
+        # gradients wherever the context points, so binding it lazily in allreduce_grads() would
+        # leave the first step's gradients in the library's own buffer and all-reduce zeros.
+        self.bind_grad_buffer()
         self.global_step = 0
         self._keep = None
 
@@ -113,8 +117,11 @@ class TacotronTrainer(object):
     def bind_grad_buffer(self):
         """Flat gradient buffer as a torch tensor (for RCCL all-reduce); returned view."""
         if self.grad_buf is None:
-            self.grad_buf = self.torch.zeros(self.n_params, dtype=self.torch.float32,
-                                             device=self.device)
+            # allocated (and zero-filled) on the trainer's stream, so the fill is ordered before
+            # the library's first use of the buffer on that stream
+            with self.torch.cuda.stream(self.stream):
+                self.grad_buf = self.torch.zeros(self.n_params, dtype=self.torch.float32,
+                                                 device=self.device)
             check(self.lib.tt2_train_bind_grads_dev(self.h, ctypes.c_void_p(self.grad_buf.data_ptr()),
                                                     None))
         return self.grad_buf
@@ -169,12 +176,17 @@ class TacotronTrainer(object):
             tower_mean_(buf, group)
 
     def apply(self, global_step=None, lr=None):
-        """clip_by_global_norm(1.0) + Adam at update count ``global_step`` (1-based)."""
+        """clip_by_global_norm(1.0) + Adam at update count ``global_step`` (1-based).
+
+        The learning rate is the schedule at ``global_step - 1``: TF's apply_gradients reads the
+        global_step variable before incrementing it (tacotron.py:1029 passes it to
+        _learning_rate_decay, evaluated in the same session.run), so the first update uses
+        step 0.  Adam's bias correction counts updates, i.e. ``global_step``."""
         if global_step is None:
             global_step = self.global_step + 1
         self.global_step = global_step
         if lr is None:
-            lr = learning_rate(global_step, self.hp)
+            lr = learning_rate(global_step - 1, self.hp)
         check(self.lib.tt2_train_apply_dev(self.h, float(lr), int(global_step),
                                            ctypes.c_void_p(self.stream.cuda_stream)))
         return lr

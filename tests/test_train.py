@@ -265,9 +265,9 @@ def test_gpu_train_adam_updates_match_oracle():
             Wcur.update(p)
             _, _, g = TRN.train_grads(Wcur, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight)
             g.pop("memory")
-            gn = TRN.clip_and_adam(p, g, m, v, step, learning_rate(step, hp))
+            gn = TRN.clip_and_adam(p, g, m, v, step, learning_rate(step - 1, hp))
             assert abs(L["grad_norm"] - gn) < 1e-4 * gn
-            assert lr == learning_rate(step, hp)
+            assert lr == learning_rate(step - 1, hp)
             for n in names:
                 got = tr.get(n, 0, p[n].shape)
                 assert np.abs(got - p[n]).max() < 1e-6 + 1e-5 * np.abs(p[n]).max(), n
