@@ -123,6 +123,12 @@ tt2_status tt2_decode(tt2_ctx* ctx, int max_iters, const uint8_t* prenet_masks, 
                       const float* targets, int T_targets, float* frames, float* stop,
                       float* align, int32_t* n_steps);
 
+/* Read-back of the device RNG tt2_decode draws its prenet keep bits from when prenet_masks is NULL:
+ * out [max_iters,2,B,prenet_units] = exactly the bits tt2_decode(..., NULL, seed, ...) uses for a
+ * context of batch B (same device function).  Parity/diagnostic: re-injecting them must reproduce
+ * the seeded run bit for bit. */
+tt2_status tt2_prenet_keep_bits(uint64_t seed, int max_iters, int B, int prenet_units, uint8_t* out);
+
 /* decoder clip + Postnet + postnet_projection + final clip (tacotron.py:362-381) on the frames of
  * the last tt2_decode (frames_in == NULL) or on caller frames [B,T,80].
  * decoder_output (nullable) and mel_out are [B,T,80]. */
@@ -247,6 +253,12 @@ tt2_status tt2_wn_last_timings(tt2_wn_ctx* ctx, float* ms3);
  * generate call, out512[stage*8 + k]: k=0 input received, 1..3 after each layer, 4 head done
  * (last stage), 5 sample handed to stage 0 (last stage). */
 tt2_status tt2_wn_debug_stamps(tt2_wn_ctx* ctx, long long* out512);
+
+/* Read-back of the device RNG tt2_wn_generate draws from when u_mix/u_log are NULL (same device
+ * functions): u_mix [T,B,nr_mix] and u_log [T,B] of a generate call of batch B; gaussian != 0:
+ * u_log = the N(0,1) draws of the Gaussian head, u_mix untouched (may be NULL). */
+tt2_status tt2_wn_noise(uint64_t seed, int T, int B, int nr_mix, int gaussian, float* u_mix,
+                        float* u_log);
 
 /* Standalone sample_from_discretized_mix_logistic (mixture.py:76-107) on the current HIP device:
  * logits [n, 3*nr_mix], u_mix [n, nr_mix], u_log [n] (host) -> x [n], k [n] (host). */

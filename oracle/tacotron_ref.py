@@ -399,14 +399,6 @@ def synthesize(ids, lengths, ref_emt, ref_spk, W, hp, prenet_masks, max_iters, t
 
 
 def get_output_lengths(stop_tokens):
-    """tacotron/synthesizer.py:384-387: first index where round(stop)==1, else the row length."""
-    out = []
-    for row in np.round(stop_tokens).tolist():
-        out.append(row.index(1) if 1 in row else len(row))
-    return out
-
-
-def get_output_lengths(stop_tokens):
     """tacotron/synthesizer.py:384-387: per row, the index of the first 1 in np.round(stop)
     (round half to even), else the row length."""
     return [row.index(1) if 1 in row else len(row) for row in np.round(stop_tokens).tolist()]

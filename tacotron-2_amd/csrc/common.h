@@ -109,6 +109,19 @@ __host__ __device__ inline int wf_idx(int k, int j) {  // within one 16-column t
 // k = 16sg + 4e + (l>>4) for both operands, so the same (l>>4, e) -> k map turns each hi/lo pair
 // of float4s into valid v_mfma_f32_16x16x16_f16 operands; A·B = Ah·Bh + Ah·Bl + Al·Bh (fp32
 // accumulation, fp16 products exact) -- 3 instead of 8 fp32 MFMAs' worth of issue per row half.
+//
+// Exact power-of-two pre-scale of the B operand (as gemm.hip's split16 path): the resident weights
+// are stored pre-multiplied by KG_SB = 2^10 (the persistent decoder's weight copies at finalize,
+// the BiLSTM's register fragments in its prologue), so the lo halves of weights down to ~1e-4
+// (trained checkpoints: 1e-3..1e-1) stay fp16 normals instead of losing bits as subnormals; every
+// accumulator fed by kg_mfma_x3 carries 2^10 and is multiplied by KG_UNSCALE where it is consumed.
+// Valid for |B| < 64 (KG_BMAX, checked on the host at finalize: larger weights route to the
+// fp32-MFMA launch path).  The A operand (activations: tanh/sigmoid-bounded h, context, prenet
+// outputs) is split unscaled: its split error is <= 2^-25 absolute even where lo is subnormal,
+// i.e. below fp32's own rounding of |a| >= 0.5 and at fp32-dot-product noise level below that
+// (|a|·sqrt(K)·2^-25 against |a|·sqrt(K)·2^-24 rounding of the fp32 sum); pre-scaling it measured
+// +1.1 us per decoder step (A/B, round 2) for no parity gain.
+constexpr float KG_SB = 1024.f, KG_UNSCALE = 1.f / 1024.f, KG_BMAX = 63.9f;
 typedef _Float16 kg_f16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void kg_split(const f32x4& v, kg_f16x4& h, kg_f16x4& l) {
 #pragma unroll
@@ -118,6 +131,7 @@ __device__ __forceinline__ void kg_split(const f32x4& v, kg_f16x4& h, kg_f16x4& 
     l[e] = (_Float16)(v[e] - (float)x);
   }
 }
+// bw is the pre-scaled (x KG_SB) weight fragment; c0/c1 accumulate A·B·2^10.
 __device__ __forceinline__ void kg_mfma_x3(const f32x4& a0, const f32x4& a1, const f32x4& bw, f32x4& c0,
                                            f32x4& c1) {
   kg_f16x4 a0h, a0l, a1h, a1l, bh, bl;
@@ -238,6 +252,26 @@ __host__ __device__ inline uint32_t hash32(uint32_t x) {  // murmur3 fmix32
 __host__ __device__ inline double u01_open(uint64_t h) {  // in [1e-5, 1-1e-5)
   const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);
   return 1e-5 + u * (1.0 - 2e-5);
+}
+
+// Device-RNG streams: the noise drawn when the caller injects none.  The generating kernels and the
+// read-back entry points (tt2_prenet_keep_bits, tt2_wn_noise) call these same functions, so a
+// seeded run can be re-run with its noise injected and must reproduce bit for bit.
+// Prenet dropout keep bit (rate 0.5, modules.py:355-356) of flat index i of [max_iters][2][B][P].
+__host__ __device__ inline uint8_t prenet_keep_bit(long i, uint64_t seed) {
+  const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32) ^ 0x9e3779b9u;
+  return (uint8_t)(hash32(hash32((uint32_t)i ^ s0) + s1) >> 31);
+}
+// MoL uniforms of sample t, utterance b (global batch Bg): channel c < nr_mix = the Gumbel draw
+// u_mix[t][b][c] (mixture.py:91), c = 15 = the logistic draw u_log[t][b] (mixture.py:104); both in
+// [1e-5, 1-1e-5), rounded to fp32 like an injected uniform.
+__host__ __device__ inline float wn_uniform(uint64_t seed, long t, int Bg, int b, int c) {
+  return (float)u01_open(mix64(seed ^ mix64(((uint64_t)t * Bg + b) * 16 + c)));
+}
+// Gaussian head: the N(0,1) draw of Normal.sample (gaussian.py:50), Box-Muller on channels 14, 15.
+__device__ inline float wn_gauss(uint64_t seed, long t, int Bg, int b) {
+  const float u1 = wn_uniform(seed, t, Bg, b, 14), u2 = wn_uniform(seed, t, Bg, b, 15);
+  return sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
 }
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }

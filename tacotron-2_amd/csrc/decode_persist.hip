@@ -251,12 +251,14 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   // ---------------- prologue: resident weights and per-row constants ----------------
   const int tid = tid_, lane = tid & 63, w = tid >> 6;
   const int em = (tid >> 2) & 31, eu = tid & 3;  // LSTM epilogue thread (tid < 128) -> row, unit
+  // every WF weight below comes pre-scaled by KG_SB (split fp16x3 range, common.h); the gate and
+  // projection sums are unscaled by KG_UNSCALE where they are consumed
   f32x4 w1p[2], w2i[8];                          // chain: L1 prenet rows, L2 input rows (8 waves)
   {
     const f32x4* L1 = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * (PD_P + PD_E2) * 16);
     const f32x4* L2 = reinterpret_cast<const f32x4*>(a.l2_w + (long)g * PD_H * 16);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) w1p[i] = L1[(2 * w + i) * 64 + lane];
+    for (int i = 0; i < 2; ++i) w1p[i] = L1[(2 * w + i) * 64 + lane];  // pre-scaled (common.h)
 #pragma unroll
     for (int i = 0; i < 8; ++i) w2i[i] = L2[(8 * w + i) * 64 + lane];
     const f32x4* L1h = reinterpret_cast<const f32x4*>(a.l1_wh + (long)g * PD_H * 16);
@@ -499,7 +501,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = em * 16 + 4 * q + eu;
-        z[q] = (sum_partials<8>(red, idx) + ssa[em] * gsv[q]) + b1v[q];
+        z[q] = (sum_partials<8>(red, idx) * KG_UNSCALE + ssa[em] * gsv[q]) + b1v[q];
       }
       const float cn = sigm_fast(z[2] + 1.0f) * c1 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
@@ -541,7 +543,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = em * 16 + 4 * q + eu;
-        z[q] = sum_partials<8>(red, idx) + b2v[q];
+        z[q] = sum_partials<8>(red, idx) * KG_UNSCALE + b2v[q];
       }
       const float cn = sigm_fast(z[2] + 1.0f) * c2 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
@@ -755,7 +757,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           float v = 0.f;
 #pragma unroll
           for (int ks = 0; ks < PD_KSP; ++ks) v += pv[ks];
-          red[tid] = (v + sc[2] * a.PS[(long)b * PD_NPF + tid]) + a.proj_b[tid];
+          red[tid] = (v * KG_UNSCALE + sc[2] * a.PS[(long)b * PD_NPF + tid]) + a.proj_b[tid];
         }
       }
       __syncthreads();
@@ -816,9 +818,14 @@ bool pd_device_ok(int dev) {
   return nb >= 1;
 }
 
+// Cooperative launch: the runtime guarantees every one of the PD_NB work-groups is resident at
+// once (or fails the launch) -- the spin-waits of the hand-offs depend on it, and a plain launch
+// could be starved of CUs by a concurrent kernel on another stream or context.
 void pd_launch(const PdArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_decode_persist, dim3(PD_NB), dim3(PD_NT), pd_lds_bytes(), s, a);
-  TT2_HIP(hipGetLastError());
+  PdArgs arg = a;
+  void* params[] = {&arg};
+  TT2_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_decode_persist), dim3(PD_NB), dim3(PD_NT),
+                                     params, (unsigned)pd_lds_bytes(), s));
 }
 
 }  // namespace tt2

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void k_enc_bilstm_persist(EncPArgs a) {
     const f32x4* Wt = reinterpret_cast<const f32x4*>(a.wh + ((long)(dir * ng + g) * U * 16));
     const int w = tid0 >> 6, lane = tid0 & 63;
 #pragma unroll
-    for (int i = 0; i < NKG; ++i) wt[i] = Wt[(NKG * w + i) * 64 + lane];
+    for (int i = 0; i < NKG; ++i) wt[i] = Wt[(NKG * w + i) * 64 + lane] * KG_SB;  // pre-scaled (common.h)
   }
   const int m = (tid0 >> 2) & 31, uu = tid0 & 3, u = 4 * g + uu;
   const int L = (tid0 < 128 && m < a.B) ? a.lengths[m] : 0;
@@ -240,10 +240,10 @@ __global__ __launch_bounds__(256) void k_enc_bilstm_persist(EncPArgs a) {
       if (act) {
         const int pos = dir == 0 ? t : L - 1 - t;
         const float* xp = a.xproj + ((long)m * a.T + pos) * (8 * U) + dir * 4 * U;
-        const float zi = G[m * 16 + 0 * 4 + uu] + xp[0 * U + u];
-        const float zj = G[m * 16 + 1 * 4 + uu] + xp[1 * U + u];
-        const float zf = G[m * 16 + 2 * 4 + uu] + xp[2 * U + u];
-        const float zz = G[m * 16 + 3 * 4 + uu] + xp[3 * U + u];
+        const float zi = G[m * 16 + 0 * 4 + uu] * KG_UNSCALE + xp[0 * U + u];
+        const float zj = G[m * 16 + 1 * 4 + uu] * KG_UNSCALE + xp[1 * U + u];
+        const float zf = G[m * 16 + 2 * 4 + uu] * KG_UNSCALE + xp[2 * U + u];
+        const float zz = G[m * 16 + 3 * 4 + uu] * KG_UNSCALE + xp[3 * U + u];
         const float cn = sigm(zf + 1.0f) * c + sigm(zi) * tanhf(zj);
         const float hn = sigm(zz) * tanhf(cn);
         c = a.one_m_zo * cn + a.zo * c;
@@ -475,12 +475,11 @@ struct DecArgs {
 };
 
 // Keep bits of the always-on prenet dropout when the caller injects none: counter-based hash of
-// (seed, flat index) -> Bernoulli(0.5), generated for the whole decode in one launch.
-// Keep bits of the always-on prenet dropout when the caller injects none: counter-based hash of
-// (seed, flat index) -> Bernoulli(0.5), generated for the whole decode in one launch.
-__global__ void k_gen_masks(uint8_t* __restrict__ m, long n, uint32_t s0, uint32_t s1) {
+// (seed, flat index) -> Bernoulli(0.5) (common.h prenet_keep_bit), generated for the whole decode
+// in one launch (also the read-back tt2_prenet_keep_bits).
+__global__ void k_gen_masks(uint8_t* __restrict__ m, long n, uint64_t seed) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    m[i] = (uint8_t)(hash32(hash32((uint32_t)i ^ s0) + s1) >> 31);
+    m[i] = prenet_keep_bit(i, seed);
 }
 
 constexpr int KSQ_C = 4;  // query split-K
@@ -1135,6 +1134,11 @@ struct tt2_ctx {
   tt2::RefNetDev ref[2];
   tt2::DevBuf mem_k;
   tt2::DevBuf kpart;  // split-K partials of the small once-per-utterance GEMMs (this ctx's stream)
+  // max |w| of the weights the split fp16x3 MFMA kernels keep resident (pre-scaled by KG_SB):
+  // the persistent decoder / BiLSTM need < KG_BMAX, larger weights take the fp32-MFMA launch path
+  float kg_wmax_dec = 0.f, kg_wmax_enc = 0.f;
+  // the persistent decoder's copies of l1_w, l1_wh, l2_w, l2_wh, proj_w, pre-scaled by KG_SB
+  tt2::DevBuf pd_l1_w, pd_l1_wh, pd_l2_w, pd_l2_wh, pd_proj_w;
   tt2::DevBuf pre_w1r, pre_b1, pre_w2, pre_b2, q_w;  // pre_w1r: row-major [nm][P] (GTA TP1 GEMM)
   tt2::DevBuf l1_w, l1_wh, l1_ws, l1_b, l2_w, l2_wh, l2_b;  // critical rows / recurrent rows / style rows
   tt2::DevBuf loc_cw, keys_b, va, proj_w, proj_ws, proj_b;
@@ -1179,6 +1183,15 @@ static void upload(DevBuf& d, const std::vector<float>& h) {
   TT2_HIP(hipMemcpy(d.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
 }
 static void upload(DevBuf& d, const HostTensor& t) { upload(d, t.data); }
+static void upload_scaled(DevBuf& d, std::vector<float> h, float scale) {
+  for (float& x : h) x *= scale;  // exact: power of two
+  upload(d, h);
+}
+static float absmax(const std::vector<float>& v) {
+  float m = 0.f;
+  for (float x : v) m = std::max(m, std::fabs(x));
+  return m;
+}
 
 // BN inference constants: y*scale + shift with scale = gamma·rsqrt(var+eps), shift = beta − mean·scale
 static void bn_consts(const WeightMap& wm, const std::string& scope, int c, DevBuf& sc, DevBuf& sh) {
@@ -1257,6 +1270,7 @@ static void finalize(tt2_ctx* c) {
     upload(c->enc_wx, wx);
     upload(c->enc_bx, bx);
     upload(c->enc_wh, wh);
+    c->kg_wmax_enc = absmax(wh);
   }
   // reference encoders + GST
   const char* tags[2] = {"emt", "spk"};
@@ -1343,8 +1357,16 @@ static void finalize(tt2_ctx* c) {
     auto cols = lstm_cols(H);
     std::vector<float> bt(cols.size());
     for (size_t i = 0; i < cols.size(); ++i) bt[i] = b.data[cols[i]];
-    upload(l == 0 ? c->l1_w : c->l2_w, pack_wf(k.data.data(), Kc, N, cols, Kc));
-    upload(l == 0 ? c->l1_wh : c->l2_wh, pack_wf(k.data.data() + (size_t)Kh0 * N, H, N, cols, H));
+    {
+      const auto wc = pack_wf(k.data.data(), Kc, N, cols, Kc);
+      const auto wr = pack_wf(k.data.data() + (size_t)Kh0 * N, H, N, cols, H);
+      if (l == 0) c->kg_wmax_dec = 0.f;
+      c->kg_wmax_dec = std::max(c->kg_wmax_dec, std::max(absmax(wc), absmax(wr)));
+      upload(l == 0 ? c->l1_w : c->l2_w, wc);
+      upload(l == 0 ? c->l1_wh : c->l2_wh, wr);
+      upload_scaled(l == 0 ? c->pd_l1_w : c->pd_l2_w, wc, KG_SB);
+      upload_scaled(l == 0 ? c->pd_l1_wh : c->pd_l2_wh, wr, KG_SB);
+    }
     upload(l == 0 ? c->l1_b : c->l2_b, bt);
     if (l == 0) {  // style rows, lstm column order, row-major [SW][4H] (B operand of the GS GEMM)
       std::vector<float> ws((size_t)c->SW * N);
@@ -1414,7 +1436,12 @@ static void finalize(tt2_ctx* c) {
     }
     std::vector<int> cols;
     for (int j = 0; j < NPF; ++j) cols.push_back(j);
-    upload(c->proj_w, pack_wf(W.data(), c->Kp, NPF, cols, c->Kp));  // rows [h2 | context_enc]
+    {
+      const auto pw = pack_wf(W.data(), c->Kp, NPF, cols, c->Kp);  // rows [h2 | context_enc]
+      c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pw));
+      upload(c->proj_w, pw);
+      upload_scaled(c->pd_proj_w, pw, KG_SB);
+    }
     std::vector<float> ws((size_t)c->SW * NPF, 0.f);                // context_style rows
     for (int r = 0; r < c->SW; ++r)
       for (int n = 0; n < NPF; ++n) ws[(size_t)r * NPF + n] = W[(size_t)(c->Kp + r) * NPF + n];
@@ -1563,7 +1590,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
   TT2_HIP(hipMemsetAsync(c->enc_out.p, 0, (size_t)BT * 2 * c->U * 4, s));
   int Tmax = 0;
   for (int b = 0; b < B; ++b) Tmax = std::max(Tmax, lens_h[b]);
-  if (c->U == ENC_U && c->pd_dev_ok && c->pd_mode == 1) {  // persistent recurrence (128 work-groups)
+  if (c->U == ENC_U && c->pd_dev_ok && c->pd_mode == 1 && c->kg_wmax_enc < KG_BMAX) {  // persistent (128 WGs)
     c->enc_hg.alloc(sizeof(unsigned long long) * 2 * 2 * 32 * ENC_U + 64);
     TT2_HIP(hipMemsetAsync(c->enc_hg.p, 0, c->enc_hg.bytes, s));
     EncPArgs a;
@@ -1571,8 +1598,9 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     a.out = c->enc_out.as<float>(); a.lengths = lens_d; a.B = B; a.T = T; a.Tmax = Tmax;
     a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
     a.err = reinterpret_cast<int*>(a.Hg + 2 * 2 * 32 * ENC_U);
-    hipLaunchKernelGGL(k_enc_bilstm_persist, dim3(2 * ENC_U / 4), dim3(256), 0, s, a);
-    TT2_HIP(hipGetLastError());
+    void* params[] = {&a};  // cooperative: all 128 work-groups co-resident (h hand-offs spin)
+    TT2_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_enc_bilstm_persist), dim3(2 * ENC_U / 4),
+                                       dim3(256), params, 0u, s));
     TT2_HIP(hipMemcpyAsync(&c->ctl_host[2], a.err, sizeof(int), hipMemcpyDeviceToHost, s));
     c->enc_err_check = true;
   } else
@@ -1818,7 +1846,7 @@ static void check_encoder(tt2_ctx* c) {
 }
 
 static bool pd_fits(tt2_ctx* c) {
-  return c->pd_mode == 1 && c->pd_dev_ok && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
+  return c->pd_mode == 1 && c->pd_dev_ok && c->kg_wmax_dec < KG_BMAX && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
          c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= PD_TMAX && c->B <= 32;
 }
 
@@ -1859,10 +1887,10 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
   a.poll_sleep = 4;
   if (const char* e = getenv("TT2_PD_SLEEP")) a.poll_sleep = atoi(e);
-  a.l1_w = c->l1_w.as<float>(); a.l1_wh = c->l1_wh.as<float>(); a.l1_b = c->l1_b.as<float>();
-  a.l2_w = c->l2_w.as<float>(); a.l2_wh = c->l2_wh.as<float>(); a.l2_b = c->l2_b.as<float>();
+  a.l1_w = c->pd_l1_w.as<float>(); a.l1_wh = c->pd_l1_wh.as<float>(); a.l1_b = c->l1_b.as<float>();  // x KG_SB
+  a.l2_w = c->pd_l2_w.as<float>(); a.l2_wh = c->pd_l2_wh.as<float>(); a.l2_b = c->l2_b.as<float>();
   a.GS = c->GS0.as<float>(); a.q_wt = c->q_wt.as<float>(); a.loc_cw = c->loc_cw.as<float>(); a.va = c->va.as<float>();
-  a.proj_w = c->proj_w.as<float>(); a.proj_b = c->proj_b.as<float>(); a.PS = c->PS.as<float>();
+  a.proj_w = c->pd_proj_w.as<float>(); a.proj_b = c->proj_b.as<float>(); a.PS = c->PS.as<float>();
   a.pre_b1 = c->pre_b1.as<float>(); a.pre_w2t = c->pre_w2t.as<float>(); a.pre_b2 = c->pre_b2.as<float>();
   a.TP1 = targets_d ? c->TP1.as<float>() : nullptr;
   a.keysT = c->keysT.as<float>(); a.valuesT = c->valuesT.as<float>(); a.lengths = c->lens.as<int>();
@@ -1923,7 +1951,7 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
     const long n = (long)max_iters * 2 * c->B * c->P;
     c->gmasks.alloc((size_t)n);
     hipLaunchKernelGGL(k_gen_masks, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, s,
-                       c->gmasks.as<uint8_t>(), n, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x9e3779b9u);
+                       c->gmasks.as<uint8_t>(), n, seed);
     TT2_HIP(hipGetLastError());
     masks_d = c->gmasks.as<uint8_t>();
   }
@@ -2180,6 +2208,20 @@ tt2_status tt2_encode(tt2_ctx* c, const int32_t* ids, const int32_t* lengths, in
         TT2_HIP(hipMemcpyAsync(style_out + (size_t)b * c->SW, c->style.as<float>() + (size_t)b * c->SW,
                                sizeof(float) * c->SW, hipMemcpyDeviceToHost, s));
     TT2_HIP(hipStreamSynchronize(s));
+  });
+}
+
+tt2_status tt2_prenet_keep_bits(uint64_t seed, int max_iters, int B, int prenet_units, uint8_t* out) {
+  return guard([&] {
+    TT2_CHECK(out, TT2_ERR_INVALID_ARG, "tt2_prenet_keep_bits: null argument");
+    TT2_CHECK(max_iters >= 1 && B >= 1 && prenet_units >= 1, TT2_ERR_INVALID_ARG, "tt2_prenet_keep_bits: bad sizes");
+    const long n = (long)max_iters * 2 * B * prenet_units;
+    DevBuf d;
+    d.alloc((size_t)n);
+    hipLaunchKernelGGL(k_gen_masks, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, 0,
+                       d.as<uint8_t>(), n, seed);
+    TT2_HIP(hipGetLastError());
+    TT2_HIP(hipMemcpy(out, d.p, (size_t)n, hipMemcpyDeviceToHost));
   });
 }
 

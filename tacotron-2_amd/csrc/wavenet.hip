@@ -353,21 +353,18 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
         if (a.u_log) {
           nz = a.u_log[(long)t * a.Bg + b];
         } else {
-          const uint64_t k0 = ((uint64_t)t * a.Bg + b) * 16;
-          const float u1 = (float)u01_open(mix64(a.seed ^ mix64(k0 + 14)));
-          const float u2 = (float)u01_open(mix64(a.seed ^ mix64(k0 + 15)));
-          nz = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+          nz = wn_gauss(a.seed, t, a.Bg, b);
         }
         gum[cb_cur * 16 + 15] = nz;
       }
     } else if (!GAUSS && last && wave == 1) {  // this sample's Gumbel terms and logistic noise
       if (lane < nr) {
         const float um = a.u_mix ? a.u_mix[((long)t * a.Bg + b) * nr + lane]
-                                 : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.Bg + b) * 16 + lane)));
+                                 : wn_uniform(a.seed, t, a.Bg, b, lane);
         gum[cb_cur * 16 + lane] = gumbel_L((double)um);
       } else if (lane == 15) {
         const float ul = a.u_log ? a.u_log[(long)t * a.Bg + b]
-                                 : (float)u01_open(mix64(a.seed ^ mix64(((uint64_t)t * a.Bg + b) * 16 + 15)));
+                                 : wn_uniform(a.seed, t, a.Bg, b, 15);
         const double uu = (double)ul;
         gum[cb_cur * 16 + 15] = (float)(log(uu) - log(1.0 - uu));
       }
@@ -765,6 +762,21 @@ static size_t gen_lds_bytes(const tt2_wn_ctx* c) {
   return sizeof(float) * (fixed + ring);
 }
 
+// Read-back of the device RNG streams of k_generate_pipe (tt2_wn_noise): row r = t*Bg + b.
+__global__ void k_wn_noise(uint64_t seed, long n, int Bg, int nr, int gaussian, float* __restrict__ um,
+                           float* __restrict__ ul) {
+  for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < n; r += (long)gridDim.x * blockDim.x) {
+    const long t = r / Bg;
+    const int b = (int)(r % Bg);
+    if (gaussian) {
+      ul[r] = wn_gauss(seed, t, Bg, b);
+    } else {
+      for (int c = 0; c < nr; ++c) um[r * nr + c] = wn_uniform(seed, t, Bg, b, c);
+      ul[r] = wn_uniform(seed, t, Bg, b, 15);
+    }
+  }
+}
+
 static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f, const float* umix_d,
                             const float* ulog_d, uint64_t seed, const float* teacher_d, float* wav_d, int* k_d,
                             float* logits_d, float* upsampled_d, hipStream_t s) {
@@ -834,8 +846,10 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
     TT2_HIP(hipMemsetAsync(c->gran.p, 0, gbytes, s));
     const int grid = cdiv(a.B, 8) * nst * 8;
     const auto kern = pipe_kernel(c->cfg.legacy != 0, c->cfg.residual_legacy != 0, c->C == 2);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(WN_THREADS), shm, s, a);
-    TT2_HIP(hipGetLastError());
+    // cooperative: every stage work-group of the launch co-resident (the stage hand-offs spin)
+    void* params[] = {&a};
+    TT2_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kern), dim3(grid), dim3(WN_THREADS), params,
+                                       (unsigned)shm, s));
     TT2_HIP(hipMemcpyAsync(c->status_host, c->gran.p, sizeof(int), hipMemcpyDeviceToHost, s));
   }
   TT2_HIP(hipEventRecord(c->ev[3], s));
@@ -1030,6 +1044,24 @@ tt2_status tt2_wn_cond_from_mels_dev(const float* mels_d, int ld_t, const int32_
     hipLaunchKernelGGL(k_cond_from_mels, dim3(cdiv(T_f, 32), cdiv(num_mels, 32), B), dim3(256), 0, s, mels_d,
                        (long)ld_t, lengths_d, num_mels, T_f, lo, hi, clip, normalize, cond_d);
     TT2_HIP(hipGetLastError());
+  });
+}
+
+tt2_status tt2_wn_noise(uint64_t seed, int T, int B, int nr_mix, int gaussian, float* u_mix, float* u_log) {
+  return guard([&] {
+    TT2_CHECK(u_log && (gaussian || u_mix), TT2_ERR_INVALID_ARG, "tt2_wn_noise: null argument");
+    TT2_CHECK(T >= 1 && B >= 1 && (gaussian || (nr_mix >= 1 && nr_mix <= 14)), TT2_ERR_INVALID_ARG,
+              "tt2_wn_noise: bad sizes");
+    const long n = (long)T * B;
+    const int nm = gaussian ? 0 : nr_mix;
+    DevBuf dm, dl;
+    if (nm) dm.alloc(sizeof(float) * n * nm);
+    dl.alloc(sizeof(float) * n);
+    hipLaunchKernelGGL(k_wn_noise, dim3((unsigned)std::min<long>((n + 255) / 256, 65535)), dim3(256), 0, 0, seed, n, B,
+                       nm, gaussian, dm.as<float>(), dl.as<float>());
+    TT2_HIP(hipGetLastError());
+    if (nm) TT2_HIP(hipMemcpy(u_mix, dm.p, sizeof(float) * n * nm, hipMemcpyDeviceToHost));
+    TT2_HIP(hipMemcpy(u_log, dl.p, sizeof(float) * n, hipMemcpyDeviceToHost));
   });
 }
 

@@ -122,6 +122,8 @@ SIGNATURES = {
     "tt2_gl_synthesize": (_I, [_P, _P, _I, _I, _I, _P]),
     "tt2_gl_synthesize_dev": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "tt2_mol_sample": (_I, [_P, _P, _P, _I, _I, _F, _P, _P]),
+    "tt2_prenet_keep_bits": (_I, [_U64, _I, _I, _I, _P]),
+    "tt2_wn_noise": (_I, [_U64, _I, _I, _I, _I, _P, _P]),
     "tt2_train_default_config": (None, [ctypes.POINTER(TrainConfig), _I, _I, _I]),
     "tt2_train_create": (_I, [ctypes.POINTER(TrainConfig), _I, ctypes.POINTER(_P)]),
     "tt2_train_destroy": (None, [_P]),

@@ -267,3 +267,22 @@ def mol_sample(logits, u_mix, u_log, log_scale_min):
     check(lib.tt2_mol_sample(ptr(logits), ptr(u_mix), ptr(u_log), n, C // 3, log_scale_min,
                              ptr(x), ptr(k)))
     return x, k
+
+
+def prenet_keep_bits(seed, max_iters, B, P):
+    """tt2_prenet_keep_bits: the keep bits [max_iters, 2, B, P] tt2_decode draws from the device RNG
+    for ``seed`` when no prenet_masks are injected."""
+    lib = _lib.load_library()
+    out = np.zeros((max_iters, 2, B, P), np.uint8)
+    check(lib.tt2_prenet_keep_bits(seed, max_iters, B, P, ptr(out)))
+    return out
+
+
+def wavenet_noise(seed, T, B, nr_mix=10, gaussian=False):
+    """tt2_wn_noise: (u_mix [T,B,nr_mix] or None, u_log [T,B]) that tt2_wn_generate draws from the
+    device RNG for ``seed`` when none are injected (Gaussian head: u_log = the N(0,1) draws)."""
+    lib = _lib.load_library()
+    um = None if gaussian else np.zeros((T, B, nr_mix), np.float32)
+    ul = np.zeros((T, B), np.float32)
+    check(lib.tt2_wn_noise(seed, T, B, nr_mix, 1 if gaussian else 0, ptr(um), ptr(ul)))
+    return um, ul

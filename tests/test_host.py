@@ -300,7 +300,7 @@ def test_wavenet_synthesizer_host_prep_rejects_global_conditioning():
 
 
 @pytest.mark.parametrize("src,kernel,max_spill", [("wavenet.hip", "k_generate_pipe", 0),
-                                                  ("decode_persist.hip", "k_decode_persist", 24)])
+                                                  ("decode_persist.hip", "k_decode_persist", 32)])
 def test_register_resident_kernels_do_not_spill(src, kernel, max_spill):
     """The WaveNet generator keeps its weights in registers: a VGPR spill on its per-sample chain
     cost 19 % (23 spills from a runtime head flag, fixed by a template parameter) — guard it at
