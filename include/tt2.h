@@ -129,6 +129,30 @@ tt2_status tt2_decode(tt2_ctx* ctx, int max_iters, const uint8_t* prenet_masks, 
  * the seeded run bit for bit. */
 tt2_status tt2_prenet_keep_bits(uint64_t seed, int max_iters, int B, int prenet_units, uint8_t* out);
 
+/* TacotronDecoderState (Architecture_wrappers.py:158-195) as caller-owned host arrays, B and T_in
+ * from the last tt2_encode: cell_state = ((c1, h1), (c2, h2)) of the two ZoneoutLSTM layers (the
+ * carried zoneout mix), attention = the context [B,D_mem], alignments [B,T_in] = the attention
+ * state (cumulated when cumulative_weights), max_attentions [B], time.  zero_state = all zeros. */
+typedef struct tt2_decoder_state {
+  float* h1; float* c1;      /* [B, decoder_lstm_units] */
+  float* h2; float* c2;      /* [B, decoder_lstm_units] */
+  float* attention;          /* [B, D_mem] */
+  float* alignments;         /* [B, T_in] */
+  int32_t* max_attentions;   /* [B] */
+  int32_t time;
+} tt2_decoder_state;
+
+/* One TacotronDecoderCell.__call__(inputs, state) -> ((frames, stop), next_state)
+ * (Architecture_wrappers.py:197-267) on the memory of the last tt2_encode: frame_in [B,80] = the
+ * cell input (GO frame = zeros, then the previous raw frame, helpers.py:57), prenet_masks [2,B,P]
+ * uint8 keep bits of this step; writes state_out (arrays may alias state_in's),
+ * frame_out [B,80], stop_out [B] (sigmoid), alignments_out [B,T_in] (nullable; the step's
+ * alignments before accumulation).  Plain fp32 kernels: the parity / debugging seam, not the fast
+ * path (tt2_decode runs the fused loop). */
+tt2_status tt2_decoder_step(tt2_ctx* ctx, const float* frame_in, const uint8_t* prenet_masks,
+                            const tt2_decoder_state* state_in, tt2_decoder_state* state_out,
+                            float* frame_out, float* stop_out, float* alignments_out);
+
 /* decoder clip + Postnet + postnet_projection + final clip (tacotron.py:362-381) on the frames of
  * the last tt2_decode (frames_in == NULL) or on caller frames [B,T,80].
  * decoder_output (nullable) and mel_out are [B,T,80]. */

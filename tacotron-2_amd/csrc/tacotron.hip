@@ -15,6 +15,7 @@
 #include "common.h"
 #include "decode_persist.h"
 #include "gemm.h"
+#include "step.h"
 
 namespace tt2 {
 
@@ -1137,6 +1138,9 @@ struct tt2_ctx {
   // max |w| of the weights the split fp16x3 MFMA kernels keep resident (pre-scaled by KG_SB):
   // the persistent decoder / BiLSTM need < KG_BMAX, larger weights take the fp32-MFMA launch path
   float kg_wmax_dec = 0.f, kg_wmax_enc = 0.f;
+  // tt2_decoder_step: row-major copies of the decoder variables (uploaded on first use), scratch
+  tt2::DevBuf st_w[16], st_io, st_scratch;
+  bool st_ready = false;
   // the persistent decoder's copies of l1_w, l1_wh, l2_w, l2_wh, proj_w, pre-scaled by KG_SB
   tt2::DevBuf pd_l1_w, pd_l1_wh, pd_l2_w, pd_l2_wh, pd_proj_w;
   tt2::DevBuf pre_w1r, pre_b1, pre_w2, pre_b2, q_w;  // pre_w1r: row-major [nm][P] (GTA TP1 GEMM)
@@ -1473,6 +1477,7 @@ static void finalize(tt2_ctx* c) {
   TT2_HIP(hipDeviceSynchronize());
   upload(c->post_pb, need(wm, P + "postnet_projection/projection_postnet_projection/bias", {c->nm}));
   c->finalized = true;
+  c->st_ready = false;
 }
 
 static void alloc_acts(tt2_ctx* c) {
@@ -2208,6 +2213,96 @@ tt2_status tt2_encode(tt2_ctx* c, const int32_t* ids, const int32_t* lengths, in
         TT2_HIP(hipMemcpyAsync(style_out + (size_t)b * c->SW, c->style.as<float>() + (size_t)b * c->SW,
                                sizeof(float) * c->SW, hipMemcpyDeviceToHost, s));
     TT2_HIP(hipStreamSynchronize(s));
+  });
+}
+
+static void decoder_step_dev(tt2_ctx* c, const float* frame_in, const uint8_t* masks,
+                             const tt2_decoder_state* in, tt2_decoder_state* out, float* frame_out, float* stop_out,
+                             float* align_out) {
+  TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_finalize_weights not called");
+  TT2_CHECK(c->encoded, TT2_ERR_STATE, "tt2_decoder_step called before tt2_encode");
+  TT2_CHECK(frame_in && masks && in && out && frame_out && stop_out, TT2_ERR_INVALID_ARG,
+            "tt2_decoder_step: null argument");
+  TT2_CHECK(in->h1 && in->c1 && in->h2 && in->c2 && in->attention && in->alignments && in->max_attentions &&
+                out->h1 && out->c1 && out->h2 && out->c2 && out->attention && out->alignments && out->max_attentions,
+            TT2_ERR_INVALID_ARG, "tt2_decoder_step: null state array");
+  const auto& cfg = c->cfg;
+  const std::string P(TP);
+  const WeightMap& wm = c->host;
+  hipStream_t s = c->stream;
+  if (!c->st_ready) {  // raw row-major variables, exactly as loaded
+    const char* names[16] = {"decoder/decoder_prenet/dense_1/kernel", "decoder/decoder_prenet/dense_1/bias",
+                             "decoder/decoder_prenet/dense_2/kernel", "decoder/decoder_prenet/dense_2/bias",
+                             "decoder/decoder_LSTM/multi_rnn_cell/cell_0/lstm_cell/kernel",
+                             "decoder/decoder_LSTM/multi_rnn_cell/cell_0/lstm_cell/bias",
+                             "decoder/decoder_LSTM/multi_rnn_cell/cell_1/lstm_cell/kernel",
+                             "decoder/decoder_LSTM/multi_rnn_cell/cell_1/lstm_cell/bias", "decoder/query_layer/kernel",
+                             "decoder/Location_Sensitive_Attention/location_features_convolution/kernel",
+                             "decoder/Location_Sensitive_Attention/location_features_layer/kernel",
+                             "decoder/Location_Sensitive_Attention/attention_variable_projection",
+                             "decoder/linear_transform_projection/projection_linear_transform_projection/kernel",
+                             "decoder/linear_transform_projection/projection_linear_transform_projection/bias",
+                             "decoder/stop_token_projection/projection_stop_token_projection/kernel",
+                             "decoder/stop_token_projection/projection_stop_token_projection/bias"};
+    for (int i = 0; i < 16; ++i) {
+      auto it = wm.find(P + names[i]);
+      TT2_CHECK(it != wm.end(), TT2_ERR_NOT_LOADED, std::string("missing variable ") + P + names[i]);
+      upload(c->st_w[i], it->second);
+    }
+    c->st_ready = true;
+  }
+  StepWeights w;
+  const float* const* wp[16] = {&w.pre_w1, &w.pre_b1, &w.pre_w2, &w.pre_b2, &w.k1, &w.b1, &w.k2, &w.b2,
+                                &w.wq, &w.wconv, &w.wloc, &w.va, &w.wf, &w.bf, &w.ws, &w.bs};
+  for (int i = 0; i < 16; ++i) *const_cast<const float**>(wp[i]) = c->st_w[i].as<float>();
+  StepDims d;
+  d.B = c->B; d.T = c->T_in; d.nm = c->nm; d.P = c->P; d.H = c->H; d.D = c->Dm; d.A = c->A; d.F = c->F; d.KL = c->KL;
+  d.zo = cfg.zoneout; d.cumulative = cfg.cumulative_weights; d.constraint = cfg.synthesis_constraint;
+  d.monotonic = cfg.constraint_monotonic; d.win = cfg.attention_win_size; d.mask_encoder = cfg.mask_encoder;
+  const size_t B = d.B, nH = B * d.H, nD = B * d.D, nT = B * d.T;
+  // device image of [frame_in | 4 states | ctx | cum | max_att | masks] in and the outputs
+  const size_t f_in = B * d.nm, n_in = f_in + 4 * nH + nD + nT, n_out = 4 * nH + nD + nT + f_in + B + nT;
+  const size_t bytes = sizeof(float) * (n_in + n_out) + 2 * sizeof(int) * B + 2 * B * d.P + 64;
+  c->st_io.alloc(bytes);
+  c->st_scratch.alloc(sizeof(float) * step_scratch_floats(d));
+  float* base = c->st_io.as<float>();
+  float* fi = base;
+  float* h1 = fi + f_in; float* c1 = h1 + nH; float* h2 = c1 + nH; float* c2 = h2 + nH;
+  float* cx = c2 + nH; float* cu = cx + nD;
+  float* o = cu + nT;
+  float* h1o = o; float* c1o = h1o + nH; float* h2o = c1o + nH; float* c2o = h2o + nH;
+  float* cxo = c2o + nH; float* cuo = cxo + nD; float* fo = cuo + nT; float* so = fo + f_in; float* ao = so + B;
+  int* ma = reinterpret_cast<int*>(ao + nT);
+  int* mao = ma + B;
+  uint8_t* mk = reinterpret_cast<uint8_t*>(mao + B);
+  auto h2d = [&](void* dst, const void* src, size_t n) { TT2_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s)); };
+  auto d2h = [&](void* dst, const void* src, size_t n) { TT2_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s)); };
+  h2d(fi, frame_in, 4 * f_in);
+  h2d(h1, in->h1, 4 * nH); h2d(c1, in->c1, 4 * nH); h2d(h2, in->h2, 4 * nH); h2d(c2, in->c2, 4 * nH);
+  h2d(cx, in->attention, 4 * nD); h2d(cu, in->alignments, 4 * nT); h2d(ma, in->max_attentions, 4 * B);
+  h2d(mk, masks, 2 * B * d.P);
+  StepIO io;
+  io.keys = c->keys.as<float>(); io.values = c->values.as<float>(); io.lengths = c->lens.as<int>();
+  io.frame_in = fi; io.masks = mk;
+  io.h1 = h1; io.c1 = c1; io.h2 = h2; io.c2 = c2; io.ctx = cx; io.cum = cu; io.max_att = ma;
+  io.h1o = h1o; io.c1o = c1o; io.h2o = h2o; io.c2o = c2o; io.ctxo = cxo; io.cumo = cuo; io.max_att_o = mao;
+  io.frame = fo; io.stop = so; io.align = ao; io.scratch = c->st_scratch.as<float>();
+  decoder_step_launch(w, d, io, s);
+  d2h(out->h1, h1o, 4 * nH); d2h(out->c1, c1o, 4 * nH); d2h(out->h2, h2o, 4 * nH); d2h(out->c2, c2o, 4 * nH);
+  d2h(out->attention, cxo, 4 * nD); d2h(out->alignments, cuo, 4 * nT); d2h(out->max_attentions, mao, 4 * B);
+  d2h(frame_out, fo, 4 * f_in); d2h(stop_out, so, 4 * B);
+  if (align_out) d2h(align_out, ao, 4 * nT);
+  TT2_HIP(hipStreamSynchronize(s));
+  out->time = in->time + 1;
+}
+
+tt2_status tt2_decoder_step(tt2_ctx* c, const float* frame_in, const uint8_t* prenet_masks,
+                            const tt2_decoder_state* state_in, tt2_decoder_state* state_out, float* frame_out,
+                            float* stop_out, float* alignments_out) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    TT2_HIP(hipSetDevice(c->dev));
+    decoder_step_dev(c, frame_in, prenet_masks, state_in, state_out, frame_out, stop_out, alignments_out);
   });
 }
 

@@ -80,6 +80,12 @@ class TrainConfig(ctypes.Structure):
         ("bn_momentum", ctypes.c_float), ("bn_eps", ctypes.c_float)]
 
 
+class DecoderState(ctypes.Structure):
+    """tt2_decoder_state (include/tt2.h): pointers to caller-owned host arrays."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("h1", "c1", "h2", "c2", "attention", "alignments",
+                                              "max_attentions")] + [("time", ctypes.c_int32)]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _U64 = ctypes.c_uint64
@@ -123,6 +129,8 @@ SIGNATURES = {
     "tt2_gl_synthesize_dev": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "tt2_mol_sample": (_I, [_P, _P, _P, _I, _I, _F, _P, _P]),
     "tt2_prenet_keep_bits": (_I, [_U64, _I, _I, _I, _P]),
+    "tt2_decoder_step": (_I, [_P, _P, _P, ctypes.POINTER(DecoderState),
+                              ctypes.POINTER(DecoderState), _P, _P, _P]),
     "tt2_wn_noise": (_I, [_U64, _I, _I, _I, _I, _P, _P]),
     "tt2_train_default_config": (None, [ctypes.POINTER(TrainConfig), _I, _I, _I]),
     "tt2_train_create": (_I, [ctypes.POINTER(TrainConfig), _I, ctypes.POINTER(_P)]),

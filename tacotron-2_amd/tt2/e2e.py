@@ -59,6 +59,11 @@ class TextToSpeech(object):
         self.wn = WaveNetEngine(hp, wn_weights, max_batch, max_iters * self.hop, device)
         self.lib = _lib.load_library()
 
+    @property
+    def torch_device(self):
+        import torch
+        return torch.device("cuda", self.device)
+
     def close(self):
         for e in (getattr(self, "taco", None), getattr(self, "wn", None)):
             if e is not None:
@@ -151,22 +156,36 @@ class TextToSpeech(object):
                     stop=out["stop"][:, :out["n_steps"]].cpu().numpy(), n_steps=out["n_steps"])
 
 
-def synthesize_sharded(tts, ids, lengths, ref_emt, ref_spk, seed=0, group=None):
+def synthesize_sharded(tts, ids, lengths, ref_emt, ref_spk, seed=0, group=None, u_mix=None,
+                       u_log=None, prenet_masks=None):
     """Utterance-sharded text -> wav over torch.distributed ranks (each rank holds ``tts`` on its
     own GPU).  Every rank passes the SAME global batch; rank r synthesises its contiguous slice
-    and one all_gather returns every rank the trimmed waveforms in global utterance order."""
+    and one all_gather returns every rank the trimmed waveforms in global utterance order.  The
+    waveforms stay on the device up to the collective (RCCL under "nccl").  Optional injected
+    noise covers the GLOBAL batch and is sliced per rank: prenet_masks [max_iters,2,B,P],
+    u_mix [T,B,10], u_log [T,B] (parity runs); None = the device RNGs keyed by ``seed + rank``."""
+    import torch
     import torch.distributed as dist
-    from .parallel import gather_padded, shard
+    from .parallel import gather_padded, shard, shard_range
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     ids_r, len_r, re_r, rs_r = shard([np.asarray(ids), np.asarray(lengths), np.asarray(ref_emt),
                                       None if ref_spk is None else np.asarray(ref_spk)], rank, world)
+    s, e = shard_range(np.asarray(ids).shape[0], rank, world)
     if ids_r.shape[0]:
-        out = tts.synthesize(ids_r, len_r, re_r, rs_r, seed + rank)
-        wavs = out["wavs"]
+        dev = tts.torch_device
+
+        def up(a, dt):
+            return None if a is None else torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)
+        lens_h = np.ascontiguousarray(len_r, np.int32)
+        out = tts.synthesize_dev(up(ids_r, np.int32), up(lens_h, np.int32), lens_h,
+                                 up(re_r, np.float32), up(rs_r, np.float32), seed + rank,
+                                 u_mix_d=None if u_mix is None else up(np.asarray(u_mix)[:, s:e], np.float32),
+                                 u_log_d=None if u_log is None else up(np.asarray(u_log)[:, s:e], np.float32),
+                                 prenet_masks_d=None if prenet_masks is None else
+                                 up(np.asarray(prenet_masks)[:, :, s:e], np.uint8))
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        local, alen = out["wav"], out["audio_lengths"]
     else:
-        wavs = []
-    Tm = max([w.shape[0] for w in wavs] + [1])
-    local = np.zeros((len(wavs), Tm), np.float32)
-    for i, w in enumerate(wavs):
-        local[i, :w.shape[0]] = w
-    return gather_padded(local, [w.shape[0] for w in wavs], group=group)
+        local, alen = np.zeros((0, 1), np.float32), np.zeros((0,), np.int64)
+    return gather_padded(local, alen, group=group)

@@ -99,6 +99,7 @@ class TacotronEngine(object):
         ids = i32(ids)
         lengths = i32(lengths)
         B, T = ids.shape
+        self._B, self._T_in = B, T
         ref_emt = f32(ref_emt)
         ref_spk = f32(ref_spk) if ref_spk is not None else None
         mem = np.zeros((B, T, self.D), np.float32)
@@ -131,6 +132,42 @@ class TacotronEngine(object):
                                   ptr(align), ctypes.byref(n)))
         n = n.value
         return frames[:, :n], stop[:, :n], align[:, :, :n]
+
+    def zero_state(self):
+        """TacotronDecoderCell.zero_state (Architecture_wrappers.py:158-195) for the batch of the last
+        encode: dict of numpy arrays h1, c1, h2, c2 [B,H], attention [B,D_mem], alignments
+        [B,T_in], max_attentions [B] int32, time."""
+        B, T, H = self._B, self._T_in, self.hp.decoder_lstm_units
+        z = lambda *s: np.zeros(s, np.float32)  # noqa: E731
+        return dict(h1=z(B, H), c1=z(B, H), h2=z(B, H), c2=z(B, H), attention=z(B, self.D),
+                    alignments=z(B, T), max_attentions=np.zeros(B, np.int32), time=0)
+
+    def decoder_step(self, frame_in, prenet_masks, state):
+        """tt2_decoder_step: one TacotronDecoderCell.__call__ (Architecture_wrappers.py:197-267)
+        on the memory of the last encode.  frame_in [B,80], prenet_masks [2,B,P] uint8, state as
+        zero_state() returns.  Returns (frame [B,80], stop [B], alignments [B,T_in], next_state)."""
+        B, T = self._B, self._T_in
+        P = self.hp.prenet_layers[0]
+        fi = f32(frame_in)
+        m = np.ascontiguousarray(prenet_masks, np.uint8)
+        if fi.shape != (B, self.hp.num_mels) or m.shape != (2, B, P):
+            raise ValueError("frame_in must be [B, num_mels] and prenet_masks [2, B, prenet_units]")
+        names = ("h1", "c1", "h2", "c2", "attention", "alignments")
+        cin = {k: f32(state[k]) for k in names}
+        cin["max_attentions"] = i32(state["max_attentions"])
+        nxt = {k: np.zeros_like(v) for k, v in cin.items()}
+
+        def struct(d, time):
+            return _lib.DecoderState(*[d[k].ctypes.data for k in names + ("max_attentions",)],
+                                     int(time))
+        sin, sout = struct(cin, state.get("time", 0)), struct(nxt, 0)
+        frame = np.zeros((B, self.hp.num_mels), np.float32)
+        stop = np.zeros((B,), np.float32)
+        align = np.zeros((B, T), np.float32)
+        check(self.lib.tt2_decoder_step(self.h, ptr(fi), ptr(m), ctypes.byref(sin),
+                                        ctypes.byref(sout), ptr(frame), ptr(stop), ptr(align)))
+        nxt["time"] = sout.time
+        return frame, stop, align, nxt
 
     def decoder_path(self):
         """(persistent, kernel_ms): 1 when the single-launch persistent decoder serves the current

@@ -29,28 +29,31 @@ def gather_padded(local, lengths, group=None, pad_value=0.0):
     """All-gather per-rank outputs [B_r, T_r, ...] with per-utterance lengths [B_r] (time axis 1).
 
     Returns (list of per-utterance arrays trimmed to their lengths, in global utterance order).
-    Works with any torch.distributed backend; tensors live on the device the backend expects
-    (CUDA for nccl, CPU for gloo)."""
+    ``local`` may be a numpy array or a torch tensor.  Under backend "nccl" (RCCL over xGMI) a CUDA
+    tensor is padded and gathered on the device -- no host round trip before the collective, only
+    the trimmed results come back to the host; gloo gathers CPU tensors."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     dev = torch.device("cuda", torch.cuda.current_device()) \
         if dist.get_backend(group) == "nccl" else torch.device("cpu")
-    local = np.asarray(local)
-    lengths = np.asarray(lengths, np.int64)
-    meta = torch.tensor([local.shape[0], local.shape[1] if local.ndim > 1 else 0], dtype=torch.int64,
+    if isinstance(local, torch.Tensor):
+        t_local = local.to(dev, torch.float32)
+    else:
+        t_local = torch.from_numpy(np.ascontiguousarray(local, np.float32)).to(dev)
+    lengths = torch.as_tensor(np.asarray(lengths, np.int64)).to(dev)
+    shape = tuple(t_local.shape)
+    meta = torch.tensor([shape[0], shape[1] if len(shape) > 1 else 0], dtype=torch.int64,
                         device=dev)
     metas = [torch.zeros_like(meta) for _ in range(world)]
     dist.all_gather(metas, meta, group=group)
+    metas = [m.cpu() for m in metas]
     bmax = int(max(m[0] for m in metas))
     tmax = int(max(m[1] for m in metas))
-    tail = local.shape[2:]
-    pad = np.full((bmax, tmax) + tail, pad_value, dtype=np.float32)
-    pad[:local.shape[0], :local.shape[1]] = local
-    lpad = np.zeros((bmax,), np.int64)
-    lpad[:lengths.shape[0]] = lengths
-    t = torch.from_numpy(pad).to(dev)
-    lt = torch.from_numpy(lpad).to(dev)
+    t = torch.full((bmax, tmax) + shape[2:], pad_value, dtype=torch.float32, device=dev)
+    t[:shape[0], :shape[1]] = t_local
+    lt = torch.zeros((bmax,), dtype=torch.int64, device=dev)
+    lt[:shape[0]] = lengths
     outs = [torch.empty_like(t) for _ in range(world)]
     louts = [torch.empty_like(lt) for _ in range(world)]
     dist.all_gather(outs, t, group=group)
@@ -58,10 +61,9 @@ def gather_padded(local, lengths, group=None, pad_value=0.0):
     res = []
     for r in range(world):
         nb = int(metas[r][0])
-        o = outs[r].cpu().numpy()
         ls = louts[r].cpu().numpy()
         for i in range(nb):
-            res.append(o[i, :int(ls[i])])
+            res.append(outs[r][i, :int(ls[i])].cpu().numpy())
     return res
 
 
@@ -76,6 +78,13 @@ def tower_mean_(flat_grads, group=None):
         return flat_grads
     world = dist.get_world_size(group)
     if world == 1:
+        return flat_grads
+    if flat_grads.is_cuda and dist.get_backend(group) != "nccl":
+        # gloo (CPU rehearsal of the DP path, e.g. two ranks sharing one GPU in a test): reduce a
+        # host copy, ordered after the producer's stream
+        host = flat_grads.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        flat_grads.copy_(host.div_(world))
         return flat_grads
     dist.all_reduce(flat_grads, op=dist.ReduceOp.SUM, group=group)
     flat_grads.div_(world)

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [os.path.join(ROOT, "tacotron-2_amd"), ROOT, os.path.join(ROOT, "tests")]
 
-from _common import small_hparams, small_wavenet_hparams  # noqa: E402
+from _common import full_hparams, small_hparams, small_wavenet_hparams  # noqa: E402
 from oracle import tacotron_ref as TR  # noqa: E402
 from oracle import wavenet_ref as WR  # noqa: E402
 from oracle.hp import oracle_hp, wavenet_oracle_hp  # noqa: E402
@@ -62,6 +62,44 @@ def tacotron_fixtures():
                         alignments=out["alignments"])
 
 
+def decoder_step_inputs(seed=61):
+    """Single decoder-step fixture inputs at the fork widths (B=2, T_in=7,
+    D_mem=1024): memory from the oracle encoder + style path, and a non-trivial carried state."""
+    hp = full_hparams()
+    W = init_tacotron_weights(hp, seed=5339)
+    oh = oracle_hp(hp)
+    B, T = 2, 7
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=seed)
+    enc = TR.encoder(ids, lens, W, oh)
+    style = TR.style_embedding(re, rs, W, oh)
+    values, keys = TR.memory_and_keys(enc, style, lens, W)
+    rng = np.random.default_rng(seed)
+    H, D = hp.decoder_lstm_units, values.shape[2]
+    st = TR.DecoderState(B, T, D, H, np.float32)
+    st.h1, st.c1, st.h2, st.c2 = [rng.uniform(-0.5, 0.5, (B, H)).astype(np.float32) for _ in range(4)]
+    a = rng.random((B, T)) * (np.arange(T)[None] < lens[:, None])
+    a = (a / a.sum(1, keepdims=True)).astype(np.float32)
+    st.ctx = np.einsum("bt,btd->bd", a, values).astype(np.float32)
+    st.cum = (a * 3.0).astype(np.float32)
+    st.max_att = np.array([min(3, lens[b] - 1) for b in range(B)], np.int32)
+    frame_in = rng.uniform(-4, 4, (B, hp.num_mels)).astype(np.float32)
+    masks = prenet_masks(1, B, hp.prenet_layers[0], seed=seed)[0]
+    return hp, W, ids, lens, re, rs, values, keys, st, frame_in, masks
+
+
+def decoder_step_fixtures():
+    hp, W, ids, lens, re, rs, values, keys, st, frame_in, masks = decoder_step_inputs()
+    state_in = dict(h1=st.h1, c1=st.c1, h2=st.h2, c2=st.c2, attention=st.ctx, alignments=st.cum,
+                    max_attentions=st.max_att)
+    frame, stop, align = TR.decoder_step(frame_in, masks, st, keys, values, lens, W, oracle_hp(hp))
+    np.savez_compressed(
+        os.path.join(HERE, "tacotron_decoder_step.npz"), ids=ids, lengths=lens, ref_emt=re,
+        ref_spk=rs, frame_in=frame_in, prenet_masks=masks, weight_checksum=weight_checksum(W),
+        **{"in_" + k: v for k, v in state_in.items()},
+        out_h1=st.h1, out_c1=st.c1, out_h2=st.h2, out_c2=st.c2, out_attention=st.ctx,
+        out_alignments=st.cum, out_max_attentions=st.max_att, frame=frame, stop=stop, align=align)
+
+
 def wavenet_fixtures():
     hp = small_wavenet_hparams(6, 2)
     W = init_wavenet_weights(hp, seed=5339)
@@ -99,6 +137,7 @@ def mol_fixtures():
 
 
 if __name__ == "__main__":
+    decoder_step_fixtures()
     tacotron_fixtures()
     wavenet_fixtures()
     mol_fixtures()

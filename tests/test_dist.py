@@ -97,6 +97,8 @@ def test_shard_arrays_none_passthrough():
 class _StubTTS(object):
     """CPU stand-in for tt2.e2e.TextToSpeech (the device path needs a GPU): utterance i gets a
     waveform of length 3 * (sum of its ids) % 17 + 1 whose samples encode its ids."""
+    import torch
+    torch_device = torch.device("cpu")
 
     def synthesize(self, ids, lengths, ref_emt, ref_spk, seed=0):
         wavs = []
@@ -104,6 +106,16 @@ class _StubTTS(object):
             n = 3 * int(ids[b, :lengths[b]].sum()) % 17 + 1
             wavs.append(np.arange(n, dtype=np.float32) + float(ids[b, 0]))
         return dict(wavs=wavs)
+
+    def synthesize_dev(self, ids_d, lens_d, lens_h, re_d, rs_d, seed=0, **noise):
+        """Same waveforms as synthesize(), returned like TextToSpeech.synthesize_dev (padded
+        tensor + per-row audio lengths)."""
+        import torch
+        wavs = self.synthesize(ids_d.numpy(), lens_h, None, None, seed)["wavs"]
+        wav = torch.zeros((len(wavs), max(w.shape[0] for w in wavs)))
+        for i, w in enumerate(wavs):
+            wav[i, :w.shape[0]] = torch.from_numpy(w)
+        return dict(wav=wav, audio_lengths=np.array([w.shape[0] for w in wavs], np.int64))
 
 
 def _e2e_worker(rank, world, port, out_dir):

@@ -370,3 +370,50 @@ def test_wavenet_shim_initialize():
     assert m.tower_y_hat[0].shape == (2, 275)
     assert m.tower_synth_upsampled_local_features[0].shape == (2, 80, 275)
     assert np.all(np.abs(m.tower_y_hat[0]) <= 1.0)
+
+
+# ----------------------------------------------------------- single-step seam (tt2_decoder_step)
+
+def test_decoder_step_golden_fixture(full_setup):
+    """tt2_decoder_step (TacotronDecoderCell.__call__, Architecture_wrappers.py:197-267) from the
+    committed fixture's non-trivial state: every output and next-state array vs the oracle's."""
+    import os
+    hp, W = full_setup
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                             "tacotron_decoder_step.npz"))
+    ids, lens = g["ids"], g["lengths"]
+    eng = _engine(hp, W, ids.shape[0], ids.shape[1], g["ref_emt"].shape[1], 4)
+    eng.encode(ids, lens, g["ref_emt"], g["ref_spk"])
+    names = ("h1", "c1", "h2", "c2", "attention", "alignments", "max_attentions")
+    state = {k: g["in_" + k] for k in names}
+    state["time"] = 5
+    frame, stop, align, nxt = eng.decoder_step(g["frame_in"], g["prenet_masks"], state)
+    eng.close()
+    np.testing.assert_allclose(frame, g["frame"], atol=1e-5)
+    np.testing.assert_allclose(stop, g["stop"], atol=1e-6)
+    np.testing.assert_allclose(align, g["align"], atol=1e-6)
+    for k in names[:-1]:
+        np.testing.assert_allclose(nxt[k], g["out_" + k], atol=1e-5, err_msg=k)
+    np.testing.assert_array_equal(nxt["max_attentions"], g["out_max_attentions"])
+    assert nxt["time"] == 6
+
+
+@pytest.mark.parametrize("constraint", [False, True])
+def test_decoder_step_chain_matches_decode(small_setup, constraint):
+    """Driving tt2_decoder_step from zero_state with the previous raw frame as input (TacoTestHelper,
+    helpers.py:57) reproduces tt2_decode's fused loop step for step."""
+    hp, W = small_setup
+    B, T, n = 3, 11, 12
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=13)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=13)
+    eng = _engine(hp, W, B, T, 64, n, constraint)
+    full = eng.synthesize(ids, lens, re, rs, n, masks)
+    eng.encode(ids, lens, re, rs)
+    state = eng.zero_state()
+    frame = np.zeros((B, hp.num_mels), np.float32)
+    for t in range(full["frames"].shape[1]):
+        frame, stop, align, state = eng.decoder_step(frame, masks[t], state)
+        np.testing.assert_allclose(frame, full["frames"][:, t], atol=1e-5)
+        np.testing.assert_allclose(stop, full["stop_token_prediction"][:, t], atol=1e-5)
+        np.testing.assert_allclose(align, full["alignments"][:, :, t], atol=1e-5)
+    eng.close()
