@@ -105,56 +105,50 @@ def _number_to_words(num, andword='and', zero='zero', group=0):
     return _ordinalize(words) if ordinal else words
 
 
-def _remove_commas(m):
-    return m.group(1).replace(',', '')
+def _plural(n, unit):
+    return '%s %s' % (n, unit if n == 1 else unit + 's')
 
 
-def _expand_decimal_point(m):
-    return m.group(1).replace('.', ' point ')
+def _dollars(m):
+    """numbers.py:22-40: '$1.50' -> '1 dollar, 50 cents'; more than one '.' is left as digits."""
+    amount = m.group(1)
+    whole, _, frac = amount.partition('.')
+    if '.' in frac:
+        return amount + ' dollars'
+    d = int(whole) if whole else 0
+    c = int(frac) if frac else 0
+    said = [_plural(v, u) for v, u in ((d, 'dollar'), (c, 'cent')) if v]
+    return ', '.join(said) if said else 'zero dollars'
 
 
-def _expand_dollars(m):
-    """numbers.py:22-40."""
-    match = m.group(1)
-    parts = match.split('.')
-    if len(parts) > 2:
-        return match + ' dollars'
-    dollars = int(parts[0]) if parts[0] else 0
-    cents = int(parts[1]) if len(parts) > 1 and parts[1] else 0
-    if dollars and cents:
-        return '%s %s, %s %s' % (dollars, 'dollar' if dollars == 1 else 'dollars',
-                                 cents, 'cent' if cents == 1 else 'cents')
-    if dollars:
-        return '%s %s' % (dollars, 'dollar' if dollars == 1 else 'dollars')
-    if cents:
-        return '%s %s' % (cents, 'cent' if cents == 1 else 'cents')
-    return 'zero dollars'
+def _cardinal_or_year(m):
+    """numbers.py:47-59: integers in (1000, 3000) are read as years (2000 'two thousand', 2001-2009
+    'two thousand <n>', whole hundreds '<nn> hundred', otherwise digit pairs with 'oh')."""
+    n = int(m.group(0))
+    if not 1000 < n < 3000:
+        return _number_to_words(n, andword='')
+    if n == 2000:
+        return 'two thousand'
+    if n < 2010 and n > 2000:
+        return 'two thousand ' + _number_to_words(n % 100)
+    if n % 100 == 0:
+        return _number_to_words(n // 100) + ' hundred'
+    return _number_to_words(n, andword='', zero='oh', group=2).replace(', ', ' ')
 
 
-def _expand_ordinal(m):
-    return _number_to_words(m.group(0))
-
-
-def _expand_number(m):
-    """numbers.py:47-59: years between 1000 and 3000 read in pairs."""
-    num = int(m.group(0))
-    if 1000 < num < 3000:
-        if num == 2000:
-            return 'two thousand'
-        if 2000 < num < 2010:
-            return 'two thousand ' + _number_to_words(num % 100)
-        if num % 100 == 0:
-            return _number_to_words(num // 100) + ' hundred'
-        return _number_to_words(num, andword='', zero='oh', group=2).replace(', ', ' ')
-    return _number_to_words(num, andword='')
+# numbers.py:62-69, applied in this order
+_RULES = (
+    (_comma_number_re, lambda m: m.group(1).replace(',', '')),
+    (_pounds_re, lambda m: m.group(1) + ' pounds'),
+    (_dollars_re, _dollars),
+    (_decimal_number_re, lambda m: m.group(1).replace('.', ' point ')),
+    (_ordinal_re, lambda m: _number_to_words(m.group(0))),
+    (_number_re, _cardinal_or_year),
+)
 
 
 def normalize_numbers(text):
-    """numbers.py:62-69."""
-    text = re.sub(_comma_number_re, _remove_commas, text)
-    text = re.sub(_pounds_re, r'\1 pounds', text)
-    text = re.sub(_dollars_re, _expand_dollars, text)
-    text = re.sub(_decimal_number_re, _expand_decimal_point, text)
-    text = re.sub(_ordinal_re, _expand_ordinal, text)
-    text = re.sub(_number_re, _expand_number, text)
+    """Spell out the numbers of ``text`` (numbers.py:62-69)."""
+    for pattern, repl in _RULES:
+        text = pattern.sub(repl, text)
     return text

@@ -1,61 +1,63 @@
-"""text_to_sequence / sequence_to_text of code/tacotron/utils/text.py:1-74.
+"""Character ids for Tacotron (the behaviour of code/tacotron/utils/text.py:1-74).
 
-Curly-brace ARPAbet spans are parsed like the reference (text.py:30-38) and, because the fork's
-symbol set has no ARPAbet entries (symbols.py:14,17), contribute no ids; EOS '~' (id 1) is
-appended; '_' and '~' inside the text are dropped (text.py:73-74).
+Input text is cut into plain runs and curly-brace ARPAbet spans with the reference's span grammar
+(text.py:30-38: shortest prefix, first ``{...}``, remainder; ``.`` stops at a newline, so the
+remainder after a newline is dropped exactly as there).  Plain runs go through the named cleaners,
+ARPAbet words become ``@``-prefixed symbols -- which the fork's symbol set does not contain
+(symbols.py:14,17), so they contribute no ids.  Symbols outside the table, the pad ``_`` and the
+EOS ``~`` are skipped (text.py:73-74), and one EOS id is appended (text.py:40-41).
 """
+import functools
 import re
 
 from . import cleaners
 from .symbols import symbols
 
-_symbol_to_id = {s: i for i, s in enumerate(symbols)}
-_id_to_symbol = {i: s for i, s in enumerate(symbols)}
+_PAD, _EOS = '_', '~'
+_ID = {s: i for i, s in enumerate(symbols)}
+_SYMBOL = dict(enumerate(symbols))
+_EMITTED = frozenset(s for s in symbols if s not in (_PAD, _EOS))
+_SPAN = re.compile(r'(.*?)\{(.+?)\}(.*)')
 
-_curly_re = re.compile(r'(.*?)\{(.+?)\}(.*)')
+
+def _segments(text):
+    """Yield (is_arpabet, piece) in text order."""
+    while text:
+        m = _SPAN.match(text)
+        if m is None:
+            yield False, text
+            return
+        prefix, phones, text = m.groups()
+        yield False, prefix
+        yield True, phones
+
+
+def _cleaned(text, cleaner_names):
+    fns = []
+    for name in cleaner_names:
+        fn = getattr(cleaners, name, None)
+        if fn is None:
+            raise Exception('Unknown cleaner: %s' % name)
+        fns.append(fn)
+    return functools.reduce(lambda acc, fn: fn(acc), fns, text)
 
 
 def text_to_sequence(text, cleaner_names):
-    sequence = []
-    while len(text):
-        m = _curly_re.match(text)
-        if not m:
-            sequence += _symbols_to_sequence(_clean_text(text, cleaner_names))
-            break
-        sequence += _symbols_to_sequence(_clean_text(m.group(1), cleaner_names))
-        sequence += _arpabet_to_sequence(m.group(2))
-        text = m.group(3)
-    sequence.append(_symbol_to_id['~'])
-    return sequence
+    """Ids of ``text`` after ``cleaner_names``, EOS-terminated."""
+    ids = []
+    for is_arpabet, piece in _segments(text):
+        syms = ['@' + p for p in piece.split()] if is_arpabet else _cleaned(piece, cleaner_names)
+        ids.extend(_ID[s] for s in syms if s in _EMITTED)
+    ids.append(_ID[_EOS])
+    return ids
 
 
 def sequence_to_text(sequence):
-    result = ''
-    for symbol_id in sequence:
-        if symbol_id in _id_to_symbol:
-            s = _id_to_symbol[symbol_id]
-            if len(s) > 1 and s[0] == '@':
-                s = '{%s}' % s[1:]
-            result += s
-    return result.replace('}{', ' ')
-
-
-def _clean_text(text, cleaner_names):
-    for name in cleaner_names:
-        cleaner = getattr(cleaners, name, None)
-        if not cleaner:
-            raise Exception('Unknown cleaner: %s' % name)
-        text = cleaner(text)
-    return text
-
-
-def _symbols_to_sequence(syms):
-    return [_symbol_to_id[s] for s in syms if _should_keep_symbol(s)]
-
-
-def _arpabet_to_sequence(text):
-    return _symbols_to_sequence(['@' + s for s in text.split()])
-
-
-def _should_keep_symbol(s):
-    return s in _symbol_to_id and s != '_' and s != '~'
+    """Inverse mapping; ARPAbet symbols render as ``{...}`` with adjacent spans space-joined."""
+    pieces = []
+    for i in sequence:
+        s = _SYMBOL.get(i)
+        if s is None:
+            continue
+        pieces.append('{%s}' % s[1:] if len(s) > 1 and s.startswith('@') else s)
+    return ''.join(pieces).replace('}{', ' ')
