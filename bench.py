@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--wavenet-frames", type=int, default=80, help="mel frames per WaveNet utterance")
     p.add_argument("--wavenet-steps", type=int, default=1)
     p.add_argument("--no-wavenet", action="store_true")
+    p.add_argument("--no-wavenet-widths", action="store_true",
+                   help="skip the R=128 / R=256 WaveNet legs (k_generate_wide)")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-frames", type=int, default=1000,
                    help="decoder frames per utterance of the end-to-end leg (configs[3])")
@@ -502,6 +504,48 @@ def main():
                                 algorithmic_bytes_per_sample=int(wbytes)),
                   diag_stage_stamps_us=wn_stamps, diag_shader_clock_mhz=wn_clock_mhz)
         weng.close()
+
+    # --- WaveNet at the reference's own widths (k_generate_wide): fork default R=128 (20 layers /
+    #     2 stacks, Gaussian head, SubPixel) and paper default R=256 (24 / 4, MoL), B=1 ---
+    if wn is not None and not a.no_wavenet_widths:
+        from tt2.hparams import hparams as fork_hp, paper_hparams
+        widths = {}
+        for tag, base in (("fork_r128", fork_hp), ("paper_r256", paper_hparams)):
+            whp = base.copy()
+            whp.override_from_dict(dict(hop_size=275, wavenet_num_gpus=1))
+            WW = init_wavenet_weights(whp, seed=whp.wavenet_random_seed)
+            nf = a.wavenet_frames
+            Tn = nf * 275
+            weng = WaveNetEngine(whp, WW, 1, Tn, local)
+            cond = ((np.random.default_rng(7 + rank).uniform(-4, 4, (1, 80, nf)) + 4) / 8).astype(np.float32)
+            cond_d = torch.from_numpy(cond).to(dev)
+            wav_d = torch.empty((1, Tn), dtype=torch.float32, device=dev)
+
+            def wstep():
+                _lib.check(lib.tt2_wn_generate_dev(weng.h, cond_d.data_ptr(), 1, nf, None, None, 5339 + rank,
+                                                   None, wav_d.data_ptr(), None, None, ctypes.c_void_p(stream)))
+            wstep()
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            wstep()
+            torch.cuda.synchronize()
+            barrier()
+            wel = max_over_ranks(time.perf_counter() - t0)
+            wms = (ctypes.c_float * 3)()
+            _lib.check(lib.tt2_wn_last_timings(weng.h, wms))
+            R, G, S_, L = whp.residual_channels, whp.gate_channels, whp.skip_out_channels, whp.layers
+            wbytes = 4 * (L * (3 * R * G + G + (G // 2) * (S_ + R) + S_ + R) + S_ * S_ + S_ * whp.out_channels)
+            gen_s = wms[2] / 1000.0
+            widths[tag] = dict(value=round(world * Tn / wel, 1), unit="audio-samples/s",
+                               realtime_factor=round(Tn / wel / 22050.0, 3), samples=Tn,
+                               residual_channels=R, layers=L, stacks=whp.stacks,
+                               head="gaussian" if whp.out_channels == 2 else "mol",
+                               us_per_sample=round(1e6 * gen_s / Tn, 3), kernel="k_generate_wide",
+                               algorithmic_bytes_per_sample=int(wbytes),
+                               achieved_gbs=round(wbytes * Tn / gen_s / 1e9, 1))
+            weng.close()
+        wn["widths"] = widths
 
     # --- end-to-end text -> mel -> wav (configs[3]): one utterance per rank, RCCL gather ---
     e2e = None

@@ -22,6 +22,7 @@
 
 #include "common.h"
 #include "gemm.h"
+#include "wavenet_wide.h"
 
 namespace tt2 {
 
@@ -636,6 +637,8 @@ struct tt2_wn_ctx {
   tt2::DevBuf up_k[8], up_b[8];
   tt2::DevBuf cin_d, up_a, up_b_buf, c_up_t, cond, umix, ulog, teacher, wav, kout, logits, gran, stamps;
   int chunk = 1;                 // utterances per generation launch
+  bool wide = false;             // R = 128 / 256: k_generate_wide (wavenet_wide.hip), one utterance per launch
+  tt2::DevBuf rings;             // k_generate_wide's per-work-group fast-WaveNet queues
   int* status_host = nullptr;    // pinned: spin-timeout word of the last launch
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool timed = false;
@@ -658,6 +661,11 @@ static void wn_finalize(tt2_wn_ctx* c) {
   constexpr int CK = WN_CK, SK = WN_SK;
   std::vector<float> cw((size_t)L * CK * WN_THREADS * 4), cb((size_t)L * G), condw((size_t)cin * L * G),
       condb((size_t)L * G), sow((size_t)L * SK * WN_THREADS * 4), sob((size_t)L * 2 * R);
+  std::vector<float> wide_cw, wide_so;
+  if (c->wide) {
+    cw.clear();
+    sow.clear();
+  }
   for (int l = 0; l < L; ++l) {
     const std::string s = P + "ResidualConv1DGLU_" + std::to_string(l) + "/";
     const std::string ln = "_ResidualConv1DGLU_" + std::to_string(l) + "/";
@@ -669,7 +677,13 @@ static void wn_finalize(tt2_wn_ctx* c) {
     const auto& bsk = need(wm, s + "residual_block_skip_conv" + ln + "bias", {S});
     const auto& ko = need(wm, s + "residual_block_out_conv" + ln + "kernel", {1, G / 2, R});
     const auto& bo = need(wm, s + "residual_block_out_conv" + ln + "bias", {R});
-    for (int tid = 0; tid < WN_THREADS; ++tid) {
+    if (c->wide) {  // k_generate_wide: gate-column blocks of ww_nc(R) work-groups per layer
+      for (int cc = 0; cc < ww_nc(R); ++cc) {
+        ww_pack_conv(k.data.data(), R, cc, wide_cw);
+        ww_pack_so(ksk.data.data(), ko.data.data(), R, cc, wide_so);
+      }
+    }
+    for (int tid = 0; tid < (c->wide ? 0 : WN_THREADS); ++tid) {
       const int q = tid / 8, ks = tid % 8;  // 32 column quads x 8 k-slices
       for (int kk = 0; kk < CK; ++kk) {
         // row of the linearized [kw*R, G] kernel (taps oldest first): kk < 16 -> tap row 16ks+kk
@@ -697,11 +711,11 @@ static void wn_finalize(tt2_wn_ctx* c) {
     for (int j = 0; j < S; ++j) sob[(size_t)l * 2 * R + j] = bsk.data[j];
     for (int j = 0; j < R; ++j) sob[(size_t)l * 2 * R + S + j] = bo.data[j];
   }
-  wupload(c->conv_w, cw);
+  wupload(c->conv_w, c->wide ? wide_cw : cw);
   wupload(c->conv_b, cb);
   wupload(c->cond_w, condw);
   wupload(c->cond_b, condb);
-  wupload(c->so_w, sow);
+  wupload(c->so_w, c->wide ? wide_so : sow);
   wupload(c->so_b, sob);
   wupload(c->f1_w, need(wm, P + "skip_convolutions/final_convolution_1/kernel", {1, S, S}).data);
   wupload(c->f1_b, need(wm, P + "skip_convolutions/final_convolution_1/bias", {S}).data);
@@ -819,6 +833,37 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   g.split16 = 1;  // conditioning in [0, 1] after the upsampler: fp16x3 split MFMA (gemm.h)
   gemm(g, s);
   TT2_HIP(hipEventRecord(c->ev[2], s));
+  if (c->wide) {
+    const int R = c->R, NG = ww_nc(R) * 2 * R;
+    c->rings.alloc(sizeof(float) * ww_ring_floats(R, c->L, c->L / c->cfg.stacks));
+    const size_t gbytes = sizeof(unsigned long long) * ((size_t)c->L * NG + 1) + 16;
+    c->gran.alloc(gbytes);
+    WideArgs w;
+    w.T = (int)T; w.L = c->L; w.per = c->L / c->cfg.stacks; w.Bg = B;
+    w.first_w = c->first_w.as<float>(); w.first_b = c->first_b.as<float>();
+    w.conv_w = c->conv_w.as<f32x4>(); w.conv_b = c->conv_b.as<float>(); w.cond = c->cond.as<float>();
+    w.so_w = c->so_w.as<f32x4>(); w.so_b = c->so_b.as<float>();
+    w.f1_w = c->f1_w.as<float>(); w.f1_b = c->f1_b.as<float>(); w.f2_w = c->f2_w.as<float>(); w.f2_b = c->f2_b.as<float>();
+    w.C = c->C; w.legacy = c->cfg.legacy; w.res_legacy = c->cfg.residual_legacy;
+    w.log_scale_min = c->cfg.log_scale_min; w.log_scale_min_gauss = c->cfg.log_scale_min_gauss;
+    w.u_mix = umix_d; w.u_log = ulog_d; w.seed = seed; w.teacher = teacher_d;
+    w.wav = wav_d; w.kout = k_d; w.logits = logits_d;
+    w.rings = c->rings.as<float>();
+    w.status = c->gran.as<int>();
+    w.gran = reinterpret_cast<unsigned long long*>(c->gran.as<char>() + 16);
+    const void* kern = ww_kernel(R, c->C == 2);
+    const unsigned shm = (unsigned)ww_lds_bytes(R, c->C);
+    for (int b = 0; b < B; ++b) {  // one utterance per launch: its layers fill NC x L CUs
+      w.b = b;
+      TT2_HIP(hipMemsetAsync(c->gran.p, 0, gbytes, s));  // every polled word starts at 0
+      void* params[] = {&w};
+      TT2_HIP(hipLaunchCooperativeKernel(kern, dim3(ww_blocks(R, c->L)), dim3(WW_THREADS), params, shm, s));
+      TT2_HIP(hipMemcpyAsync(c->status_host, c->gran.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    }
+    TT2_HIP(hipEventRecord(c->ev[3], s));
+    c->timed = true;
+    return;
+  }
   const int nst = wn_stages(c);
   const int chunk = c->chunk;  // utterances per launch: every stage of every utterance co-resident
   const size_t gbytes = sizeof(unsigned long long) * (size_t)chunk * nst * WN_GR + 16;
@@ -880,9 +925,11 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
     int ndev = 0;
     TT2_HIP(hipGetDeviceCount(&ndev));
     TT2_CHECK(hip_device >= 0 && hip_device < ndev, TT2_ERR_INVALID_ARG, "tt2_wn_create: bad device index");
-    TT2_CHECK(cfg->residual_channels == 64 && cfg->gate_channels == 128 && cfg->skip_out_channels == 64,
+    const int Rc = cfg->residual_channels;
+    TT2_CHECK((Rc == 64 || Rc == 128 || Rc == 256) && cfg->gate_channels == 2 * Rc && cfg->skip_out_channels == Rc,
               TT2_ERR_INVALID_ARG,
-              "this build's generation kernel is specialised for R=64, G=128, S=64 (BASELINE config 3)");
+              "generation kernels: residual_channels R = 64 (k_generate_pipe, BASELINE config 3), 128 (fork "
+              "default) or 256 (paper default), with gate_channels = 2R and skip_out_channels = R");
     TT2_CHECK(cfg->kernel_size == 3, TT2_ERR_INVALID_ARG, "kernel_size must be 3");
     TT2_CHECK(cfg->out_channels == 2 || (cfg->out_channels % 3 == 0 && cfg->out_channels <= 30 && cfg->out_channels >= 3),
               TT2_ERR_INVALID_ARG, "head needs out_channels = 2 (Gaussian) or 3*nr_mix <= 30 (MoL)");
@@ -905,14 +952,31 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
     TT2_HIP(hipSetDevice(hip_device));
     TT2_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
+    int ncu = 0;
+    TT2_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
+    if (Rc != 64) {  // k_generate_wide: NC work-groups per layer + a head, queues in global memory
+      c->wide = true;
+      const void* wk = ww_kernel(Rc, cfg->out_channels == 2);
+      const size_t wshm = ww_lds_bytes(Rc, cfg->out_channels);
+      TT2_HIP(hipFuncSetAttribute(wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wshm));
+      int nbw = 0;
+      TT2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbw, wk, WW_THREADS, wshm));
+      TT2_CHECK(nbw >= 1, TT2_ERR_INVALID_ARG, "wide generation kernel does not fit on a CU");
+      TT2_CHECK(ww_blocks(Rc, cfg->layers) <= ncu, TT2_ERR_INVALID_ARG,
+                "wide WaveNet: layers x work-groups per layer + head exceed the device's CUs");
+      c->chunk = 1;
+      TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->status_host), sizeof(int), hipHostMallocDefault));
+      *c->status_host = 0;
+      *out = c.release();
+      return;
+    }
     const size_t shm = gen_lds_bytes(c.get());
     TT2_CHECK(shm <= 160 * 1024, TT2_ERR_INVALID_ARG, "queue rings exceed the 160 KiB LDS of a CU");
     const void* kern = reinterpret_cast<const void*>(pipe_kernel(cfg->legacy != 0, cfg->residual_legacy != 0, cfg->out_channels == 2));
     TT2_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     // co-residency: one stage workgroup per CU, every workgroup of a launch resident at once
-    int nb = 0, ncu = 0;
+    int nb = 0;
     TT2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, WN_THREADS, shm));
-    TT2_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     TT2_CHECK(nb >= 1, TT2_ERR_INVALID_ARG, "generation kernel does not fit on a CU");
     const int nst = wn_stages(c.get());
     TT2_CHECK(nst * 8 <= ncu, TT2_ERR_INVALID_ARG, "too many pipeline stages for this device");

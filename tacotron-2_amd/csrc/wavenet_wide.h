@@ -1,0 +1,49 @@
+// Wide-channel WaveNet generator (residual channels R = 128 / 256): the fork default
+// (hparams.py:222-239: R=128, G=256, S=128, 20 layers / 2 stacks, Gaussian head) and the paper
+// default (paper_hparams.py:199-204: R=256, G=512, S=256, 24 layers / 4 stacks, MoL head).
+#pragma once
+#include "common.h"
+
+namespace tt2 {
+
+constexpr int WW_THREADS = 256;  // 4 waves, one per SIMD: up to 512 registers per lane
+constexpr int WW_TAPK = 32;      // tap rows (of [x(t-2d) | x(t-d)]) per k-slice
+constexpr int WW_XK = 16;        // x(t) rows per k-slice
+constexpr int WW_CK = WW_TAPK + WW_XK;
+constexpr int WW_SOK = 16;       // z rows per skip/out k-slice
+
+// CUs (work-groups) per layer: every layer's weights stay register-resident, 256 floats per lane
+__host__ __device__ constexpr int ww_nc(int R) { return R == 128 ? 2 : 8; }
+
+struct WideArgs {
+  int T, L, per;              // samples, layers, layers per stack
+  int b, Bg;                  // this launch's utterance, global batch (noise / cond indexing)
+  const float* first_w; const float* first_b;  // [R], [R]
+  const f32x4* conv_w;        // [L][NC][WW_CK][256] float4 (ww_pack_conv)
+  const float* conv_b;        // [L][G] gate-permuted (gate_col order)
+  const float* cond;          // [Bg][T][L][G] gate-permuted, cin_conv bias included
+  const f32x4* so_w;          // [L][NC][WW_SOK][256] float4 (ww_pack_so)
+  const float* so_b;          // [L][S + R] = [bs | bo]
+  const float* f1_w; const float* f1_b;  // [S][S], [S]
+  const float* f2_w; const float* f2_b;  // [S][C], [C]
+  int C, legacy, res_legacy;
+  float log_scale_min, log_scale_min_gauss;
+  const float* u_mix; const float* u_log;  // [T][Bg][nr], [T][Bg] or null
+  uint64_t seed;
+  const float* teacher;       // [Bg][T] or null
+  float* wav; int* kout; float* logits;    // [Bg][T], [Bg][T], [Bg][T][C]
+  float* rings;               // per (layer, CU): [2d+1][R] fast-WaveNet queue, zeroed by the kernel
+  unsigned long long* gran;   // [L][NC][S+R] + 1 sample granule; zeroed before the launch
+  int* status;
+};
+
+// Host packing of one layer's weights for CU c (row-major TF kernels: conv [3R][G], skip [R][S],
+// out [R][R]); appended to out.
+void ww_pack_conv(const float* conv, int R, int c, std::vector<float>& out);
+void ww_pack_so(const float* skip, const float* outk, int R, int c, std::vector<float>& out);
+size_t ww_ring_floats(int R, int L, int per);
+size_t ww_lds_bytes(int R, int C);
+int ww_blocks(int R, int L);
+const void* ww_kernel(int R, bool gauss);
+
+}  // namespace tt2

@@ -1,0 +1,421 @@
+// Wide-channel WaveNet generator for MI355X (gfx950): WaveNet.incremental (wavenet.py:821-886) with
+// R = 128 (fork default, hparams.py:222-239) or R = 256 (paper default, paper_hparams.py:199-204).
+//
+// At R=64 one CU holds three layers in registers (k_generate_pipe, wavenet.hip).  A layer at R=128
+// is 0.5 MB of fp32 weights (dilated conv 3R x 2R + skip/out R x 2R), at R=256 2 MB -- more than
+// one CU's 512 KB register file.  So each layer is split over NC = 2 / 8 work-groups by GATE
+// COLUMNS: work-group c owns the gate pairs (a_i, b_i) of z channels [c·R/NC, (c+1)·R/NC), i.e. a
+// contiguous block of the gate-permuted columns, computes its slice of z = tanh(a)·σ(b) and the
+// partial skip/out 1x1 products of that z slice, and publishes them as data-tagged granules
+// {tag = t+1, fp32} (the data is the flag; MI355X_MICROARCH.md Guideline 16 R2).  The next layer's
+// work-groups sum the NC partials (work-group 0 folds in the biases, the residual and the running
+// skip sum, and the legacy sqrt(1/2) scalings, which are linear) -- one hand-off per layer.  A
+// head work-group runs ReLU -> 1x1 -> ReLU -> 1x1 and the MoL / Gaussian sampler and hands the
+// sample back to layer 0.  Per lane: 32x4 tap weights + 16x4 x(t) weights + 16x4 skip/out weights
+// = 256 registers (VGPR + AGPR at one wave per SIMD).
+//
+// The fast-WaveNet queues (2d+1 rows of R, up to d = 512 at 10 layers per stack) exceed the LDS,
+// so every work-group keeps a private copy of its layer's queue in global memory (L2-resident):
+// written with plain stores, read back with L1-bypassing sc1 loads after the storing wave drained
+// -- the same CU only, so no cross-CU visibility is involved.  The taps x(t-2d), x(t-d) are read
+// and multiplied before the sample's input arrives (off the serial chain).
+#include "wavenet_wide.h"
+
+namespace tt2 {
+
+typedef __attribute__((address_space(1))) unsigned long long ww_gu64;
+typedef __attribute__((address_space(1))) int ww_gi32;
+
+__device__ __forceinline__ void ww_put(unsigned long long* g, unsigned tag, float v) {
+  __hip_atomic_store((ww_gu64*)g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ww_get(const unsigned long long* g) {
+  return __hip_atomic_load((ww_gu64*)const_cast<unsigned long long*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ f32x4 ww_ld4(const float* base, long i4) {  // sc1: bypass L1, L2-served
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i4 * 16), 0, 16));
+}
+
+// Bounded wave-uniform spin until ok() holds on every lane; false on timeout (4 s) or a peer's
+// failure (status word), which is then recorded.
+template <class F>
+__device__ __forceinline__ bool ww_spin(int* status, int lane, F ok) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned it = 0;; ++it) {
+    if (__all(ok())) return true;
+    if ((it & 255) == 255) {
+      if (__hip_atomic_load((ww_gi32*)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+        if (lane == 0) __hip_atomic_store((ww_gi32*)status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
+}
+
+// Sum over N adjacent lanes (N <= 16, a power of two); every lane of the group ends with the sum.
+template <int N>
+__device__ __forceinline__ void ww_reduce(f32x4& a) {
+#define TT2_STEP(C)                                                                                  \
+  {                                                                                                  \
+    const float t0 = dpp_f<C>(a[0]), t1 = dpp_f<C>(a[1]), t2 = dpp_f<C>(a[2]), t3 = dpp_f<C>(a[3]); \
+    a[0] += t0; a[1] += t1; a[2] += t2; a[3] += t3;                                                  \
+  }
+  if (N >= 2) TT2_STEP(DPP_XOR1)
+  if (N >= 4) TT2_STEP(DPP_XOR2)
+  if (N >= 8) TT2_STEP(DPP_HALF_MIRROR)
+  if (N >= 16) TT2_STEP(DPP_MIRROR)
+#undef TT2_STEP
+}
+
+__device__ __forceinline__ void ww_fma4(f32x4& acc, float x, const f32x4& w) {
+  acc[0] += x * w[0]; acc[1] += x * w[1]; acc[2] += x * w[2]; acc[3] += x * w[3];
+}
+
+template <int R, bool GAUSS>
+__global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
+  constexpr int NC = ww_nc(R), S = R, G = 2 * R, ZC = R / NC, GC = 2 * ZC, NQ = GC / 4, NKS = WW_THREADS / NQ;
+  constexpr int OUT = S + R, NQ2 = OUT / 4, NKS2 = WW_THREADS / NQ2, NG = NC * OUT;
+  static_assert(2 * R / NKS == WW_TAPK && R / NKS == WW_XK && ZC / NKS2 == WW_SOK, "k-slice geometry");
+  const float SQH = 0.70710677f;  // float32(np.sqrt(0.5))
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int L = a.L;
+  unsigned long long* const sample_gran = a.gran + (long)L * NG;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  int* flag = reinterpret_cast<int*>(sm);
+  if (tid == 0) flag[0] = 0;
+
+  if ((int)blockIdx.x == L * NC) {
+    // ======================= head: ReLU -> 1x1 -> ReLU -> 1x1 -> sampler =======================
+    constexpr int NQH = S / 4, NKSH = WW_THREADS / NQH, HK = S / NKSH;
+    float* skv = sm + 16;          // [S] relu(skips)
+    float* h1 = skv + S;           // [S]
+    float* lg = h1 + S;            // [32]
+    float* gum = lg + 32;          // [2][16] Gumbel terms (+ [15] logistic / normal draw) by t&1
+    float* f2 = gum + 32;          // [S][32]
+    float* red = f2 + S * 32;      // [32][32] f2 partials
+    const int qh = tid / NKSH, kh = tid % NKSH;
+    f32x4 w1[HK];
+#pragma unroll
+    for (int i = 0; i < HK; ++i) w1[i] = reinterpret_cast<const f32x4*>(a.f1_w + (long)(kh * HK + i) * S)[qh];
+    const f32x4 b1 = reinterpret_cast<const f32x4*>(a.f1_b)[qh];
+    for (int i = tid; i < S * 32; i += WW_THREADS) {
+      const int k = i >> 5, cc = i & 31;
+      f2[i] = cc < a.C ? a.f2_w[k * a.C + cc] : 0.f;
+    }
+    const float b2 = tid < a.C ? a.f2_b[tid] : 0.f;
+    const int nr = a.C / 3;
+    const unsigned long long* gin = a.gran + (long)(L - 1) * NG;
+    __syncthreads();
+    for (int t = 0; t < a.T; ++t) {
+      const int cb = t & 1;
+      if (wave == 1) {  // this sample's noise (injected, or the device RNG of common.h)
+        if (GAUSS) {
+          if (lane == 15) gum[cb * 16 + 15] = a.u_log ? a.u_log[(long)t * a.Bg + a.b] : wn_gauss(a.seed, t, a.Bg, a.b);
+        } else if (lane < nr) {
+          const float um = a.u_mix ? a.u_mix[((long)t * a.Bg + a.b) * nr + lane] : wn_uniform(a.seed, t, a.Bg, a.b, lane);
+          gum[cb * 16 + lane] = (float)log(-log((double)um));
+        } else if (lane == 15) {
+          const float ul = a.u_log ? a.u_log[(long)t * a.Bg + a.b] : wn_uniform(a.seed, t, a.Bg, a.b, 15);
+          const double uu = (double)ul;
+          gum[cb * 16 + 15] = (float)(log(uu) - log(1.0 - uu));
+        }
+      }
+      {  // skips = Σ of the last layer's NC skip partials (running sum and scalings folded in)
+        float v[S / WW_THREADS > 0 ? S / WW_THREADS : 1][NC];
+        const bool ok = ww_spin(a.status, lane, [&] {
+          bool good = true;
+#pragma unroll
+          for (int r = 0; r < (S + WW_THREADS - 1) / WW_THREADS; ++r) {
+            const int j = tid + r * WW_THREADS;
+            if (j >= S) continue;
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) {
+              const unsigned long long x = ww_get(gin + cc * OUT + j);
+              v[r][cc] = __uint_as_float((unsigned)x);
+              good = good && (unsigned)(x >> 32) == (unsigned)(t + 1);
+            }
+          }
+          return good;
+        });
+        if (!ok) flag[0] = 1;
+#pragma unroll
+        for (int r = 0; r < (S + WW_THREADS - 1) / WW_THREADS; ++r) {
+          const int j = tid + r * WW_THREADS;
+          if (j >= S) continue;
+          float s = 0.f;
+#pragma unroll
+          for (int cc = 0; cc < NC; ++cc) s += v[r][cc];
+          skv[j] = fmaxf(s, 0.f);
+        }
+      }
+      __syncthreads();
+      if (flag[0]) return;
+      {  // f1 (wavenet.py:840-842)
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const f32x4* xv4 = reinterpret_cast<const f32x4*>(skv + kh * HK);
+#pragma unroll
+        for (int i4 = 0; i4 < HK / 4; ++i4) {
+          const f32x4 xv = xv4[i4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ww_fma4(acc, xv[e], w1[4 * i4 + e]);
+        }
+        ww_reduce<NKSH>(acc);
+        if (kh == 0) {
+          f32x4 hv;
+          for (int e = 0; e < 4; ++e) hv[e] = fmaxf(acc[e] + b1[e], 0.f);
+          reinterpret_cast<f32x4*>(h1)[qh] = hv;
+        }
+      }
+      __syncthreads();
+      {  // f2 (wavenet.py:843-844): 8 column quads x 32 row slices of S/32, partials through LDS
+        constexpr int RK = S / 32;
+        const int cq = tid & 7, ksl = tid >> 3;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < RK; ++i) {
+          const int k = ksl * RK + i;
+          ww_fma4(acc, h1[k], reinterpret_cast<const f32x4*>(f2 + k * 32)[cq]);
+        }
+        reinterpret_cast<f32x4*>(red + ksl * 32)[cq] = acc;
+      }
+      __syncthreads();
+      if (tid < 32) {
+        float s = b2;
+        for (int k = 0; k < 32; ++k) s += red[k * 32 + tid];
+        lg[tid] = s;
+        if (a.logits && tid < a.C) a.logits[((long)a.b * a.T + t) * a.C + tid] = s;
+      }
+      __syncthreads();
+      if (wave == 0) {  // sampler (mixture.py:76-107 / gaussian.py:39-52), as k_generate_pipe
+        float temp = -INFINITY;
+        int idx = lane;
+        if (!GAUSS && lane < nr) temp = lg[lane] - gum[cb * 16 + lane];
+        argmax16(temp, idx);  // nr <= 10: the mixture logits sit in lanes 0..15
+        if (lane == 0) {
+          if (GAUSS) idx = 0;
+          const float mean = GAUSS ? lg[0] : lg[nr + idx];
+          const float ls = GAUSS ? fmaxf(lg[1], a.log_scale_min_gauss) : fmaxf(lg[2 * nr + idx], a.log_scale_min);
+          float x = mean + expf(ls) * gum[cb * 16 + 15];
+          x = fminf(fmaxf(x, -1.f), 1.f);
+          const float xn = a.teacher ? a.teacher[(long)a.b * a.T + t] : x;  // wavenet.py:876-878
+          ww_put(sample_gran, (unsigned)(t + 1), xn);
+          a.wav[(long)a.b * a.T + t] = x;
+          if (a.kout) a.kout[(long)a.b * a.T + t] = idx;
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+
+  // ============================ layer l, gate-column block c ============================
+  const int l = blockIdx.x / NC, c = blockIdx.x % NC;
+  float* xin = sm + 16;   // [R] x(t) of this layer
+  float* skin = xin + R;  // [S] running skip sum received
+  float* z = skin + S;    // [ZC]
+  const int q = tid / NKS, ks = tid % NKS;
+  const int q2 = tid / NKS2, ks2 = tid % NKS2;
+  const int d = 1 << (l % a.per), Lr = 2 * d + 1;
+  long roff = 0;
+  for (int l2 = 0; l2 < l; ++l2) roff += (long)NC * (2 * (1 << (l2 % a.per)) + 1) * R;
+  float* const ring = a.rings + roff + (long)c * Lr * R;
+  for (int i = tid; i < Lr * R; i += WW_THREADS) ring[i] = 0.f;
+  f32x4 wt[WW_TAPK], wx[WW_XK], wso[WW_SOK];
+  {
+    const f32x4* CW = a.conv_w + (long)(l * NC + c) * WW_CK * WW_THREADS + tid;
+#pragma unroll
+    for (int k = 0; k < WW_TAPK; ++k) wt[k] = CW[(long)k * WW_THREADS];
+#pragma unroll
+    for (int k = 0; k < WW_XK; ++k) wx[k] = CW[(long)(WW_TAPK + k) * WW_THREADS];
+    const f32x4* SW = a.so_w + (long)(l * NC + c) * WW_SOK * WW_THREADS + tid;
+#pragma unroll
+    for (int k = 0; k < WW_SOK; ++k) wso[k] = SW[(long)k * WW_THREADS];
+  }
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 cbias = ks == 0 ? reinterpret_cast<const f32x4*>(a.conv_b + (long)l * G + c * GC)[q] : zero4;
+  const f32x4 sob = (ks2 == 0 && c == 0) ? reinterpret_cast<const f32x4*>(a.so_b + (long)l * OUT)[q2] : zero4;
+  const int tap_r0 = ks * WW_TAPK, tap_blk = tap_r0 / R, tap_off = tap_r0 % R;  // blk 0: x(t-2d), 1: x(t-d)
+  const unsigned long long* gin = l > 0 ? a.gran + (long)(l - 1) * NG : sample_gran;
+  unsigned long long* gout = a.gran + (long)l * NG + c * OUT;
+  const float* condp = a.cond + ((long)a.b * a.T) * L * G + (long)l * G + c * GC;
+  const bool skip_scale = a.legacy && l > 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int p = 0;  // ring slot of x(t)
+  for (int t = 0; t < a.T; ++t) {
+    // ---- taps x(t-2d) | x(t-d) of this k-slice, conditioning and bias: before the input arrives ----
+    f32x4 acc = zero4;
+    {
+      const int slot = tap_blk == 0 ? (p + 1 == Lr ? 0 : p + 1) : (p >= d ? p - d : p - d + Lr);
+      const float* row = ring + (long)slot * R + tap_off;
+#pragma unroll
+      for (int i4 = 0; i4 < WW_TAPK / 4; ++i4) {
+        const f32x4 xv = ww_ld4(row, i4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ww_fma4(acc, xv[e], wt[4 * i4 + e]);
+      }
+      if (ks == 0) {
+        const f32x4 cd = reinterpret_cast<const f32x4*>(condp + (long)t * L * G)[q];
+        for (int e = 0; e < 4; ++e) acc[e] += cbias[e] + cd[e];
+      }
+    }
+    // ---- input x(t) (and the running skip sum) ----
+    if (l == 0) {
+      if (wave == 0) {  // first_conv 1x1 of the previous sample (wavenet.py:822-826); y_{-1} = 0
+        float y = 0.f;
+        bool ok = true;
+        if (t > 0)
+          ok = ww_spin(a.status, lane, [&] {
+            const unsigned long long x = ww_get(sample_gran);
+            y = __uint_as_float((unsigned)x);
+            return (unsigned)(x >> 32) == (unsigned)t;
+          });
+        if (!ok && lane == 0) flag[0] = 1;
+        for (int j = lane; j < R; j += 64) xin[j] = y * a.first_w[j] + a.first_b[j];
+      }
+    } else {
+      constexpr int NR = (OUT + WW_THREADS - 1) / WW_THREADS;
+      float v[NR][NC];
+      const bool ok = ww_spin(a.status, lane, [&] {
+        bool good = true;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int j = tid + r * WW_THREADS;
+#pragma unroll
+          for (int cc = 0; cc < NC; ++cc) {
+            const unsigned long long x = ww_get(gin + cc * OUT + j);
+            v[r][cc] = __uint_as_float((unsigned)x);
+            good = good && (unsigned)(x >> 32) == (unsigned)(t + 1);
+          }
+        }
+        return good;
+      });
+      if (!ok) flag[0] = 1;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int j = tid + r * WW_THREADS;  // [skip S | out R] column
+        float s = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc) s += v[r][cc];
+        if (j < S) skin[j] = s;
+        else xin[j - S] = s;
+      }
+    }
+    __syncthreads();
+    if (flag[0]) return;
+    for (int j = tid; j < R; j += WW_THREADS) ring[(long)p * R + j] = xin[j];  // queue append (modules.py:285-288)
+    // ---- x(t) rows of the dilated conv (modules.py:291-297), gated activation (:494-510) ----
+    {
+      const f32x4* xv4 = reinterpret_cast<const f32x4*>(xin + ks * WW_XK);
+#pragma unroll
+      for (int i4 = 0; i4 < WW_XK / 4; ++i4) {
+        const f32x4 xv = xv4[i4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ww_fma4(acc, xv[e], wx[4 * i4 + e]);
+      }
+    }
+    ww_reduce<NKS>(acc);
+    if (ks == 0) {
+      float2 zz;
+      zz.x = tanhf(acc[0]) * sigm(acc[2]);
+      zz.y = tanhf(acc[1]) * sigm(acc[3]);
+      reinterpret_cast<float2*>(z)[q] = zz;
+    }
+    __syncthreads();
+    // ---- skip / out 1x1 partials of this z slice (modules.py:512-520), published ----
+    {
+      f32x4 acc2 = zero4;
+      const f32x4* zv4 = reinterpret_cast<const f32x4*>(z + ks2 * WW_SOK);
+#pragma unroll
+      for (int i4 = 0; i4 < WW_SOK / 4; ++i4) {
+        const f32x4 zv = zv4[i4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ww_fma4(acc2, zv[e], wso[4 * i4 + e]);
+      }
+      ww_reduce<NKS2>(acc2);
+      if (ks2 == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = 4 * q2 + e;
+          float v = acc2[e];
+          if (col < S) {  // skips (wavenet.py:833-836)
+            if (c == 0) v += sob[e] + (l > 0 ? skin[col] : 0.f);
+            if (skip_scale) v *= SQH;
+          } else {        // residual output
+            if (c == 0) v += sob[e] + xin[col - S];
+            if (a.res_legacy) v *= SQH;
+          }
+          ww_put(gout + col, (unsigned)(t + 1), v);
+        }
+      }
+    }
+    p = p + 1 == Lr ? 0 : p + 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the queue append drained before its reads
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------------------------- host side
+
+static inline int gate_col_w(int R, int q, int e) { return (e < 2 ? 2 * q + e : R + 2 * q + (e - 2)); }
+
+void ww_pack_conv(const float* conv, int R, int c, std::vector<float>& out) {
+  const int NC = ww_nc(R), ZC = R / NC, GC = 2 * ZC, NQ = GC / 4, NKS = WW_THREADS / NQ, G = 2 * R;
+  const size_t base = out.size();
+  out.resize(base + (size_t)WW_CK * WW_THREADS * 4);
+  for (int tid = 0; tid < WW_THREADS; ++tid) {
+    const int q = tid / NKS, ks = tid % NKS;
+    const int gq = c * NQ + q;  // global gate-permuted quad
+    for (int kk = 0; kk < WW_CK; ++kk) {
+      // rows of the linearised [3R, G] kernel (taps oldest first): tap rows 32ks.. of [x(t-2d) | x(t-d)],
+      // then x(t) rows 2R + 16ks..
+      const int row = kk < WW_TAPK ? ks * WW_TAPK + kk : 2 * R + ks * WW_XK + (kk - WW_TAPK);
+      for (int e = 0; e < 4; ++e)
+        out[base + ((size_t)kk * WW_THREADS + tid) * 4 + e] = conv[(size_t)row * G + gate_col_w(R, gq, e)];
+    }
+  }
+}
+
+void ww_pack_so(const float* skip, const float* outk, int R, int c, std::vector<float>& out) {
+  const int NC = ww_nc(R), ZC = R / NC, S = R, OUT = S + R, NQ2 = OUT / 4, NKS2 = WW_THREADS / NQ2;
+  (void)NQ2;
+  const size_t base = out.size();
+  out.resize(base + (size_t)WW_SOK * WW_THREADS * 4);
+  for (int tid = 0; tid < WW_THREADS; ++tid) {
+    const int q2 = tid / NKS2, ks2 = tid % NKS2;
+    for (int kk = 0; kk < WW_SOK; ++kk) {
+      const int zrow = c * ZC + ks2 * WW_SOK + kk;
+      for (int e = 0; e < 4; ++e) {
+        const int col = 4 * q2 + e;
+        out[base + ((size_t)kk * WW_THREADS + tid) * 4 + e] =
+            col < S ? skip[(size_t)zrow * S + col] : outk[(size_t)zrow * R + (col - S)];
+      }
+    }
+  }
+}
+
+size_t ww_ring_floats(int R, int L, int per) {
+  size_t n = 0;
+  for (int l = 0; l < L; ++l) n += (size_t)ww_nc(R) * (2 * (1 << (l % per)) + 1) * R;
+  return n;
+}
+
+size_t ww_lds_bytes(int R, int C) {
+  (void)C;
+  const int S = R;
+  return sizeof(float) * (size_t)(16 + 2 * S + 32 + 32 + S * 32 + 32 * 32 + 64);
+}
+
+int ww_blocks(int R, int L) { return L * ww_nc(R) + 1; }
+
+const void* ww_kernel(int R, bool gauss) {
+  if (R == 128) return gauss ? reinterpret_cast<const void*>(k_generate_wide<128, true>)
+                             : reinterpret_cast<const void*>(k_generate_wide<128, false>);
+  return gauss ? reinterpret_cast<const void*>(k_generate_wide<256, true>)
+               : reinterpret_cast<const void*>(k_generate_wide<256, false>);
+}
+
+}  // namespace tt2
