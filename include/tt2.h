@@ -360,6 +360,17 @@ typedef struct tt2_train_config {
   int postnet;             /* 1: also the Postnet (training-mode BN + dropout) and the after loss */
   int postnet_layers, postnet_channels, postnet_kernel;  /* 5, 512, 5 */
   float bn_momentum, bn_eps;                               /* 0.99, 1e-3 (tf.layers defaults) */
+  /* front end (frontend = 1): the step starts from character ids + reference mels
+   * (tt2_train_forward_backward_text_dev) and also trains the encoder (embedding, 3x conv + BN +
+   * ReLU + dropout, bidirectional Zoneout-LSTM), both reference encoders (6x conv2d + BN + ReLU,
+   * GRU, dense tanh) and both GST attentions (tacotron.py:215-308, modules.py:9-64,251-323,
+   * multihead_attention.py:35-132); memory_dim = 2*encoder_lstm_units + (emt_only ? 1 : 2) *
+   * style_embed_depth */
+  int frontend;
+  int n_symbols, embedding_dim, enc_conv_layers, enc_conv_kernel, enc_conv_channels, encoder_lstm_units;
+  int emt_only, num_gst, num_heads, style_embed_depth, style_att_dim, reference_depth;
+  int reference_filters[6];
+  int max_T_ref;                                           /* reference mel frames (capacity) */
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;
@@ -387,6 +398,23 @@ tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* ctx, const float* memor
                                           const uint8_t* zoneout_masks_d,
                                           const uint8_t* postnet_masks_d, int T_in, int T_out,
                                           void* stream);
+/* The whole configs[4] step on a frontend context: ids [B,T_in] int32 (pad 0) and lengths [B],
+ * reference mels ref_emt / ref_spk [B,T_ref,80] (ref_spk NULL when emt_only) -> front end in
+ * training mode -> memory -> the decoder + Postnet step above -> backward through everything.
+ * enc_conv_masks [enc_conv_layers,B,T_in,enc_conv_channels] u8 dropout keep bits (rate 0.5) or NULL
+ * (no dropout); enc_zoneout_masks [T_in,2 (fw,bw),2 (c,h),B,encoder_lstm_units] u8 zoneout keep bits
+ * by recurrence step or NULL (inference mix).  Replaces Tacotron.initialize(is_training=True) +
+ * add_loss + the gradient half of add_optimizer (tacotron.py:31-35, 683-1109). */
+tt2_status tt2_train_forward_backward_text_dev(tt2_train_ctx* ctx, const int32_t* ids_d,
+                                               const int32_t* lengths_d, const float* ref_emt_d,
+                                               const float* ref_spk_d, int T_ref,
+                                               const float* targets_d, const float* stop_targets_d,
+                                               const uint8_t* prenet_masks_d,
+                                               const uint8_t* zoneout_masks_d,
+                                               const uint8_t* postnet_masks_d,
+                                               const uint8_t* enc_conv_masks_d,
+                                               const uint8_t* enc_zoneout_masks_d, int T_in, int T_out,
+                                               void* stream);
 /* clip_by_global_norm + Adam with learning rate lr at update count global_step (>= 1). */
 tt2_status tt2_train_apply_dev(tt2_train_ctx* ctx, float lr, int global_step, void* stream);
 /* Synchronise; out5 = {before_loss, stop_loss, reg_loss, grad_global_norm (after apply),
@@ -394,7 +422,9 @@ tt2_status tt2_train_apply_dev(tt2_train_ctx* ctx, float lr, int global_step, vo
  * forward_backward.  apply also runs the Postnet BN moving-average updates. */
 tt2_status tt2_train_losses(tt2_train_ctx* ctx, float* out5, float* fb_ms);
 /* which: 0 = parameter, 1 = gradient, 2 = Adam m, 3 = Adam v; name "memory" (which ignored) =
- * d loss / d memory [B,T_in,D] of the last forward_backward. */
+ * d loss / d memory [B,T_in,D] of the last forward_backward; on a frontend context also
+ * "frontend:memory" = the memory the front end produced [B,T_in,D] and "frontend:refnet_emt" /
+ * "frontend:refnet_spk" = the reference embeddings [B,128] (diagnostic read-backs). */
 tt2_status tt2_train_get_tensor(tt2_train_ctx* ctx, const char* tf_name, int which, float* host);
 /* Last forward's decoder frames [B,T,80], stop logits [B,T], alignments [B,T_in,T] (nullable). */
 tt2_status tt2_train_outputs(tt2_train_ctx* ctx, float* frames, float* stop_logits,

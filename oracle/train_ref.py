@@ -15,7 +15,8 @@ losses ``before`` (MSE, mask_decoder=False: tacotron.py:774) + stop sigmoid cros
 gradients → tower mean + clip_by_global_norm(1.0) (tacotron.py:1194-1221) → TF AdamOptimizer
 (tacotron.py:1029) with the exponential learning-rate decay (tacotron.py:1227-1251;
 hparams.py:272-282).  The Postnet
-``after`` loss and the encoder backward are outside this slice.
+``after`` loss is ``postnet=True``; the front end (encoder, reference encoders, GST) in training
+mode is ``frontend_forward`` / ``train_grads_frontend``.
 
 Training-mode zoneout (modules.py:236-240): ``c = (1-z)·dropout(c_new - c_prev, 1-z) + c_prev``,
 i.e. ``c = c_prev + m·(c_new - c_prev)`` with keep bits m ~ Bernoulli(1-z) (injected).
@@ -174,6 +175,216 @@ def postnet_train(W, dec, masks, eps=1e-3, layers=5):
              + W[s + "batch_normalization/beta"])
         x = y if masks is None else y / 0.5 * masks[i - 1]
     return x @ W[PP + "kernel"] + W[PP + "bias"], stats
+
+
+# ---- front end: encoder + reference encoders + GST in training mode ----------
+
+EC = P + "encoder_convolutions/conv_layer_{}_encoder_convolutions/"
+EL = P + "encoder_LSTM/bidirectional_rnn/{}/lstm_cell/"
+RN = P + "refnet_{}/"
+MH = P + "Multihead-attention-{}/"
+
+
+def frontend_var_names(emt_only=False, conv_layers=3, ref_layers=6):
+    """Trainable front-end variables (tacotron.py:215-308, modules.py:9-64,251-323,
+    multihead_attention.py:35-132), in the library's flat-buffer order."""
+    names = [P + "inputs_embedding"]
+    for i in range(1, conv_layers + 1):
+        s = EC.format(i)
+        names += [s + "conv1d/kernel", s + "conv1d/bias", s + "batch_normalization/gamma",
+                  s + "batch_normalization/beta"]
+    for d in ("fw", "bw"):
+        names += [EL.format(d) + "kernel", EL.format(d) + "bias"]
+    for tag in (("emt",) if emt_only else ("emt", "spk")):
+        r = RN.format(tag)
+        for i in range(ref_layers):
+            s = r + "conv2d_{}/".format(i)
+            names += [s + "conv2d/kernel", s + "conv2d/bias", s + "batch_normalization/gamma",
+                      s + "batch_normalization/beta"]
+        names += [r + "rnn/gru_cell/gates/kernel", r + "rnn/gru_cell/gates/bias",
+                  r + "rnn/gru_cell/candidate/kernel", r + "rnn/gru_cell/candidate/bias",
+                  r + "dense/kernel", r + "dense/bias", P + "style_tokens_" + tag]
+        m = MH.format(tag)
+        names += [m + "conv1d/kernel", m + "conv1d/bias", m + "conv1d_1/kernel", m + "conv1d_1/bias",
+                  m + "attention_v", m + "attention_g", m + "attention_b"]
+    return names
+
+
+def _bn_train(a, gamma, beta, dims, eps=1e-3, moving=None):
+    """tf.layers.batch_normalization(training=True): batch statistics over ``dims`` (biased);
+    ``moving`` = (moving_mean, moving_variance) evaluates it in inference mode instead."""
+    if moving is not None:
+        mean, var = moving
+    else:
+        mean = a.mean(dim=dims)
+        var = ((a - mean) ** 2).mean(dim=dims)
+    return gamma * (a - mean) / torch.sqrt(var + eps) + beta, (mean, var)
+
+
+def _conv2d_same_s2(x, k, b):
+    """tf.layers.conv2d 3x3 stride 2 padding='same' NHWC (odd pad bottom/right)."""
+    N, H, Wd, C = x.shape
+    outs = []
+    pads = []
+    for n, kk in ((H, k.shape[0]), (Wd, k.shape[1])):
+        o = -(-n // 2)
+        tot = max((o - 1) * 2 + kk - n, 0)
+        pads.append((tot // 2, tot - tot // 2))
+    xp = torch.nn.functional.pad(x, (0, 0, pads[1][0], pads[1][1], pads[0][0], pads[0][1]))
+    Ho, Wo = -(-H // 2), -(-Wd // 2)
+    cols = []
+    for i in range(k.shape[0]):
+        for j in range(k.shape[1]):
+            cols.append(xp[:, i:i + (Ho - 1) * 2 + 1:2, j:j + (Wo - 1) * 2 + 1:2, :])
+    cols = torch.cat(cols, -1)
+    return cols @ k.reshape(-1, k.shape[3]) + b
+
+
+def _lstm_dir(x, lengths, k, b, masks, reverse):
+    """One direction of bidirectional_dynamic_rnn (modules.py:315-321) with training zoneout:
+    c = c_prev + m_c·(c_new - c_prev), h likewise (modules.py:236-240), emitted output h_new; past a
+    row's length output 0 and state copied; the backward direction runs on the length-reversed
+    sequence.  masks [T, 2 (c, h), B, U] keep bits by recurrence step, or None (inference mix)."""
+    B, T, _ = x.shape
+    U = b.shape[0] // 4
+    dt = x.dtype
+    c = h = torch.zeros(B, U, dtype=dt)
+    lens = torch.as_tensor(np.asarray(lengths))
+    out = [None] * T
+    for t in range(T):
+        act = (t < lens)[:, None].to(dt)
+        if reverse:
+            pos = torch.clamp(lens - 1 - t, min=0)
+            xt = x[torch.arange(B), pos]
+        else:
+            xt = x[:, t]
+        z = torch.cat([xt, h], 1) @ k + b
+        i, j, f, o = z.chunk(4, 1)
+        cn = torch.sigmoid(f + 1.0) * c + torch.sigmoid(i) * torch.tanh(j)
+        hn = torch.sigmoid(o) * torch.tanh(cn)
+        if masks is None:
+            c2, h2 = 0.9 * cn + 0.1 * c, 0.9 * hn + 0.1 * h
+        else:
+            c2, h2 = c + masks[t, 0] * (cn - c), h + masks[t, 1] * (hn - h)
+        out[t] = hn * act
+        c = act * c2 + (1 - act) * c
+        h = act * h2 + (1 - act) * h
+    o = torch.stack(out, 1)                                   # step-major
+    if not reverse:
+        return o
+    rows = []
+    for bi in range(B):                                       # back to position order
+        L = int(lens[bi])
+        rows.append(torch.cat([o[bi, :L].flip(0), o[bi, L:]], 0))
+    return torch.stack(rows, 0)
+
+
+def _gru_last(x, W, r):
+    kg, bg = W[r + "rnn/gru_cell/gates/kernel"], W[r + "rnn/gru_cell/gates/bias"]
+    kc, bc = W[r + "rnn/gru_cell/candidate/kernel"], W[r + "rnn/gru_cell/candidate/bias"]
+    N, T2, _ = x.shape
+    D = bc.shape[0]
+    h = torch.zeros(N, D, dtype=x.dtype)
+    for t in range(T2):
+        v = torch.sigmoid(torch.cat([x[:, t], h], 1) @ kg + bg)
+        rr, u = v[:, :D], v[:, D:]
+        cc = torch.tanh(torch.cat([x[:, t], rr * h], 1) @ kc + bc)
+        h = u * h + (1 - u) * cc
+    return h
+
+
+def _gst(ref, W, tag, heads=4):
+    m = MH.format(tag)
+    tok = torch.tanh(W[P + "style_tokens_" + tag])              # [10, 64]
+    q = ref @ W[m + "conv1d/kernel"][0] + W[m + "conv1d/bias"]
+    kk = tok @ W[m + "conv1d_1/kernel"][0] + W[m + "conv1d_1/bias"]
+    N, A = q.shape
+    d = A // heads
+    v, g, bb = W[m + "attention_v"], W[m + "attention_g"], W[m + "attention_b"]
+    nv = g * v / torch.sqrt((v ** 2).sum())
+    qs = q.reshape(N, heads, 1, d)
+    ks = kk.reshape(1, -1, heads, d).permute(0, 2, 1, 3)
+    s = (nv * torch.tanh(ks + qs + bb)).sum(-1)                   # [N, H, 10]
+    w = torch.softmax(s, -1)
+    return (w @ tok).reshape(N, -1)
+
+
+def frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks=None, enc_zm=None, emt_only=False,
+                     eps=1e-3, moving=None):
+    """Training-mode front end -> memory [B,T_in,D] (unmasked: the decoder masks it) and the batch
+    statistics [(mean, var)] of every batch norm (encoder convs, then refnet convs).
+    enc_masks [3, B, T_in, C] conv dropout keep bits (rate 0.5) or None; enc_zm [T_in, 2 (fw, bw),
+    2 (c, h), B, U] LSTM zoneout keep bits or None.  ``moving`` (dict name -> array) evaluates the
+    batch norms with the moving statistics: with no masks that is the inference graph, pinned to
+    oracle/tacotron_ref.py (tests/test_train.py)."""
+    def mv(scope):
+        if moving is None:
+            return None
+        return tuple(torch.as_tensor(np.asarray(moving[scope + "batch_normalization/" + n]), dtype=dt)
+                     for n in ("moving_mean", "moving_variance"))
+    dt = W[P + "inputs_embedding"].dtype
+    x = W[P + "inputs_embedding"][torch.as_tensor(np.asarray(ids)).long()]
+    stats = []
+    for i in range(1, 4):                        # modules.py:485-497, bnorm 'after': conv->relu->BN->dropout
+        s = EC.format(i)
+        k = W[s + "conv1d/kernel"]
+        kw = k.shape[0]
+        pad = (kw - 1) // 2
+        xp = torch.nn.functional.pad(x, (0, 0, pad, kw - 1 - pad))
+        a = torch.relu(torch.einsum("btck,kcn->btn", xp.unfold(1, kw, 1), k) + W[s + "conv1d/bias"])
+        y, st = _bn_train(a, W[s + "batch_normalization/gamma"], W[s + "batch_normalization/beta"],
+                          (0, 1), eps, mv(s))
+        stats.append(st)
+        x = y if enc_masks is None else y / 0.5 * torch.as_tensor(np.asarray(enc_masks[i - 1]), dtype=dt)
+    zm = None if enc_zm is None else torch.as_tensor(np.asarray(enc_zm), dtype=dt)
+    fw = _lstm_dir(x, lengths, W[EL.format("fw") + "kernel"], W[EL.format("fw") + "bias"],
+                   None if zm is None else zm[:, 0], False)
+    bw = _lstm_dir(x, lengths, W[EL.format("bw") + "kernel"], W[EL.format("bw") + "bias"],
+                   None if zm is None else zm[:, 1], True)
+    parts = [fw, bw]
+    B, T = x.shape[:2]
+    for tag, ref in (("emt", ref_emt),) + ((() if emt_only else (("spk", ref_spk),))):
+        r = RN.format(tag)
+        h = torch.as_tensor(np.asarray(ref), dtype=dt)[..., None]
+        for i in range(6):                       # conv2d(): conv -> BN (training) -> ReLU
+            s = r + "conv2d_{}/".format(i)
+            a = _conv2d_same_s2(h, W[s + "conv2d/kernel"], W[s + "conv2d/bias"])
+            y, st = _bn_train(a, W[s + "batch_normalization/gamma"],
+                              W[s + "batch_normalization/beta"], (0, 1, 2), eps, mv(s))
+            stats.append(st)
+            h = torch.relu(y)
+        N, T2, F2, C = h.shape
+        hl = _gru_last(h.reshape(N, T2, F2 * C), W, r)
+        refo = torch.tanh(hl @ W[r + "dense/kernel"] + W[r + "dense/bias"])
+        style = _gst(refo, W, tag)
+        parts.append(style[:, None, :].expand(B, T, style.shape[1]))
+    return torch.cat(parts, -1), stats
+
+
+def train_grads_frontend(Wnp, ids, lengths, ref_emt, ref_spk, targets, stop_targets, prenet_masks,
+                         zoneout_masks, enc_masks, enc_zm, reg_weight=1e-6, dtype=torch.float64,
+                         clip=(-4.1, 4.0), postnet_masks=None, emt_only=False):
+    """The whole configs[4] step: front end (training mode) -> memory -> decoder + Postnet; returns
+    (losses, grads of every front-end, decoder and Postnet variable, [(mean, var)] batch stats of
+    the front end's batch norms)."""
+    names = frontend_var_names(emt_only) + train_var_names() + postnet_var_names()
+    W = {n: torch.tensor(np.asarray(Wnp[n]), dtype=dtype, requires_grad=True) for n in names}
+    mem, stats = frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks, enc_zm, emt_only)
+    tg = torch.tensor(np.asarray(targets), dtype=dtype)
+    st = torch.tensor(np.asarray(stop_targets), dtype=dtype)
+    pm = torch.tensor(np.asarray(prenet_masks), dtype=dtype)
+    zm = None if zoneout_masks is None else torch.tensor(np.asarray(zoneout_masks), dtype=dtype)
+    fr, sl, al = forward(W, mem, lengths, tg, pm, zm)
+    b, s, r = losses(fr, sl, tg, st, W, reg_weight, clip)
+    dec = clip_decoder_output(fr, clip)
+    pmk = None if postnet_masks is None else torch.tensor(np.asarray(postnet_masks), dtype=dtype)
+    proj, _ = postnet_train(W, dec, pmk)
+    mel = clip_decoder_output(dec + proj, clip)
+    after = ((mel - tg) ** 2).mean()
+    (b + s + r + after).backward()
+    g = {n: W[n].grad.numpy() for n in names}
+    return (b.item(), s.item(), r.item(), after.item()), g, \
+        [(m.detach().numpy(), v.detach().numpy()) for m, v in stats]
 
 
 def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,

@@ -20,9 +20,11 @@
 // of the step-t inputs, so a step's carry-ins are read from slot t+1.
 #include <cmath>
 #include <cstring>
+#include <functional>
 
 #include "common.h"
 #include "gemm.h"
+#include "train_front.h"
 
 namespace tt2 {
 
@@ -73,6 +75,14 @@ struct tt2_train_ctx {
   hipStream_t last_stream = nullptr;  // stream of the last forward_backward / apply (read-backs)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
+  // front end (cfg.frontend: encoder + reference encoders + GST, train_front.hip)
+  int f_nref = 0, f_gin = 0, f_T2 = 0, f_T2max = 0;
+  bool f_ran = false;
+  DevBuf fEX, fEA[8], fEY[9], fXP, fGZ, fGA, fCN, fCS, fHS, fENC, fMEM, fSTY, fDSTY, fDZ, fDHC, fDCC, fDHP, fdXP, fdA,
+      fdB, fLWxT, fLWhT;
+  DevBuf fRA[2][6], fRY[2][6], fXG[2], fGR[2], fGU[2], fGCC[2], fGRH[2], fHG[2], fREF[2], fGG, fGC, fFBUF, fDY, fDY2,
+      fDZc;
+  DevBuf fGq, fGkk, fGv, fGnv, fGbb, fGsum, fdREF, fDZD, fDH, fDHA, fDRH, fDCP, fDGP, fDXG, fWT, fBN, fpart;
 };
 
 namespace tt2 {
@@ -829,7 +839,8 @@ __global__ void k_pn_bn_bwd_dz(const float* __restrict__ dy, const float* __rest
   const float xh = (av - mean[c]) * rs;
   const float inv_m = 1.0f / (float)M;
   float g = gamma[c] * rs * (dy[i] - sums[c] * inv_m - xh * sums[C + c] * inv_m);
-  if (tanh_act) g *= 1.f - av * av;
+  if (tanh_act == 1) g *= 1.f - av * av;        // tanh (Postnet)
+  else if (tanh_act == 2) g *= av > 0.f ? 1.f : 0.f;  // ReLU (encoder convolutions): av = relu output
   dz[i] = g;
 }
 // im2col^T of a conv1d input x(b, t, c) = x[b*xs_b + t*xs_t + c]:
@@ -969,6 +980,9 @@ static std::string vn(const char* s) { return std::string(TP) + s; }
 #define SPV(x) vn("decoder/stop_token_projection/projection_stop_token_projection/" x)
 #define PRV(i, x) vn((std::string("decoder/decoder_prenet/dense_") + std::to_string(i) + "/" x).c_str())
 
+static void tr_front_build_vars(tt2_train_ctx* c,
+                                const std::function<void(const std::string&, std::vector<int64_t>, bool)>& add);
+
 static void tr_build_vars(tt2_train_ctx* c) {
   const int D = c->D, A = c->A, F = c->F, KW = c->KW, P = c->P, H = c->H, NM = c->NM;
   auto add = [&](const std::string& n, std::vector<int64_t> sh, bool reg) {
@@ -1003,6 +1017,7 @@ static void tr_build_vars(tt2_train_ctx* c) {
   add(FPV("bias"), {NM}, false);
   add(SPV("kernel"), {H + D, 1}, false);
   add(SPV("bias"), {1}, false);
+  if (c->cfg.frontend) tr_front_build_vars(c, add);
   if (!c->cfg.postnet) return;
   // Postnet (oracle/train_ref.py postnet_var_names / postnet_stat_names); moving statistics are
   // non-trainable slots of the same table (zero gradient -> Adam leaves them alone)
@@ -1023,6 +1038,8 @@ static void tr_build_vars(tt2_train_ctx* c) {
 static std::string pn_scope(int i) {
   return vn("postnet_convolutions/conv_layer_") + std::to_string(i) + "_postnet_convolutions/";
 }
+
+static void tr_front_alloc(tt2_train_ctx* c);
 
 static void tr_alloc(tt2_train_ctx* c) {
   const long B = c->B, T = c->Tm, Tin = c->Tin, D = c->D, H = c->H, P = c->P, A = c->A, F = c->F, KW = c->KW,
@@ -1060,6 +1077,7 @@ static void tr_alloc(tt2_train_ctx* c) {
     h(c->hWq, H * A); h(c->hWqT, H * A);
   }
   f(c->kpart, 4L << 20);
+  if (c->cfg.frontend) tr_front_alloc(c);
   if (c->cfg.postnet) {
     const long PC = c->PC, PK = c->PK;
     for (int i = 0; i < c->PL; ++i) f(c->PA[i], TB * PC);
@@ -1361,7 +1379,12 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
           c->DVAL.as<float>(), D);
   hipLaunchKernelGGL(k_tr_mask_rows, dim3(nblk((long)B * Tin * D)), dim3(256), 0, s, c->DVAL.as<float>(), lens, B, Tin,
                      D, c->DMEM.as<float>());
-  // L2 regularisation of the regularised kernels
+  g_tr_kpart = nullptr;
+  g_tr_prec = 0;
+}
+
+// L2 regularisation of the regularised kernels (after every gradient of the step has landed)
+static void tr_regularize(tt2_train_ctx* c, hipStream_t s) {
   int nreg = 0;
   for (const auto& v : c->vars) {
     if (!v.reg) continue;
@@ -1370,10 +1393,448 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     ++nreg;
   }
   hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 64 * nreg, c->cfg.reg_weight,
-                     red + 2, 0);
-  g_tr_kpart = nullptr;
-  g_tr_prec = 0;
+                     c->red.as<float>() + 2, 0);
 }
+
+// ---- front end (cfg.frontend): encoder, reference encoders, GST in training mode -------------------
+// The step starts from ids / reference mels: forward builds the memory the decoder slice consumes
+// (tacotron.py:215-308), backward continues from the decoder's d memory (DMEM) into every front-end
+// variable (train_front.hip kernels + gemm.hip products).
+static std::string fe_conv_scope(int i) {
+  return vn("encoder_convolutions/conv_layer_") + std::to_string(i) + "_encoder_convolutions/";
+}
+static std::string fe_ref_scope(int r) { return vn(r == 0 ? "refnet_emt/" : "refnet_spk/"); }
+static std::string fe_mh_scope(int r) { return vn(r == 0 ? "Multihead-attention-emt/" : "Multihead-attention-spk/"); }
+static std::string fe_lstm_scope(int d) {
+  return vn(d == 0 ? "encoder_LSTM/bidirectional_rnn/fw/lstm_cell/" : "encoder_LSTM/bidirectional_rnn/bw/lstm_cell/");
+}
+static bool fe_regularized(const std::string& n) {  // tacotron.py:865-867 (oracle/train_ref.py regularized)
+  return !(n.find("bias") != std::string::npos || n.find("Bias") != std::string::npos ||
+           n.find("_projection") != std::string::npos || n.find("inputs_embedding") != std::string::npos ||
+           n.find("RNN") != std::string::npos || n.find("LSTM") != std::string::npos);
+}
+
+static void tr_front_build_vars(tt2_train_ctx* c, const std::function<void(const std::string&, std::vector<int64_t>, bool)>& add) {
+  const auto& f = c->cfg;
+  const int E = f.embedding_dim, C = f.enc_conv_channels, K = f.enc_conv_kernel, U = f.encoder_lstm_units;
+  auto addr = [&](const std::string& n, std::vector<int64_t> sh) { add(n, sh, fe_regularized(n)); };
+  addr(vn("inputs_embedding"), {f.n_symbols, E});
+  for (int i = 1; i <= f.enc_conv_layers; ++i) {
+    const std::string s = fe_conv_scope(i);
+    addr(s + "conv1d/kernel", {K, i == 1 ? E : C, C});
+    addr(s + "conv1d/bias", {C});
+    addr(s + "batch_normalization/gamma", {C});
+    addr(s + "batch_normalization/beta", {C});
+    add(s + "batch_normalization/moving_mean", {C}, false);
+    add(s + "batch_normalization/moving_variance", {C}, false);
+  }
+  for (int d = 0; d < 2; ++d) {
+    addr(fe_lstm_scope(d) + "kernel", {C + U, 4 * U});
+    addr(fe_lstm_scope(d) + "bias", {4 * U});
+  }
+  const int RD = f.reference_depth, tokd = f.style_embed_depth / f.num_heads, A = f.style_att_dim, dh = A / f.num_heads;
+  for (int r = 0; r < c->f_nref; ++r) {
+    const std::string rs = fe_ref_scope(r);
+    int ci = 1;
+    for (int i = 0; i < 6; ++i) {
+      const std::string s = rs + "conv2d_" + std::to_string(i) + "/";
+      addr(s + "conv2d/kernel", {3, 3, ci, f.reference_filters[i]});
+      addr(s + "conv2d/bias", {f.reference_filters[i]});
+      addr(s + "batch_normalization/gamma", {f.reference_filters[i]});
+      addr(s + "batch_normalization/beta", {f.reference_filters[i]});
+      add(s + "batch_normalization/moving_mean", {f.reference_filters[i]}, false);
+      add(s + "batch_normalization/moving_variance", {f.reference_filters[i]}, false);
+      ci = f.reference_filters[i];
+    }
+    addr(rs + "rnn/gru_cell/gates/kernel", {c->f_gin + RD, 2 * RD});
+    addr(rs + "rnn/gru_cell/gates/bias", {2 * RD});
+    addr(rs + "rnn/gru_cell/candidate/kernel", {c->f_gin + RD, RD});
+    addr(rs + "rnn/gru_cell/candidate/bias", {RD});
+    addr(rs + "dense/kernel", {RD, 128});
+    addr(rs + "dense/bias", {128});
+    addr(vn(r == 0 ? "style_tokens_emt" : "style_tokens_spk"), {f.num_gst, tokd});
+    const std::string m = fe_mh_scope(r);
+    addr(m + "conv1d/kernel", {1, 128, A});
+    addr(m + "conv1d/bias", {A});
+    addr(m + "conv1d_1/kernel", {1, tokd, A});
+    addr(m + "conv1d_1/bias", {A});
+    addr(m + "attention_v", {dh});
+    addr(m + "attention_g", {});
+    addr(m + "attention_b", {dh});
+  }
+}
+
+static void tr_front_alloc(tt2_train_ctx* c) {
+  const auto& f = c->cfg;
+  const long B = c->B, T = c->Tin, C = f.enc_conv_channels, E = f.embedding_dim, U = f.encoder_lstm_units;
+  const long BT = B * T, K = f.enc_conv_kernel;
+  auto a = [](DevBuf& d, long n) { d.alloc(sizeof(float) * (size_t)std::max<long>(n, 1)); };
+  a(c->fEX, BT * E);
+  for (int i = 0; i < f.enc_conv_layers; ++i) {
+    a(c->fEA[i], BT * C);
+    a(c->fEY[i + 1], BT * C);
+  }
+  a(c->fXP, BT * 8 * U); a(c->fGZ, 2 * B * 4 * U); a(c->fGA, 2 * T * B * 4 * U); a(c->fCN, 2 * T * B * U);
+  a(c->fCS, 2 * (T + 1) * B * U); a(c->fHS, 2 * (T + 1) * B * U); a(c->fENC, BT * 2 * U);
+  a(c->fMEM, BT * c->D); a(c->fSTY, B * (c->D - 2 * U)); a(c->fDSTY, B * (c->D - 2 * U));
+  a(c->fDZ, 2 * T * B * 4 * U); a(c->fDHC, 2 * B * U); a(c->fDCC, 2 * B * U); a(c->fDHP, 2 * B * U);
+  a(c->fdXP, BT * 8 * U); a(c->fdA, BT * std::max(C, E)); a(c->fdB, BT * std::max(C, E));
+  a(c->fLWxT, 2 * 4 * U * C); a(c->fLWhT, 2 * 4 * U * U);
+  // reference encoders at max_T_ref
+  const int RD = f.reference_depth, nm = c->NM;
+  long fbuf = BT * K * std::max(C, E);  // encoder im2col^T
+  long mmax = 1;
+  int H = f.max_T_ref, W = nm, ci = 1;
+  for (int i = 0; i < 6; ++i) {
+    const int Ho = (H + 1) / 2, Wo = (W + 1) / 2, fo = f.reference_filters[i];
+    const long M = B * Ho * Wo;
+    for (int r = 0; r < c->f_nref; ++r) {
+      a(c->fRA[r][i], M * fo);
+      a(c->fRY[r][i], M * fo);
+    }
+    fbuf = std::max(fbuf, 9L * ci * M);
+    mmax = std::max(mmax, std::max(M * fo, B * (long)H * W * ci));
+    H = Ho; W = Wo; ci = fo;
+  }
+  const long T2 = H;
+  c->f_T2max = (int)T2;
+  for (int r = 0; r < c->f_nref; ++r) {
+    a(c->fXG[r], B * T2 * 3 * RD); a(c->fGR[r], T2 * B * RD); a(c->fGU[r], T2 * B * RD); a(c->fGCC[r], T2 * B * RD);
+    a(c->fGRH[r], T2 * B * RD); a(c->fHG[r], (T2 + 1) * B * RD); a(c->fREF[r], B * 128);
+  }
+  a(c->fGG, B * 2 * RD); a(c->fGC, B * RD);
+  a(c->fFBUF, fbuf); a(c->fDY, mmax); a(c->fDY2, mmax); a(c->fDZc, mmax);
+  const int ntok = f.num_gst, tokd = f.style_embed_depth / f.num_heads, A = f.style_att_dim, dh = A / f.num_heads;
+  a(c->fGq, B * A); a(c->fGkk, B * ntok * A); a(c->fGv, B * ntok * tokd); a(c->fGnv, B * dh); a(c->fGbb, B * dh);
+  a(c->fGsum, ntok * A + ntok * tokd + 2 * dh);
+  a(c->fdREF, B * 128); a(c->fDZD, B * 128); a(c->fDH, B * RD); a(c->fDHA, B * RD); a(c->fDRH, B * RD);
+  a(c->fDCP, T2 * B * RD); a(c->fDGP, T2 * B * 2 * RD); a(c->fDXG, B * T2 * 3 * RD);
+  a(c->fWT, std::max<long>({9L * 128 * 128, 3L * RD * std::max<long>(c->f_gin, RD), 128L * RD, 128L * A, (long)K * C * C}));
+  a(c->fBN, 2L * (f.enc_conv_layers + 6 * c->f_nref) * 512);
+  a(c->fpart, 64L * 2 * 512 + 1024);
+}
+
+// batch statistics over M rows of [M][C] into mean / var (k_pn_colstat: biased variance)
+static void fe_stats(tt2_train_ctx* c, const float* x, long M, int C, float* mean, float* var, hipStream_t s) {
+  const int S = (int)std::min<long>(64, std::max<long>(1, M / 64));
+  float* part = c->fpart.as<float>();
+  hipLaunchKernelGGL(k_pn_colstat_part, dim3((C + 63) / 64, S), dim3(256), 0, s, x, M, C, nullptr, 0, part);
+  hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, mean);
+  hipLaunchKernelGGL(k_pn_colstat_part, dim3((C + 63) / 64, S), dim3(256), 0, s, x, M, C, mean, 1, part);
+  hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, var);
+}
+// BN backward (batch statistics) from dy -> dz (act: 0 none, 2 relu' from the pre-BN activation)
+static void fe_bn_bwd(tt2_train_ctx* c, const float* dxn, const uint8_t* keep, const float* a, long M, int C,
+                      const float* mean, const float* var, const std::string& sc, int act, float* dy, float* dz,
+                      hipStream_t s) {
+  const int S = (int)std::min<long>(64, std::max<long>(1, M / 64));
+  float* part = c->fpart.as<float>();
+  float* sums = part + 64L * 2 * 512;
+  const float eps = c->cfg.bn_eps;
+  hipLaunchKernelGGL(k_pn_bn_bwd_part, dim3((C + 63) / 64, S), dim3(256), 0, s, dxn, keep, a, M, C, mean, var, eps, dy,
+                     part);
+  hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, sums,
+                     gvar(c, sc + "batch_normalization/gamma"), gvar(c, sc + "batch_normalization/beta"));
+  hipLaunchKernelGGL(k_pn_bn_bwd_dz, dim3(nblk(M * C)), dim3(256), 0, s, dy, a, M, C, mean, var, eps,
+                     pvar(c, sc + "batch_normalization/gamma"), sums, act, dz);
+}
+
+static FeGst fe_gst_args(tt2_train_ctx* c, int r, int B) {
+  const auto& f = c->cfg;
+  const std::string m = fe_mh_scope(r);
+  FeGst g{};
+  g.ref = c->fREF[r].as<float>();
+  g.tokens = pvar(c, vn(r == 0 ? "style_tokens_emt" : "style_tokens_spk"));
+  g.wq = pvar(c, m + "conv1d/kernel"); g.bq = pvar(c, m + "conv1d/bias");
+  g.wk = pvar(c, m + "conv1d_1/kernel"); g.bk = pvar(c, m + "conv1d_1/bias");
+  g.v = pvar(c, m + "attention_v"); g.g = pvar(c, m + "attention_g"); g.bb = pvar(c, m + "attention_b");
+  g.N = B; g.ntok = f.num_gst; g.tokd = f.style_embed_depth / f.num_heads; g.A = f.style_att_dim; g.heads = f.num_heads;
+  g.refd = 128;
+  g.style = c->fSTY.as<float>(); g.style_ld = c->D - 2 * f.encoder_lstm_units; g.style_off = r * f.style_embed_depth;
+  g.dstyle = c->fDSTY.as<float>();
+  g.dq = c->fGq.as<float>(); g.pdkk = c->fGkk.as<float>(); g.pdv = c->fGv.as<float>(); g.pdnv = c->fGnv.as<float>();
+  g.pdbb = c->fGbb.as<float>();
+  return g;
+}
+
+static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, const float* const* refs, int T_ref,
+                             const uint8_t* encm, const uint8_t* enczm, int T, hipStream_t s) {
+  const auto& f = c->cfg;
+  const int B = c->B, E = f.embedding_dim, C = f.enc_conv_channels, K = f.enc_conv_kernel, U = f.encoder_lstm_units;
+  const long M = (long)B * T;
+  const float eps = f.bn_eps;
+  float* BN = c->fBN.as<float>();
+  fe_embed(ids, pvar(c, vn("inputs_embedding")), M, E, c->fEX.as<float>(), s);
+  // EncoderConvolutions (modules.py:251-280, conv1d() :485-497 with bnorm 'after'): conv -> ReLU ->
+  // BN (batch statistics over all B·T positions) -> dropout(0.5, keep bits)
+  for (int i = 0; i < f.enc_conv_layers; ++i) {
+    const std::string sc = fe_conv_scope(i + 1);
+    const int cin = i == 0 ? E : C;
+    GemmArgs g;
+    g.a_mode = A_CONV1D; g.M = (int)M; g.N = C; g.T = T; g.kw = K; g.pad = (K - 1) / 2; g.C = cin;
+    g.A = i == 0 ? c->fEX.as<float>() : c->fEY[i].as<float>(); g.xs_b = (long)T * cin; g.xs_t = cin; g.K = K * cin;
+    g.Bw = pvar(c, sc + "conv1d/kernel"); g.ldb = C; g.Cout = c->fEA[i].as<float>(); g.ldc = C;
+    g.bias = pvar(c, sc + "conv1d/bias"); g.act = ACT_RELU;
+    tr_gemm_run(g, s);
+    float* mean = BN + (long)i * 2 * 512;
+    float* var = mean + 512;
+    fe_stats(c, c->fEA[i].as<float>(), M, C, mean, var, s);
+    hipLaunchKernelGGL(k_pn_bn_fwd, dim3(nblk(M * C)), dim3(256), 0, s, c->fEA[i].as<float>(), M, C, mean, var,
+                       pvar(c, sc + "batch_normalization/gamma"), pvar(c, sc + "batch_normalization/beta"), eps,
+                       encm ? encm + (long)i * M * C : nullptr, c->fEY[i + 1].as<float>());
+  }
+  // EncoderRNN (modules.py:283-323): input projections of both directions for every position
+  const float* X = c->fEY[f.enc_conv_layers].as<float>();
+  for (int d = 0; d < 2; ++d)
+    tr_gemm((int)M, 4 * U, C, X, C, pvar(c, fe_lstm_scope(d) + "kernel"), 4 * U, c->fXP.as<float>() + d * 4 * U, 8 * U,
+            s, pvar(c, fe_lstm_scope(d) + "bias"));
+  TT2_HIP(hipMemsetAsync(c->fENC.p, 0, sizeof(float) * (size_t)M * 2 * U, s));
+  for (int d = 0; d < 2; ++d) {  // zero initial states
+    TT2_HIP(hipMemsetAsync(c->fCS.as<float>() + (long)d * (T + 1) * B * U, 0, sizeof(float) * (size_t)B * U, s));
+    TT2_HIP(hipMemsetAsync(c->fHS.as<float>() + (long)d * (T + 1) * B * U, 0, sizeof(float) * (size_t)B * U, s));
+  }
+  FeLstm l{};
+  l.XP = c->fXP.as<float>(); l.GZ = c->fGZ.as<float>(); l.GA = c->fGA.as<float>(); l.CN = c->fCN.as<float>();
+  l.CS = c->fCS.as<float>(); l.HS = c->fHS.as<float>(); l.ENC = c->fENC.as<float>(); l.zm = enczm; l.lens = lens;
+  l.B = B; l.T = T; l.U = U; l.zo = f.zoneout;
+  for (int t = 0; t < T; ++t) {
+    for (int d = 0; d < 2; ++d)
+      tr_gemm(B, 4 * U, U, c->fHS.as<float>() + ((long)d * (T + 1) + t) * B * U, U,
+              pvar(c, fe_lstm_scope(d) + "kernel") + (long)C * 4 * U, 4 * U, c->fGZ.as<float>() + (long)d * B * 4 * U,
+              4 * U, s);
+    l.t = t;
+    fe_lstm_cell(l, s);
+  }
+  // reference encoders (modules.py:9-64) + GST (tacotron.py:276-282)
+  const int RD = f.reference_depth;
+  int nbn = f.enc_conv_layers;
+  for (int r = 0; r < c->f_nref; ++r) {
+    const std::string rs = fe_ref_scope(r);
+    int H = T_ref, W = c->NM, ci = 1;
+    const float* x = refs[r];
+    for (int i = 0; i < 6; ++i, ++nbn) {
+      const std::string sc = rs + "conv2d_" + std::to_string(i) + "/";
+      const int fo = f.reference_filters[i], Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+      GemmArgs g;
+      g.M = B * Ho * Wo; g.N = fo; g.K = 9 * ci; g.a_mode = A_CONV2D; g.A = x;
+      g.H = H; g.Wd = W; g.C = ci; g.Ho = Ho; g.Wo = Wo; g.kh = 3; g.kw2 = 3; g.sh = 2; g.sw = 2;
+      g.pt = std::max((Ho - 1) * 2 + 3 - H, 0) / 2; g.pl = std::max((Wo - 1) * 2 + 3 - W, 0) / 2;
+      g.Bw = pvar(c, sc + "conv2d/kernel"); g.ldb = fo; g.Cout = c->fRA[r][i].as<float>(); g.ldc = fo;
+      g.bias = pvar(c, sc + "conv2d/bias");
+      tr_gemm_run(g, s);
+      float* mean = BN + (long)nbn * 2 * 512;
+      float* var = mean + 512;
+      fe_stats(c, c->fRA[r][i].as<float>(), g.M, fo, mean, var, s);
+      fe_bn_relu_fwd(c->fRA[r][i].as<float>(), g.M, fo, mean, var, pvar(c, sc + "batch_normalization/gamma"),
+                     pvar(c, sc + "batch_normalization/beta"), eps, c->fRY[r][i].as<float>(), s);
+      x = c->fRY[r][i].as<float>();
+      H = Ho; W = Wo; ci = fo;
+    }
+    const int T2 = H, gin = W * ci;
+    c->f_T2 = T2;
+    const float* kg = pvar(c, rs + "rnn/gru_cell/gates/kernel");
+    const float* kcn = pvar(c, rs + "rnn/gru_cell/candidate/kernel");
+    float* XG = c->fXG[r].as<float>();
+    tr_gemm(B * T2, 2 * RD, gin, x, gin, kg, 2 * RD, XG, 3 * RD, s, pvar(c, rs + "rnn/gru_cell/gates/bias"));
+    tr_gemm(B * T2, RD, gin, x, gin, kcn, RD, XG + 2 * RD, 3 * RD, s, pvar(c, rs + "rnn/gru_cell/candidate/bias"));
+    TT2_HIP(hipMemsetAsync(c->fHG[r].p, 0, sizeof(float) * (size_t)B * RD, s));
+    for (int t = 0; t < T2; ++t) {
+      float* h = c->fHG[r].as<float>() + (long)t * B * RD;
+      tr_gemm(B, 2 * RD, RD, h, RD, kg + (long)gin * 2 * RD, 2 * RD, c->fGG.as<float>(), 2 * RD, s);
+      fe_gru_a(XG, c->fGG.as<float>(), c->fHG[r].as<float>(), B, T2, RD, t, c->fGR[r].as<float>(),
+               c->fGU[r].as<float>(), c->fGRH[r].as<float>(), s);
+      tr_gemm(B, RD, RD, c->fGRH[r].as<float>() + (long)t * B * RD, RD, kcn + (long)gin * RD, RD, c->fGC.as<float>(), RD,
+              s);
+      fe_gru_b(XG, c->fGC.as<float>(), c->fGU[r].as<float>(), B, T2, RD, t, c->fGCC[r].as<float>(),
+               c->fHG[r].as<float>(), s);
+    }
+    tr_gemm(B, 128, RD, c->fHG[r].as<float>() + (long)T2 * B * RD, RD, pvar(c, rs + "dense/kernel"), 128,
+            c->fREF[r].as<float>(), 128, s, pvar(c, rs + "dense/bias"), nullptr, 0, ACT_TANH);
+    fe_gst_fwd(fe_gst_args(c, r, B), s);
+  }
+  fe_memory(c->fENC.as<float>(), c->fSTY.as<float>(), B, T, 2 * U, c->D - 2 * U, c->fMEM.as<float>(), s);
+  c->f_ran = true;
+}
+
+static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens, const float* const* refs, int T_ref,
+                              const uint8_t* encm, const uint8_t* enczm, int T, hipStream_t s) {
+  const auto& f = c->cfg;
+  const int B = c->B, E = f.embedding_dim, C = f.enc_conv_channels, K = f.enc_conv_kernel, U = f.encoder_lstm_units;
+  const int D = c->D, RD = f.reference_depth, SW = D - 2 * U;
+  const long M = (long)B * T;
+  float* BN = c->fBN.as<float>();
+  float* WT = c->fWT.as<float>();
+  float* FB = c->fFBUF.as<float>();
+  // memory assembly: style gradient = Σ_t over the (length-masked) d memory rows
+  fe_style_grad(c->DMEM.as<float>(), B, T, D, 2 * U, c->fDSTY.as<float>(), s);
+  for (int r = 0; r < c->f_nref; ++r) {
+    const std::string rs = fe_ref_scope(r), m = fe_mh_scope(r);
+    const FeGst ga = fe_gst_args(c, r, B);
+    fe_gst_bwd(ga, s);
+    const int ntok = ga.ntok, tokd = ga.tokd, A = ga.A, dh = A / ga.heads;
+    float* sum = c->fGsum.as<float>();
+    tr_colsum(c, ga.pdkk, B, ntok * A, (long)ntok * A, sum, s);
+    tr_colsum(c, ga.pdv, B, ntok * tokd, (long)ntok * tokd, sum + ntok * A, s);
+    tr_colsum(c, ga.pdnv, B, dh, dh, sum + ntok * A + ntok * tokd, s);
+    tr_colsum(c, ga.pdbb, B, dh, dh, sum + ntok * A + ntok * tokd + dh, s);
+    fe_gst_final(ga, sum, sum + ntok * A, sum + ntok * A + ntok * tokd, sum + ntok * A + ntok * tokd + dh,
+                 gvar(c, m + "conv1d_1/kernel"), gvar(c, m + "conv1d_1/bias"),
+                 gvar(c, vn(r == 0 ? "style_tokens_emt" : "style_tokens_spk")), gvar(c, m + "attention_v"),
+                 gvar(c, m + "attention_g"), gvar(c, m + "attention_b"), s);
+    // query conv1d (1x1): d Wq = refᵀ dq, d bq, d ref = dq Wqᵀ
+    tr_transpose(c->fREF[r].as<float>(), B, 128, 128, WT, B, s);
+    tr_gemm(128, A, B, WT, B, ga.dq, A, gvar(c, m + "conv1d/kernel"), A, s);
+    tr_colsum(c, ga.dq, B, A, A, gvar(c, m + "conv1d/bias"), s);
+    tr_transpose(pvar(c, m + "conv1d/kernel"), 128, A, A, WT, 128, s);
+    tr_gemm(B, 128, A, ga.dq, A, WT, 128, c->fdREF.as<float>(), 128, s);
+    // dense tanh (modules.py:63)
+    fe_tanh_bwd(c->fdREF.as<float>(), c->fREF[r].as<float>(), (long)B * 128, c->fDZD.as<float>(), s);
+    const int T2 = c->f_T2;
+    const float* hT = c->fHG[r].as<float>() + (long)T2 * B * RD;
+    tr_transpose(hT, B, RD, RD, WT, B, s);
+    tr_gemm(RD, 128, B, WT, B, c->fDZD.as<float>(), 128, gvar(c, rs + "dense/kernel"), 128, s);
+    tr_colsum(c, c->fDZD.as<float>(), B, 128, 128, gvar(c, rs + "dense/bias"), s);
+    tr_transpose(pvar(c, rs + "dense/kernel"), RD, 128, 128, WT, RD, s);
+    tr_gemm(B, RD, 128, c->fDZD.as<float>(), 128, WT, RD, c->fDH.as<float>(), RD, s);
+    // GRU BPTT (TF1 GRUCell): recurrent weight transposes once
+    const int gin = c->f_gin;
+    const float* kg = pvar(c, rs + "rnn/gru_cell/gates/kernel");
+    const float* kcn = pvar(c, rs + "rnn/gru_cell/candidate/kernel");
+    float* WghT = WT;                       // [2RD][RD]
+    float* WchT = WT + 2L * RD * RD;        // [RD][RD]
+    tr_transpose(kg + (long)gin * 2 * RD, RD, 2 * RD, 2 * RD, WghT, RD, s);
+    tr_transpose(kcn + (long)gin * RD, RD, RD, RD, WchT, RD, s);
+    for (int t = T2 - 1; t >= 0; --t) {
+      fe_gru_bwd_a(c->fDH.as<float>(), c->fGU[r].as<float>(), c->fGCC[r].as<float>(), c->fHG[r].as<float>(), B, RD, t,
+                   c->fDCP.as<float>(), c->fDHA.as<float>(), s);
+      tr_gemm(B, RD, RD, c->fDCP.as<float>() + (long)t * B * RD, RD, WchT, RD, c->fDRH.as<float>(), RD, s);
+      fe_gru_bwd_b(c->fDRH.as<float>(), c->fGR[r].as<float>(), c->fGU[r].as<float>(), c->fHG[r].as<float>(),
+                   c->fGCC[r].as<float>(), c->fDH.as<float>(), B, RD, t, c->fDGP.as<float>(), c->fDHA.as<float>(), s);
+      tr_gemm(B, RD, 2 * RD, c->fDGP.as<float>() + (long)t * B * 2 * RD, 2 * RD, WghT, RD, c->fDH.as<float>(), RD, s,
+              nullptr, c->fDHA.as<float>(), RD);
+    }
+    // recurrent weight gradients over all steps: d Wg_h = Σ h(t)ᵀ dGP(t), d Wc_h = Σ (r h)(t)ᵀ dCP(t)
+    const long R2 = (long)T2 * B;
+    tr_transpose(c->fHG[r].as<float>(), R2, RD, RD, FB, R2, s);
+    tr_gemm(RD, 2 * RD, (int)R2, FB, R2, c->fDGP.as<float>(), 2 * RD, gvar(c, rs + "rnn/gru_cell/gates/kernel") +
+            (long)gin * 2 * RD, 2 * RD, s);
+    tr_transpose(c->fGRH[r].as<float>(), R2, RD, RD, FB, R2, s);
+    tr_gemm(RD, RD, (int)R2, FB, R2, c->fDCP.as<float>(), RD, gvar(c, rs + "rnn/gru_cell/candidate/kernel") +
+            (long)gin * RD, RD, s);
+    // input side over all (n, t) rows: DXG = [dGP | dCP] in (n, t) order
+    fe_gru_dxg(c->fDGP.as<float>(), c->fDCP.as<float>(), B, T2, RD, c->fDXG.as<float>(), s);
+    const float* x6 = c->fRY[r][5].as<float>();
+    tr_transpose(x6, R2, gin, gin, FB, R2, s);
+    tr_gemm(gin, 2 * RD, (int)R2, FB, R2, c->fDXG.as<float>(), 3 * RD, gvar(c, rs + "rnn/gru_cell/gates/kernel"),
+            2 * RD, s);
+    tr_gemm(gin, RD, (int)R2, FB, R2, c->fDXG.as<float>() + 2 * RD, 3 * RD,
+            gvar(c, rs + "rnn/gru_cell/candidate/kernel"), RD, s);
+    tr_colsum(c, c->fDXG.as<float>(), R2, 2 * RD, 3 * RD, gvar(c, rs + "rnn/gru_cell/gates/bias"), s);
+    tr_colsum(c, c->fDXG.as<float>() + 2 * RD, R2, RD, 3 * RD, gvar(c, rs + "rnn/gru_cell/candidate/bias"), s);
+    float* dY = c->fDY.as<float>();
+    tr_transpose(kg, gin, 2 * RD, 2 * RD, WT, gin, s);  // [2RD][gin]
+    tr_gemm((int)R2, gin, 2 * RD, c->fDXG.as<float>(), 3 * RD, WT, gin, dY, gin, s);
+    tr_transpose(kcn, gin, RD, RD, WT, gin, s);
+    tr_gemm((int)R2, gin, RD, c->fDXG.as<float>() + 2 * RD, 3 * RD, WT, gin, dY, gin, s, nullptr, dY, gin);
+    // conv2d stack backward (conv -> BN -> ReLU per layer)
+    int dims[7][3];
+    {
+      int H = T_ref, W = c->NM, ci = 1;
+      for (int i = 0; i < 6; ++i) {
+        dims[i][0] = H; dims[i][1] = W; dims[i][2] = ci;
+        H = (H + 1) / 2; W = (W + 1) / 2; ci = f.reference_filters[i];
+      }
+      dims[6][0] = H; dims[6][1] = W; dims[6][2] = ci;
+    }
+    for (int i = 5; i >= 0; --i) {
+      const int nbn = f.enc_conv_layers + 6 * r + i;  // forward order: encoder convs, then refnet r's layers
+      const std::string sc = rs + "conv2d_" + std::to_string(i) + "/";
+      const int H = dims[i][0], W = dims[i][1], ci = dims[i][2], Ho = dims[i + 1][0], Wo = dims[i + 1][1];
+      const int fo = f.reference_filters[i];
+      const long Mi = (long)B * Ho * Wo;
+      const float* mean = BN + (long)nbn * 2 * 512;
+      const float* var = mean + 512;
+      float* dYr = c->fDY2.as<float>();
+      fe_relu_mask(dY, c->fRY[r][i].as<float>(), Mi * fo, dYr, s);
+      float* dz = c->fDZc.as<float>();
+      fe_bn_bwd(c, dYr, nullptr, c->fRA[r][i].as<float>(), Mi, fo, mean, var, sc, 0, dYr, dz, s);
+      tr_colsum(c, dz, Mi, fo, fo, gvar(c, sc + "conv2d/bias"), s);
+      const int pt = std::max((Ho - 1) * 2 + 3 - H, 0) / 2, pl = std::max((Wo - 1) * 2 + 3 - W, 0) / 2;
+      const float* xin = i == 0 ? refs[r] : c->fRY[r][i - 1].as<float>();
+      fe_im2col2d_t(xin, B, H, W, ci, Ho, Wo, pt, pl, FB, Mi, s);
+      tr_gemm(9 * ci, fo, (int)Mi, FB, Mi, dz, fo, gvar(c, sc + "conv2d/kernel"), fo, s);
+      if (i > 0) {
+        tr_transpose(pvar(c, sc + "conv2d/kernel"), 9L * ci, fo, fo, WT, 9L * ci, s);  // [fo][9ci]
+        tr_gemm((int)Mi, 9 * ci, fo, dz, fo, WT, 9 * ci, FB, 9 * ci, s);
+        fe_col2im2d(FB, B, H, W, ci, Ho, Wo, pt, pl, dY, s);
+      }
+    }
+  }
+  // BiLSTM BPTT (the decoder's DMEM rows carry d enc_out in columns [0, 2U))
+  for (int d = 0; d < 2; ++d) {
+    const float* k = pvar(c, fe_lstm_scope(d) + "kernel");
+    tr_transpose(k + (long)C * 4 * U, U, 4 * U, 4 * U, c->fLWhT.as<float>() + (long)d * 4 * U * U, U, s);
+    tr_transpose(k, C, 4 * U, 4 * U, c->fLWxT.as<float>() + (long)d * 4 * U * C, C, s);
+  }
+  TT2_HIP(hipMemsetAsync(c->fDHC.p, 0, c->fDHC.bytes, s));
+  TT2_HIP(hipMemsetAsync(c->fDCC.p, 0, c->fDCC.bytes, s));
+  FeLstm l{};
+  l.GA = c->fGA.as<float>(); l.CN = c->fCN.as<float>(); l.CS = c->fCS.as<float>(); l.HS = c->fHS.as<float>();
+  l.zm = enczm; l.lens = lens; l.B = B; l.T = T; l.U = U; l.zo = f.zoneout;
+  l.DENC = c->DMEM.as<float>(); l.ld_denc = D; l.DZ = c->fDZ.as<float>(); l.DHC = c->fDHC.as<float>();
+  l.DCC = c->fDCC.as<float>(); l.DHP = c->fDHP.as<float>();
+  for (int t = T - 1; t >= 0; --t) {
+    l.t = t;
+    fe_lstm_cell_bwd(l, s);
+    for (int d = 0; d < 2; ++d)
+      tr_gemm(B, U, 4 * U, c->fDZ.as<float>() + ((long)d * T + t) * B * 4 * U, 4 * U,
+              c->fLWhT.as<float>() + (long)d * 4 * U * U, U, c->fDHC.as<float>() + (long)d * B * U, U, s, nullptr,
+              c->fDHP.as<float>() + (long)d * B * U, U);
+  }
+  for (int d = 0; d < 2; ++d) {  // recurrent weights: Σ_t HS(t)ᵀ DZ(t); biases
+    const long R = (long)T * B;
+    tr_transpose(c->fHS.as<float>() + (long)d * (T + 1) * B * U, R, U, U, FB, R, s);
+    tr_gemm(U, 4 * U, (int)R, FB, R, c->fDZ.as<float>() + (long)d * T * B * 4 * U, 4 * U,
+            gvar(c, fe_lstm_scope(d) + "kernel") + (long)C * 4 * U, 4 * U, s);
+    tr_colsum(c, c->fDZ.as<float>() + (long)d * T * B * 4 * U, R, 4 * U, 4 * U, gvar(c, fe_lstm_scope(d) + "bias"), s);
+  }
+  fe_lstm_dxp(c->fDZ.as<float>(), lens, B, T, U, c->fdXP.as<float>(), s);
+  const float* X3 = c->fEY[f.enc_conv_layers].as<float>();
+  tr_transpose(X3, M, C, C, FB, M, s);
+  float* dxn = c->fdA.as<float>();
+  float* dxo = c->fdB.as<float>();
+  for (int d = 0; d < 2; ++d) {
+    tr_gemm(C, 4 * U, (int)M, FB, M, c->fdXP.as<float>() + d * 4 * U, 8 * U, gvar(c, fe_lstm_scope(d) + "kernel"),
+            4 * U, s);
+    tr_gemm((int)M, C, 4 * U, c->fdXP.as<float>() + d * 4 * U, 8 * U, c->fLWxT.as<float>() + (long)d * 4 * U * C, C,
+            dxn, C, s, nullptr, d ? dxn : nullptr, C);
+  }
+  // encoder convolutions backward (dropout -> BN -> ReLU -> conv)
+  for (int i = f.enc_conv_layers - 1; i >= 0; --i) {
+    const std::string sc = fe_conv_scope(i + 1);
+    const float* mean = BN + (long)i * 2 * 512;
+    const float* var = mean + 512;
+    float* dz = c->fDZc.as<float>();
+    fe_bn_bwd(c, dxn, encm ? encm + (long)i * M * C : nullptr, c->fEA[i].as<float>(), M, C, mean, var, sc, 2,
+              c->fDY.as<float>(), dz, s);
+    tr_colsum(c, dz, M, C, C, gvar(c, sc + "conv1d/bias"), s);
+    const int cin = i == 0 ? E : C, pad = (K - 1) / 2;
+    const float* xin = i == 0 ? c->fEX.as<float>() : c->fEY[i].as<float>();
+    hipLaunchKernelGGL(k_pn_im2col_t, dim3(nblk((long)K * cin * M)), dim3(256), 0, s, xin, (long)T * cin, (long)cin, B,
+                       T, cin, K, pad, FB, M);
+    tr_gemm(K * cin, C, (int)M, FB, M, dz, C, gvar(c, sc + "conv1d/kernel"), C, s);
+    hipLaunchKernelGGL(k_pn_flip, dim3(nblk((long)K * cin * C)), dim3(256), 0, s, pvar(c, sc + "conv1d/kernel"), K, cin,
+                       C, WT);
+    GemmArgs g;
+    g.a_mode = A_CONV1D; g.M = (int)M; g.N = cin; g.T = T; g.kw = K; g.pad = K - 1 - pad;
+    g.A = dz; g.C = C; g.xs_b = (long)T * C; g.xs_t = C; g.K = K * C;
+    g.Bw = WT; g.ldb = cin; g.Cout = dxo; g.ldc = cin;
+    tr_gemm_run(g, s);
+    std::swap(dxn, dxo);
+  }
+  fe_embed_bwd(ids, dxn, M, E, f.n_symbols, gvar(c, vn("inputs_embedding")), s);
+}
+
 
 static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s) {
   float* red = c->red.as<float>();
@@ -1385,6 +1846,19 @@ static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s)
                          c->BNV.as<float>() + (long)i * c->PC, c->PC, c->cfg.bn_momentum);
     }
     c->pn_ran = false;
+  }
+  if (c->cfg.frontend && c->f_ran) {  // front-end BN UPDATE_OPS (encoder convs, then refnet convs)
+    int nbn = 0;
+    auto upd = [&](const std::string& sc, int C) {
+      const float* st = c->fBN.as<float>() + (long)nbn * 2 * 512;
+      hipLaunchKernelGGL(k_pn_moving, dim3((C + 255) / 256), dim3(256), 0, s, pvar(c, sc + "batch_normalization/moving_mean"),
+                         pvar(c, sc + "batch_normalization/moving_variance"), st, st + 512, C, c->cfg.bn_momentum);
+      ++nbn;
+    };
+    for (int i = 0; i < c->cfg.enc_conv_layers; ++i) upd(fe_conv_scope(i + 1), c->cfg.enc_conv_channels);
+    for (int r = 0; r < c->f_nref; ++r)
+      for (int i = 0; i < 6; ++i) upd(fe_ref_scope(r) + "conv2d_" + std::to_string(i) + "/", c->cfg.reference_filters[i]);
+    c->f_ran = false;
   }
   hipLaunchKernelGGL(k_tr_sumsq, dim3(256), dim3(256), 0, s, c->grads, c->total, c->part.as<float>());
   hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, 1.f, red + 3, 1);
@@ -1439,6 +1913,22 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   c->postnet_kernel = 5;
   c->bn_momentum = 0.99f;
   c->bn_eps = 1e-3f;
+  c->frontend = 0;
+  c->n_symbols = 66;
+  c->embedding_dim = 512;
+  c->enc_conv_layers = 3;
+  c->enc_conv_kernel = 5;
+  c->enc_conv_channels = 512;
+  c->encoder_lstm_units = 256;
+  c->emt_only = 0;
+  c->num_gst = 10;
+  c->num_heads = 4;
+  c->style_embed_depth = 256;
+  c->style_att_dim = 128;
+  c->reference_depth = 128;
+  const int rf[6] = {32, 32, 64, 64, 128, 128};
+  for (int i = 0; i < 6; ++i) c->reference_filters[i] = rf[i];
+  c->max_T_ref = max_T_out;
 }
 
 tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_train_ctx** out) {
@@ -1472,6 +1962,25 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
       TT2_CHECK(!cfg->postnet || (c->PL >= 1 && c->PL <= 8 && c->PC >= 1 && c->PK >= 1 && c->PK <= 64),
                 TT2_ERR_INVALID_ARG,
                 "bad postnet shape");
+      if (cfg->frontend) {
+        c->f_nref = cfg->emt_only ? 1 : 2;
+        int W = cfg->num_mels;
+        for (int i = 0; i < 6; ++i) W = (W + 1) / 2;
+        c->f_gin = W * cfg->reference_filters[5];
+        const int tokd = cfg->num_heads > 0 ? cfg->style_embed_depth / cfg->num_heads : 0;
+        TT2_CHECK(cfg->memory_dim == 2 * cfg->encoder_lstm_units + c->f_nref * cfg->num_heads * tokd, TT2_ERR_INVALID_ARG,
+                  "memory_dim must be 2*encoder_lstm_units + (emt_only ? 1 : 2) * style_embed_depth");
+        TT2_CHECK(cfg->enc_conv_layers >= 1 && cfg->enc_conv_layers <= 8 && cfg->enc_conv_channels <= 512 &&
+                      cfg->n_symbols >= 1 && cfg->embedding_dim >= 1 && cfg->max_T_ref >= 1,
+                  TT2_ERR_INVALID_ARG, "bad front-end shape");
+        TT2_CHECK(cfg->style_att_dim <= 128 && cfg->num_gst <= 16 && tokd <= 64 && cfg->num_heads >= 1 &&
+                      cfg->style_att_dim % cfg->num_heads == 0 && cfg->style_att_dim / cfg->num_heads <= 32 &&
+                      cfg->num_heads * cfg->num_gst <= 64,
+                  TT2_ERR_INVALID_ARG, "GST shape outside the fe_gst kernels' LDS tiles");
+        for (int i = 0; i < 6; ++i)
+          TT2_CHECK(cfg->reference_filters[i] >= 1 && cfg->reference_filters[i] <= 512, TT2_ERR_INVALID_ARG,
+                    "reference_filters must be in [1, 512]");
+      }
       TT2_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       TT2_HIP(hipEventCreate(&c->ev0));
       TT2_HIP(hipEventCreate(&c->ev1));
@@ -1545,8 +2054,47 @@ tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* c, const float* memory_
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     c->last_stream = s;
     TT2_HIP(hipEventRecord(c->ev0, s));
+    TT2_CHECK(!c->cfg.frontend, TT2_ERR_STATE,
+              "front-end context: use tt2_train_forward_backward_text_dev (ids + reference mels)");
     tr_forward_backward(c, memory_d, lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d,
                         postnet_masks_d, T_in, T_out, s);
+    tr_regularize(c, s);
+    TT2_HIP(hipEventRecord(c->ev1, s));
+    TT2_HIP(hipGetLastError());
+  });
+}
+
+tt2_status tt2_train_forward_backward_text_dev(tt2_train_ctx* c, const int32_t* ids_d, const int32_t* lengths_d,
+                                               const float* ref_emt_d, const float* ref_spk_d, int T_ref,
+                                               const float* targets_d, const float* stop_targets_d,
+                                               const uint8_t* prenet_masks_d, const uint8_t* zoneout_masks_d,
+                                               const uint8_t* postnet_masks_d, const uint8_t* enc_conv_masks_d,
+                                               const uint8_t* enc_zoneout_masks_d, int T_in, int T_out, void* stream) {
+  return guard([&] {
+    TT2_CHECK(c && ids_d && lengths_d && ref_emt_d && targets_d && stop_targets_d && prenet_masks_d,
+              TT2_ERR_INVALID_ARG, "tt2_train_forward_backward_text_dev: null argument");
+    TT2_CHECK(c->cfg.frontend, TT2_ERR_STATE, "context built without cfg.frontend");
+    TT2_CHECK(c->f_nref == 1 || ref_spk_d, TT2_ERR_INVALID_ARG, "ref_spk required unless emt_only");
+    TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_train_finalize not called");
+    TT2_CHECK(T_in >= 1 && T_in <= c->Tin && T_out >= 1 && T_out <= c->Tm, TT2_ERR_SHAPE_MISMATCH,
+              "T_in/T_out exceed capacity");
+    TT2_CHECK(T_ref >= 1 && T_ref <= c->cfg.max_T_ref, TT2_ERR_SHAPE_MISMATCH, "T_ref exceeds capacity");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    c->last_stream = s;
+    TT2_HIP(hipEventRecord(c->ev0, s));
+    const float* refs[2] = {ref_emt_d, ref_spk_d};
+    g_tr_kpart = &c->kpart;
+    g_tr_prec = c->cfg.precision ? 2 : 0;
+    tr_front_forward(c, ids_d, lengths_d, refs, T_ref, enc_conv_masks_d, enc_zoneout_masks_d, T_in, s);
+    tr_forward_backward(c, c->fMEM.as<float>(), lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d,
+                        postnet_masks_d, T_in, T_out, s);
+    g_tr_kpart = &c->kpart;
+    g_tr_prec = c->cfg.precision ? 2 : 0;
+    tr_front_backward(c, ids_d, lengths_d, refs, T_ref, enc_conv_masks_d, enc_zoneout_masks_d, T_in, s);
+    g_tr_kpart = nullptr;
+    g_tr_prec = 0;
+    tr_regularize(c, s);
     TT2_HIP(hipEventRecord(c->ev1, s));
     TT2_HIP(hipGetLastError());
   });
@@ -1586,6 +2134,15 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
       tr_d2h(c, host, c->DMEM.p, sizeof(float) * (size_t)c->B * c->Tin_last * c->D);
       return;
     }
+    if (c->cfg.frontend && std::string(name) == "frontend:memory") {  // the front end's memory [B,T_in,D]
+      tr_d2h(c, host, c->fMEM.p, sizeof(float) * (size_t)c->B * c->Tin_last * c->D);
+      return;
+    }
+    for (int r = 0; r < c->f_nref; ++r)  // reference embeddings (ReferenceEncoder outputs) [B,128]
+      if (std::string(name) == (r == 0 ? "frontend:refnet_emt" : "frontend:refnet_spk")) {
+        tr_d2h(c, host, c->fREF[r].p, sizeof(float) * (size_t)c->B * 128);
+        return;
+      }
     auto it = c->index.find(name);
     TT2_CHECK(it != c->index.end(), TT2_ERR_INVALID_ARG, std::string("unknown variable ") + name);
     const TrVar& v = c->vars[it->second];

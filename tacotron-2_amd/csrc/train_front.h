@@ -1,0 +1,90 @@
+// Front end of the configs[4] training step (train_front.hip): embedding, encoder convolutions
+// and bidirectional Zoneout-LSTM, both reference encoders (conv2d + BN + ReLU, GRU, dense) and
+// both GST attentions, forward in training mode and backward.  Elementwise / recurrent kernels
+// here; every matrix product goes through gemm.hip from train.hip's orchestration.
+#pragma once
+#include "common.h"
+
+namespace tt2 {
+
+// ---- encoder --------------------------------------------------------------------------------
+void fe_embed(const int* ids, const float* table, long M, int E, float* out, hipStream_t s);
+void fe_embed_bwd(const int* ids, const float* dx, long M, int E, int n_symbols, float* dtable, hipStream_t s);
+
+// BiLSTM step t of both directions (bidirectional_dynamic_rnn, modules.py:315-321): layouts are
+// direction-major: XP [B][T][8U] input projections (+ biases), GZ [2][B][4U] recurrent products of
+// this step, GA [2][T][B][4U] activations (σi, tanh j, σ(f+1), σo), CN [2][T][B][U] c_new,
+// CS / HS [2][T+1][B][U] carried (zoned) states, ENC [B][T][2U] outputs (h_new, 0 past length).
+// zm [T][2][2][B][U] training zoneout keep bits (c, h) by step, or null (inference mix).
+struct FeLstm {
+  const float* XP; const float* GZ; float* GA; float* CN; float* CS; float* HS; float* ENC;
+  const uint8_t* zm; const int* lens;
+  int B, T, U, t;
+  float zo;
+  // backward
+  const float* DENC; long ld_denc;  // d enc_out rows (stride ld_denc, the decoder's d memory)
+  float* DZ;                        // [2][T][B][4U]
+  float* DHC; float* DCC;           // [2][B][U] gradient wrt the carried h / c after step t
+  float* DHP;                       // [2][B][U] direct part of d h_prev (before + DZ·Whᵀ)
+};
+void fe_lstm_cell(const FeLstm& a, hipStream_t s);
+void fe_lstm_cell_bwd(const FeLstm& a, hipStream_t s);
+// dXP[b][pos][dir*4U + c] = DZ[dir][t][b][c] at the step that visited pos (0 past length)
+void fe_lstm_dxp(const float* DZ, const int* lens, int B, int T, int U, float* dXP, hipStream_t s);
+
+// ---- reference encoder ----------------------------------------------------------------------
+// BN (batch statistics) + ReLU forward; backward sums use the post-ReLU output as the ReLU mask
+void fe_bn_relu_fwd(const float* a, long M, int C, const float* mean, const float* var, const float* gamma,
+                    const float* beta, float eps, float* y, hipStream_t s);
+void fe_relu_mask(const float* dy, const float* y, long n, float* out, hipStream_t s);
+// conv2d 3x3 stride 2 'same' (TF: odd pad bottom/right) on NHWC x [N][H][W][C]
+void fe_im2col2d_t(const float* x, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* out, long ldo,
+                   hipStream_t s);
+void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* dx,
+                 hipStream_t s);
+// GRU (TF1 GRUCell, modules.py:59): XG [N][T2][3D] = x·[Wg_x | Wc_x] + [bg | bc]; per step
+// GG = h·Wg_h [N][2D], GC = (r·h)·Wc_h [N][D]; stored step-major R, U, CC [T2][N][D], RH [T2][N][D],
+// HG [T2+1][N][D]
+void fe_gru_a(const float* XG, const float* GG, const float* HG, int N, int T2, int D, int t, float* R, float* Uu,
+              float* RH, hipStream_t s);
+void fe_gru_b(const float* XG, const float* GC, const float* Uu, int N, int T2, int D, int t, float* CC, float* HG,
+              hipStream_t s);
+// backward of step t: dH [N][D] in (gradient wrt h(t+1)); writes DCP[t] (pre-tanh candidate grad),
+// DHA = dh·u; then (after the d(r·h) product) DGP[t] and DHA += d(rh)·r
+void fe_gru_bwd_a(const float* dH, const float* Uu, const float* CC, const float* HG, int N, int D, int t, float* DCP,
+                  float* DHA, hipStream_t s);
+void fe_gru_bwd_b(const float* DRH, const float* R, const float* Uu, const float* HG, const float* CC, const float* dH,
+                  int N, int D, int t, float* DGP, float* DHA, hipStream_t s);
+// DXG [N][T2][3D] (row n*T2 + t) from step-major DGP [T2][N][2D] / DCP [T2][N][D]
+void fe_gru_dxg(const float* DGP, const float* DCP, int N, int T2, int D, float* DXG, hipStream_t s);
+void fe_tanh_bwd(const float* dy, const float* y, long n, float* out, hipStream_t s);
+
+// ---- GST multi-head attention (multihead_attention.py:35-132, mlp attention, normalize) -------
+struct FeGst {
+  const float* ref;     // [N][128] reference embedding
+  const float* tokens;  // [ntok][tokd]
+  const float* wq; const float* bq;  // [128][A], [A]
+  const float* wk; const float* bk;  // [tokd][A], [A]
+  const float* v; const float* g; const float* bb;  // [A/heads], scalar, [A/heads]
+  int N, ntok, tokd, A, heads, refd;
+  float* style; int style_ld, style_off;  // output [N][style_ld] at column style_off (heads*tokd wide)
+  // backward
+  const float* dstyle;   // [N][style_ld] (same column window)
+  float* dq;             // [N][A]
+  float* pdkk;           // [N][ntok][A]
+  float* pdv;            // [N][ntok][tokd]  (value path)
+  float* pdnv;           // [N][A/heads]
+  float* pdbb;           // [N][A/heads]
+};
+void fe_gst_fwd(const FeGst& a, hipStream_t s);
+void fe_gst_bwd(const FeGst& a, hipStream_t s);
+// from the row-summed partials: d Wk, d bk, d tokens, d v, d g, d attention_b
+void fe_gst_final(const FeGst& a, const float* dkk, const float* dval, const float* dnv, const float* dbb,
+                  float* dwk, float* dbk, float* dtok, float* dv, float* dg, float* dbbo, hipStream_t s);
+
+// ---- memory assembly --------------------------------------------------------------------------
+// MEM[b][t] = [ENC[b][t] (2U) | STY[b] (SW)]; style gradient = Σ_t DMEM[b][t][2U:]
+void fe_memory(const float* ENC, const float* STY, int B, int T, int E2, int SW, float* MEM, hipStream_t s);
+void fe_style_grad(const float* DMEM, int B, int T, int D, int E2, float* DSTY, hipStream_t s);
+
+}  // namespace tt2

@@ -1,0 +1,481 @@
+// Front end of the configs[4] training step (train_front.h): embedding_lookup (tacotron.py:215-217),
+// EncoderRNN bidirectional Zoneout-LSTM (modules.py:283-323, 187-248, training zoneout), the
+// ReferenceEncoder's conv2d/BN/ReLU stack and GRU (modules.py:9-64, 499-511) and the GST mlp
+// multi-head attention (multihead_attention.py:35-132), forward and backward.  Plain fp32
+// elementwise / per-row kernels; the matrix products run as gemm.hip GEMMs from train.hip.
+#include "train_front.h"
+
+namespace tt2 {
+
+static inline unsigned fe_blk(long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+__device__ __forceinline__ float fe_sig(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ---- embedding --------------------------------------------------------------------------------
+__global__ void k_fe_embed(const int* __restrict__ ids, const float* __restrict__ tab, long M, int E,
+                           float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * E) return;
+  out[i] = tab[(long)ids[i / E] * E + i % E];
+}
+// d table[s][e] = Σ over positions with id s (deterministic order, one thread per (s, e))
+__global__ void k_fe_embed_bwd(const int* __restrict__ ids, const float* __restrict__ dx, long M, int E, int NS,
+                               float* __restrict__ dtab) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)NS * E) return;
+  const int sym = (int)(i / E), e = (int)(i % E);
+  float acc = 0.f;
+  for (long m = 0; m < M; ++m)
+    if (ids[m] == sym) acc += dx[m * E + e];
+  dtab[i] = acc;
+}
+void fe_embed(const int* ids, const float* table, long M, int E, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_embed, dim3(fe_blk(M * E)), dim3(256), 0, s, ids, table, M, E, out);
+}
+void fe_embed_bwd(const int* ids, const float* dx, long M, int E, int n_symbols, float* dtable, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_embed_bwd, dim3(fe_blk((long)n_symbols * E)), dim3(256), 0, s, ids, dx, M, E, n_symbols,
+                     dtable);
+}
+
+// ---- BiLSTM -------------------------------------------------------------------------------------
+__global__ void k_fe_lstm_cell(FeLstm a) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int B = a.B, U = a.U, T = a.T, t = a.t;
+  if (i >= 2L * B * U) return;
+  const int dir = (int)(i / ((long)B * U)), b = (int)((i / U) % B), u = (int)(i % U);
+  const int len = a.lens[b];
+  const long st0 = ((long)dir * (T + 1) + t) * B * U + (long)b * U + u;  // CS/HS at t
+  const long st1 = st0 + (long)B * U;                                    // at t+1
+  const float cp = a.CS[st0], hp = a.HS[st0];
+  if (t >= len) {  // past the row's length: state copied, output stays 0 (TF rnn._rnn_step)
+    a.CS[st1] = cp;
+    a.HS[st1] = hp;
+    return;
+  }
+  const int pos = dir == 0 ? t : len - 1 - t;
+  const float* xp = a.XP + ((long)b * T + pos) * 8 * U + dir * 4 * U;
+  const float* gz = a.GZ + ((long)dir * B + b) * 4 * U;
+  const float zi = gz[u] + xp[u], zj = gz[U + u] + xp[U + u], zf = gz[2 * U + u] + xp[2 * U + u],
+              zo = gz[3 * U + u] + xp[3 * U + u];
+  const float si = fe_sig(zi), tj = tanhf(zj), sf = fe_sig(zf + 1.0f), so = fe_sig(zo);
+  const float cn = sf * cp + si * tj;
+  const float hn = so * tanhf(cn);
+  float* ga = a.GA + (((long)dir * T + t) * B + b) * 4 * U;
+  ga[u] = si; ga[U + u] = tj; ga[2 * U + u] = sf; ga[3 * U + u] = so;
+  a.CN[((long)dir * T + t) * B * U + (long)b * U + u] = cn;
+  float mc, mh;
+  if (a.zm) {  // training zoneout (modules.py:236-240): keep bits by step
+    mc = (float)a.zm[((((long)t * 2 + dir) * 2 + 0) * B + b) * U + u];
+    mh = (float)a.zm[((((long)t * 2 + dir) * 2 + 1) * B + b) * U + u];
+  } else {
+    mc = mh = 1.f - a.zo;
+  }
+  a.CS[st1] = cp + mc * (cn - cp);
+  a.HS[st1] = hp + mh * (hn - hp);
+  a.ENC[((long)b * T + pos) * 2 * U + dir * U + u] = hn;
+}
+
+__global__ void k_fe_lstm_cell_bwd(FeLstm a) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int B = a.B, U = a.U, T = a.T, t = a.t;
+  if (i >= 2L * B * U) return;
+  const int dir = (int)(i / ((long)B * U)), b = (int)((i / U) % B), u = (int)(i % U);
+  const int len = a.lens[b];
+  const long sidx = ((long)dir * B + b) * U + u;
+  float* dz = a.DZ + (((long)dir * T + t) * B + b) * 4 * U;
+  if (t >= len) {  // copied state: gradients pass through, no gate gradient
+    dz[u] = dz[U + u] = dz[2 * U + u] = dz[3 * U + u] = 0.f;
+    a.DHP[sidx] = a.DHC[sidx];
+    return;
+  }
+  const int pos = dir == 0 ? t : len - 1 - t;
+  const float* ga = a.GA + (((long)dir * T + t) * B + b) * 4 * U;
+  const float si = ga[u], tj = ga[U + u], sf = ga[2 * U + u], so = ga[3 * U + u];
+  const float cn = a.CN[((long)dir * T + t) * B * U + (long)b * U + u];
+  const float cp = a.CS[((long)dir * (T + 1) + t) * B * U + (long)b * U + u];
+  float mc, mh;
+  if (a.zm) {
+    mc = (float)a.zm[((((long)t * 2 + dir) * 2 + 0) * B + b) * U + u];
+    mh = (float)a.zm[((((long)t * 2 + dir) * 2 + 1) * B + b) * U + u];
+  } else {
+    mc = mh = 1.f - a.zo;
+  }
+  const float dhc = a.DHC[sidx], dcc = a.DCC[sidx];
+  const float dout = a.DENC[((long)b * T + pos) * a.ld_denc + dir * U + u];
+  const float dhn = dout + mh * dhc;
+  const float tc = tanhf(cn);
+  const float dcn = mc * dcc + dhn * so * (1.f - tc * tc);
+  dz[u] = dcn * tj * si * (1.f - si);
+  dz[U + u] = dcn * si * (1.f - tj * tj);
+  dz[2 * U + u] = dcn * cp * sf * (1.f - sf);
+  dz[3 * U + u] = dhn * tc * so * (1.f - so);
+  a.DCC[sidx] = (1.f - mc) * dcc + dcn * sf;
+  a.DHP[sidx] = (1.f - mh) * dhc;
+}
+void fe_lstm_cell(const FeLstm& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_lstm_cell, dim3(fe_blk(2L * a.B * a.U)), dim3(256), 0, s, a);
+}
+void fe_lstm_cell_bwd(const FeLstm& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_lstm_cell_bwd, dim3(fe_blk(2L * a.B * a.U)), dim3(256), 0, s, a);
+}
+__global__ void k_fe_lstm_dxp(const float* __restrict__ DZ, const int* __restrict__ lens, int B, int T, int U,
+                              float* __restrict__ dXP) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * T * 8 * U) return;
+  const int col = (int)(i % (8 * U));
+  const long bp = i / (8 * U);
+  const int pos = (int)(bp % T), b = (int)(bp / T);
+  const int dir = col / (4 * U), c = col % (4 * U);
+  const int len = lens[b];
+  float v = 0.f;
+  if (pos < len) {
+    const int t = dir == 0 ? pos : len - 1 - pos;
+    v = DZ[(((long)dir * T + t) * B + b) * 4 * U + c];
+  }
+  dXP[i] = v;
+}
+void fe_lstm_dxp(const float* DZ, const int* lens, int B, int T, int U, float* dXP, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_lstm_dxp, dim3(fe_blk((long)B * T * 8 * U)), dim3(256), 0, s, DZ, lens, B, T, U, dXP);
+}
+
+// ---- reference encoder ---------------------------------------------------------------------------
+__global__ void k_fe_bn_relu_fwd(const float* __restrict__ a, long M, int C, const float* __restrict__ mean,
+                                 const float* __restrict__ var, const float* __restrict__ gamma,
+                                 const float* __restrict__ beta, float eps, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const int c = (int)(i % C);
+  y[i] = fmaxf(gamma[c] * (a[i] - mean[c]) * rsqrtf(var[c] + eps) + beta[c], 0.f);
+}
+void fe_bn_relu_fwd(const float* a, long M, int C, const float* mean, const float* var, const float* gamma,
+                    const float* beta, float eps, float* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_bn_relu_fwd, dim3(fe_blk(M * C)), dim3(256), 0, s, a, M, C, mean, var, gamma, beta, eps, y);
+}
+__global__ void k_fe_relu_mask(const float* __restrict__ dy, const float* __restrict__ y, long n,
+                               float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = y[i] > 0.f ? dy[i] : 0.f;
+}
+void fe_relu_mask(const float* dy, const float* y, long n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_relu_mask, dim3(fe_blk(n)), dim3(256), 0, s, dy, y, n, out);
+}
+// out[((i*3 + j)*C + c) * ldo + m] = x(n, 2ho + i - pt, 2wo + j - pl, c), m = (n*Ho + ho)*Wo + wo
+__global__ void k_fe_im2col2d_t(const float* __restrict__ x, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl,
+                                float* __restrict__ out, long ldo) {
+  const long M = (long)N * Ho * Wo;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 9L * C * M) return;
+  const long m = i % M, k = i / M;
+  const int c = (int)(k % C), ij = (int)(k / C), ii = ij / 3, jj = ij % 3;
+  const int wo = (int)(m % Wo), ho = (int)((m / Wo) % Ho), n = (int)(m / ((long)Wo * Ho));
+  const int h = 2 * ho + ii - pt, w = 2 * wo + jj - pl;
+  out[k * ldo + m] = (h >= 0 && h < H && w >= 0 && w < W) ? x[(((long)n * H + h) * W + w) * C + c] : 0.f;
+}
+void fe_im2col2d_t(const float* x, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* out, long ldo,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_im2col2d_t, dim3(fe_blk(9L * C * N * Ho * Wo)), dim3(256), 0, s, x, N, H, W, C, Ho, Wo, pt,
+                     pl, out, ldo);
+}
+// dx(n, h, w, c) = Σ_{i,j} dcols[(n, ho, wo)][(i*3+j)*C + c] over the outputs whose taps read it
+__global__ void k_fe_col2im2d(const float* __restrict__ dcols, int N, int H, int W, int C, int Ho, int Wo, int pt,
+                              int pl, float* __restrict__ dx) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)N * H * W * C) return;
+  const int c = (int)(i % C), w = (int)((i / C) % W), h = (int)((i / ((long)C * W)) % H);
+  const int n = (int)(i / ((long)C * W * H));
+  float acc = 0.f;
+  for (int ii = 0; ii < 3; ++ii) {
+    const int hh = h + pt - ii;
+    if (hh < 0 || (hh & 1) || (hh >> 1) >= Ho) continue;
+    for (int jj = 0; jj < 3; ++jj) {
+      const int ww = w + pl - jj;
+      if (ww < 0 || (ww & 1) || (ww >> 1) >= Wo) continue;
+      const long m = ((long)n * Ho + (hh >> 1)) * Wo + (ww >> 1);
+      acc += dcols[m * 9 * C + (ii * 3 + jj) * C + c];
+    }
+  }
+  dx[i] = acc;
+}
+void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* dx,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_col2im2d, dim3(fe_blk((long)N * H * W * C)), dim3(256), 0, s, dcols, N, H, W, C, Ho, Wo, pt,
+                     pl, dx);
+}
+
+// GRU step t, part a: [r, u] = σ(XG_g + h·Wg_h); RH = r·h
+__global__ void k_fe_gru_a(const float* __restrict__ XG, const float* __restrict__ GG, const float* __restrict__ HG,
+                           int N, int T2, int D, int t, float* __restrict__ R, float* __restrict__ Uu,
+                           float* __restrict__ RH) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * D) return;
+  const int n = i / D, d = i % D;
+  const float* xg = XG + ((long)n * T2 + t) * 3 * D;
+  const float r = fe_sig(xg[d] + GG[(long)n * 2 * D + d]);
+  const float u = fe_sig(xg[D + d] + GG[(long)n * 2 * D + D + d]);
+  const long o = ((long)t * N + n) * D + d;
+  R[o] = r;
+  Uu[o] = u;
+  RH[o] = r * HG[o];  // HG[t] = h(t), step-major [T2+1][N][D]
+}
+// part b: c = tanh(XG_c + (r·h)·Wc_h); h(t+1) = u·h + (1 - u)·c
+__global__ void k_fe_gru_b(const float* __restrict__ XG, const float* __restrict__ GC, const float* __restrict__ Uu,
+                           int N, int T2, int D, int t, float* __restrict__ CC, float* __restrict__ HG) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * D) return;
+  const int n = i / D, d = i % D;
+  const float c = tanhf(XG[((long)n * T2 + t) * 3 * D + 2 * D + d] + GC[(long)n * D + d]);
+  const long o = ((long)t * N + n) * D + d;
+  const float u = Uu[o];
+  CC[o] = c;
+  HG[o + (long)N * D] = u * HG[o] + (1.f - u) * c;
+}
+void fe_gru_a(const float* XG, const float* GG, const float* HG, int N, int T2, int D, int t, float* R, float* Uu,
+              float* RH, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_gru_a, dim3(fe_blk((long)N * D)), dim3(256), 0, s, XG, GG, HG, N, T2, D, t, R, Uu, RH);
+}
+void fe_gru_b(const float* XG, const float* GC, const float* Uu, int N, int T2, int D, int t, float* CC, float* HG,
+              hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_gru_b, dim3(fe_blk((long)N * D)), dim3(256), 0, s, XG, GC, Uu, N, T2, D, t, CC, HG);
+}
+// backward a: dh = dH; du = dh (h - c); dc = dh (1 - u); DCP = dc (1 - c^2); DHA = dh u
+__global__ void k_fe_gru_bwd_a(const float* __restrict__ dH, const float* __restrict__ Uu, const float* __restrict__ CC,
+                               const float* __restrict__ HG, int N, int D, int t, float* __restrict__ DCP,
+                               float* __restrict__ DHA) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * D) return;
+  const long o = (long)t * N * D + i;
+  const float dh = dH[i], u = Uu[o], c = CC[o];
+  DCP[o] = dh * (1.f - u) * (1.f - c * c);
+  DHA[i] = dh * u;
+}
+// backward b: dr = d(rh)·h; DHA += d(rh)·r; DGP = [dr r(1-r), du u(1-u)]
+__global__ void k_fe_gru_bwd_b(const float* __restrict__ DRH, const float* __restrict__ R, const float* __restrict__ Uu,
+                               const float* __restrict__ HG, const float* __restrict__ CC, const float* __restrict__ dH,
+                               int N, int D, int t, float* __restrict__ DGP, float* __restrict__ DHA) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * D) return;
+  const int n = i / D, d = i % D;
+  const long o = (long)t * N * D + i;
+  const float h = HG[o], r = R[o], u = Uu[o], c = CC[o];
+  const float drh = DRH[i];
+  const float du = dH[i] * (h - c);
+  float* dg = DGP + ((long)t * N + n) * 2 * D;
+  dg[d] = drh * h * r * (1.f - r);
+  dg[D + d] = du * u * (1.f - u);
+  DHA[i] += drh * r;
+}
+void fe_gru_bwd_a(const float* dH, const float* Uu, const float* CC, const float* HG, int N, int D, int t, float* DCP,
+                  float* DHA, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_gru_bwd_a, dim3(fe_blk((long)N * D)), dim3(256), 0, s, dH, Uu, CC, HG, N, D, t, DCP, DHA);
+}
+void fe_gru_bwd_b(const float* DRH, const float* R, const float* Uu, const float* HG, const float* CC, const float* dH,
+                  int N, int D, int t, float* DGP, float* DHA, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_gru_bwd_b, dim3(fe_blk((long)N * D)), dim3(256), 0, s, DRH, R, Uu, HG, CC, dH, N, D, t, DGP,
+                     DHA);
+}
+__global__ void k_fe_gru_dxg(const float* __restrict__ DGP, const float* __restrict__ DCP, int N, int T2, int D,
+                             float* __restrict__ DXG) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)N * T2 * 3 * D) return;
+  const int col = (int)(i % (3 * D));
+  const long nt = i / (3 * D);
+  const int t = (int)(nt % T2), n = (int)(nt / T2);
+  DXG[i] = col < 2 * D ? DGP[((long)t * N + n) * 2 * D + col] : DCP[((long)t * N + n) * D + col - 2 * D];
+}
+void fe_gru_dxg(const float* DGP, const float* DCP, int N, int T2, int D, float* DXG, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_gru_dxg, dim3(fe_blk((long)N * T2 * 3 * D)), dim3(256), 0, s, DGP, DCP, N, T2, D, DXG);
+}
+__global__ void k_fe_tanh_bwd(const float* __restrict__ dy, const float* __restrict__ y, long n,
+                              float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = dy[i] * (1.f - y[i] * y[i]);
+}
+void fe_tanh_bwd(const float* dy, const float* y, long n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_tanh_bwd, dim3(fe_blk(n)), dim3(256), 0, s, dy, y, n, out);
+}
+
+// ---- GST --------------------------------------------------------------------------------------
+// LDS of one row: q [A], kk [ntok][A], val [ntok][tokd] (= tanh(tokens)), nv [A/heads], w [heads][ntok]
+constexpr int FE_GST_LDS = 128 + 16 * 128 + 16 * 64 + 32 + 4 * 16 + 64;
+
+__device__ void fe_gst_common(const FeGst& a, int n, float* q, float* kk, float* val, float* nv, float* w) {
+  const int tid = threadIdx.x, A = a.A, dh = A / a.heads;
+  for (int i = tid; i < a.ntok * a.tokd; i += blockDim.x) val[i] = tanhf(a.tokens[i]);
+  __syncthreads();
+  for (int i = tid; i < A; i += blockDim.x) {
+    float s = a.bq[i];
+    for (int k = 0; k < a.refd; ++k) s += a.ref[(long)n * a.refd + k] * a.wq[(long)k * A + i];
+    q[i] = s;
+  }
+  for (int i = tid; i < a.ntok * A; i += blockDim.x) {
+    const int j = i / A, c = i % A;
+    float s = a.bk[c];
+    for (int k = 0; k < a.tokd; ++k) s += val[j * a.tokd + k] * a.wk[(long)k * A + c];
+    kk[i] = s;
+  }
+  if (tid == 0) {  // normed_v = g v / ||v|| (multihead_attention.py:110-112)
+    float ss = 0.f;
+    for (int d = 0; d < dh; ++d) ss += a.v[d] * a.v[d];
+    const float sc = a.g[0] / sqrtf(ss);
+    for (int d = 0; d < dh; ++d) nv[d] = sc * a.v[d];
+  }
+  __syncthreads();
+  if (tid < a.heads * a.ntok) {  // scores and softmax over tokens, per head
+    const int h = tid / a.ntok, j = tid % a.ntok;
+    float s = 0.f;
+    for (int d = 0; d < dh; ++d) s += nv[d] * tanhf(kk[j * A + h * dh + d] + q[h * dh + d] + a.bb[d]);
+    w[tid] = s;
+  }
+  __syncthreads();
+  if (tid < a.heads) {
+    float mx = -INFINITY, sum = 0.f;
+    for (int j = 0; j < a.ntok; ++j) mx = fmaxf(mx, w[tid * a.ntok + j]);
+    for (int j = 0; j < a.ntok; ++j) sum += expf(w[tid * a.ntok + j] - mx);
+    for (int j = 0; j < a.ntok; ++j) w[tid * a.ntok + j] = expf(w[tid * a.ntok + j] - mx) / sum;
+  }
+  __syncthreads();
+}
+
+__global__ void k_fe_gst_fwd(FeGst a) {
+  extern __shared__ float sm[];
+  float* q = sm; float* kk = q + 128; float* val = kk + 16 * 128; float* nv = val + 16 * 64; float* w = nv + 32;
+  const int n = blockIdx.x;
+  fe_gst_common(a, n, q, kk, val, nv, w);
+  for (int i = threadIdx.x; i < a.heads * a.tokd; i += blockDim.x) {  // context over tiled values
+    const int h = i / a.tokd, e = i % a.tokd;
+    float s = 0.f;
+    for (int j = 0; j < a.ntok; ++j) s += w[h * a.ntok + j] * val[j * a.tokd + e];
+    a.style[(long)n * a.style_ld + a.style_off + i] = s;
+  }
+}
+void fe_gst_fwd(const FeGst& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_gst_fwd, dim3(a.N), dim3(256), sizeof(float) * FE_GST_LDS, s, a);
+}
+
+__global__ void k_fe_gst_bwd(FeGst a) {
+  extern __shared__ float sm[];
+  float* q = sm; float* kk = q + 128; float* val = kk + 16 * 128; float* nv = val + 16 * 64; float* w = nv + 32;
+  float* dw = w + 64;  // [heads][ntok], then ds
+  const int n = blockIdx.x, tid = threadIdx.x, A = a.A, dh = A / a.heads;
+  fe_gst_common(a, n, q, kk, val, nv, w);
+  const float* dout = a.dstyle + (long)n * a.style_ld + a.style_off;
+  if (tid < a.heads * a.ntok) {  // d w[h][j] = Σ_e dout[h][e] val[j][e]
+    const int h = tid / a.ntok, j = tid % a.ntok;
+    float s = 0.f;
+    for (int e = 0; e < a.tokd; ++e) s += dout[h * a.tokd + e] * val[j * a.tokd + e];
+    dw[tid] = s;
+  }
+  __syncthreads();
+  if (tid < a.heads) {  // softmax backward: ds = w (dw - Σ w dw)
+    float s = 0.f;
+    for (int j = 0; j < a.ntok; ++j) s += w[tid * a.ntok + j] * dw[tid * a.ntok + j];
+    for (int j = 0; j < a.ntok; ++j) dw[tid * a.ntok + j] = w[tid * a.ntok + j] * (dw[tid * a.ntok + j] - s);
+  }
+  __syncthreads();
+  // value path: d val[j][e] = Σ_h w[h][j] dout[h][e]
+  for (int i = tid; i < a.ntok * a.tokd; i += blockDim.x) {
+    const int j = i / a.tokd, e = i % a.tokd;
+    float s = 0.f;
+    for (int h = 0; h < a.heads; ++h) s += w[h * a.ntok + j] * dout[h * a.tokd + e];
+    a.pdv[(long)n * a.ntok * a.tokd + i] = s;
+  }
+  // d pre[h][j][d] = ds[h][j] nv[d] (1 - th^2): d kk, d q, d bb, d nv
+  for (int i = tid; i < a.ntok * A; i += blockDim.x) {
+    const int j = i / A, c = i % A, h = c / dh, d = c % dh;
+    const float th = tanhf(kk[i] + q[c] + a.bb[d]);
+    a.pdkk[(long)n * a.ntok * A + i] = dw[h * a.ntok + j] * nv[d] * (1.f - th * th);
+  }
+  for (int c = tid; c < A; c += blockDim.x) {
+    const int h = c / dh, d = c % dh;
+    float s = 0.f;
+    for (int j = 0; j < a.ntok; ++j) {
+      const float th = tanhf(kk[j * A + c] + q[c] + a.bb[d]);
+      s += dw[h * a.ntok + j] * nv[d] * (1.f - th * th);
+    }
+    a.dq[(long)n * A + c] = s;
+  }
+  for (int d = tid; d < dh; d += blockDim.x) {
+    float snv = 0.f, sbb = 0.f;
+    for (int h = 0; h < a.heads; ++h)
+      for (int j = 0; j < a.ntok; ++j) {
+        const float th = tanhf(kk[j * A + h * dh + d] + q[h * dh + d] + a.bb[d]);
+        snv += dw[h * a.ntok + j] * th;
+        sbb += dw[h * a.ntok + j] * nv[d] * (1.f - th * th);
+      }
+    a.pdnv[(long)n * dh + d] = snv;
+    a.pdbb[(long)n * dh + d] = sbb;
+  }
+}
+void fe_gst_bwd(const FeGst& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_gst_bwd, dim3(a.N), dim3(256), sizeof(float) * (FE_GST_LDS + 64), s, a);
+}
+
+// one block: d Wk = valᵀ·dkk, d bk = Σ_j dkk, d val += dkk·Wkᵀ, d tokens = d val (1 - val^2),
+// d v / d g through normed_v = g v / ||v||, d attention_b
+__global__ void k_fe_gst_final(FeGst a, const float* __restrict__ dkk, const float* __restrict__ dval,
+                               const float* __restrict__ dnv, const float* __restrict__ dbb, float* __restrict__ dwk,
+                               float* __restrict__ dbk, float* __restrict__ dtok, float* __restrict__ dv,
+                               float* __restrict__ dg, float* __restrict__ dbbo) {
+  const int tid = threadIdx.x, A = a.A, dh = A / a.heads;
+  for (int i = tid; i < a.tokd * A; i += blockDim.x) {
+    const int e = i / A, c = i % A;
+    float s = 0.f;
+    for (int j = 0; j < a.ntok; ++j) s += tanhf(a.tokens[j * a.tokd + e]) * dkk[j * A + c];
+    dwk[i] = s;
+  }
+  for (int c = tid; c < A; c += blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < a.ntok; ++j) s += dkk[j * A + c];
+    dbk[c] = s;
+  }
+  for (int i = tid; i < a.ntok * a.tokd; i += blockDim.x) {
+    const int j = i / a.tokd, e = i % a.tokd;
+    float s = dval[i];
+    for (int c = 0; c < A; ++c) s += dkk[j * A + c] * a.wk[(long)e * A + c];
+    const float vt = tanhf(a.tokens[i]);
+    dtok[i] = s * (1.f - vt * vt);
+  }
+  if (tid == 0) {
+    float ss = 0.f, vd = 0.f;
+    for (int d = 0; d < dh; ++d) {
+      ss += a.v[d] * a.v[d];
+      vd += a.v[d] * dnv[d];
+    }
+    const float nrm = sqrtf(ss), g = a.g[0];
+    dg[0] = vd / nrm;
+    for (int d = 0; d < dh; ++d) dv[d] = g * (dnv[d] / nrm - a.v[d] * vd / (nrm * nrm * nrm));
+    for (int d = 0; d < dh; ++d) dbbo[d] = dbb[d];
+  }
+}
+void fe_gst_final(const FeGst& a, const float* dkk, const float* dval, const float* dnv, const float* dbb, float* dwk,
+                  float* dbk, float* dtok, float* dv, float* dg, float* dbbo, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_gst_final, dim3(1), dim3(256), 0, s, a, dkk, dval, dnv, dbb, dwk, dbk, dtok, dv, dg, dbbo);
+}
+
+// ---- memory ---------------------------------------------------------------------------------------
+__global__ void k_fe_memory(const float* __restrict__ ENC, const float* __restrict__ STY, int B, int T, int E2,
+                            int SW, float* __restrict__ MEM) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int D = E2 + SW;
+  if (i >= (long)B * T * D) return;
+  const int d = (int)(i % D);
+  const long bt = i / D;
+  const int b = (int)(bt / T);
+  MEM[i] = d < E2 ? ENC[bt * E2 + d] : STY[(long)b * SW + d - E2];
+}
+void fe_memory(const float* ENC, const float* STY, int B, int T, int E2, int SW, float* MEM, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_memory, dim3(fe_blk((long)B * T * (E2 + SW))), dim3(256), 0, s, ENC, STY, B, T, E2, SW, MEM);
+}
+__global__ void k_fe_style_grad(const float* __restrict__ DMEM, int B, int T, int D, int E2, float* __restrict__ DSTY) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int SW = D - E2;
+  if (i >= B * SW) return;
+  const int b = i / SW, c = i % SW;
+  float s = 0.f;
+  for (int t = 0; t < T; ++t) s += DMEM[((long)b * T + t) * D + E2 + c];
+  DSTY[i] = s;
+}
+void fe_style_grad(const float* DMEM, int B, int T, int D, int E2, float* DSTY, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_style_grad, dim3(fe_blk((long)B * (D - E2))), dim3(256), 0, s, DMEM, B, T, D, E2, DSTY);
+}
+
+}  // namespace tt2

@@ -77,7 +77,12 @@ class TrainConfig(ctypes.Structure):
         ("precision", ctypes.c_int), ("clip_outputs", ctypes.c_int), ("clip_lo", ctypes.c_float),
         ("clip_hi", ctypes.c_float)] + [(n, ctypes.c_int) for n in (
             "postnet", "postnet_layers", "postnet_channels", "postnet_kernel")] + [
-        ("bn_momentum", ctypes.c_float), ("bn_eps", ctypes.c_float)]
+        ("bn_momentum", ctypes.c_float), ("bn_eps", ctypes.c_float)] + [
+        (n, ctypes.c_int) for n in (
+            "frontend", "n_symbols", "embedding_dim", "enc_conv_layers", "enc_conv_kernel",
+            "enc_conv_channels", "encoder_lstm_units", "emt_only", "num_gst", "num_heads",
+            "style_embed_depth", "style_att_dim", "reference_depth")] + [
+        ("reference_filters", ctypes.c_int * 6), ("max_T_ref", ctypes.c_int)]
 
 
 class DecoderState(ctypes.Structure):
@@ -139,6 +144,8 @@ SIGNATURES = {
     "tt2_train_finalize": (_I, [_P]),
     "tt2_train_bind_grads_dev": (_I, [_P, _P, ctypes.POINTER(ctypes.c_int64)]),
     "tt2_train_forward_backward_dev": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "tt2_train_forward_backward_text_dev": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P,
+                                                 _P, _I, _I, _P]),
     "tt2_train_apply_dev": (_I, [_P, _F, _I, _P]),
     "tt2_train_losses": (_I, [_P, _P, _P]),
     "tt2_train_get_tensor": (_I, [_P, ctypes.c_char_p, _I, _P]),

@@ -61,3 +61,15 @@ def postnet_masks(layers, B, T, C, rate=0.5, seed=5339):
     """Postnet dropout keep bits (modules.py:496-497, tacotron_dropout_rate 0.5, training=True):
     [layers, B, T, C] uint8."""
     return (np.random.default_rng(seed + 2).random((layers, B, T, C)) >= rate).astype(np.uint8)
+
+
+def enc_conv_masks(layers, B, T, C, rate=0.5, seed=5339):
+    """Encoder-convolution dropout keep bits (modules.py:496-497 in EncoderConvolutions,
+    tacotron_dropout_rate 0.5, training=True): [layers, B, T, C] uint8."""
+    return (np.random.default_rng(seed + 3).random((layers, B, T, C)) >= rate).astype(np.uint8)
+
+
+def enc_zoneout_masks(T, B, U, rate=0.1, seed=5339):
+    """Encoder BiLSTM training-zoneout keep bits by recurrence step (modules.py:236-240):
+    [T, 2 (fw, bw), 2 (c, h), B, U] uint8."""
+    return (np.random.default_rng(seed + 4).random((T, 2, 2, B, U)) >= rate).astype(np.uint8)

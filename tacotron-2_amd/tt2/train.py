@@ -28,7 +28,8 @@ def learning_rate(step, hp):
     return min(max(lr, hp.tacotron_final_learning_rate), init)
 
 
-def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32", postnet=True):
+def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32", postnet=True,
+                 frontend=False, max_T_ref=None):
     lib = _lib.load_library()
     cfg = _lib.TrainConfig()
     lib.tt2_train_default_config(ctypes.byref(cfg), batch, max_T_in, max_T_out)
@@ -71,6 +72,27 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
     cfg.postnet_layers = hp.postnet_num_layers
     cfg.postnet_channels = hp.postnet_channels
     cfg.postnet_kernel = hp.postnet_kernel_size[0]
+    # front end (encoder + reference encoders + GST, tacotron.py:215-308)
+    cfg.frontend = 1 if frontend else 0
+    if frontend:
+        from tacotron.utils.symbols import symbols
+        if not hp.use_gst:
+            raise NotImplementedError("use_gst=False front end is not built")
+        cfg.n_symbols = len(symbols)
+        cfg.embedding_dim = hp.embedding_dim
+        cfg.enc_conv_layers = hp.enc_conv_num_layers
+        cfg.enc_conv_kernel = hp.enc_conv_kernel_size[0]
+        cfg.enc_conv_channels = hp.enc_conv_channels
+        cfg.encoder_lstm_units = hp.encoder_lstm_units
+        cfg.emt_only = 1 if emt_only else 0
+        cfg.num_gst = hp.num_gst
+        cfg.num_heads = hp.num_heads
+        cfg.style_embed_depth = hp.style_embed_depth
+        cfg.style_att_dim = hp.style_att_dim
+        cfg.reference_depth = hp.reference_depth
+        for i, f in enumerate(hp.reference_filters):
+            cfg.reference_filters[i] = f
+        cfg.max_T_ref = max_T_ref or max_T_out
     return cfg
 
 
@@ -79,13 +101,15 @@ class TacotronTrainer(object):
     runs on the trainer's own torch stream (passed to the library explicitly)."""
 
     def __init__(self, hp, weights, batch, max_T_in, max_T_out, device=0, emt_only=False,
-                 precision="fp32", postnet=True):
+                 precision="fp32", postnet=True, frontend=False, max_T_ref=None):
         import torch
         self.torch = torch
         self.lib = _lib.load_library()
         self.hp = hp
         self.device = torch.device("cuda", device)
-        self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only, precision, postnet)
+        self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only, precision, postnet, frontend,
+                                max_T_ref)
+        self.frontend = frontend
         self.postnet = postnet
         self.B = batch
         h = ctypes.c_void_p()
@@ -163,6 +187,49 @@ class TacotronTrainer(object):
             ptr = (lambda x: None if x is None else ctypes.c_void_p(x.data_ptr()))
             check(self.lib.tt2_train_forward_backward_dev(
                 self.h, ptr(mem), ptr(lens), ptr(tg), ptr(st), ptr(pm), ptr(zm), ptr(pnm), T_in, T_out,
+                ctypes.c_void_p(self.stream.cuda_stream)))
+
+    def forward_backward_text(self, ids, lengths, ref_emt, ref_spk, targets, stop_targets,
+                              prenet_masks, zoneout_masks=None, postnet_masks=None,
+                              enc_conv_masks=None, enc_zoneout_masks=None):
+        """The whole configs[4] step (frontend context): ids [B,T_in] + lengths, reference mels
+        [B,T_ref,80] -> encoder / reference encoders / GST in training mode -> decoder + Postnet ->
+        backward through everything.  enc_conv_masks [layers,B,T_in,C] and enc_zoneout_masks
+        [T_in,2,2,B,U] are keep bits (None = no conv dropout / inference zoneout mix)."""
+        t = self.torch
+        if not self.frontend:
+            raise RuntimeError("trainer built without frontend=True")
+        with t.cuda.stream(self.stream):
+            ids_d = self._dev(ids, t.int32)
+            lens = self._dev(lengths, t.int32)
+            re = self._dev(ref_emt, t.float32)
+            rs = self._dev(ref_spk, t.float32)
+            tg = self._dev(targets, t.float32)
+            st = self._dev(stop_targets, t.float32)
+            pm = self._dev(prenet_masks, t.uint8)
+            zm = self._dev(zoneout_masks, t.uint8)
+            pnm = self._dev(postnet_masks, t.uint8) if self.postnet else None
+            em = self._dev(enc_conv_masks, t.uint8)
+            ezm = self._dev(enc_zoneout_masks, t.uint8)
+            B, T_in = ids_d.shape
+            T_out = tg.shape[1]
+            T_ref = re.shape[1]
+            if B != self.B:
+                raise ValueError("batch {} != trainer batch {}".format(B, self.B))
+            if rs is not None and tuple(rs.shape) != tuple(re.shape):
+                raise ValueError("ref_emt and ref_spk must have the same shape")
+            if tuple(pm.shape) != (T_out, 2, B, self.cfg.prenet_units):
+                raise ValueError("prenet_masks must be [T_out, 2, B, prenet_units]")
+            if em is not None and tuple(em.shape) != (self.cfg.enc_conv_layers, B, T_in,
+                                                      self.cfg.enc_conv_channels):
+                raise ValueError("enc_conv_masks must be [layers, B, T_in, channels]")
+            if ezm is not None and tuple(ezm.shape) != (T_in, 2, 2, B, self.cfg.encoder_lstm_units):
+                raise ValueError("enc_zoneout_masks must be [T_in, 2, 2, B, encoder_lstm_units]")
+            self._keep = (ids_d, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+            ptr = (lambda x: None if x is None else ctypes.c_void_p(x.data_ptr()))
+            check(self.lib.tt2_train_forward_backward_text_dev(
+                self.h, ptr(ids_d), ptr(lens), ptr(re), ptr(rs), T_ref, ptr(tg), ptr(st), ptr(pm),
+                ptr(zm), ptr(pnm), ptr(em), ptr(ezm), T_in, T_out,
                 ctypes.c_void_p(self.stream.cuda_stream)))
 
     def allreduce_grads(self, group=None):

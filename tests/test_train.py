@@ -420,3 +420,152 @@ def test_gpu_train_full_size_properties():
         assert abs(a - b) < 1e-3 * abs(a), (k, a, b)
     a, b = res["fp32"][0]["grad_norm"], res["bf16"][0]["grad_norm"]
     assert abs(a - b) < 2e-2 * a, (a, b)
+
+
+def test_frontend_oracle_inference_mode_matches_numpy_oracle():
+    """The torch front-end restatement with moving BN statistics and no masks IS the inference
+    graph: its memory equals oracle/tacotron_ref.py's encoder + style path (pins the restatement
+    the front-end gradients come from)."""
+    import torch
+    hp = small_hparams()
+    W = init_tacotron_weights(hp, seed=5339)
+    from tt2.synthetic import tacotron_inputs
+    ids, lens, re, rs = tacotron_inputs(3, 9, 70, seed=4)
+    Wt = {n: torch.tensor(np.asarray(W[n]), dtype=torch.float64) for n in TRN.frontend_var_names()}
+    mem, _ = TRN.frontend_forward(Wt, ids, lens, re, rs, moving=W)
+    oh = oracle_hp(hp)
+    enc = TR.encoder(ids, lens, W, oh, np.float64)
+    st = TR.style_embedding(re, rs, W, oh, np.float64)
+    mask = (np.arange(9)[None] < lens[:, None])[..., None]
+    want = np.concatenate([enc, np.broadcast_to(st[:, None], (3, 9, st.shape[1]))], -1)
+    np.testing.assert_allclose(mem.numpy() * mask, want * mask, rtol=0, atol=1e-9)
+
+
+def _front_case(hp, B=3, T_in=9, T_out=6, T_ref=70, seed=32, masks=True):
+    from tt2.synthetic import enc_conv_masks, enc_zoneout_masks, tacotron_inputs
+    W = init_tacotron_weights(hp, seed=5339)
+    ids, lens, re, rs = tacotron_inputs(B, T_in, T_ref, seed=seed)
+    _, _, tg, st = train_batch(B, T_in, T_out, memory_width(hp), seed=seed)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=seed)
+    zm = zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=seed)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=seed)
+    em = enc_conv_masks(hp.enc_conv_num_layers, B, T_in, hp.enc_conv_channels, seed=seed) if masks else None
+    ezm = enc_zoneout_masks(T_in, B, hp.encoder_lstm_units, seed=seed) if masks else None
+    return W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm
+
+
+def test_frontend_oracle_gradients_match_finite_differences():
+    """Spot-check the front-end autograd (embedding, encoder conv / BN / dropout, BiLSTM with
+    training zoneout and lengths, refnet conv2d / BN / GRU / dense, GST) with central differences."""
+    hp = small_hparams()
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, B=2, T_in=6, T_out=3, T_ref=40)
+    _, g, _ = TRN.train_grads_frontend(W, ids, lens, re, rs, tg, st, pm, zm, em, ezm, reg_weight=1e-3,
+                                       postnet_masks=pnm)
+
+    def loss_of(W2):
+        names = TRN.frontend_var_names() + TRN.train_var_names() + TRN.postnet_var_names()
+        Wt = {n: torch.tensor(np.asarray(W2[n]), dtype=torch.float64) for n in names}
+        mem, _ = TRN.frontend_forward(Wt, ids, lens, re, rs, em, ezm)
+        tg_t = torch.tensor(tg, dtype=torch.float64)
+        fr, sl, _ = TRN.forward(Wt, mem, lens, tg_t, torch.tensor(pm, dtype=torch.float64),
+                                torch.tensor(zm, dtype=torch.float64))
+        b, s, r = TRN.losses(fr, sl, tg_t, torch.tensor(st, dtype=torch.float64), Wt, 1e-3)
+        dec = TRN.clip_decoder_output(fr)
+        proj, _ = TRN.postnet_train(Wt, dec, torch.tensor(pnm, dtype=torch.float64))
+        after = ((TRN.clip_decoder_output(dec + proj) - tg_t) ** 2).mean()
+        return float(b + s + r + after)
+
+    rng = np.random.default_rng(3)
+    P = "Tacotron_model/inference/"
+    for name in [P + "inputs_embedding",
+                 P + "encoder_convolutions/conv_layer_2_encoder_convolutions/conv1d/kernel",
+                 P + "encoder_convolutions/conv_layer_1_encoder_convolutions/batch_normalization/gamma",
+                 P + "encoder_LSTM/bidirectional_rnn/bw/lstm_cell/kernel",
+                 P + "refnet_emt/conv2d_1/conv2d/kernel", P + "refnet_spk/rnn/gru_cell/gates/kernel",
+                 P + "refnet_emt/dense/kernel", P + "style_tokens_spk",
+                 P + "Multihead-attention-emt/attention_v", P + "Multihead-attention-spk/attention_g"]:
+        w = np.asarray(W[name], np.float64)
+        idx = np.unravel_index(np.argmax(np.abs(g[name])), w.shape) if w.ndim else ()
+        eps = 1e-5
+        Wp, Wm = dict(W), dict(W)
+        wp, wm = w.copy(), w.copy()
+        wp[idx] += eps
+        wm[idx] -= eps
+        Wp[name], Wm[name] = wp, wm
+        fd = (loss_of(Wp) - loss_of(Wm)) / (2 * eps)
+        assert abs(fd - g[name][idx]) < 1e-5 + 1e-4 * abs(fd), (name, fd, g[name][idx])
+
+
+def _relu_margin(W, ids, re, rs, em):
+    """Smallest |pre-activation| of every front-end ReLU (encoder convs; refnet BN outputs) in
+    float64: below ~1e-6 an fp32 device run may take the other side of the kink than the float64
+    oracle, and one flipped element moves a batch-norm parameter's gradient by percents."""
+    P = "Tacotron_model/inference/"
+    Wt = {n: torch.tensor(np.asarray(W[n]), dtype=torch.float64) for n in TRN.frontend_var_names()}
+    m = np.inf
+    for tag, ref in (("emt", re), ("spk", rs)):
+        r = TRN.RN.format(tag)
+        h = torch.as_tensor(ref, dtype=torch.float64)[..., None]
+        for i in range(6):
+            s = r + "conv2d_{}/".format(i)
+            a = TRN._conv2d_same_s2(h, Wt[s + "conv2d/kernel"], Wt[s + "conv2d/bias"])
+            y, _ = TRN._bn_train(a, Wt[s + "batch_normalization/gamma"],
+                                 Wt[s + "batch_normalization/beta"], (0, 1, 2))
+            m = min(m, float(y.abs().min()))
+            h = torch.relu(y)
+    x = Wt[P + "inputs_embedding"][torch.as_tensor(ids).long()]
+    for i in range(1, 4):
+        s = TRN.EC.format(i)
+        k = Wt[s + "conv1d/kernel"]
+        pad = (k.shape[0] - 1) // 2
+        xp = torch.nn.functional.pad(x, (0, 0, pad, k.shape[0] - 1 - pad))
+        z = torch.einsum("btck,kcn->btn", xp.unfold(1, k.shape[0], 1), k) + Wt[s + "conv1d/bias"]
+        m = min(m, float(z.abs().min()))
+        y, _ = TRN._bn_train(torch.relu(z), Wt[s + "batch_normalization/gamma"],
+                             Wt[s + "batch_normalization/beta"], (0, 1))
+        x = y if em is None else y / 0.5 * torch.as_tensor(em[i - 1], dtype=torch.float64)
+    return m
+
+
+@pytest.mark.parametrize("masks", [True, False])
+def test_frontend_case_has_relu_margin(masks):
+    """The GPU front-end parity case keeps every ReLU input >= 1e-5 away from the kink."""
+    hp = small_hparams()
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, masks=masks)
+    assert _relu_margin(W, ids, re, rs, em) > 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("masks", [True, False])
+def test_gpu_train_frontend_matches_oracle(masks):
+    """The whole configs[4] step from ids + reference mels (tt2_train_forward_backward_text_dev):
+    every front-end, decoder and Postnet gradient within 2e-4 (relative to its max) of the torch
+    float64 oracle, the losses, and the front-end BN moving averages after apply."""
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, masks=masks)
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1])
+    try:
+        tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+        L = tr.losses()
+        (b, s_, r, a), g, stats = TRN.train_grads_frontend(W, ids, lens, re, rs, tg, st, pm, zm, em, ezm,
+                                                           hp.tacotron_reg_weight, postnet_masks=pnm)
+        assert abs(L["before"] - b) < 1e-4 * b and abs(L["after"] - a) < 1e-4 * a
+        assert abs(L["regularization"] - r) < 1e-4 * r + 1e-12
+        for n in TRN.frontend_var_names() + TRN.train_var_names() + TRN.postnet_var_names():
+            got = tr.get(n, 1, np.asarray(W[n]).shape)
+            if np.abs(g[n]).max() < 1e-12:   # a conv bias feeding batch-statistics BN: exactly 0
+                assert np.abs(got).max() < 1e-6, (n, np.abs(got).max())
+                continue
+            assert _rel(got, g[n]) < 2e-4, (n, _rel(got, g[n]))
+        tr.apply(1)
+        P = "Tacotron_model/inference/"
+        scopes = ["encoder_convolutions/conv_layer_{}_encoder_convolutions/".format(i) for i in (1, 2, 3)]
+        scopes += ["refnet_{}/conv2d_{}/".format(t, i) for t in ("emt", "spk") for i in range(6)]
+        for sc, (mean, var) in zip(scopes, stats):
+            mm = tr.get(P + sc + "batch_normalization/moving_mean", 0, mean.shape)
+            want = TRN.bn_moving_update(np.asarray(W[P + sc + "batch_normalization/moving_mean"], np.float64), mean)
+            np.testing.assert_allclose(mm, want, rtol=1e-5, atol=1e-5, err_msg=sc)
+    finally:
+        tr.close()
