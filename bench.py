@@ -53,6 +53,10 @@ def parse():
     p.add_argument("--train-t-in", type=int, default=150)
     p.add_argument("--train-t-out", type=int, default=800)
     p.add_argument("--train-steps", type=int, default=2)
+    p.add_argument("--train-decoder-only", action="store_true",
+                   help="time the decoder + Postnet slice from a given memory (round-1 leg) instead "
+                        "of the whole step from ids + reference mels")
+    p.add_argument("--train-t-ref", type=int, default=800, help="reference mel frames (configs[4])")
     p.add_argument("--train-precision", default="bf16", choices=["bf16", "fp32"],
                    help="configs[4] names bf16 (GEMM operands; fp32 accumulation and state)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -195,6 +199,24 @@ def train_step_flops(B, T_in, T, hp, D):
     return B * T * (3 * row + 2 * att + 3 * post) + 3 * 2 * B * T_in * D * A
 
 
+def front_end_flops(B, Ti, T_ref, hp, emt_only=False):
+    """Forward FLOPs of the training front end (matrix products): encoder convs, BiLSTM input and
+    recurrent products, reference-encoder conv2d stacks, GRU, dense, GST."""
+    E, C, K, U = hp.embedding_dim, hp.enc_conv_channels, hp.enc_conv_kernel_size[0], hp.encoder_lstm_units
+    M = B * Ti
+    fl = sum(2.0 * M * K * (E if i == 0 else C) * C for i in range(hp.enc_conv_num_layers))
+    fl += 2.0 * M * C * 8 * U + 2.0 * M * U * 8 * U
+    H, W, ci = T_ref, hp.num_mels, 1
+    ref = 0.0
+    for f in hp.reference_filters:
+        H, W = (H + 1) // 2, (W + 1) // 2
+        ref += 2.0 * B * H * W * 9 * ci * f
+        ci = f
+    D = hp.reference_depth
+    ref += 2.0 * B * H * (W * ci + D) * 3 * D + 2.0 * B * D * 128
+    return fl + ref * (1 if emt_only else 2)
+
+
 def bench_train(a, rank, world, local, barrier, max_over_ranks):
     """configs[4]: teacher-forced decoder training step (fork-default widths, D_mem 1024) at
     B = 64 rows per GPU, T_in = 150, T_out = 800 (LJSpeech-shaped); data-parallel over ranks with
@@ -210,7 +232,10 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
     B, Ti, T = a.train_batch, a.train_t_in, a.train_t_out
     D = memory_width(hp)
     W = init_tacotron_weights(hp, seed=hp.tacotron_random_seed)
-    tr = TacotronTrainer(hp, W, B, Ti, T, local, precision=a.train_precision)
+    front = not a.train_decoder_only
+    Tr = a.train_t_ref
+    tr = TacotronTrainer(hp, W, B, Ti, T, local, precision=a.train_precision, frontend=front,
+                         max_T_ref=Tr)
     if world > 1:
         tr.bind_grad_buffer()
     dev = torch.device("cuda", local)
@@ -220,10 +245,20 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
     batch.append(torch.from_numpy(zoneout_masks(T, B, hp.decoder_lstm_units, seed=7 + rank)).to(dev))
     batch.append(torch.from_numpy(postnet_masks(hp.postnet_num_layers, B, T, hp.postnet_channels,
                                                 seed=7 + rank)).to(dev))
+    if front:  # the whole configs[4] step: ids + reference mels, encoder dropout / zoneout bits
+        from tt2.synthetic import enc_conv_masks, enc_zoneout_masks, tacotron_inputs
+        ids, tlens, re, rs = tacotron_inputs(B, Ti, Tr, seed=1234 + rank)
+        fb = [torch.from_numpy(x).to(dev) for x in (ids, tlens, re, rs)] + batch[2:]
+        fb.append(torch.from_numpy(enc_conv_masks(hp.enc_conv_num_layers, B, Ti, hp.enc_conv_channels,
+                                                  seed=7 + rank)).to(dev))
+        fb.append(torch.from_numpy(enc_zoneout_masks(Ti, B, hp.encoder_lstm_units, seed=7 + rank)).to(dev))
     losses = []
 
     def step():
-        tr.forward_backward(*batch)
+        if front:
+            tr.forward_backward_text(*fb)
+        else:
+            tr.forward_backward(*batch)
         tr.allreduce_grads()
         tr.apply()
 
@@ -240,7 +275,7 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
     L = tr.losses()
     tr.close()
     ms = 1e3 * el / a.train_steps
-    fl = train_step_flops(B, Ti, T, hp, D)
+    fl = train_step_flops(B, Ti, T, hp, D) + (3.0 * front_end_flops(B, Ti, Tr, hp) if front else 0.0)
     tf = fl / (ms * 1e-3) / 1e12
     peak = 2500.0 if a.train_precision == "bf16" else 157.3
     return dict(metric="mel-frames/sec (teacher-forced training step)",
@@ -249,9 +284,12 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
                 forward_backward_ms=round(L["forward_backward_ms"], 2),
                 loss_first=round(losses[0]["loss"], 5), loss_last=round(L["loss"], 5),
                 grad_norm=round(L["grad_norm"], 5), dtype=a.train_precision,
-                config=dict(workload="configs[4]: Tacotron-2 decoder training step (teacher-forced), "
-                                     "+ Postnet (training BN/dropout), B={} rows/GPU, T_in={}, T_out={}, "
-                                     "D_mem={}".format(B, Ti, T, D),
+                config=dict(workload=("configs[4]: whole Tacotron-2 training step from ids + reference mels "
+                                      "(encoder, 2 reference encoders + GST, teacher-forced decoder, Postnet; "
+                                      "training BN / dropout / zoneout), B={} rows/GPU, T_in={}, T_out={}, "
+                                      "T_ref={}, D_mem={}".format(B, Ti, T, Tr, D)) if front else
+                                     ("configs[4] slice: decoder + Postnet training step from a given memory, "
+                                      "B={} rows/GPU, T_in={}, T_out={}, D_mem={}".format(B, Ti, T, D)),
                             global_batch=B * world, parallelism="dp{} (RCCL grad all-reduce)".format(world)),
                 roofline=dict(bound="mfma", achieved=round(tf, 2), peak=peak, unit="TFLOP/s",
                               frac=round(tf / peak, 4), algorithmic_flops_per_step=int(fl),
