@@ -85,6 +85,13 @@ typedef struct tt2_config {
   int max_T_in;            /* longest character sequence incl. EOS */
   int max_T_ref;           /* longest reference mel (frames) */
   int max_iters;           /* decoder step capacity (hparams.max_iters) */
+  /* Tacotron_emt_attn (tacotron_emt_attn.py, chosen by args.emt_attn at synthesizer.py:24):
+   * memory = encoder outputs only, no GST; the decoder attends every step over the emotion
+   * reference encoder's outputs (or 24 style tokens) and feeds that context to LSTM-1
+   * (Architecture_wrappers.py:203-211, 228-240).  use_gst is ignored when emt_attn != 0. */
+  int emt_attn;            /* args.attn: 0 = Tacotron model, 1 'simple', 2 'multihead', 3 'style_tokens' */
+  int emt_ref_gru;         /* args.emt_ref_gru: 0 'none', 1 'gru', 2 'gru_multi' (modules.py:35-55) */
+  int n_emt;               /* style_tokens: one-hot emotion label width (synthesizer.py:45: 4) */
 } tt2_config;
 
 typedef struct tt2_ctx tt2_ctx;
@@ -152,6 +159,15 @@ typedef struct tt2_decoder_state {
 tt2_status tt2_decoder_step(tt2_ctx* ctx, const float* frame_in, const uint8_t* prenet_masks,
                             const tt2_decoder_state* state_in, tt2_decoder_state* state_out,
                             float* frame_out, float* stop_out, float* alignments_out);
+
+/* Tacotron_emt_attn: emotion labels [B] int32 of the next tt2_encode (the emt_labels placeholder,
+ * synthesizer.py:35, one-hot in the style_tokens query, Architecture_wrappers.py:236; an
+ * out-of-range label is a zero one-hot row like tf.one_hot).  Persist until set again. */
+tt2_status tt2_set_emt_labels(tt2_ctx* ctx, const int32_t* labels, int B);
+/* Tacotron_emt_attn: emotion attention weights of the last decode (tower_alignments_emt,
+ * tacotron_emt_attn.py / Architecture_wrappers.py:251) as out[n_steps][B][heads][T_v]; *heads and
+ * *T_v receive the shape (out may be NULL to query it after tt2_encode). */
+tt2_status tt2_emt_alignments(tt2_ctx* ctx, float* out, int32_t* heads, int32_t* T_v);
 
 /* decoder clip + Postnet + postnet_projection + final clip (tacotron.py:362-381) on the frames of
  * the last tt2_decode (frames_in == NULL) or on caller frames [B,T,80].

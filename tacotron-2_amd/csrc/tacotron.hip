@@ -15,6 +15,7 @@
 #include "common.h"
 #include "decode_persist.h"
 #include "gemm.h"
+#include "emt.h"
 #include "step.h"
 
 namespace tt2 {
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(256) void k_ref_gru_gst(RefGstArgs a) {
     ref[tid] = tanhf(s + a.bd[tid]);
     a.ref_out[b * 128 + tid] = ref[tid];
   }
+  if (!a.tokens) return;  // reference embedding only (uniform across the block)
   // GST values = tanh(tokens)
   for (int i = tid; i < a.ntok * a.tokd; i += blockDim.x) vals[i] = tanhf(a.tokens[i]);
   __syncthreads();
@@ -1176,6 +1178,9 @@ struct tt2_ctx {
   bool pd_dev_ok = false; // all PD_NB work-groups can be resident on this device
   bool last_pd = false;   // the last decode ran the persistent kernel
   tt2::DevBuf q_wt, pre_w2t, keysT, valuesT, pd_ctl, H1x, H2x, Ex, CTXx, SSx, PPx, PREx;
+  // Tacotron_emt_attn variant (emt.h): off for the Tacotron model
+  tt2::EmtModel emt;
+  std::vector<int> emt_labels;  // tt2_set_emt_labels (style_tokens)
   hipEvent_t pd_ev[2] = {nullptr, nullptr};
   float pd_kernel_ms = 0.f;
 };
@@ -1276,8 +1281,10 @@ static void finalize(tt2_ctx* c) {
     upload(c->enc_wh, wh);
     c->kg_wmax_enc = absmax(wh);
   }
-  // reference encoders + GST
+  // reference encoders + GST (emt variant: convolutions of refnet_emt, whose outputs emt.hip
+  // consumes, and refnet_spk's GRU + dense; no style tokens)
   const char* tags[2] = {"emt", "spk"};
+  const bool emt_model = c->emt.on();
   for (int r = 0; r < c->nref; ++r) {
     auto& R = c->ref[r];
     const std::string s = P + "refnet_" + tags[r] + "/";
@@ -1292,6 +1299,8 @@ static void finalize(tt2_ctx* c) {
       F = (F + 1) / 2;
     }
     const int gin = F * ci, D = cfg.reference_depth;
+    R.gin = gin;
+    if (emt_model && r == 0) continue;
     {
       const auto& kg = need(wm, s + "rnn/gru_cell/gates/kernel", {gin + D, 2 * D});
       const auto& bg = need(wm, s + "rnn/gru_cell/gates/bias", {2 * D});
@@ -1312,6 +1321,7 @@ static void finalize(tt2_ctx* c) {
     }
     upload(R.kd, need(wm, s + "dense/kernel", {D, 128}));
     upload(R.bd, need(wm, s + "dense/bias", {128}));
+    if (emt_model) continue;
     const int tokd = cfg.style_embed_depth / cfg.num_heads, Aa = cfg.style_att_dim;
     upload(R.tok, need(wm, P + "style_tokens_" + tags[r], {cfg.num_gst, tokd}));
     const std::string mh = P + "Multihead-attention-" + tags[r] + "/";
@@ -1323,6 +1333,7 @@ static void finalize(tt2_ctx* c) {
     upload(R.ag, need(wm, mh + "attention_g", {}));
     upload(R.ab, need(wm, mh + "attention_b", {Aa / cfg.num_heads}));
   }
+  emt_load(c->emt, wm, P);
   upload(c->mem_k, need(wm, P + "memory_layer/kernel", {c->Dm, c->A}));
   split_weights(c->mem_k.as<float>(), c->Dm, c->A, c->A, c->mem_k_s, nullptr);
   c->kpart.alloc(sizeof(float) * (8u << 20));
@@ -1353,9 +1364,10 @@ static void finalize(tt2_ctx* c) {
     // layer 1 rows: [prenet P | context_enc E2 | context_style SW | h H]; layer 2 rows: [h1_new H | h H]
     const std::string s = P + "decoder/decoder_LSTM/multi_rnn_cell/cell_" + std::to_string(l) + "/lstm_cell/";
     const int H = c->H, N = 4 * H;
-    const int Kfull = l == 0 ? c->P + c->Dm + H : 2 * H;
+    // layer-1 rows: [prenet | context (enc, style) | emotion block (emt variant) | h]
+    const int Kfull = l == 0 ? c->P + c->Dm + c->emt.XW + H : 2 * H;
     const int Kc = l == 0 ? c->K1 : H;   // critical rows
-    const int Kh0 = l == 0 ? c->P + c->Dm : H;  // first recurrent row
+    const int Kh0 = l == 0 ? c->K1 + c->SW : H;  // first recurrent row
     const auto& k = need(wm, s + "kernel", {Kfull, N});
     const auto& b = need(wm, s + "bias", {N});
     auto cols = lstm_cols(H);
@@ -1372,7 +1384,7 @@ static void finalize(tt2_ctx* c) {
       upload_scaled(l == 0 ? c->pd_l1_wh : c->pd_l2_wh, wr, KG_SB);
     }
     upload(l == 0 ? c->l1_b : c->l2_b, bt);
-    if (l == 0) {  // style rows, lstm column order, row-major [SW][4H] (B operand of the GS GEMM)
+    if (l == 0 && c->SW) {  // style rows, lstm column order, row-major [SW][4H] (B operand of the GS GEMM)
       std::vector<float> ws((size_t)c->SW * N);
       for (int r = 0; r < c->SW; ++r)
         for (int i = 0; i < N; ++i) ws[(size_t)r * N + i] = k.data[(size_t)(c->P + c->E2 + r) * N + cols[i]];
@@ -1449,7 +1461,7 @@ static void finalize(tt2_ctx* c) {
     std::vector<float> ws((size_t)c->SW * NPF, 0.f);                // context_style rows
     for (int r = 0; r < c->SW; ++r)
       for (int n = 0; n < NPF; ++n) ws[(size_t)r * NPF + n] = W[(size_t)(c->Kp + r) * NPF + n];
-    upload(c->proj_ws, ws);
+    if (c->SW) upload(c->proj_ws, ws);
     std::vector<float> pb(NPF, 0.f);
     for (int n = 0; n < c->nm; ++n) pb[n] = fb.data[n];
     pb[c->nm] = sb.data[0];
@@ -1553,9 +1565,11 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
   for (int b = 0; b < B; ++b)
     TT2_CHECK(lens_h[b] >= 1 && lens_h[b] <= T, TT2_ERR_INVALID_ARG, "input_lengths must be in [1, T_in]");
   const int BT = B * T;
+  if (c->emt.on())  // emotion labels (style_tokens query), pinned by tt2_set_emt_labels
+    TT2_HIP(hipMemcpyAsync(c->emt.labels.p, c->emt_labels.data(), sizeof(int) * 32, hipMemcpyHostToDevice, s));
   // fork: the reference encoders (GST) depend only on the reference mels -> own stream, joined
   // before k_memory; they fill the CUs the 128-work-group persistent BiLSTM leaves idle
-  const hipStream_t sr = (cfg.use_gst && c->ref_stream) ? c->ref_stream : s;
+  const hipStream_t sr = ((cfg.use_gst || c->emt.on()) && c->ref_stream) ? c->ref_stream : s;
   if (sr != s) {
     TT2_HIP(hipEventRecord(c->ref_ev[0], s));
     TT2_HIP(hipStreamWaitEvent(sr, c->ref_ev[0], 0));
@@ -1618,7 +1632,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
   }
   TT2_HIP(hipGetLastError());
   // reference encoders + GST
-  if (cfg.use_gst) {
+  if (cfg.use_gst || c->emt.on()) {
     for (int r = 0; r < c->nref; ++r) {
       auto& R = c->ref[r];
       const int TR = T_ref[r];
@@ -1644,6 +1658,10 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
       }
       const int D = cfg.reference_depth;
       TT2_CHECK(Wd * C == R.gin, TT2_ERR_SHAPE_MISMATCH, "reference encoder: GRU input width mismatch");
+      if (c->emt.on() && r == 0) {  // all_outputs=True: attended values of the emotion attention
+        emt_encode(c->emt, x, B, H, sr);
+        continue;
+      }
       c->refxg.alloc(sizeof(float) * (size_t)B * H * 3 * D);
       {  // x rows of the GRU gates + candidate kernels for every frame at once
         GemmArgs g;
@@ -1657,7 +1675,8 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
       RefGstArgs a;
       a.xg = c->refxg.as<float>(); a.T2 = H; a.D = D;
       a.whg = R.whg.as<float>(); a.whc = R.whc.as<float>();
-      a.kd = R.kd.as<float>(); a.bd = R.bd.as<float>(); a.tokens = R.tok.as<float>();
+      a.kd = R.kd.as<float>(); a.bd = R.bd.as<float>();
+      a.tokens = c->emt.on() ? nullptr : R.tok.as<float>();  // null: GRU + dense only (refnet_spk of the emt variant)
       a.kq = R.kq.as<float>(); a.bq = R.bq.as<float>(); a.kk = R.kk.as<float>(); a.bk = R.bk.as<float>();
       a.av = R.av.as<float>(); a.ag = R.ag.as<float>(); a.ab = R.ab.as<float>();
       a.ntok = cfg.num_gst; a.tokd = cfg.style_embed_depth / cfg.num_heads; a.A = cfg.style_att_dim;
@@ -1669,6 +1688,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
       TT2_HIP(hipGetLastError());
     }
   }
+  if (c->emt.attn == EMT_STYLE_TOKENS) emt_encode(c->emt, nullptr, B, 0, sr);
   if (sr != s) {  // join
     TT2_HIP(hipEventRecord(c->ref_ev[1], sr));
     TT2_HIP(hipStreamWaitEvent(s, c->ref_ev[1], 0));
@@ -1686,7 +1706,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
   }
-  {  // per-utterance style terms of the decoder: GS = style·W_lstm1[style rows], PS = style·W_proj[style rows]
+  if (c->SW) {  // per-utterance style terms of the decoder: GS = style·W_lstm1[style rows], PS = style·W_proj[style rows]
     GemmArgs g;
     g.M = B; g.N = 4 * c->H; g.K = c->SW; g.A = c->style.as<float>(); g.lda = c->SW;
     g.Bw = c->l1_ws.as<float>(); g.ldb = 4 * c->H; g.Cout = c->GS0.as<float>(); g.ldc = 4 * c->H;
@@ -1739,6 +1759,11 @@ static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, 
   }
   a.frames = frames_d; a.stop = stop_d; a.align = align_d;
   return a;
+}
+
+// refnet_spk output of the emt variant (null when it has none)
+static const float* emt_spk(tt2_ctx* c) {
+  return c->emt.spk ? c->ref_out.as<float>() + (size_t)c->cfg.max_batch * 128 : nullptr;
 }
 
 // The per-step launches (shared by the captured decode graph and the profiler).  `par` = step
@@ -1830,6 +1855,8 @@ static void enqueue_step(tt2_ctx* c, const DecArgs& a, int i, int t, hipStream_t
   }
   if (c->side_mode == 1 && i > 0) TT2_HIP(hipStreamWaitEvent(s, c->sev[2 * ((i - 1) & 1) + 1], 0));
   launch_lstm(lstm_args(c, a, 1, par), c->H, s);
+  if (c->emt.on())  // emotion context of step t -> LSTM-1 input block of step t+1
+    emt_step_launch(c->emt, &a.ctl->done, a.Xp, a.X1[par ^ 1], c->P + c->E2, emt_spk(c), t, s);
   if (c->side_mode == 1) {  // RG1 for step i+1 from h1(i)
     TT2_HIP(hipEventRecord(c->sev[5], s));
     TT2_HIP(hipStreamWaitEvent(s2, c->sev[5], 0));
@@ -1851,7 +1878,7 @@ static void check_encoder(tt2_ctx* c) {
 }
 
 static bool pd_fits(tt2_ctx* c) {
-  return c->pd_mode == 1 && c->pd_dev_ok && c->kg_wmax_dec < KG_BMAX && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
+  return !c->emt.on() && c->pd_mode == 1 && c->pd_dev_ok && c->kg_wmax_dec < KG_BMAX && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
          c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= PD_TMAX && c->B <= 32;
 }
 
@@ -1952,6 +1979,7 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
   TT2_HIP(hipMemsetAsync(c->cum.p, 0, c->cum.bytes, s));
   TT2_HIP(hipMemsetAsync(c->max_att.p, 0, c->max_att.bytes, s));
   TT2_HIP(hipMemsetAsync(c->ctl.p, 0, sizeof(DecCtl), s));
+  emt_init_launch(c->emt, emt_spk(c), c->X1[0].as<float>(), c->X1[1].as<float>(), c->P + c->E2, s);
   if (!masks_d) {  // prenet dropout keep bits from the counter-based device RNG
     const long n = (long)max_iters * 2 * c->B * c->P;
     c->gmasks.alloc((size_t)n);
@@ -2095,6 +2123,7 @@ void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_re
   c->clip_outputs = 1; c->stop_at_any = 0; c->mask_encoder = 1; c->cumulative_weights = 1;
   c->synthesis_constraint = 0; c->constraint_monotonic = 0; c->attention_win_size = 7;
   c->max_batch = max_batch; c->max_T_in = max_T_in; c->max_T_ref = max_T_ref; c->max_iters = max_iters;
+  c->emt_attn = 0; c->emt_ref_gru = 0; c->n_emt = 4;
 }
 
 tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
@@ -2126,13 +2155,26 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     c->KLp = (c->KL + 15) / 16 * 16; c->Fp = (c->F + 15) / 16 * 16;
     TT2_CHECK(c->KLp <= 64 && c->Fp <= 64, TT2_ERR_INVALID_ARG, "attention_kernel / attention_filters must be <= 64");
     TT2_CHECK(c->A <= 256, TT2_ERR_INVALID_ARG, "attention_dim must be <= 256");
-    c->nref = cfg->use_gst ? (cfg->emt_only ? 1 : 2) : 0;
-    c->SW = cfg->use_gst ? c->nref * cfg->style_embed_depth : 0;
+    const bool emt = cfg->emt_attn != EMT_OFF;
+    if (emt) {
+      // Tacotron_emt_attn: the attention memory is the encoder output alone (tacotron_emt_attn.py:
+      // 244-246); refnet_emt feeds the emotion attention, refnet_spk the LSTM input; no GST
+      c->nref = cfg->emt_attn == EMT_STYLE_TOKENS ? 0 : (cfg->emt_only ? 1 : 2);
+      c->SW = 0;
+    } else {
+      c->nref = cfg->use_gst ? (cfg->emt_only ? 1 : 2) : 0;
+      c->SW = cfg->use_gst ? c->nref * cfg->style_embed_depth : 0;
+      TT2_CHECK(cfg->use_gst, TT2_ERR_INVALID_ARG, "use_gst=False (paper Tacotron-2 memory) is not built yet");
+    }
     c->Dm = 2 * c->U + c->SW;
     TT2_CHECK(c->Dm % 64 == 0, TT2_ERR_INVALID_ARG, "memory width must be a multiple of 64");
-    TT2_CHECK(cfg->use_gst, TT2_ERR_INVALID_ARG, "use_gst=False (paper Tacotron-2 memory) is not built yet");
     c->E2 = 2 * c->U;
-    c->K1 = c->P + c->E2; c->Kp = c->H + c->E2;
+    emt_configure(c->emt, cfg->emt_attn, cfg->emt_ref_gru, cfg->emt_only, cfg->n_emt, c->H, c->A, cfg->style_att_dim,
+                  cfg->num_heads, cfg->reference_depth, c->nm, cfg->reference_filters, cfg->max_batch,
+                  cfg->max_T_ref, cfg->max_iters);
+    c->emt_labels.assign(32, 0);
+    // LSTM-1 critical rows: [prenet | context_enc | emotion block (emt variant)]
+    c->K1 = c->P + c->E2 + c->emt.XW; c->Kp = c->H + c->E2;
     TT2_CHECK(c->E2 % 64 == 0, TT2_ERR_INVALID_ARG, "2*encoder_lstm_units must be a multiple of 64");
     c->NPJ = ((c->nm + 1 + 15) / 16) * 16;
     c->NPF = c->NPJ + c->P;
@@ -2189,8 +2231,8 @@ tt2_status tt2_encode(tt2_ctx* c, const int32_t* ids, const int32_t* lengths, in
     TT2_CHECK(c && ids && lengths, TT2_ERR_INVALID_ARG, "tt2_encode: null argument");
     TT2_CHECK(B >= 1 && B <= c->cfg.max_batch, TT2_ERR_SHAPE_MISMATCH, "batch exceeds capacity");
     TT2_CHECK(T_in >= 1 && T_in <= c->cfg.max_T_in, TT2_ERR_SHAPE_MISMATCH, "T_in exceeds capacity");
-    TT2_CHECK(!c->cfg.use_gst || (ref_emt && (c->nref < 2 || ref_spk)), TT2_ERR_INVALID_ARG,
-              "must provide references");  // tacotron.py:66-67
+    TT2_CHECK(c->nref == 0 || (ref_emt && (c->nref < 2 || ref_spk)), TT2_ERR_INVALID_ARG,
+              "must provide references");  // tacotron.py:66-67, tacotron_emt_attn.py:72-73
     TT2_HIP(hipSetDevice(c->dev));
     hipStream_t s = c->stream;
     TT2_HIP(hipMemcpyAsync(c->ids.p, ids, sizeof(int) * B * T_in, hipMemcpyHostToDevice, s));
@@ -2221,6 +2263,8 @@ static void decoder_step_dev(tt2_ctx* c, const float* frame_in, const uint8_t* m
                              float* align_out) {
   TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_finalize_weights not called");
   TT2_CHECK(c->encoded, TT2_ERR_STATE, "tt2_decoder_step called before tt2_encode");
+  TT2_CHECK(!c->emt.on(), TT2_ERR_INVALID_ARG,
+            "tt2_decoder_step: the Tacotron_emt_attn variant decodes through tt2_decode / tt2_synthesize_dev");
   TT2_CHECK(frame_in && masks && in && out && frame_out && stop_out, TT2_ERR_INVALID_ARG,
             "tt2_decoder_step: null argument");
   TT2_CHECK(in->h1 && in->c1 && in->h2 && in->c2 && in->attention && in->alignments && in->max_attentions &&
@@ -2484,6 +2528,30 @@ tt2_status tt2_decoder_path(tt2_ctx* c, int* persistent, float* kernel_ms) {
     TT2_CHECK(c && persistent && kernel_ms, TT2_ERR_INVALID_ARG, "null argument");
     *persistent = c->last_pd ? 1 : (pd_fits(c) ? 1 : 0);
     *kernel_ms = c->last_pd ? c->pd_kernel_ms : 0.f;
+  });
+}
+
+tt2_status tt2_set_emt_labels(tt2_ctx* c, const int32_t* labels, int B) {
+  return guard([&] {
+    TT2_CHECK(c && labels, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_CHECK(c->emt.on(), TT2_ERR_STATE, "tt2_set_emt_labels: the context is not the Tacotron_emt_attn variant");
+    TT2_CHECK(B >= 1 && B <= c->cfg.max_batch, TT2_ERR_SHAPE_MISMATCH, "batch exceeds capacity");
+    for (int b = 0; b < B; ++b) c->emt_labels[b] = labels[b];
+  });
+}
+
+tt2_status tt2_emt_alignments(tt2_ctx* c, float* out, int32_t* heads, int32_t* T_v) {
+  return guard([&] {
+    TT2_CHECK(c && heads && T_v, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_CHECK(c->emt.on(), TT2_ERR_STATE, "tt2_emt_alignments: the context is not the Tacotron_emt_attn variant");
+    TT2_CHECK(c->encoded, TT2_ERR_STATE, "tt2_emt_alignments called before tt2_encode");
+    *heads = c->emt.heads;
+    *T_v = c->emt.Tv;
+    if (!out) return;
+    TT2_CHECK(c->decoded, TT2_ERR_STATE, "tt2_emt_alignments called before tt2_decode");
+    TT2_HIP(hipStreamSynchronize(c->stream));
+    const size_t n = (size_t)std::min(c->n_steps, c->emt.max_iters) * c->B * c->emt.heads * c->emt.Tv;
+    TT2_HIP(hipMemcpy(out, c->emt.hist.p, sizeof(float) * n, hipMemcpyDeviceToHost));
   });
 }
 

@@ -25,6 +25,46 @@ def split_func(x, split_pos):
     return rst
 
 
+def split_towers(hp, inputs, input_lengths, split_infos, ref_mel_emt, ref_mel_spk, mel_targets):
+    """Per-tower inputs exactly as the reference packs them (tacotron.py:83-138,
+    tacotron_emt_attn.py:81-137): split_func on the time-axis-packed batch when
+    tacotron_num_gpus > 1."""
+    inputs = np.asarray(inputs, np.int32)
+    input_lengths = np.asarray(input_lengths, np.int32).reshape(-1)
+    ntow = hp.tacotron_num_gpus
+    asf = lambda x: None if x is None else np.asarray(x, np.float32)  # noqa: E731
+    if split_infos is not None and ntow > 1:
+        split_infos = np.asarray(split_infos, np.int32)
+        tower_inputs = split_func(inputs, split_infos[:, 0])
+        tower_ref_emt = (split_func(asf(ref_mel_emt), split_infos[:, 5])
+                         if ref_mel_emt is not None else [None] * ntow)
+        tower_ref_spk = (split_func(asf(ref_mel_spk), split_infos[:, 6])
+                         if ref_mel_spk is not None else [None] * ntow)
+        tower_targets = (split_func(asf(mel_targets), split_infos[:, 1])
+                         if mel_targets is not None else [None] * ntow)
+        # tf.split(input_lengths, num_or_size_splits=tacotron_num_gpus) (tacotron.py:89): an
+        # integer split, so the reference itself requires equal tower sizes
+        if input_lengths.shape[0] % ntow:
+            raise ValueError("input_lengths ({}) must split evenly over tacotron_num_gpus={} "
+                             "(tacotron.py:89 tf.split)".format(input_lengths.shape[0], ntow))
+        tower_lengths = np.split(input_lengths, ntow)
+    else:
+        tower_inputs, tower_lengths = [inputs], [input_lengths]
+        tower_ref_emt, tower_ref_spk = [asf(ref_mel_emt)], [asf(ref_mel_spk)]
+        tower_targets = [asf(mel_targets)]
+    return tower_inputs, tower_lengths, tower_ref_emt, tower_ref_spk, tower_targets
+
+
+def tower_masks(prenet_masks, i, row0, B):
+    """prenet_masks covers every utterance of every tower, [max_iters, 2, ntow*B, P] in tower-major
+    row order, or is a list with one [max_iters, 2, B, P] array per tower (None = device RNG)."""
+    if prenet_masks is None:
+        return None
+    if isinstance(prenet_masks, (list, tuple)):
+        return prenet_masks[i]
+    return np.asarray(prenet_masks)[:, :, row0:row0 + B]
+
+
 class Tacotron():
     """Tacotron-2 Feature prediction Model."""
 
@@ -139,34 +179,12 @@ class Tacotron():
                                       "not built; the fork default GST path is")
         if not hp.use_gst:
             raise NotImplementedError("use_gst=False is not built")
-        if ref_mel_spk is None and not emt_only:
-            raise ValueError("must provide references")
+        if ref_mel_emt is None or (ref_mel_spk is None and not emt_only):
+            raise ValueError("must provide references")  # refnet_emt / refnet_spk inputs (:251-259)
         constraint = bool(getattr(args, "synth_constraint", False))
 
-        inputs = np.asarray(inputs, np.int32)
-        input_lengths = np.asarray(input_lengths, np.int32).reshape(-1)
-        ntow = hp.tacotron_num_gpus
-        # split towers exactly as the reference packs them (tacotron.py:83-138)
-        if split_infos is not None and ntow > 1:
-            split_infos = np.asarray(split_infos, np.int32)
-            tower_inputs = split_func(inputs, split_infos[:, 0])
-            tower_ref_emt = split_func(np.asarray(ref_mel_emt, np.float32), split_infos[:, 5])
-            tower_ref_spk = (split_func(np.asarray(ref_mel_spk, np.float32), split_infos[:, 6])
-                             if ref_mel_spk is not None else [None] * ntow)
-            tower_targets = (split_func(np.asarray(mel_targets, np.float32), split_infos[:, 1])
-                             if mel_targets is not None else [None] * ntow)
-            # tf.split(input_lengths, num_or_size_splits=tacotron_num_gpus) (tacotron.py:89): an
-            # integer split, so the reference itself requires equal tower sizes
-            if input_lengths.shape[0] % ntow:
-                raise ValueError("input_lengths ({}) must split evenly over tacotron_num_gpus={} "
-                                 "(tacotron.py:89 tf.split)".format(input_lengths.shape[0], ntow))
-            tower_lengths = np.split(input_lengths, ntow)
-        else:
-            tower_inputs, tower_lengths = [inputs], [input_lengths]
-            tower_ref_emt = [np.asarray(ref_mel_emt, np.float32)]
-            tower_ref_spk = [np.asarray(ref_mel_spk, np.float32) if ref_mel_spk is not None else None]
-            tower_targets = [np.asarray(mel_targets, np.float32) if mel_targets is not None else None]
-
+        tower_inputs, tower_lengths, tower_ref_emt, tower_ref_spk, tower_targets = split_towers(
+            hp, inputs, input_lengths, split_infos, ref_mel_emt, ref_mel_spk, mel_targets)
         self.tower_decoder_output = []
         self.tower_alignments = []
         self.tower_stop_token_prediction = []
@@ -190,14 +208,7 @@ class Tacotron():
             if gta and tower_targets[i] is not None:
                 tg = tower_targets[i].reshape(B, -1, hp.num_mels)[:, hp.outputs_per_step - 1::hp.outputs_per_step]
             eng = self._get_engine(B, T_in, T_ref, max_iters, emt_only, constraint)
-            # prenet_masks covers every utterance of every tower, [max_iters, 2, ntow*B, P] in
-            # tower-major row order (or a list with one [max_iters, 2, B, P] array per tower)
-            if prenet_masks is None:
-                masks = None
-            elif isinstance(prenet_masks, (list, tuple)):
-                masks = prenet_masks[i]
-            else:
-                masks = np.asarray(prenet_masks)[:, :, row0:row0 + B]
+            masks = tower_masks(prenet_masks, i, row0, B)
             row0 += B
             out = eng.synthesize(ids, tower_lengths[i], ref_e, ref_s, max_iters, masks, seed, tg)
             self.tower_decoder_output.append(out["decoder_output"])

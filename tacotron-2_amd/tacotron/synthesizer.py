@@ -26,12 +26,16 @@ class Synthesizer:
         self.args = args
         model_name = 'Tacotron_emt_attn' if getattr(args, 'emt_attn', False) else 'Tacotron'
         self.model = create_model(model_name, hparams)
+        init = dict(emt_only=bool(getattr(args, 'emt_only', False)))
+        if model_name == 'Tacotron_emt_attn':  # its variables depend on args.attn / emt_ref_gru
+            init.update(attn=getattr(args, 'attn', None), emt_ref_gru=getattr(args, 'emt_ref_gru', 'none'),
+                        n_emt=n_emt)
         if checkpoint_path is None:
-            self.model.init_random_weights(emt_only=bool(getattr(args, 'emt_only', False)))
+            self.model.init_random_weights(**init)
         elif str(checkpoint_path).endswith('.npz'):
             self.model.load_weights(checkpoint_path)
         else:
-            self.model.init_random_weights(emt_only=bool(getattr(args, 'emt_only', False)))
+            self.model.init_random_weights(**init)
             self.model.load_checkpoint(checkpoint_path)
         self.gta = gta
         self._hparams = hparams
@@ -66,6 +70,9 @@ class Synthesizer:
                               emt_labels=emt_labels_synth, spk_labels=spk_labels_synth, synth=True,
                               n_emt=4, n_spk=2, prenet_masks=prenet_masks, seed=seed)
         if emb_only:
+            if not hasattr(self.model, 'tower_style_embeddings'):
+                raise NotImplementedError('emb_only of Tacotron_emt_attn (refnet / context outputs, '
+                                          'synthesizer.py:136-142) is not exposed')
             return (self.model.tower_style_embeddings[0], None, None, None, 1.0)
         # Linearize outputs (n_gpus -> 1D), synthesizer.py:164-167
         mels = [m for tower in self.model.tower_mel_outputs for m in tower]
@@ -113,7 +120,7 @@ def filenames_to_inputs(hparams, texts, basenames, mel_filenames, basenames_refs
     pad = 0
     target_pad = -hparams.max_abs_value if hparams.symmetric_mels else 0
     cleaner_names = [x.strip() for x in hparams.cleaners.split(',')]
-    if mel_ref_filenames_emt is None:
+    if mel_ref_filenames_emt is None and mel_ref_filenames_spk is None:
         raise ValueError('must provide references')  # tacotron.py:66-67
     lists = [texts, basenames, basenames_refs, mel_filenames, mel_ref_filenames_emt,
              mel_ref_filenames_spk, emt_labels_synth, spk_labels_synth]
@@ -129,7 +136,8 @@ def filenames_to_inputs(hparams, texts, basenames, mel_filenames, basenames_refs
     seqs = [np.asarray(text_to_sequence(text, cleaner_names)) for text in texts]
     input_lengths = [len(seq) for seq in seqs]
     size_per_device = len(seqs) // hparams.tacotron_num_gpus
-    np_refs_emt = [_load_mel(f) for f in mel_ref_filenames_emt]
+    np_refs_emt = [_load_mel(f) for f in mel_ref_filenames_emt] if mel_ref_filenames_emt is not None \
+        else None
     np_refs_spk = [_load_mel(f) for f in mel_ref_filenames_spk] if mel_ref_filenames_spk is not None \
         else None
     input_seqs = mel_ref_seqs_emt = mel_ref_seqs_spk = None
@@ -138,10 +146,11 @@ def filenames_to_inputs(hparams, texts, basenames, mel_filenames, basenames_refs
         sl = slice(size_per_device * i, size_per_device * (i + 1))
         d_in, max_seq_len = _prepare_inputs(seqs[sl], pad)
         input_seqs = d_in if input_seqs is None else np.concatenate((input_seqs, d_in), axis=1)
-        d_e, len_e = _prepare_targets(np_refs_emt[sl], hparams.outputs_per_step, target_pad)
-        mel_ref_seqs_emt = d_e if mel_ref_seqs_emt is None else \
-            np.concatenate((mel_ref_seqs_emt, d_e), axis=1)
-        len_s = 0
+        len_e = len_s = 0
+        if np_refs_emt is not None:
+            d_e, len_e = _prepare_targets(np_refs_emt[sl], hparams.outputs_per_step, target_pad)
+            mel_ref_seqs_emt = d_e if mel_ref_seqs_emt is None else \
+                np.concatenate((mel_ref_seqs_emt, d_e), axis=1)
         if np_refs_spk is not None:
             d_s, len_s = _prepare_targets(np_refs_spk[sl], hparams.outputs_per_step, target_pad)
             mel_ref_seqs_spk = d_s if mel_ref_seqs_spk is None else \

@@ -42,7 +42,7 @@ class Config(ctypes.Structure):
         ("lower_bound_decay", ctypes.c_float)] + [(n, ctypes.c_int) for n in (
             "symmetric_mels", "clip_outputs", "stop_at_any", "mask_encoder", "cumulative_weights",
             "synthesis_constraint", "constraint_monotonic", "attention_win_size", "max_batch",
-            "max_T_in", "max_T_ref", "max_iters")]
+            "max_T_in", "max_T_ref", "max_iters", "emt_attn", "emt_ref_gru", "n_emt")]
 
 
 class WnConfig(ctypes.Structure):
@@ -116,6 +116,8 @@ SIGNATURES = {
     "tt2_debug_stamps": (_I, [_P, _P]),
     "tt2_decoder_path": (_I, [_P, _P, _P]),
     "tt2_debug_pd_stamps": (_I, [_P, _P]),
+    "tt2_set_emt_labels": (_I, [_P, _P, _I]),
+    "tt2_emt_alignments": (_I, [_P, _P, _P, _P]),
     "tt2_wn_last_timings": (_I, [_P, _P]),
     "tt2_wn_debug_stamps": (_I, [_P, _P]),
     "tt2_wn_default_config": (None, [ctypes.POINTER(WnConfig), _I, ctypes.c_int64]),

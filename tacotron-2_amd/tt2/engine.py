@@ -10,12 +10,14 @@ import numpy as np
 from . import _lib
 from ._lib import check, f32, i32, ptr
 from .hparams import get_hop_size
-from .weights import memory_width
+from .weights import EMT_ATTN, EMT_REF_GRU, memory_width
 
 
 def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=False,
-                    synthesis_constraint=False):
-    """tt2_config from hparams (names mirror code/hparams.py)."""
+                    synthesis_constraint=False, emt_attn=None, emt_ref_gru="none", n_emt=4):
+    """tt2_config from hparams (names mirror code/hparams.py).  ``emt_attn`` selects the
+    Tacotron_emt_attn model (args.attn: 'simple' / 'multihead' / 'style_tokens'; None = the
+    Tacotron model), ``emt_ref_gru`` its args.emt_ref_gru."""
     lib = _lib.load_library()
     cfg = _lib.Config()
     lib.tt2_default_config(ctypes.byref(cfg), max_batch, max_T_in, max_T_ref, max_iters)
@@ -61,6 +63,13 @@ def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=Fals
         raise NotImplementedError("outputs_per_step (r) must be 1 on this build (hparams.py:140)")
     if hp.smoothing:
         raise NotImplementedError("smoothing attention normalisation is not built")
+    if emt_attn is not None:
+        if emt_attn not in EMT_ATTN or emt_ref_gru not in EMT_REF_GRU:
+            raise ValueError("emt_attn must be one of {}, emt_ref_gru one of {}".format(
+                EMT_ATTN, EMT_REF_GRU))
+        cfg.emt_attn = 1 + EMT_ATTN.index(emt_attn)
+        cfg.emt_ref_gru = EMT_REF_GRU.index(emt_ref_gru)
+        cfg.n_emt = n_emt
     return cfg
 
 
@@ -68,14 +77,17 @@ class TacotronEngine(object):
     """Owns one tt2_ctx."""
 
     def __init__(self, hp, weights, max_batch, max_T_in, max_T_ref, max_iters, device=0,
-                 emt_only=False, synthesis_constraint=False):
+                 emt_only=False, synthesis_constraint=False, emt_attn=None, emt_ref_gru="none",
+                 n_emt=4):
         self.lib = _lib.load_library()
         self.hp = hp
         self.emt_only = emt_only
+        self.emt_attn = emt_attn
         self.cfg = tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only,
-                                   synthesis_constraint)
+                                   synthesis_constraint, emt_attn, emt_ref_gru, n_emt)
         self.caps = (max_batch, max_T_in, max_T_ref, max_iters)
-        self.D = memory_width(hp, emt_only)
+        # Tacotron_emt_attn attends over the encoder outputs alone (tacotron_emt_attn.py:244-246)
+        self.D = 2 * hp.encoder_lstm_units if emt_attn else memory_width(hp, emt_only)
         h = ctypes.c_void_p()
         check(self.lib.tt2_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
         self.h = h
@@ -100,13 +112,13 @@ class TacotronEngine(object):
         lengths = i32(lengths)
         B, T = ids.shape
         self._B, self._T_in = B, T
-        ref_emt = f32(ref_emt)
+        ref_emt = f32(ref_emt) if ref_emt is not None else None
         ref_spk = f32(ref_spk) if ref_spk is not None else None
         mem = np.zeros((B, T, self.D), np.float32)
         sw = self.D - 2 * self.hp.encoder_lstm_units
         style = np.zeros((B, max(sw, 1)), np.float32)
         check(self.lib.tt2_encode(self.h, ptr(ids), ptr(lengths), B, T, ptr(ref_emt),
-                                  ref_emt.shape[1], ptr(ref_spk),
+                                  ref_emt.shape[1] if ref_emt is not None else 0, ptr(ref_spk),
                                   ref_spk.shape[1] if ref_spk is not None else 0, ptr(mem),
                                   ptr(style)))
         return mem, style[:, :sw]
@@ -131,6 +143,7 @@ class TacotronEngine(object):
                                   tg.shape[1] if tg is not None else 0, ptr(frames), ptr(stop),
                                   ptr(align), ctypes.byref(n)))
         n = n.value
+        self._n_steps = n
         return frames[:, :n], stop[:, :n], align[:, :, :n]
 
     def zero_state(self):
@@ -168,6 +181,22 @@ class TacotronEngine(object):
                                         ctypes.byref(sout), ptr(frame), ptr(stop), ptr(align)))
         nxt["time"] = sout.time
         return frame, stop, align, nxt
+
+    def set_emt_labels(self, labels):
+        """Tacotron_emt_attn: emotion labels [B] (the emt_labels placeholder, synthesizer.py:35) used
+        by the next encode ('style_tokens' one-hot query)."""
+        lab = i32(labels)
+        check(self.lib.tt2_set_emt_labels(self.h, ptr(lab), lab.shape[0]))
+
+    def emt_alignments(self):
+        """Tacotron_emt_attn: emotion attention weights of the last decode, [B, heads, T_v, n_steps]
+        (tower_alignments_emt)."""
+        heads, tv = ctypes.c_int32(), ctypes.c_int32()
+        check(self.lib.tt2_emt_alignments(self.h, None, ctypes.byref(heads), ctypes.byref(tv)))
+        n = self._n_steps
+        out = np.zeros((n, self._B, heads.value, tv.value), np.float32)
+        check(self.lib.tt2_emt_alignments(self.h, ptr(out), ctypes.byref(heads), ctypes.byref(tv)))
+        return out.transpose(1, 2, 3, 0)
 
     def decoder_path(self):
         """(persistent, kernel_ms): 1 when the single-launch persistent decoder serves the current

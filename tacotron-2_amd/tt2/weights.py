@@ -20,8 +20,8 @@ def _bn(scope, c):
             (s + "moving_mean", (c,), "bn_mean"), (s + "moving_variance", (c,), "bn_var")]
 
 
-def tacotron_weight_specs(hp, emt_only=False):
-    """(name, shape, init) for every variable on the synthesis path (tacotron.py:215-381)."""
+def _text_encoder_specs(hp):
+    """embedding, EncoderConvolutions, EncoderRNN (tacotron.py:215-231)."""
     S = []
     n_sym = 66  # tacotron/utils/symbols.py:9-17
     E = hp.embedding_dim
@@ -39,38 +39,43 @@ def tacotron_weight_specs(hp, emt_only=False):
         sc = TP + "encoder_LSTM/bidirectional_rnn/{}/lstm_cell/".format(d)
         S.append((sc + "kernel", (cin + U, 4 * U), "glorot"))
         S.append((sc + "bias", (4 * U,), "bias"))
-    # reference encoders (modules.py:9-64) and GST (tacotron.py:219-282)
-    tags = ["emt"] if emt_only else ["emt", "spk"]
-    for tag in tags:
-        sc = TP + "refnet_{}/".format(tag)
-        c_in, F = 1, hp.num_mels
-        for i, f in enumerate(hp.reference_filters):
-            s2 = sc + "conv2d_{}/".format(i)
-            S.append((s2 + "conv2d/kernel", (3, 3, c_in, f), "glorot"))
-            S.append((s2 + "conv2d/bias", (f,), "bias"))
-            S += _bn(s2, f)
-            c_in = f
-            F = -(-F // 2)
-        gin = F * c_in
-        D = hp.reference_depth
-        S.append((sc + "rnn/gru_cell/gates/kernel", (gin + D, 2 * D), "glorot"))
-        S.append((sc + "rnn/gru_cell/gates/bias", (2 * D,), "gru_gate_bias"))
-        S.append((sc + "rnn/gru_cell/candidate/kernel", (gin + D, D), "glorot"))
-        S.append((sc + "rnn/gru_cell/candidate/bias", (D,), "bias"))
-        S.append((sc + "dense/kernel", (D, 128), "glorot"))
-        S.append((sc + "dense/bias", (128,), "bias"))
-        tok_d = hp.style_embed_depth // hp.num_heads
-        S.append((TP + "style_tokens_{}".format(tag), (hp.num_gst, tok_d), "gst_tokens"))
-        mh = TP + "Multihead-attention-{}/".format(tag)
-        A = hp.style_att_dim
-        S.append((mh + "conv1d/kernel", (1, 128, A), "glorot"))
-        S.append((mh + "conv1d/bias", (A,), "bias"))
-        S.append((mh + "conv1d_1/kernel", (1, tok_d, A), "glorot"))
-        S.append((mh + "conv1d_1/bias", (A,), "bias"))
-        S.append((mh + "attention_v", (A // hp.num_heads,), "glorot"))
-        S.append((mh + "attention_g", (), "mha_g"))
-        S.append((mh + "attention_b", (A // hp.num_heads,), "bias"))
-    Dm = memory_width(hp, emt_only)
+    return S
+
+
+def _refnet_convs(hp, sc):
+    """ReferenceEncoder CNN stack (modules.py:22-33); returns (specs, flattened output width)."""
+    S = []
+    c_in, F = 1, hp.num_mels
+    for i, f in enumerate(hp.reference_filters):
+        s2 = sc + "conv2d_{}/".format(i)
+        S.append((s2 + "conv2d/kernel", (3, 3, c_in, f), "glorot"))
+        S.append((s2 + "conv2d/bias", (f,), "bias"))
+        S += _bn(s2, f)
+        c_in = f
+        F = -(-F // 2)
+    return S, F * c_in
+
+
+def _gru_specs(sc, gin, D):
+    """TF1 GRUCell variables under ``sc`` (gates [r, u] and candidate)."""
+    return [(sc + "gates/kernel", (gin + D, 2 * D), "glorot"),
+            (sc + "gates/bias", (2 * D,), "gru_gate_bias"),
+            (sc + "candidate/kernel", (gin + D, D), "glorot"),
+            (sc + "candidate/bias", (D,), "bias")]
+
+
+def _mha_specs(mh, q_in, v_in, A, heads):
+    """MultiheadAttention mlp_attention, normalize=True (multihead_attention.py:43-110)."""
+    return [(mh + "conv1d/kernel", (1, q_in, A), "glorot"), (mh + "conv1d/bias", (A,), "bias"),
+            (mh + "conv1d_1/kernel", (1, v_in, A), "glorot"), (mh + "conv1d_1/bias", (A,), "bias"),
+            (mh + "attention_v", (A // heads,), "glorot"), (mh + "attention_g", (), "mha_g"),
+            (mh + "attention_b", (A // heads,), "bias")]
+
+
+def _decoder_specs(hp, Dm, extra=0):
+    """memory layer, LocationSensitiveAttention, Prenet, DecoderRNN, projections
+    (tacotron.py:310-338); ``extra`` = LSTM-1 input columns after [prenet | context]."""
+    S = []
     Ad = hp.attention_dim
     S.append((TP + "memory_layer/kernel", (Dm, Ad), "glorot"))
     S.append((TP + "decoder/query_layer/kernel", (hp.decoder_lstm_units, Ad), "glorot"))
@@ -88,7 +93,7 @@ def tacotron_weight_specs(hp, emt_only=False):
         S.append((sc + "bias", (n,), "bias"))
         p_in = n
     H = hp.decoder_lstm_units
-    x_in = p_in + Dm
+    x_in = p_in + Dm + extra
     for l in range(hp.decoder_layers):
         sc = TP + "decoder/decoder_LSTM/multi_rnn_cell/cell_{}/lstm_cell/".format(l)
         S.append((sc + "kernel", (x_in + H, 4 * H), "glorot"))
@@ -100,6 +105,12 @@ def tacotron_weight_specs(hp, emt_only=False):
     sp = TP + "decoder/stop_token_projection/projection_stop_token_projection/"
     S.append((sp + "kernel", (H + Dm, hp.outputs_per_step), "glorot"))
     S.append((sp + "bias", (hp.outputs_per_step,), "stop_bias"))
+    return S
+
+
+def _postnet_specs(hp):
+    """Postnet + postnet_projection (tacotron.py:366-375)."""
+    S = []
     cin = hp.num_mels
     kw = hp.postnet_kernel_size[0]
     for i in range(1, hp.postnet_num_layers + 1):
@@ -112,6 +123,106 @@ def tacotron_weight_specs(hp, emt_only=False):
     S.append((pp + "kernel", (cin, hp.num_mels), "glorot"))
     S.append((pp + "bias", (hp.num_mels,), "bias"))
     return S
+
+
+def tacotron_weight_specs(hp, emt_only=False):
+    """(name, shape, init) for every variable on the synthesis path (tacotron.py:215-381)."""
+    S = _text_encoder_specs(hp)
+    # reference encoders (modules.py:9-64) and GST (tacotron.py:219-282)
+    tags = ["emt"] if emt_only else ["emt", "spk"]
+    for tag in tags:
+        sc = TP + "refnet_{}/".format(tag)
+        conv, gin = _refnet_convs(hp, sc)
+        S += conv
+        D = hp.reference_depth
+        S += _gru_specs(sc + "rnn/gru_cell/", gin, D)
+        S.append((sc + "dense/kernel", (D, 128), "glorot"))
+        S.append((sc + "dense/bias", (128,), "bias"))
+        tok_d = hp.style_embed_depth // hp.num_heads
+        S.append((TP + "style_tokens_{}".format(tag), (hp.num_gst, tok_d), "gst_tokens"))
+        S += _mha_specs(TP + "Multihead-attention-{}/".format(tag), 128, tok_d, hp.style_att_dim,
+                        hp.num_heads)
+    S += _decoder_specs(hp, memory_width(hp, emt_only))
+    return S + _postnet_specs(hp)
+
+
+#: args.attn / args.emt_ref_gru values of Tacotron_emt_attn (train.py:147-150); codes 1.. / 0..
+EMT_ATTN = ("simple", "multihead", "style_tokens")
+EMT_REF_GRU = ("none", "gru", "gru_multi")
+
+
+def emt_value_width(hp, attn, emt_ref_gru):
+    """Width of one attended row: tanh(style_tokens) 16; refnet_emt all_outputs (modules.py:35-55):
+    the reshaped CNN output ('none'), [fw | bw] GRU outputs ('gru'), dense(128) ('gru_multi')."""
+    if attn == "style_tokens":
+        return 16
+    _, gin = _refnet_convs(hp, "")
+    return {"none": gin, "gru": 2 * hp.reference_depth, "gru_multi": 128}[emt_ref_gru]
+
+
+def emt_lstm_extra(hp, attn, emt_only=False):
+    """LSTM-1 input columns after [prenet | context] (Architecture_wrappers.py:203-211): the emotion
+    context (attention_dim / 128 / 64 wide, :116-123) and, concatenated ('simple') or added
+    ('multihead'), refnet_spk's 128."""
+    spk = attn != "style_tokens" and not emt_only
+    if attn == "simple":
+        return hp.attention_dim + (128 if spk else 0)
+    if attn == "multihead":
+        return 128
+    return 4 * 16
+
+
+def tacotron_emt_weight_specs(hp, attn, emt_ref_gru="none", emt_only=False, n_emt=4):
+    """(name, shape, init) of Tacotron_emt_attn's synthesis graph (tacotron_emt_attn.py:198-381).
+
+    Variables built inside the decoder cell live under ``decoder/`` (dynamic_decode's scope):
+    SimpleBahdanauAttention's Dense layers ``W1``/``W2``/``V`` (built at first call,
+    attention.py:237-250), ``Multihead-attention-attn_emt`` and the multi-head output dense
+    ``attn_emt/dense`` (Architecture_wrappers.py:233-234).  Like the other TF-internal scope names
+    these are unverified without TensorFlow (no checkpoint of this model ships)."""
+    if attn not in EMT_ATTN or emt_ref_gru not in EMT_REF_GRU:
+        raise ValueError("attn must be one of {} and emt_ref_gru one of {}".format(EMT_ATTN,
+                                                                                  EMT_REF_GRU))
+    S = _text_encoder_specs(hp)
+    D = hp.reference_depth
+    H = hp.decoder_lstm_units
+    if attn == "style_tokens":
+        S.append((TP + "style_tokens", (24, 16), "gst_tokens"))
+    else:
+        sc = TP + "refnet_emt/"
+        conv, gin = _refnet_convs(hp, sc)
+        S += conv
+        if emt_ref_gru == "gru":
+            for d in ("fw", "bw"):
+                S += _gru_specs(sc + "bidirectional_rnn/{}/gru_cell/".format(d), gin, D)
+        elif emt_ref_gru == "gru_multi":
+            for i in range(8):
+                S += _gru_specs(sc + "gru_{}/rnn/gru_cell/".format(i), gin, D)
+                S.append((sc + "gru_{}/dense/kernel".format(i), (D, 128), "glorot"))
+                S.append((sc + "gru_{}/dense/bias".format(i), (128,), "bias"))
+        if not emt_only:
+            sc = TP + "refnet_spk/"
+            conv, gin = _refnet_convs(hp, sc)
+            S += conv
+            S += _gru_specs(sc + "rnn/gru_cell/", gin, D)
+            S.append((sc + "dense/kernel", (D, 128), "glorot"))
+            S.append((sc + "dense/bias", (128,), "bias"))
+    Dm = 2 * hp.encoder_lstm_units
+    S += _decoder_specs(hp, Dm, emt_lstm_extra(hp, attn, emt_only))
+    Dv = emt_value_width(hp, attn, emt_ref_gru)
+    if attn == "simple":
+        A = hp.attention_dim
+        S += [(TP + "decoder/W1/kernel", (Dv, A), "glorot"), (TP + "decoder/W1/bias", (A,), "bias"),
+              (TP + "decoder/W2/kernel", (H, A), "glorot"), (TP + "decoder/W2/bias", (A,), "bias"),
+              (TP + "decoder/V/kernel", (A, 1), "glorot"), (TP + "decoder/V/bias", (1,), "bias")]
+    else:
+        q_in = H + (n_emt if attn == "style_tokens" else 0)
+        S += _mha_specs(TP + "decoder/Multihead-attention-attn_emt/", q_in, Dv, hp.style_att_dim,
+                        hp.num_heads)
+        if attn == "multihead":
+            S += [(TP + "decoder/attn_emt/dense/kernel", (hp.num_heads * Dv, 128), "glorot"),
+                  (TP + "decoder/attn_emt/dense/bias", (128,), "bias")]
+    return S + _postnet_specs(hp)
 
 
 def memory_width(hp, emt_only=False):
@@ -222,6 +333,10 @@ def init_weights(specs, hp, seed=5339):
 
 def init_tacotron_weights(hp, seed=5339, emt_only=False):
     return init_weights(tacotron_weight_specs(hp, emt_only), hp, seed)
+
+
+def init_tacotron_emt_weights(hp, attn, emt_ref_gru="none", emt_only=False, n_emt=4, seed=5339):
+    return init_weights(tacotron_emt_weight_specs(hp, attn, emt_ref_gru, emt_only, n_emt), hp, seed)
 
 
 def init_wavenet_weights(hp, seed=5339):

@@ -184,8 +184,8 @@ def test_create_model_names():
     from tacotron.models import create_model
     with pytest.raises(Exception, match="Unknown model"):
         create_model("Nope", small_hparams())
-    with pytest.raises(NotImplementedError):
-        create_model("Tacotron_emt_attn", small_hparams())
+    from tacotron.models import Tacotron_emt_attn
+    assert isinstance(create_model("Tacotron_emt_attn", small_hparams()), Tacotron_emt_attn)
 
 
 @pytest.mark.parametrize("kw,exc", [
