@@ -60,7 +60,6 @@ def parse():
     p.add_argument("--train-precision", default="bf16", choices=["bf16", "fp32"],
                    help="configs[4] names bf16 (GEMM operands; fp32 accumulation and state)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-steps", type=int, default=100)
     p.add_argument("--profile-iters", type=int, default=50)
     return p.parse_args()
 
@@ -87,50 +86,57 @@ def decoder_step_bytes(W, hp, B, T):
     return 4 * (params + B * T * hp.attention_dim + B * T * D + 2 * B * T)
 
 
-def cpu_baseline_tacotron(hp, W, B, T, T_ref, t_out, steps):
-    """Oracle (numpy) on this host: encoder + `steps` decoder steps + Postnet over `steps` frames,
-    extrapolated linearly to T_out frames."""
-    from oracle.hp import oracle_hp
+def cpu_baseline_tacotron(hp, W, B, T, T_ref, t_out, seed):
+    """libtt2_cpu.so (cpu/tt2_cpu.cpp: the same C ABI on host cores, fp32, OpenMP) on the WHOLE
+    configs[1] workload of the GPU leg: same weights, ids, reference mels and prenet keep bits
+    (rng.h stream of `seed`), encoder + every decoder step + Postnet, no extrapolation."""
+    from tt2.engine import TacotronEngine
     from tt2.synthetic import tacotron_inputs
-    from oracle import tacotron_ref as TR
-    ids, lens, re, rs = tacotron_inputs(B, T, T_ref, seed=1234, ragged=False)
-    oh = oracle_hp(hp)
-    masks = (np.random.default_rng(5339).random((steps, 2, B, hp.prenet_layers[0])) < 0.5)
+    lib = _lib.load_cpu_library()
+    ids, lens, re, rs = tacotron_inputs(B, T, T_ref, seed=seed, ragged=False)
+    eng = TacotronEngine(hp, W, B, T, T_ref, t_out, 0, lib=lib)
     t0 = time.perf_counter()
-    enc = TR.encoder(ids, lens, W, oh)
-    st = TR.style_embedding(re, rs, W, oh)
-    vals, keys = TR.memory_and_keys(enc, st, lens, W)
+    eng.encode(ids, lens, re, rs)
     t1 = time.perf_counter()
-    frames, _, _ = TR.dynamic_decode(keys, vals, lens, W, oh, masks.astype(np.uint8), steps)
+    frames, _, _ = eng.decode(t_out, None, 5339)
     t2 = time.perf_counter()
-    TR.postnet_and_clip(frames, W, oh)
+    eng.postnet(None, B, frames.shape[1])
     t3 = time.perf_counter()
-    scale = t_out / float(frames.shape[1])
-    t_full = (t1 - t0) + scale * ((t2 - t1) + (t3 - t2))
-    return dict(value=B * t_out / t_full, t_encoder_s=t1 - t0, t_decoder_s=t2 - t1,
+    eng.close()
+    return dict(value=B * frames.shape[1] / (t3 - t0), t_encoder_s=t1 - t0, t_decoder_s=t2 - t1,
                 t_postnet_s=t3 - t2, decoded=int(frames.shape[1]))
 
 
 def cpu_baseline_wavenet(hp, W, samples):
-    from oracle import wavenet_ref as WR
-    from oracle.hp import wavenet_oracle_hp
+    """libtt2_cpu.so tt2_wn_generate: B=1, `samples` audio samples of configs[2] (conditioning
+    upsampling included), injected uniforms."""
+    from tt2.engine import WaveNetEngine
+    lib = _lib.load_cpu_library()
+    hop = int(np.prod(hp.upsample_scales))
+    T_f = max(1, samples // hop)
     rng = np.random.default_rng(5339)
-    T = samples
-    c_up = rng.uniform(0, 1, (1, T, 80)).astype(np.float32)
+    cond = rng.uniform(0, 1, (1, T_f, hp.num_mels)).astype(np.float32)
+    T = T_f * hop
     um = rng.uniform(1e-5, 1 - 1e-5, (T, 1, 10)).astype(np.float32)
     ul = rng.uniform(1e-5, 1 - 1e-5, (T, 1)).astype(np.float32)
+    eng = WaveNetEngine(hp, W, 1, T, 0, lib=lib)
     t0 = time.perf_counter()
-    WR.incremental(c_up, W, wavenet_oracle_hp(hp), um, ul)
-    return T / (time.perf_counter() - t0)
+    eng.generate(cond, um, ul, 0, None)
+    dt = time.perf_counter() - t0
+    eng.close()
+    return T / dt, T
 
 
 def threads_used():
+    """OpenMP threads of libtt2_cpu.so (libgomp honours OMP_NUM_THREADS; 16 on the GPU box)."""
     try:
         from threadpoolctl import threadpool_info
-        n = [i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"]
-        return max(n) if n else 1
+        n = [i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "openmp"]
+        if n:
+            return max(n)
     except Exception:
-        return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        pass
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
 
 def load_traffic(kernel):
@@ -603,21 +609,22 @@ def main():
     # --- CPU baseline (rank 0, N = 1 only) ---
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        c = cpu_baseline_tacotron(hp, W, B, T, a.ref_frames, a.t_out, a.cpu_steps)
+        c = cpu_baseline_tacotron(hp, W, B, T, a.ref_frames, a.t_out, 1234 + rank)
         cores = threads_used()
         cpu = dict(value=round(c["value"], 2), unit="mel-frames/s", cores=cores, kind="port",
-                   sample="numpy oracle (oracle/tacotron_ref.py), B=32x201 chars: encoder + {} of {} "
-                          "decoder steps + Postnet on {} frames, extrapolated linearly to T_out={} "
-                          "(enc {:.2f}s, dec {:.2f}s, postnet {:.2f}s)".format(
-                              c["decoded"], a.t_out, c["decoded"], a.t_out, c["t_encoder_s"],
-                              c["t_decoder_s"], c["t_postnet_s"]),
+                   sample="libtt2_cpu.so (cpu/tt2_cpu.cpp, same C ABI, fp32, OpenMP x{}) on the whole "
+                          "configs[1] workload: B=32x201 chars, encoder + {} decoder steps + Postnet, "
+                          "no extrapolation (enc {:.2f}s, dec {:.2f}s, postnet {:.2f}s)".format(
+                              cores, c["decoded"], c["t_encoder_s"], c["t_decoder_s"],
+                              c["t_postnet_s"]),
                    label="CPU restatement of the reference path (not TF)")
         if wn is not None:
             whp = bench_wavenet_hparams()
             WW = init_wavenet_weights(whp, seed=whp.wavenet_random_seed)
-            wn["cpu_baseline"] = dict(value=round(cpu_baseline_wavenet(whp, WW, 2000), 1),
-                                      unit="audio-samples/s", cores=cores, kind="port",
-                                      sample="numpy oracle incremental(), 2000 samples, B=1")
+            v, n = cpu_baseline_wavenet(whp, WW, 2000)
+            wn["cpu_baseline"] = dict(value=round(v, 1), unit="audio-samples/s", cores=1, kind="port",
+                                      sample="libtt2_cpu.so tt2_wn_generate, {} samples, B=1 "
+                                             "(one utterance: sequential per sample)".format(n))
 
     if rank == 0:
         out = dict(metric=METRIC, value=round(value, 1), unit="mel-frames/s", n_gpus=world,

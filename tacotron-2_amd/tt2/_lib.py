@@ -177,9 +177,37 @@ def load_library(path=LIB_PATH):
     return lib
 
 
-def check(status):
+#: the synthesis subset libtt2_cpu.so (cpu/tt2_cpu.cpp) exports, same signatures
+CPU_SYMBOLS = (
+    "tt2_last_error", "tt2_version", "tt2_default_config", "tt2_create", "tt2_destroy",
+    "tt2_load_tensor", "tt2_finalize_weights", "tt2_encode", "tt2_decode", "tt2_decoder_step",
+    "tt2_postnet", "tt2_prenet_keep_bits", "tt2_wn_default_config", "tt2_wn_create",
+    "tt2_wn_destroy", "tt2_wn_load_tensor", "tt2_wn_finalize", "tt2_wn_generate", "tt2_wn_noise",
+    "tt2_mol_sample")
+CPU_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libtt2_cpu.so")
+_cpu_lib = None
+
+
+def load_cpu_library(path=CPU_LIB_PATH):
+    """libtt2_cpu.so: the same ABI on host cores (the CPU baseline / second implementation).
+    Loaded RTLD_LOCAL beside libtt2.so; never a fallback of the HIP path."""
+    global _cpu_lib
+    if _cpu_lib is not None:
+        return _cpu_lib
+    if not os.path.exists(path):
+        raise TT2NotBuilt("CPU library not built: {} is missing (run `make -C tacotron-2_amd`)"
+                          .format(path))
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    for name in CPU_SYMBOLS:
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = SIGNATURES[name]
+    _cpu_lib = lib
+    return lib
+
+
+def check(status, lib=None):
     if status != TT2_OK:
-        msg = load_library().tt2_last_error()
+        msg = (lib or load_library()).tt2_last_error()
         raise TT2Error(status, msg.decode() if msg else "")
 
 
@@ -199,7 +227,7 @@ def i32(a):
     return None if a is None else np.ascontiguousarray(a, dtype=np.int32)
 
 
-def load_tensor(fn, handle, name, arr):
+def load_tensor(fn, handle, name, arr, lib=None):
     arr = np.ascontiguousarray(arr, dtype=np.float32)
     shape = (ctypes.c_int64 * max(arr.ndim, 1))(*arr.shape)
-    check(fn(handle, name.encode(), ptr(arr), ctypes.cast(shape, ctypes.c_void_p), arr.ndim))
+    check(fn(handle, name.encode(), ptr(arr), ctypes.cast(shape, ctypes.c_void_p), arr.ndim), lib)

@@ -14,11 +14,12 @@ from .weights import EMT_ATTN, EMT_REF_GRU, memory_width
 
 
 def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=False,
-                    synthesis_constraint=False, emt_attn=None, emt_ref_gru="none", n_emt=4):
+                    synthesis_constraint=False, emt_attn=None, emt_ref_gru="none", n_emt=4,
+                    lib=None):
     """tt2_config from hparams (names mirror code/hparams.py).  ``emt_attn`` selects the
     Tacotron_emt_attn model (args.attn: 'simple' / 'multihead' / 'style_tokens'; None = the
     Tacotron model), ``emt_ref_gru`` its args.emt_ref_gru."""
-    lib = _lib.load_library()
+    lib = lib or _lib.load_library()
     cfg = _lib.Config()
     lib.tt2_default_config(ctypes.byref(cfg), max_batch, max_T_in, max_T_ref, max_iters)
     cfg.num_mels = hp.num_mels
@@ -78,23 +79,27 @@ class TacotronEngine(object):
 
     def __init__(self, hp, weights, max_batch, max_T_in, max_T_ref, max_iters, device=0,
                  emt_only=False, synthesis_constraint=False, emt_attn=None, emt_ref_gru="none",
-                 n_emt=4):
-        self.lib = _lib.load_library()
+                 n_emt=4, lib=None):
+        # lib: libtt2.so by default; _lib.load_cpu_library() binds the same ABI on host cores
+        self.lib = lib or _lib.load_library()
         self.hp = hp
         self.emt_only = emt_only
         self.emt_attn = emt_attn
         self.cfg = tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only,
-                                   synthesis_constraint, emt_attn, emt_ref_gru, n_emt)
+                                   synthesis_constraint, emt_attn, emt_ref_gru, n_emt, self.lib)
         self.caps = (max_batch, max_T_in, max_T_ref, max_iters)
         # Tacotron_emt_attn attends over the encoder outputs alone (tacotron_emt_attn.py:244-246)
         self.D = 2 * hp.encoder_lstm_units if emt_attn else memory_width(hp, emt_only)
         h = ctypes.c_void_p()
-        check(self.lib.tt2_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
+        self._ok(self.lib.tt2_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
         self.h = h
         for name, arr in weights.items():
             if name.startswith("Tacotron_model/"):
-                _lib.load_tensor(self.lib.tt2_load_tensor, self.h, name, arr)
-        check(self.lib.tt2_finalize_weights(self.h))
+                _lib.load_tensor(self.lib.tt2_load_tensor, self.h, name, arr, self.lib)
+        self._ok(self.lib.tt2_finalize_weights(self.h))
+
+    def _ok(self, status):
+        _lib.check(status, self.lib)
 
     def close(self):
         if getattr(self, "h", None):
@@ -117,7 +122,7 @@ class TacotronEngine(object):
         mem = np.zeros((B, T, self.D), np.float32)
         sw = self.D - 2 * self.hp.encoder_lstm_units
         style = np.zeros((B, max(sw, 1)), np.float32)
-        check(self.lib.tt2_encode(self.h, ptr(ids), ptr(lengths), B, T, ptr(ref_emt),
+        self._ok(self.lib.tt2_encode(self.h, ptr(ids), ptr(lengths), B, T, ptr(ref_emt),
                                   ref_emt.shape[1] if ref_emt is not None else 0, ptr(ref_spk),
                                   ref_spk.shape[1] if ref_spk is not None else 0, ptr(mem),
                                   ptr(style)))
@@ -139,7 +144,7 @@ class TacotronEngine(object):
         stop = np.zeros((B, max_iters), np.float32)
         align = np.zeros((B, self._T_in, max_iters), np.float32)
         n = ctypes.c_int32()
-        check(self.lib.tt2_decode(self.h, max_iters, ptr(masks), seed, ptr(tg),
+        self._ok(self.lib.tt2_decode(self.h, max_iters, ptr(masks), seed, ptr(tg),
                                   tg.shape[1] if tg is not None else 0, ptr(frames), ptr(stop),
                                   ptr(align), ctypes.byref(n)))
         n = n.value
@@ -177,7 +182,7 @@ class TacotronEngine(object):
         frame = np.zeros((B, self.hp.num_mels), np.float32)
         stop = np.zeros((B,), np.float32)
         align = np.zeros((B, T), np.float32)
-        check(self.lib.tt2_decoder_step(self.h, ptr(fi), ptr(m), ctypes.byref(sin),
+        self._ok(self.lib.tt2_decoder_step(self.h, ptr(fi), ptr(m), ctypes.byref(sin),
                                         ctypes.byref(sout), ptr(frame), ptr(stop), ptr(align)))
         nxt["time"] = sout.time
         return frame, stop, align, nxt
@@ -186,16 +191,16 @@ class TacotronEngine(object):
         """Tacotron_emt_attn: emotion labels [B] (the emt_labels placeholder, synthesizer.py:35) used
         by the next encode ('style_tokens' one-hot query)."""
         lab = i32(labels)
-        check(self.lib.tt2_set_emt_labels(self.h, ptr(lab), lab.shape[0]))
+        self._ok(self.lib.tt2_set_emt_labels(self.h, ptr(lab), lab.shape[0]))
 
     def emt_alignments(self):
         """Tacotron_emt_attn: emotion attention weights of the last decode, [B, heads, T_v, n_steps]
         (tower_alignments_emt)."""
         heads, tv = ctypes.c_int32(), ctypes.c_int32()
-        check(self.lib.tt2_emt_alignments(self.h, None, ctypes.byref(heads), ctypes.byref(tv)))
+        self._ok(self.lib.tt2_emt_alignments(self.h, None, ctypes.byref(heads), ctypes.byref(tv)))
         n = self._n_steps
         out = np.zeros((n, self._B, heads.value, tv.value), np.float32)
-        check(self.lib.tt2_emt_alignments(self.h, ptr(out), ctypes.byref(heads), ctypes.byref(tv)))
+        self._ok(self.lib.tt2_emt_alignments(self.h, ptr(out), ctypes.byref(heads), ctypes.byref(tv)))
         return out.transpose(1, 2, 3, 0)
 
     def decoder_path(self):
@@ -204,7 +209,7 @@ class TacotronEngine(object):
         persistent decode launch."""
         p = ctypes.c_int()
         ms = ctypes.c_float()
-        check(self.lib.tt2_decoder_path(self.h, ctypes.byref(p), ctypes.byref(ms)))
+        self._ok(self.lib.tt2_decoder_path(self.h, ctypes.byref(p), ctypes.byref(ms)))
         return p.value, ms.value
 
     def postnet(self, frames=None, B=None, T=None):
@@ -213,7 +218,7 @@ class TacotronEngine(object):
             B, T = frames.shape[:2]
         dec = np.zeros((B, T, self.hp.num_mels), np.float32)
         mel = np.zeros((B, T, self.hp.num_mels), np.float32)
-        check(self.lib.tt2_postnet(self.h, ptr(frames), B, T, ptr(dec), ptr(mel)))
+        self._ok(self.lib.tt2_postnet(self.h, ptr(frames), B, T, ptr(dec), ptr(mel)))
         return dec, mel
 
     def synthesize(self, ids, lengths, ref_emt, ref_spk, max_iters, prenet_masks=None, seed=0,
@@ -232,8 +237,8 @@ class TacotronEngine(object):
 UPSAMPLE_TYPES = ("2D", "1D", "Resize", "SubPixel", "NearestNeighbor")
 
 
-def wavenet_config(hp, max_batch, max_samples):
-    lib = _lib.load_library()
+def wavenet_config(hp, max_batch, max_samples, lib=None):
+    lib = lib or _lib.load_library()
     cfg = _lib.WnConfig()
     lib.tt2_wn_default_config(ctypes.byref(cfg), max_batch, max_samples)
     cfg.layers = hp.layers
@@ -271,19 +276,22 @@ def wavenet_config(hp, max_batch, max_samples):
 class WaveNetEngine(object):
     """Owns one tt2_wn_ctx."""
 
-    def __init__(self, hp, weights, max_batch, max_samples, device=0):
-        self.lib = _lib.load_library()
+    def __init__(self, hp, weights, max_batch, max_samples, device=0, lib=None):
+        self.lib = lib or _lib.load_library()
         self.hp = hp
-        self.cfg = wavenet_config(hp, max_batch, max_samples)
+        self.cfg = wavenet_config(hp, max_batch, max_samples, self.lib)
         self.caps = (max_batch, max_samples)
         self.hop = int(np.prod(hp.upsample_scales))
         h = ctypes.c_void_p()
-        check(self.lib.tt2_wn_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
+        self._ok(self.lib.tt2_wn_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
         self.h = h
         for name, arr in weights.items():
             if name.startswith("WaveNet_model/"):
-                _lib.load_tensor(self.lib.tt2_wn_load_tensor, self.h, name, arr)
-        check(self.lib.tt2_wn_finalize(self.h))
+                _lib.load_tensor(self.lib.tt2_wn_load_tensor, self.h, name, arr, self.lib)
+        self._ok(self.lib.tt2_wn_finalize(self.h))
+
+    def _ok(self, status):
+        _lib.check(status, self.lib)
 
     def close(self):
         if getattr(self, "h", None):
@@ -316,7 +324,7 @@ class WaveNetEngine(object):
         k = np.zeros((B, T), np.int32)
         lg = np.zeros((B, T, self.hp.out_channels), np.float32) if want_logits else None
         up = np.zeros((B, F, T), np.float32) if want_upsampled else None
-        check(self.lib.tt2_wn_generate(self.h, ptr(cond), B, T_f, ptr(um), ptr(ul), seed, ptr(tg),
+        self._ok(self.lib.tt2_wn_generate(self.h, ptr(cond), B, T_f, ptr(um), ptr(ul), seed, ptr(tg),
                                        ptr(y), ptr(k), ptr(lg), ptr(up)))
         return dict(y=y, k=k, logits=lg, upsampled=up)
 

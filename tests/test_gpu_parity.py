@@ -417,3 +417,26 @@ def test_decoder_step_chain_matches_decode(small_setup, constraint):
         np.testing.assert_allclose(stop, full["stop_token_prediction"][:, t], atol=1e-5)
         np.testing.assert_allclose(align, full["alignments"][:, :, t], atol=1e-5)
     eng.close()
+
+
+def test_cpu_backend_noise_streams_match_device():
+    """libtt2_cpu.so and libtt2.so draw identical seeded prenet keep bits and MoL uniforms (one
+    rng.h): the CPU baseline runs exactly the GPU bench's workload."""
+    import os
+    import subprocess
+    from tt2 import _lib
+    from tt2.engine import prenet_keep_bits, wavenet_noise
+    if not os.path.exists(_lib.CPU_LIB_PATH):
+        subprocess.check_call(["make", "-C", os.path.dirname(_lib.CPU_LIB_PATH), "libtt2_cpu.so"])
+    cpu = _lib.load_cpu_library()
+    n, B, P = 7, 3, 256
+    bits = np.zeros((n, 2, B, P), np.uint8)
+    _lib.check(cpu.tt2_prenet_keep_bits(5339, n, B, P, _lib.ptr(bits)), cpu)
+    np.testing.assert_array_equal(bits, prenet_keep_bits(5339, n, B, P))
+    T = 50
+    um = np.zeros((T, B, 10), np.float32)
+    ul = np.zeros((T, B), np.float32)
+    _lib.check(cpu.tt2_wn_noise(91, T, B, 10, 0, _lib.ptr(um), _lib.ptr(ul)), cpu)
+    gm, gl = wavenet_noise(91, T, B, 10)
+    np.testing.assert_array_equal(um, gm)
+    np.testing.assert_array_equal(ul, gl)
