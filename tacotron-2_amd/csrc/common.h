@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -248,6 +249,15 @@ __device__ inline float wn_gauss(uint64_t seed, long t, int Bg, int b) {
 }
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Persistent kernels (their work-groups spin on each other's hand-offs) launch cooperatively, which
+// makes the runtime refuse a grid that cannot be co-resident.  TT2_COOP=0 launches the same grid
+// with hipLaunchKernel (after the same occupancy checks): a diagnostic switch for profiler runs.
+inline hipError_t launch_persistent(const void* f, dim3 grid, dim3 block, void** args, size_t shm, hipStream_t s) {
+  static const bool coop = !(getenv("TT2_COOP") && atoi(getenv("TT2_COOP")) == 0);
+  return coop ? hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)shm, s)
+              : hipLaunchKernel(f, grid, block, args, shm, s);
+}
 
 // ------------------------------------------------------------------------------------------
 // DPP cross-lane reductions inside one 16-lane row (VALU only, no LDS round trip).  Every step

@@ -824,7 +824,7 @@ bool pd_device_ok(int dev) {
 void pd_launch(const PdArgs& a, hipStream_t s) {
   PdArgs arg = a;
   void* params[] = {&arg};
-  TT2_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_decode_persist), dim3(PD_NB), dim3(PD_NT),
+  TT2_HIP(launch_persistent(reinterpret_cast<const void*>(k_decode_persist), dim3(PD_NB), dim3(PD_NT),
                                      params, (unsigned)pd_lds_bytes(), s));
 }
 

@@ -1618,7 +1618,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
     a.err = reinterpret_cast<int*>(a.Hg + 2 * 2 * 32 * ENC_U);
     void* params[] = {&a};  // cooperative: all 128 work-groups co-resident (h hand-offs spin)
-    TT2_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_enc_bilstm_persist), dim3(2 * ENC_U / 4),
+    TT2_HIP(launch_persistent(reinterpret_cast<const void*>(k_enc_bilstm_persist), dim3(2 * ENC_U / 4),
                                        dim3(256), params, 0u, s));
     TT2_HIP(hipMemcpyAsync(&c->ctl_host[2], a.err, sizeof(int), hipMemcpyDeviceToHost, s));
     c->enc_err_check = true;

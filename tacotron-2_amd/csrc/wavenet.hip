@@ -857,7 +857,7 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
       w.b = b;
       TT2_HIP(hipMemsetAsync(c->gran.p, 0, gbytes, s));  // every polled word starts at 0
       void* params[] = {&w};
-      TT2_HIP(hipLaunchCooperativeKernel(kern, dim3(ww_blocks(R, c->L)), dim3(WW_THREADS), params, shm, s));
+      TT2_HIP(launch_persistent(kern, dim3(ww_blocks(R, c->L)), dim3(WW_THREADS), params, shm, s));
       TT2_HIP(hipMemcpyAsync(c->status_host, c->gran.p, sizeof(int), hipMemcpyDeviceToHost, s));
     }
     TT2_HIP(hipEventRecord(c->ev[3], s));
@@ -893,7 +893,7 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
     const auto kern = pipe_kernel(c->cfg.legacy != 0, c->cfg.residual_legacy != 0, c->C == 2);
     // cooperative: every stage work-group of the launch co-resident (the stage hand-offs spin)
     void* params[] = {&a};
-    TT2_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kern), dim3(grid), dim3(WN_THREADS), params,
+    TT2_HIP(launch_persistent(reinterpret_cast<const void*>(kern), dim3(grid), dim3(WN_THREADS), params,
                                        (unsigned)shm, s));
     TT2_HIP(hipMemcpyAsync(c->status_host, c->gran.p, sizeof(int), hipMemcpyDeviceToHost, s));
   }
