@@ -92,6 +92,10 @@ typedef struct tt2_config {
   int emt_attn;            /* args.attn: 0 = Tacotron model, 1 'simple', 2 'multihead', 3 'style_tokens' */
   int emt_ref_gru;         /* args.emt_ref_gru: 0 'none', 1 'gru', 2 'gru_multi' (modules.py:35-55) */
   int n_emt;               /* style_tokens: one-hot emotion label width (synthesizer.py:45: 4) */
+  /* style path of the Tacotron model (tacotron.py:236-308): 0 GST over style tokens (fork default),
+   * 1 the 128-wide reference embeddings themselves (args.pretrained_emb_disc_all; use_gst=0 implies
+   * it), 2 ReferenceEncoderAdaIn (args.adain: one shared 'refnet', both mels, D_mem = 2U + 128) */
+  int style_mode;
 } tt2_config;
 
 typedef struct tt2_ctx tt2_ctx;

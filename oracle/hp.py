@@ -1,8 +1,10 @@
 """TEST INFRASTRUCTURE ONLY — adapters from an HParams object to the oracle's plain dicts."""
 
 
-def oracle_hp(hp, synthesis_constraint=False):
-    return dict(zoneout=hp.tacotron_zoneout_rate, num_mels=hp.num_mels,
+def oracle_hp(hp, synthesis_constraint=False, style="gst"):
+    """style: 'gst' | 'embed' | 'adain' (tacotron.py:236-308); 'gst' without hp.use_gst is 'embed'."""
+    return dict(style="embed" if style == "gst" and not hp.use_gst else style,
+                zoneout=hp.tacotron_zoneout_rate, num_mels=hp.num_mels,
                 max_abs_value=hp.max_abs_value, lower_bound_decay=hp.lower_bound_decay,
                 clip_outputs=hp.clip_outputs, stop_at_any=hp.stop_at_any,
                 mask_encoder=hp.mask_encoder, cumulative=hp.cumulative_weights,

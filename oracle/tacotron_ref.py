@@ -225,14 +225,52 @@ def gst_attention(ref, W, tag, num_heads=4, dt=np.float32):
     return ctx.reshape(N, num_heads * value.shape[-1])
 
 
+def reference_encoder_adain(mel_spk, mel_emt, W, dt=np.float32, scope="refnet/"):
+    """ReferenceEncoderAdaIn.__call__ (modules.py:75-107) with strides (2,2),(2,2),(1,1)x4
+    (tacotron.py:237): shared conv2d + ReLU stack without batch norm on both mels; per sample and
+    channel moments over (time, freq); spk_norm = tf.nn.batch_normalization(spk, mean_spk, var_spk,
+    offset=mean_emt, scale=var_emt, 1e-9); spk = 0.9·spk + 0.1·spk_norm; GRU over every frame;
+    last output -> Dense(128, tanh)."""
+    strides = [(2, 2), (2, 2), (1, 1), (1, 1), (1, 1), (1, 1)]
+    xs = [np.asarray(m, dt)[..., None] for m in (mel_spk, mel_emt)]
+    for i in range(6):
+        s = scope + "conv2d_{}/".format(i)
+        k, b = _w(W, s + "conv2d/kernel", dt), _w(W, s + "conv2d/bias", dt)
+        xs = [np.maximum(conv2d_same(x, k, b, strides[i]), dt(0)) for x in xs]
+    spk, emt = xs
+    m_s = spk.mean(axis=(1, 2), keepdims=True)
+    v_s = np.square(spk - m_s).mean(axis=(1, 2), keepdims=True)
+    m_e = emt.mean(axis=(1, 2), keepdims=True)
+    v_e = np.square(emt - m_e).mean(axis=(1, 2), keepdims=True)
+    inv = (dt(1) / np.sqrt(v_s + dt(1e-9))) * v_e                 # nn.batch_normalization
+    norm = spk * inv + (m_e - m_s * inv)
+    spk = spk * dt(0.9) + norm * dt(0.1)
+    N, T2, F2, C = spk.shape
+    x = spk.reshape(N, T2, F2 * C)
+    kg = _w(W, scope + "rnn/gru_cell/gates/kernel", dt)
+    bg = _w(W, scope + "rnn/gru_cell/gates/bias", dt)
+    kc = _w(W, scope + "rnn/gru_cell/candidate/kernel", dt)
+    bc = _w(W, scope + "rnn/gru_cell/candidate/bias", dt)
+    h = np.zeros((N, bc.shape[0]), dt)
+    for t in range(T2):
+        h = gru_cell(x[:, t], h, kg, bg, kc, bc)
+    return np.tanh(dense(h, _w(W, scope + "dense/kernel", dt), _w(W, scope + "dense/bias", dt)))
+
+
 def style_embedding(ref_emt, ref_spk, W, hp, dt=np.float32):
-    """tacotron.py:251-308 for the fork defaults (use_gst, not adain, not pretrained_emb_disc_all):
-    refnet_emt/refnet_spk → GST emt/spk → concat [N, 512] (or emt only when emt_only)."""
+    """tacotron.py:236-308: hp['style'] 'gst' (the fork default: refnet_emt/refnet_spk → GST
+    emt/spk → concat [N, 512]), 'embed' (args.pretrained_emb_disc_all or use_gst=False: the
+    reference embeddings themselves, :284-291) or 'adain' (args.adain, :266-268); emt_only drops
+    the speaker half."""
+    mode = hp.get("style", "gst")
+    if mode == "adain":
+        return reference_encoder_adain(ref_spk, ref_emt, W, dt)
     r_e = reference_encoder(ref_emt, W, "refnet_emt/", dt)
-    parts = [gst_attention(r_e, W, "emt", hp.get("num_heads", 4), dt)]
+    parts = [gst_attention(r_e, W, "emt", hp.get("num_heads", 4), dt) if mode == "gst" else r_e]
     if not hp.get("emt_only", False):
         r_s = reference_encoder(ref_spk, W, "refnet_spk/", dt)
-        parts.append(gst_attention(r_s, W, "spk", hp.get("num_heads", 4), dt))
+        parts.append(gst_attention(r_s, W, "spk", hp.get("num_heads", 4), dt) if mode == "gst"
+                     else r_s)
     return np.concatenate(parts, axis=-1)
 
 

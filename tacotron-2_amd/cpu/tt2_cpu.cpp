@@ -212,7 +212,7 @@ struct tt2_ctx {
   tt2_config cfg;
   WeightMap wm;
   bool finalized = false;
-  int nm, E, Cenc, U, A, F, KL, P, H, PC, Dm, SW, nref;
+  int nm, E, Cenc, U, A, F, KL, P, H, PC, Dm, SW, nref, nmel, style_mode;
   // encoded batch
   int B = 0, T_in = 0;
   bool encoded = false, decoded = false;
@@ -270,49 +270,59 @@ void bilstm(tt2_ctx* c, const float* x, int B, int T, int C, float* out) {
   }
 }
 
-// ReferenceEncoder (modules.py:20-64) + GST MultiheadAttention (multihead_attention.py:35-132,
-// tacotron.py:276-282): mel [B][T_ref][nm] -> style [B][sed] written at column off of style [B][SW]
-void refnet_gst(tt2_ctx* c, const char* tag, const float* mel, int B, int TR, float* style, int off) {
+// ReferenceEncoder CNN stack (modules.py:20-33; conv2d() :499-511 = conv, BN, ReLU) or, adain,
+// ReferenceEncoderAdaIn's (modules.py:75-87: conv + ReLU, no BN, strides (2,2),(2,2),(1,1)x4):
+// mel [B][TR][nm] -> NHWC [B][H][W][C]
+std::vector<float> conv_stack(tt2_ctx* c, const std::string& s, const float* mel, int B, int TR, bool adain, int& H,
+                              int& Wd, int& C) {
   const auto& cfg = c->cfg;
-  const std::string s = std::string("refnet_") + tag + "/";
   std::vector<float> x(mel, mel + (size_t)B * TR * c->nm), y;
-  int H = TR, Wd = c->nm, C = 1;
+  H = TR; Wd = c->nm; C = 1;
   for (int i = 0; i < 6; ++i) {
     const std::string s2 = s + "conv2d_" + std::to_string(i) + "/";
-    const int f = cfg.reference_filters[i];
+    const int f = cfg.reference_filters[i], st = adain && i >= 2 ? 1 : 2;
     const auto& k = W(c, s2 + "conv2d/kernel", {3, 3, C, f});
     const auto& bi = W(c, s2 + "conv2d/bias", {f});
-    const BN bn = bn_consts(c->wm, TP + s2, f);
-    const int Ho = (H + 1) / 2, Wo = (Wd + 1) / 2;
-    const int pt = std::max((Ho - 1) * 2 + 3 - H, 0) / 2, pl = std::max((Wo - 1) * 2 + 3 - Wd, 0) / 2;
+    BN bn;
+    if (!adain) bn = bn_consts(c->wm, TP + s2, f);
+    const int Ho = (H + st - 1) / st, Wo = (Wd + st - 1) / st;
+    const int pt = std::max((Ho - 1) * st + 3 - H, 0) / 2, pl = std::max((Wo - 1) * st + 3 - Wd, 0) / 2;
     const long rows = (long)B * Ho * Wo;
     std::vector<float> col(rows * 9 * C, 0.f);
 #pragma omp parallel for schedule(static)
     for (long r = 0; r < rows; ++r) {
-      const int bb = (int)(r / (Ho * Wo)), ho = (int)(r / Wo % Ho), wo = (int)(r % Wo);
+      const int bb = (int)(r / ((long)Ho * Wo)), ho = (int)(r / Wo % Ho), wo = (int)(r % Wo);
       for (int ki = 0; ki < 3; ++ki)
         for (int kj = 0; kj < 3; ++kj) {
-          const int hi = ho * 2 + ki - pt, wi = wo * 2 + kj - pl;
+          const int hi = ho * st + ki - pt, wi = wo * st + kj - pl;
           if (hi < 0 || hi >= H || wi < 0 || wi >= Wd) continue;
           std::memcpy(&col[(r * 9 + ki * 3 + kj) * C], &x[(((size_t)bb * H + hi) * Wd + wi) * C], sizeof(float) * C);
         }
     }
     y.assign(rows * f, 0.f);
     gemm(col.data(), (int)rows, 9 * C, 9 * C, k.data(), f, bi.data(), y.data(), f);
-    for (long i = 0; i < rows; ++i)
-      for (int o = 0; o < f; ++o) y[i * f + o] = std::max(y[i * f + o] * bn.inv[o] + bn.sh[o], 0.f);
+    for (long i2 = 0; i2 < rows; ++i2)
+      for (int o = 0; o < f; ++o) {
+        const float v = adain ? y[i2 * f + o] : y[i2 * f + o] * bn.inv[o] + bn.sh[o];
+        y[i2 * f + o] = std::max(v, 0.f);
+      }
     x.swap(y);
     H = Ho; Wd = Wo; C = f;
   }
-  const int gin = Wd * C, D = cfg.reference_depth;
+  return x;
+}
+
+// GRU over every frame, last output -> dense(128, tanh) (modules.py:57-64): x [B][H][gin] -> ref
+std::vector<float> gru_dense(tt2_ctx* c, const std::string& s, const float* x, int B, int H, int gin) {
+  const int D = c->cfg.reference_depth;
   const auto& kg = W(c, s + "rnn/gru_cell/gates/kernel", {gin + D, 2 * D});
   const auto& bg = W(c, s + "rnn/gru_cell/gates/bias", {2 * D});
   const auto& kc = W(c, s + "rnn/gru_cell/candidate/kernel", {gin + D, D});
   const auto& bc = W(c, s + "rnn/gru_cell/candidate/bias", {D});
   std::vector<float> h((size_t)B * D, 0.f), g((size_t)B * 2 * D), cd((size_t)B * D), rh((size_t)B * D);
   std::vector<float> xg((size_t)B * H * 2 * D), xc((size_t)B * H * D);
-  gemm(x.data(), B * H, gin, gin, kg.data(), 2 * D, bg.data(), xg.data(), 2 * D);
-  gemm(x.data(), B * H, gin, gin, kc.data(), D, bc.data(), xc.data(), D);
+  gemm(x, B * H, gin, gin, kg.data(), 2 * D, bg.data(), xg.data(), 2 * D);
+  gemm(x, B * H, gin, gin, kc.data(), D, bc.data(), xc.data(), D);
   for (int t = 0; t < H; ++t) {
     gemm(h.data(), B, D, D, kg.data() + (size_t)gin * 2 * D, 2 * D, nullptr, g.data(), 2 * D);
     for (int bb = 0; bb < B; ++bb)
@@ -331,9 +341,14 @@ void refnet_gst(tt2_ctx* c, const char* tag, const float* mel, int B, int TR, fl
   gemm(h.data(), B, D, D, W(c, s + "dense/kernel", {D, 128}).data(), 128, W(c, s + "dense/bias", {128}).data(),
        ref.data(), 128);
   for (auto& v : ref) v = std::tanh(v);
-  // GST: values tanh(tokens) [ntok][tokd]; q = ref·Wq + bq; k = values·Wk + bk; per head
-  // normed_v·tanh(k + q + b), softmax over tokens, context = weights·values (every head sees all
-  // tokd channels of the values), heads concatenated
+  return ref;
+}
+
+// GST MultiheadAttention (multihead_attention.py:35-132, tacotron.py:276-282): values tanh(tokens);
+// q = ref·Wq + bq; k = values·Wk + bk; per head normed_v·tanh(k + q + b), softmax over tokens,
+// context = weights·values (every head sees all tokd channels), heads concatenated into style
+void gst(tt2_ctx* c, const char* tag, const std::vector<float>& ref, int B, float* style, int off) {
+  const auto& cfg = c->cfg;
   const int ntok = cfg.num_gst, heads = cfg.num_heads, tokd = cfg.style_embed_depth / heads, Aa = cfg.style_att_dim;
   const int dh = Aa / heads;
   const std::string mh = std::string("Multihead-attention-") + tag + "/";
@@ -371,6 +386,39 @@ void refnet_gst(tt2_ctx* c, const char* tag, const float* mel, int B, int TR, fl
     }
 }
 
+// ReferenceEncoderAdaIn (modules.py:89-107): per (row, channel) moments over (time, freq) of both
+// maps; spk = 0.9·spk + 0.1·batch_normalization(spk, m_s, v_s, offset=m_e, scale=v_e, 1e-9)
+void adain_mix(std::vector<float>& spk, const std::vector<float>& emt, int B, int HWs, int HWe, int C) {
+  auto moments = [&](const std::vector<float>& x, int HW, std::vector<float>& m, std::vector<float>& v) {
+    m.assign((size_t)B * C, 0.f);
+    v.assign((size_t)B * C, 0.f);
+    for (int b = 0; b < B; ++b)
+      for (int ch = 0; ch < C; ++ch) {
+        double s1 = 0.0;
+        for (int i = 0; i < HW; ++i) s1 += x[((size_t)b * HW + i) * C + ch];
+        const float mean = (float)(s1 / HW);
+        double s2 = 0.0;
+        for (int i = 0; i < HW; ++i) {
+          const float d = x[((size_t)b * HW + i) * C + ch] - mean;
+          s2 += (double)d * d;
+        }
+        m[(size_t)b * C + ch] = mean;
+        v[(size_t)b * C + ch] = (float)(s2 / HW);
+      }
+  };
+  std::vector<float> ms, vs, me, ve;
+  moments(spk, HWs, ms, vs);
+  moments(emt, HWe, me, ve);
+  for (int b = 0; b < B; ++b)
+    for (int i = 0; i < HWs; ++i)
+      for (int ch = 0; ch < C; ++ch) {
+        const size_t k = (size_t)b * C + ch;
+        const float inv = (1.f / std::sqrt(vs[k] + 1e-9f)) * ve[k];
+        float& x = spk[((size_t)b * HWs + i) * C + ch];
+        x = x * 0.9f + (x * inv + (me[k] - ms[k] * inv)) * 0.1f;
+      }
+}
+
 void encode(tt2_ctx* c, const int* ids, const int* lengths, int B, int T, const float* ref[2], const int TR[2]) {
   const auto& cfg = c->cfg;
   CK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_finalize_weights not called");
@@ -400,12 +448,31 @@ void encode(tt2_ctx* c, const int* ids, const int* lengths, int B, int T, const 
   }
   std::vector<float> enc((size_t)B * T * 2 * c->U);
   bilstm(c, x.data(), B, T, cin, enc.data());
-  // reference encoders + GST (tacotron.py:251-308)
+  // reference encoders + style (tacotron.py:236-308): GST, the embeddings themselves, or AdaIN
   c->style.assign((size_t)B * std::max(c->SW, 1), 0.f);
   const char* tags[2] = {"emt", "spk"};
-  for (int r = 0; r < c->nref; ++r) {
+  for (int r = 0; r < c->nmel; ++r)
     CK(ref[r] && TR[r] >= 1 && TR[r] <= cfg.max_T_ref, TT2_ERR_SHAPE_MISMATCH, "T_ref exceeds capacity");
-    refnet_gst(c, tags[r], ref[r], B, TR[r], c->style.data(), r * cfg.style_embed_depth);
+  int H, Wd, C;
+  if (c->style_mode == 2) {
+    int He, We, Ce;
+    const std::vector<float> xe = conv_stack(c, "refnet/", ref[0], B, TR[0], true, He, We, Ce);
+    std::vector<float> xs = conv_stack(c, "refnet/", ref[1], B, TR[1], true, H, Wd, C);
+    adain_mix(xs, xe, B, H * Wd, He * We, C);
+    const auto r = gru_dense(c, "refnet/", xs.data(), B, H, Wd * C);
+    for (int b = 0; b < B; ++b) std::memcpy(&c->style[(size_t)b * c->SW], &r[(size_t)b * 128], sizeof(float) * 128);
+  } else {
+    for (int r = 0; r < c->nref; ++r) {
+      const std::string sc = std::string("refnet_") + tags[r] + "/";
+      const std::vector<float> x = conv_stack(c, sc, ref[r], B, TR[r], false, H, Wd, C);
+      const auto e = gru_dense(c, sc, x.data(), B, H, Wd * C);
+      if (c->style_mode == 0) {
+        gst(c, tags[r], e, B, c->style.data(), r * cfg.style_embed_depth);
+      } else {
+        for (int b = 0; b < B; ++b)
+          std::memcpy(&c->style[(size_t)b * c->SW + r * 128], &e[(size_t)b * 128], sizeof(float) * 128);
+      }
+    }
   }
   // values = [enc | tiled style] masked past each row's length; keys = memory_layer(values)
   const int E2 = 2 * c->U;
@@ -600,7 +667,7 @@ void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_re
   c->clip_outputs = 1; c->stop_at_any = 0; c->mask_encoder = 1; c->cumulative_weights = 1;
   c->synthesis_constraint = 0; c->constraint_monotonic = 0; c->attention_win_size = 7;
   c->max_batch = max_batch; c->max_T_in = max_T_in; c->max_T_ref = max_T_ref; c->max_iters = max_iters;
-  c->emt_attn = 0; c->emt_ref_gru = 0; c->n_emt = 4;
+  c->emt_attn = 0; c->emt_ref_gru = 0; c->n_emt = 4; c->style_mode = 0;
 }
 
 tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
@@ -610,15 +677,20 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     *out = nullptr;
     CK(cfg->max_batch >= 1 && cfg->max_T_in >= 1 && cfg->max_iters >= 1, TT2_ERR_INVALID_ARG, "capacities must be >= 1");
     CK(cfg->emt_attn == 0, TT2_ERR_INVALID_ARG, "the CPU backend builds the Tacotron model only (emt_attn = 0)");
-    CK(cfg->use_gst, TT2_ERR_INVALID_ARG, "use_gst=False (paper Tacotron-2 memory) is not built yet");
+
     CK(cfg->attention_filters <= 64, TT2_ERR_INVALID_ARG, "attention_filters must be <= 64");
     auto c = std::make_unique<tt2_ctx>();
     c->cfg = *cfg;
     c->nm = cfg->num_mels; c->E = cfg->embedding_dim; c->Cenc = cfg->enc_conv_channels; c->U = cfg->encoder_lstm_units;
     c->A = cfg->attention_dim; c->F = cfg->attention_filters; c->KL = cfg->attention_kernel; c->P = cfg->prenet_units;
     c->H = cfg->decoder_lstm_units; c->PC = cfg->postnet_channels;
-    c->nref = cfg->emt_only ? 1 : 2;
-    c->SW = c->nref * cfg->style_embed_depth;
+    // style path (tacotron.py:236-308): use_gst=False takes the reference embeddings themselves
+    c->style_mode = (!cfg->use_gst && cfg->style_mode == 0) ? 1 : cfg->style_mode;
+    CK(c->style_mode >= 0 && c->style_mode <= 2, TT2_ERR_INVALID_ARG, "style_mode must be 0..2");
+    CK(!(c->style_mode == 2 && cfg->emt_only), TT2_ERR_INVALID_ARG, "must provide speaker reference to use AdaIn");
+    c->nref = c->style_mode == 2 ? 1 : (cfg->emt_only ? 1 : 2);
+    c->nmel = c->style_mode == 2 ? 2 : c->nref;
+    c->SW = c->style_mode == 0 ? c->nref * cfg->style_embed_depth : 128 * c->nref;
     c->Dm = 2 * c->U + c->SW;
     *out = c.release();
   });
@@ -650,7 +722,7 @@ tt2_status tt2_encode(tt2_ctx* c, const int32_t* ids, const int32_t* lengths, in
                       int T_ref_emt, const float* ref_spk, int T_ref_spk, float* memory_out, float* style_out) {
   return guard([&] {
     CK(c && ids && lengths, TT2_ERR_INVALID_ARG, "tt2_encode: null argument");
-    CK(ref_emt && (c->nref < 2 || ref_spk), TT2_ERR_INVALID_ARG, "must provide references");  // tacotron.py:66-67
+    CK(ref_emt && (c->nmel < 2 || ref_spk), TT2_ERR_INVALID_ARG, "must provide references");  // tacotron.py:66-67
     const float* refs[2] = {ref_emt, ref_spk};
     const int trs[2] = {T_ref_emt, T_ref_spk};
     encode(c, ids, lengths, B, T_in, refs, trs);

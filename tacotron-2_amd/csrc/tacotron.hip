@@ -335,7 +335,11 @@ __global__ __launch_bounds__(256) void k_ref_gru_gst(RefGstArgs a) {
     ref[tid] = tanhf(s + a.bd[tid]);
     a.ref_out[b * 128 + tid] = ref[tid];
   }
-  if (!a.tokens) return;  // reference embedding only (uniform across the block)
+  if (!a.tokens) {  // the reference embedding itself: pretrained_emb_disc_all / use_gst=False /
+                    // AdaIN (tacotron.py:266-291), or refnet_spk of the emt variant (style null)
+    if (a.style && tid < 128) a.style[(long)b * a.style_w + a.style_off + tid] = ref[tid];
+    return;
+  }
   // GST values = tanh(tokens)
   for (int i = tid; i < a.ntok * a.tokd; i += blockDim.x) vals[i] = tanhf(a.tokens[i]);
   __syncthreads();
@@ -398,6 +402,55 @@ __global__ void k_memory(const float* __restrict__ enc, const float* __restrict_
     if (valid) v = d < E2 ? enc[(long)row * E2 + d] : style[(long)b * SW + d - E2];
     values[(long)row * D + d] = v;
   }
+}
+
+// ReferenceEncoderAdaIn (modules.py:89-98): tf.nn.moments(x, axes=[1, 2]) of the NHWC conv output
+// x [B][HW][C] per (row, channel), two-pass (mean, then mean squared deviation) -> mv[b][c] = {m, v}
+__global__ __launch_bounds__(256) void k_adain_moments(const float* __restrict__ x, int HW, int C,
+                                                       float* __restrict__ mv) {
+  __shared__ float red[256];
+  const int b = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x;
+  const float* xb = x + (long)b * HW * C + ch;
+  float acc = 0.f;
+  for (int i = tid; i < HW; i += 256) acc += xb[(long)i * C];
+  red[tid] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  const float mean = red[0] / (float)HW;
+  __syncthreads();
+  acc = 0.f;
+  for (int i = tid; i < HW; i += 256) {
+    const float d = xb[(long)i * C] - mean;
+    acc += d * d;
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    mv[((long)b * C + ch) * 2] = mean;
+    mv[((long)b * C + ch) * 2 + 1] = red[0] / (float)HW;
+  }
+}
+
+// spk = 0.9·spk + 0.1·tf.nn.batch_normalization(spk, mean_spk, var_spk, offset=mean_emt,
+// scale=var_emt, 1e-9) (modules.py:94-98): inv = rsqrt(var_s + eps)·var_e, x·inv + (m_e − m_s·inv)
+__global__ void k_adain_mix(float* __restrict__ x, long n, int HW, int C, const float* __restrict__ mv_s,
+                            const float* __restrict__ mv_e) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int ch = (int)(i % C);
+  const long b = i / ((long)HW * C);
+  const float* s = mv_s + (b * C + ch) * 2;
+  const float* e = mv_e + (b * C + ch) * 2;
+  const float inv = (1.0f / sqrtf(s[1] + 1e-9f)) * e[1];
+  const float v = x[i];
+  x[i] = v * 0.9f + (v * inv + (e[0] - s[0] * inv)) * 0.1f;
 }
 
 // ---- decoder -------------------------------------------------------------------------------
@@ -1106,6 +1159,9 @@ __global__ void k_clip_frames(const float* __restrict__ src, long src_bstride, f
 // ==========================================================================================
 // Host side
 // ==========================================================================================
+// ReferenceEncoder strides (2,2) everywhere; ReferenceEncoderAdaIn (2,2),(2,2),(1,1)x4 (tacotron.py:237)
+inline int refnet_stride(bool adain, int layer) { return adain && layer >= 2 ? 1 : 2; }
+
 struct RefNetDev {
   DevBuf cw[6], cb[6], bs[6], bh[6];
   DevBuf wx, bx, whg, whc, kd, bd, tok, kq, bq, kk, bk, av, ag, ab;  // wx = [Wg_x | Wc_x], bx = [bg | bc]
@@ -1129,7 +1185,10 @@ struct tt2_ctx {
   tt2::WeightMap host;
   bool finalized = false;
   int nm, E, Cenc, U, Dm, E2, A, F, KL, P, H, PC, SW, K1, Kp, NPJ, NPF, KSQ = tt2::KSQ_C, KSP = tt2::KSP_C, KLp, Fp;
-  int nref;
+  int nref;        // reference encoders with their own weights
+  int nmel = 0;    // reference mels the encode reads (AdaIN: one encoder, both mels)
+  int style_mode = 0;  // 0 GST, 1 reference embeddings, 2 AdaIN (tt2_config.style_mode)
+  tt2::DevBuf adain_mv;  // [2][B][C][2] per-channel moments (emt, spk)
   // weights
   tt2::DevBuf emb;
   tt2::DevBuf enc_cw[8], enc_cb[8], enc_bs[8], enc_bh[8];
@@ -1285,18 +1344,19 @@ static void finalize(tt2_ctx* c) {
   // consumes, and refnet_spk's GRU + dense; no style tokens)
   const char* tags[2] = {"emt", "spk"};
   const bool emt_model = c->emt.on();
+  const bool adain = c->style_mode == 2;  // one 'refnet' without batch norm (modules.py:66-107)
   for (int r = 0; r < c->nref; ++r) {
     auto& R = c->ref[r];
-    const std::string s = P + "refnet_" + tags[r] + "/";
+    const std::string s = P + (adain ? std::string("refnet") : std::string("refnet_") + tags[r]) + "/";
     int ci = 1, F = cfg.num_mels;
     for (int i = 0; i < 6; ++i) {
       const std::string s2 = s + "conv2d_" + std::to_string(i) + "/";
       const int f = cfg.reference_filters[i];
       upload(R.cw[i], need(wm, s2 + "conv2d/kernel", {3, 3, ci, f}));
       upload(R.cb[i], need(wm, s2 + "conv2d/bias", {f}));
-      bn_consts(wm, s2, f, R.bs[i], R.bh[i]);
+      if (!adain) bn_consts(wm, s2, f, R.bs[i], R.bh[i]);
       ci = f;
-      F = (F + 1) / 2;
+      if (refnet_stride(adain, i) == 2) F = (F + 1) / 2;
     }
     const int gin = F * ci, D = cfg.reference_depth;
     R.gin = gin;
@@ -1321,7 +1381,7 @@ static void finalize(tt2_ctx* c) {
     }
     upload(R.kd, need(wm, s + "dense/kernel", {D, 128}));
     upload(R.bd, need(wm, s + "dense/bias", {128}));
-    if (emt_model) continue;
+    if (emt_model || c->style_mode != 0) continue;
     const int tokd = cfg.style_embed_depth / cfg.num_heads, Aa = cfg.style_att_dim;
     upload(R.tok, need(wm, P + "style_tokens_" + tags[r], {cfg.num_gst, tokd}));
     const std::string mh = P + "Multihead-attention-" + tags[r] + "/";
@@ -1510,11 +1570,14 @@ static void alloc_acts(tt2_ctx* c) {
   {
     long t = TR, f = c->nm;
     for (int i = 0; i < 6; ++i) {
-      t = (t + 1) / 2;
-      f = (f + 1) / 2;
+      if (refnet_stride(c->style_mode == 2, i) == 2) {
+        t = (t + 1) / 2;
+        f = (f + 1) / 2;
+      }
       mx = std::max(mx, B * t * f * cfg.reference_filters[i]);
     }
   }
+  if (c->style_mode == 2) c->adain_mv.alloc(sizeof(float) * 2 * B * cfg.reference_filters[5] * 2);
   c->conv_a.alloc(std::max(mx, 16L) * 4);
   c->conv_b.alloc(std::max(mx, 16L) * 4);
   c->ref_out.alloc(2 * B * 128 * 4);
@@ -1569,7 +1632,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     TT2_HIP(hipMemcpyAsync(c->emt.labels.p, c->emt_labels.data(), sizeof(int) * 32, hipMemcpyHostToDevice, s));
   // fork: the reference encoders (GST) depend only on the reference mels -> own stream, joined
   // before k_memory; they fill the CUs the 128-work-group persistent BiLSTM leaves idle
-  const hipStream_t sr = ((cfg.use_gst || c->emt.on()) && c->ref_stream) ? c->ref_stream : s;
+  const hipStream_t sr = (c->nmel > 0 && c->ref_stream) ? c->ref_stream : s;
   if (sr != s) {
     TT2_HIP(hipEventRecord(c->ref_ev[0], s));
     TT2_HIP(hipStreamWaitEvent(sr, c->ref_ev[0], 0));
@@ -1632,36 +1695,42 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
   }
   TT2_HIP(hipGetLastError());
   // reference encoders + GST
-  if (cfg.use_gst || c->emt.on()) {
-    for (int r = 0; r < c->nref; ++r) {
-      auto& R = c->ref[r];
-      const int TR = T_ref[r];
+  {
+    const bool adain = c->style_mode == 2;
+    float* bufs[2] = {c->conv_a.as<float>(), c->conv_b.as<float>()};
+    // conv2d 3x3 'same' stack of reference encoder R over mel [B][TR][nm] (conv2d(), modules.py:
+    // 499-511: conv, BN, ReLU; AdaIN: conv + ReLU, no BN, modules.py:84-87); NHWC out [B][H][W][C]
+    auto conv_stack = [&](const RefNetDev& R, const float* x, int TR, int& H, int& Wd, int& C) -> float* {
       TT2_CHECK(TR >= 1 && TR <= cfg.max_T_ref, TT2_ERR_SHAPE_MISMATCH, "T_ref exceeds capacity");
-      const float* x = ref_d[r];
-      int H = TR, Wd = c->nm, C = 1;
-      float* bufs[2] = {c->conv_a.as<float>(), c->conv_b.as<float>()};
+      H = TR; Wd = c->nm; C = 1;
+      float* out = nullptr;
       for (int i = 0; i < 6; ++i) {
-        const int f = cfg.reference_filters[i];
-        const int Ho = (H + 1) / 2, Wo = (Wd + 1) / 2;
+        const int f = cfg.reference_filters[i], st = refnet_stride(adain, i);
+        const int Ho = (H + st - 1) / st, Wo = (Wd + st - 1) / st;
         GemmArgs g;
         g.M = B * Ho * Wo; g.N = f; g.K = 9 * C; g.a_mode = A_CONV2D; g.A = x;
-        g.H = H; g.Wd = Wd; g.C = C; g.Ho = Ho; g.Wo = Wo; g.kh = 3; g.kw2 = 3; g.sh = 2; g.sw = 2;
-        g.pt = std::max((Ho - 1) * 2 + 3 - H, 0) / 2; g.pl = std::max((Wo - 1) * 2 + 3 - Wd, 0) / 2;
+        g.H = H; g.Wd = Wd; g.C = C; g.Ho = Ho; g.Wo = Wo; g.kh = 3; g.kw2 = 3; g.sh = st; g.sw = st;
+        g.pt = std::max((Ho - 1) * st + 3 - H, 0) / 2; g.pl = std::max((Wo - 1) * st + 3 - Wd, 0) / 2;
         g.Bw = R.cw[i].as<float>(); g.ldb = f; g.Cout = bufs[i & 1]; g.ldc = f;
-        g.bias = R.cb[i].as<float>(); g.act = ACT_BN_RELU;
-        g.bn_scale = R.bs[i].as<float>(); g.bn_shift = R.bh[i].as<float>();
+        g.bias = R.cb[i].as<float>();
+        if (adain) {
+          g.act = ACT_RELU;
+        } else {
+          g.act = ACT_BN_RELU;
+          g.bn_scale = R.bs[i].as<float>(); g.bn_shift = R.bh[i].as<float>();
+        }
         g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
         g.kpart = c->kpart.as<float>(); g.kpart_floats = (long)(c->kpart.bytes / sizeof(float));  // deep layers: few tiles
         gemm(g, sr);
-        x = bufs[i & 1];
+        x = out = bufs[i & 1];
         H = Ho; Wd = Wo; C = f;
       }
+      return out;
+    };
+    // GRU over every frame + dense(128, tanh) (modules.py:57-64), then GST (gst=true) or the
+    // embedding itself into the style columns [style_off, +128)
+    auto gru_head = [&](const RefNetDev& R, const float* x, int H, int r, bool gst, float* style, int style_off) {
       const int D = cfg.reference_depth;
-      TT2_CHECK(Wd * C == R.gin, TT2_ERR_SHAPE_MISMATCH, "reference encoder: GRU input width mismatch");
-      if (c->emt.on() && r == 0) {  // all_outputs=True: attended values of the emotion attention
-        emt_encode(c->emt, x, B, H, sr);
-        continue;
-      }
       c->refxg.alloc(sizeof(float) * (size_t)B * H * 3 * D);
       {  // x rows of the GRU gates + candidate kernels for every frame at once
         GemmArgs g;
@@ -1676,16 +1745,47 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
       a.xg = c->refxg.as<float>(); a.T2 = H; a.D = D;
       a.whg = R.whg.as<float>(); a.whc = R.whc.as<float>();
       a.kd = R.kd.as<float>(); a.bd = R.bd.as<float>();
-      a.tokens = c->emt.on() ? nullptr : R.tok.as<float>();  // null: GRU + dense only (refnet_spk of the emt variant)
+      a.tokens = gst ? R.tok.as<float>() : nullptr;
       a.kq = R.kq.as<float>(); a.bq = R.bq.as<float>(); a.kk = R.kk.as<float>(); a.bk = R.bk.as<float>();
       a.av = R.av.as<float>(); a.ag = R.ag.as<float>(); a.ab = R.ab.as<float>();
       a.ntok = cfg.num_gst; a.tokd = cfg.style_embed_depth / cfg.num_heads; a.A = cfg.style_att_dim;
       a.heads = cfg.num_heads; a.ref_out = c->ref_out.as<float>() + r * cfg.max_batch * 128;
-      a.style = c->style.as<float>(); a.style_w = c->SW; a.style_off = r * cfg.style_embed_depth;
+      a.style = style; a.style_w = c->SW; a.style_off = style_off;
       const size_t shm = sizeof(float) * (a.D + a.D + 2 * a.D + 128 + a.A + a.ntok * a.A + a.ntok * a.tokd +
                                           a.heads * a.ntok + 16);
       hipLaunchKernelGGL(k_ref_gru_gst, dim3(B), dim3(256), shm, sr, a);
       TT2_HIP(hipGetLastError());
+    };
+    int H = 0, Wd = 0, C = 0;
+    if (adain && !c->emt.on()) {
+      // ReferenceEncoderAdaIn(spk, emt) (modules.py:75-107): the emotion map's per-channel moments
+      // restyle the speaker map, which alone goes through the GRU (tacotron.py:242, 266-268)
+      const RefNetDev& R = c->ref[0];
+      float* mv_e = c->adain_mv.as<float>();
+      float* mv_s = mv_e + (size_t)cfg.max_batch * cfg.reference_filters[5] * 2;
+      float* xe = conv_stack(R, ref_d[0], T_ref[0], H, Wd, C);
+      hipLaunchKernelGGL(k_adain_moments, dim3(B, C), dim3(256), 0, sr, xe, H * Wd, C, mv_e);
+      float* xs = conv_stack(R, ref_d[1], T_ref[1], H, Wd, C);
+      hipLaunchKernelGGL(k_adain_moments, dim3(B, C), dim3(256), 0, sr, xs, H * Wd, C, mv_s);
+      const long n = (long)B * H * Wd * C;
+      hipLaunchKernelGGL(k_adain_mix, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, sr, xs, n, H * Wd, C, mv_s,
+                         mv_e);
+      TT2_HIP(hipGetLastError());
+      TT2_CHECK(Wd * C == R.gin, TT2_ERR_SHAPE_MISMATCH, "reference encoder: GRU input width mismatch");
+      gru_head(R, xs, H, 0, false, c->style.as<float>(), 0);
+    } else {
+      for (int r = 0; r < c->nref; ++r) {
+        const RefNetDev& R = c->ref[r];
+        const float* x = conv_stack(R, ref_d[r], T_ref[r], H, Wd, C);
+        TT2_CHECK(Wd * C == R.gin, TT2_ERR_SHAPE_MISMATCH, "reference encoder: GRU input width mismatch");
+        if (c->emt.on()) {
+          if (r == 0) emt_encode(c->emt, x, B, H, sr);  // all_outputs=True: the attended values
+          else gru_head(R, x, H, r, false, nullptr, 0);   // refnet_spk: the LSTM-1 speaker term
+          continue;
+        }
+        const bool gst = c->style_mode == 0;
+        gru_head(R, x, H, r, gst, c->style.as<float>(), r * (gst ? cfg.style_embed_depth : 128));
+      }
     }
   }
   if (c->emt.attn == EMT_STYLE_TOKENS) emt_encode(c->emt, nullptr, B, 0, sr);
@@ -2123,7 +2223,7 @@ void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_re
   c->clip_outputs = 1; c->stop_at_any = 0; c->mask_encoder = 1; c->cumulative_weights = 1;
   c->synthesis_constraint = 0; c->constraint_monotonic = 0; c->attention_win_size = 7;
   c->max_batch = max_batch; c->max_T_in = max_T_in; c->max_T_ref = max_T_ref; c->max_iters = max_iters;
-  c->emt_attn = 0; c->emt_ref_gru = 0; c->n_emt = 4;
+  c->emt_attn = 0; c->emt_ref_gru = 0; c->n_emt = 4; c->style_mode = 0;
 }
 
 tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
@@ -2162,10 +2262,15 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
       c->nref = cfg->emt_attn == EMT_STYLE_TOKENS ? 0 : (cfg->emt_only ? 1 : 2);
       c->SW = 0;
     } else {
-      c->nref = cfg->use_gst ? (cfg->emt_only ? 1 : 2) : 0;
-      c->SW = cfg->use_gst ? c->nref * cfg->style_embed_depth : 0;
-      TT2_CHECK(cfg->use_gst, TT2_ERR_INVALID_ARG, "use_gst=False (paper Tacotron-2 memory) is not built yet");
+      // style path (tacotron.py:236-308): use_gst=False takes the reference embeddings themselves
+      c->style_mode = (!cfg->use_gst && cfg->style_mode == 0) ? 1 : cfg->style_mode;
+      TT2_CHECK(c->style_mode >= 0 && c->style_mode <= 2, TT2_ERR_INVALID_ARG, "style_mode must be 0..2");
+      c->nref = c->style_mode == 2 ? 1 : (cfg->emt_only ? 1 : 2);
+      TT2_CHECK(!(c->style_mode == 2 && cfg->emt_only), TT2_ERR_INVALID_ARG,
+                "must provide speaker reference to use AdaIn");  // tacotron.py:60-61
+      c->SW = c->style_mode == 0 ? c->nref * cfg->style_embed_depth : 128 * c->nref;
     }
+    c->nmel = c->style_mode == 2 ? 2 : c->nref;
     c->Dm = 2 * c->U + c->SW;
     TT2_CHECK(c->Dm % 64 == 0, TT2_ERR_INVALID_ARG, "memory width must be a multiple of 64");
     c->E2 = 2 * c->U;
@@ -2231,7 +2336,7 @@ tt2_status tt2_encode(tt2_ctx* c, const int32_t* ids, const int32_t* lengths, in
     TT2_CHECK(c && ids && lengths, TT2_ERR_INVALID_ARG, "tt2_encode: null argument");
     TT2_CHECK(B >= 1 && B <= c->cfg.max_batch, TT2_ERR_SHAPE_MISMATCH, "batch exceeds capacity");
     TT2_CHECK(T_in >= 1 && T_in <= c->cfg.max_T_in, TT2_ERR_SHAPE_MISMATCH, "T_in exceeds capacity");
-    TT2_CHECK(c->nref == 0 || (ref_emt && (c->nref < 2 || ref_spk)), TT2_ERR_INVALID_ARG,
+    TT2_CHECK(c->nmel == 0 || (ref_emt && (c->nmel < 2 || ref_spk)), TT2_ERR_INVALID_ARG,
               "must provide references");  // tacotron.py:66-67, tacotron_emt_attn.py:72-73
     TT2_HIP(hipSetDevice(c->dev));
     hipStream_t s = c->stream;
@@ -2240,7 +2345,7 @@ tt2_status tt2_encode(tt2_ctx* c, const int32_t* ids, const int32_t* lengths, in
     const float* refs[2] = {ref_emt, ref_spk};
     const int trs[2] = {T_ref_emt, T_ref_spk};
     const float* ref_d[2] = {nullptr, nullptr};
-    for (int r = 0; r < c->nref; ++r) {
+    for (int r = 0; r < c->nmel; ++r) {
       TT2_CHECK(trs[r] >= 1 && trs[r] <= c->cfg.max_T_ref, TT2_ERR_SHAPE_MISMATCH, "T_ref exceeds capacity");
       TT2_HIP(hipMemcpyAsync(c->refm[r].p, refs[r], sizeof(float) * B * trs[r] * c->nm, hipMemcpyHostToDevice, s));
       ref_d[r] = c->refm[r].as<float>();

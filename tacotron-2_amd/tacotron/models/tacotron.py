@@ -107,23 +107,24 @@ class Tacotron():
         self._engine = None
         return sorted(values)
 
-    def init_random_weights(self, seed=None, emt_only=False):
+    def init_random_weights(self, seed=None, emt_only=False, style="gst"):
+        """style: 'gst' | 'embed' (args.pretrained_emb_disc_all) | 'adain' (args.adain)."""
         hp = self._hparams
         self.load_weights(init_tacotron_weights(
-            hp, hp.tacotron_random_seed if seed is None else seed, emt_only))
+            hp, hp.tacotron_random_seed if seed is None else seed, emt_only, style))
 
-    def _get_engine(self, B, T_in, T_ref, max_iters, emt_only, constraint):
+    def _get_engine(self, B, T_in, T_ref, max_iters, emt_only, constraint, style="gst"):
         if self._weights is None:
             raise RuntimeError("Tacotron weights not loaded: call load_weights() (checkpoint) or "
                                "init_random_weights()")
         e = self._engine
         if (e is None or not e.fits(B, T_in, T_ref, max_iters) or e.emt_only != emt_only
-                or e.cfg.synthesis_constraint != int(constraint)):
+                or e.cfg.synthesis_constraint != int(constraint) or e.style != style):
             if e is not None:
                 e.close()
             self._engine = None
             e = TacotronEngine(self._hparams, self._weights, max(B, 1), T_in, max(T_ref, 1),
-                               max_iters, self.device, emt_only, constraint)
+                               max_iters, self.device, emt_only, constraint, style=style)
             self._engine = e
         return e
 
@@ -174,11 +175,13 @@ class Tacotron():
             raise NotImplementedError("training / eval-loss graphs of the whole model are not built "
                                       "(no encoder/GST backward); the decoder + Postnet training "
                                       "step is tt2.train.TacotronTrainer")
-        if adain or getattr(args, "pretrained_emb_disc_all", False) or use_unpaired:
-            raise NotImplementedError("adain / pretrained_emb_disc_all / unpaired style paths are "
-                                      "not built; the fork default GST path is")
-        if not hp.use_gst:
-            raise NotImplementedError("use_gst=False is not built")
+        if use_unpaired:
+            raise NotImplementedError("the unpaired decode (tacotron.py:389-461) is a training-graph "
+                                      "branch (teacher-forced on mel_targets); synthesis never builds it")
+        # style path (tacotron.py:236-308): AdaIN, the reference embeddings themselves
+        # (pretrained_emb_disc_all, or hp.use_gst=False), or GST
+        style = ("adain" if adain else
+                 "embed" if getattr(args, "pretrained_emb_disc_all", False) else "gst")
         if ref_mel_emt is None or (ref_mel_spk is None and not emt_only):
             raise ValueError("must provide references")  # refnet_emt / refnet_spk inputs (:251-259)
         constraint = bool(getattr(args, "synth_constraint", False))
@@ -207,7 +210,7 @@ class Tacotron():
             tg = None
             if gta and tower_targets[i] is not None:
                 tg = tower_targets[i].reshape(B, -1, hp.num_mels)[:, hp.outputs_per_step - 1::hp.outputs_per_step]
-            eng = self._get_engine(B, T_in, T_ref, max_iters, emt_only, constraint)
+            eng = self._get_engine(B, T_in, T_ref, max_iters, emt_only, constraint, style)
             masks = tower_masks(prenet_masks, i, row0, B)
             row0 += B
             out = eng.synthesize(ids, tower_lengths[i], ref_e, ref_s, max_iters, masks, seed, tg)

@@ -30,6 +30,9 @@ class Synthesizer:
         if model_name == 'Tacotron_emt_attn':  # its variables depend on args.attn / emt_ref_gru
             init.update(attn=getattr(args, 'attn', None), emt_ref_gru=getattr(args, 'emt_ref_gru', 'none'),
                         n_emt=n_emt)
+        else:  # style path of the Tacotron model (tacotron.py:236-308)
+            init.update(style='adain' if getattr(args, 'adain', False) else
+                        'embed' if getattr(args, 'pretrained_emb_disc_all', False) else 'gst')
         if checkpoint_path is None:
             self.model.init_random_weights(**init)
         elif str(checkpoint_path).endswith('.npz'):

@@ -42,7 +42,7 @@ class Config(ctypes.Structure):
         ("lower_bound_decay", ctypes.c_float)] + [(n, ctypes.c_int) for n in (
             "symmetric_mels", "clip_outputs", "stop_at_any", "mask_encoder", "cumulative_weights",
             "synthesis_constraint", "constraint_monotonic", "attention_win_size", "max_batch",
-            "max_T_in", "max_T_ref", "max_iters", "emt_attn", "emt_ref_gru", "n_emt")]
+            "max_T_in", "max_T_ref", "max_iters", "emt_attn", "emt_ref_gru", "n_emt", "style_mode")]
 
 
 class WnConfig(ctypes.Structure):

@@ -10,15 +10,16 @@ import numpy as np
 from . import _lib
 from ._lib import check, f32, i32, ptr
 from .hparams import get_hop_size
-from .weights import EMT_ATTN, EMT_REF_GRU, memory_width
+from .weights import EMT_ATTN, EMT_REF_GRU, STYLE_MODES, memory_width, style_mode
 
 
 def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=False,
                     synthesis_constraint=False, emt_attn=None, emt_ref_gru="none", n_emt=4,
-                    lib=None):
+                    lib=None, style="gst"):
     """tt2_config from hparams (names mirror code/hparams.py).  ``emt_attn`` selects the
     Tacotron_emt_attn model (args.attn: 'simple' / 'multihead' / 'style_tokens'; None = the
-    Tacotron model), ``emt_ref_gru`` its args.emt_ref_gru."""
+    Tacotron model), ``emt_ref_gru`` its args.emt_ref_gru; ``style`` the Tacotron model's style path
+    ('gst' | 'embed' = args.pretrained_emb_disc_all | 'adain' = args.adain, tacotron.py:236-308)."""
     lib = lib or _lib.load_library()
     cfg = _lib.Config()
     lib.tt2_default_config(ctypes.byref(cfg), max_batch, max_T_in, max_T_ref, max_iters)
@@ -64,6 +65,7 @@ def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=Fals
         raise NotImplementedError("outputs_per_step (r) must be 1 on this build (hparams.py:140)")
     if hp.smoothing:
         raise NotImplementedError("smoothing attention normalisation is not built")
+    cfg.style_mode = STYLE_MODES.index(style_mode(hp, style))
     if emt_attn is not None:
         if emt_attn not in EMT_ATTN or emt_ref_gru not in EMT_REF_GRU:
             raise ValueError("emt_attn must be one of {}, emt_ref_gru one of {}".format(
@@ -79,17 +81,18 @@ class TacotronEngine(object):
 
     def __init__(self, hp, weights, max_batch, max_T_in, max_T_ref, max_iters, device=0,
                  emt_only=False, synthesis_constraint=False, emt_attn=None, emt_ref_gru="none",
-                 n_emt=4, lib=None):
+                 n_emt=4, lib=None, style="gst"):
         # lib: libtt2.so by default; _lib.load_cpu_library() binds the same ABI on host cores
         self.lib = lib or _lib.load_library()
         self.hp = hp
         self.emt_only = emt_only
         self.emt_attn = emt_attn
         self.cfg = tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only,
-                                   synthesis_constraint, emt_attn, emt_ref_gru, n_emt, self.lib)
+                                   synthesis_constraint, emt_attn, emt_ref_gru, n_emt, self.lib, style)
         self.caps = (max_batch, max_T_in, max_T_ref, max_iters)
         # Tacotron_emt_attn attends over the encoder outputs alone (tacotron_emt_attn.py:244-246)
-        self.D = 2 * hp.encoder_lstm_units if emt_attn else memory_width(hp, emt_only)
+        self.style = style
+        self.D = 2 * hp.encoder_lstm_units if emt_attn else memory_width(hp, emt_only, style)
         h = ctypes.c_void_p()
         self._ok(self.lib.tt2_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
         self.h = h

@@ -125,24 +125,61 @@ def _postnet_specs(hp):
     return S
 
 
-def tacotron_weight_specs(hp, emt_only=False):
+#: style paths of Tacotron.initialize (tacotron.py:236-308): GST attention over style tokens, the
+#: reference embeddings themselves (args.pretrained_emb_disc_all, or hp.use_gst=False), or the AdaIN
+#: reference encoder (args.adain)
+STYLE_MODES = ("gst", "embed", "adain")
+
+
+def style_mode(hp, style="gst"):
+    """Effective style path: 'gst' needs hp.use_gst (tacotron.py:269), else the embeddings."""
+    if style not in STYLE_MODES:
+        raise ValueError("style must be one of {}".format(STYLE_MODES))
+    return "embed" if style == "gst" and not hp.use_gst else style
+
+
+def _adain_refnet_specs(hp, sc):
+    """ReferenceEncoderAdaIn (modules.py:66-107): conv2d without batch norm, strides
+    (2,2),(2,2),(1,1)x4 (tacotron.py:237), one GRU + dense(128, tanh) over the mixed speaker map."""
+    S = []
+    c_in, F = 1, hp.num_mels
+    for i, f in enumerate(hp.reference_filters):
+        s2 = sc + "conv2d_{}/".format(i)
+        S.append((s2 + "conv2d/kernel", (3, 3, c_in, f), "glorot"))
+        S.append((s2 + "conv2d/bias", (f,), "bias"))
+        c_in = f
+        if i < 2:
+            F = -(-F // 2)
+    D = hp.reference_depth
+    S += _gru_specs(sc + "rnn/gru_cell/", F * c_in, D)
+    S.append((sc + "dense/kernel", (D, 128), "glorot"))
+    S.append((sc + "dense/bias", (128,), "bias"))
+    return S
+
+
+def tacotron_weight_specs(hp, emt_only=False, style="gst"):
     """(name, shape, init) for every variable on the synthesis path (tacotron.py:215-381)."""
+    mode = style_mode(hp, style)
     S = _text_encoder_specs(hp)
-    # reference encoders (modules.py:9-64) and GST (tacotron.py:219-282)
-    tags = ["emt"] if emt_only else ["emt", "spk"]
-    for tag in tags:
-        sc = TP + "refnet_{}/".format(tag)
-        conv, gin = _refnet_convs(hp, sc)
-        S += conv
-        D = hp.reference_depth
-        S += _gru_specs(sc + "rnn/gru_cell/", gin, D)
-        S.append((sc + "dense/kernel", (D, 128), "glorot"))
-        S.append((sc + "dense/bias", (128,), "bias"))
-        tok_d = hp.style_embed_depth // hp.num_heads
-        S.append((TP + "style_tokens_{}".format(tag), (hp.num_gst, tok_d), "gst_tokens"))
-        S += _mha_specs(TP + "Multihead-attention-{}/".format(tag), 128, tok_d, hp.style_att_dim,
-                        hp.num_heads)
-    S += _decoder_specs(hp, memory_width(hp, emt_only))
+    if mode == "adain":   # one shared encoder 'refnet' over both references (tacotron.py:236-242)
+        S += _adain_refnet_specs(hp, TP + "refnet/")
+    else:
+        # reference encoders (modules.py:9-64) and GST (tacotron.py:219-282)
+        tags = ["emt"] if emt_only else ["emt", "spk"]
+        for tag in tags:
+            sc = TP + "refnet_{}/".format(tag)
+            conv, gin = _refnet_convs(hp, sc)
+            S += conv
+            D = hp.reference_depth
+            S += _gru_specs(sc + "rnn/gru_cell/", gin, D)
+            S.append((sc + "dense/kernel", (D, 128), "glorot"))
+            S.append((sc + "dense/bias", (128,), "bias"))
+            if mode == "gst":
+                tok_d = hp.style_embed_depth // hp.num_heads
+                S.append((TP + "style_tokens_{}".format(tag), (hp.num_gst, tok_d), "gst_tokens"))
+                S += _mha_specs(TP + "Multihead-attention-{}/".format(tag), 128, tok_d,
+                                hp.style_att_dim, hp.num_heads)
+    S += _decoder_specs(hp, memory_width(hp, emt_only, style))
     return S + _postnet_specs(hp)
 
 
@@ -225,10 +262,15 @@ def tacotron_emt_weight_specs(hp, attn, emt_ref_gru="none", emt_only=False, n_em
     return S + _postnet_specs(hp)
 
 
-def memory_width(hp, emt_only=False):
-    """D_mem = 2·encoder_lstm_units + style width (tacotron.py:297-308)."""
-    style = hp.style_embed_depth if hp.use_gst else 128
-    return 2 * hp.encoder_lstm_units + (style if emt_only else 2 * style)
+def memory_width(hp, emt_only=False, style="gst"):
+    """D_mem = 2·encoder_lstm_units + style width (tacotron.py:297-308): per
+    reference a GST embedding (style_embed_depth) or the 128-wide reference embedding; AdaIN
+    passes one 128-wide embedding (:266-268)."""
+    mode = style_mode(hp, style)
+    if mode == "adain":
+        return 2 * hp.encoder_lstm_units + 128
+    w = hp.style_embed_depth if mode == "gst" else 128
+    return 2 * hp.encoder_lstm_units + (w if emt_only else 2 * w)
 
 
 def wavenet_weight_specs(hp):
@@ -331,8 +373,8 @@ def init_weights(specs, hp, seed=5339):
             for name, shape, kind in specs}
 
 
-def init_tacotron_weights(hp, seed=5339, emt_only=False):
-    return init_weights(tacotron_weight_specs(hp, emt_only), hp, seed)
+def init_tacotron_weights(hp, seed=5339, emt_only=False, style="gst"):
+    return init_weights(tacotron_weight_specs(hp, emt_only, style), hp, seed)
 
 
 def init_tacotron_emt_weights(hp, attn, emt_ref_gru="none", emt_only=False, n_emt=4, seed=5339):

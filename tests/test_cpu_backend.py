@@ -215,3 +215,40 @@ def test_golden_mol_sampler(cpu):
                                   float(g["log_scale_min"]), _lib.ptr(x), _lib.ptr(k)), cpu)
     np.testing.assert_array_equal(k, g["k"])                   # the mixture choice: exact
     np.testing.assert_allclose(x, g["x"], rtol=0, atol=1e-6)   # expf / fused multiply-add rounding
+
+
+@pytest.mark.parametrize("style", ["embed", "adain"])
+def test_style_paths(cpu, style):
+    """The non-GST style paths (tacotron.py:236-308) at both widths, emotion and speaker
+    references of different lengths: 'embed' (args.pretrained_emb_disc_all / use_gst=False) and
+    'adain' (ReferenceEncoderAdaIn, modules.py:66-107)."""
+    from tt2.engine import TacotronEngine
+    for hp in (small_hparams(), full_hparams()):
+        W = init_tacotron_weights(hp, seed=5339, style=style)
+        B, T, n = 3, 11, 8
+        ids, lens, re, rs = tacotron_inputs(B, T, 100, seed=12)
+        rs = np.ascontiguousarray(rs[:, :72])
+        masks = prenet_masks(n, B, hp.prenet_layers[0], seed=12)
+        eng = TacotronEngine(hp, W, B, T, 100, n, lib=cpu, style=style)
+        out = eng.synthesize(ids, lens, re, rs, n, masks)
+        eng.close()
+        ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp, style=style), masks, n)
+        np.testing.assert_allclose(out["style"], ref["style"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], rtol=0, atol=1e-4)
+
+
+def test_use_gst_false_is_embed(cpu):
+    """hp.use_gst=False selects the reference embeddings (tacotron.py:269, 284-291)."""
+    from tt2.engine import TacotronEngine
+    hp = small_hparams()
+    W = init_tacotron_weights(hp, seed=5339, style="embed")
+    hp.use_gst = False
+    B, T, n = 2, 7, 5
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=13)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=13)
+    eng = TacotronEngine(hp, W, B, T, 64, n, lib=cpu)
+    assert eng.D == 2 * hp.encoder_lstm_units + 256
+    out = eng.synthesize(ids, lens, re, rs, n, masks)
+    eng.close()
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, n)
+    np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], rtol=0, atol=1e-4)
