@@ -96,6 +96,18 @@ typedef struct tt2_config {
    * 1 the 128-wide reference embeddings themselves (args.pretrained_emb_disc_all; use_gst=0 implies
    * it), 2 ReferenceEncoderAdaIn (args.adain: one shared 'refnet', both mels, D_mem = 2U + 128) */
   int style_mode;
+  /* predict_linear post-processing net (CBHG, modules.py:125-184 + FrameProjection(num_freq); the
+   * reference's caller is commented out at tacotron.py:466-478): weights loaded when set */
+  int predict_linear;
+  int num_freq;                 /* 1025 */
+  int cbhg_kernels;             /* 8: conv bank kernel sizes 1..K */
+  int cbhg_conv_channels;       /* 128 */
+  int cbhg_pool_size;           /* 2 */
+  int cbhg_projection;          /* 256 (the second projection is num_mels) */
+  int cbhg_projection_kernel_size; /* 3 */
+  int cbhg_highwaynet_layers;   /* 4 */
+  int cbhg_highway_units;       /* 128 */
+  int cbhg_rnn_units;           /* 128 per direction */
 } tt2_config;
 
 typedef struct tt2_ctx tt2_ctx;
@@ -163,6 +175,12 @@ typedef struct tt2_decoder_state {
 tt2_status tt2_decoder_step(tt2_ctx* ctx, const float* frame_in, const uint8_t* prenet_masks,
                             const tt2_decoder_state* state_in, tt2_decoder_state* state_out,
                             float* frame_out, float* stop_out, float* alignments_out);
+
+/* linear_outputs = clip(FrameProjection(num_freq)(CBHG(mel_outputs, None))) (tacotron.py:466-481,
+ * commented out in the reference; needs predict_linear): mels [B,T,num_mels] -> linear_out
+ * [B,T,num_freq] (host), or device pointers on `stream`. */
+tt2_status tt2_linear_outputs(tt2_ctx* ctx, const float* mels, int B, int T, float* linear_out);
+tt2_status tt2_linear_outputs_dev(tt2_ctx* ctx, const float* mels_d, int B, int T, float* linear_d, void* stream);
 
 /* Tacotron_emt_attn: emotion labels [B] int32 of the next tt2_encode (the emt_labels placeholder,
  * synthesizer.py:35, one-hot in the style_tokens query, Architecture_wrappers.py:236; an

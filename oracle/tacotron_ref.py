@@ -440,3 +440,74 @@ def get_output_lengths(stop_tokens):
     """tacotron/synthesizer.py:384-387: per row, the index of the first 1 in np.round(stop)
     (round half to even), else the row length."""
     return [row.index(1) if 1 in row else len(row) for row in np.round(stop_tokens).tolist()]
+
+
+# ---------------------------------------------------------------------------------------------
+# CBHG post-processing network (modules.py:110-184; its one caller is commented out at
+# tacotron.py:466-478: linear_outputs = clip(FrameProjection(num_freq)(CBHG(mel_outputs)))
+# ---------------------------------------------------------------------------------------------
+
+def max_pool1d_same(x, pool):
+    """tf.layers.max_pooling1d(strides=1, padding='same'): window [t − (pool−1)//2, +pool),
+    padded positions ignored."""
+    B, T, C = x.shape
+    pl = (pool - 1) // 2
+    out = np.full_like(x, -np.inf)
+    for d in range(pool):
+        src = np.arange(T) + d - pl
+        ok = (src >= 0) & (src < T)
+        out[:, ok] = np.maximum(out[:, ok], x[:, src[ok]])
+    return out
+
+
+def highway(x, W, scope, dt):
+    """HighwayNet (modules.py:110-122): H = relu(x·W_H + b_H), T = σ(x·W_T + b_T),
+    y = H·T + x·(1 − T)."""
+    Hh = np.maximum(dense(x, _w(W, scope + "H/kernel", dt), _w(W, scope + "H/bias", dt)), dt(0))
+    Tg = sigmoid(dense(x, _w(W, scope + "T/kernel", dt), _w(W, scope + "T/bias", dt)))
+    return Hh * Tg + x * (dt(1) - Tg)
+
+
+def _gru_seq(x, W, scope, dt, reverse=False):
+    kg, bg = _w(W, scope + "gates/kernel", dt), _w(W, scope + "gates/bias", dt)
+    kc, bc = _w(W, scope + "candidate/kernel", dt), _w(W, scope + "candidate/bias", dt)
+    N, T, _ = x.shape
+    h = np.zeros((N, bc.shape[0]), dt)
+    out = np.zeros((N, T, bc.shape[0]), dt)
+    for t in (range(T - 1, -1, -1) if reverse else range(T)):
+        h = gru_cell(x[:, t], h, kg, bg, kc, bc)
+        out[:, t] = h
+    return out
+
+
+def cbhg(x, W, hp, dt=np.float32, name="CBHG_postnet"):
+    """CBHG.__call__(inputs, None) (modules.py:143-184): conv bank of kernel sizes 1..K (conv1d()
+    with ReLU, bnorm 'after'), max-pool 'same' stride 1, two projection convs (ReLU, linear), the
+    residual with the input, dense to the highway width when they differ, the highway stack, a
+    bidirectional GRU over every frame (input_lengths None); [B, T, 2·rnn_units]."""
+    sc = name + "/"
+    x = np.asarray(x, dt)
+    relu = lambda v: np.maximum(v, dt(0))   # noqa: E731
+    bank = np.concatenate([conv1d_block(x, W, sc + "conv_bank/conv1d_{}/".format(k), relu, dt)
+                           for k in range(1, hp["cbhg_kernels"] + 1)], axis=-1)
+    mp = max_pool1d_same(bank, hp["cbhg_pool_size"])
+    p1 = conv1d_block(mp, W, sc + "proj1/", relu, dt)
+    p2 = conv1d_block(p1, W, sc + "proj2/", lambda v: v, dt)
+    h = p2 + x
+    if h.shape[-1] != hp["cbhg_highway_units"]:
+        h = dense(h, _w(W, sc + "dense/kernel", dt), _w(W, sc + "dense/bias", dt))
+    for i in range(hp["cbhg_highwaynet_layers"]):
+        h = highway(h, W, sc + "{}_highwaynet_{}/".format(name, i + 1), dt)
+    fw = _gru_seq(h, W, sc + "bidirectional_rnn/fw/{}_forward_RNN/".format(name), dt)
+    bw = _gru_seq(h, W, sc + "bidirectional_rnn/bw/{}_backward_RNN/".format(name), dt, reverse=True)
+    return np.concatenate([fw, bw], axis=-1)
+
+
+def linear_outputs(mel, W, hp, dt=np.float32):
+    """The post-processing net of tacotron.py:466-478: CBHG → FrameProjection(num_freq) → clip."""
+    ps = "cbhg_linear_specs_projection/projection_cbhg_linear_specs_projection/"
+    y = dense(cbhg(mel, W, hp, dt), _w(W, ps + "kernel", dt), _w(W, ps + "bias", dt))
+    if hp.get("clip_outputs", True):
+        y = np.minimum(np.maximum(y, dt(-hp["max_abs_value"] - hp["lower_bound_decay"])),
+                       dt(hp["max_abs_value"]))
+    return y

@@ -4,7 +4,7 @@ SRC=$1; OUT=$2
 D=$(mktemp -d)
 cp -r tacotron-2_amd/csrc $D/csrc && cp $SRC $D/csrc/decode_persist.hip && mkdir -p $D/include && cp include/tt2.h $D/include/
 sed -i 's#../../include/tt2.h#../include/tt2.h#' $D/csrc/common.h
-for f in gemm tacotron decode_persist wavenet griffinlim train step wavenet_wide train_front emt; do
+for f in gemm tacotron decode_persist wavenet griffinlim train step wavenet_wide train_front emt cbhg; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-variable -Wno-pass-failed -c $D/csrc/$f.hip -o $D/$f.o &
 done
 wait

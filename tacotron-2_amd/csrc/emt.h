@@ -52,4 +52,11 @@ void emt_init_launch(const EmtModel& m, const float* spk, float* X1a, float* X1b
 void emt_step_launch(const EmtModel& m, const int* done, const float* Xp, float* X1, int col0, const float* spk, int t,
                      hipStream_t s);
 
+// TF1 GRUCell over every frame of B rows by NG independent GRUs (k_emt_gru), xg [B][T][NG][3D] the
+// x products + biases: mode 0 all outputs with GRU 1 walking backwards (a full-length BiGRU,
+// out [B][T][NG·D]); mode 1 last output -> dense(128, tanh) (out [B][NG][128]).  Also the CBHG's
+// bidirectional GRU (cbhg.hip).
+void gru_sequence(const float* xg, int B, int T, int D, int NG, const float* whg, const float* whc, int mode,
+                  const float* kd, const float* bd, float* out, hipStream_t s);
+
 }  // namespace tt2

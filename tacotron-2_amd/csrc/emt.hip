@@ -64,6 +64,14 @@ __global__ __launch_bounds__(256) void k_emt_gru(const float* __restrict__ xg, i
   }
 }
 
+void gru_sequence(const float* xg, int B, int T, int D, int NG, const float* whg, const float* whc, int mode,
+                  const float* kd, const float* bd, float* out, hipStream_t s) {
+  TT2_CHECK(D >= 1 && D <= 256, TT2_ERR_INVALID_ARG, "gru_sequence: GRU units must be <= 256");
+  hipLaunchKernelGGL(k_emt_gru, dim3(B, NG), dim3(256), sizeof(float) * 4 * D, s, xg, T, D, NG, whg, whc, mode, kd, bd,
+                     out);
+  TT2_HIP(hipGetLastError());
+}
+
 // style_tokens values: tanh(tokens) (tacotron_emt_attn.py:214; the batch tile is a broadcast)
 __global__ void k_emt_tanh(const float* __restrict__ x, int n, float* __restrict__ y) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -374,11 +382,8 @@ void emt_encode(EmtModel& m, const float* x, int B, int T2, hipStream_t s) {
       g.M = B * T2; g.N = m.NG * 3 * m.D; g.K = m.gin; g.A = x; g.lda = m.gin;
       g.Bw = m.gwx.as<float>(); g.ldb = g.N; g.Cout = m.xg.as<float>(); g.ldc = g.N; g.bias = m.gbx.as<float>();
       gemm(g, s);
-      const size_t shm = sizeof(float) * 4 * m.D;
-      hipLaunchKernelGGL(k_emt_gru, dim3(B, m.NG), dim3(256), shm, s, m.xg.as<float>(), T2, m.D, m.NG,
-                         m.gwhg.as<float>(), m.gwhc.as<float>(), m.ref_gru == EMT_GRU_MULTI ? 1 : 0,
-                         m.gkd.as<float>(), m.gbd.as<float>(), m.val.as<float>());
-      TT2_HIP(hipGetLastError());
+      gru_sequence(m.xg.as<float>(), B, T2, m.D, m.NG, m.gwhg.as<float>(), m.gwhc.as<float>(),
+                   m.ref_gru == EMT_GRU_MULTI ? 1 : 0, m.gkd.as<float>(), m.gbd.as<float>(), m.val.as<float>(), s);
     }
     vals = m.val.as<float>();
     rows = B * m.Tv;

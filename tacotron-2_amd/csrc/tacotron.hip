@@ -15,6 +15,7 @@
 #include "common.h"
 #include "decode_persist.h"
 #include "gemm.h"
+#include "cbhg.h"
 #include "emt.h"
 #include "step.h"
 
@@ -1239,6 +1240,7 @@ struct tt2_ctx {
   tt2::DevBuf q_wt, pre_w2t, keysT, valuesT, pd_ctl, H1x, H2x, Ex, CTXx, SSx, PPx, PREx;
   // Tacotron_emt_attn variant (emt.h): off for the Tacotron model
   tt2::EmtModel emt;
+  tt2::CbhgModel cbhg;  // predict_linear post-processing net (cbhg.h)
   std::vector<int> emt_labels;  // tt2_set_emt_labels (style_tokens)
   hipEvent_t pd_ev[2] = {nullptr, nullptr};
   float pd_kernel_ms = 0.f;
@@ -1394,6 +1396,14 @@ static void finalize(tt2_ctx* c) {
     upload(R.ab, need(wm, mh + "attention_b", {Aa / cfg.num_heads}));
   }
   emt_load(c->emt, wm, P);
+  if (cfg.predict_linear) {
+    cbhg_load(c->cbhg, wm, P, c->nm, cfg.cbhg_kernels, cfg.cbhg_conv_channels, cfg.cbhg_pool_size, cfg.cbhg_projection,
+              cfg.cbhg_projection_kernel_size, cfg.cbhg_highwaynet_layers, cfg.cbhg_highway_units, cfg.cbhg_rnn_units,
+              cfg.num_freq);
+    c->cbhg.clip = cfg.clip_outputs;
+    c->cbhg.clip_lo = cfg.symmetric_mels ? -cfg.max_abs_value - cfg.lower_bound_decay : -cfg.lower_bound_decay;
+    c->cbhg.clip_hi = cfg.max_abs_value;
+  }
   upload(c->mem_k, need(wm, P + "memory_layer/kernel", {c->Dm, c->A}));
   split_weights(c->mem_k.as<float>(), c->Dm, c->A, c->A, c->mem_k_s, nullptr);
   c->kpart.alloc(sizeof(float) * (8u << 20));
@@ -2224,6 +2234,9 @@ void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_re
   c->synthesis_constraint = 0; c->constraint_monotonic = 0; c->attention_win_size = 7;
   c->max_batch = max_batch; c->max_T_in = max_T_in; c->max_T_ref = max_T_ref; c->max_iters = max_iters;
   c->emt_attn = 0; c->emt_ref_gru = 0; c->n_emt = 4; c->style_mode = 0;
+  c->predict_linear = 0; c->num_freq = 1025; c->cbhg_kernels = 8; c->cbhg_conv_channels = 128;
+  c->cbhg_pool_size = 2; c->cbhg_projection = 256; c->cbhg_projection_kernel_size = 3;
+  c->cbhg_highwaynet_layers = 4; c->cbhg_highway_units = 128; c->cbhg_rnn_units = 128;
 }
 
 tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
@@ -2633,6 +2646,35 @@ tt2_status tt2_decoder_path(tt2_ctx* c, int* persistent, float* kernel_ms) {
     TT2_CHECK(c && persistent && kernel_ms, TT2_ERR_INVALID_ARG, "null argument");
     *persistent = c->last_pd ? 1 : (pd_fits(c) ? 1 : 0);
     *kernel_ms = c->last_pd ? c->pd_kernel_ms : 0.f;
+  });
+}
+
+tt2_status tt2_linear_outputs_dev(tt2_ctx* c, const float* mels_d, int B, int T, float* linear_d, void* stream) {
+  return guard([&] {
+    TT2_CHECK(c && mels_d && linear_d, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_finalize_weights not called");
+    TT2_CHECK(B >= 1 && T >= 1, TT2_ERR_INVALID_ARG, "B and T must be >= 1");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    cbhg_linear(c->cbhg, mels_d, B, T, linear_d, c->kpart.as<float>(), (long)(c->kpart.bytes / sizeof(float)), s);
+  });
+}
+
+tt2_status tt2_linear_outputs(tt2_ctx* c, const float* mels, int B, int T, float* linear_out) {
+  return guard([&] {
+    TT2_CHECK(c && mels && linear_out, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_finalize_weights not called");
+    TT2_CHECK(B >= 1 && T >= 1, TT2_ERR_INVALID_ARG, "B and T must be >= 1");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = c->stream;
+    DevBuf in, out;
+    in.alloc(sizeof(float) * (size_t)B * T * c->nm);
+    out.alloc(sizeof(float) * (size_t)B * T * c->cfg.num_freq);
+    TT2_HIP(hipMemcpyAsync(in.p, mels, in.bytes, hipMemcpyHostToDevice, s));
+    cbhg_linear(c->cbhg, in.as<float>(), B, T, out.as<float>(), c->kpart.as<float>(),
+                (long)(c->kpart.bytes / sizeof(float)), s);
+    TT2_HIP(hipMemcpyAsync(linear_out, out.p, out.bytes, hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipStreamSynchronize(s));
   });
 }
 

@@ -194,6 +194,7 @@ class Tacotron():
         self.tower_mel_outputs = []
         self.tower_encoder_outputs = []
         self.tower_style_embeddings = []
+        self.tower_linear_outputs = []
         self.tower_inputs = tower_inputs
         self.tower_input_lengths = tower_lengths
         self.tower_mel_targets = [t for t in tower_targets if t is not None]
@@ -220,4 +221,6 @@ class Tacotron():
             self.tower_mel_outputs.append(out["mel_outputs"])
             self.tower_encoder_outputs.append(out["encoder_outputs"])
             self.tower_style_embeddings.append(out["style"][:, None, :])
+            if hp.predict_linear and not gta:  # post_condition (tacotron.py:214, 466-481)
+                self.tower_linear_outputs.append(eng.linear_outputs(out["mel_outputs"]))
         self.all_vars = list(self._weights.keys())

@@ -42,7 +42,10 @@ class Config(ctypes.Structure):
         ("lower_bound_decay", ctypes.c_float)] + [(n, ctypes.c_int) for n in (
             "symmetric_mels", "clip_outputs", "stop_at_any", "mask_encoder", "cumulative_weights",
             "synthesis_constraint", "constraint_monotonic", "attention_win_size", "max_batch",
-            "max_T_in", "max_T_ref", "max_iters", "emt_attn", "emt_ref_gru", "n_emt", "style_mode")]
+            "max_T_in", "max_T_ref", "max_iters", "emt_attn", "emt_ref_gru", "n_emt", "style_mode",
+            "predict_linear", "num_freq", "cbhg_kernels", "cbhg_conv_channels", "cbhg_pool_size",
+            "cbhg_projection", "cbhg_projection_kernel_size", "cbhg_highwaynet_layers",
+            "cbhg_highway_units", "cbhg_rnn_units")]
 
 
 class WnConfig(ctypes.Structure):
@@ -117,6 +120,8 @@ SIGNATURES = {
     "tt2_decoder_path": (_I, [_P, _P, _P]),
     "tt2_debug_pd_stamps": (_I, [_P, _P]),
     "tt2_set_emt_labels": (_I, [_P, _P, _I]),
+    "tt2_linear_outputs": (_I, [_P, _P, _I, _I, _P]),
+    "tt2_linear_outputs_dev": (_I, [_P, _P, _I, _I, _P, _P]),
     "tt2_emt_alignments": (_I, [_P, _P, _P, _P]),
     "tt2_wn_last_timings": (_I, [_P, _P]),
     "tt2_wn_debug_stamps": (_I, [_P, _P]),

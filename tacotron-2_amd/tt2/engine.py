@@ -66,6 +66,12 @@ def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=Fals
     if hp.smoothing:
         raise NotImplementedError("smoothing attention normalisation is not built")
     cfg.style_mode = STYLE_MODES.index(style_mode(hp, style))
+    cfg.predict_linear = 1 if hp.predict_linear else 0    # CBHG post-net (tacotron.py:466-481)
+    cfg.num_freq = hp.num_freq
+    for k in ("cbhg_kernels", "cbhg_conv_channels", "cbhg_pool_size", "cbhg_projection",
+              "cbhg_projection_kernel_size", "cbhg_highwaynet_layers", "cbhg_highway_units",
+              "cbhg_rnn_units"):
+        setattr(cfg, k, getattr(hp, k))
     if emt_attn is not None:
         if emt_attn not in EMT_ATTN or emt_ref_gru not in EMT_REF_GRU:
             raise ValueError("emt_attn must be one of {}, emt_ref_gru one of {}".format(
@@ -189,6 +195,15 @@ class TacotronEngine(object):
                                         ctypes.byref(sout), ptr(frame), ptr(stop), ptr(align)))
         nxt["time"] = sout.time
         return frame, stop, align, nxt
+
+    def linear_outputs(self, mels):
+        """tt2_linear_outputs: clip(FrameProjection(num_freq)(CBHG(mels))) for mels [B,T,num_mels]
+        (hp.predict_linear; tacotron.py:466-481)."""
+        m = f32(mels)
+        B, T, _ = m.shape
+        out = np.zeros((B, T, self.hp.num_freq), np.float32)
+        self._ok(self.lib.tt2_linear_outputs(self.h, ptr(m), B, T, ptr(out)))
+        return out
 
     def set_emt_labels(self, labels):
         """Tacotron_emt_attn: emotion labels [B] (the emt_labels placeholder, synthesizer.py:35) used

@@ -111,6 +111,9 @@ _FORK = dict(
     prenet_layers=[256, 256], decoder_layers=2, decoder_lstm_units=1024, max_iters=1000,
     postnet_num_layers=5, postnet_kernel_size=(5,), postnet_channels=512,
     mask_encoder=True, mask_decoder=False, predict_linear=False,
+    cbhg_kernels=8, cbhg_conv_channels=128, cbhg_pool_size=2, cbhg_projection=256,
+    cbhg_projection_kernel_size=3, cbhg_highwaynet_layers=4, cbhg_highway_units=128,
+    cbhg_rnn_units=128,
     tacotron_zoneout_rate=0.1, tacotron_dropout_rate=0.5,
     tacotron_random_seed=5339, tacotron_data_random_state=1234,
     tacotron_synthesis_batch_size=1, tacotron_spk_emb_dim=1024, tacotron_se_concat=True,

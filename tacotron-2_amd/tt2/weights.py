@@ -157,6 +157,40 @@ def _adain_refnet_specs(hp, sc):
     return S
 
 
+def cbhg_weight_specs(hp, name="CBHG_postnet"):
+    """The post-processing CBHG + linear projection (modules.py:125-184, tacotron.py:466-478:
+    commented out in the reference, built by predict_linear here).  Conv bank / projections via
+    conv1d() (conv1d + batch_normalization scopes), the residual dense when num_mels !=
+    highway_units, HighwayNet H / T layers (T bias init -1), named GRU cells under
+    bidirectional_rnn/{fw,bw} (TF-internal naming unverified, like the other cells)."""
+    S = []
+    sc = TP + name + "/"
+    nm, C = hp.num_mels, hp.cbhg_conv_channels
+    for k in range(1, hp.cbhg_kernels + 1):
+        s2 = sc + "conv_bank/conv1d_{}/".format(k)
+        S += [(s2 + "conv1d/kernel", (k, nm, C), "glorot"), (s2 + "conv1d/bias", (C,), "bias")]
+        S += _bn(s2, C)
+    kp = hp.cbhg_projection_kernel_size
+    for nm_, cin, cout in (("proj1", hp.cbhg_kernels * C, hp.cbhg_projection),
+                           ("proj2", hp.cbhg_projection, nm)):
+        s2 = sc + nm_ + "/"
+        S += [(s2 + "conv1d/kernel", (kp, cin, cout), "glorot"), (s2 + "conv1d/bias", (cout,), "bias")]
+        S += _bn(s2, cout)
+    Hu = hp.cbhg_highway_units
+    if nm != Hu:
+        S += [(sc + "dense/kernel", (nm, Hu), "glorot"), (sc + "dense/bias", (Hu,), "bias")]
+    for i in range(1, hp.cbhg_highwaynet_layers + 1):
+        s2 = sc + "{}_highwaynet_{}/".format(name, i)
+        S += [(s2 + "H/kernel", (Hu, Hu), "glorot"), (s2 + "H/bias", (Hu,), "bias"),
+              (s2 + "T/kernel", (Hu, Hu), "glorot"), (s2 + "T/bias", (Hu,), "highway_t_bias")]
+    R = hp.cbhg_rnn_units
+    for d, cell in (("fw", "forward"), ("bw", "backward")):
+        S += _gru_specs(sc + "bidirectional_rnn/{}/{}_{}_RNN/".format(d, name, cell), Hu, R)
+    ps = TP + "cbhg_linear_specs_projection/projection_cbhg_linear_specs_projection/"
+    S += [(ps + "kernel", (2 * R, hp.num_freq), "glorot"), (ps + "bias", (hp.num_freq,), "bias")]
+    return S
+
+
 def tacotron_weight_specs(hp, emt_only=False, style="gst"):
     """(name, shape, init) for every variable on the synthesis path (tacotron.py:215-381)."""
     mode = style_mode(hp, style)
@@ -180,7 +214,8 @@ def tacotron_weight_specs(hp, emt_only=False, style="gst"):
                 S += _mha_specs(TP + "Multihead-attention-{}/".format(tag), 128, tok_d,
                                 hp.style_att_dim, hp.num_heads)
     S += _decoder_specs(hp, memory_width(hp, emt_only, style))
-    return S + _postnet_specs(hp)
+    S += _postnet_specs(hp)
+    return S + (cbhg_weight_specs(hp) if hp.predict_linear else [])
 
 
 #: args.attn / args.emt_ref_gru values of Tacotron_emt_attn (train.py:147-150); codes 1.. / 0..
@@ -329,6 +364,8 @@ def _init(rng, shape, kind, hp):
         # negative so that an untrained (random) model decodes to max_iters instead of stopping on
         # a coin flip; tests that exercise the stop rule override this bias explicitly
         return rng.uniform(-3.5, -2.5, shape).astype(np.float32)
+    if kind == "highway_t_bias":  # HighwayNet T layer: bias_initializer=constant(-1) (modules.py:116)
+        return (-1.0 + rng.uniform(-0.1, 0.1, shape)).astype(np.float32)
     if kind == "gru_gate_bias":
         return (1.0 + rng.uniform(-0.1, 0.1, shape)).astype(np.float32)  # TF GRUCell bias init 1.0
     if kind == "bn_gamma":
