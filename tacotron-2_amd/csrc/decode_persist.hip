@@ -357,17 +357,18 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     __syncthreads();
     {
-      const int k16 = tid >> 5;
+      const int k16 = tid >> 5;  // wave w: k16 = 2w (lanes 0..31), 2w + 1 (lanes 32..63)
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) s += x1[16 * k16 + i] * o.w2p[i >> 2][i & 3];
-      red[k16 * 32 + (tid & 31)] = s;
+      s += __shfl_xor(s, 32);
+      if ((tid & 63) < 32) red[(tid >> 6) * 32 + (tid & 31)] = s;
     }
     __syncthreads();
     if (tid < 32) {
       float v = 0.f;
 #pragma unroll
-      for (int k16 = 0; k16 < 16; ++k16) v += red[k16 * 32 + tid];
+      for (int ww = 0; ww < 8; ++ww) v += red[ww * 32 + tid];
       const int n = 32 * j + tid;
       const float out = rowv ? (fmaxf(v + b2p, 0.f) / 0.5f) * red[3072 + tid] : 0.f;
       pd_put(a.PREg + par * 32 * PD_P + af_idx(b, n), tag, out);
@@ -530,7 +531,6 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) kg_mfma(x0[i], x1v[i], w2i[4 * h + i], s0, s1);
-        __builtin_amdgcn_sched_barrier(0);
       }
       PD_STAMP(16);
       put_partials(s0, s1, red, w, lane);
@@ -575,24 +575,24 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 
     if (rowv) {
       const float* X = a.H2x + p * 32 * PD_H;
+      // wave w reads exactly the h2 units [128w, 128w+128) its own lanes multiply: wave-local
+      // exchange (LDS ops of one wave complete in order), one block barrier for the 8 wave partials
       red[128 * w + lane] = pd_ld(X + af_idx(b, 128 * w + lane));
       red[128 * w + 64 + lane] = pd_ld(X + af_idx(b, 128 * w + 64 + lane));
-      __syncthreads();
+      __builtin_amdgcn_wave_barrier();
       {
-        const int k = tid & 15, seg = tid >> 4;
+        const int seg = tid >> 4;
         float s = 0.f;
 #pragma unroll
         for (int ii = 0; ii < 32; ++ii) s += red[seg * 32 + ii] * wq[ii >> 2][ii & 3];
-        red[1024 + seg * 16 + k] = s;
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if (lane < 16) red[1024 + w * 16 + lane] = s;
       }
       __syncthreads();
-      if (tid < 16) {
-        float q = 0.f;
-        for (int s2 = 0; s2 < 32; ++s2) q += red[1024 + s2 * 16 + tid];
-        qv[tid] = q;
-      }
-      __syncthreads();
-      const float qk = qv[lane & 15];
+      float qk = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) qk += red[1024 + ww * 16 + (lane & 15)];
       unsigned long long* E = a.Eg + (((long)p * 32 + b) * 8 + j) * PD_TMAX;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -619,10 +619,12 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       const unsigned long long* E = a.Eg + ((long)p * 32 + b) * 8 * PD_TMAX;
       if (tid == 0) si[5] = 1;
       __syncthreads();
+      // waves 0..3 hold one energy per lane; max and sum as wave shuffles + one LDS exchange of the
+      // four wave results each
+      float e = -INFINITY;
       if (tid < PD_TMAX) {
         float ev[8];
         if (!pd_take<8>(a, PD_F_E, E, tid, PD_TMAX, tg, tid < T, ev)) si[5] = 0;
-        float e = -INFINITY;
         if (tid < T) {
           e = 0.f;
 #pragma unroll
@@ -636,25 +638,23 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           }
           if (a.mask_encoder && tid >= len) e = -INFINITY;
         }
-        red[tid] = e;
+        float mx = e;
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        if (lane == 0) red[w] = mx;
       }
       __syncthreads();
       if (!si[5]) return;
-      if (w == 0) {
-        float mx = -INFINITY;
-        for (int i = lane; i < T; i += 64) mx = fmaxf(mx, red[i]);
-        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-        float sum = 0.f;
-        for (int i = lane; i < T; i += 64) sum += expf(red[i] - mx);
+      float ex = 0.f;
+      if (tid < PD_TMAX) {
+        const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        ex = tid < T ? expf(e - mx) : 0.f;
+        float sum = ex;
         for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-        if (lane == 0) {
-          sc[0] = mx;
-          sc[1] = sum;
-        }
+        if (lane == 0) red[8 + w] = sum;
       }
       __syncthreads();
       PD_STAMP(21);
-      if (tid < PD_TMAX) al[tid] = tid < T ? expf(red[tid] - sc[0]) / sc[1] : 0.f;
+      if (tid < PD_TMAX) al[tid] = tid < T ? ex / ((red[8] + red[9]) + (red[10] + red[11])) : 0.f;
       __syncthreads();
       if (tid < T) {
         const float cp = cw[15 + tid];
