@@ -531,6 +531,26 @@ struct DecArgs {
   float* align;   // [B][T_in][max_iters] or null
 };
 
+// Zero-fill of up to ZL_MAX device buffers in ONE launch (decoder / encoder state resets: one
+// launch instead of a hipMemsetAsync per buffer, ~5 us each).  Buffers are DevBuf allocations
+// (256-byte aligned); 16-byte stores, byte tail by the first threads.
+constexpr int ZL_MAX = 24;
+struct ZeroList {
+  void* p[ZL_MAX];
+  unsigned long long n[ZL_MAX];
+  int count;
+};
+__global__ void k_zero_many(ZeroList z) {
+  const unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x,
+                           stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (int i = 0; i < z.count; ++i) {
+    uint4* q = reinterpret_cast<uint4*>(z.p[i]);
+    const unsigned long long n16 = z.n[i] / 16;
+    for (unsigned long long k = t; k < n16; k += stride) q[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (t < z.n[i] % 16) reinterpret_cast<unsigned char*>(z.p[i])[n16 * 16 + t] = 0;
+  }
+}
+
 // Keep bits of the always-on prenet dropout when the caller injects none: counter-based hash of
 // (seed, flat index) -> Bernoulli(0.5) (common.h prenet_keep_bit), generated for the whole decode
 // in one launch (also the read-back tt2_prenet_keep_bits).
@@ -1160,6 +1180,21 @@ __global__ void k_clip_frames(const float* __restrict__ src, long src_bstride, f
 // ==========================================================================================
 // Host side
 // ==========================================================================================
+static void zero_many(std::initializer_list<std::pair<void*, size_t>> bufs, hipStream_t s) {
+  ZeroList z;
+  z.count = 0;
+  for (const auto& b : bufs) {
+    if (!b.first || !b.second) continue;
+    TT2_CHECK(z.count < ZL_MAX, TT2_ERR_INVALID_ARG, "zero_many: too many buffers");
+    TT2_CHECK((reinterpret_cast<uintptr_t>(b.first) & 15) == 0, TT2_ERR_INVALID_ARG, "zero_many: unaligned buffer");
+    z.p[z.count] = b.first;
+    z.n[z.count] = b.second;
+    ++z.count;
+  }
+  if (!z.count) return;
+  hipLaunchKernelGGL(k_zero_many, dim3(1024), dim3(256), 0, s, z);
+  TT2_HIP(hipGetLastError());
+}
 // ReferenceEncoder strides (2,2) everywhere; ReferenceEncoderAdaIn (2,2),(2,2),(1,1)x4 (tacotron.py:237)
 inline int refnet_stride(bool adain, int layer) { return adain && layer >= 2 ? 1 : 2; }
 
@@ -1677,9 +1712,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
   }
-  TT2_HIP(hipMemsetAsync(c->enc_h.p, 0, c->enc_h.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->enc_c.p, 0, c->enc_c.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->enc_out.p, 0, (size_t)BT * 2 * c->U * 4, s));
+  zero_many({{c->enc_h.p, c->enc_h.bytes}, {c->enc_c.p, c->enc_c.bytes}, {c->enc_out.p, (size_t)BT * 2 * c->U * 4}}, s);
   int Tmax = 0;
   for (int b = 0; b < B; ++b) Tmax = std::max(Tmax, lens_h[b]);
   if (c->U == ENC_U && c->pd_dev_ok && c->pd_mode == 1 && c->kg_wmax_enc < KG_BMAX) {  // persistent (128 WGs)
@@ -1820,10 +1853,14 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     GemmArgs g;
     g.M = B; g.N = 4 * c->H; g.K = c->SW; g.A = c->style.as<float>(); g.lda = c->SW;
     g.Bw = c->l1_ws.as<float>(); g.ldb = 4 * c->H; g.Cout = c->GS0.as<float>(); g.ldc = 4 * c->H;
+    g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
+    g.kpart = c->kpart.as<float>(); g.kpart_floats = (long)(c->kpart.bytes / sizeof(float));
     gemm(g, s);
     GemmArgs p;
     p.M = B; p.N = c->NPF; p.K = c->SW; p.A = c->style.as<float>(); p.lda = c->SW;
     p.Bw = c->proj_ws.as<float>(); p.ldb = c->NPF; p.Cout = c->PS.as<float>(); p.ldc = c->NPF;
+    p.split16 = 1;
+    p.kpart = c->kpart.as<float>(); p.kpart_floats = (long)(c->kpart.bytes / sizeof(float));
     gemm(p, s);
   }
   c->B = B;
@@ -2013,11 +2050,10 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   hipLaunchKernelGGL(k_transpose_bt, dim3(PD_TMAX / 32, PD_E2 / 32, c->B), dim3(256), 0, s, c->values.as<float>(),
                      (long)c->Dm, c->valuesT.as<float>(), c->T_in, PD_E2);
   TT2_HIP(hipGetLastError());
-  TT2_HIP(hipMemsetAsync(c->pd_ctl.p, 0, c->pd_ctl.bytes, s));  // flags + ctl words, every launch
-  // granule tags restart at 1 every launch: a stale tag of an earlier decode must never match
-  TT2_HIP(hipMemsetAsync(c->Ex.p, 0, c->Ex.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->PPx.p, 0, c->PPx.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->PREx.p, 0, c->PREx.bytes, s));
+  // flags + ctl words, every launch; granule tags restart at 1 every launch: a stale tag of an
+  // earlier decode must never match
+  zero_many({{c->pd_ctl.p, c->pd_ctl.bytes}, {c->Ex.p, c->Ex.bytes}, {c->PPx.p, c->PPx.bytes},
+             {c->PREx.p, c->PREx.bytes}}, s);
   PdArgs a;
   a.flags = c->pd_ctl.as<unsigned>();
   a.flags2 = a.flags + PD_NPH * PD_NB;
@@ -2073,22 +2109,12 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
   TT2_CHECK(max_iters >= 1 && max_iters <= c->cfg.max_iters, TT2_ERR_SHAPE_MISMATCH, "max_iters exceeds capacity");
   TT2_CHECK(!targets_d || T_lim >= 1, TT2_ERR_INVALID_ARG, "targets given with T_targets < 1");
   // zero decoder state (zero_state, Architecture_wrappers.py:158-195; _go_frames helpers.py:136)
-  for (int p = 0; p < 2; ++p) {
-    TT2_HIP(hipMemsetAsync(c->X1[p].p, 0, c->X1[p].bytes, s));
-    TT2_HIP(hipMemsetAsync(c->H0s[p].p, 0, c->H0s[p].bytes, s));
-    TT2_HIP(hipMemsetAsync(c->H1s[p].p, 0, c->H1s[p].bytes, s));
-  }
-  TT2_HIP(hipMemsetAsync(c->X2.p, 0, c->X2.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->Xp.p, 0, c->Xp.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->RG0.p, 0, c->RG0.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->RG1.p, 0, c->RG1.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->ssum.p, 0, c->ssum.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->pcnt.p, 0, c->pcnt.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->c1.p, 0, c->c1.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->c2.p, 0, c->c2.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->cum.p, 0, c->cum.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->max_att.p, 0, c->max_att.bytes, s));
-  TT2_HIP(hipMemsetAsync(c->ctl.p, 0, sizeof(DecCtl), s));
+  zero_many({{c->X1[0].p, c->X1[0].bytes}, {c->X1[1].p, c->X1[1].bytes}, {c->H0s[0].p, c->H0s[0].bytes},
+             {c->H0s[1].p, c->H0s[1].bytes}, {c->H1s[0].p, c->H1s[0].bytes}, {c->H1s[1].p, c->H1s[1].bytes},
+             {c->X2.p, c->X2.bytes}, {c->Xp.p, c->Xp.bytes}, {c->RG0.p, c->RG0.bytes}, {c->RG1.p, c->RG1.bytes},
+             {c->ssum.p, c->ssum.bytes}, {c->pcnt.p, c->pcnt.bytes}, {c->c1.p, c->c1.bytes}, {c->c2.p, c->c2.bytes},
+             {c->cum.p, c->cum.bytes}, {c->max_att.p, c->max_att.bytes}, {c->ctl.p, sizeof(DecCtl)}},
+            s);
   emt_init_launch(c->emt, emt_spk(c), c->X1[0].as<float>(), c->X1[1].as<float>(), c->P + c->E2, s);
   if (!masks_d) {  // prenet dropout keep bits from the counter-based device RNG
     const long n = (long)max_iters * 2 * c->B * c->P;
