@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--train-precision", default="bf16", choices=["bf16", "fp32"],
                    help="configs[4] names bf16 (GEMM operands; fp32 accumulation and state)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-variants", action="store_true",
+                   help="skip the model-variant legs (Tacotron_emt_attn, style paths, CBHG)")
     p.add_argument("--profile-iters", type=int, default=50)
     return p.parse_args()
 
@@ -366,6 +368,85 @@ def bench_e2e(a, rank, world, local, barrier, max_over_ranks):
                        "GPU, waveforms all-gathered{}".format(world, " over RCCL" if world > 1 else ""))
 
 
+def bench_variants(a, local):
+    """Model variants on the configs[1] shape (B=32 x 201 chars, T_ref 400, T_out 1000; rank 0):
+    Tacotron_emt_attn (args.attn 'multihead' / 'style_tokens': per-step launch path + k_emt_step),
+    the AdaIN and reference-embedding style paths (persistent decoder), and the CBHG linear post-net
+    over the 32 x 1000 mel frames.  Device-resident inputs, tt2_synthesize_dev, HIP-event phases."""
+    import torch
+    from tt2.engine import TacotronEngine
+    from tt2.hparams import hparams
+    from tt2.synthetic import tacotron_inputs
+    from tt2.weights import init_tacotron_emt_weights, init_tacotron_weights
+    dev = torch.device("cuda", local)
+    B, T, TR, n = a.batch, a.chars + 1, a.ref_frames, a.t_out
+    ids, lens, re, rs = tacotron_inputs(B, T, TR, seed=1234, ragged=False)
+    ids_d, lens_d = torch.from_numpy(ids).to(dev), torch.from_numpy(lens).to(dev)
+    re_d, rs_d = torch.from_numpy(re).to(dev), torch.from_numpy(rs).to(dev)
+    mel_d = torch.empty((B, n, 80), dtype=torch.float32, device=dev)
+    stop_d = torch.empty((B, n), dtype=torch.float32, device=dev)
+    lens_h = np.ascontiguousarray(lens, np.int32)
+    out = {}
+
+    def run(eng, label, extra=None):
+        lib, ns = eng.lib, ctypes.c_int32()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+
+        def once():
+            _lib.check(lib.tt2_synthesize_dev(
+                eng.h, ids_d.data_ptr(), lens_d.data_ptr(), _lib.ptr(lens_h), B, T, re_d.data_ptr(), TR,
+                rs_d.data_ptr(), TR, n, None, 5339, mel_d.data_ptr(), stop_d.data_ptr(),
+                ctypes.byref(ns), ctypes.c_void_p(stream)), lib)
+        once()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        once()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ms3 = (ctypes.c_float * 3)()
+        _lib.check(lib.tt2_last_timings(eng.h, ms3), lib)
+        persist, _ = eng.decoder_path()
+        d = dict(value=round(B * ns.value / el, 1), unit="mel-frames/s", ms_per_batch=round(1e3 * el, 2),
+                 decode_us_per_step=round(1e3 * ms3[1] / max(ns.value, 1), 2), steps=ns.value,
+                 decoder="persistent" if persist else "launch path")
+        if extra:
+            d.update(extra)
+        out[label] = d
+
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1, max_iters=n))
+    for attn, rg in (("multihead", "gru"), ("style_tokens", "none")):
+        W = init_tacotron_emt_weights(hp, attn, rg, seed=hp.tacotron_random_seed)
+        eng = TacotronEngine(hp, W, B, T, TR, n, local, emt_attn=attn, emt_ref_gru=rg)
+        if attn == "style_tokens":
+            eng.set_emt_labels(np.arange(B, dtype=np.int32) % 4)
+        run(eng, "emt_attn_" + attn, dict(emt_ref_gru=rg))
+        eng.close()
+    for style in ("adain", "embed"):
+        W = init_tacotron_weights(hp, seed=hp.tacotron_random_seed, style=style)
+        eng = TacotronEngine(hp, W, B, T, TR, n, local, style=style)
+        run(eng, "style_" + style)
+        eng.close()
+    hpl = hp.copy()
+    hpl.predict_linear = True
+    W = init_tacotron_weights(hpl, seed=hp.tacotron_random_seed)
+    eng = TacotronEngine(hpl, W, B, T, TR, n, local)
+    lin_d = torch.empty((B, n, hpl.num_freq), dtype=torch.float32, device=dev)
+    x_d = torch.rand((B, n, 80), dtype=torch.float32, device=dev) * 8 - 4
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _lib.check(eng.lib.tt2_linear_outputs_dev(eng.h, x_d.data_ptr(), B, n, lin_d.data_ptr(),
+                                                  ctypes.c_void_p(stream)), eng.lib)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    eng.close()
+    out["cbhg_linear"] = dict(value=round(B * n / el, 1), unit="mel-frames/s", ms_per_batch=round(1e3 * el, 2),
+                              frames=B * n, num_freq=hpl.num_freq)
+    return out
+
+
 def main():
     a = parse()
     import torch
@@ -606,6 +687,11 @@ def main():
     if not a.no_train:
         trn = bench_train(a, rank, world, local, barrier, max_over_ranks)
 
+    # --- model variants (rank 0, N = 1 only) ---
+    variants = None
+    if rank == 0 and world == 1 and not a.no_variants:
+        variants = bench_variants(a, local)
+
     # --- CPU baseline (rank 0, N = 1 only) ---
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -637,7 +723,7 @@ def main():
                                decoded_steps=n_steps.value, ref_frames=a.ref_frames,
                                parallelism="utterance-batch sharding x{}".format(world)),
                    phases=phases, roofline=roofline, cpu_baseline=cpu, wavenet=wn, e2e=e2e,
-                   griffin_lim=glr, train=trn,
+                   griffin_lim=glr, train=trn, variants=variants,
                    diag_stamps=stamps)
         print(json.dumps(out))
     eng.close()

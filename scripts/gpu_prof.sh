@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 # profiled process segfaults at exit (after the run, before the next pass; seen r02b)
 export TT2_COOP=0
 TAG=${1:-p}
-ARGS="${PROF_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-wavenet --no-e2e --no-griffin-lim}"
+ARGS="${PROF_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-wavenet --no-e2e --no-griffin-lim --no-variants}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG/trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_$TAG.bench.json 2>/dev/null && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_$TAG/fetch -o run --output-format csv -- python3 bench.py $ARGS > /dev/null 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_$TAG/write -o run --output-format csv -- python3 bench.py $ARGS > /dev/null 2>&1 && \

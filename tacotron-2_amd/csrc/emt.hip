@@ -95,6 +95,20 @@ __global__ void k_emt_qrow(const float* __restrict__ qb, const float* __restrict
 }
 
 // ---- decoder step --------------------------------------------------------------------------------
+// Σ_{k0 <= k < k1} x[k]·W[k·ld + col]: 8 independent accumulators so 8 weight loads are in flight
+// per thread (one dependent chain of L2 loads would cost ~0.5 us per 2 k)
+__device__ __forceinline__ float dot_col(const float* __restrict__ x, const float* __restrict__ W, int ld, int col, int k0,
+                                         int k1) {
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = k0;
+  for (; k + 8 <= k1; k += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = fmaf(x[k + u], W[(long)(k + u) * ld + col], acc[u]);
+  }
+  for (; k < k1; ++k) acc[0] = fmaf(x[k], W[(long)k * ld + col], acc[0]);
+  return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
 struct EmtStepArgs {
   const int* done;
   const float* Xp;                    // AF [32 x ...]: h2 = LSTM_output at columns [0, H)
@@ -132,10 +146,7 @@ __global__ __launch_bounds__(512) void k_emt_step(EmtStepArgs a) {
   const int col = tid & 127, ks = tid >> 7;
   {
     float acc = 0.f;
-    if (col < a.Aq) {
-      const int k0 = ks * a.H / 4, k1 = (ks + 1) * a.H / 4;
-      for (int k = k0; k < k1; ++k) acc = fmaf(h2[k], a.wq[(long)k * a.Aq + col], acc);
-    }
+    if (col < a.Aq) acc = dot_col(h2, a.wq, a.Aq, col, ks * a.H / 4, (ks + 1) * a.H / 4);
     part[ks * 128 + col] = acc;
   }
   __syncthreads();
@@ -178,10 +189,7 @@ __global__ __launch_bounds__(512) void k_emt_step(EmtStepArgs a) {
   __syncthreads();
   if (a.wd) {
     const int K = a.heads * a.Dv;
-    float acc = 0.f;
-    const int k0 = ks * K / 4, k1 = (ks + 1) * K / 4;
-    for (int k = k0; k < k1; ++k) acc = fmaf(comb[k], a.wd[(long)k * EMT_OUT + col], acc);
-    part[ks * 128 + col] = acc;
+    part[ks * 128 + col] = dot_col(comb, a.wd, EMT_OUT, col, ks * K / 4, (ks + 1) * K / 4);
     __syncthreads();
     if (tid < EMT_OUT) {
       float o = ((part[tid] + part[128 + tid]) + (part[256 + tid] + part[384 + tid])) + a.bd[tid];

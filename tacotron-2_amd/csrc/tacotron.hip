@@ -771,6 +771,7 @@ static void launch_lstm(const LstmArgs& l, int H, hipStream_t s) {
   const int npw = nsg % 8 == 0 ? nsg / 8 : 0;
   if (npw == 18) hipLaunchKernelGGL(k_lstm<18>, grid, blk, 0, s, l);
   else if (npw == 8) hipLaunchKernelGGL(k_lstm<8>, grid, blk, 0, s, l);
+  else if (npw == 7) hipLaunchKernelGGL(k_lstm<7>, grid, blk, 0, s, l);  // emt 'multihead': K1 = 896
   else if (npw == 6) hipLaunchKernelGGL(k_lstm<6>, grid, blk, 0, s, l);
   else if (npw == 4) hipLaunchKernelGGL(k_lstm<4>, grid, blk, 0, s, l);
   else if (npw == 2) hipLaunchKernelGGL(k_lstm<2>, grid, blk, 0, s, l);
