@@ -21,6 +21,9 @@ constexpr int PD_KSP = 8;     // projection K split (128 h2 rows + 64 context ro
 constexpr int PD_TMAX = 256;  // max encoder steps (T_in)
 constexpr int PD_KLP = 32;    // location-conv taps padded to 16
 constexpr int PD_NREP = 8;    // replicas of the H1/H2 flag lines (32 pollers per line)
+// Hidden unit q (0..3) of LSTM tile g: the four units of a tile are the four components of one AF
+// float4 (common.h af_idx), 16(g/4) + g%4 + 4q.  Tiles [32w, 32w+32) own units [128w, 128w+128).
+__host__ __device__ inline int pd_unit(int g, int q) { return 16 * (g >> 2) + (g & 3) + 4 * q; }
 enum { PD_F_PRE = 0, PD_F_H1, PD_F_H2, PD_F_E, PD_F_CTX, PD_F_PP, PD_NPH };
 
 struct PdArgs {

@@ -10,7 +10,8 @@
 // work-groups.
 //
 // Roles of work-group g (every work-group has all three):
-//   LSTM   hidden units [4g, 4g+4) of both layers = one 16-column gate tile (lstm_cols order)
+//   LSTM   hidden units pd_unit(g, 0..3) of both layers = one 16-column gate tile (pd_lstm_cols
+//          order): one AF float4 per row, so the h1/h2 exchange stores are whole 16-byte stores
 //   row    attention row b = (g&7)*4 + ((g>>3)&3), slice j = g>>5: attention dims [16j, 16j+16),
 //          context channels [64j, 64j+64), prenet-L2 outputs [32j, 32j+32).  The 8 siblings of a
 //          row have equal g%8 (one XCD under round-robin placement: faster, never required).
@@ -36,6 +37,8 @@
 #include "decode_persist.h"
 
 namespace tt2 {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 typedef __attribute__((address_space(1))) float pd_gf32;
 typedef __attribute__((address_space(1))) unsigned pd_gu32;
@@ -171,6 +174,19 @@ __device__ __forceinline__ bool pd_take(const PdArgs& a, int ph, const unsigned 
   }
 }
 
+// LSTM epilogue store: the 4 hidden units this work-group owns for row em (pd_unit) are one AF
+// float4, held by the 4 consecutive lanes eu = 0..3; lane eu = 0 writes it as ONE 16-byte
+// write-through store (rows 0..15 / 16..31 of a work-group fill 256 contiguous bytes each).
+__device__ __forceinline__ void pd_st_h4(float* X, int em, int u0, float hn, int lane) {
+  const int src = lane & ~3;
+  const float v0 = __shfl(hn, src), v1 = __shfl(hn, src + 1), v2 = __shfl(hn, src + 2), v3 = __shfl(hn, src + 3);
+  if ((lane & 3) == 0) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(X, (short)0, 0x7fffffff, 0x00020000);
+    const u32x4 d = {__float_as_uint(v0), __float_as_uint(v1), __float_as_uint(v2), __float_as_uint(v3)};
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, af_idx(em, u0) * 4, 0, 16);  // sc1
+  }
+}
+
 // Every storing wave drains its sc1 stores, then one lane raises this work-group's flag.
 __device__ __forceinline__ void pd_publish(const PdArgs& a, int ph, unsigned val, int tid) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -291,9 +307,11 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     wl[1] = LW[64 + lane];
   }
   float b1v[4], b2v[4], gsv[4];
+  const int u0 = pd_unit(g, 0);  // this work-group's hidden units pd_unit(g, 0..3): one AF float4 per row
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int col = g * 16 + 4 * q + eu;
+    const int u = pd_unit(g, eu);
+    const int col = (u >> 2) * 16 + 4 * q + (u & 3);  // biases / style terms come in lstm_cols order
     b1v[q] = a.l1_b[col];
     b2v[q] = a.l2_b[col];
     gsv[q] = a.GS[(long)em * 4 * PD_H + col];
@@ -507,7 +525,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       const float cn = sigm_fast(z[2] + 1.0f) * c1 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
       c1 = a.one_m_zo * cn + a.zo * c1;
-      pd_st(a.H1x + p * 32 * PD_H + af_idx(em, 4 * g + eu), hn);
+      pd_st_h4(a.H1x + p * 32 * PD_H, em, u0, hn, lane);
     }
     pd_publish_rep(a, 0, tg, tid);
     PD_STAMP(2);
@@ -548,7 +566,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       const float cn = sigm_fast(z[2] + 1.0f) * c2 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
       c2 = a.one_m_zo * cn + a.zo * c2;
-      pd_st(a.H2x + p * 32 * PD_H + af_idx(em, 4 * g + eu), hn);
+      pd_st_h4(a.H2x + p * 32 * PD_H, em, u0, hn, lane);
     }
     pd_publish_rep(a, 1, tg, tid);
     PD_STAMP(5);

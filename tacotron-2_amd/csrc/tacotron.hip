@@ -1343,6 +1343,15 @@ static std::vector<int> lstm_cols(int H) {
   return cols;
 }
 
+// the persistent decoder's tile order: tile g owns units pd_unit(g, 0..3) (decode_persist.h)
+static std::vector<int> pd_lstm_cols(int H) {
+  std::vector<int> cols;
+  for (int g = 0; g < H / 4; ++g)
+    for (int gate = 0; gate < 4; ++gate)
+      for (int uu = 0; uu < 4; ++uu) cols.push_back(gate * H + pd_unit(g, uu));
+  return cols;
+}
+
 static void finalize(tt2_ctx* c) {
   const auto& cfg = c->cfg;
   const WeightMap& wm = c->host;
@@ -1486,8 +1495,11 @@ static void finalize(tt2_ctx* c) {
       c->kg_wmax_dec = std::max(c->kg_wmax_dec, std::max(absmax(wc), absmax(wr)));
       upload(l == 0 ? c->l1_w : c->l2_w, wc);
       upload(l == 0 ? c->l1_wh : c->l2_wh, wr);
-      upload_scaled(l == 0 ? c->pd_l1_w : c->pd_l2_w, wc, KG_SB);
-      upload_scaled(l == 0 ? c->pd_l1_wh : c->pd_l2_wh, wr, KG_SB);
+      if (H % 16 == 0) {  // persistent decoder tiles (pd_fits also requires H == PD_H)
+        const auto pc = pd_lstm_cols(H);
+        upload_scaled(l == 0 ? c->pd_l1_w : c->pd_l2_w, pack_wf(k.data.data(), Kc, N, pc, Kc), KG_SB);
+        upload_scaled(l == 0 ? c->pd_l1_wh : c->pd_l2_wh, pack_wf(k.data.data() + (size_t)Kh0 * N, H, N, pc, H), KG_SB);
+      }
     }
     upload(l == 0 ? c->l1_b : c->l2_b, bt);
     if (l == 0 && c->SW) {  // style rows, lstm column order, row-major [SW][4H] (B operand of the GS GEMM)
