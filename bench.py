@@ -269,6 +269,7 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
             tr.forward_backward(*batch)
         tr.allreduce_grads()
         tr.apply()
+        tr.sync_moving_stats()
 
     step()
     losses.append(tr.losses())

@@ -424,6 +424,14 @@ tt2_status tt2_train_finalize(tt2_train_ctx* ctx);
 /* Use a caller-owned device buffer (e.g. a torch tensor RCCL all-reduces) as the flat gradient
  * buffer; NULL restores the internal one.  *n_out = its length in floats. */
 tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* ctx, float* grads_d, int64_t* n_out);
+/* Every batch-norm moving_mean / moving_variance (Postnet, encoder convs, reference-encoder
+ * convs) packed in variable order into a caller-owned device buffer (unpack = 0) or written back
+ * from it (unpack = 1), enqueued on `stream`; buf_d NULL only sets *n_out = the float count.
+ * Data-parallel ranks update these from their own shard's batch statistics; the host averages the
+ * packed buffer over ranks after apply, where the reference's towers all update ONE shared set of
+ * UPDATE_OPS variables (tacotron.py:1088-1090, tower loop 1194-1208). */
+tt2_status tt2_train_moving_stats_dev(tt2_train_ctx* ctx, float* buf_d, int64_t* n_out, int unpack,
+                                      void* stream);
 /* Forward + losses + backward on DEVICE inputs: memory [B,T_in,D] (encoder outputs ⊕ style),
  * lengths int32 [B], mel targets [B,T_out,80], stop targets [B,T_out], prenet keep bits u8
  * [T_out,2,B,P], zoneout keep bits u8 [T_out,4,B,H] (c1,h1,c2,h2) or NULL (inference mix),

@@ -2040,6 +2040,37 @@ tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* c, float* grads_d, int64_t* n
   });
 }
 
+tt2_status tt2_train_moving_stats_dev(tt2_train_ctx* c, float* buf_d, int64_t* n_out, int unpack, void* stream) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_train_finalize not called");
+    auto is_stat = [](const std::string& n) {
+      auto ends = [&](const char* s) {
+        const size_t k = std::strlen(s);
+        return n.size() >= k && n.compare(n.size() - k, k, s) == 0;
+      };
+      return ends("moving_mean") || ends("moving_variance");
+    };
+    int64_t total = 0;
+    for (const auto& v : c->vars)
+      if (is_stat(v.name)) total += v.n;
+    if (n_out) *n_out = total;
+    if (!buf_d) return;
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    int64_t o = 0;
+    for (const auto& v : c->vars) {
+      if (!is_stat(v.name)) continue;
+      float* p = c->params.as<float>() + v.off;
+      if (unpack)
+        TT2_HIP(hipMemcpyAsync(p, buf_d + o, v.n * sizeof(float), hipMemcpyDeviceToDevice, s));
+      else
+        TT2_HIP(hipMemcpyAsync(buf_d + o, p, v.n * sizeof(float), hipMemcpyDeviceToDevice, s));
+      o += v.n;
+    }
+  });
+}
+
 tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* c, const float* memory_d, const int32_t* lengths_d,
                                           const float* targets_d, const float* stop_targets_d,
                                           const uint8_t* prenet_masks_d, const uint8_t* zoneout_masks_d,

@@ -150,6 +150,7 @@ SIGNATURES = {
     "tt2_train_load_tensor": (_I, [_P, ctypes.c_char_p, _P, _P, _I]),
     "tt2_train_finalize": (_I, [_P]),
     "tt2_train_bind_grads_dev": (_I, [_P, _P, ctypes.POINTER(ctypes.c_int64)]),
+    "tt2_train_moving_stats_dev": (_I, [_P, _P, ctypes.POINTER(ctypes.c_int64), _I, _P]),
     "tt2_train_forward_backward_dev": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "tt2_train_forward_backward_text_dev": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P,
                                                  _P, _I, _I, _P]),

@@ -242,6 +242,33 @@ class TacotronTrainer(object):
         with self.torch.cuda.stream(self.stream):
             tower_mean_(buf, group)
 
+    def sync_moving_stats(self, group=None):
+        """Average every batch-norm moving_mean / moving_variance over the data-parallel ranks.
+
+        In the reference all towers run the UPDATE_OPS of ONE shared set of moving-statistics
+        variables (tacotron.py:1088-1090 inside the tower loop 1194-1208), so a checkpoint holds a
+        single set.  Here every rank updates its own copy from its shard's batch statistics in
+        apply(); one all-reduce (mean) of the packed statistics right after it keeps the ranks'
+        copies identical (the mean of the per-shard momentum updates, where TF applies the towers'
+        updates one after another in an unspecified order)."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+            return
+        from .parallel import tower_mean_
+        n = ctypes.c_int64()
+        check(self.lib.tt2_train_moving_stats_dev(self.h, None, ctypes.byref(n), 0, None))
+        if n.value == 0:
+            return
+        with self.torch.cuda.stream(self.stream):
+            buf = self.torch.empty(n.value, dtype=self.torch.float32, device=self.device)
+            sp = ctypes.c_void_p(self.stream.cuda_stream)
+            check(self.lib.tt2_train_moving_stats_dev(self.h, ctypes.c_void_p(buf.data_ptr()), None,
+                                                      0, sp))
+            tower_mean_(buf, group)
+            check(self.lib.tt2_train_moving_stats_dev(self.h, ctypes.c_void_p(buf.data_ptr()), None,
+                                                      1, sp))
+            self.stream.synchronize()
+
     def apply(self, global_step=None, lr=None):
         """clip_by_global_norm(1.0) + Adam at update count ``global_step`` (1-based).
 
@@ -266,6 +293,7 @@ class TacotronTrainer(object):
                               postnet_masks)
         self.allreduce_grads()
         self.apply()
+        self.sync_moving_stats()
         return self.losses()
 
     def losses(self):

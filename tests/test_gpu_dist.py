@@ -7,7 +7,8 @@ library (the world>1 branches had only run with the oracle standing
   single-process full-batch run.
 * One data-parallel training step: each rank forward/backward on its tower, the tower mean as an
   all-reduce of the flat gradient buffer, clipped Adam: the updated parameters equal a single
-  process that averages the two towers' device gradients itself, and they moved at step 1.
+  process that averages the two towers' device gradients itself, and they moved at step 1; the
+  batch-norm moving statistics are the rank mean of the per-shard updates and equal on both ranks.
 """
 import os
 import socket
@@ -68,6 +69,8 @@ def _tower(batch, s, e):
 
 
 VAR = "Tacotron_model/inference/decoder/decoder_LSTM/multi_rnn_cell/cell_0/lstm_cell/kernel"
+BNM = ("Tacotron_model/inference/postnet_convolutions/conv_layer_1_postnet_convolutions/"
+       "batch_normalization/moving_mean")
 
 
 def _worker(rank, world, port, out_dir):
@@ -92,6 +95,7 @@ def _worker(rank, world, port, out_dir):
         np.save(os.path.join(out_dir, "param_{}.npy".format(rank)),
                 tr.get(VAR, 0, np.asarray(TW[VAR]).shape))
         np.save(os.path.join(out_dir, "loss_{}.npy".format(rank)), np.array([L["loss"]]))
+        np.save(os.path.join(out_dir, "bnm_{}.npy".format(rank)), tr.get(BNM, 0, (thp.postnet_channels,)))
         tr.close()
     finally:
         dist.destroy_process_group()
@@ -133,3 +137,16 @@ def test_gloo_world2_product_path_on_one_gpu(tmp_path):
     for r in range(world):
         got = np.load(str(tmp_path / "param_{}.npy".format(r)))
         np.testing.assert_allclose(got, want, rtol=0, atol=1e-6)
+    # BN moving statistics: each rank's momentum update from its own shard, averaged over ranks
+    # (sync_moving_stats) = the mean of the two single-tower updates; identical on both ranks
+    per_tower = []
+    for s, e in ((0, B // 2), (B // 2, B)):
+        t1 = TacotronTrainer(thp, TW, B // 2, T_in, T, 0)
+        t1.forward_backward(*_tower(batch, s, e))
+        t1.apply(1)
+        per_tower.append(t1.get(BNM, 0, (thp.postnet_channels,)))
+        t1.close()
+    assert np.abs(per_tower[0] - per_tower[1]).max() > 1e-6   # the shards' statistics differ
+    bn = [np.load(str(tmp_path / "bnm_{}.npy".format(r))) for r in range(world)]
+    np.testing.assert_array_equal(bn[0], bn[1])
+    np.testing.assert_allclose(bn[0], (per_tower[0] + per_tower[1]) / 2, rtol=0, atol=1e-6)
