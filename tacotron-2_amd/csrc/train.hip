@@ -22,6 +22,8 @@
 #include <cstring>
 #include <functional>
 
+#include <rocblas/rocblas.h>
+
 #include "common.h"
 #include "gemm.h"
 #include "train_front.h"
@@ -62,6 +64,11 @@ struct tt2_train_ctx {
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
   DevBuf TH, E, DF, PQ, FALL, ALN;
+  // bf16 operand copies + rocBLAS handle of the large plain products (tr_gemm_blas)
+  DevBuf blasA, blasB;
+  rocblas_handle blas = nullptr;
+  bool blas_on = true;  // TT2_TRAIN_BLAS=0 at create: every product on the hand-written kernels
+  long blas_calls = 0;
   // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
   DevBuf hK1, hK1T, hK2, hK2T, hWq, hWqT;
   // Postnet training (cfg.postnet): PA[i] activations (pre-BN), PX[i] layer inputs (PX[0] unused:
@@ -925,10 +932,68 @@ static void tr_colsum(tt2_train_ctx* c, const float* in, long M, int N, long ld,
 // distinct contexts driven from different threads stay independent)
 static thread_local DevBuf* g_tr_kpart = nullptr;  // split-K scratch (stream-ordered)
 static thread_local int g_tr_prec = 0;             // GemmArgs::split16 (0 fp32, 2 bf16)
+static thread_local tt2_train_ctx* g_tr_ctx = nullptr;  // bf16 BLAS scratch + handle of that context
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// fp32 [rows][cols] (leading dimension ld) -> dense bf16 [rows][cols], round to nearest even (the
+// same rounding the bf16 GEMM kernels apply when they stage operands)
+__global__ void k_tr_to_bf16(const float* __restrict__ src, long rows, long cols, long ld, __bf16* __restrict__ dst) {
+  const long n = rows * cols;
+  for (long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (long)gridDim.x * blockDim.x * 4) {
+    const long r = i / cols, cc = i % cols;
+    if (cc + 3 < cols && (ld & 3) == 0) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + r * ld + cc);
+      bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(dst + i) = o;
+    } else {
+      for (int e = 0; e < 4 && i + e < n; ++e) {
+        const long r2 = (i + e) / cols, c2 = (i + e) % cols;
+        dst[i + e] = (__bf16)src[r2 * ld + c2];
+      }
+    }
+  }
+}
+
+// The large plain products of the bf16 step (weight gradients over all T·B rows, the Postnet
+// convolution gradients): C[M][N] = A[M][K]·B[K][N] as one rocBLAS bf16 GEMM with fp32
+// accumulation after a one-pass bf16 conversion of both operands.  Same operand rounding as the
+// hand-written bf16 kernels; these shapes (K up to 51 200 rows, 0.1-1 TFLOP each) are library
+// GEMMs, the hand-written kernels keep the small per-step products and every fused epilogue.
+static constexpr double kTrBlasMinFlops = 2.0e10;
+static bool tr_gemm_blas(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
+                         hipStream_t s) {
+  tt2_train_ctx* c = g_tr_ctx;
+  if (!c) return false;
+  if (!c->blas) {
+    TT2_CHECK(rocblas_create_handle(&c->blas) == rocblas_status_success, TT2_ERR_HIP, "rocblas_create_handle failed");
+  }
+  const size_t na = (size_t)M * K, nb = (size_t)K * N;
+  if (c->blasA.bytes < na * 2) c->blasA.alloc(na * 2);
+  if (c->blasB.bytes < nb * 2) c->blasB.alloc(nb * 2);
+  __bf16* a16 = reinterpret_cast<__bf16*>(c->blasA.p);
+  __bf16* b16 = reinterpret_cast<__bf16*>(c->blasB.p);
+  hipLaunchKernelGGL(k_tr_to_bf16, dim3(2048), dim3(256), 0, s, A, (long)M, (long)K, lda, a16);
+  hipLaunchKernelGGL(k_tr_to_bf16, dim3(2048), dim3(256), 0, s, Bw, (long)K, (long)N, ldb, b16);
+  TT2_HIP(hipGetLastError());
+  TT2_CHECK(rocblas_set_stream(c->blas, s) == rocblas_status_success, TT2_ERR_HIP, "rocblas_set_stream failed");
+  const float alpha = 1.f, beta = 0.f;
+  // row-major C = A·B is column-major C^T (N x M) = B^T (N x K, ld N) · A^T (K x M, ld K)
+  const rocblas_status st = rocblas_gemm_ex(c->blas, rocblas_operation_none, rocblas_operation_none, N, M, K, &alpha,
+                                            b16, rocblas_datatype_bf16_r, N, a16, rocblas_datatype_bf16_r, K, &beta, C,
+                                            rocblas_datatype_f32_r, (int)ldc, C, rocblas_datatype_f32_r, (int)ldc,
+                                            rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
+  TT2_CHECK(st == rocblas_status_success, TT2_ERR_HIP, "rocblas_gemm_ex failed: status " + std::to_string((int)st));
+  ++c->blas_calls;
+  return true;
+}
 
 static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
                     hipStream_t s, const float* bias = nullptr, const float* residual = nullptr, long ldr = 0,
                     int act = ACT_NONE, const DevBuf* bt16 = nullptr, long ldbt = 0) {
+  if (g_tr_ctx && g_tr_ctx->blas_on && g_tr_prec == 2 && !bias && !residual && act == ACT_NONE &&
+      2.0 * M * (double)N * K >= kTrBlasMinFlops && tr_gemm_blas(M, N, K, A, lda, Bw, ldb, C, ldc, s))
+    return;
   GemmArgs g;
   if (g_tr_prec == 2 && bt16 && bt16->p && ldbt % 8 == 0) {  // weights pre-converted: B^T in bf16
     g.Bt16 = bt16->p;
@@ -1191,6 +1256,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   c->Tin_last = Tin;
   g_tr_kpart = &c->kpart;
   g_tr_prec = c->cfg.precision ? 2 : 0;
+  g_tr_ctx = c;
   // weight transposes for the backward products
   tr_transpose(pvar(c, L1V("kernel")), LX1, 4 * H, 4 * H, c->K1T.as<float>(), LX1, s);
   tr_transpose(pvar(c, L2V("kernel")), 2 * H, 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, s);
@@ -1381,6 +1447,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
                      D, c->DMEM.as<float>());
   g_tr_kpart = nullptr;
   g_tr_prec = 0;
+  g_tr_ctx = nullptr;
 }
 
 // L2 regularisation of the regularised kernels (after every gradient of the step has landed)
@@ -1952,6 +2019,7 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
     TT2_CHECK(hip_device >= 0 && hip_device < n, TT2_ERR_HIP, "no such HIP device");
     TT2_HIP(hipSetDevice(hip_device));
     auto* c = new tt2_train_ctx();
+    if (const char* e = std::getenv("TT2_TRAIN_BLAS")) c->blas_on = std::atoi(e) != 0;
     try {
       c->dev = hip_device;
       c->cfg = *cfg;
@@ -1999,6 +2067,7 @@ void tt2_train_destroy(tt2_train_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->blas) (void)rocblas_destroy_handle(c->blas);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2117,14 +2186,17 @@ tt2_status tt2_train_forward_backward_text_dev(tt2_train_ctx* c, const int32_t* 
     const float* refs[2] = {ref_emt_d, ref_spk_d};
     g_tr_kpart = &c->kpart;
     g_tr_prec = c->cfg.precision ? 2 : 0;
+    g_tr_ctx = c;
     tr_front_forward(c, ids_d, lengths_d, refs, T_ref, enc_conv_masks_d, enc_zoneout_masks_d, T_in, s);
     tr_forward_backward(c, c->fMEM.as<float>(), lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d,
                         postnet_masks_d, T_in, T_out, s);
     g_tr_kpart = &c->kpart;
     g_tr_prec = c->cfg.precision ? 2 : 0;
+    g_tr_ctx = c;
     tr_front_backward(c, ids_d, lengths_d, refs, T_ref, enc_conv_masks_d, enc_zoneout_masks_d, T_in, s);
     g_tr_kpart = nullptr;
     g_tr_prec = 0;
+    g_tr_ctx = nullptr;
     tr_regularize(c, s);
     TT2_HIP(hipEventRecord(c->ev1, s));
     TT2_HIP(hipGetLastError());
@@ -2161,6 +2233,10 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
     TT2_CHECK(c && name && host, TT2_ERR_INVALID_ARG, "null argument");
     TT2_HIP(hipSetDevice(c->dev));
     TT2_HIP(hipDeviceSynchronize());
+    if (std::string(name) == "diag:blas_calls") {  // library GEMMs issued since create (1 float)
+      host[0] = (float)c->blas_calls;
+      return;
+    }
     if (std::string(name) == "memory") {  // d loss / d memory of the last forward_backward
       tr_d2h(c, host, c->DMEM.p, sizeof(float) * (size_t)c->B * c->Tin_last * c->D);
       return;

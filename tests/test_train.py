@@ -569,3 +569,49 @@ def test_gpu_train_frontend_matches_oracle(masks):
             np.testing.assert_allclose(mm, want, rtol=1e-5, atol=1e-5, err_msg=sc)
     finally:
         tr.close()
+
+
+@pytest.mark.gpu
+def test_gpu_train_bf16_library_gemms_match_kernels():
+    """bf16 mode routes the large plain products (weight gradients over all T·B rows, >= 2e10
+    flops) through rocBLAS bf16 GEMMs after the same bf16 operand rounding; TT2_TRAIN_BLAS=0 keeps
+    them on the hand-written kernels.  Same inputs, fork-default widths, T·B = 2000 rows: the
+    forward, the losses and d memory are identical (those products only produce terminal weight
+    gradients), every gradient agrees to fp32 accumulation-order level (measured: bit-identical --
+    the library accumulates K in the same MFMA order), and the context counts the library calls."""
+    import os
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    hp.override_from_dict(dict(attention_dim=128, attention_filters=32, prenet_layers=[256, 256],
+                               decoder_lstm_units=1024))
+    B, T_in, T_out = 8, 40, 250
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
+    names = TRN.train_var_names()
+    res = {}
+    old = os.environ.get("TT2_TRAIN_BLAS")
+    try:
+        for flag in ("1", "0"):
+            os.environ["TT2_TRAIN_BLAS"] = flag
+            tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", postnet=False)
+            try:
+                tr.forward_backward(mem, lens, tg, st, pm, zm)
+                L = tr.losses()
+                grads = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}
+                gmem = tr.get("memory", 1, mem.shape)
+                nblas = int(tr.get("diag:blas_calls", 0, (1,))[0])
+            finally:
+                tr.close()
+            res[flag] = (L, grads, gmem)
+            # on: the two LSTM kernel gradients (2e10+ flops each at T·B = 2000); off: none
+            assert nblas == (2 if flag == "1" else 0), (flag, nblas)
+    finally:
+        if old is None:
+            os.environ.pop("TT2_TRAIN_BLAS", None)
+        else:
+            os.environ["TT2_TRAIN_BLAS"] = old
+    (La, ga, ma), (Lb, gb, mb) = res["1"], res["0"]
+    assert La["before"] == Lb["before"] and La["stop_token"] == Lb["stop_token"]
+    np.testing.assert_array_equal(ma, mb)
+    for n in names:
+        frob = float(np.linalg.norm(ga[n] - gb[n]) / max(np.linalg.norm(gb[n]), 1e-30))
+        assert frob < 1e-4, (n, frob)
