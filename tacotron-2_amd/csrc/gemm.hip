@@ -212,19 +212,42 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 
 // split-K combine: C = epilogue(sum_z kpart[z]) (same epilogue as epilogue_tile)
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)g.M * g.N) return;
-  const int row = (int)(i / g.N), col = (int)(i % g.N);
-  float y = 0.f;
-  for (int z = 0; z < g.ksplit; ++z) y += g.kpart[(long)z * g.M * g.N + i];
-  if (g.bias) y += g.bias[col];
-  if (g.act == ACT_RELU) y = fmaxf(y, 0.f);
-  else if (g.act == ACT_TANH) y = tanhf(y);
-  if (g.bn_scale) y = y * g.bn_scale[col] + g.bn_shift[col];
-  if (g.act == ACT_BN_RELU) y = fmaxf(y, 0.f);
-  if (g.residual) y = g.residual[(long)row * g.ldr + col] + y;
-  if (g.clip) y = fminf(fmaxf(y, g.clip_lo), g.clip_hi);
-  g.Cout[(long)row * g.ldc + col] = y;
+  // 4 consecutive outputs per thread: 16-byte partial loads when N % 4 == 0, two independent
+  // accumulator chains over the splits (the same summation order as the scalar loop pairwise)
+  const long MN = (long)g.M * g.N;
+  const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i0 >= MN) return;
+  float y[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((g.N & 3) == 0) {
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+    int z = 0;
+    for (; z + 1 < g.ksplit; z += 2) {
+      a0 += *reinterpret_cast<const f32x4*>(g.kpart + (long)z * MN + i0);
+      a1 += *reinterpret_cast<const f32x4*>(g.kpart + (long)(z + 1) * MN + i0);
+    }
+    if (z < g.ksplit) a0 += *reinterpret_cast<const f32x4*>(g.kpart + (long)z * MN + i0);
+    const f32x4 t = a0 + a1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = t[e];
+  } else {
+    for (int e = 0; e < 4 && i0 + e < MN; ++e)
+      for (int z = 0; z < g.ksplit; ++z) y[e] += g.kpart[(long)z * MN + i0 + e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long i = i0 + e;
+    if (i >= MN) break;
+    const int row = (int)(i / g.N), col = (int)(i % g.N);
+    float v = y[e];
+    if (g.bias) v += g.bias[col];
+    if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
+    else if (g.act == ACT_TANH) v = tanhf(v);
+    if (g.bn_scale) v = v * g.bn_scale[col] + g.bn_shift[col];
+    if (g.act == ACT_BN_RELU) v = fmaxf(v, 0.f);
+    if (g.residual) v = g.residual[(long)row * g.ldr + col] + v;
+    if (g.clip) v = fminf(fmaxf(v, g.clip_lo), g.clip_hi);
+    g.Cout[(long)row * g.ldc + col] = v;
+  }
 }
 
 
@@ -532,7 +555,7 @@ int gemm_impl(const GemmArgs& a, hipStream_t s) {
 #undef TT2_X3
     TT2_HIP(hipGetLastError());
     if (g.ksplit > 1 && !g.raw) {
-      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256)), dim3(256), 0, s, g);
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 1023) / 1024)), dim3(256), 0, s, g);
       TT2_HIP(hipGetLastError());
     }
     return g.ksplit;
@@ -560,7 +583,7 @@ int gemm_impl(const GemmArgs& a, hipStream_t s) {
   else if (wnb == 2) launch<1, 2>(g, va, vb, s);
   else launch<1, 1>(g, va, vb, s);
   if (g.ksplit > 1 && !g.raw) {
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256)), dim3(256), 0, s, g);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 1023) / 1024)), dim3(256), 0, s, g);
     TT2_HIP(hipGetLastError());
   }
   return g.ksplit;

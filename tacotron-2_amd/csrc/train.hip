@@ -150,19 +150,41 @@ __global__ __launch_bounds__(256) void k_tr_transpose(const float* __restrict__ 
   }
 }
 
-// partial column sums: part[s][n] = sum over rows m = s, s+S, ... of in[m*ld + n]
+// Column reductions over M rows of a row-major [M][N] matrix (column sums, BN statistics, BN
+// backward sums) run as a (column tile, row split) grid: a tile is TW = 32 or 64 columns (32 when
+// N < 64, so narrow matrices -- the reference encoders' 32-channel BN over ~10^6 positions -- keep
+// every lane busy), the 256 threads of a work-group cover R = 256 / TW rows per pass, and the number
+// of row splits S (tr_splits) fills the chip: ~2048 work-groups, at most TR_SMAX partials per column
+// and at most `cap` partial floats (the partial buffers keep their sizes: 64 splits of the widest
+// matrix each one serves, so narrow matrices get proportionally more splits).
+constexpr int TR_SMAX = 512;
+__host__ __device__ inline int tr_tw(int N) { return N < 64 ? 32 : 64; }
+static inline int tr_splits(long M, int N, long cap) {
+  const int tiles = (N + tr_tw(N) - 1) / tr_tw(N);
+  const long rows_min = 64;  // >= 64 rows per split
+  return (int)std::max<long>(1, std::min<long>({(long)TR_SMAX, 2048L / tiles, M / rows_min, cap / N}));
+}
+
+// partial column sums: part[s][n] = sum over rows m = s*R + r, + S*R, ... of in[m*ld + n]
 __global__ __launch_bounds__(256) void k_tr_colsum_part(const float* __restrict__ in, long M, int N, long ld,
                                                         float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + c;
+  __shared__ float red[256];
+  const int TW = tr_tw(N), R = 256 / TW;
+  const int c = threadIdx.x % TW, r = threadIdx.x / TW;
+  const int n = blockIdx.x * TW + c;
   const int S = gridDim.y, s = blockIdx.y;
   float acc = 0.f;
-  if (n < N)
-    for (long m = (long)s * 4 + r; m < M; m += (long)S * 4) acc += in[m * ld + n];
-  red[r][c] = acc;
+  if (n < N) {
+#pragma unroll 4
+    for (long m = (long)s * R + r; m < M; m += (long)S * R) acc += in[m * ld + n];
+  }
+  red[threadIdx.x] = acc;
   __syncthreads();
-  if (r == 0 && n < N) part[(long)s * N + n] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  if (r == 0 && n < N) {
+    float v = 0.f;
+    for (int rr = 0; rr < R; ++rr) v += red[rr * TW + c];
+    part[(long)s * N + n] = v;
+  }
 }
 __global__ void k_tr_colsum_final(const float* __restrict__ part, int S, int N, float* __restrict__ out) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -754,21 +776,27 @@ __global__ void k_tr_adam(float* __restrict__ w, const float* __restrict__ g, fl
 __global__ __launch_bounds__(256) void k_pn_colstat_part(const float* __restrict__ x, long M, int N,
                                                          const float* __restrict__ ctr, int mode,
                                                          float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int cc = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + cc;
+  __shared__ float red[256];
+  const int TW = tr_tw(N), R = 256 / TW;
+  const int cc = threadIdx.x % TW, r = threadIdx.x / TW;
+  const int n = blockIdx.x * TW + cc;
   const int S = gridDim.y, sp = blockIdx.y;
   float acc = 0.f;
   if (n < N) {
     const float c0 = mode ? ctr[n] : 0.f;
-    for (long m = (long)sp * 4 + r; m < M; m += (long)S * 4) {
+#pragma unroll 4
+    for (long m = (long)sp * R + r; m < M; m += (long)S * R) {
       const float v = x[m * N + n] - c0;
       acc += mode ? v * v : v;
     }
   }
-  red[r][cc] = acc;
+  red[threadIdx.x] = acc;
   __syncthreads();
-  if (r == 0 && n < N) part[(long)sp * N + n] = red[0][cc] + red[1][cc] + red[2][cc] + red[3][cc];
+  if (r == 0 && n < N) {
+    float v = 0.f;
+    for (int rr = 0; rr < R; ++rr) v += red[rr * TW + cc];
+    part[(long)sp * N + n] = v;
+  }
 }
 __global__ void k_pn_colstat_final(const float* __restrict__ part, int S, int N, float scale, float* __restrict__ out) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -794,14 +822,16 @@ __global__ __launch_bounds__(256) void k_pn_bn_bwd_part(const float* __restrict_
                                                         const float* __restrict__ a, long M, int C,
                                                         const float* __restrict__ mean, const float* __restrict__ var,
                                                         float eps, float* __restrict__ dy, float* __restrict__ part) {
-  __shared__ float r1[4][64], r2[4][64];
-  const int cc = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cc;
+  __shared__ float r1[256], r2[256];
+  const int TW = tr_tw(C), R = 256 / TW;
+  const int cc = threadIdx.x % TW, r = threadIdx.x / TW;
+  const int c = blockIdx.x * TW + cc;
   const int S = gridDim.y, sp = blockIdx.y;
   float s1 = 0.f, s2 = 0.f;
   if (c < C) {
     const float mu = mean[c], rs = rsqrtf(var[c] + eps);
-    for (long m = (long)sp * 4 + r; m < M; m += (long)S * 4) {
+#pragma unroll 4
+    for (long m = (long)sp * R + r; m < M; m += (long)S * R) {
       const long i = m * C + c;
       float g = dxn[i];
       if (keep) g = g * 2.f * (float)keep[i];
@@ -810,12 +840,17 @@ __global__ __launch_bounds__(256) void k_pn_bn_bwd_part(const float* __restrict_
       s2 += g * (a[i] - mu) * rs;
     }
   }
-  r1[r][cc] = s1;
-  r2[r][cc] = s2;
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
   __syncthreads();
   if (r == 0 && c < C) {
-    part[(long)sp * 2 * C + c] = r1[0][cc] + r1[1][cc] + r1[2][cc] + r1[3][cc];
-    part[(long)sp * 2 * C + C + c] = r2[0][cc] + r2[1][cc] + r2[2][cc] + r2[3][cc];
+    float v1 = 0.f, v2 = 0.f;
+    for (int rr = 0; rr < R; ++rr) {
+      v1 += r1[rr * TW + cc];
+      v2 += r2[rr * TW + cc];
+    }
+    part[(long)sp * 2 * C + c] = v1;
+    part[(long)sp * 2 * C + C + c] = v2;
   }
 }
 // finalize: d beta = S1, d gamma = S2 (written into the gradient slots)
@@ -923,8 +958,9 @@ static void tr_transpose(const float* src, long rows, long cols, long lds, float
 }
 
 static void tr_colsum(tt2_train_ctx* c, const float* in, long M, int N, long ld, float* out, hipStream_t s) {
-  const int S = (int)std::min<long>(64, std::max<long>(1, M / 64));
-  hipLaunchKernelGGL(k_tr_colsum_part, dim3((N + 63) / 64, S), dim3(256), 0, s, in, M, N, ld, c->part.as<float>());
+  const int S = tr_splits(M, N, 64 * std::max<long>(4L * c->H, c->LX1));
+  hipLaunchKernelGGL(k_tr_colsum_part, dim3((N + tr_tw(N) - 1) / tr_tw(N), S), dim3(256), 0, s, in, M, N, ld,
+                     c->part.as<float>());
   hipLaunchKernelGGL(k_tr_colsum_final, dim3((N + 255) / 256), dim3(256), 0, s, c->part.as<float>(), S, N, out);
 }
 
@@ -1166,9 +1202,10 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
   float* part = c->pn_part.as<float>();
   float* sums = part + 64L * 2 * C;
   float* TBUF = c->TBUF.as<float>();
-  const int S = (int)std::min<long>(64, std::max<long>(1, M / 64));
+  const int S = tr_splits(M, C, 64L * C);
+  const unsigned CT = (unsigned)((C + tr_tw(C) - 1) / tr_tw(C));
   auto colstat = [&](const float* x, const float* ctr, int mode, float* out) {
-    hipLaunchKernelGGL(k_pn_colstat_part, dim3((C + 63) / 64, S), dim3(256), 0, s, x, M, C, ctr, mode, part);
+    hipLaunchKernelGGL(k_pn_colstat_part, dim3(CT, S), dim3(256), 0, s, x, M, C, ctr, mode, part);
     hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, out);
   };
   auto conv_in = [&](int i, GemmArgs& g) {  // layer i's input as an implicit-im2col conv1d operand
@@ -1214,7 +1251,7 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
     const std::string sc = pn_scope(i + 1);
     const float* mean = c->BNM.as<float>() + (long)i * C;
     const float* var = c->BNV.as<float>() + (long)i * C;
-    hipLaunchKernelGGL(k_pn_bn_bwd_part, dim3((C + 63) / 64, S), dim3(256), 0, s, dxn,
+    hipLaunchKernelGGL(k_pn_bn_bwd_part, dim3(CT, S), dim3(256), 0, s, dxn,
                        pnm ? pnm + (long)i * M * C : nullptr, c->PA[i].as<float>(), M, C, mean, var, eps,
                        c->DYb.as<float>(), part);
     hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, sums,
@@ -1583,23 +1620,24 @@ static void tr_front_alloc(tt2_train_ctx* c) {
 
 // batch statistics over M rows of [M][C] into mean / var (k_pn_colstat: biased variance)
 static void fe_stats(tt2_train_ctx* c, const float* x, long M, int C, float* mean, float* var, hipStream_t s) {
-  const int S = (int)std::min<long>(64, std::max<long>(1, M / 64));
+  const int S = tr_splits(M, C, 64L * 512);
+  const unsigned CT = (unsigned)((C + tr_tw(C) - 1) / tr_tw(C));
   float* part = c->fpart.as<float>();
-  hipLaunchKernelGGL(k_pn_colstat_part, dim3((C + 63) / 64, S), dim3(256), 0, s, x, M, C, nullptr, 0, part);
+  hipLaunchKernelGGL(k_pn_colstat_part, dim3(CT, S), dim3(256), 0, s, x, M, C, nullptr, 0, part);
   hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, mean);
-  hipLaunchKernelGGL(k_pn_colstat_part, dim3((C + 63) / 64, S), dim3(256), 0, s, x, M, C, mean, 1, part);
+  hipLaunchKernelGGL(k_pn_colstat_part, dim3(CT, S), dim3(256), 0, s, x, M, C, mean, 1, part);
   hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, var);
 }
 // BN backward (batch statistics) from dy -> dz (act: 0 none, 2 relu' from the pre-BN activation)
 static void fe_bn_bwd(tt2_train_ctx* c, const float* dxn, const uint8_t* keep, const float* a, long M, int C,
                       const float* mean, const float* var, const std::string& sc, int act, float* dy, float* dz,
                       hipStream_t s) {
-  const int S = (int)std::min<long>(64, std::max<long>(1, M / 64));
+  const int S = tr_splits(M, C, 64L * 512);
   float* part = c->fpart.as<float>();
   float* sums = part + 64L * 2 * 512;
   const float eps = c->cfg.bn_eps;
-  hipLaunchKernelGGL(k_pn_bn_bwd_part, dim3((C + 63) / 64, S), dim3(256), 0, s, dxn, keep, a, M, C, mean, var, eps, dy,
-                     part);
+  hipLaunchKernelGGL(k_pn_bn_bwd_part, dim3((unsigned)((C + tr_tw(C) - 1) / tr_tw(C)), S), dim3(256), 0, s, dxn, keep,
+                     a, M, C, mean, var, eps, dy, part);
   hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, sums,
                      gvar(c, sc + "batch_normalization/gamma"), gvar(c, sc + "batch_normalization/beta"));
   hipLaunchKernelGGL(k_pn_bn_bwd_dz, dim3(nblk(M * C)), dim3(256), 0, s, dy, a, M, C, mean, var, eps,

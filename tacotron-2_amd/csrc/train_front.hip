@@ -20,13 +20,22 @@ __global__ void k_fe_embed(const int* __restrict__ ids, const float* __restrict_
 // d table[s][e] = Σ over positions with id s (deterministic order, one thread per (s, e))
 __global__ void k_fe_embed_bwd(const int* __restrict__ ids, const float* __restrict__ dx, long M, int E, int NS,
                                float* __restrict__ dtab) {
+  // ids staged 256 at a time in LDS (one coalesced load per chunk instead of a dependent global
+  // load per position); every thread still sums its positions in order m = 0..M-1
+  __shared__ int sid[256];
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)NS * E) return;
-  const int sym = (int)(i / E), e = (int)(i % E);
+  const bool act = i < (long)NS * E;
+  const int sym = act ? (int)(i / E) : -1, e = act ? (int)(i % E) : 0;
   float acc = 0.f;
-  for (long m = 0; m < M; ++m)
-    if (ids[m] == sym) acc += dx[m * E + e];
-  dtab[i] = acc;
+  for (long m0 = 0; m0 < M; m0 += 256) {
+    __syncthreads();
+    sid[threadIdx.x] = m0 + threadIdx.x < M ? ids[m0 + threadIdx.x] : -2;
+    __syncthreads();
+    const int n = (int)std::min<long>(256, M - m0);
+    for (int jj = 0; jj < n; ++jj)
+      if (sid[jj] == sym) acc += dx[(m0 + jj) * E + e];
+  }
+  if (act) dtab[i] = acc;
 }
 void fe_embed(const int* ids, const float* table, long M, int E, float* out, hipStream_t s) {
   hipLaunchKernelGGL(k_fe_embed, dim3(fe_blk(M * E)), dim3(256), 0, s, ids, table, M, E, out);
