@@ -8,5 +8,5 @@ for f in gemm tacotron decode_persist wavenet griffinlim train step wavenet_wide
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-variable -Wno-pass-failed -c $D/csrc/$f.hip -o $D/$f.o &
 done
 wait
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT $D/*.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT $D/*.o -L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib
 rm -rf $D
