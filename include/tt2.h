@@ -409,6 +409,12 @@ typedef struct tt2_train_config {
   int emt_only, num_gst, num_heads, style_embed_depth, style_att_dim, reference_depth;
   int reference_filters[6];
   int max_T_ref;                                           /* reference mel frames (capacity) */
+  /* loss options (tacotron.py:758-767, modules.py:532-575; hparams.py:192-193): mask_decoder = 1
+   * masks the before / after MSE and the stop cross entropy past each row's target length
+   * (tt2_train_set_target_lengths), the stop loss then being TF's weighted cross entropy with
+   * pos_weight (the unmasked stop loss ignores pos_weight, as the reference's does) */
+  int mask_decoder;
+  float pos_weight;
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;
@@ -461,6 +467,18 @@ tt2_status tt2_train_forward_backward_text_dev(tt2_train_ctx* ctx, const int32_t
                                                const uint8_t* enc_conv_masks_d,
                                                const uint8_t* enc_zoneout_masks_d, int T_in, int T_out,
                                                void* stream);
+/* Target lengths [B] (host int32, copied) for cfg.mask_decoder: the next forward_backward calls
+ * mask every loss past t >= lengths[b] (TacoTrainingHelper + MaskedMSE / MaskedSigmoidCrossEntropy,
+ * tacotron.py:56,758-767).  NULL clears them; a masked context without them fails the step like
+ * the reference's RuntimeError (tacotron.py:56-57). */
+tt2_status tt2_train_set_target_lengths(tt2_train_ctx* ctx, const int32_t* lengths);
+/* Teacher-forcing draw of the next forward_backward calls (TacoTrainingHelper.next_inputs,
+ * helpers.py:122-133): feed_target[t] (host u8 [T_out], copied) = 1 feeds the target frame t-1 to
+ * step t, 0 feeds the decoder's own (unclipped) frame t-1, whose gradient then flows back through
+ * the prenet into frame t-1; feed_target[0] is ignored (go frame).  It is the outcome of the
+ * reference's per-step draw u < ratio (ratio: constant or _teacher_forcing_ratio_decay,
+ * helpers.py:140-180), injected like the dropout keep bits.  NULL = every step teacher-forced. */
+tt2_status tt2_train_set_teacher_forcing(tt2_train_ctx* ctx, const uint8_t* feed_target, int T_out);
 /* clip_by_global_norm + Adam with learning rate lr at update count global_step (>= 1). */
 tt2_status tt2_train_apply_dev(tt2_train_ctx* ctx, float lr, int global_step, void* stream);
 /* Synchronise; out5 = {before_loss, stop_loss, reg_loss, grad_global_norm (after apply),

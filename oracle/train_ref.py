@@ -80,10 +80,13 @@ def _conv_same(cum, k, b):
     return cols @ k[:, 0, :] + b                       # [B,T,F]
 
 
-def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneout=0.1):
+def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneout=0.1, feed_target=None):
     """Teacher-forced decoder forward.  W: dict name -> torch tensor (requires_grad as wanted);
     memory [B,T_in,D]; lengths [B]; targets [B,T,80]; prenet_masks [T,2,B,P] keep bits;
-    zoneout_masks [T,4,B,H] keep bits (c1,h1,c2,h2; training zoneout) or None (inference mix).
+    zoneout_masks [T,4,B,H] keep bits (c1,h1,c2,h2; training zoneout) or None (inference mix);
+    feed_target [T] (None = all 1): the outcome of TacoTrainingHelper.next_inputs' per-step draw
+    u < ratio (helpers.py:122-133) -- step t (t >= 1) gets the target frame t-1 when 1, else the
+    decoder's own unclipped frame t-1 (outputs[:, -output_dim:]), through which gradients flow.
     Returns frames [B,T,80], stop logits [B,T], alignments [B,T_in,T]."""
     B, T_in, D = memory.shape
     T = targets.shape[1]
@@ -131,7 +134,10 @@ def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneo
         frames.append(pin @ W[FP + "kernel"] + W[FP + "bias"])
         stops.append((pin @ W[SP + "kernel"] + W[SP + "bias"])[:, 0])
         aligns.append(a)
-        frame_in = targets[:, t]
+        if feed_target is None or t + 1 >= T or feed_target[t + 1]:
+            frame_in = targets[:, t]
+        else:
+            frame_in = frames[-1]
     return torch.stack(frames, 1), torch.stack(stops, 1), torch.stack(aligns, 2)
 
 
@@ -141,12 +147,39 @@ def clip_decoder_output(frames, clip=(-4.1, 4.0)):
     return frames if clip is None else torch.clamp(frames, clip[0], clip[1])
 
 
-def losses(frames, stop_logits, targets, stop_targets, W, reg_weight, clip=(-4.1, 4.0)):
+def masked_mse(targets, outputs, target_lengths):
+    """MaskedMSE (modules.py:532-551): tf.losses.mean_squared_error with weights = the [B,T,1]
+    sequence mask broadcast over the mels, reduced SUM_BY_NONZERO_WEIGHTS."""
+    T = targets.shape[1]
+    w = (torch.arange(T)[None, :] < torch.as_tensor(target_lengths)[:, None]).to(targets.dtype)
+    w = w[:, :, None].expand_as(targets)
+    return (w * (outputs - targets) ** 2).sum() / (w != 0).sum()
+
+
+def masked_stop_loss(stop_targets, logits, target_lengths, pos_weight):
+    """MaskedSigmoidCrossEntropy (modules.py:553-575): TF weighted_cross_entropy_with_logits
+    (1-z)x + (1+(q-1)z)(log1p(exp(-|x|)) + max(-x,0)), masked, summed, divided by the count of
+    nonzero masked losses."""
+    T = logits.shape[1]
+    w = (torch.arange(T)[None, :] < torch.as_tensor(target_lengths)[:, None]).to(logits.dtype)
+    x, z = logits, stop_targets
+    l = 1 + (pos_weight - 1) * z
+    v = w * ((1 - z) * x + l * (torch.log1p(torch.exp(-x.abs())) + torch.clamp(-x, min=0)))
+    return v.sum() / (v != 0).sum()
+
+
+def losses(frames, stop_logits, targets, stop_targets, W, reg_weight, clip=(-4.1, 4.0),
+           target_lengths=None, pos_weight=1.0):
     """before (tf.losses.mean_squared_error on the clipped decoder output), stop (mean sigmoid
-    CE, pos_weight 1), reg."""
-    before = ((clip_decoder_output(frames, clip) - targets) ** 2).mean()
-    x, z = stop_logits, stop_targets
-    stop = (torch.clamp(x, min=0) - x * z + torch.log1p(torch.exp(-x.abs()))).mean()
+    CE: the unmasked path ignores pos_weight, tacotron.py:778-779), reg; target_lengths given =
+    mask_decoder (tacotron.py:758-767)."""
+    if target_lengths is not None:
+        before = masked_mse(targets, clip_decoder_output(frames, clip), target_lengths)
+        stop = masked_stop_loss(stop_targets, stop_logits, target_lengths, pos_weight)
+    else:
+        before = ((clip_decoder_output(frames, clip) - targets) ** 2).mean()
+        x, z = stop_logits, stop_targets
+        stop = (torch.clamp(x, min=0) - x * z + torch.log1p(torch.exp(-x.abs()))).mean()
     reg = sum((v ** 2).sum() / 2 for n, v in W.items() if regularized(n)) * reg_weight
     return before, stop, reg
 
@@ -389,10 +422,11 @@ def train_grads_frontend(Wnp, ids, lengths, ref_emt, ref_spk, targets, stop_targ
 
 def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,
                 reg_weight=1e-6, dtype=torch.float64, clip=(-4.1, 4.0), postnet=False,
-                postnet_masks=None):
+                postnet_masks=None, feed_target=None, target_lengths=None, pos_weight=1.0):
     """One forward + backward; returns (outputs dict, losses tuple, grads dict incl. 'memory').
     postnet=True adds the Postnet and the ``after`` loss (tacotron.py:362-381, 775-776): losses
-    become (before, stop, reg, after) and outputs gain 'mel_outputs' and 'bn_stats'."""
+    become (before, stop, reg, after) and outputs gain 'mel_outputs' and 'bn_stats'.
+    feed_target: teacher-forcing draw (forward); target_lengths: mask_decoder losses."""
     names = train_var_names() + (postnet_var_names() if postnet else [])
     W = {n: torch.tensor(np.asarray(Wnp[n]), dtype=dtype, requires_grad=True) for n in names}
     mem = torch.tensor(np.asarray(memory), dtype=dtype, requires_grad=True)
@@ -400,8 +434,8 @@ def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneo
     st = torch.tensor(np.asarray(stop_targets), dtype=dtype)
     pm = torch.tensor(np.asarray(prenet_masks), dtype=dtype)
     zm = None if zoneout_masks is None else torch.tensor(np.asarray(zoneout_masks), dtype=dtype)
-    fr, sl, al = forward(W, mem, lengths, tg, pm, zm)
-    b, s, r = losses(fr, sl, tg, st, W, reg_weight, clip)
+    fr, sl, al = forward(W, mem, lengths, tg, pm, zm, feed_target=feed_target)
+    b, s, r = losses(fr, sl, tg, st, W, reg_weight, clip, target_lengths, pos_weight)
     total = b + s + r
     out = dict(frames=clip_decoder_output(fr, clip).detach().numpy(), stop_logits=sl.detach().numpy(),
                alignments=al.detach().numpy())
@@ -410,7 +444,7 @@ def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneo
         pmk = None if postnet_masks is None else torch.tensor(np.asarray(postnet_masks), dtype=dtype)
         proj, stats = postnet_train(W, dec, pmk)
         mel = clip_decoder_output(dec + proj, clip)                      # tacotron.py:375-378
-        after = ((mel - tg) ** 2).mean()
+        after = ((mel - tg) ** 2).mean() if target_lengths is None else masked_mse(tg, mel, target_lengths)
         total = total + after
         out["mel_outputs"] = mel.detach().numpy()
         out["bn_stats"] = [(m.detach().numpy(), v.detach().numpy()) for m, v in stats]
@@ -425,6 +459,19 @@ def bn_moving_update(moving, batch, momentum=0.99):
     """tf.layers.batch_normalization UPDATE_OPS (run with the optimizer, tacotron.py:1088-1090):
     moving -= (moving - batch)·(1 - momentum)."""
     return moving - (moving - batch) * (1 - momentum)
+
+
+def teacher_forcing_ratio(global_step, hp):
+    """TacoTrainingHelper's ratio (helpers.py:65,113-118,140-180): constant mode ->
+    tacotron_teacher_forcing_ratio; scheduled -> init before start_decay, else
+    exponential_decay(init, gs - start_decay, decay_steps, decay_exp_rate) (not staircase)."""
+    if hp.tacotron_teacher_forcing_mode != "scheduled":
+        return float(hp.tacotron_teacher_forcing_ratio)
+    init = hp.tacotron_teacher_forcing_init_ratio
+    if global_step < hp.tacotron_teacher_forcing_start_decay:
+        return float(init)
+    return float(init * hp.tacotron_teacher_forcing_decay_exp_rate ** (
+        (global_step - hp.tacotron_teacher_forcing_start_decay) / hp.tacotron_teacher_forcing_decay_steps))
 
 
 def learning_rate(step, hp):

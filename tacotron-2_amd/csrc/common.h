@@ -37,10 +37,27 @@ void set_last_error(const std::string& msg);
     if (!(cond)) throw ::tt2::Error(status, msg);                                          \
   } while (0)
 
+std::string redzone_check_all(const char* phase);  // TT2_REDZONE: every live buffer, unnamed
+
+// Redzones (TT2_REDZONE=1, debug only): every DevBuf gets kRedzone extra bytes past its end filled
+// with kRedByte; redzone_check() (called by the training entry points between phases) reports the
+// first buffer whose redzone a kernel wrote -- the buffer that overflowed, whatever the address
+// layout of the process puts behind it.
+inline bool redzone_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("TT2_REDZONE");
+    return e && e[0] && e[0] != '0';
+  }();
+  return on;
+}
 template <class F>
 tt2_status guard(F&& f) {
   try {
     f();
+    if (redzone_on()) {  // debug: every ABI call leaves every live buffer's redzone intact
+      const std::string r = redzone_check_all("ABI call");
+      if (!r.empty()) throw Error(TT2_ERR_HIP, "redzone violation: " + r);
+    }
     return TT2_OK;
   } catch (const Error& e) {
     set_last_error(e.what());
@@ -50,6 +67,29 @@ tt2_status guard(F&& f) {
     return TT2_ERR_INVALID_ARG;
   }
 }
+
+// Debug fill of fresh allocations (TT2_POISON_ALLOC=1): every DevBuf starts as 0xFF bytes (fp32
+// NaN, int -1, u8 255), so a kernel that reads a buffer before the call writes it shows up as a
+// NaN / wrong value deterministically instead of depending on what an earlier allocation left.
+// TT2_POISON_ALLOC=<byte> picks another fill (e.g. 66 = 0x42424242 = 48.6f, finite, so a stale read
+// that a max / compare would swallow as NaN still changes the result).
+inline int poison_alloc() {
+  static const int fill = [] {
+    const char* e = std::getenv("TT2_POISON_ALLOC");
+    if (!e || !e[0] || (e[0] == '0' && !e[1])) return -1;
+    const long v = std::strtol(e, nullptr, 0);
+    return v == 1 ? 0xFF : (int)(v & 0xFF);
+  }();
+  return fill;
+}
+
+constexpr size_t kRedzone = 1 << 16;
+constexpr unsigned char kRedByte = 0xA5;
+struct DevBuf;
+// "" = every registered redzone intact (defined in tacotron.hip); namer (may be null) names a buffer
+std::string redzone_check(const char* phase, std::string (*namer)(const void* owner, const DevBuf* b),
+                          const void* owner);
+void redzone_register(DevBuf* b, bool add);
 
 // Device buffer owned by a context.
 struct DevBuf {
@@ -62,11 +102,21 @@ struct DevBuf {
   void alloc(size_t n) {
     if (n == bytes && p) return;
     free();
-    if (n) TT2_HIP(hipMalloc(&p, n));
-    bytes = n;
+    if (n) {
+      const bool rz = redzone_on();
+      TT2_HIP(hipMalloc(&p, n + (rz ? kRedzone : 0)));
+      if (poison_alloc() >= 0) TT2_HIP(hipMemset(p, poison_alloc(), n));
+      if (rz) TT2_HIP(hipMemset(static_cast<char*>(p) + n, kRedByte, kRedzone));
+      if (rz || poison_alloc() >= 0) TT2_HIP(hipDeviceSynchronize());
+      bytes = n;
+      if (rz) redzone_register(this, true);
+    }
   }
   void free() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      if (redzone_on()) redzone_register(this, false);
+      (void)hipFree(p);
+    }
     p = nullptr;
     bytes = 0;
   }

@@ -12,6 +12,11 @@
 #include <memory>
 #include <tuple>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+#include <mutex>
+#include <set>
 #include "common.h"
 #include "decode_persist.h"
 #include "gemm.h"
@@ -23,6 +28,66 @@ namespace tt2 {
 
 static thread_local std::string g_last_error;
 void set_last_error(const std::string& m) { g_last_error = m; }
+
+// TT2_SEGV_TRACE=1 (debug): a SIGSEGV / SIGABRT prints the native backtrace to stderr before the
+// default action (the rocprofv3 exit crash of round 2 left only "Segmentation fault")
+static void tt2_fatal_signal(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char* m = sig == SIGSEGV ? "libtt2: SIGSEGV, native backtrace:\n" : "libtt2: fatal signal, native backtrace:\n";
+  (void)!write(2, m, strlen(m));
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+static const bool g_segv_trace = [] {
+  const char* e = std::getenv("TT2_SEGV_TRACE");
+  if (!e || !e[0] || e[0] == '0') return false;
+  signal(SIGSEGV, tt2_fatal_signal);
+  signal(SIGABRT, tt2_fatal_signal);
+  return true;
+}();
+
+// TT2_REDZONE debug registry (common.h): every live DevBuf with a redzone
+static std::mutex& rz_mu() {
+  static std::mutex m;
+  return m;
+}
+static std::set<DevBuf*>& rz_set() {
+  static std::set<DevBuf*> s;
+  return s;
+}
+void redzone_register(DevBuf* b, bool add) {
+  std::lock_guard<std::mutex> l(rz_mu());
+  if (add) rz_set().insert(b);
+  else rz_set().erase(b);
+}
+std::string redzone_check_all(const char* phase) { return redzone_check(phase, nullptr, nullptr); }
+std::string redzone_check(const char* phase, std::string (*namer)(const void*, const DevBuf*), const void* owner) {
+  if (!redzone_on()) return "";
+  TT2_HIP(hipDeviceSynchronize());
+  std::lock_guard<std::mutex> l(rz_mu());
+  std::vector<unsigned char> h(kRedzone);
+  std::string out;
+  for (DevBuf* b : rz_set()) {
+    TT2_HIP(hipMemcpy(h.data(), static_cast<char*>(b->p) + b->bytes, kRedzone, hipMemcpyDeviceToHost));
+    size_t first = kRedzone, last = 0;
+    for (size_t i = 0; i < kRedzone; ++i)
+      if (h[i] != kRedByte) {
+        first = std::min(first, i);
+        last = i;
+      }
+    if (first == kRedzone) continue;
+    // re-arm, so a later call reports its own overflows rather than this one again
+    TT2_HIP(hipMemset(static_cast<char*>(b->p) + b->bytes, kRedByte, kRedzone));
+    TT2_HIP(hipDeviceSynchronize());
+    std::string name = namer ? namer(owner, b) : std::string();
+    if (name.empty()) name = "?";
+    out += std::string("[") + phase + "] redzone of " + name + " (" + std::to_string(b->bytes) +
+           " bytes) written at +" + std::to_string(first) + "..+" + std::to_string(last) + "; ";
+  }
+  return out;
+}
 
 void put_tensor(WeightMap& wm, const char* name, const float* host, const int64_t* shape, int ndim) {
   TT2_CHECK(name && host && ndim >= 0 && (ndim == 0 || shape), TT2_ERR_INVALID_ARG,
@@ -1665,7 +1730,7 @@ static void alloc_acts(tt2_ctx* c) {
   c->cum.alloc(B * T * 4);
   c->max_att.alloc(64 * 4);
   c->PP.alloc((long)c->KSP * 32 * c->NPF * 4);
-  c->ctl.alloc(std::max<size_t>(sizeof(DecCtl), 65536));  // >= 64 KiB: see train.hip on 256-byte allocations
+  c->ctl.alloc(sizeof(DecCtl));
   c->frames.alloc(B * MI * c->nm * 4);
   c->stop.alloc(B * MI * 4);
   c->align.alloc(B * T * MI * 4);

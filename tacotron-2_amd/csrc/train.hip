@@ -90,6 +90,15 @@ struct tt2_train_ctx {
   DevBuf fRA[2][6], fRY[2][6], fXG[2], fGR[2], fGU[2], fGCC[2], fGRH[2], fHG[2], fREF[2], fGG, fGC, fFBUF, fDY, fDY2,
       fDZc;
   DevBuf fGq, fGkk, fGv, fGnv, fGbb, fGsum, fdREF, fDZD, fDH, fDHA, fDRH, fDCP, fDGP, fDXG, fWT, fBN, fpart;
+  // loss masks (cfg.mask_decoder): target lengths [B] on the device, their sum
+  DevBuf TLEN;
+  bool has_tlen = false;
+  long tlen_sum = 0;
+  int tlen_max = 0;
+  // teacher-forcing draw (tt2_train_set_teacher_forcing): feed[t] = 1 target frame t-1, 0 own frame
+  std::vector<uint8_t> feed;
+  // free-running steps: prenet-1 kernel transposed [P][NM], per-step scratch
+  DevBuf W1T, sDZ, sDP, sDX;
 };
 
 namespace tt2 {
@@ -436,15 +445,21 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
 
 // frame MSE + stop sigmoid CE (tacotron.py:774,778-779) and their output gradients.  Frames are
 // time-major [T][B][NM]; targets [B][T][NM].  Deterministic per-block partials.
+// tlen (mask_decoder, tacotron.py:758-767): MaskedMSE = Σ w·d² / (NM·Σ lengths) (the count of nonzero
+// weights, tf.losses SUM_BY_NONZERO_WEIGHTS), MaskedSigmoidCrossEntropy = Σ w·wce / count_nonzero(w·wce)
+// with TF's weighted_cross_entropy_with_logits (pos_weight q): (1-z)x + (1+(q-1)z)·softplus(-x)
+// (modules.py:532-575).  The masked stop gradient is left unnormalised (the count is only known after
+// the reduction; k_tr_loss_final / k_tr_div finish it).  inv_f = 1 / (MSE normaliser).
 __global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const float* __restrict__ ST,
                                                  const float* __restrict__ tg, const float* __restrict__ stg, int B,
                                                  int T, int NM, int clip, float lo, float hi, float* __restrict__ dFR,
                                                  float* __restrict__ dST, float* __restrict__ part,
-                                                 uint8_t* __restrict__ clipm) {
+                                                 uint8_t* __restrict__ clipm, const int* __restrict__ tlen, float inv_f,
+                                                 float pos_weight) {
   __shared__ float s4[16];
   const long nf = (long)T * B * NM;
-  const float inv_f = 1.0f / (float)nf, inv_s = 1.0f / (float)((long)T * B);
-  float sq = 0.f, ce = 0.f;
+  const float inv_s = 1.0f / (float)((long)T * B);
+  float sq = 0.f, ce = 0.f, nz = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % NM);
     const int b = (int)((i / NM) % B);
@@ -453,7 +468,8 @@ __global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const f
     // gradient passes where lo <= x <= hi (TF maximum/minimum)
     const float x = FR[i];
     const float y = clip ? fminf(fmaxf(x, lo), hi) : x;
-    const float d = y - tg[((long)b * T + t) * NM + c];
+    const float w = (!tlen || t < tlen[b]) ? 1.f : 0.f;
+    const float d = (y - tg[((long)b * T + t) * NM + c]) * w;
     sq += d * d;
     const bool pass = !clip || (x >= lo && x <= hi);
     dFR[i] = pass ? 2.f * d * inv_f : 0.f;
@@ -463,25 +479,45 @@ __global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const f
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < (long)T * B; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i % B), t = (int)(i / B);
     const float x = ST[i], z = stg[(long)b * T + t];
-    ce += fmaxf(x, 0.f) - x * z + log1pf(expf(-fabsf(x)));
-    dST[i] = (sigm_acc(x) - z) * inv_s;
+    if (!tlen) {
+      ce += fmaxf(x, 0.f) - x * z + log1pf(expf(-fabsf(x)));
+      dST[i] = (sigm_acc(x) - z) * inv_s;
+    } else {
+      const float w = t < tlen[b] ? 1.f : 0.f;
+      const float l = 1.f + (pos_weight - 1.f) * z;
+      const float v = w * ((1.f - z) * x + l * (log1pf(expf(-fabsf(x))) + fmaxf(-x, 0.f)));
+      ce += v;
+      nz += v != 0.f ? 1.f : 0.f;
+      dST[i] = w * ((1.f - z) - l * sigm_acc(-x));  // / count, by k_tr_div
+    }
   }
   sq = block_sum(sq, s4);
   ce = block_sum(ce, s4);
+  nz = block_sum(nz, s4);
   if (threadIdx.x == 0) {
-    part[blockIdx.x * 2] = sq;
-    part[blockIdx.x * 2 + 1] = ce;
+    part[blockIdx.x * 3] = sq;
+    part[blockIdx.x * 3 + 1] = ce;
+    part[blockIdx.x * 3 + 2] = nz;
   }
 }
+// out[0] = before loss, out[1] = stop loss; masked (ns = 0): the stop normaliser is the count of
+// nonzero masked losses, also stored in out[5] for k_tr_div
 __global__ void k_tr_loss_final(const float* __restrict__ part, int nb, long nf, long ns, float* __restrict__ out) {
   if (threadIdx.x != 0) return;
-  double sq = 0, ce = 0;
+  double sq = 0, ce = 0, nz = 0;
   for (int i = 0; i < nb; ++i) {
-    sq += part[2 * i];
-    ce += part[2 * i + 1];
+    sq += part[3 * i];
+    ce += part[3 * i + 1];
+    nz += part[3 * i + 2];
   }
   out[0] = (float)(sq / (double)nf);
-  out[1] = (float)(ce / (double)ns);
+  const double cnt = ns > 0 ? (double)ns : nz;
+  out[1] = (float)(ce / cnt);
+  out[5] = (float)cnt;
+}
+__global__ void k_tr_div(float* __restrict__ x, long n, const float* __restrict__ by) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] /= by[0];
 }
 
 // ---- backward ------------------------------------------------------------------------------
@@ -909,13 +945,14 @@ __global__ void k_pn_flip(const float* __restrict__ w, int kw, int cin, int cout
   wf[i] = w[((long)(kw - 1 - tp) * cin + ci) * cout + co];
 }
 // after loss: mel = clip(dec[t][b] + proj[b][t]) (tacotron.py:375-378); MSE partials; d proj
+// inv = 1 / (MSE normaliser); tlen masks t >= lengths[b] (mask_decoder, MaskedMSE)
 __global__ __launch_bounds__(256) void k_pn_after_loss(const float* __restrict__ FR, const float* __restrict__ prj,
                                                        const float* __restrict__ tg, int B, int T, int NM, int clip,
                                                        float lo, float hi, float* __restrict__ dprj,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, const int* __restrict__ tlen,
+                                                       float inv) {
   __shared__ float s16[16];
   const long n = (long)B * T * NM;
-  const float inv = 1.0f / (float)n;
   float sq = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % NM);
@@ -923,7 +960,7 @@ __global__ __launch_bounds__(256) void k_pn_after_loss(const float* __restrict__
     const int t = (int)(bt % T), b = (int)(bt / T);
     const float x = FR[((long)t * B + b) * NM + c] + prj[i];
     const float y = clip ? fminf(fmaxf(x, lo), hi) : x;
-    const float d = y - tg[i];
+    const float d = (!tlen || t < tlen[b]) ? y - tg[i] : 0.f;
     sq += d * d;
     dprj[i] = (!clip || (x >= lo && x <= hi)) ? 2.f * d * inv : 0.f;
   }
@@ -978,7 +1015,7 @@ __global__ void k_tr_to_bf16(const float* __restrict__ src, long rows, long cols
   const long n = rows * cols;
   for (long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (long)gridDim.x * blockDim.x * 4) {
     const long r = i / cols, cc = i % cols;
-    if (cc + 3 < cols && (ld & 3) == 0) {
+    if (cc + 3 < cols && ((r * ld + cc) & 3) == 0) {  // 16-byte aligned source quad
       const f32x4 v = *reinterpret_cast<const f32x4*>(src + r * ld + cc);
       bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
       *reinterpret_cast<bf16x4*>(dst + i) = o;
@@ -1005,6 +1042,8 @@ static bool tr_gemm_blas(int M, int N, int K, const float* A, long lda, const fl
     TT2_CHECK(rocblas_create_handle(&c->blas) == rocblas_status_success, TT2_ERR_HIP, "rocblas_create_handle failed");
   }
   const size_t na = (size_t)M * K, nb = (size_t)K * N;
+  // sized at create for the decoder / Postnet weight gradients (tr_alloc); a larger front-end
+  // product grows them once (the hipFree of the old buffer synchronises the device)
   if (c->blasA.bytes < na * 2) c->blasA.alloc(na * 2);
   if (c->blasB.bytes < nb * 2) c->blasB.alloc(nb * 2);
   __bf16* a16 = reinterpret_cast<__bf16*>(c->blasA.p);
@@ -1080,6 +1119,44 @@ static std::string vn(const char* s) { return std::string(TP) + s; }
 #define FPV(x) vn("decoder/linear_transform_projection/projection_linear_transform_projection/" x)
 #define SPV(x) vn("decoder/stop_token_projection/projection_stop_token_projection/" x)
 #define PRV(i, x) vn((std::string("decoder/decoder_prenet/dense_") + std::to_string(i) + "/" x).c_str())
+
+// TT2_REDZONE: name of one of the context's buffers (redzone reports)
+static std::string tr_bufname(const void* owner, const DevBuf* b) {
+  const tt2_train_ctx* c = static_cast<const tt2_train_ctx*>(owner);
+#define TT2_NM(x) if (b == &c->x) return #x;
+#define TT2_NMA(x, n) for (int i_ = 0; i_ < (n); ++i_) if (b == &c->x[i_]) return std::string(#x "[") + std::to_string(i_) + "]";
+  TT2_NM(params) TT2_NM(grads_own) TT2_NM(adam_m) TT2_NM(adam_v) TT2_NM(K1T) TT2_NM(K2T) TT2_NM(WqT) TT2_NM(WfT)
+  TT2_NM(WsT) TT2_NM(WmT) TT2_NM(Wp2T) TT2_NM(values) TT2_NM(keys) TT2_NM(X1) TT2_NM(X2) TT2_NM(PIN) TT2_NM(G1)
+  TT2_NM(G2) TT2_NM(C1) TT2_NM(C2) TT2_NM(CN1) TT2_NM(CN2) TT2_NM(Q) TT2_NM(ALIGN) TT2_NM(CUM) TT2_NM(P1)
+  TT2_NM(XIN) TT2_NM(FR) TT2_NM(ST) TT2_NM(dFR) TT2_NM(dST) TT2_NM(dPIN) TT2_NM(dX1) TT2_NM(dX2) TT2_NM(dG1)
+  TT2_NM(dG2) TT2_NM(DC1) TT2_NM(DC2) TT2_NM(R1) TT2_NM(R2) TT2_NM(DQ) TT2_NM(DCTX) TT2_NM(DKEYS) TT2_NM(DCUM)
+  TT2_NM(dV) TT2_NM(dBA) TT2_NM(dKC) TT2_NM(dBC) TT2_NM(DVAL) TT2_NM(DMEM) TT2_NM(dZ) TT2_NM(dPre) TT2_NM(TBUF)
+  TT2_NM(part) TT2_NM(red) TT2_NM(kpart) TT2_NM(TH) TT2_NM(E) TT2_NM(DF) TT2_NM(PQ) TT2_NM(FALL) TT2_NM(ALN)
+  TT2_NM(blasA) TT2_NM(blasB) TT2_NM(hK1) TT2_NM(hK1T) TT2_NM(hK2) TT2_NM(hK2T) TT2_NM(hWq) TT2_NM(hWqT)
+  TT2_NMA(PA, 8) TT2_NMA(PX, 9) TT2_NM(BNM) TT2_NM(BNV) TT2_NM(PPRJ) TT2_NM(dPP) TT2_NM(DYb) TT2_NM(DZb)
+  TT2_NM(dPXa) TT2_NM(dPXb) TT2_NM(WFLIP) TT2_NM(PWT) TT2_NM(CLIPM) TT2_NM(pn_part) TT2_NM(fEX) TT2_NMA(fEA, 8)
+  TT2_NMA(fEY, 9) TT2_NM(fXP) TT2_NM(fGZ) TT2_NM(fGA) TT2_NM(fCN) TT2_NM(fCS) TT2_NM(fHS) TT2_NM(fENC)
+  TT2_NM(fMEM) TT2_NM(fSTY) TT2_NM(fDSTY) TT2_NM(fDZ) TT2_NM(fDHC) TT2_NM(fDCC) TT2_NM(fDHP) TT2_NM(fdXP)
+  TT2_NM(fdA) TT2_NM(fdB) TT2_NM(fLWxT) TT2_NM(fLWhT) TT2_NMA(fXG, 2) TT2_NMA(fGR, 2) TT2_NMA(fGU, 2)
+  TT2_NMA(fGCC, 2) TT2_NMA(fGRH, 2) TT2_NMA(fHG, 2) TT2_NMA(fREF, 2) TT2_NM(fGG) TT2_NM(fGC) TT2_NM(fFBUF)
+  TT2_NM(fDY) TT2_NM(fDY2) TT2_NM(fDZc) TT2_NM(fGq) TT2_NM(fGkk) TT2_NM(fGv) TT2_NM(fGnv) TT2_NM(fGbb)
+  TT2_NM(fGsum) TT2_NM(fdREF) TT2_NM(fDZD) TT2_NM(fDH) TT2_NM(fDHA) TT2_NM(fDRH) TT2_NM(fDCP) TT2_NM(fDGP)
+  TT2_NM(fDXG) TT2_NM(fWT) TT2_NM(fBN) TT2_NM(fpart)
+  for (int r = 0; r < 2; ++r)
+    for (int i = 0; i < 6; ++i) {
+      if (b == &c->fRA[r][i]) return "fRA[" + std::to_string(r) + "][" + std::to_string(i) + "]";
+      if (b == &c->fRY[r][i]) return "fRY[" + std::to_string(r) + "][" + std::to_string(i) + "]";
+    }
+#undef TT2_NM
+#undef TT2_NMA
+  return "";
+}
+// TT2_REDZONE: fail the call naming every buffer a kernel of this phase wrote past
+static void tr_redzones(tt2_train_ctx* c, const char* phase) {
+  if (!redzone_on()) return;
+  const std::string r = redzone_check(phase, tr_bufname, c);
+  TT2_CHECK(r.empty(), TT2_ERR_HIP, "redzone violation: " + r);
+}
 
 static void tr_front_build_vars(tt2_train_ctx* c,
                                 const std::function<void(const std::string&, std::vector<int64_t>, bool)>& add);
@@ -1164,18 +1241,22 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F); f(c->FALL, TB * Tin * F); f(c->ALN, TB * Tin);
   f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
   f(c->dZ, TB * P); f(c->dPre, TB * P);
+  f(c->W1T, P * NM); f(c->sDZ, B * P); f(c->sDP, B * P); f(c->sDX, B * NM); c->TLEN.alloc(sizeof(int) * (size_t)B);
   const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM, TB * Tin * F,
-                              c->cfg.postnet ? TB * (long)c->PK * c->PC : 0L});
+                              // Postnet im2col^T: K·cin rows per position, cin = num_mels for layer 1
+                              c->cfg.postnet ? TB * (long)c->PK * std::max<long>(c->PC, NM) : 0L});
   f(c->TBUF, tmax);
   f(c->part, 64 * std::max<long>(4 * H, LX1) + 4096);
-  // loss / norm slots in a 64 KiB allocation: with a 256-byte hipMalloc, in a process that had
-  // run the end-to-end tests first, the kernels' writes to it never showed up in read-backs
-  // (observed on ROCm 7.2 / MI355X; gradients in large buffers were correct) -- cause not found
-  f(c->red, 16384);
+  f(c->red, 64);  // loss / norm slots
   if (c->cfg.precision) {
     auto h = [](DevBuf& d, long n) { d.alloc(2 * (size_t)std::max<long>(n, 1)); };
     h(c->hK1, LX1 * 4 * H); h(c->hK1T, LX1 * 4 * H); h(c->hK2, 8 * H * H); h(c->hK2T, 8 * H * H);
     h(c->hWq, H * A); h(c->hWqT, H * A);
+    // bf16 operand copies of the library GEMMs (tr_gemm_blas): the largest weight gradients over all
+    // T·B rows -- LSTM-1 [LX1 x TB]·[TB x 4H], the Postnet convs [K·cin x TB]·[TB x PC]
+    const long pcin = c->cfg.postnet ? (long)c->PK * std::max<long>(c->PC, NM) : 0L;
+    h(c->blasA, TB * std::max({LX1, 2 * H, pcin}));
+    h(c->blasB, TB * std::max<long>(4 * H, c->cfg.postnet ? c->PC : 0));
   }
   f(c->kpart, 4L << 20);
   if (c->cfg.frontend) tr_front_alloc(c);
@@ -1186,7 +1267,8 @@ static void tr_alloc(tt2_train_ctx* c) {
     f(c->BNM, c->PL * PC); f(c->BNV, c->PL * PC); f(c->PPRJ, TB * NM); f(c->dPP, TB * NM);
     // layer inputs' gradients: PC channels, num_mels for the first layer (may exceed PC)
     f(c->DYb, TB * PC); f(c->DZb, TB * PC); f(c->dPXa, TB * std::max(PC, NM)); f(c->dPXb, TB * std::max(PC, NM));
-    f(c->WFLIP, PK * PC * PC); f(c->PWT, NM * PC); f(c->pn_part, 64 * 2 * PC + 1024);
+    f(c->WFLIP, PK * std::max(PC, NM) * PC);  // flipped kernels: layer 1's are [PK][num_mels][PC]
+    f(c->PWT, NM * PC); f(c->pn_part, 64 * 2 * PC + 1024);
     c->CLIPM.alloc((size_t)TB * NM);
   }
 }
@@ -1235,9 +1317,12 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
   const std::string pp = vn("postnet_projection/projection_postnet_projection/");
   tr_gemm((int)M, NM, C, c->PX[L].as<float>(), C, pvar(c, pp + "kernel"), NM, c->PPRJ.as<float>(), NM, s,
           pvar(c, pp + "bias"));
+  const int* tlen = c->cfg.mask_decoder ? c->TLEN.as<int>() : nullptr;
+  const double nmse = c->cfg.mask_decoder ? (double)c->tlen_sum * NM : (double)M * NM;
   hipLaunchKernelGGL(k_pn_after_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->PPRJ.as<float>(), tg, B, T,
-                     NM, c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dPP.as<float>(), c->part.as<float>());
-  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, 1.0f / (float)(M * NM),
+                     NM, c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dPP.as<float>(), c->part.as<float>(),
+                     tlen, (float)(1.0 / nmse));
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, (float)(1.0 / nmse),
                      red + 4, 0);
   // backward: projection
   tr_transpose(c->PX[L].as<float>(), M, C, C, TBUF, M, s);
@@ -1282,6 +1367,16 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
   c->pn_ran = true;
 }
 
+// any step of the next T fed its own previous frame (tt2_train_set_teacher_forcing)
+static bool tr_has_free_steps(const tt2_train_ctx* c, int T) {
+  if (c->feed.empty()) return false;
+  TT2_CHECK((int)c->feed.size() >= T, TT2_ERR_SHAPE_MISMATCH,
+            "teacher-forcing draw shorter than T_out (tt2_train_set_teacher_forcing)");
+  for (int t = 1; t < T; ++t)
+    if (!c->feed[t]) return true;
+  return false;
+}
+
 // forward + losses + backward for one batch; grads complete (incl. L2) on return (stream order)
 static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* lens, const float* tg, const float* stg,
                                 const uint8_t* pm, const uint8_t* zm, const uint8_t* pnm, int Tin, int T,
@@ -1289,6 +1384,13 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   const int B = c->B, D = c->D, H = c->H, P = c->P, A = c->A, F = c->F, KW = c->KW, NM = c->NM, LX1 = c->LX1;
   const long TB = (long)T * B;
   const float z = c->cfg.zoneout;
+  // tacotron.py:56-57 (the reference raises RuntimeError) and the MaskedMSE shape assert
+  // (modules.py:549-550: mask length = max(lengths) must equal T_out)
+  TT2_CHECK(!c->cfg.mask_decoder || c->has_tlen, TT2_ERR_STATE,
+            "Model set to mask paddings but no targets lengths provided for the mask! "
+            "(tt2_train_set_target_lengths)");
+  TT2_CHECK(!c->cfg.mask_decoder || c->tlen_max == T, TT2_ERR_SHAPE_MISMATCH,
+            "mask_decoder: max(target lengths) must equal T_out");
   c->T_last = T;
   c->Tin_last = Tin;
   g_tr_kpart = &c->kpart;
@@ -1357,8 +1459,27 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   const dim3 att_grid(NT, B);
   const unsigned bh = nblk((long)B * H);
 
+  // teacher-forcing draw (TacoTrainingHelper.next_inputs, helpers.py:122-133): a step fed its own
+  // previous frame re-runs the prenet for its B rows from that frame (unclipped frame projection,
+  // Architecture_wrappers.py:258-263); XIN / P1 / X1 then hold what the step actually consumed
+  const bool free_run = tr_has_free_steps(c, T);
+  if (free_run) tr_transpose(pvar(c, PRV(1, "kernel")), NM, P, P, c->W1T.as<float>(), NM, s);
   for (int t = 0; t < T; ++t) {
     const long s1 = (long)t * B;
+    if (free_run && t > 0 && !c->feed[t]) {
+      float* xin = c->XIN.as<float>() + s1 * NM;
+      float* p1 = c->P1.as<float>() + s1 * P;
+      tr_gemm(B, NM, H + D, PIN + (s1 - B) * (H + D), H + D, pvar(c, FPV("kernel")), NM, xin, NM, s,
+              pvar(c, FPV("bias")));
+      tr_gemm(B, P, NM, xin, NM, pvar(c, PRV(1, "kernel")), P, p1, P, s, pvar(c, PRV(1, "bias")), nullptr, 0,
+              ACT_RELU);
+      hipLaunchKernelGGL(k_tr_prenet_mask, dim3(nblk((long)B * P)), dim3(256), 0, s, p1, (long)P,
+                         pm + (long)t * 2 * B * P, 0, 1, B, P);
+      tr_gemm(B, P, P, p1, P, pvar(c, PRV(2, "kernel")), P, X1 + s1 * LX1, LX1, s, pvar(c, PRV(2, "bias")), nullptr,
+              0, ACT_RELU);
+      hipLaunchKernelGGL(k_tr_prenet_mask, dim3(nblk((long)B * P)), dim3(256), 0, s, X1 + s1 * LX1, (long)LX1,
+                         pm + (long)t * 2 * B * P, 1, 1, B, P);
+    }
     // LSTM-1: raw split-K product, combine + bias + cell + zoneout fused in k_tr_lstm_fwd
     const int k1 = tr_gemm_raw(B, 4 * H, LX1, X1 + s1 * LX1, LX1, pvar(c, L1V("kernel")), 4 * H, s, &c->hK1T, LX1);
     TrLstmFwd l1{};
@@ -1386,10 +1507,14 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
   tr_gemm((int)TB, 1, H + D, PIN, H + D, pvar(c, SPV("kernel")), 1, c->ST.as<float>(), 1, s, pvar(c, SPV("bias")));
   float* red = c->red.as<float>();
+  const int* tlen = c->cfg.mask_decoder ? c->TLEN.as<int>() : nullptr;
+  const long nmse = c->cfg.mask_decoder ? c->tlen_sum * NM : TB * NM;
   hipLaunchKernelGGL(k_tr_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->ST.as<float>(), tg, stg, B, T, NM,
                      c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dFR.as<float>(), c->dST.as<float>(),
-                     c->part.as<float>(), c->cfg.postnet ? c->CLIPM.as<uint8_t>() : nullptr);
-  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, TB * NM, TB, red);
+                     c->part.as<float>(), c->cfg.postnet ? c->CLIPM.as<uint8_t>() : nullptr, tlen,
+                     (float)(1.0 / (double)nmse), c->cfg.pos_weight);
+  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, nmse, tlen ? 0L : TB, red);
+  if (tlen) hipLaunchKernelGGL(k_tr_div, dim3(nblk(TB)), dim3(256), 0, s, c->dST.as<float>(), TB, red + 5);
   c->pn_ran = false;
   if (c->cfg.postnet) tr_postnet(c, tg, pnm, T, s);
 
@@ -1431,6 +1556,24 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b1);
     tr_gemm(B, LX1, 4 * H, c->dG1.as<float>() + s1 * 4 * H, 4 * H, c->K1T.as<float>(), LX1, dX1 + s1 * LX1, LX1, s,
             nullptr, c->R1.as<float>(), LX1, ACT_NONE, &c->hK1, 4 * H);
+    if (free_run && t > 0 && !c->feed[t]) {
+      // step t consumed frame t-1: d prenet input -> d frame t-1 (dFR, for the projection weight
+      // gradients after the loop) and through the frame projection into d [h2 | ctx] of step t-1
+      // (dPIN, consumed by the next iteration)
+      float* dz = c->sDZ.as<float>();
+      float* dp = c->sDP.as<float>();
+      float* dx = c->sDX.as<float>();
+      hipLaunchKernelGGL(k_tr_prenet_bwd, dim3(nblk((long)B * P)), dim3(256), 0, s, dX1 + s1 * LX1, (long)LX1,
+                         X1 + s1 * LX1, (long)LX1, (long)B, P, dz);
+      tr_gemm(B, P, P, dz, P, c->Wp2T.as<float>(), P, dp, P, s);
+      hipLaunchKernelGGL(k_tr_prenet_bwd, dim3(nblk((long)B * P)), dim3(256), 0, s, dp, (long)P,
+                         c->P1.as<float>() + s1 * P, (long)P, (long)B, P, dz);
+      tr_gemm(B, NM, P, dz, P, c->W1T.as<float>(), NM, dx, NM, s);
+      float* dfr = c->dFR.as<float>() + (s1 - B) * NM;
+      tr_gemm(B, NM, P, dz, P, c->W1T.as<float>(), NM, dfr, NM, s, nullptr, dfr, NM);
+      float* dpin = dPIN + (s1 - B) * (H + D);
+      tr_gemm(B, H + D, NM, dx, NM, c->WfT.as<float>(), H + D, dpin, H + D, s, nullptr, dpin, H + D);
+    }
   }
 
   // ---- weight gradients over all T·B rows ----
@@ -1587,7 +1730,10 @@ static void tr_front_alloc(tt2_train_ctx* c) {
   // reference encoders at max_T_ref
   const int RD = f.reference_depth, nm = c->NM;
   long fbuf = BT * K * std::max(C, E);  // encoder im2col^T
-  long mmax = 1;
+  // fDY / fDZc hold the refnet conv activations' gradients AND the encoder convs' BN backward
+  // (dy, dz: B·T_in·C each)
+  long mmax = BT * C;
+  long wt_conv2d = 1;  // largest 3x3 conv2d kernel transpose [fo][9·ci]
   int H = f.max_T_ref, W = nm, ci = 1;
   for (int i = 0; i < 6; ++i) {
     const int Ho = (H + 1) / 2, Wo = (W + 1) / 2, fo = f.reference_filters[i];
@@ -1598,10 +1744,13 @@ static void tr_front_alloc(tt2_train_ctx* c) {
     }
     fbuf = std::max(fbuf, 9L * ci * M);
     mmax = std::max(mmax, std::max(M * fo, B * (long)H * W * ci));
+    wt_conv2d = std::max(wt_conv2d, 9L * ci * fo);
     H = Ho; W = Wo; ci = fo;
   }
   const long T2 = H;
   c->f_T2max = (int)T2;
+  // FB also holds the transposes of the GRU states / inputs over all T2·B rows and the BiLSTM states
+  fbuf = std::max({fbuf, T2 * B * std::max<long>((long)W * ci, RD), BT * U, BT * C});
   for (int r = 0; r < c->f_nref; ++r) {
     a(c->fXG[r], B * T2 * 3 * RD); a(c->fGR[r], T2 * B * RD); a(c->fGU[r], T2 * B * RD); a(c->fGCC[r], T2 * B * RD);
     a(c->fGRH[r], T2 * B * RD); a(c->fHG[r], (T2 + 1) * B * RD); a(c->fREF[r], B * 128);
@@ -1613,7 +1762,10 @@ static void tr_front_alloc(tt2_train_ctx* c) {
   a(c->fGsum, ntok * A + ntok * tokd + 2 * dh);
   a(c->fdREF, B * 128); a(c->fDZD, B * 128); a(c->fDH, B * RD); a(c->fDHA, B * RD); a(c->fDRH, B * RD);
   a(c->fDCP, T2 * B * RD); a(c->fDGP, T2 * B * 2 * RD); a(c->fDXG, B * T2 * 3 * RD);
-  a(c->fWT, std::max<long>({9L * 128 * 128, 3L * RD * std::max<long>(c->f_gin, RD), 128L * RD, 128L * A, (long)K * C * C}));
+  // transposed / flipped weight scratch: refnet conv2d kernels, GRU gates + candidate, dense, GST
+  // query, and the encoder conv flip K·cin·C with cin = E for the first layer
+  a(c->fWT, std::max<long>({wt_conv2d, 3L * RD * std::max<long>(c->f_gin, RD), 128L * RD, 128L * A,
+                            (long)K * std::max(C, E) * C}));
   a(c->fBN, 2L * (f.enc_conv_layers + 6 * c->f_nref) * 512);
   a(c->fpart, 64L * 2 * 512 + 1024);
 }
@@ -2034,6 +2186,43 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   const int rf[6] = {32, 32, 64, 64, 128, 128};
   for (int i = 0; i < 6; ++i) c->reference_filters[i] = rf[i];
   c->max_T_ref = max_T_out;
+  c->mask_decoder = 0;
+  c->pos_weight = 1.0f;
+}
+
+tt2_status tt2_train_set_target_lengths(tt2_train_ctx* c, const int32_t* lengths) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    if (!lengths) {
+      c->has_tlen = false;
+      return;
+    }
+    long sum = 0;
+    int mx = 0;
+    for (int b = 0; b < c->B; ++b) {
+      TT2_CHECK(lengths[b] >= 1 && lengths[b] <= c->Tm, TT2_ERR_SHAPE_MISMATCH,
+                "target length out of [1, max_T_out]");
+      sum += lengths[b];
+      mx = std::max(mx, (int)lengths[b]);
+    }
+    TT2_HIP(hipSetDevice(c->dev));
+    TT2_HIP(hipMemcpy(c->TLEN.p, lengths, sizeof(int) * (size_t)c->B, hipMemcpyHostToDevice));
+    c->has_tlen = true;
+    c->tlen_sum = sum;
+    c->tlen_max = mx;
+  });
+}
+
+tt2_status tt2_train_set_teacher_forcing(tt2_train_ctx* c, const uint8_t* feed_target, int T_out) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    if (!feed_target) {
+      c->feed.clear();
+      return;
+    }
+    TT2_CHECK(T_out >= 1 && T_out <= c->Tm, TT2_ERR_SHAPE_MISMATCH, "T_out out of [1, max_T_out]");
+    c->feed.assign(feed_target, feed_target + T_out);
+  });
 }
 
 tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_train_ctx** out) {
@@ -2196,6 +2385,7 @@ tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* c, const float* memory_
               "front-end context: use tt2_train_forward_backward_text_dev (ids + reference mels)");
     tr_forward_backward(c, memory_d, lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d,
                         postnet_masks_d, T_in, T_out, s);
+    tr_redzones(c, "decoder + postnet");
     tr_regularize(c, s);
     TT2_HIP(hipEventRecord(c->ev1, s));
     TT2_HIP(hipGetLastError());
@@ -2226,12 +2416,15 @@ tt2_status tt2_train_forward_backward_text_dev(tt2_train_ctx* c, const int32_t* 
     g_tr_prec = c->cfg.precision ? 2 : 0;
     g_tr_ctx = c;
     tr_front_forward(c, ids_d, lengths_d, refs, T_ref, enc_conv_masks_d, enc_zoneout_masks_d, T_in, s);
+    tr_redzones(c, "front forward");
     tr_forward_backward(c, c->fMEM.as<float>(), lengths_d, targets_d, stop_targets_d, prenet_masks_d, zoneout_masks_d,
                         postnet_masks_d, T_in, T_out, s);
+    tr_redzones(c, "decoder + postnet");
     g_tr_kpart = &c->kpart;
     g_tr_prec = c->cfg.precision ? 2 : 0;
     g_tr_ctx = c;
     tr_front_backward(c, ids_d, lengths_d, refs, T_ref, enc_conv_masks_d, enc_zoneout_masks_d, T_in, s);
+    tr_redzones(c, "front backward");
     g_tr_kpart = nullptr;
     g_tr_prec = 0;
     g_tr_ctx = nullptr;
@@ -2248,6 +2441,7 @@ tt2_status tt2_train_apply_dev(tt2_train_ctx* c, float lr, int global_step, void
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     c->last_stream = s;
     tr_apply(c, lr, global_step, s);
+    tr_redzones(c, "apply");
     TT2_HIP(hipGetLastError());
   });
 }
@@ -2281,6 +2475,17 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
     }
     if (c->cfg.frontend && std::string(name) == "frontend:memory") {  // the front end's memory [B,T_in,D]
       tr_d2h(c, host, c->fMEM.p, sizeof(float) * (size_t)c->B * c->Tin_last * c->D);
+      return;
+    }
+    if (c->cfg.frontend && std::string(name).rfind("debug:", 0) == 0) {
+      // the encoder conv-1 backward operands as the last text step left them: the embedding output
+      // [B*T_in][E], its transposed im2col [K*E][B*T_in] and conv-1's dz [B*T_in][C]
+      const long M = (long)c->B * c->Tin_last, E = c->cfg.embedding_dim, C = c->cfg.enc_conv_channels;
+      const std::string n(name);
+      if (n == "debug:enc_embedded") tr_d2h(c, host, c->fEX.p, sizeof(float) * (size_t)(M * E));
+      else if (n == "debug:enc_conv1_im2col") tr_d2h(c, host, c->fFBUF.p, sizeof(float) * (size_t)(c->cfg.enc_conv_kernel * E * M));
+      else if (n == "debug:enc_conv1_dz") tr_d2h(c, host, c->fDZc.p, sizeof(float) * (size_t)(M * C));
+      else TT2_CHECK(false, TT2_ERR_INVALID_ARG, "unknown debug tensor " + n);
       return;
     }
     for (int r = 0; r < c->f_nref; ++r)  // reference embeddings (ReferenceEncoder outputs) [B,128]

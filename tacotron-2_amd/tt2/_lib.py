@@ -85,7 +85,8 @@ class TrainConfig(ctypes.Structure):
             "frontend", "n_symbols", "embedding_dim", "enc_conv_layers", "enc_conv_kernel",
             "enc_conv_channels", "encoder_lstm_units", "emt_only", "num_gst", "num_heads",
             "style_embed_depth", "style_att_dim", "reference_depth")] + [
-        ("reference_filters", ctypes.c_int * 6), ("max_T_ref", ctypes.c_int)]
+        ("reference_filters", ctypes.c_int * 6), ("max_T_ref", ctypes.c_int),
+        ("mask_decoder", ctypes.c_int), ("pos_weight", ctypes.c_float)]
 
 
 class DecoderState(ctypes.Structure):
@@ -155,6 +156,8 @@ SIGNATURES = {
     "tt2_train_forward_backward_text_dev": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P,
                                                  _P, _I, _I, _P]),
     "tt2_train_apply_dev": (_I, [_P, _F, _I, _P]),
+    "tt2_train_set_target_lengths": (_I, [_P, _P]),
+    "tt2_train_set_teacher_forcing": (_I, [_P, _P, _I]),
     "tt2_train_losses": (_I, [_P, _P, _P]),
     "tt2_train_get_tensor": (_I, [_P, ctypes.c_char_p, _I, _P]),
     "tt2_train_outputs": (_I, [_P, _P, _P, _P]),

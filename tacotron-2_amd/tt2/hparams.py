@@ -126,6 +126,11 @@ _FORK = dict(
     tacotron_adam_epsilon=1e-6, tacotron_reg_weight=1e-6, tacotron_scale_regularization=False,
     tacotron_clip_gradients=True, tacotron_teacher_forcing_mode="constant",
     tacotron_teacher_forcing_ratio=1.0, cross_entropy_pos_weight=1,
+    # teacher-forcing schedule (hparams.py:302-307) and natural eval (hparams.py:292)
+    tacotron_teacher_forcing_init_ratio=1.0, tacotron_teacher_forcing_final_ratio=0.0,
+    tacotron_teacher_forcing_start_decay=10000, tacotron_teacher_forcing_decay_steps=40000,
+    tacotron_teacher_forcing_decay_alpha=None, tacotron_teacher_forcing_decay_exp_rate=0.1,
+    tacotron_natural_eval=True,
     # WaveNet (hparams.py:207-253)
     input_type="raw", quantize_channels=2 ** 16, use_bias=True, legacy=True, residual_legacy=True,
     log_scale_min=float(np.log(1e-14)), log_scale_min_gauss=float(np.log(1e-7)), cdf_loss=False,

@@ -28,6 +28,32 @@ def learning_rate(step, hp):
     return min(max(lr, hp.tacotron_final_learning_rate), init)
 
 
+def teacher_forcing_ratio(global_step, hp):
+    """TacoTrainingHelper's teacher-forcing ratio (helpers.py:65, 113-118): 'constant' ->
+    tacotron_teacher_forcing_ratio; 'scheduled' -> _teacher_forcing_ratio_decay (helpers.py:140-180):
+    the initial ratio before tacotron_teacher_forcing_start_decay, then
+    tf.train.exponential_decay(init, global_step - start_decay, decay_steps, decay_exp_rate)."""
+    if hp.tacotron_teacher_forcing_mode not in ("constant", "scheduled"):
+        raise ValueError("tacotron_teacher_forcing_mode must be 'constant' or 'scheduled'")  # tacotron.py:202
+    if hp.tacotron_teacher_forcing_mode == "constant":
+        return float(hp.tacotron_teacher_forcing_ratio)
+    init = float(hp.tacotron_teacher_forcing_init_ratio)
+    if global_step < hp.tacotron_teacher_forcing_start_decay:
+        return init
+    return init * hp.tacotron_teacher_forcing_decay_exp_rate ** (
+        (global_step - hp.tacotron_teacher_forcing_start_decay) / hp.tacotron_teacher_forcing_decay_steps)
+
+
+def draw_teacher_forcing(T_out, ratio, rng):
+    """The per-step draw of TacoTrainingHelper.next_inputs (helpers.py:126-131): for every step
+    t >= 1 one uniform u for the whole batch, target frame t-1 fed when u < ratio.  Returns the
+    u8 feed_target [T_out] the library takes (entry 0 = the go frame, always 1).  TF's Philox
+    stream cannot be reproduced, so the draw is injected like the dropout keep bits."""
+    feed = (rng.random(T_out) < ratio).astype(np.uint8)
+    feed[0] = 1
+    return feed
+
+
 def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32", postnet=True,
                  frontend=False, max_T_ref=None):
     lib = _lib.load_library()
@@ -37,11 +63,10 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
         raise NotImplementedError("prenet_layers must be two equal widths on this build")
     if hp.decoder_layers != 2 or hp.outputs_per_step != 1:
         raise NotImplementedError("decoder_layers = 2 and outputs_per_step = 1 on this build")
-    if hp.tacotron_teacher_forcing_mode != "constant" or hp.tacotron_teacher_forcing_ratio != 1.0:
-        raise NotImplementedError("only constant teacher forcing with ratio 1 is built "
-                                  "(hparams.py:300-301 defaults)")
-    if hp.mask_decoder or hp.predict_linear or hp.cross_entropy_pos_weight != 1:
-        raise NotImplementedError("mask_decoder / predict_linear / pos_weight != 1 are not built")
+    if hp.tacotron_teacher_forcing_mode not in ("constant", "scheduled"):
+        raise ValueError("tacotron_teacher_forcing_mode must be 'constant' or 'scheduled'")
+    if hp.predict_linear:
+        raise NotImplementedError("predict_linear (CBHG linear loss) is not built in the training step")
     cfg.memory_dim = memory_width(hp, emt_only)
     cfg.num_mels = hp.num_mels
     cfg.prenet_units = hp.prenet_layers[0]
@@ -58,6 +83,8 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
     cfg.adam_beta2 = hp.tacotron_adam_beta2
     cfg.adam_epsilon = hp.tacotron_adam_epsilon
     cfg.clip_norm = 1.0 if hp.tacotron_clip_gradients else 0.0
+    cfg.mask_decoder = 1 if hp.mask_decoder else 0                    # tacotron.py:758-767
+    cfg.pos_weight = float(hp.cross_entropy_pos_weight)               # modules.py:570
     if precision not in ("fp32", "bf16"):
         raise ValueError("precision must be 'fp32' or 'bf16'")
     cfg.precision = 1 if precision == "bf16" else 0
@@ -158,11 +185,30 @@ class TacotronTrainer(object):
             return a.to(self.device, dtype).contiguous()
         return t.from_numpy(np.ascontiguousarray(a)).to(self.device, dtype, non_blocking=False)
 
+    def set_step_inputs(self, targets_lengths=None, feed_target=None):
+        """Per-step inputs of the reference's training graph beyond the tensors: targets_lengths
+        [B] (mask_decoder's loss masks, tacotron.py:56,758-767; required when hp.mask_decoder) and
+        feed_target [T_out] u8 (the teacher-forcing draw, draw_teacher_forcing; None = every
+        step teacher-forced).  They stay in effect for later steps until changed."""
+        if targets_lengths is None:
+            check(self.lib.tt2_train_set_target_lengths(self.h, None))
+        else:
+            tl = np.ascontiguousarray(np.asarray(targets_lengths, np.int32))
+            if tl.shape != (self.B,):
+                raise ValueError("targets_lengths must be [batch]")
+            check(self.lib.tt2_train_set_target_lengths(self.h, tl.ctypes.data_as(ctypes.c_void_p)))
+        if feed_target is None:
+            check(self.lib.tt2_train_set_teacher_forcing(self.h, None, 0))
+        else:
+            ft = np.ascontiguousarray(np.asarray(feed_target, np.uint8))
+            check(self.lib.tt2_train_set_teacher_forcing(self.h, ft.ctypes.data_as(ctypes.c_void_p),
+                                                         int(ft.shape[0])))
+
     def forward_backward(self, memory, lengths, targets, stop_targets, prenet_masks,
                          zoneout_masks=None, postnet_masks=None):
         """Teacher-forced forward + losses + backward; gradients land in the flat buffer.
         postnet_masks: Postnet dropout keep bits [layers, B, T_out, channels] (None = no
-        dropout)."""
+        dropout).  Target lengths / teacher-forcing draw: set_step_inputs."""
         t = self.torch
         with t.cuda.stream(self.stream):
             mem = self._dev(memory, t.float32)
