@@ -19,6 +19,10 @@ import time
 
 import ctypes
 
+if os.environ.get("TT2_DUMP_MAPS"):  # debug: the process's mappings at interpreter exit (maps native
+    import atexit                    # backtrace addresses of an exit-time crash to libraries)
+    atexit.register(lambda: open(os.environ["TT2_DUMP_MAPS"], "w").write(open("/proc/self/maps").read()))
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -448,6 +452,12 @@ def bench_variants(a, local):
     return out
 
 
+def _profiled():
+    """Running under rocprofv3 (its tool library is preloaded), or TT2_EXIT_GUARD=1."""
+    return ("rocprofiler" in os.environ.get("LD_PRELOAD", "")
+            or os.environ.get("TT2_EXIT_GUARD", "0") != "0")
+
+
 def main():
     a = parse()
     import torch
@@ -455,6 +465,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    guard = _profiled()
+    if guard:  # before the first device call: see tt2_exit_guard (include/tt2.h), DESIGN.md §7
+        _lib.load_library().tt2_exit_guard(1, 1)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
@@ -730,6 +743,8 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+    if guard:
+        _lib.load_library().tt2_exit_guard(0, 0)  # success: the guard's _exit status
 
 
 if __name__ == "__main__":

@@ -36,6 +36,14 @@ typedef int tt2_status;
 
 /* Thread-local message of the last failing call on this thread ("" if none). */
 const char* tt2_last_error(void);
+/* Process exit guard for profiled runs (not part of any reference interface).  install = 1
+ * registers an atexit handler that flushes stdio and _exit()s with the last `status` passed here
+ * (1 until the caller reports success), skipping the handlers registered before it -- the HIP
+ * runtime's static teardown.  Call it after the HIP runtime is loaded and before the first device
+ * call, so a profiler that registers its finalisation at HSA initialisation still runs first:
+ * under rocprofv3, after the tool's finalisation, the runtime's exit-time teardown of the
+ * cooperative-launch queue faults inside libhsa-runtime64. */
+void tt2_exit_guard(int install, int status);
 /* Library / kernel build identification string (arch, version). */
 const char* tt2_version(void);
 

@@ -3,9 +3,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-# persistent kernels launched with hipLaunchKernel under the profiler: with cooperative launches the
-# profiled process segfaults at exit (after the run, before the next pass; seen r02b)
-export TT2_COOP=0
+# cooperative launches as in the product; bench.py installs tt2_exit_guard under rocprofv3 (the HIP
+# runtime's exit-time teardown of the cooperative queue faults after the profiler finalised)
 TAG=${1:-p}
 ARGS="${PROF_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-wavenet --no-e2e --no-griffin-lim --no-variants}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG/trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_$TAG.bench.json 2>/dev/null && \

@@ -2321,6 +2321,21 @@ using namespace tt2;
 extern "C" {
 
 const char* tt2_last_error(void) { return g_last_error.c_str(); }
+
+static int g_exit_status = 1;
+static void tt2_exit_guard_handler() {
+  std::fflush(stdout);
+  std::fflush(stderr);
+  _exit(g_exit_status);
+}
+void tt2_exit_guard(int install, int status) {
+  static bool installed = false;
+  if (install && !installed) {
+    std::atexit(tt2_exit_guard_handler);
+    installed = true;
+  }
+  g_exit_status = status;
+}
 const char* tt2_version(void) { return "libtt2 0.1 gfx950 fp32 (MFMA f32)"; }
 
 void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_ref, int max_iters) {

@@ -157,6 +157,7 @@ SIGNATURES = {
                                                  _P, _I, _I, _P]),
     "tt2_train_apply_dev": (_I, [_P, _F, _I, _P]),
     "tt2_train_set_target_lengths": (_I, [_P, _P]),
+    "tt2_exit_guard": (None, [_I, _I]),
     "tt2_train_set_teacher_forcing": (_I, [_P, _P, _I]),
     "tt2_train_losses": (_I, [_P, _P, _P]),
     "tt2_train_get_tensor": (_I, [_P, ctypes.c_char_p, _I, _P]),
