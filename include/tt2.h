@@ -274,6 +274,9 @@ typedef struct tt2_wn_config {
   int NN_init;             /* SubPixel: 0 = every output channel uses channel 0's kernel
                               (SubPixelConvolution.build, modules.py:585-593) */
   float log_scale_min_gauss; /* Gaussian head (out_channels == 2): log(1e-7) fork / paper value */
+  int gin_channels;        /* global conditioning width (<= 0: off, the fork default -1;
+                              wavenet.py:152-158, modules.py:427-433, 505-509) */
+  int n_speakers;          /* > 0: use_speaker_embedding, the gc_embedding table [n_speakers, gin] */
 } tt2_wn_config;
 
 typedef struct tt2_wn_ctx tt2_wn_ctx;
@@ -284,6 +287,15 @@ void tt2_wn_destroy(tt2_wn_ctx* ctx);
 tt2_status tt2_wn_load_tensor(tt2_wn_ctx* ctx, const char* tf_name, const float* host,
                               const int64_t* shape, int ndim);
 tt2_status tt2_wn_finalize(tt2_wn_ctx* ctx);
+/* Global condition of the next generate calls (cfg.gin_channels > 0), replacing g in
+ * WaveNet.incremental (wavenet.py:770-775) and the per-layer conv1x1g term added to both gate
+ * halves (ResidualConv1DGLU.step, modules.py:505-509): speaker_ids [B] (int32, rows of the
+ * gc_embedding table; cfg.n_speakers > 0) or features [B, gin_channels] (the g tensor itself).
+ * g is constant over time, so every layer's term g·W_g + b_g is folded once into the conditioning
+ * of each row.  Both NULL: clear (the row-b term then comes from no global condition, an error
+ * when gin_channels > 0). */
+tt2_status tt2_wn_set_global_condition(tt2_wn_ctx* ctx, const int32_t* speaker_ids,
+                                       const float* features, int B);
 
 /* Fast-WaveNet incremental synthesis of T = T_f * prod(upsample_scales) samples per row.
  *   cond     [B,T_f,cin] conditioning ALREADY clipped + _interp'd to [0,1]

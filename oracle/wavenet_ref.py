@@ -183,12 +183,14 @@ def mol_sample(logits, u_mix, u_log, log_scale_min):
     return np.minimum(np.maximum(x, np.float32(-1)), np.float32(1)).astype(np.float32), k
 
 
-def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False):
+def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False, g=None):
     """WaveNet.incremental (wavenet.py:724-911) for scalar ('raw') input, MoL or Gaussian head
     (out_channels == 2: u_log carries the N(0,1) draws, u_mix is unused).
 
     c_up: upsampled conditioning [B, T, cin]; u_mix [T, B, nr_mix]; u_log [T, B];
-    test_inputs [B, T] overrides next_input (wavenet.py:876-878).  Returns y [B, T] (float32),
+    test_inputs [B, T] overrides next_input (wavenet.py:876-878); g: global condition -- speaker
+    ids [B] (int: rows of WaveNet_model/gc_embedding, wavenet.py:770-773) or features [B, gin]
+    (float) -- whose conv1x1g term joins both gate halves (modules.py:505-509).  Returns y [B, T] (float32),
     k [B, T] (int32) and, optionally, logits [B, T, out_channels]."""
     c_up = np.asarray(c_up, np.float32)
     B, T, _ = c_up.shape
@@ -199,6 +201,11 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
     kw = hp.get("kernel_size", 3)
     first_k = _w(W, "input_convolution/kernel").reshape(1, R)
     first_b = _w(W, "input_convolution/bias")
+    if g is not None:
+        g = np.asarray(g)
+        if np.issubdtype(g.dtype, np.integer):
+            g = np.asarray(W["WaveNet_model/gc_embedding"], np.float32)[g.reshape(B)]
+        g = np.asarray(g, np.float32).reshape(B, -1)
     layers = []
     for l in range(L):
         s = "ResidualConv1DGLU_{}/".format(l)
@@ -212,6 +219,9 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
             bs=_w(W, s + "residual_block_skip_conv_ResidualConv1DGLU_{}/bias".format(l)),
             ko=_w(W, s + "residual_block_out_conv_ResidualConv1DGLU_{}/kernel".format(l))[0],
             bo=_w(W, s + "residual_block_out_conv_ResidualConv1DGLU_{}/bias".format(l))))
+        if g is not None:                                  # conv1x1g of g, constant over time
+            gs = s + "residual_block_gin_conv_ResidualConv1DGLU_{}/".format(l)
+            layers[-1]["gc"] = g @ _w(W, gs + "kernel")[0] + _w(W, gs + "bias")
     f1k = _w(W, "skip_convolutions/final_convolution_1/kernel")[0]
     f1b = _w(W, "skip_convolutions/final_convolution_1/bias")
     f2k = _w(W, "skip_convolutions/final_convolution_2/kernel")[0]
@@ -234,6 +244,8 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
             h = taps.reshape(B, -1) @ ly["k"] + ly["b"]   # modules.py:295-297
             G2 = h.shape[1] // 2
             cc = ct @ ly["kc"] + ly["bc"]                 # modules.py:497-501
+            if g is not None:
+                cc = cc + ly["gc"]                        # modules.py:505-509
             a = h[:, :G2] + cc[:, :G2]
             bgate = h[:, G2:] + cc[:, G2:]
             z = np.tanh(a) * (1.0 / (1.0 + np.exp(-bgate))).astype(np.float32)   # :510

@@ -640,11 +640,22 @@ struct tt2_wn_ctx {
   bool wide = false;             // R = 128 / 256: k_generate_wide (wavenet_wide.hip), one utterance per launch
   tt2::DevBuf rings;             // k_generate_wide's per-work-group fast-WaveNet queues
   int* status_host = nullptr;    // pinned: spin-timeout word of the last launch
+  tt2::DevBuf gcv;               // [gc_B][L][G] gate-permuted global-condition terms (set_global_condition)
+  int gc_B = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool timed = false;
 };
 
 namespace tt2 {
+
+// cond[b][t][:] += gcv[b][:]: the per-row, time-invariant global-condition term of every layer
+__global__ void k_add_gc(float* __restrict__ cond, const float* __restrict__ gcv, int B, long T, int LG) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * T * LG) return;
+  const int n = (int)(i % LG);
+  const int b = (int)(i / ((long)T * LG));
+  cond[i] += gcv[(long)b * LG + n];
+}
 
 static void wupload(DevBuf& d, const std::vector<float>& h) {
   d.alloc(h.size() * sizeof(float));
@@ -713,6 +724,16 @@ static void wn_finalize(tt2_wn_ctx* c) {
   }
   wupload(c->conv_w, c->wide ? wide_cw : cw);
   wupload(c->conv_b, cb);
+  if (c->cfg.gin_channels > 0) {  // conv1x1g of every layer (modules.py:427-433) and the embedding
+    for (int l = 0; l < L; ++l) {
+      const std::string s = P + "ResidualConv1DGLU_" + std::to_string(l) + "/";
+      const std::string ln = "_ResidualConv1DGLU_" + std::to_string(l) + "/";
+      (void)need(wm, s + "residual_block_gin_conv" + ln + "kernel", {1, c->cfg.gin_channels, G});
+      (void)need(wm, s + "residual_block_gin_conv" + ln + "bias", {G});
+    }
+    if (c->cfg.n_speakers > 0) (void)need(wm, "WaveNet_model/gc_embedding", {c->cfg.n_speakers, c->cfg.gin_channels});
+  }
+  c->gc_B = 0;
   wupload(c->cond_w, condw);
   wupload(c->cond_b, condb);
   wupload(c->so_w, c->wide ? wide_so : sow);
@@ -832,6 +853,14 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   g.bias = c->cond_b.as<float>();
   g.split16 = 1;  // conditioning in [0, 1] after the upsampler: fp16x3 split MFMA (gemm.h)
   gemm(g, s);
+  if (c->cfg.gin_channels > 0) {  // + g·W_g + b_g of every layer (constant over time)
+    TT2_CHECK(c->gc_B >= B, TT2_ERR_STATE,
+              "gin_channels > 0: tt2_wn_set_global_condition for these rows before generating");
+    const long n = (long)B * T * c->L * c->G;
+    hipLaunchKernelGGL(k_add_gc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->cond.as<float>(),
+                       c->gcv.as<float>(), B, (long)T, c->L * c->G);
+    TT2_HIP(hipGetLastError());
+  }
   TT2_HIP(hipEventRecord(c->ev[2], s));
   if (c->wide) {
     const int R = c->R, NG = ww_nc(R) * 2 * R;
@@ -916,6 +945,7 @@ void tt2_wn_default_config(tt2_wn_config* c, int max_batch, int64_t max_samples)
   c->freq_axis_kernel_size = 3; c->max_batch = max_batch; c->max_samples = max_samples;
   c->upsample_type = 0; c->upsample_activation = 1; c->leaky_alpha = 0.4f; c->NN_init = 1;
   c->log_scale_min_gauss = (float)std::log(1e-7);
+  c->gin_channels = -1; c->n_speakers = 0;
 }
 
 tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** out) {
@@ -984,6 +1014,52 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
     TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->status_host), sizeof(int), hipHostMallocDefault));
     *c->status_host = 0;
     *out = c.release();
+  });
+}
+
+tt2_status tt2_wn_set_global_condition(tt2_wn_ctx* c, const int32_t* ids, const float* feat, int B) {
+  return guard([&] {
+    TT2_CHECK(c && c->finalized, TT2_ERR_NOT_LOADED, "tt2_wn_set_global_condition: not finalized");
+    const int gin = c->cfg.gin_channels, L = c->L, G = c->G, R = c->R;
+    TT2_CHECK(gin > 0, TT2_ERR_STATE, "global conditioning off (gin_channels <= 0)");
+    if (!ids && !feat) {
+      c->gc_B = 0;
+      return;
+    }
+    TT2_CHECK(B >= 1 && B <= c->cfg.max_batch, TT2_ERR_SHAPE_MISMATCH, "B out of [1, max_batch]");
+    TT2_CHECK(!ids || c->cfg.n_speakers > 0, TT2_ERR_INVALID_ARG,
+              "speaker ids need the gc_embedding table (n_speakers > 0, use_speaker_embedding)");
+    const WeightMap& wm = c->host;
+    std::vector<float> g((size_t)B * gin);
+    for (int b = 0; b < B; ++b) {
+      if (ids) {  // embedding_lookup (modules.py:13-23)
+        const auto& emb = need(wm, "WaveNet_model/gc_embedding", {c->cfg.n_speakers, gin});
+        TT2_CHECK(ids[b] >= 0 && ids[b] < c->cfg.n_speakers, TT2_ERR_INVALID_ARG, "speaker id out of range");
+        std::copy(emb.data.begin() + (size_t)ids[b] * gin, emb.data.begin() + (size_t)(ids[b] + 1) * gin,
+                  g.begin() + (size_t)b * gin);
+      } else {
+        std::copy(feat + (size_t)b * gin, feat + (size_t)(b + 1) * gin, g.begin() + (size_t)b * gin);
+      }
+    }
+    std::vector<float> gcv((size_t)B * L * G);
+    const std::string P(WP);
+    for (int l = 0; l < L; ++l) {
+      const std::string s = P + "ResidualConv1DGLU_" + std::to_string(l) + "/";
+      const std::string ln = "_ResidualConv1DGLU_" + std::to_string(l) + "/";
+      const auto& kg = need(wm, s + "residual_block_gin_conv" + ln + "kernel", {1, gin, G});
+      const auto& bg = need(wm, s + "residual_block_gin_conv" + ln + "bias", {G});
+      for (int b = 0; b < B; ++b)
+        for (int q = 0; q < G / 4; ++q)
+          for (int e = 0; e < 4; ++e) {
+            const int src = gate_col(R, q, e), dst = 4 * q + e;  // the conditioning's gate permutation
+            double v = bg.data[src];
+            for (int i = 0; i < gin; ++i) v += (double)g[(size_t)b * gin + i] * kg.data[(size_t)i * G + src];
+            gcv[((size_t)b * L + l) * G + dst] = (float)v;
+          }
+    }
+    TT2_HIP(hipSetDevice(c->dev));
+    wupload(c->gcv, gcv);
+    c->gc_B = B;
   });
 }
 

@@ -58,7 +58,8 @@ class WnConfig(ctypes.Structure):
         ("max_batch", ctypes.c_int), ("max_samples", ctypes.c_int64),
         ("upsample_type", ctypes.c_int), ("upsample_activation", ctypes.c_int),
         ("leaky_alpha", ctypes.c_float), ("NN_init", ctypes.c_int),
-        ("log_scale_min_gauss", ctypes.c_float)]
+        ("log_scale_min_gauss", ctypes.c_float), ("gin_channels", ctypes.c_int),
+        ("n_speakers", ctypes.c_int)]
 
 
 class GlConfig(ctypes.Structure):
@@ -158,6 +159,7 @@ SIGNATURES = {
     "tt2_train_apply_dev": (_I, [_P, _F, _I, _P]),
     "tt2_train_set_target_lengths": (_I, [_P, _P]),
     "tt2_exit_guard": (None, [_I, _I]),
+    "tt2_wn_set_global_condition": (_I, [_P, _P, _P, _I]),
     "tt2_train_set_teacher_forcing": (_I, [_P, _P, _I]),
     "tt2_train_losses": (_I, [_P, _P, _P]),
     "tt2_train_get_tensor": (_I, [_P, ctypes.c_char_p, _I, _P]),

@@ -280,6 +280,8 @@ def wavenet_config(hp, max_batch, max_samples, lib=None):
     cfg.leaky_alpha = hp.leaky_alpha
     cfg.NN_init = 1 if hp.NN_init else 0
     cfg.log_scale_min_gauss = hp.log_scale_min_gauss
+    cfg.gin_channels = hp.gin_channels if hp.gin_channels > 0 else -1       # wavenet.py:152-158
+    cfg.n_speakers = hp.n_speakers if (hp.gin_channels > 0 and hp.use_speaker_embedding) else 0
     cfg.n_upsample = len(hp.upsample_scales)
     for i, s in enumerate(hp.upsample_scales):
         cfg.upsample_scales[i] = s
@@ -321,12 +323,33 @@ class WaveNetEngine(object):
     def fits(self, B, T):
         return B <= self.caps[0] and T <= self.caps[1]
 
+    def set_global_condition(self, g, B):
+        """g: speaker ids [B] (int, with the gc_embedding table) or features [B, gin_channels]
+        (float); None clears it.  WaveNet.incremental's g (wavenet.py:770-775)."""
+        if g is None:
+            self._ok(self.lib.tt2_wn_set_global_condition(self.h, None, None, 0))
+            return
+        g = np.asarray(g)
+        if np.issubdtype(g.dtype, np.integer):
+            ids = np.ascontiguousarray(g.reshape(B), np.int32)
+            self._ok(self.lib.tt2_wn_set_global_condition(self.h, ptr(ids), None, B))
+        else:
+            feat = np.ascontiguousarray(g.reshape(B, -1), np.float32)
+            if feat.shape[1] != self.hp.gin_channels:
+                raise ValueError("global condition features must be [B, gin_channels]")
+            self._ok(self.lib.tt2_wn_set_global_condition(self.h, None, ptr(feat), B))
+
     def generate(self, cond, u_mix=None, u_log=None, seed=0, teacher=None, want_logits=False,
-                 want_upsampled=False):
-        """cond [B, T_f, cin] (clipped + interp'd).  Returns dict(y [B,T], k [B,T], logits?,
+                 want_upsampled=False, g=None):
+        """cond [B, T_f, cin] (clipped + interp'd); g: global condition (set_global_condition;
+        required when gin_channels > 0).  Returns dict(y [B,T], k [B,T], logits?,
         upsampled? [B, cin, T])."""
         cond = f32(cond)
         B, T_f, F = cond.shape
+        if self.hp.gin_channels > 0:
+            if g is None:
+                raise ValueError("gin_channels > 0: a global condition g is required")
+            self.set_global_condition(g, B)
         T = T_f * self.hop
         nr = self.hp.out_channels // 3
         um, ul, tg = f32(u_mix), f32(u_log), f32(teacher)

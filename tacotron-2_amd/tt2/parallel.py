@@ -67,6 +67,21 @@ def gather_padded(local, lengths, group=None, pad_value=0.0):
     return res
 
 
+def all_reduce_sum_(t, group=None):
+    """In-place SUM all-reduce: RCCL over xGMI for CUDA tensors under "nccl"; under gloo a CUDA
+    tensor is reduced through a host copy (the CPU rehearsal of the path)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return t
+    if t.is_cuda and dist.get_backend(group) != "nccl":
+        host = t.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(host)
+        return t
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
 def tower_mean_(flat_grads, group=None):
     """Data-parallel training: the reference averages the per-tower gradients on the CPU
     (Tacotron.get_clipped_grads, tacotron.py:1194-1208: reduce_mean over the tower axis) before
@@ -76,16 +91,6 @@ def tower_mean_(flat_grads, group=None):
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return flat_grads
-    world = dist.get_world_size(group)
-    if world == 1:
-        return flat_grads
-    if flat_grads.is_cuda and dist.get_backend(group) != "nccl":
-        # gloo (CPU rehearsal of the DP path, e.g. two ranks sharing one GPU in a test): reduce a
-        # host copy, ordered after the producer's stream
-        host = flat_grads.cpu()
-        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-        flat_grads.copy_(host.div_(world))
-        return flat_grads
-    dist.all_reduce(flat_grads, op=dist.ReduceOp.SUM, group=group)
-    flat_grads.div_(world)
+    all_reduce_sum_(flat_grads, group)
+    flat_grads.div_(dist.get_world_size(group))
     return flat_grads

@@ -288,32 +288,49 @@ class TacotronTrainer(object):
         with self.torch.cuda.stream(self.stream):
             tower_mean_(buf, group)
 
-    def sync_moving_stats(self, group=None):
-        """Average every batch-norm moving_mean / moving_variance over the data-parallel ranks.
-
-        In the reference all towers run the UPDATE_OPS of ONE shared set of moving-statistics
-        variables (tacotron.py:1088-1090 inside the tower loop 1194-1208), so a checkpoint holds a
-        single set.  Here every rank updates its own copy from its shard's batch statistics in
-        apply(); one all-reduce (mean) of the packed statistics right after it keeps the ranks'
-        copies identical (the mean of the per-shard momentum updates, where TF applies the towers'
-        updates one after another in an unspecified order)."""
-        import torch.distributed as dist
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-            return
-        from .parallel import tower_mean_
+    def _stats(self):
+        """Every BN moving_mean / moving_variance packed into one device buffer (library order)."""
         n = ctypes.c_int64()
         check(self.lib.tt2_train_moving_stats_dev(self.h, None, ctypes.byref(n), 0, None))
         if n.value == 0:
-            return
+            return None
         with self.torch.cuda.stream(self.stream):
             buf = self.torch.empty(n.value, dtype=self.torch.float32, device=self.device)
-            sp = ctypes.c_void_p(self.stream.cuda_stream)
-            check(self.lib.tt2_train_moving_stats_dev(self.h, ctypes.c_void_p(buf.data_ptr()), None,
-                                                      0, sp))
-            tower_mean_(buf, group)
-            check(self.lib.tt2_train_moving_stats_dev(self.h, ctypes.c_void_p(buf.data_ptr()), None,
-                                                      1, sp))
-            self.stream.synchronize()
+            check(self.lib.tt2_train_moving_stats_dev(self.h, ctypes.c_void_p(buf.data_ptr()), None, 0,
+                                                      ctypes.c_void_p(self.stream.cuda_stream)))
+        return buf
+
+    def sync_moving_stats(self, before=None, group=None):
+        """Make every rank's batch-norm moving statistics the reference's single shared set.
+
+        In the reference all towers run the UPDATE_OPS of ONE set of moving-statistics variables
+        (tacotron.py:1088-1090 inside the tower loop 1194-1208): the towers' updates
+        m <- mu·m + (1-mu)·x_k compose one after another.  Here each rank applied its own update
+        in apply(); with ``before`` (the packed statistics before that apply, as step() passes
+        them) the ranks rebuild the composition in rank order with one SUM all-reduce:
+        m_N = mu^N·m_0 + Σ_k mu^(N-1-k)·(m_k - mu·m_0), where m_k is rank k's own update.  TF runs
+        the towers' ops in an unspecified order; rank order is one of the orders it may take.
+        Without ``before`` the ranks keep the mean of their updates (order-free, not exactly any
+        of TF's orders).  Stream-ordered: no host synchronisation."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+            return
+        from .parallel import all_reduce_sum_, tower_mean_
+        buf = self._stats()
+        if buf is None:
+            return
+        N, k = dist.get_world_size(group), dist.get_rank(group)
+        mu = float(self.cfg.bn_momentum)
+        with self.torch.cuda.stream(self.stream):
+            if before is None:
+                tower_mean_(buf, group)
+            else:
+                buf.sub_(before, alpha=mu).mul_(mu ** (N - 1 - k))
+                all_reduce_sum_(buf, group)
+                buf.add_(before, alpha=mu ** N)
+            check(self.lib.tt2_train_moving_stats_dev(self.h, ctypes.c_void_p(buf.data_ptr()), None, 1,
+                                                      ctypes.c_void_p(self.stream.cuda_stream)))
+        self._stats_keep = (buf, before)  # alive until the stream has consumed them
 
     def apply(self, global_step=None, lr=None):
         """clip_by_global_norm(1.0) + Adam at update count ``global_step`` (1-based).
@@ -338,8 +355,12 @@ class TacotronTrainer(object):
         self.forward_backward(memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,
                               postnet_masks)
         self.allreduce_grads()
+        import torch.distributed as dist
+        dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        before = self._stats() if dp else None
         self.apply()
-        self.sync_moving_stats()
+        if dp:
+            self.sync_moving_stats(before)
         return self.losses()
 
     def losses(self):

@@ -316,8 +316,11 @@ def wavenet_weight_specs(hp):
     S.append((WP + "input_convolution/bias", (R,), "bias"))
     for l in range(hp.layers):
         s = WP + "ResidualConv1DGLU_{}/".format(l)
-        for kind, shape in (("causal", (hp.kernel_size, R, G)), ("cin", (1, hp.cin_channels, G)),
-                            ("skip", (1, G // 2, Sk)), ("out", (1, G // 2, R))):
+        kinds = [("causal", (hp.kernel_size, R, G)), ("cin", (1, hp.cin_channels, G)),
+                 ("skip", (1, G // 2, Sk)), ("out", (1, G // 2, R))]
+        if hp.gin_channels > 0:   # conv1x1g (modules.py:427-433)
+            kinds.insert(2, ("gin", (1, hp.gin_channels, G)))
+        for kind, shape in kinds:
             sc = s + "residual_block_{}_conv_ResidualConv1DGLU_{}/".format(kind, l)
             S.append((sc + "kernel", shape, "glorot"))
             S.append((sc + "bias", (shape[-1],), "bias"))
@@ -325,6 +328,8 @@ def wavenet_weight_specs(hp):
     S.append((WP + "skip_convolutions/final_convolution_1/bias", (Sk,), "bias"))
     S.append((WP + "skip_convolutions/final_convolution_2/kernel", (1, Sk, hp.out_channels), "glorot"))
     S.append((WP + "skip_convolutions/final_convolution_2/bias", (hp.out_channels,), "bias"))
+    if hp.gin_channels > 0 and hp.use_speaker_embedding:   # Embedding, truncated normal std 0.1
+        S.append(("WaveNet_model/gc_embedding", (hp.n_speakers, hp.gin_channels), "embed:0.1"))
     ut = hp.upsample_type
     if ut == "NearestNeighbor":  # NearestNeighborUpsample: no variables (modules.py:524-536)
         return S
@@ -374,6 +379,9 @@ def _init(rng, shape, kind, hp):
         return rng.uniform(-0.1, 0.1, shape).astype(np.float32)
     if kind == "bn_var":
         return rng.uniform(0.8, 1.2, shape).astype(np.float32)
+    if kind.startswith("embed:"):  # truncated_normal_initializer(0, std) (modules.py:13-20)
+        std = float(kind.split(":")[1])
+        return np.clip(rng.normal(0, std, shape), -2 * std, 2 * std).astype(np.float32)
     if kind == "gst_tokens":  # truncated_normal(stddev=0.5), tacotron.py:221-224
         v = rng.normal(0, 0.5, shape)
         return np.clip(v, -1.0, 1.0).astype(np.float32)

@@ -89,8 +89,6 @@ class WaveNet():
         hp = self._hparams
         if not is_scalar_input(hp.input_type) or is_mulaw(hp.input_type):
             raise NotImplementedError("only input_type='raw' is on the MI355X path")
-        if self.global_conditioning_enabled():
-            raise NotImplementedError("global conditioning (gin_channels > 0) is not built")
         if not self.local_conditioning_enabled():
             raise NotImplementedError("unconditional synthesis (cin_channels <= 0) is not built")
 
@@ -125,8 +123,12 @@ class WaveNet():
         if c.ndim != 3 or c.shape[2] != hp.cin_channels:
             raise ValueError('Expected 3 dimension shape [batch_size(1), time_length, {}] for local '
                              'condition features but found {}'.format(hp.cin_channels, c.shape))
+        if self.global_conditioning_enabled() and g is None:
+            raise ValueError("gin_channels > 0 needs the global condition g (speaker ids)")
         ntow = hp.wavenet_num_gpus
         cs = np.split(c, ntow, axis=0) if ntow > 1 else [c]
+        gs = [None] * ntow if not self.global_conditioning_enabled() else \
+            np.split(np.asarray(g).reshape(c.shape[0], -1), ntow, axis=0)
         tis = ([None] * ntow if test_inputs is None else
                np.split(np.asarray(test_inputs, np.float32).reshape(c.shape[0], -1), ntow, axis=0))
         self.tower_y_hat = []
@@ -140,7 +142,8 @@ class WaveNet():
             if u_mix is not None:
                 um = np.asarray(u_mix, np.float32)[:, i * B:(i + 1) * B]
                 ul = np.asarray(u_log, np.float32)[:, i * B:(i + 1) * B]
-            out = self._get_engine(B, T).generate(ci, um, ul, seed, tis[i], want_upsampled=True)
+            out = self._get_engine(B, T).generate(ci, um, ul, seed, tis[i], want_upsampled=True,
+                                                  g=gs[i])
             self.tower_y_hat.append(out["y"])
             self.tower_synth_upsampled_local_features.append(out["upsampled"])
             self.tower_mix_indices.append(out["k"])
@@ -160,7 +163,8 @@ class WaveNet():
         out = self._get_engine(c.shape[0], c.shape[1] * get_hop_size(self._hparams)).generate(
             c, u_mix, u_log, seed,
             None if test_inputs is None else np.asarray(test_inputs, np.float32).reshape(c.shape[0], -1),
-            want_logits=return_logits, want_upsampled=True)
+            want_logits=return_logits, want_upsampled=True,
+            g=g if self.global_conditioning_enabled() else None)
         self.upsampled_local_features = out["upsampled"]
         y = out["y"][:, None, :]
         return (y, out["logits"]) if return_logits else y

@@ -32,9 +32,8 @@ class Synthesizer:
     def load(self, checkpoint_path, hparams, model_name='WaveNet'):
         self._hparams = hparams
         local_cond, global_cond = self._check_conditions()
-        if not local_cond or global_cond:
-            raise NotImplementedError('only local (mel) conditioning without global conditioning '
-                                      'is on the MI355X path')
+        if not local_cond:
+            raise NotImplementedError('synthesis without local (mel) conditioning is not built')
         self.model = create_model(model_name, hparams)
         if checkpoint_path is None:
             self.model.init_random_weights()
@@ -49,8 +48,10 @@ class Synthesizer:
         """mel_spectrograms: list of [T_i, num_mels] arrays.  Returns the wav paths (or, with
         ``out_dir=None``, the trimmed waveforms)."""
         hp = self._hparams
-        if speaker_ids is not None and any(s != '<no_g>' for s in speaker_ids):
-            raise NotImplementedError('global conditioning (speaker ids) is not on the MI355X path')
+        local_cond, global_cond = self._check_conditions()
+        # synthesizer.py:71 (g = speaker ids [B, 1] int32) -> WaveNet.initialize's g
+        g = None if (speaker_ids is None or not global_cond) else \
+            np.asarray(speaker_ids, dtype=np.int32).reshape(len(mel_spectrograms), 1)
         mel_spectrograms = [np.asarray(m, np.float32) for m in mel_spectrograms]
         audio_lengths = [len(x) * get_hop_size(hp) for x in mel_spectrograms]
         maxlen = max([len(x) for x in mel_spectrograms])
@@ -63,7 +64,7 @@ class Synthesizer:
                             for x in mel_spectrograms]).astype(np.float32)
         if hp.normalize_for_wavenet:
             c_batch = _interp(c_batch, T2_output_range).astype(np.float32)
-        self.model.initialize(None, c_batch, None, None, u_mix=u_mix, u_log=u_log, seed=seed)
+        self.model.initialize(None, c_batch, g, None, u_mix=u_mix, u_log=u_log, seed=seed)
         generated_wavs = [w for tower in self.model.tower_y_hat for w in tower]
         upsampled = [f for tower in self.model.tower_synth_upsampled_local_features for f in tower]
         generated_wavs = [w[:n] for w, n in zip(generated_wavs, audio_lengths)]

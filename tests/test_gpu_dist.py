@@ -8,7 +8,8 @@ library (the world>1 branches had only run with the oracle standing
 * One data-parallel training step: each rank forward/backward on its tower, the tower mean as an
   all-reduce of the flat gradient buffer, clipped Adam: the updated parameters equal a single
   process that averages the two towers' device gradients itself, and they moved at step 1; the
-  batch-norm moving statistics are the rank mean of the per-shard updates and equal on both ranks.
+  batch-norm moving statistics are the per-shard updates composed in rank order (as the
+  reference's towers update one shared variable) and equal on both ranks.
 """
 import os
 import socket
@@ -137,8 +138,9 @@ def test_gloo_world2_product_path_on_one_gpu(tmp_path):
     for r in range(world):
         got = np.load(str(tmp_path / "param_{}.npy".format(r)))
         np.testing.assert_allclose(got, want, rtol=0, atol=1e-6)
-    # BN moving statistics: each rank's momentum update from its own shard, averaged over ranks
-    # (sync_moving_stats) = the mean of the two single-tower updates; identical on both ranks
+    # BN moving statistics: the reference's towers compose their updates of ONE variable; with the
+    # rank order m2 = mu·(mu·m0 + (1-mu)·x0) + (1-mu)·x1 = mu·u0 + u1 - mu·m0 for the single-tower
+    # updates u_k (sync_moving_stats); identical on both ranks
     per_tower = []
     for s, e in ((0, B // 2), (B // 2, B)):
         t1 = TacotronTrainer(thp, TW, B // 2, T_in, T, 0)
@@ -149,4 +151,45 @@ def test_gloo_world2_product_path_on_one_gpu(tmp_path):
     assert np.abs(per_tower[0] - per_tower[1]).max() > 1e-6   # the shards' statistics differ
     bn = [np.load(str(tmp_path / "bnm_{}.npy".format(r))) for r in range(world)]
     np.testing.assert_array_equal(bn[0], bn[1])
-    np.testing.assert_allclose(bn[0], (per_tower[0] + per_tower[1]) / 2, rtol=0, atol=1e-6)
+    mu, m0 = 0.99, np.asarray(TW[BNM], np.float64)
+    np.testing.assert_allclose(bn[0], mu * per_tower[0] + per_tower[1] - mu * m0, rtol=0, atol=1e-6)
+
+
+def _nccl_worker(rank, port, q):
+    """One rank, backend "nccl" (RCCL): the device branches of gather_padded and tower_mean_ and
+    TacotronTrainer.sync_moving_stats' collective, which only the RCCL backend takes."""
+    _paths()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from tt2.parallel import gather_padded, tower_mean_
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(3)
+        x = rng.normal(size=(3, 7, 5)).astype(np.float32)
+        lens = np.array([7, 2, 5])
+        xd = torch.from_numpy(x).cuda()
+        got = gather_padded(xd, lens)                       # RCCL all_gather of device tensors
+        ok_gather = len(got) == 3 and all(np.array_equal(g, x[i, :lens[i]]) for i, g in enumerate(got))
+        g = torch.arange(1000, dtype=torch.float32, device="cuda")
+        tower_mean_(g)                                      # RCCL all_reduce SUM / world, in place
+        torch.cuda.synchronize()
+        ok_reduce = bool(torch.equal(g.cpu(), torch.arange(1000, dtype=torch.float32)))
+        q.put((ok_gather, ok_reduce, dist.get_backend()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_backend_paths_one_rank():
+    """The "nccl" (RCCL) branches of the multi-GPU helpers execute on the device: a one-rank process
+    group on the box's GPU (two ranks cannot share one GPU under RCCL; the two-rank product path
+    above runs on gloo)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(0, _free_port(), q))
+    p.start()
+    p.join(120)
+    assert p.exitcode == 0, p.exitcode
+    ok_gather, ok_reduce, backend = q.get(timeout=5)
+    assert backend == "nccl" and ok_gather and ok_reduce

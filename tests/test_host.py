@@ -238,7 +238,7 @@ def test_wavenet_shim_scope_checks():
     with pytest.raises(RuntimeError, match="weights not loaded"):
         m.initialize(None, np.zeros((1, 2, 80), np.float32), None, None, synthesis_length=None)
     hp2 = bench_wavenet_hparams().override_from_dict(dict(gin_channels=16))  # global conditioning
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError, match="global condition"):                 # ... needs g
         create_model("WaveNet", hp2).initialize(None, np.zeros((1, 2, 80), np.float32), None, None)
 
 
@@ -290,13 +290,27 @@ def test_synthesizer_filenames_to_inputs_pads_per_tower(tmp_path):
     assert get_output_lengths(np.array([[0.2, 0.7], [0.1, 0.1]])) == [1, 2]
 
 
-def test_wavenet_synthesizer_host_prep_rejects_global_conditioning():
+def test_wavenet_synthesizer_host_prep_rejects_unconditional():
     from wavenet_vocoder.synthesizer import Synthesizer, _interp
     np.testing.assert_allclose(_interp(np.array([-4.0, 0.0, 4.0]), (-4, 4)), [0, 0.5, 1])
     hp = bench_wavenet_hparams()
-    hp.gin_channels = 4
+    hp.cin_channels = -1
     with pytest.raises(NotImplementedError):
         Synthesizer().load(None, hp)
+
+
+def test_wavenet_gc_weight_specs():
+    """gin_channels > 0 adds conv1x1g to every layer (modules.py:427-433) and, with
+    use_speaker_embedding, the gc_embedding table (wavenet.py:152-156); off by default."""
+    from tt2.weights import wavenet_weight_specs
+    hp = bench_wavenet_hparams()
+    names = [n for n, _, _ in wavenet_weight_specs(hp)]
+    assert not any("gin_conv" in n or "gc_embedding" in n for n in names)
+    hp.gin_channels, hp.use_speaker_embedding, hp.n_speakers = 16, True, 7
+    specs = {n: s for n, s, _ in wavenet_weight_specs(hp)}
+    k = "WaveNet_model/inference/ResidualConv1DGLU_3/residual_block_gin_conv_ResidualConv1DGLU_3/kernel"
+    assert specs[k] == (1, 16, hp.gate_channels)
+    assert specs["WaveNet_model/gc_embedding"] == (7, 16)
 
 
 @pytest.mark.parametrize("src,kernel,max_spill", [("wavenet.hip", "k_generate_pipe", 0),
