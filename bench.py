@@ -113,24 +113,25 @@ def cpu_baseline_tacotron(hp, W, B, T, T_ref, t_out, seed):
                 t_postnet_s=t3 - t2, decoded=int(frames.shape[1]))
 
 
-def cpu_baseline_wavenet(hp, W, samples):
-    """libtt2_cpu.so tt2_wn_generate: B=1, `samples` audio samples of configs[2] (conditioning
-    upsampling included), injected uniforms."""
+def cpu_baseline_wavenet(hp, W, samples, B=1):
+    """libtt2_cpu.so tt2_wn_generate: B utterances of `samples` audio samples of configs[2]
+    (conditioning upsampling included), injected uniforms; the library runs one OpenMP thread per
+    utterance (the sample chain inside an utterance is sequential).  Returns (samples/s, T)."""
     from tt2.engine import WaveNetEngine
     lib = _lib.load_cpu_library()
     hop = int(np.prod(hp.upsample_scales))
     T_f = max(1, samples // hop)
     rng = np.random.default_rng(5339)
-    cond = rng.uniform(0, 1, (1, T_f, hp.num_mels)).astype(np.float32)
+    cond = rng.uniform(0, 1, (B, T_f, hp.num_mels)).astype(np.float32)
     T = T_f * hop
-    um = rng.uniform(1e-5, 1 - 1e-5, (T, 1, 10)).astype(np.float32)
-    ul = rng.uniform(1e-5, 1 - 1e-5, (T, 1)).astype(np.float32)
-    eng = WaveNetEngine(hp, W, 1, T, 0, lib=lib)
+    um = rng.uniform(1e-5, 1 - 1e-5, (T, B, 10)).astype(np.float32)
+    ul = rng.uniform(1e-5, 1 - 1e-5, (T, B)).astype(np.float32)
+    eng = WaveNetEngine(hp, W, B, T, 0, lib=lib)
     t0 = time.perf_counter()
     eng.generate(cond, um, ul, 0, None)
     dt = time.perf_counter() - t0
     eng.close()
-    return T / dt, T
+    return B * T / dt, T
 
 
 def threads_used():
@@ -643,6 +644,31 @@ def main():
                                 algorithmic_bytes_per_sample=int(wbytes)),
                   diag_stage_stamps_us=wn_stamps, diag_shader_clock_mhz=wn_clock_mhz)
         weng.close()
+        # batched synthesis at wavenet_synthesis_batch_size (hparams.py:332): 20 utterances of the
+        # configs[2] model in one generation launch (k_generate_pipe, 8 CUs per utterance)
+        nb = whp.wavenet_synthesis_batch_size
+        weng = WaveNetEngine(whp, WW, nb, Tn, local)
+        condb = ((rng.uniform(-4, 4, (nb, 80, a.wavenet_frames)) + 4) / 8).astype(np.float32)
+        condb_d = torch.from_numpy(condb).to(dev)
+        wavb_d = torch.empty((nb, Tn), dtype=torch.float32, device=dev)
+
+        def wstep_b():
+            _lib.check(lib.tt2_wn_generate_dev(weng.h, condb_d.data_ptr(), nb, a.wavenet_frames, None,
+                                               None, 5339 + rank, None, wavb_d.data_ptr(), None,
+                                               None, ctypes.c_void_p(stream)))
+        wstep_b()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        wstep_b()
+        torch.cuda.synchronize()
+        barrier()
+        welb = max_over_ranks(time.perf_counter() - t0)
+        _lib.check(lib.tt2_wn_last_timings(weng.h, wms))
+        wn["batch"] = dict(per_gpu_batch=nb, value=round(world * nb * Tn / welb, 1), unit="audio-samples/s",
+                           realtime_factor_per_utterance=round(Tn / welb / 22050.0, 3),
+                           us_per_sample=round(1e3 * wms[2] / Tn, 3), samples_per_utterance=Tn)
+        weng.close()
 
     # --- WaveNet at the reference's own widths (k_generate_wide): fork default R=128 (20 layers /
     #     2 stacks, Gaussian head, SubPixel) and paper default R=256 (24 / 4, MoL), B=1 ---
@@ -723,8 +749,15 @@ def main():
             WW = init_wavenet_weights(whp, seed=whp.wavenet_random_seed)
             v, n = cpu_baseline_wavenet(whp, WW, 2000)
             wn["cpu_baseline"] = dict(value=round(v, 1), unit="audio-samples/s", cores=1, kind="port",
-                                      sample="libtt2_cpu.so tt2_wn_generate, {} samples, B=1 "
-                                             "(one utterance: sequential per sample)".format(n))
+                                      sample="libtt2_cpu.so tt2_wn_generate, {} samples, B=1: one "
+                                             "utterance is a sequential per-sample chain, one core "
+                                             "(the GPU leg is B=1 too)".format(n))
+            if "batch" in wn:  # batched synthesis on as many threads as the decoder baseline
+                vb, nb_ = cpu_baseline_wavenet(whp, WW, 1100, B=cores)
+                wn["batch"]["cpu_baseline"] = dict(
+                    value=round(vb, 1), unit="audio-samples/s", cores=cores, kind="port",
+                    sample="libtt2_cpu.so tt2_wn_generate, B={} utterances x {} samples, one OpenMP "
+                           "thread per utterance".format(cores, nb_))
 
     if rank == 0:
         out = dict(metric=METRIC, value=round(value, 1), unit="mel-frames/s", n_gpus=world,

@@ -1060,6 +1060,10 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* c, const float* cond, int B, int T_f, con
     const auto& f1b = WW(c, "skip_convolutions/final_convolution_1/bias", {S});
     const auto& f2k = WW(c, "skip_convolutions/final_convolution_2/kernel", {1, S, C});
     const auto& f2b = WW(c, "skip_convolutions/final_convolution_2/bias", {C});
+    CK(!gauss || u_log, TT2_ERR_INVALID_ARG, "the CPU backend's Gaussian head needs injected N(0,1) draws (u_log)");
+    // utterances are independent (the reference's batched synthesis, hparams.py:332): one OpenMP
+    // thread per row; inside a row the sample chain is sequential
+#pragma omp parallel for schedule(dynamic, 1) if (B > 1)
     for (int b = 0; b < B; ++b) {
       // conditioning: [T_f][Cin] -> channels-first, upsampled [Cin][T]; per layer cin conv of
       // every sample at once (one GEMM per layer)
@@ -1130,7 +1134,6 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* c, const float* cond, int B, int T_f, con
         float y;
         int kidx = 0;
         if (gauss) {  // sample_from_gaussian (gaussian.py:39-52): u_log carries the N(0,1) draws
-          CK(u_log, TT2_ERR_INVALID_ARG, "the CPU backend's Gaussian head needs injected N(0,1) draws (u_log)");
           const float ls = std::max(o2[1], cfg.log_scale_min_gauss);
           y = std::min(std::max(o2[0] + std::exp(ls) * u_log[(size_t)t * B + b], -1.f), 1.f);
         } else {  // sample_from_discretized_mix_logistic (mixture.py:76-107)

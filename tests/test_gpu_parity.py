@@ -308,13 +308,14 @@ def _wn(hp, W, maxB, maxT):
     return WaveNetEngine(hp, W, maxB, maxT, 0)
 
 
-@pytest.mark.parametrize("layers,stacks", [(6, 2), (24, 4)])
-def test_wavenet_teacher_forced(layers, stacks):
+@pytest.mark.parametrize("layers,stacks,B,T_f", [(6, 2, 2, 2), (24, 4, 2, 2), (24, 4, 20, 1)])
+def test_wavenet_teacher_forced(layers, stacks, B, T_f):
+    """B = 20: the reference's batched synthesis (wavenet_synthesis_batch_size, hparams.py:332), all
+    rows in one generation launch of k_generate_pipe."""
     from tt2.weights import init_wavenet_weights
     hp = small_wavenet_hparams(layers, stacks)
     W = init_wavenet_weights(hp, seed=5339)
     rng = np.random.default_rng(21)
-    B, T_f = 2, 2
     T = T_f * 275
     mel = rng.uniform(-4, 4, (B, T_f, 80)).astype(np.float32)
     cond = WR.interp_condition(mel)
