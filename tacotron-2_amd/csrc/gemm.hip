@@ -473,6 +473,122 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
     for (int j = 0; j < 2; ++j) epilogue_tile(g, acc[i][j], m0 + wm * 32 * WMB + i * 32, n0 + wn * 64 + j * 32, lane);
 }
 
+// ---- skinny bf16 product (training: M <= 64 rows per decoder step) ---------------------------
+// C[M<=64][N] = A[M][K] (fp32, rounded to bf16 as staged) · B (pre-transposed bf16 Bt16[N][ldbt]).
+// One work-group = 64 rows x 64 columns x one K slice (blockIdx.z), 4 waves of one 32x32
+// v_mfma_f32_32x32x16_bf16 accumulator each.  The WHOLE K slice of both operands is staged into LDS
+// in one burst (every thread issues all its loads before any LDS write) -- the round trip to HBM /
+// MALL is paid once per work-group instead of once per 32-deep k tile, which is what bound the
+// 64x128x32 double-buffered kernel (gemm_x3_kernel) at these shapes.  The host picks the K split so
+// the grid stays near one work-group per CU and the slice fits LDS; partials [z][M][N] as in
+// gemm_x3_kernel (combined by the caller or gemm_splitk_reduce), or the epilogue when unsplit.
+constexpr int SK_BN = 64, SK_BM = 64, SK_GMAX = 19;  // groups of 8 per thread: 64 x 608 / 8 / 256
+__host__ __device__ constexpr int sk_ld(int kslice) { return kslice + 8; }  // padded k stride (bf16)
+size_t sk_lds_bytes(int kslice) { return (size_t)(SK_BM + SK_BN) * sk_ld(kslice) * 2; }
+
+template <bool VA>
+__global__ __launch_bounds__(256, 1) void gemm_sk_kernel(GemmArgs g, int kslice) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 sk_sm[];
+  const int KP = sk_ld(kslice);
+  __bf16* As = sk_sm;               // [64][KP]
+  __bf16* Bs = sk_sm + SK_BM * KP;  // [64][KP]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n0 = blockIdx.x * SK_BN, k0 = blockIdx.z * kslice;
+  const int g8 = kslice >> 3;  // 8-element groups per row of the slice
+  const int ng = 64 * g8;      // groups per operand tile (A and B alike: 64 rows / columns)
+  // every load of both operands is issued before the first LDS write: one round trip to
+  // HBM / MALL per work-group (one wave per SIMD, so the staging registers are affordable)
+  f32x4 va[SK_GMAX][2];
+  bf16x8 vb[SK_GMAX];
+  const __bf16* Bt = reinterpret_cast<const __bf16*>(g.Bt16);
+#pragma unroll
+  for (int u = 0; u < SK_GMAX; ++u) {
+    const int idx = tid + 256 * u;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    va[u][0] = z;
+    va[u][1] = z;
+    for (int e = 0; e < 8; ++e) vb[u][e] = (__bf16)0.f;
+    if (idx < ng) {
+      const int r = idx / g8, kk = (idx - r * g8) * 8, k = k0 + kk;
+      if (r < g.M) {
+        const float* p = g.A + (long)r * g.lda + k;
+        if (VA && k + 8 <= g.K) {
+          va[u][0] = *reinterpret_cast<const f32x4*>(p);
+          va[u][1] = *reinterpret_cast<const f32x4*>(p + 4);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (k + e < g.K) va[u][e >> 2][e & 3] = p[e];
+        }
+      }
+      const int n = n0 + r;  // B: column r of the tile
+      if (n < g.N) {
+        const __bf16* q = Bt + (long)n * g.ldbt + k;
+        if (k + 8 <= g.K) {
+          vb[u] = *reinterpret_cast<const bf16x8*>(q);
+        } else {
+          for (int e = 0; e < 8; ++e)
+            if (k + e < g.K) vb[u][e] = q[e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < SK_GMAX; ++u) {
+    const int idx = tid + 256 * u;
+    if (idx < ng) {
+      const int r = idx / g8, kk = (idx - r * g8) * 8;
+      bf16x8 h;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) h[e] = (__bf16)va[u][e >> 2][e & 3];
+      *reinterpret_cast<bf16x8*>(As + r * KP + kk) = h;
+      *reinterpret_cast<bf16x8*>(Bs + r * KP + kk) = vb[u];
+    }
+  }
+  __syncthreads();
+  const int rw = (w & 1) * 32, cw = (w >> 1) * 32, r = lane & 31, h8 = (lane >> 5) * 8;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  const __bf16* pa = As + (rw + r) * KP + h8;
+  const __bf16* pb = Bs + (cw + r) * KP + h8;
+  for (int kk = 0; kk < kslice; kk += 16) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(pa + kk);
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(pb + kk);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
+  if (g.ksplit > 1 || g.raw) {
+    float* P = g.kpart + (long)blockIdx.z * g.M * g.N;
+    const int col = n0 + cw + (lane & 31);
+    if (col < g.N) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = rw + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+        if (row < g.M) P[(long)row * g.N + col] = acc[q];
+      }
+    }
+    return;
+  }
+  epilogue_tile(g, acc, rw, n0 + cw, lane);
+}
+
+// K split / slice of the skinny kernel: ~one work-group per CU, slice <= SK_KMAX (LDS), multiple of 32
+constexpr int SK_KMAX = 608;
+static bool sk_plan(const GemmArgs& a, int& ks, int& kslice) {
+  if (a.split16 != 2 || !a.Bt16 || a.a_mode != A_DENSE || a.M > SK_BM || a.K < 32) return false;
+  const int nt = (a.N + SK_BN - 1) / SK_BN;
+  ks = std::max(1, std::min(16, 256 / std::max(nt, 1)));
+  for (;;) {
+    kslice = ((a.K + ks - 1) / ks + 31) / 32 * 32;
+    if (kslice <= SK_KMAX) break;
+    ++ks;
+  }
+  ks = (a.K + kslice - 1) / kslice;  // no empty slices
+  if (ks > 1 && !a.kpart) return false;
+  if (ks > 1 && (long)ks * a.M * a.N > a.kpart_floats) return false;
+  return true;
+}
+
 template <int WMB, int WNB>
 static void launch(const GemmArgs& a, bool va, bool vb, hipStream_t s) {
   dim3 grid(cdiv(a.N, 64 * WNB), cdiv(a.M, 64 * WMB), a.ksplit);
@@ -519,6 +635,36 @@ int gemm_impl(const GemmArgs& a, hipStream_t s) {
   if (a.split16) {
     TT2_CHECK(!a.Bt16 || (al16(a.Bt16) && a.ldbt % 8 == 0 && (a.split16 == 2 || (a.Bt16lo && al16(a.Bt16lo)))),
               TT2_ERR_INVALID_ARG, "gemm: Bt16 needs 16-byte alignment, ldbt % 8 == 0 (and Bt16lo for split16 == 1)");
+    int sks = 0, skl = 0;
+    static const bool sk_on = [] {  // opt-in (TT2_GEMM_SKINNY=1): measured no faster, DESIGN §5.6
+      const char* e = std::getenv("TT2_GEMM_SKINNY");
+      return e && e[0] == '1';
+    }();
+    if (sk_on && sk_plan(a, sks, skl)) {  // skinny bf16 product with pre-transposed weights
+      GemmArgs g = a;
+      g.ksplit = sks;
+      const bool vsk = va && a.lda % 4 == 0;
+      const void* kern = vsk ? reinterpret_cast<const void*>(gemm_sk_kernel<true>)
+                             : reinterpret_cast<const void*>(gemm_sk_kernel<false>);
+      static bool attr_set = false;
+      if (!attr_set) {
+        TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_sk_kernel<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sk_lds_bytes(SK_KMAX)));
+        TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_sk_kernel<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sk_lds_bytes(SK_KMAX)));
+        attr_set = true;
+      }
+      dim3 grid(cdiv(a.N, SK_BN), 1, sks);
+      if (vsk) hipLaunchKernelGGL(gemm_sk_kernel<true>, grid, dim3(256), sk_lds_bytes(skl), s, g, skl);
+      else hipLaunchKernelGGL(gemm_sk_kernel<false>, grid, dim3(256), sk_lds_bytes(skl), s, g, skl);
+      (void)kern;
+      TT2_HIP(hipGetLastError());
+      if (sks > 1 && !g.raw) {
+        hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 1023) / 1024)), dim3(256), 0, s, g);
+        TT2_HIP(hipGetLastError());
+      }
+      return sks;
+    }
     const int wm16 = a.M <= 64 ? 1 : 2;
     GemmArgs g = a;
     g.ksplit = 1;
