@@ -68,7 +68,7 @@ struct PdArgs {
   // outputs
   float* frames;  // [B][max_iters][nm]
   float* stop;    // [B][max_iters]
-  float* align;   // [B][T_in][max_iters] or null
+  float* align;   // [B][max_iters][T_in] step-major (tacotron.hip transposes after the launch) or null
   long long* stamps;  // diagnostic s_memrealtime stamps of one step (null = off)
   int stamp_step;
 };

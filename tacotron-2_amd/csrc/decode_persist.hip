@@ -677,7 +677,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       if (tid < T) {
         const float cp = cw[15 + tid];
         cw[15 + tid] = a.cumulative ? al[tid] + cp : al[tid];
-        if (j == 0 && a.align) a.align[((long)b * T + tid) * a.max_iters + t] = al[tid];
+        if (j == 0 && a.align) a.align[((long)b * a.max_iters + t) * T + tid] = al[tid];  // step-major
       }
       if (w == 1) {  // max_att = argmax (ties -> first), Σ_{t<len} alignments
         float best = -INFINITY, ss = 0.f;

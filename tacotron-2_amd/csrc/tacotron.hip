@@ -1212,6 +1212,22 @@ __global__ void k_transpose_bt(const float* __restrict__ src, long ld, float* __
   for (int r = ty; r < 32; r += 8) dst[((long)b * C + c0 + r) * 256 + t0 + tx] = tile[tx][r];
 }
 
+// step-major alignments [B][n][T] -> the reference layout [B][T][ldt] (tower_alignments), columns < n
+__global__ void k_align_t(const float* __restrict__ src, int n, int T, long lds, float* __restrict__ dst, long ldt) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z, j0 = blockIdx.y * 32, s0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int r = ty; r < 32; r += 8) {
+    const int st = s0 + r, j = j0 + tx;
+    tile[r][tx] = (st < n && j < T) ? src[((long)b * lds + st) * T + j] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int j = j0 + r, st = s0 + tx;
+    if (j < T && st < n) dst[((long)b * T + j) * ldt + st] = tile[tx][r];
+  }
+}
+
 // decoder_output clip (tacotron.py:362-363): dst[b][t][n] = clip(src[b][t][n])
 // get_output_lengths (tacotron/synthesizer.py:384-387): per row, the first step whose stop
 // probability rounds to 1 (np.round = round-half-even = rintf), else n_steps.  One wave per row,
@@ -1339,6 +1355,7 @@ struct tt2_ctx {
   bool pd_dev_ok = false; // all PD_NB work-groups can be resident on this device
   bool last_pd = false;   // the last decode ran the persistent kernel
   tt2::DevBuf q_wt, pre_w2t, keysT, valuesT, pd_ctl, H1x, H2x, Ex, CTXx, SSx, PPx, PREx;
+  tt2::DevBuf pd_alnT;  // [B][max_iters][T_in] step-major alignments of the persistent decoder
   // Tacotron_emt_attn variant (emt.h): off for the Tacotron model
   tt2::EmtModel emt;
   tt2::CbhgModel cbhg;  // predict_linear post-processing net (cbhg.h)
@@ -2153,7 +2170,15 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   a.masks = masks_d;
   a.H1x = c->H1x.as<float>(); a.H2x = c->H2x.as<float>(); a.Eg = c->Ex.as<unsigned long long>(); a.CTXx = c->CTXx.as<float>();
   a.SSx = c->SSx.as<float>(); a.PPg = c->PPx.as<unsigned long long>(); a.PREg = c->PREx.as<unsigned long long>();
-  a.frames = frames_d; a.stop = stop_d; a.align = align_d;
+  a.frames = frames_d; a.stop = stop_d;
+  // alignments are written step-major (one contiguous T_in row per step and row: whole-line stores
+  // instead of T_in scattered ones, which the CTX drain of the step waited for) and transposed to the
+  // reference layout after the loop
+  a.align = nullptr;
+  if (align_d) {
+    c->pd_alnT.alloc(sizeof(float) * (size_t)c->B * max_iters * c->T_in);
+    a.align = c->pd_alnT.as<float>();
+  }
   a.stamps = nullptr;
   a.stamp_step = -1;
   if (const char* st = getenv("TT2_STAMP_STEP")) {  // diagnostic: stage stamps of one decode step
@@ -2175,6 +2200,11 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
                 "); set TT2_DECODER=launch to use the per-step launch path");
   TT2_CHECK(h[0] == 1, TT2_ERR_STATE, "persistent decoder did not terminate");
   c->n_steps = h[1];
+  if (align_d && h[1] > 0) {
+    hipLaunchKernelGGL(k_align_t, dim3((unsigned)((h[1] + 31) / 32), (unsigned)((c->T_in + 31) / 32), (unsigned)c->B),
+                       dim3(256), 0, s, c->pd_alnT.as<float>(), h[1], c->T_in, (long)max_iters, align_d, (long)max_iters);
+    TT2_HIP(hipGetLastError());
+  }
   c->last_max_iters = max_iters;
   c->last_pd = true;
   c->have_args = false;
