@@ -77,8 +77,16 @@ __device__ __forceinline__ void ww_fma4(f32x4& acc, float x, const f32x4& w) {
 template <int R, bool GAUSS>
 __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
   constexpr int NC = ww_nc(R), S = R, G = 2 * R, ZC = R / NC, GC = 2 * ZC, NQ = GC / 4, NKS = WW_THREADS / NQ;
-  constexpr int OUT = S + R, NQ2 = OUT / 4, NKS2 = WW_THREADS / NQ2, NG = NC * OUT;
-  static_assert(2 * R / NKS == WW_TAPK && R / NKS == WW_XK && ZC / NKS2 == WW_SOK, "k-slice geometry");
+  // TWO_HOP (R = 256): work-group c gathers the whole z (an all-gather of the layer's NC z slices)
+  // and produces COMPLETE outputs for its slice of OC = OUT / NC columns of [skip | out] -- two
+  // small hops per layer (256 z granules, then <= 320 output granules per consumer) instead of
+  // every consumer summing NC partial rows of OUT (4096 granules, 32 KB per consumer and layer)
+  constexpr bool TWO_HOP = NC == 8;
+  constexpr int OUT = S + R, OC = TWO_HOP ? OUT / NC : OUT, NQ2 = OC / 4, NKS2 = WW_THREADS / NQ2;
+  constexpr int NG = NC * OUT;
+  static_assert(2 * R / NKS == WW_TAPK && R / NKS == WW_XK && (TWO_HOP ? R : ZC) / NKS2 == WW_SOK,
+                "k-slice geometry");
+  static_assert(!TWO_HOP || (R == WW_THREADS && OC == 64 && S % OC == 0), "two-hop geometry: R = 256");
   const float SQH = 0.70710677f;  // float32(np.sqrt(0.5))
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int L = a.L;
@@ -123,7 +131,16 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
           gum[cb * 16 + 15] = (float)(log(uu) - log(1.0 - uu));
         }
       }
-      {  // skips = Σ of the last layer's NC skip partials (running sum and scalings folded in)
+      if constexpr (TWO_HOP) {  // skips = the last layer's skip slices (complete: WGs 0..S/OC-1)
+        float v = 0.f;
+        const bool ok = ww_spin(a.status, lane, [&] {
+          const unsigned long long x = ww_get(gin + 256 + tid);  // x granules after the 256 z granules
+          v = __uint_as_float((unsigned)x);
+          return (unsigned)(x >> 32) == (unsigned)(t + 1);
+        });
+        if (!ok) flag[0] = 1;
+        skv[tid] = fmaxf(v, 0.f);
+      } else {  // skips = Σ of the last layer's NC skip partials (running sum and scalings folded in)
         float v[S / WW_THREADS > 0 ? S / WW_THREADS : 1][NC];
         const bool ok = ww_spin(a.status, lane, [&] {
           bool good = true;
@@ -216,6 +233,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
   float* xin = sm + 16;   // [R] x(t) of this layer
   float* skin = xin + R;  // [S] running skip sum received
   float* z = skin + S;    // [ZC]
+  float* zall = z + ZC;   // [R] the layer's whole z (TWO_HOP)
   const int q = tid / NKS, ks = tid % NKS;
   const int q2 = tid / NKS2, ks2 = tid % NKS2;
   const int d = 1 << (l % a.per), Lr = 2 * d + 1;
@@ -236,10 +254,13 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
   }
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const f32x4 cbias = ks == 0 ? reinterpret_cast<const f32x4*>(a.conv_b + (long)l * G + c * GC)[q] : zero4;
-  const f32x4 sob = (ks2 == 0 && c == 0) ? reinterpret_cast<const f32x4*>(a.so_b + (long)l * OUT)[q2] : zero4;
+  const f32x4 sob = TWO_HOP ? (ks2 == 0 ? reinterpret_cast<const f32x4*>(a.so_b + (long)l * OUT + c * OC)[q2] : zero4)
+                            : ((ks2 == 0 && c == 0) ? reinterpret_cast<const f32x4*>(a.so_b + (long)l * OUT)[q2] : zero4);
   const int tap_r0 = ks * WW_TAPK, tap_blk = tap_r0 / R, tap_off = tap_r0 % R;  // blk 0: x(t-2d), 1: x(t-d)
   const unsigned long long* gin = l > 0 ? a.gran + (long)(l - 1) * NG : sample_gran;
   unsigned long long* gout = a.gran + (long)l * NG + c * OUT;
+  unsigned long long* const gout_z = a.gran + (long)l * NG;            // TWO_HOP: [NC][ZC] z slices
+  unsigned long long* const gout_x = a.gran + (long)l * NG + 256 + c * OC;  // TWO_HOP: this WG's columns
   const float* condp = a.cond + ((long)a.b * a.T) * L * G + (long)l * G + c * GC;
   const bool skip_scale = a.legacy && l > 0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -276,6 +297,26 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
         if (!ok && lane == 0) flag[0] = 1;
         for (int j = lane; j < R; j += 64) xin[j] = y * a.first_w[j] + a.first_b[j];
       }
+    } else if constexpr (TWO_HOP) {
+      // x(t) = the out slices of layer l-1 (WGs S/OC..NC-1, granules [256 + S, 256 + OUT)); the running
+      // skip of this WG's own skip slice (c < S/OC) = layer l-1's slice c
+      const unsigned long long* gx = gin + 256;
+      float xv = 0.f, sv = 0.f;
+      const bool own_skip = c < S / OC && tid < OC;
+      const bool ok = ww_spin(a.status, lane, [&] {
+        const unsigned long long x = ww_get(gx + S + tid);
+        xv = __uint_as_float((unsigned)x);
+        bool good = (unsigned)(x >> 32) == (unsigned)(t + 1);
+        if (own_skip) {
+          const unsigned long long y = ww_get(gx + c * OC + tid);
+          sv = __uint_as_float((unsigned)y);
+          good = good && (unsigned)(y >> 32) == (unsigned)(t + 1);
+        }
+        return good;
+      });
+      if (!ok) flag[0] = 1;
+      xin[tid] = xv;
+      if (own_skip) skin[tid] = sv;
     } else {
       constexpr int NR = (OUT + WW_THREADS - 1) / WW_THREADS;
       float v[NR][NC];
@@ -325,6 +366,46 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
       reinterpret_cast<float2*>(z)[q] = zz;
     }
     __syncthreads();
+    if constexpr (TWO_HOP) {
+      // ---- all-gather of the layer's z, then complete skip / out columns of slice c ----
+      if (tid < ZC) ww_put(gout_z + c * ZC + tid, (unsigned)(t + 1), z[tid]);
+      {
+        float zv = 0.f;
+        const bool ok = ww_spin(a.status, lane, [&] {
+          const unsigned long long x = ww_get(gout_z + tid);
+          zv = __uint_as_float((unsigned)x);
+          return (unsigned)(x >> 32) == (unsigned)(t + 1);
+        });
+        if (!ok) flag[0] = 1;
+        zall[tid] = zv;
+      }
+      __syncthreads();
+      if (flag[0]) return;
+      f32x4 acc2 = zero4;
+      const f32x4* zv4 = reinterpret_cast<const f32x4*>(zall + ks2 * WW_SOK);
+#pragma unroll
+      for (int i4 = 0; i4 < WW_SOK / 4; ++i4) {
+        const f32x4 zv = zv4[i4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ww_fma4(acc2, zv[e], wso[4 * i4 + e]);
+      }
+      ww_reduce<NKS2>(acc2);
+      if (ks2 == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lc = 4 * q2 + e, col = c * OC + lc;  // column of [skip S | out R]
+          float v = acc2[e] + sob[e];
+          if (col < S) {  // skips (wavenet.py:833-836): + running sum of this slice
+            if (l > 0) v += skin[lc];
+            if (skip_scale) v *= SQH;
+          } else {        // residual output
+            v += xin[col - S];
+            if (a.res_legacy) v *= SQH;
+          }
+          ww_put(gout_x + lc, (unsigned)(t + 1), v);
+        }
+      }
+    } else {
     // ---- skip / out 1x1 partials of this z slice (modules.py:512-520), published ----
     {
       f32x4 acc2 = zero4;
@@ -351,6 +432,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
           ww_put(gout + col, (unsigned)(t + 1), v);
         }
       }
+    }
     }
     p = p + 1 == Lr ? 0 : p + 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the queue append drained before its reads
@@ -380,16 +462,19 @@ void ww_pack_conv(const float* conv, int R, int c, std::vector<float>& out) {
 }
 
 void ww_pack_so(const float* skip, const float* outk, int R, int c, std::vector<float>& out) {
-  const int NC = ww_nc(R), ZC = R / NC, S = R, OUT = S + R, NQ2 = OUT / 4, NKS2 = WW_THREADS / NQ2;
-  (void)NQ2;
+  // NC = 2: the partial product of z slice c over all OUT columns; NC = 8 (two-hop): all R z rows
+  // for the OUT / NC columns of slice c
+  const int NC = ww_nc(R), ZC = R / NC, S = R, OUT = S + R;
+  const bool two = NC == 8;
+  const int OC = two ? OUT / NC : OUT, NQ2 = OC / 4, NKS2 = WW_THREADS / NQ2;
   const size_t base = out.size();
   out.resize(base + (size_t)WW_SOK * WW_THREADS * 4);
   for (int tid = 0; tid < WW_THREADS; ++tid) {
     const int q2 = tid / NKS2, ks2 = tid % NKS2;
     for (int kk = 0; kk < WW_SOK; ++kk) {
-      const int zrow = c * ZC + ks2 * WW_SOK + kk;
+      const int zrow = two ? ks2 * WW_SOK + kk : c * ZC + ks2 * WW_SOK + kk;
       for (int e = 0; e < 4; ++e) {
-        const int col = 4 * q2 + e;
+        const int col = (two ? c * OC : 0) + 4 * q2 + e;
         out[base + ((size_t)kk * WW_THREADS + tid) * 4 + e] =
             col < S ? skip[(size_t)zrow * S + col] : outk[(size_t)zrow * R + (col - S)];
       }
