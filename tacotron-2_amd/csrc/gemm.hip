@@ -572,6 +572,128 @@ __global__ __launch_bounds__(256, 1) void gemm_sk_kernel(GemmArgs g, int kslice)
   epilogue_tile(g, acc, rw, n0 + cw, lane);
 }
 
+// ---- register-direct skinny bf16 product (training: M <= 64 rows per decoder step) -------------
+// C[M<=64][N] = A[M][K] (fp32, rounded to bf16 as staged) · B (pre-transposed bf16 Bt16[N][ldbt]).
+// One work-group = 64 rows x 128 columns x one K slice (blockIdx.z) of <= 32·RD_KT; wave w owns
+// columns [32w, 32w+32) as 4 x 2 v_mfma_f32_16x16x32_bf16 accumulators.  The B fragments are loaded
+// straight from Bt16 into registers (a lane's 8 k of one column are 16 contiguous bytes in the
+// pre-transposed layout: no LDS round trip, no barrier between the weight stream and the MFMAs),
+// the whole slice at once; only A (64 rows, shared by the 4 waves, L2-resident) is staged in LDS.
+constexpr int RD_BN = 128, RD_KT = 12;
+constexpr int RD_AG = (64 * RD_KT * 32 / 8 + 255) / 256;  // 8-element A groups per thread (12)
+__host__ __device__ constexpr int rd_ld(int kslice) { return kslice + 8; }  // padded k stride (bf16)
+size_t rd_lds_bytes(int kslice) { return (size_t)64 * rd_ld(kslice) * 2; }
+
+__device__ __forceinline__ void epilogue_one(const GemmArgs& g, int row, int col, float acc) {
+  float y = acc + (g.bias ? g.bias[col] : 0.f);
+  if (g.act == ACT_RELU) y = fmaxf(y, 0.f);
+  else if (g.act == ACT_TANH) y = tanhf(y);
+  if (g.bn_scale) y = y * g.bn_scale[col] + g.bn_shift[col];
+  if (g.act == ACT_BN_RELU) y = fmaxf(y, 0.f);
+  if (g.residual) y = g.residual[(long)row * g.ldr + col] + y;
+  if (g.clip) y = fminf(fmaxf(y, g.clip_lo), g.clip_hi);
+  g.Cout[(long)row * g.ldc + col] = y;
+}
+
+__global__ __launch_bounds__(256, 1) void gemm_rd_kernel(GemmArgs g, int kslice) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 rd_sm[];
+  const int LD = rd_ld(kslice);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n0 = blockIdx.x * RD_BN, k0 = blockIdx.z * kslice;
+  const int kend = min(g.K, k0 + kslice);
+  const int nks = (kend - k0 + 31) >> 5;  // 32-deep steps of this slice (<= RD_KT, host-checked)
+  const int g8 = kslice >> 3, ng = 64 * g8;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  // A slice -> registers first (L2 hits, back before the weight stream)
+  f32x4 va[RD_AG][2];
+#pragma unroll
+  for (int u = 0; u < RD_AG; ++u) {
+    va[u][0] = z4;
+    va[u][1] = z4;
+    const int idx = tid + 256 * u;
+    if (idx < ng) {
+      const int r = idx / g8, k = k0 + (idx - r * g8) * 8;
+      if (r < g.M && k < kend) {  // K % 8 == 0, 16-byte aligned rows (rd_plan): whole groups
+        const float* p = g.A + (long)r * g.lda + k;
+        va[u][0] = *reinterpret_cast<const f32x4*>(p);
+        va[u][1] = *reinterpret_cast<const f32x4*>(p + 4);
+      }
+    }
+  }
+  // every B fragment of the slice: lane -> column (lane & 15) of block cb, k = 32s + 8(lane >> 4)
+  bf16x8 vb[RD_KT][2];
+  const __bf16* Bt = reinterpret_cast<const __bf16*>(g.Bt16);
+#pragma unroll
+  for (int s = 0; s < RD_KT; ++s)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      for (int e = 0; e < 8; ++e) vb[s][cb][e] = (__bf16)0.f;
+      const int col = n0 + 32 * w + 16 * cb + (lane & 15), k = k0 + 32 * s + 8 * (lane >> 4);
+      if (s < nks && col < g.N && k < kend) vb[s][cb] = *reinterpret_cast<const bf16x8*>(Bt + (long)col * g.ldbt + k);
+    }
+#pragma unroll
+  for (int u = 0; u < RD_AG; ++u) {
+    const int idx = tid + 256 * u;
+    if (idx < ng) {
+      const int r = idx / g8, kk = (idx - r * g8) * 8;
+      bf16x8 h;
+      to_bf16x8(reinterpret_cast<const float*>(&va[u][0]), h);
+      *reinterpret_cast<bf16x8*>(rd_sm + r * LD + kk) = h;
+    }
+  }
+  __syncthreads();
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc[mb][0] = acc[mb][1] = z4;
+  const __bf16* pa = rd_sm + (lane & 15) * LD + 8 * (lane >> 4);
+#pragma unroll
+  for (int s = 0; s < RD_KT; ++s) {
+    if (s < nks) {
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(pa + 16 * mb * LD + 32 * s);
+        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, vb[s][0], acc[mb][0], 0, 0, 0);
+        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, vb[s][1], acc[mb][1], 0, 0, 0);
+      }
+    }
+  }
+  // D layout: lane -> column lane & 15, rows 4(lane >> 4) + r of each 16 x 16 block
+  const bool part = g.ksplit > 1 || g.raw;
+  float* P = part ? g.kpart + (long)blockIdx.z * g.M * g.N : nullptr;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int col = n0 + 32 * w + 16 * cb + (lane & 15);
+    if (col >= g.N) continue;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * mb + 4 * (lane >> 4) + r;
+        if (row >= g.M) continue;
+        if (part) P[(long)row * g.N + col] = acc[mb][cb][r];
+        else epilogue_one(g, row, col, acc[mb][cb][r]);
+      }
+  }
+}
+
+// K split / slice of the register-direct kernel: ~one work-group per CU, slice <= 32·RD_KT
+static bool rd_plan(const GemmArgs& a, int& ks, int& kslice) {
+  if (a.split16 != 2 || !a.Bt16 || a.a_mode != A_DENSE || a.M > 64 || a.K < 32 || a.K % 8 || a.lda % 4 ||
+      (reinterpret_cast<uintptr_t>(a.A) & 15))
+    return false;
+  const int nt = (a.N + RD_BN - 1) / RD_BN;
+  ks = std::max(1, std::min(a.K / 32, 256 / std::max(nt, 1)));
+  for (;;) {
+    kslice = ((a.K + ks - 1) / ks + 31) / 32 * 32;
+    if (kslice <= 32 * RD_KT) break;
+    ++ks;
+  }
+  ks = (a.K + kslice - 1) / kslice;  // no empty slices
+  if (ks > 1 && !a.kpart) return false;
+  if (ks > 1 && (long)ks * a.M * a.N > a.kpart_floats) return false;
+  return true;
+}
+
 // K split / slice of the skinny kernel: ~one work-group per CU, slice <= SK_KMAX (LDS), multiple of 32
 constexpr int SK_KMAX = 608;
 static bool sk_plan(const GemmArgs& a, int& ks, int& kslice) {
@@ -636,11 +758,29 @@ int gemm_impl(const GemmArgs& a, hipStream_t s) {
     TT2_CHECK(!a.Bt16 || (al16(a.Bt16) && a.ldbt % 8 == 0 && (a.split16 == 2 || (a.Bt16lo && al16(a.Bt16lo)))),
               TT2_ERR_INVALID_ARG, "gemm: Bt16 needs 16-byte alignment, ldbt % 8 == 0 (and Bt16lo for split16 == 1)");
     int sks = 0, skl = 0;
-    static const bool sk_on = [] {  // opt-in (TT2_GEMM_SKINNY=1): measured no faster, DESIGN §5.6
-      const char* e = std::getenv("TT2_GEMM_SKINNY");
-      return e && e[0] == '1';
+    static const int sk_mode = [] {  // TT2_GEMM_SKINNY: 2 (default) = register-direct kernel, 1 =
+      const char* e = std::getenv("TT2_GEMM_SKINNY");  // LDS-staged skinny kernel, 0 = gemm_x3_kernel
+      return e ? std::atoi(e) : 2;                     // (A/B: DESIGN §5.6)
     }();
-    if (sk_on && sk_plan(a, sks, skl)) {  // skinny bf16 product with pre-transposed weights
+    if (sk_mode == 2 && rd_plan(a, sks, skl)) {
+      GemmArgs g = a;
+      g.ksplit = sks;
+      static bool rd_attr = false;
+      if (!rd_attr) {
+        TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_rd_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)rd_lds_bytes(32 * RD_KT)));
+        rd_attr = true;
+      }
+      dim3 grid(cdiv(a.N, RD_BN), 1, sks);
+      hipLaunchKernelGGL(gemm_rd_kernel, grid, dim3(256), rd_lds_bytes(skl), s, g, skl);
+      TT2_HIP(hipGetLastError());
+      if (sks > 1 && !g.raw) {
+        hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)a.M * a.N + 1023) / 1024)), dim3(256), 0, s, g);
+        TT2_HIP(hipGetLastError());
+      }
+      return sks;
+    }
+    if (sk_mode == 1 && sk_plan(a, sks, skl)) {  // skinny bf16 product with pre-transposed weights
       GemmArgs g = a;
       g.ksplit = sks;
       const bool vsk = va && a.lda % 4 == 0;
