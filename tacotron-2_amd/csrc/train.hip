@@ -195,12 +195,36 @@ __global__ __launch_bounds__(256) void k_tr_colsum_part(const float* __restrict_
     part[(long)s * N + n] = v;
   }
 }
-__global__ void k_tr_colsum_final(const float* __restrict__ part, int S, int N, float* __restrict__ out) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float acc = 0.f;
-  for (int s = 0; s < S; ++s) acc += part[(long)s * N + n];
-  out[n] = acc;
+// Final pass of a split column reduction: Σ_s part[s·ld + n] for 32 columns per 1024-thread block
+// (32 row groups x 8 independent accumulators: S = 512 partials are 2 rounds of loads, not 512
+// dependent ones).  Valid on threads < 32 (row group 0); every thread must call it.
+constexpr int TR_FIN = 1024;
+__device__ __forceinline__ float colsum_fin(const float* __restrict__ part, int S, long ld, int n, bool ok,
+                                            float* red /* [32][33] */) {
+  const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (ok)
+    for (int s0 = g; s0 < S; s0 += 256) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int sp = s0 + 32 * u;
+        if (sp < S) acc[u] += part[(long)sp * ld + n];
+      }
+    }
+  red[g * 33 + c] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  float tot = 0.f;
+  if (g == 0)
+    for (int i = 0; i < 32; ++i) tot += red[i * 33 + c];
+  __syncthreads();
+  return tot;
+}
+__global__ __launch_bounds__(TR_FIN) void k_tr_colsum_final(const float* __restrict__ part, int S, int N,
+                                                            float* __restrict__ out) {
+  __shared__ float red[32 * 33];
+  const int n = blockIdx.x * 32 + (threadIdx.x & 31);
+  const float tot = colsum_fin(part, S, N, n, n < N, red);
+  if (threadIdx.x < 32 && n < N) out[n] = tot;
 }
 
 __global__ void k_tr_to_bf16(const float* __restrict__ src, long n, __bf16* __restrict__ dst) {
@@ -394,6 +418,89 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy(TrAtt a) {
   }
 }
 
+// Same energies with 256 threads (A <= 128): the lane's two W_loc columns live in registers (64
+// VGPRs, loaded once from L2), so a row costs 8 broadcast 16-byte LDS reads of its location features
+// instead of 64 LDS reads per column pair; the wave's 4 rows have their keys prefetched with the
+// staging loads.  Four 256-thread work-groups fit a CU where one 1024-thread one did: the (j-tile,
+// row) grid runs in one wave of work-groups.
+constexpr int TR_E2T = 256;
+__global__ __launch_bounds__(TR_E2T) void k_tr_att_energy2(TrAtt a) {
+  __shared__ float cseg[TR_JT + 64];
+  __shared__ __attribute__((aligned(16))) float f[TR_JT * 32];
+  __shared__ float Kcs[65 * 32];
+  const int b = blockIdx.y, j0 = blockIdx.x * TR_JT, tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int F = a.F, A = a.A, Tin = a.Tin, pad = (a.KW - 1) / 2;
+  const long tb = (long)a.t * a.B + b;
+  const int k0 = lane, k1 = lane + 64;
+  const bool ok0 = k0 < A, ok1 = k1 < A;
+  float wl0[32], wl1[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    wl0[c] = (c < F && ok0) ? a.Wl[c * A + k0] : 0.f;
+    wl1[c] = (c < F && ok1) ? a.Wl[c * A + k1] : 0.f;
+  }
+  float key0[4], key1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = j0 + w + 4 * r;
+    const bool jok = j < Tin;
+    key0[r] = (jok && ok0) ? a.keys[((long)b * Tin + j) * A + k0] : 0.f;
+    key1[r] = (jok && ok1) ? a.keys[((long)b * Tin + j) * A + k1] : 0.f;
+  }
+  const float* q = a.Q + tb * A;
+  const float qb0 = ok0 ? q[k0] + a.ba[k0] : 0.f, qb1 = ok1 ? q[k1] + a.ba[k1] : 0.f;
+  const float va0 = ok0 ? a.va[k0] : 0.f, va1 = ok1 ? a.va[k1] : 0.f;
+  const float* cum_prev = a.CUM + tb * Tin;
+  for (int i = tid; i < TR_JT + a.KW - 1; i += TR_E2T) {
+    const int j = j0 + i - pad;
+    cseg[i] = (j >= 0 && j < Tin) ? cum_prev[j] : 0.f;
+  }
+  for (int i = tid; i < a.KW * F; i += TR_E2T) Kcs[i] = a.Kc[i];
+  __syncthreads();
+  for (int i = tid; i < TR_JT * 32; i += TR_E2T) {  // location features (attention.py:193-195)
+    const int jj = i >> 5, c = i & 31;
+    float acc = 0.f;
+    if (c < F) {
+      acc = a.bc[c];
+      for (int tap = 0; tap < a.KW; ++tap) acc += cseg[jj + tap] * Kcs[tap * F + c];
+      if (j0 + jj < Tin) a.FALL[(tb * Tin + j0 + jj) * F + c] = acc;
+    }
+    f[i] = acc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int jj = w + 4 * r, j = j0 + jj;
+    if (j >= Tin) break;
+    const f32x4* fr = reinterpret_cast<const f32x4*>(f + jj * 32);
+    float u0 = key0[r] + qb0, u1 = key1[r] + qb1;
+#pragma unroll
+    for (int c4 = 0; c4 < 8; ++c4) {
+      const f32x4 fv = fr[c4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        u0 += fv[e] * wl0[4 * c4 + e];
+        u1 += fv[e] * wl1[4 * c4 + e];
+      }
+    }
+    float acc = 0.f;
+    const long hrow = (tb * Tin + j) * A;
+    if (ok0) {
+      const float th = tanhf(u0);
+      a.TH[hrow + k0] = th;
+      acc += va0 * th;
+    }
+    if (ok1) {
+      const float th = tanhf(u1);
+      a.TH[hrow + k1] = th;
+      acc += va1 * th;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) a.E[(long)b * Tin + j] = acc;
+  }
+}
+
 // Masked softmax (attention.py:218, TF _maybe_mask_score) recomputed by every block of the row,
 // cumulative alignments (:222-225) by block 0, then context_t = align_t · values (:27)
 // -> PIN[t][b][H:], X1[t+1][b][P:P+D].
@@ -502,14 +609,32 @@ __global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const f
 }
 // out[0] = before loss, out[1] = stop loss; masked (ns = 0): the stop normaliser is the count of
 // nonzero masked losses, also stored in out[5] for k_tr_div
-__global__ void k_tr_loss_final(const float* __restrict__ part, int nb, long nf, long ns, float* __restrict__ out) {
-  if (threadIdx.x != 0) return;
+// fixed-order double tree over the 256 threads of the block (every thread calls it; result on all)
+__device__ __forceinline__ double block_sum256_d(double v, double* sd) {
+  const int tid = threadIdx.x;
+  sd[tid] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) sd[tid] += sd[tid + o];
+    __syncthreads();
+  }
+  const double r = sd[0];
+  __syncthreads();
+  return r;
+}
+__global__ __launch_bounds__(256) void k_tr_loss_final(const float* __restrict__ part, int nb, long nf, long ns,
+                                                       float* __restrict__ out) {
+  __shared__ double sd[256];
   double sq = 0, ce = 0, nz = 0;
-  for (int i = 0; i < nb; ++i) {
+  for (int i = threadIdx.x; i < nb; i += 256) {
     sq += part[3 * i];
     ce += part[3 * i + 1];
     nz += part[3 * i + 2];
   }
+  sq = block_sum256_d(sq, sd);
+  ce = block_sum256_d(ce, sd);
+  nz = block_sum256_d(nz, sd);
+  if (threadIdx.x != 0) return;
   out[0] = (float)(sq / (double)nf);
   const double cnt = ns > 0 ? (double)ns : nz;
   out[1] = (float)(ce / cnt);
@@ -694,6 +819,130 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy_bwd(TrAtt a) {
   }
 }
 
+// Sum over all 64 lanes of each of 32 per-lane values (butterfly reduce-scatter, 32 shuffles): lane l
+// returns the total of p[l >> 1].
+__device__ __forceinline__ float wave_reduce_scatter32(float (&p)[32], int lane) {
+  float q[16], r[8], u[4], v2[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bool hi = lane & 32;
+    q[i] = (hi ? p[16 + i] : p[i]) + __shfl_xor(hi ? p[i] : p[16 + i], 32, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bool hi = lane & 16;
+    r[i] = (hi ? q[8 + i] : q[i]) + __shfl_xor(hi ? q[i] : q[8 + i], 16, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool hi = lane & 8;
+    u[i] = (hi ? r[4 + i] : r[i]) + __shfl_xor(hi ? r[i] : r[4 + i], 8, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const bool hi = lane & 4;
+    v2[i] = (hi ? u[2 + i] : u[i]) + __shfl_xor(hi ? u[i] : u[2 + i], 4, 64);
+  }
+  const bool hi = lane & 2;
+  const float x = (hi ? v2[1] : v2[0]) + __shfl_xor(hi ? v2[0] : v2[1], 2, 64);
+  return x + __shfl_xor(x, 1, 64);
+}
+
+// k_tr_att_energy_bwd with 256 threads (A <= 128, F <= 32, D % 4 == 0, D <= 1024): wave w owns rows
+// w + 4r of the tile; the lane's two W_loc columns in registers turn d f = du·W_locᵀ into 64 FMAs +
+// one 32-value butterfly reduction per row instead of an LDS-staged transposed W_loc; every global
+// operand of a row pair is loaded before its arithmetic.
+__global__ __launch_bounds__(TR_E2T) void k_tr_att_energy_bwd2(TrAtt a) {
+  __shared__ __attribute__((aligned(16))) float dctx[1024];
+  __shared__ float racc[2][4][128];
+  __shared__ float s16[16];
+  const int b = blockIdx.y, tile = blockIdx.x, j0 = tile * TR_JT, tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int F = a.F, A = a.A, Tin = a.Tin, D = a.D;
+  const long tb = (long)a.t * a.B + b;
+  const int len = a.lens[b];
+  const int k0 = lane, k1 = lane + 64;
+  const bool ok0 = k0 < A, ok1 = k1 < A;
+  float wl0[32], wl1[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    wl0[c] = (c < F && ok0) ? a.Wl[c * A + k0] : 0.f;
+    wl1[c] = (c < F && ok1) ? a.Wl[c * A + k1] : 0.f;
+  }
+  const float va0 = ok0 ? a.va[k0] : 0.f, va1 = ok1 ? a.va[k1] : 0.f;
+  float sp = 0.f;
+  for (int n = tid; n < D; n += TR_E2T) {
+    const float v = a.dPIN[tb * (a.H + D) + a.H + n] + a.dX1[(tb + a.B) * (a.P + D + a.H) + a.P + n];
+    dctx[n] = v;
+    if (tile == 0) a.DCTX[tb * D + n] = v;
+    sp += v * a.PIN[tb * (a.H + D) + a.H + n];
+  }
+  // s = Σ_j a_j da_j = dctx·ctx_t + Σ_j a_j dcum_j (every tile gets it without the other tiles' da)
+  for (int j = tid; j < len; j += TR_E2T) sp += a.ALN[tb * Tin + j] * a.DCUM[(long)b * Tin + j];
+  const float s = block_sum(sp, s16);  // its barriers also publish dctx
+  float dv0 = 0.f, dv1 = 0.f, dq0 = 0.f, dq1 = 0.f;
+  const f32x4* d4 = reinterpret_cast<const f32x4*>(dctx);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = j0 + w + 4 * r;
+    if (j >= Tin) break;
+    // d align_j = dctx·values_j + d cum_t[j] (16-byte loads of the values row: the dominant read)
+    const f32x4* v4 = reinterpret_cast<const f32x4*>(a.values + ((long)b * Tin + j) * D);
+    f32x4 vv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vv[i] = (lane + 64 * i) * 4 < D ? v4[lane + 64 * i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    const long hrow = (tb * Tin + j) * A, krow = ((long)b * Tin + j) * A;
+    const float th0 = ok0 ? a.TH[hrow + k0] : 0.f, th1 = ok1 ? a.TH[hrow + k1] : 0.f;
+    const float dk0 = ok0 ? a.DKEYS[krow + k0] : 0.f, dk1 = ok1 ? a.DKEYS[krow + k1] : 0.f;
+    const float aln = a.ALN[tb * Tin + j], dcum = a.DCUM[(long)b * Tin + j];
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if ((lane + 64 * i) * 4 < D) {
+        const f32x4 y = d4[lane + 64 * i];
+        acc += vv[i][0] * y[0] + vv[i][1] * y[1] + vv[i][2] * y[2] + vv[i][3] * y[3];
+      }
+    }
+    acc = wave_sum(acc);
+    const float de = j < len ? aln * ((acc + dcum) - s) : 0.f;
+    const float du0 = de * va0 * (1.f - th0 * th0), du1 = de * va1 * (1.f - th1 * th1);
+    dv0 += de * th0;
+    dv1 += de * th1;
+    dq0 += du0;
+    dq1 += du1;
+    if (ok0) {
+      a.DKEYS[krow + k0] = dk0 + du0;
+      a.TH[hrow + k0] = du0;  // d W_loc = FALL^T · du after the loop
+    }
+    if (ok1) {
+      a.DKEYS[krow + k1] = dk1 + du1;
+      a.TH[hrow + k1] = du1;
+    }
+    float p[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) p[c] = du0 * wl0[c] + du1 * wl1[c];
+    const float dfc = wave_reduce_scatter32(p, lane);
+    if ((lane & 1) == 0 && (lane >> 1) < F) a.DF[((long)b * Tin + j) * F + (lane >> 1)] = dfc;
+  }
+  if (ok0) {
+    racc[0][w][k0] = dv0;
+    racc[1][w][k0] = dq0;
+  }
+  if (ok1) {
+    racc[0][w][k1] = dv1;
+    racc[1][w][k1] = dq1;
+  }
+  __syncthreads();
+  if (tid < A) {
+    const float sv = (racc[0][0][tid] + racc[0][1][tid]) + (racc[0][2][tid] + racc[0][3][tid]);
+    const float sq = (racc[1][0][tid] + racc[1][1][tid]) + (racc[1][2][tid] + racc[1][3][tid]);
+    const long pt = (long)b * a.nt + tile;
+    a.PQ[pt * A + tid] = sq;
+    a.dV[pt * A + tid] += sv;
+    a.dBA[pt * A + tid] += sq;
+  }
+}
+
 // (2) d query (sum of the tile partials), location-conv backward: per-tile partials of d Kc and
 // d bc, and d cum_{t-1}[i] = d cum_t[i] + Σ_tap,c df[i - tap + pad][c]·Kc[tap][c]
 __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
@@ -746,6 +995,44 @@ __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
   }
 }
 
+// d W_loc (location_features_layer, attention.py:59-62) = Σ_r f[r][c]·du[r][k] over all R = T·B·T_in
+// rows of FALL [R][F] and the du copy in TH [R][A], on fp32 MFMA (v_mfma_f32_32x32x2f32, exact fp32
+// products): one streaming pass over the two fp32 arrays instead of a transpose, two bf16 copies and a
+// K = R library GEMM.  Work-group = 4 waves, wave w owns output columns [32w, 32w+32) (A <= 128,
+// F <= 32); rows [blockIdx.x·rpb, +rpb), 16 row pairs per round with every load issued first;
+// partial [F][A] per work-group (summed by tr_colsum).
+typedef float tr_f32x16 __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(256) void k_tr_dwloc(const float* __restrict__ f, const float* __restrict__ du, long R,
+                                                  int F, int A, long rpb, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long r0 = (long)blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+  const int c = lane & 31, h = lane >> 5, k = 32 * w + (lane & 31);
+  const bool cok = c < F, kok = k < A;
+  tr_f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  for (long rb = r0; rb < r1; rb += 32) {
+    float av[16], bv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const long rr = rb + 2 * u + h;
+      const bool ok = rr < r1;
+      av[u] = (ok && cok) ? f[rr * F + c] : 0.f;
+      bv[u] = (ok && kok) ? du[rr * A + k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+  }
+  // D: column k (lane & 31), row c' = (q & 3) + 8 (q >> 2) + 4h
+  float* P = part + (long)blockIdx.x * F * A;
+  if (kok)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int cr = (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (cr < F) P[(long)cr * A + k] = acc[q];
+    }
+}
+
 // prenet backward through dropout + ReLU: dz = (p > 0) ? 2·dp : 0   (p = relu(z)/0.5·keep)
 __global__ void k_tr_prenet_bwd(const float* __restrict__ dp, long ld_dp, const float* __restrict__ p, long ld_p,
                                 long M, int N, float* __restrict__ dz) {
@@ -785,10 +1072,13 @@ __global__ __launch_bounds__(256) void k_tr_sumsq(const float* __restrict__ g, l
   acc = block_sum(acc, s4);
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
-__global__ void k_tr_sum_final(const float* __restrict__ part, int nb, float scale, float* __restrict__ out, int sq) {
-  if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(256) void k_tr_sum_final(const float* __restrict__ part, int nb, float scale,
+                                                      float* __restrict__ out, int sq) {
+  __shared__ double sd[256];
   double s = 0;
-  for (int i = 0; i < nb; ++i) s += part[i];
+  for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+  s = block_sum256_d(s, sd);
+  if (threadIdx.x != 0) return;
   out[0] = sq ? (float)sqrt(s) : (float)(s * scale);
 }
 
@@ -834,12 +1124,12 @@ __global__ __launch_bounds__(256) void k_pn_colstat_part(const float* __restrict
     part[(long)sp * N + n] = v;
   }
 }
-__global__ void k_pn_colstat_final(const float* __restrict__ part, int S, int N, float scale, float* __restrict__ out) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float acc = 0.f;
-  for (int sp = 0; sp < S; ++sp) acc += part[(long)sp * N + n];
-  out[n] = acc * scale;
+__global__ __launch_bounds__(TR_FIN) void k_pn_colstat_final(const float* __restrict__ part, int S, int N, float scale,
+                                                             float* __restrict__ out) {
+  __shared__ float red[32 * 33];
+  const int n = blockIdx.x * 32 + (threadIdx.x & 31);
+  const float tot = colsum_fin(part, S, N, n, n < N, red);
+  if (threadIdx.x < 32 && n < N) out[n] = tot * scale;
 }
 // y = gamma (a - mean) rsqrt(var + eps) + beta, then dropout(0.5) with keep bits (or identity)
 __global__ void k_pn_bn_fwd(const float* __restrict__ a, long M, int C, const float* __restrict__ mean,
@@ -890,15 +1180,14 @@ __global__ __launch_bounds__(256) void k_pn_bn_bwd_part(const float* __restrict_
   }
 }
 // finalize: d beta = S1, d gamma = S2 (written into the gradient slots)
-__global__ void k_pn_bn_bwd_final(const float* __restrict__ part, int S, int C, float* __restrict__ sums,
-                                  float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int sp = 0; sp < S; ++sp) {
-    s1 += part[(long)sp * 2 * C + c];
-    s2 += part[(long)sp * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(TR_FIN) void k_pn_bn_bwd_final(const float* __restrict__ part, int S, int C,
+                                                            float* __restrict__ sums, float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta) {
+  __shared__ float red[32 * 33];
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const float s1 = colsum_fin(part, S, 2L * C, c, c < C, red);
+  const float s2 = colsum_fin(part + C, S, 2L * C, c, c < C, red);
+  if (threadIdx.x >= 32 || c >= C) return;
   sums[c] = s1;
   sums[C + c] = s2;
   dbeta[c] = s1;
@@ -998,7 +1287,7 @@ static void tr_colsum(tt2_train_ctx* c, const float* in, long M, int N, long ld,
   const int S = tr_splits(M, N, 64 * std::max<long>(4L * c->H, c->LX1));
   hipLaunchKernelGGL(k_tr_colsum_part, dim3((N + tr_tw(N) - 1) / tr_tw(N), S), dim3(256), 0, s, in, M, N, ld,
                      c->part.as<float>());
-  hipLaunchKernelGGL(k_tr_colsum_final, dim3((N + 255) / 256), dim3(256), 0, s, c->part.as<float>(), S, N, out);
+  hipLaunchKernelGGL(k_tr_colsum_final, dim3((N + 31) / 32), dim3(TR_FIN), 0, s, c->part.as<float>(), S, N, out);
 }
 
 // per calling thread: the context a tt2_train_* call is driving (a call runs on one thread, so
@@ -1288,7 +1577,7 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
   const unsigned CT = (unsigned)((C + tr_tw(C) - 1) / tr_tw(C));
   auto colstat = [&](const float* x, const float* ctr, int mode, float* out) {
     hipLaunchKernelGGL(k_pn_colstat_part, dim3(CT, S), dim3(256), 0, s, x, M, C, ctr, mode, part);
-    hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, out);
+    hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 31) / 32), dim3(TR_FIN), 0, s, part, S, C, 1.0f / (float)M, out);
   };
   auto conv_in = [&](int i, GemmArgs& g) {  // layer i's input as an implicit-im2col conv1d operand
     if (i == 0) {  // clipped decoder frames, time-major [T][B][NM]
@@ -1322,7 +1611,7 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
   hipLaunchKernelGGL(k_pn_after_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->PPRJ.as<float>(), tg, B, T,
                      NM, c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dPP.as<float>(), c->part.as<float>(),
                      tlen, (float)(1.0 / nmse));
-  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, (float)(1.0 / nmse),
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 256, (float)(1.0 / nmse),
                      red + 4, 0);
   // backward: projection
   tr_transpose(c->PX[L].as<float>(), M, C, C, TBUF, M, s);
@@ -1339,7 +1628,7 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
     hipLaunchKernelGGL(k_pn_bn_bwd_part, dim3(CT, S), dim3(256), 0, s, dxn,
                        pnm ? pnm + (long)i * M * C : nullptr, c->PA[i].as<float>(), M, C, mean, var, eps,
                        c->DYb.as<float>(), part);
-    hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, sums,
+    hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 31) / 32), dim3(TR_FIN), 0, s, part, S, C, sums,
                        gvar(c, sc + "batch_normalization/gamma"), gvar(c, sc + "batch_normalization/beta"));
     hipLaunchKernelGGL(k_pn_bn_bwd_dz, dim3(nblk(M * C)), dim3(256), 0, s, c->DYb.as<float>(), c->PA[i].as<float>(),
                        M, C, mean, var, eps, pvar(c, sc + "batch_normalization/gamma"), sums, i < L - 1 ? 1 : 0,
@@ -1457,6 +1746,10 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   const int NT = (Tin + TR_JT - 1) / TR_JT;
   at.nt = NT;
   const dim3 att_grid(NT, B);
+  static const bool tr_e2 = [] {  // TT2_TR_E2=0: the 1024-thread energy kernel (A/B)
+    const char* e = std::getenv("TT2_TR_E2");
+    return !(e && e[0] == '0');
+  }();
   const unsigned bh = nblk((long)B * H);
 
   // teacher-forcing draw (TacoTrainingHelper.next_inputs, helpers.py:122-133): a step fed its own
@@ -1501,7 +1794,8 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
             c->Q.as<float>() + s1 * A, A, s, nullptr, nullptr, 0, ACT_NONE, &c->hWqT, H);
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(TR_AT), 0, s, at);
+    if (A <= 128 && tr_e2) hipLaunchKernelGGL(k_tr_att_energy2, att_grid, dim3(TR_E2T), 0, s, at);
+    else hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(TR_AT), 0, s, at);
     hipLaunchKernelGGL(k_tr_ctx, dim3((D + 63) / 64, B), dim3(256), sizeof(float) * Tin, s, at);
   }
   tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
@@ -1513,7 +1807,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
                      c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dFR.as<float>(), c->dST.as<float>(),
                      c->part.as<float>(), c->cfg.postnet ? c->CLIPM.as<uint8_t>() : nullptr, tlen,
                      (float)(1.0 / (double)nmse), c->cfg.pos_weight);
-  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, nmse, tlen ? 0L : TB, red);
+  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 256, nmse, tlen ? 0L : TB, red);
   if (tlen) hipLaunchKernelGGL(k_tr_div, dim3(nblk(TB)), dim3(256), 0, s, c->dST.as<float>(), TB, red + 5);
   c->pn_ran = false;
   if (c->cfg.postnet) tr_postnet(c, tg, pnm, T, s);
@@ -1531,7 +1825,8 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   for (int t = T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
     at.t = t;
-    hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(TR_AT), 0, s, at);
+    if (A <= 128 && D <= 1024 && D % 4 == 0 && tr_e2) hipLaunchKernelGGL(k_tr_att_energy_bwd2, att_grid, dim3(TR_E2T), 0, s, at);
+    else hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(TR_AT), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
     // LSTM-2 backward: d h2 = DQ·Wq^T (raw split-K) + d PIN[t][:, :H], combined in the cell kernel
     const int kq = tr_gemm_raw(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, s, &c->hWq, A);
@@ -1609,8 +1904,16 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_colsum(c, c->dBA.as<float>(), BNT, A, A, gvar(c, LAV("attention_bias")), s);
   {  // d W_loc = Σ_{t,b,j} f ⊗ du over all T·B·Tin rows
     const long R = TB * Tin;
-    tr_transpose(c->FALL.as<float>(), R, F, F, TBUF, R, s);
-    tr_gemm(F, A, (int)R, TBUF, R, c->TH.as<float>(), A, gvar(c, LAV("location_features_layer/kernel")), A, s);
+    if (F <= 32 && A <= 128) {  // one streaming fp32-MFMA pass (k_tr_dwloc), partials in TBUF
+      const long rpb = ((R + 511) / 512 + 31) / 32 * 32;
+      const int nbk = (int)((R + rpb - 1) / rpb);
+      hipLaunchKernelGGL(k_tr_dwloc, dim3(nbk), dim3(256), 0, s, c->FALL.as<float>(), c->TH.as<float>(), R, F, A, rpb,
+                         TBUF);
+      tr_colsum(c, TBUF, nbk, F * A, (long)F * A, gvar(c, LAV("location_features_layer/kernel")), s);
+    } else {
+      tr_transpose(c->FALL.as<float>(), R, F, F, TBUF, R, s);
+      tr_gemm(F, A, (int)R, TBUF, R, c->TH.as<float>(), A, gvar(c, LAV("location_features_layer/kernel")), A, s);
+    }
   }
   tr_colsum(c, c->dKC.as<float>(), BNT, KW * F, (long)KW * F,
             gvar(c, LAV("location_features_convolution/kernel")), s);
@@ -1639,7 +1942,7 @@ static void tr_regularize(tt2_train_ctx* c, hipStream_t s) {
                        c->cfg.reg_weight, c->part.as<float>() + 64 * nreg);
     ++nreg;
   }
-  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 64 * nreg, c->cfg.reg_weight,
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 64 * nreg, c->cfg.reg_weight,
                      c->red.as<float>() + 2, 0);
 }
 
@@ -1776,9 +2079,9 @@ static void fe_stats(tt2_train_ctx* c, const float* x, long M, int C, float* mea
   const unsigned CT = (unsigned)((C + tr_tw(C) - 1) / tr_tw(C));
   float* part = c->fpart.as<float>();
   hipLaunchKernelGGL(k_pn_colstat_part, dim3(CT, S), dim3(256), 0, s, x, M, C, nullptr, 0, part);
-  hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, mean);
+  hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 31) / 32), dim3(TR_FIN), 0, s, part, S, C, 1.0f / (float)M, mean);
   hipLaunchKernelGGL(k_pn_colstat_part, dim3(CT, S), dim3(256), 0, s, x, M, C, mean, 1, part);
-  hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, 1.0f / (float)M, var);
+  hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 31) / 32), dim3(TR_FIN), 0, s, part, S, C, 1.0f / (float)M, var);
 }
 // BN backward (batch statistics) from dy -> dz (act: 0 none, 2 relu' from the pre-BN activation)
 static void fe_bn_bwd(tt2_train_ctx* c, const float* dxn, const uint8_t* keep, const float* a, long M, int C,
@@ -1790,7 +2093,7 @@ static void fe_bn_bwd(tt2_train_ctx* c, const float* dxn, const uint8_t* keep, c
   const float eps = c->cfg.bn_eps;
   hipLaunchKernelGGL(k_pn_bn_bwd_part, dim3((unsigned)((C + tr_tw(C) - 1) / tr_tw(C)), S), dim3(256), 0, s, dxn, keep,
                      a, M, C, mean, var, eps, dy, part);
-  hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 255) / 256), dim3(256), 0, s, part, S, C, sums,
+  hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 31) / 32), dim3(TR_FIN), 0, s, part, S, C, sums,
                      gvar(c, sc + "batch_normalization/gamma"), gvar(c, sc + "batch_normalization/beta"));
   hipLaunchKernelGGL(k_pn_bn_bwd_dz, dim3(nblk(M * C)), dim3(256), 0, s, dy, a, M, C, mean, var, eps,
                      pvar(c, sc + "batch_normalization/gamma"), sums, act, dz);
@@ -2118,7 +2421,7 @@ static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s)
     c->f_ran = false;
   }
   hipLaunchKernelGGL(k_tr_sumsq, dim3(256), dim3(256), 0, s, c->grads, c->total, c->part.as<float>());
-  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(64), 0, s, c->part.as<float>(), 256, 1.f, red + 3, 1);
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 256, 1.f, red + 3, 1);
   const double b1 = c->cfg.adam_beta1, b2 = c->cfg.adam_beta2;
   const int t = std::max(1, global_step);
   const float lr_t = (float)(lr * std::sqrt(1.0 - std::pow(b2, t)) / (1.0 - std::pow(b1, t)));
