@@ -24,13 +24,19 @@ constexpr int PD_NREP = 8;    // replicas of the H1/H2 flag lines (32 pollers pe
 // Hidden unit q (0..3) of LSTM tile g: the four units of a tile are the four components of one AF
 // float4 (common.h af_idx), 16(g/4) + g%4 + 4q.  Tiles [32w, 32w+32) own units [128w, 128w+128).
 __host__ __device__ inline int pd_unit(int g, int q) { return 16 * (g >> 2) + (g & 3) + 4 * q; }
-enum { PD_F_PRE = 0, PD_F_H1, PD_F_H2, PD_F_E, PD_F_CTX, PD_F_PP, PD_NPH };
+enum { PD_F_PRE = 0, PD_F_H1, PD_F_H2, PD_F_E, PD_F_CTX, PD_F_PP, PD_F_QE, PD_F_CMB, PD_F_EO, PD_F_EMT, PD_NPH };
+// Tacotron_emt_attn 'multihead' in the persistent decoder (k_decode_persist<true>): the emotion query
+// (128) rides as 8 more projection tiles; 16 emotion work-groups own 2 rows each; the attn_emt dense
+// (KC -> 128) runs on the 64 emotion-query projection work-groups.
+constexpr int PD_ENT = 8;        // emotion-query projection tiles (128 = style_att_dim)
+constexpr int PD_EG0 = 240;      // first emotion work-group (rows 2(g-240), +1)
+constexpr int PD_EQ = 128;       // emotion query width = attn_emt dense output width
 
 struct PdArgs {
   unsigned* flags;  // [PD_NPH][PD_NB] hand-off tags (zeroed before every launch)
   unsigned* flags2; // [PD_NPH][8 groups][32] group-level tags of the all-producer waits
   int* ctl;         // [4]: done, n_steps, err, pad (zeroed before every launch)
-  unsigned* rflags; // [2: H1, H2][PD_NREP replicas][PD_NB] hand-off tags, one replica per consumer XCD group
+  unsigned* rflags; // [3: H1, H2, EMT][PD_NREP replicas][PD_NB] hand-off tags, one replica per consumer XCD group
   int B, T_in, max_iters, T_lim, nm;
   int stop_at_any, mask_encoder, cumulative, constraint, monotonic, win;
   float zo, one_m_zo;
@@ -71,11 +77,27 @@ struct PdArgs {
   float* align;   // [B][max_iters][T_in] step-major (tacotron.hip transposes after the launch) or null
   long long* stamps;  // diagnostic s_memrealtime stamps of one step (null = off)
   int stamp_step;
+  // Tacotron_emt_attn 'multihead' (k_decode_persist<true> only)
+  int K1;               // LSTM-1 critical rows per tile: P + E2 (+ 128 emotion block)
+  int e_Tv, e_Dv, e_KC, e_heads, e_dh;  // attended rows, value width, heads x Dv, heads, dims per head
+  const float* e_ke;    // [B][Tv][128] keys of the attended values (conv1d_1 + bias)
+  const float* e_val;   // [B][Tv][Dv] attended values
+  const float* e_qrow;  // [32][128] query bias per row
+  const float* e_vv;    // [dh] g·v/|v|
+  const float* e_ab;    // [dh] attention_b
+  const float* e_wd;    // [8 tiles][KC x 16] WF (x KG_SB): attn_emt dense kernel
+  const float* e_bd;    // [128] its bias
+  const float* e_spk;   // [B][128] refnet_spk (added to the dense output), or null
+  float* e_hist;        // [max_iters][B][heads][Tv] emotion alignments
+  unsigned long long* QEg;  // [2][8 K splits][32][128] emotion-query partial granules (x KG_SB)
+  float* CMBx;          // [2][32 x KC] AF emotion contexts (heads concatenated)
+  unsigned long long* EOg;  // [2][8 K splits][32][128] dense partial granules (x KG_SB)
+  float* EMTx;          // [2][32 x 128] AF emotion block of the next step's LSTM-1 input
 };
 
 size_t pd_lds_bytes();
 // True when this device can keep all PD_NB work-groups resident at once.
 bool pd_device_ok(int dev);
-void pd_launch(const PdArgs& a, hipStream_t s);
+void pd_launch(const PdArgs& a, hipStream_t s, bool emt = false);
 
 }  // namespace tt2

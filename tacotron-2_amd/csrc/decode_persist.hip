@@ -122,9 +122,10 @@ __device__ __forceinline__ bool pd_poll_all(const PdArgs& a, int ph, int nprod, 
 // Wave-level poll of the 32 producers [base, base+32) of h-phase r (0: H1, 1: H2) on this work-group's
 // replica of their flag line (replica g%8: 32 pollers per line).  Each wave waits only for the
 // producers of the rows it loads, so early waves start their MFMAs while late producers finish.
-__device__ __forceinline__ bool pd_poll_rep(const PdArgs& a, int ph, int r, int base, unsigned need, int lane) {
+__device__ __forceinline__ bool pd_poll_rep(const PdArgs& a, int ph, int r, int base, unsigned need, int lane,
+                                            int n = 32) {
   const unsigned* f = a.rflags + (r * PD_NREP + (blockIdx.x & (PD_NREP - 1))) * PD_NB + base;
-  return pd_spin(a, ph, lane, [&] { return lane >= 32 || pd_flag(f + lane) >= need; });
+  return pd_spin(a, ph, lane, [&] { return lane >= n || pd_flag(f + lane) >= need; });
 }
 
 // Block-level waits: wave 0 polls, the work-group joins at a barrier (result via LDS slot).
@@ -152,13 +153,19 @@ __device__ __forceinline__ bool pd_take(const PdArgs& a, int ph, const unsigned 
   long long t0 = 0;
   for (unsigned spin = 0;; ++spin) {
     bool ok = true;
-    if (active) {
+    if (active) {  // every load issued before any tag is compared (no short-circuit: a branch per
+                   // granule would let the compiler serialise the loads)
+      unsigned tags[N];
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off * 8, i * stride * 8, 16);  // sc1
         v[i] = __uint_as_float(x[0]);
-        ok = ok && x[1] == tag;
+        tags[i] = x[1];
       }
+      unsigned bad = 0u;
+#pragma unroll
+      for (int i = 0; i < N; ++i) bad |= tags[i] ^ tag;
+      ok = bad == 0u;
     }
     if (__all(ok)) return true;
     if ((spin & 31) == 0) {
@@ -238,6 +245,7 @@ __device__ __forceinline__ void tail_bar(int* ctr, unsigned& gen, int lane) {
     if (stp && tid == 0) stp[g * 32 + (i)] = __builtin_amdgcn_s_memrealtime();        \
   } while (0)
 
+template <bool EMT>
 __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* const sW1h = sm;              // [64 kg][64 lanes] f32x4: W1 recurrent rows of this tile
@@ -258,8 +266,13 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   const int g = blockIdx.x, tid_ = threadIdx.x;
   const int b = (g & 7) * 4 + ((g >> 3) & 3), j = g >> 5;
   const bool rowv = b < a.B;
-  const bool isproj = g < PD_NTILE * PD_KSP;
-  const int pn = g % PD_NTILE, pks = g / PD_NTILE;
+  // EMT: 8 more projection tiles = the emotion query (pn >= PD_NTILE, "q" blocks, which also run the
+  // attn_emt dense: output tile pn - PD_NTILE, K split pks); g >= PD_EG0: emotion rows 2(g-PD_EG0), +1
+  constexpr int NTL = EMT ? PD_NTILE + PD_ENT : PD_NTILE;
+  const bool isproj = g < NTL * PD_KSP;
+  const int pn = g % NTL, pks = g / NTL;
+  const bool isq = EMT && isproj && pn >= PD_NTILE;
+  const int K1S = EMT ? a.K1 : PD_P + PD_E2;  // LSTM-1 critical rows per tile
   const int T = a.T_in;
   const int sib0 = (b >> 2) + 8 * (b & 3);  // siblings of row b: sib0 + 32*jj
   long long* const stp0 = a.stamps;
@@ -271,7 +284,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   // projection sums are unscaled by KG_UNSCALE where they are consumed
   f32x4 w1p[2], w2i[8];                          // chain: L1 prenet rows, L2 input rows (8 waves)
   {
-    const f32x4* L1 = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * (PD_P + PD_E2) * 16);
+    const f32x4* L1 = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * K1S * 16);
     const f32x4* L2 = reinterpret_cast<const f32x4*>(a.l2_w + (long)g * PD_H * 16);
 #pragma unroll
     for (int i = 0; i < 2; ++i) w1p[i] = L1[(2 * w + i) * 64 + lane];  // pre-scaled (common.h)
@@ -288,7 +301,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   }
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   f32x4 wpc = zero4;
-  if (isproj && w < 4) {
+  if (isproj && w < 4 && !isq) {
     const f32x4* PW = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16);
     wpc = PW[(PD_H / 16 + 4 * pks + w) * 64 + lane];
   }
@@ -296,9 +309,15 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   const f32x4* const WPH = reinterpret_cast<const f32x4*>(a.proj_w + (long)pn * (PD_H + PD_E2) * 16) + (8 * pks) * 64;
   f32x4 w1c[4];  // L1 context rows, k-groups 16 + 4w + i of the tile
   {
-    const f32x4* W1C = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * (PD_P + PD_E2) * 16) + (PD_P / 16 + 4 * w) * 64;
+    const f32x4* W1C = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * K1S * 16) + (PD_P / 16 + 4 * w) * 64;
 #pragma unroll
     for (int i = 0; i < 4; ++i) w1c[i] = W1C[i * 64 + lane];
+  }
+  f32x4 w1e = zero4, wdf = zero4;  // EMT: L1 emotion-block rows (k-group 48 + w); dense fragment (q blocks)
+  if constexpr (EMT) {
+    w1e = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * K1S * 16)[((PD_P + PD_E2) / 16 + w) * 64 + lane];
+    if (isq && w < a.e_KC / 128)
+      wdf = reinterpret_cast<const f32x4*>(a.e_wd + (long)(pn - PD_NTILE) * a.e_KC * 16)[(pks * (a.e_KC / 128) + w) * 64 + lane];
   }
   f32x4 wl[2];
   {
@@ -338,6 +357,10 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   }
   f32x4 loc[2] = {zero4, zero4};  // location features of the next step (cum = 0)
   f32x4 accC0 = zero4, accC1 = zero4;  // L1 context rows of the next step (context(-1) = 0)
+  if constexpr (EMT) {  // the emotion block of step 0 (zero_state: refnet_spk alone), host-written at parity 1
+    const float* XE = a.EMTx + 32 * PD_EQ;
+    kg_mfma(pd_ld4(XE, (w * 2) * 64 + lane), pd_ld4(XE, (w * 2 + 1) * 64 + lane), w1e, accC0, accC1);
+  }
   f32x4 q1a = zero4, q1b = zero4, q2a = zero4, q2b = zero4;  // this wave's Q partials of RG1, RG2
   const long BP = (long)a.B * PD_P;
 
@@ -629,7 +652,12 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       f32x4 s0 = zero4, s1 = zero4;
       kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), WPH[w * 64 + lane], s0, s1);
       reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
-      PPh[tid] = G[tid];
+      if (isq) {  // emotion query: h2 rows are all of it -> granules for the emotion work-groups
+        const int m = tid >> 4, col = tid & 15;
+        pd_put(a.QEg + (((long)p * PD_KSP + pks) * 32 + m) * PD_EQ + 16 * (pn - PD_NTILE) + col, tg, G[tid]);
+      } else {
+        PPh[tid] = G[tid];
+      }
     }
     // ================= D: softmax, cumulative alignments, context (attention.py:10-35, 202-227) ==========
     PD_STAMP(9);
@@ -722,6 +750,9 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       if (tid < 64) pd_st(a.CTXx + p * 32 * PD_E2 + af_idx(b, 64 * j + tid), 0.f);
       if (tid == 64 && j == 0) pd_st(a.SSx + p * 32 + b, 0.f);
     }
+    if constexpr (EMT) {
+      if (tid == 0) si[6] = 1;  // emotion-stage failure flag (read after barriers below)
+    }
     pd_publish(a, PD_F_CTX, tg, tid);
     PD_STAMP(10);
     rec_half(a.H1x + p * 32 * PD_H, sW1h, 1, q1a, q1b, w, lane);  // RG1(t+1), 2nd half
@@ -738,7 +769,132 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       loc[i] = l;
     }
     // ================= E: projection partial, context rows =================
-    if (isproj) {
+    if constexpr (EMT) {
+      if (g >= PD_EG0) {  // emotion rows r0, r0+1 (Architecture_wrappers.py:228-240, multihead_attention.py:35-132)
+        const int r0 = 2 * (g - PD_EG0);
+        float* qe = red;         // [2][128] query
+        float* sco = red + 256;  // [2][heads][Tv] scores -> weights
+        float* vls = red + 256 + 2 * a.e_heads * a.e_Tv;  // [2][Tv][Dv] values of the two rows, when they fit
+        const int nv = a.e_Tv * a.e_Dv;
+        const bool vl = 256 + 2 * a.e_heads * a.e_Tv + 2 * nv <= 4096;
+        // the value loads are issued first and stored to LDS after the query take, so the two memory
+        // round trips overlap
+        float vt[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = tid + PD_NT * u, rr = e >= nv, b2 = r0 + rr;
+          vt[u] = (vl && e < 2 * nv && b2 < a.B) ? a.e_val[(long)b2 * nv + (e - rr * nv)] : 0.f;
+        }
+        {  // 4 of the 8 K-split partials per thread (threads 256.. take splits 4..7): few registers
+          const int row = r0 + ((tid >> 7) & 1), col = tid & 127, hs = tid >> 8;
+          float pv[PD_KSP / 2];
+          if (!pd_take<PD_KSP / 2>(a, PD_F_QE, a.QEg + (((long)p * PD_KSP + 4 * hs) * 32 + row) * PD_EQ, col, 32 * PD_EQ,
+                                   tg, true, pv))
+            si[6] = 0;
+          G[tid] = (pv[0] + pv[1]) + (pv[2] + pv[3]);
+        }
+        if (vl)
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (tid + PD_NT * u < 2 * nv) vls[tid + PD_NT * u] = vt[u];
+        __syncthreads();
+        if (tid < 256) qe[tid] = (G[tid] + G[256 + tid]) * KG_UNSCALE + a.e_qrow[(r0 + (tid >> 7)) * PD_EQ + (tid & 127)];
+        __syncthreads();
+        PD_STAMP(22);
+        if (!si[6]) return;
+        const int HT = a.e_heads * a.e_Tv;
+        {  // s = Σ_d normed_v·tanh(keys + q + attention_b): lane d of a 32-lane group per dim (dh <= 32),
+           // 16 scores per pass of 512 threads, the keys of 4 passes loaded before their arithmetic
+          const int dh = a.e_dh, d = tid & 31;
+          const float vvd = d < dh ? a.e_vv[d] : 0.f, abd = d < dh ? a.e_ab[d] : 0.f;
+          for (int s0 = 0; s0 < 2 * HT; s0 += 64) {
+            float kx[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int sidx = s0 + (tid >> 5) + 16 * u;
+              const int rr = sidx / HT, hh = (sidx % HT) / a.e_Tv, tv = sidx % a.e_Tv, b2 = r0 + rr;
+              kx[u] = (sidx < 2 * HT && b2 < a.B && d < dh) ? a.e_ke[((long)b2 * a.e_Tv + tv) * PD_EQ + hh * dh + d] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int sidx = s0 + (tid >> 5) + 16 * u;
+              const int rr = sidx / HT, hh = (sidx % HT) / a.e_Tv;
+              float x = 0.f;
+              if (sidx < 2 * HT && d < dh) x = vvd * tanh_fast(kx[u] + qe[rr * PD_EQ + hh * dh + d] + abd);
+#pragma unroll
+              for (int o = 16; o >= 1; o >>= 1) x += __shfl_xor(x, o, 32);
+              if (d == 0 && sidx < 2 * HT) sco[sidx] = x;
+            }
+          }
+        }
+        __syncthreads();
+        PD_STAMP(23);
+        for (int pr = w; pr < 2 * a.e_heads; pr += PD_NT / 64) {  // softmax over the attended rows, one
+          float* r = sco + pr * a.e_Tv;                            // (row, head) per wave, lanes over t
+          const float x = lane < a.e_Tv ? r[lane] : -INFINITY;     // (no mask: padded frames count)
+          float mx = x;
+          for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+          const float ex = lane < a.e_Tv ? expf(x - mx) : 0.f;
+          float sum = ex;
+          for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+          if (lane < a.e_Tv) r[lane] = ex / sum;
+        }
+        __syncthreads();
+        PD_STAMP(30);
+        {  // contexts, heads concatenated (_combine_heads): one AF float4 = k = i0 + 4c (c < 4, one head) of
+           // one row per thread, stored as ONE 16-byte write-through store
+          const int nq = a.e_KC / 4;
+          const auto rc = __builtin_amdgcn_make_buffer_rsrc(a.CMBx + (long)p * 32 * a.e_KC, (short)0, 0x7fffffff, 0x00020000);
+          for (int e = tid; e < 2 * nq; e += PD_NT) {
+            const int rr = e >= nq, q = e - rr * nq, b2 = r0 + rr;
+            const int i0 = 16 * (q >> 2) + (q & 3), hh = i0 / a.e_Dv, d0 = i0 - hh * a.e_Dv;
+            const float* al = sco + (rr * a.e_heads + hh) * a.e_Tv;
+            const float* v = vl ? vls + rr * nv + d0 : a.e_val + (long)min(b2, a.B - 1) * nv + d0;
+            float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+            for (int tv = 0; tv < a.e_Tv; ++tv) {
+              const float wt = al[tv];
+              const float* vr = v + tv * a.e_Dv;
+              c0 = fmaf(wt, vr[0], c0);
+              c1 = fmaf(wt, vr[4], c1);
+              c2 = fmaf(wt, vr[8], c2);
+              c3 = fmaf(wt, vr[12], c3);
+            }
+            const bool ok = b2 < a.B;
+            const u32x4 dv = {__float_as_uint(ok ? c0 : 0.f), __float_as_uint(ok ? c1 : 0.f),
+                              __float_as_uint(ok ? c2 : 0.f), __float_as_uint(ok ? c3 : 0.f)};
+            __builtin_amdgcn_raw_buffer_store_b128(dv, rc, af_idx(b2, i0) * 4, 0, 16);  // sc1
+          }
+        }
+        PD_STAMP(31);
+        pd_publish(a, PD_F_CMB, tg, tid);
+        PD_STAMP(24);
+        for (int e = tid; e < 2 * HT; e += PD_NT) {  // emotion alignments (output only: after the publish)
+          const int rr = e / HT, b2 = r0 + rr;
+          if (b2 < a.B) a.e_hist[((long)t * a.B + b2) * HT + (e - rr * HT)] = sco[e];
+        }
+      } else if (isq) {  // attn_emt dense (Architecture_wrappers.py:233-234): tile pn - PD_NTILE, K split pks
+        if (!pd_block_wait(si + 6, [&] { return pd_poll(a, PD_F_CMB, PD_EG0, 1, 16, tg, 0, lane); })) return;
+        PD_STAMP(25);
+        const int nkg = a.e_KC / 128;  // k-groups per split
+        if (w < nkg) {
+          const float* X = a.CMBx + (long)p * 32 * a.e_KC;
+          const int sg = pks * nkg + w;
+          f32x4 s0 = zero4, s1 = zero4;
+          kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wdf, s0, s1);
+          put_partials(s0, s1, red, w, lane);
+        }
+        __syncthreads();
+        {
+          const int m = tid >> 4, col = tid & 15;
+          float v = 0.f;
+          for (int ww = 0; ww < nkg; ++ww) v += red[ww * 512 + tid];
+          pd_put(a.EOg + (((long)p * PD_KSP + pks) * 32 + m) * PD_EQ + 16 * (pn - PD_NTILE) + col, tg, v);
+        }
+        __syncthreads();
+        PD_STAMP(26);
+      }
+    }
+    if (isproj && !isq) {
       if (!pd_block_wait(si + 6, [&] { return pd_poll(a, PD_F_CTX, 32 * pks, 1, 32, tg, 0, lane); })) return;
       PD_STAMP(11);
       if (w < 4) {
@@ -801,6 +957,31 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     __syncthreads();  // red reuse by stage A
     PD_STAMP(14);
+    if constexpr (EMT) {
+      if (g >= PD_EG0) {  // dense partials of rows r0, r0+1 -> the next step's emotion block (+ refnet_spk),
+                          // after this work-group's own prenet hand-off
+        const int r0 = 2 * (g - PD_EG0);
+        {
+          const int row = r0 + ((tid >> 7) & 1), col = tid & 127, hs = tid >> 8;
+          float pv[PD_KSP / 2];
+          if (!pd_take<PD_KSP / 2>(a, PD_F_EO, a.EOg + (((long)p * PD_KSP + 4 * hs) * 32 + row) * PD_EQ, col, 32 * PD_EQ,
+                                   tg, true, pv))
+            si[6] = 0;
+          G[tid] = (pv[0] + pv[1]) + (pv[2] + pv[3]);
+        }
+        __syncthreads();
+        if (tid < 256) {
+          const int row = r0 + (tid >> 7), col = tid & 127;
+          float o = (G[tid] + G[256 + tid]) * KG_UNSCALE + a.e_bd[col];
+          if (a.e_spk && row < a.B) o += a.e_spk[row * PD_EQ + col];
+          pd_st(a.EMTx + p * 32 * PD_EQ + af_idx(row, col), row < a.B ? o : 0.f);
+        }
+        PD_STAMP(27);
+        pd_publish_rep(a, 2, tg, tid);
+        PD_STAMP(28);
+        if (!si[6]) return;
+      }
+    }
     {  // L1 context rows of step t+1 and the style scales: every context slice of t landed before
        // any PP flag (PP <- CTX slices of all 8 splits), and this work-group has seen all PP flags
       const float* XC = a.CTXx + p * 32 * PD_E2;
@@ -812,6 +993,12 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         kg_mfma(pd_ld4(XC, (sg * 2) * 64 + lane), pd_ld4(XC, (sg * 2 + 1) * 64 + lane), w1c[i], accC0, accC1);
       }
       if (tid < 32) ssa[tid] = pd_ld(a.SSx + p * 32 + tid);
+    }
+    if constexpr (EMT) {  // the emotion block of step t joins the next step's LSTM-1 input (wave w: k-group w)
+      if (!pd_block_wait(si + 6, [&] { return pd_poll_rep(a, PD_F_EMT, 2, PD_EG0, tg, lane, 16); })) return;
+      PD_STAMP(29);
+      const float* XE = a.EMTx + p * 32 * PD_EQ;
+      kg_mfma(pd_ld4(XE, (w * 2) * 64 + lane), pd_ld4(XE, (w * 2 + 1) * 64 + lane), w1e, accC0, accC1);
     }
     PD_STAMP(15);
   }
@@ -827,23 +1014,26 @@ bool pd_device_ok(int dev) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   if (prop.multiProcessorCount < PD_NB) return false;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_decode_persist),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)pd_lds_bytes()) != hipSuccess)
+  for (const void* k : {reinterpret_cast<const void*>(k_decode_persist<false>),
+                        reinterpret_cast<const void*>(k_decode_persist<true>)})
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pd_lds_bytes()) != hipSuccess)
+      return false;
+  int nb = 0, ne = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_persist<false>, PD_NT, pd_lds_bytes()) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&ne, k_decode_persist<true>, PD_NT, pd_lds_bytes()) != hipSuccess)
     return false;
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_persist, PD_NT, pd_lds_bytes()) != hipSuccess)
-    return false;
-  return nb >= 1;
+  return nb >= 1 && ne >= 1;
 }
 
 // Cooperative launch: the runtime guarantees every one of the PD_NB work-groups is resident at
 // once (or fails the launch) -- the spin-waits of the hand-offs depend on it, and a plain launch
 // could be starved of CUs by a concurrent kernel on another stream or context.
-void pd_launch(const PdArgs& a, hipStream_t s) {
+void pd_launch(const PdArgs& a, hipStream_t s, bool emt) {
   PdArgs arg = a;
   void* params[] = {&arg};
-  TT2_HIP(launch_persistent(reinterpret_cast<const void*>(k_decode_persist), dim3(PD_NB), dim3(PD_NT),
-                                     params, (unsigned)pd_lds_bytes(), s));
+  const void* k = emt ? reinterpret_cast<const void*>(k_decode_persist<true>)
+                      : reinterpret_cast<const void*>(k_decode_persist<false>);
+  TT2_HIP(launch_persistent(k, dim3(PD_NB), dim3(PD_NT), params, (unsigned)pd_lds_bytes(), s));
 }
 
 }  // namespace tt2

@@ -1200,6 +1200,12 @@ __global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t
 
 // Encoder-step-fastest copies of keys / values for the persistent decoder:
 // dst[b][c][t] = src[b][t][c] (t < T, c < C; row stride ld), 0 for T <= t < 256.
+// rows [B][C] -> AF [32 x C] (rows >= B untouched): the persistent decoder's step-0 emotion block
+__global__ void k_af_rows(const float* __restrict__ src, int C, float* __restrict__ dst) {
+  const int b = blockIdx.x;
+  for (int n = threadIdx.x; n < C; n += blockDim.x) dst[af_idx(b, n)] = src[(long)b * C + n];
+}
+
 __global__ void k_transpose_bt(const float* __restrict__ src, long ld, float* __restrict__ dst, int T, int C) {
   __shared__ float tile[32][33];
   const int b = blockIdx.z, c0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
@@ -1322,6 +1328,7 @@ struct tt2_ctx {
   bool st_ready = false;
   // the persistent decoder's copies of l1_w, l1_wh, l2_w, l2_wh, proj_w, pre-scaled by KG_SB
   tt2::DevBuf pd_l1_w, pd_l1_wh, pd_l2_w, pd_l2_wh, pd_proj_w;
+  tt2::DevBuf pd_e_wd;  // emt 'multihead' in the persistent decoder: attn_emt dense as WF tiles (x KG_SB)
   tt2::DevBuf pre_w1r, pre_b1, pre_w2, pre_b2, q_w;  // pre_w1r: row-major [nm][P] (GTA TP1 GEMM)
   tt2::DevBuf l1_w, l1_wh, l1_ws, l1_b, l2_w, l2_wh, l2_b;  // critical rows / recurrent rows / style rows
   tt2::DevBuf loc_cw, keys_b, va, proj_w, proj_ws, proj_b;
@@ -1354,7 +1361,7 @@ struct tt2_ctx {
   int pd_mode = 1;        // TT2_DECODER env: 1 persistent when the shapes fit, 0 launch path only
   bool pd_dev_ok = false; // all PD_NB work-groups can be resident on this device
   bool last_pd = false;   // the last decode ran the persistent kernel
-  tt2::DevBuf q_wt, pre_w2t, keysT, valuesT, pd_ctl, H1x, H2x, Ex, CTXx, SSx, PPx, PREx;
+  tt2::DevBuf q_wt, pre_w2t, keysT, valuesT, pd_ctl, H1x, H2x, Ex, CTXx, SSx, PPx, PREx, QEx, CMBx, EOx, EMTx;
   tt2::DevBuf pd_alnT;  // [B][max_iters][T_in] step-major alignments of the persistent decoder
   // Tacotron_emt_attn variant (emt.h): off for the Tacotron model
   tt2::EmtModel emt;
@@ -1656,7 +1663,32 @@ static void finalize(tt2_ctx* c) {
       const auto pw = pack_wf(W.data(), c->Kp, NPF, cols, c->Kp);  // rows [h2 | context_enc]
       c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pw));
       upload(c->proj_w, pw);
-      upload_scaled(c->pd_proj_w, pw, KG_SB);
+      if (c->emt.attn == EMT_MULTIHEAD && c->emt.Aq == PD_EQ) {
+        // persistent decoder: 8 more tiles = the emotion query h2·W_q (multihead conv1d, first H rows;
+        // zero context rows), Architecture_wrappers.py:228-232 / multihead_attention.py:71
+        const auto& kq = need(wm, P + "decoder/Multihead-attention-attn_emt/conv1d/kernel", {1, c->H, PD_EQ});
+        const int NX = NPF + PD_EQ;
+        std::vector<float> Wx((size_t)c->Kp * NX, 0.f);
+        std::vector<int> colx;
+        for (int j = 0; j < NX; ++j) colx.push_back(j);
+        for (int k = 0; k < c->Kp; ++k) {
+          for (int n = 0; n < NPF; ++n) Wx[(size_t)k * NX + n] = W[(size_t)k * NPF + n];
+          if (k < c->H)
+            for (int n = 0; n < PD_EQ; ++n) Wx[(size_t)k * NX + NPF + n] = kq.data[(size_t)k * PD_EQ + n];
+        }
+        const auto pwx = pack_wf(Wx.data(), c->Kp, NX, colx, c->Kp);
+        c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pwx));
+        upload_scaled(c->pd_proj_w, pwx, KG_SB);
+        const int KC = c->emt.heads * c->emt.Dv;
+        const auto& kd = need(wm, P + "decoder/attn_emt/dense/kernel", {KC, EMT_OUT});
+        std::vector<int> ocols;
+        for (int j = 0; j < EMT_OUT; ++j) ocols.push_back(j);
+        const auto pwd = pack_wf(kd.data.data(), KC, EMT_OUT, ocols, KC);
+        c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pwd));
+        upload_scaled(c->pd_e_wd, pwd, KG_SB);
+      } else {
+        upload_scaled(c->pd_proj_w, pw, KG_SB);
+      }
     }
     std::vector<float> ws((size_t)c->SW * NPF, 0.f);                // context_style rows
     for (int r = 0; r < c->SW; ++r)
@@ -2119,15 +2151,26 @@ static void check_encoder(tt2_ctx* c) {
   TT2_CHECK(c->ctl_host[2] == 0, TT2_ERR_HIP, "persistent BiLSTM encoder: a hand-off wait timed out");
 }
 
+// Tacotron_emt_attn decodes persistently in its 'multihead' form with the fork-default widths
+// (query 128, heads x value width 512 or 1024, 2 x heads x attended rows <= 128, <= 32 dims per
+// head); the other forms use the launch path
+static bool pd_emt(const tt2_ctx* c) {
+  const auto& m = c->emt;
+  const int KC = m.heads * m.Dv;
+  return m.attn == EMT_MULTIHEAD && m.Aq == PD_EQ && m.XW == PD_EQ && (KC == 512 || KC == 1024) && m.Tv >= 1 &&
+         m.Tv <= 64 && 2 * m.heads * m.Tv <= 128 && m.dh <= 32 && c->K1 == PD_P + PD_E2 + PD_EQ &&
+         c->pd_e_wd.p;
+}
+
 static bool pd_fits(tt2_ctx* c) {
-  return !c->emt.on() && c->pd_mode == 1 && c->pd_dev_ok && c->kg_wmax_dec < KG_BMAX && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
+  return (!c->emt.on() || pd_emt(c)) && c->pd_mode == 1 && c->pd_dev_ok && c->kg_wmax_dec < KG_BMAX && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
          c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= PD_TMAX && c->B <= 32;
 }
 
 static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, const float* targets_d, int T_lim,
                                float* frames_d, float* stop_d, float* align_d, hipStream_t s) {
   if (!c->H1x.p) {
-    c->pd_ctl.alloc(sizeof(unsigned) * (2 * PD_NPH * PD_NB + 32 + 2 * PD_NREP * PD_NB));
+    c->pd_ctl.alloc(sizeof(unsigned) * (2 * PD_NPH * PD_NB + 32 + 3 * PD_NREP * PD_NB));
     c->H1x.alloc(2L * 32 * PD_H * 4);
     c->H2x.alloc(2L * 32 * PD_H * 4);
     c->Ex.alloc(2L * 32 * 8 * PD_TMAX * 8);
@@ -2136,6 +2179,13 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     c->PPx.alloc(2L * PD_KSP * 32 * PD_NPF * 8);
     c->PREx.alloc(2L * 32 * PD_P * 8);
     for (auto& e : c->pd_ev) TT2_HIP(hipEventCreate(&e));
+  }
+  const bool emt = c->emt.on();
+  if (emt && !c->QEx.p) {
+    c->QEx.alloc(2L * PD_KSP * 32 * PD_EQ * 8);
+    c->CMBx.alloc(2L * 32 * 1024 * 4);
+    c->EOx.alloc(2L * PD_KSP * 32 * PD_EQ * 8);
+    c->EMTx.alloc(2L * 32 * PD_EQ * 4);
   }
   const auto& cfg = c->cfg;
   c->keysT.alloc(sizeof(float) * (size_t)cfg.max_batch * PD_A * PD_TMAX);
@@ -2149,6 +2199,13 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   // earlier decode must never match
   zero_many({{c->pd_ctl.p, c->pd_ctl.bytes}, {c->Ex.p, c->Ex.bytes}, {c->PPx.p, c->PPx.bytes},
              {c->PREx.p, c->PREx.bytes}}, s);
+  if (emt) {
+    zero_many({{c->QEx.p, c->QEx.bytes}, {c->EOx.p, c->EOx.bytes}, {c->EMTx.p, c->EMTx.bytes}}, s);
+    // zero_state (Architecture_wrappers.py:182): the step-0 emotion block is refnet_spk alone
+    const float* spk = emt_spk(c);
+    if (spk)
+      hipLaunchKernelGGL(k_af_rows, dim3(c->B), dim3(PD_EQ), 0, s, spk, PD_EQ, c->EMTx.as<float>() + 32 * PD_EQ);
+  }
   PdArgs a;
   a.flags = c->pd_ctl.as<unsigned>();
   a.flags2 = a.flags + PD_NPH * PD_NB;
@@ -2179,6 +2236,16 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     c->pd_alnT.alloc(sizeof(float) * (size_t)c->B * max_iters * c->T_in);
     a.align = c->pd_alnT.as<float>();
   }
+  a.K1 = c->K1;
+  if (emt) {
+    const auto& m = c->emt;
+    a.e_Tv = m.Tv; a.e_Dv = m.Dv; a.e_KC = m.heads * m.Dv; a.e_heads = m.heads; a.e_dh = m.dh;
+    a.e_ke = m.ke.as<float>(); a.e_val = m.val.as<float>(); a.e_qrow = m.qrow.as<float>();
+    a.e_vv = m.vv.as<float>(); a.e_ab = m.ab.as<float>(); a.e_wd = c->pd_e_wd.as<float>(); a.e_bd = m.bd.as<float>();
+    a.e_spk = emt_spk(c); a.e_hist = m.hist.as<float>();
+    a.QEg = c->QEx.as<unsigned long long>(); a.CMBx = c->CMBx.as<float>(); a.EOg = c->EOx.as<unsigned long long>();
+    a.EMTx = c->EMTx.as<float>();
+  }
   a.stamps = nullptr;
   a.stamp_step = -1;
   if (const char* st = getenv("TT2_STAMP_STEP")) {  // diagnostic: stage stamps of one decode step
@@ -2188,7 +2255,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     a.stamp_step = atoi(st);
   }
   TT2_HIP(hipEventRecord(c->pd_ev[0], s));
-  pd_launch(a, s);
+  pd_launch(a, s, emt);
   TT2_HIP(hipEventRecord(c->pd_ev[1], s));
   int h[4];
   TT2_HIP(hipMemcpyAsync(h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));

@@ -870,6 +870,8 @@ __global__ __launch_bounds__(TR_E2T) void k_tr_att_energy_bwd2(TrAtt a) {
     wl1[c] = (c < F && ok1) ? a.Wl[c * A + k1] : 0.f;
   }
   const float va0 = ok0 ? a.va[k0] : 0.f, va1 = ok1 ? a.va[k1] : 0.f;
+  const long pt = (long)b * a.nt + tile;
+  const float odv = tid < A ? a.dV[pt * A + tid] : 0.f, odb = tid < A ? a.dBA[pt * A + tid] : 0.f;
   float sp = 0.f;
   for (int n = tid; n < D; n += TR_E2T) {
     const float v = a.dPIN[tb * (a.H + D) + a.H + n] + a.dX1[(tb + a.B) * (a.P + D + a.H) + a.P + n];
@@ -936,10 +938,9 @@ __global__ __launch_bounds__(TR_E2T) void k_tr_att_energy_bwd2(TrAtt a) {
   if (tid < A) {
     const float sv = (racc[0][0][tid] + racc[0][1][tid]) + (racc[0][2][tid] + racc[0][3][tid]);
     const float sq = (racc[1][0][tid] + racc[1][1][tid]) + (racc[1][2][tid] + racc[1][3][tid]);
-    const long pt = (long)b * a.nt + tile;
     a.PQ[pt * A + tid] = sq;
-    a.dV[pt * A + tid] += sv;
-    a.dBA[pt * A + tid] += sq;
+    a.dV[pt * A + tid] = odv + sv;
+    a.dBA[pt * A + tid] = odb + sq;
   }
 }
 
@@ -951,12 +952,20 @@ __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
   const int b = blockIdx.y, tile = blockIdx.x, j0 = tile * TR_JT, tid = threadIdx.x;
   const int pad = (a.KW - 1) / 2, lo = a.KW - 1 - pad;  // halo below / above
   const long tb = (long)a.t * a.B + b;
-  if (tile == 0)
-    for (int k = tid; k < a.A; k += blockDim.x) {
-      float acc = 0.f;
-      for (int g = 0; g < a.nt; ++g) acc += a.PQ[((long)b * a.nt + g) * a.A + k];
-      a.DQ[tb * a.A + k] = acc;
-    }
+  const long pt = (long)b * a.nt + tile;
+  // the accumulators' old values are loaded with the staging loads: one memory round trip before
+  // the arithmetic instead of one per read-modify-write (KW·F <= 65·32 = 8 per thread)
+  constexpr int KCM = (65 * 32 + 255) / 256;
+  float okc[KCM];
+#pragma unroll
+  for (int u = 0; u < KCM; ++u) {
+    const int i = tid + 256 * u;
+    okc[u] = i < a.KW * a.F ? a.dKC[pt * a.KW * a.F + i] : 0.f;
+  }
+  const float obc = tid < a.F ? a.dBC[pt * a.F + tid] : 0.f;
+  float dq = 0.f;
+  if (tile == 0 && tid < a.A)
+    for (int g = 0; g < a.nt; ++g) dq += a.PQ[((long)b * a.nt + g) * a.A + tid];
   const float* cum_prev = a.CUM + tb * a.Tin;
   for (int i = tid; i < TR_JT + a.KW - 1; i += blockDim.x) {
     const int j = j0 + i - pad;
@@ -968,30 +977,41 @@ __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
     const int j = j0 - lo + i / a.F, c = i % a.F;
     dfh[i] = (j >= 0 && j < a.Tin) ? a.DF[((long)b * a.Tin + j) * a.F + c] : 0.f;
   }
+  // 32 lanes per position (lane = filter), 8 positions per pass: old d cum values first
+  const int c32 = tid & 31;
+  float odc[TR_JT / 8];
+#pragma unroll
+  for (int u = 0; u < TR_JT / 8; ++u) {
+    const int i = j0 + 8 * u + tid / 32;
+    odc[u] = (c32 == 0 && i < a.Tin) ? a.DCUM[(long)b * a.Tin + i] : 0.f;
+  }
+  if (tile == 0 && tid < a.A) a.DQ[tb * a.A + tid] = dq;
   __syncthreads();
-  const long pt = (long)b * a.nt + tile;
   const float* dfs = dfh + lo * a.F;  // the tile's own rows
-  for (int i = tid; i < a.KW * a.F; i += blockDim.x) {
-    const int tap = i / a.F, c = i % a.F;
-    float acc = 0.f;
-    for (int jj = 0; jj < TR_JT; ++jj) acc += dfs[jj * a.F + c] * cseg[jj + tap];
-    a.dKC[pt * a.KW * a.F + i] += acc;
+#pragma unroll
+  for (int u = 0; u < KCM; ++u) {
+    const int i = tid + 256 * u;
+    if (i < a.KW * a.F) {
+      const int tap = i / a.F, c = i % a.F;
+      float acc = 0.f;
+      for (int jj = 0; jj < TR_JT; ++jj) acc += dfs[jj * a.F + c] * cseg[jj + tap];
+      a.dKC[pt * a.KW * a.F + i] = okc[u] + acc;
+    }
   }
-  for (int c = tid; c < a.F; c += blockDim.x) {
+  if (tid < a.F) {
     float acc = 0.f;
-    for (int jj = 0; jj < TR_JT; ++jj) acc += dfs[jj * a.F + c];
-    a.dBC[pt * a.F + c] += acc;
+    for (int jj = 0; jj < TR_JT; ++jj) acc += dfs[jj * a.F + tid];
+    a.dBC[pt * a.F + tid] = obc + acc;
   }
-  // 32 lanes per position (lane = filter), 8 positions per pass
-  const int c = tid & 31;
-  for (int i0 = 0; i0 < TR_JT; i0 += blockDim.x / 32) {
-    const int ii = i0 + tid / 32, i = j0 + ii;
+#pragma unroll
+  for (int u = 0; u < TR_JT / 8; ++u) {
+    const int ii = 8 * u + tid / 32, i = j0 + ii;
     float acc = 0.f;
-    if (c < a.F)
-      for (int tap = 0; tap < a.KW; ++tap) acc += dfs[(ii - tap + pad) * a.F + c] * a.Kc[tap * a.F + c];
+    if (c32 < a.F)
+      for (int tap = 0; tap < a.KW; ++tap) acc += dfs[(ii - tap + pad) * a.F + c32] * a.Kc[tap * a.F + c32];
 #pragma unroll
     for (int o = 16; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (c == 0 && i < a.Tin) a.DCUM[(long)b * a.Tin + i] += acc;
+    if (c32 == 0 && i < a.Tin) a.DCUM[(long)b * a.Tin + i] = odc[u] + acc;
   }
 }
 

@@ -1,5 +1,6 @@
-"""Tacotron_emt_attn (tacotron_emt_attn.py) on the launch-path decoder:
-libtt2.so vs oracle/tacotron_emt_ref.py on identical seeded inputs and injected prenet masks.
+"""Tacotron_emt_attn (tacotron_emt_attn.py): libtt2.so vs
+oracle/tacotron_emt_ref.py on identical seeded inputs and injected prenet masks -- on the launch-path
+decoder, and ('multihead' at the fork widths, round 3) in the persistent decoder.
 
 Each emotion-attention type the reference builds ('simple', 'multihead', 'style_tokens') with the
 reference-encoder output variants args.emt_ref_gru = 'none' / 'gru' / 'gru_multi', with and without
@@ -19,7 +20,7 @@ TOL = 1e-4
 
 
 def _case(hp, attn, ref_gru, emt_only=False, B=3, T=11, T_ref=300, n=24, seed=21, targets=None,
-          labels=None, n_emt=4):
+          labels=None, n_emt=4, persistent_expected=0):
     from tt2.engine import TacotronEngine
     from tt2.weights import init_tacotron_emt_weights
     W = init_tacotron_emt_weights(hp, attn, ref_gru, emt_only, n_emt, seed=5339)
@@ -38,7 +39,7 @@ def _case(hp, attn, ref_gru, emt_only=False, B=3, T=11, T_ref=300, n=24, seed=21
     eng.close()
     ref = ER.synthesize(ids, lens, re, rs, W, oracle_hp(hp), attn, ref_gru, masks, n, labels,
                         n_emt, emt_only, targets)
-    assert persistent == 0  # the variant runs on the per-step launch path
+    assert persistent == persistent_expected
     assert out["frames"].shape == ref["decoder_output"].shape
     np.testing.assert_allclose(out["stop_token_prediction"], ref["stop_token_prediction"], atol=TOL)
     np.testing.assert_allclose(out["alignments"], ref["alignments"], atol=TOL)
@@ -117,3 +118,55 @@ def test_shim_initialize_and_synthesizer():
     mels = syn.synthesize(["hello there"], None, None, None, [None], mel_ref_filenames_emt=[re[0]],
                           mel_ref_filenames_spk=[rs[0]])
     assert len(mels) == 1 and mels[0].shape[1] == hp.num_mels and np.isfinite(mels[0]).all()
+
+
+@pytest.mark.parametrize("ref_gru", ["gru", "gru_multi", "none"])
+def test_multihead_full_width_persistent(ref_gru):
+    """'multihead' at the fork widths runs in k_decode_persist<true>: the emotion query as 8 more
+    projection tiles, 16 emotion work-groups (scores, softmax, heads-concatenated contexts), the
+    attn_emt dense on the query blocks, the emotion block folded into the next step's LSTM-1 rows.
+    heads x value width: 'gru' 4 x 256, 'gru_multi' 4 x 128, 'none' 4 x 256 (the CNN output)."""
+    _case(full_hparams(), "multihead", ref_gru, B=3, T=9, T_ref=80, n=12, persistent_expected=1)
+
+
+def test_multihead_full_width_persistent_emt_only_gta():
+    """emt_only (no refnet_spk term) + GTA, padding rows of the 32-row tiles, persistent decoder."""
+    hp = full_hparams()
+    tg = np.random.default_rng(3).normal(0, 1, (2, 10, hp.num_mels)).astype(np.float32)
+    _case(hp, "multihead", "gru_multi", emt_only=True, B=2, T=9, T_ref=80, n=14, targets=tg,
+          persistent_expected=1)
+
+
+def test_multihead_persistent_matches_launch_path_b32():
+    """configs[1]-shaped batch (B = 32, T_ref 400): persistent decoder against the launch path over
+    80 free-running steps, same weights, inputs and prenet masks (split fp16x3 vs fp32 MFMA products:
+    the two paths agree to float rounding, compared at 1e-3)."""
+    import os
+    from tt2.engine import TacotronEngine
+    from tt2.weights import init_tacotron_emt_weights
+    hp = full_hparams()
+    B, T, TR, n = 32, 41, 400, 80
+    W = init_tacotron_emt_weights(hp, "multihead", "gru", seed=5339)
+    ids, lens, re, rs = tacotron_inputs(B, T, TR, seed=7)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=7)
+    outs = []
+    for mode in ("persistent", "launch"):
+        old = os.environ.get("TT2_DECODER")
+        os.environ["TT2_DECODER"] = mode
+        try:
+            eng = TacotronEngine(hp, W, B, T, TR, n, 0, False, False, "multihead", "gru", 4)
+        finally:
+            if old is None:
+                del os.environ["TT2_DECODER"]
+            else:
+                os.environ["TT2_DECODER"] = old
+        out = eng.synthesize(ids, lens, re, rs, n, masks)
+        persistent, _ = eng.decoder_path()
+        outs.append((out, eng.emt_alignments(), persistent))
+        eng.close()
+    (a, ea, pa), (b, eb, pb) = outs
+    assert pa == 1 and pb == 0
+    steps = min(a["frames"].shape[1], b["frames"].shape[1])
+    assert steps >= 20
+    np.testing.assert_allclose(a["frames"][:, :steps], b["frames"][:, :steps], atol=1e-3)
+    np.testing.assert_allclose(ea[..., :steps], eb[..., :steps], atol=1e-3)
