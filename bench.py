@@ -543,7 +543,7 @@ def main():
         n = n_steps.value
         step_bytes = decoder_step_bytes(W, hp, B, T)
         achieved = step_bytes * n / (pd_ms * 1e-3) / 1e9
-        traffic = load_traffic("k_decode_persist")
+        traffic = load_traffic("k_decode_persist<false>") or load_traffic("k_decode_persist")
         # priced against the HBM roofline, but the PMC counters show the weights
         # resident on chip (traffic ~0.1x the algorithmic bytes): the limiter is the latency of
         # the chip-wide hand-offs per step, hence the bound label

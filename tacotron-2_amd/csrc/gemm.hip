@@ -212,21 +212,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 
 // split-K combine: C = epilogue(sum_z kpart[z]) (same epilogue as epilogue_tile)
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g) {
-  // 4 consecutive outputs per thread: 16-byte partial loads when N % 4 == 0, two independent
-  // accumulator chains over the splits (the same summation order as the scalar loop pairwise)
+  // 4 consecutive outputs per thread: 16-byte partial loads when N % 4 == 0, eight independent
+  // accumulator chains over the splits (8 loads in flight per round, not a dependent chain)
   const long MN = (long)g.M * g.N;
   const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i0 >= MN) return;
   float y[4] = {0.f, 0.f, 0.f, 0.f};
   if ((g.N & 3) == 0) {
-    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
-    int z = 0;
-    for (; z + 1 < g.ksplit; z += 2) {
-      a0 += *reinterpret_cast<const f32x4*>(g.kpart + (long)z * MN + i0);
-      a1 += *reinterpret_cast<const f32x4*>(g.kpart + (long)(z + 1) * MN + i0);
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 a[8] = {z4, z4, z4, z4, z4, z4, z4, z4};
+    for (int z0 = 0; z0 < g.ksplit; z0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (z0 + u < g.ksplit) a[u] += *reinterpret_cast<const f32x4*>(g.kpart + (long)(z0 + u) * MN + i0);
     }
-    if (z < g.ksplit) a0 += *reinterpret_cast<const f32x4*>(g.kpart + (long)z * MN + i0);
-    const f32x4 t = a0 + a1;
+    const f32x4 t = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 #pragma unroll
     for (int e = 0; e < 4; ++e) y[e] = t[e];
   } else {
@@ -682,7 +682,8 @@ static bool rd_plan(const GemmArgs& a, int& ks, int& kslice) {
       (reinterpret_cast<uintptr_t>(a.A) & 15))
     return false;
   const int nt = (a.N + RD_BN - 1) / RD_BN;
-  ks = std::max(1, std::min(a.K / 32, 256 / std::max(nt, 1)));
+  // ~one work-group per CU, but >= 4 k-steps per slice: a small product is not worth its partials
+  ks = std::max(1, std::min(a.K / 128, 256 / std::max(nt, 1)));
   for (;;) {
     kslice = ((a.K + ks - 1) / ks + 31) / 32 * 32;
     if (kslice <= 32 * RD_KT) break;

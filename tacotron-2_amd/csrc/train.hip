@@ -1924,9 +1924,15 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_colsum(c, c->dBA.as<float>(), BNT, A, A, gvar(c, LAV("attention_bias")), s);
   {  // d W_loc = Σ_{t,b,j} f ⊗ du over all T·B·Tin rows
     const long R = TB * Tin;
-    if (F <= 32 && A <= 128) {  // one streaming fp32-MFMA pass (k_tr_dwloc), partials in TBUF
-      const long rpb = ((R + 511) / 512 + 31) / 32 * 32;
+    // one streaming fp32-MFMA pass (k_tr_dwloc), partials [nbk][F·A] in TBUF: at most 512 blocks
+    // and never more than TBUF holds (small T·B configurations have a small TBUF)
+    const long cap = (long)(c->TBUF.bytes / sizeof(float)) / ((long)F * A);
+    if (F <= 32 && A <= 128 && cap >= 1) {
+      const long nb = std::min<long>(512, cap);
+      const long rpb = ((R + nb - 1) / nb + 31) / 32 * 32;
       const int nbk = (int)((R + rpb - 1) / rpb);
+      TT2_CHECK((long)nbk * F * A * (long)sizeof(float) <= (long)c->TBUF.bytes, TT2_ERR_STATE,
+                "d W_loc partials exceed TBUF");
       hipLaunchKernelGGL(k_tr_dwloc, dim3(nbk), dim3(256), 0, s, c->FALL.as<float>(), c->TH.as<float>(), R, F, A, rpb,
                          TBUF);
       tr_colsum(c, TBUF, nbk, F * A, (long)F * A, gvar(c, LAV("location_features_layer/kernel")), s);

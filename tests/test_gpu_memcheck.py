@@ -40,8 +40,10 @@ def _run(specs, env_extra, timeout=280):
 
 @pytest.mark.gpu
 def test_training_step_redzones_intact():
-    """No kernel of the decoder / Postnet / front-end training step writes past its buffer."""
-    _run(POSTNET + FRONT, {"TT2_REDZONE": "1"})
+    """No kernel of the decoder / Postnet / front-end training step writes past its buffer.  The bf16
+    case at decoder width 1024 with a small T·B: the round-3 d W_loc pass once sized its 512 blocks
+    of partials without checking TBUF, which is T·B-sized (full run order: an illegal access)."""
+    _run(POSTNET + FRONT + ["test_gpu_train_bf16_gemms_close_to_oracle"], {"TT2_REDZONE": "1"})
 
 
 @pytest.mark.gpu
