@@ -531,9 +531,43 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
     }
   }
   __syncthreads();
-  // 64 channels per work-group, the 4 waves split the encoder rows (j = wave mod 4), LDS combine
-  __shared__ float red[4][64];
-  const int nl = threadIdx.x & 63, wq = threadIdx.x >> 6;
+  // 64 channels per work-group.  D % 4 == 0: 16 float4 columns x 16 row groups, every row of a batch
+  // of 10 loaded before its products (the values rows are the kernel's whole read); else 4 row groups
+  __shared__ float red[16][64];
+  const int tid = threadIdx.x;
+  if ((a.D & 3) == 0) {
+    const int cg = tid & 15, rg = tid >> 4, nc0 = blockIdx.x * 64 + 4 * cg;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (nc0 < a.D) {
+      const float* vb = a.values + (long)b * a.Tin * a.D + nc0;
+      for (int j0 = rg; j0 < a.Tin; j0 += 160) {
+        f32x4 v[10];
+#pragma unroll
+        for (int u = 0; u < 10; ++u) {
+          const int j = j0 + 16 * u;
+          v[u] = j < a.Tin ? *reinterpret_cast<const f32x4*>(vb + (long)j * a.D) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 10; ++u) {
+          const int j = j0 + 16 * u;
+          if (j < a.Tin) acc += al[j] * v[u];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[rg][4 * cg + i] = acc[i];
+    __syncthreads();
+    const int nc = blockIdx.x * 64 + tid;
+    if (tid < 64 && nc < a.D) {
+      float r = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) r += red[g][tid];
+      a.PIN[tb * (a.H + a.D) + a.H + nc] = r;
+      a.X1[(tb + a.B) * (a.P + a.D + a.H) + a.P + nc] = r;
+    }
+    return;
+  }
+  const int nl = tid & 63, wq = tid >> 6;
   const int nc = blockIdx.x * 64 + nl;
   float acc = 0.f;
   if (nc < a.D) {
@@ -949,6 +983,7 @@ __global__ __launch_bounds__(TR_E2T) void k_tr_att_energy_bwd2(TrAtt a) {
 __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
   __shared__ float cseg[TR_JT + 64];
   __shared__ float dfh[(TR_JT + 64) * 32];
+  __shared__ float Kcs[65 * 32];  // conv taps from LDS: the d cum loop runs KW dependent steps
   const int b = blockIdx.y, tile = blockIdx.x, j0 = tile * TR_JT, tid = threadIdx.x;
   const int pad = (a.KW - 1) / 2, lo = a.KW - 1 - pad;  // halo below / above
   const long tb = (long)a.t * a.B + b;
@@ -985,6 +1020,7 @@ __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
     const int i = j0 + 8 * u + tid / 32;
     odc[u] = (c32 == 0 && i < a.Tin) ? a.DCUM[(long)b * a.Tin + i] : 0.f;
   }
+  for (int i = tid; i < a.KW * a.F; i += blockDim.x) Kcs[i] = a.Kc[i];
   if (tile == 0 && tid < a.A) a.DQ[tb * a.A + tid] = dq;
   __syncthreads();
   const float* dfs = dfh + lo * a.F;  // the tile's own rows
@@ -1008,7 +1044,7 @@ __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
     const int ii = 8 * u + tid / 32, i = j0 + ii;
     float acc = 0.f;
     if (c32 < a.F)
-      for (int tap = 0; tap < a.KW; ++tap) acc += dfs[(ii - tap + pad) * a.F + c32] * a.Kc[tap * a.F + c32];
+      for (int tap = 0; tap < a.KW; ++tap) acc += dfs[(ii - tap + pad) * a.F + c32] * Kcs[tap * a.F + c32];
 #pragma unroll
     for (int o = 16; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if (c32 == 0 && i < a.Tin) a.DCUM[(long)b * a.Tin + i] = odc[u] + acc;
@@ -2418,7 +2454,8 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
     tr_gemm_run(g, s);
     std::swap(dxn, dxo);
   }
-  fe_embed_bwd(ids, dxn, M, E, f.n_symbols, gvar(c, vn("inputs_embedding")), s);
+  fe_embed_bwd(ids, dxn, M, E, f.n_symbols, gvar(c, vn("inputs_embedding")), s, FB,
+               (long)(c->fFBUF.bytes / sizeof(float)));  // FB is free after the conv loop
 }
 
 

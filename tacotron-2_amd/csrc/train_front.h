@@ -9,7 +9,9 @@ namespace tt2 {
 
 // ---- encoder --------------------------------------------------------------------------------
 void fe_embed(const int* ids, const float* table, long M, int E, float* out, hipStream_t s);
-void fe_embed_bwd(const int* ids, const float* dx, long M, int E, int n_symbols, float* dtable, hipStream_t s);
+// scratch (>= min(64, M/128) x n_symbols x E floats, or null): the position-segmented two-pass form
+void fe_embed_bwd(const int* ids, const float* dx, long M, int E, int n_symbols, float* dtable, hipStream_t s,
+                  float* scratch = nullptr, long scratch_floats = 0);
 
 // BiLSTM step t of both directions (bidirectional_dynamic_rnn, modules.py:315-321): layouts are
 // direction-major: XP [B][T][8U] input projections (+ biases), GZ [2][B][4U] recurrent products of

@@ -40,9 +40,48 @@ __global__ void k_fe_embed_bwd(const int* __restrict__ ids, const float* __restr
 void fe_embed(const int* ids, const float* table, long M, int E, float* out, hipStream_t s) {
   hipLaunchKernelGGL(k_fe_embed, dim3(fe_blk(M * E)), dim3(256), 0, s, ids, table, M, E, out);
 }
-void fe_embed_bwd(const int* ids, const float* dx, long M, int E, int n_symbols, float* dtable, hipStream_t s) {
-  hipLaunchKernelGGL(k_fe_embed_bwd, dim3(fe_blk((long)n_symbols * E)), dim3(256), 0, s, ids, dx, M, E, n_symbols,
-                     dtable);
+// Segmented form: blockIdx.y = segment of L positions; part[seg][sym][e] = Σ over the segment's
+// positions of that symbol, in position order.  Then a fixed-order sum over the segments.
+__global__ void k_fe_embed_bwd_seg(const int* __restrict__ ids, const float* __restrict__ dx, long M, int E, int NS,
+                                   long L, float* __restrict__ part) {
+  __shared__ int sid[256];
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < (long)NS * E;
+  const int sym = act ? (int)(i / E) : -1, e = act ? (int)(i % E) : 0;
+  const long m0 = (long)blockIdx.y * L, m1 = std::min<long>(M, m0 + L);
+  float acc = 0.f;
+  for (long c0 = m0; c0 < m1; c0 += 256) {
+    __syncthreads();
+    sid[threadIdx.x] = c0 + threadIdx.x < m1 ? ids[c0 + threadIdx.x] : -2;
+    __syncthreads();
+    const int n = (int)std::min<long>(256, m1 - c0);
+    for (int jj = 0; jj < n; ++jj)
+      if (sid[jj] == sym) acc += dx[(c0 + jj) * E + e];
+  }
+  if (act) part[(long)blockIdx.y * NS * E + i] = acc;
+}
+__global__ void k_fe_embed_bwd_sum(const float* __restrict__ part, int S, long n, float* __restrict__ dtab) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < S; s0 += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (s0 + u < S) a[u] += part[(long)(s0 + u) * n + i];
+  }
+  dtab[i] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+void fe_embed_bwd(const int* ids, const float* dx, long M, int E, int n_symbols, float* dtable, hipStream_t s,
+                  float* scratch, long scratch_floats) {
+  const long n = (long)n_symbols * E;
+  const int S = (int)std::min<long>(64, (M + 127) / 128);
+  if (scratch && S > 1 && (long)S * n <= scratch_floats) {  // positions split over S segments
+    const long L = (M + S - 1) / S;
+    hipLaunchKernelGGL(k_fe_embed_bwd_seg, dim3(fe_blk(n), S), dim3(256), 0, s, ids, dx, M, E, n_symbols, L, scratch);
+    hipLaunchKernelGGL(k_fe_embed_bwd_sum, dim3(fe_blk(n)), dim3(256), 0, s, scratch, S, n, dtable);
+    return;
+  }
+  hipLaunchKernelGGL(k_fe_embed_bwd, dim3(fe_blk(n)), dim3(256), 0, s, ids, dx, M, E, n_symbols, dtable);
 }
 
 // ---- BiLSTM -------------------------------------------------------------------------------------
