@@ -682,8 +682,13 @@ static bool rd_plan(const GemmArgs& a, int& ks, int& kslice) {
       (reinterpret_cast<uintptr_t>(a.A) & 15))
     return false;
   const int nt = (a.N + RD_BN - 1) / RD_BN;
-  // ~one work-group per CU, but >= 4 k-steps per slice: a small product is not worth its partials
-  ks = std::max(1, std::min(a.K / 128, 256 / std::max(nt, 1)));
+  // ~one work-group per CU (TT2_RD_TARGET work-groups), but >= 4 k-steps per slice: a small
+  // product is not worth its partials
+  static const int target = [] {
+    const char* e = std::getenv("TT2_RD_TARGET");
+    return e ? std::max(1, std::atoi(e)) : 256;
+  }();
+  ks = std::max(1, std::min(a.K / 128, target / std::max(nt, 1)));
   for (;;) {
     kslice = ((a.K + ks - 1) / ks + 31) / 32 * 32;
     if (kslice <= 32 * RD_KT) break;
