@@ -764,6 +764,8 @@ def main():
         out = dict(metric=METRIC, value=round(value, 1), unit="mel-frames/s", n_gpus=world,
                    steps=a.steps, warmup=a.warmup, ms_per_step=round(1000.0 * el / a.steps, 3),
                    higher_is_better=True, scaling="weak", vs_baseline=None, dtype="f32",
+                   dtype_note=("fp32 storage and accumulation; the decoder / encoder / WaveNet products run as "
+                               "split fp16x3 MFMA (hi/lo fp16 halves, ~2^-22 relative; DESIGN 5.1)"),
                    data="synthetic (seeded ids/ref mels, random-init weights)",
                    config=dict(workload="configs[1]: Tacotron-2 encoder+decoder+Postnet inference, "
                                         "batch=32x200-char synthetic, T_out=1000, 1 batch per GPU",
