@@ -336,6 +336,8 @@ struct TrAtt {
   const float* keys;    // [B,Tin,A]
   const float* values;  // [B,Tin,D]
   const float* Q;       // [T][B][A]
+  const float* qpart;   // non-null: the step's query as raw split-K partials [qks][B][A] (k_tr_att_energy2
+  int qks;              // sums them: no combine launch), else Q
   const float* Kc;      // [KW][F] location conv kernel
   const float* bc;      // [F]
   const float* Wl;      // [F][A]
@@ -448,8 +450,19 @@ __global__ __launch_bounds__(TR_E2T) void k_tr_att_energy2(TrAtt a) {
     key0[r] = (jok && ok0) ? a.keys[((long)b * Tin + j) * A + k0] : 0.f;
     key1[r] = (jok && ok1) ? a.keys[((long)b * Tin + j) * A + k1] : 0.f;
   }
-  const float* q = a.Q + tb * A;
-  const float qb0 = ok0 ? q[k0] + a.ba[k0] : 0.f, qb1 = ok1 ? q[k1] + a.ba[k1] : 0.f;
+  float q0 = 0.f, q1 = 0.f;
+  if (a.qpart) {  // fused split-K combine of the query product (partials in split order)
+    const float* qp = a.qpart + (long)b * A;
+    for (int z = 0; z < a.qks; ++z) {
+      if (ok0) q0 += qp[(long)z * a.B * A + k0];
+      if (ok1) q1 += qp[(long)z * a.B * A + k1];
+    }
+  } else {
+    const float* q = a.Q + tb * A;
+    q0 = ok0 ? q[k0] : 0.f;
+    q1 = ok1 ? q[k1] : 0.f;
+  }
+  const float qb0 = ok0 ? q0 + a.ba[k0] : 0.f, qb1 = ok1 ? q1 + a.ba[k1] : 0.f;
   const float va0 = ok0 ? a.va[k0] : 0.f, va1 = ok1 ? a.va[k1] : 0.f;
   const float* cum_prev = a.CUM + tb * Tin;
   for (int i = tid; i < TR_JT + a.KW - 1; i += TR_E2T) {
@@ -1847,11 +1860,18 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     l2.cn = c->CN2.as<float>() + s1 * H; l2.c_out = c->C2.as<float>() + (s1 + B) * H;
     l2.h_out = PIN + s1 * (H + D); l2.ld_h = H + D; l2.hz_out = X2 + (s1 + B) * 2 * H + H; l2.ld_hz = 2 * H;
     hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l2);
-    tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
-            c->Q.as<float>() + s1 * A, A, s, nullptr, nullptr, 0, ACT_NONE, &c->hWqT, H);
     at.t = t;
-    if (A <= 128 && tr_e2) hipLaunchKernelGGL(k_tr_att_energy2, att_grid, dim3(TR_E2T), 0, s, at);
-    else hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(TR_AT), 0, s, at);
+    if (A <= 128 && tr_e2) {  // query as raw split-K partials, combined inside the energy kernel
+      at.qks = tr_gemm_raw(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A, s,
+                           &c->hWqT, H);
+      at.qpart = c->kpart.as<float>();
+      hipLaunchKernelGGL(k_tr_att_energy2, att_grid, dim3(TR_E2T), 0, s, at);
+      at.qpart = nullptr;
+    } else {
+      tr_gemm(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A,
+              c->Q.as<float>() + s1 * A, A, s, nullptr, nullptr, 0, ACT_NONE, &c->hWqT, H);
+      hipLaunchKernelGGL(k_tr_att_energy, att_grid, dim3(TR_AT), 0, s, at);
+    }
     hipLaunchKernelGGL(k_tr_ctx, dim3((D + 63) / 64, B), dim3(256), sizeof(float) * Tin, s, at);
   }
   tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
