@@ -492,6 +492,15 @@ def main():
     from tt2.synthetic import tacotron_inputs
 
     lib = _lib.load_library()
+    # measured HBM copy bandwidth of this GPU (the spec peak confirmed on the box),
+    # reported beside the spec-priced roofline fractions
+    hbm_meas = ctypes.c_double(0.0)
+    _lib.check(lib.tt2_hbm_copy_gbps(local, ctypes.c_longlong(1 << 30), 5, ctypes.byref(hbm_meas)))
+    hbm_meas = round(hbm_meas.value, 1)
+
+    def meas(achieved):  # the measured-peak companion fields of an HBM roofline
+        return dict(peak_measured=hbm_meas, frac_of_measured=round(achieved / hbm_meas, 4),
+                    peak_measured_how="tt2_hbm_copy_gbps: 1 GiB -> 1 GiB float4 copy, best of 6 shapes x 5, read + write")
     hp = hparams.copy()
     hp.override_from_dict(dict(tacotron_num_gpus=1, max_iters=a.t_out))
     B, T = a.batch, a.chars + 1
@@ -555,7 +564,7 @@ def main():
                         algorithmic_bytes_per_step=int(step_bytes), steps_per_launch=n,
                         avg_launch_us=round(pd_ms * 1000.0, 1),
                         us_per_step=round(pd_ms * 1000.0 / max(n, 1), 3),
-                        traffic_per_step=(round(traffic / n) if traffic else None))
+                        traffic_per_step=(round(traffic / n) if traffic else None), **meas(achieved))
         if os.environ.get("TT2_STAMP_STEP"):
             st = (ctypes.c_longlong * 8192)()
             _lib.check(lib.tt2_debug_pd_stamps(eng.h, st))
@@ -642,7 +651,7 @@ def main():
                                 bound="latency (serial sample chain; weights register-resident)",
                                 achieved=round(wach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                                 frac=round(wach / HBM_PEAK_GBS, 5),
-                                algorithmic_bytes_per_sample=int(wbytes)),
+                                algorithmic_bytes_per_sample=int(wbytes), **meas(wach)),
                   diag_stage_stamps_us=wn_stamps, diag_shader_clock_mhz=wn_clock_mhz)
         weng.close()
         # batched synthesis at wavenet_synthesis_batch_size (hparams.py:332): 20 utterances of the

@@ -244,6 +244,11 @@ tt2_status tt2_decoder_path(tt2_ctx* ctx, int* persistent, float* kernel_ms);
 /* Persistent decode run with env TT2_STAMP_STEP=k: s_memrealtime (100 MHz) stamps [256 work-groups]
  * [32 stage points] of step k (k_decode_persist PD_STAMP sites).  Diagnostic only. */
 tt2_status tt2_debug_pd_stamps(tt2_ctx* ctx, long long* out8192);
+/* Measured HBM bandwidth of this device (the spec peak confirmed on the box): a
+ * STREAM-like copy between two `bytes`-sized device buffers (choose >> the 256 MB MALL), 16-byte
+ * loads/stores; *gbps = (read + write bytes) / the best of `iters` timed copies, in GB/s.  No
+ * reference counterpart (measurement only). */
+tt2_status tt2_hbm_copy_gbps(int hip_device, long long bytes, int iters, double* gbps);
 
 /* ------------------------------------------------------------------------------------------ */
 /* WaveNet MoL vocoder (replaces wavenet_vocoder/models/wavenet.py WaveNet.initialize synthesis */

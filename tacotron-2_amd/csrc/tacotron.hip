@@ -2415,6 +2415,30 @@ static void postnet_dev(tt2_ctx* c, const float* frames_d, long frames_bstride, 
 
 using namespace tt2;
 
+namespace tt2 {
+// STREAM-like copy (confirm the HBM peak on the box next to the 8 TB/s spec):
+// dst = src over two `bytes` buffers (>> the 256 MB MALL), 16-byte loads and stores; each
+// work-group copies contiguous 256·U-float4 blocks with all U loads in flight before the stores
+// (NT: non-temporal loads / stores).  Counted bytes = read + write.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_hbm_copy(const f32x4* __restrict__ src, f32x4* __restrict__ dst, long n4) {
+  const long nblk = n4 / (256L * U);
+  for (long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const long base = blk * 256L * U + threadIdx.x;
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + base + 256L * u) : src[base + 256L * u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT) __builtin_nontemporal_store(v[u], dst + base + 256L * u);
+      else dst[base + 256L * u] = v[u];
+    }
+  }
+  for (long i = nblk * 256L * U + (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
+}  // namespace tt2
+
 extern "C" {
 
 const char* tt2_last_error(void) { return g_last_error.c_str(); }
@@ -2854,6 +2878,47 @@ tt2_status tt2_profile_decoder_kernels(tt2_ctx* c, int iters, float* avg_us) {
     TT2_HIP(hipEventDestroy(e1));
     TT2_HIP(hipMemcpy(c->stamps_host, g_stamps_dev, 64 * sizeof(long long), hipMemcpyDeviceToHost));
     c->decoded = false;
+  });
+}
+
+tt2_status tt2_hbm_copy_gbps(int hip_device, long long bytes, int iters, double* gbps) {
+  return guard([&] {
+    TT2_CHECK(gbps && bytes >= (1LL << 20) && iters >= 1, TT2_ERR_INVALID_ARG,
+              "tt2_hbm_copy_gbps: bytes >= 1 MiB, iters >= 1, gbps non-null");
+    TT2_HIP(hipSetDevice(hip_device));
+    hipDeviceProp_t prop;
+    TT2_HIP(hipGetDeviceProperties(&prop, hip_device));
+    const long n4 = (long)(bytes / 16);
+    DevBuf a, b;
+    a.alloc((size_t)n4 * 16);
+    b.alloc((size_t)n4 * 16);
+    TT2_HIP(hipMemset(a.p, 0, (size_t)n4 * 16));
+    hipStream_t s;
+    TT2_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipEvent_t e0, e1;
+    TT2_HIP(hipEventCreate(&e0));
+    TT2_HIP(hipEventCreate(&e1));
+    // a few copy shapes (blocks in flight per CU x float4s in flight per thread x cache policy);
+    // the best of all timed copies is the measured peak
+    float best = 1e30f;
+    for (int v = 0; v < 6; ++v) {
+      const dim3 grid((unsigned)((v % 3 == 0 ? 4 : v % 3 == 1 ? 8 : 16) * prop.multiProcessorCount));
+      for (int it = -1; it < iters; ++it) {  // it = -1: warm-up (page mapping, clocks)
+        TT2_HIP(hipEventRecord(e0, s));
+        if (v < 3) hipLaunchKernelGGL((k_hbm_copy<8, false>), grid, dim3(256), 0, s, a.as<f32x4>(), b.as<f32x4>(), n4);
+        else hipLaunchKernelGGL((k_hbm_copy<8, true>), grid, dim3(256), 0, s, a.as<f32x4>(), b.as<f32x4>(), n4);
+        TT2_HIP(hipGetLastError());
+        TT2_HIP(hipEventRecord(e1, s));
+        TT2_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
+        TT2_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (it >= 0) best = std::min(best, ms);
+      }
+    }
+    TT2_HIP(hipEventDestroy(e0));
+    TT2_HIP(hipEventDestroy(e1));
+    TT2_HIP(hipStreamDestroy(s));
+    *gbps = 2.0 * (double)n4 * 16.0 / ((double)best * 1e-3) / 1e9;
   });
 }
 

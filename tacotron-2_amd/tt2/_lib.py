@@ -121,6 +121,7 @@ SIGNATURES = {
     "tt2_debug_stamps": (_I, [_P, _P]),
     "tt2_decoder_path": (_I, [_P, _P, _P]),
     "tt2_debug_pd_stamps": (_I, [_P, _P]),
+    "tt2_hbm_copy_gbps": (_I, [_I, ctypes.c_longlong, _I, _P]),
     "tt2_set_emt_labels": (_I, [_P, _P, _I]),
     "tt2_linear_outputs": (_I, [_P, _P, _I, _I, _P]),
     "tt2_linear_outputs_dev": (_I, [_P, _P, _I, _I, _P, _P]),
