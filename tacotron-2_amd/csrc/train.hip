@@ -451,11 +451,27 @@ __global__ __launch_bounds__(TR_E2T) void k_tr_att_energy2(TrAtt a) {
     key1[r] = (jok && ok1) ? a.keys[((long)b * Tin + j) * A + k1] : 0.f;
   }
   float q0 = 0.f, q1 = 0.f;
-  if (a.qpart) {  // fused split-K combine of the query product (partials in split order)
+  if (a.qpart) {  // fused split-K combine of the query product (partials in split order; up to 16
+                  // splits loaded in one round trip, before any sum)
     const float* qp = a.qpart + (long)b * A;
-    for (int z = 0; z < a.qks; ++z) {
-      if (ok0) q0 += qp[(long)z * a.B * A + k0];
-      if (ok1) q1 += qp[(long)z * a.B * A + k1];
+    const long zs = (long)a.B * A;
+    if (a.qks <= 16) {
+      float p0[16], p1[16];
+#pragma unroll
+      for (int z = 0; z < 16; ++z) {
+        p0[z] = (z < a.qks && ok0) ? qp[z * zs + k0] : 0.f;
+        p1[z] = (z < a.qks && ok1) ? qp[z * zs + k1] : 0.f;
+      }
+#pragma unroll
+      for (int z = 0; z < 16; ++z) {
+        q0 += p0[z];
+        q1 += p1[z];
+      }
+    } else {
+      for (int z = 0; z < a.qks; ++z) {
+        if (ok0) q0 += qp[z * zs + k0];
+        if (ok1) q1 += qp[z * zs + k1];
+      }
     }
   } else {
     const float* q = a.Q + tb * A;
