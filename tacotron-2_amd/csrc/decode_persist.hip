@@ -325,15 +325,19 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     wl[0] = LW[lane];
     wl[1] = LW[64 + lane];
   }
-  float b1v[4], b2v[4], gsv[4];
+  // LSTM epilogue constants of thread tid < 128 (row em, unit eu) in LDS, not VGPRs (the kernel
+  // is at its 256-VGPR budget): cst[(k*4 + q)*128 + tid], k = 0 b1, 1 b2, 2 style term
+  float* const cst = RG1;  // RG1 | RG2 | RGc: 1536 floats, otherwise unused
   const int u0 = pd_unit(g, 0);  // this work-group's hidden units pd_unit(g, 0..3): one AF float4 per row
+  if (tid < 128) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int u = pd_unit(g, eu);
-    const int col = (u >> 2) * 16 + 4 * q + (u & 3);  // biases / style terms come in lstm_cols order
-    b1v[q] = a.l1_b[col];
-    b2v[q] = a.l2_b[col];
-    gsv[q] = a.GS[(long)em * 4 * PD_H + col];
+    for (int q = 0; q < 4; ++q) {
+      const int u = pd_unit(g, eu);
+      const int col = (u >> 2) * 16 + 4 * q + (u & 3);  // biases / style terms come in lstm_cols order
+      cst[q * 128 + tid] = a.l1_b[col];
+      cst[(4 + q) * 128 + tid] = a.l2_b[col];
+      cst[(8 + q) * 128 + tid] = a.GS[(long)em * 4 * PD_H + col];
+    }
   }
   float c1 = 0.f, c2 = 0.f;  // cell states of (em, unit 4g+eu), threads < 128
   const int len = rowv ? a.lengths[b] : 0;
@@ -543,7 +547,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = em * 16 + 4 * q + eu;
-        z[q] = (sum_partials<8>(red, idx) * KG_UNSCALE + ssa[em] * gsv[q]) + b1v[q];
+        z[q] = (sum_partials<8>(red, idx) * KG_UNSCALE + ssa[em] * cst[(8 + q) * 128 + tid]) + cst[q * 128 + tid];
       }
       const float cn = sigm_fast(z[2] + 1.0f) * c1 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
@@ -584,7 +588,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = em * 16 + 4 * q + eu;
-        z[q] = sum_partials<8>(red, idx) * KG_UNSCALE + b2v[q];
+        z[q] = sum_partials<8>(red, idx) * KG_UNSCALE + cst[(4 + q) * 128 + tid];
       }
       const float cn = sigm_fast(z[2] + 1.0f) * c2 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
