@@ -47,7 +47,7 @@ typedef __attribute__((address_space(1))) unsigned long long pd_gu64;
 #define PD_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 
 constexpr long long PD_TIMEOUT = 200000000LL;  // 2 s of s_memrealtime (100 MHz)
-constexpr int PD_LDS_FLOATS = 16384 * 2 + 4096 + 512 * 5 + 288 + 256 * 2 + 32 + 16 + 16 + 16;  // 157.6 KB
+constexpr int PD_LDS_FLOATS = 16384 * 2 + 4096 + 512 * 5 + 288 + 256 * 2 + 32 + 16 + 16 + 16 + 512;  // 159.6 KB
 
 // write-through (sc1) stores and L1-bypassing (sc1) loads of hand-off data
 __device__ __forceinline__ float pd_ld(const float* p) {
@@ -319,12 +319,9 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     if (isq && w < a.e_KC / 128)
       wdf = reinterpret_cast<const f32x4*>(a.e_wd + (long)(pn - PD_NTILE) * a.e_KC * 16)[(pks * (a.e_KC / 128) + w) * 64 + lane];
   }
-  f32x4 wl[2];
-  {
-    const f32x4* LW = reinterpret_cast<const f32x4*>(a.loc_cw + (long)j * PD_KLP * 16);
-    wl[0] = LW[lane];
-    wl[1] = LW[64 + lane];
-  }
+  // location-conv WF fragments of this slice in LDS (2 KB after si: the same for every wave)
+  f32x4* const swl = reinterpret_cast<f32x4*>(si + 16);
+  if (tid < 128) swl[tid] = reinterpret_cast<const f32x4*>(a.loc_cw + (long)j * PD_KLP * 16)[tid];
   // LSTM epilogue constants of thread tid < 128 (row em, unit eu) in LDS, not VGPRs (the kernel
   // is at its 256-VGPR budget): cst[(k*4 + q)*128 + tid], k = 0 b1, 1 b2, 2 style term
   float* const cst = RG1;  // RG1 | RG2 | RGc: 1536 floats, otherwise unused
@@ -769,7 +766,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          l = __builtin_amdgcn_mfma_f32_16x16x4f32(cw[t0 + 16 * sg + 4 * e], wl[sg][e], l, 0, 0, 0);
+          l = __builtin_amdgcn_mfma_f32_16x16x4f32(cw[t0 + 16 * sg + 4 * e], swl[64 * sg + lane][e], l, 0, 0, 0);
       loc[i] = l;
     }
     // ================= E: projection partial, context rows =================
