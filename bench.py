@@ -7,8 +7,9 @@ synthesis of a 32-utterance batch (200 chars + EOS, T_out = 1000 decoder frames,
 weights of the fork-default architecture, D_mem = 1024).  The ``wavenet`` object carries
 configs[2] (24-layer R=64 MoL WaveNet, batch 1, 22.05 kHz): audio-samples/s.
 
-Multi-GPU (``--gpus N`` under torch.distributed.run): one rank per GPU, each rank synthesises its
-own batch (utterance-batch sharding) — weak scaling, no collective in the timed
+Multi-GPU (``--gpus N``; bench.py starts the N ranks itself under torch.distributed.run when it is
+not already one of them, and refuses a WORLD_SIZE that disagrees with --gpus): one rank per GPU,
+each rank synthesises its own batch (utterance-batch sharding) — weak scaling, no collective in the timed
 region; the timed region is bracketed by barrier + synchronize and the max over ranks is reported.
 """
 import argparse
@@ -67,7 +68,87 @@ def parse():
     p.add_argument("--no-variants", action="store_true",
                    help="skip the model-variant legs (Tacotron_emt_attn, style paths, CBHG)")
     p.add_argument("--profile-iters", type=int, default=50)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher rehearsal without a GPU: the ranks rendezvous over gloo, run the "
+                        "barrier / max-over-ranks timing around a CPU stand-in step and print the JSON "
+                        "line (tests/test_bench_launcher.py)")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def launch_ranks(a):
+    """``--gpus N`` (N > 1) outside torch.distributed.run: start the N ranks as ONE child
+    ``python -m torch.distributed.run --nproc-per-node N`` (rendezvous on 127.0.0.1) and return its
+    exit status.  Runs before anything touches the GPU (counting devices does not initialise HIP on
+    this image), and never exec()s: the ranks are children of this process."""
+    import subprocess
+    if not a.dry_run:
+        import torch
+        n = torch.cuda.device_count()
+        if n < a.gpus:
+            sys.exit("bench.py: --gpus {} but only {} GPU(s) visible".format(a.gpus, n))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node={}".format(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ, TT2_BENCH_LAUNCHED="1")
+    return subprocess.call(cmd, env=env)
+
+
+def world_from_env(a):
+    """(world, rank, local) of this rank; the world must agree with --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        sys.exit("bench.py: --gpus {} disagrees with WORLD_SIZE={} (run `python bench.py --gpus N` "
+                 "or torch.distributed.run --nproc-per-node N ... bench.py --gpus N)".format(a.gpus, world))
+    return world, rank, local
+
+
+def dry_run(a, world, rank):
+    """The multi-rank skeleton of main() on CPU: gloo rendezvous, warmup, barrier-bracketed timed
+    steps of a fixed CPU stand-in workload, max over ranks, one JSON line from rank 0."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+    x = np.random.default_rng(rank).standard_normal((256, 256)).astype(np.float32)
+
+    def step():
+        y = x
+        for _ in range(4):
+            y = np.tanh(y @ x)
+        return int(a.batch)
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    frames = sum(step() for _ in range(a.steps))
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        fr = torch.tensor([frames], dtype=torch.int64)
+        dist.all_reduce(fr)
+        frames = int(fr.item())
+    if rank == 0:
+        print(json.dumps(dict(metric=METRIC, value=round(frames / el, 1), unit="stand-in rows/s", n_gpus=world,
+                              steps=a.steps, warmup=a.warmup, ms_per_step=round(1e3 * el / a.steps, 3),
+                              higher_is_better=True, scaling="weak", dry_run=True,
+                              ranks_launched_by_bench=os.environ.get("TT2_BENCH_LAUNCHED") == "1")))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def lstm_bytes(K, H, M=32):
@@ -462,11 +543,17 @@ def _profiled():
 
 def main():
     a = parse()
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))  # the N ranks run as children; their rank 0 prints the line
+    world, rank, local = world_from_env(a)
+    if a.dry_run:
+        return dry_run(a, world, rank)
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.device_count() < world:
+        sys.exit("bench.py: WORLD_SIZE={} but only {} GPU(s) visible".format(world, torch.cuda.device_count()))
     guard = _profiled()
     if guard:  # before the first device call: see tt2_exit_guard (include/tt2.h), DESIGN.md §7
         _lib.load_library().tt2_exit_guard(1, 1)
