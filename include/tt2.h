@@ -513,7 +513,9 @@ tt2_status tt2_train_losses(tt2_train_ctx* ctx, float* out5, float* fb_ms);
 /* which: 0 = parameter, 1 = gradient, 2 = Adam m, 3 = Adam v; name "memory" (which ignored) =
  * d loss / d memory [B,T_in,D] of the last forward_backward; on a frontend context also
  * "frontend:memory" = the memory the front end produced [B,T_in,D] and "frontend:refnet_emt" /
- * "frontend:refnet_spk" = the reference embeddings [B,128] (diagnostic read-backs); "diag:blas_calls"
+ * "frontend:refnet_spk" = the reference embeddings [B,128] (diagnostic read-backs); with the Postnet
+ * "postnet:projection" = the Postnet projection [B,T,80] of the last forward (mel_outputs =
+ * clip(decoder_output + it), tacotron.py:375-378); "diag:blas_calls"
  * = one float, the number of products routed to rocBLAS since create (bf16 mode). */
 tt2_status tt2_train_get_tensor(tt2_train_ctx* ctx, const char* tf_name, int which, float* host);
 /* Last forward's decoder frames [B,T,80], stop logits [B,T], alignments [B,T_in,T] (nullable). */

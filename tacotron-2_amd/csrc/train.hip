@@ -2608,6 +2608,9 @@ tt2_status tt2_train_set_target_lengths(tt2_train_ctx* c, const int32_t* lengths
       mx = std::max(mx, (int)lengths[b]);
     }
     TT2_HIP(hipSetDevice(c->dev));
+    // TLEN is read by the loss kernels of a forward_backward that may still be running on the
+    // caller's (non-blocking) stream: let it finish before the lengths change under it
+    if (c->last_stream) TT2_HIP(hipStreamSynchronize(c->last_stream));
     TT2_HIP(hipMemcpy(c->TLEN.p, lengths, sizeof(int) * (size_t)c->B, hipMemcpyHostToDevice));
     c->has_tlen = true;
     c->tlen_sum = sum;
@@ -2873,6 +2876,10 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
     }
     if (std::string(name) == "memory") {  // d loss / d memory of the last forward_backward
       tr_d2h(c, host, c->DMEM.p, sizeof(float) * (size_t)c->B * c->Tin_last * c->D);
+      return;
+    }
+    if (c->cfg.postnet && std::string(name) == "postnet:projection") {  // Postnet residual [B,T,NM]
+      tr_d2h(c, host, c->PPRJ.p, sizeof(float) * (size_t)c->B * c->T_last * c->NM);
       return;
     }
     if (c->cfg.frontend && std::string(name) == "frontend:memory") {  // the front end's memory [B,T_in,D]

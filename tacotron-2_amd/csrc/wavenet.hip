@@ -854,8 +854,8 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   g.split16 = 1;  // conditioning in [0, 1] after the upsampler: fp16x3 split MFMA (gemm.h)
   gemm(g, s);
   if (c->cfg.gin_channels > 0) {  // + g·W_g + b_g of every layer (constant over time)
-    TT2_CHECK(c->gc_B >= B, TT2_ERR_STATE,
-              "gin_channels > 0: tt2_wn_set_global_condition for these rows before generating");
+    TT2_CHECK(c->gc_B == B, TT2_ERR_STATE,
+              "gin_channels > 0: tt2_wn_set_global_condition for exactly these B rows before generating");
     const long n = (long)B * T * c->L * c->G;
     hipLaunchKernelGGL(k_add_gc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->cond.as<float>(),
                        c->gcv.as<float>(), B, (long)T, c->L * c->G);

@@ -3,9 +3,14 @@
 ``Tacotron.initialize`` keeps the reference's signature and argument validation but runs eagerly:
 instead of building a TF graph it executes encoder → decoder loop → Postnet through libtt2.so and
 stores numpy arrays in the reference's ``tower_*`` attributes (one list entry per tower).
-Training through this class (is_training=True) would also train the encoder, GST and reference
-encoders, whose backward is not built; the decoder + Postnet training step is
-``tt2.train.TacotronTrainer``.
+
+Training keeps the reference's three calls (tacotron/train.py:104-139 builds them once and runs
+them every step; here each call does its part of the step eagerly):
+``initialize(..., is_training=True)`` runs the whole teacher-forced forward + backward (encoder,
+both reference encoders + GST, decoder, Postnet; training-mode batch norm, dropout and zoneout)
+on ``tt2.train.TacotronTrainer``, ``add_loss()`` exposes the losses under the reference's names,
+``add_optimizer(global_step)`` runs the tower mean (RCCL, one process per tower), clip + Adam and
+the moving-statistics update.
 """
 import os
 
@@ -74,6 +79,8 @@ class Tacotron():
         self._engine = None
         self.device = int(os.environ.get("LOCAL_RANK", "0")) if "TT2_DEVICE" not in os.environ \
             else int(os.environ["TT2_DEVICE"])
+        self._trainer = None
+        self._train_key = None
 
     # -- weights (replaces tf.train.Saver.restore, tacotron/synthesizer.py:93-94) -------------
     def load_weights(self, weights):
@@ -135,11 +142,20 @@ class Tacotron():
                    ref_mel_emt=None, ref_mel_spk=None, ref_mel_up_emt=None, ref_mel_up_spk=None,
                    use_emt_disc=False, use_spk_disc=False, use_intercross=False,
                    use_unpaired=False, n_emt=None, n_spk=None, synth=False,
-                   prenet_masks=None, seed=0):
+                   prenet_masks=None, seed=0, train_masks=None, train_capacity=None,
+                   precision="fp32"):
         """Same arguments as the reference (tacotron.py:31-35) plus the injected prenet dropout
         keep-masks ``prenet_masks`` [max_iters, 2, B_total, 256] over every tower's utterances in
         tower order, or a list with one [max_iters, 2, B, 256] array per tower (None = device RNG
-        keyed by ``seed``)."""
+        keyed by ``seed``).
+
+        is_training=True: the training step's forward + backward (see the module docstring).
+        ``train_masks`` = dict of injected keep bits of this process's tower (keys 'prenet',
+        'zoneout', 'postnet', 'enc_conv', 'enc_zoneout' in the layouts TacotronTrainer takes;
+        missing ones are drawn at the hparams' rates from a generator seeded by ``seed``);
+        ``train_capacity`` = dict(max_T_in, max_T_out, max_T_ref) sizes the training context at
+        the first call (default: that call's sizes); ``precision`` 'fp32' or 'bf16' (GEMM operands,
+        configs[4])."""
         hp = self._hparams
         # argument validation, tacotron.py:48-71
         if mel_targets is None and stop_token_targets is not None:
@@ -171,10 +187,9 @@ class Tacotron():
         if use_unpaired and not (getattr(args, "pretrained_emb_disc_all", False)):
             raise ValueError('must use unpaired with pretrained_emb_disc_all')
         # scope of the MI355X path
-        if is_training or is_evaluating:
-            raise NotImplementedError("training / eval-loss graphs of the whole model are not built "
-                                      "(no encoder/GST backward); the decoder + Postnet training "
-                                      "step is tt2.train.TacotronTrainer")
+        if is_evaluating:
+            raise NotImplementedError("the eval-loss graph (is_evaluating=True) is not built; "
+                                      "evaluate by synthesis (gta=True) or a training step's losses")
         if use_unpaired:
             raise NotImplementedError("the unpaired decode (tacotron.py:389-461) is a training-graph "
                                       "branch (teacher-forced on mel_targets); synthesis never builds it")
@@ -185,6 +200,11 @@ class Tacotron():
         if ref_mel_emt is None or (ref_mel_spk is None and not emt_only):
             raise ValueError("must provide references")  # refnet_emt / refnet_spk inputs (:251-259)
         constraint = bool(getattr(args, "synth_constraint", False))
+        if is_training:
+            return self._initialize_training(
+                inputs, input_lengths, mel_targets, stop_token_targets, targets_lengths, split_infos,
+                ref_mel_emt, ref_mel_spk, emt_only, style, use_emt_disc or use_spk_disc or use_intercross,
+                train_masks, train_capacity, precision, seed)
 
         tower_inputs, tower_lengths, tower_ref_emt, tower_ref_spk, tower_targets = split_towers(
             hp, inputs, input_lengths, split_infos, ref_mel_emt, ref_mel_spk, mel_targets)
@@ -224,3 +244,164 @@ class Tacotron():
             if hp.predict_linear and not gta:  # post_condition (tacotron.py:214, 466-481)
                 self.tower_linear_outputs.append(eng.linear_outputs(out["mel_outputs"]))
         self.all_vars = list(self._weights.keys())
+
+    # -- training (tacotron.py:31-35 is_training=True, add_loss :683, add_optimizer :1002) ----------
+    def _tower_index(self, ntow):
+        """This process's tower: one process per GPU (torch.distributed), rank r = tower r; the
+        reference's towers share one process and average on the CPU (tacotron.py:1194-1208).
+        Each rank passes either the packed batch of every tower (split_infos) or its own."""
+        if ntow == 1:
+            return 0
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() != ntow:
+            raise NotImplementedError("tacotron_num_gpus={} towers train as one process per GPU: launch "
+                                      "{} ranks (torch.distributed) or set tacotron_num_gpus=1".format(ntow, ntow))
+        return dist.get_rank()
+
+    def _initialize_training(self, inputs, input_lengths, mel_targets, stop_token_targets, targets_lengths,
+                             split_infos, ref_mel_emt, ref_mel_spk, emt_only, style, disc, train_masks,
+                             train_capacity, precision, seed):
+        from tt2 import synthetic as S
+        from tt2.train import TacotronTrainer
+        hp = self._hparams
+        if self._weights is None:
+            raise RuntimeError("Tacotron weights not loaded: call load_weights() (checkpoint) or "
+                               "init_random_weights()")
+        if mel_targets is None or stop_token_targets is None:
+            raise ValueError("training needs mel_targets and stop_token_targets")
+        if style != "gst" or not hp.use_gst:
+            raise NotImplementedError("training builds the GST style path (adain / embeddings-only "
+                                      "front ends are synthesis-only on this build)")
+        if disc:
+            raise NotImplementedError("the style-embedding discriminators (use_emt_disc / use_spk_disc / "
+                                      "intercross) are not built")
+        if hp.outputs_per_step != 1:
+            raise NotImplementedError("outputs_per_step = 1 on this build")
+        if hp.tacotron_use_style_emb_disc or hp.tacotron_use_orthog_loss:
+            raise NotImplementedError("the style-embedding classifier / orthogonality losses "
+                                      "(tacotron.py:486-495, 812-846) are not built yet: set "
+                                      "tacotron_use_style_emb_disc=False, tacotron_use_orthog_loss=False")
+        tower_inputs, tower_lengths, tower_ref_emt, tower_ref_spk, tower_targets = split_towers(
+            hp, inputs, input_lengths, split_infos, ref_mel_emt, ref_mel_spk, mel_targets)
+        ntow = len(tower_inputs)
+        rank = self._tower_index(hp.tacotron_num_gpus)
+        # the time-axis-packed batch of every tower (split_infos), or this rank's own batch
+        i = rank if ntow > 1 else 0
+        B = tower_lengths[i].shape[0]
+        ids = np.ascontiguousarray(tower_inputs[i].reshape(B, -1))
+        T_in = ids.shape[1]
+        ref_e = np.ascontiguousarray(tower_ref_emt[i].reshape(B, -1, hp.num_mels))
+        ref_s = (ref_e if emt_only or tower_ref_spk[i] is None
+                 else np.ascontiguousarray(tower_ref_spk[i].reshape(B, -1, hp.num_mels)))
+        T_ref = ref_e.shape[1]
+        tg = np.ascontiguousarray(tower_targets[i].reshape(B, -1, hp.num_mels))
+        T_out = tg.shape[1]
+        stop = np.asarray(stop_token_targets, np.float32)
+        if split_infos is not None and ntow > 1:
+            stop = split_func(stop, np.asarray(split_infos, np.int32)[:, 2])[i]
+        stop = np.ascontiguousarray(stop.reshape(B, T_out))
+        tlen = None
+        if targets_lengths is not None:
+            tlen = np.split(np.asarray(targets_lengths, np.int32).reshape(-1), ntow)[i]
+        cap = dict(max_T_in=T_in, max_T_out=T_out, max_T_ref=T_ref)
+        cap.update(train_capacity or {})
+        key = (B, emt_only, precision)
+        tr = self._trainer
+        if tr is not None and (self._train_key != key or T_in > self._train_cap["max_T_in"]
+                               or T_out > self._train_cap["max_T_out"] or T_ref > self._train_cap["max_T_ref"]):
+            raise ValueError("training batch {} exceeds the training context sized at the first step {}: "
+                             "pass train_capacity= with the largest sizes on the first call".format(
+                                 dict(B=B, T_in=T_in, T_out=T_out, T_ref=T_ref), self._train_cap))
+        if tr is None:
+            tr = TacotronTrainer(hp, self._weights, B, cap["max_T_in"], cap["max_T_out"], self.device,
+                                 emt_only=emt_only, precision=precision, postnet=True, frontend=True,
+                                 max_T_ref=cap["max_T_ref"], tf_seed=seed)
+            self._trainer, self._train_key, self._train_cap = tr, key, cap
+            self._mask_rng = np.random.default_rng(seed)
+        tr.set_step_inputs(targets_lengths=tlen)
+        m = dict(train_masks or {})
+        r = self._mask_rng
+        sub = lambda: int(r.integers(1 << 31))  # noqa: E731  (one fresh stream per mask per step)
+        P, H, U = hp.prenet_layers[0], hp.decoder_lstm_units, hp.encoder_lstm_units
+        zr, dr = hp.tacotron_zoneout_rate, hp.tacotron_dropout_rate
+        masks = dict(
+            prenet=m.get("prenet") if "prenet" in m else S.prenet_masks(T_out, B, P, seed=sub()),
+            zoneout=m.get("zoneout") if "zoneout" in m else S.zoneout_masks(T_out, B, H, zr, seed=sub()),
+            postnet=m.get("postnet") if "postnet" in m else S.postnet_masks(
+                hp.postnet_num_layers, B, T_out, hp.postnet_channels, dr, seed=sub()),
+            enc_conv=m.get("enc_conv") if "enc_conv" in m else S.enc_conv_masks(
+                hp.enc_conv_num_layers, B, T_in, hp.enc_conv_channels, dr, seed=sub()),
+            enc_zoneout=m.get("enc_zoneout") if "enc_zoneout" in m else S.enc_zoneout_masks(
+                T_in, B, U, zr, seed=sub()))
+        tr.forward_backward_text(ids, tower_lengths[i], ref_e, ref_s, tg, stop, masks["prenet"],
+                                 masks["zoneout"], masks["postnet"], masks["enc_conv"], masks["enc_zoneout"])
+        fr, st, al = tr.outputs(T_in, T_out)
+        self.ratio = tr.ratio if tr.ratio is not None else 1.0
+        self.tower_decoder_output = [fr]
+        self.tower_stop_token_prediction = [st]   # logits: StopProjection skips the sigmoid in training
+        self.tower_alignments = [al]
+        self.tower_mel_outputs = [tr.mel_outputs(T_out)]
+        self.tower_inputs, self.tower_input_lengths = [ids], [tower_lengths[i]]
+        self.tower_mel_targets, self.tower_stop_token_targets = [tg], [stop]
+        self.tower_ref_mel_emt, self.tower_ref_mel_spk = [ref_e], [ref_s]
+        self.tower_linear_outputs = []
+        self.all_vars = list(self._weights.keys())
+        self._losses = None
+
+    def add_loss(self):
+        """tacotron.py:683-1000 for this process's tower: before / after / stop-token /
+        regularization losses of the step initialize(is_training=True) just ran (the
+        discriminator / unpaired losses are 0: those graphs are not built)."""
+        tr = self._trainer
+        if tr is None:
+            raise RuntimeError("add_loss: call initialize(..., is_training=True) first")
+        L = tr.losses()
+        self._losses = L
+        self.before_loss, self.after_loss = L["before"], L["after"]
+        self.stop_token_loss, self.regularization_loss = L["stop_token"], L["regularization"]
+        self.linear_loss = 0.0
+        for n in ("style_emb_loss_emt", "style_emb_loss_spk", "style_emb_orthog_loss", "style_emb_loss_up_emt",
+                  "style_emb_loss_up_spk", "style_emb_loss_mel_out_up_emt", "style_emb_loss_mel_out_up_spk",
+                  "g_loss_p", "g_loss_up"):
+            setattr(self, n, 0.0)
+            setattr(self, "tower_" + n, [0.0])
+        self.loss = L["loss"]
+        self.loss_no_mo_up = L["loss"]
+        self.tower_before_loss, self.tower_after_loss = [self.before_loss], [self.after_loss]
+        self.tower_stop_token_loss = [self.stop_token_loss]
+        self.tower_regularization_loss = [self.regularization_loss]
+        self.tower_linear_loss = [0.0]
+        self.tower_loss = [self.loss]
+        return self.loss
+
+    def add_optimizer(self, global_step=None):
+        """tacotron.py:1002-1109: tower mean of the gradients (one RCCL all-reduce across the
+        ranks), clip_by_global_norm(1.0), Adam at the decayed learning rate of ``global_step``
+        (the value BEFORE this update, as TF reads the variable; None = the trainer's own count),
+        then the batch-norm moving statistics (UPDATE_OPS) composed over the ranks.  Sets
+        ``learning_rate``, ``optimize`` (the global step after the update) and ``grad_norm``."""
+        tr = self._trainer
+        if tr is None:
+            raise RuntimeError("add_optimizer: call initialize(..., is_training=True) first")
+        gs = tr.global_step if global_step is None else int(global_step)
+        L = tr.optimizer_step(gs + 1)
+        from tt2.train import learning_rate
+        self.learning_rate = learning_rate(gs, self._hparams)
+        self.optimize = tr.global_step
+        self.grad_norm = L["grad_norm"]
+        return self.optimize
+
+    def trained_weights(self):
+        """The trainer's current parameters as {TF variable name: array} (what tf.train.Saver
+        would save), also made this model's weights for synthesis."""
+        tr = self._trainer
+        if tr is None:
+            return dict(self._weights)
+        from tt2._lib import TT2Error
+        for n, v in list(self._weights.items()):
+            try:
+                self._weights[n] = tr.get(n, 0, np.asarray(v).shape)
+            except TT2Error:  # not a variable of the training graph (e.g. the CBHG / emt heads)
+                pass
+        self._engine = None
+        return dict(self._weights)

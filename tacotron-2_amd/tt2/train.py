@@ -54,6 +54,9 @@ def draw_teacher_forcing(T_out, ratio, rng):
     return feed
 
 
+_UNSET = object()
+
+
 def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32", postnet=True,
                  frontend=False, max_T_ref=None):
     lib = _lib.load_library()
@@ -128,7 +131,7 @@ class TacotronTrainer(object):
     runs on the trainer's own torch stream (passed to the library explicitly)."""
 
     def __init__(self, hp, weights, batch, max_T_in, max_T_out, device=0, emt_only=False,
-                 precision="fp32", postnet=True, frontend=False, max_T_ref=None):
+                 precision="fp32", postnet=True, frontend=False, max_T_ref=None, tf_seed=None):
         import torch
         self.torch = torch
         self.lib = _lib.load_library()
@@ -157,6 +160,11 @@ class TacotronTrainer(object):
         self.bind_grad_buffer()
         self.global_step = 0
         self._keep = None
+        # teacher forcing: drawn per step from the ratio schedule (TacoTrainingHelper) unless the
+        # caller injects the draw through set_step_inputs(feed_target=...)
+        self._feed_explicit = False
+        self._tf_rng = np.random.default_rng(hp.tacotron_random_seed if tf_seed is None else tf_seed)
+        self.ratio = None
 
     def close(self):
         if getattr(self, "h", None):
@@ -185,24 +193,46 @@ class TacotronTrainer(object):
             return a.to(self.device, dtype).contiguous()
         return t.from_numpy(np.ascontiguousarray(a)).to(self.device, dtype, non_blocking=False)
 
-    def set_step_inputs(self, targets_lengths=None, feed_target=None):
-        """Per-step inputs of the reference's training graph beyond the tensors: targets_lengths
-        [B] (mask_decoder's loss masks, tacotron.py:56,758-767; required when hp.mask_decoder) and
-        feed_target [T_out] u8 (the teacher-forcing draw, draw_teacher_forcing; None = every
-        step teacher-forced).  They stay in effect for later steps until changed."""
-        if targets_lengths is None:
-            check(self.lib.tt2_train_set_target_lengths(self.h, None))
-        else:
-            tl = np.ascontiguousarray(np.asarray(targets_lengths, np.int32))
-            if tl.shape != (self.B,):
-                raise ValueError("targets_lengths must be [batch]")
-            check(self.lib.tt2_train_set_target_lengths(self.h, tl.ctypes.data_as(ctypes.c_void_p)))
+    def set_step_inputs(self, targets_lengths=_UNSET, feed_target=_UNSET):
+        """Per-step inputs of the reference's training graph beyond the tensors; an argument left
+        out keeps its current setting.  targets_lengths [B] (mask_decoder's loss masks,
+        tacotron.py:56,758-767; required when hp.mask_decoder; None clears them).  feed_target
+        [T_out] u8 injects the teacher-forcing draw (draw_teacher_forcing) for this and later
+        steps; None = every step teacher-forced; auto_teacher_forcing() returns to drawing from
+        the ratio schedule, which is the default."""
+        if targets_lengths is not _UNSET:
+            if targets_lengths is None:
+                check(self.lib.tt2_train_set_target_lengths(self.h, None))
+            else:
+                tl = np.ascontiguousarray(np.asarray(targets_lengths, np.int32))
+                if tl.shape != (self.B,):
+                    raise ValueError("targets_lengths must be [batch]")
+                check(self.lib.tt2_train_set_target_lengths(self.h, tl.ctypes.data_as(ctypes.c_void_p)))
+        if feed_target is not _UNSET:
+            self._feed_explicit = True
+            self._set_feed(feed_target)
+
+    def auto_teacher_forcing(self):
+        """Draw the teacher forcing per step from the ratio schedule again (the default)."""
+        self._feed_explicit = False
+
+    def _set_feed(self, feed_target):
         if feed_target is None:
             check(self.lib.tt2_train_set_teacher_forcing(self.h, None, 0))
         else:
             ft = np.ascontiguousarray(np.asarray(feed_target, np.uint8))
             check(self.lib.tt2_train_set_teacher_forcing(self.h, ft.ctypes.data_as(ctypes.c_void_p),
                                                          int(ft.shape[0])))
+
+    def _teacher_forcing(self, T_out):
+        """TacoTrainingHelper (helpers.py:99-131): the ratio of this step -- the schedule at the
+        global step BEFORE this step's update, as TF reads the variable -- and one uniform draw
+        per decoder step from the trainer's seeded generator (TF's Philox stream cannot be
+        reproduced).  A ratio >= 1 feeds every target frame and draws nothing."""
+        if self._feed_explicit:
+            return
+        self.ratio = teacher_forcing_ratio(self.global_step, self.hp)
+        self._set_feed(None if self.ratio >= 1.0 else draw_teacher_forcing(T_out, self.ratio, self._tf_rng))
 
     def forward_backward(self, memory, lengths, targets, stop_targets, prenet_masks,
                          zoneout_masks=None, postnet_masks=None):
@@ -224,6 +254,7 @@ class TacotronTrainer(object):
                 raise ValueError("batch {} != trainer batch {}".format(B, self.B))
             if tuple(pm.shape) != (T_out, 2, B, self.cfg.prenet_units):
                 raise ValueError("prenet_masks must be [T_out, 2, B, prenet_units]")
+            self._teacher_forcing(T_out)
             if zm is not None and tuple(zm.shape) != (T_out, 4, B, self.cfg.decoder_lstm_units):
                 raise ValueError("zoneout_masks must be [T_out, 4, B, decoder_lstm_units]")
             if pnm is not None and tuple(pnm.shape) != (self.cfg.postnet_layers, B, T_out,
@@ -266,6 +297,7 @@ class TacotronTrainer(object):
                 raise ValueError("ref_emt and ref_spk must have the same shape")
             if tuple(pm.shape) != (T_out, 2, B, self.cfg.prenet_units):
                 raise ValueError("prenet_masks must be [T_out, 2, B, prenet_units]")
+            self._teacher_forcing(T_out)
             if em is not None and tuple(em.shape) != (self.cfg.enc_conv_layers, B, T_in,
                                                       self.cfg.enc_conv_channels):
                 raise ValueError("enc_conv_masks must be [layers, B, T_in, channels]")
@@ -354,11 +386,23 @@ class TacotronTrainer(object):
         returns the losses dict."""
         self.forward_backward(memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,
                               postnet_masks)
+        return self.optimizer_step()
+
+    def step_text(self, *args, **kwargs):
+        """The whole configs[4] step: forward_backward_text(*args, **kwargs), then
+        optimizer_step(); returns the losses dict."""
+        self.forward_backward_text(*args, **kwargs)
+        return self.optimizer_step()
+
+    def optimizer_step(self, global_step=None):
+        """After a forward_backward: DP all-reduce (when initialised), clipped Adam at
+        ``global_step`` (default: the next update), BN moving statistics composed over ranks;
+        returns the losses dict."""
         self.allreduce_grads()
         import torch.distributed as dist
         dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         before = self._stats() if dp else None
-        self.apply()
+        self.apply(global_step)
         if dp:
             self.sync_moving_stats(before)
         return self.losses()
@@ -382,11 +426,20 @@ class TacotronTrainer(object):
                                             out.ctypes.data_as(ctypes.c_void_p)))
         return out
 
+    def mel_outputs(self, T_out):
+        """mel_outputs of the last forward (tacotron.py:375-378): clip(decoder_output + Postnet
+        projection) [B, T_out, 80] (decoder_output alone without the Postnet)."""
+        fr, _, _ = self.outputs(None, T_out)
+        if not self.postnet:
+            return fr
+        x = fr + self.get("postnet:projection", 0, fr.shape)
+        return np.clip(x, self.cfg.clip_lo, self.cfg.clip_hi) if self.cfg.clip_outputs else x
+
     def outputs(self, T_in, T_out):
         fr = np.zeros((self.B, T_out, self.cfg.num_mels), np.float32)
         st = np.zeros((self.B, T_out), np.float32)
-        al = np.zeros((self.B, T_in, T_out), np.float32)
+        al = None if T_in is None else np.zeros((self.B, T_in, T_out), np.float32)
         check(self.lib.tt2_train_outputs(self.h, fr.ctypes.data_as(ctypes.c_void_p),
                                          st.ctypes.data_as(ctypes.c_void_p),
-                                         al.ctypes.data_as(ctypes.c_void_p)))
+                                         None if al is None else al.ctypes.data_as(ctypes.c_void_p)))
         return fr, st, al

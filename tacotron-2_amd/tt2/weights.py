@@ -380,8 +380,14 @@ def _init(rng, shape, kind, hp):
     if kind == "bn_var":
         return rng.uniform(0.8, 1.2, shape).astype(np.float32)
     if kind.startswith("embed:"):  # truncated_normal_initializer(0, std) (modules.py:13-20)
+        # TF redraws samples beyond 2 std (it does not clip them onto the bound)
         std = float(kind.split(":")[1])
-        return np.clip(rng.normal(0, std, shape), -2 * std, 2 * std).astype(np.float32)
+        v = rng.normal(0, std, shape)
+        bad = np.abs(v) > 2 * std
+        while bad.any():
+            v[bad] = rng.normal(0, std, int(bad.sum()))
+            bad = np.abs(v) > 2 * std
+        return v.astype(np.float32)
     if kind == "gst_tokens":  # truncated_normal(stddev=0.5), tacotron.py:221-224
         v = rng.normal(0, 0.5, shape)
         return np.clip(v, -1.0, 1.0).astype(np.float32)

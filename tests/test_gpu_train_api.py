@@ -1,0 +1,150 @@
+"""The training step behind the reference's own training API (tacotron/train.py:104-139,
+411-416): ``Tacotron.initialize(..., is_training=True)`` -> ``add_loss()`` ->
+``add_optimizer(global_step)`` drives tt2.train.TacotronTrainer, and the teacher-forcing ratio
+schedule is applied by the trainer itself (TacoTrainingHelper, helpers.py:99-131)."""
+import types
+
+import numpy as np
+import pytest
+
+from _common import small_hparams
+from tt2.synthetic import (enc_conv_masks, enc_zoneout_masks, postnet_masks, prenet_masks, tacotron_inputs,
+                           train_batch, zoneout_masks)
+from tt2.weights import init_tacotron_weights, memory_width
+
+ARGS = types.SimpleNamespace(adain=False, emt_only=False, unpaired=False, pretrained_emb_disc_all=False,
+                             synth_constraint=False, nat_gan=False)
+
+
+def _batch(hp, B=3, T_in=9, T_out=6, T_ref=70, seed=32):
+    ids, lens, re, rs = tacotron_inputs(B, T_in, T_ref, seed=seed)
+    _, _, tg, st = train_batch(B, T_in, T_out, memory_width(hp), seed=seed)
+    m = dict(prenet=prenet_masks(T_out, B, hp.prenet_layers[0], seed=seed),
+             zoneout=zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=seed),
+             postnet=postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=seed),
+             enc_conv=enc_conv_masks(hp.enc_conv_num_layers, B, T_in, hp.enc_conv_channels, seed=seed),
+             enc_zoneout=enc_zoneout_masks(T_in, B, hp.encoder_lstm_units, seed=seed))
+    return ids, lens, re, rs, tg, st, m
+
+
+def _hp():
+    hp = small_hparams()
+    hp.override_from_dict(dict(tacotron_use_style_emb_disc=False, tacotron_use_orthog_loss=False))
+    return hp
+
+
+def _model(hp, W):
+    from tacotron.models import create_model
+    model = create_model("Tacotron", hp)
+    model.load_weights(W)
+    return model
+
+
+def test_training_api_validation():
+    """Refusals that need no GPU: eval graphs, unbuilt style paths, towers in one process,
+    missing targets (tacotron.py:48-71 and the build's scope)."""
+    hp = _hp()
+    W = init_tacotron_weights(hp, seed=5339)
+    ids, lens, re, rs, tg, st, _ = _batch(hp)
+    model = _model(hp, W)
+    with pytest.raises(NotImplementedError, match="eval"):
+        model.initialize(ARGS, ids, lens, tg, st, is_evaluating=True, ref_mel_emt=re, ref_mel_spk=rs)
+    with pytest.raises(ValueError, match="without corresponding token_targets"):
+        model.initialize(ARGS, ids, lens, tg, None, is_training=True, ref_mel_emt=re, ref_mel_spk=rs)
+    with pytest.raises(NotImplementedError, match="GST"):
+        model.initialize(types.SimpleNamespace(**dict(vars(ARGS), pretrained_emb_disc_all=True)), ids, lens, tg, st,
+                         is_training=True, ref_mel_emt=re, ref_mel_spk=rs)
+    with pytest.raises(NotImplementedError, match="discriminators"):
+        model.initialize(ARGS, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs,
+                         use_emt_disc=True)
+    hp2 = hp.copy()
+    hp2.override_from_dict(dict(tacotron_num_gpus=3))
+    with pytest.raises(NotImplementedError, match="one process per GPU"):
+        _model(hp2, W).initialize(ARGS, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs)
+    with pytest.raises(RuntimeError, match="initialize"):
+        _model(hp, W).add_loss()
+
+
+@pytest.mark.gpu
+def test_reference_named_calls_match_trainer_step():
+    """Two steps through initialize(is_training=True) / add_loss() / add_optimizer(global_step)
+    equal TacotronTrainer.step_text on the same inputs and keep bits bit for bit: losses, the
+    updated parameters of every training variable, decoder outputs; mel_outputs =
+    clip(decoder_output + Postnet projection)."""
+    from oracle import train_ref as TRN
+    from tt2.train import TacotronTrainer
+    hp = _hp()
+    W = init_tacotron_weights(hp, seed=5339)
+    ids, lens, re, rs, tg, st, m = _batch(hp)
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    model = _model(hp, W)
+    got = []
+    for step in range(2):
+        model.initialize(ARGS, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs, train_masks=m)
+        loss = model.add_loss()
+        gs = model.add_optimizer(step)
+        assert gs == step + 1 and model.optimize == step + 1
+        got.append(dict(loss=loss, before=model.before_loss, after=model.after_loss, stop=model.stop_token_loss,
+                        reg=model.regularization_loss, dec=model.tower_decoder_output[0].copy(),
+                        mel=model.tower_mel_outputs[0].copy(), stop_logits=model.tower_stop_token_prediction[0].copy()))
+    names = TRN.frontend_var_names() + TRN.train_var_names() + TRN.postnet_var_names()
+    params = {n: model._trainer.get(n, 0, np.asarray(W[n]).shape) for n in names}
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1])
+    try:
+        for step in range(2):
+            L = tr.step_text(ids, lens, re, rs, tg, st, m["prenet"], m["zoneout"], m["postnet"], m["enc_conv"],
+                             m["enc_zoneout"])
+            fr, sl, _ = tr.outputs(T_in, T_out)
+            g = got[step]
+            assert g["loss"] == L["loss"] and g["before"] == L["before"] and g["after"] == L["after"]
+            assert g["stop"] == L["stop_token"] and g["reg"] == L["regularization"]
+            assert np.array_equal(g["dec"], fr) and np.array_equal(g["stop_logits"], sl)
+            proj = tr.get("postnet:projection", 0, fr.shape)
+            lo, hi = tr.cfg.clip_lo, tr.cfg.clip_hi
+            np.testing.assert_array_equal(g["mel"], np.clip(fr + proj, lo, hi))
+        for n in names:
+            assert np.array_equal(params[n], tr.get(n, 0, params[n].shape)), n
+        assert any(not np.array_equal(params[n], np.asarray(W[n], np.float32)) for n in names)
+    finally:
+        tr.close()
+    tw = model.trained_weights()
+    assert np.array_equal(tw[names[0]], params[names[0]])
+    model._trainer.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["constant", "scheduled"])
+def test_trainer_applies_teacher_forcing_schedule(mode):
+    """a ratio below 1 ('constant') or the 'scheduled' decay is applied by the trainer
+    itself -- the ratio at the global step before the update and one draw per decoder step from
+    the trainer's seeded generator -- and equals injecting the same draw explicitly."""
+    from tt2.train import TacotronTrainer, draw_teacher_forcing, teacher_forcing_ratio
+    hp = _hp()
+    if mode == "constant":
+        hp.override_from_dict(dict(tacotron_teacher_forcing_ratio=0.5))
+    else:
+        hp.override_from_dict(dict(tacotron_teacher_forcing_mode="scheduled", tacotron_teacher_forcing_init_ratio=1.0,
+                                   tacotron_teacher_forcing_start_decay=1, tacotron_teacher_forcing_decay_steps=1,
+                                   tacotron_teacher_forcing_decay_exp_rate=0.5))
+    W = init_tacotron_weights(hp, seed=5339)
+    ids, lens, re, rs, tg, st, m = _batch(hp, T_out=8)
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    args = (ids, lens, re, rs, tg, st, m["prenet"], m["zoneout"], m["postnet"], m["enc_conv"], m["enc_zoneout"])
+    auto = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1], tf_seed=7)
+    inj = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1])
+    rng = np.random.default_rng(7)
+    try:
+        fed_own = 0
+        for step in range(3):
+            La = auto.step_text(*args)
+            ratio = teacher_forcing_ratio(step, hp)
+            assert auto.ratio == ratio
+            feed = None if ratio >= 1.0 else draw_teacher_forcing(T_out, ratio, rng)
+            fed_own += 0 if feed is None else int((feed == 0).sum())
+            inj.set_step_inputs(feed_target=feed)
+            Li = inj.step_text(*args)
+            assert La["loss"] == Li["loss"] and La["grad_norm"] == Li["grad_norm"], step
+        assert fed_own > 0   # the draw did feed predicted frames somewhere
+    finally:
+        auto.close()
+        inj.close()

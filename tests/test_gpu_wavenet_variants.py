@@ -95,13 +95,14 @@ def test_gaussian_device_rng_is_standard_normal():
     assert len(np.unique(out["y"][0])) > T - 5                          # a fresh draw per sample
 
 
-@pytest.mark.parametrize("R,mode", [(64, "ids"), (64, "features"), (128, "ids")])
+@pytest.mark.parametrize("R,mode", [(64, "ids"), (64, "features"), (128, "ids"), (256, "features")])
 def test_global_conditioning(R, mode):
     """Global conditioning (wavenet.py:152-158, 770-775; modules.py:427-433, 505-509): speaker ids
     through the gc_embedding table, or the g features themselves; every layer's conv1x1g term joins
     both gate halves.  Teacher-forced logits within 1e-4 of the oracle at the narrow pipe (R = 64)
-    and the wide generator (R = 128), rows of different speakers differ, and the Synthesizer shim
-    passes speaker ids through."""
+    and the wide generator (R = 128 one-hop, R = 256 two-hop), rows of different speakers differ,
+    and the Synthesizer shim passes speaker ids through.  A batch other than the one the global
+    condition was set for is refused (stale rows would be used otherwise)."""
     from tt2.engine import WaveNetEngine
     from tt2.weights import init_wavenet_weights
     kw = dict(gin_channels=16, use_speaker_embedding=(mode == "ids"), n_speakers=5)
@@ -126,6 +127,16 @@ def test_global_conditioning(R, mode):
     c_up = WR.upsample_network(cond.transpose(0, 2, 1), W, ohp)
     _, _, lg = WR.incremental(c_up.transpose(0, 2, 1), W, ohp, um, ul, tg, return_logits=True, g=g)
     np.testing.assert_allclose(out["logits"], lg, atol=1e-4, rtol=1e-4)
+    from tt2._lib import TT2Error, ptr
+    eng1 = WaveNetEngine(hp, W, B, T, 0)
+    eng1.set_global_condition(g, B)                        # set for B rows, generate 1: refused
+    c1 = np.ascontiguousarray(cond[:1])
+    y1 = np.zeros((1, T), np.float32)
+    with pytest.raises(TT2Error, match="exactly these B rows"):
+        eng1._ok(eng1.lib.tt2_wn_generate(eng1.h, ptr(c1), 1, T_f, ptr(np.ascontiguousarray(um[:, :1])),
+                                          ptr(np.ascontiguousarray(ul[:, :1])), 0, None, ptr(y1), None, None,
+                                          None))
+    eng1.close()
     # identical conditioning and inputs, different global condition -> different logits
     assert np.abs(same["logits"][0] - same["logits"][1]).max() > 1e-3
     if mode == "ids":
