@@ -328,8 +328,14 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
     W = init_tacotron_weights(hp, seed=hp.tacotron_random_seed)
     front = not a.train_decoder_only
     Tr = a.train_t_ref
+    # the default training graph's style-embedding classifiers (tacotron.py:486-495, 812-820) over
+    # 4 emotion / 4 speaker classes with synthetic labels, and the orthogonality loss
+    n_cls = 4 if front else 0
     tr = TacotronTrainer(hp, W, B, Ti, T, local, precision=a.train_precision, frontend=front,
-                         max_T_ref=Tr)
+                         max_T_ref=Tr, n_emt=n_cls, n_spk=n_cls)
+    if n_cls:
+        lab = np.random.default_rng(99 + rank).integers(0, n_cls, (2, B))
+        tr.set_style_labels(lab[0], lab[1])
     if world > 1:
         tr.bind_grad_buffer()
     dev = torch.device("cuda", local)
@@ -381,7 +387,8 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
                 grad_norm=round(L["grad_norm"], 5), dtype=a.train_precision,
                 config=dict(workload=("configs[4]: whole Tacotron-2 training step from ids + reference mels "
                                       "(encoder, 2 reference encoders + GST, teacher-forced decoder, Postnet; "
-                                      "training BN / dropout / zoneout), B={} rows/GPU, T_in={}, T_out={}, "
+                                      "training BN / dropout / zoneout; style-embedding classifiers (4+4 "
+                                      "classes) + orthogonality loss), B={} rows/GPU, T_in={}, T_out={}, "
                                       "T_ref={}, D_mem={}".format(B, Ti, T, Tr, D)) if front else
                                      ("configs[4] slice: decoder + Postnet training step from a given memory, "
                                       "B={} rows/GPU, T_in={}, T_out={}, D_mem={}".format(B, Ti, T, D)),

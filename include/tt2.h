@@ -440,6 +440,14 @@ typedef struct tt2_train_config {
    * pos_weight (the unmasked stop loss ignores pos_weight, as the reference's does) */
   int mask_decoder;
   float pos_weight;
+  /* style-embedding losses of the default GST training graph (frontend = 1; tacotron.py:486-495,
+   * 812-820, 840-846; hparams tacotron_use_style_emb_disc / tacotron_use_orthog_loss):
+   * n_emt > 0 adds Style_Emb_Disc 'style_disc_emt' (dense 128 -> n_emt) on refnet_emt's output
+   * with softmax cross entropy against the emotion labels (tt2_train_set_style_labels), n_spk > 0
+   * the same for refnet_spk and the speaker labels (not emt_only); orthog_weight > 0 adds
+   * orthog_weight * ||refnet_emt · refnet_spkᵀ||_F (0.02 in the reference; not emt_only).  0 = off. */
+  int n_emt, n_spk;
+  float orthog_weight;
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;
@@ -504,6 +512,13 @@ tt2_status tt2_train_set_target_lengths(tt2_train_ctx* ctx, const int32_t* lengt
  * reference's per-step draw u < ratio (ratio: constant or _teacher_forcing_ratio_decay,
  * helpers.py:140-180), injected like the dropout keep bits.  NULL = every step teacher-forced. */
 tt2_status tt2_train_set_teacher_forcing(tt2_train_ctx* ctx, const uint8_t* feed_target, int T_out);
+/* Per-step emotion / speaker labels [B] of the style-embedding classifiers (feeder.emt_labels /
+ * spk_labels, tacotron/train.py:127-130); both NULL clears them.  Required before a step when
+ * n_emt / n_spk > 0.  An out-of-range label is tf.one_hot's zero row (loss 0). */
+tt2_status tt2_train_set_style_labels(tt2_train_ctx* ctx, const int32_t* emt_labels, const int32_t* spk_labels);
+/* Synchronise; out3 = {style_emb_loss_emt, style_emb_loss_spk, style_emb_orthog_loss} of the last
+ * text step (zeros when off); they are part of the step's loss and gradients. */
+tt2_status tt2_train_style_losses(tt2_train_ctx* ctx, float* out3);
 /* clip_by_global_norm + Adam with learning rate lr at update count global_step (>= 1). */
 tt2_status tt2_train_apply_dev(tt2_train_ctx* ctx, float lr, int global_step, void* stream);
 /* Synchronise; out5 = {before_loss, stop_loss, reg_loss, grad_global_norm (after apply),

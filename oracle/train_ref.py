@@ -343,13 +343,14 @@ def _gst(ref, W, tag, heads=4):
 
 
 def frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks=None, enc_zm=None, emt_only=False,
-                     eps=1e-3, moving=None):
+                     eps=1e-3, moving=None, refs_out=None):
     """Training-mode front end -> memory [B,T_in,D] (unmasked: the decoder masks it) and the batch
     statistics [(mean, var)] of every batch norm (encoder convs, then refnet convs).
     enc_masks [3, B, T_in, C] conv dropout keep bits (rate 0.5) or None; enc_zm [T_in, 2 (fw, bw),
     2 (c, h), B, U] LSTM zoneout keep bits or None.  ``moving`` (dict name -> array) evaluates the
     batch norms with the moving statistics: with no masks that is the inference graph, pinned to
-    oracle/tacotron_ref.py (tests/test_train.py)."""
+    oracle/tacotron_ref.py (tests/test_train.py).  ``refs_out`` (a list) receives the reference
+    encoders' outputs refnet_outputs_emt / _spk [B, 128] (tacotron.py:260-261)."""
     def mv(scope):
         if moving is None:
             return None
@@ -389,20 +390,62 @@ def frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks=None, enc_zm=N
         N, T2, F2, C = h.shape
         hl = _gru_last(h.reshape(N, T2, F2 * C), W, r)
         refo = torch.tanh(hl @ W[r + "dense/kernel"] + W[r + "dense/bias"])
+        if refs_out is not None:
+            refs_out.append(refo)
         style = _gst(refo, W, tag)
         parts.append(style[:, None, :].expand(B, T, style.shape[1]))
     return torch.cat(parts, -1), stats
 
 
+def style_disc_var_names(emt_only=False, n_emt=0, n_spk=0):
+    """Style_Emb_Disc dense layers (modules.py:626-644 under scopes style_disc_emt / _spk,
+    tacotron.py:489-493): built when n_emt (n_spk, unless emt_only) classes are given."""
+    names = []
+    for tag, n in (("emt", n_emt),) + ((() if emt_only else (("spk", n_spk),))):
+        if n:
+            names += [P + "style_disc_{}/dense/kernel".format(tag), P + "style_disc_{}/dense/bias".format(tag)]
+    return names
+
+
+def style_emb_losses(W, refs, emt_labels, spk_labels, n_emt=0, n_spk=0, orthog_weight=0.0):
+    """The style-embedding losses of the default (GST, not adain / pretrained_emb_disc_all)
+    training graph (tacotron.py:812-820, 840-846): per reference encoder a dense classifier of
+    its output and tf.nn.softmax_cross_entropy_with_logits against tf.one_hot(labels) (an
+    out-of-range label is a zero row: loss 0, gradient 0), averaged over the batch; the
+    orthogonality loss orthog_weight * ||refnet_emt · refnet_spkᵀ||_F (Frobenius; 0.02 in the
+    reference, off for emt_only).  Returns (loss_emt, loss_spk, loss_orthog) tensors."""
+    out = []
+    for i, (tag, lab, n) in enumerate((("emt", emt_labels, n_emt), ("spk", spk_labels, n_spk))):
+        if not n or i >= len(refs):
+            out.append(torch.zeros((), dtype=refs[0].dtype))
+            continue
+        logit = refs[i] @ W[P + "style_disc_{}/dense/kernel".format(tag)] + W[P + "style_disc_{}/dense/bias".format(tag)]
+        lab = np.asarray(lab).astype(np.int64)
+        y = torch.zeros_like(logit)
+        ok = (lab >= 0) & (lab < n)
+        y[np.nonzero(ok)[0], lab[ok]] = 1.0
+        out.append((-(y * torch.log_softmax(logit, -1)).sum(-1)).mean())
+    if orthog_weight and len(refs) > 1:
+        out.append(orthog_weight * torch.linalg.norm(refs[0] @ refs[1].T))
+    else:
+        out.append(torch.zeros((), dtype=refs[0].dtype))
+    return tuple(out)
+
+
 def train_grads_frontend(Wnp, ids, lengths, ref_emt, ref_spk, targets, stop_targets, prenet_masks,
                          zoneout_masks, enc_masks, enc_zm, reg_weight=1e-6, dtype=torch.float64,
-                         clip=(-4.1, 4.0), postnet_masks=None, emt_only=False):
+                         clip=(-4.1, 4.0), postnet_masks=None, emt_only=False, style=None):
     """The whole configs[4] step: front end (training mode) -> memory -> decoder + Postnet; returns
     (losses, grads of every front-end, decoder and Postnet variable, [(mean, var)] batch stats of
-    the front end's batch norms)."""
-    names = frontend_var_names(emt_only) + train_var_names() + postnet_var_names()
+    the front end's batch norms).  ``style`` = dict(emt_labels, spk_labels, n_emt, n_spk,
+    orthog_weight) adds the style-embedding losses (style_emb_losses); the losses tuple then
+    gains (loss_emt, loss_spk, loss_orthog)."""
+    st_kw = dict(style or {})
+    names = (frontend_var_names(emt_only) + style_disc_var_names(emt_only, st_kw.get("n_emt", 0), st_kw.get("n_spk", 0))
+             + train_var_names() + postnet_var_names())
     W = {n: torch.tensor(np.asarray(Wnp[n]), dtype=dtype, requires_grad=True) for n in names}
-    mem, stats = frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks, enc_zm, emt_only)
+    refs = []
+    mem, stats = frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks, enc_zm, emt_only, refs_out=refs)
     tg = torch.tensor(np.asarray(targets), dtype=dtype)
     st = torch.tensor(np.asarray(stop_targets), dtype=dtype)
     pm = torch.tensor(np.asarray(prenet_masks), dtype=dtype)
@@ -414,9 +457,16 @@ def train_grads_frontend(Wnp, ids, lengths, ref_emt, ref_spk, targets, stop_targ
     proj, _ = postnet_train(W, dec, pmk)
     mel = clip_decoder_output(dec + proj, clip)
     after = ((mel - tg) ** 2).mean()
-    (b + s + r + after).backward()
+    total = b + s + r + after
+    extra = ()
+    if style is not None:
+        extra = style_emb_losses(W, refs, st_kw.get("emt_labels"), st_kw.get("spk_labels"), st_kw.get("n_emt", 0),
+                                 0 if emt_only else st_kw.get("n_spk", 0),
+                                 0.0 if emt_only else st_kw.get("orthog_weight", 0.0))
+        total = total + sum(extra)
+    total.backward()
     g = {n: W[n].grad.numpy() for n in names}
-    return (b.item(), s.item(), r.item(), after.item()), g, \
+    return (b.item(), s.item(), r.item(), after.item()) + tuple(x.item() for x in extra), g, \
         [(m.detach().numpy(), v.detach().numpy()) for m, v in stats]
 
 

@@ -22,7 +22,7 @@ B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
 tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1])
 tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
 L, g, stats = TRN.train_grads_frontend(W, ids, lens, re, rs, tg, st, pm, zm, em, ezm, hp.tacotron_reg_weight,
-                                        postnet_masks=pnm)
+                                        postnet_masks=pnm, style=dict(orthog_weight=0.02))
 bad = []
 for n in TRN.frontend_var_names() + TRN.train_var_names() + TRN.postnet_var_names():
     got = tr.get(n, 1, np.asarray(W[n]).shape)

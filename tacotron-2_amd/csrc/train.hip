@@ -93,6 +93,10 @@ struct tt2_train_ctx {
   // loss masks (cfg.mask_decoder): target lengths [B] on the device, their sum
   DevBuf TLEN;
   bool has_tlen = false;
+  // style-embedding losses (cfg.n_emt / n_spk / orthog_weight): labels [2][B], the extra d refnet
+  // outputs [2][B][128], classifier logit gradients [B][max(n)], the orthogonality product [B][B]
+  DevBuf sLAB, sXREF, sDL, sOM;
+  bool has_labels = false;
   long tlen_sum = 0;
   int tlen_max = 0;
   // teacher-forcing draw (tt2_train_set_teacher_forcing): feed[t] = 1 target frame t-1, 0 own frame
@@ -2110,6 +2114,14 @@ static void tr_front_build_vars(tt2_train_ctx* c, const std::function<void(const
     addr(m + "attention_g", {});
     addr(m + "attention_b", {dh});
   }
+  // Style_Emb_Disc dense layers (modules.py:626-644, tacotron.py:489-493; oracle style_disc_var_names)
+  for (int r = 0; r < c->f_nref; ++r) {
+    const int n = r == 0 ? f.n_emt : f.n_spk;
+    if (n <= 0) continue;
+    const std::string sd = vn(r == 0 ? "style_disc_emt/dense/" : "style_disc_spk/dense/");
+    addr(sd + "kernel", {128, n});
+    addr(sd + "bias", {n});
+  }
 }
 
 static void tr_front_alloc(tt2_train_ctx* c) {
@@ -2161,6 +2173,8 @@ static void tr_front_alloc(tt2_train_ctx* c) {
   const int ntok = f.num_gst, tokd = f.style_embed_depth / f.num_heads, A = f.style_att_dim, dh = A / f.num_heads;
   a(c->fGq, B * A); a(c->fGkk, B * ntok * A); a(c->fGv, B * ntok * tokd); a(c->fGnv, B * dh); a(c->fGbb, B * dh);
   a(c->fGsum, ntok * A + ntok * tokd + 2 * dh);
+  a(c->sXREF, 2 * B * 128); a(c->sDL, B * std::max(1, std::max(f.n_emt, f.n_spk))); a(c->sOM, B * B);
+  c->sLAB.alloc(sizeof(int) * (size_t)(2 * B));
   a(c->fdREF, B * 128); a(c->fDZD, B * 128); a(c->fDH, B * RD); a(c->fDHA, B * RD); a(c->fDRH, B * RD);
   a(c->fDCP, T2 * B * RD); a(c->fDGP, T2 * B * 2 * RD); a(c->fDXG, B * T2 * 3 * RD);
   // transposed / flipped weight scratch: refnet conv2d kernels, GRU gates + candidate, dense, GST
@@ -2314,6 +2328,139 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
   c->f_ran = true;
 }
 
+// ---- style-embedding losses (tacotron.py:486-495, 812-820, 840-846; oracle style_emb_losses) ----------
+// Style_Emb_Disc: logits = ref·W + b [B, n]; softmax_cross_entropy_with_logits against tf.one_hot(label)
+// (out-of-range label: zero row -> loss 0, gradient 0), batch mean.  One work-group per row: the
+// row's loss -> part[b], d logits = (softmax·Σy - y) / B -> DL, d ref += DL·Wᵀ -> XR.
+__global__ __launch_bounds__(128) void k_fe_disc(const float* __restrict__ ref, const float* __restrict__ Wk,
+                                                 const float* __restrict__ bk, const int* __restrict__ lab, int B,
+                                                 int n, float* __restrict__ DL, float* __restrict__ XR,
+                                                 float* __restrict__ part) {
+  extern __shared__ float sd[];  // [128] ref row, [n] logits
+  const int b = blockIdx.x, k = threadIdx.x;
+  float* lg = sd + 128;
+  sd[k] = ref[(long)b * 128 + k];
+  __syncthreads();
+  for (int j = k; j < n; j += 128) {
+    float v = bk[j];
+    for (int i = 0; i < 128; ++i) v = fmaf(sd[i], Wk[(long)i * n + j], v);
+    lg[j] = v;
+  }
+  __syncthreads();
+  const int y = lab[b];
+  const bool hot = y >= 0 && y < n;
+  if (k == 0) {  // serial over n (small): max, log-sum-exp, loss
+    float mx = -INFINITY;
+    for (int j = 0; j < n; ++j) mx = fmaxf(mx, lg[j]);
+    double se = 0;
+    for (int j = 0; j < n; ++j) se += exp((double)(lg[j] - mx));
+    const float lse = mx + (float)log(se);
+    part[b] = hot ? lse - lg[y] : 0.f;
+    sd[128 + n] = lse;
+  }
+  __syncthreads();
+  const float lse = sd[128 + n];
+  for (int j = k; j < n; j += 128) {
+    const float d = hot ? (expf(lg[j] - lse) - (j == y ? 1.f : 0.f)) / (float)B : 0.f;
+    DL[(long)b * n + j] = d;
+    lg[j] = d;
+  }
+  __syncthreads();
+  float g = 0.f;
+  for (int j = 0; j < n; ++j) g = fmaf(lg[j], Wk[(long)k * n + j], g);
+  XR[(long)b * 128 + k] += g;
+}
+// d W[k][j] = Σ_b ref[b][k] DL[b][j], d b[j] = Σ_b DL[b][j] (written, not accumulated)
+__global__ void k_fe_disc_wgrad(const float* __restrict__ ref, const float* __restrict__ DL, int B, int n,
+                                float* __restrict__ dW, float* __restrict__ db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 128 * n) {
+    const int k = i / n, j = i % n;
+    float v = 0.f;
+    for (int b = 0; b < B; ++b) v = fmaf(ref[(long)b * 128 + k], DL[(long)b * n + j], v);
+    dW[i] = v;
+  } else if (i < 129 * n) {
+    const int j = i - 128 * n;
+    float v = 0.f;
+    for (int b = 0; b < B; ++b) v += DL[(long)b * n + j];
+    db[j] = v;
+  }
+}
+// orthogonality loss w·||E·Sᵀ||_F: M = E·Sᵀ [B][B] (row b per work-group), Σ M² partials
+__global__ __launch_bounds__(128) void k_fe_orthog_m(const float* __restrict__ E, const float* __restrict__ S, int B,
+                                                     float* __restrict__ M, float* __restrict__ part) {
+  __shared__ float e[128];
+  __shared__ float s4[4];
+  const int b = blockIdx.x, t = threadIdx.x;
+  e[t] = E[(long)b * 128 + t];
+  __syncthreads();
+  float sq = 0.f;
+  for (int jj = t; jj < B; jj += 128) {
+    float v = 0.f;
+    for (int i = 0; i < 128; ++i) v = fmaf(e[i], S[(long)jj * 128 + i], v);
+    M[(long)b * B + jj] = v;
+    sq += v * v;
+  }
+  for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+  if ((t & 63) == 0) s4[t >> 6] = sq;
+  __syncthreads();
+  if (t == 0) part[b] = s4[0] + s4[1];
+}
+// loss = w·||M|| -> red[0]; d E = (w/||M||)·M·S -> XE, d S = (w/||M||)·Mᵀ·E -> XS (accumulated);
+// blocks [0, B) rows of d E, [B, 2B) rows of d S.  ||M|| = 0: TF's norm gradient is NaN there; 0 here.
+__global__ __launch_bounds__(128) void k_fe_orthog_g(const float* __restrict__ E, const float* __restrict__ S,
+                                                     const float* __restrict__ M, int B, float w,
+                                                     const float* __restrict__ n2, float* __restrict__ red,
+                                                     float* __restrict__ XE, float* __restrict__ XS) {
+  const int r = blockIdx.x, k = threadIdx.x;
+  const float nrm = sqrtf(n2[0]);
+  if (r == 0 && k == 0) red[0] = w * nrm;
+  const float coef = nrm > 0.f ? w / nrm : 0.f;
+  float g = 0.f;
+  if (r < B) {
+    for (int j = 0; j < B; ++j) g = fmaf(M[(long)r * B + j], S[(long)j * 128 + k], g);
+    XE[(long)r * 128 + k] += coef * g;
+  } else {
+    const int j = r - B;
+    for (int b = 0; b < B; ++b) g = fmaf(M[(long)b * B + j], E[(long)b * 128 + k], g);
+    XS[(long)j * 128 + k] += coef * g;
+  }
+}
+
+// The style-embedding losses' gradients into the refnet outputs (sXREF[r]) and the classifier
+// weights; losses -> red[5] (emt), red[6] (spk), red[7] (orthogonality).  Before the refnet backward.
+static void tr_style_losses(tt2_train_ctx* c, hipStream_t s) {
+  const auto& f = c->cfg;
+  const int B = c->B;
+  float* red = c->red.as<float>();
+  float* XR = c->sXREF.as<float>();
+  TT2_HIP(hipMemsetAsync(XR, 0, sizeof(float) * (size_t)2 * B * 128, s));
+  TT2_HIP(hipMemsetAsync(red + 5, 0, sizeof(float) * 3, s));
+  for (int r = 0; r < c->f_nref; ++r) {
+    const int n = r == 0 ? f.n_emt : f.n_spk;
+    if (n <= 0) continue;
+    const std::string sd = vn(r == 0 ? "style_disc_emt/dense/" : "style_disc_spk/dense/");
+    hipLaunchKernelGGL(k_fe_disc, dim3(B), dim3(128), sizeof(float) * (129 + n), s, c->fREF[r].as<float>(),
+                       pvar(c, sd + "kernel"), pvar(c, sd + "bias"), c->sLAB.as<int>() + r * B, B, n, c->sDL.as<float>(),
+                       XR + (long)r * B * 128, c->part.as<float>());
+    hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), B, 1.0f / B, red + 5 + r, 0);
+    hipLaunchKernelGGL(k_fe_disc_wgrad, dim3((129 * n + 255) / 256), dim3(256), 0, s, c->fREF[r].as<float>(),
+                       c->sDL.as<float>(), B, n, gvar(c, sd + "kernel"), gvar(c, sd + "bias"));
+  }
+  if (f.orthog_weight > 0.f && c->f_nref == 2) {
+    hipLaunchKernelGGL(k_fe_orthog_m, dim3(B), dim3(128), 0, s, c->fREF[0].as<float>(), c->fREF[1].as<float>(), B,
+                       c->sOM.as<float>(), c->part.as<float>());
+    hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), B, 1.0f, red + 8, 0);
+    hipLaunchKernelGGL(k_fe_orthog_g, dim3(2 * B), dim3(128), 0, s, c->fREF[0].as<float>(), c->fREF[1].as<float>(),
+                       c->sOM.as<float>(), B, f.orthog_weight, red + 8, red + 7, XR, XR + (long)B * 128);
+  }
+  TT2_HIP(hipGetLastError());
+}
+
+static bool tr_style_on(const tt2_train_ctx* c) {
+  return c->cfg.n_emt > 0 || (c->f_nref == 2 && (c->cfg.n_spk > 0 || c->cfg.orthog_weight > 0.f));
+}
+
 static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens, const float* const* refs, int T_ref,
                               const uint8_t* encm, const uint8_t* enczm, int T, hipStream_t s) {
   const auto& f = c->cfg;
@@ -2325,6 +2472,8 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
   float* FB = c->fFBUF.as<float>();
   // memory assembly: style gradient = Σ_t over the (length-masked) d memory rows
   fe_style_grad(c->DMEM.as<float>(), B, T, D, 2 * U, c->fDSTY.as<float>(), s);
+  const bool style_on = tr_style_on(c);
+  if (style_on) tr_style_losses(c, s);
   for (int r = 0; r < c->f_nref; ++r) {
     const std::string rs = fe_ref_scope(r), m = fe_mh_scope(r);
     const FeGst ga = fe_gst_args(c, r, B);
@@ -2344,7 +2493,8 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
     tr_gemm(128, A, B, WT, B, ga.dq, A, gvar(c, m + "conv1d/kernel"), A, s);
     tr_colsum(c, ga.dq, B, A, A, gvar(c, m + "conv1d/bias"), s);
     tr_transpose(pvar(c, m + "conv1d/kernel"), 128, A, A, WT, 128, s);
-    tr_gemm(B, 128, A, ga.dq, A, WT, 128, c->fdREF.as<float>(), 128, s);
+    tr_gemm(B, 128, A, ga.dq, A, WT, 128, c->fdREF.as<float>(), 128, s, nullptr,
+            style_on ? c->sXREF.as<float>() + (long)r * B * 128 : nullptr, 128);  // + style-loss terms
     // dense tanh (modules.py:63)
     fe_tanh_bwd(c->fdREF.as<float>(), c->fREF[r].as<float>(), (long)B * 128, c->fDZD.as<float>(), s);
     const int T2 = c->f_T2;
@@ -2580,6 +2730,9 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   c->enc_conv_channels = 512;
   c->encoder_lstm_units = 256;
   c->emt_only = 0;
+  c->n_emt = 0;
+  c->n_spk = 0;
+  c->orthog_weight = 0.f;
   c->num_gst = 10;
   c->num_heads = 4;
   c->style_embed_depth = 256;
@@ -2615,6 +2768,40 @@ tt2_status tt2_train_set_target_lengths(tt2_train_ctx* c, const int32_t* lengths
     c->has_tlen = true;
     c->tlen_sum = sum;
     c->tlen_max = mx;
+  });
+}
+
+tt2_status tt2_train_set_style_labels(tt2_train_ctx* c, const int32_t* emt_labels, const int32_t* spk_labels) {
+  return guard([&] {
+    TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
+    if (!emt_labels && !spk_labels) {
+      c->has_labels = false;
+      return;
+    }
+    TT2_CHECK(emt_labels && (spk_labels || c->f_nref == 1), TT2_ERR_INVALID_ARG,
+              "emotion labels (and speaker labels unless emt_only) required");
+    std::vector<int> lab((size_t)2 * c->B, -1);
+    for (int b = 0; b < c->B; ++b) {
+      lab[b] = emt_labels[b];
+      if (spk_labels) lab[c->B + b] = spk_labels[b];
+    }
+    TT2_HIP(hipSetDevice(c->dev));
+    if (c->last_stream) TT2_HIP(hipStreamSynchronize(c->last_stream));  // a running step reads them
+    TT2_HIP(hipMemcpy(c->sLAB.p, lab.data(), sizeof(int) * lab.size(), hipMemcpyHostToDevice));
+    c->has_labels = true;
+  });
+}
+
+tt2_status tt2_train_style_losses(tt2_train_ctx* c, float* out3) {
+  return guard([&] {
+    TT2_CHECK(c && out3, TT2_ERR_INVALID_ARG, "null argument");
+    TT2_HIP(hipSetDevice(c->dev));
+    if (!c->cfg.frontend || !tr_style_on(c) || !c->last_stream) {
+      out3[0] = out3[1] = out3[2] = 0.f;
+      return;
+    }
+    TT2_HIP(hipMemcpyAsync(out3, c->red.as<float>() + 5, sizeof(float) * 3, hipMemcpyDeviceToHost, c->last_stream));
+    TT2_HIP(hipStreamSynchronize(c->last_stream));
   });
 }
 
@@ -2664,6 +2851,8 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
                 "bad postnet shape");
       if (cfg->frontend) {
         c->f_nref = cfg->emt_only ? 1 : 2;
+        TT2_CHECK(cfg->n_emt >= 0 && cfg->n_spk >= 0 && cfg->orthog_weight >= 0.f, TT2_ERR_INVALID_ARG,
+                  "n_emt / n_spk / orthog_weight must be >= 0");
         int W = cfg->num_mels;
         for (int i = 0; i < 6; ++i) W = (W + 1) / 2;
         c->f_gin = W * cfg->reference_filters[5];
@@ -2812,6 +3001,8 @@ tt2_status tt2_train_forward_backward_text_dev(tt2_train_ctx* c, const int32_t* 
     TT2_CHECK(T_in >= 1 && T_in <= c->Tin && T_out >= 1 && T_out <= c->Tm, TT2_ERR_SHAPE_MISMATCH,
               "T_in/T_out exceed capacity");
     TT2_CHECK(T_ref >= 1 && T_ref <= c->cfg.max_T_ref, TT2_ERR_SHAPE_MISMATCH, "T_ref exceeds capacity");
+    TT2_CHECK(!(c->cfg.n_emt > 0 || (c->f_nref == 2 && c->cfg.n_spk > 0)) || c->has_labels, TT2_ERR_STATE,
+              "style-embedding classifiers (n_emt / n_spk > 0) need tt2_train_set_style_labels first");
     TT2_HIP(hipSetDevice(c->dev));
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     c->last_stream = s;

@@ -204,7 +204,7 @@ class Tacotron():
             return self._initialize_training(
                 inputs, input_lengths, mel_targets, stop_token_targets, targets_lengths, split_infos,
                 ref_mel_emt, ref_mel_spk, emt_only, style, use_emt_disc or use_spk_disc or use_intercross,
-                train_masks, train_capacity, precision, seed)
+                train_masks, train_capacity, precision, seed, n_emt, n_spk, emt_labels, spk_labels)
 
         tower_inputs, tower_lengths, tower_ref_emt, tower_ref_spk, tower_targets = split_towers(
             hp, inputs, input_lengths, split_infos, ref_mel_emt, ref_mel_spk, mel_targets)
@@ -260,27 +260,27 @@ class Tacotron():
 
     def _initialize_training(self, inputs, input_lengths, mel_targets, stop_token_targets, targets_lengths,
                              split_infos, ref_mel_emt, ref_mel_spk, emt_only, style, disc, train_masks,
-                             train_capacity, precision, seed):
+                             train_capacity, precision, seed, n_emt=None, n_spk=None, emt_labels=None,
+                             spk_labels=None):
         from tt2 import synthetic as S
         from tt2.train import TacotronTrainer
         hp = self._hparams
-        if self._weights is None:
-            raise RuntimeError("Tacotron weights not loaded: call load_weights() (checkpoint) or "
-                               "init_random_weights()")
         if mel_targets is None or stop_token_targets is None:
             raise ValueError("training needs mel_targets and stop_token_targets")
         if style != "gst" or not hp.use_gst:
             raise NotImplementedError("training builds the GST style path (adain / embeddings-only "
                                       "front ends are synthesis-only on this build)")
-        if disc:
-            raise NotImplementedError("the style-embedding discriminators (use_emt_disc / use_spk_disc / "
-                                      "intercross) are not built")
+        # use_emt_disc / use_spk_disc / use_intercross are stored and never read by the reference
+        # graph (tacotron.py:74-76): accepted and ignored alike
         if hp.outputs_per_step != 1:
             raise NotImplementedError("outputs_per_step = 1 on this build")
-        if hp.tacotron_use_style_emb_disc or hp.tacotron_use_orthog_loss:
-            raise NotImplementedError("the style-embedding classifier / orthogonality losses "
-                                      "(tacotron.py:486-495, 812-846) are not built yet: set "
-                                      "tacotron_use_style_emb_disc=False, tacotron_use_orthog_loss=False")
+        n_emt, n_spk = (int(n_emt or 0), int(n_spk or 0)) if hp.tacotron_use_style_emb_disc else (0, 0)
+        if n_emt and emt_labels is None or (n_spk and not emt_only and spk_labels is None):
+            raise ValueError("the style-embedding classifiers (tacotron_use_style_emb_disc) need emt_labels "
+                             "and spk_labels")
+        if self._weights is None:
+            raise RuntimeError("Tacotron weights not loaded: call load_weights() (checkpoint) or "
+                               "init_random_weights()")
         tower_inputs, tower_lengths, tower_ref_emt, tower_ref_spk, tower_targets = split_towers(
             hp, inputs, input_lengths, split_infos, ref_mel_emt, ref_mel_spk, mel_targets)
         ntow = len(tower_inputs)
@@ -305,7 +305,8 @@ class Tacotron():
             tlen = np.split(np.asarray(targets_lengths, np.int32).reshape(-1), ntow)[i]
         cap = dict(max_T_in=T_in, max_T_out=T_out, max_T_ref=T_ref)
         cap.update(train_capacity or {})
-        key = (B, emt_only, precision)
+        n_emt, n_spk = (int(n_emt or 0), int(n_spk or 0)) if hp.tacotron_use_style_emb_disc else (0, 0)
+        key = (B, emt_only, precision, n_emt, n_spk)
         tr = self._trainer
         if tr is not None and (self._train_key != key or T_in > self._train_cap["max_T_in"]
                                or T_out > self._train_cap["max_T_out"] or T_ref > self._train_cap["max_T_ref"]):
@@ -315,10 +316,14 @@ class Tacotron():
         if tr is None:
             tr = TacotronTrainer(hp, self._weights, B, cap["max_T_in"], cap["max_T_out"], self.device,
                                  emt_only=emt_only, precision=precision, postnet=True, frontend=True,
-                                 max_T_ref=cap["max_T_ref"], tf_seed=seed)
+                                 max_T_ref=cap["max_T_ref"], tf_seed=seed, n_emt=n_emt, n_spk=n_spk)
             self._trainer, self._train_key, self._train_cap = tr, key, cap
             self._mask_rng = np.random.default_rng(seed)
         tr.set_step_inputs(targets_lengths=tlen)
+        if n_emt or n_spk:  # Style_Emb_Disc targets (tf.one_hot of the labels, tacotron.py:813-814)
+            el = np.split(np.asarray(emt_labels, np.int32).reshape(-1), ntow)[i]
+            sl = None if emt_only else np.split(np.asarray(spk_labels, np.int32).reshape(-1), ntow)[i]
+            tr.set_style_labels(el, sl)
         m = dict(train_masks or {})
         r = self._mask_rng
         sub = lambda: int(r.integers(1 << 31))  # noqa: E731  (one fresh stream per mask per step)
@@ -350,8 +355,9 @@ class Tacotron():
 
     def add_loss(self):
         """tacotron.py:683-1000 for this process's tower: before / after / stop-token /
-        regularization losses of the step initialize(is_training=True) just ran (the
-        discriminator / unpaired losses are 0: those graphs are not built)."""
+        regularization losses, the style-embedding classifier and orthogonality losses of the step
+        initialize(is_training=True) just ran (the unpaired / GAN losses are 0: those graphs are
+        not built)."""
         tr = self._trainer
         if tr is None:
             raise RuntimeError("add_loss: call initialize(..., is_training=True) first")
@@ -360,11 +366,13 @@ class Tacotron():
         self.before_loss, self.after_loss = L["before"], L["after"]
         self.stop_token_loss, self.regularization_loss = L["stop_token"], L["regularization"]
         self.linear_loss = 0.0
-        for n in ("style_emb_loss_emt", "style_emb_loss_spk", "style_emb_orthog_loss", "style_emb_loss_up_emt",
-                  "style_emb_loss_up_spk", "style_emb_loss_mel_out_up_emt", "style_emb_loss_mel_out_up_spk",
-                  "g_loss_p", "g_loss_up"):
+        for n in ("style_emb_loss_up_emt", "style_emb_loss_up_spk", "style_emb_loss_mel_out_up_emt",
+                  "style_emb_loss_mel_out_up_spk", "g_loss_p", "g_loss_up"):
             setattr(self, n, 0.0)
             setattr(self, "tower_" + n, [0.0])
+        for n in ("style_emb_loss_emt", "style_emb_loss_spk", "style_emb_orthog_loss"):
+            setattr(self, n, L[n])
+            setattr(self, "tower_" + n, [L[n]])
         self.loss = L["loss"]
         self.loss_no_mo_up = L["loss"]
         self.tower_before_loss, self.tower_after_loss = [self.before_loss], [self.after_loss]

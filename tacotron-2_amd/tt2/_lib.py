@@ -87,7 +87,8 @@ class TrainConfig(ctypes.Structure):
             "enc_conv_channels", "encoder_lstm_units", "emt_only", "num_gst", "num_heads",
             "style_embed_depth", "style_att_dim", "reference_depth")] + [
         ("reference_filters", ctypes.c_int * 6), ("max_T_ref", ctypes.c_int),
-        ("mask_decoder", ctypes.c_int), ("pos_weight", ctypes.c_float)]
+        ("mask_decoder", ctypes.c_int), ("pos_weight", ctypes.c_float),
+        ("n_emt", ctypes.c_int), ("n_spk", ctypes.c_int), ("orthog_weight", ctypes.c_float)]
 
 
 class DecoderState(ctypes.Structure):
@@ -162,6 +163,8 @@ SIGNATURES = {
     "tt2_exit_guard": (None, [_I, _I]),
     "tt2_wn_set_global_condition": (_I, [_P, _P, _P, _I]),
     "tt2_train_set_teacher_forcing": (_I, [_P, _P, _I]),
+    "tt2_train_set_style_labels": (_I, [_P, _P, _P]),
+    "tt2_train_style_losses": (_I, [_P, _P]),
     "tt2_train_losses": (_I, [_P, _P, _P]),
     "tt2_train_get_tensor": (_I, [_P, ctypes.c_char_p, _I, _P]),
     "tt2_train_outputs": (_I, [_P, _P, _P, _P]),

@@ -58,7 +58,7 @@ _UNSET = object()
 
 
 def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32", postnet=True,
-                 frontend=False, max_T_ref=None):
+                 frontend=False, max_T_ref=None, n_emt=0, n_spk=0):
     lib = _lib.load_library()
     cfg = _lib.TrainConfig()
     lib.tt2_train_default_config(ctypes.byref(cfg), batch, max_T_in, max_T_out)
@@ -123,7 +123,29 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
         for i, f in enumerate(hp.reference_filters):
             cfg.reference_filters[i] = f
         cfg.max_T_ref = max_T_ref or max_T_out
+        # style-embedding losses of the default training graph (tacotron.py:486-495, 812-846): the
+        # classifiers need the class counts (feeder.total_emt / total_spk); the orthogonality loss
+        # needs both reference encoders
+        if hp.tacotron_use_style_emb_disc:
+            cfg.n_emt = int(n_emt)
+            cfg.n_spk = 0 if emt_only else int(n_spk)
+        if hp.tacotron_use_orthog_loss and not emt_only:
+            cfg.orthog_weight = 0.02
     return cfg
+
+
+def init_style_disc_weights(hp, n_emt, n_spk, emt_only=False, seed=None):
+    """Fresh Style_Emb_Disc variables (tf.layers.dense: glorot-uniform kernel, zero bias) for
+    the classes of this dataset, as TF initialises them at the start of training."""
+    rng = np.random.default_rng(hp.tacotron_random_seed if seed is None else seed)
+    W = {}
+    for tag, n in (("emt", n_emt),) + ((() if emt_only else (("spk", n_spk),))):
+        if n:
+            lim = np.sqrt(6.0 / (128 + n))
+            W["Tacotron_model/inference/style_disc_{}/dense/kernel".format(tag)] = \
+                rng.uniform(-lim, lim, (128, n)).astype(np.float32)
+            W["Tacotron_model/inference/style_disc_{}/dense/bias".format(tag)] = np.zeros(n, np.float32)
+    return W
 
 
 class TacotronTrainer(object):
@@ -131,14 +153,23 @@ class TacotronTrainer(object):
     runs on the trainer's own torch stream (passed to the library explicitly)."""
 
     def __init__(self, hp, weights, batch, max_T_in, max_T_out, device=0, emt_only=False,
-                 precision="fp32", postnet=True, frontend=False, max_T_ref=None, tf_seed=None):
+                 precision="fp32", postnet=True, frontend=False, max_T_ref=None, tf_seed=None,
+                 n_emt=0, n_spk=0):
+        """n_emt / n_spk: classes of the style-embedding classifiers (frontend, when
+        hp.tacotron_use_style_emb_disc); their variables are taken from ``weights`` or freshly
+        initialised (init_style_disc_weights), and set_style_labels() feeds the labels."""
         import torch
         self.torch = torch
         self.lib = _lib.load_library()
         self.hp = hp
         self.device = torch.device("cuda", device)
         self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only, precision, postnet, frontend,
-                                max_T_ref)
+                                max_T_ref, n_emt if frontend else 0, n_spk if frontend else 0)
+        if self.cfg.n_emt or self.cfg.n_spk:
+            fresh = init_style_disc_weights(hp, self.cfg.n_emt, self.cfg.n_spk, emt_only)
+            weights = dict(weights)
+            for k, v in fresh.items():
+                weights.setdefault(k, v)
         self.frontend = frontend
         self.postnet = postnet
         self.B = batch
@@ -211,6 +242,19 @@ class TacotronTrainer(object):
         if feed_target is not _UNSET:
             self._feed_explicit = True
             self._set_feed(feed_target)
+
+    def set_style_labels(self, emt_labels, spk_labels=None):
+        """Emotion / speaker labels [B] of this step's references (the style-embedding
+        classifiers' targets, feeder.emt_labels / spk_labels); None, None clears them."""
+        if emt_labels is None and spk_labels is None:
+            check(self.lib.tt2_train_set_style_labels(self.h, None, None))
+            return
+        e = np.ascontiguousarray(np.asarray(emt_labels, np.int32).reshape(-1))
+        sp = None if spk_labels is None else np.ascontiguousarray(np.asarray(spk_labels, np.int32).reshape(-1))
+        if e.shape != (self.B,) or (sp is not None and sp.shape != (self.B,)):
+            raise ValueError("labels must be [batch]")
+        check(self.lib.tt2_train_set_style_labels(self.h, e.ctypes.data_as(ctypes.c_void_p),
+                                                  None if sp is None else sp.ctypes.data_as(ctypes.c_void_p)))
 
     def auto_teacher_forcing(self):
         """Draw the teacher forcing per step from the ratio schedule again (the default)."""
@@ -412,8 +456,12 @@ class TacotronTrainer(object):
         ms = ctypes.c_float()
         check(self.lib.tt2_train_losses(self.h, out.ctypes.data_as(ctypes.c_void_p),
                                         ctypes.byref(ms)))
+        sl = np.zeros(3, np.float32)
+        check(self.lib.tt2_train_style_losses(self.h, sl.ctypes.data_as(ctypes.c_void_p)))
         return dict(before=float(out[0]), stop_token=float(out[1]), regularization=float(out[2]),
-                    after=float(out[4]), loss=float(out[0] + out[1] + out[2] + out[4]),
+                    after=float(out[4]), style_emb_loss_emt=float(sl[0]), style_emb_loss_spk=float(sl[1]),
+                    style_emb_orthog_loss=float(sl[2]),
+                    loss=float(out[0] + out[1] + out[2] + out[4] + sl[0] + sl[1] + sl[2]),
                     grad_norm=float(out[3]),
                     forward_backward_ms=float(ms.value))
 

@@ -54,9 +54,12 @@ def test_training_api_validation():
     with pytest.raises(NotImplementedError, match="GST"):
         model.initialize(types.SimpleNamespace(**dict(vars(ARGS), pretrained_emb_disc_all=True)), ids, lens, tg, st,
                          is_training=True, ref_mel_emt=re, ref_mel_spk=rs)
-    with pytest.raises(NotImplementedError, match="discriminators"):
-        model.initialize(ARGS, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs,
-                         use_emt_disc=True)
+    hp3 = small_hparams()   # the default graph's style classifiers need the classes and labels
+    with pytest.raises(ValueError, match="number of emotions"):
+        _model(hp3, W).initialize(ARGS, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs)
+    with pytest.raises(ValueError, match="emt_labels"):
+        _model(hp3, W).initialize(ARGS, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs,
+                                  n_emt=4, n_spk=3)
     hp2 = hp.copy()
     hp2.override_from_dict(dict(tacotron_num_gpus=3))
     with pytest.raises(NotImplementedError, match="one process per GPU"):
@@ -66,31 +69,41 @@ def test_training_api_validation():
 
 
 @pytest.mark.gpu
-def test_reference_named_calls_match_trainer_step():
+@pytest.mark.parametrize("style", [False, True])
+def test_reference_named_calls_match_trainer_step(style):
     """Two steps through initialize(is_training=True) / add_loss() / add_optimizer(global_step)
     equal TacotronTrainer.step_text on the same inputs and keep bits bit for bit: losses, the
     updated parameters of every training variable, decoder outputs; mel_outputs =
     clip(decoder_output + Postnet projection)."""
     from oracle import train_ref as TRN
-    from tt2.train import TacotronTrainer
-    hp = _hp()
+    from tt2.train import TacotronTrainer, init_style_disc_weights
+    hp = small_hparams() if style else _hp()   # style: the default graph's classifier + orthogonality losses
     W = init_tacotron_weights(hp, seed=5339)
+    ne, ns = (4, 3) if style else (0, 0)
+    W.update(init_style_disc_weights(hp, ne, ns, seed=3))
+    el, sl = np.array([1, 3, 0], np.int32), np.array([2, 0, 1], np.int32)
     ids, lens, re, rs, tg, st, m = _batch(hp)
     B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
     model = _model(hp, W)
     got = []
     for step in range(2):
-        model.initialize(ARGS, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs, train_masks=m)
+        model.initialize(ARGS, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs, train_masks=m,
+                         n_emt=ne or None, n_spk=ns or None, emt_labels=el, spk_labels=sl)
         loss = model.add_loss()
         gs = model.add_optimizer(step)
         assert gs == step + 1 and model.optimize == step + 1
+        if style:
+            assert model.style_emb_loss_emt > 0 and model.style_emb_loss_spk > 0 and model.style_emb_orthog_loss > 0
         got.append(dict(loss=loss, before=model.before_loss, after=model.after_loss, stop=model.stop_token_loss,
                         reg=model.regularization_loss, dec=model.tower_decoder_output[0].copy(),
                         mel=model.tower_mel_outputs[0].copy(), stop_logits=model.tower_stop_token_prediction[0].copy()))
-    names = TRN.frontend_var_names() + TRN.train_var_names() + TRN.postnet_var_names()
+    names = (TRN.frontend_var_names() + TRN.style_disc_var_names(False, ne, ns) + TRN.train_var_names()
+             + TRN.postnet_var_names())
     params = {n: model._trainer.get(n, 0, np.asarray(W[n]).shape) for n in names}
-    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1])
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1], n_emt=ne, n_spk=ns)
     try:
+        if style:
+            tr.set_style_labels(el, sl)
         for step in range(2):
             L = tr.step_text(ids, lens, re, rs, tg, st, m["prenet"], m["zoneout"], m["postnet"], m["enc_conv"],
                              m["enc_zoneout"])

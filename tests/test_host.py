@@ -212,9 +212,11 @@ def test_tacotron_needs_weights_before_engine():
                      ref_mel_spk=np.zeros((1, 20, 80)), n_emt=4, n_spk=4)
 
 
-def test_tacotron_training_not_on_path():
+def test_tacotron_training_needs_style_labels():
+    """is_training=True is built (tests/test_gpu_train_api.py); the default graph's style-embedding
+    classifiers need the labels, refused before any device work."""
     m, hp = _taco()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError, match="emt_labels"):
         m.initialize(_args(), np.ones((1, 5), np.int32), [5], mel_targets=np.zeros((1, 3, 80)),
                      stop_token_targets=np.zeros((1, 3)), targets_lengths=[3], is_training=True,
                      ref_mel_emt=np.zeros((1, 20, 80)), ref_mel_spk=np.zeros((1, 20, 80)),

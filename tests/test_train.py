@@ -541,19 +541,31 @@ def test_gpu_train_frontend_matches_oracle(masks):
     """The whole configs[4] step from ids + reference mels (tt2_train_forward_backward_text_dev):
     every front-end, decoder and Postnet gradient within 2e-4 (relative to its max) of the torch
     float64 oracle, the losses, and the front-end BN moving averages after apply."""
-    from tt2.train import TacotronTrainer
+    from tt2.train import TacotronTrainer, init_style_disc_weights
     hp = small_hparams()
     W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, masks=masks)
     B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
-    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1])
+    # the default graph's style-embedding losses (tacotron.py:486-495, 812-846): orthogonality
+    # always (hp default), the classifiers in the masked case (labels incl. an out-of-range one)
+    n_emt, n_spk = (4, 3) if masks else (0, 0)
+    W.update(init_style_disc_weights(hp, n_emt, n_spk, seed=3))
+    el, sl = np.array([1, 3, 0], np.int32), np.array([2, 0, 7], np.int32)
+    style = dict(emt_labels=el, spk_labels=sl, n_emt=n_emt, n_spk=n_spk, orthog_weight=0.02)
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1], n_emt=n_emt, n_spk=n_spk)
     try:
+        if masks:
+            tr.set_style_labels(el, sl)
         tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
         L = tr.losses()
-        (b, s_, r, a), g, stats = TRN.train_grads_frontend(W, ids, lens, re, rs, tg, st, pm, zm, em, ezm,
-                                                           hp.tacotron_reg_weight, postnet_masks=pnm)
+        (b, s_, r, a, le, ls, lo), g, stats = TRN.train_grads_frontend(
+            W, ids, lens, re, rs, tg, st, pm, zm, em, ezm, hp.tacotron_reg_weight, postnet_masks=pnm, style=style)
         assert abs(L["before"] - b) < 1e-4 * b and abs(L["after"] - a) < 1e-4 * a
         assert abs(L["regularization"] - r) < 1e-4 * r + 1e-12
-        for n in TRN.frontend_var_names() + TRN.train_var_names() + TRN.postnet_var_names():
+        assert abs(L["style_emb_orthog_loss"] - lo) < 1e-4 * lo and lo > 0
+        assert abs(L["style_emb_loss_emt"] - le) < 1e-4 * max(le, 1e-3) and abs(L["style_emb_loss_spk"] - ls) < 1e-4 * max(ls, 1e-3)
+        assert (le > 0) == bool(masks)
+        for n in (TRN.frontend_var_names() + TRN.style_disc_var_names(False, n_emt, n_spk) + TRN.train_var_names()
+                  + TRN.postnet_var_names()):
             got = tr.get(n, 1, np.asarray(W[n]).shape)
             if np.abs(g[n]).max() < 1e-12:   # a conv bias feeding batch-statistics BN: exactly 0
                 assert np.abs(got).max() < 1e-6, (n, np.abs(got).max())
