@@ -11,7 +11,7 @@ import numpy as np
 from tt2.engine import WaveNetEngine
 from tt2.hparams import get_hop_size
 from tt2.weights import init_wavenet_weights
-from wavenet_vocoder.util import is_mulaw, is_mulaw_quantize, is_scalar_input
+from wavenet_vocoder.util import inv_mulaw, is_mulaw, is_mulaw_quantize, is_scalar_input
 
 
 def receptive_field_size(total_layers, num_cycles, kernel_size, dilation=lambda x: 2 ** x):
@@ -87,8 +87,9 @@ class WaveNet():
 
     def _check_path(self):
         hp = self._hparams
-        if not is_scalar_input(hp.input_type) or is_mulaw(hp.input_type):
-            raise NotImplementedError("only input_type='raw' is on the MI355X path")
+        if not is_scalar_input(hp.input_type):
+            raise NotImplementedError("input_type='mulaw-quantize' (one-hot input, softmax head) is "
+                                      "not on the MI355X path; 'raw' and 'mulaw' are")
         if not self.local_conditioning_enabled():
             raise NotImplementedError("unconditional synthesis (cin_channels <= 0) is not built")
 
@@ -144,7 +145,10 @@ class WaveNet():
                 ul = np.asarray(u_log, np.float32)[:, i * B:(i + 1) * B]
             out = self._get_engine(B, T).generate(ci, um, ul, seed, tis[i], want_upsampled=True,
                                                   g=gs[i])
-            self.tower_y_hat.append(out["y"])
+            y = out["y"]
+            if is_mulaw(hp.input_type):  # wavenet.py:459-460: samples are companded, expand them
+                y = inv_mulaw(y, hp.quantize_channels).astype(np.float32)
+            self.tower_y_hat.append(y)
             self.tower_synth_upsampled_local_features.append(out["upsampled"])
             self.tower_mix_indices.append(out["k"])
 
@@ -156,7 +160,8 @@ class WaveNet():
         reference passes it at wavenet.py:427) — upsampled inside, like the reference."""
         self._check_path()
         if initial_input is not None and np.any(np.asarray(initial_input) != 0):
-            raise NotImplementedError("initial_input must be the 'raw' silence value 0")
+            # the start silence of both scalar input types: 0.0 ('raw'), mulaw(0.0) = 0 ('mulaw')
+            raise NotImplementedError("initial_input must be the silence value 0")
         if abs(log_scale_min - self._hparams.log_scale_min) > 1e-6:
             raise ValueError("log_scale_min must equal hparams.log_scale_min on this build")
         c = np.asarray(c, np.float32).transpose(0, 2, 1)

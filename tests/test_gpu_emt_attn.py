@@ -137,6 +137,19 @@ def test_multihead_full_width_persistent_emt_only_gta():
           persistent_expected=1)
 
 
+@pytest.mark.parametrize("ref_gru", ["gru", "gru_multi"])
+def test_multihead_persistent_configs1_gta_vs_oracle(ref_gru):
+    """configs[1] shape (B = 32 ragged rows x 201 chars, T_ref 400) through k_decode_persist<true>,
+    200 teacher-forced steps against the oracle at the north_star 1e-4: frames, stop tokens,
+    alignments, mels and every step's emotion attention weights."""
+    hp = full_hparams()
+    B, T, TR, n = 32, 201, 400, 200
+    tg = np.random.default_rng(3).normal(0, 1, (B, n, hp.num_mels)).astype(np.float32)
+    out, _ = _case(hp, "multihead", ref_gru, B=B, T=T, T_ref=TR, n=n, seed=7, targets=tg,
+                   persistent_expected=1)
+    assert out["frames"].shape[1] == n
+
+
 def test_multihead_persistent_matches_launch_path_b32():
     """configs[1]-shaped batch (B = 32, T_ref 400): persistent decoder against the launch path over
     80 free-running steps, same weights, inputs and prenet masks (split fp16x3 vs fp32 MFMA products:

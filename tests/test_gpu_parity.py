@@ -373,6 +373,26 @@ def test_wavenet_shim_initialize():
     assert np.all(np.abs(m.tower_y_hat[0]) <= 1.0)
 
 
+def test_wavenet_shim_mulaw_input_type():
+    """input_type='mulaw' (wavenet.py:459-460): the same scalar-input generation as 'raw' (start
+    silence mulaw(0.0) = 0), the companded samples expanded with inv_mulaw (mu = 255) at the end."""
+    from wavenet_vocoder.models import create_model
+    from wavenet_vocoder.util import inv_mulaw
+    rng = np.random.default_rng(6)
+    c = WR.interp_condition(rng.uniform(-4, 4, (2, 1, 80)).astype(np.float32))
+    um, ul = mol_uniforms(275, 2, seed=1)
+    ys = {}
+    for it in ("raw", "mulaw"):
+        hp = small_wavenet_hparams(6, 2)
+        hp.override_from_dict(dict(input_type=it))
+        m = create_model("WaveNet", hp)
+        m.init_random_weights()
+        m.initialize(None, c, None, None, u_mix=um, u_log=ul)
+        ys[it] = m.tower_y_hat[0]
+    np.testing.assert_allclose(ys["mulaw"], inv_mulaw(ys["raw"]).astype(np.float32), rtol=1e-6, atol=1e-7)
+    assert np.abs(ys["mulaw"]).max() < np.abs(ys["raw"]).max() + 1e-6
+
+
 # ----------------------------------------------------------- single-step seam (tt2_decoder_step)
 
 def test_decoder_step_golden_fixture(full_setup):

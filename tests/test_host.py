@@ -342,3 +342,19 @@ def test_register_resident_kernels_do_not_spill(src, kernel, max_spill):
     for b in mine:
         spill = re.search(r"VGPRs Spill: (\d+)", b)
         assert spill and int(spill.group(1)) <= max_spill, b.splitlines()[0] + " spills VGPRs"
+
+
+def test_mulaw_companding_matches_reference_formulas():
+    """wavenet_vocoder/util.py:29-127 (mu fixed at 255 whatever the argument): known values and
+    round trips of mulaw / inv_mulaw / mulaw_quantize / inv_mulaw_quantize."""
+    import numpy as np
+    from wavenet_vocoder.util import inv_mulaw, inv_mulaw_quantize, mulaw, mulaw_quantize
+    assert mulaw(0.0) == 0.0 and abs(mulaw(1.0) - 1.0) < 1e-12 and abs(mulaw(-1.0) + 1.0) < 1e-12
+    assert mulaw_quantize(0.0) == 127 and mulaw_quantize(1.0) == 255 and mulaw_quantize(-1.0) == 0
+    x = np.linspace(-1, 1, 1001)
+    np.testing.assert_allclose(inv_mulaw(mulaw(x)), x, atol=1e-12)
+    np.testing.assert_allclose(mulaw(0.5), np.log1p(127.5) / np.log1p(255.0), rtol=1e-12)
+    np.testing.assert_allclose(mulaw(0.5, mu=65536), mulaw(0.5))
+    q = mulaw_quantize(x)
+    assert q.min() == 0 and q.max() == 255
+    assert np.abs(inv_mulaw_quantize(q) - x).max() < 0.05
