@@ -46,6 +46,12 @@ typedef __attribute__((address_space(1))) int pd_gi32;
 typedef __attribute__((address_space(1))) unsigned long long pd_gu64;
 #define PD_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 
+// h1 hand-off protocol (A/B switch): 0 = write-through stores, drain, replicated flag, consumer
+// polls its 32 producers' flags then loads; 1 = self-tagged values, flag as a hint polled after an
+// optimistic load missed; 2 = self-tagged values, the consumer re-loads the data until it is valid
+#ifndef PD_TAG_H1
+#define PD_TAG_H1 0
+#endif
 constexpr long long PD_TIMEOUT = 200000000LL;  // 2 s of s_memrealtime (100 MHz)
 constexpr int PD_LDS_FLOATS = 16384 * 2 + 4096 + 512 * 5 + 288 + 256 * 2 + 32 + 16 + 16 + 16 + 512;  // 159.6 KB
 
@@ -181,12 +187,74 @@ __device__ __forceinline__ bool pd_take(const PdArgs& a, int ph, const unsigned 
   }
 }
 
+// Self-tagged exchange values (h1, h2, context slices, Σ align): bit 0 of every fp32 value written at
+// step t carries tb(t) = ((t >> 1) & 1) ^ 1.  A buffer of parity t & 1 otherwise holds step t-2's
+// values (the other tag bit) or the per-launch zeros (bit 0 = 0 never matches steps 0, 1), so a
+// consumer can check every value it loaded: the producer needs no drain before its flag, and the
+// consumer no flag round trip before its data load when the data has landed.  The flag stays as a
+// hint polled only after an optimistic load missed.  Cost: one ulp (2^-23 relative) on exchanged
+// values, below the split fp16x3 products' own 2^-22.
+__device__ __forceinline__ unsigned pd_tb(int t) { return ((unsigned)(t >> 1) & 1u) ^ 1u; }
+__device__ __forceinline__ float pd_tag(float v, unsigned tb) { return __uint_as_float((__float_as_uint(v) & ~1u) | tb); }
+__device__ __forceinline__ bool pd_ok1(float v, unsigned tb) { return ((__float_as_uint(v) ^ tb) & 1u) == 0u; }
+__device__ __forceinline__ bool pd_ok4(const f32x4& v, unsigned tb) {
+  return (((__float_as_uint(v[0]) ^ tb) | (__float_as_uint(v[1]) ^ tb) | (__float_as_uint(v[2]) ^ tb) |
+           (__float_as_uint(v[3]) ^ tb)) & 1u) == 0u;
+}
+
+// Wave-level take of N self-tagged values X[idx(i)] (sc1 loads; V = f32x4 or float).  The first pass
+// is optimistic; after a miss hint() runs once (a flag poll: the producers have at least issued
+// their stores) and the loads repeat until every value carries tb (bounded spin; one copy of the
+// loads in the loop keeps the register footprint of the fast path).  false: timeout or a peer failed.
+__device__ __forceinline__ f32x4 pd_ldv(const float* X, int i, f32x4) { return pd_ld4(X, i); }
+__device__ __forceinline__ float pd_ldv(const float* X, int i, float) { return pd_ld(X + i); }
+__device__ __forceinline__ bool pd_okv(const f32x4& v, unsigned tb) { return pd_ok4(v, tb); }
+__device__ __forceinline__ bool pd_okv(float v, unsigned tb) { return pd_ok1(v, tb); }
+template <int N, class V, class I, class H>
+__device__ __forceinline__ bool pd_takev(const PdArgs& a, int ph, const float* X, I idx, unsigned tb, V (&v)[N],
+                                         H hint) {
+  long long t0 = 0;
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = pd_ldv(X, idx(i), v[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) ok = ok && pd_okv(v[i], tb);
+    if (__all(ok)) return true;
+    if (spin == 0) {
+      if (!hint()) return false;
+      t0 = __builtin_amdgcn_s_memrealtime();
+      continue;
+    }
+    if ((spin & 31) == 0) {
+      if (__hip_atomic_load((pd_gi32*)(a.ctl + 2), PD_RLX) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > PD_TIMEOUT) {
+        if ((threadIdx.x & 63) == 0) __hip_atomic_store((pd_gi32*)(a.ctl + 2), 1 + ph, PD_RLX);
+        return false;
+      }
+    }
+    for (int z = 0; z < a.poll_sleep; ++z) __builtin_amdgcn_s_sleep(1);
+  }
+}
+template <int N, class I, class H>
+__device__ __forceinline__ bool pd_take4(const PdArgs& a, int ph, const float* X, I idx, unsigned tb, f32x4 (&v)[N],
+                                         H hint) {
+  return pd_takev<N>(a, ph, X, idx, tb, v, hint);
+}
+template <int N, class I, class H>
+__device__ __forceinline__ bool pd_take1(const PdArgs& a, int ph, const float* X, I idx, unsigned tb, float (&v)[N],
+                                         H hint) {
+  return pd_takev<N>(a, ph, X, idx, tb, v, hint);
+}
+
 // LSTM epilogue store: the 4 hidden units this work-group owns for row em (pd_unit) are one AF
 // float4, held by the 4 consecutive lanes eu = 0..3; lane eu = 0 writes it as ONE 16-byte
-// write-through store (rows 0..15 / 16..31 of a work-group fill 256 contiguous bytes each).
-__device__ __forceinline__ void pd_st_h4(float* X, int em, int u0, float hn, int lane) {
+// write-through store (rows 0..15 / 16..31 of a work-group fill 256 contiguous bytes each),
+// every value self-tagged with tb (tb = ~0u: stored as computed, for the flag protocol).
+__device__ __forceinline__ void pd_st_h4(float* X, int em, int u0, float hn, int lane, unsigned tb) {
   const int src = lane & ~3;
-  const float v0 = __shfl(hn, src), v1 = __shfl(hn, src + 1), v2 = __shfl(hn, src + 2), v3 = __shfl(hn, src + 3);
+  const auto tg = [&](float v) { return tb > 1u ? v : pd_tag(v, tb); };
+  const float v0 = tg(__shfl(hn, src)), v1 = tg(__shfl(hn, src + 1));
+  const float v2 = tg(__shfl(hn, src + 2)), v3 = tg(__shfl(hn, src + 3));
   if ((lane & 3) == 0) {
     const auto r = __builtin_amdgcn_make_buffer_rsrc(X, (short)0, 0x7fffffff, 0x00020000);
     const u32x4 d = {__float_as_uint(v0), __float_as_uint(v1), __float_as_uint(v2), __float_as_uint(v3)};
@@ -199,6 +267,17 @@ __device__ __forceinline__ void pd_publish(const PdArgs& a, int ph, unsigned val
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) __hip_atomic_store((pd_gu32*)(a.flags + ph * PD_NB + blockIdx.x), val, PD_RLX);
+}
+
+// Flag hint of self-tagged data: no drain (the consumers check the tags), the barrier only so the
+// flag follows every wave's stores in issue order.
+__device__ __forceinline__ void pd_hint(const PdArgs& a, int ph, unsigned val, int tid) {
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store((pd_gu32*)(a.flags + ph * PD_NB + blockIdx.x), val, PD_RLX);
+}
+__device__ __forceinline__ void pd_hint_rep(const PdArgs& a, int r, unsigned val, int tid) {
+  __syncthreads();
+  if (tid < PD_NREP) __hip_atomic_store((pd_gu32*)(a.rflags + (r * PD_NREP + tid) * PD_NB + blockIdx.x), val, PD_RLX);
 }
 
 // pd_publish to every replica of h-phase r's flag line.
@@ -422,14 +501,20 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   // keeps its own K-slice partial Q_w with RG = (1-z)·Σ_w Q_w:  Q_w(t+1) = z·Q_w(t) + h_new(t)·W_h
   // (its slice), in registers.  No reduction: the partials join the gate accumulators of stage A/B,
   // whose cross-wave reduction runs anyway.  The two halves sit in two hand-off windows.
-  auto rec_half = [&](const float* X, const float* Wl, int h, f32x4& Qa, f32x4& Qb, int w, int lane) {
+  // Recurrent tail loads.  Only the RG2 tail of the F window (h2 of this step, all rows) checks the
+  // tags: the other tails read values this work-group already depends on (RG1: the k-slice this wave
+  // took in stage B; RG2 in the A window: h2 of step t-1, which every context, projection partial
+  // and prenet granule of t-1 -- taken before stage A -- was computed from).
+  auto rec_half = [&](int ph, const float* X, unsigned tb, const float* Wl, int h, f32x4& Qa, f32x4& Qb, int w,
+                      int lane, bool check) {
     const f32x4* Wv = reinterpret_cast<const f32x4*>(Wl);
-    f32x4 x0[4], x1v[4];
+    f32x4 xv[8];
+    const auto ix = [&](int i) { return ((8 * w + 4 * h + (i >> 1)) * 2 + (i & 1)) * 64 + lane; };
+    if (check) {
+      if (!pd_take4<8>(a, ph, X, ix, tb, xv, [] { return true; })) si[8] = 1;
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int sg = 8 * w + 4 * h + i;
-      x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
-      x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
+      for (int i = 0; i < 8; ++i) xv[i] = pd_ld4(X, ix(i));
     }
     if (h == 0) {
       Qa = a.zo * Qa;
@@ -438,7 +523,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int sg = 8 * w + 4 * h + i;
-      kg_mfma(x0[i], x1v[i], Wv[sg * 64 + lane], Qa, Qb);
+      kg_mfma(xv[2 * i], xv[2 * i + 1], Wv[sg * 64 + lane], Qa, Qb);
     }
   };
   __syncthreads();
@@ -454,6 +539,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   for (int t = 0; t < a.max_iters; ++t) {
     const unsigned tg = t + 1;
     const int p = t & 1;
+    const unsigned tb = pd_tb(t), tbp = pd_tb(t - 1);  // self-tag bits of steps t, t-1
     long long* const stp = (stp0 && t == a.stamp_step) ? stp0 : nullptr;
     // Thread indices re-derived from an opaque copy every step: otherwise every loop-invariant
     // LDS/global address of the body is hoisted out of the step loop and spilled.
@@ -549,30 +635,36 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       const float cn = sigm_fast(z[2] + 1.0f) * c1 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
       c1 = a.one_m_zo * cn + a.zo * c1;
-      pd_st_h4(a.H1x + p * 32 * PD_H, em, u0, hn, lane);
+      pd_st_h4(a.H1x + p * 32 * PD_H, em, u0, hn, lane, PD_TAG_H1 ? tb : ~0u);
     }
-    pd_publish_rep(a, 0, tg, tid);
+    if constexpr (PD_TAG_H1) pd_hint_rep(a, 0, tg, tid);
+    else pd_publish_rep(a, 0, tg, tid);
     PD_STAMP(2);
-    if (t > 0) rec_half(a.H2x + (p ^ 1) * 32 * PD_H, sW2h, 1, q2a, q2b, w, lane);  // RG2(t), 2nd half
+    if (t > 0) rec_half(PD_F_H2, a.H2x + (p ^ 1) * 32 * PD_H, tbp, sW2h, 1, q2a, q2b, w, lane, false);  // RG2(t), 2nd half
     PD_STAMP(3);
     // ================= B: LSTM layer 2 =================
     // wave w multiplies h1 units [128w, 128w+128) = the rows of producers [32w, 32w+32)
-    if (!pd_poll_rep(a, PD_F_H1, 0, 32 * w, tg, lane)) si[8] = 1;
+    if constexpr (!PD_TAG_H1)
+      if (!pd_poll_rep(a, PD_F_H1, 0, 32 * w, tg, lane)) si[8] = 1;
     PD_STAMP(4);
     {
       const float* X = a.H1x + p * 32 * PD_H;
       f32x4 s0 = a.one_m_zo * q2a, s1 = a.one_m_zo * q2b;  // + this wave's RG2 partial
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        f32x4 x0[4], x1v[4];
+        f32x4 xv[8];
+        const auto ix = [&](int i) { return ((8 * w + 4 * h + (i >> 1)) * 2 + (i & 1)) * 64 + lane; };
+        if constexpr (PD_TAG_H1 == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int sg = 8 * w + 4 * h + i;
-          x0[i] = pd_ld4(X, (sg * 2) * 64 + lane);
-          x1v[i] = pd_ld4(X, (sg * 2 + 1) * 64 + lane);
+          for (int i = 0; i < 8; ++i) xv[i] = pd_ld4(X, ix(i));
+        } else if constexpr (PD_TAG_H1 == 1) {
+          if (!pd_take4<8>(a, PD_F_H1, X, ix, tb, xv, [&] { return pd_poll_rep(a, PD_F_H1, 0, 32 * w, tg, lane); }))
+            si[8] = 1;
+        } else {
+          if (!pd_take4<8>(a, PD_F_H1, X, ix, tb, xv, [] { return true; })) si[8] = 1;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) kg_mfma(x0[i], x1v[i], w2i[4 * h + i], s0, s1);
+        for (int i = 0; i < 4; ++i) kg_mfma(xv[2 * i], xv[2 * i + 1], w2i[4 * h + i], s0, s1);
       }
       PD_STAMP(16);
       put_partials(s0, s1, red, w, lane);
@@ -590,9 +682,9 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       const float cn = sigm_fast(z[2] + 1.0f) * c2 + sigm_fast(z[0]) * tanh_rcp(z[1]);
       const float hn = sigm_fast(z[3]) * tanh_rcp(cn);
       c2 = a.one_m_zo * cn + a.zo * c2;
-      pd_st_h4(a.H2x + p * 32 * PD_H, em, u0, hn, lane);
+      pd_st_h4(a.H2x + p * 32 * PD_H, em, u0, hn, lane, tb);
     }
-    pd_publish_rep(a, 1, tg, tid);
+    pd_hint_rep(a, 1, tg, tid);
     PD_STAMP(5);
     // issued ahead of the RG1 tail and the H2 wait (L2-resident: shared by the 32 rows of slice j):
     f32x4 wq[8];  // W_q[32*(tid/16) + 4i + e][16j + tid%16] (q_wt is [A][H])
@@ -607,20 +699,22 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) kv[i] = K[(w + 8 * i) * 4 + (lane >> 4)];
     }
-    rec_half(a.H1x + p * 32 * PD_H, sW1h, 0, q1a, q1b, w, lane);  // RG1(t+1) from h1_new(t), 1st half
+    rec_half(PD_F_H1, a.H1x + p * 32 * PD_H, tb, sW1h, 0, q1a, q1b, w, lane, false);  // RG1(t+1) from h1_new(t), 1st half
     PD_STAMP(6);
     // ================= C: query slice + partial energies (attention.py:37-69, 186-201) =================
-    // wave w: producers [32w, 32w+32) = h2 units [128w, 128w+128), the units its RG2 tails read
-    // too; after the next barrier every wave may read all of h2_new (projection h2 rows)
-    if (!pd_poll_rep(a, PD_F_H2, 1, 32 * w, tg, lane)) si[8] = 1;
+    // wave w: h2 units [128w, 128w+128) of row b (producers [32w, 32w+32)), tagged loads
     PD_STAMP(7);
 
     if (rowv) {
       const float* X = a.H2x + p * 32 * PD_H;
       // wave w reads exactly the h2 units [128w, 128w+128) its own lanes multiply: wave-local
       // exchange (LDS ops of one wave complete in order), one block barrier for the 8 wave partials
-      red[128 * w + lane] = pd_ld(X + af_idx(b, 128 * w + lane));
-      red[128 * w + 64 + lane] = pd_ld(X + af_idx(b, 128 * w + 64 + lane));
+      float hv[2];
+      if (!pd_take1<2>(a, PD_F_H2, X, [&](int i) { return af_idx(b, 128 * w + 64 * i + lane); }, tb, hv,
+                       [&] { return pd_poll_rep(a, PD_F_H2, 1, 32 * w, tg, lane); }))
+        si[8] = 1;
+      red[128 * w + lane] = hv[0];
+      red[128 * w + 64 + lane] = hv[1];
       __builtin_amdgcn_wave_barrier();
       {
         const int seg = tid >> 4;
@@ -636,22 +730,34 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int ww = 0; ww < 8; ++ww) qk += red[1024 + ww * 16 + (lane & 15)];
       unsigned long long* E = a.Eg + (((long)p * 32 + b) * 8 + j) * PD_TMAX;
+      // after sum16 every lane of group q = lane/16 holds the energies of positions 4q + r; one
+      // shuffle gathers position l (l < 16) of i = 0 on lane l and of i = 1 on lane 16 + l, so the
+      // 32 granules leave as ONE store instruction of two whole 128-B lines (not 8 stores of 4
+      // lanes at a 32-B stride, each its own fabric write)
+      float sel[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        float e4[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = sum16(va_k * tanh_fast(kv[i][r] + qk + loc[i][r]));
-          if ((lane & 15) == 0) pd_put(E + (w + 8 * i) * 16 + (lane >> 4) * 4 + r, tg, e);
-        }
+        for (int r = 0; r < 4; ++r) e4[r] = sum16(va_k * tanh_fast(kv[i][r] + qk + loc[i][r]));
+        const int rr = lane & 3;
+        sel[i] = rr == 0 ? e4[0] : rr == 1 ? e4[1] : rr == 2 ? e4[2] : e4[3];
+      }
+      const int src = ((lane >> 2) & 3) * 16 + (lane & 3);
+      const float v0 = __shfl(sel[0], src), v1 = __shfl(sel[1], src);
+      if (lane < 32) pd_put(E + (w + 8 * (lane >> 4)) * 16 + (lane & 15), tg, lane < 16 ? v0 : v1);
     }
     __syncthreads();  // red / qv reuse below
     if (si[8]) return;
     PD_STAMP(8);
     if (isproj) {  // projection partial, h2_new rows of this split (Architecture_wrappers.py:243-247)
       const float* X = a.H2x + p * 32 * PD_H;
-      const int sg = 8 * pks + w;
-      f32x4 s0 = zero4, s1 = zero4;
-      kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), WPH[w * 64 + lane], s0, s1);
+      const int sg = 8 * pks + w;  // h2 units [128 pks + 16w, +16): producers [32 pks, 32 pks + 32)
+      f32x4 s0 = zero4, s1 = zero4, xv[2];
+      if (!pd_take4<2>(a, PD_F_H2, X, [&](int i) { return (sg * 2 + i) * 64 + lane; }, tb, xv,
+                       [&] { return pd_poll_rep(a, PD_F_H2, 1, 32 * pks, tg, lane); }))
+        si[8] = 1;
+      kg_mfma(xv[0], xv[1], WPH[w * 64 + lane], s0, s1);
       reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
       if (isq) {  // emotion query: h2 rows are all of it -> granules for the emotion work-groups
         const int m = tid >> 4, col = tid & 15;
@@ -744,19 +850,19 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         float s = 0.f;
 #pragma unroll
         for (int ts = 0; ts < 8; ++ts) s += red[ts * 64 + tid];
-        pd_st(a.CTXx + p * 32 * PD_E2 + af_idx(b, 64 * j + tid), s);
+        pd_st(a.CTXx + p * 32 * PD_E2 + af_idx(b, 64 * j + tid), pd_tag(s, tb));
       }
-      if (tid == 64 && j == 0) pd_st(a.SSx + p * 32 + b, sc[2]);
+      if (tid == 64 && j == 0) pd_st(a.SSx + p * 32 + b, pd_tag(sc[2], tb));
     } else {
-      if (tid < 64) pd_st(a.CTXx + p * 32 * PD_E2 + af_idx(b, 64 * j + tid), 0.f);
-      if (tid == 64 && j == 0) pd_st(a.SSx + p * 32 + b, 0.f);
+      if (tid < 64) pd_st(a.CTXx + p * 32 * PD_E2 + af_idx(b, 64 * j + tid), pd_tag(0.f, tb));
+      if (tid == 64 && j == 0) pd_st(a.SSx + p * 32 + b, pd_tag(0.f, tb));
     }
     if constexpr (EMT) {
       if (tid == 0) si[6] = 1;  // emotion-stage failure flag (read after barriers below)
     }
-    pd_publish(a, PD_F_CTX, tg, tid);
+    pd_hint(a, PD_F_CTX, tg, tid);
     PD_STAMP(10);
-    rec_half(a.H1x + p * 32 * PD_H, sW1h, 1, q1a, q1b, w, lane);  // RG1(t+1), 2nd half
+    rec_half(PD_F_H1, a.H1x + p * 32 * PD_H, tb, sW1h, 1, q1a, q1b, w, lane, false);  // RG1(t+1), 2nd half
     // location features of step t+1: im2col(cum) · (W_conv·W_loc) on MFMA (attention.py:59-62)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -896,16 +1002,19 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       }
     }
     if (isproj && !isq) {
-      if (!pd_block_wait(si + 6, [&] { return pd_poll(a, PD_F_CTX, 32 * pks, 1, 32, tg, 0, lane); })) return;
       PD_STAMP(11);
-      if (w < 4) {
+      if (w < 4) {  // context channels [64 pks + 16w, +16): slice j = pks, producers [32 pks, 32 pks + 32)
         const float* X = a.CTXx + p * 32 * PD_E2;
         const int sg = 4 * pks + w;
-        f32x4 s0 = zero4, s1 = zero4;
-        kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wpc, s0, s1);
+        f32x4 s0 = zero4, s1 = zero4, xv[2];
+        if (!pd_take4<2>(a, PD_F_CTX, X, [&](int i) { return (sg * 2 + i) * 64 + lane; }, tb, xv,
+                         [&] { return pd_poll(a, PD_F_CTX, 32 * pks, 1, 32, tg, 0, lane); }))
+          si[8] = 1;
+        kg_mfma(xv[0], xv[1], wpc, s0, s1);
         put_partials(s0, s1, red, w, lane);
       }
       __syncthreads();
+      if (si[8]) return;
       {
         const int m = tid >> 4, col = tid & 15;
         pd_put(a.PPg + (((long)p * PD_KSP + pks) * 32 + m) * PD_NPF + 16 * pn + col, tg, sum_partials<4>(red, tid) + PPh[tid]);
@@ -914,7 +1023,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       PD_STAMP(12);
     }
     // ================= F: frame / stop (modules.py:392-448), prenet of step t+1 =================
-    rec_half(a.H2x + p * 32 * PD_H, sW2h, 0, q2a, q2b, w, lane);  // RG2(t+1) from h2_new(t), 1st half
+    rec_half(PD_F_H2, a.H2x + p * 32 * PD_H, tb, sW2h, 0, q2a, q2b, w, lane, true);  // RG2(t+1) from h2_new(t), 1st half
     PD_STAMP(13);
     int stopbit = 0;
     if (tid == 0) si[5] = 1;
@@ -983,17 +1092,24 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         if (!si[6]) return;
       }
     }
-    {  // L1 context rows of step t+1 and the style scales: every context slice of t landed before
-       // any PP flag (PP <- CTX slices of all 8 splits), and this work-group has seen all PP flags
+    {  // L1 context rows of step t+1 and the style scales (tagged loads: every context slice of t was
+       // taken by a projection block before its PP partial, so the values have normally landed)
       const float* XC = a.CTXx + p * 32 * PD_E2;
       accC0 = zero4;
       accC1 = zero4;
+      f32x4 xv[8];  // wave w: channels [64w, 64w + 64) = slice j = w, producers [32w, 32w + 32)
+      if (!pd_take4<8>(a, PD_F_CTX, XC, [&](int i) { return ((4 * w + (i >> 1)) * 2 + (i & 1)) * 64 + lane; }, tb, xv,
+                       [&] { return pd_poll(a, PD_F_CTX, 32 * w, 1, 32, tg, 0, lane); }))
+        si[8] = 1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int sg = 4 * w + i;
-        kg_mfma(pd_ld4(XC, (sg * 2) * 64 + lane), pd_ld4(XC, (sg * 2 + 1) * 64 + lane), w1c[i], accC0, accC1);
+      for (int i = 0; i < 4; ++i) kg_mfma(xv[2 * i], xv[2 * i + 1], w1c[i], accC0, accC1);
+      if (w == 0) {  // Σ_{t<len} align of every row (written by the j = 0 work-groups, producers [0, 32))
+        float sv[1];
+        if (!pd_take1<1>(a, PD_F_CTX, a.SSx + p * 32, [&](int) { return lane & 31; }, tb, sv,
+                         [&] { return pd_poll(a, PD_F_CTX, 0, 1, 32, tg, 0, lane); }))
+          si[8] = 1;
+        if (lane < 32) ssa[lane] = sv[0];
       }
-      if (tid < 32) ssa[tid] = pd_ld(a.SSx + p * 32 + tid);
     }
     if constexpr (EMT) {  // the emotion block of step t joins the next step's LSTM-1 input (wave w: k-group w)
       if (!pd_block_wait(si + 6, [&] { return pd_poll_rep(a, PD_F_EMT, 2, PD_EG0, tg, lane, 16); })) return;

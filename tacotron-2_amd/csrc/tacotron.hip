@@ -2196,9 +2196,11 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
                      (long)c->Dm, c->valuesT.as<float>(), c->T_in, PD_E2);
   TT2_HIP(hipGetLastError());
   // flags + ctl words, every launch; granule tags restart at 1 every launch: a stale tag of an
-  // earlier decode must never match
+  // earlier decode must never match.  The self-tagged h1 / h2 / context / Σ-align buffers are zeroed
+  // too (tag bit 0, which steps 0 and 1 never expect: decode_persist.hip pd_tb)
   zero_many({{c->pd_ctl.p, c->pd_ctl.bytes}, {c->Ex.p, c->Ex.bytes}, {c->PPx.p, c->PPx.bytes},
-             {c->PREx.p, c->PREx.bytes}}, s);
+             {c->PREx.p, c->PREx.bytes}, {c->H1x.p, c->H1x.bytes}, {c->H2x.p, c->H2x.bytes},
+             {c->CTXx.p, c->CTXx.bytes}, {c->SSx.p, c->SSx.bytes}}, s);
   if (emt) {
     zero_many({{c->QEx.p, c->QEx.bytes}, {c->EOx.p, c->EOx.bytes}, {c->EMTx.p, c->EMTx.bytes}}, s);
     // zero_state (Architecture_wrappers.py:182): the step-0 emotion block is refnet_spk alone
