@@ -448,6 +448,11 @@ typedef struct tt2_train_config {
    * orthog_weight * ||refnet_emt · refnet_spkᵀ||_F (0.02 in the reference; not emt_only).  0 = off. */
   int n_emt, n_spk;
   float orthog_weight;
+  /* hp.use_gst (tacotron.py:269-291): 1 = each reference embedding passes through its GST
+   * multi-head attention (style_embed_depth wide); 0 = the 128-wide reference embeddings themselves
+   * are the style embeddings (no style tokens / attention variables; memory_dim = 2*U + (emt_only ?
+   * 1 : 2) * 128) */
+  int use_gst;
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;

@@ -218,9 +218,10 @@ RN = P + "refnet_{}/"
 MH = P + "Multihead-attention-{}/"
 
 
-def frontend_var_names(emt_only=False, conv_layers=3, ref_layers=6):
+def frontend_var_names(emt_only=False, conv_layers=3, ref_layers=6, use_gst=True):
     """Trainable front-end variables (tacotron.py:215-308, modules.py:9-64,251-323,
-    multihead_attention.py:35-132), in the library's flat-buffer order."""
+    multihead_attention.py:35-132), in the library's flat-buffer order.  use_gst=False: no style
+    tokens / style attention (tacotron.py:284-291)."""
     names = [P + "inputs_embedding"]
     for i in range(1, conv_layers + 1):
         s = EC.format(i)
@@ -236,7 +237,10 @@ def frontend_var_names(emt_only=False, conv_layers=3, ref_layers=6):
                       s + "batch_normalization/beta"]
         names += [r + "rnn/gru_cell/gates/kernel", r + "rnn/gru_cell/gates/bias",
                   r + "rnn/gru_cell/candidate/kernel", r + "rnn/gru_cell/candidate/bias",
-                  r + "dense/kernel", r + "dense/bias", P + "style_tokens_" + tag]
+                  r + "dense/kernel", r + "dense/bias"]
+        if not use_gst:
+            continue
+        names += [P + "style_tokens_" + tag]
         m = MH.format(tag)
         names += [m + "conv1d/kernel", m + "conv1d/bias", m + "conv1d_1/kernel", m + "conv1d_1/bias",
                   m + "attention_v", m + "attention_g", m + "attention_b"]
@@ -343,14 +347,15 @@ def _gst(ref, W, tag, heads=4):
 
 
 def frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks=None, enc_zm=None, emt_only=False,
-                     eps=1e-3, moving=None, refs_out=None):
+                     eps=1e-3, moving=None, refs_out=None, use_gst=True):
     """Training-mode front end -> memory [B,T_in,D] (unmasked: the decoder masks it) and the batch
     statistics [(mean, var)] of every batch norm (encoder convs, then refnet convs).
     enc_masks [3, B, T_in, C] conv dropout keep bits (rate 0.5) or None; enc_zm [T_in, 2 (fw, bw),
     2 (c, h), B, U] LSTM zoneout keep bits or None.  ``moving`` (dict name -> array) evaluates the
     batch norms with the moving statistics: with no masks that is the inference graph, pinned to
     oracle/tacotron_ref.py (tests/test_train.py).  ``refs_out`` (a list) receives the reference
-    encoders' outputs refnet_outputs_emt / _spk [B, 128] (tacotron.py:260-261)."""
+    encoders' outputs refnet_outputs_emt / _spk [B, 128] (tacotron.py:260-261).  use_gst=False:
+    those outputs are the style embeddings themselves (tacotron.py:284-291)."""
     def mv(scope):
         if moving is None:
             return None
@@ -392,7 +397,7 @@ def frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks=None, enc_zm=N
         refo = torch.tanh(hl @ W[r + "dense/kernel"] + W[r + "dense/bias"])
         if refs_out is not None:
             refs_out.append(refo)
-        style = _gst(refo, W, tag)
+        style = _gst(refo, W, tag) if use_gst else refo
         parts.append(style[:, None, :].expand(B, T, style.shape[1]))
     return torch.cat(parts, -1), stats
 
@@ -434,18 +439,19 @@ def style_emb_losses(W, refs, emt_labels, spk_labels, n_emt=0, n_spk=0, orthog_w
 
 def train_grads_frontend(Wnp, ids, lengths, ref_emt, ref_spk, targets, stop_targets, prenet_masks,
                          zoneout_masks, enc_masks, enc_zm, reg_weight=1e-6, dtype=torch.float64,
-                         clip=(-4.1, 4.0), postnet_masks=None, emt_only=False, style=None):
+                         clip=(-4.1, 4.0), postnet_masks=None, emt_only=False, style=None, use_gst=True):
     """The whole configs[4] step: front end (training mode) -> memory -> decoder + Postnet; returns
     (losses, grads of every front-end, decoder and Postnet variable, [(mean, var)] batch stats of
     the front end's batch norms).  ``style`` = dict(emt_labels, spk_labels, n_emt, n_spk,
     orthog_weight) adds the style-embedding losses (style_emb_losses); the losses tuple then
     gains (loss_emt, loss_spk, loss_orthog)."""
     st_kw = dict(style or {})
-    names = (frontend_var_names(emt_only) + style_disc_var_names(emt_only, st_kw.get("n_emt", 0), st_kw.get("n_spk", 0))
+    names = (frontend_var_names(emt_only, use_gst=use_gst) + style_disc_var_names(emt_only, st_kw.get("n_emt", 0), st_kw.get("n_spk", 0))
              + train_var_names() + postnet_var_names())
     W = {n: torch.tensor(np.asarray(Wnp[n]), dtype=dtype, requires_grad=True) for n in names}
     refs = []
-    mem, stats = frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks, enc_zm, emt_only, refs_out=refs)
+    mem, stats = frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks, enc_zm, emt_only, refs_out=refs,
+                                  use_gst=use_gst)
     tg = torch.tensor(np.asarray(targets), dtype=dtype)
     st = torch.tensor(np.asarray(stop_targets), dtype=dtype)
     pm = torch.tensor(np.asarray(prenet_masks), dtype=dtype)

@@ -71,6 +71,9 @@ struct tt2_train_ctx {
   long blas_calls = 0;
   // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
   DevBuf hK1, hK1T, hK2, hK2T, hWq, hWqT;
+  DevBuf X1h, X2h;  // bf16 shadows of the X1 / X2 rows (inputs of the fused LSTM products)
+  DevBuf dGh;       // bf16 shadows of one step's dG2 | dG1 rows (fused backward products)
+  DevBuf tK1T, tK2T, tWq, tK2, tK1;  // the fused products' weights in TF layout (k_tr_tf_weights)
   // Postnet training (cfg.postnet): PA[i] activations (pre-BN), PX[i] layer inputs (PX[0] unused:
   // layer 1 reads the clipped frames), batch stats, projection, scratch
   DevBuf PA[8], PX[9];  // postnet_layers <= 8
@@ -334,6 +337,256 @@ __global__ void k_tr_lstm_fwd(TrLstmFwd a) {
   a.hz_out[(long)b * a.ld_hz + n] = h;
 }
 
+// ---- fused skinny products of the decoder steps: bf16 product + epilogue in ONE launch ----------
+// One decoder step's B <= 64-row products C = X·W (W as its pre-transposed bf16 copy Wt[N][K], so any
+// column set is a set of contiguous K-vectors) with the consumer's epilogue fused, WHOLE K per
+// work-group: no split-K partials and no combine launch.  Work-group = 32 output columns x one
+// 32-row half; its 8 waves split K (K/8 each) and load their fragments 16 k-steps at a time
+// (v_mfma_f32_32x32x16_bf16, one accumulator per wave); the 8 wave partials are summed in LDS.
+// The two row halves of a column group are blocks g and g + 8, which share an XCD under
+// round-robin dispatch, so the second read of the weight columns is an L2 hit (speed only).
+//   TF_FWD   LSTM layer forward: columns {q·H + u0 + k} (q < 4 gates, k < 8 units), epilogue =
+//            k_tr_lstm_fwd's cell + zoneout (Architecture_wrappers.py:214-224, zoneout_lstm.py)
+//   TF_BWD_H LSTM layer-2 backward: columns = 32 units of d h (= d query · Wq^T, K = A, fp32 A
+//            rows converted in-register) + d h from the frame projection, epilogue = k_tr_lstm_bwd's
+//   TF_BWD_S LSTM layer-1 backward: columns = 16 units of d h1 and the same 16 of d hz2_{t-1}
+//            (= dG2 · K2^T), the latter written out (+ R2), epilogue = k_tr_lstm_bwd's
+//   TF_PLAIN C = X·W + residual (d X1 = dG1 · K1^T + R1)
+// A operands are bf16 shadows of the fp32 rows written by their producers (same round-to-nearest-
+// even as the staged operands of the bf16 GEMMs), except TF_BWD_H's.
+enum { TF_FWD = 0, TF_BWD_H = 1, TF_BWD_S = 2, TF_PLAIN = 3 };
+// Fragment-major bf16 layout of a [rows][K] operand ("TF layout"): 32-row blocks x 16-deep k-steps x
+// [32 rows][16 k], so one wave's v_mfma_f32_32x32x16_bf16 fragment load of a k-step (lane l: row l%32,
+// k = 8(l/32) .. +8) is ONE contiguous kilobyte instead of 32 rows a K-stride apart.  The weights are
+// re-laid once per step in their column-group order (k_tr_tf_weights), the activation shadows are
+// written in it by their producers; a step's row blocks cover Bp = B rounded up to 32 rows.
+__host__ __device__ inline long tf_sw(int r, int k, int K) {
+  return ((((long)(r >> 5) * (K >> 4) + (k >> 4)) * 32 + (r & 31)) << 4) + (k & 15);
+}
+__host__ __device__ inline long tf_colmap(int mode, int cg, int c, int H) {
+  if (mode == TF_FWD) return (long)(c >> 3) * H + cg * 8 + (c & 7);
+  if (mode == TF_BWD_S) return c < 16 ? cg * 16 + c : H + cg * 16 + (c - 16);
+  return (long)cg * 32 + c;
+}
+// W^T [N][K] bf16 -> TF layout in the fused kernel's column-group order (columns past N are zero)
+__global__ void k_tr_tf_weights(const __bf16* __restrict__ src, int N, int K, int ncg, int mode, int H,
+                                __bf16* __restrict__ dst) {
+  const long n = (long)ncg * 32 * K;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / K), k = (int)(i % K);  // r = 32 cg + c
+    const long col = tf_colmap(mode, r >> 5, r & 31, H);
+    dst[tf_sw(r, k, K)] = col < N ? src[col * K + k] : (__bf16)0.f;
+  }
+}
+constexpr int TLG_U = 8, TLG_NT = 512, TLG_KSMAX = 16;
+typedef float tlg_f32x16 __attribute__((ext_vector_type(16)));
+struct TrFused {
+  const __bf16* Ah;  // this step's bf16 input rows, TF layout of width K, or
+  const float* Af;   // fp32 input rows (TF_BWD_H)
+  long lda;
+  const __bf16* Wt;  // W^T in TF layout, column-group order (k_tr_tf_weights)
+  int K, B, H, N;
+  int t, layer;
+  float z;
+  const uint8_t* zm;     // [T][4][B][H] zoneout keep masks or null
+  const float* G;        // fwd: out [B][4H] activated gates; bwd: in
+  const float* bias;     // fwd
+  const float* c_prev;   // [B,H]
+  const float* hz_prev;  // fwd, strided
+  long ld_hz_prev;
+  float* cn;             // fwd out / bwd in [B,H]
+  float* c_out;          // fwd [B,H]
+  float* h_out;          // fwd strided h_new
+  long ld_h;
+  float* hz_out;         // fwd strided zoned h
+  long ld_hz;
+  __bf16* h_out_h;       // fwd bf16 TF-layout shadows (step block base, width ld_*_h, column offset
+  long ld_h_h;           // *_col0) or null
+  __bf16* hz_out_h;
+  long ld_hz_h;
+  int h_col0, hz_col0;
+  const float* dh_ext;   // bwd: d h_new from the frame projection (strided) or null
+  long ld_dh;
+  float* side;           // TF_BWD_S: d hz2_{t-1} out (strided), = product + side_res[.][H + n]
+  long ld_side;
+  const float* side_res;
+  long ld_side_res;
+  const float* dhz;      // bwd: d(zoned h_t) from step t+1 (strided)
+  long ld_dhz;
+  float* DC;             // bwd [B,H] in/out
+  float* dG;             // bwd out [B][4H]
+  __bf16* dGh;           // bwd bf16 shadow of dG or null
+  float* R;              // bwd [B][ldr] at off_r + n
+  long ldr;
+  int off_r;
+  float* C;              // TF_PLAIN out (ld ldc) = product + residual
+  long ldc;
+  const float* residual;
+  long ldres;
+};
+
+// LSTM cell backward of one (row, unit) (k_tr_lstm_bwd): dext = d h_new from outside the cell
+__device__ __forceinline__ void tf_cell_bwd(const TrFused& a, int b, int n, float dext) {
+  const long i = (long)b * a.H + n;
+  const float* g = a.G + (long)b * 4 * a.H;
+  const float si = g[n], tj = g[a.H + n], sf = g[2 * a.H + n], so = g[3 * a.H + n];
+  float kc, kh;
+  if (a.zm) {
+    const long base = (((long)a.t * 4 + 2 * a.layer) * a.B + b) * a.H + n;
+    kc = (float)a.zm[base];
+    kh = (float)a.zm[base + (long)a.B * a.H];
+  } else {
+    kc = kh = 1.f - a.z;
+  }
+  const float dhz = a.dhz[(long)b * a.ld_dhz + n];
+  const float dcz = a.DC[i];
+  const float dhn = dext + kh * dhz;
+  const float tc = tanhf(a.cn[i]);
+  const float dcn = kc * dcz + dhn * so * (1.f - tc * tc);
+  const float dso = dhn * tc, dsf = dcn * a.c_prev[i], dsi = dcn * tj, dtj = dcn * si;
+  const float d0 = dsi * si * (1.f - si), d1 = dtj * (1.f - tj * tj), d2 = dsf * sf * (1.f - sf), d3 = dso * so * (1.f - so);
+  float* dg = a.dG + (long)b * 4 * a.H;
+  dg[n] = d0;
+  dg[a.H + n] = d1;
+  dg[2 * a.H + n] = d2;
+  dg[3 * a.H + n] = d3;
+  if (a.dGh) {  // TF layout, width 4H
+    const int K4 = 4 * a.H;
+    a.dGh[tf_sw(b, n, K4)] = (__bf16)d0;
+    a.dGh[tf_sw(b, a.H + n, K4)] = (__bf16)d1;
+    a.dGh[tf_sw(b, 2 * a.H + n, K4)] = (__bf16)d2;
+    a.dGh[tf_sw(b, 3 * a.H + n, K4)] = (__bf16)d3;
+  }
+  a.DC[i] = (1.f - kc) * dcz + dcn * sf;
+  a.R[(long)b * a.ldr + a.off_r + n] = (1.f - kh) * dhz;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
+  typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+  __shared__ float red[8][32][33];  // wave partials [w][row][col] (padded)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ncg = gridDim.x >> 1, bid = blockIdx.x;
+  const int cg = (ncg & 7) == 0 ? (bid & 7) + 8 * (bid >> 4) : bid >> 1;
+  const int rh = (ncg & 7) == 0 ? (bid >> 3) & 1 : bid & 1;
+  const int r0 = 32 * rh;
+  const int kw = a.K >> 3, k0 = w * kw, ks = kw >> 4;  // host: K % 128 == 0
+  const int c = lane & 31, kh = 8 * (lane >> 5);
+  const bool rok = r0 + c < a.B;
+  const bf8 z8 = {};
+  tlg_f32x16 acc = {};
+  for (int s0 = 0; s0 < ks; s0 += TLG_KSMAX) {
+    bf8 va[TLG_KSMAX], vb[TLG_KSMAX];
+#pragma unroll
+    for (int s = 0; s < TLG_KSMAX; ++s) {
+      if (s0 + s < ks) {
+        const int k = k0 + 16 * (s0 + s) + kh;
+        vb[s] = *reinterpret_cast<const bf8*>(a.Wt + tf_sw(32 * cg + c, k, a.K));
+        if constexpr (MODE == TF_BWD_H) {
+          if (rok) {
+            const float* p = a.Af + (long)(r0 + c) * a.lda + k;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+            va[s] = bf8{(__bf16)x0[0], (__bf16)x0[1], (__bf16)x0[2], (__bf16)x0[3],
+                        (__bf16)x1[0], (__bf16)x1[1], (__bf16)x1[2], (__bf16)x1[3]};
+          } else {
+            va[s] = z8;
+          }
+        } else {
+          va[s] = rok ? *reinterpret_cast<const bf8*>(a.Ah + tf_sw(r0 + c, k, a.K)) : z8;
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < TLG_KSMAX; ++s)
+      if (s0 + s < ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s], vb[s], acc, 0, 0, 0);
+  }
+  // D layout: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[w][(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][c] = acc[r];
+  __syncthreads();
+  const auto sum8 = [&](int rl, int cc) {
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) v += red[ww][rl][cc];
+    return v;
+  };
+  if constexpr (MODE == TF_FWD) {
+    if (tid >= 256) return;
+    const int rl = tid >> 3, b = r0 + rl, kk = tid & 7, n = cg * 8 + kk;
+    if (b >= a.B) return;
+    float pre[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pre[q] = a.bias[q * a.H + n] + sum8(rl, q * 8 + kk);
+    const float si = sigm_acc(pre[0]), tj = tanhf(pre[1]), sf = sigm_acc(pre[2] + 1.0f), so = sigm_acc(pre[3]);
+    float* g = const_cast<float*>(a.G) + (long)b * 4 * a.H;
+    g[n] = si;
+    g[a.H + n] = tj;
+    g[2 * a.H + n] = sf;
+    g[3 * a.H + n] = so;
+    const long i = (long)b * a.H + n;
+    const float cp = a.c_prev[i];
+    const float hp = a.hz_prev[(long)b * a.ld_hz_prev + n];
+    const float cnew = sf * cp + si * tj;
+    const float hnew = so * tanhf(cnew);
+    float cz, hz;
+    if (a.zm) {
+      const long base = (((long)a.t * 4 + 2 * a.layer) * a.B + b) * a.H + n;
+      const float mc = (float)a.zm[base], mh = (float)a.zm[base + (long)a.B * a.H];
+      cz = cp + mc * (cnew - cp);
+      hz = hp + mh * (hnew - hp);
+    } else {
+      cz = (1.f - a.z) * cnew + a.z * cp;
+      hz = (1.f - a.z) * hnew + a.z * hp;
+    }
+    a.cn[i] = cnew;
+    a.c_out[i] = cz;
+    a.h_out[(long)b * a.ld_h + n] = hnew;
+    a.hz_out[(long)b * a.ld_hz + n] = hz;
+    if (a.h_out_h) a.h_out_h[tf_sw(b, a.h_col0 + n, (int)a.ld_h_h)] = (__bf16)hnew;
+    if (a.hz_out_h) a.hz_out_h[tf_sw(b, a.hz_col0 + n, (int)a.ld_hz_h)] = (__bf16)hz;
+  } else if constexpr (MODE == TF_BWD_H) {  // 32 rows x 32 units, two per thread
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int pidx = tid + TLG_NT * e, rl = pidx >> 5, kk = pidx & 31, b = r0 + rl, n = cg * 32 + kk;
+      if (b < a.B) tf_cell_bwd(a, b, n, sum8(rl, kk) + (a.dh_ext ? a.dh_ext[(long)b * a.ld_dh + n] : 0.f));
+    }
+  } else if constexpr (MODE == TF_BWD_S) {  // 32 rows x 16 units
+    const int rl = tid >> 4, kk = tid & 15, b = r0 + rl, n = cg * 16 + kk;
+    if (b >= a.B) return;
+    a.side[(long)b * a.ld_side + n] = sum8(rl, 16 + kk) + a.side_res[(long)b * a.ld_side_res + a.H + n];
+    tf_cell_bwd(a, b, n, sum8(rl, kk));
+  } else {  // TF_PLAIN: 32 rows x 32 columns, two per thread
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int pidx = tid + TLG_NT * e, rl = pidx >> 5, kk = pidx & 31, b = r0 + rl;
+      const long n = (long)cg * 32 + kk;
+      if (b < a.B && n < a.N)
+        a.C[(long)b * a.ldc + n] = sum8(rl, kk) + (a.residual ? a.residual[(long)b * a.ldres + n] : 0.f);
+    }
+  }
+}
+
+// dst[r][c] = src[r][c] (+ add[r][c]): strided row-block copies (use_gst = 0 style embeddings)
+__global__ void k_tr_rows_copy(const float* __restrict__ src, long lds, long rows, int cols, float* __restrict__ dst,
+                               long ldd, const float* __restrict__ add, long ldadd) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const long r = i / cols, cc = i % cols;
+  dst[r * ldd + cc] = src[r * lds + cc] + (add ? add[r * ldadd + cc] : 0.f);
+}
+
+// fp32 rows [rows][cols] (ld lds; row r = step r / B, row r % B) -> the bf16 TF-layout shadow of width
+// K (steps of Bp rows): the fused products' input rows that no kernel writes as a by-product (prenet)
+__global__ void k_tr_rows_bf16(const float* __restrict__ src, long lds, long rows, int cols, int B, int K,
+                               __bf16* __restrict__ dst) {
+  const long n = rows * cols;
+  const long Bp = (B + 31) & ~31;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols, cc = i % cols;
+    dst[(r / B) * Bp * K + tf_sw((int)(r % B), (int)cc, K)] = (__bf16)src[r * lds + cc];
+  }
+}
+
 struct TrAtt {
   int B, Tin, T, A, F, KW, D, H, P, t, nt;  // nt = j-tiles per row (TR_JT rows each)
   const int* lens;
@@ -356,6 +609,7 @@ struct TrAtt {
   // forward outputs of the context
   float* PIN;
   float* X1;
+  __bf16* X1h;  // bf16 shadow of X1 (fused LSTM products) or null
   // backward
   const float* dPIN;
   const float* dX1;
@@ -597,6 +851,10 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
       for (int g = 0; g < 16; ++g) r += red[g][tid];
       a.PIN[tb * (a.H + a.D) + a.H + nc] = r;
       a.X1[(tb + a.B) * (a.P + a.D + a.H) + a.P + nc] = r;
+      if (a.X1h) {  // TF layout, step block t+1 of Bp rows
+        const int LX = a.P + a.D + a.H, Bp = (a.B + 31) & ~31;
+        a.X1h[(long)(a.t + 1) * Bp * LX + tf_sw(b, a.P + nc, LX)] = (__bf16)r;
+      }
     }
     return;
   }
@@ -1510,7 +1768,7 @@ static std::string tr_bufname(const void* owner, const DevBuf* b) {
   TT2_NM(dG2) TT2_NM(DC1) TT2_NM(DC2) TT2_NM(R1) TT2_NM(R2) TT2_NM(DQ) TT2_NM(DCTX) TT2_NM(DKEYS) TT2_NM(DCUM)
   TT2_NM(dV) TT2_NM(dBA) TT2_NM(dKC) TT2_NM(dBC) TT2_NM(DVAL) TT2_NM(DMEM) TT2_NM(dZ) TT2_NM(dPre) TT2_NM(TBUF)
   TT2_NM(part) TT2_NM(red) TT2_NM(kpart) TT2_NM(TH) TT2_NM(E) TT2_NM(DF) TT2_NM(PQ) TT2_NM(FALL) TT2_NM(ALN)
-  TT2_NM(blasA) TT2_NM(blasB) TT2_NM(hK1) TT2_NM(hK1T) TT2_NM(hK2) TT2_NM(hK2T) TT2_NM(hWq) TT2_NM(hWqT)
+  TT2_NM(blasA) TT2_NM(blasB) TT2_NM(hK1) TT2_NM(hK1T) TT2_NM(hK2) TT2_NM(hK2T) TT2_NM(hWq) TT2_NM(hWqT) TT2_NM(X1h) TT2_NM(X2h) TT2_NM(dGh) TT2_NM(tK1T) TT2_NM(tK2T) TT2_NM(tWq) TT2_NM(tK2) TT2_NM(tK1)
   TT2_NMA(PA, 8) TT2_NMA(PX, 9) TT2_NM(BNM) TT2_NM(BNV) TT2_NM(PPRJ) TT2_NM(dPP) TT2_NM(DYb) TT2_NM(DZb)
   TT2_NM(dPXa) TT2_NM(dPXb) TT2_NM(WFLIP) TT2_NM(PWT) TT2_NM(CLIPM) TT2_NM(pn_part) TT2_NM(fEX) TT2_NMA(fEA, 8)
   TT2_NMA(fEY, 9) TT2_NM(fXP) TT2_NM(fGZ) TT2_NM(fGA) TT2_NM(fCN) TT2_NM(fCS) TT2_NM(fHS) TT2_NM(fENC)
@@ -1630,6 +1888,10 @@ static void tr_alloc(tt2_train_ctx* c) {
     auto h = [](DevBuf& d, long n) { d.alloc(2 * (size_t)std::max<long>(n, 1)); };
     h(c->hK1, LX1 * 4 * H); h(c->hK1T, LX1 * 4 * H); h(c->hK2, 8 * H * H); h(c->hK2T, 8 * H * H);
     h(c->hWq, H * A); h(c->hWqT, H * A);
+    const long Bp = (B + 31) & ~31L;  // TF-layout shadows: row blocks of 32
+    h(c->X1h, (T + 1) * Bp * LX1); h(c->X2h, (T + 1) * Bp * 2 * H); h(c->dGh, 2 * Bp * 4 * H);
+    h(c->tK1T, LX1 * 4 * H); h(c->tK2T, 8 * H * H); h(c->tWq, H * A); h(c->tK2, 8 * H * H);
+    h(c->tK1, ((LX1 + 31) / 32 * 32) * 4 * H);
     // bf16 operand copies of the library GEMMs (tr_gemm_blas): the largest weight gradients over all
     // T·B rows -- LSTM-1 [LX1 x TB]·[TB x 4H], the Postnet convs [K·cin x TB]·[TB x PC]
     const long pcin = c->cfg.postnet ? (long)c->PK * std::max<long>(c->PC, NM) : 0L;
@@ -1816,6 +2078,33 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_gemm((int)TB, P, P, c->P1.as<float>(), P, pvar(c, PRV(2, "kernel")), P, X1, LX1, s, pvar(c, PRV(2, "bias")),
           nullptr, 0, ACT_RELU);
   hipLaunchKernelGGL(k_tr_prenet_mask, dim3(nblk(TB * P)), dim3(256), 0, s, X1, (long)LX1, pm, 1, T, B, P);
+  // fused per-step products (k_tr_fused: product + consumer epilogue in one launch, forward and
+  // backward) on bf16 shadows of their input rows; TT2_TR_FUSED=0 keeps the split-K products +
+  // combines (A/B)
+  const char* fe = std::getenv("TT2_TR_FUSED");
+  const bool fused_env = !(fe && fe[0] == '0');
+  const bool fused = fused_env && g_tr_prec == 2 && B <= 64 && H % 32 == 0 && LX1 % 128 == 0 && A % 128 == 0;
+  __bf16* X1h = fused ? c->X1h.as<__bf16>() : nullptr;
+  __bf16* X2h = fused ? c->X2h.as<__bf16>() : nullptr;
+  const long Bp = (B + 31) & ~31L;  // rows per step of the TF-layout shadows
+  if (fused) {
+    TT2_HIP(hipMemsetAsync(X1h, 0, 2 * (size_t)Bp * LX1, s));      // slot 0: ctx_{-1} = h_{-1} = 0
+    TT2_HIP(hipMemsetAsync(X2h, 0, 2 * (size_t)Bp * 2 * H, s));
+    TT2_HIP(hipMemsetAsync(c->dGh.p, 0, c->dGh.bytes, s));          // padding rows stay 0
+    hipLaunchKernelGGL(k_tr_rows_bf16, dim3(2048), dim3(256), 0, s, X1, (long)LX1, TB, P, B, LX1, X1h);
+    // the fused products' weights in TF layout, column-group order (once per step: the weights change
+    // with every apply)
+    auto tw = [&](const DevBuf& src, int N, int K, int ncg, int mode, DevBuf& dst) {
+      hipLaunchKernelGGL(k_tr_tf_weights, dim3(2048), dim3(256), 0, s, src.as<__bf16>(), N, K, ncg, mode, H,
+                         dst.as<__bf16>());
+    };
+    tw(c->hK1T, 4 * H, LX1, H / 8, TF_FWD, c->tK1T);
+    tw(c->hK2T, 4 * H, 2 * H, H / 8, TF_FWD, c->tK2T);
+    tw(c->hWq, H, A, H / 32, TF_BWD_H, c->tWq);
+    tw(c->hK2, 2 * H, 4 * H, H / 16, TF_BWD_S, c->tK2);
+    tw(c->hK1, LX1, 4 * H, (LX1 + 31) / 32, TF_PLAIN, c->tK1);
+    TT2_HIP(hipGetLastError());
+  }
 
   TrAtt at{};
   at.B = B; at.Tin = Tin; at.T = T; at.A = A; at.F = F; at.KW = KW; at.D = D; at.H = H; at.P = P;
@@ -1826,6 +2115,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   at.va = pvar(c, LAV("attention_variable_projection"));
   at.ba = pvar(c, LAV("attention_bias"));
   at.ALIGN = c->ALIGN.as<float>(); at.CUM = c->CUM.as<float>(); at.PIN = PIN; at.X1 = X1;
+  at.X1h = fused ? c->X1h.as<__bf16>() : nullptr;
   at.dPIN = c->dPIN.as<float>(); at.dX1 = c->dX1.as<float>(); at.DCTX = c->DCTX.as<float>(); at.DQ = c->DQ.as<float>();
   at.DKEYS = c->DKEYS.as<float>(); at.DCUM = c->DCUM.as<float>(); at.dV = c->dV.as<float>(); at.dBA = c->dBA.as<float>();
   at.dKC = c->dKC.as<float>(); at.dBC = c->dBC.as<float>();
@@ -1861,25 +2151,49 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
               0, ACT_RELU);
       hipLaunchKernelGGL(k_tr_prenet_mask, dim3(nblk((long)B * P)), dim3(256), 0, s, X1 + s1 * LX1, (long)LX1,
                          pm + (long)t * 2 * B * P, 1, 1, B, P);
+      if (fused)
+        hipLaunchKernelGGL(k_tr_rows_bf16, dim3(nblk((long)B * P)), dim3(256), 0, s, X1 + s1 * LX1, (long)LX1, (long)B,
+                           P, B, LX1, X1h + t * Bp * LX1);
     }
-    // LSTM-1: raw split-K product, combine + bias + cell + zoneout fused in k_tr_lstm_fwd
-    const int k1 = tr_gemm_raw(B, 4 * H, LX1, X1 + s1 * LX1, LX1, pvar(c, L1V("kernel")), 4 * H, s, &c->hK1T, LX1);
-    TrLstmFwd l1{};
-    l1.G = c->G1.as<float>() + s1 * 4 * H; l1.part = c->kpart.as<float>(); l1.ks = k1; l1.bias = pvar(c, L1V("bias"));
-    l1.c_prev = c->C1.as<float>() + s1 * H; l1.hz_prev = X1 + s1 * LX1 + P + D; l1.ld_hz_prev = LX1;
-    l1.zm = zm; l1.t = t; l1.layer = 0; l1.B = B; l1.H = H; l1.z = z;
-    l1.cn = c->CN1.as<float>() + s1 * H; l1.c_out = c->C1.as<float>() + (s1 + B) * H;
-    l1.h_out = X2 + s1 * 2 * H; l1.ld_h = 2 * H; l1.hz_out = X1 + (s1 + B) * LX1 + P + D; l1.ld_hz = LX1;
-    hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l1);
-    const int k2 = tr_gemm_raw(B, 4 * H, 2 * H, X2 + s1 * 2 * H, 2 * H, pvar(c, L2V("kernel")), 4 * H, s, &c->hK2T,
-                               2 * H);
-    TrLstmFwd l2{};
-    l2.G = c->G2.as<float>() + s1 * 4 * H; l2.part = c->kpart.as<float>(); l2.ks = k2; l2.bias = pvar(c, L2V("bias"));
-    l2.c_prev = c->C2.as<float>() + s1 * H; l2.hz_prev = X2 + s1 * 2 * H + H; l2.ld_hz_prev = 2 * H;
-    l2.zm = zm; l2.t = t; l2.layer = 1; l2.B = B; l2.H = H; l2.z = z;
-    l2.cn = c->CN2.as<float>() + s1 * H; l2.c_out = c->C2.as<float>() + (s1 + B) * H;
-    l2.h_out = PIN + s1 * (H + D); l2.ld_h = H + D; l2.hz_out = X2 + (s1 + B) * 2 * H + H; l2.ld_hz = 2 * H;
-    hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l2);
+    if (fused) {  // LSTM-1 and LSTM-2: product + bias + cell + zoneout in one launch each
+      TrFused f{};
+      f.Ah = X1h + t * Bp * LX1; f.Wt = c->tK1T.as<__bf16>(); f.K = LX1; f.bias = pvar(c, L1V("bias"));
+      f.c_prev = c->C1.as<float>() + s1 * H; f.hz_prev = X1 + s1 * LX1 + P + D; f.ld_hz_prev = LX1;
+      f.zm = zm; f.t = t; f.layer = 0; f.B = B; f.H = H; f.z = z;
+      f.G = c->G1.as<float>() + s1 * 4 * H; f.cn = c->CN1.as<float>() + s1 * H; f.c_out = c->C1.as<float>() + (s1 + B) * H;
+      f.h_out = X2 + s1 * 2 * H; f.ld_h = 2 * H; f.hz_out = X1 + (s1 + B) * LX1 + P + D; f.ld_hz = LX1;
+      f.h_out_h = X2h + t * Bp * 2 * H; f.ld_h_h = 2 * H; f.h_col0 = 0;
+      f.hz_out_h = X1h + (t + 1) * Bp * LX1; f.ld_hz_h = LX1; f.hz_col0 = P + D;
+      hipLaunchKernelGGL(k_tr_fused<TF_FWD>, dim3(2 * H / TLG_U), dim3(TLG_NT), 0, s, f);
+      TrFused f2{};
+      f2.Ah = X2h + t * Bp * 2 * H; f2.Wt = c->tK2T.as<__bf16>(); f2.K = 2 * H; f2.bias = pvar(c, L2V("bias"));
+      f2.c_prev = c->C2.as<float>() + s1 * H; f2.hz_prev = X2 + s1 * 2 * H + H; f2.ld_hz_prev = 2 * H;
+      f2.zm = zm; f2.t = t; f2.layer = 1; f2.B = B; f2.H = H; f2.z = z;
+      f2.G = c->G2.as<float>() + s1 * 4 * H; f2.cn = c->CN2.as<float>() + s1 * H;
+      f2.c_out = c->C2.as<float>() + (s1 + B) * H;
+      f2.h_out = PIN + s1 * (H + D); f2.ld_h = H + D; f2.hz_out = X2 + (s1 + B) * 2 * H + H; f2.ld_hz = 2 * H;
+      f2.hz_out_h = X2h + (t + 1) * Bp * 2 * H; f2.ld_hz_h = 2 * H; f2.hz_col0 = H;
+      hipLaunchKernelGGL(k_tr_fused<TF_FWD>, dim3(2 * H / TLG_U), dim3(TLG_NT), 0, s, f2);
+    } else {
+      // LSTM-1: raw split-K product, combine + bias + cell + zoneout fused in k_tr_lstm_fwd
+      const int k1 = tr_gemm_raw(B, 4 * H, LX1, X1 + s1 * LX1, LX1, pvar(c, L1V("kernel")), 4 * H, s, &c->hK1T, LX1);
+      TrLstmFwd l1{};
+      l1.G = c->G1.as<float>() + s1 * 4 * H; l1.part = c->kpart.as<float>(); l1.ks = k1; l1.bias = pvar(c, L1V("bias"));
+      l1.c_prev = c->C1.as<float>() + s1 * H; l1.hz_prev = X1 + s1 * LX1 + P + D; l1.ld_hz_prev = LX1;
+      l1.zm = zm; l1.t = t; l1.layer = 0; l1.B = B; l1.H = H; l1.z = z;
+      l1.cn = c->CN1.as<float>() + s1 * H; l1.c_out = c->C1.as<float>() + (s1 + B) * H;
+      l1.h_out = X2 + s1 * 2 * H; l1.ld_h = 2 * H; l1.hz_out = X1 + (s1 + B) * LX1 + P + D; l1.ld_hz = LX1;
+      hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l1);
+      const int k2 = tr_gemm_raw(B, 4 * H, 2 * H, X2 + s1 * 2 * H, 2 * H, pvar(c, L2V("kernel")), 4 * H, s, &c->hK2T,
+                                 2 * H);
+      TrLstmFwd l2{};
+      l2.G = c->G2.as<float>() + s1 * 4 * H; l2.part = c->kpart.as<float>(); l2.ks = k2; l2.bias = pvar(c, L2V("bias"));
+      l2.c_prev = c->C2.as<float>() + s1 * H; l2.hz_prev = X2 + s1 * 2 * H + H; l2.ld_hz_prev = 2 * H;
+      l2.zm = zm; l2.t = t; l2.layer = 1; l2.B = B; l2.H = H; l2.z = z;
+      l2.cn = c->CN2.as<float>() + s1 * H; l2.c_out = c->C2.as<float>() + (s1 + B) * H;
+      l2.h_out = PIN + s1 * (H + D); l2.ld_h = H + D; l2.hz_out = X2 + (s1 + B) * 2 * H + H; l2.ld_hz = 2 * H;
+      hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l2);
+    }
     at.t = t;
     if (A <= 128 && tr_e2) {  // query as raw split-K partials, combined inside the energy kernel
       at.qks = tr_gemm_raw(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A, s,
@@ -1924,29 +2238,54 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     if (A <= 128 && D <= 1024 && D % 4 == 0 && tr_e2) hipLaunchKernelGGL(k_tr_att_energy_bwd2, att_grid, dim3(TR_E2T), 0, s, at);
     else hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(TR_AT), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
-    // LSTM-2 backward: d h2 = DQ·Wq^T (raw split-K) + d PIN[t][:, :H], combined in the cell kernel
-    const int kq = tr_gemm_raw(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, s, &c->hWq, A);
-    TrLstmBwd b2{};
-    b2.dh_ext = dPIN + s1 * (H + D); b2.ld_dh = H + D; b2.part = c->kpart.as<float>(); b2.ks = kq; b2.pN = H;
-    b2.dhz = dX2 + (s1 + B) * 2 * H + H; b2.ld_dhz = 2 * H; b2.DC = c->DC2.as<float>();
-    b2.G = c->G2.as<float>() + s1 * 4 * H; b2.cn = c->CN2.as<float>() + s1 * H; b2.c_prev = c->C2.as<float>() + s1 * H;
-    b2.zm = zm; b2.t = t; b2.layer = 1; b2.B = B; b2.H = H; b2.z = z;
-    b2.dG = c->dG2.as<float>() + s1 * 4 * H; b2.R = c->R2.as<float>(); b2.ldr = 2 * H; b2.off_r = H;
-    hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b2);
-    // dX2 = dG2·K2^T + R2 (raw split-K): columns [0,H) are d h1_new (consumed by the LSTM-1
-    // backward), columns [H,2H) = d hz2_{t-1} are written to dX2[t] by the same kernel
-    const int kx = tr_gemm_raw(B, 2 * H, 4 * H, c->dG2.as<float>() + s1 * 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, s,
-                               &c->hK2, 4 * H);
-    TrLstmBwd b1{};
-    b1.dh_ext = nullptr; b1.ld_dh = 0; b1.part = c->kpart.as<float>(); b1.ks = kx; b1.pN = 2 * H;
-    b1.side = dX2 + s1 * 2 * H + H; b1.ld_side = 2 * H; b1.side_res = c->R2.as<float>(); b1.ld_side_res = 2 * H;
-    b1.dhz = dX1 + (s1 + B) * LX1 + P + D; b1.ld_dhz = LX1; b1.DC = c->DC1.as<float>();
-    b1.G = c->G1.as<float>() + s1 * 4 * H; b1.cn = c->CN1.as<float>() + s1 * H; b1.c_prev = c->C1.as<float>() + s1 * H;
-    b1.zm = zm; b1.t = t; b1.layer = 0; b1.B = B; b1.H = H; b1.z = z;
-    b1.dG = c->dG1.as<float>() + s1 * 4 * H; b1.R = c->R1.as<float>(); b1.ldr = LX1; b1.off_r = P + D;
-    hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b1);
-    tr_gemm(B, LX1, 4 * H, c->dG1.as<float>() + s1 * 4 * H, 4 * H, c->K1T.as<float>(), LX1, dX1 + s1 * LX1, LX1, s,
-            nullptr, c->R1.as<float>(), LX1, ACT_NONE, &c->hK1, 4 * H);
+    if (fused) {  // the three per-step products of the LSTM backward, each fused with its consumer
+      __bf16* dGh = c->dGh.as<__bf16>();
+      TrFused f{};  // LSTM-2: d h2 = DQ·Wq^T + d PIN[t][:, :H] -> cell backward -> dG2
+      f.Af = c->DQ.as<float>() + s1 * A; f.lda = A; f.Wt = c->tWq.as<__bf16>(); f.K = A; f.B = B; f.H = H;
+      f.t = t; f.layer = 1; f.z = z; f.zm = zm;
+      f.G = c->G2.as<float>() + s1 * 4 * H; f.cn = c->CN2.as<float>() + s1 * H; f.c_prev = c->C2.as<float>() + s1 * H;
+      f.dh_ext = dPIN + s1 * (H + D); f.ld_dh = H + D;
+      f.dhz = dX2 + (s1 + B) * 2 * H + H; f.ld_dhz = 2 * H; f.DC = c->DC2.as<float>();
+      f.dG = c->dG2.as<float>() + s1 * 4 * H; f.dGh = dGh; f.R = c->R2.as<float>(); f.ldr = 2 * H; f.off_r = H;
+      hipLaunchKernelGGL(k_tr_fused<TF_BWD_H>, dim3(2 * H / 32), dim3(TLG_NT), 0, s, f);
+      TrFused f1{};  // LSTM-1: [d h1 | d hz2_{t-1}] = dG2·K2^T (+ R2) -> cell backward -> dG1
+      f1.Ah = dGh; f1.Wt = c->tK2.as<__bf16>(); f1.K = 4 * H; f1.B = B; f1.H = H;
+      f1.t = t; f1.layer = 0; f1.z = z; f1.zm = zm;
+      f1.G = c->G1.as<float>() + s1 * 4 * H; f1.cn = c->CN1.as<float>() + s1 * H; f1.c_prev = c->C1.as<float>() + s1 * H;
+      f1.side = dX2 + s1 * 2 * H + H; f1.ld_side = 2 * H; f1.side_res = c->R2.as<float>(); f1.ld_side_res = 2 * H;
+      f1.dhz = dX1 + (s1 + B) * LX1 + P + D; f1.ld_dhz = LX1; f1.DC = c->DC1.as<float>();
+      f1.dG = c->dG1.as<float>() + s1 * 4 * H; f1.dGh = dGh + Bp * 4 * H; f1.R = c->R1.as<float>(); f1.ldr = LX1;
+      f1.off_r = P + D;
+      hipLaunchKernelGGL(k_tr_fused<TF_BWD_S>, dim3(2 * H / 16), dim3(TLG_NT), 0, s, f1);
+      TrFused f3{};  // d X1[t] = dG1·K1^T + R1
+      f3.Ah = dGh + Bp * 4 * H; f3.Wt = c->tK1.as<__bf16>(); f3.K = 4 * H; f3.B = B; f3.H = H;
+      f3.N = LX1; f3.C = dX1 + s1 * LX1; f3.ldc = LX1; f3.residual = c->R1.as<float>(); f3.ldres = LX1;
+      hipLaunchKernelGGL(k_tr_fused<TF_PLAIN>, dim3(2 * ((LX1 + 31) / 32)), dim3(TLG_NT), 0, s, f3);
+    } else {
+      // LSTM-2 backward: d h2 = DQ·Wq^T (raw split-K) + d PIN[t][:, :H], combined in the cell kernel
+      const int kq = tr_gemm_raw(B, H, A, c->DQ.as<float>() + s1 * A, A, c->WqT.as<float>(), H, s, &c->hWq, A);
+      TrLstmBwd b2{};
+      b2.dh_ext = dPIN + s1 * (H + D); b2.ld_dh = H + D; b2.part = c->kpart.as<float>(); b2.ks = kq; b2.pN = H;
+      b2.dhz = dX2 + (s1 + B) * 2 * H + H; b2.ld_dhz = 2 * H; b2.DC = c->DC2.as<float>();
+      b2.G = c->G2.as<float>() + s1 * 4 * H; b2.cn = c->CN2.as<float>() + s1 * H; b2.c_prev = c->C2.as<float>() + s1 * H;
+      b2.zm = zm; b2.t = t; b2.layer = 1; b2.B = B; b2.H = H; b2.z = z;
+      b2.dG = c->dG2.as<float>() + s1 * 4 * H; b2.R = c->R2.as<float>(); b2.ldr = 2 * H; b2.off_r = H;
+      hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b2);
+      // dX2 = dG2·K2^T + R2 (raw split-K): columns [0,H) are d h1_new (consumed by the LSTM-1
+      // backward), columns [H,2H) = d hz2_{t-1} are written to dX2[t] by the same kernel
+      const int kx = tr_gemm_raw(B, 2 * H, 4 * H, c->dG2.as<float>() + s1 * 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, s,
+                                 &c->hK2, 4 * H);
+      TrLstmBwd b1{};
+      b1.dh_ext = nullptr; b1.ld_dh = 0; b1.part = c->kpart.as<float>(); b1.ks = kx; b1.pN = 2 * H;
+      b1.side = dX2 + s1 * 2 * H + H; b1.ld_side = 2 * H; b1.side_res = c->R2.as<float>(); b1.ld_side_res = 2 * H;
+      b1.dhz = dX1 + (s1 + B) * LX1 + P + D; b1.ld_dhz = LX1; b1.DC = c->DC1.as<float>();
+      b1.G = c->G1.as<float>() + s1 * 4 * H; b1.cn = c->CN1.as<float>() + s1 * H; b1.c_prev = c->C1.as<float>() + s1 * H;
+      b1.zm = zm; b1.t = t; b1.layer = 0; b1.B = B; b1.H = H; b1.z = z;
+      b1.dG = c->dG1.as<float>() + s1 * 4 * H; b1.R = c->R1.as<float>(); b1.ldr = LX1; b1.off_r = P + D;
+      hipLaunchKernelGGL(k_tr_lstm_bwd, dim3(bh), dim3(256), 0, s, b1);
+      tr_gemm(B, LX1, 4 * H, c->dG1.as<float>() + s1 * 4 * H, 4 * H, c->K1T.as<float>(), LX1, dX1 + s1 * LX1, LX1, s,
+              nullptr, c->R1.as<float>(), LX1, ACT_NONE, &c->hK1, 4 * H);
+    }
     if (free_run && t > 0 && !c->feed[t]) {
       // step t consumed frame t-1: d prenet input -> d frame t-1 (dFR, for the projection weight
       // gradients after the loop) and through the frame projection into d [h2 | ctx] of step t-1
@@ -2104,6 +2443,7 @@ static void tr_front_build_vars(tt2_train_ctx* c, const std::function<void(const
     addr(rs + "rnn/gru_cell/candidate/bias", {RD});
     addr(rs + "dense/kernel", {RD, 128});
     addr(rs + "dense/bias", {128});
+    if (!f.use_gst) continue;  // hp.use_gst = False: no style tokens / style attention (tacotron.py:284-291)
     addr(vn(r == 0 ? "style_tokens_emt" : "style_tokens_spk"), {f.num_gst, tokd});
     const std::string m = fe_mh_scope(r);
     addr(m + "conv1d/kernel", {1, 128, A});
@@ -2322,7 +2662,13 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
     }
     tr_gemm(B, 128, RD, c->fHG[r].as<float>() + (long)T2 * B * RD, RD, pvar(c, rs + "dense/kernel"), 128,
             c->fREF[r].as<float>(), 128, s, pvar(c, rs + "dense/bias"), nullptr, 0, ACT_TANH);
-    fe_gst_fwd(fe_gst_args(c, r, B), s);
+    if (f.use_gst) {
+      fe_gst_fwd(fe_gst_args(c, r, B), s);
+    } else {  // the reference embedding is the style embedding (tacotron.py:284-291)
+      const int SW = c->D - 2 * f.encoder_lstm_units;
+      hipLaunchKernelGGL(k_tr_rows_copy, dim3(nblk((long)B * 128)), dim3(256), 0, s, c->fREF[r].as<float>(), 128L,
+                         (long)B, 128, c->fSTY.as<float>() + r * 128, (long)SW, (const float*)nullptr, 0L);
+    }
   }
   fe_memory(c->fENC.as<float>(), c->fSTY.as<float>(), B, T, 2 * U, c->D - 2 * U, c->fMEM.as<float>(), s);
   c->f_ran = true;
@@ -2476,6 +2822,12 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
   if (style_on) tr_style_losses(c, s);
   for (int r = 0; r < c->f_nref; ++r) {
     const std::string rs = fe_ref_scope(r), m = fe_mh_scope(r);
+    if (!f.use_gst) {  // d ref = d style slice (+ style-loss terms)
+      hipLaunchKernelGGL(k_tr_rows_copy, dim3(nblk((long)B * 128)), dim3(256), 0, s, c->fDSTY.as<float>() + r * 128,
+                         (long)SW, (long)B, 128, c->fdREF.as<float>(), 128L,
+                         style_on ? (const float*)(c->sXREF.as<float>() + (long)r * B * 128) : (const float*)nullptr,
+                         128L);
+    } else {
     const FeGst ga = fe_gst_args(c, r, B);
     fe_gst_bwd(ga, s);
     const int ntok = ga.ntok, tokd = ga.tokd, A = ga.A, dh = A / ga.heads;
@@ -2495,6 +2847,7 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
     tr_transpose(pvar(c, m + "conv1d/kernel"), 128, A, A, WT, 128, s);
     tr_gemm(B, 128, A, ga.dq, A, WT, 128, c->fdREF.as<float>(), 128, s, nullptr,
             style_on ? c->sXREF.as<float>() + (long)r * B * 128 : nullptr, 128);  // + style-loss terms
+    }
     // dense tanh (modules.py:63)
     fe_tanh_bwd(c->fdREF.as<float>(), c->fREF[r].as<float>(), (long)B * 128, c->fDZD.as<float>(), s);
     const int T2 = c->f_T2;
@@ -2733,6 +3086,7 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   c->n_emt = 0;
   c->n_spk = 0;
   c->orthog_weight = 0.f;
+  c->use_gst = 1;
   c->num_gst = 10;
   c->num_heads = 4;
   c->style_embed_depth = 256;
@@ -2857,8 +3211,10 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
         for (int i = 0; i < 6; ++i) W = (W + 1) / 2;
         c->f_gin = W * cfg->reference_filters[5];
         const int tokd = cfg->num_heads > 0 ? cfg->style_embed_depth / cfg->num_heads : 0;
-        TT2_CHECK(cfg->memory_dim == 2 * cfg->encoder_lstm_units + c->f_nref * cfg->num_heads * tokd, TT2_ERR_INVALID_ARG,
-                  "memory_dim must be 2*encoder_lstm_units + (emt_only ? 1 : 2) * style_embed_depth");
+        const int sw = cfg->use_gst ? cfg->num_heads * tokd : 128;  // style embedding width
+        TT2_CHECK(cfg->memory_dim == 2 * cfg->encoder_lstm_units + c->f_nref * sw, TT2_ERR_INVALID_ARG,
+                  cfg->use_gst ? "memory_dim must be 2*encoder_lstm_units + (emt_only ? 1 : 2) * style_embed_depth"
+                               : "use_gst = 0: memory_dim must be 2*encoder_lstm_units + (emt_only ? 1 : 2) * 128");
         TT2_CHECK(cfg->enc_conv_layers >= 1 && cfg->enc_conv_layers <= 8 && cfg->enc_conv_channels <= 512 &&
                       cfg->n_symbols >= 1 && cfg->embedding_dim >= 1 && cfg->max_T_ref >= 1,
                   TT2_ERR_INVALID_ARG, "bad front-end shape");

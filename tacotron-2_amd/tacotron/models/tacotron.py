@@ -267,9 +267,10 @@ class Tacotron():
         hp = self._hparams
         if mel_targets is None or stop_token_targets is None:
             raise ValueError("training needs mel_targets and stop_token_targets")
-        if style != "gst" or not hp.use_gst:
-            raise NotImplementedError("training builds the GST style path (adain / embeddings-only "
-                                      "front ends are synthesis-only on this build)")
+        if style != "gst":
+            raise NotImplementedError("training builds the GST and hp.use_gst = False style paths (the "
+                                      "adain / pretrained_emb_disc_all front ends are synthesis-only on "
+                                      "this build)")
         # use_emt_disc / use_spk_disc / use_intercross are stored and never read by the reference
         # graph (tacotron.py:74-76): accepted and ignored alike
         if hp.outputs_per_step != 1:

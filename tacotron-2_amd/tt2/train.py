@@ -106,8 +106,6 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
     cfg.frontend = 1 if frontend else 0
     if frontend:
         from tacotron.utils.symbols import symbols
-        if not hp.use_gst:
-            raise NotImplementedError("use_gst=False front end is not built")
         cfg.n_symbols = len(symbols)
         cfg.embedding_dim = hp.embedding_dim
         cfg.enc_conv_layers = hp.enc_conv_num_layers
@@ -115,6 +113,8 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
         cfg.enc_conv_channels = hp.enc_conv_channels
         cfg.encoder_lstm_units = hp.encoder_lstm_units
         cfg.emt_only = 1 if emt_only else 0
+        # hp.use_gst = False: the reference embeddings are the style embeddings (tacotron.py:284-291)
+        cfg.use_gst = 1 if hp.use_gst else 0
         cfg.num_gst = hp.num_gst
         cfg.num_heads = hp.num_heads
         cfg.style_embed_depth = hp.style_embed_depth

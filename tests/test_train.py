@@ -627,3 +627,94 @@ def test_gpu_train_bf16_library_gemms_match_kernels():
     for n in names:
         frob = float(np.linalg.norm(ga[n] - gb[n]) / max(np.linalg.norm(gb[n]), 1e-30))
         assert frob < 1e-4, (n, frob)
+
+
+@pytest.mark.gpu
+def test_gpu_train_fused_lstm_matches_split_k_path():
+    """k_tr_fused (each per-step LSTM product with its consumer's epilogue in one launch, forward
+    and backward, on bf16 row shadows) against the split-K products + combines (TT2_TR_FUSED=0) on
+    the same bf16 step at fork widths: same operand rounding rule, different fp32 summation order.
+    The order moves activations by ~1e-7, which occasionally flips the bf16 rounding of a later
+    operand (2^-8 relative), so the gradients agree to bf16-rounding level, not bit for bit: losses
+    within 1e-5 relative, every gradient within 1e-2 (Frobenius, relative; measured <= 3e-3 for the
+    prenet kernels, the most sensitive; a wrong column or row would be O(1))."""
+    import os
+    from tt2.hparams import hparams
+    from tt2.train import TacotronTrainer
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    B, T_in, T_out = 16, 40, 24
+    W = init_tacotron_weights(hp, seed=5339)
+    mem, lens, tg, st = train_batch(B, T_in, T_out, memory_width(hp), seed=3)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=3)
+    zm = zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=3)
+    res = {}
+    for mode in ("1", "0"):
+        old = os.environ.get("TT2_TR_FUSED")
+        os.environ["TT2_TR_FUSED"] = mode
+        try:
+            tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", postnet=False)
+            try:
+                tr.forward_backward(mem, lens, tg, st, pm, zm)
+                L = tr.losses()
+                g = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in TRN.train_var_names()}
+            finally:
+                tr.close()
+        finally:
+            if old is None:
+                del os.environ["TT2_TR_FUSED"]
+            else:
+                os.environ["TT2_TR_FUSED"] = old
+        res[mode] = (L, g)
+    (La, ga), (Lb, gb) = res["1"], res["0"]
+    for k in ("before", "stop_token"):
+        assert abs(La[k] - Lb[k]) < 1e-5 * abs(Lb[k]), (k, La[k], Lb[k])
+    for n in ga:
+        rel = float(np.linalg.norm(ga[n] - gb[n]) / max(np.linalg.norm(gb[n]), 1e-30))
+        print("  {:90s} rel {:.3e}".format(n, rel))
+        assert rel < 1e-2, (n, rel)
+
+
+@pytest.mark.gpu
+def test_gpu_train_frontend_without_gst_matches_oracle():
+    """hp.use_gst = False (tacotron.py:284-291): the 128-wide reference embeddings are the style
+    embeddings (no style tokens, no style attention; D_mem = 2U + 2·128).  The whole step from ids
+    + reference mels against the torch float64 oracle: losses and every gradient within 2e-4."""
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    hp.override_from_dict(dict(use_gst=False))
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, masks=True)
+    assert memory_width(hp) == 2 * hp.encoder_lstm_units + 256
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1])
+    try:
+        tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+        L = tr.losses()
+        # the default graph's orthogonality loss on the two reference embeddings (hp default on)
+        style = dict(emt_labels=None, spk_labels=None, n_emt=0, n_spk=0, orthog_weight=0.02)
+        (b, s_, r, a, le, ls, lo), g, _ = TRN.train_grads_frontend(
+            W, ids, lens, re, rs, tg, st, pm, zm, em, ezm, hp.tacotron_reg_weight, postnet_masks=pnm,
+            style=style, use_gst=False)
+        assert abs(L["before"] - b) < 1e-4 * b and abs(L["after"] - a) < 1e-4 * a
+        assert abs(L["style_emb_orthog_loss"] - lo) < 1e-4 * lo and lo > 0
+        names = TRN.frontend_var_names(use_gst=False) + TRN.train_var_names() + TRN.postnet_var_names()
+        assert not any("style_tokens" in n or "Multihead" in n for n in names)
+        for n in names:
+            got = tr.get(n, 1, np.asarray(W[n]).shape)
+            if np.abs(g[n]).max() < 1e-12:   # a conv bias feeding batch-statistics BN: exactly 0
+                assert np.abs(got).max() < 1e-6, (n, np.abs(got).max())
+                continue
+            assert _rel(got, g[n]) < 2e-4, (n, _rel(got, g[n]))
+    finally:
+        tr.close()
+
+
+def test_train_config_use_gst_without_gpu():
+    """train_config carries hp.use_gst and the matching memory width (tacotron.py:284-291)."""
+    from tt2.train import train_config
+    hp = small_hparams()
+    cfg = train_config(hp, 4, 9, 6, frontend=True)
+    assert cfg.use_gst == 1 and cfg.memory_dim == 2 * hp.encoder_lstm_units + 2 * hp.style_embed_depth
+    hp.override_from_dict(dict(use_gst=False))
+    cfg = train_config(hp, 4, 9, 6, frontend=True)
+    assert cfg.use_gst == 0 and cfg.memory_dim == 2 * hp.encoder_lstm_units + 256
