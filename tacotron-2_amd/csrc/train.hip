@@ -425,25 +425,56 @@ struct TrFused {
   long ldres;
 };
 
-// LSTM cell backward of one (row, unit) (k_tr_lstm_bwd): dext = d h_new from outside the cell
-__device__ __forceinline__ void tf_cell_bwd(const TrFused& a, int b, int n, float dext) {
+// Epilogue operands of one (row, unit), loaded BEFORE the product so their round trip overlaps the
+// operand stream instead of following the reduction barrier.
+struct TfCellIn {
+  float g0, g1, g2, g3;  // fwd: bias of the 4 gates; bwd: the activated gates
+  float cp, hp;          // c_{t-1}; fwd: zoned h_{t-1}
+  float cn, dhz, dcz;    // bwd: c_new, d zoned h_t, d zoned c_t
+  float ext, sres;       // bwd: d h_new from outside the product; TF_BWD_S: side residual
+  float kc, kh;          // zoneout keep (mask) or 1 - z
+};
+template <int MODE>
+__device__ __forceinline__ TfCellIn tf_cell_load(const TrFused& a, int b, int n) {
+  TfCellIn v{};
   const long i = (long)b * a.H + n;
-  const float* g = a.G + (long)b * 4 * a.H;
-  const float si = g[n], tj = g[a.H + n], sf = g[2 * a.H + n], so = g[3 * a.H + n];
-  float kc, kh;
   if (a.zm) {
     const long base = (((long)a.t * 4 + 2 * a.layer) * a.B + b) * a.H + n;
-    kc = (float)a.zm[base];
-    kh = (float)a.zm[base + (long)a.B * a.H];
+    v.kc = (float)a.zm[base];
+    v.kh = (float)a.zm[base + (long)a.B * a.H];
   } else {
-    kc = kh = 1.f - a.z;
+    v.kc = v.kh = 1.f - a.z;
   }
-  const float dhz = a.dhz[(long)b * a.ld_dhz + n];
-  const float dcz = a.DC[i];
-  const float dhn = dext + kh * dhz;
-  const float tc = tanhf(a.cn[i]);
-  const float dcn = kc * dcz + dhn * so * (1.f - tc * tc);
-  const float dso = dhn * tc, dsf = dcn * a.c_prev[i], dsi = dcn * tj, dtj = dcn * si;
+  v.cp = a.c_prev[i];
+  if constexpr (MODE == TF_FWD) {
+    v.g0 = a.bias[n];
+    v.g1 = a.bias[a.H + n];
+    v.g2 = a.bias[2 * a.H + n];
+    v.g3 = a.bias[3 * a.H + n];
+    v.hp = a.hz_prev[(long)b * a.ld_hz_prev + n];
+  } else {
+    const float* g = a.G + (long)b * 4 * a.H;
+    v.g0 = g[n];
+    v.g1 = g[a.H + n];
+    v.g2 = g[2 * a.H + n];
+    v.g3 = g[3 * a.H + n];
+    v.cn = a.cn[i];
+    v.dhz = a.dhz[(long)b * a.ld_dhz + n];
+    v.dcz = a.DC[i];
+    v.ext = a.dh_ext ? a.dh_ext[(long)b * a.ld_dh + n] : 0.f;
+    if constexpr (MODE == TF_BWD_S) v.sres = a.side_res[(long)b * a.ld_side_res + a.H + n];
+  }
+  return v;
+}
+
+// LSTM cell backward of one (row, unit) (k_tr_lstm_bwd): dext = d h_new from outside the cell
+__device__ __forceinline__ void tf_cell_bwd(const TrFused& a, int b, int n, float dext, const TfCellIn& v) {
+  const long i = (long)b * a.H + n;
+  const float si = v.g0, tj = v.g1, sf = v.g2, so = v.g3;
+  const float dhn = dext + v.kh * v.dhz;
+  const float tc = tanhf(v.cn);
+  const float dcn = v.kc * v.dcz + dhn * so * (1.f - tc * tc);
+  const float dso = dhn * tc, dsf = dcn * v.cp, dsi = dcn * tj, dtj = dcn * si;
   const float d0 = dsi * si * (1.f - si), d1 = dtj * (1.f - tj * tj), d2 = dsf * sf * (1.f - sf), d3 = dso * so * (1.f - so);
   float* dg = a.dG + (long)b * 4 * a.H;
   dg[n] = d0;
@@ -457,8 +488,8 @@ __device__ __forceinline__ void tf_cell_bwd(const TrFused& a, int b, int n, floa
     a.dGh[tf_sw(b, 2 * a.H + n, K4)] = (__bf16)d2;
     a.dGh[tf_sw(b, 3 * a.H + n, K4)] = (__bf16)d3;
   }
-  a.DC[i] = (1.f - kc) * dcz + dcn * sf;
-  a.R[(long)b * a.ldr + a.off_r + n] = (1.f - kh) * dhz;
+  a.DC[i] = (1.f - v.kc) * v.dcz + dcn * sf;
+  a.R[(long)b * a.ldr + a.off_r + n] = (1.f - v.kh) * v.dhz;
 }
 
 template <int MODE>
@@ -470,6 +501,29 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
   const int cg = (ncg & 7) == 0 ? (bid & 7) + 8 * (bid >> 4) : bid >> 1;
   const int rh = (ncg & 7) == 0 ? (bid >> 3) & 1 : bid & 1;
   const int r0 = 32 * rh;
+  // this thread's epilogue element(s): FWD 32 rows x 8 units (threads < 256), BWD_S 32 x 16, BWD_H
+  // 32 x 32 and PLAIN 32 x 32 columns (two per thread)
+  constexpr int NE = (MODE == TF_BWD_H || MODE == TF_PLAIN) ? 2 : 1;
+  constexpr int UPR = MODE == TF_FWD ? 8 : MODE == TF_BWD_S ? 16 : 32;  // epilogue columns per row
+  int eb[NE], en[NE], erl[NE], ekk[NE];
+  bool eok[NE];
+  TfCellIn ev[NE];
+  float eres[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int pidx = tid + TLG_NT * e;
+    erl[e] = pidx / UPR;
+    ekk[e] = pidx % UPR;
+    eb[e] = r0 + erl[e];
+    en[e] = cg * UPR + ekk[e];
+    eok[e] = erl[e] < 32 && eb[e] < a.B && (MODE != TF_PLAIN || en[e] < a.N);
+    eres[e] = 0.f;
+    if constexpr (MODE == TF_PLAIN) {
+      if (eok[e] && a.residual) eres[e] = a.residual[(long)eb[e] * a.ldres + en[e]];
+    } else {
+      if (eok[e]) ev[e] = tf_cell_load<MODE>(a, eb[e], en[e]);
+    }
+  }
   const int kw = a.K >> 3, k0 = w * kw, ks = kw >> 4;  // host: K % 128 == 0
   const int c = lane & 31, kh = 8 * (lane >> 5);
   const bool rok = r0 + c < a.B;
@@ -510,58 +564,44 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
     for (int ww = 0; ww < 8; ++ww) v += red[ww][rl][cc];
     return v;
   };
-  if constexpr (MODE == TF_FWD) {
-    if (tid >= 256) return;
-    const int rl = tid >> 3, b = r0 + rl, kk = tid & 7, n = cg * 8 + kk;
-    if (b >= a.B) return;
-    float pre[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) pre[q] = a.bias[q * a.H + n] + sum8(rl, q * 8 + kk);
-    const float si = sigm_acc(pre[0]), tj = tanhf(pre[1]), sf = sigm_acc(pre[2] + 1.0f), so = sigm_acc(pre[3]);
-    float* g = const_cast<float*>(a.G) + (long)b * 4 * a.H;
-    g[n] = si;
-    g[a.H + n] = tj;
-    g[2 * a.H + n] = sf;
-    g[3 * a.H + n] = so;
-    const long i = (long)b * a.H + n;
-    const float cp = a.c_prev[i];
-    const float hp = a.hz_prev[(long)b * a.ld_hz_prev + n];
-    const float cnew = sf * cp + si * tj;
-    const float hnew = so * tanhf(cnew);
-    float cz, hz;
-    if (a.zm) {
-      const long base = (((long)a.t * 4 + 2 * a.layer) * a.B + b) * a.H + n;
-      const float mc = (float)a.zm[base], mh = (float)a.zm[base + (long)a.B * a.H];
-      cz = cp + mc * (cnew - cp);
-      hz = hp + mh * (hnew - hp);
+  for (int e = 0; e < NE; ++e) {
+    if (!eok[e]) continue;
+    const int rl = erl[e], kk = ekk[e], b = eb[e], n = en[e];
+    if constexpr (MODE == TF_FWD) {
+      const TfCellIn& v = ev[e];
+      const float pre0 = v.g0 + sum8(rl, kk), pre1 = v.g1 + sum8(rl, 8 + kk);
+      const float pre2 = v.g2 + sum8(rl, 16 + kk), pre3 = v.g3 + sum8(rl, 24 + kk);
+      const float si = sigm_acc(pre0), tj = tanhf(pre1), sf = sigm_acc(pre2 + 1.0f), so = sigm_acc(pre3);
+      float* g = const_cast<float*>(a.G) + (long)b * 4 * a.H;
+      g[n] = si;
+      g[a.H + n] = tj;
+      g[2 * a.H + n] = sf;
+      g[3 * a.H + n] = so;
+      const long i = (long)b * a.H + n;
+      const float cnew = sf * v.cp + si * tj;
+      const float hnew = so * tanhf(cnew);
+      float cz, hz;
+      if (a.zm) {
+        cz = v.cp + v.kc * (cnew - v.cp);
+        hz = v.hp + v.kh * (hnew - v.hp);
+      } else {
+        cz = (1.f - a.z) * cnew + a.z * v.cp;
+        hz = (1.f - a.z) * hnew + a.z * v.hp;
+      }
+      a.cn[i] = cnew;
+      a.c_out[i] = cz;
+      a.h_out[(long)b * a.ld_h + n] = hnew;
+      a.hz_out[(long)b * a.ld_hz + n] = hz;
+      if (a.h_out_h) a.h_out_h[tf_sw(b, a.h_col0 + n, (int)a.ld_h_h)] = (__bf16)hnew;
+      if (a.hz_out_h) a.hz_out_h[tf_sw(b, a.hz_col0 + n, (int)a.ld_hz_h)] = (__bf16)hz;
+    } else if constexpr (MODE == TF_BWD_H) {
+      tf_cell_bwd(a, b, n, sum8(rl, kk) + ev[e].ext, ev[e]);
+    } else if constexpr (MODE == TF_BWD_S) {
+      a.side[(long)b * a.ld_side + n] = sum8(rl, 16 + kk) + ev[e].sres;
+      tf_cell_bwd(a, b, n, sum8(rl, kk), ev[e]);
     } else {
-      cz = (1.f - a.z) * cnew + a.z * cp;
-      hz = (1.f - a.z) * hnew + a.z * hp;
-    }
-    a.cn[i] = cnew;
-    a.c_out[i] = cz;
-    a.h_out[(long)b * a.ld_h + n] = hnew;
-    a.hz_out[(long)b * a.ld_hz + n] = hz;
-    if (a.h_out_h) a.h_out_h[tf_sw(b, a.h_col0 + n, (int)a.ld_h_h)] = (__bf16)hnew;
-    if (a.hz_out_h) a.hz_out_h[tf_sw(b, a.hz_col0 + n, (int)a.ld_hz_h)] = (__bf16)hz;
-  } else if constexpr (MODE == TF_BWD_H) {  // 32 rows x 32 units, two per thread
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int pidx = tid + TLG_NT * e, rl = pidx >> 5, kk = pidx & 31, b = r0 + rl, n = cg * 32 + kk;
-      if (b < a.B) tf_cell_bwd(a, b, n, sum8(rl, kk) + (a.dh_ext ? a.dh_ext[(long)b * a.ld_dh + n] : 0.f));
-    }
-  } else if constexpr (MODE == TF_BWD_S) {  // 32 rows x 16 units
-    const int rl = tid >> 4, kk = tid & 15, b = r0 + rl, n = cg * 16 + kk;
-    if (b >= a.B) return;
-    a.side[(long)b * a.ld_side + n] = sum8(rl, 16 + kk) + a.side_res[(long)b * a.ld_side_res + a.H + n];
-    tf_cell_bwd(a, b, n, sum8(rl, kk));
-  } else {  // TF_PLAIN: 32 rows x 32 columns, two per thread
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int pidx = tid + TLG_NT * e, rl = pidx >> 5, kk = pidx & 31, b = r0 + rl;
-      const long n = (long)cg * 32 + kk;
-      if (b < a.B && n < a.N)
-        a.C[(long)b * a.ldc + n] = sum8(rl, kk) + (a.residual ? a.residual[(long)b * a.ldres + n] : 0.f);
+      a.C[(long)b * a.ldc + n] = sum8(rl, kk) + eres[e];
     }
   }
 }
@@ -791,6 +831,178 @@ __global__ __launch_bounds__(TR_E2T) void k_tr_att_energy2(TrAtt a) {
 // Masked softmax (attention.py:218, TF _maybe_mask_score) recomputed by every block of the row,
 // cumulative alignments (:222-225) by block 0, then context_t = align_t · values (:27)
 // -> PIN[t][b][H:], X1[t+1][b][P:P+D].
+// ---- the whole attention forward of one decoder step and row in ONE work-group (round 4) ------
+// k_tr_att_energy2 + k_tr_ctx of one row fused (attention.py:170-227 + the context, Architecture_
+// wrappers.py:235-240): location features of cum_{t-1} (F <= 32 channels, W_loc in LDS), energies over
+// every encoder position with the query's split-K partials summed in, the masked softmax, cum /
+// alignment outputs and the context -- the energies never leave the CU and the context launch with its
+// own softmax is gone.  1024 threads: 8 position groups x 128 attention dims for the energies, 2 x 512
+// channels for the context.  Same outputs (TH, FALL, E, ALIGN, ALN, CUM, PIN, X1 / X1h) as the two
+// kernels; host: A == 128, F <= 32, D <= 1024.
+constexpr int TR_AR_NT = 1024;
+size_t tr_att_row_lds(int Tin, int KW) { return sizeof(float) * (size_t)(2 * 128 + 32 * 128 + KW * 32 + 32 + (Tin + KW) + Tin * 33 + 3 * Tin + 64 + 512); }
+__global__ __launch_bounds__(TR_AR_NT) void k_tr_att_row(TrAtt a) {
+  extern __shared__ __attribute__((aligned(16))) float sm_ar[];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int F = a.F, A = a.A, Tin = a.Tin, KW = a.KW, pad = (KW - 1) / 2, D = a.D;
+  const long tb = (long)a.t * a.B + b;
+  const int len = a.lens[b];
+  float* qS = sm_ar;               // [128] q + b_a
+  float* vaS = qS + 128;           // [128]
+  float* Wl = vaS + 128;           // [32][128]
+  float* Kc = Wl + 32 * 128;       // [KW][32]
+  float* bc = Kc + KW * 32;        // [32]
+  float* cseg = bc + 32;           // [Tin + KW - 1] cum_{t-1}, zero padded
+  float* fS = cseg + Tin + KW;     // [Tin][33] location features
+  float* ep = fS + Tin * 33;       // [Tin][2] energy halves
+  float* al = ep + 2 * Tin;        // [Tin]
+  float* rs = al + Tin;            // [64] reductions
+  float* chf = rs + 64;            // [512] context: the second position half's sums
+  if (tid < 128) {
+    float q = 0.f;
+    if (tid < A) {
+      if (a.qpart) {
+        const float* qp = a.qpart + (long)b * A + tid;
+        const long zs = (long)a.B * A;
+        float p[16];
+#pragma unroll
+        for (int z = 0; z < 16; ++z) p[z] = z < a.qks ? qp[z * zs] : 0.f;
+        for (int z = 16; z < a.qks; ++z) p[z & 15] += qp[z * zs];
+#pragma unroll
+        for (int z = 0; z < 16; ++z) q += p[z];
+      } else {
+        q = a.Q[tb * A + tid];
+      }
+      q += a.ba[tid];
+    }
+    qS[tid] = q;
+    vaS[tid] = tid < A ? a.va[tid] : 0.f;
+  }
+  for (int i = tid; i < 32 * 128; i += TR_AR_NT) {
+    const int c = i >> 7, k = i & 127;
+    Wl[i] = (c < F && k < A) ? a.Wl[c * A + k] : 0.f;
+  }
+  for (int i = tid; i < KW * 32; i += TR_AR_NT) {
+    const int tap = i >> 5, c = i & 31;
+    Kc[i] = c < F ? a.Kc[tap * F + c] : 0.f;
+  }
+  if (tid < 32) bc[tid] = tid < F ? a.bc[tid] : 0.f;
+  const float* cum_prev = a.CUM + tb * Tin;
+  for (int i = tid; i < Tin + KW - 1; i += TR_AR_NT) {
+    const int j = i - pad;
+    cseg[i] = (j >= 0 && j < Tin) ? cum_prev[j] : 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < Tin * 32; i += TR_AR_NT) {  // location features (attention.py:193-195)
+    const int j = i >> 5, c = i & 31;
+    float acc = 0.f;
+    if (c < F) {
+      acc = bc[c];
+      for (int tap = 0; tap < KW; ++tap) acc += cseg[j + tap] * Kc[tap * 32 + c];
+      a.FALL[(tb * Tin + j) * F + c] = acc;
+    }
+    fS[j * 33 + c] = acc;
+  }
+  __syncthreads();
+  {  // energies: thread = (position group jg, attention dim k); keys of 4 positions loaded ahead
+    const int k = tid & 127, jg = tid >> 7;
+    const bool kok = k < A;
+    float wl[32];
+#pragma unroll
+    for (int cc = 0; cc < 32; ++cc) wl[cc] = Wl[cc * 128 + k];
+    const float qk = qS[k], vk = vaS[k];
+    const float* kb = a.keys + (long)b * Tin * A + k;
+    for (int j0 = jg; j0 < Tin; j0 += 32) {
+      float kv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + 8 * r;
+        kv[r] = (j < Tin && kok) ? kb[(long)j * A] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + 8 * r;
+        if (j >= Tin) break;
+        float u = kv[r] + qk;
+        const float* fr = fS + j * 33;
+#pragma unroll
+        for (int cc = 0; cc < 32; ++cc) u += fr[cc] * wl[cc];
+        float e = 0.f;
+        if (kok) {
+          const float th = tanhf(u);
+          a.TH[(tb * Tin + j) * A + k] = th;
+          e = vk * th;
+        }
+        e = wave_sum(e);
+        if (lane == 0) ep[2 * j + (k >> 6)] = e;
+      }
+    }
+  }
+  __syncthreads();
+  // masked softmax over j < len (k_tr_ctx)
+  float mx = -INFINITY;
+  for (int j = tid; j < Tin; j += TR_AR_NT) {
+    const float e = ep[2 * j] + ep[2 * j + 1];
+    a.E[(long)b * Tin + j] = e;
+    if (j < len) mx = fmaxf(mx, e);
+  }
+  {
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (lane == 0) rs[w] = mx;
+    __syncthreads();
+    mx = rs[0];
+    for (int i = 1; i < TR_AR_NT / 64; ++i) mx = fmaxf(mx, rs[i]);
+    __syncthreads();
+  }
+  float sm = 0.f;
+  for (int j = tid; j < Tin; j += TR_AR_NT) {
+    const float x = j < len ? expf(ep[2 * j] + ep[2 * j + 1] - mx) : 0.f;
+    al[j] = x;
+    sm += x;
+  }
+  {
+    for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
+    if (lane == 0) rs[w] = sm;
+    __syncthreads();
+    sm = 0.f;
+    for (int i = 0; i < TR_AR_NT / 64; ++i) sm += rs[i];
+  }
+  for (int j = tid; j < Tin; j += TR_AR_NT) {
+    const float x = al[j] / sm;
+    al[j] = x;
+    a.ALIGN[((long)b * Tin + j) * a.T + a.t] = x;
+    a.ALN[tb * Tin + j] = x;
+    a.CUM[(tb + a.B) * Tin + j] = cum_prev[j] + x;
+  }
+  __syncthreads();
+  // context: channel n, two position halves per channel pass
+  const float* vb = a.values + (long)b * Tin * D;
+  const int LX = a.P + a.D + a.H, Bp = (a.B + 31) & ~31;
+  for (int n0 = 0; n0 < D; n0 += 512) {
+    const int n = n0 + (tid & 511), hf = tid >> 9;
+    float acc = 0.f;
+    if (n < D) {
+      const int jb = hf ? (Tin + 1) / 2 : 0, je = hf ? Tin : (Tin + 1) / 2;
+      int j = jb;
+      for (; j + 4 <= je; j += 4) {
+        const float v0 = vb[(long)j * D + n], v1 = vb[(long)(j + 1) * D + n];
+        const float v2 = vb[(long)(j + 2) * D + n], v3 = vb[(long)(j + 3) * D + n];
+        acc += al[j] * v0 + al[j + 1] * v1 + al[j + 2] * v2 + al[j + 3] * v3;
+      }
+      for (; j < je; ++j) acc += al[j] * vb[(long)j * D + n];
+    }
+    if (hf) chf[tid & 511] = acc;
+    __syncthreads();
+    if (!hf && n < D) {
+      const float r = acc + chf[tid & 511];
+      a.PIN[tb * (a.H + a.D) + a.H + n] = r;
+      a.X1[(tb + a.B) * LX + a.P + n] = r;
+      if (a.X1h) a.X1h[(long)(a.t + 1) * Bp * LX + tf_sw(b, a.P + n, LX)] = (__bf16)r;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
   extern __shared__ float al[];
   __shared__ float s16[16];
@@ -2134,6 +2346,18 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   // teacher-forcing draw (TacoTrainingHelper.next_inputs, helpers.py:122-133): a step fed its own
   // previous frame re-runs the prenet for its B rows from that frame (unclipped frame projection,
   // Architecture_wrappers.py:258-263); XIN / P1 / X1 then hold what the step actually consumed
+  // k_tr_att_row (the whole attention forward of a row in one work-group); TT2_TR_ATTROW=0 keeps the
+  // (j-tile, row) energy launch + the context launch (A/B)
+  const char* ae = std::getenv("TT2_TR_ATTROW");
+  const bool att_row = !(ae && ae[0] == '0') && A == 128 && F <= 32 && Tin <= 320 && tr_e2;
+  if (att_row) {
+    static bool attr = false;
+    if (!attr) {
+      TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tr_att_row),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)tr_att_row_lds(320, 64)));
+      attr = true;
+    }
+  }
   const bool free_run = tr_has_free_steps(c, T);
   if (free_run) tr_transpose(pvar(c, PRV(1, "kernel")), NM, P, P, c->W1T.as<float>(), NM, s);
   for (int t = 0; t < T; ++t) {
@@ -2195,6 +2419,14 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
       hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l2);
     }
     at.t = t;
+    if (att_row) {  // query as raw split-K partials; energies + softmax + context in one launch per row
+      at.qks = tr_gemm_raw(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A, s,
+                           &c->hWqT, H);
+      at.qpart = c->kpart.as<float>();
+      hipLaunchKernelGGL(k_tr_att_row, dim3(B), dim3(TR_AR_NT), tr_att_row_lds(Tin, KW), s, at);
+      at.qpart = nullptr;
+      continue;
+    }
     if (A <= 128 && tr_e2) {  // query as raw split-K partials, combined inside the energy kernel
       at.qks = tr_gemm_raw(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A, s,
                            &c->hWqT, H);
