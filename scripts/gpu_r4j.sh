@@ -1,0 +1,17 @@
+# the whole per-row attention forward in one work-group (k_tr_att_row): training tests, A/B against
+# the split energy + context launches (TT2_TR_ATTROW=0), kernel trace
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r4j
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_train.py tests/test_gpu_train_api.py tests/test_train_options.py -x -q -m gpu --timeout 600 --timeout-method thread > gpurun_out/r4j/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|error" gpurun_out/r4j/tests.log | head -20; tail -30 gpurun_out/r4j/tests.log; exit 1; }
+tail -1 gpurun_out/r4j/tests.log
+ARGS="--steps 1 --warmup 1 --no-wavenet --no-e2e --no-griffin-lim --no-cpu-baseline --no-variants --train-steps 3"
+for rep in 1 2; do
+  for F in 1 0; do
+    TT2_TR_ATTROW=$F timeout -k 10 300 python bench.py $ARGS > gpurun_out/r4j/b$F.json 2> gpurun_out/r4j/b$F.err || { echo "bench failed"; tail -5 gpurun_out/r4j/b$F.err; exit 1; }
+    python -c "import json; d=json.loads(open('gpurun_out/r4j/b$F.json').read().strip().splitlines()[-1]); print('attrow=$F', d['train']['ms_per_step'], d['train']['loss_last'])"
+  done
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4j/trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/r4j/prof.json 2>/dev/null
+echo rc=$?

@@ -831,178 +831,6 @@ __global__ __launch_bounds__(TR_E2T) void k_tr_att_energy2(TrAtt a) {
 // Masked softmax (attention.py:218, TF _maybe_mask_score) recomputed by every block of the row,
 // cumulative alignments (:222-225) by block 0, then context_t = align_t · values (:27)
 // -> PIN[t][b][H:], X1[t+1][b][P:P+D].
-// ---- the whole attention forward of one decoder step and row in ONE work-group (round 4) ------
-// k_tr_att_energy2 + k_tr_ctx of one row fused (attention.py:170-227 + the context, Architecture_
-// wrappers.py:235-240): location features of cum_{t-1} (F <= 32 channels, W_loc in LDS), energies over
-// every encoder position with the query's split-K partials summed in, the masked softmax, cum /
-// alignment outputs and the context -- the energies never leave the CU and the context launch with its
-// own softmax is gone.  1024 threads: 8 position groups x 128 attention dims for the energies, 2 x 512
-// channels for the context.  Same outputs (TH, FALL, E, ALIGN, ALN, CUM, PIN, X1 / X1h) as the two
-// kernels; host: A == 128, F <= 32, D <= 1024.
-constexpr int TR_AR_NT = 1024;
-size_t tr_att_row_lds(int Tin, int KW) { return sizeof(float) * (size_t)(2 * 128 + 32 * 128 + KW * 32 + 32 + (Tin + KW) + Tin * 33 + 3 * Tin + 64 + 512); }
-__global__ __launch_bounds__(TR_AR_NT) void k_tr_att_row(TrAtt a) {
-  extern __shared__ __attribute__((aligned(16))) float sm_ar[];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int F = a.F, A = a.A, Tin = a.Tin, KW = a.KW, pad = (KW - 1) / 2, D = a.D;
-  const long tb = (long)a.t * a.B + b;
-  const int len = a.lens[b];
-  float* qS = sm_ar;               // [128] q + b_a
-  float* vaS = qS + 128;           // [128]
-  float* Wl = vaS + 128;           // [32][128]
-  float* Kc = Wl + 32 * 128;       // [KW][32]
-  float* bc = Kc + KW * 32;        // [32]
-  float* cseg = bc + 32;           // [Tin + KW - 1] cum_{t-1}, zero padded
-  float* fS = cseg + Tin + KW;     // [Tin][33] location features
-  float* ep = fS + Tin * 33;       // [Tin][2] energy halves
-  float* al = ep + 2 * Tin;        // [Tin]
-  float* rs = al + Tin;            // [64] reductions
-  float* chf = rs + 64;            // [512] context: the second position half's sums
-  if (tid < 128) {
-    float q = 0.f;
-    if (tid < A) {
-      if (a.qpart) {
-        const float* qp = a.qpart + (long)b * A + tid;
-        const long zs = (long)a.B * A;
-        float p[16];
-#pragma unroll
-        for (int z = 0; z < 16; ++z) p[z] = z < a.qks ? qp[z * zs] : 0.f;
-        for (int z = 16; z < a.qks; ++z) p[z & 15] += qp[z * zs];
-#pragma unroll
-        for (int z = 0; z < 16; ++z) q += p[z];
-      } else {
-        q = a.Q[tb * A + tid];
-      }
-      q += a.ba[tid];
-    }
-    qS[tid] = q;
-    vaS[tid] = tid < A ? a.va[tid] : 0.f;
-  }
-  for (int i = tid; i < 32 * 128; i += TR_AR_NT) {
-    const int c = i >> 7, k = i & 127;
-    Wl[i] = (c < F && k < A) ? a.Wl[c * A + k] : 0.f;
-  }
-  for (int i = tid; i < KW * 32; i += TR_AR_NT) {
-    const int tap = i >> 5, c = i & 31;
-    Kc[i] = c < F ? a.Kc[tap * F + c] : 0.f;
-  }
-  if (tid < 32) bc[tid] = tid < F ? a.bc[tid] : 0.f;
-  const float* cum_prev = a.CUM + tb * Tin;
-  for (int i = tid; i < Tin + KW - 1; i += TR_AR_NT) {
-    const int j = i - pad;
-    cseg[i] = (j >= 0 && j < Tin) ? cum_prev[j] : 0.f;
-  }
-  __syncthreads();
-  for (int i = tid; i < Tin * 32; i += TR_AR_NT) {  // location features (attention.py:193-195)
-    const int j = i >> 5, c = i & 31;
-    float acc = 0.f;
-    if (c < F) {
-      acc = bc[c];
-      for (int tap = 0; tap < KW; ++tap) acc += cseg[j + tap] * Kc[tap * 32 + c];
-      a.FALL[(tb * Tin + j) * F + c] = acc;
-    }
-    fS[j * 33 + c] = acc;
-  }
-  __syncthreads();
-  {  // energies: thread = (position group jg, attention dim k); keys of 4 positions loaded ahead
-    const int k = tid & 127, jg = tid >> 7;
-    const bool kok = k < A;
-    float wl[32];
-#pragma unroll
-    for (int cc = 0; cc < 32; ++cc) wl[cc] = Wl[cc * 128 + k];
-    const float qk = qS[k], vk = vaS[k];
-    const float* kb = a.keys + (long)b * Tin * A + k;
-    for (int j0 = jg; j0 < Tin; j0 += 32) {
-      float kv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = j0 + 8 * r;
-        kv[r] = (j < Tin && kok) ? kb[(long)j * A] : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = j0 + 8 * r;
-        if (j >= Tin) break;
-        float u = kv[r] + qk;
-        const float* fr = fS + j * 33;
-#pragma unroll
-        for (int cc = 0; cc < 32; ++cc) u += fr[cc] * wl[cc];
-        float e = 0.f;
-        if (kok) {
-          const float th = tanhf(u);
-          a.TH[(tb * Tin + j) * A + k] = th;
-          e = vk * th;
-        }
-        e = wave_sum(e);
-        if (lane == 0) ep[2 * j + (k >> 6)] = e;
-      }
-    }
-  }
-  __syncthreads();
-  // masked softmax over j < len (k_tr_ctx)
-  float mx = -INFINITY;
-  for (int j = tid; j < Tin; j += TR_AR_NT) {
-    const float e = ep[2 * j] + ep[2 * j + 1];
-    a.E[(long)b * Tin + j] = e;
-    if (j < len) mx = fmaxf(mx, e);
-  }
-  {
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    if (lane == 0) rs[w] = mx;
-    __syncthreads();
-    mx = rs[0];
-    for (int i = 1; i < TR_AR_NT / 64; ++i) mx = fmaxf(mx, rs[i]);
-    __syncthreads();
-  }
-  float sm = 0.f;
-  for (int j = tid; j < Tin; j += TR_AR_NT) {
-    const float x = j < len ? expf(ep[2 * j] + ep[2 * j + 1] - mx) : 0.f;
-    al[j] = x;
-    sm += x;
-  }
-  {
-    for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
-    if (lane == 0) rs[w] = sm;
-    __syncthreads();
-    sm = 0.f;
-    for (int i = 0; i < TR_AR_NT / 64; ++i) sm += rs[i];
-  }
-  for (int j = tid; j < Tin; j += TR_AR_NT) {
-    const float x = al[j] / sm;
-    al[j] = x;
-    a.ALIGN[((long)b * Tin + j) * a.T + a.t] = x;
-    a.ALN[tb * Tin + j] = x;
-    a.CUM[(tb + a.B) * Tin + j] = cum_prev[j] + x;
-  }
-  __syncthreads();
-  // context: channel n, two position halves per channel pass
-  const float* vb = a.values + (long)b * Tin * D;
-  const int LX = a.P + a.D + a.H, Bp = (a.B + 31) & ~31;
-  for (int n0 = 0; n0 < D; n0 += 512) {
-    const int n = n0 + (tid & 511), hf = tid >> 9;
-    float acc = 0.f;
-    if (n < D) {
-      const int jb = hf ? (Tin + 1) / 2 : 0, je = hf ? Tin : (Tin + 1) / 2;
-      int j = jb;
-      for (; j + 4 <= je; j += 4) {
-        const float v0 = vb[(long)j * D + n], v1 = vb[(long)(j + 1) * D + n];
-        const float v2 = vb[(long)(j + 2) * D + n], v3 = vb[(long)(j + 3) * D + n];
-        acc += al[j] * v0 + al[j + 1] * v1 + al[j + 2] * v2 + al[j + 3] * v3;
-      }
-      for (; j < je; ++j) acc += al[j] * vb[(long)j * D + n];
-    }
-    if (hf) chf[tid & 511] = acc;
-    __syncthreads();
-    if (!hf && n < D) {
-      const float r = acc + chf[tid & 511];
-      a.PIN[tb * (a.H + a.D) + a.H + n] = r;
-      a.X1[(tb + a.B) * LX + a.P + n] = r;
-      if (a.X1h) a.X1h[(long)(a.t + 1) * Bp * LX + tf_sw(b, a.P + n, LX)] = (__bf16)r;
-    }
-    __syncthreads();
-  }
-}
-
 __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
   extern __shared__ float al[];
   __shared__ float s16[16];
@@ -2346,18 +2174,6 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   // teacher-forcing draw (TacoTrainingHelper.next_inputs, helpers.py:122-133): a step fed its own
   // previous frame re-runs the prenet for its B rows from that frame (unclipped frame projection,
   // Architecture_wrappers.py:258-263); XIN / P1 / X1 then hold what the step actually consumed
-  // k_tr_att_row (the whole attention forward of a row in one work-group); TT2_TR_ATTROW=0 keeps the
-  // (j-tile, row) energy launch + the context launch (A/B)
-  const char* ae = std::getenv("TT2_TR_ATTROW");
-  const bool att_row = !(ae && ae[0] == '0') && A == 128 && F <= 32 && Tin <= 320 && tr_e2;
-  if (att_row) {
-    static bool attr = false;
-    if (!attr) {
-      TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tr_att_row),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)tr_att_row_lds(320, 64)));
-      attr = true;
-    }
-  }
   const bool free_run = tr_has_free_steps(c, T);
   if (free_run) tr_transpose(pvar(c, PRV(1, "kernel")), NM, P, P, c->W1T.as<float>(), NM, s);
   for (int t = 0; t < T; ++t) {
@@ -2419,14 +2235,6 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
       hipLaunchKernelGGL(k_tr_lstm_fwd, dim3(bh), dim3(256), 0, s, l2);
     }
     at.t = t;
-    if (att_row) {  // query as raw split-K partials; energies + softmax + context in one launch per row
-      at.qks = tr_gemm_raw(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A, s,
-                           &c->hWqT, H);
-      at.qpart = c->kpart.as<float>();
-      hipLaunchKernelGGL(k_tr_att_row, dim3(B), dim3(TR_AR_NT), tr_att_row_lds(Tin, KW), s, at);
-      at.qpart = nullptr;
-      continue;
-    }
     if (A <= 128 && tr_e2) {  // query as raw split-K partials, combined inside the energy kernel
       at.qks = tr_gemm_raw(B, A, H, PIN + s1 * (H + D), H + D, pvar(c, vn("decoder/query_layer/kernel")), A, s,
                            &c->hWqT, H);

@@ -718,42 +718,3 @@ def test_train_config_use_gst_without_gpu():
     hp.override_from_dict(dict(use_gst=False))
     cfg = train_config(hp, 4, 9, 6, frontend=True)
     assert cfg.use_gst == 0 and cfg.memory_dim == 2 * hp.encoder_lstm_units + 256
-
-
-@pytest.mark.gpu
-def test_gpu_train_attention_row_kernel_matches_split_kernels():
-    """k_tr_att_row (one work-group per row: location features, energies with the query partials,
-    masked softmax, cum / alignments and the context) against the (j-tile, row) energy launch + the
-    context launch (TT2_TR_ATTROW=0), fp32 step at attention_dim 128 with ragged lengths: frames,
-    alignments, losses and every gradient agree to fp32 summation order (1e-5 relative)."""
-    import os
-    from tt2.train import TacotronTrainer
-    hp = small_hparams()
-    hp.override_from_dict(dict(attention_dim=128, attention_filters=32))
-    B, T_in, T_out = 6, 37, 12
-    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
-    res = {}
-    for mode in ("1", "0"):
-        old = os.environ.get("TT2_TR_ATTROW")
-        os.environ["TT2_TR_ATTROW"] = mode
-        try:
-            tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, postnet=False)
-            try:
-                tr.forward_backward(mem, lens, tg, st, pm, zm)
-                L = tr.losses()
-                fr, sl, al = tr.outputs(T_in, T_out)
-                g = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in TRN.train_var_names()}
-            finally:
-                tr.close()
-        finally:
-            if old is None:
-                del os.environ["TT2_TR_ATTROW"]
-            else:
-                os.environ["TT2_TR_ATTROW"] = old
-        res[mode] = (L, fr, al, g)
-    (La, fa, aa, ga), (Lb, fb, ab, gb) = res["1"], res["0"]
-    np.testing.assert_allclose(fa, fb, atol=1e-5)
-    np.testing.assert_allclose(aa, ab, atol=1e-6)
-    assert abs(La["before"] - Lb["before"]) < 1e-5 * Lb["before"]
-    for n in ga:
-        assert _rel(ga[n], gb[n]) < 1e-5, (n, _rel(ga[n], gb[n]))
