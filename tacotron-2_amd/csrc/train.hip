@@ -88,6 +88,7 @@ struct tt2_train_ctx {
   // front end (cfg.frontend: encoder + reference encoders + GST, train_front.hip)
   int f_nref = 0, f_gin = 0, f_T2 = 0, f_T2max = 0;
   bool f_ran = false;
+  DevBuf fTWf, fTWb, fHSh, fDZh;  // encoder BiLSTM fused steps: TF-layout weights and state / dZ shadows
   DevBuf fEX, fEA[8], fEY[9], fXP, fGZ, fGA, fCN, fCS, fHS, fENC, fMEM, fSTY, fDSTY, fDZ, fDHC, fDCC, fDHP, fdXP, fdA,
       fdB, fLWxT, fLWhT;
   DevBuf fRA[2][6], fRY[2][6], fXG[2], fGR[2], fGU[2], fGCC[2], fGRH[2], fHG[2], fREF[2], fGG, fGC, fFBUF, fDY, fDY2,
@@ -354,7 +355,7 @@ __global__ void k_tr_lstm_fwd(TrLstmFwd a) {
 //   TF_PLAIN C = X·W + residual (d X1 = dG1 · K1^T + R1)
 // A operands are bf16 shadows of the fp32 rows written by their producers (same round-to-nearest-
 // even as the staged operands of the bf16 GEMMs), except TF_BWD_H's.
-enum { TF_FWD = 0, TF_BWD_H = 1, TF_BWD_S = 2, TF_PLAIN = 3 };
+enum { TF_FWD = 0, TF_BWD_H = 1, TF_BWD_S = 2, TF_PLAIN = 3, TF_EFWD = 4, TF_EBWD = 5 };
 // Fragment-major bf16 layout of a [rows][K] operand ("TF layout"): 32-row blocks x 16-deep k-steps x
 // [32 rows][16 k], so one wave's v_mfma_f32_32x32x16_bf16 fragment load of a k-step (lane l: row l%32,
 // k = 8(l/32) .. +8) is ONE contiguous kilobyte instead of 32 rows a K-stride apart.  The weights are
@@ -364,7 +365,7 @@ __host__ __device__ inline long tf_sw(int r, int k, int K) {
   return ((((long)(r >> 5) * (K >> 4) + (k >> 4)) * 32 + (r & 31)) << 4) + (k & 15);
 }
 __host__ __device__ inline long tf_colmap(int mode, int cg, int c, int H) {
-  if (mode == TF_FWD) return (long)(c >> 3) * H + cg * 8 + (c & 7);
+  if (mode == TF_FWD || mode == TF_EFWD) return (long)(c >> 3) * H + cg * 8 + (c & 7);
   if (mode == TF_BWD_S) return c < 16 ? cg * 16 + c : H + cg * 16 + (c - 16);
   return (long)cg * 32 + c;
 }
@@ -376,6 +377,18 @@ __global__ void k_tr_tf_weights(const __bf16* __restrict__ src, int N, int K, in
     const int r = (int)(i / K), k = (int)(i % K);  // r = 32 cg + c
     const long col = tf_colmap(mode, r >> 5, r & 31, H);
     dst[tf_sw(r, k, K)] = col < N ? src[col * K + k] : (__bf16)0.f;
+  }
+}
+// fp32 weights -> TF layout directly: element (column n, k) = src[n·ld + k], or src[k·ld + n] when
+// transposed (the encoder LSTM's recurrent kernel serves both products: [U][4U] is W for the forward
+// gates and W^T for the backward d h)
+__global__ void k_tr_tf_weights_f32(const float* __restrict__ src, long ld, int transposed, int N, int K, int ncg,
+                                    int mode, int H, __bf16* __restrict__ dst) {
+  const long n = (long)ncg * 32 * K;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / K), k = (int)(i % K);
+    const long col = tf_colmap(mode, r >> 5, r & 31, H);
+    dst[tf_sw(r, k, K)] = col < N ? (__bf16)(transposed ? src[(long)k * ld + col] : src[col * ld + k]) : (__bf16)0.f;
   }
 }
 constexpr int TLG_U = 8, TLG_NT = 512, TLG_KSMAX = 16;
@@ -423,6 +436,17 @@ struct TrFused {
   long ldc;
   const float* residual;
   long ldres;
+  // encoder BiLSTM (TF_EFWD / TF_EBWD, FeLstm's buffers; H = U, both directions in one launch)
+  const int* lens;
+  int T;                 // encoder steps
+  float zo;
+  long wdir, adir;       // per-direction strides of Wt and of the bf16 state shadow (elements)
+  const float* XP;       // [B][T][8U] input projections (+ bias)
+  float* GA; float* CN; float* CS; float* HS; float* ENC;
+  __bf16* HSh;           // [2][T+1][Bp][U] TF layout: h state shadow (EFWD: A operand and output)
+  const float* DENC; long ld_denc;
+  float* DZ; float* DCC; float* DHP;
+  __bf16* DZh;           // [2 dirs][2 slots][Bp][4U] TF layout: dZ shadow (EBWD: A of step t-1)
 };
 
 // Epilogue operands of one (row, unit), loaded BEFORE the product so their round trip overlaps the
@@ -492,6 +516,114 @@ __device__ __forceinline__ void tf_cell_bwd(const TrFused& a, int b, int n, floa
   a.R[(long)b * a.ldr + a.off_r + n] = (1.f - v.kh) * v.dhz;
 }
 
+// Encoder BiLSTM cell of (direction, row, unit) at encoder step a.t (k_fe_lstm_cell /
+// k_fe_lstm_cell_bwd of train_front.hip: TF's rnn step past a row's length copies the state and emits
+// 0; the backward direction visits positions len-1-t), operands loaded before the product.
+// TfCellIn: g0..g3 = input projections (fwd) / activated gates (bwd); cp, hp = c, h of step t (fwd)
+// / c of step t (bwd); kc, kh = zoneout keep bits; dhz = d h_t from the output (bwd), dcz = d carried
+// c, ext = the carried d h's direct part (DHP) of step t+1, cn = c_new (bwd), sres = the row's length
+template <int MODE>
+__device__ __forceinline__ TfCellIn tf_enc_load(const TrFused& a, int dir, int b, int u) {
+  TfCellIn v{};
+  const int U = a.H, B = a.B, T = a.T, t = a.t;
+  const int len = a.lens[b];
+  v.sres = (float)len;
+  if (a.zm) {
+    v.kc = (float)a.zm[((((long)t * 2 + dir) * 2 + 0) * B + b) * U + u];
+    v.kh = (float)a.zm[((((long)t * 2 + dir) * 2 + 1) * B + b) * U + u];
+  } else {
+    v.kc = v.kh = 1.f - a.zo;
+  }
+  const long st0 = ((long)dir * (T + 1) + t) * B * U + (long)b * U + u;
+  const int pos = dir == 0 ? t : len - 1 - t;
+  if constexpr (MODE == TF_EFWD) {
+    v.cp = a.CS[st0];
+    v.hp = a.HS[st0];
+    if (t < len) {
+      const float* xp = a.XP + ((long)b * T + pos) * 8 * U + dir * 4 * U;
+      v.g0 = xp[u];
+      v.g1 = xp[U + u];
+      v.g2 = xp[2 * U + u];
+      v.g3 = xp[3 * U + u];
+    }
+  } else {
+    const long sidx = ((long)dir * B + b) * U + u;
+    v.ext = a.DHP[sidx];
+    v.dcz = a.DCC[sidx];
+    if (t < len) {
+      const float* ga = a.GA + (((long)dir * T + t) * B + b) * 4 * U;
+      v.g0 = ga[u];
+      v.g1 = ga[U + u];
+      v.g2 = ga[2 * U + u];
+      v.g3 = ga[3 * U + u];
+      v.cn = a.CN[((long)dir * T + t) * B * U + (long)b * U + u];
+      v.cp = a.CS[st0];
+      v.dhz = a.DENC[((long)b * T + pos) * a.ld_denc + dir * U + u];
+    }
+  }
+  return v;
+}
+__device__ __forceinline__ void tf_enc_fwd(const TrFused& a, int dir, int b, int u, float p0, float p1, float p2, float p3,
+                                           const TfCellIn& v) {
+  const int U = a.H, B = a.B, T = a.T, t = a.t, len = (int)v.sres;
+  const long st1 = ((long)dir * (T + 1) + t + 1) * B * U + (long)b * U + u;
+  const int Bp = (B + 31) & ~31;
+  __bf16* hs1 = a.HSh + dir * a.adir + (long)(t + 1) * Bp * U;
+  if (t >= len) {  // past the row's length: state copied, output stays 0 (TF rnn._rnn_step)
+    a.CS[st1] = v.cp;
+    a.HS[st1] = v.hp;
+    hs1[tf_sw(b, u, U)] = (__bf16)v.hp;
+    return;
+  }
+  const int pos = dir == 0 ? t : len - 1 - t;
+  const float si = 1.0f / (1.0f + expf(-(p0 + v.g0))), tj = tanhf(p1 + v.g1);
+  const float sf = 1.0f / (1.0f + expf(-(p2 + v.g2 + 1.0f))), so = 1.0f / (1.0f + expf(-(p3 + v.g3)));
+  const float cn = sf * v.cp + si * tj;
+  const float hn = so * tanhf(cn);
+  float* ga = a.GA + (((long)dir * T + t) * B + b) * 4 * U;
+  ga[u] = si;
+  ga[U + u] = tj;
+  ga[2 * U + u] = sf;
+  ga[3 * U + u] = so;
+  a.CN[((long)dir * T + t) * B * U + (long)b * U + u] = cn;
+  const float hs = v.hp + v.kh * (hn - v.hp);
+  a.CS[st1] = v.cp + v.kc * (cn - v.cp);
+  a.HS[st1] = hs;
+  hs1[tf_sw(b, u, U)] = (__bf16)hs;
+  a.ENC[((long)b * T + pos) * 2 * U + dir * U + u] = hn;
+}
+__device__ __forceinline__ void tf_enc_bwd(const TrFused& a, int dir, int b, int u, float prod, const TfCellIn& v) {
+  const int U = a.H, B = a.B, T = a.T, t = a.t, len = (int)v.sres;
+  const long sidx = ((long)dir * B + b) * U + u;
+  const int Bp = (B + 31) & ~31;
+  const float dhc = prod + v.ext;  // d h carried out of step t = dZ(t+1)·Wh^T + its direct part
+  float* dz = a.DZ + (((long)dir * T + t) * B + b) * 4 * U;
+  __bf16* dzh = a.DZh + dir * a.adir + (long)(t & 1) * Bp * 4 * U;
+  if (t >= len) {  // copied state: gradients pass through, no gate gradient
+    dz[u] = dz[U + u] = dz[2 * U + u] = dz[3 * U + u] = 0.f;
+    dzh[tf_sw(b, u, 4 * U)] = dzh[tf_sw(b, U + u, 4 * U)] = dzh[tf_sw(b, 2 * U + u, 4 * U)] =
+        dzh[tf_sw(b, 3 * U + u, 4 * U)] = (__bf16)0.f;
+    a.DHP[sidx] = dhc;
+    return;
+  }
+  const float si = v.g0, tj = v.g1, sf = v.g2, so = v.g3;
+  const float dhn = v.dhz + v.kh * dhc;
+  const float tc = tanhf(v.cn);
+  const float dcn = v.kc * v.dcz + dhn * so * (1.f - tc * tc);
+  const float d0 = dcn * tj * si * (1.f - si), d1 = dcn * si * (1.f - tj * tj);
+  const float d2 = dcn * v.cp * sf * (1.f - sf), d3 = dhn * tc * so * (1.f - so);
+  dz[u] = d0;
+  dz[U + u] = d1;
+  dz[2 * U + u] = d2;
+  dz[3 * U + u] = d3;
+  dzh[tf_sw(b, u, 4 * U)] = (__bf16)d0;
+  dzh[tf_sw(b, U + u, 4 * U)] = (__bf16)d1;
+  dzh[tf_sw(b, 2 * U + u, 4 * U)] = (__bf16)d2;
+  dzh[tf_sw(b, 3 * U + u, 4 * U)] = (__bf16)d3;
+  a.DCC[sidx] = (1.f - v.kc) * v.dcz + dcn * sf;
+  a.DHP[sidx] = (1.f - v.kh) * dhc;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
   typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
@@ -501,10 +633,18 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
   const int cg = (ncg & 7) == 0 ? (bid & 7) + 8 * (bid >> 4) : bid >> 1;
   const int rh = (ncg & 7) == 0 ? (bid >> 3) & 1 : bid & 1;
   const int r0 = 32 * rh;
-  // this thread's epilogue element(s): FWD 32 rows x 8 units (threads < 256), BWD_S 32 x 16, BWD_H
-  // 32 x 32 and PLAIN 32 x 32 columns (two per thread)
-  constexpr int NE = (MODE == TF_BWD_H || MODE == TF_PLAIN) ? 2 : 1;
-  constexpr int UPR = MODE == TF_FWD ? 8 : MODE == TF_BWD_S ? 16 : 32;  // epilogue columns per row
+  // encoder modes: the column groups of direction 1 follow those of direction 0
+  constexpr bool ENC = MODE == TF_EFWD || MODE == TF_EBWD;
+  const int dir = ENC ? cg / (ncg >> 1) : 0, cgl = ENC ? cg % (ncg >> 1) : cg;
+  const __bf16* const Wb = a.Wt + (ENC ? dir * a.wdir : 0L);
+  const int Bp = (a.B + 31) & ~31;
+  const __bf16* const Ab = MODE == TF_EFWD ? a.HSh + dir * a.adir + (long)a.t * Bp * a.H
+                           : MODE == TF_EBWD ? a.DZh + dir * a.adir + (long)((a.t + 1) & 1) * Bp * 4 * a.H
+                                             : a.Ah;
+  // this thread's epilogue element(s): FWD / EFWD 32 rows x 8 units (threads < 256), BWD_S 32 x 16,
+  // BWD_H / EBWD 32 x 32 units and PLAIN 32 x 32 columns (two per thread)
+  constexpr int NE = (MODE == TF_BWD_H || MODE == TF_PLAIN || MODE == TF_EBWD) ? 2 : 1;
+  constexpr int UPR = (MODE == TF_FWD || MODE == TF_EFWD) ? 8 : MODE == TF_BWD_S ? 16 : 32;  // columns per row
   int eb[NE], en[NE], erl[NE], ekk[NE];
   bool eok[NE];
   TfCellIn ev[NE];
@@ -515,11 +655,13 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
     erl[e] = pidx / UPR;
     ekk[e] = pidx % UPR;
     eb[e] = r0 + erl[e];
-    en[e] = cg * UPR + ekk[e];
+    en[e] = cgl * UPR + ekk[e];
     eok[e] = erl[e] < 32 && eb[e] < a.B && (MODE != TF_PLAIN || en[e] < a.N);
     eres[e] = 0.f;
     if constexpr (MODE == TF_PLAIN) {
       if (eok[e] && a.residual) eres[e] = a.residual[(long)eb[e] * a.ldres + en[e]];
+    } else if constexpr (ENC) {
+      if (eok[e]) ev[e] = tf_enc_load<MODE>(a, dir, eb[e], en[e]);
     } else {
       if (eok[e]) ev[e] = tf_cell_load<MODE>(a, eb[e], en[e]);
     }
@@ -535,7 +677,7 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
     for (int s = 0; s < TLG_KSMAX; ++s) {
       if (s0 + s < ks) {
         const int k = k0 + 16 * (s0 + s) + kh;
-        vb[s] = *reinterpret_cast<const bf8*>(a.Wt + tf_sw(32 * cg + c, k, a.K));
+        vb[s] = *reinterpret_cast<const bf8*>(Wb + tf_sw(32 * cgl + c, k, a.K));
         if constexpr (MODE == TF_BWD_H) {
           if (rok) {
             const float* p = a.Af + (long)(r0 + c) * a.lda + k;
@@ -546,7 +688,7 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
             va[s] = z8;
           }
         } else {
-          va[s] = rok ? *reinterpret_cast<const bf8*>(a.Ah + tf_sw(r0 + c, k, a.K)) : z8;
+          va[s] = rok ? *reinterpret_cast<const bf8*>(Ab + tf_sw(r0 + c, k, a.K)) : z8;
         }
       }
     }
@@ -595,6 +737,10 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
       a.hz_out[(long)b * a.ld_hz + n] = hz;
       if (a.h_out_h) a.h_out_h[tf_sw(b, a.h_col0 + n, (int)a.ld_h_h)] = (__bf16)hnew;
       if (a.hz_out_h) a.hz_out_h[tf_sw(b, a.hz_col0 + n, (int)a.ld_hz_h)] = (__bf16)hz;
+    } else if constexpr (MODE == TF_EFWD) {
+      tf_enc_fwd(a, dir, b, n, sum8(rl, kk), sum8(rl, 8 + kk), sum8(rl, 16 + kk), sum8(rl, 24 + kk), ev[e]);
+    } else if constexpr (MODE == TF_EBWD) {
+      tf_enc_bwd(a, dir, b, n, sum8(rl, kk), ev[e]);
     } else if constexpr (MODE == TF_BWD_H) {
       tf_cell_bwd(a, b, n, sum8(rl, kk) + ev[e].ext, ev[e]);
     } else if constexpr (MODE == TF_BWD_S) {
@@ -1812,7 +1958,7 @@ static std::string tr_bufname(const void* owner, const DevBuf* b) {
   TT2_NMA(PA, 8) TT2_NMA(PX, 9) TT2_NM(BNM) TT2_NM(BNV) TT2_NM(PPRJ) TT2_NM(dPP) TT2_NM(DYb) TT2_NM(DZb)
   TT2_NM(dPXa) TT2_NM(dPXb) TT2_NM(WFLIP) TT2_NM(PWT) TT2_NM(CLIPM) TT2_NM(pn_part) TT2_NM(fEX) TT2_NMA(fEA, 8)
   TT2_NMA(fEY, 9) TT2_NM(fXP) TT2_NM(fGZ) TT2_NM(fGA) TT2_NM(fCN) TT2_NM(fCS) TT2_NM(fHS) TT2_NM(fENC)
-  TT2_NM(fMEM) TT2_NM(fSTY) TT2_NM(fDSTY) TT2_NM(fDZ) TT2_NM(fDHC) TT2_NM(fDCC) TT2_NM(fDHP) TT2_NM(fdXP)
+  TT2_NM(fTWf) TT2_NM(fTWb) TT2_NM(fHSh) TT2_NM(fDZh) TT2_NM(fMEM) TT2_NM(fSTY) TT2_NM(fDSTY) TT2_NM(fDZ) TT2_NM(fDHC) TT2_NM(fDCC) TT2_NM(fDHP) TT2_NM(fdXP)
   TT2_NM(fdA) TT2_NM(fdB) TT2_NM(fLWxT) TT2_NM(fLWhT) TT2_NMA(fXG, 2) TT2_NMA(fGR, 2) TT2_NMA(fGU, 2)
   TT2_NMA(fGCC, 2) TT2_NMA(fGRH, 2) TT2_NMA(fHG, 2) TT2_NMA(fREF, 2) TT2_NM(fGG) TT2_NM(fGC) TT2_NM(fFBUF)
   TT2_NM(fDY) TT2_NM(fDY2) TT2_NM(fDZc) TT2_NM(fGq) TT2_NM(fGkk) TT2_NM(fGv) TT2_NM(fGnv) TT2_NM(fGbb)
@@ -2504,6 +2650,14 @@ static void tr_front_build_vars(tt2_train_ctx* c, const std::function<void(const
   }
 }
 
+// the encoder BiLSTM steps as fused products (k_tr_fused TF_EFWD / TF_EBWD): bf16 step, B <= 64,
+// U a multiple of 128; TT2_TR_FUSED=0 keeps the split products + cell launches
+static bool fe_enc_fused(tt2_train_ctx* c) {
+  const char* fe = std::getenv("TT2_TR_FUSED");
+  const int U = c->cfg.encoder_lstm_units;
+  return !(fe && fe[0] == '0') && g_tr_prec == 2 && c->B <= 64 && U % 128 == 0;
+}
+
 static void tr_front_alloc(tt2_train_ctx* c) {
   const auto& f = c->cfg;
   const long B = c->B, T = c->Tin, C = f.enc_conv_channels, E = f.embedding_dim, U = f.encoder_lstm_units;
@@ -2520,6 +2674,11 @@ static void tr_front_alloc(tt2_train_ctx* c) {
   a(c->fDZ, 2 * T * B * 4 * U); a(c->fDHC, 2 * B * U); a(c->fDCC, 2 * B * U); a(c->fDHP, 2 * B * U);
   a(c->fdXP, BT * 8 * U); a(c->fdA, BT * std::max(C, E)); a(c->fdB, BT * std::max(C, E));
   a(c->fLWxT, 2 * 4 * U * C); a(c->fLWhT, 2 * 4 * U * U);
+  {  // bf16 TF-layout operands of the fused encoder LSTM steps (k_tr_fused TF_EFWD / TF_EBWD)
+    const long Bp = (B + 31) & ~31L;
+    auto h = [](DevBuf& d, long n) { d.alloc(2 * (size_t)std::max<long>(n, 1)); };
+    h(c->fTWf, 2 * 4 * U * U); h(c->fTWb, 2 * 4 * U * U); h(c->fHSh, 2 * (T + 1) * Bp * U); h(c->fDZh, 2 * 2 * Bp * 4 * U);
+  }
   // reference encoders at max_T_ref
   const int RD = f.reference_depth, nm = c->NM;
   long fbuf = BT * K * std::max(C, E);  // encoder im2col^T
@@ -2649,13 +2808,31 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
   l.XP = c->fXP.as<float>(); l.GZ = c->fGZ.as<float>(); l.GA = c->fGA.as<float>(); l.CN = c->fCN.as<float>();
   l.CS = c->fCS.as<float>(); l.HS = c->fHS.as<float>(); l.ENC = c->fENC.as<float>(); l.zm = enczm; l.lens = lens;
   l.B = B; l.T = T; l.U = U; l.zo = f.zoneout;
-  for (int t = 0; t < T; ++t) {
+  if (fe_enc_fused(c)) {  // both directions' recurrent product + cell in one launch per step
+    const long Bp = (B + 31) & ~31L;
     for (int d = 0; d < 2; ++d)
-      tr_gemm(B, 4 * U, U, c->fHS.as<float>() + ((long)d * (T + 1) + t) * B * U, U,
-              pvar(c, fe_lstm_scope(d) + "kernel") + (long)C * 4 * U, 4 * U, c->fGZ.as<float>() + (long)d * B * 4 * U,
-              4 * U, s);
-    l.t = t;
-    fe_lstm_cell(l, s);
+      hipLaunchKernelGGL(k_tr_tf_weights_f32, dim3(1024), dim3(256), 0, s, pvar(c, fe_lstm_scope(d) + "kernel") + (long)C * 4 * U,
+                         (long)4 * U, 1, 4 * U, U, U / 8, (int)TF_EFWD, U, c->fTWf.as<__bf16>() + (long)d * 4 * U * U);
+    for (int d = 0; d < 2; ++d)  // zero initial h
+      TT2_HIP(hipMemsetAsync(c->fHSh.as<__bf16>() + (long)d * (T + 1) * Bp * U, 0, 2 * (size_t)Bp * U, s));
+    TrFused e{};
+    e.Wt = c->fTWf.as<__bf16>(); e.wdir = (long)4 * U * U; e.K = U; e.B = B; e.H = U; e.T = T; e.lens = lens;
+    e.zm = enczm; e.zo = f.zoneout; e.XP = c->fXP.as<float>(); e.GA = c->fGA.as<float>(); e.CN = c->fCN.as<float>();
+    e.CS = c->fCS.as<float>(); e.HS = c->fHS.as<float>(); e.ENC = c->fENC.as<float>(); e.HSh = c->fHSh.as<__bf16>();
+    e.adir = (T + 1) * Bp * U;
+    for (int t = 0; t < T; ++t) {
+      e.t = t;
+      hipLaunchKernelGGL(k_tr_fused<TF_EFWD>, dim3(2 * 2 * U / 8), dim3(TLG_NT), 0, s, e);
+    }
+  } else {
+    for (int t = 0; t < T; ++t) {
+      for (int d = 0; d < 2; ++d)
+        tr_gemm(B, 4 * U, U, c->fHS.as<float>() + ((long)d * (T + 1) + t) * B * U, U,
+                pvar(c, fe_lstm_scope(d) + "kernel") + (long)C * 4 * U, 4 * U, c->fGZ.as<float>() + (long)d * B * 4 * U,
+                4 * U, s);
+      l.t = t;
+      fe_lstm_cell(l, s);
+    }
   }
   // reference encoders (modules.py:9-64) + GST (tacotron.py:276-282)
   const int RD = f.reference_depth;
@@ -2984,13 +3161,31 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
   l.zm = enczm; l.lens = lens; l.B = B; l.T = T; l.U = U; l.zo = f.zoneout;
   l.DENC = c->DMEM.as<float>(); l.ld_denc = D; l.DZ = c->fDZ.as<float>(); l.DHC = c->fDHC.as<float>();
   l.DCC = c->fDCC.as<float>(); l.DHP = c->fDHP.as<float>();
-  for (int t = T - 1; t >= 0; --t) {
-    l.t = t;
-    fe_lstm_cell_bwd(l, s);
+  if (fe_enc_fused(c)) {  // d h carried = dZ(t+1)·Wh^T + its direct part, fused with the cell backward
+    const long Bp = (B + 31) & ~31L;
     for (int d = 0; d < 2; ++d)
-      tr_gemm(B, U, 4 * U, c->fDZ.as<float>() + ((long)d * T + t) * B * 4 * U, 4 * U,
-              c->fLWhT.as<float>() + (long)d * 4 * U * U, U, c->fDHC.as<float>() + (long)d * B * U, U, s, nullptr,
-              c->fDHP.as<float>() + (long)d * B * U, U);
+      hipLaunchKernelGGL(k_tr_tf_weights_f32, dim3(1024), dim3(256), 0, s, pvar(c, fe_lstm_scope(d) + "kernel") + (long)C * 4 * U,
+                         (long)4 * U, 0, U, 4 * U, U / 32, (int)TF_PLAIN, U, c->fTWb.as<__bf16>() + (long)d * 4 * U * U);
+    TT2_HIP(hipMemsetAsync(c->fDZh.p, 0, c->fDZh.bytes, s));  // dZ(T) = 0
+    TT2_HIP(hipMemsetAsync(c->fDHP.p, 0, c->fDHP.bytes, s));
+    TrFused e{};
+    e.Wt = c->fTWb.as<__bf16>(); e.wdir = (long)4 * U * U; e.K = 4 * U; e.B = B; e.H = U; e.T = T; e.lens = lens;
+    e.zm = enczm; e.zo = f.zoneout; e.GA = c->fGA.as<float>(); e.CN = c->fCN.as<float>(); e.CS = c->fCS.as<float>();
+    e.DENC = c->DMEM.as<float>(); e.ld_denc = D; e.DZ = c->fDZ.as<float>(); e.DCC = c->fDCC.as<float>();
+    e.DHP = c->fDHP.as<float>(); e.DZh = c->fDZh.as<__bf16>(); e.adir = 2 * Bp * 4 * U;
+    for (int t = T - 1; t >= 0; --t) {
+      e.t = t;
+      hipLaunchKernelGGL(k_tr_fused<TF_EBWD>, dim3(2 * 2 * U / 32), dim3(TLG_NT), 0, s, e);
+    }
+  } else {
+    for (int t = T - 1; t >= 0; --t) {
+      l.t = t;
+      fe_lstm_cell_bwd(l, s);
+      for (int d = 0; d < 2; ++d)
+        tr_gemm(B, U, 4 * U, c->fDZ.as<float>() + ((long)d * T + t) * B * 4 * U, 4 * U,
+                c->fLWhT.as<float>() + (long)d * 4 * U * U, U, c->fDHC.as<float>() + (long)d * B * U, U, s, nullptr,
+                c->fDHP.as<float>() + (long)d * B * U, U);
+    }
   }
   for (int d = 0; d < 2; ++d) {  // recurrent weights: Σ_t HS(t)ᵀ DZ(t); biases
     const long R = (long)T * B;

@@ -718,3 +718,43 @@ def test_train_config_use_gst_without_gpu():
     hp.override_from_dict(dict(use_gst=False))
     cfg = train_config(hp, 4, 9, 6, frontend=True)
     assert cfg.use_gst == 0 and cfg.memory_dim == 2 * hp.encoder_lstm_units + 256
+
+
+@pytest.mark.gpu
+def test_gpu_train_fused_encoder_lstm_matches_split_k_path():
+    """The whole bf16 step from ids at the fork's encoder width (encoder_lstm_units 256): the
+    encoder BiLSTM steps as fused products (k_tr_fused TF_EFWD / TF_EBWD: both directions' h·W_h +
+    the cell in one launch per step, and dZ·W_h^T + the cell backward) against the split products
+    + cell launches (TT2_TR_FUSED=0), like the decoder comparison: losses within 1e-5 relative, every
+    gradient within 1e-2 (bf16 operand rounding level)."""
+    import os
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    hp.override_from_dict(dict(encoder_lstm_units=256, enc_conv_channels=128, embedding_dim=128))
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, B=6, T_in=23, T_out=8, T_ref=64)
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    res = {}
+    for mode in ("1", "0"):
+        old = os.environ.get("TT2_TR_FUSED")
+        os.environ["TT2_TR_FUSED"] = mode
+        try:
+            tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", frontend=True, max_T_ref=re.shape[1])
+            try:
+                tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+                L = tr.losses()
+                g = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in TRN.frontend_var_names()}
+            finally:
+                tr.close()
+        finally:
+            if old is None:
+                del os.environ["TT2_TR_FUSED"]
+            else:
+                os.environ["TT2_TR_FUSED"] = old
+        res[mode] = (L, g)
+    (La, ga), (Lb, gb) = res["1"], res["0"]
+    for k in ("before", "after"):
+        assert abs(La[k] - Lb[k]) < 1e-4 * abs(Lb[k]), (k, La[k], Lb[k])
+    for n in ga:
+        rel = float(np.linalg.norm(ga[n] - gb[n]) / max(np.linalg.norm(gb[n]), 1e-30))
+        print("  {:90s} rel {:.3e}".format(n, rel))
+        assert rel < 2e-2, (n, rel)
