@@ -67,6 +67,39 @@ struct SplitB {
 };
 void split_weights(const float* B, int K, int N, long ldb, SplitB& out, hipStream_t s);
 
+// ---- conv1d 'same' over pre-split activation planes ---------------------------
+// Activations between stacked conv layers live as two fp16 planes (hi, lo of x·2^4, the split
+// GemmArgs::split16 == 1 applies at load) in a PADDED row layout: CX_G guard rows, then for every
+// batch row b the CX_P zero rows, its T frames, CX_P zero rows (Tp = T + 2·CX_P rows per b), then
+// guard rows up to the 256-row tile multiple + CX_G.  Channel stride Cp (C rounded up to 32, zero
+// padded).  A conv tap is then a plain row shift, so the product streams dense 16-byte rows with no
+// im2col arithmetic and no per-load split, and the producing layer writes the next layer's planes
+// from its epilogue (pad rows as zeros).
+constexpr int CX_P = 2, CX_G = 2, CX_BM = 128, CX_BN = 128;
+inline long cx_rows(int B, int T) { return 2L * CX_G + (((long)B * (T + 2 * CX_P) + 255) / 256) * 256; }
+struct ConvX3Args {
+  const _Float16 *Ah = nullptr, *Al = nullptr;  // input planes (allocation base: guard rows first)
+  int Cp = 0;                                   // input channel stride (multiple of 32)
+  int B = 0, T = 0, kw = 1;                     // 'same' conv of width kw (odd, <= 2·CX_P + 1)
+  const _Float16 *Bh = nullptr, *Bl = nullptr;  // weights [N][ldbt], k = tap·Cp + c (split_conv_weights)
+  long ldbt = 0;
+  int N = 0;
+  const float *bias = nullptr, *bn_scale = nullptr, *bn_shift = nullptr;
+  int act = ACT_NONE;
+  _Float16 *Oh = nullptr, *Ol = nullptr;  // split output planes, channel stride N (N % 128 == 0), or
+  float* Cout = nullptr;                  // fp32 output rows b·T + t (stride ldc) with residual / clip
+  long ldc = 0;
+  const float* residual = nullptr;
+  long ldr = 0;
+  int clip = 0;
+  float clip_lo = 0.f, clip_hi = 0.f;
+};
+void conv_x3(const ConvX3Args& a, hipStream_t s);
+// fp32 X[b][t][c] (batch stride xs_b, frame stride C) -> padded planes (zero pads, channels C..Cp)
+void split_rows(const float* X, int B, int T, int C, long xs_b, _Float16* hi, _Float16* lo, int Cp, hipStream_t s);
+// conv weight W[kw][C][N] fp32 -> pre-scaled split planes [N][kw·Cp] (zero for c >= C)
+void split_conv_weights(const float* W, int kw, int C, int Cp, int N, SplitB& out, hipStream_t s);
+
 void gemm(const GemmArgs& a, hipStream_t s);
 // Same product, but the raw fp32 partial sums are left in a.kpart as [ks][M][N] (no epilogue, no
 // combine launch; ks >= 1 is returned) for a caller-fused combine.  a.kpart is required.

@@ -741,6 +741,422 @@ void split_weights(const float* B, int K, int N, long ldb, SplitB& out, hipStrea
   TT2_HIP(hipGetLastError());
 }
 
+// ---- conv1d over pre-split activation planes (gemm.h ConvX3Args) ---------------
+// In the padded row layout a tap is a row shift, so with Cp the channel stride the operand is the
+// overlapping-row view A[m][k] = plane[(CX_G + m - pad)·Cp + k], k = tap·Cp + c: a dense row-major
+// matrix of row stride Cp over K = kw·Cp.  Same block tile, split and MFMA order as
+// gemm_x3_kernel<·, 1, 2, true> (so the result matches the im2col path bit for bit when C == Cp);
+// the blockIdx -> tile map keeps the N tiles of one row tile on one XCD (shared A rows in its L2);
+// the planes epilogue stages the 128 x 128 output tile in LDS and writes whole 16-byte chunks.
+__global__ void k_split_rows(const float* __restrict__ X, int B, int T, int C, long xs_b, _Float16* __restrict__ hi,
+                             _Float16* __restrict__ lo, int Cp, long rows) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * Cp) return;
+  const long r = i / Cp;
+  const int c = (int)(i - r * Cp);
+  const long rr = r - CX_G;
+  const int Tp = T + 2 * CX_P;
+  float x = 0.f;
+  if (rr >= 0 && rr < (long)B * Tp && c < C) {
+    const int b = (int)(rr / Tp), t = (int)(rr - (long)b * Tp) - CX_P;
+    if (t >= 0 && t < T) x = X[b * xs_b + (long)t * C + c];
+  }
+  x *= X3_SA;
+  const _Float16 h = (_Float16)x;
+  hi[i] = h;
+  lo[i] = (_Float16)(x - (float)h);
+}
+
+__global__ void k_split_conv_w(const float* __restrict__ W, int kw, int C, int Cp, int N, _Float16* __restrict__ hi,
+                               _Float16* __restrict__ lo) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = kw * Cp;
+  if (i >= (long)N * K) return;
+  const int n = (int)(i / K), k = (int)(i - (long)n * K), tap = k / Cp, c = k - tap * Cp;
+  const float x = c < C ? W[((long)tap * C + c) * N + n] * X3_SB : 0.f;
+  const _Float16 h = (_Float16)x;
+  hi[i] = h;
+  lo[i] = (_Float16)(x - (float)h);
+}
+
+// Per-column epilogue constants (bias, BN scale / shift; the identity when absent), loaded once
+// per thread, and the activation as a compile-time branch of one uniform dispatch: the element
+// loops are straight-line code with no loads in them.
+struct CxCol {
+  float b, s, h;
+};
+__device__ __forceinline__ CxCol cx_col(const ConvX3Args& g, int col) {
+  CxCol c;
+  c.b = g.bias ? g.bias[col] : 0.f;
+  c.s = g.bn_scale ? g.bn_scale[col] : 1.f;
+  c.h = g.bn_shift ? g.bn_shift[col] : 0.f;
+  return c;
+}
+// tanh = 1 - 2 / (e^{2x} + 1) on v_exp_f32 + v_rcp_f32: |abs err| < 3e-7 (libm tanhf: ~10x the
+// instructions, which made the 65k-element epilogue of a 256 x 256 tile cost ~20 us per layer)
+__device__ __forceinline__ float cx_tanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * x) + 1.f); }
+template <int ACT>
+__device__ __forceinline__ float cx_epi(float acc, const CxCol& c) {
+  float y = acc * X3_UNSCALE + c.b;
+  if constexpr (ACT == ACT_RELU) y = fmaxf(y, 0.f);
+  if constexpr (ACT == ACT_TANH) y = cx_tanh(y);
+  y = y * c.s + c.h;
+  if constexpr (ACT == ACT_BN_RELU) y = fmaxf(y, 0.f);
+  return y;
+}
+template <class F>
+__device__ __forceinline__ void cx_act(int act, F&& f) {
+  if (act == ACT_TANH) f(std::integral_constant<int, ACT_TANH>{});
+  else if (act == ACT_RELU) f(std::integral_constant<int, ACT_RELU>{});
+  else if (act == ACT_BN_RELU) f(std::integral_constant<int, ACT_BN_RELU>{});
+  else f(std::integral_constant<int, ACT_NONE>{});
+}
+
+template <bool F32OUT>
+__global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvX3Args g, int n_mt, int n_nt) {
+  constexpr int BK = X3_BK, LD = X3_LD, OLD = CX_BN + 8;
+  __shared__ __attribute__((aligned(16))) _Float16 sm[2][2][CX_BM + CX_BN][LD];  // [plane][buf][A rows | B cols][k]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int mt = (jb / n_nt) * 8 + xcd, nt = jb - (jb / n_nt) * n_nt;
+  if (mt >= n_mt) return;
+  const int m0 = mt * CX_BM, n0 = nt * CX_BN;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int am = tid >> 1, ak = (tid & 1) * 16;    // A: row am, k [ak, ak + 16)
+  const int bn = tid & 127, bk = (tid >> 7) * 16;  // B: column bn, k [bk, bk + 16)
+  const int pad = (g.kw - 1) >> 1;
+  const long aoff = (long)(CX_G + m0 + am - pad) * g.Cp + ak;
+  const _Float16* pah = g.Ah + aoff;
+  const _Float16* pal = g.Al + aoff;
+  const bool bok = n0 + bn < g.N;
+  const long boff = (long)(bok ? n0 + bn : 0) * g.ldbt + bk;
+  const _Float16* pbh = g.Bh + boff;
+  const _Float16* pbl = g.Bl + boff;
+  const int nk = g.kw * g.Cp / BK;
+  f16x8 ra[2][2], rb[2][2];  // [plane][8-k half]
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  auto gload = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      ra[0][h] = *reinterpret_cast<const f16x8*>(pah + k0 + 8 * h);
+      ra[1][h] = *reinterpret_cast<const f16x8*>(pal + k0 + 8 * h);
+      if (bok) {
+        rb[0][h] = *reinterpret_cast<const f16x8*>(pbh + k0 + 8 * h);
+        rb[1][h] = *reinterpret_cast<const f16x8*>(pbl + k0 + 8 * h);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rb[0][h][e] = rb[1][h][e] = (_Float16)0.f;
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        *reinterpret_cast<f16x8*>(&sm[p][buf][am][ak + 8 * h]) = ra[p][h];
+        *reinterpret_cast<f16x8*>(&sm[p][buf][CX_BM + bn][bk + 8 * h]) = rb[p][h];
+      }
+  };
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int r = lane & 31, h8 = (lane >> 5) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+#pragma unroll
+    for (int s16 = 0; s16 < BK; s16 += 16) {
+      f16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = *reinterpret_cast<const f16x8*>(&sm[0][cur][wm * 64 + i * 32 + r][s16 + h8]);
+        al[i] = *reinterpret_cast<const f16x8*>(&sm[1][cur][wm * 64 + i * 32 + r][s16 + h8]);
+        bh[i] = *reinterpret_cast<const f16x8*>(&sm[0][cur][CX_BM + wn * 64 + i * 32 + r][s16 + h8]);
+        bl[i] = *reinterpret_cast<const f16x8*>(&sm[1][cur][CX_BM + wn * 64 + i * 32 + r][s16 + h8]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue: padded row m -> (b, t); pad rows (and rows past B·Tp) are not frames
+  const int Tp = g.T + 2 * CX_P;
+  const long mrows = (long)g.B * Tp;
+  _Float16* ot = &sm[0][0][0][0];  // [plane][128][OLD] output tile (the loop's last barrier freed LDS)
+  int orow[2][16];                 // output row b·T + t of (i, q), -1 for pad / tail rows
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int mb0 = m0 + wm * 64 + i * 32 + 4 * (lane >> 5), b0 = mb0 / Tp, t00 = mb0 - b0 * Tp;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rq = (q & 3) + 8 * (q >> 2);
+      int t = t00 + rq, b = b0;
+      while (t >= Tp) { t -= Tp; ++b; }
+      const bool frame = (long)mb0 + rq < mrows && t >= CX_P && t < CX_P + g.T;
+      orow[i][q] = frame ? b * g.T + (t - CX_P) : -1;
+    }
+  }
+  CxCol cc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) cc[j] = cx_col(g, min(n0 + wn * 64 + j * 32 + (lane & 31), g.N - 1));
+  if constexpr (F32OUT) {
+    float res[2][2][16];  // residual operands, all loads issued before any use
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int col = min(n0 + wn * 64 + j * 32 + (lane & 31), g.N - 1);
+          res[i][j][q] = g.residual ? g.residual[(long)max(orow[i][q], 0) * g.ldr + col] : 0.f;
+        }
+    cx_act(g.act, [&](auto A) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            float y = res[i][j][q] + cx_epi<decltype(A)::value>(acc[i][j][q], cc[j]);
+            if (g.clip) y = fminf(fmaxf(y, g.clip_lo), g.clip_hi);
+            if (orow[i][q] >= 0 && col < g.N) g.Cout[(long)orow[i][q] * g.ldc + col] = y;
+          }
+        }
+    });
+  } else {
+    cx_act(g.act, [&](auto A) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rl = wm * 64 + i * 32 + 4 * (lane >> 5) + (q & 3) + 8 * (q >> 2);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int cl = wn * 64 + j * 32 + (lane & 31);
+            const float y = orow[i][q] >= 0 ? cx_epi<decltype(A)::value>(acc[i][j][q], cc[j]) * X3_SA : 0.f;
+            const _Float16 hv = (_Float16)y;
+            ot[rl * OLD + cl] = hv;
+            ot[CX_BM * OLD + rl * OLD + cl] = (_Float16)(y - (float)hv);
+          }
+        }
+    });
+  }
+  if constexpr (!F32OUT) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = tid + 256 * u, p = idx >> 11, rl = (idx >> 4) & 127, ch = idx & 15;
+      const long m = (long)m0 + rl;
+      if (m < mrows)
+        *reinterpret_cast<f16x8*>((p ? g.Ol : g.Oh) + (CX_G + m) * g.N + n0 + 8 * ch) =
+            *reinterpret_cast<const f16x8*>(ot + p * CX_BM * OLD + rl * OLD + 8 * ch);
+    }
+  }
+}
+
+// Wide form for planes output with N % 256 == 0 (the 512-channel Postnet layers): 256 x 256 tile,
+// 8 waves (2 along M x 4 along N, wave tile 128 x 64 = 4 x 2 accumulators), one work-group per CU.
+// Operands are staged by LDS-DMA (global_load_lds, 16 B per lane) into a lane-linear image of
+// 64-byte rows (32 k of one operand plane); the 16-byte chunks of row R sit XOR-swizzled by
+// (R >> 2) & 3, applied on the DMA source address and on the fragment read, so the 16 lanes of a
+// ds_read_b128 group hit 16 distinct bank slots.  Two stages: the next k-step's DMA is issued
+// before the current step's 48 MFMAs per wave and retired (vmcnt 0 + barrier) after them.
+constexpr int CXW_BM = 256, CXW_BN = 256, CXW_PLANE = 256 * X3_BK, CXW_OLD = CXW_BN + 8;
+constexpr int CXW_LDS = (2 * 4 * CXW_PLANE > CXW_BM * CXW_OLD) ? 2 * 4 * CXW_PLANE : CXW_BM * CXW_OLD;  // halfs
+
+template <int ACT>
+__device__ __forceinline__ void cxw_apply(f32x16 (&acc)[4][2], const unsigned (&fm)[4], const CxCol (&cc)[2]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j][q] = ((fm[i] >> q) & 1u) ? cx_epi<ACT>(acc[i][j][q], cc[j]) * X3_SA : 0.f;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt, int n_nt) {
+  __shared__ __attribute__((aligned(16))) _Float16 sm[CXW_LDS];  // [stage][A hi, A lo, B hi, B lo][256][32]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int mt = (jb / n_nt) * 8 + xcd, nt = jb - (jb / n_nt) * n_nt;
+  if (mt >= n_mt) return;
+  const int m0 = mt * CXW_BM, n0 = nt * CXW_BN;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int pad = (g.kw - 1) >> 1;
+  // DMA pieces: wave w fills rows [32w, 32w + 32) of every plane as two 16-row pieces; lane l lands
+  // at row (l >> 2), physical chunk l & 3, and fetches logical chunk (l & 3) ^ ((l >> 4) & 3)
+  const int srow = 32 * wave + (lane >> 2), sc = (lane & 3) ^ ((lane >> 4) & 3);
+  const _Float16 *ga[2][2], *gb[2][2];  // [plane][piece]
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long ao = (long)(CX_G + m0 + srow + 16 * i - pad) * g.Cp + 8 * sc;
+    const long bo = (long)(n0 + srow + 16 * i) * g.ldbt + 8 * sc;
+    ga[0][i] = g.Ah + ao;
+    ga[1][i] = g.Al + ao;
+    gb[0][i] = g.Bh + bo;
+    gb[1][i] = g.Bl + bo;
+  }
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  auto stage = [&](int kt, int buf) {
+    const int k0 = kt * X3_BK;
+    _Float16* base = sm + buf * 4 * CXW_PLANE + 32 * wave * X3_BK;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        __builtin_amdgcn_global_load_lds(ga[p][i] + k0, (lds_ptr)(base + p * CXW_PLANE + 16 * i * X3_BK), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(gb[p][i] + k0, (lds_ptr)(base + (2 + p) * CXW_PLANE + 16 * i * X3_BK), 16, 0, 0);
+      }
+  };
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  const int nk = g.kw * g.Cp / X3_BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int r = lane & 31, hl = lane >> 5, sw = (r >> 2) & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const _Float16* S = sm + cur * 4 * CXW_PLANE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int off = r * X3_BK + 8 * ((2 * s + hl) ^ sw);
+      f16x8 bh[2], bl[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bh[j] = *reinterpret_cast<const f16x8*>(S + 2 * CXW_PLANE + (wn * 64 + j * 32) * X3_BK + off);
+        bl[j] = *reinterpret_cast<const f16x8*>(S + 3 * CXW_PLANE + (wn * 64 + j * 32) * X3_BK + off);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(S + (wm * 128 + i * 32) * X3_BK + off);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(S + CXW_PLANE + (wm * 128 + i * 32) * X3_BK + off);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // epilogue: y·2^4 in place (pad rows and rows past B·Tp -> 0), then each plane through LDS
+  const int Tp = g.T + 2 * CX_P;
+  const long mrows = (long)g.B * Tp;
+  unsigned fm[4] = {0u, 0u, 0u, 0u};  // frame bit of (i, q)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int mb0 = m0 + wm * 128 + i * 32 + 4 * hl, b0 = mb0 / Tp, t00 = mb0 - b0 * Tp;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rq = (q & 3) + 8 * (q >> 2);
+      int t = t00 + rq;
+      while (t >= Tp) t -= Tp;
+      if ((long)mb0 + rq < mrows && t >= CX_P && t < CX_P + g.T) fm[i] |= 1u << q;
+    }
+  }
+  CxCol cc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) cc[j] = cx_col(g, n0 + wn * 64 + j * 32 + r);
+  cxw_apply<ACT>(acc, fm, cc);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if (p) __syncthreads();  // the hi plane's copy-out has read the tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int rl = wm * 128 + i * 32 + 4 * hl + (q & 3) + 8 * (q >> 2);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float v = acc[i][j][q];
+          const _Float16 hv = (_Float16)v;
+          sm[rl * CXW_OLD + wn * 64 + j * 32 + r] = p ? (_Float16)(v - (float)hv) : hv;
+        }
+      }
+    __syncthreads();
+    _Float16* O = p ? g.Ol : g.Oh;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = tid + 512 * u, rl = idx >> 5, ch = idx & 31;
+      const long m = (long)m0 + rl;
+      if (m < mrows)
+        *reinterpret_cast<f16x8*>(O + (CX_G + m) * g.N + n0 + 8 * ch) =
+            *reinterpret_cast<const f16x8*>(sm + rl * CXW_OLD + 8 * ch);
+    }
+  }
+}
+
+void split_rows(const float* X, int B, int T, int C, long xs_b, _Float16* hi, _Float16* lo, int Cp, hipStream_t s) {
+  const long rows = cx_rows(B, T), n = rows * Cp;
+  hipLaunchKernelGGL(k_split_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, X, B, T, C, xs_b, hi, lo, Cp, rows);
+  TT2_HIP(hipGetLastError());
+}
+
+void split_conv_weights(const float* W, int kw, int C, int Cp, int N, SplitB& out, hipStream_t s) {
+  out.ldbt = (long)kw * Cp;
+  const size_t n = (size_t)N * out.ldbt;
+  out.hi.alloc(n * sizeof(_Float16));
+  out.lo.alloc(n * sizeof(_Float16));
+  hipLaunchKernelGGL(k_split_conv_w, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, kw, C, Cp, N,
+                     out.hi.as<_Float16>(), out.lo.as<_Float16>());
+  TT2_HIP(hipGetLastError());
+}
+
+void conv_x3(const ConvX3Args& a, hipStream_t s) {
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  TT2_CHECK(a.B > 0 && a.T > 0 && a.N > 0 && a.Cp > 0 && a.Cp % X3_BK == 0 && (a.kw & 1) && a.kw <= 2 * CX_P + 1,
+            TT2_ERR_SHAPE_MISMATCH, "conv_x3: needs Cp % 32 == 0 and an odd kw <= 5");
+  TT2_CHECK(a.Ah && a.Al && a.Bh && a.Bl && a16(a.Ah) && a16(a.Al) && a16(a.Bh) && a16(a.Bl) &&
+                a.ldbt >= (long)a.kw * a.Cp && a.ldbt % 8 == 0,
+            TT2_ERR_INVALID_ARG, "conv_x3: operand planes missing or misaligned");
+  TT2_CHECK((a.Oh != nullptr) != (a.Cout != nullptr), TT2_ERR_INVALID_ARG, "conv_x3: exactly one output");
+  TT2_CHECK(!a.Oh || (a.Ol && a.N % CX_BN == 0 && a16(a.Oh) && a16(a.Ol)), TT2_ERR_INVALID_ARG,
+            "conv_x3: planes output needs N % 128 == 0 and aligned planes");
+  const char* ew = std::getenv("TT2_CX_WIDE");  // 0: the 128 x 128 register-staged kernel for every layer
+  const bool wide = !ew || std::atoi(ew) != 0;
+  if (wide && a.Oh && a.N % CXW_BN == 0) {
+    const int n_mt = cdiv(a.B * (a.T + 2 * CX_P), CXW_BM), n_nt = a.N / CXW_BN;
+    const dim3 grid((unsigned)(cdiv(n_mt, 8) * 8 * n_nt));
+    if (a.act == ACT_TANH) hipLaunchKernelGGL(conv_x3w_kernel<ACT_TANH>, grid, dim3(512), 0, s, a, n_mt, n_nt);
+    else if (a.act == ACT_RELU) hipLaunchKernelGGL(conv_x3w_kernel<ACT_RELU>, grid, dim3(512), 0, s, a, n_mt, n_nt);
+    else if (a.act == ACT_BN_RELU) hipLaunchKernelGGL(conv_x3w_kernel<ACT_BN_RELU>, grid, dim3(512), 0, s, a, n_mt, n_nt);
+    else hipLaunchKernelGGL(conv_x3w_kernel<ACT_NONE>, grid, dim3(512), 0, s, a, n_mt, n_nt);
+    TT2_HIP(hipGetLastError());
+    return;
+  }
+  const int n_mt = cdiv(a.B * (a.T + 2 * CX_P), CX_BM), n_nt = cdiv(a.N, CX_BN);
+  const dim3 grid((unsigned)(cdiv(n_mt, 8) * 8 * n_nt));
+  if (a.Cout) hipLaunchKernelGGL(conv_x3_kernel<true>, grid, dim3(256), 0, s, a, n_mt, n_nt);
+  else hipLaunchKernelGGL(conv_x3_kernel<false>, grid, dim3(256), 0, s, a, n_mt, n_nt);
+  TT2_HIP(hipGetLastError());
+}
+
 int gemm_raw(const GemmArgs& a, hipStream_t s) {
   TT2_CHECK(a.kpart, TT2_ERR_INVALID_ARG, "gemm_raw: kpart required");
   GemmArgs g = a;

@@ -1335,6 +1335,11 @@ struct tt2_ctx {
   tt2::DevBuf post_cw[8], post_cb[8], post_bs[8], post_bh[8], post_pw, post_pb;
   // pre-split fp16 planes of the static conv / projection weights (split16 GEMMs, gemm.h SplitB)
   tt2::SplitB enc_cw_s[8], post_cw_s[8], post_pw_s, mem_k_s;
+  // Postnet over pre-split padded planes (gemm.h conv_x3): conv 1's weights at Cp = nm rounded to 32,
+  // the input planes of conv 1 and two ping-pong plane pairs; post_cx = 0 runs the im2col GEMMs
+  tt2::SplitB post_cx0_s;
+  tt2::DevBuf px_in_h, px_in_l, px_h[2], px_l[2];
+  bool post_cx = false;
   // activations
   tt2::DevBuf refxg;  // reference-encoder GRU input projections [B][T2][3D]
   tt2::DevBuf enc_hg;  // persistent BiLSTM h granules [2][2][32 x U] + timeout word
@@ -1718,6 +1723,9 @@ static void finalize(tt2_ctx* c) {
   }
   upload(c->post_pw, need(wm, P + "postnet_projection/projection_postnet_projection/kernel", {c->PC, c->nm}));
   split_weights(c->post_pw.as<float>(), c->PC, c->nm, c->nm, c->post_pw_s, nullptr);
+  if (c->post_cx)
+    split_conv_weights(c->post_cw[0].as<float>(), cfg.postnet_kernel_size, c->nm, (c->nm + 31) / 32 * 32, c->PC,
+                       c->post_cx0_s, nullptr);
   TT2_HIP(hipDeviceSynchronize());
   upload(c->post_pb, need(wm, P + "postnet_projection/projection_postnet_projection/bias", {c->nm}));
   c->finalized = true;
@@ -1787,6 +1795,20 @@ static void alloc_acts(tt2_ctx* c) {
   c->post_a.alloc(B * MI * std::max(c->PC, c->nm) * 4);
   c->post_b.alloc(B * MI * std::max(c->PC, c->nm) * 4);
   c->mel.alloc(B * MI * c->nm * 4);
+  {  // conv_x3 Postnet: TT2_POSTNET_CX=0 selects the im2col GEMMs
+    const char* e = std::getenv("TT2_POSTNET_CX");
+    c->post_cx = (!e || std::atoi(e) != 0) && c->PC % CX_BN == 0 && (cfg.postnet_kernel_size & 1) &&
+                 cfg.postnet_kernel_size <= 2 * CX_P + 1;
+  }
+  if (c->post_cx) {
+    const long rows = cx_rows((int)B, (int)MI), cp0 = (c->nm + 31) / 32 * 32;
+    c->px_in_h.alloc(rows * cp0 * 2);
+    c->px_in_l.alloc(rows * cp0 * 2);
+    for (int i = 0; i < 2; ++i) {
+      c->px_h[i].alloc(rows * c->PC * 2);
+      c->px_l[i].alloc(rows * c->PC * 2);
+    }
+  }
   TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ctl_host), 4 * sizeof(int)));
 }
 
@@ -2387,6 +2409,30 @@ static void postnet_dev(tt2_ctx* c, const float* frames_d, long frames_bstride, 
   hipLaunchKernelGGL(k_clip_frames, dim3((unsigned)std::min<long>(cdiv((int)std::min<long>(n, 1L << 30), 256), 4096)),
                      dim3(256), 0, s, frames_d, frames_bstride, dec_d, B, T, c->nm, lo, hi, cfg.clip_outputs);
   TT2_HIP(hipGetLastError());
+  if (c->post_cx) {  // padded split planes between the layers (gemm.h conv_x3)
+    const int cp0 = (c->nm + 31) / 32 * 32;
+    split_rows(dec_d, B, T, c->nm, (long)T * c->nm, c->px_in_h.as<_Float16>(), c->px_in_l.as<_Float16>(), cp0, s);
+    const _Float16 *ih = c->px_in_h.as<_Float16>(), *il = c->px_in_l.as<_Float16>();
+    int cp = cp0;
+    for (int i = 0; i < cfg.postnet_num_layers; ++i) {
+      const SplitB& w = i == 0 ? c->post_cx0_s : c->post_cw_s[i];
+      ConvX3Args a;
+      a.Ah = ih; a.Al = il; a.Cp = cp; a.B = B; a.T = T; a.kw = cfg.postnet_kernel_size;
+      a.Bh = w.hi.as<_Float16>(); a.Bl = w.lo.as<_Float16>(); a.ldbt = w.ldbt; a.N = c->PC;
+      a.bias = c->post_cb[i].as<float>(); a.act = (i < cfg.postnet_num_layers - 1) ? ACT_TANH : ACT_NONE;
+      a.bn_scale = c->post_bs[i].as<float>(); a.bn_shift = c->post_bh[i].as<float>();
+      a.Oh = c->px_h[i & 1].as<_Float16>(); a.Ol = c->px_l[i & 1].as<_Float16>();
+      conv_x3(a, s);
+      ih = a.Oh; il = a.Ol; cp = c->PC;
+    }
+    ConvX3Args a;  // projection = a width-1 conv over the last planes, + residual, clip
+    a.Ah = ih; a.Al = il; a.Cp = cp; a.B = B; a.T = T; a.kw = 1;
+    a.Bh = c->post_pw_s.hi.as<_Float16>(); a.Bl = c->post_pw_s.lo.as<_Float16>(); a.ldbt = c->post_pw_s.ldbt;
+    a.N = c->nm; a.bias = c->post_pb.as<float>(); a.Cout = mel_d; a.ldc = c->nm;
+    a.residual = dec_d; a.ldr = c->nm; a.clip = cfg.clip_outputs; a.clip_lo = lo; a.clip_hi = hi;
+    conv_x3(a, s);
+    return;
+  }
   const float* xin = dec_d;
   float* bufs[2] = {c->post_a.as<float>(), c->post_b.as<float>()};
   int cin = c->nm;

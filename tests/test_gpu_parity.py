@@ -158,6 +158,31 @@ def test_postnet_standalone(small_setup):
     eng.close()
 
 
+@pytest.mark.parametrize("B,T", [(4, 150), (3, 1), (5, 61)])
+def test_postnet_planes_path_full_dims(full_setup, monkeypatch, B, T):
+    """512-channel Postnet over pre-split padded planes (gemm.h conv_x3) against the
+    oracle and against the im2col GEMM path (TT2_POSTNET_CX=0); T=1 and B·(T+4) not a multiple of
+    the 128-row tile cover the pad / guard rows."""
+    hp, W = full_setup
+    rng = np.random.default_rng(40 + T)
+    frames = rng.uniform(-5, 5, (B, T, hp.num_mels)).astype(np.float32)
+    outs = {}
+    for cx, wide in (("1", "1"), ("1", "0"), ("0", "1")):
+        monkeypatch.setenv("TT2_POSTNET_CX", cx)
+        monkeypatch.setenv("TT2_CX_WIDE", wide)
+        eng = _engine(hp, W, B, 8, 64, T)
+        outs[cx + wide] = eng.postnet(frames)
+        eng.close()
+    rd, rm = TR.postnet_and_clip(frames, W, oracle_hp(hp))
+    for k in ("11", "10"):  # 256 x 256 LDS-DMA kernel, 128 x 128 register-staged kernel
+        np.testing.assert_allclose(outs[k][0], rd, atol=1e-6)
+        np.testing.assert_allclose(outs[k][1], rm, atol=MEL_TOL)
+    # same split, same MFMA order: the planes kernels agree bit for bit; the im2col path differs
+    # only in conv 1's k grouping
+    np.testing.assert_array_equal(outs["11"][1], outs["10"][1])
+    np.testing.assert_allclose(outs["11"][1], outs["01"][1], atol=1e-5)
+
+
 def test_full_dims_free_run(full_setup):
     """Fork-default dimensions (D_mem 1024, 2x1024 LSTM, 512-ch postnet), short horizon."""
     hp, W = full_setup
