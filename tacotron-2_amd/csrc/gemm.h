@@ -93,6 +93,12 @@ struct ConvX3Args {
   long ldr = 0;
   int clip = 0;
   float clip_lo = 0.f, clip_hi = 0.f;
+  // split-K for few-row products (the text encoder's 6.4k rows): ks > 1 slices K over blockIdx.y
+  // of the 128 x 128 kernel, raw fp32 partials [ks][B·Tp][N] go to part (>= part_floats floats,
+  // stream-ordered) and one reduce launch applies the epilogue and writes the output
+  int ks = 1;
+  float* part = nullptr;
+  long part_floats = 0;
 };
 void conv_x3(const ConvX3Args& a, hipStream_t s);
 // fp32 X[b][t][c] (batch stride xs_b, frame stride C) -> padded planes (zero pads, channels C..Cp)

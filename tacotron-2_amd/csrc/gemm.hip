@@ -812,6 +812,14 @@ __device__ __forceinline__ void cx_act(int act, F&& f) {
   else f(std::integral_constant<int, ACT_NONE>{});
 }
 
+// k-step order: 32-channel chunk major, tap minor (k0 = tap·Cp + 32·chunk), so the kw taps that
+// re-read one row block (shifted by one row each) run back to back and hit L2; tap-major order
+// re-streamed the A rows from MALL once per tap (~5x the unique operand bytes)
+__device__ __forceinline__ int cx_k0(int kt, int kw, int Cp) {
+  const int chunk = kt / kw;
+  return (kt - chunk * kw) * Cp + chunk * X3_BK;
+}
+
 template <bool F32OUT>
 __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvX3Args g, int n_mt, int n_nt) {
   constexpr int BK = X3_BK, LD = X3_LD, OLD = CX_BN + 8;
@@ -825,6 +833,9 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvX3Args g, int n_mt,
   const int am = tid >> 1, ak = (tid & 1) * 16;    // A: row am, k [ak, ak + 16)
   const int bn = tid & 127, bk = (tid >> 7) * 16;  // B: column bn, k [bk, bk + 16)
   const int pad = (g.kw - 1) >> 1;
+  // split-K slice blockIdx.y of gridDim.y: k-steps [kt0, kt0 + nk)
+  const int nkt = g.kw * g.Cp / BK, per = (nkt + gridDim.y - 1) / gridDim.y, kt0 = blockIdx.y * per;
+  const int nk = min(nkt, kt0 + per) - kt0;
   const long aoff = (long)(CX_G + m0 + am - pad) * g.Cp + ak;
   const _Float16* pah = g.Ah + aoff;
   const _Float16* pal = g.Al + aoff;
@@ -832,7 +843,6 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvX3Args g, int n_mt,
   const long boff = (long)(bok ? n0 + bn : 0) * g.ldbt + bk;
   const _Float16* pbh = g.Bh + boff;
   const _Float16* pbl = g.Bl + boff;
-  const int nk = g.kw * g.Cp / BK;
   f16x8 ra[2][2], rb[2][2];  // [plane][8-k half]
   f32x16 acc[2][2];
 #pragma unroll
@@ -842,7 +852,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvX3Args g, int n_mt,
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
   auto gload = [&](int kt) {
-    const int k0 = kt * BK;
+    const int k0 = cx_k0(kt0 + kt, g.kw, g.Cp);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       ra[0][h] = *reinterpret_cast<const f16x8*>(pah + k0 + 8 * h);
@@ -897,6 +907,21 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvX3Args g, int n_mt,
   // epilogue: padded row m -> (b, t); pad rows (and rows past B·Tp) are not frames
   const int Tp = g.T + 2 * CX_P;
   const long mrows = (long)g.B * Tp;
+  if (g.ks > 1) {  // raw partials of this K slice (padded rows), reduced by k_cx_reduce
+    float* P = g.part + (long)blockIdx.y * mrows * g.N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const long m = m0 + wm * 64 + i * 32 + 4 * (lane >> 5) + (q & 3) + 8 * (q >> 2);
+          if (m < mrows && col < g.N) P[m * g.N + col] = acc[i][j][q];
+        }
+      }
+    return;
+  }
   _Float16* ot = &sm[0][0][0][0];  // [plane][128][OLD] output tile (the loop's last barrier freed LDS)
   int orow[2][16];                 // output row b·T + t of (i, q), -1 for pad / tail rows
 #pragma unroll
@@ -1015,7 +1040,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt
   }
   typedef __attribute__((address_space(3))) void* lds_ptr;
   auto stage = [&](int kt, int buf) {
-    const int k0 = kt * X3_BK;
+    const int k0 = cx_k0(kt, g.kw, g.Cp);
     _Float16* base = sm + buf * 4 * CXW_PLANE + 32 * wave * X3_BK;
 #pragma unroll
     for (int p = 0; p < 2; ++p)
@@ -1112,6 +1137,44 @@ __global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt
   }
 }
 
+// split-K combine of conv_x3_kernel partials: 4 consecutive channels of one padded row per thread,
+// the same epilogue as the kernels (planes with zero pad rows, or fp32 frame rows + residual / clip)
+template <int ACT>
+__global__ __launch_bounds__(256) void k_cx_reduce(ConvX3Args g, long mrows) {
+  const int n4 = g.N >> 2;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= mrows * n4) return;
+  const long m = i / n4;
+  const int c = (int)(i - m * n4) * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < g.ks; ++z) acc += *reinterpret_cast<const f32x4*>(g.part + ((long)z * mrows + m) * g.N + c);
+  const int Tp = g.T + 2 * CX_P, b = (int)(m / Tp), t = (int)(m - (long)b * Tp) - CX_P;
+  const bool frame = t >= 0 && t < g.T;
+  float y[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) y[e] = frame ? cx_epi<ACT>(acc[e], cx_col(g, c + e)) : 0.f;
+  if (g.Oh) {
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    f16x4 h, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x = y[e] * X3_SA;
+      h[e] = (_Float16)x;
+      l[e] = (_Float16)(x - (float)h[e]);
+    }
+    *reinterpret_cast<f16x4*>(g.Oh + (CX_G + m) * g.N + c) = h;
+    *reinterpret_cast<f16x4*>(g.Ol + (CX_G + m) * g.N + c) = l;
+  } else if (frame) {
+    const long orow = (long)b * g.T + t;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = y[e] + (g.residual ? g.residual[orow * g.ldr + c + e] : 0.f);
+      if (g.clip) v = fminf(fmaxf(v, g.clip_lo), g.clip_hi);
+      g.Cout[orow * g.ldc + c + e] = v;
+    }
+  }
+}
+
 void split_rows(const float* X, int B, int T, int C, long xs_b, _Float16* hi, _Float16* lo, int Cp, hipStream_t s) {
   const long rows = cx_rows(B, T), n = rows * Cp;
   hipLaunchKernelGGL(k_split_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, X, B, T, C, xs_b, hi, lo, Cp, rows);
@@ -1140,6 +1203,22 @@ void conv_x3(const ConvX3Args& a, hipStream_t s) {
             "conv_x3: planes output needs N % 128 == 0 and aligned planes");
   const char* ew = std::getenv("TT2_CX_WIDE");  // 0: the 128 x 128 register-staged kernel for every layer
   const bool wide = !ew || std::atoi(ew) != 0;
+  if (a.ks > 1) {  // split K over blockIdx.y of the 128 x 128 kernel + one combine launch
+    const long mrows = (long)a.B * (a.T + 2 * CX_P);
+    TT2_CHECK(a.part && a.N % 4 == 0 && (long)a.ks * mrows * a.N <= a.part_floats && a.ks <= a.kw * a.Cp / X3_BK,
+              TT2_ERR_INVALID_ARG, "conv_x3: split-K needs part >= ks x rows x N floats, N % 4 == 0");
+    const int n_mt = cdiv(a.B * (a.T + 2 * CX_P), CX_BM), n_nt = cdiv(a.N, CX_BN);
+    const dim3 grid((unsigned)(cdiv(n_mt, 8) * 8 * n_nt), (unsigned)a.ks);
+    hipLaunchKernelGGL(conv_x3_kernel<false>, grid, dim3(256), 0, s, a, n_mt, n_nt);
+    TT2_HIP(hipGetLastError());
+    const dim3 rg((unsigned)((mrows * (a.N / 4) + 255) / 256));
+    if (a.act == ACT_TANH) hipLaunchKernelGGL(k_cx_reduce<ACT_TANH>, rg, dim3(256), 0, s, a, mrows);
+    else if (a.act == ACT_RELU) hipLaunchKernelGGL(k_cx_reduce<ACT_RELU>, rg, dim3(256), 0, s, a, mrows);
+    else if (a.act == ACT_BN_RELU) hipLaunchKernelGGL(k_cx_reduce<ACT_BN_RELU>, rg, dim3(256), 0, s, a, mrows);
+    else hipLaunchKernelGGL(k_cx_reduce<ACT_NONE>, rg, dim3(256), 0, s, a, mrows);
+    TT2_HIP(hipGetLastError());
+    return;
+  }
   if (wide && a.Oh && a.N % CXW_BN == 0) {
     const int n_mt = cdiv(a.B * (a.T + 2 * CX_P), CXW_BM), n_nt = a.N / CXW_BN;
     const dim3 grid((unsigned)(cdiv(n_mt, 8) * 8 * n_nt));

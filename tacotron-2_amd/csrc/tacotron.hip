@@ -1340,6 +1340,11 @@ struct tt2_ctx {
   tt2::SplitB post_cx0_s;
   tt2::DevBuf px_in_h, px_in_l, px_h[2], px_l[2];
   bool post_cx = false;
+  // text encoder over the same planes (conv_x3 with split K), BiLSTM input projection as a width-1
+  // conv; enc_cx = 0 runs the im2col GEMMs
+  tt2::SplitB enc_wx_s;
+  tt2::DevBuf ex_h[2], ex_l[2], ex_part;
+  bool enc_cx = false;
   // activations
   tt2::DevBuf refxg;  // reference-encoder GRU input projections [B][T2][3D]
   tt2::DevBuf enc_hg;  // persistent BiLSTM h granules [2][2][32 x U] + timeout word
@@ -1478,6 +1483,7 @@ static void finalize(tt2_ctx* c) {
     }
     upload(c->enc_wx, wx);
     upload(c->enc_bx, bx);
+    if (c->enc_cx) split_weights(c->enc_wx.as<float>(), cin, 8 * U, 8 * U, c->enc_wx_s, nullptr);
     upload(c->enc_wh, wh);
     c->kg_wmax_enc = absmax(wh);
   }
@@ -1732,6 +1738,13 @@ static void finalize(tt2_ctx* c) {
   c->st_ready = false;
 }
 
+// K split of the text-encoder convolutions on the planes path (TT2_ENC_SPLITK, 1..8; default 4)
+constexpr int kEncSplitK = 8;
+static int enc_split_k() {
+  const char* e = std::getenv("TT2_ENC_SPLITK");
+  return e ? std::max(1, std::min(kEncSplitK, std::atoi(e))) : 4;
+}
+
 static void alloc_acts(tt2_ctx* c) {
   const auto& cfg = c->cfg;
   const long B = cfg.max_batch, T = cfg.max_T_in, TR = std::max(cfg.max_T_ref, 1), MI = cfg.max_iters;
@@ -1800,6 +1813,19 @@ static void alloc_acts(tt2_ctx* c) {
     c->post_cx = (!e || std::atoi(e) != 0) && c->PC % CX_BN == 0 && (cfg.postnet_kernel_size & 1) &&
                  cfg.postnet_kernel_size <= 2 * CX_P + 1;
   }
+  {  // conv_x3 text encoder: TT2_ENC_CX=0 selects the im2col GEMMs
+    const char* e = std::getenv("TT2_ENC_CX");
+    c->enc_cx = (!e || std::atoi(e) != 0) && c->Cenc % CX_BN == 0 && c->E % 32 == 0 && (8 * c->U) % 4 == 0 &&
+                (cfg.enc_conv_kernel_size & 1) && cfg.enc_conv_kernel_size <= 2 * CX_P + 1;
+  }
+  if (c->enc_cx) {
+    const long rows = cx_rows((int)B, (int)T), w = std::max(c->E, c->Cenc);
+    for (int i = 0; i < 2; ++i) {
+      c->ex_h[i].alloc(rows * w * 2);
+      c->ex_l[i].alloc(rows * w * 2);
+    }
+    c->ex_part.alloc((size_t)kEncSplitK * B * (T + 2 * CX_P) * c->Cenc * 4);
+  }
   if (c->post_cx) {
     const long rows = cx_rows((int)B, (int)MI), cp0 = (c->nm + 31) / 32 * 32;
     c->px_in_h.alloc(rows * cp0 * 2);
@@ -1835,6 +1861,29 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
                      cfg.n_symbols);
   TT2_HIP(hipGetLastError());
   // encoder convolutions: relu inside conv, then BN (modules.py:485-497, bnorm='after')
+  if (c->enc_cx) {  // padded split planes, K split kEncSplitK ways (6.4k rows fill 204 tiles only)
+    split_rows(c->x_a.as<float>(), B, T, c->E, (long)T * c->E, c->ex_h[0].as<_Float16>(), c->ex_l[0].as<_Float16>(),
+               c->E, s);
+    int cp = c->E, cur = 0;
+    for (int i = 0; i < cfg.enc_conv_num_layers; ++i) {
+      ConvX3Args a;
+      a.Ah = c->ex_h[cur].as<_Float16>(); a.Al = c->ex_l[cur].as<_Float16>(); a.Cp = cp;
+      a.B = B; a.T = T; a.kw = cfg.enc_conv_kernel_size;
+      a.Bh = c->enc_cw_s[i].hi.as<_Float16>(); a.Bl = c->enc_cw_s[i].lo.as<_Float16>(); a.ldbt = c->enc_cw_s[i].ldbt;
+      a.N = c->Cenc; a.bias = c->enc_cb[i].as<float>(); a.act = ACT_RELU;
+      a.bn_scale = c->enc_bs[i].as<float>(); a.bn_shift = c->enc_bh[i].as<float>();
+      a.Oh = c->ex_h[cur ^ 1].as<_Float16>(); a.Ol = c->ex_l[cur ^ 1].as<_Float16>();
+      a.ks = enc_split_k(); a.part = c->ex_part.as<float>(); a.part_floats = (long)(c->ex_part.bytes / 4);
+      conv_x3(a, s);
+      cur ^= 1;
+      cp = c->Cenc;
+    }
+    ConvX3Args a;  // BiLSTM input projection x·Wx + b for both directions: a width-1 conv -> xproj rows
+    a.Ah = c->ex_h[cur].as<_Float16>(); a.Al = c->ex_l[cur].as<_Float16>(); a.Cp = cp; a.B = B; a.T = T; a.kw = 1;
+    a.Bh = c->enc_wx_s.hi.as<_Float16>(); a.Bl = c->enc_wx_s.lo.as<_Float16>(); a.ldbt = c->enc_wx_s.ldbt;
+    a.N = 8 * c->U; a.bias = c->enc_bx.as<float>(); a.Cout = c->xproj.as<float>(); a.ldc = 8 * c->U;
+    conv_x3(a, s);
+  } else {
   float* xin = c->x_a.as<float>();
   float* xout = c->x_b.as<float>();
   int cin = c->E;
@@ -1860,6 +1909,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     g.bias = c->enc_bx.as<float>();
     g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
     gemm(g, s);
+  }
   }
   zero_many({{c->enc_h.p, c->enc_h.bytes}, {c->enc_c.p, c->enc_c.bytes}, {c->enc_out.p, (size_t)BT * 2 * c->U * 4}}, s);
   int Tmax = 0;

@@ -177,10 +177,33 @@ def test_postnet_planes_path_full_dims(full_setup, monkeypatch, B, T):
     for k in ("11", "10"):  # 256 x 256 LDS-DMA kernel, 128 x 128 register-staged kernel
         np.testing.assert_allclose(outs[k][0], rd, atol=1e-6)
         np.testing.assert_allclose(outs[k][1], rm, atol=MEL_TOL)
-    # same split, same MFMA order: the planes kernels agree bit for bit; the im2col path differs
-    # only in conv 1's k grouping
+    # same split, same k-step order (chunk-major, tap-minor): the planes kernels agree bit for bit;
+    # the im2col path sums the same products in tap-major order
     np.testing.assert_array_equal(outs["11"][1], outs["10"][1])
     np.testing.assert_allclose(outs["11"][1], outs["01"][1], atol=1e-5)
+
+
+@pytest.mark.parametrize("split", ["4", "1", "7"])
+def test_encoder_planes_path_full_dims(full_setup, monkeypatch, split):
+    """Text encoder on the planes path (3 convs with K split over work-groups + the BiLSTM input
+    projection as a width-1 conv) at configs[1]'s B=32 x 201 ragged, against the
+    oracle and the im2col GEMM path (TT2_ENC_CX=0)."""
+    hp, W = full_setup
+    B, T = 32, 201
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=21)
+    monkeypatch.setenv("TT2_ENC_SPLITK", split)
+    outs = {}
+    for cx in ("1", "0"):
+        monkeypatch.setenv("TT2_ENC_CX", cx)
+        eng = _engine(hp, W, B, T, 64, 4)
+        outs[cx] = eng.encode(ids, lens, re, rs)
+        eng.close()
+    oh = oracle_hp(hp)
+    enc = TR.encoder(ids, lens, W, oh)
+    st = TR.style_embedding(re, rs, W, oh)
+    vals, _ = TR.memory_and_keys(enc, st, lens, W)
+    np.testing.assert_allclose(outs["1"][0], vals, atol=1e-4)
+    np.testing.assert_allclose(outs["1"][0], outs["0"][0], atol=2e-5)
 
 
 def test_full_dims_free_run(full_setup):
