@@ -106,6 +106,26 @@ void split_rows(const float* X, int B, int T, int C, long xs_b, _Float16* hi, _F
 // conv weight W[kw][C][N] fp32 -> pre-scaled split planes [N][kw·Cp] (zero for c >= C)
 void split_conv_weights(const float* W, int kw, int C, int Cp, int N, SplitB& out, hipStream_t s);
 
+// ---- large bf16 product C[M][N] = A[M][K]·B[K][N] (training weight / conv gradients) ----------
+// A (K contiguous, row stride lda) and B (N contiguous, row stride ldb) are rounded to bf16 into
+// padded K-contiguous copies a16 [Mp][Kp] and b16 [Np][Kp] (B transposed on the way), then a
+// 256 x 256 x 64 LDS-DMA MFMA kernel (fp32 accumulation) with K split over work-groups when the
+// tiles alone do not fill the chip (partials in part, one combine launch).  The buffers grow on
+// demand; all work is ordered on stream s.
+// a_kmajor: A is given as its transpose At[K][M] (row stride lda), e.g. the activations X[T·B][M] of
+// a weight gradient X^T·dG, and is transposed by the same conversion pass as B.
+// conv: A is the transposed im2col of a 'same' conv1d input X[b][t][c] (batch / frame strides xs_b,
+// xs_t): A[tap·C + c][b·T + t] = X[b][t + tap - pad][c] (0 outside [0, T)), M = kw·C, K = B·T --
+// the conv weight gradient im2colᵀ·dZ, gathered straight into the bf16 copy.
+struct KcConvA {
+  const float* x = nullptr;
+  long xs_b = 0, xs_t = 0;
+  int B = 0, T = 0, C = 0, kw = 0, pad = 0;
+};
+void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
+                  DevBuf& a16, DevBuf& b16, DevBuf& part, hipStream_t s, bool a_kmajor = false,
+                  const KcConvA* conv = nullptr);
+
 void gemm(const GemmArgs& a, hipStream_t s);
 // Same product, but the raw fp32 partial sums are left in a.kpart as [ks][M][N] (no epilogue, no
 // combine launch; ks >= 1 is returned) for a caller-fused combine.  a.kpart is required.

@@ -1236,6 +1236,189 @@ void conv_x3(const ConvX3Args& a, hipStream_t s) {
   TT2_HIP(hipGetLastError());
 }
 
+// ---- large bf16 product over K-contiguous operands (gemm.h gemm_bf16_kc) ----------------------
+constexpr int KC_BM = 256, KC_BN = 256, KC_BK = 64, KC_PLANE = 256 * KC_BK;  // bf16 per operand per stage
+
+// A[M][K] fp32 (row stride lda) -> a16[Mp][Kp] bf16, zero padded
+__global__ void k_kc_pad(const float* __restrict__ A, int M, int K, long lda, __bf16* __restrict__ out, int Kp,
+                         long n4) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long e = i * 4, r = e / Kp;
+    const int k = (int)(e - r * Kp);
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (__bf16)((r < M && k + q < K) ? A[r * lda + k + q] : 0.f);
+    *reinterpret_cast<bf16x4*>(out + e) = o;
+  }
+}
+
+// B[K][N] fp32 (row stride ldb) -> b16[Np][Kp] bf16 (transposed, zero padded): 64 x 64 tiles through
+// LDS, 256-byte coalesced row reads, 128-byte coalesced transposed row writes
+__global__ __launch_bounds__(256) void k_kc_tr(const float* __restrict__ B, int K, int N, long ldb,
+                                               __bf16* __restrict__ out, int Kp) {
+  __shared__ float t[64][65];
+  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int kk = ty; kk < 64; kk += 4)
+    t[kk][tx] = (k0 + kk < K && n0 + tx < N) ? B[(long)(k0 + kk) * ldb + n0 + tx] : 0.f;
+  __syncthreads();
+#pragma unroll 4
+  for (int nn = ty; nn < 64; nn += 4) out[(long)(n0 + nn) * Kp + k0 + tx] = (__bf16)t[tx][nn];
+}
+
+// the conv weight gradient's transposed im2col (KcConvA) -> a16[Mp][Kp] bf16: 64 (frames) x 64 (tap,
+// channel) tiles; reads are 256-byte runs of one frame's channels, writes 128-byte runs of frames
+__global__ __launch_bounds__(256) void k_kc_im2col(KcConvA cv, __bf16* __restrict__ out, int Kp) {
+  __shared__ float t[64][65];
+  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int K = cv.B * cv.T, M = cv.kw * cv.C;
+  const int n = n0 + tx, tap = n / cv.C, c = n - tap * cv.C;
+#pragma unroll 4
+  for (int kk = ty; kk < 64; kk += 4) {
+    const int m = k0 + kk;
+    float v = 0.f;
+    if (m < K && n < M) {
+      const int b = m / cv.T, ts = m - b * cv.T + tap - cv.pad;
+      if (ts >= 0 && ts < cv.T) v = cv.x[(long)b * cv.xs_b + (long)ts * cv.xs_t + c];
+    }
+    t[kk][tx] = v;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int nn = ty; nn < 64; nn += 4) out[(long)(n0 + nn) * Kp + k0 + tx] = (__bf16)t[tx][nn];
+}
+
+// 256 x 256 tile, 8 waves (2 x 4, wave tile 128 x 64 = 4 x 2 v_mfma_f32_32x32x16_bf16 accumulators),
+// 64-deep k-steps staged by LDS-DMA into 128-byte rows whose 16-byte chunks sit XOR-swizzled by
+// (row >> 1) & 7 (source address and fragment read), two stages; K split over blockIdx.y
+__global__ __launch_bounds__(512, 1) void k_gemm_kc(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                                                    int Kp, int M, int N, float* __restrict__ C, long ldc,
+                                                    float* __restrict__ part, int n_mt, int n_nt) {
+  __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 2 * KC_PLANE];  // [stage][A, B][256][64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int mt = (jb / n_nt) * 8 + xcd, nt = jb - (jb / n_nt) * n_nt;
+  if (mt >= n_mt) return;
+  const int m0 = mt * KC_BM, n0 = nt * KC_BN;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nkt = Kp / KC_BK, per = (nkt + gridDim.y - 1) / gridDim.y, kt0 = blockIdx.y * per;
+  const int nk = min(nkt, kt0 + per) - kt0;
+  // DMA pieces: 8 rows x 128 B; wave w fills pieces 4w .. 4w+3 of each operand; lane l lands at row
+  // 8p + (l >> 3), physical chunk l & 7, and fetches logical chunk (l & 7) ^ ((row >> 1) & 7)
+  const __bf16 *ga[4], *gb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wave + i) + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+    ga[i] = A + (long)(m0 + row) * Kp + 8 * c + (long)kt0 * KC_BK;
+    gb[i] = Bt + (long)(n0 + row) * Kp + 8 * c + (long)kt0 * KC_BK;
+  }
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  auto stage = [&](int kt, int buf) {
+    const int k0 = kt * KC_BK;
+    __bf16* base = sm + buf * 2 * KC_PLANE + 8 * 4 * wave * KC_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds(ga[i] + k0, (lds_ptr)(base + 8 * i * KC_BK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(gb[i] + k0, (lds_ptr)(base + KC_PLANE + 8 * i * KC_BK), 16, 0, 0);
+    }
+  };
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  if (nk > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int r = lane & 31, hl = lane >> 5, sw = (r >> 1) & 7;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const __bf16* S = sm + cur * 2 * KC_PLANE;
+#pragma unroll
+    for (int sl = 0; sl < KC_BK / 16; ++sl) {
+      const int off = r * KC_BK + 8 * ((2 * sl + hl) ^ sw);
+      bf16x8 b[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const bf16x8*>(S + KC_PLANE + (wn * 64 + j * 32) * KC_BK + off);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(S + (wm * 128 + i * 32) * KC_BK + off);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  float* out = part ? part + (long)blockIdx.y * M * N : C;
+  const long ld = part ? N : ldc;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + j * 32 + r;
+      if (col >= N) continue;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = m0 + wm * 128 + i * 32 + 4 * hl + (q & 3) + 8 * (q >> 2);
+        if (row < M) out[(long)row * ld + col] = acc[i][j][q];
+      }
+    }
+}
+
+void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
+                  DevBuf& a16, DevBuf& b16, DevBuf& part, hipStream_t s, bool a_kmajor, const KcConvA* conv) {
+  TT2_CHECK(M > 0 && N > 0 && K > 0, TT2_ERR_SHAPE_MISMATCH, "gemm_bf16_kc: empty problem");
+  const int n_mt = cdiv(M, KC_BM), n_nt = cdiv(N, KC_BN), tiles = n_mt * n_nt;
+  const int nkt = cdiv(K, KC_BK);
+  // K split: one work-group per CU, so the time is ~ rounds x k-steps per work-group, rounds =
+  // ceil(tiles·ks / 256); plus the combine's partial traffic (ks x M x N fp32 written + read, ~9 MB
+  // per k-step time of ~1.8 us at 5 TB/s): the cheapest ks <= 32 with >= 16 k-steps each and all
+  // work-groups in one round (measured: 144 tiles x 7 splits over 4 rounds ran each k-step at twice
+  // the time of 144 unsplit tiles -- the splits' disjoint K ranges share nothing in L2 / MALL)
+  int ks = 1;
+  double best = 1e30;
+  for (int k = 1; k <= 32 && (k == 1 || (nkt / k >= 16 && tiles * k <= 256)); ++k) {
+    const int per_k = cdiv(nkt, k), kk = cdiv(nkt, per_k);
+    const double cost = (double)cdiv(tiles * kk, 256) * per_k + (kk > 1 ? kk * (double)M * N * 8 / 9e6 : 0.0);
+    if (cost < best - 1e-9) { best = cost; ks = kk; }
+  }
+  const int per = cdiv(nkt, ks);
+  ks = cdiv(nkt, per);  // no empty slices
+  const int Kp = per * ks * KC_BK, Mp = n_mt * KC_BM, Np = n_nt * KC_BN;
+  const size_t na = (size_t)Mp * Kp * 2, nb = (size_t)Np * Kp * 2, np = ks > 1 ? (size_t)ks * M * N * 4 : 0;
+  if (a16.bytes < na) a16.alloc(na);  // growth frees the old buffer (device-synchronising hipFree)
+  if (b16.bytes < nb) b16.alloc(nb);
+  if (part.bytes < np) part.alloc(np);
+  __bf16* a = reinterpret_cast<__bf16*>(a16.p);
+  __bf16* b = reinterpret_cast<__bf16*>(b16.p);
+  const long n4 = (long)Mp * Kp / 4;
+  if (conv) {
+    TT2_CHECK(conv->kw * conv->C == M && conv->B * conv->T == K, TT2_ERR_SHAPE_MISMATCH, "gemm_bf16_kc: conv shape");
+    hipLaunchKernelGGL(k_kc_im2col, dim3(Kp / 64, Mp / 64), dim3(256), 0, s, *conv, a, Kp);
+  } else if (a_kmajor) hipLaunchKernelGGL(k_kc_tr, dim3(Kp / 64, Mp / 64), dim3(256), 0, s, A, K, M, lda, a, Kp);
+  else hipLaunchKernelGGL(k_kc_pad, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, A, M, K,
+                          lda, a, Kp, n4);
+  hipLaunchKernelGGL(k_kc_tr, dim3(Kp / 64, Np / 64), dim3(256), 0, s, B, K, N, ldb, b, Kp);
+  TT2_HIP(hipGetLastError());
+  float* pp = ks > 1 ? reinterpret_cast<float*>(part.p) : nullptr;
+  hipLaunchKernelGGL(k_gemm_kc, dim3((unsigned)(cdiv(n_mt, 8) * 8 * n_nt), (unsigned)ks), dim3(512), 0, s, a, b, Kp,
+                     M, N, C, ldc, pp, n_mt, n_nt);
+  TT2_HIP(hipGetLastError());
+  if (ks > 1) {
+    GemmArgs g;
+    g.M = M; g.N = N; g.kpart = pp; g.ksplit = ks; g.Cout = C; g.ldc = ldc;
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(((long)M * N + 1023) / 1024)), dim3(256), 0, s, g);
+    TT2_HIP(hipGetLastError());
+  }
+}
+
 int gemm_raw(const GemmArgs& a, hipStream_t s) {
   TT2_CHECK(a.kpart, TT2_ERR_INVALID_ARG, "gemm_raw: kpart required");
   GemmArgs g = a;

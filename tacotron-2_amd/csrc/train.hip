@@ -22,7 +22,6 @@
 #include <cstring>
 #include <functional>
 
-#include <rocblas/rocblas.h>
 
 #include "common.h"
 #include "gemm.h"
@@ -64,10 +63,9 @@ struct tt2_train_ctx {
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
   DevBuf TH, E, DF, PQ, FALL, ALN;
-  // bf16 operand copies + rocBLAS handle of the large plain products (tr_gemm_blas)
-  DevBuf blasA, blasB;
-  rocblas_handle blas = nullptr;
-  bool blas_on = true;  // TT2_TRAIN_BLAS=0 at create: every product on the hand-written kernels
+  // the large plain products (tr_gemm_big)
+  DevBuf blasA, blasB, blasP;  // gemm_bf16_kc: bf16 operand copies, split-K partials
+  bool blas_on = true;  // TT2_TRAIN_BLAS=0 at create: the large products on gemm_x3_kernel too
   long blas_calls = 0;
   // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
   DevBuf hK1, hK1T, hK2, hK2T, hWq, hWqT;
@@ -1851,45 +1849,45 @@ __global__ void k_tr_to_bf16(const float* __restrict__ src, long rows, long cols
 }
 
 // The large plain products of the bf16 step (weight gradients over all T·B rows, the Postnet
-// convolution gradients): C[M][N] = A[M][K]·B[K][N] as one rocBLAS bf16 GEMM with fp32
-// accumulation after a one-pass bf16 conversion of both operands.  Same operand rounding as the
-// hand-written bf16 kernels; these shapes (K up to 51 200 rows, 0.1-1 TFLOP each) are library
-// GEMMs, the hand-written kernels keep the small per-step products and every fused epilogue.
-static constexpr double kTrBlasMinFlops = 2.0e10;
-static bool tr_gemm_blas(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
-                         hipStream_t s) {
+// convolution gradients): C[M][N] = A[M][K]·B[K][N] on the hand-written 256 x 256 x 64 LDS-DMA bf16
+// kernel (gemm.h gemm_bf16_kc: both operands rounded to bf16 into padded K-contiguous copies, B
+// transposed on the way, K split over work-groups for the few-tile shapes, fp32 accumulation) --
+// the same operand rounding as the per-step bf16 kernels.  Products below kTrBigMinFlops keep the
+// per-step kernels' paths.
+static constexpr double kTrBigMinFlops = 2.0e10;
+static bool tr_gemm_big(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
+                        hipStream_t s) {
   tt2_train_ctx* c = g_tr_ctx;
   if (!c) return false;
-  if (!c->blas) {
-    TT2_CHECK(rocblas_create_handle(&c->blas) == rocblas_status_success, TT2_ERR_HIP, "rocblas_create_handle failed");
-  }
-  const size_t na = (size_t)M * K, nb = (size_t)K * N;
-  // sized at create for the decoder / Postnet weight gradients (tr_alloc); a larger front-end
-  // product grows them once (the hipFree of the old buffer synchronises the device)
-  if (c->blasA.bytes < na * 2) c->blasA.alloc(na * 2);
-  if (c->blasB.bytes < nb * 2) c->blasB.alloc(nb * 2);
-  __bf16* a16 = reinterpret_cast<__bf16*>(c->blasA.p);
-  __bf16* b16 = reinterpret_cast<__bf16*>(c->blasB.p);
-  hipLaunchKernelGGL(k_tr_to_bf16, dim3(2048), dim3(256), 0, s, A, (long)M, (long)K, lda, a16);
-  hipLaunchKernelGGL(k_tr_to_bf16, dim3(2048), dim3(256), 0, s, Bw, (long)K, (long)N, ldb, b16);
-  TT2_HIP(hipGetLastError());
-  TT2_CHECK(rocblas_set_stream(c->blas, s) == rocblas_status_success, TT2_ERR_HIP, "rocblas_set_stream failed");
-  const float alpha = 1.f, beta = 0.f;
-  // row-major C = A·B is column-major C^T (N x M) = B^T (N x K, ld N) · A^T (K x M, ld K)
-  const rocblas_status st = rocblas_gemm_ex(c->blas, rocblas_operation_none, rocblas_operation_none, N, M, K, &alpha,
-                                            b16, rocblas_datatype_bf16_r, N, a16, rocblas_datatype_bf16_r, K, &beta, C,
-                                            rocblas_datatype_f32_r, (int)ldc, C, rocblas_datatype_f32_r, (int)ldc,
-                                            rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
-  TT2_CHECK(st == rocblas_status_success, TT2_ERR_HIP, "rocblas_gemm_ex failed: status " + std::to_string((int)st));
+  gemm_bf16_kc(M, N, K, A, lda, Bw, ldb, C, ldc, c->blasA, c->blasB, c->blasP, s);
   ++c->blas_calls;
   return true;
+}
+
+static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
+                    hipStream_t s, const float* bias, const float* residual, long ldr, int act, const DevBuf* bt16,
+                    long ldbt);
+
+// Weight gradient C[M][N] = X^T·dG over K = T·B rows, X[K][M] (row stride ldx), dG[K][N]: the large
+// ones straight from X on gemm_bf16_kc (its conversion pass transposes X), the rest through
+// tr_transpose into TBUF and tr_gemm
+static void tr_gemm_xtg(int M, int N, int K, const float* X, long ldx, const float* dG, long ldg, float* C, long ldc,
+                        float* TBUF, hipStream_t s) {
+  tt2_train_ctx* c = g_tr_ctx;
+  if (c && c->blas_on && g_tr_prec == 2 && 2.0 * M * (double)N * K >= kTrBigMinFlops) {
+    gemm_bf16_kc(M, N, K, X, ldx, dG, ldg, C, ldc, c->blasA, c->blasB, c->blasP, s, true);
+    ++c->blas_calls;
+    return;
+  }
+  tr_transpose(X, K, M, ldx, TBUF, K, s);
+  tr_gemm(M, N, K, TBUF, K, dG, ldg, C, ldc, s, nullptr, nullptr, 0, ACT_NONE, nullptr, 0);
 }
 
 static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
                     hipStream_t s, const float* bias = nullptr, const float* residual = nullptr, long ldr = 0,
                     int act = ACT_NONE, const DevBuf* bt16 = nullptr, long ldbt = 0) {
   if (g_tr_ctx && g_tr_ctx->blas_on && g_tr_prec == 2 && !bias && !residual && act == ACT_NONE &&
-      2.0 * M * (double)N * K >= kTrBlasMinFlops && tr_gemm_blas(M, N, K, A, lda, Bw, ldb, C, ldc, s))
+      2.0 * M * (double)N * K >= kTrBigMinFlops && tr_gemm_big(M, N, K, A, lda, Bw, ldb, C, ldc, s))
     return;
   GemmArgs g;
   if (g_tr_prec == 2 && bt16 && bt16->p && ldbt % 8 == 0) {  // weights pre-converted: B^T in bf16
@@ -1954,7 +1952,7 @@ static std::string tr_bufname(const void* owner, const DevBuf* b) {
   TT2_NM(dG2) TT2_NM(DC1) TT2_NM(DC2) TT2_NM(R1) TT2_NM(R2) TT2_NM(DQ) TT2_NM(DCTX) TT2_NM(DKEYS) TT2_NM(DCUM)
   TT2_NM(dV) TT2_NM(dBA) TT2_NM(dKC) TT2_NM(dBC) TT2_NM(DVAL) TT2_NM(DMEM) TT2_NM(dZ) TT2_NM(dPre) TT2_NM(TBUF)
   TT2_NM(part) TT2_NM(red) TT2_NM(kpart) TT2_NM(TH) TT2_NM(E) TT2_NM(DF) TT2_NM(PQ) TT2_NM(FALL) TT2_NM(ALN)
-  TT2_NM(blasA) TT2_NM(blasB) TT2_NM(hK1) TT2_NM(hK1T) TT2_NM(hK2) TT2_NM(hK2T) TT2_NM(hWq) TT2_NM(hWqT) TT2_NM(X1h) TT2_NM(X2h) TT2_NM(dGh) TT2_NM(tK1T) TT2_NM(tK2T) TT2_NM(tWq) TT2_NM(tK2) TT2_NM(tK1)
+  TT2_NM(blasA) TT2_NM(blasB) TT2_NM(blasP) TT2_NM(hK1) TT2_NM(hK1T) TT2_NM(hK2) TT2_NM(hK2T) TT2_NM(hWq) TT2_NM(hWqT) TT2_NM(X1h) TT2_NM(X2h) TT2_NM(dGh) TT2_NM(tK1T) TT2_NM(tK2T) TT2_NM(tWq) TT2_NM(tK2) TT2_NM(tK1)
   TT2_NMA(PA, 8) TT2_NMA(PX, 9) TT2_NM(BNM) TT2_NM(BNV) TT2_NM(PPRJ) TT2_NM(dPP) TT2_NM(DYb) TT2_NM(DZb)
   TT2_NM(dPXa) TT2_NM(dPXb) TT2_NM(WFLIP) TT2_NM(PWT) TT2_NM(CLIPM) TT2_NM(pn_part) TT2_NM(fEX) TT2_NMA(fEA, 8)
   TT2_NMA(fEY, 9) TT2_NM(fXP) TT2_NM(fGZ) TT2_NM(fGA) TT2_NM(fCN) TT2_NM(fCS) TT2_NM(fHS) TT2_NM(fENC)
@@ -2078,11 +2076,15 @@ static void tr_alloc(tt2_train_ctx* c) {
     h(c->X1h, (T + 1) * Bp * LX1); h(c->X2h, (T + 1) * Bp * 2 * H); h(c->dGh, 2 * Bp * 4 * H);
     h(c->tK1T, LX1 * 4 * H); h(c->tK2T, 8 * H * H); h(c->tWq, H * A); h(c->tK2, 8 * H * H);
     h(c->tK1, ((LX1 + 31) / 32 * 32) * 4 * H);
-    // bf16 operand copies of the library GEMMs (tr_gemm_blas): the largest weight gradients over all
-    // T·B rows -- LSTM-1 [LX1 x TB]·[TB x 4H], the Postnet convs [K·cin x TB]·[TB x PC]
+    // padded bf16 operand copies of the large products (tr_gemm_big -> gemm_bf16_kc): the largest
+    // weight gradients over all T·B rows -- LSTM-1 [LX1 x TB]·[TB x 4H], the Postnet convs
+    // [K·cin x TB]·[TB x PC]; rows to 256, K to the split's 64-multiple (<= TB + 64·257), and the
+    // split-K partials (ks·Mp·Np <= 256 tiles of 256 x 256)
     const long pcin = c->cfg.postnet ? (long)c->PK * std::max<long>(c->PC, NM) : 0L;
-    h(c->blasA, TB * std::max({LX1, 2 * H, pcin}));
-    h(c->blasB, TB * std::max<long>(4 * H, c->cfg.postnet ? c->PC : 0));
+    const long Kpm = TB + 64L * 257, r256 = 255;
+    h(c->blasA, ((std::max({LX1, 2 * H, pcin}) + r256) & ~r256) * Kpm);
+    h(c->blasB, ((std::max<long>(4 * H, c->cfg.postnet ? c->PC : 0) + r256) & ~r256) * Kpm);
+    f(c->blasP, 256L * 256 * 256);
   }
   f(c->kpart, 4L << 20);
   if (c->cfg.frontend) tr_front_alloc(c);
@@ -2175,10 +2177,18 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
     {
       GemmArgs gi;
       conv_in(i, gi);
-      hipLaunchKernelGGL(k_pn_im2col_t, dim3(nblk((long)KW * cin * M)), dim3(256), 0, s, gi.A, gi.xs_b, gi.xs_t, B,
-                         T, cin, KW, pad, TBUF, M);
+      if (c->blas_on && g_tr_prec == 2 && 2.0 * KW * cin * (double)C * M >= kTrBigMinFlops) {
+        KcConvA cv;  // im2colᵀ gathered straight into gemm_bf16_kc's bf16 operand copy
+        cv.x = gi.A; cv.xs_b = gi.xs_b; cv.xs_t = gi.xs_t; cv.B = B; cv.T = T; cv.C = cin; cv.kw = KW; cv.pad = pad;
+        gemm_bf16_kc(KW * cin, C, (int)M, nullptr, 0, c->DZb.as<float>(), C, gvar(c, sc + "conv1d/kernel"), C,
+                     c->blasA, c->blasB, c->blasP, s, false, &cv);
+        ++c->blas_calls;
+      } else {
+        hipLaunchKernelGGL(k_pn_im2col_t, dim3(nblk((long)KW * cin * M)), dim3(256), 0, s, gi.A, gi.xs_b, gi.xs_t, B,
+                           T, cin, KW, pad, TBUF, M);
+        tr_gemm(KW * cin, C, (int)M, TBUF, M, c->DZb.as<float>(), C, gvar(c, sc + "conv1d/kernel"), C, s);
+      }
     }
-    tr_gemm(KW * cin, C, (int)M, TBUF, M, c->DZb.as<float>(), C, gvar(c, sc + "conv1d/kernel"), C, s);
     hipLaunchKernelGGL(k_pn_flip, dim3(nblk((long)KW * cin * C)), dim3(256), 0, s, pvar(c, sc + "conv1d/kernel"), KW,
                        cin, C, c->WFLIP.as<float>());
     GemmArgs g;
@@ -2495,11 +2505,9 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   // ---- weight gradients over all T·B rows ----
   float* TBUF = c->TBUF.as<float>();
   const int TBi = (int)TB;
-  tr_transpose(X1, TB, LX1, LX1, TBUF, TB, s);
-  tr_gemm(LX1, 4 * H, TBi, TBUF, TB, c->dG1.as<float>(), 4 * H, gvar(c, L1V("kernel")), 4 * H, s);
+  tr_gemm_xtg(LX1, 4 * H, TBi, X1, LX1, c->dG1.as<float>(), 4 * H, gvar(c, L1V("kernel")), 4 * H, TBUF, s);
   tr_colsum(c, c->dG1.as<float>(), TB, 4 * H, 4 * H, gvar(c, L1V("bias")), s);
-  tr_transpose(X2, TB, 2 * H, 2 * H, TBUF, TB, s);
-  tr_gemm(2 * H, 4 * H, TBi, TBUF, TB, c->dG2.as<float>(), 4 * H, gvar(c, L2V("kernel")), 4 * H, s);
+  tr_gemm_xtg(2 * H, 4 * H, TBi, X2, 2 * H, c->dG2.as<float>(), 4 * H, gvar(c, L2V("kernel")), 4 * H, TBUF, s);
   tr_colsum(c, c->dG2.as<float>(), TB, 4 * H, 4 * H, gvar(c, L2V("bias")), s);
   tr_transpose(PIN, TB, H + D, H + D, TBUF, TB, s);
   tr_gemm(H, A, TBi, TBUF, TB, c->DQ.as<float>(), A, gvar(c, vn("decoder/query_layer/kernel")), A, s);
@@ -3139,6 +3147,8 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
       tr_colsum(c, dz, Mi, fo, fo, gvar(c, sc + "conv2d/bias"), s);
       const int pt = std::max((Ho - 1) * 2 + 3 - H, 0) / 2, pl = std::max((Wo - 1) * 2 + 3 - W, 0) / 2;
       const float* xin = i == 0 ? refs[r] : c->fRY[r][i - 1].as<float>();
+      // (gemm_bf16_kc with the im2colᵀ gathered into bf16 measured 458 us per layer here against
+      // 525 + ~60 for the fp32 columns + gemm_x3_kernel: its 256-wide N tile is 8x idle at fo = 32)
       fe_im2col2d_t(xin, B, H, W, ci, Ho, Wo, pt, pl, FB, Mi, s);
       tr_gemm(9 * ci, fo, (int)Mi, FB, Mi, dz, fo, gvar(c, sc + "conv2d/kernel"), fo, s);
       if (i > 0) {
@@ -3479,7 +3489,6 @@ void tt2_train_destroy(tt2_train_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->blas) (void)rocblas_destroy_handle(c->blas);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -3652,7 +3661,7 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
     TT2_CHECK(c && name && host, TT2_ERR_INVALID_ARG, "null argument");
     TT2_HIP(hipSetDevice(c->dev));
     TT2_HIP(hipDeviceSynchronize());
-    if (std::string(name) == "diag:blas_calls") {  // library GEMMs issued since create (1 float)
+    if (std::string(name) == "diag:blas_calls") {  // gemm_bf16_kc products issued since create (1 float)
       host[0] = (float)c->blas_calls;
       return;
     }

@@ -586,11 +586,12 @@ def test_gpu_train_frontend_matches_oracle(masks):
 @pytest.mark.gpu
 def test_gpu_train_bf16_library_gemms_match_kernels():
     """bf16 mode routes the large plain products (weight gradients over all T·B rows, >= 2e10
-    flops) through rocBLAS bf16 GEMMs after the same bf16 operand rounding; TT2_TRAIN_BLAS=0 keeps
-    them on the hand-written kernels.  Same inputs, fork-default widths, T·B = 2000 rows: the
-    forward, the losses and d memory are identical (those products only produce terminal weight
-    gradients), every gradient agrees to fp32 accumulation-order level (measured: bit-identical --
-    the library accumulates K in the same MFMA order), and the context counts the library calls."""
+    flops) through the 256 x 256 x 64 LDS-DMA bf16 kernel (gemm.h gemm_bf16_kc: padded K-contiguous
+    bf16 copies, K split over work-groups) after the same bf16 operand rounding; TT2_TRAIN_BLAS=0
+    keeps them on gemm_x3_kernel.  Same inputs, fork-default widths, T·B = 2000 rows (K not a
+    multiple of the 64-deep step, M not of the 256-row tile): the forward, the losses and d memory
+    are identical (those products only produce terminal weight gradients), every gradient agrees
+    to fp32 accumulation-order level, and the context counts the large-product calls."""
     import os
     from tt2.train import TacotronTrainer
     hp = small_hparams()
@@ -757,4 +758,45 @@ def test_gpu_train_fused_encoder_lstm_matches_split_k_path():
     for n in ga:
         rel = float(np.linalg.norm(ga[n] - gb[n]) / max(np.linalg.norm(gb[n]), 1e-30))
         print("  {:90s} rel {:.3e}".format(n, rel))
+        assert rel < 2e-2, (n, rel)
+
+
+@pytest.mark.gpu
+def test_gpu_train_im2col_gathered_large_products_match_kernels():
+    """The whole bf16 step from ids with the Postnet conv weight gradients on gemm_bf16_kc's
+    gathered operand (gemm.h KcConvA: the conv1d im2colᵀ written straight into the kernel's bf16
+    copy, no fp32 columns) and the LSTM weight gradients transposed by its conversion pass, against
+    TT2_TRAIN_BLAS=0 (fp32 transposes / im2colᵀ + gemm_x3_kernel).  The 512-channel Postnet convs
+    are 2·5·512·512·(8·960) >= 2e10 flops, so the gathered form runs.  Losses within 1e-5 relative,
+    every gradient within 2e-2 (bf16 operand rounding, K split / accumulation order)."""
+    import os
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    hp.override_from_dict(dict(reference_filters=[32, 32, 64, 64, 128, 128], postnet_channels=512))
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, B=8, T_in=11, T_out=960, T_ref=400)
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    names = TRN.frontend_var_names() + TRN.postnet_var_names()
+    res = {}
+    old = os.environ.get("TT2_TRAIN_BLAS")
+    try:
+        for flag in ("1", "0"):
+            os.environ["TT2_TRAIN_BLAS"] = flag
+            tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", frontend=True, max_T_ref=re.shape[1])
+            try:
+                tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+                L = tr.losses()
+                g = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}
+            finally:
+                tr.close()
+            res[flag] = (L, g)
+    finally:
+        if old is None:
+            os.environ.pop("TT2_TRAIN_BLAS", None)
+        else:
+            os.environ["TT2_TRAIN_BLAS"] = old
+    (La, ga), (Lb, gb) = res["1"], res["0"]
+    for k in ("before", "after"):
+        assert abs(La[k] - Lb[k]) < 1e-5 * abs(Lb[k]), (k, La[k], Lb[k])
+    for n in ga:
+        rel = float(np.linalg.norm(ga[n] - gb[n]) / max(np.linalg.norm(gb[n]), 1e-30))
         assert rel < 2e-2, (n, rel)
