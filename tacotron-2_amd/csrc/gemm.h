@@ -126,6 +126,19 @@ void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B,
                   DevBuf& a16, DevBuf& b16, DevBuf& part, hipStream_t s, bool a_kmajor = false,
                   const KcConvA* conv = nullptr);
 
+// gemm_bf16_kc's kernel as a 'same' conv1d over padded bf16 planes (one plane, the CX_* row layout
+// above, channel stride Cp % 64 == 0): out[b·T + t][n] = act(Σ_k ... + bias[n]) for n < N, with the
+// weights as Bt[Np][ldbt] bf16 (k = tap·Cp + c, Np >= N rounded up to 256 rows) -- the training
+// Postnet's forward and input-gradient convolutions.
+struct KcEpi {
+  int T = 0, B = 0;  // T > 0: conv epilogue (padded rows -> frames)
+  const float* bias = nullptr;
+};
+void conv_bf16_planes(const __bf16* planes, int Cp, int B, int T, int kw, const __bf16* Bt, long ldbt, int N,
+                      const float* bias, int act, float* out, long ldo, hipStream_t s);
+// B[K][N] fp32 -> out[Np][Kp] bf16 transposed, zero padded (Kp, Np multiples of 64)
+void kc_transpose_bf16(const float* B, int K, int N, long ldb, __bf16* out, int Kp, int Np, hipStream_t s);
+
 void gemm(const GemmArgs& a, hipStream_t s);
 // Same product, but the raw fp32 partial sums are left in a.kpart as [ks][M][N] (no epilogue, no
 // combine launch; ks >= 1 is returned) for a caller-fused combine.  a.kpart is required.

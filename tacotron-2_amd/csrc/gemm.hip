@@ -1292,9 +1292,11 @@ __global__ __launch_bounds__(256) void k_kc_im2col(KcConvA cv, __bf16* __restric
 // 256 x 256 tile, 8 waves (2 x 4, wave tile 128 x 64 = 4 x 2 v_mfma_f32_32x32x16_bf16 accumulators),
 // 64-deep k-steps staged by LDS-DMA into 128-byte rows whose 16-byte chunks sit XOR-swizzled by
 // (row >> 1) & 7 (source address and fragment read), two stages; K split over blockIdx.y
-__global__ __launch_bounds__(512, 1) void k_gemm_kc(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                                                    int Kp, int M, int N, float* __restrict__ C, long ldc,
-                                                    float* __restrict__ part, int n_mt, int n_nt) {
+template <int ACT>
+__global__ __launch_bounds__(512, 1) void k_gemm_kc(const __bf16* __restrict__ A, long lda,
+                                                    const __bf16* __restrict__ Bt, long ldb, int Kp, int M, int N,
+                                                    float* __restrict__ C, long ldc, float* __restrict__ part,
+                                                    int n_mt, int n_nt, KcEpi ep) {
   __shared__ __attribute__((aligned(16))) __bf16 sm[2 * 2 * KC_PLANE];  // [stage][A, B][256][64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
@@ -1310,8 +1312,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_kc(const __bf16* __restrict__ A
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = 8 * (4 * wave + i) + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
-    ga[i] = A + (long)(m0 + row) * Kp + 8 * c + (long)kt0 * KC_BK;
-    gb[i] = Bt + (long)(n0 + row) * Kp + 8 * c + (long)kt0 * KC_BK;
+    ga[i] = A + (long)(m0 + row) * lda + 8 * c + (long)kt0 * KC_BK;
+    gb[i] = Bt + (long)(n0 + row) * ldb + 8 * c + (long)kt0 * KC_BK;
   }
   typedef __attribute__((address_space(3))) void* lds_ptr;
   auto stage = [&](int kt, int buf) {
@@ -1356,6 +1358,29 @@ __global__ __launch_bounds__(512, 1) void k_gemm_kc(const __bf16* __restrict__ A
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  if (ep.T > 0) {  // conv over padded planes: padded row -> frame (b, t); act(acc + bias) -> C rows b·T + t
+    const int Tp = ep.T + 2 * CX_P;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mb0 = m0 + wm * 128 + i * 32 + 4 * hl, b0 = mb0 / Tp, t00 = mb0 - b0 * Tp;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + r;
+        const float bias = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rq = (q & 3) + 8 * (q >> 2);
+          int t = t00 + rq, b = b0;
+          while (t >= Tp) { t -= Tp; ++b; }
+          float y = acc[i][j][q] + bias;
+          if constexpr (ACT == ACT_TANH) y = cx_tanh(y);
+          if constexpr (ACT == ACT_RELU) y = fmaxf(y, 0.f);
+          if (b < ep.B && t >= CX_P && t < CX_P + ep.T && col < N) C[((long)b * ep.T + t - CX_P) * ldc + col] = y;
+        }
+      }
+    }
+    return;
+  }
   float* out = part ? part + (long)blockIdx.y * M * N : C;
   const long ld = part ? N : ldc;
 #pragma unroll
@@ -1370,6 +1395,33 @@ __global__ __launch_bounds__(512, 1) void k_gemm_kc(const __bf16* __restrict__ A
         if (row < M) out[(long)row * ld + col] = acc[i][j][q];
       }
     }
+}
+
+void conv_bf16_planes(const __bf16* planes, int Cp, int B, int T, int kw, const __bf16* Bt, long ldbt, int N,
+                      const float* bias, int act, float* out, long ldo, hipStream_t s) {
+  TT2_CHECK(Cp % KC_BK == 0 && (kw & 1) && kw <= 2 * CX_P + 1 && ldbt >= (long)kw * Cp, TT2_ERR_SHAPE_MISMATCH,
+            "conv_bf16_planes: needs Cp % 64 == 0, odd kw <= 5");
+  const int Mr = B * (T + 2 * CX_P), n_mt = cdiv(Mr, KC_BM), n_nt = cdiv(N, KC_BN);
+  KcEpi ep;
+  ep.T = T; ep.B = B; ep.bias = bias;
+  const __bf16* A = planes + (long)(CX_G - (kw - 1) / 2) * Cp;  // the overlapping-row view, row stride Cp
+  const dim3 grid((unsigned)(cdiv(n_mt, 8) * 8 * n_nt));
+  if (act == ACT_TANH)
+    hipLaunchKernelGGL(k_gemm_kc<ACT_TANH>, grid, dim3(512), 0, s, A, (long)Cp, Bt, ldbt, kw * Cp, Mr, N, out, ldo,
+                       nullptr, n_mt, n_nt, ep);
+  else if (act == ACT_RELU)
+    hipLaunchKernelGGL(k_gemm_kc<ACT_RELU>, grid, dim3(512), 0, s, A, (long)Cp, Bt, ldbt, kw * Cp, Mr, N, out, ldo,
+                       nullptr, n_mt, n_nt, ep);
+  else
+    hipLaunchKernelGGL(k_gemm_kc<ACT_NONE>, grid, dim3(512), 0, s, A, (long)Cp, Bt, ldbt, kw * Cp, Mr, N, out, ldo,
+                       nullptr, n_mt, n_nt, ep);
+  TT2_HIP(hipGetLastError());
+}
+
+void kc_transpose_bf16(const float* B, int K, int N, long ldb, __bf16* out, int Kp, int Np, hipStream_t s) {
+  TT2_CHECK(Kp % 64 == 0 && Np % 64 == 0 && Kp >= K && Np >= N, TT2_ERR_SHAPE_MISMATCH, "kc_transpose_bf16: padding");
+  hipLaunchKernelGGL(k_kc_tr, dim3(Kp / 64, Np / 64), dim3(256), 0, s, B, K, N, ldb, out, Kp);
+  TT2_HIP(hipGetLastError());
 }
 
 void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
@@ -1408,8 +1460,8 @@ void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B,
   hipLaunchKernelGGL(k_kc_tr, dim3(Kp / 64, Np / 64), dim3(256), 0, s, B, K, N, ldb, b, Kp);
   TT2_HIP(hipGetLastError());
   float* pp = ks > 1 ? reinterpret_cast<float*>(part.p) : nullptr;
-  hipLaunchKernelGGL(k_gemm_kc, dim3((unsigned)(cdiv(n_mt, 8) * 8 * n_nt), (unsigned)ks), dim3(512), 0, s, a, b, Kp,
-                     M, N, C, ldc, pp, n_mt, n_nt);
+  hipLaunchKernelGGL(k_gemm_kc<ACT_NONE>, dim3((unsigned)(cdiv(n_mt, 8) * 8 * n_nt), (unsigned)ks), dim3(512), 0, s, a,
+                     (long)Kp, b, (long)Kp, Kp, M, N, C, ldc, pp, n_mt, n_nt, KcEpi());
   TT2_HIP(hipGetLastError());
   if (ks > 1) {
     GemmArgs g;

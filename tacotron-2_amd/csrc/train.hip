@@ -80,6 +80,11 @@ struct tt2_train_ctx {
   bool pn_masks = false;
   int T_last = 0, Tin_last = 0;
   bool pn_ran = false;  // batch stats of the last forward are valid (moving averages in apply)
+  // bf16 Postnet convolutions over padded planes (gemm.h conv_bf16_planes): the layer input / dz
+  // planes (pad rows zeroed when the shape changes) and the transposed bf16 weights of one layer
+  DevBuf pnPl, pnWt;
+  int pn_pl_B = -1, pn_pl_T = -1;
+  bool pn_planes = false;
   hipStream_t last_stream = nullptr;  // stream of the last forward_backward / apply (read-backs)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
@@ -1663,16 +1668,23 @@ __global__ __launch_bounds__(TR_FIN) void k_pn_colstat_final(const float* __rest
   if (threadIdx.x < 32 && n < N) out[n] = tot * scale;
 }
 // y = gamma (a - mean) rsqrt(var + eps) + beta, then dropout(0.5) with keep bits (or identity)
+// planes (nullable): the next conv's padded bf16 input (gemm.h CX_* layout, rows b·T + t of y)
+__device__ __forceinline__ void pn_plane_put(__bf16* planes, int T, long i, int C, float v) {
+  const long m = i / C;
+  const int c = (int)(i - m * C), b = (int)(m / T), t = (int)(m - (long)b * T);
+  planes[(CX_G + (long)b * (T + 2 * CX_P) + CX_P + t) * C + c] = (__bf16)v;
+}
 __global__ void k_pn_bn_fwd(const float* __restrict__ a, long M, int C, const float* __restrict__ mean,
                             const float* __restrict__ var, const float* __restrict__ gamma,
                             const float* __restrict__ beta, float eps, const uint8_t* __restrict__ keep,
-                            float* __restrict__ y) {
+                            float* __restrict__ y, __bf16* __restrict__ planes = nullptr, int T = 1) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M * C) return;
   const int c = (int)(i % C);
   float v = gamma[c] * (a[i] - mean[c]) * rsqrtf(var[c] + eps) + beta[c];
   if (keep) v = (v / 0.5f) * (float)keep[i];
   y[i] = v;
+  if (planes) pn_plane_put(planes, T, i, C, v);
 }
 // BN backward sums over rows: S1 = sum dy, S2 = sum dy * xhat, with dy = dx_next * dropout
 __global__ __launch_bounds__(256) void k_pn_bn_bwd_part(const float* __restrict__ dxn, const uint8_t* __restrict__ keep,
@@ -1728,7 +1740,7 @@ __global__ __launch_bounds__(TR_FIN) void k_pn_bn_bwd_final(const float* __restr
 __global__ void k_pn_bn_bwd_dz(const float* __restrict__ dy, const float* __restrict__ a, long M, int C,
                                const float* __restrict__ mean, const float* __restrict__ var, float eps,
                                const float* __restrict__ gamma, const float* __restrict__ sums, int tanh_act,
-                               float* __restrict__ dz) {
+                               float* __restrict__ dz, __bf16* __restrict__ planes = nullptr, int T = 1) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M * C) return;
   const int c = (int)(i % C);
@@ -1740,6 +1752,7 @@ __global__ void k_pn_bn_bwd_dz(const float* __restrict__ dy, const float* __rest
   if (tanh_act == 1) g *= 1.f - av * av;        // tanh (Postnet)
   else if (tanh_act == 2) g *= av > 0.f ? 1.f : 0.f;  // ReLU (encoder convolutions): av = relu output
   dz[i] = g;
+  if (planes) pn_plane_put(planes, T, i, C, g);
 }
 // im2col^T of a conv1d input x(b, t, c) = x[b*xs_b + t*xs_t + c]:
 // out[(tap*C + c) * ldo + b*T + t] = x(b, t + tap - pad, c) (0 outside [0, T))
@@ -2097,6 +2110,15 @@ static void tr_alloc(tt2_train_ctx* c) {
     f(c->DYb, TB * PC); f(c->DZb, TB * PC); f(c->dPXa, TB * std::max(PC, NM)); f(c->dPXb, TB * std::max(PC, NM));
     f(c->WFLIP, PK * std::max(PC, NM) * PC);  // flipped kernels: layer 1's are [PK][num_mels][PC]
     f(c->PWT, NM * PC); f(c->pn_part, 64 * 2 * PC + 1024);
+    {
+      const char* e = std::getenv("TT2_PN_PLANES");  // 0: the implicit-im2col gemm_x3_kernel convs
+      c->pn_planes = (!e || std::atoi(e) != 0) && c->cfg.precision && PC % 64 == 0 && (PK & 1) && PK <= 2 * CX_P + 1;
+    }
+    if (c->pn_planes) {
+      const long W = std::max<long>(PC, NM), Wr = (W + 255) / 256 * 256;
+      c->pnPl.alloc((size_t)cx_rows(c->B, (int)(TB / c->B)) * PC * 2);
+      c->pnWt.alloc((size_t)Wr * PK * W * 2);
+    }
     c->CLIPM.alloc((size_t)TB * NM);
   }
 }
@@ -2125,22 +2147,38 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
       g.A = c->PX[i].as<float>(); g.C = C; g.xs_b = (long)T * C; g.xs_t = C;
     }
   };
+  const bool planes = c->pn_planes && g_tr_prec == 2;
+  __bf16* pl = reinterpret_cast<__bf16*>(c->pnPl.p);
+  __bf16* wt = reinterpret_cast<__bf16*>(c->pnWt.p);
+  if (planes && (c->pn_pl_B != B || c->pn_pl_T != T)) {  // pad and guard rows stay zero from here on
+    TT2_HIP(hipMemsetAsync(c->pnPl.p, 0, (size_t)cx_rows(B, T) * C * 2, s));
+    c->pn_pl_B = B;
+    c->pn_pl_T = T;
+  }
+  const int Cr = (C + 255) / 256 * 256;
   for (int i = 0; i < L; ++i) {
     const std::string sc = pn_scope(i + 1);
-    GemmArgs g;
-    g.a_mode = A_CONV1D; g.M = (int)M; g.N = C; g.T = T; g.kw = KW; g.pad = pad;
-    conv_in(i, g);
-    g.K = KW * g.C;
-    g.Bw = pvar(c, sc + "conv1d/kernel"); g.ldb = C; g.Cout = c->PA[i].as<float>(); g.ldc = C;
-    g.bias = pvar(c, sc + "conv1d/bias"); g.act = i < L - 1 ? ACT_TANH : ACT_NONE;
-    tr_gemm_run(g, s);
+    if (planes && i > 0) {  // layer i's input planes were written by layer i-1's BN forward
+      kc_transpose_bf16(pvar(c, sc + "conv1d/kernel"), KW * C, C, C, wt, KW * C, Cr, s);
+      conv_bf16_planes(pl, C, B, T, KW, wt, (long)KW * C, C, pvar(c, sc + "conv1d/bias"),
+                       i < L - 1 ? ACT_TANH : ACT_NONE, c->PA[i].as<float>(), C, s);
+    } else {
+      GemmArgs g;
+      g.a_mode = A_CONV1D; g.M = (int)M; g.N = C; g.T = T; g.kw = KW; g.pad = pad;
+      conv_in(i, g);
+      g.K = KW * g.C;
+      g.Bw = pvar(c, sc + "conv1d/kernel"); g.ldb = C; g.Cout = c->PA[i].as<float>(); g.ldc = C;
+      g.bias = pvar(c, sc + "conv1d/bias"); g.act = i < L - 1 ? ACT_TANH : ACT_NONE;
+      tr_gemm_run(g, s);
+    }
     float* mean = c->BNM.as<float>() + (long)i * C;
     float* var = c->BNV.as<float>() + (long)i * C;
     colstat(c->PA[i].as<float>(), nullptr, 0, mean);
     colstat(c->PA[i].as<float>(), mean, 1, var);
     hipLaunchKernelGGL(k_pn_bn_fwd, dim3(nblk(M * C)), dim3(256), 0, s, c->PA[i].as<float>(), M, C, mean, var,
                        pvar(c, sc + "batch_normalization/gamma"), pvar(c, sc + "batch_normalization/beta"), eps,
-                       pnm ? pnm + (long)i * M * C : nullptr, c->PX[i + 1].as<float>());
+                       pnm ? pnm + (long)i * M * C : nullptr, c->PX[i + 1].as<float>(),
+                       planes && i < L - 1 ? pl : nullptr, T);
   }
   const std::string pp = vn("postnet_projection/projection_postnet_projection/");
   tr_gemm((int)M, NM, C, c->PX[L].as<float>(), C, pvar(c, pp + "kernel"), NM, c->PPRJ.as<float>(), NM, s,
@@ -2171,7 +2209,7 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
                        gvar(c, sc + "batch_normalization/gamma"), gvar(c, sc + "batch_normalization/beta"));
     hipLaunchKernelGGL(k_pn_bn_bwd_dz, dim3(nblk(M * C)), dim3(256), 0, s, c->DYb.as<float>(), c->PA[i].as<float>(),
                        M, C, mean, var, eps, pvar(c, sc + "batch_normalization/gamma"), sums, i < L - 1 ? 1 : 0,
-                       c->DZb.as<float>());
+                       c->DZb.as<float>(), planes ? pl : nullptr, T);
     tr_colsum(c, c->DZb.as<float>(), M, C, C, gvar(c, sc + "conv1d/bias"), s);
     const int cin = i == 0 ? NM : C;
     {
@@ -2191,11 +2229,16 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
     }
     hipLaunchKernelGGL(k_pn_flip, dim3(nblk((long)KW * cin * C)), dim3(256), 0, s, pvar(c, sc + "conv1d/kernel"), KW,
                        cin, C, c->WFLIP.as<float>());
-    GemmArgs g;
-    g.a_mode = A_CONV1D; g.M = (int)M; g.N = cin; g.T = T; g.kw = KW; g.pad = KW - 1 - pad;
-    g.A = c->DZb.as<float>(); g.C = C; g.xs_b = (long)T * C; g.xs_t = C; g.K = KW * C;
-    g.Bw = c->WFLIP.as<float>(); g.ldb = cin; g.Cout = dxo; g.ldc = cin;
-    tr_gemm_run(g, s);
+    if (planes) {  // input gradient: conv of the dz planes with the flipped kernel (pad KW-1-pad = pad)
+      kc_transpose_bf16(c->WFLIP.as<float>(), KW * C, cin, cin, wt, KW * C, (cin + 255) / 256 * 256, s);
+      conv_bf16_planes(pl, C, B, T, KW, wt, (long)KW * C, cin, nullptr, ACT_NONE, dxo, cin, s);
+    } else {
+      GemmArgs g;
+      g.a_mode = A_CONV1D; g.M = (int)M; g.N = cin; g.T = T; g.kw = KW; g.pad = KW - 1 - pad;
+      g.A = c->DZb.as<float>(); g.C = C; g.xs_b = (long)T * C; g.xs_t = C; g.K = KW * C;
+      g.Bw = c->WFLIP.as<float>(); g.ldb = cin; g.Cout = dxo; g.ldc = cin;
+      tr_gemm_run(g, s);
+    }
     std::swap(dxn, dxo);
   }
   hipLaunchKernelGGL(k_pn_add_ddec, dim3(nblk(M * NM)), dim3(256), 0, s, c->dPP.as<float>(), dxn,

@@ -800,3 +800,49 @@ def test_gpu_train_im2col_gathered_large_products_match_kernels():
     for n in ga:
         rel = float(np.linalg.norm(ga[n] - gb[n]) / max(np.linalg.norm(gb[n]), 1e-30))
         assert rel < 2e-2, (n, rel)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T_out", [37, 300])
+def test_gpu_train_postnet_planes_match_im2col(T_out):
+    """bf16 training Postnet with the forward and input-gradient convolutions over padded bf16 planes
+    (gemm.h conv_bf16_planes; the planes written by the BN forward / BN backward kernels) against
+    the implicit-im2col gemm_x3_kernel convs (TT2_PN_PLANES=0), at 512 channels: after loss within
+    1e-4 relative (measured 1.7e-5: a 3e-7 tanh difference flips the bf16 rounding of some next-layer
+    inputs), every decoder and Postnet gradient within 2e-2 (bf16 operand rounding, tanh on
+    v_exp/v_rcp against libm, accumulation order)."""
+    import os
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    hp.override_from_dict(dict(postnet_channels=512))
+    B, T_in = 6, 17
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=3)
+    names = TRN.train_var_names() + TRN.postnet_var_names()
+    res = {}
+    old = os.environ.get("TT2_PN_PLANES")
+    try:
+        for flag in ("1", "0"):
+            os.environ["TT2_PN_PLANES"] = flag
+            tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", postnet=True)
+            try:
+                tr.forward_backward(mem, lens, tg, st, pm, zm, pnm)
+                L = tr.losses()
+                g = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}
+            finally:
+                tr.close()
+            res[flag] = (L, g)
+    finally:
+        if old is None:
+            os.environ.pop("TT2_PN_PLANES", None)
+        else:
+            os.environ["TT2_PN_PLANES"] = old
+    (La, ga), (Lb, gb) = res["1"], res["0"]
+    assert abs(La["after"] - Lb["after"]) < 1e-4 * abs(Lb["after"]), (La["after"], Lb["after"])
+    for n in ga:
+        den = np.linalg.norm(gb[n])
+        if n.endswith("conv_layer_5_postnet_convolutions/conv1d/bias"):
+            # conv -> training BN with no activation between: d bias = Σ dz = 0 up to rounding noise
+            den = max(den, np.linalg.norm(gb[n.replace("/bias", "/kernel")]))
+        rel = float(np.linalg.norm(ga[n] - gb[n]) / max(den, 1e-30))
+        assert rel < 2e-2, (n, rel)
