@@ -83,6 +83,8 @@ struct tt2_train_ctx {
   // bf16 Postnet convolutions over padded planes (gemm.h conv_bf16_planes): the layer input / dz
   // planes (pad rows zeroed when the shape changes) and the transposed bf16 weights of one layer
   DevBuf pnPl, pnWt;
+  DevBuf values16;         // bf16 values for the per-step context / d align reads (TT2_TR_VALUES16)
+  bool values16_on = true;
   int pn_pl_B = -1, pn_pl_T = -1;
   bool pn_planes = false;
   hipStream_t last_stream = nullptr;  // stream of the last forward_backward / apply (read-backs)
@@ -776,11 +778,14 @@ __global__ void k_tr_rows_bf16(const float* __restrict__ src, long lds, long row
   }
 }
 
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 struct TrAtt {
   int B, Tin, T, A, F, KW, D, H, P, t, nt;  // nt = j-tiles per row (TR_JT rows each)
   const int* lens;
   const float* keys;    // [B,Tin,A]
   const float* values;  // [B,Tin,D]
+  const __bf16* values16;  // non-null (bf16 step): the same values rounded to bf16, read by the context
+                           // product (half the bytes of its dominant read)
   const float* Q;       // [T][B][A]
   const float* qpart;   // non-null: the step's query as raw split-K partials [qks][B][A] (k_tr_att_energy2
   int qks;              // sums them: no combine launch), else Q
@@ -1016,12 +1021,23 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (nc0 < a.D) {
       const float* vb = a.values + (long)b * a.Tin * a.D + nc0;
+      const __bf16* vb16 = a.values16 ? a.values16 + (long)b * a.Tin * a.D + nc0 : nullptr;
       for (int j0 = rg; j0 < a.Tin; j0 += 160) {
         f32x4 v[10];
+        if (vb16) {
 #pragma unroll
-        for (int u = 0; u < 10; ++u) {
-          const int j = j0 + 16 * u;
-          v[u] = j < a.Tin ? *reinterpret_cast<const f32x4*>(vb + (long)j * a.D) : f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int u = 0; u < 10; ++u) {
+            const int j = j0 + 16 * u;
+            bf16x4 h = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+            if (j < a.Tin) h = *reinterpret_cast<const bf16x4*>(vb16 + (long)j * a.D);
+            v[u] = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 10; ++u) {
+            const int j = j0 + 16 * u;
+            v[u] = j < a.Tin ? *reinterpret_cast<const f32x4*>(vb + (long)j * a.D) : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
         }
 #pragma unroll
         for (int u = 0; u < 10; ++u) {
@@ -1840,7 +1856,6 @@ static thread_local DevBuf* g_tr_kpart = nullptr;  // split-K scratch (stream-or
 static thread_local int g_tr_prec = 0;             // GemmArgs::split16 (0 fp32, 2 bf16)
 static thread_local tt2_train_ctx* g_tr_ctx = nullptr;  // bf16 BLAS scratch + handle of that context
 
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 // fp32 [rows][cols] (leading dimension ld) -> dense bf16 [rows][cols], round to nearest even (the
 // same rounding the bf16 GEMM kernels apply when they stage operands)
@@ -2348,6 +2363,14 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   TrAtt at{};
   at.B = B; at.Tin = Tin; at.T = T; at.A = A; at.F = F; at.KW = KW; at.D = D; at.H = H; at.P = P;
   at.lens = lens; at.keys = c->keys.as<float>(); at.values = c->values.as<float>(); at.Q = c->Q.as<float>();
+  at.values16 = nullptr;
+  if (g_tr_prec == 2 && c->values16_on && (D & 3) == 0) {  // bf16 copy of this step's values (once per step)
+    c->values16.alloc((size_t)B * Tin * D * 2);
+    hipLaunchKernelGGL(k_tr_to_bf16, dim3(2048), dim3(256), 0, s, c->values.as<float>(), (long)B * Tin, (long)D, (long)D,
+                       c->values16.as<__bf16>());
+    TT2_HIP(hipGetLastError());
+    at.values16 = c->values16.as<__bf16>();
+  }
   at.Kc = pvar(c, LAV("location_features_convolution/kernel"));
   at.bc = pvar(c, LAV("location_features_convolution/bias"));
   at.Wl = pvar(c, LAV("location_features_layer/kernel"));
@@ -2474,6 +2497,8 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   for (int t = T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
     at.t = t;
+    // (d align from the bf16 values copy measured 28.3 against 18.7 us per launch: hipcc waits
+    // vmcnt(0) behind the bf16 loads of each row -- the fp32 rows stay)
     if (A <= 128 && D <= 1024 && D % 4 == 0 && tr_e2) hipLaunchKernelGGL(k_tr_att_energy_bwd2, att_grid, dim3(TR_E2T), 0, s, at);
     else hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(TR_AT), 0, s, at);
     hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
@@ -3481,6 +3506,7 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
     TT2_HIP(hipSetDevice(hip_device));
     auto* c = new tt2_train_ctx();
     if (const char* e = std::getenv("TT2_TRAIN_BLAS")) c->blas_on = std::atoi(e) != 0;
+    if (const char* e = std::getenv("TT2_TR_VALUES16")) c->values16_on = std::atoi(e) != 0;
     try {
       c->dev = hip_device;
       c->cfg = *cfg;
