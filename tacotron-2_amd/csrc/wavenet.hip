@@ -634,6 +634,7 @@ struct tt2_wn_ctx {
   int R, G, S, L, C, cin;
   long hop;
   tt2::DevBuf first_w, first_b, conv_w, conv_b, cond_w, cond_b, so_w, so_b, f1_w, f1_b, f2_w, f2_b;
+  tt2::DevBuf w1, gb1;  // R = 256 one-hop form (wavenet_wide.h WideArgs::w1 / gb1)
   tt2::DevBuf up_k[8], up_b[8];
   tt2::DevBuf cin_d, up_a, up_b_buf, c_up_t, cond, umix, ulog, teacher, wav, kout, logits, gran, stamps;
   int chunk = 1;                 // utterances per generation launch
@@ -724,6 +725,58 @@ static void wn_finalize(tt2_wn_ctx* c) {
   }
   wupload(c->conv_w, c->wide ? wide_cw : cw);
   wupload(c->conv_b, cb);
+  if (c->wide && ww_onehop(R)) {  // one-hop R = 256 form: per layer M = rs·W_x(l)·O(l-1), folded biases
+    TT2_CHECK(R == 256 && G == 512 && S == 256, TT2_ERR_INVALID_ARG, "one-hop wide WaveNet needs R = 256");
+    const float rs = c->cfg.residual_legacy ? 0.70710677f : 1.f;
+    std::vector<float> w1, gb1((size_t)L * G);
+    std::vector<double> M((size_t)R * G);
+    const float* prev_o = nullptr;
+    const float* prev_s = nullptr;
+    const float* prev_bo = nullptr;
+    for (int l = 0; l <= L; ++l) {
+      const float* conv = nullptr;
+      const float* ko = nullptr;
+      const float* ksk = nullptr;
+      const float* bo = nullptr;
+      if (l < L) {
+        const std::string s = P + "ResidualConv1DGLU_" + std::to_string(l) + "/";
+        const std::string ln = "_ResidualConv1DGLU_" + std::to_string(l) + "/";
+        conv = need(wm, s + "residual_block_causal_conv" + ln + "kernel", {kw, R, G}).data.data();
+        ko = need(wm, s + "residual_block_out_conv" + ln + "kernel", {1, G / 2, R}).data.data();
+        ksk = need(wm, s + "residual_block_skip_conv" + ln + "kernel", {1, G / 2, S}).data.data();
+        bo = need(wm, s + "residual_block_out_conv" + ln + "bias", {R}).data.data();
+        for (int q = 0; q < G / 4; ++q)  // gate bias + rs·W_x(l)·bo(l-1), gate-permuted like conv_b
+          for (int e = 0; e < 4; ++e) {
+            const int src = gate_col(R, q, e);
+            double v = cb[(size_t)l * G + 4 * q + e];
+            if (prev_bo) {
+              double acc = 0.0;
+              for (int x = 0; x < R; ++x) acc += (double)conv[(size_t)(2 * R + x) * G + src] * prev_bo[x];
+              v += rs * acc;
+            }
+            gb1[(size_t)l * G + 4 * q + e] = (float)v;
+          }
+        if (prev_o) {  // M[z][g] = rs · Σ_x O(l-1)[z][x] · W_x(l)[x][g]
+          for (int z = 0; z < R; ++z) {
+            double* mr = M.data() + (size_t)z * G;
+            for (int g = 0; g < G; ++g) mr[g] = 0.0;
+            for (int x = 0; x < R; ++x) {
+              const double o = prev_o[(size_t)z * R + x];
+              const float* wr = conv + (size_t)(2 * R + x) * G;
+              for (int g = 0; g < G; ++g) mr[g] += o * wr[g];
+            }
+            for (int g = 0; g < G; ++g) mr[g] *= rs;
+          }
+        }
+      }
+      for (int cc = 0; cc < ww_nc(R); ++cc) ww1_pack(conv, prev_o, prev_s, prev_o && conv ? M.data() : nullptr, rs, cc, w1);
+      prev_o = ko;
+      prev_s = ksk;
+      prev_bo = bo;
+    }
+    wupload(c->w1, w1);
+    wupload(c->gb1, gb1);
+  }
   if (c->cfg.gin_channels > 0) {  // conv1x1g of every layer (modules.py:427-433) and the embedding
     for (int l = 0; l < L; ++l) {
       const std::string s = P + "ResidualConv1DGLU_" + std::to_string(l) + "/";
@@ -880,6 +933,8 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
     w.rings = c->rings.as<float>();
     w.status = c->gran.as<int>();
     w.gran = reinterpret_cast<unsigned long long*>(c->gran.as<char>() + 16);
+    w.w1 = c->w1.p ? c->w1.as<f32x4>() : nullptr;
+    w.gb1 = c->gb1.p ? c->gb1.as<float>() : nullptr;
     const void* kern = ww_kernel(R, c->C == 2);
     const unsigned shm = (unsigned)ww_lds_bytes(R, c->C);
     for (int b = 0; b < B; ++b) {  // one utterance per launch: its layers fill NC x L CUs

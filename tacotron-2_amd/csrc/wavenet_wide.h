@@ -35,7 +35,20 @@ struct WideArgs {
   float* rings;               // per (layer, CU): [2d+1][R] fast-WaveNet queue, zeroed by the kernel
   unsigned long long* gran;   // [L][NC][S+R] + 1 sample granule; zeroed before the launch
   int* status;
+  // R = 256 one-hop form (k_generate_wide<256, ·, true>, ww1_pack): per (layer, WG) [taps 32 | x rows 16
+  // | z rows (rs·W_x·O of the previous layer) 16 | [out | skip] columns of the previous layer 16]
+  // float4 per thread, for layers 0..L (L = the tail: the last layer's skips); gate biases with the
+  // previous layer's out bias folded in [L][G] (gate-permuted)
+  const f32x4* w1;
+  const float* gb1;
 };
+constexpr int W1_NW = 80;         // float4 weights per thread and (layer, WG) in the one-hop form
+constexpr int W1_GB = 3 * 256;    // granules per layer block: [z | x | skip]
+bool ww_onehop(int R);            // R == 256 and TT2_WW_ONEHOP != 0
+// one-hop packing of layer l (0..L; l == L the tail) for WG c: conv_l [3R][G] (null for the tail),
+// out / skip kernels of layer l-1 (null for l == 0), M = rs·W_x(l)·O(l-1) [R z][G] (null for l == 0)
+void ww1_pack(const float* conv_l, const float* out_prev, const float* skip_prev, const double* M, float rs, int c,
+              std::vector<float>& out);
 
 // Host packing of one layer's weights for CU c (row-major TF kernels: conv [3R][G], skip [R][S],
 // out [R][R]); appended to out.

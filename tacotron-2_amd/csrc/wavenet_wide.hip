@@ -21,6 +21,9 @@
 // and multiplied before the sample's input arrives (off the serial chain).
 #include "wavenet_wide.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace tt2 {
 
 typedef __attribute__((address_space(1))) unsigned long long ww_gu64;
@@ -74,7 +77,10 @@ __device__ __forceinline__ void ww_fma4(f32x4& acc, float x, const f32x4& w) {
   acc[0] += x * w[0]; acc[1] += x * w[1]; acc[2] += x * w[2]; acc[3] += x * w[3];
 }
 
-template <int R, bool GAUSS>
+template <bool GAUSS>
+__device__ void ww1_layer(const WideArgs& a, float* sm, const unsigned long long* sample_gran);
+
+template <int R, bool GAUSS, bool ONEHOP = false>
 __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
   constexpr int NC = ww_nc(R), S = R, G = 2 * R, ZC = R / NC, GC = 2 * ZC, NQ = GC / 4, NKS = WW_THREADS / NQ;
   // TWO_HOP (R = 256): work-group c gathers the whole z (an all-gather of the layer's NC z slices)
@@ -90,12 +96,12 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
   const float SQH = 0.70710677f;  // float32(np.sqrt(0.5))
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int L = a.L;
-  unsigned long long* const sample_gran = a.gran + (long)L * NG;
+  unsigned long long* const sample_gran = ONEHOP ? a.gran + (long)(L + 1) * W1_GB : a.gran + (long)L * NG;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   int* flag = reinterpret_cast<int*>(sm);
   if (tid == 0) flag[0] = 0;
 
-  if ((int)blockIdx.x == L * NC) {
+  if ((int)blockIdx.x == (ONEHOP ? (L + 1) * NC : L * NC)) {
     // ======================= head: ReLU -> 1x1 -> ReLU -> 1x1 -> sampler =======================
     constexpr int NQH = S / 4, NKSH = WW_THREADS / NQH, HK = S / NKSH;
     float* skv = sm + 16;          // [S] relu(skips)
@@ -115,7 +121,8 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
     }
     const float b2 = tid < a.C ? a.f2_b[tid] : 0.f;
     const int nr = a.C / 3;
-    const unsigned long long* gin = a.gran + (long)(L - 1) * NG;
+    // one-hop: the tail's skip block, read at [256 + tid] like the two-hop layer's x granules
+    const unsigned long long* gin = ONEHOP ? a.gran + (long)L * W1_GB + 2 * R - 256 : a.gran + (long)(L - 1) * NG;
     __syncthreads();
     for (int t = 0; t < a.T; ++t) {
       const int cb = t & 1;
@@ -131,7 +138,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
           gum[cb * 16 + 15] = (float)(log(uu) - log(1.0 - uu));
         }
       }
-      if constexpr (TWO_HOP) {  // skips = the last layer's skip slices (complete: WGs 0..S/OC-1)
+      if constexpr (TWO_HOP || ONEHOP) {  // skips = the last layer's complete skip slices
         float v = 0.f;
         const bool ok = ww_spin(a.status, lane, [&] {
           const unsigned long long x = ww_get(gin + 256 + tid);  // x granules after the 256 z granules
@@ -228,6 +235,10 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
     return;
   }
 
+  if constexpr (ONEHOP) {
+    ww1_layer<GAUSS>(a, sm, sample_gran);
+    return;
+  }
   // ============================ layer l, gate-column block c ============================
   const int l = blockIdx.x / NC, c = blockIdx.x % NC;
   float* xin = sm + 16;   // [R] x(t) of this layer
@@ -440,6 +451,201 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
   }
 }
 
+// ======================= R = 256 one-hop layer (k_generate_wide<256, ·, true>) =======================
+// The two-hop form all-gathers z inside a layer and then hands complete [skip | out] columns to the
+// next layer: two chip-wide hops per layer.  Here the next layer does both halves itself from ONE
+// all-gather of the previous layer's (z, x) slices:
+//   x_l = rs·(x_{l-1} + O_{l-1}·z_{l-1} + bo_{l-1})              (rs = sqrt(1/2) with legacy residuals)
+//   W_x(l)·x_l = rs·W_x(l)·x_{l-1} + [rs·W_x(l)·O_{l-1}]·z_{l-1} + rs·W_x(l)·bo_{l-1}
+// so work-group c of layer l holds rs·W_x(l) (its 64 gate columns over 256 x rows), the product
+// M = rs·W_x(l)·O_{l-1} (64 gate columns over 256 z rows, formed on the host in float64) and the
+// 32 + 32 [out | skip] columns of layer l-1 it completes for the chain (x_l slice c, skip_{l-1}
+// slice c) -- 192 weight registers per lane; the tap weights (x(t-2d) | x(t-d), off the serial
+// chain) sit in LDS (128 KB).  Per layer and sample the chain is: all-gather (z_{l-1}, x_{l-1}) ->
+// gates -> publish (z_l, x_l, skip_{l-1}) slices.  A layer appends x_l(t-1) to its queue from its
+// own work-groups' x slices at the start of sample t (off the chain); a tail of NC work-groups
+// completes the last layer's skips for the head.  Granules per layer block: [z R | x R | skip R].
+template <bool GAUSS>
+__device__ void ww1_layer(const WideArgs& a, float* sm, const unsigned long long* sample_gran) {
+  constexpr int R = 256, S = 256, G = 512, NC = 8, ZC = 32, GC = 64;
+  const float SQH = 0.70710677f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int* flag = reinterpret_cast<int*>(sm);
+  const int L = a.L;
+  const int l = blockIdx.x / NC, c = blockIdx.x % NC;
+  const bool tail = l == L;
+  f32x4* tapw = reinterpret_cast<f32x4*>(sm + 16);  // [32][256] tap weights
+  float* xprev = sm + 16 + 32 * WW_THREADS * 4;      // [R] x_{l-1}(t) (layer 0: x_0(t))
+  float* zin = xprev + R;                            // [R] z_{l-1}(t)
+  float* sk = zin + R;                               // [32] skip_{l-2}(t), slice c
+  const int q = tid >> 4, ks = tid & 15;             // gate / [out | skip] quad, k-slice of 16
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const f32x4* W = a.w1 + (long)(l * NC + c) * W1_NW * WW_THREADS + tid;
+  f32x4 wx[16], wm[16], wso[16];
+  for (int k = 0; k < 32; ++k) tapw[k * WW_THREADS + tid] = W[(long)k * WW_THREADS];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    wx[k] = W[(long)(32 + k) * WW_THREADS];
+    wm[k] = W[(long)(48 + k) * WW_THREADS];
+    wso[k] = W[(long)(64 + k) * WW_THREADS];
+  }
+  const float rs = a.res_legacy ? SQH : 1.f;
+  int d = 1, Lr = 3;
+  float* ring = nullptr;
+  if (!tail) {
+    d = 1 << (l % a.per);
+    Lr = 2 * d + 1;
+    long roff = 0;
+    for (int l2 = 0; l2 < l; ++l2) roff += (long)NC * (2 * (1 << (l2 % a.per)) + 1) * R;
+    ring = a.rings + roff + (long)c * Lr * R;
+    for (int i = tid; i < Lr * R; i += WW_THREADS) ring[i] = 0.f;
+  }
+  const f32x4 gbias = (ks == 0 && !tail) ? reinterpret_cast<const f32x4*>(a.gb1 + (long)l * G + c * GC)[q] : zero4;
+  // [out | skip] column constants of this quad: lc = 4q + e (< 32: out column c·32 + lc, else skip)
+  f32x4 sob = zero4;
+  if (l > 0 && ks == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int lc = 4 * q + e;
+      sob[e] = lc < 32 ? a.so_b[(long)(l - 1) * 2 * R + S + c * 32 + lc] : a.so_b[(long)(l - 1) * 2 * R + c * 32 + lc - 32];
+    }
+  }
+  const int tap_r0 = ks * 32, tap_blk = tap_r0 / R, tap_off = tap_r0 % R;  // blk 0: x(t-2d), 1: x(t-d)
+  const unsigned long long* gprev = l > 0 ? a.gran + (long)(l - 1) * W1_GB : nullptr;
+  unsigned long long* const gmine = a.gran + (long)l * W1_GB;
+  const float* condp = a.cond + ((long)a.b * a.T) * L * G + (long)(tail ? 0 : l) * G + c * GC;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int p = 0, pprev = 0;  // ring slot of x(t), of x(t-1)
+  for (int t = 0; t < a.T; ++t) {
+    f32x4 acc = zero4;
+    if (!tail) {
+      if (l > 0 && t > 0) {  // queue append of x_l(t-1): this layer's x slices of sample t-1 (tag t)
+        float v = 0.f;
+        const bool ok = ww_spin(a.status, lane, [&] {
+          const unsigned long long x = ww_get(gmine + R + tid);
+          v = __uint_as_float((unsigned)x);
+          return (unsigned)(x >> 32) == (unsigned)t;
+        });
+        if (!ok) flag[0] = 1;
+        ring[(long)pprev * R + tid] = v;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (flag[0]) return;
+      }
+      // ---- taps x(t-2d) | x(t-d) of this k-slice + conditioning + bias: before the input arrives ----
+      const int slot = tap_blk == 0 ? (p + 1 == Lr ? 0 : p + 1) : (p >= d ? p - d : p - d + Lr);
+      const float* row = ring + (long)slot * R + tap_off;
+#pragma unroll
+      for (int i4 = 0; i4 < 8; ++i4) {
+        const f32x4 xv = ww_ld4(row, i4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ww_fma4(acc, xv[e], tapw[(4 * i4 + e) * WW_THREADS + tid]);
+      }
+      if (ks == 0) {
+        const f32x4 cd = reinterpret_cast<const f32x4*>(condp + (long)t * L * G)[q];
+        for (int e = 0; e < 4; ++e) acc[e] += gbias[e] + cd[e];
+      }
+    }
+    // ---- input ----
+    if (l == 0) {
+      if (wave == 0) {  // first_conv 1x1 of the previous sample (wavenet.py:822-826); y_{-1} = 0
+        float y = 0.f;
+        bool ok = true;
+        if (t > 0)
+          ok = ww_spin(a.status, lane, [&] {
+            const unsigned long long x = ww_get(sample_gran);
+            y = __uint_as_float((unsigned)x);
+            return (unsigned)(x >> 32) == (unsigned)t;
+          });
+        if (!ok && lane == 0) flag[0] = 1;
+        for (int j = lane; j < R; j += 64) xprev[j] = y * a.first_w[j] + a.first_b[j];
+      }
+      __syncthreads();
+      if (flag[0]) return;
+      ring[(long)p * R + tid] = xprev[tid];  // queue append of x_0(t) (modules.py:285-288)
+    } else {  // the ONE hop: z_{l-1}(t), x_{l-1}(t) (all NC slices) and skip_{l-2}(t) slice c
+      float zv = 0.f, xv = 0.f, sv = 0.f;
+      const bool want_sk = l >= 2 && tid < 32;
+      const bool ok = ww_spin(a.status, lane, [&] {
+        const unsigned long long x0 = ww_get(gprev + tid), x1 = ww_get(gprev + R + tid);
+        zv = __uint_as_float((unsigned)x0);
+        xv = __uint_as_float((unsigned)x1);
+        bool good = (unsigned)(x0 >> 32) == (unsigned)(t + 1) && (unsigned)(x1 >> 32) == (unsigned)(t + 1);
+        if (want_sk) {
+          const unsigned long long x2 = ww_get(gprev + 2 * R + c * 32 + tid);
+          sv = __uint_as_float((unsigned)x2);
+          good = good && (unsigned)(x2 >> 32) == (unsigned)(t + 1);
+        }
+        return good;
+      });
+      if (!ok) flag[0] = 1;
+      zin[tid] = zv;
+      xprev[tid] = xv;
+      if (want_sk) sk[tid] = sv;
+      __syncthreads();
+      if (flag[0]) return;
+      // ---- complete [out | skip] columns of layer l-1 for slice c: x_l slice, skip_{l-1} slice ----
+      f32x4 acc2 = zero4;
+      const f32x4* zv4 = reinterpret_cast<const f32x4*>(zin + ks * 16);
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const f32x4 z4 = zv4[i4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ww_fma4(acc2, z4[e], wso[4 * i4 + e]);
+      }
+      ww_reduce<16>(acc2);
+      if (ks == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lc = 4 * q + e;
+          if (lc < 32) {  // residual output of layer l-1 = this layer's input slice
+            if (!tail) {
+              const int j = c * 32 + lc;
+              ww_put(gmine + R + j, (unsigned)(t + 1), (xprev[j] + acc2[e] + sob[e]) * rs);
+            }
+          } else {        // skips (wavenet.py:833-836): + running sum, legacy scaling past layer 0
+            const int j = c * 32 + lc - 32;
+            float v = acc2[e] + sob[e];
+            if (l - 1 > 0) v += sk[lc - 32];
+            if (a.legacy && l - 1 > 0) v *= SQH;
+            ww_put(gmine + 2 * R + j, (unsigned)(t + 1), v);
+          }
+        }
+      }
+    }
+    if (!tail) {
+      // ---- gates: layer 0 W_x·x_0(t); else rs·W_x·x_{l-1} + M·z_{l-1} (biases folded) ----
+      const f32x4* xv4 = reinterpret_cast<const f32x4*>(xprev + ks * 16);
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const f32x4 x4 = xv4[i4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ww_fma4(acc, x4[e], wx[4 * i4 + e]);
+      }
+      if (l > 0) {
+        const f32x4* zv4 = reinterpret_cast<const f32x4*>(zin + ks * 16);
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const f32x4 z4 = zv4[i4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ww_fma4(acc, z4[e], wm[4 * i4 + e]);
+        }
+      }
+      ww_reduce<16>(acc);
+      if (ks == 0) {
+        ww_put(gmine + c * ZC + 2 * q, (unsigned)(t + 1), tanhf(acc[0]) * sigm(acc[2]));
+        ww_put(gmine + c * ZC + 2 * q + 1, (unsigned)(t + 1), tanhf(acc[1]) * sigm(acc[3]));
+      }
+      if (l == 0 && tid < 32) ww_put(gmine + R + c * 32 + tid, (unsigned)(t + 1), xprev[c * 32 + tid]);
+      pprev = p;
+      p = p + 1 == Lr ? 0 : p + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // queue appends drained before their reads
+    __syncthreads();
+  }
+}
+
 // ----------------------------------------------------------------------------------- host side
 
 static inline int gate_col_w(int R, int q, int e) { return (e < 2 ? 2 * q + e : R + 2 * q + (e - 2)); }
@@ -488,19 +694,59 @@ size_t ww_ring_floats(int R, int L, int per) {
   return n;
 }
 
+bool ww_onehop(int R) {
+  static const bool on = [] {
+    const char* e = std::getenv("TT2_WW_ONEHOP");  // 0: the two-hop R = 256 form
+    return !e || std::atoi(e) != 0;
+  }();
+  return R == 256 && on;
+}
+
 size_t ww_lds_bytes(int R, int C) {
   (void)C;
   const int S = R;
-  return sizeof(float) * (size_t)(16 + 2 * S + 32 + 32 + S * 32 + 32 * 32 + 64);
+  const size_t head = 16 + 2 * S + 32 + 32 + S * 32 + 32 * 32 + 64;
+  const size_t layer1 = 16 + 32 * WW_THREADS * 4 + 2 * R + 32;  // one-hop layer: tap weights + x, z, skip
+  return sizeof(float) * (ww_onehop(R) ? std::max(head, layer1) : head);
 }
 
-int ww_blocks(int R, int L) { return L * ww_nc(R) + 1; }
+int ww_blocks(int R, int L) { return ww_onehop(R) ? (L + 1) * ww_nc(R) + 1 : L * ww_nc(R) + 1; }
 
 const void* ww_kernel(int R, bool gauss) {
   if (R == 128) return gauss ? reinterpret_cast<const void*>(k_generate_wide<128, true>)
                              : reinterpret_cast<const void*>(k_generate_wide<128, false>);
+  if (ww_onehop(R))
+    return gauss ? reinterpret_cast<const void*>(k_generate_wide<256, true, true>)
+                 : reinterpret_cast<const void*>(k_generate_wide<256, false, true>);
   return gauss ? reinterpret_cast<const void*>(k_generate_wide<256, true>)
                : reinterpret_cast<const void*>(k_generate_wide<256, false>);
+}
+
+void ww1_pack(const float* conv_l, const float* out_prev, const float* skip_prev, const double* M, float rs, int c,
+              std::vector<float>& out) {
+  constexpr int R = 256, S = 256, G = 512;
+  const size_t base = out.size();
+  out.resize(base + (size_t)W1_NW * WW_THREADS * 4, 0.f);
+  for (int tid = 0; tid < WW_THREADS; ++tid) {
+    const int q = tid >> 4, ks = tid & 15, gq = c * 16 + q;
+    auto put = [&](int kk, int e, float v) { out[base + ((size_t)kk * WW_THREADS + tid) * 4 + e] = v; };
+    for (int e = 0; e < 4; ++e) {
+      const int col = gate_col_w(R, gq, e);
+      if (conv_l) {
+        for (int kk = 0; kk < 32; ++kk) put(kk, e, conv_l[(size_t)(ks * 32 + kk) * G + col]);
+        for (int kk = 0; kk < 16; ++kk) put(32 + kk, e, (out_prev ? rs : 1.f) * conv_l[(size_t)(2 * R + ks * 16 + kk) * G + col]);
+        if (M)
+          for (int kk = 0; kk < 16; ++kk) put(48 + kk, e, (float)M[(size_t)(ks * 16 + kk) * G + col]);
+      }
+      if (out_prev) {
+        const int lc = 4 * q + e;
+        for (int kk = 0; kk < 16; ++kk) {
+          const int zrow = ks * 16 + kk;
+          put(64 + kk, e, lc < 32 ? out_prev[(size_t)zrow * R + c * 32 + lc] : skip_prev[(size_t)zrow * S + c * 32 + lc - 32]);
+        }
+      }
+    }
+  }
 }
 
 }  // namespace tt2
