@@ -73,6 +73,10 @@ __device__ __forceinline__ void ww_reduce(f32x4& a) {
 #undef TT2_STEP
 }
 
+// gate nonlinearities of the one-hop form on v_exp_f32 + one division (|abs err| < 3e-7)
+__device__ __forceinline__ float ww_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
+__device__ __forceinline__ float ww_sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
 __device__ __forceinline__ void ww_fma4(f32x4& acc, float x, const f32x4& w) {
   acc[0] += x * w[0]; acc[1] += x * w[1]; acc[2] += x * w[2]; acc[3] += x * w[3];
 }
@@ -634,8 +638,8 @@ __device__ void ww1_layer(const WideArgs& a, float* sm, const unsigned long long
       }
       ww_reduce<16>(acc);
       if (ks == 0) {
-        ww_put(gmine + c * ZC + 2 * q, (unsigned)(t + 1), tanhf(acc[0]) * sigm(acc[2]));
-        ww_put(gmine + c * ZC + 2 * q + 1, (unsigned)(t + 1), tanhf(acc[1]) * sigm(acc[3]));
+        ww_put(gmine + c * ZC + 2 * q, (unsigned)(t + 1), ww_tanh(acc[0]) * ww_sigm(acc[2]));
+        ww_put(gmine + c * ZC + 2 * q + 1, (unsigned)(t + 1), ww_tanh(acc[1]) * ww_sigm(acc[3]));
       }
       if (l == 0 && tid < 32) ww_put(gmine + R + c * 32 + tid, (unsigned)(t + 1), xprev[c * 32 + tid]);
       pprev = p;
