@@ -83,6 +83,8 @@ struct tt2_train_ctx {
   // bf16 Postnet convolutions over padded planes (gemm.h conv_bf16_planes): the layer input / dz
   // planes (pad rows zeroed when the shape changes) and the transposed bf16 weights of one layer
   DevBuf pnPl, pnWt;
+  DevBuf fePl, feWt;  // the same for the text encoder's convolutions (TT2_PN_PLANES gates both)
+  int fe_pl_B = -1, fe_pl_T = -1;
   DevBuf values16;         // bf16 values for the per-step context / d align reads (TT2_TR_VALUES16)
   bool values16_on = true;
   int pn_pl_B = -1, pn_pl_T = -1;
@@ -2740,6 +2742,13 @@ static void tr_front_alloc(tt2_train_ctx* c) {
   const long BT = B * T, K = f.enc_conv_kernel;
   auto a = [](DevBuf& d, long n) { d.alloc(sizeof(float) * (size_t)std::max<long>(n, 1)); };
   a(c->fEX, BT * E);
+  const char* pe = std::getenv("TT2_PN_PLANES");  // 0: implicit-im2col gemm_x3_kernel convs here too
+  if ((!pe || std::atoi(pe) != 0) && c->cfg.precision && C % 64 == 0 && E % 64 == 0 && (K & 1) &&
+      K <= 2 * CX_P + 1) {
+    const long W = std::max(C, E), Wr = (W + 255) / 256 * 256;
+    c->fePl.alloc((size_t)cx_rows((int)B, (int)T) * W * 2);
+    c->feWt.alloc((size_t)Wr * K * W * 2);
+  }
   for (int i = 0; i < f.enc_conv_layers; ++i) {
     a(c->fEA[i], BT * C);
     a(c->fEY[i + 1], BT * C);
@@ -2813,7 +2822,7 @@ static void fe_stats(tt2_train_ctx* c, const float* x, long M, int C, float* mea
 // BN backward (batch statistics) from dy -> dz (act: 0 none, 2 relu' from the pre-BN activation)
 static void fe_bn_bwd(tt2_train_ctx* c, const float* dxn, const uint8_t* keep, const float* a, long M, int C,
                       const float* mean, const float* var, const std::string& sc, int act, float* dy, float* dz,
-                      hipStream_t s) {
+                      hipStream_t s, __bf16* planes = nullptr, int T = 1) {
   const int S = tr_splits(M, C, 64L * 512);
   float* part = c->fpart.as<float>();
   float* sums = part + 64L * 2 * 512;
@@ -2823,7 +2832,13 @@ static void fe_bn_bwd(tt2_train_ctx* c, const float* dxn, const uint8_t* keep, c
   hipLaunchKernelGGL(k_pn_bn_bwd_final, dim3((C + 31) / 32), dim3(TR_FIN), 0, s, part, S, C, sums,
                      gvar(c, sc + "batch_normalization/gamma"), gvar(c, sc + "batch_normalization/beta"));
   hipLaunchKernelGGL(k_pn_bn_bwd_dz, dim3(nblk(M * C)), dim3(256), 0, s, dy, a, M, C, mean, var, eps,
-                     pvar(c, sc + "batch_normalization/gamma"), sums, act, dz);
+                     pvar(c, sc + "batch_normalization/gamma"), sums, act, dz, planes, T);
+}
+
+// fp32 rows [B·T][C] (batch-major) -> the padded bf16 planes of conv_bf16_planes (frame rows only)
+__global__ void k_rows_to_planes(const float* __restrict__ x, long M, int C, int T, __bf16* __restrict__ planes) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < M * C) pn_plane_put(planes, T, i, C, x[i]);
 }
 
 static FeGst fe_gst_args(tt2_train_ctx* c, int r, int B) {
@@ -2854,21 +2869,41 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
   fe_embed(ids, pvar(c, vn("inputs_embedding")), M, E, c->fEX.as<float>(), s);
   // EncoderConvolutions (modules.py:251-280, conv1d() :485-497 with bnorm 'after'): conv -> ReLU ->
   // BN (batch statistics over all B·T positions) -> dropout(0.5, keep bits)
+  // bf16 conv over padded planes (conv_bf16_planes, as the Postnet's): planes of the embedding here,
+  // of each layer's output from its BN forward; pad rows zeroed once per shape
+  const bool planes = c->fePl.p && g_tr_prec == 2;
+  __bf16* pl = reinterpret_cast<__bf16*>(c->fePl.p);
+  __bf16* wt = reinterpret_cast<__bf16*>(c->feWt.p);
+  if (planes) {
+    if (c->fe_pl_B != B || c->fe_pl_T != T) {
+      TT2_HIP(hipMemsetAsync(c->fePl.p, 0, c->fePl.bytes, s));
+      c->fe_pl_B = B;
+      c->fe_pl_T = T;
+    }
+    hipLaunchKernelGGL(k_rows_to_planes, dim3(nblk(M * E)), dim3(256), 0, s, c->fEX.as<float>(), M, E, T, pl);
+  }
   for (int i = 0; i < f.enc_conv_layers; ++i) {
     const std::string sc = fe_conv_scope(i + 1);
     const int cin = i == 0 ? E : C;
-    GemmArgs g;
-    g.a_mode = A_CONV1D; g.M = (int)M; g.N = C; g.T = T; g.kw = K; g.pad = (K - 1) / 2; g.C = cin;
-    g.A = i == 0 ? c->fEX.as<float>() : c->fEY[i].as<float>(); g.xs_b = (long)T * cin; g.xs_t = cin; g.K = K * cin;
-    g.Bw = pvar(c, sc + "conv1d/kernel"); g.ldb = C; g.Cout = c->fEA[i].as<float>(); g.ldc = C;
-    g.bias = pvar(c, sc + "conv1d/bias"); g.act = ACT_RELU;
-    tr_gemm_run(g, s);
+    if (planes) {
+      kc_transpose_bf16(pvar(c, sc + "conv1d/kernel"), K * cin, C, C, wt, K * cin, (C + 255) / 256 * 256, s);
+      conv_bf16_planes(pl, cin, B, T, K, wt, (long)K * cin, C, pvar(c, sc + "conv1d/bias"), ACT_RELU,
+                       c->fEA[i].as<float>(), C, s);
+    } else {
+      GemmArgs g;
+      g.a_mode = A_CONV1D; g.M = (int)M; g.N = C; g.T = T; g.kw = K; g.pad = (K - 1) / 2; g.C = cin;
+      g.A = i == 0 ? c->fEX.as<float>() : c->fEY[i].as<float>(); g.xs_b = (long)T * cin; g.xs_t = cin; g.K = K * cin;
+      g.Bw = pvar(c, sc + "conv1d/kernel"); g.ldb = C; g.Cout = c->fEA[i].as<float>(); g.ldc = C;
+      g.bias = pvar(c, sc + "conv1d/bias"); g.act = ACT_RELU;
+      tr_gemm_run(g, s);
+    }
     float* mean = BN + (long)i * 2 * 512;
     float* var = mean + 512;
     fe_stats(c, c->fEA[i].as<float>(), M, C, mean, var, s);
     hipLaunchKernelGGL(k_pn_bn_fwd, dim3(nblk(M * C)), dim3(256), 0, s, c->fEA[i].as<float>(), M, C, mean, var,
                        pvar(c, sc + "batch_normalization/gamma"), pvar(c, sc + "batch_normalization/beta"), eps,
-                       encm ? encm + (long)i * M * C : nullptr, c->fEY[i + 1].as<float>());
+                       encm ? encm + (long)i * M * C : nullptr, c->fEY[i + 1].as<float>(),
+                       planes && i + 1 < f.enc_conv_layers ? pl : nullptr, T);
   }
   // EncoderRNN (modules.py:283-323): input projections of both directions for every position
   const float* X = c->fEY[f.enc_conv_layers].as<float>();
@@ -3289,21 +3324,37 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
     const float* mean = BN + (long)i * 2 * 512;
     const float* var = mean + 512;
     float* dz = c->fDZc.as<float>();
+    const bool bplanes = c->fePl.p && g_tr_prec == 2;
+    __bf16* bpl = reinterpret_cast<__bf16*>(c->fePl.p);
     fe_bn_bwd(c, dxn, encm ? encm + (long)i * M * C : nullptr, c->fEA[i].as<float>(), M, C, mean, var, sc, 2,
-              c->fDY.as<float>(), dz, s);
+              c->fDY.as<float>(), dz, s, bplanes ? bpl : nullptr, T);
     tr_colsum(c, dz, M, C, C, gvar(c, sc + "conv1d/bias"), s);
     const int cin = i == 0 ? E : C, pad = (K - 1) / 2;
     const float* xin = i == 0 ? c->fEX.as<float>() : c->fEY[i].as<float>();
-    hipLaunchKernelGGL(k_pn_im2col_t, dim3(nblk((long)K * cin * M)), dim3(256), 0, s, xin, (long)T * cin, (long)cin, B,
-                       T, cin, K, pad, FB, M);
-    tr_gemm(K * cin, C, (int)M, FB, M, dz, C, gvar(c, sc + "conv1d/kernel"), C, s);
+    if (c->blas_on && g_tr_prec == 2 && 2.0 * K * cin * (double)C * M >= kTrBigMinFlops) {
+      KcConvA cv;  // im2colᵀ gathered straight into gemm_bf16_kc's bf16 operand copy
+      cv.x = xin; cv.xs_b = (long)T * cin; cv.xs_t = cin; cv.B = B; cv.T = T; cv.C = cin; cv.kw = K; cv.pad = pad;
+      gemm_bf16_kc(K * cin, C, (int)M, nullptr, 0, dz, C, gvar(c, sc + "conv1d/kernel"), C, c->blasA, c->blasB,
+                   c->blasP, s, false, &cv);
+      ++c->blas_calls;
+    } else {
+      hipLaunchKernelGGL(k_pn_im2col_t, dim3(nblk((long)K * cin * M)), dim3(256), 0, s, xin, (long)T * cin, (long)cin,
+                         B, T, cin, K, pad, FB, M);
+      tr_gemm(K * cin, C, (int)M, FB, M, dz, C, gvar(c, sc + "conv1d/kernel"), C, s);
+    }
     hipLaunchKernelGGL(k_pn_flip, dim3(nblk((long)K * cin * C)), dim3(256), 0, s, pvar(c, sc + "conv1d/kernel"), K, cin,
                        C, WT);
-    GemmArgs g;
-    g.a_mode = A_CONV1D; g.M = (int)M; g.N = cin; g.T = T; g.kw = K; g.pad = K - 1 - pad;
-    g.A = dz; g.C = C; g.xs_b = (long)T * C; g.xs_t = C; g.K = K * C;
-    g.Bw = WT; g.ldb = cin; g.Cout = dxo; g.ldc = cin;
-    tr_gemm_run(g, s);
+    if (bplanes) {  // input gradient: conv of the dz planes with the flipped kernel
+      __bf16* bwt = reinterpret_cast<__bf16*>(c->feWt.p);
+      kc_transpose_bf16(WT, K * C, cin, cin, bwt, K * C, (cin + 255) / 256 * 256, s);
+      conv_bf16_planes(bpl, C, B, T, K, bwt, (long)K * C, cin, nullptr, ACT_NONE, dxo, cin, s);
+    } else {
+      GemmArgs g;
+      g.a_mode = A_CONV1D; g.M = (int)M; g.N = cin; g.T = T; g.kw = K; g.pad = K - 1 - pad;
+      g.A = dz; g.C = C; g.xs_b = (long)T * C; g.xs_t = C; g.K = K * C;
+      g.Bw = WT; g.ldb = cin; g.Cout = dxo; g.ldc = cin;
+      tr_gemm_run(g, s);
+    }
     std::swap(dxn, dxo);
   }
   fe_embed_bwd(ids, dxn, M, E, f.n_symbols, gvar(c, vn("inputs_embedding")), s, FB,

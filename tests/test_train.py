@@ -848,3 +848,49 @@ def test_gpu_train_postnet_planes_match_im2col(T_out):
         # the prenet's gradients move 2-6 % under any bf16 perturbation (bf16-rounded
         # pre-activations near zero flip ReLU decisions)
         assert rel < (6e-2 if "decoder_prenet" in n else 2e-2), (n, rel)
+
+
+@pytest.mark.gpu
+def test_gpu_train_encoder_planes_match_im2col():
+    """bf16 step from ids with the text encoder's conv forward / input-gradient products over padded
+    bf16 planes (conv_bf16_planes; the embedding's planes from k_rows_to_planes, the layers' from
+    the BN forward / backward kernels) and the Postnet's, against TT2_PN_PLANES=0: losses within
+    1e-4 relative, gradients within 5e-2 (measured up to 2.2e-2: the same bf16 operands summed in
+    another order move the ReLU / BN-sensitive front-end gradients, e.g. the GST weight norm g, by
+    about that much)."""
+    import os
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    hp.override_from_dict(dict(enc_conv_channels=128, embedding_dim=128, encoder_lstm_units=64))
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, B=6, T_in=23, T_out=8, T_ref=64)
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    names = TRN.frontend_var_names() + TRN.postnet_var_names()
+    res = {}
+    old = os.environ.get("TT2_PN_PLANES")
+    try:
+        for flag in ("1", "0"):
+            os.environ["TT2_PN_PLANES"] = flag
+            tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", frontend=True, max_T_ref=re.shape[1])
+            try:
+                tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+                L = tr.losses()
+                g = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}
+            finally:
+                tr.close()
+            res[flag] = (L, g)
+    finally:
+        if old is None:
+            os.environ.pop("TT2_PN_PLANES", None)
+        else:
+            os.environ["TT2_PN_PLANES"] = old
+    (La, ga), (Lb, gb) = res["1"], res["0"]
+    for k in ("before", "after"):
+        assert abs(La[k] - Lb[k]) < 1e-4 * abs(Lb[k]), (k, La[k], Lb[k])
+    for n in ga:
+        den = np.linalg.norm(gb[n])
+        if n.endswith("conv_layer_5_postnet_convolutions/conv1d/bias") or n.endswith("conv2d/bias"):
+            # conv -> training BN with no activation between (Postnet layer 5, every refnet conv2d):
+            # d bias = Σ dz = 0 up to rounding noise; measured against the kernel gradient's norm
+            den = max(den, np.linalg.norm(gb[n.replace("/bias", "/kernel")]))
+        rel = float(np.linalg.norm(ga[n] - gb[n]) / max(den, 1e-30))
+        assert rel < 5e-2, (n, rel)
