@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
+#include <cstdio>
 
 namespace tt2 {
 

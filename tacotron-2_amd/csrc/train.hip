@@ -1883,7 +1883,8 @@ __global__ void k_tr_to_bf16(const float* __restrict__ src, long rows, long cols
 // kernel (gemm.h gemm_bf16_kc: both operands rounded to bf16 into padded K-contiguous copies, B
 // transposed on the way, K split over work-groups for the few-tile shapes, fp32 accumulation) --
 // the same operand rounding as the per-step bf16 kernels.  Products below kTrBigMinFlops keep the
-// per-step kernels' paths.
+// per-step kernels' paths, except tall ones (>= 16k rows, N >= 256, K >= 64: e.g. d [h2 | ctx] =
+// d frames · W_f^T over all T·B rows, bound by its output, which gemm_x3_kernel wrote at 0.6 TB/s).
 static constexpr double kTrBigMinFlops = 2.0e10;
 static bool tr_gemm_big(int M, int N, int K, const float* A, long lda, const float* Bw, long ldb, float* C, long ldc,
                         hipStream_t s) {
@@ -1917,7 +1918,8 @@ static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* 
                     hipStream_t s, const float* bias = nullptr, const float* residual = nullptr, long ldr = 0,
                     int act = ACT_NONE, const DevBuf* bt16 = nullptr, long ldbt = 0) {
   if (g_tr_ctx && g_tr_ctx->blas_on && g_tr_prec == 2 && !bias && !residual && act == ACT_NONE &&
-      2.0 * M * (double)N * K >= kTrBigMinFlops && tr_gemm_big(M, N, K, A, lda, Bw, ldb, C, ldc, s))
+      (2.0 * M * (double)N * K >= kTrBigMinFlops || (M >= 16384 && N >= 256 && K >= 64)) &&
+      tr_gemm_big(M, N, K, A, lda, Bw, ldb, C, ldc, s))
     return;
   GemmArgs g;
   if (g_tr_prec == 2 && bt16 && bt16->p && ldbt % 8 == 0) {  // weights pre-converted: B^T in bf16
@@ -2274,6 +2276,19 @@ static bool tr_has_free_steps(const tt2_train_ctx* c, int T) {
 }
 
 // forward + losses + backward for one batch; grads complete (incl. L2) on return (stream order)
+// Y[m][n] += u[m]·v[n] over M x N (N % 4 == 0, 16-byte rows): the stop projection's d input
+__global__ void k_tr_rank1_add(float* __restrict__ Y, long ld, const float* __restrict__ u, const float* __restrict__ v,
+                               long M, int N) {
+  const int n4 = N >> 2;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < M * n4; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / n4;
+    const int c = (int)(i - m * n4) * 4;
+    f32x4* y = reinterpret_cast<f32x4*>(Y + m * ld + c);
+    const f32x4 w = *reinterpret_cast<const f32x4*>(v + c);
+    *y += u[m] * w;
+  }
+}
+
 static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* lens, const float* tg, const float* stg,
                                 const uint8_t* pm, const uint8_t* zm, const uint8_t* pnm, int Tin, int T,
                                 hipStream_t s) {
@@ -2491,7 +2506,12 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   float* dX1 = c->dX1.as<float>();
   float* dX2 = c->dX2.as<float>();
   tr_gemm((int)TB, H + D, NM, c->dFR.as<float>(), NM, c->WfT.as<float>(), H + D, dPIN, H + D, s);
-  tr_gemm((int)TB, H + D, 1, c->dST.as<float>(), 1, c->WsT.as<float>(), H + D, dPIN, H + D, s, nullptr, dPIN, H + D);
+  // + dST·W_s^T: a rank-1 update, streamed (as a K = 1 GEMM with the residual it took 0.69 ms)
+  if ((H + D) % 4 == 0)
+    hipLaunchKernelGGL(k_tr_rank1_add, dim3(2048), dim3(256), 0, s, dPIN, (long)(H + D), c->dST.as<float>(),
+                       c->WsT.as<float>(), TB, H + D);
+  else
+    tr_gemm((int)TB, H + D, 1, c->dST.as<float>(), 1, c->WsT.as<float>(), H + D, dPIN, H + D, s, nullptr, dPIN, H + D);
   TT2_HIP(hipMemsetAsync(dX1 + TB * LX1, 0, sizeof(float) * (size_t)B * LX1, s));
   TT2_HIP(hipMemsetAsync(dX2 + TB * 2 * H, 0, sizeof(float) * (size_t)B * 2 * H, s));
   for (DevBuf* d : {&c->DC1, &c->DC2, &c->R1, &c->R2, &c->DKEYS, &c->DCUM, &c->dV, &c->dBA, &c->dKC, &c->dBC})
