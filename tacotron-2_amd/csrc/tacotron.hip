@@ -219,6 +219,7 @@ struct EncPArgs {
   int B, T, Tmax;
   float zo, one_m_zo;
   int* err;            // timeout flag
+  int sentinel;        // poll one sentinel granule per producer before the full h load (TT2_ENC_SENTINEL)
 };
 
 __global__ __launch_bounds__(256) void k_enc_bilstm_persist(EncPArgs a) {
@@ -245,13 +246,22 @@ __global__ __launch_bounds__(256) void k_enc_bilstm_persist(EncPArgs a) {
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, w = tid >> 6;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    // this step's input projections, loaded before the h hand-off (off the serial chain)
+    const bool act = tid < 128 && t < L;
+    float xz[4] = {0.f, 0.f, 0.f, 0.f};
+    const int pos = dir == 0 ? t : L - 1 - t;
+    if (act) {
+      const float* xp = a.xproj + ((long)m * a.T + pos) * (8 * U) + dir * 4 * U;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) xz[gq] = xp[gq * U + u];
+    }
     if (t > 0) {  // h(t-1): parity (t-1)&1, tag t
       const auto rp = (t & 1) ? r0 : r1;
       f32x4 x0[NKG], x1[NKG];
       long long t0 = 0;
       // cheap poll first: one sentinel granule (row 0 of the producer's first unit) per producer
       // work-group of this wave's k-slice (units [U/4·w, U/4·(w+1)) = producers [16w, 16w+16))
-      for (unsigned spin = 0;; ++spin) {
+      for (unsigned spin = 0; a.sentinel; ++spin) {
         bool ok = true;
         if (lane < U / 16) {
           const unsigned long long* sp = Hd + ((t - 1) & 1) * 32 * U + af_idx(0, 4 * (U / 16 * w + lane));
@@ -304,14 +314,11 @@ __global__ __launch_bounds__(256) void k_enc_bilstm_persist(EncPArgs a) {
     }
     reduce_waves_32x16<4>(acc0, acc1, red, G, w, lane, tid);
     if (tid < 128) {
-      const bool act = t < L;
       if (act) {
-        const int pos = dir == 0 ? t : L - 1 - t;
-        const float* xp = a.xproj + ((long)m * a.T + pos) * (8 * U) + dir * 4 * U;
-        const float zi = G[m * 16 + 0 * 4 + uu] * KG_UNSCALE + xp[0 * U + u];
-        const float zj = G[m * 16 + 1 * 4 + uu] * KG_UNSCALE + xp[1 * U + u];
-        const float zf = G[m * 16 + 2 * 4 + uu] * KG_UNSCALE + xp[2 * U + u];
-        const float zz = G[m * 16 + 3 * 4 + uu] * KG_UNSCALE + xp[3 * U + u];
+        const float zi = G[m * 16 + 0 * 4 + uu] * KG_UNSCALE + xz[0];
+        const float zj = G[m * 16 + 1 * 4 + uu] * KG_UNSCALE + xz[1];
+        const float zf = G[m * 16 + 2 * 4 + uu] * KG_UNSCALE + xz[2];
+        const float zz = G[m * 16 + 3 * 4 + uu] * KG_UNSCALE + xz[3];
         const float cn = sigm(zf + 1.0f) * c + sigm(zi) * tanhf(zj);
         const float hn = sigm(zz) * tanhf(cn);
         c = a.one_m_zo * cn + a.zo * c;
@@ -1922,6 +1929,10 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     a.out = c->enc_out.as<float>(); a.lengths = lens_d; a.B = B; a.T = T; a.Tmax = Tmax;
     a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
     a.err = reinterpret_cast<int*>(a.Hg + 2 * 2 * 32 * ENC_U);
+    {
+      const char* e = std::getenv("TT2_ENC_SENTINEL");
+      a.sentinel = e ? std::atoi(e) : 1;
+    }
     void* params[] = {&a};  // cooperative: all 128 work-groups co-resident (h hand-offs spin)
     TT2_HIP(launch_persistent(reinterpret_cast<const void*>(k_enc_bilstm_persist), dim3(2 * ENC_U / 4),
                                        dim3(256), params, 0u, s));
