@@ -1016,7 +1016,7 @@ __device__ __forceinline__ void cxw_apply(f32x16 (&acc)[4][2], const unsigned (&
       for (int j = 0; j < 2; ++j) acc[i][j][q] = ((fm[i] >> q) & 1u) ? cx_epi<ACT>(acc[i][j][q], cc[j]) * X3_SA : 0.f;
 }
 
-template <int ACT>
+template <int ACT, bool SPLIT = false>
 __global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt, int n_nt) {
   __shared__ __attribute__((aligned(16))) _Float16 sm[CXW_LDS];  // [stage][A hi, A lo, B hi, B lo][256][32]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1058,14 +1058,16 @@ __global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-  const int nk = g.kw * g.Cp / X3_BK;
-  stage(0, 0);
+  // K split over blockIdx.y (ConvX3Args::ks): k-steps [kt0, kt0 + nk)
+  const int nkt = g.kw * g.Cp / X3_BK, per = SPLIT ? (nkt + gridDim.y - 1) / gridDim.y : nkt;
+  const int kt0 = SPLIT ? blockIdx.y * per : 0, nk = SPLIT ? min(nkt, kt0 + per) - kt0 : nkt;
+  stage(kt0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int r = lane & 31, hl = lane >> 5, sw = (r >> 2) & 3;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    if (kt + 1 < nk) stage(kt0 + kt + 1, cur ^ 1);
     const _Float16* S = sm + cur * 4 * CXW_PLANE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1094,6 +1096,21 @@ __global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt
   // epilogue: y·2^4 in place (pad rows and rows past B·Tp -> 0), then each plane through LDS
   const int Tp = g.T + 2 * CX_P;
   const long mrows = (long)g.B * Tp;
+  if constexpr (SPLIT) {  // raw partials of this K slice (padded rows), combined by k_cx_reduce
+    float* P = g.part + (long)blockIdx.y * mrows * g.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + r;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const long m = m0 + wm * 128 + i * 32 + 4 * hl + (q & 3) + 8 * (q >> 2);
+          if (m < mrows) P[m * g.N + col] = acc[i][j][q];
+        }
+      }
+    return;
+  }
   unsigned fm[4] = {0u, 0u, 0u, 0u};  // frame bit of (i, q)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1204,13 +1221,20 @@ void conv_x3(const ConvX3Args& a, hipStream_t s) {
             "conv_x3: planes output needs N % 128 == 0 and aligned planes");
   const char* ew = std::getenv("TT2_CX_WIDE");  // 0: the 128 x 128 register-staged kernel for every layer
   const bool wide = !ew || std::atoi(ew) != 0;
-  if (a.ks > 1) {  // split K over blockIdx.y of the 128 x 128 kernel + one combine launch
+  if (a.ks > 1) {  // split K over blockIdx.y + one combine launch
     const long mrows = (long)a.B * (a.T + 2 * CX_P);
     TT2_CHECK(a.part && a.N % 4 == 0 && (long)a.ks * mrows * a.N <= a.part_floats && a.ks <= a.kw * a.Cp / X3_BK,
               TT2_ERR_INVALID_ARG, "conv_x3: split-K needs part >= ks x rows x N floats, N % 4 == 0");
-    const int n_mt = cdiv(a.B * (a.T + 2 * CX_P), CX_BM), n_nt = cdiv(a.N, CX_BN);
-    const dim3 grid((unsigned)(cdiv(n_mt, 8) * 8 * n_nt), (unsigned)a.ks);
-    hipLaunchKernelGGL(conv_x3_kernel<false>, grid, dim3(256), 0, s, a, n_mt, n_nt);
+    const char* ewk = std::getenv("TT2_CX_WIDE_SPLIT");  // 0: the 128 x 128 kernel for the K-split layers
+    if (a.N % CXW_BN == 0 && (!ewk || std::atoi(ewk) != 0)) {
+      const int n_mt = cdiv(a.B * (a.T + 2 * CX_P), CXW_BM), n_nt = a.N / CXW_BN;
+      hipLaunchKernelGGL((conv_x3w_kernel<ACT_NONE, true>), dim3((unsigned)(cdiv(n_mt, 8) * 8 * n_nt), (unsigned)a.ks),
+                         dim3(512), 0, s, a, n_mt, n_nt);
+    } else {
+      const int n_mt = cdiv(a.B * (a.T + 2 * CX_P), CX_BM), n_nt = cdiv(a.N, CX_BN);
+      const dim3 grid((unsigned)(cdiv(n_mt, 8) * 8 * n_nt), (unsigned)a.ks);
+      hipLaunchKernelGGL(conv_x3_kernel<false>, grid, dim3(256), 0, s, a, n_mt, n_nt);
+    }
     TT2_HIP(hipGetLastError());
     const dim3 rg((unsigned)((mrows * (a.N / 4) + 255) / 256));
     if (a.act == ACT_TANH) hipLaunchKernelGGL(k_cx_reduce<ACT_TANH>, rg, dim3(256), 0, s, a, mrows);
