@@ -1016,7 +1016,7 @@ __device__ __forceinline__ void cxw_apply(f32x16 (&acc)[4][2], const unsigned (&
       for (int j = 0; j < 2; ++j) acc[i][j][q] = ((fm[i] >> q) & 1u) ? cx_epi<ACT>(acc[i][j][q], cc[j]) * X3_SA : 0.f;
 }
 
-template <int ACT, bool SPLIT = false>
+template <int ACT, bool SPLIT = false, bool F32OUT = false>
 __global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt, int n_nt) {
   __shared__ __attribute__((aligned(16))) _Float16 sm[CXW_LDS];  // [stage][A hi, A lo, B hi, B lo][256][32]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1109,6 +1109,26 @@ __global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt
           if (m < mrows) P[m * g.N + col] = acc[i][j][q];
         }
       }
+    return;
+  }
+  if constexpr (F32OUT) {  // fp32 frame rows b·T + t (no activation / BN / residual: the projections)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mb0 = m0 + wm * 128 + i * 32 + 4 * hl, b0 = mb0 / Tp, t00 = mb0 - b0 * Tp;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + r;
+        const float bias = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rq = (q & 3) + 8 * (q >> 2);
+          int t = t00 + rq, b = b0;
+          while (t >= Tp) { t -= Tp; ++b; }
+          if (b < g.B && t >= CX_P && t < CX_P + g.T)
+            g.Cout[((long)b * g.T + t - CX_P) * g.ldc + col] = acc[i][j][q] * X3_UNSCALE + bias;
+        }
+      }
+    }
     return;
   }
   unsigned fm[4] = {0u, 0u, 0u, 0u};  // frame bit of (i, q)
@@ -1241,6 +1261,13 @@ void conv_x3(const ConvX3Args& a, hipStream_t s) {
     else if (a.act == ACT_RELU) hipLaunchKernelGGL(k_cx_reduce<ACT_RELU>, rg, dim3(256), 0, s, a, mrows);
     else if (a.act == ACT_BN_RELU) hipLaunchKernelGGL(k_cx_reduce<ACT_BN_RELU>, rg, dim3(256), 0, s, a, mrows);
     else hipLaunchKernelGGL(k_cx_reduce<ACT_NONE>, rg, dim3(256), 0, s, a, mrows);
+    TT2_HIP(hipGetLastError());
+    return;
+  }
+  if (wide && a.Cout && a.N % CXW_BN == 0 && a.act == ACT_NONE && !a.bn_scale && !a.residual && !a.clip) {
+    const int n_mt = cdiv(a.B * (a.T + 2 * CX_P), CXW_BM), n_nt = a.N / CXW_BN;
+    hipLaunchKernelGGL((conv_x3w_kernel<ACT_NONE, false, true>), dim3((unsigned)(cdiv(n_mt, 8) * 8 * n_nt)), dim3(512),
+                       0, s, a, n_mt, n_nt);
     TT2_HIP(hipGetLastError());
     return;
   }
