@@ -116,6 +116,10 @@ typedef struct tt2_config {
   int cbhg_highwaynet_layers;   /* 4 */
   int cbhg_highway_units;       /* 128 */
   int cbhg_rnn_units;           /* 128 per direction */
+  /* hp.smoothing (attention.py:71-80,150): a = sigmoid(e) / sum_j sigmoid(e) instead of softmax
+   * (Chorowski et al. 2015); masked scores (-inf / -2^32+1) get sigmoid = 0.  Launch path only: a
+   * context with it set never takes the persistent decoder. */
+  int smoothing;                /* 0 */
 } tt2_config;
 
 typedef struct tt2_ctx tt2_ctx;

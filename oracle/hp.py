@@ -10,7 +10,8 @@ def oracle_hp(hp, synthesis_constraint=False, style="gst"):
                 mask_encoder=hp.mask_encoder, cumulative=hp.cumulative_weights,
                 synthesis_constraint=synthesis_constraint,
                 synthesis_constraint_type=hp.synthesis_constraint_type,
-                attention_win_size=hp.attention_win_size, num_heads=hp.num_heads)
+                attention_win_size=hp.attention_win_size, num_heads=hp.num_heads,
+                smoothing=hp.smoothing)
 
 
 def wavenet_oracle_hp(hp):

@@ -338,9 +338,13 @@ def attention_step(query, st, keys, values, lengths, W, hp, dt):
         energy = np.where(key_m | rev_m, dt(-2 ** 32 + 1), energy)
     if hp.get("mask_encoder", True):                                           # TF _maybe_mask_score
         energy = np.where(tt < np.asarray(lengths)[:, None], energy, dt(-np.inf))
-    m = energy.max(axis=1, keepdims=True)
-    e = np.exp(energy - m)
-    align = (e / e.sum(axis=1, keepdims=True)).astype(dt)                     # softmax :218
+    if hp.get("smoothing", False):                                             # :71-80, :150
+        with np.errstate(over="ignore"):
+            e = (1 / (1 + np.exp(-energy))).astype(dt)                        # sigmoid(-inf) = 0
+    else:
+        m = energy.max(axis=1, keepdims=True)
+        e = np.exp(energy - m)
+    align = (e / e.sum(axis=1, keepdims=True)).astype(dt)                     # probability_fn :218
     max_att = np.argmax(align, axis=1).astype(np.int32)                       # :219
     cum = align + st.cum if hp.get("cumulative", True) else align             # :222-225
     ctx = np.einsum("bt,btd->bd", align, values)                              # :27

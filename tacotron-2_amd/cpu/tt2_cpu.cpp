@@ -593,7 +593,10 @@ void dec_step(tt2_ctx* c, const float* frame_in, const uint8_t* masks, DecState&
       mx = std::max(mx, e);
     }
     float sum = 0.f;
-    for (int j = 0; j < T; ++j) sum += (sc[j] = std::exp(sc[j] - mx));
+    if (cfg.smoothing)  // _smoothing_normalization (attention.py:71-80): sigmoid(e) / sum sigmoid(e)
+      for (int j = 0; j < T; ++j) sum += (sc[j] = 1.f / (1.f + std::exp(-sc[j])));
+    else
+      for (int j = 0; j < T; ++j) sum += (sc[j] = std::exp(sc[j] - mx));
     float best = -INFINITY;
     int bi = 0;
     for (int j = 0; j < T; ++j) {
@@ -668,6 +671,7 @@ void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_re
   c->synthesis_constraint = 0; c->constraint_monotonic = 0; c->attention_win_size = 7;
   c->max_batch = max_batch; c->max_T_in = max_T_in; c->max_T_ref = max_T_ref; c->max_iters = max_iters;
   c->emt_attn = 0; c->emt_ref_gru = 0; c->n_emt = 4; c->style_mode = 0;
+  c->smoothing = 0;
 }
 
 tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {

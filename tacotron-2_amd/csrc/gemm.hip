@@ -876,8 +876,10 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvX3Args g, int n_mt,
         *reinterpret_cast<f16x8*>(&sm[p][buf][CX_BM + bn][bk + 8 * h]) = rb[p][h];
       }
   };
-  gload(0);
-  sstore(0);
+  if (nk > 0) {  // an uneven K split can leave a slice empty: it still writes its zero partial
+    gload(0);
+    sstore(0);
+  }
   __syncthreads();
   const int r = lane & 31, h8 = (lane >> 5) * 8;
   for (int kt = 0; kt < nk; ++kt) {
@@ -1061,7 +1063,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3w_kernel(ConvX3Args g, int n_mt
   // K split over blockIdx.y (ConvX3Args::ks): k-steps [kt0, kt0 + nk)
   const int nkt = g.kw * g.Cp / X3_BK, per = SPLIT ? (nkt + gridDim.y - 1) / gridDim.y : nkt;
   const int kt0 = SPLIT ? blockIdx.y * per : 0, nk = SPLIT ? min(nkt, kt0 + per) - kt0 : nkt;
-  stage(kt0, 0);
+  if (nk > 0) stage(kt0, 0);  // an empty K slice (uneven split) reads nothing, writes zeros
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int r = lane & 31, hl = lane >> 5, sw = (r >> 2) & 3;

@@ -23,7 +23,7 @@ struct StepWeights {               // row-major device copies of the TF variable
 struct StepDims {
   int B, T, nm, P, H, D, A, F, KL;
   float zo;
-  int cumulative, constraint, monotonic, win, mask_encoder;
+  int cumulative, constraint, monotonic, win, mask_encoder, smoothing;
 };
 
 struct StepIO {

@@ -83,7 +83,7 @@ __global__ void k_step_energy(const float* __restrict__ keys, const float* __res
 __global__ void k_step_softmax(const float* __restrict__ energy, const float* __restrict__ cum,
                                const int* __restrict__ max_att, const int* __restrict__ lengths, int T,
                                int constraint, int monotonic, int win, int mask_encoder, int cumulative,
-                               float* __restrict__ align, float* __restrict__ cum_out, int* __restrict__ max_att_o) {
+                               int smoothing, float* __restrict__ align, float* __restrict__ cum_out, int* __restrict__ max_att_o) {
   __shared__ float red[256];
   __shared__ int redi[256];
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -98,6 +98,8 @@ __global__ void k_step_softmax(const float* __restrict__ energy, const float* __
     if (mask_encoder && j >= len) e = -INFINITY;
     return e;
   };
+  // probability_fn: softmax, or _smoothing_normalization (attention.py:71-80) = sigmoid / sum sigmoid
+  auto prob = [&](int j, float mx) { return smoothing ? 1.f / (1.f + expf(-score(j))) : expf(score(j) - mx); };
   float mx = -INFINITY;
   for (int j = tid; j < T; j += blockDim.x) mx = fmaxf(mx, score(j));
   red[tid] = mx;
@@ -109,7 +111,7 @@ __global__ void k_step_softmax(const float* __restrict__ energy, const float* __
   mx = red[0];
   __syncthreads();
   float sum = 0.f;
-  for (int j = tid; j < T; j += blockDim.x) sum += expf(score(j) - mx);
+  for (int j = tid; j < T; j += blockDim.x) sum += prob(j, mx);
   red[tid] = sum;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -121,7 +123,7 @@ __global__ void k_step_softmax(const float* __restrict__ energy, const float* __
   float best = -INFINITY;
   int bi = 0x7fffffff;
   for (int j = tid; j < T; j += blockDim.x) {
-    const float a = expf(score(j) - mx) / sum;
+    const float a = prob(j, mx) / sum;
     align[(long)b * T + j] = a;
     cum_out[(long)b * T + j] = cumulative ? a + cum[(long)b * T + j] : a;
     if (a > best) {
@@ -189,7 +191,7 @@ void decoder_step_launch(const StepWeights& w, const StepDims& d, const StepIO& 
   hipLaunchKernelGGL(k_step_energy, dim3(cdiv(d.T, 64), B), dim3(64), 0, s, io.keys, q, io.cum, w.wconv, w.wloc, w.va,
                      B, d.T, d.A, d.F, d.KL, en);
   hipLaunchKernelGGL(k_step_softmax, dim3(B), dim3(256), 0, s, en, io.cum, io.max_att, io.lengths, d.T, d.constraint,
-                     d.monotonic, d.win, d.mask_encoder, d.cumulative, io.align, io.cumo, io.max_att_o);
+                     d.monotonic, d.win, d.mask_encoder, d.cumulative, d.smoothing, io.align, io.cumo, io.max_att_o);
   hipLaunchKernelGGL(k_step_context, dim3(cdiv(d.D, 256), B), dim3(256), 0, s, io.align, io.values, d.T, d.D,
                      io.ctxo);
   // FrameProjection / StopProjection on [h2_new, context] (Architecture_wrappers.py:243-247)

@@ -569,6 +569,7 @@ struct DecArgs {
   int K1, Kp;                      // LSTM-1 / projection critical input widths
   float zo, one_m_zo;
   int stop_at_any, mask_encoder, cumulative, constraint, monotonic, win;
+  int smoothing;  // hp.smoothing: sigmoid normalisation (attention.py:71-80)
   // weights
   const float* pre_b1; const float* pre_w2; const float* pre_b2;
   const float* q_w; const float* loc_cw;  // WF-packed; loc_cw = W_conv·W_loc [KLp taps x A]
@@ -1143,17 +1144,30 @@ __global__ __launch_bounds__(256) void k_softmax_ctx(DecArgs a, int istep, int t
   for (int i = tid; i < T; i += blockDim.x) al[i] = a.energy[(long)b * T + i];
   if (done) return;
   __syncthreads();
-  if (tid < 64) {
-    float mx = -INFINITY;
-    for (int i = tid; i < T; i += 64) mx = fmaxf(mx, al[i]);
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    float sum = 0.f;
-    for (int i = tid; i < T; i += 64) sum += expf(al[i] - mx);
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    if (tid == 0) { s_max = mx; s_sum = sum; }
+  if (a.smoothing) {  // _smoothing_normalization (attention.py:71-80): sigmoid(e) / sum_j sigmoid(e)
+    for (int i = tid; i < T; i += blockDim.x) al[i] = 1.f / (1.f + expf(-al[i]));
+    __syncthreads();
+    if (tid < 64) {
+      float sum = 0.f;
+      for (int i = tid; i < T; i += 64) sum += al[i];
+      for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+      if (tid == 0) s_sum = sum;
+    }
+    __syncthreads();
+    for (int i = tid; i < T; i += blockDim.x) al[i] = al[i] / s_sum;
+  } else {
+    if (tid < 64) {
+      float mx = -INFINITY;
+      for (int i = tid; i < T; i += 64) mx = fmaxf(mx, al[i]);
+      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      float sum = 0.f;
+      for (int i = tid; i < T; i += 64) sum += expf(al[i] - mx);
+      for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+      if (tid == 0) { s_max = mx; s_sum = sum; }
+    }
+    __syncthreads();
+    for (int i = tid; i < T; i += blockDim.x) al[i] = expf(al[i] - s_max) / s_sum;
   }
-  __syncthreads();
-  for (int i = tid; i < T; i += blockDim.x) al[i] = expf(al[i] - s_max) / s_sum;
   __syncthreads();
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2094,6 +2108,7 @@ static DecArgs make_dec_args(tt2_ctx* c, int max_iters, const uint8_t* masks_d, 
   a.zo = cfg.zoneout; a.one_m_zo = (float)(1.0 - (double)cfg.zoneout);
   a.stop_at_any = cfg.stop_at_any; a.mask_encoder = cfg.mask_encoder; a.cumulative = cfg.cumulative_weights;
   a.constraint = cfg.synthesis_constraint; a.monotonic = cfg.constraint_monotonic; a.win = cfg.attention_win_size;
+  a.smoothing = cfg.smoothing;
   a.pre_b1 = c->pre_b1.as<float>();
   a.pre_w2 = c->pre_w2.as<float>(); a.pre_b2 = c->pre_b2.as<float>();
   a.KLp = c->KLp; a.Fp = c->Fp;
@@ -2247,7 +2262,8 @@ static bool pd_emt(const tt2_ctx* c) {
 
 static bool pd_fits(tt2_ctx* c) {
   return (!c->emt.on() || pd_emt(c)) && c->pd_mode == 1 && c->pd_dev_ok && c->kg_wmax_dec < KG_BMAX && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
-         c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= PD_TMAX && c->B <= 32;
+         c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= PD_TMAX && c->B <= 32 &&
+         !c->cfg.smoothing;
 }
 
 static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, const float* targets_d, int T_lim,
@@ -2586,6 +2602,7 @@ void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_re
   c->predict_linear = 0; c->num_freq = 1025; c->cbhg_kernels = 8; c->cbhg_conv_channels = 128;
   c->cbhg_pool_size = 2; c->cbhg_projection = 256; c->cbhg_projection_kernel_size = 3;
   c->cbhg_highwaynet_layers = 4; c->cbhg_highway_units = 128; c->cbhg_rnn_units = 128;
+  c->smoothing = 0;
 }
 
 tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
@@ -2770,6 +2787,7 @@ static void decoder_step_dev(tt2_ctx* c, const float* frame_in, const uint8_t* m
   d.B = c->B; d.T = c->T_in; d.nm = c->nm; d.P = c->P; d.H = c->H; d.D = c->Dm; d.A = c->A; d.F = c->F; d.KL = c->KL;
   d.zo = cfg.zoneout; d.cumulative = cfg.cumulative_weights; d.constraint = cfg.synthesis_constraint;
   d.monotonic = cfg.constraint_monotonic; d.win = cfg.attention_win_size; d.mask_encoder = cfg.mask_encoder;
+  d.smoothing = cfg.smoothing;
   const size_t B = d.B, nH = B * d.H, nD = B * d.D, nT = B * d.T;
   // device image of [frame_in | 4 states | ctx | cum | max_att | masks] in and the outputs
   const size_t f_in = B * d.nm, n_in = f_in + 4 * nH + nD + nT, n_out = 4 * nH + nD + nT + f_in + B + nT;

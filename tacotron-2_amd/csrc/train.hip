@@ -2382,7 +2382,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   at.lens = lens; at.keys = c->keys.as<float>(); at.values = c->values.as<float>(); at.Q = c->Q.as<float>();
   at.values16 = nullptr;
   if (g_tr_prec == 2 && c->values16_on && (D & 3) == 0) {  // bf16 copy of this step's values (once per step)
-    c->values16.alloc((size_t)B * Tin * D * 2);
+    if (c->values16.bytes < (size_t)B * Tin * D * 2) c->values16.alloc((size_t)B * Tin * D * 2);  // grow only
     hipLaunchKernelGGL(k_tr_to_bf16, dim3(2048), dim3(256), 0, s, c->values.as<float>(), (long)B * Tin, (long)D, (long)D,
                        c->values16.as<__bf16>());
     TT2_HIP(hipGetLastError());
@@ -2763,7 +2763,10 @@ static void tr_front_alloc(tt2_train_ctx* c) {
   auto a = [](DevBuf& d, long n) { d.alloc(sizeof(float) * (size_t)std::max<long>(n, 1)); };
   a(c->fEX, BT * E);
   const char* pe = std::getenv("TT2_PN_PLANES");  // 0: implicit-im2col gemm_x3_kernel convs here too
-  if ((!pe || std::atoi(pe) != 0) && c->cfg.precision && C % 64 == 0 && E % 64 == 0 && (K & 1) &&
+  // one plane buffer serves the embedding (stride E) and the conv layers (stride C): the pad rows
+  // are zeroed once per shape, so the two strides must agree or the stride-E frames land on the
+  // stride-C pad rows (the im2col path serves E != C)
+  if ((!pe || std::atoi(pe) != 0) && c->cfg.precision && C % 64 == 0 && E == C && (K & 1) &&
       K <= 2 * CX_P + 1) {
     const long W = std::max(C, E), Wr = (W + 255) / 256 * 256;
     c->fePl.alloc((size_t)cx_rows((int)B, (int)T) * W * 2);

@@ -319,6 +319,9 @@ class Tacotron():
                                  emt_only=emt_only, precision=precision, postnet=True, frontend=True,
                                  max_T_ref=cap["max_T_ref"], tf_seed=seed, n_emt=n_emt, n_spk=n_spk)
             self._trainer, self._train_key, self._train_cap = tr, key, cap
+            # the classifiers' variables are trained and saved like the rest (tf.train.Saver)
+            for k, v in tr.style_disc_weights.items():
+                self._weights.setdefault(k, np.asarray(v, np.float32))
             self._mask_rng = np.random.default_rng(seed)
         tr.set_step_inputs(targets_lengths=tlen)
         if n_emt or n_spk:  # Style_Emb_Disc targets (tf.one_hot of the labels, tacotron.py:813-814)

@@ -115,6 +115,7 @@ class TextToSpeech(object):
         lengths = lengths_d.cpu().numpy()  # the one host round trip (on this stream): sizes WaveNet
         T_f = int(lengths.max()) if B else 0
         wav = torch.zeros((B, max(T_f, 0) * self.hop), dtype=torch.float32, device=dev)
+        cond = None
         if T_f > 0:
             lo, hi = output_range(hp)
             cond = torch.empty((B, hp.num_mels, T_f), dtype=torch.float32, device=dev)
@@ -130,7 +131,7 @@ class TextToSpeech(object):
                 None, None, st))
         return dict(wav=wav, lengths=lengths, audio_lengths=lengths.astype(np.int64) * self.hop,
                     mel=mel.view(-1)[:B * n * hp.num_mels].view(B, n, hp.num_mels), stop=stop,
-                    n_steps=n)
+                    n_steps=n, cond=cond)
 
     def synthesize(self, ids, lengths, ref_emt, ref_spk, seed=0, u_mix=None, u_log=None,
                    prenet_masks=None):
@@ -153,7 +154,8 @@ class TextToSpeech(object):
         wav = out["wav"].cpu().numpy()
         wavs = [wav[b, :int(out["audio_lengths"][b])] for b in range(wav.shape[0])]
         return dict(wavs=wavs, lengths=out["lengths"], mel=out["mel"].cpu().numpy(),
-                    stop=out["stop"][:, :out["n_steps"]].cpu().numpy(), n_steps=out["n_steps"])
+                    stop=out["stop"][:, :out["n_steps"]].cpu().numpy(), n_steps=out["n_steps"],
+                    cond=None if out["cond"] is None else out["cond"].cpu().numpy())
 
 
 def synthesize_sharded(tts, ids, lengths, ref_emt, ref_spk, seed=0, group=None, u_mix=None,

@@ -63,8 +63,7 @@ def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=Fals
     cfg.attention_win_size = hp.attention_win_size
     if hp.outputs_per_step != 1:
         raise NotImplementedError("outputs_per_step (r) must be 1 on this build (hparams.py:140)")
-    if hp.smoothing:
-        raise NotImplementedError("smoothing attention normalisation is not built")
+    cfg.smoothing = 1 if hp.smoothing else 0        # attention.py:71-80,150
     cfg.style_mode = STYLE_MODES.index(style_mode(hp, style))
     cfg.predict_linear = 1 if hp.predict_linear else 0    # CBHG post-net (tacotron.py:466-481)
     cfg.num_freq = hp.num_freq

@@ -70,6 +70,8 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
         raise ValueError("tacotron_teacher_forcing_mode must be 'constant' or 'scheduled'")
     if hp.predict_linear:
         raise NotImplementedError("predict_linear (CBHG linear loss) is not built in the training step")
+    if hp.smoothing:
+        raise NotImplementedError("smoothing attention normalisation is built for synthesis only")
     cfg.memory_dim = memory_width(hp, emt_only)
     cfg.num_mels = hp.num_mels
     cfg.prenet_units = hp.prenet_layers[0]
@@ -165,11 +167,15 @@ class TacotronTrainer(object):
         self.device = torch.device("cuda", device)
         self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only, precision, postnet, frontend,
                                 max_T_ref, n_emt if frontend else 0, n_spk if frontend else 0)
+        # the Style_Emb_Disc variables this context trains, with the values it starts from (the
+        # caller's, else a fresh draw): callers that save checkpoints merge them into their weights
+        self.style_disc_weights = {}
         if self.cfg.n_emt or self.cfg.n_spk:
             fresh = init_style_disc_weights(hp, self.cfg.n_emt, self.cfg.n_spk, emt_only)
             weights = dict(weights)
             for k, v in fresh.items():
                 weights.setdefault(k, v)
+                self.style_disc_weights[k] = weights[k]
         self.frontend = frontend
         self.postnet = postnet
         self.B = batch
@@ -194,7 +200,12 @@ class TacotronTrainer(object):
         # teacher forcing: drawn per step from the ratio schedule (TacoTrainingHelper) unless the
         # caller injects the draw through set_step_inputs(feed_target=...)
         self._feed_explicit = False
-        self._tf_rng = np.random.default_rng(hp.tacotron_random_seed if tf_seed is None else tf_seed)
+        # each data-parallel rank is its own tower and draws its own feed pattern (the reference's
+        # towers draw independently): the rank joins the seed once torch.distributed is up
+        seed = hp.tacotron_random_seed if tf_seed is None else tf_seed
+        dist = torch.distributed
+        rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self._tf_rng = np.random.default_rng([int(seed), rank] if rank else int(seed))
         self.ratio = None
 
     def close(self):

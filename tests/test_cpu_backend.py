@@ -252,3 +252,29 @@ def test_use_gst_false_is_embed(cpu):
     eng.close()
     ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, n)
     np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize("constraint", [False, True])
+def test_smoothing_normalization_matches_oracle(cpu, constraint):
+    """hp.smoothing: _smoothing_normalization (attention.py:71-80, chosen at :150) = sigmoid(e) /
+    sum_j sigmoid(e) instead of softmax; masked scores (length mask -inf, window -2^32+1) get 0."""
+    hp = small_hparams()
+    hp.override_from_dict(dict(smoothing=True))
+    W = init_tacotron_weights(hp, seed=5339)
+    B, T, n = 3, 11, 9
+    ids, lens, re, rs = tacotron_inputs(B, T, 40, seed=71)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=71)
+    eng = _taco(cpu, hp, W, B, T, 40, n, constraint)
+    out = eng.synthesize(ids, lens, re, rs, n, masks)
+    eng.close()
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp, constraint), masks, n)
+    np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(out["alignments"], ref["alignments"], rtol=0, atol=1e-5)
+    al = ref["alignments"]                      # [B, T_in, n]
+    np.testing.assert_allclose(al.sum(axis=1), 1.0, atol=1e-5)
+    for b in range(B):
+        assert np.all(al[b, lens[b]:] == 0)
+    # a different normalisation than softmax: the same weights without smoothing differ
+    hp.override_from_dict(dict(smoothing=False))
+    ref0 = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp, constraint), masks, n)
+    assert np.abs(ref0["alignments"] - al).max() > 1e-3

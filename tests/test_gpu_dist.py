@@ -193,3 +193,48 @@ def test_rccl_backend_paths_one_rank():
     assert p.exitcode == 0, p.exitcode
     ok_gather, ok_reduce, backend = q.get(timeout=5)
     assert backend == "nccl" and ok_gather and ok_reduce
+
+
+N_FORK = 60
+
+
+def _fork_worker(rank, world, port, out_dir):
+    _paths()
+    import torch.distributed as dist
+    from _common import fork_e2e_case
+    from tt2.e2e import TextToSpeech, synthesize_sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hp, W, WW, ids, lens, re, rs, pm, um, ul = fork_e2e_case(N_FORK, B=4)
+        tts = TextToSpeech(hp, W, WW, 2, ids.shape[1], re.shape[1], N_FORK, 0)
+        wavs = synthesize_sharded(tts, ids, lens, re, rs, seed=3, u_mix=um, u_log=ul,
+                                  prenet_masks=pm)
+        path = tts.taco.decoder_path()[0]
+        tts.close()
+        np.savez(os.path.join(out_dir, "fork_{}.npz".format(rank)), np.array([path]), *wavs)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_configs3_fork_widths(tmp_path):
+    """configs[3] at the fork widths (4 utterances of 136-201 characters, 60 decoder steps on the
+    persistent decoder, 16,500 samples each) sharded 2 + 2 over two gloo ranks sharing the GPU:
+    every gathered waveform equals the single-process full-batch run."""
+    world = 2
+    mp.start_processes(_fork_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    from _common import fork_e2e_case
+    from tt2.e2e import TextToSpeech
+    hp, W, WW, ids, lens, re, rs, pm, um, ul = fork_e2e_case(N_FORK, B=4)
+    tts = TextToSpeech(hp, W, WW, 4, ids.shape[1], re.shape[1], N_FORK, 0)
+    ref = tts.synthesize(ids, lens, re, rs, seed=3, u_mix=um, u_log=ul, prenet_masks=pm)["wavs"]
+    tts.close()
+    for r in range(world):
+        with np.load(str(tmp_path / "fork_{}.npz".format(r)), allow_pickle=False) as z:
+            assert int(z["arr_0"][0]) == 1              # the persistent decoder served each shard
+            got = [z["arr_{}".format(i)] for i in range(1, len(z.files))]
+        assert len(got) == 4
+        for g, w in zip(got, ref):
+            assert g.shape == w.shape == (N_FORK * 275,)
+            np.testing.assert_allclose(g, w, atol=1e-5)

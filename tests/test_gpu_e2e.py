@@ -172,3 +172,58 @@ def test_synthesizer_file_contract(tmp_path):
         sr, data = wavfile.read(w)
         assert sr == hp.sample_rate and data.dtype == np.int16
         assert data.shape == (len(m) * hp.hop_size,)
+
+
+def test_configs3_fork_widths_product_chain_matches_oracle():
+    """configs[3]'s product chain at the fork-default widths: text frontend ->
+    encoder -> the PERSISTENT decoder (k_decode_persist; D_mem 1024, 2 x 1024 LSTM) -> Postnet ->
+    tt2_output_lengths_dev -> tt2_wn_cond_from_mels_dev -> 24-layer R=64 MoL WaveNet
+    (k_generate_pipe), all on one stream through TextToSpeech.synthesize, B=3 utterances of 136-201
+    characters, 60 decoder steps, 16,500 samples per row.  Checks: mels within 1e-4 of the oracle,
+    lengths exact, conditioning within 1e-6 of condition_batch on the device mels, the free-running
+    waveform identical to the oracle's on a >= 200-sample prefix, and along the device's own
+    trajectory (its waveform fed back as the teacher) logits within 1e-4 and mixture indices exact
+    wherever the oracle's top-2 Gumbel margin exceeds 1e-4.
+    Reference chain: synthesize.py:33-43, tacotron/synthesizer.py:186-189,384-387,
+    wavenet_vocoder/synthesizer.py:56-70."""
+    from _common import fork_e2e_case
+    from tt2.e2e import TextToSpeech
+    from tt2.engine import WaveNetEngine
+    n = 60
+    hp, W, WW, ids, lens, re, rs, masks, um, ul = fork_e2e_case(n)
+    B, T_in = ids.shape
+    assert T_in == 201 and hp.decoder_lstm_units == 1024
+    tts = TextToSpeech(hp, W, WW, B, T_in, re.shape[1], n, 0)
+    out = tts.synthesize(ids, lens, re, rs, 0, um, ul, masks)
+    assert tts.taco.decoder_path()[0] == 1          # the persistent decoder served it
+    tts.close()
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, n)
+    assert out["n_steps"] == n
+    np.testing.assert_allclose(out["mel"], ref["mel_outputs"], atol=1e-4)
+    assert list(out["lengths"]) == TR.get_output_lengths(ref["stop_token_prediction"]) == [n] * B
+    mels = [out["mel"][b, :out["lengths"][b]] for b in range(B)]
+    cond = WR.condition_batch(mels)                 # [B, T_f, 80]
+    np.testing.assert_allclose(out["cond"], cond.transpose(0, 2, 1), rtol=0, atol=1e-6)
+    c_up = WR.upsample_2d(cond.transpose(0, 2, 1), WW, hp.upsample_scales).transpose(0, 2, 1)
+    whp = wavenet_oracle_hp(hp)
+    y, k = WR.incremental(c_up, WW, whp, um, ul)
+    T = n * hp.hop_size
+    dev_y = np.stack(out["wavs"])
+    assert dev_y.shape == (B, T)
+    for b in range(B):
+        same = np.abs(dev_y[b] - y[b]) < 1e-4
+        first = int(np.argmin(same)) if not same.all() else T
+        assert first >= 200, (b, first)
+    # the whole length along the device's trajectory: teacher = the device's free-run waveform
+    eng = WaveNetEngine(hp, WW, B, T, 0)
+    tf = eng.generate(cond, um, ul, 0, dev_y, want_logits=True)
+    eng.close()
+    yo, ko, lo = WR.incremental(c_up, WW, whp, um, ul, dev_y, return_logits=True)
+    np.testing.assert_allclose(tf["logits"], lo, atol=1e-4, rtol=1e-4)
+    gl = np.log(-np.log(um.astype(np.float64))).astype(np.float32)
+    temp = lo[..., :10] - gl.transpose(1, 0, 2)
+    srt = np.sort(temp, -1)
+    safe = (srt[..., -1] - srt[..., -2]) > 1e-4
+    assert safe.mean() > 0.99
+    np.testing.assert_array_equal(tf["k"][safe], ko[safe])
+    np.testing.assert_allclose(tf["y"][safe], yo[safe], atol=1e-4)

@@ -509,3 +509,31 @@ def test_cpu_backend_noise_streams_match_device():
     gm, gl = wavenet_noise(91, T, B, 10)
     np.testing.assert_array_equal(um, gm)
     np.testing.assert_array_equal(ul, gl)
+
+
+@pytest.mark.parametrize("widths", ["small", "fork"])
+def test_smoothing_normalization(widths):
+    """hp.smoothing (attention.py:71-80,150): sigmoid normalisation on the launch path (the
+    persistent decoder is never chosen for it), free running, within 1e-4 of the oracle; a chain of
+    tt2_decoder_step calls (the step seam's own kernels) reproduces the fused loop."""
+    from tt2.weights import init_tacotron_weights
+    hp = small_hparams() if widths == "small" else full_hparams()
+    hp.override_from_dict(dict(smoothing=True))
+    W = init_tacotron_weights(hp, seed=5339)
+    B, T, n = 3, 23, 12
+    ids, lens, re, rs = tacotron_inputs(B, T, 40, seed=72)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=72)
+    eng = _engine(hp, W, B, T, 40, n)
+    out = eng.synthesize(ids, lens, re, rs, n, masks)
+    assert eng.decoder_path()[0] == 0
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, n)
+    np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], rtol=0, atol=MEL_TOL)
+    np.testing.assert_allclose(out["alignments"], ref["alignments"], rtol=0, atol=1e-4)
+    eng.encode(ids, lens, re, rs)
+    state = eng.zero_state()
+    frame = np.zeros((B, hp.num_mels), np.float32)
+    for t in range(out["frames"].shape[1]):
+        frame, stop, align, state = eng.decoder_step(frame, masks[t], state)
+        np.testing.assert_allclose(align, out["alignments"][:, :, t], atol=1e-5)
+        np.testing.assert_allclose(frame, out["frames"][:, t], atol=1e-5)
+    eng.close()

@@ -161,3 +161,37 @@ def test_trainer_applies_teacher_forcing_schedule(mode):
     finally:
         auto.close()
         inj.close()
+
+
+@pytest.mark.gpu
+def test_style_classifier_variables_saved_and_restored():
+    """the Style_Emb_Disc variables the trainer draws fresh (the loaded weights lack
+    them) are part of the saved weights after training, and a model resumed from those weights
+    trains from the saved values, not a re-drawn initialisation (tf.train.Saver round trip)."""
+    from oracle import train_ref as TRN
+    hp = small_hparams()
+    W = init_tacotron_weights(hp, seed=5339)
+    ne, ns = 4, 3
+    names = TRN.style_disc_var_names(False, ne, ns)
+    assert names and not any(n in W for n in names)
+    el, sl = np.array([1, 3, 0], np.int32), np.array([2, 0, 1], np.int32)
+    ids, lens, re, rs, tg, st, m = _batch(hp)
+    kw = dict(is_training=True, ref_mel_emt=re, ref_mel_spk=rs, train_masks=m, n_emt=ne, n_spk=ns,
+              emt_labels=el, spk_labels=sl)
+    model = _model(hp, W)
+    model.initialize(ARGS, ids, lens, tg, st, **kw)
+    model.add_loss()
+    model.add_optimizer(0)
+    assert all(n in model.all_vars for n in names)
+    saved = model.trained_weights()
+    trained = {n: model._trainer.get(n, 0, saved[n].shape) for n in names}
+    model._trainer.close()
+    for n in names:
+        np.testing.assert_array_equal(saved[n], trained[n])
+    resumed = _model(hp, saved)
+    resumed.initialize(ARGS, ids, lens, tg, st, **kw)
+    try:
+        for n in names:     # the resumed context starts from the saved values (no optimizer step yet)
+            np.testing.assert_array_equal(resumed._trainer.get(n, 0, saved[n].shape), saved[n])
+    finally:
+        resumed._trainer.close()
