@@ -771,7 +771,7 @@ tt2_status tt2_decode(tt2_ctx* c, int max_iters, const uint8_t* prenet_masks, ui
       // TacoTestHelper stop rule (helpers.py:36-59): round(stop) == 1 for all (or any) rows
       int fin_rows = 0;
       for (int b = 0; b < B; ++b) fin_rows += std::nearbyint(sp[b]) == 1.f;
-      if (c->cfg.stop_at_any ? fin_rows > 0 : fin_rows == B) {
+      if (c->cfg.stop_at_any == 2 ? false : c->cfg.stop_at_any ? fin_rows > 0 : fin_rows == B) {
         ++t;
         break;
       }

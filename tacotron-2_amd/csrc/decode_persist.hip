@@ -602,7 +602,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           const bool v0 = lane < 16 && r0 < a.B, v1 = lane < 16 && r0 + 16 < a.B;
           const unsigned long long f0 = __ballot(v0 && sb[0]), f1 = __ballot(v1 && sb[1]);
           const unsigned long long m0 = __ballot(v0), m1 = __ballot(v1);
-          dn = a.stop_at_any ? ((f0 | f1) != 0ull) : (f0 == m0 && f1 == m1);
+          dn = a.stop_at_any == 2 ? 0 : a.stop_at_any ? ((f0 | f1) != 0ull) : (f0 == m0 && f1 == m1);
         }
         if (lane == 0 && dn) atomicMax(si + 1, 1);
       }

@@ -26,6 +26,7 @@
 #include "common.h"
 #include "gemm.h"
 #include "train_front.h"
+#include "train_persist.h"
 
 namespace tt2 {
 
@@ -114,6 +115,11 @@ struct tt2_train_ctx {
   std::vector<uint8_t> feed;
   // free-running steps: prenet-1 kernel transposed [P][NM], per-step scratch
   DevBuf W1T, sDZ, sDP, sDX;
+  // persistent forward (train_persist.hip; opt-in with TT2_TR_PERSIST=1, else the per-step launches): exchange
+  // buffers, energy granules, flags + control words, the prenet rows in bf16 fragment layout
+  DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps;
+  bool tp_on = false, tp_last = false, tp_check = false;
+  int* tp_ctl_host = nullptr;  // pinned [2]: the launch's control words, checked at the next read-back
 };
 
 namespace tt2 {
@@ -2289,6 +2295,81 @@ __global__ void k_tr_rank1_add(float* __restrict__ Y, long ld, const float* __re
   }
 }
 
+// Persistent forward (train_persist.hip): fork widths (H 1024, prenet 256, memory 1024, attention 128
+// x 32 filters), B <= 64, T_in <= TP_TMAX, bf16 operands with the bf16 values copy, every step
+// teacher-forced (a step fed its own frame needs the frame projection inside the loop).
+static bool tr_persist_fits(const tt2_train_ctx* c, int Tin, bool free_run, bool values16) {
+  return c->tp_on && !free_run && values16 && c->B <= 64 && Tin <= TP_TMAX && c->H == TP_H && c->P == TP_P &&
+         c->D == TP_D && c->A == TP_A && c->F == TP_F && c->KW == TP_KWMAX && c->LX1 == TP_LX1;
+}
+
+static void tr_persist_forward(tt2_train_ctx* c, const TrAtt& at, const uint8_t* zm, int Tin, int T, hipStream_t s) {
+  const size_t xb = 2ul * 64 * 1024 * sizeof(__bf16);  // two parities of [64][1024] bf16
+  auto grow = [](DevBuf& d, size_t n) {
+    if (d.bytes < n) d.alloc(n);
+  };
+  for (DevBuf* d : {&c->tpCX, &c->tpH1X, &c->tpZ1X, &c->tpH2X, &c->tpZ2X}) grow(*d, xb);
+  grow(c->tpEX, 2ul * 64 * 4 * TP_TMAX * sizeof(unsigned long long));
+  grow(c->tpCtl, sizeof(unsigned) * (3ul * TP_NREP * TP_NB + 16));
+  grow(c->tpPre, (size_t)T * 64 * TP_P * sizeof(__bf16));
+  if (!c->tp_ctl_host) TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->tp_ctl_host), 4 * sizeof(int)));
+  // rows >= B of the exchange buffers stay zero (they are A-operand padding); the flags and the
+  // granules restart their tags at 1 every launch
+  for (DevBuf* d : {&c->tpCX, &c->tpH1X, &c->tpZ1X, &c->tpH2X, &c->tpZ2X, &c->tpEX, &c->tpCtl})
+    TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+  tp_prenet_rows(c->X1.as<float>(), c->LX1, c->B, T, c->tpPre.as<__bf16>(), s);
+  TpArgs a{};
+  a.B = c->B; a.T = T; a.Tin = Tin; a.KW = c->KW; a.z = c->cfg.zoneout;
+  a.K1T = c->hK1T.as<__bf16>(); a.K2T = c->hK2T.as<__bf16>(); a.Wq = c->hWq.as<__bf16>();
+  a.b1 = pvar(c, L1V("bias")); a.b2 = pvar(c, L2V("bias"));
+  a.Kc = at.Kc; a.bc = at.bc; a.Wl = at.Wl; a.va = at.va; a.ba = at.ba;
+  a.keys = at.keys; a.values16 = at.values16; a.lens = at.lens; a.zm = zm; a.preh = c->tpPre.as<__bf16>();
+  a.X1 = c->X1.as<float>(); a.X2 = c->X2.as<float>(); a.PIN = c->PIN.as<float>();
+  a.G1 = c->G1.as<float>(); a.G2 = c->G2.as<float>(); a.CN1 = c->CN1.as<float>(); a.CN2 = c->CN2.as<float>();
+  a.C1 = c->C1.as<float>(); a.C2 = c->C2.as<float>(); a.ALIGN = at.ALIGN; a.CUM = at.CUM; a.TH = at.TH;
+  a.FALL = at.FALL; a.ALN = at.ALN;
+  a.CX = c->tpCX.as<__bf16>(); a.H1X = c->tpH1X.as<__bf16>(); a.Z1X = c->tpZ1X.as<__bf16>();
+  a.H2X = c->tpH2X.as<__bf16>(); a.Z2X = c->tpZ2X.as<__bf16>();
+  a.EX = c->tpEX.as<unsigned long long>();
+  a.flags = c->tpCtl.as<unsigned>();
+  a.ctl = reinterpret_cast<int*>(a.flags + 3 * TP_NREP * TP_NB);
+  // TT2_TP_STAMP=<step>: stage stamps of that step -> TT2_TP_STAMP_FILE (int64 [256][32], diagnostic)
+  const char* st = std::getenv("TT2_TP_STAMP");
+  a.stamp_step = st ? std::atoi(st) : -1;
+  a.stamps = nullptr;
+  if (st) {
+    grow(c->tpStamps, sizeof(long long) * TP_NB * 32);
+    TT2_HIP(hipMemsetAsync(c->tpStamps.p, 0, c->tpStamps.bytes, s));
+    a.stamps = c->tpStamps.as<long long>();
+  }
+  tp_launch(a, s);
+  if (st) {
+    std::vector<long long> h((size_t)TP_NB * 32);
+    TT2_HIP(hipMemcpyAsync(h.data(), a.stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipStreamSynchronize(s));
+    const char* fn = std::getenv("TT2_TP_STAMP_FILE");
+    if (FILE* f = std::fopen(fn ? fn : "tp_stamps.bin", "wb")) {
+      std::fwrite(h.data(), sizeof(long long), h.size(), f);
+      std::fclose(f);
+    }
+  }
+  TT2_HIP(hipMemcpyAsync(c->tp_ctl_host, a.ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+  c->tp_check = true;
+}
+
+// Control words of the last persistent forward (after the stream has passed it): a timed-out
+// hand-off or a launch that did not run every step fails the read-back that follows the step.
+static void tr_persist_check(tt2_train_ctx* c) {
+  if (!c->tp_check) return;
+  TT2_HIP(hipStreamSynchronize(c->last_stream));
+  c->tp_check = false;
+  const int ph = c->tp_ctl_host[0], steps = c->tp_ctl_host[1];
+  TT2_CHECK(ph == 0, TT2_ERR_HIP,
+            "persistent training forward: a hand-off wait timed out (phase " + std::to_string(ph - 1) +
+                "); TT2_TR_PERSIST=0 runs the per-step launches");
+  TT2_CHECK(steps == c->T_last, TT2_ERR_STATE, "persistent training forward did not complete every step");
+}
+
 static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* lens, const float* tg, const float* stg,
                                 const uint8_t* pm, const uint8_t* zm, const uint8_t* pnm, int Tin, int T,
                                 hipStream_t s) {
@@ -2415,7 +2496,10 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   // Architecture_wrappers.py:258-263); XIN / P1 / X1 then hold what the step actually consumed
   const bool free_run = tr_has_free_steps(c, T);
   if (free_run) tr_transpose(pvar(c, PRV(1, "kernel")), NM, P, P, c->W1T.as<float>(), NM, s);
-  for (int t = 0; t < T; ++t) {
+  // the whole teacher-forced loop as one persistent launch when the shapes are the fork's
+  c->tp_last = fused && tr_persist_fits(c, Tin, free_run, at.values16 != nullptr);
+  if (c->tp_last) tr_persist_forward(c, at, zm, Tin, T, s);
+  for (int t = 0; t < (c->tp_last ? 0 : T); ++t) {
     const long s1 = (long)t * B;
     if (free_run && t > 0 && !c->feed[t]) {
       float* xin = c->XIN.as<float>() + s1 * NM;
@@ -3581,6 +3665,10 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
     auto* c = new tt2_train_ctx();
     if (const char* e = std::getenv("TT2_TRAIN_BLAS")) c->blas_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("TT2_TR_VALUES16")) c->values16_on = std::atoi(e) != 0;
+    {
+      const char* e = std::getenv("TT2_TR_PERSIST");
+      c->tp_on = e && e[0] == '1' && tp_device_ok(hip_device);
+    }
     try {
       c->dev = hip_device;
       c->cfg = *cfg;
@@ -3632,6 +3720,7 @@ void tt2_train_destroy(tt2_train_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->tp_ctl_host) (void)hipHostFree(c->tp_ctl_host);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -3794,6 +3883,7 @@ tt2_status tt2_train_losses(tt2_train_ctx* c, float* out4 /* [5] */, float* fb_m
     // by the host through the BAR and missed the last kernels' L2-resident writes)
     TT2_HIP(hipMemcpyAsync(out4, c->red.p, sizeof(float) * 5, hipMemcpyDeviceToHost, c->last_stream));
     TT2_HIP(hipStreamSynchronize(c->last_stream));
+    tr_persist_check(c);
     if (!c->cfg.postnet) out4[4] = 0.f;
     if (fb_ms) TT2_HIP(hipEventElapsedTime(fb_ms, c->ev0, c->ev1));
   });
@@ -3804,8 +3894,13 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
     TT2_CHECK(c && name && host, TT2_ERR_INVALID_ARG, "null argument");
     TT2_HIP(hipSetDevice(c->dev));
     TT2_HIP(hipDeviceSynchronize());
+    tr_persist_check(c);
     if (std::string(name) == "diag:blas_calls") {  // gemm_bf16_kc products issued since create (1 float)
       host[0] = (float)c->blas_calls;
+      return;
+    }
+    if (std::string(name) == "diag:persist") {  // 1 when the last forward ran the persistent launch
+      host[0] = c->tp_last ? 1.f : 0.f;
       return;
     }
     if (std::string(name) == "memory") {  // d loss / d memory of the last forward_backward

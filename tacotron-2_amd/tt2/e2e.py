@@ -21,7 +21,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check
-from .engine import TacotronEngine, WaveNetEngine
+from .engine import MAX_CONTEXT_BATCH, TacotronEngine, WaveNetEngine
 from .hparams import bench_wavenet_hparams, get_hop_size
 
 
@@ -48,6 +48,10 @@ class TextToSpeech(object):
 
     def __init__(self, hp, taco_weights, wn_weights, max_batch, max_T_in, max_T_ref, max_iters,
                  device=0, synthesis_constraint=False):
+        if max_batch > MAX_CONTEXT_BATCH:
+            # the device-resident chain drives one tt2_ctx; TacotronEngine splits larger towers
+            raise ValueError("TextToSpeech holds at most {} rows per call (got {}); split the batch"
+                             .format(MAX_CONTEXT_BATCH, max_batch))
         self.hp = hp
         self.device = device
         self.max_iters = max_iters

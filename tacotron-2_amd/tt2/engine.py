@@ -81,19 +81,62 @@ def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=Fals
     return cfg
 
 
+#: rows of one tt2_ctx (tt2_create's capacity: the persistent decoder's 32-row blocks)
+MAX_CONTEXT_BATCH = 32
+
+
+def chunk_ranges(B, cap=MAX_CONTEXT_BATCH):
+    """Row ranges [(s, e)] of a batch split into ceil(B / cap) near-equal contexts."""
+    n = max(1, -(-B // cap))
+    q, r = divmod(B, n)
+    out, s = [], 0
+    for i in range(n):
+        e = s + q + (1 if i < r else 0)
+        out.append((s, e))
+        s = e
+    return out
+
+
+def global_stop_steps(stop, stop_at_any):
+    """dynamic_decode's batch-level stop over the whole tower (TacoTestHelper, helpers.py:40-54):
+    the first step at which every row's stop probability rounds to 1 (stop_at_any: any row),
+    round half to even as tf.round; the step is emitted, so the decode keeps step + 1 frames.
+    stop [B, n] -> n_steps (n when the rule never fires)."""
+    fin = np.rint(np.asarray(stop, np.float32)) == 1.0
+    cond = fin.any(axis=0) if stop_at_any else fin.all(axis=0)
+    return int(np.argmax(cond)) + 1 if cond.any() else fin.shape[1]
+
+
 class TacotronEngine(object):
-    """Owns one tt2_ctx."""
+    """Owns one tt2_ctx, or for a batch above MAX_CONTEXT_BATCH rows one context per row chunk
+    decoding without its own stop rule, with the tower's one batch-level stop step taken over all
+    chunks' stop tokens afterwards (the reference decodes a tower in one dynamic_decode,
+    tacotron.py:349-354; hparams.py:44 tacotron_batch_size 96)."""
 
     def __init__(self, hp, weights, max_batch, max_T_in, max_T_ref, max_iters, device=0,
                  emt_only=False, synthesis_constraint=False, emt_attn=None, emt_ref_gru="none",
-                 n_emt=4, lib=None, style="gst"):
+                 n_emt=4, lib=None, style="gst", never_stop=False):
         # lib: libtt2.so by default; _lib.load_cpu_library() binds the same ABI on host cores
         self.lib = lib or _lib.load_library()
         self.hp = hp
         self.emt_only = emt_only
         self.emt_attn = emt_attn
+        self.h = None
+        self._chunks = None
+        if max_batch > MAX_CONTEXT_BATCH:
+            rng = chunk_ranges(max_batch)
+            self._chunks = [TacotronEngine(hp, weights, e - s, max_T_in, max_T_ref, max_iters, device, emt_only,
+                                           synthesis_constraint, emt_attn, emt_ref_gru, n_emt, lib, style,
+                                           never_stop=True) for s, e in rng]
+            self.cfg = self._chunks[0].cfg
+            self.caps = (max_batch, max_T_in, max_T_ref, max_iters)
+            self.style = style
+            self.D = self._chunks[0].D
+            return
         self.cfg = tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only,
                                    synthesis_constraint, emt_attn, emt_ref_gru, n_emt, self.lib, style)
+        if never_stop:
+            self.cfg.stop_at_any = 2
         self.caps = (max_batch, max_T_in, max_T_ref, max_iters)
         # Tacotron_emt_attn attends over the encoder outputs alone (tacotron_emt_attn.py:244-246)
         self.style = style
@@ -110,6 +153,8 @@ class TacotronEngine(object):
         _lib.check(status, self.lib)
 
     def close(self):
+        for ch in getattr(self, "_chunks", None) or ():
+            ch.close()
         if getattr(self, "h", None):
             self.lib.tt2_destroy(self.h)
             self.h = None
@@ -120,11 +165,25 @@ class TacotronEngine(object):
         c = self.caps
         return B <= c[0] and T_in <= c[1] and T_ref <= c[2] and max_iters <= c[3]
 
+    def _ranges(self, B):
+        """Row ranges of the chunk contexts for a batch of B rows (the first chunks fill first)."""
+        out, s = [], 0
+        for ch in self._chunks:
+            e = min(B, s + ch.caps[0])
+            out.append((s, e))
+            s = e
+        return out
+
     def encode(self, ids, lengths, ref_emt, ref_spk):
         ids = i32(ids)
         lengths = i32(lengths)
         B, T = ids.shape
         self._B, self._T_in = B, T
+        if self._chunks:
+            parts = [ch.encode(ids[s:e], lengths[s:e], None if ref_emt is None else f32(ref_emt)[s:e],
+                               None if ref_spk is None else f32(ref_spk)[s:e])
+                     for ch, (s, e) in zip(self._chunks, self._ranges(B)) if e > s]
+            return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
         ref_emt = f32(ref_emt) if ref_emt is not None else None
         ref_spk = f32(ref_spk) if ref_spk is not None else None
         mem = np.zeros((B, T, self.D), np.float32)
@@ -138,6 +197,8 @@ class TacotronEngine(object):
 
     def decode(self, max_iters, prenet_masks=None, seed=0, targets=None):
         B = self._B
+        if self._chunks:
+            return self._decode_chunked(max_iters, prenet_masks, seed, targets)
         masks = None if prenet_masks is None else np.ascontiguousarray(prenet_masks, np.uint8)
         if masks is not None and masks.shape[0] < max_iters:
             raise ValueError("prenet_masks must cover max_iters steps")
@@ -159,6 +220,28 @@ class TacotronEngine(object):
         self._n_steps = n
         return frames[:, :n], stop[:, :n], align[:, :, :n]
 
+    def _decode_chunked(self, max_iters, prenet_masks, seed, targets):
+        """Every chunk decodes max_iters steps (T_targets under GTA) without its own stop rule; the
+        tower's stop step over all rows truncates the outputs.  Injected prenet masks cover the
+        whole batch and are sliced per chunk; the device RNG of chunk c is keyed by seed + c."""
+        B = self._B
+        fr, st, al = [], [], []
+        for c, (ch, (s, e)) in enumerate(zip(self._chunks, self._ranges(B))):
+            if e <= s:
+                continue
+            pm = None if prenet_masks is None else np.asarray(prenet_masks)[:, :, s:e]
+            tg = None if targets is None else f32(targets)[s:e]
+            f, so, a = ch.decode(max_iters, pm, seed + c, tg)
+            fr.append(f)
+            st.append(so)
+            al.append(a)
+        frames, stop, align = np.concatenate(fr), np.concatenate(st), np.concatenate(al)
+        n = frames.shape[1] if targets is not None else global_stop_steps(stop, self.hp.stop_at_any)
+        self._n_steps = n
+        # each chunk decoded past the tower's stop step: postnet(None) takes these n frames
+        self._frames = np.ascontiguousarray(frames[:, :n])
+        return self._frames, stop[:, :n], align[:, :, :n]
+
     def zero_state(self):
         """TacotronDecoderCell.zero_state (Architecture_wrappers.py:158-195) for the batch of the last
         encode: dict of numpy arrays h1, c1, h2, c2 [B,H], attention [B,D_mem], alignments
@@ -176,6 +259,16 @@ class TacotronEngine(object):
         P = self.hp.prenet_layers[0]
         fi = f32(frame_in)
         m = np.ascontiguousarray(prenet_masks, np.uint8)
+        if self._chunks:
+            outs = []
+            for ch, (s, e) in zip(self._chunks, self._ranges(B)):
+                if e > s:
+                    sub = {k: (v if k == "time" else np.asarray(v)[s:e]) for k, v in state.items()}
+                    outs.append(ch.decoder_step(fi[s:e], m[:, s:e], sub))
+            nxt = {k: np.concatenate([o[3][k] for o in outs]) for k in outs[0][3] if k != "time"}
+            nxt["time"] = outs[0][3]["time"]
+            return (np.concatenate([o[0] for o in outs]), np.concatenate([o[1] for o in outs]),
+                    np.concatenate([o[2] for o in outs]), nxt)
         if fi.shape != (B, self.hp.num_mels) or m.shape != (2, B, P):
             raise ValueError("frame_in must be [B, num_mels] and prenet_masks [2, B, prenet_units]")
         names = ("h1", "c1", "h2", "c2", "attention", "alignments")
@@ -200,6 +293,9 @@ class TacotronEngine(object):
         (hp.predict_linear; tacotron.py:466-481)."""
         m = f32(mels)
         B, T, _ = m.shape
+        if self._chunks:
+            return np.concatenate([ch.linear_outputs(m[s:e]) for ch, (s, e) in
+                                   zip(self._chunks, self._ranges(B)) if e > s])
         out = np.zeros((B, T, self.hp.num_freq), np.float32)
         self._ok(self.lib.tt2_linear_outputs(self.h, ptr(m), B, T, ptr(out)))
         return out
@@ -208,11 +304,20 @@ class TacotronEngine(object):
         """Tacotron_emt_attn: emotion labels [B] (the emt_labels placeholder, synthesizer.py:35) used
         by the next encode ('style_tokens' one-hot query)."""
         lab = i32(labels)
+        if self._chunks:
+            for ch, (s, e) in zip(self._chunks, self._ranges(lab.shape[0])):
+                if e > s:
+                    ch.set_emt_labels(lab[s:e])
+            return
         self._ok(self.lib.tt2_set_emt_labels(self.h, ptr(lab), lab.shape[0]))
 
     def emt_alignments(self):
         """Tacotron_emt_attn: emotion attention weights of the last decode, [B, heads, T_v, n_steps]
         (tower_alignments_emt)."""
+        if self._chunks:
+            n = self._n_steps
+            return np.concatenate([ch.emt_alignments()[..., :n] for ch, (s, e) in
+                                   zip(self._chunks, self._ranges(self._B)) if e > s])
         heads, tv = ctypes.c_int32(), ctypes.c_int32()
         self._ok(self.lib.tt2_emt_alignments(self.h, None, ctypes.byref(heads), ctypes.byref(tv)))
         n = self._n_steps
@@ -224,6 +329,8 @@ class TacotronEngine(object):
         """(persistent, kernel_ms): 1 when the single-launch persistent decoder serves the current
         shapes (k_decode_persist), 0 for the per-step launch path; HIP-event time of the last
         persistent decode launch."""
+        if self._chunks:
+            return self._chunks[0].decoder_path()
         p = ctypes.c_int()
         ms = ctypes.c_float()
         self._ok(self.lib.tt2_decoder_path(self.h, ctypes.byref(p), ctypes.byref(ms)))
@@ -233,6 +340,13 @@ class TacotronEngine(object):
         if frames is not None:
             frames = f32(frames)
             B, T = frames.shape[:2]
+        if self._chunks:
+            if frames is None:
+                frames = self._frames
+                T = frames.shape[1]
+            parts = [ch.postnet(frames[s:e], e - s, T)
+                     for ch, (s, e) in zip(self._chunks, self._ranges(B)) if e > s]
+            return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
         dec = np.zeros((B, T, self.hp.num_mels), np.float32)
         mel = np.zeros((B, T, self.hp.num_mels), np.float32)
         self._ok(self.lib.tt2_postnet(self.h, ptr(frames), B, T, ptr(dec), ptr(mel)))

@@ -278,3 +278,52 @@ def test_smoothing_normalization_matches_oracle(cpu, constraint):
     hp.override_from_dict(dict(smoothing=False))
     ref0 = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp, constraint), masks, n)
     assert np.abs(ref0["alignments"] - al).max() > 1e-3
+
+
+def test_chunk_ranges_and_global_stop():
+    """Row chunks of a tower above one context's 32 rows, and the tower-level stop step
+    (TacoTestHelper, helpers.py:40-54: all rows' rounded stop tokens, or any with stop_at_any)."""
+    from tt2.engine import chunk_ranges, global_stop_steps
+    assert chunk_ranges(32) == [(0, 32)]
+    assert chunk_ranges(33) == [(0, 17), (17, 33)]
+    assert chunk_ranges(96) == [(0, 32), (32, 64), (64, 96)]
+    assert chunk_ranges(65) == [(0, 22), (22, 44), (44, 65)]
+    st = np.full((4, 9), 0.2, np.float32)
+    assert global_stop_steps(st, False) == 9 and global_stop_steps(st, True) == 9
+    st[1, 3] = 0.9                       # one row only: the any-rule fires at step 3
+    assert global_stop_steps(st, True) == 4 and global_stop_steps(st, False) == 9
+    st[:, 6] = 0.75
+    assert global_stop_steps(st, False) == 7
+    st[:, 5] = 0.5                       # tf.round: half to even -> 0, no stop at step 5
+    assert global_stop_steps(st, False) == 7
+
+
+@pytest.mark.parametrize("stop_at_any,bias,scale,steps", [(False, -6.0, 1, 12), (True, -3.0, 30, 3),
+                                                         (False, 4.0, 1, 1)])
+def test_chunked_tower_matches_oracle(cpu, stop_at_any, bias, scale, steps):
+    """A 40-row tower (two 20-row contexts, no stop rule of their own) against one oracle decode
+    of all 40 rows: frames, alignments and the tower's stop step.  The stop
+    projection is biased / scaled so the rule never fires, fires mid-run on a few rows (any), or
+    fires on every row at the first step (all)."""
+    from tt2.engine import TacotronEngine
+    from _common import STOP_BIAS
+    hp = small_hparams()
+    hp.override_from_dict(dict(stop_at_any=stop_at_any))
+    W = init_tacotron_weights(hp, seed=5339)
+    W[STOP_BIAS] = np.full((1,), bias, np.float32)
+    K = STOP_BIAS.replace("/bias", "/kernel")
+    W[K] = W[K] * scale
+    B, T, n = 40, 9, 12
+    ids, lens, re, rs = tacotron_inputs(B, T, 40, seed=17)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=17)
+    eng = TacotronEngine(hp, W, B, T, 40, n, lib=cpu)
+    assert eng._chunks is not None and [c.caps[0] for c in eng._chunks] == [20, 20]
+    out = eng.synthesize(ids, lens, re, rs, n, masks)
+    eng.close()
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, n)
+    assert ref["mel_outputs"].shape[1] == steps
+    assert out["mel_outputs"].shape == ref["mel_outputs"].shape
+    np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(out["alignments"], ref["alignments"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(out["stop_token_prediction"], ref["stop_token_prediction"], rtol=0,
+                               atol=1e-5)

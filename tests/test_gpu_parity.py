@@ -537,3 +537,33 @@ def test_smoothing_normalization(widths):
         np.testing.assert_allclose(align, out["alignments"][:, :, t], atol=1e-5)
         np.testing.assert_allclose(frame, out["frames"][:, t], atol=1e-5)
     eng.close()
+
+
+@pytest.mark.parametrize("stop_at_any,bias,scale,steps", [(False, -6.0, 1, 14), (True, -3.0, 30, None)])
+def test_chunked_tower_b48_matches_oracle(stop_at_any, bias, scale, steps):
+    """A 48-row tower (two 24-row contexts decoding without their own stop rule, the tower's stop
+    step taken over all rows afterwards) against one oracle decode of all 48 rows (VERDICT r04
+    item 7; hparams.py:44 batches up to 96 rows per tower)."""
+    from _common import STOP_BIAS
+    from tt2.weights import init_tacotron_weights
+    hp = small_hparams()
+    hp.override_from_dict(dict(stop_at_any=stop_at_any))
+    W = init_tacotron_weights(hp, seed=5339)
+    W[STOP_BIAS] = np.full((1,), bias, np.float32)
+    K = STOP_BIAS.replace("/bias", "/kernel")
+    W[K] = W[K] * scale
+    B, T, n = 48, 11, 14
+    ids, lens, re, rs = tacotron_inputs(B, T, 40, seed=23)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=23)
+    eng = _engine(hp, W, B, T, 40, n)
+    assert [c.caps[0] for c in eng._chunks] == [24, 24]
+    out = eng.synthesize(ids, lens, re, rs, n, masks)
+    eng.close()
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp), masks, n)
+    if steps is not None:
+        assert ref["mel_outputs"].shape[1] == steps
+    else:
+        assert 1 < ref["mel_outputs"].shape[1] < n
+    assert out["mel_outputs"].shape == ref["mel_outputs"].shape
+    np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], rtol=0, atol=MEL_TOL)
+    np.testing.assert_allclose(out["alignments"], ref["alignments"], rtol=0, atol=1e-5)

@@ -894,3 +894,89 @@ def test_gpu_train_encoder_planes_match_im2col():
             den = max(den, np.linalg.norm(gb[n.replace("/bias", "/kernel")]))
         rel = float(np.linalg.norm(ga[n] - gb[n]) / max(den, 1e-30))
         assert rel < 5e-2, (n, rel)
+
+
+def _trainer_run(hp, W, case, env, postnet=False):
+    """One bf16 forward/backward under the given TT2_* environment (read at context creation)."""
+    import os
+    from tt2.train import TacotronTrainer
+    mem, lens, tg, st, pm, zm = case
+    B, T_in, T_out = tg.shape[0], mem.shape[1], tg.shape[1]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", postnet=postnet)
+        try:
+            tr.forward_backward(mem, lens, tg, st, pm, zm)
+            L = tr.losses()
+            fr, sl, al = tr.outputs(T_in, T_out)
+            g = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in TRN.train_var_names()}
+            gmem = tr.get("memory", 1, mem.shape)
+            persist = float(tr.get("diag:persist", 0, (1,))[0])
+        finally:
+            tr.close()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return dict(L=L, fr=fr, sl=sl, al=al, g=g, gmem=gmem, persist=persist)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T_in,T_out,zmask", [(16, 40, 24, True), (5, 7, 3, False), (64, 150, 12, True)])
+def test_gpu_train_persistent_forward_matches_launch_loop(B, T_in, T_out, zmask):
+    """The persistent teacher-forced forward (train_persist.hip: one launch for the whole decoder
+    loop, LSTM weights resident) against the per-step launch loop (TT2_TR_PERSIST=0) at the fork
+    widths, bf16 step, ragged lengths: same operand rounding, different fp32 summation order
+    (K split over waves, energies summed over attention-dim quarters).  Frames / stop logits within
+    1e-3, alignments within 1e-4, losses within 1e-5 relative, every gradient within 1e-2
+    (Frobenius, relative: the test_gpu_train_fused_lstm_matches_split_k_path tolerance)."""
+    from tt2.hparams import hparams
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    assert memory_width(hp) == 1024
+    W = init_tacotron_weights(hp, seed=5339)
+    mem, lens, tg, st = train_batch(B, T_in, T_out, memory_width(hp), seed=7)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=7)
+    zm = zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=7) if zmask else None
+    case = (mem, lens, tg, st, pm, zm)
+    p = _trainer_run(hp, W, case, {"TT2_TR_PERSIST": "1"})
+    q = _trainer_run(hp, W, case, {"TT2_TR_PERSIST": "0"})
+    assert p["persist"] == 1.0 and q["persist"] == 0.0
+    print("frames {:.3e} stop {:.3e} align {:.3e}".format(float(np.abs(p["fr"] - q["fr"]).max()),
+                                                         float(np.abs(p["sl"] - q["sl"]).max()),
+                                                         float(np.abs(p["al"] - q["al"]).max())))
+    assert np.abs(p["fr"] - q["fr"]).max() < 1e-3
+    assert np.abs(p["sl"] - q["sl"]).max() < 1e-3
+    assert np.abs(p["al"] - q["al"]).max() < 1e-4
+    for k in ("before", "stop_token"):
+        assert abs(p["L"][k] - q["L"][k]) < 1e-5 * abs(q["L"][k]), (k, p["L"][k], q["L"][k])
+    for n in list(p["g"]) + ["memory"]:
+        a, b = (p["gmem"], q["gmem"]) if n == "memory" else (p["g"][n], q["g"][n])
+        rel = float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+        print("  {:90s} rel {:.3e}".format(n, rel))
+        assert rel < 1e-2, (n, rel)
+
+
+@pytest.mark.gpu
+def test_gpu_train_persistent_forward_close_to_oracle():
+    """The persistent forward's bf16 step at the fork widths (D_mem 1024) against the float64
+    oracle: the mixed-precision tolerance of test_gpu_train_bf16_gemms_close_to_oracle."""
+    from tt2.hparams import hparams
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    B, T_in, T_out = 4, 37, 10
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
+    assert mem.shape[2] == 1024
+    r = _trainer_run(hp, W, (mem, lens, tg, st, pm, zm), {"TT2_TR_PERSIST": "1"})
+    assert r["persist"] == 1.0
+    out, (b, s, _), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight, clip=_clip(hp))
+    assert np.abs(r["fr"] - out["frames"]).max() < 1e-2
+    assert np.abs(r["al"] - out["alignments"]).max() < 1e-3
+    assert abs(r["L"]["before"] - b) < 1e-3 * b
+    for n in TRN.train_var_names():
+        frob = float(np.linalg.norm(r["g"][n] - g[n]) / max(np.linalg.norm(g[n]), 1e-30))
+        print("  {:90s} frob {:.3e}".format(n, frob))
+        assert frob < (0.1 if "prenet" in n else 1e-2), (n, frob)
