@@ -6,8 +6,8 @@ import sys
 import numpy as np
 
 NAMES = ["start", "L1 ctx waited", "L1 mfma", "L1 red", "H1 published", "H1 waited", "L2 mfma",
-         "H2 published", "H2 waited", "h2 row", "q + f", "qv", "energies", "offchain1", "E taken",
-         "softmax", "context", "CTX published", "offchain2"]
+         "H2 published", "H2 waited", "hz1 part", "query", "qv", "energies", "hz2 part", "E taken",
+         "softmax", "context", "CTX published", "prenet part"]
 s = np.fromfile(sys.argv[1], dtype=np.int64).reshape(256, 32)
 r = (s - s[:, 0].min()) * 0.01
 for i, n in enumerate(NAMES):

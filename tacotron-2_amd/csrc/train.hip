@@ -63,6 +63,7 @@ struct tt2_train_ctx {
   // backward
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
+  DevBuf DF2, DCUM2, PQ2, SC2;  // k_tr_att_bwd_q: df / d cum / d query / Σ a·d cum partials by step parity
   DevBuf TH, E, DF, PQ, FALL, ALN;
   // the large plain products (tr_gemm_big)
   DevBuf blasA, blasB, blasP;  // gemm_bf16_kc: bf16 operand copies, split-K partials
@@ -117,7 +118,7 @@ struct tt2_train_ctx {
   DevBuf W1T, sDZ, sDP, sDX;
   // persistent forward (train_persist.hip; opt-in with TT2_TR_PERSIST=1, else the per-step launches): exchange
   // buffers, energy granules, flags + control words, the prenet rows in bf16 fragment layout
-  DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps;
+  DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps, tpKWT;
   bool tp_on = false, tp_last = false, tp_check = false;
   int* tp_ctl_host = nullptr;  // pinned [2]: the launch's control words, checked at the next read-back
 };
@@ -410,6 +411,8 @@ struct TrFused {
   const __bf16* Ah;  // this step's bf16 input rows, TF layout of width K, or
   const float* Af;   // fp32 input rows (TF_BWD_H)
   long lda;
+  int af_parts;      // > 1: each Af row is the sum of af_parts partial rows af_pstride apart (in order)
+  int af_pstride;
   const __bf16* Wt;  // W^T in TF layout, column-group order (k_tr_tf_weights)
   int K, B, H, N;
   int t, layer;
@@ -694,7 +697,11 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
         if constexpr (MODE == TF_BWD_H) {
           if (rok) {
             const float* p = a.Af + (long)(r0 + c) * a.lda + k;
-            const f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+            f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+            for (int g = 1; g < a.af_parts; ++g) {
+              x0 += *reinterpret_cast<const f32x4*>(p + (long)g * a.af_pstride);
+              x1 += *reinterpret_cast<const f32x4*>(p + (long)g * a.af_pstride + 4);
+            }
             va[s] = bf8{(__bf16)x0[0], (__bf16)x0[1], (__bf16)x0[2], (__bf16)x0[3],
                         (__bf16)x1[0], (__bf16)x1[1], (__bf16)x1[2], (__bf16)x1[3]};
           } else {
@@ -825,6 +832,8 @@ struct TrAtt {
   float* dBA;    // [B][nt][A]
   float* dKC;    // [B][nt][KW][F]
   float* dBC;    // [B][nt][F]
+  long long* stamps;  // diagnostic: k_tr_att_bwd_q stage stamps of step stamp_t ([B][4][16]) or null
+  int stamp_t;
 };
 
 // Location features of rows j0..j0+TR_JT-1 of utterance b (attention.py:193-195):
@@ -1555,6 +1564,380 @@ __global__ __launch_bounds__(256) void k_tr_att_conv_bwd(TrAtt a) {
   }
 }
 
+// The whole attention backward of one step (k_tr_att_energy_bwd2 + k_tr_att_conv_bwd) in ONE launch of
+// nq <= 4 work-groups per row (256 work-groups at B = 64): work-group (q, b) owns the positions
+// [j0, j1) of row b.  The location-conv backward into d cum crosses positions; it is deferred by one
+// step so no work-group waits for another in the same launch:
+//   d cum_t[i] = d cum_{t+1}[i] + Σ_tap,c df_{t+1}[i - tap + pad][c]·Kc[tap][c]
+// is formed for the own positions from the previous launch's df (the rows [j0 - pad, j1 + pad)), and
+// the full-row Σ_i a_t[i]·d cum_t[i] of the softmax backward as Σ_i a_t[i]·d cum_{t+1}[i] plus the
+// previous launch's per-range partials Σ_{j'} Σ_c df_{t+1}[j'][c]·Σ_tap a_t[j' + tap - pad]·Kc[tap][c]
+// (the same sum with the conv moved onto the alignments).  d cum, df, those partials and the d query
+// partials are double-buffered by step parity; the LSTM-2 backward of the step sums the nq d query
+// partials of its A-operand rows itself (TrFused::af_parts) and the next launch writes the step's sum
+// to DQ (for the query-layer kernel gradient after the loop).
+//   d align_j = dctx·values_j + d cum_j (the bf16 values copy the forward's context read, when present)
+//   de_j = a_j (d align_j - s), du_jk = de_j v_k (1 - th_jk²), d keys += du, d v_a, d b_a
+//   df = du·W_locᵀ and the d Kc partial Σ_j df[j][c]·cum_{t-1}[j + tap - pad] on fp32 MFMA
+//   (v_mfma_f32_16x16x4f32: exact fp32 products); cross-lane sums by DPP (no LDS round trips)
+constexpr int TRQ_NT = 256;
+constexpr int TRQ_RB = 16;  // own rows per wave per batch of loads
+typedef float trq_f4 __attribute__((ext_vector_type(4)));
+struct TrQ {
+  int nq;
+  const float* dcum_in;  // [B][Tin] d cum input of the previous launch (full rows)
+  const float* df_in;    // [B][Tin][F] df of the previous launch
+  const float* pq_in;    // [B][nt][A] d query partials of the previous launch
+  const float* sc_in;    // [B][4] the previous launch's conv-moved Σ a·d cum partials
+  float *dcum_out, *df_out, *pq_out, *sc_out;
+};
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float trq_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, RMASK, 0xf, false));
+}
+// sum of the 16 lanes of each row, in every lane of the row (xor 1, xor 2, half mirror, mirror)
+__device__ __forceinline__ float trq_row_sum(float v) {
+  v += trq_dpp<0xB1, 0xf>(v);
+  v += trq_dpp<0x4E, 0xf>(v);
+  v += trq_dpp<0x141, 0xf>(v);
+  v += trq_dpp<0x140, 0xf>(v);
+  return v;
+}
+// wave sum (uniform result): row sums, rows chained by row_bcast:15 / row_bcast:31 into lane 63
+__device__ __forceinline__ float trq_wave_sum(float v) {
+  v = trq_row_sum(v);
+  v += trq_dpp<0x142, 0xa>(v);
+  v += trq_dpp<0x143, 0xc>(v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+__global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
+  constexpr int A = 128, F = 32, KW = 31, PAD = 15, NW = TRQ_NT / 64, TMX = 256, RQX = 64, HR = RQX + 2 * PAD + 2;
+  __shared__ __attribute__((aligned(16))) float dctx[1024];
+  constexpr int WLS = A + 4;                                  // padded W_loc rows: conflict-free A fragments
+  __shared__ __attribute__((aligned(16))) float wls[F * WLS];  // W_loc [c][k]
+  __shared__ __attribute__((aligned(16))) float kcs[32 * F];  // Kc [tap][c] (tap 31 zero)
+  __shared__ __attribute__((aligned(16))) float dfin[HR * F]; // previous df, row r = position j0 - pad - 1 + r
+  __shared__ float alns[TMX];                                 // a_t
+  __shared__ float dcin[TMX];                                 // d cum_{t+1}
+  __shared__ float alnh[RQX + 32];                            // a_{t-1}[j0 - pad + i] (the next step's alignments)
+  __shared__ float dcum[RQX];                                 // d cum_t of the own rows
+  __shared__ float de[RQX];
+  __shared__ float dus[RQX * (A + 1)];                        // du of the own rows (stride A + 1)
+  __shared__ float dfo[RQX * F];                              // this launch's df of the own rows (zero past nown)
+  __shared__ float cseg[RQX + 32];                            // cum_{t-1}[j0 + i - pad]
+  __shared__ float red[2][NW][A];
+  __shared__ float s16[16];
+  const int q = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int Tin = a.Tin, D = a.D, nq = z.nq;
+  const long tb = (long)a.t * a.B + b;
+  const int len = a.lens[b];
+  const int RQ = (Tin + nq - 1) / nq, j0 = min(Tin, q * RQ), j1 = min(Tin, j0 + RQ), nown = j1 - j0;
+  const int k0 = lane, k1 = lane + 64;
+  const int jl = lane & 15, g4 = lane >> 4;
+  long long* const stp = (a.stamps && a.t == a.stamp_t && tid == 0) ? a.stamps + ((long)b * 4 + q) * 16 : nullptr;
+#define TRQ_STAMP(i) \
+  if (stp) stp[i] = __builtin_amdgcn_s_memrealtime()
+  TRQ_STAMP(0);
+  const long pt = (long)b * a.nt + q;
+  // ---- the own rows' values (bf16 step) and tanh / d keys rows first: their round trip overlaps the
+  // staging and the d cum phase (wave w: rows jr = w + NW u; nown <= NW·TRQ_RB)
+  typedef unsigned trq_u4 __attribute__((ext_vector_type(4)));
+  const bool v16 = a.values16 && (a.D & 7) == 0;
+  trq_u4 vv[TRQ_RB][2];
+  float t0[TRQ_RB], t1[TRQ_RB], e0[TRQ_RB], e1[TRQ_RB];
+#pragma unroll
+  for (int u = 0; u < TRQ_RB; ++u) {
+    const int jr = w + NW * u;
+    const bool ok = jr < nown;
+    const trq_u4* v8 = reinterpret_cast<const trq_u4*>(a.values16 + ((long)b * Tin + j0 + (ok ? jr : 0)) * D);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      vv[u][i] = (v16 && ok && (lane + 64 * i) * 8 < D) ? v8[lane + 64 * i] : trq_u4{0u, 0u, 0u, 0u};
+    const long hrow = (tb * Tin + j0 + (ok ? jr : 0)) * A, krow = ((long)b * Tin + j0 + (ok ? jr : 0)) * A;
+    t0[u] = ok ? a.TH[hrow + k0] : 0.f;
+    t1[u] = ok ? a.TH[hrow + k1] : 0.f;
+    e0[u] = ok ? a.DKEYS[krow + k0] : 0.f;
+    e1[u] = ok ? a.DKEYS[krow + k1] : 0.f;
+  }
+  // ---- staging: every load of the prologue in flight at once (16-byte loads where the rows allow)
+  const trq_f4 zf4 = {0.f, 0.f, 0.f, 0.f};
+  const bool d4ok = tid * 4 < D;  // host: D % 4 == 0, D <= 1024
+  const long ofs_p = tb * (a.H + D) + a.H, ofs_x = (tb + a.B) * (a.P + D + a.H) + a.P;
+  const trq_f4 xp = d4ok ? *reinterpret_cast<const trq_f4*>(a.dPIN + ofs_p + 4 * tid) : zf4;
+  const trq_f4 xx = d4ok ? *reinterpret_cast<const trq_f4*>(a.dX1 + ofs_x + 4 * tid) : zf4;
+  const trq_f4 xc = d4ok ? *reinterpret_cast<const trq_f4*>(a.PIN + ofs_p + 4 * tid) : zf4;
+  trq_f4 wlv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) wlv[u] = reinterpret_cast<const trq_f4*>(a.Wl)[tid + TRQ_NT * u];
+  const trq_f4 kcv = tid < KW * F / 4 ? reinterpret_cast<const trq_f4*>(a.Kc)[tid] : zf4;
+  constexpr int NH = (HR * F / 4 + TRQ_NT - 1) / TRQ_NT;
+  trq_f4 dfv[NH];
+  const float* dfrow = z.df_in + (long)b * Tin * F;
+#pragma unroll
+  for (int u = 0; u < NH; ++u) {
+    const int i4 = tid + TRQ_NT * u, r = i4 / (F / 4), j = j0 - PAD - 1 + r;
+    dfv[u] = (i4 < HR * F / 4 && j >= 0 && j < Tin) ? reinterpret_cast<const trq_f4*>(dfrow + (long)j * F)[i4 % (F / 4)]
+                                                    : zf4;
+  }
+  const float aln_v = tid < Tin ? a.ALN[tb * Tin + tid] : 0.f;
+  const float dci_v = tid < Tin ? z.dcum_in[(long)b * Tin + tid] : 0.f;
+  const int jc = j0 + tid - PAD;
+  const bool hal = tid < RQX + 32 && jc >= 0 && jc < Tin;
+  const float cs_v = hal ? a.CUM[tb * Tin + jc] : 0.f;
+  const float an_v = (hal && a.t > 0) ? a.ALN[(tb - a.B) * Tin + jc] : 0.f;
+  float scv = 0.f;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) scv += g < nq ? z.sc_in[(long)b * 4 + g] : 0.f;
+  const float odv = tid < A ? a.dV[pt * A + tid] : 0.f, odb = tid < A ? a.dBA[pt * A + tid] : 0.f;
+  const float obc = tid < F ? a.dBC[pt * F + tid] : 0.f;
+  // the d Kc slot entries of this lane's MFMA output (wave w < 4: tap tile w >> 1, filter tile w & 1)
+  const int kt0 = 16 * (w >> 1) + 4 * g4, kcc = 16 * (w & 1) + jl;
+  float okc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) okc[i] = kt0 + i < KW ? a.dKC[pt * KW * F + (kt0 + i) * F + kcc] : 0.f;
+  // d query of step t + 1 = the sum of that launch's partials (in range order), written by q == 0
+  const bool dq_prev = q == 0 && tid < A && a.t + 1 < a.T;
+  float pqv[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) pqv[g] = (dq_prev && g < nq) ? z.pq_in[((long)b * a.nt + g) * A + tid] : 0.f;
+  // ---- LDS writes
+  float sp = 0.f;
+  if (d4ok) {
+    const trq_f4 v = xp + xx;
+    *reinterpret_cast<trq_f4*>(dctx + 4 * tid) = v;
+    sp = v[0] * xc[0] + v[1] * xc[1] + v[2] * xc[2] + v[3] * xc[3];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i4 = tid + TRQ_NT * u;  // W_loc element 4 i4 = row i4 / 32, column 4 (i4 % 32)
+    *reinterpret_cast<trq_f4*>(wls + (i4 >> 5) * WLS + 4 * (i4 & 31)) = wlv[u];
+  }
+  reinterpret_cast<trq_f4*>(kcs)[tid] = kcv;  // 256 x 4 = 32 x F: the tap-31 row zero
+#pragma unroll
+  for (int u = 0; u < NH; ++u) {
+    const int i4 = tid + TRQ_NT * u;
+    if (i4 < HR * F / 4) reinterpret_cast<trq_f4*>(dfin)[i4] = dfv[u];
+  }
+  alns[tid] = aln_v;
+  dcin[tid] = dci_v;
+  if (tid < RQX + 32) {
+    cseg[tid] = cs_v;
+    alnh[tid] = an_v;
+  }
+  for (int i = tid; i < RQX * F; i += TRQ_NT) dfo[i] = 0.f;
+  sp += aln_v * dci_v;  // Σ_i a_t[i] d cum_{t+1}[i] (a_t = 0 past the length)
+  __syncthreads();
+  TRQ_STAMP(1);
+  // ---- d cum_t of the own rows: 32 lanes (filters c, taps in registers) per position, then across the
+  // filters by DPP (lanes 31 / 63 hold positions p, p + 1)
+  float kcr[KW];
+#pragma unroll
+  for (int tp = 0; tp < KW; ++tp) kcr[tp] = kcs[tp * F + (tid & 31)];
+  for (int p0 = 0; p0 < nown; p0 += TRQ_NT / 32) {
+    const int ir = p0 + (tid >> 5), c = tid & 31;  // own row
+    float acc = 0.f;
+    if (ir < nown) {
+      const float* dr = dfin + (ir + 2 * PAD + 1) * F + c;  // row of position (j0 + ir) - tap + pad at -tap
+#pragma unroll
+      for (int tp = 0; tp < KW; ++tp) acc += dr[-tp * F] * kcr[tp];
+    }
+    acc = trq_row_sum(acc);
+    acc += trq_dpp<0x142, 0xa>(acc);
+    if ((lane & 31) == 31 && ir < nown) {
+      const float v = dcin[j0 + ir] + acc;
+      dcum[ir] = v;
+      z.dcum_out[(long)b * Tin + j0 + ir] = v;
+    }
+  }
+  TRQ_STAMP(2);
+  // s = Σ_j a_j da_j = dctx·ctx_t + Σ_j a_j d cum_t[j]   (block_sum's barriers also publish dcum)
+  const float s = block_sum(sp, s16) + scv;
+  TRQ_STAMP(3);
+  // ---- d align of the own rows (jr = w + NW u): every row's values in flight before the dot products
+  const trq_f4* d4 = reinterpret_cast<const trq_f4*>(dctx);
+  if (v16) {
+    trq_f4 dc[4];  // channels 8 (lane + 64 i) .. +8
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = (lane + 64 * i) * 8 < D;
+      dc[2 * i] = ok ? d4[2 * (lane + 64 * i)] : zf4;
+      dc[2 * i + 1] = ok ? d4[2 * (lane + 64 * i) + 1] : zf4;
+    }
+#pragma unroll
+    for (int u = 0; u < TRQ_RB; ++u) {
+      const int jr = w + NW * u;
+      if (jr >= nown) break;  // wave-uniform
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const unsigned x0 = vv[u][i][2 * h], x1 = vv[u][i][2 * h + 1];
+          const trq_f4 y = dc[2 * i + h];
+          acc += __uint_as_float(x0 << 16) * y[0] + __uint_as_float(x0 & 0xffff0000u) * y[1] +
+                 __uint_as_float(x1 << 16) * y[2] + __uint_as_float(x1 & 0xffff0000u) * y[3];
+        }
+      acc = trq_wave_sum(acc);
+      if (lane == 0) {
+        const int j = j0 + jr;
+        de[jr] = j < len ? alns[j] * ((acc + dcum[jr]) - s) : 0.f;
+      }
+    }
+  } else {
+    trq_f4 dc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dc[i] = (lane + 64 * i) * 4 < D ? d4[lane + 64 * i] : zf4;
+    for (int r0 = w; r0 < nown; r0 += NW * (TRQ_RB / 2)) {
+      trq_f4 vv[TRQ_RB / 2][4];
+#pragma unroll
+      for (int u = 0; u < TRQ_RB / 2; ++u) {
+        const int jr = r0 + NW * u;
+        const bool ok = jr < nown;
+        const trq_f4* v4 = reinterpret_cast<const trq_f4*>(a.values + ((long)b * Tin + j0 + (ok ? jr : 0)) * D);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vv[u][i] = (ok && (lane + 64 * i) * 4 < D) ? v4[lane + 64 * i] : zf4;
+      }
+#pragma unroll
+      for (int u = 0; u < TRQ_RB / 2; ++u) {
+        const int jr = r0 + NW * u;
+        if (jr >= nown) break;
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc += vv[u][i][0] * dc[i][0] + vv[u][i][1] * dc[i][1] + vv[u][i][2] * dc[i][2] + vv[u][i][3] * dc[i][3];
+        acc = trq_wave_sum(acc);
+        if (lane == 0) {
+          const int j = j0 + jr;
+          de[jr] = j < len ? alns[j] * ((acc + dcum[jr]) - s) : 0.f;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  TRQ_STAMP(4);
+  // ---- tanh backward, d keys, d v_a / d b_a partials of the own rows; du -> LDS
+  const float va0 = a.va[k0], va1 = a.va[k1];
+  float dv0 = 0.f, dv1 = 0.f, dq0 = 0.f, dq1 = 0.f;
+#pragma unroll
+  for (int u = 0; u < TRQ_RB; ++u) {
+    const int jr = w + NW * u;
+    if (jr >= nown) break;  // wave-uniform
+    const long hrow = (tb * Tin + j0 + jr) * A, krow = ((long)b * Tin + j0 + jr) * A;
+    const float dej = de[jr];
+    const float du0 = dej * va0 * (1.f - t0[u] * t0[u]), du1 = dej * va1 * (1.f - t1[u] * t1[u]);
+    dv0 += dej * t0[u];
+    dv1 += dej * t1[u];
+    dq0 += du0;
+    dq1 += du1;
+    a.DKEYS[krow + k0] = e0[u] + du0;
+    a.DKEYS[krow + k1] = e1[u] + du1;
+    a.TH[hrow + k0] = du0;  // d W_loc = FALL^T · du after the loop
+    a.TH[hrow + k1] = du1;
+    dus[jr * (A + 1) + k0] = du0;
+    dus[jr * (A + 1) + k1] = du1;
+  }
+  for (int i = nown * (A + 1) + tid; i < RQX * (A + 1); i += TRQ_NT) dus[i] = 0.f;
+  red[0][w][k0] = dv0;
+  red[0][w][k1] = dv1;
+  red[1][w][k0] = dq0;
+  red[1][w][k1] = dq1;
+  __syncthreads();
+  TRQ_STAMP(5);
+  if (tid < A) {
+    const float sv = (red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid]);
+    const float sq = (red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid]);
+    a.dV[pt * A + tid] = odv + sv;
+    a.dBA[pt * A + tid] = odb + sq;
+    z.pq_out[pt * A + tid] = sq;
+  }
+  // ---- df^T[c][j] = Σ_k W_loc[c][k] du[j][k]: wave w owns the position tile 16 w (16 rows), both
+  // filter tiles; A [c = 16 mt + jl][k = 4 ks + g4] from wls, B [k][j = 16 w + jl] from dus
+  if (16 * w < nown) {
+    trq_f4 acc[2] = {};
+    const float* dr = dus + (16 * w + jl) * (A + 1) + g4;
+#pragma unroll
+    for (int ks = 0; ks < 32; ++ks) {
+      const float bv = dr[4 * ks];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wls[(16 * mt + jl) * WLS + 4 * ks + g4], bv, acc[mt], 0, 0, 0);
+    }
+    const int jr = 16 * w + jl;
+    if (jr < nown) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int c0 = 16 * mt + 4 * g4;
+        *reinterpret_cast<trq_f4*>(dfo + jr * F + c0) = acc[mt];
+        *reinterpret_cast<trq_f4*>(z.df_out + ((long)b * Tin + j0 + jr) * F + c0) = acc[mt];
+      }
+    }
+  }
+  __syncthreads();
+  TRQ_STAMP(6);
+  // ---- d Kc partial [tap][c] = Σ_jr cseg[jr + tap]·dfo[jr][c]: wave w -> tap tile w >> 1, filter
+  // tile w & 1; A [tap = 16 mt + jl][jr = 4 ks + g4], B [jr = 4 ks + g4][c = 16 nt + jl]
+  {
+    const int mt = w >> 1, nt = w & 1;
+    trq_f4 acc = {};
+#pragma unroll
+    for (int ks = 0; ks < RQX / 4; ++ks) {
+      const int jr = 4 * ks + g4;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(cseg[jr + 16 * mt + jl], dfo[jr * F + 16 * nt + jl], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (kt0 + i < KW) a.dKC[pt * KW * F + (kt0 + i) * F + kcc] = okc[i] + acc[i];
+  }
+  // ---- d bc partial and the next launch's conv-moved partial Σ_jr Σ_c df[jr][c]·Σ_tap a_{t-1}[j0 + jr +
+  // tap - pad]·Kc[tap][c]: thread (c = tid & 31, row group tid >> 5)
+  {
+    const int c = tid & 31, gq = tid >> 5;
+    float accb = 0.f, accs = 0.f;
+    for (int jr = gq; jr < nown; jr += 8) {
+      const float dfv1 = dfo[jr * F + c];
+      accb += dfv1;
+      float g = 0.f;
+#pragma unroll
+      for (int tp = 0; tp < KW; ++tp) g += alnh[jr + tp] * kcr[tp];
+      accs += dfv1 * g;
+    }
+    float* const rbc = &red[0][0][0];  // free again: read before the df barrier
+    rbc[tid] = accb;
+    rbc[TRQ_NT + tid] = accs;
+    __syncthreads();
+    if (tid < F) {
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) v += rbc[g * 32 + tid];
+      a.dBC[pt * F + tid] = obc + v;
+    }
+    if (w == 1) {  // one wave: Σ over the 256 partials
+      float v = rbc[TRQ_NT + lane] + rbc[TRQ_NT + 64 + lane] + rbc[TRQ_NT + 128 + lane] + rbc[TRQ_NT + 192 + lane];
+      v = trq_wave_sum(v);
+      if (lane == 0) z.sc_out[(long)b * 4 + q] = v;
+    }
+  }
+  if (q == 0)  // stored last: a store ahead of the loads would hold up their waits (one vmcnt counter)
+    for (int n = tid; n < D; n += TRQ_NT) a.DCTX[tb * D + n] = dctx[n];
+  if (dq_prev) {
+    float dq = 0.f;
+    for (int g = 0; g < nq; ++g) dq += pqv[g];
+    a.DQ[(tb + a.B) * A + tid] = dq;
+  }
+  TRQ_STAMP(7);
+#undef TRQ_STAMP
+}
+
+// d query of the last backward launch (step 0): the sum of its position-range partials
+__global__ void k_tr_dq_sum(const float* __restrict__ pq, int nt, int nq, int A, float* __restrict__ dq) {
+  const int b = blockIdx.x;
+  for (int k = threadIdx.x; k < A; k += blockDim.x) {
+    float v = 0.f;
+    for (int g = 0; g < nq; ++g) v += pq[((long)b * nt + g) * A + k];
+    dq[(long)b * A + k] = v;
+  }
+}
+
 // d W_loc (location_features_layer, attention.py:59-62) = Σ_r f[r][c]·du[r][k] over all R = T·B·T_in
 // rows of FALL [R][F] and the du copy in TH [R][A], on fp32 MFMA (v_mfma_f32_32x32x2f32, exact fp32
 // products): one streaming pass over the two fp32 arrays instead of a transpose, two bf16 copies and a
@@ -2099,6 +2482,7 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F); f(c->FALL, TB * Tin * F); f(c->ALN, TB * Tin);
   f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
   f(c->dZ, TB * P); f(c->dPre, TB * P);
+  f(c->DF2, 2 * B * Tin * F); f(c->DCUM2, 2 * B * Tin); f(c->PQ2, 2 * B * NT * A); f(c->SC2, 2 * B * 4);
   f(c->W1T, P * NM); f(c->sDZ, B * P); f(c->sDP, B * P); f(c->sDX, B * NM); c->TLEN.alloc(sizeof(int) * (size_t)B);
   const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM, TB * Tin * F,
                               // Postnet im2col^T: K·cin rows per position, cin = num_mels for layer 1
@@ -2312,17 +2696,19 @@ static void tr_persist_forward(tt2_train_ctx* c, const TrAtt& at, const uint8_t*
   grow(c->tpEX, 2ul * 64 * 4 * TP_TMAX * sizeof(unsigned long long));
   grow(c->tpCtl, sizeof(unsigned) * (3ul * TP_NREP * TP_NB + 16));
   grow(c->tpPre, (size_t)T * 64 * TP_P * sizeof(__bf16));
+  grow(c->tpKWT, sizeof(float) * TP_A * 32);
   if (!c->tp_ctl_host) TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->tp_ctl_host), 4 * sizeof(int)));
   // rows >= B of the exchange buffers stay zero (they are A-operand padding); the flags and the
   // granules restart their tags at 1 every launch
   for (DevBuf* d : {&c->tpCX, &c->tpH1X, &c->tpZ1X, &c->tpH2X, &c->tpZ2X, &c->tpEX, &c->tpCtl})
     TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
   tp_prenet_rows(c->X1.as<float>(), c->LX1, c->B, T, c->tpPre.as<__bf16>(), s);
+  tp_prepare(at.Kc, at.bc, at.Wl, c->tpKWT.as<float>(), s);
   TpArgs a{};
   a.B = c->B; a.T = T; a.Tin = Tin; a.KW = c->KW; a.z = c->cfg.zoneout;
   a.K1T = c->hK1T.as<__bf16>(); a.K2T = c->hK2T.as<__bf16>(); a.Wq = c->hWq.as<__bf16>();
   a.b1 = pvar(c, L1V("bias")); a.b2 = pvar(c, L2V("bias"));
-  a.Kc = at.Kc; a.bc = at.bc; a.Wl = at.Wl; a.va = at.va; a.ba = at.ba;
+  a.Kc = at.Kc; a.bc = at.bc; a.Wl = at.Wl; a.va = at.va; a.ba = at.ba; a.KWT = c->tpKWT.as<float>();
   a.keys = at.keys; a.values16 = at.values16; a.lens = at.lens; a.zm = zm; a.preh = c->tpPre.as<__bf16>();
   a.X1 = c->X1.as<float>(); a.X2 = c->X2.as<float>(); a.PIN = c->PIN.as<float>();
   a.G1 = c->G1.as<float>(); a.G2 = c->G2.as<float>(); a.CN1 = c->CN1.as<float>(); a.CN2 = c->CN2.as<float>();
@@ -2343,6 +2729,7 @@ static void tr_persist_forward(tt2_train_ctx* c, const TrAtt& at, const uint8_t*
     a.stamps = c->tpStamps.as<long long>();
   }
   tp_launch(a, s);
+  tp_location_features(at.CUM, at.Kc, at.bc, c->B, T, Tin, at.FALL, s);
   if (st) {
     std::vector<long long> h((size_t)TP_NB * 32);
     TT2_HIP(hipMemcpyAsync(h.data(), a.stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, s));
@@ -2600,18 +2987,57 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   TT2_HIP(hipMemsetAsync(dX2 + TB * 2 * H, 0, sizeof(float) * (size_t)B * 2 * H, s));
   for (DevBuf* d : {&c->DC1, &c->DC2, &c->R1, &c->R2, &c->DKEYS, &c->DCUM, &c->dV, &c->dBA, &c->dKC, &c->dBC})
     TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+  // the attention backward as one launch of nq work-groups per row (k_tr_att_bwd_q; TT2_TR_ATTQ=0: the
+  // two per-tile launches)
+  static const bool att_q_env = [] {
+    const char* e = std::getenv("TT2_TR_ATTQ");
+    return !(e && e[0] == '0');
+  }();
+  const bool att_q = att_q_env && fused && A == 128 && F == 32 && KW == 31 && D % 4 == 0 && D <= 1024 && Tin <= 256;
+  const int nq = std::min(4, NT);
+  if (att_q)
+    for (DevBuf* d : {&c->DF2, &c->DCUM2, &c->SC2}) TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+  // TT2_ATTQ_STAMP=<step>: k_tr_att_bwd_q stage stamps of that step -> TT2_ATTQ_STAMP_FILE (diagnostic)
+  const char* aqs = std::getenv("TT2_ATTQ_STAMP");
+  at.stamps = nullptr;
+  at.stamp_t = aqs ? std::atoi(aqs) : -1;
+  if (aqs && att_q) {
+    if (c->tpStamps.bytes < sizeof(long long) * (size_t)B * 64) c->tpStamps.alloc(sizeof(long long) * (size_t)B * 64);
+    TT2_HIP(hipMemsetAsync(c->tpStamps.p, 0, c->tpStamps.bytes, s));
+    at.stamps = c->tpStamps.as<long long>();
+  }
   for (int t = T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
     at.t = t;
     // (d align from the bf16 values copy measured 28.3 against 18.7 us per launch: hipcc waits
     // vmcnt(0) behind the bf16 loads of each row -- the fp32 rows stay)
-    if (A <= 128 && D <= 1024 && D % 4 == 0 && tr_e2) hipLaunchKernelGGL(k_tr_att_energy_bwd2, att_grid, dim3(TR_E2T), 0, s, at);
-    else hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(TR_AT), 0, s, at);
-    hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
+    if (att_q) {
+      const long o1 = (long)((t + 1) & 1) * B * Tin, o0 = (long)(t & 1) * B * Tin;
+      float* dcum2 = c->DCUM2.as<float>();
+      float* df2 = c->DF2.as<float>();
+      float* pq2 = c->PQ2.as<float>();
+      float* sc2 = c->SC2.as<float>();
+      const long po1 = (long)((t + 1) & 1) * B * NT * A, po0 = (long)(t & 1) * B * NT * A;
+      TrQ z{};
+      z.nq = nq;
+      z.dcum_in = dcum2 + o1; z.df_in = df2 + o1 * F; z.pq_in = pq2 + po1; z.sc_in = sc2 + ((t + 1) & 1) * B * 4;
+      z.dcum_out = dcum2 + o0; z.df_out = df2 + o0 * F; z.pq_out = pq2 + po0; z.sc_out = sc2 + (t & 1) * B * 4;
+      hipLaunchKernelGGL(k_tr_att_bwd_q, dim3(nq, B), dim3(TRQ_NT), 0, s, at, z);
+    } else {
+      if (A <= 128 && D <= 1024 && D % 4 == 0 && tr_e2)
+        hipLaunchKernelGGL(k_tr_att_energy_bwd2, att_grid, dim3(TR_E2T), 0, s, at);
+      else
+        hipLaunchKernelGGL(k_tr_att_energy_bwd, att_grid, dim3(TR_AT), 0, s, at);
+      hipLaunchKernelGGL(k_tr_att_conv_bwd, att_grid, dim3(256), 0, s, at);
+    }
     if (fused) {  // the three per-step products of the LSTM backward, each fused with its consumer
       __bf16* dGh = c->dGh.as<__bf16>();
       TrFused f{};  // LSTM-2: d h2 = DQ·Wq^T + d PIN[t][:, :H] -> cell backward -> dG2
       f.Af = c->DQ.as<float>() + s1 * A; f.lda = A; f.Wt = c->tWq.as<__bf16>(); f.K = A; f.B = B; f.H = H;
+      f.af_parts = 1;
+      if (att_q) {  // the d query partials of this step's position ranges, summed by the consumer
+        f.Af = c->PQ2.as<float>() + (long)(t & 1) * B * NT * A; f.lda = (long)NT * A; f.af_parts = nq; f.af_pstride = A;
+      }
       f.t = t; f.layer = 1; f.z = z; f.zm = zm;
       f.G = c->G2.as<float>() + s1 * 4 * H; f.cn = c->CN2.as<float>() + s1 * H; f.c_prev = c->C2.as<float>() + s1 * H;
       f.dh_ext = dPIN + s1 * (H + D); f.ld_dh = H + D;
@@ -2676,6 +3102,19 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     }
   }
 
+  if (att_q)  // d query of step 0 (the later steps' sums were written by the launch after them)
+    hipLaunchKernelGGL(k_tr_dq_sum, dim3(B), dim3(128), 0, s, c->PQ2.as<float>(), NT, nq, A, c->DQ.as<float>());
+  if (at.stamps) {
+    std::vector<long long> h((size_t)B * 64);
+    TT2_HIP(hipMemcpyAsync(h.data(), at.stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipStreamSynchronize(s));
+    const char* fn = std::getenv("TT2_ATTQ_STAMP_FILE");
+    if (FILE* f = std::fopen(fn ? fn : "attq_stamps.bin", "wb")) {
+      std::fwrite(h.data(), sizeof(long long), h.size(), f);
+      std::fclose(f);
+    }
+    at.stamps = nullptr;
+  }
   // ---- weight gradients over all T·B rows ----
   float* TBUF = c->TBUF.as<float>();
   const int TBi = (int)TB;

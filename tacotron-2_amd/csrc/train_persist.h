@@ -36,6 +36,7 @@ struct TpArgs {
   const float* Wl;           // [F][A] location_features_layer
   const float* va;           // [A]
   const float* ba;           // [A]
+  const float* KWT;          // [A][32]: [a][tap < KW] = (Kc·W_loc)[tap][a], [a][31] = (bc·W_loc)[a] (tp_prepare)
   const float* keys;         // [B][Tin][A] fp32
   const __bf16* values16;    // [B][Tin][D] bf16
   const int* lens;           // [B]
@@ -63,5 +64,11 @@ bool tp_device_ok(int dev);
 void tp_launch(const TpArgs& a, hipStream_t s);
 // prenet rows X1[t][b][0:P] (fp32, row stride ld) -> bf16 A-fragment layout, rows >= B zero
 void tp_prenet_rows(const float* X1, long ld, int B, int T, __bf16* preh, hipStream_t s);
+// KWT (above) from the location conv kernel Kc [KW][F], its bias bc [F] and W_loc [F][A]
+void tp_prepare(const float* Kc, const float* bc, const float* Wl, float* KWT, hipStream_t s);
+// the location features of every step, FALL[t][b][j][c] = bc[c] + Σ_tap CUM[t][b][j + tap - 15]·Kc[tap][c]
+// (the launch loop's tr_locf_tile order), from the cumulative alignments the persistent loop wrote
+void tp_location_features(const float* CUM, const float* Kc, const float* bc, int B, int T, int Tin, float* FALL,
+                          hipStream_t s);
 
 }  // namespace tt2

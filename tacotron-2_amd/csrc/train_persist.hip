@@ -37,19 +37,6 @@
 // the host reports the phase.
 #include "train_persist.h"
 
-#ifndef TP_V_ASMLD
-#define TP_V_ASMLD 1
-#endif
-#ifndef TP_V_BST
-#define TP_V_BST 1
-#endif
-#ifndef TP_V_ZMBUF
-#define TP_V_ZMBUF 1
-#endif
-#ifndef TP_V_AGPR
-#define TP_V_AGPR 1
-#endif
-
 namespace tt2 {
 
 typedef __bf16 tp_bf8 __attribute__((ext_vector_type(8)));
@@ -71,25 +58,34 @@ static_assert(TP_KSW % 4 == 0 && TP_PKW >= 1 && TP_H == 1024 && TP_D == 1024, "t
 
 // LDS layout (floats)
 constexpr int TP_KW = 31;                       // attention_kernel (fork default; tr_persist_fits)
-constexpr int TP_JB = TP_TMAX / 8;              // encoder positions per row group (8 groups of 32 lanes)
 constexpr int TPL_RED = 0;                      // [TP_NW waves][64][16] partial gate tiles
-constexpr int TPL_OC1 = TPL_RED + TP_NW * 1024; // [64][16] off-chain LSTM-1 terms of the next step
-constexpr int TPL_OC2 = TPL_OC1 + 1024;         // [64][16] off-chain LSTM-2 terms
-constexpr int TPL_WQ = TPL_OC2 + 1024;          // query columns of this quarter as bf16 B fragments
-constexpr int TPL_F = TPL_WQ + TP_H * 32 / 2;   // [TMAX][32] location features
-constexpr int TPL_CW = TPL_F + TP_TMAX * 32;    // [15 + TMAX + 17 + 16] cumulative alignments, zero padded
-constexpr int TPL_KC = TPL_CW + TP_TMAX + 48;   // [32 taps][32] location conv kernel (zero padded)
-constexpr int TPL_WL = TPL_KC + 32 * 32;        // [F][32] location_features_layer columns of this quarter
-constexpr int TPL_QP = TPL_WL + TP_F * 32;      // [TP_NW][32] query partials
+constexpr int TPL_WQ = TPL_RED + TP_NW * 1024;  // query columns of this quarter as bf16 B fragments
+constexpr int TPL_CW = TPL_WQ + TP_H * 32 / 2;  // [15 + TMAX + 17 + 16] cumulative alignments, zero padded
+constexpr int TPL_QP = TPL_CW + TP_TMAX + 48;   // [TP_NW][32] query partials
 constexpr int TPL_QV = TPL_QP + TP_NW * 32;     // [32] q + b_a
 constexpr int TPL_EP = TPL_QV + 32;             // [TMAX] this quarter's energy partials
 constexpr int TPL_AL = TPL_EP + TP_TMAX;        // [TMAX] energies -> alignments (zero past T_in)
 constexpr int TPL_CR = TPL_AL + TP_TMAX;        // [TP_VG][256] context partials
 constexpr int TPL_SC = TPL_CR + TP_VG * 256;    // [16] reduction scratch, then ints
 constexpr int TPL_END = TPL_SC + 32;
-static_assert(TP_TMAX % 32 == 0 && TP_VG == 2, "train_persist attention geometry");
+static_assert(TP_TMAX % 64 == 0 && TP_TMAX <= TP_NT && TP_VG == 2, "train_persist attention geometry");
 
 size_t tp_lds_bytes() { return sizeof(float) * (size_t)TPL_END; }
+
+// constant address space: uniform reads of kernel-lifetime constants become scalar (s_load) reads
+typedef const __attribute__((address_space(4))) float tp_cf;
+__device__ __forceinline__ tp_cf* tp_const(const float* p) { return (tp_cf*)(p); }
+
+// branch-free tanh (tanhf's two paths diverge per lane): odd Taylor polynomial below |x| = 1/16
+// (truncation < 2e-13), (1 - e) / (1 + e) with e = exp(-2|x|) above (the subtraction exact, the result
+// within ~1e-6 relative); the sign restored by copysign
+__device__ __forceinline__ float tp_tanh(float x) {
+  const float ax = fabsf(x), x2 = x * x;
+  const float p = x * (1.f + x2 * (-1.f / 3.f + x2 * (2.f / 15.f + x2 * (-17.f / 315.f))));
+  const float e = __expf(-2.f * ax);
+  const float r = copysignf(__fdividef(1.f - e, 1.f + e), x);
+  return ax < 0.0625f ? p : r;
+}
 
 __device__ __forceinline__ float tp_sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float tp_lo(unsigned v) { return __uint_as_float(v << 16); }
@@ -101,17 +97,11 @@ __device__ __forceinline__ unsigned tp_pack(float lo, float hi) {
 // explicit AGPR residency for the per-row constants the attention reads once per step (keys, the
 // values quarter): the VGPRs stay free for the LSTM products' fragments in flight
 __device__ __forceinline__ float tp_aput(float v) {
-#if !TP_V_AGPR
-  return v;
-#endif
   float r;
   asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(r) : "v"(v));
   return r;
 }
 __device__ __forceinline__ float tp_aget(float r) {
-#if !TP_V_AGPR
-  return r;
-#endif
   float v;
   asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(r));
   return v;
@@ -124,10 +114,6 @@ __device__ __forceinline__ auto tp_rsrc(const void* p) {
 // plain buffer store / load of one dword: per-lane byte offset + uniform byte offset (no per-lane
 // 64-bit addresses in the step loop, where the compiler would keep one per store site alive)
 __device__ __forceinline__ void tp_bst(const void* base, int vbyte, int sbyte, float v) {
-#if !TP_V_BST
-  *reinterpret_cast<float*>(reinterpret_cast<char*>(const_cast<void*>(base)) + vbyte + sbyte) = v;
-  return;
-#endif
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), tp_rsrc(base), vbyte, sbyte, 0);
 }
 __device__ __forceinline__ void tp_st8(void* base, int byte_off, tp_u2 v) {
@@ -183,28 +169,27 @@ __device__ __forceinline__ void tp_put_tiles(float* red, const tp_f4 (&acc)[4], 
 
 // 16-byte buffer load issued by inline asm: the compiler schedules at most two of its own loads
 // ahead of their MFMAs here (measured: one round trip per fragment), so a batch of fragments is
-// issued back to back and waited for once (tp_wait), one L2 round trip per batch
+// issued back to back and waited for once (tp_wait), one L2 round trip per batch.  The compiler's
+// hazard recognizer does not see into the asm: an soffset / resource SGPR it has just reloaded
+// from a spill lane (v_readlane, a VALU write of an SGPR) needs 5 wait states before a VMEM
+// instruction reads it, hence the s_nop 4 in front of every load (without it the load reads the
+// stale SGPR: a wrong offset, measured as a device fault)
 template <bool SC1>
 __device__ __forceinline__ tp_bf8 tp_ldx4(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
   tp_bf8 r;
-#if !TP_V_ASMLD
-  return __builtin_bit_cast(tp_bf8, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, SC1 ? 16 : 0));
-#endif
   if constexpr (SC1)
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen sc1" : "=v"(r) : "v"(vo), "s"(rs), "s"(so) : "memory");
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen sc1" : "=v"(r) : "v"(vo), "s"(rs), "s"(so) : "memory");
   else
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(r) : "v"(vo), "s"(rs), "s"(so) : "memory");
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(r) : "v"(vo), "s"(rs), "s"(so) : "memory");
   return r;
 }
 // wait for every load of the batch; the fragments pass through as operands so no use is scheduled
 // above the wait
 template <int N>
 __device__ __forceinline__ void tp_wait(tp_bf8 (&f)[N]) {
-#if TP_V_ASMLD
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int i = 0; i < N; ++i) asm volatile("" : "+v"(f[i]));
-#endif
 }
 
 // acc[mt] += X[rows of tile mt][k-steps ks0 .. ks0 + N) · W (B fragments wf[0..N)), X a [64][K]
@@ -288,13 +273,8 @@ __device__ __forceinline__ float tp_block_sum(float v, float* scr) {
 __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* const red = sm + TPL_RED;
-  float* const oc1 = sm + TPL_OC1;
-  float* const oc2 = sm + TPL_OC2;
   tp_bf8* const wqf = reinterpret_cast<tp_bf8*>(sm + TPL_WQ);
-  float* const fs = sm + TPL_F;
   float* const cw = sm + TPL_CW;
-  float* const kcs = sm + TPL_KC;
-  float* const wls = sm + TPL_WL;
   float* const qps = sm + TPL_QP;
   float* const qv = sm + TPL_QV;
   float* const ep = sm + TPL_EP;
@@ -302,7 +282,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
   float* const cr = sm + TPL_CR;
   float* const scr = sm + TPL_SC;
   int* const sfail = reinterpret_cast<int*>(sm + TPL_SC + 16);
-  constexpr int H = TP_H, P = TP_P, D = TP_D, A = TP_A, LX1 = TP_LX1, TM = TP_TMAX, JB = TP_JB;
+  constexpr int H = TP_H, P = TP_P, D = TP_D, A = TP_A, LX1 = TP_LX1, TM = TP_TMAX;
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: offsets live in SGPRs
   const int B = a.B, T = a.T, Tin = a.Tin;
@@ -335,17 +315,36 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
   float c1 = 0.f, hz1 = 0.f, c2 = 0.f, hz2 = 0.f;
   const int evo = er * H + en;  // (row, unit) element offset in the [B][H] planes
 
-  // ---- attention row constants.  Thread (aa = tid & 31, grp = tid >> 5): attention dim / filter aa
-  // of this quarter, encoder positions [JB grp, JB grp + JB) (location features, energies); context:
-  // channel pair vcp, positions [TM/2 vg, TM/2 vg + TM/2)
-  const int aa = tid & 31, grp = tid >> 5, adim = 32 * sib + aa;
+  // ---- attention row constants.  Energies as v_mfma_f32_16x16x4f32 tiles of U^T = KW^T·C^T (dims x
+  // positions, C the cum Toeplitz): wave w owns the position tiles nt = w + 4r, lane l the position
+  // 16 nt + (l & 15) and the dims 16 mt + 4 (l >> 4) + i of both dim tiles mt.  Context: channel pair
+  // vcp, positions [TM/2 vg, TM/2 vg + TM/2)
   const int vcp = tid & 127, vg = tid >> 7;
-  float key[JB];          // AGPRs: keys[rb][JB grp + i][adim]
+  const int jl = lane & 15, g4 = lane >> 4;
+  constexpr int NTW = TM / 16 / TP_NW;  // position tiles per wave
+  float key[NTW * 8];     // AGPRs: keys[rb][16 (w + 4 r) + jl][32 sib + 16 mt + 4 g4 + i] at [8 r + 4 mt + i]
   float vals[TM / 2];     // AGPRs: bf16 pairs of values16[rb][TM/2 vg + i][256 sib + 2 vcp]
+  float kwa[16];          // A fragments: KW^T[32 sib + 16 mt + jl][4 ks + g4] at [8 mt + ks] (tap 31 -> 0)
+  float vav[8];           // v_a of the lane's dims [4 mt + i]
 #pragma unroll
-  for (int i = 0; i < JB; ++i) {
-    const int j = JB * grp + i;
-    key[i] = tp_aput((arow && j < Tin) ? a.keys[((long)rb * Tin + j) * A + adim] : 0.f);
+  for (int r = 0; r < NTW; ++r) {
+    const int j = 16 * (w + 4 * r) + jl;
+    const bool kj = arow && j < Tin;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const tp_f4 v = kj ? *reinterpret_cast<const tp_f4*>(a.keys + ((long)rb * Tin + j) * A + 32 * sib + 16 * mt + 4 * g4)
+                         : tp_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) key[8 * r + 4 * mt + i] = tp_aput(v[i]);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      kwa[8 * mt + ks] = (4 * ks + g4 < TP_KW) ? a.KWT[(32 * sib + 16 * mt + jl) * 32 + 4 * ks + g4] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vav[4 * mt + i] = a.va[32 * sib + 16 * mt + 4 * g4 + i];
   }
 #pragma unroll
   for (int i = 0; i < TM / 2; ++i) {
@@ -355,12 +354,10 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
                            : 0u;
     vals[i] = tp_aput(__uint_as_float(v));
   }
-  float vav = 0.f, bav = 0.f, bcv = 0.f;
+  // q-side constant of dim tid < 32: b_a + bc·W_loc (the location conv's bias through W_loc)
+  const float qbias = (arow && tid < 32) ? a.ba[32 * sib + tid] + a.KWT[(32 * sib + tid) * 32 + 31] : 0.f;
   int len = 0;
   if (arow) {
-    vav = a.va[adim];
-    bav = a.ba[adim];
-    bcv = a.bc[aa];
     len = a.lens[rb];
     // query columns as B fragments: k-step ks, column tile nt, lane l holds
     // Wq[32 ks + 8 (l >> 4) + e][32 sib + 16 nt + (l & 15)], e < 8
@@ -372,48 +369,32 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
       for (int k = 0; k < 8; ++k) v[k] = src[(long)k * A];
       wqf[e] = v;
     }
-    for (int e = tid; e < 32 * 32; e += TP_NT) kcs[e] = (e >> 5) < TP_KW ? a.Kc[(e >> 5) * TP_F + (e & 31)] : 0.f;
-    for (int e = tid; e < TP_F * 32; e += TP_NT) wls[e] = a.Wl[(e >> 5) * A + 32 * sib + (e & 31)];
   }
   for (int e = tid; e < TM + 48; e += TP_NT) cw[e] = 0.f;
   for (int e = tid; e < TM; e += TP_NT) al[e] = 0.f;
   if (tid == 0) sfail[0] = 0;
 
-  // ---- off-chain products: wave partials -> red, summed into dst[64][16]
-  auto reduce_into = [&](float* dst, const tp_f4 (&acc)[4]) {
-    tp_put_tiles(red, acc, w, lane);
-    __syncthreads();
-    for (int e = tid; e < 1024; e += TP_NT) {
-      float s = red[e];
-#pragma unroll
-      for (int ww = 1; ww < TP_NW; ++ww) s += red[ww * 1024 + e];
-      dst[e] = s;
-    }
-    __syncthreads();
+  // ---- off-chain products, accumulated per wave in registers between the chain's waits and added to
+  // the wave's chain partial tiles (so the cell's sum over the waves covers both):
+  //   ao1 = prenet_{t+1}·W1p (after CTX(t) is published) + hz1_t·W1h (after H2(t) is published)
+  //   ao2 = hz2_t·W2h (while the energy partials of step t travel)
+  tp_f4 ao1[4] = {}, ao2[4] = {};
+  auto prenet_part = [&](int tn) {  // prenet_tn·W1p, k-steps [TP_PKW w, TP_PKW (w + 1)) of the prenet rows
+    tp_mfma_stream<TP_PKW, false>(ao1, a.preh + (long)tn * 64 * P, P, TP_PKW * w, a.K1T, wvo1, 32 * TP_PKW * w, lane);
   };
-  // LSTM-1 terms of step tn: prenet_tn·W1p (+ hz1_{tn-1}·W1h, parity (tn-1) & 1)
-  auto offchain1 = [&](int tn) {
-    tp_f4 acc[4] = {};
-    tp_mfma_stream<TP_PKW, false>(acc, a.preh + (long)tn * 64 * P, P, TP_PKW * w, a.K1T, wvo1, 32 * TP_PKW * w, lane);
-    if (tn > 0) {
-#pragma unroll
-      for (int c = 0; c < TP_KSW; c += 4)
-        tp_mfma_stream<4, true>(acc, a.Z1X + (long)((tn - 1) & 1) * 64 * H, H, TP_KSW * w + c, a.K1T, wvo1,
-                                P + D + wk0 + 32 * c, lane);
-    }
-    reduce_into(oc1, acc);
-  };
-  // LSTM-2 terms of step tn: hz2_{tn-1}·W2h
-  auto offchain2 = [&](int tn) {
-    tp_f4 acc[4] = {};
+  auto hz1_part = [&](int t0) {  // hz1_t0·W1h, this wave's k-range (the producers its L2 wait covered)
 #pragma unroll
     for (int c = 0; c < TP_KSW; c += 4)
-      tp_mfma_stream<4, true>(acc, a.Z2X + (long)((tn - 1) & 1) * 64 * H, H, TP_KSW * w + c, a.K2T, wvo2, H + wk0 + 32 * c,
+      tp_mfma_stream<4, true>(ao1, a.Z1X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w + c, a.K1T, wvo1, P + D + wk0 + 32 * c,
                               lane);
-    reduce_into(oc2, acc);
   };
-  offchain1(0);  // hz1_{-1} = 0
-  for (int e = tid; e < 1024; e += TP_NT) oc2[e] = 0.f;
+  auto hz2_part = [&](int t0) {  // hz2_t0·W2h, this wave's k-range (the producers its H2 wait covered)
+#pragma unroll
+    for (int c = 0; c < TP_KSW; c += 4)
+      tp_mfma_stream<4, true>(ao2, a.Z2X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w + c, a.K2T, wvo2, H + wk0 + 32 * c,
+                              lane);
+  };
+  prenet_part(0);  // hz1_{-1} = hz2_{-1} = 0
   __syncthreads();
 
   // one LSTM layer's epilogue for thread (er, eu): gates = bias + off-chain + Σ wave partials
@@ -421,7 +402,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
   struct Cell {
     float si, tj, sf, so, cn, hn, cz, hz;
   };
-  auto cell = [&](const float* oc, const float (&bias)[4], float cp, float hp, float kc, float kh) {
+  auto cell = [&](const float (&bias)[4], float cp, float hp, float kc, float kh) {
     float pre[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -429,7 +410,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
       float s = red[ci];
 #pragma unroll
       for (int ww = 1; ww < TP_NW; ++ww) s += red[ww * 1024 + ci];
-      pre[q] = bias[q] + (oc[ci] + s);
+      pre[q] = bias[q] + s;
     }
     Cell o;
     o.si = tp_sigm(pre[0]);
@@ -476,35 +457,28 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
     if (erow && a.zm) {
       const auto rz = tp_rsrc(a.zm + (long)t * 4 * B * H);
       const int zs = B * H;
-#if !TP_V_ZMBUF
-      const uint8_t* zp = a.zm + (long)t * 4 * B * H + evo;
-      kc1 = (float)zp[0];
-      kh1 = (float)zp[zs];
-      kc2 = (float)zp[2 * zs];
-      kh2 = (float)zp[3 * zs];
-      (void)rz;
-#else
       kc1 = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 0, 0);
       kh1 = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, zs, 0);
       kc2 = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 2 * zs, 0);
       kh2 = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 3 * zs, 0);
-#endif
     }
     // ================= L1: ctx_{t-1}·W1c (wave w: context k of quarter (TP_KSW w) / 8)
     {
-      tp_f4 acc[4] = {};
+      tp_f4 acc[4] = {ao1[0], ao1[1], ao1[2], ao1[3]};
       if (t > 0) {
         if (!tp_poll(a, TP_PH_CTX, 64 * ((TP_KSW * w) >> 3), B, tag - 1u)) sfail[0] = 1;
         TP_STAMP(1);
         tp_mfma_seg(acc, a.CX + (long)((t - 1) & 1) * 64 * D, D, TP_KSW * w, w1c, lane);
       }
       tp_put_tiles(red, acc, w, lane);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) ao1[mt] = tp_f4{0.f, 0.f, 0.f, 0.f};
       TP_STAMP(2);
       __syncthreads();
       TP_STAMP(3);
       if (sfail[0]) return;
       Cell o{};
-      if (eth) o = cell(oc1, bias1, c1, hz1, kc1, kh1);
+      if (eth) o = cell(bias1, c1, hz1, kc1, kh1);
       xstore(a.H1X, o.hn, o.hz, a.Z1X, par);
       tp_publish(a, TP_PH_H1, tag);
       TP_STAMP(4);
@@ -526,16 +500,18 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
     }
     // ================= L2: h1_t·W2i (wave w: k-steps [TP_KSW w, TP_KSW (w+1)) = producers [8 TP_KSW w, ..))
     {
-      tp_f4 acc[4] = {};
+      tp_f4 acc[4] = {ao2[0], ao2[1], ao2[2], ao2[3]};
       if (!tp_poll(a, TP_PH_H1, 8 * TP_KSW * w, 8 * TP_KSW, tag)) sfail[0] = 1;
       TP_STAMP(5);
       tp_mfma_seg(acc, a.H1X + (long)par * 64 * H, H, TP_KSW * w, w2i, lane);
       tp_put_tiles(red, acc, w, lane);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) ao2[mt] = tp_f4{0.f, 0.f, 0.f, 0.f};
       TP_STAMP(6);
       __syncthreads();
       if (sfail[0]) return;
       Cell o{};
-      if (eth) o = cell(oc2, bias2, c2, hz2, kc2, kh2);
+      if (eth) o = cell(bias2, c2, hz2, kc2, kh2);
       xstore(a.H2X, o.hn, o.hz, a.Z2X, par);
       tp_publish(a, TP_PH_H2, tag);
       TP_STAMP(7);
@@ -555,25 +531,30 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
         hz2 = o.hz;
       }
     }
+    const bool more = t + 1 < T;
+    // off-chain LSTM-1 term hz1_t·W1h of step t+1 while the other work-groups' h2 travel
+    if (more) hz1_part(t);
+    TP_STAMP(9);
     // ================= H2 of every producer (wave w polls its 8 TP_KSW producers), then the attention row
     if (!tp_poll(a, TP_PH_H2, 8 * TP_KSW * w, 8 * TP_KSW, tag)) sfail[0] = 1;
     __syncthreads();
     TP_STAMP(8);
     if (sfail[0]) return;
-    const bool more = t + 1 < T;
     if (arow) {
       {  // query quarter = bf16(h2 row) · bf16(Wq columns), v_mfma_f32_16x16x32_bf16 with the row in
-         // A-row 0 (lanes l & 15 == 0), wave w over k-steps [8w, 8w+8), 2 column tiles
+         // A-row 0 (lanes l & 15 == 0), wave w over k-steps [8w, 8w+8), 2 column tiles; the 8 row
+         // fragments in flight at once (one round trip)
         tp_f4 qa[2] = {};
         const auto rs = tp_rsrc(a.H2X);
         const bool r0 = (lane & 15) == 0;
-        const int vo = r0 ? (int)(((long)par * 64 * H + tp_afl(rb, 8 * (lane >> 4), H)) * 2) : 0;
+        const int vo = (int)(((long)par * 64 * H + tp_afl(rb, 8 * (lane >> 4), H)) * 2);
         tp_bf8 hf[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          hf[i] = __builtin_bit_cast(tp_bf8, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (8 * w + i) * 1024, 16));
+        for (int i = 0; i < 8; ++i) hf[i] = tp_ldx4<true>(rs, vo, (8 * w + i) * 1024);
+        tp_wait(hf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
           if (!r0) hf[i] = tp_bf8{};
-        }
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -584,68 +565,67 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
           qps[w * 32 + 16 + lane] = qa[1][0];
         }
       }
-      {  // location features of positions [JB grp, JB grp + JB), filter aa: the tap window in registers
-        float kc[TP_KW], win[JB + TP_KW - 1];
-#pragma unroll
-        for (int tp = 0; tp < TP_KW; ++tp) kc[tp] = kcs[tp * 32 + aa];
-#pragma unroll
-        for (int i = 0; i < JB + TP_KW - 1; ++i) win[i] = cw[JB * grp + i];  // cw[15 + j] = cum[j], pad 15
-#pragma unroll
-        for (int jj = 0; jj < JB; ++jj) {
-          float f = bcv;
-#pragma unroll
-          for (int tp = 0; tp < TP_KW; ++tp) f += win[jj + tp] * kc[tp];
-          const int j = JB * grp + jj;
-          fs[j * 32 + aa] = f;
-          if (sib == 0 && j < Tin) tp_bst(a.FALL + ((long)t * B + rb) * Tin * TP_F, (JB * grp * TP_F + aa) * 4, jj * TP_F * 4, f);
-        }
-      }
       __syncthreads();
       TP_STAMP(10);
       if (tid < 32) {
         float q = qps[tid];
 #pragma unroll
         for (int i = 1; i < TP_NW; ++i) q += qps[i * 32 + tid];
-        qv[tid] = q + bav;
+        qv[tid] = q + qbias;
       }
       __syncthreads();
       TP_STAMP(11);
-      {  // energy partials of this quarter: e_j = Σ_{a in quarter} v_a·tanh(keys + q + b_a + f·W_loc)
-        const float qb = qv[aa];
-        float wl[TP_F];
-#pragma unroll
-        for (int c = 0; c < TP_F; ++c) wl[c] = wls[c * 32 + aa];
+      // energy partials of this quarter: e_j = Σ_a v_a tanh(u_ja), a over the quarter's 32 dims,
+      //   u_ja = keys_ja + q_a + b_a + Σ_c f_jc W_loc[c][a],  f_jc = bc_c + Σ_tap cum[j + tap - 15] Kc[tap][c]
+      // with the conv folded through W_loc: Σ_c f_jc W_loc[c][a] = Σ_tap cum[j + tap - 15] KW[a][tap] +
+      // (bc·W_loc)_a (the bias term is in qv).  U^T[a][j] = Σ_tap KW[a][tap] C[tap][j] on fp32 MFMA
+      // (exact fp32 products), C[tap][j] = cum[j + tap - 15] read straight from the zero-padded LDS
+      // copy.  The location features themselves (FALL, the backward's operand) are written after the loop.
+      {
         const float* thb = a.TH + ((long)t * B + rb) * Tin * A;  // this row's [Tin][A] block of step t
-        const auto rge = tp_rsrc(a.EX + (((long)par * 64 + rb) * 4 + sib) * TM);
+        const tp_f4 q0 = *reinterpret_cast<const tp_f4*>(qv + 4 * g4), q1 = *reinterpret_cast<const tp_f4*>(qv + 16 + 4 * g4);
 #pragma unroll
-        for (int i = 0; i < JB; ++i) {
-          const int j = JB * grp + i;
-          if (j < Tin) {
-            float u = tp_aget(key[i]) + qb;
-            const tp_f4* fr = reinterpret_cast<const tp_f4*>(fs + j * 32);
+        for (int r = 0; r < NTW; ++r) {
+          const int nt = w + 4 * r;
+          if (16 * nt >= Tin) break;  // wave-uniform
+          const int j = 16 * nt + jl;
+          float cb[8];
 #pragma unroll
-            for (int c4 = 0; c4 < 8; ++c4) {
-              const tp_f4 fv = fr[c4];
+          for (int ks = 0; ks < 8; ++ks) cb[ks] = cw[j + 4 * ks + g4];
+          tp_f4 acc[2] = {};
 #pragma unroll
-              for (int e = 0; e < 4; ++e) u += fv[e] * wl[4 * c4 + e];
+          for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+              acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(kwa[8 * mt + ks], cb[ks], acc[mt], 0, 0, 0);
+          float e = 0.f;
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const tp_f4 qq = mt ? q1 : q0;
+            tp_f4 th4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              th4[i] = tp_tanh(acc[mt][i] + tp_aget(key[8 * r + 4 * mt + i]) + qq[i]);
+              e += vav[4 * mt + i] * th4[i];
             }
-            const float th = tanhf(u);
-            tp_bst(thb, (JB * grp * A + adim) * 4, i * A * 4, th);
-            float e = vav * th;
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) e += __shfl_xor(e, o, 64);
-            if (aa == 0) {
-              ep[j] = e;
-              __builtin_amdgcn_raw_buffer_store_b64(tp_u2{__float_as_uint(e), tag}, rge, JB * grp * 8, i * 8, 16);
-            }
+            if (j < Tin)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tp_u4, th4), tp_rsrc(thb),
+                                                     (j * A + 32 * sib + 16 * mt + 4 * g4) * 4, 0, 0);
+          }
+          e += __shfl_xor(e, 16, 64);
+          e += __shfl_xor(e, 32, 64);
+          if (g4 == 0 && j < Tin) {
+            ep[j] = e;
+            __builtin_amdgcn_raw_buffer_store_b64(tp_u2{__float_as_uint(e), tag},
+                                                  tp_rsrc(a.EX + (((long)par * 64 + rb) * 4 + sib) * TM), j * 8, 0, 16);
           }
         }
       }
     }
     TP_STAMP(12);
-    // off-chain LSTM-1 terms of t+1 while the other quarters' energy partials travel
-    if (more) offchain1(t + 1);
-    else __syncthreads();  // the own partials in ep[] (offchain1's barriers order them otherwise)
+    // off-chain LSTM-2 term hz2_t·W2h of step t+1 while the other quarters' energy partials travel
+    if (more) hz2_part(t);
+    __syncthreads();  // the own partials in ep[]
     TP_STAMP(13);
     if (arow) {
       // take the other quarters' partials of energy j = tid (granules), sum in quarter order
@@ -730,8 +710,8 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
         tp_bst(a.X1 + (i + B) * LX1, (P + 256 * sib + tid) * 4, 0, ctx);
       }
     }
-    // off-chain LSTM-2 terms of t+1 (needed only after the next context)
-    if (more) offchain2(t + 1);
+    // off-chain LSTM-1 term prenet_{t+1}·W1p while the contexts travel
+    if (more) prenet_part(t + 1);
     TP_STAMP(18);
   }
 #undef TP_STAMP
@@ -744,6 +724,53 @@ __global__ void k_tp_prenet_rows(const float* __restrict__ X1, long ld, int B, i
     const int t = (int)(i / (64 * TP_P)), rem = (int)(i % (64 * TP_P)), r = rem / TP_P, k = rem % TP_P;
     preh[(long)t * 64 * TP_P + tp_afl(r, k, TP_P)] = r < B ? (__bf16)X1[((long)t * B + r) * ld + k] : (__bf16)0.f;
   }
+}
+
+__global__ __launch_bounds__(256) void k_tp_kwt(const float* __restrict__ Kc, const float* __restrict__ bc,
+                                                const float* __restrict__ Wl, float* __restrict__ KWT) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (a, tap)
+  if (i >= TP_A * 32) return;
+  const int a = i >> 5, tp = i & 31;
+  float acc = 0.f;
+  for (int c = 0; c < TP_F; ++c) acc += (tp < TP_KW ? Kc[tp * TP_F + c] : tp == 31 ? bc[c] : 0.f) * Wl[c * TP_A + a];
+  KWT[i] = acc;
+}
+
+void tp_prepare(const float* Kc, const float* bc, const float* Wl, float* KWT, hipStream_t s) {
+  hipLaunchKernelGGL(k_tp_kwt, dim3(TP_A * 32 / 256), dim3(256), 0, s, Kc, bc, Wl, KWT);
+  TT2_HIP(hipGetLastError());
+}
+
+// one thread per (step, row, position, filter): the 32 filters of a position are 32 adjacent lanes
+// (coalesced stores), the cum window is shared through L1
+__global__ __launch_bounds__(256) void k_tp_fall(const float* __restrict__ CUM, const float* __restrict__ Kc,
+                                                 const float* __restrict__ bc, long npos, int Tin,
+                                                 float* __restrict__ FALL) {
+  __shared__ float kcs[TP_KW * TP_F + TP_F];
+  for (int i = threadIdx.x; i < TP_KW * TP_F; i += blockDim.x) kcs[i] = Kc[i];
+  if (threadIdx.x < TP_F) kcs[TP_KW * TP_F + threadIdx.x] = bc[threadIdx.x];
+  __syncthreads();
+  constexpr int pad = (TP_KW - 1) / 2;
+  const long n = npos * TP_F;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i & (TP_F - 1));
+    const long pos = i >> 5;                   // (t, b) row-block * Tin + j
+    const int j = (int)(pos % Tin);
+    const float* cum = CUM + (pos - j);        // CUM[t][b][0..Tin)
+    float acc = kcs[TP_KW * TP_F + c];
+    for (int tp = 0; tp < TP_KW; ++tp) {
+      const int jj = j + tp - pad;
+      acc += ((jj >= 0 && jj < Tin) ? cum[jj] : 0.f) * kcs[tp * TP_F + c];
+    }
+    FALL[i] = acc;
+  }
+}
+
+void tp_location_features(const float* CUM, const float* Kc, const float* bc, int B, int T, int Tin, float* FALL,
+                          hipStream_t s) {
+  static_assert(TP_F == 32, "k_tp_fall: one lane per filter");
+  hipLaunchKernelGGL(k_tp_fall, dim3(4096), dim3(256), 0, s, CUM, Kc, bc, (long)T * B * Tin, Tin, FALL);
+  TT2_HIP(hipGetLastError());
 }
 
 void tp_prenet_rows(const float* X1, long ld, int B, int T, __bf16* preh, hipStream_t s) {
