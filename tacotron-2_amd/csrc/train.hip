@@ -63,7 +63,8 @@ struct tt2_train_ctx {
   // backward
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
-  DevBuf DF2, DCUM2, PQ2, SC2;  // k_tr_att_bwd_q: df / d cum / d query / Σ a·d cum partials by step parity
+  DevBuf DF2, DCUM2, PQ2, SC2;
+  DevBuf DWG;  // [32][A] k_tr_dwloc_cum: Σ cum_{t-1}·du per tap (+ the Σ du row)  // k_tr_att_bwd_q: df / d cum / d query / Σ a·d cum partials by step parity
   DevBuf TH, E, DF, PQ, FALL, ALN;
   // the large plain products (tr_gemm_big)
   DevBuf blasA, blasB, blasP;  // gemm_bf16_kc: bf16 operand copies, split-K partials
@@ -116,7 +117,7 @@ struct tt2_train_ctx {
   std::vector<uint8_t> feed;
   // free-running steps: prenet-1 kernel transposed [P][NM], per-step scratch
   DevBuf W1T, sDZ, sDP, sDX;
-  // persistent forward (train_persist.hip; opt-in with TT2_TR_PERSIST=1, else the per-step launches): exchange
+  // persistent forward (train_persist.hip; TT2_TR_PERSIST=0 keeps the per-step launches): exchange
   // buffers, energy granules, flags + control words, the prenet rows in bf16 fragment layout
   DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps, tpKWT;
   bool tp_on = false, tp_last = false, tp_check = false;
@@ -1639,67 +1640,87 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
   if (stp) stp[i] = __builtin_amdgcn_s_memrealtime()
   TRQ_STAMP(0);
   const long pt = (long)b * a.nt + q;
-  // ---- the own rows' values (bf16 step) and tanh / d keys rows first: their round trip overlaps the
-  // staging and the d cum phase (wave w: rows jr = w + NW u; nown <= NW·TRQ_RB)
-  typedef unsigned trq_u4 __attribute__((ext_vector_type(4)));
-  const bool v16 = a.values16 && (a.D & 7) == 0;
-  trq_u4 vv[TRQ_RB][2];
-  float t0[TRQ_RB], t1[TRQ_RB], e0[TRQ_RB], e1[TRQ_RB];
-#pragma unroll
-  for (int u = 0; u < TRQ_RB; ++u) {
-    const int jr = w + NW * u;
-    const bool ok = jr < nown;
-    const trq_u4* v8 = reinterpret_cast<const trq_u4*>(a.values16 + ((long)b * Tin + j0 + (ok ? jr : 0)) * D);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      vv[u][i] = (v16 && ok && (lane + 64 * i) * 8 < D) ? v8[lane + 64 * i] : trq_u4{0u, 0u, 0u, 0u};
-    const long hrow = (tb * Tin + j0 + (ok ? jr : 0)) * A, krow = ((long)b * Tin + j0 + (ok ? jr : 0)) * A;
-    t0[u] = ok ? a.TH[hrow + k0] : 0.f;
-    t1[u] = ok ? a.TH[hrow + k1] : 0.f;
-    e0[u] = ok ? a.DKEYS[krow + k0] : 0.f;
-    e1[u] = ok ? a.DKEYS[krow + k1] : 0.f;
-  }
   // ---- staging: every load of the prologue in flight at once (16-byte loads where the rows allow)
   const trq_f4 zf4 = {0.f, 0.f, 0.f, 0.f};
+  // every load below is unconditional (clamped address, the value selected afterwards): a load under a
+  // branch makes the wait-count pass fall back to vmcnt(0) at the join, serialising the round trips
   const bool d4ok = tid * 4 < D;  // host: D % 4 == 0, D <= 1024
+  const int n4 = d4ok ? 4 * tid : 0;
   const long ofs_p = tb * (a.H + D) + a.H, ofs_x = (tb + a.B) * (a.P + D + a.H) + a.P;
-  const trq_f4 xp = d4ok ? *reinterpret_cast<const trq_f4*>(a.dPIN + ofs_p + 4 * tid) : zf4;
-  const trq_f4 xx = d4ok ? *reinterpret_cast<const trq_f4*>(a.dX1 + ofs_x + 4 * tid) : zf4;
-  const trq_f4 xc = d4ok ? *reinterpret_cast<const trq_f4*>(a.PIN + ofs_p + 4 * tid) : zf4;
+  trq_f4 xp = *reinterpret_cast<const trq_f4*>(a.dPIN + ofs_p + n4);
+  trq_f4 xx = *reinterpret_cast<const trq_f4*>(a.dX1 + ofs_x + n4);
+  trq_f4 xc = *reinterpret_cast<const trq_f4*>(a.PIN + ofs_p + n4);
   trq_f4 wlv[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) wlv[u] = reinterpret_cast<const trq_f4*>(a.Wl)[tid + TRQ_NT * u];
-  const trq_f4 kcv = tid < KW * F / 4 ? reinterpret_cast<const trq_f4*>(a.Kc)[tid] : zf4;
+  trq_f4 kcv = reinterpret_cast<const trq_f4*>(a.Kc)[min(tid, KW * F / 4 - 1)];
   constexpr int NH = (HR * F / 4 + TRQ_NT - 1) / TRQ_NT;
   trq_f4 dfv[NH];
+  bool dfok[NH];
   const float* dfrow = z.df_in + (long)b * Tin * F;
 #pragma unroll
   for (int u = 0; u < NH; ++u) {
     const int i4 = tid + TRQ_NT * u, r = i4 / (F / 4), j = j0 - PAD - 1 + r;
-    dfv[u] = (i4 < HR * F / 4 && j >= 0 && j < Tin) ? reinterpret_cast<const trq_f4*>(dfrow + (long)j * F)[i4 % (F / 4)]
-                                                    : zf4;
+    dfok[u] = i4 < HR * F / 4 && j >= 0 && j < Tin;
+    dfv[u] = reinterpret_cast<const trq_f4*>(dfrow + (long)(dfok[u] ? j : 0) * F)[i4 % (F / 4)];
   }
-  const float aln_v = tid < Tin ? a.ALN[tb * Tin + tid] : 0.f;
-  const float dci_v = tid < Tin ? z.dcum_in[(long)b * Tin + tid] : 0.f;
+  const int tc = min(tid, Tin - 1);
+  float aln_v = a.ALN[tb * Tin + tc];
+  float dci_v = z.dcum_in[(long)b * Tin + tc];
   const int jc = j0 + tid - PAD;
   const bool hal = tid < RQX + 32 && jc >= 0 && jc < Tin;
-  const float cs_v = hal ? a.CUM[tb * Tin + jc] : 0.f;
-  const float an_v = (hal && a.t > 0) ? a.ALN[(tb - a.B) * Tin + jc] : 0.f;
-  float scv = 0.f;
+  const int jcc = hal ? jc : 0;
+  float cs_v = a.CUM[tb * Tin + jcc];
+  float an_v = a.ALN[(a.t > 0 ? tb - a.B : tb) * Tin + jcc];
+  float scp[4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) scv += g < nq ? z.sc_in[(long)b * 4 + g] : 0.f;
-  const float odv = tid < A ? a.dV[pt * A + tid] : 0.f, odb = tid < A ? a.dBA[pt * A + tid] : 0.f;
-  const float obc = tid < F ? a.dBC[pt * F + tid] : 0.f;
+  for (int g = 0; g < 4; ++g) scp[g] = z.sc_in[(long)b * 4 + min(g, nq - 1)];
+  const int ta = min(tid, A - 1), tf = min(tid, F - 1);
+  float odv = a.dV[pt * A + ta], odb = a.dBA[pt * A + ta];
+  float obc = a.dBC[pt * F + tf];
   // the d Kc slot entries of this lane's MFMA output (wave w < 4: tap tile w >> 1, filter tile w & 1)
   const int kt0 = 16 * (w >> 1) + 4 * g4, kcc = 16 * (w & 1) + jl;
   float okc[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) okc[i] = kt0 + i < KW ? a.dKC[pt * KW * F + (kt0 + i) * F + kcc] : 0.f;
+  for (int i = 0; i < 4; ++i) okc[i] = a.dKC[pt * KW * F + min(kt0 + i, KW - 1) * F + kcc];
   // d query of step t + 1 = the sum of that launch's partials (in range order), written by q == 0
   const bool dq_prev = q == 0 && tid < A && a.t + 1 < a.T;
   float pqv[4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) pqv[g] = (dq_prev && g < nq) ? z.pq_in[((long)b * a.nt + g) * A + tid] : 0.f;
+  for (int g = 0; g < 4; ++g) pqv[g] = z.pq_in[((long)b * a.nt + min(g, nq - 1)) * A + ta];
+  // ---- the own rows' values (bf16 step) and tanh / d keys rows, behind the staging loads: their round
+  // trip overlaps the d cum phase (wave w: rows jr = w + NW u, clamped to the last own row)
+  typedef unsigned trq_u4 __attribute__((ext_vector_type(4)));
+  const bool v16 = a.values16 && (a.D & 7) == 0;
+  trq_u4 vv[TRQ_RB][2];
+  float t0[TRQ_RB], t1[TRQ_RB], e0[TRQ_RB], e1[TRQ_RB];
+  if (nown > 0) {
+    const __bf16* vbase = v16 ? a.values16 : reinterpret_cast<const __bf16*>(a.values);  // any valid row
+#pragma unroll
+    for (int u = 0; u < TRQ_RB; ++u) {
+      const int jr = min(w + NW * u, nown - 1);
+      const trq_u4* v8 = reinterpret_cast<const trq_u4*>(vbase + ((long)b * Tin + j0 + jr) * D);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) vv[u][i] = v8[min(lane + 64 * i, D / 8 - 1)];
+      const long hrow = (tb * Tin + j0 + jr) * A, krow = ((long)b * Tin + j0 + jr) * A;
+      t0[u] = a.TH[hrow + k0];
+      t1[u] = a.TH[hrow + k1];
+      e0[u] = a.DKEYS[krow + k0];
+      e1[u] = a.DKEYS[krow + k1];
+    }
+  }
+  // the selections of the clamped loads
+  if (!d4ok) xp = xx = xc = zf4;
+  if (tid >= KW * F / 4) kcv = zf4;
+#pragma unroll
+  for (int u = 0; u < NH; ++u)
+    if (!dfok[u]) dfv[u] = zf4;
+  if (tid >= Tin) aln_v = dci_v = 0.f;
+  if (!hal) cs_v = 0.f;
+  if (!hal || a.t == 0) an_v = 0.f;
+  float scv = 0.f;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) scv += g < nq ? scp[g] : 0.f;
   // ---- LDS writes
   float sp = 0.f;
   if (d4ok) {
@@ -1773,7 +1794,7 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const unsigned x0 = vv[u][i][2 * h], x1 = vv[u][i][2 * h + 1];
-          const trq_f4 y = dc[2 * i + h];
+          const trq_f4 y = dc[2 * i + h];  // zero for channel chunks past D (the clamped loads' duplicates)
           acc += __uint_as_float(x0 << 16) * y[0] + __uint_as_float(x0 & 0xffff0000u) * y[1] +
                  __uint_as_float(x1 << 16) * y[2] + __uint_as_float(x1 & 0xffff0000u) * y[3];
         }
@@ -1974,6 +1995,57 @@ __global__ __launch_bounds__(256) void k_tr_dwloc(const float* __restrict__ f, c
       const int cr = (q & 3) + 8 * (q >> 2) + 4 * h;
       if (cr < F) P[(long)cr * A + k] = acc[q];
     }
+}
+
+// d W_loc without the location features: f = bc + conv(cum_{t-1}, Kc) is linear in Kc and bc, so
+//   d W_loc[c][a] = bc[c]·Σ_r du[r][a] + Σ_tap Kc[tap][c]·G[tap][a],  G[tap][a] = Σ_r cum_{t-1}[j + tap - pad]·du[r][a]
+// over all rows r = (t, b, j).  k_tr_dwloc's streaming fp32-MFMA pass with the A operand generated from
+// the cumulative alignments (rows tap < KW; row 31 = 1, the Σ du row): one read of du and no FALL
+// (T·B·T_in·F floats written by the forward, read back here).
+__global__ __launch_bounds__(256) void k_tr_dwloc_cum(const float* __restrict__ CUM, const float* __restrict__ du,
+                                                      long R, int Tin, int A, int KW, long rpb, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long r0 = (long)blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+  const int c = lane & 31, h = lane >> 5, k = 32 * w + (lane & 31);
+  const bool kok = k < A;
+  const int pad = (KW - 1) / 2;
+  tr_f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  int jb = (int)(r0 % Tin);  // position of row rb (one 64-bit remainder per work-group)
+  for (long rb = r0; rb < r1; rb += 32) {
+    float av[16], bv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const long rr = rb + 2 * u + h;
+      const bool ok = rr < r1;
+      int j = jb + 2 * u + h;
+      while (j >= Tin) j -= Tin;
+      const int jj = j + c - pad;
+      const bool cv = ok && c < KW && jj >= 0 && jj < Tin;
+      const float x = CUM[cv ? rr - j + jj : 0];
+      av[u] = cv ? x : (ok && c == 31 ? 1.f : 0.f);
+      bv[u] = (ok && kok) ? du[rr * A + k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+    jb += 32;
+    while (jb >= Tin) jb -= Tin;
+  }
+  float* P = part + (long)blockIdx.x * 32 * A;
+  if (kok)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) P[(long)((q & 3) + 8 * (q >> 2) + 4 * h) * A + k] = acc[q];
+}
+
+__global__ void k_tr_dwloc_fin(const float* __restrict__ G, const float* __restrict__ Kc, const float* __restrict__ bc,
+                               int F, int A, int KW, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F * A) return;
+  const int c = i / A, a = i % A;
+  float v = bc[c] * G[31 * A + a];
+  for (int tap = 0; tap < KW; ++tap) v += Kc[tap * F + c] * G[(long)tap * A + a];
+  out[i] = v;
 }
 
 // prenet backward through dropout + ReLU: dz = (p > 0) ? 2·dp : 0   (p = relu(z)/0.5·keep)
@@ -2482,7 +2554,7 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->dKC, B * NT * KW * F); f(c->dBC, B * NT * F); f(c->FALL, TB * Tin * F); f(c->ALN, TB * Tin);
   f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
   f(c->dZ, TB * P); f(c->dPre, TB * P);
-  f(c->DF2, 2 * B * Tin * F); f(c->DCUM2, 2 * B * Tin); f(c->PQ2, 2 * B * NT * A); f(c->SC2, 2 * B * 4);
+  f(c->DF2, 2 * B * Tin * F); f(c->DCUM2, 2 * B * Tin); f(c->PQ2, 2 * B * NT * A); f(c->SC2, 2 * B * 4); f(c->DWG, 32 * A);
   f(c->W1T, P * NM); f(c->sDZ, B * P); f(c->sDP, B * P); f(c->sDX, B * NM); c->TLEN.alloc(sizeof(int) * (size_t)B);
   const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM, TB * Tin * F,
                               // Postnet im2col^T: K·cin rows per position, cin = num_mels for layer 1
@@ -2679,6 +2751,16 @@ __global__ void k_tr_rank1_add(float* __restrict__ Y, long ld, const float* __re
   }
 }
 
+// d W_loc from the cumulative alignments (k_tr_dwloc_cum) instead of the stored location features:
+// the forward then skips FALL (TT2_TR_DWLOC_CUM=0: FALL + k_tr_dwloc)
+static bool tr_dwloc_cum_ok(const tt2_train_ctx* c) {
+  static const bool env = [] {
+    const char* e = std::getenv("TT2_TR_DWLOC_CUM");
+    return !(e && e[0] == '0');
+  }();
+  return env && c->KW <= 31 && c->F <= 32 && c->A <= 128;
+}
+
 // Persistent forward (train_persist.hip): fork widths (H 1024, prenet 256, memory 1024, attention 128
 // x 32 filters), B <= 64, T_in <= TP_TMAX, bf16 operands with the bf16 values copy, every step
 // teacher-forced (a step fed its own frame needs the frame projection inside the loop).
@@ -2729,7 +2811,7 @@ static void tr_persist_forward(tt2_train_ctx* c, const TrAtt& at, const uint8_t*
     a.stamps = c->tpStamps.as<long long>();
   }
   tp_launch(a, s);
-  tp_location_features(at.CUM, at.Kc, at.bc, c->B, T, Tin, at.FALL, s);
+  if (!tr_dwloc_cum_ok(c)) tp_location_features(at.CUM, at.Kc, at.bc, c->B, T, Tin, at.FALL, s);
   if (st) {
     std::vector<long long> h((size_t)TP_NB * 32);
     TT2_HIP(hipMemcpyAsync(h.data(), a.stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, s));
@@ -3149,7 +3231,19 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     // one streaming fp32-MFMA pass (k_tr_dwloc), partials [nbk][F·A] in TBUF: at most 512 blocks
     // and never more than TBUF holds (small T·B configurations have a small TBUF)
     const long cap = (long)(c->TBUF.bytes / sizeof(float)) / ((long)F * A);
-    if (F <= 32 && A <= 128 && cap >= 1) {
+    const long cap32 = (long)(c->TBUF.bytes / sizeof(float)) / (32L * A);
+    if (tr_dwloc_cum_ok(c) && cap32 >= 1) {
+      const long nb = std::min<long>(512, cap32);
+      const long rpb = ((R + nb - 1) / nb + 31) / 32 * 32;
+      const int nbk = (int)((R + rpb - 1) / rpb);
+      hipLaunchKernelGGL(k_tr_dwloc_cum, dim3(nbk), dim3(256), 0, s, c->CUM.as<float>(), c->TH.as<float>(), R, Tin, A, KW,
+                         rpb, TBUF);
+      tr_colsum(c, TBUF, nbk, 32 * A, 32L * A, c->DWG.as<float>(), s);
+      hipLaunchKernelGGL(k_tr_dwloc_fin, dim3((F * A + 255) / 256), dim3(256), 0, s, c->DWG.as<float>(),
+                         pvar(c, LAV("location_features_convolution/kernel")),
+                         pvar(c, LAV("location_features_convolution/bias")), F, A, KW,
+                         gvar(c, LAV("location_features_layer/kernel")));
+    } else if (F <= 32 && A <= 128 && cap >= 1) {
       const long nb = std::min<long>(512, cap);
       const long rpb = ((R + nb - 1) / nb + 31) / 32 * 32;
       const int nbk = (int)((R + rpb - 1) / rpb);
@@ -4106,7 +4200,7 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
     if (const char* e = std::getenv("TT2_TR_VALUES16")) c->values16_on = std::atoi(e) != 0;
     {
       const char* e = std::getenv("TT2_TR_PERSIST");
-      c->tp_on = e && e[0] == '1' && tp_device_ok(hip_device);
+      c->tp_on = !(e && e[0] == '0') && tp_device_ok(hip_device);
     }
     try {
       c->dev = hip_device;

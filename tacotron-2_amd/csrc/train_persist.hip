@@ -37,6 +37,12 @@
 // the host reports the phase.
 #include "train_persist.h"
 
+// 1: every LSTM weight fragment of the work-group's 16 gate columns register-resident (the off-chain
+// rows too: 72 more registers per lane); 0: the off-chain rows streamed from L2 / MALL each step
+#ifndef TP_RESIDENT_OFFCHAIN
+#define TP_RESIDENT_OFFCHAIN 1
+#endif
+
 namespace tt2 {
 
 typedef __bf16 tp_bf8 __attribute__((ext_vector_type(8)));
@@ -294,6 +300,9 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
   // chain weights (context rows of W1, h1 rows of W2) resident; the off-chain rows (prenet, zoned
   // h) are streamed by the off-chain products from L2 / MALL
   tp_bf8 w1c[TP_KSW], w2i[TP_KSW];
+#if TP_RESIDENT_OFFCHAIN
+  tp_bf8 w1h[TP_KSW], w2h[TP_KSW], w1p[TP_PKW];  // the off-chain rows too (zoned h of both layers, prenet)
+#endif
   const int wcol = (fn >> 2) * H + 4 * g + (fn & 3);
   const int wvo1 = (wcol * LX1 + fk) * 2, wvo2 = (wcol * 2 * H + fk) * 2;  // bytes (K1T / K2T < 2 GB)
   const int wk0 = 32 * TP_KSW * w;
@@ -301,7 +310,15 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
   for (int i = 0; i < TP_KSW; ++i) {
     w1c[i] = *reinterpret_cast<const tp_bf8*>(a.K1T + (long)wcol * LX1 + P + wk0 + 32 * i + fk);
     w2i[i] = *reinterpret_cast<const tp_bf8*>(a.K2T + (long)wcol * 2 * H + wk0 + 32 * i + fk);
+#if TP_RESIDENT_OFFCHAIN
+    w1h[i] = *reinterpret_cast<const tp_bf8*>(a.K1T + (long)wcol * LX1 + P + D + wk0 + 32 * i + fk);
+    w2h[i] = *reinterpret_cast<const tp_bf8*>(a.K2T + (long)wcol * 2 * H + H + wk0 + 32 * i + fk);
+#endif
   }
+#if TP_RESIDENT_OFFCHAIN
+#pragma unroll
+  for (int i = 0; i < TP_PKW; ++i) w1p[i] = *reinterpret_cast<const tp_bf8*>(a.K1T + (long)wcol * LX1 + 32 * TP_PKW * w + 32 * i + fk);
+#endif
   // LSTM epilogue thread (tid < 256): row er, unit en = 4g + eu; its cell state lives in registers
   static_assert(TP_NT >= 256, "one epilogue thread per (row, unit)");
   const int er = tid >> 2, eu = tid & 3, en = 4 * g + eu;
@@ -379,6 +396,17 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
   //   ao1 = prenet_{t+1}·W1p (after CTX(t) is published) + hz1_t·W1h (after H2(t) is published)
   //   ao2 = hz2_t·W2h (while the energy partials of step t travel)
   tp_f4 ao1[4] = {}, ao2[4] = {};
+#if TP_RESIDENT_OFFCHAIN
+  auto prenet_part = [&](int tn) {  // prenet_tn·W1p, k-steps [TP_PKW w, TP_PKW (w + 1)) of the prenet rows
+    tp_mfma_rows<TP_PKW, false>(ao1, a.preh + (long)tn * 64 * P, P, TP_PKW * w, w1p, lane);
+  };
+  auto hz1_part = [&](int t0) {  // hz1_t0·W1h, this wave's k-range (the producers its L2 wait covered)
+    tp_mfma_seg(ao1, a.Z1X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w, w1h, lane);
+  };
+  auto hz2_part = [&](int t0) {  // hz2_t0·W2h, this wave's k-range (the producers its H2 wait covered)
+    tp_mfma_seg(ao2, a.Z2X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w, w2h, lane);
+  };
+#else
   auto prenet_part = [&](int tn) {  // prenet_tn·W1p, k-steps [TP_PKW w, TP_PKW (w + 1)) of the prenet rows
     tp_mfma_stream<TP_PKW, false>(ao1, a.preh + (long)tn * 64 * P, P, TP_PKW * w, a.K1T, wvo1, 32 * TP_PKW * w, lane);
   };
@@ -394,6 +422,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
       tp_mfma_stream<4, true>(ao2, a.Z2X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w + c, a.K2T, wvo2, H + wk0 + 32 * c,
                               lane);
   };
+#endif
   prenet_part(0);  // hz1_{-1} = hz2_{-1} = 0
   __syncthreads();
 
