@@ -287,6 +287,10 @@ typedef struct tt2_wn_config {
   int gin_channels;        /* global conditioning width (<= 0: off, the fork default -1;
                               wavenet.py:152-158, modules.py:427-433, 505-509) */
   int n_speakers;          /* > 0: use_speaker_embedding, the gc_embedding table [n_speakers, gin] */
+  int input_type;          /* 0 'raw', 1 'mulaw' (scalar input), 2 'mulaw-quantize': one-hot input of
+                              quantize_channels classes and the softmax head sampled by tf.multinomial
+                              (wavenet.py:433-452, 861-867); out_channels must equal quantize_channels */
+  int quantize_channels;   /* 256 */
 } tt2_wn_config;
 
 typedef struct tt2_wn_ctx tt2_wn_ctx;
@@ -320,6 +324,17 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* ctx, const float* cond, int B, int T_f,
                            const float* u_mix, const float* u_log, uint64_t seed,
                            const float* teacher, float* wav_out, int32_t* mix_idx_out,
                            float* logits_out, float* upsampled_out);
+/* input_type 2 ('mulaw-quantize') through tt2_wn_generate / tt2_wn_generate_unconditional:
+ * u_log [T,B] carries the uniforms of tf.multinomial (u_mix unused), teacher [B,T] holds class
+ * indices (the one-hot test_inputs, wavenet.py:752-759), mix_idx_out the drawn classes, wav_out
+ * inv_mulaw_quantize of them, logits_out [B,T,quantize_channels]. */
+
+/* Unconditional synthesis (cin_channels <= 0, no local condition: wavenet.py:410-411 with
+ * synthesis_length T): T samples per row, the same sampler / teacher / output contract as
+ * tt2_wn_generate (the global condition still applies when gin_channels > 0). */
+tt2_status tt2_wn_generate_unconditional(tt2_wn_ctx* ctx, int B, int64_t T, const float* u_mix,
+                                         const float* u_log, uint64_t seed, const float* teacher,
+                                         float* wav_out, int32_t* mix_idx_out, float* logits_out);
 
 /* Same on DEVICE pointers, enqueued on `stream` (hipStream_t as void*).  cond_d is
  * CHANNELS-FIRST [B, cin, T_f] (the layout tt2_wn_cond_from_mels_dev writes; the reference

@@ -21,4 +21,5 @@ def wavenet_oracle_hp(hp):
                 freq_axis_kernel_size=hp.freq_axis_kernel_size, max_abs_value=hp.max_abs_value,
                 kernel_size=hp.kernel_size, upsample_type=hp.upsample_type,
                 upsample_activation=hp.upsample_activation, leaky_alpha=hp.leaky_alpha,
-                NN_init=hp.NN_init, log_scale_min_gauss=hp.log_scale_min_gauss)
+                NN_init=hp.NN_init, log_scale_min_gauss=hp.log_scale_min_gauss,
+                input_type=getattr(hp, "input_type", "raw"), quantize_channels=hp.quantize_channels)

@@ -183,23 +183,58 @@ def mol_sample(logits, u_mix, u_log, log_scale_min):
     return np.minimum(np.maximum(x, np.float32(-1)), np.float32(1)).astype(np.float32), k
 
 
-def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False, g=None):
-    """WaveNet.incremental (wavenet.py:724-911) for scalar ('raw') input, MoL or Gaussian head
-    (out_channels == 2: u_log carries the N(0,1) draws, u_mix is unused).
+def categorical_sample(logits, u):
+    """tf.multinomial(logits, 1) (wavenet.py:861-867 with softmax=False: the logits are the
+    unnormalised log-probabilities) with injected uniforms, restating TF's multinomial kernel: the
+    running total of exp(logit - max) in float64 over the finite logits (the cdf), then the first
+    class whose cdf exceeds u * total (std::upper_bound).  logits [N, Q]; u [N] (fp32 uniforms in
+    [0, 1)).  Returns k int32 [N]."""
+    lg = np.asarray(logits, np.float32).astype(np.float64)
+    u = np.asarray(u, np.float32).astype(np.float64)
+    fin = np.isfinite(lg)
+    mx = np.max(np.where(fin, lg, -np.inf), axis=1, keepdims=True)
+    e = np.where(fin, np.exp(lg - mx), 0.0)
+    cdf = np.cumsum(e, axis=1)
+    target = u * cdf[:, -1]
+    k = np.array([np.searchsorted(cdf[i], target[i], side="right") for i in range(lg.shape[0])])
+    return np.minimum(k, lg.shape[1] - 1).astype(np.int32)
+
+
+def inv_mulaw_quantize_f32(k):
+    """util.inv_mulaw_quantize on the synthesis graph's tensors (wavenet.py:450-452): float32
+    arithmetic, mu hard-coded to 255 (util.py:105-129)."""
+    mu = np.float32(255.0)
+    y = np.float32(2.0) * np.asarray(k, np.float32) / mu - np.float32(1.0)
+    return (np.sign(y) * (np.float32(1.0) / mu) * (np.power(np.float32(1.0) + mu, np.abs(y)) - np.float32(1.0))
+            ).astype(np.float32)
+
+
+def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False, g=None, T=None):
+    """WaveNet.incremental (wavenet.py:724-911) for scalar ('raw' / 'mulaw') input with the MoL or
+    Gaussian head (out_channels == 2: u_log carries the N(0,1) draws, u_mix is unused), or for
+    'mulaw-quantize' input (one-hot of quantize_channels classes, wavenet.py:433-446) with the
+    softmax head sampled by tf.multinomial (u_log [T, B] carries its uniforms; y is the sampled
+    class through inv_mulaw_quantize, k the class).  c_up None: unconditional synthesis of T samples
+    (no conv1x1c term, wavenet.py:410-411).
 
     c_up: upsampled conditioning [B, T, cin]; u_mix [T, B, nr_mix]; u_log [T, B];
     test_inputs [B, T] overrides next_input (wavenet.py:876-878); g: global condition -- speaker
     ids [B] (int: rows of WaveNet_model/gc_embedding, wavenet.py:770-773) or features [B, gin]
     (float) -- whose conv1x1g term joins both gate halves (modules.py:505-509).  Returns y [B, T] (float32),
     k [B, T] (int32) and, optionally, logits [B, T, out_channels]."""
-    c_up = np.asarray(c_up, np.float32)
-    B, T, _ = c_up.shape
+    quant = hp.get("input_type", "raw") == "mulaw-quantize"
+    if c_up is None:
+        B = np.asarray(u_log).shape[1] if test_inputs is None else np.asarray(test_inputs).shape[0]
+    else:
+        c_up = np.asarray(c_up, np.float32)
+        B, T, _ = c_up.shape
     L, stacks = hp["layers"], hp["stacks"]
     per = L // stacks
     R = hp["residual_channels"]
     legacy, res_legacy = hp.get("legacy", False), hp.get("residual_legacy", False)
     kw = hp.get("kernel_size", 3)
-    first_k = _w(W, "input_convolution/kernel").reshape(1, R)
+    Q = hp.get("quantize_channels", 256) if quant else 1
+    first_k = _w(W, "input_convolution/kernel").reshape(Q, R)
     first_b = _w(W, "input_convolution/bias")
     if g is not None:
         g = np.asarray(g)
@@ -213,8 +248,8 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
         layers.append(dict(
             d=2 ** (l % per),
             k=_w(W, cs + "kernel").reshape(kw * R, -1), b=_w(W, cs + "bias"),
-            kc=_w(W, s + "residual_block_cin_conv_ResidualConv1DGLU_{}/kernel".format(l))[0],
-            bc=_w(W, s + "residual_block_cin_conv_ResidualConv1DGLU_{}/bias".format(l)),
+            kc=None if c_up is None else _w(W, s + "residual_block_cin_conv_ResidualConv1DGLU_{}/kernel".format(l))[0],
+            bc=None if c_up is None else _w(W, s + "residual_block_cin_conv_ResidualConv1DGLU_{}/bias".format(l)),
             ks=_w(W, s + "residual_block_skip_conv_ResidualConv1DGLU_{}/kernel".format(l))[0],
             bs=_w(W, s + "residual_block_skip_conv_ResidualConv1DGLU_{}/bias".format(l)),
             ko=_w(W, s + "residual_block_out_conv_ResidualConv1DGLU_{}/kernel".format(l))[0],
@@ -228,13 +263,17 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
     f2b = _w(W, "skip_convolutions/final_convolution_2/bias")
     queues = [np.zeros((B, kw + (kw - 1) * (ly["d"] - 1), R), np.float32) for ly in layers]  # :815
     cur = np.zeros((B, 1), np.float32)   # initial_input = 0 ('raw'), wavenet.py:437-445
+    kcur = np.full((B,), 127, np.int64)  # 'mulaw-quantize': one_hot(mulaw_quantize(0)) (util.py:99-102: mu = 255)
     ys = np.zeros((B, T), np.float32)
     ks = np.zeros((B, T), np.int32)
     lg = np.zeros((B, T, f2b.shape[0]), np.float32) if return_logits else None
     zero = np.float32(0)
     for t in range(T):
-        ct = c_up[:, t]
-        x = cur @ first_k + first_b                       # first_conv.incremental_step :826
+        ct = None if c_up is None else c_up[:, t]
+        if quant:   # first_conv of a one-hot row = that row of the kernel
+            x = first_k[kcur] + first_b
+        else:
+            x = cur @ first_k + first_b                   # first_conv.incremental_step :826
         skips = None
         for ly, q in zip(layers, queues):                 # :830-837
             residual = x
@@ -243,7 +282,7 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
             taps = q[:, ::ly["d"]]                        # modules.py:291-292
             h = taps.reshape(B, -1) @ ly["k"] + ly["b"]   # modules.py:295-297
             G2 = h.shape[1] // 2
-            cc = ct @ ly["kc"] + ly["bc"]                 # modules.py:497-501
+            cc = np.zeros_like(h) if ct is None else ct @ ly["kc"] + ly["bc"]   # modules.py:497-501
             if g is not None:
                 cc = cc + ly["gc"]                        # modules.py:505-509
             a = h[:, :G2] + cc[:, :G2]
@@ -260,7 +299,10 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
         x = np.maximum(x, zero) @ f2k + f2b
         if lg is not None:
             lg[:, t] = x
-        if x.shape[1] == 2:   # Gaussian head: sample_from_gaussian (gaussian.py:39-52), u_log = N(0,1)
+        if quant:             # tf.multinomial over the logits, one_hot of the draw (wavenet.py:861-867)
+            k = categorical_sample(x, u_log[t])
+            y = inv_mulaw_quantize_f32(k)
+        elif x.shape[1] == 2:   # Gaussian head: sample_from_gaussian (gaussian.py:39-52), u_log = N(0,1)
             ls = np.maximum(x[:, 1], np.float32(hp["log_scale_min_gauss"]))
             y = np.clip(x[:, 0] + np.exp(ls) * np.asarray(u_log[t], np.float32), -1, 1).astype(np.float32)
             k = np.zeros((B,), np.int32)
@@ -268,6 +310,8 @@ def incremental(c_up, W, hp, u_mix, u_log, test_inputs=None, return_logits=False
             y, k = mol_sample(x, u_mix[t], u_log[t], hp["log_scale_min"])
         ys[:, t] = y
         ks[:, t] = k
+        if quant:
+            kcur = k.astype(np.int64) if test_inputs is None else np.asarray(test_inputs)[:, t].astype(np.int64)
         cur = y[:, None] if test_inputs is None else np.asarray(test_inputs, np.float32)[:, t:t + 1]
     return (ys, ks, lg) if return_logits else (ys, ks)
 

@@ -986,6 +986,8 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
     (void)hip_device;
     *out = nullptr;
     CK(cfg->gin_channels <= 0, TT2_ERR_INVALID_ARG, "global conditioning is GPU-only (libtt2.so)");
+    CK(cfg->input_type != 2 && cfg->cin_channels > 0, TT2_ERR_INVALID_ARG,
+       "mulaw-quantize input and unconditional synthesis are GPU-only (libtt2.so)");
     CK(cfg->kernel_size >= 1 && cfg->layers >= 1 && cfg->stacks >= 1 && cfg->layers % cfg->stacks == 0,
        TT2_ERR_INVALID_ARG, "layers must be a multiple of stacks");
     CK(cfg->upsample_type >= 0 && cfg->upsample_type <= 4, TT2_ERR_INVALID_ARG, "upsample_type must be 0..4");

@@ -22,6 +22,7 @@
 
 #include "common.h"
 #include "gemm.h"
+#include "wavenet_q.h"
 #include "wavenet_wide.h"
 
 namespace tt2 {
@@ -643,6 +644,7 @@ struct tt2_wn_ctx {
   int* status_host = nullptr;    // pinned: spin-timeout word of the last launch
   tt2::DevBuf gcv;               // [gc_B][L][G] gate-permuted global-condition terms (set_global_condition)
   int gc_B = 0;
+  bool quantize = false;         // input_type 'mulaw-quantize': k_generate_q (wavenet_q.hip), natural layouts
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool timed = false;
 };
@@ -663,7 +665,97 @@ static void wupload(DevBuf& d, const std::vector<float>& h) {
   TT2_HIP(hipMemcpy(d.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
 }
 
+// upsampling-network weights (local conditioning on)
+static void wn_upload_upsampler(tt2_wn_ctx* c) {
+  const WeightMap& wm = c->host;
+  const std::string P(WP);
+  const int cin = c->cin;
+  static const char* kUpName[4] = {"ConvTranspose2D_layer_", "ConvTranspose1D_layer_", "ResizeConvolution_layer_",
+                                   "SubPixelConvolution_layer_"};
+  const int ut = c->cfg.upsample_type;
+  for (int i = 0; cin > 0 && ut != WN_UP_NN && i < c->cfg.n_upsample; ++i) {
+    const std::string sc = P + "local_conditioning_upsampling_" + std::to_string(i + 1) + "/" + kUpName[ut] +
+                           std::to_string(i) + "/";
+    const int s = c->cfg.upsample_scales[i], kf = c->cfg.freq_axis_kernel_size;
+    if (ut == WN_UP_1D) {
+      wupload(c->up_k[i], need(wm, sc + "kernel", {1, s, cin, cin}).data);
+      wupload(c->up_b[i], need(wm, sc + "bias", {cin}).data);
+    } else if (ut == WN_UP_SUBPIXEL) {
+      std::vector<float> k = need(wm, sc + "kernel", {kf, 3, 1, s}).data;
+      if (!c->cfg.NN_init)  // SubPixelConvolution.build (modules.py:585-593): every channel = channel 0
+        for (int q = 0; q < kf * 3; ++q)
+          for (int o = 1; o < s; ++o) k[(size_t)q * s + o] = k[(size_t)q * s];
+      wupload(c->up_k[i], k);
+      wupload(c->up_b[i], need(wm, sc + "bias", {s}).data);
+    } else {
+      wupload(c->up_k[i], need(wm, sc + "kernel", {kf, s, 1, 1}).data);
+      wupload(c->up_b[i], need(wm, sc + "bias", {1}).data);
+    }
+  }
+}
+
+// 'mulaw-quantize' (k_generate_q): natural column orders -- the first conv [Q][R], the dilated
+// convs [L][3R][G], [skip | out] [L][R][S + R], the conditioning 1x1s [cin][L][G]
+static void wn_finalize_q(tt2_wn_ctx* c) {
+  const WeightMap& wm = c->host;
+  const std::string P(WP);
+  const int R = c->R, G = c->G, S = c->S, L = c->L, Q = c->C, cin = c->cin, kw = c->cfg.kernel_size;
+  TT2_HIP(hipSetDevice(c->dev));
+  wupload(c->first_w, need(wm, P + "input_convolution/kernel", {1, Q, R}).data);
+  wupload(c->first_b, need(wm, P + "input_convolution/bias", {R}).data);
+  std::vector<float> cw((size_t)L * kw * R * G), cb((size_t)L * G), sow((size_t)L * R * (S + R)), sob((size_t)L * (S + R));
+  std::vector<float> condw((size_t)std::max(cin, 1) * L * G, 0.f), condb((size_t)L * G, 0.f);
+  for (int l = 0; l < L; ++l) {
+    const std::string s = P + "ResidualConv1DGLU_" + std::to_string(l) + "/";
+    const std::string ln = "_ResidualConv1DGLU_" + std::to_string(l) + "/";
+    const auto& k = need(wm, s + "residual_block_causal_conv" + ln + "kernel", {kw, R, G});
+    const auto& bb = need(wm, s + "residual_block_causal_conv" + ln + "bias", {G});
+    const auto& ksk = need(wm, s + "residual_block_skip_conv" + ln + "kernel", {1, G / 2, S});
+    const auto& bsk = need(wm, s + "residual_block_skip_conv" + ln + "bias", {S});
+    const auto& ko = need(wm, s + "residual_block_out_conv" + ln + "kernel", {1, G / 2, R});
+    const auto& bo = need(wm, s + "residual_block_out_conv" + ln + "bias", {R});
+    std::copy(k.data.begin(), k.data.end(), cw.begin() + (size_t)l * kw * R * G);
+    std::copy(bb.data.begin(), bb.data.end(), cb.begin() + (size_t)l * G);
+    for (int j = 0; j < R; ++j) {
+      for (int o = 0; o < S; ++o) sow[((size_t)l * R + j) * (S + R) + o] = ksk.data[(size_t)j * S + o];
+      for (int o = 0; o < R; ++o) sow[((size_t)l * R + j) * (S + R) + S + o] = ko.data[(size_t)j * R + o];
+    }
+    for (int o = 0; o < S; ++o) sob[(size_t)l * (S + R) + o] = bsk.data[o];
+    for (int o = 0; o < R; ++o) sob[(size_t)l * (S + R) + S + o] = bo.data[o];
+    if (cin > 0) {
+      const auto& kc = need(wm, s + "residual_block_cin_conv" + ln + "kernel", {1, cin, G});
+      const auto& bc = need(wm, s + "residual_block_cin_conv" + ln + "bias", {G});
+      for (int i = 0; i < cin; ++i)
+        for (int g = 0; g < G; ++g) condw[(size_t)i * L * G + (size_t)l * G + g] = kc.data[(size_t)i * G + g];
+      for (int g = 0; g < G; ++g) condb[(size_t)l * G + g] = bc.data[g];
+    }
+    if (c->cfg.gin_channels > 0) {
+      (void)need(wm, s + "residual_block_gin_conv" + ln + "kernel", {1, c->cfg.gin_channels, G});
+      (void)need(wm, s + "residual_block_gin_conv" + ln + "bias", {G});
+    }
+  }
+  if (c->cfg.gin_channels > 0 && c->cfg.n_speakers > 0)
+    (void)need(wm, "WaveNet_model/gc_embedding", {c->cfg.n_speakers, c->cfg.gin_channels});
+  c->gc_B = 0;
+  wupload(c->conv_w, cw);
+  wupload(c->conv_b, cb);
+  wupload(c->so_w, sow);
+  wupload(c->so_b, sob);
+  wupload(c->cond_w, condw);
+  wupload(c->cond_b, condb);
+  wupload(c->f1_w, need(wm, P + "skip_convolutions/final_convolution_1/kernel", {1, S, S}).data);
+  wupload(c->f1_b, need(wm, P + "skip_convolutions/final_convolution_1/bias", {S}).data);
+  wupload(c->f2_w, need(wm, P + "skip_convolutions/final_convolution_2/kernel", {1, S, Q}).data);
+  wupload(c->f2_b, need(wm, P + "skip_convolutions/final_convolution_2/bias", {Q}).data);
+  wn_upload_upsampler(c);
+  c->finalized = true;
+}
+
 static void wn_finalize(tt2_wn_ctx* c) {
+  if (c->quantize) {
+    wn_finalize_q(c);
+    return;
+  }
   const WeightMap& wm = c->host;
   const std::string P(WP);
   const int R = c->R, G = c->G, S = c->S, L = c->L, C = c->C, cin = c->cin, kw = c->cfg.kernel_size;
@@ -671,7 +763,7 @@ static void wn_finalize(tt2_wn_ctx* c) {
   wupload(c->first_w, need(wm, P + "input_convolution/kernel", {1, 1, R}).data);
   wupload(c->first_b, need(wm, P + "input_convolution/bias", {R}).data);
   constexpr int CK = WN_CK, SK = WN_SK;
-  std::vector<float> cw((size_t)L * CK * WN_THREADS * 4), cb((size_t)L * G), condw((size_t)cin * L * G),
+  std::vector<float> cw((size_t)L * CK * WN_THREADS * 4), cb((size_t)L * G), condw((size_t)std::max(cin, 1) * L * G, 0.f),
       condb((size_t)L * G), sow((size_t)L * SK * WN_THREADS * 4), sob((size_t)L * 2 * R);
   std::vector<float> wide_cw, wide_so;
   if (c->wide) {
@@ -683,8 +775,9 @@ static void wn_finalize(tt2_wn_ctx* c) {
     const std::string ln = "_ResidualConv1DGLU_" + std::to_string(l) + "/";
     const auto& k = need(wm, s + "residual_block_causal_conv" + ln + "kernel", {kw, R, G});
     const auto& bb = need(wm, s + "residual_block_causal_conv" + ln + "bias", {G});
-    const auto& kc = need(wm, s + "residual_block_cin_conv" + ln + "kernel", {1, cin, G});
-    const auto& bc = need(wm, s + "residual_block_cin_conv" + ln + "bias", {G});
+    // local conditioning off (cin_channels <= 0): no conv1x1c (modules.py:416-424)
+    const HostTensor* kc = cin > 0 ? &need(wm, s + "residual_block_cin_conv" + ln + "kernel", {1, cin, G}) : nullptr;
+    const HostTensor* bc = cin > 0 ? &need(wm, s + "residual_block_cin_conv" + ln + "bias", {G}) : nullptr;
     const auto& ksk = need(wm, s + "residual_block_skip_conv" + ln + "kernel", {1, G / 2, S});
     const auto& bsk = need(wm, s + "residual_block_skip_conv" + ln + "bias", {S});
     const auto& ko = need(wm, s + "residual_block_out_conv" + ln + "kernel", {1, G / 2, R});
@@ -717,8 +810,8 @@ static void wn_finalize(tt2_wn_ctx* c) {
       for (int e = 0; e < 4; ++e) {
         const int src = gate_col(R, q, e), dst = 4 * q + e;
         cb[(size_t)l * G + dst] = bb.data[src];
-        condb[(size_t)l * G + dst] = bc.data[src];
-        for (int i = 0; i < cin; ++i) condw[(size_t)i * L * G + l * G + dst] = kc.data[(size_t)i * G + src];
+        condb[(size_t)l * G + dst] = bc ? bc->data[src] : 0.f;
+        for (int i = 0; i < cin; ++i) condw[(size_t)i * L * G + l * G + dst] = kc->data[(size_t)i * G + src];
       }
     for (int j = 0; j < S; ++j) sob[(size_t)l * 2 * R + j] = bsk.data[j];
     for (int j = 0; j < R; ++j) sob[(size_t)l * 2 * R + S + j] = bo.data[j];
@@ -795,28 +888,7 @@ static void wn_finalize(tt2_wn_ctx* c) {
   wupload(c->f1_b, need(wm, P + "skip_convolutions/final_convolution_1/bias", {S}).data);
   wupload(c->f2_w, need(wm, P + "skip_convolutions/final_convolution_2/kernel", {1, S, C}).data);
   wupload(c->f2_b, need(wm, P + "skip_convolutions/final_convolution_2/bias", {C}).data);
-  static const char* kUpName[4] = {"ConvTranspose2D_layer_", "ConvTranspose1D_layer_", "ResizeConvolution_layer_",
-                                   "SubPixelConvolution_layer_"};
-  const int ut = c->cfg.upsample_type;
-  for (int i = 0; ut != WN_UP_NN && i < c->cfg.n_upsample; ++i) {
-    const std::string sc = P + "local_conditioning_upsampling_" + std::to_string(i + 1) + "/" + kUpName[ut] +
-                           std::to_string(i) + "/";
-    const int s = c->cfg.upsample_scales[i], kf = c->cfg.freq_axis_kernel_size;
-    if (ut == WN_UP_1D) {
-      wupload(c->up_k[i], need(wm, sc + "kernel", {1, s, cin, cin}).data);
-      wupload(c->up_b[i], need(wm, sc + "bias", {cin}).data);
-    } else if (ut == WN_UP_SUBPIXEL) {
-      std::vector<float> k = need(wm, sc + "kernel", {kf, 3, 1, s}).data;
-      if (!c->cfg.NN_init)  // SubPixelConvolution.build (modules.py:585-593): every channel = channel 0
-        for (int q = 0; q < kf * 3; ++q)
-          for (int o = 1; o < s; ++o) k[(size_t)q * s + o] = k[(size_t)q * s];
-      wupload(c->up_k[i], k);
-      wupload(c->up_b[i], need(wm, sc + "bias", {s}).data);
-    } else {
-      wupload(c->up_k[i], need(wm, sc + "kernel", {kf, s, 1, 1}).data);
-      wupload(c->up_b[i], need(wm, sc + "bias", {1}).data);
-    }
-  }
+  wn_upload_upsampler(c);
   c->finalized = true;
 }
 
@@ -867,17 +939,31 @@ __global__ void k_wn_noise(uint64_t seed, long n, int Bg, int nr, int gaussian, 
 
 static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f, const float* umix_d,
                             const float* ulog_d, uint64_t seed, const float* teacher_d, float* wav_d, int* k_d,
-                            float* logits_d, float* upsampled_d, hipStream_t s) {
+                            float* logits_d, float* upsampled_d, hipStream_t s, long T_uncond = 0) {
   TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_wn_finalize not called");
   TT2_CHECK(B >= 1 && B <= c->cfg.max_batch, TT2_ERR_SHAPE_MISMATCH, "batch exceeds capacity");
-  const long T = (long)T_f * c->hop;
-  TT2_CHECK(T_f >= 1 && T <= c->cfg.max_samples, TT2_ERR_SHAPE_MISMATCH, "synthesis length exceeds capacity");
+  // cond_in null: unconditional synthesis of T_uncond samples (wavenet.py:410-411)
+  const bool uncond = cond_in == nullptr;
+  TT2_CHECK(uncond == (c->cin == 0), TT2_ERR_INVALID_ARG,
+            uncond ? "local conditioning on (cin_channels > 0): a condition is required"
+                   : "cin_channels <= 0: unconditional synthesis (tt2_wn_generate_unconditional)");
+  const long T = uncond ? T_uncond : (long)T_f * c->hop;
+  TT2_CHECK((uncond || T_f >= 1) && T >= 1 && T <= c->cfg.max_samples, TT2_ERR_SHAPE_MISMATCH,
+            "synthesis length exceeds capacity");
   const int F = c->cin;
+  TT2_HIP(hipEventRecord(c->ev[0], s));
+  const bool need_cond = !uncond || c->cfg.gin_channels > 0 || !c->quantize;
+  if (uncond) {  // no conv1x1c term: zero conditioning (+ the global term below)
+    TT2_HIP(hipEventRecord(c->ev[1], s));
+    if (need_cond) {
+      c->cond.alloc(sizeof(float) * B * T * c->L * c->G);
+      TT2_HIP(hipMemsetAsync(c->cond.p, 0, sizeof(float) * B * T * c->L * c->G, s));
+    }
+  } else {
   // upsampling network: [B][F][T_f] -> [B][F][T]
   c->up_a.alloc(sizeof(float) * B * F * T);
   c->up_b_buf.alloc(sizeof(float) * B * F * T);
   c->c_up_t.alloc(sizeof(float) * B * T * F);
-  TT2_HIP(hipEventRecord(c->ev[0], s));
   const float* src = cond_in;  // [B][F][T_f] channels-first
   long Tcur = T_f;
   float* bufs[2] = {c->up_a.as<float>(), c->up_b_buf.as<float>()};
@@ -906,6 +992,7 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
   g.bias = c->cond_b.as<float>();
   g.split16 = 1;  // conditioning in [0, 1] after the upsampler: fp16x3 split MFMA (gemm.h)
   gemm(g, s);
+  }
   if (c->cfg.gin_channels > 0) {  // + g·W_g + b_g of every layer (constant over time)
     TT2_CHECK(c->gc_B == B, TT2_ERR_STATE,
               "gin_channels > 0: tt2_wn_set_global_condition for exactly these B rows before generating");
@@ -915,6 +1002,29 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
     TT2_HIP(hipGetLastError());
   }
   TT2_HIP(hipEventRecord(c->ev[2], s));
+  if (c->quantize) {  // one-hot input, Q-class softmax head (wavenet_q.hip)
+    const int per = c->L / c->cfg.stacks;
+    const long rf = wq_ring_floats(c->R, c->L, per);
+    c->rings.alloc(sizeof(float) * B * rf);
+    TT2_HIP(hipMemsetAsync(c->rings.p, 0, sizeof(float) * B * rf, s));
+    QGenArgs q{};
+    q.T = (int)T; q.L = c->L; q.per = per; q.R = c->R; q.G = c->G; q.S = c->S; q.Q = c->C; q.Bg = B;
+    q.legacy = c->cfg.legacy; q.res_legacy = c->cfg.residual_legacy;
+    q.k0 = 127;  // mulaw_quantize(0) = int((0 + 1) / 2 * 255), mu hard-coded to 255 (util.py:71-102)
+    q.first_w = c->first_w.as<float>(); q.first_b = c->first_b.as<float>();
+    q.conv_w = c->conv_w.as<float>(); q.conv_b = c->conv_b.as<float>();
+    q.cond = need_cond ? c->cond.as<float>() : nullptr;
+    q.so_w = c->so_w.as<float>(); q.so_b = c->so_b.as<float>();
+    q.f1_w = c->f1_w.as<float>(); q.f1_b = c->f1_b.as<float>(); q.f2_w = c->f2_w.as<float>(); q.f2_b = c->f2_b.as<float>();
+    q.u = ulog_d; q.seed = seed; q.teacher = teacher_d;
+    q.wav = wav_d; q.kout = k_d; q.logits = logits_d;
+    q.rings = c->rings.as<float>(); q.ring_floats = rf;
+    wq_launch(q, s);
+    *c->status_host = 0;
+    TT2_HIP(hipEventRecord(c->ev[3], s));
+    c->timed = true;
+    return;
+  }
   if (c->wide) {
     const int R = c->R, NG = ww_nc(R) * 2 * R;
     c->rings.alloc(sizeof(float) * ww_ring_floats(R, c->L, c->L / c->cfg.stacks));
@@ -1001,6 +1111,7 @@ void tt2_wn_default_config(tt2_wn_config* c, int max_batch, int64_t max_samples)
   c->upsample_type = 0; c->upsample_activation = 1; c->leaky_alpha = 0.4f; c->NN_init = 1;
   c->log_scale_min_gauss = (float)std::log(1e-7);
   c->gin_channels = -1; c->n_speakers = 0;
+  c->input_type = 0; c->quantize_channels = 256;
 }
 
 tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** out) {
@@ -1016,27 +1127,47 @@ tt2_status tt2_wn_create(const tt2_wn_config* cfg, int hip_device, tt2_wn_ctx** 
               "generation kernels: residual_channels R = 64 (k_generate_pipe, BASELINE config 3), 128 (fork "
               "default) or 256 (paper default), with gate_channels = 2R and skip_out_channels = R");
     TT2_CHECK(cfg->kernel_size == 3, TT2_ERR_INVALID_ARG, "kernel_size must be 3");
-    TT2_CHECK(cfg->out_channels == 2 || (cfg->out_channels % 3 == 0 && cfg->out_channels <= 30 && cfg->out_channels >= 3),
-              TT2_ERR_INVALID_ARG, "head needs out_channels = 2 (Gaussian) or 3*nr_mix <= 30 (MoL)");
-    TT2_CHECK(cfg->upsample_type >= WN_UP_2D && cfg->upsample_type <= WN_UP_NN, TT2_ERR_INVALID_ARG,
-              "upsample_type out of range");
-    TT2_CHECK(cfg->upsample_activation >= WN_ACT_NONE && cfg->upsample_activation <= WN_ACT_LEAKY,
-              TT2_ERR_INVALID_ARG, "upsample_activation out of range");
+    TT2_CHECK(cfg->input_type >= 0 && cfg->input_type <= 2, TT2_ERR_INVALID_ARG,
+              "input_type: 0 'raw', 1 'mulaw', 2 'mulaw-quantize'");
+    const bool quant = cfg->input_type == 2;
+    if (quant)
+      TT2_CHECK(cfg->out_channels == cfg->quantize_channels && cfg->quantize_channels >= 4 &&
+                    cfg->quantize_channels <= WQ_QMAX && cfg->quantize_channels % 4 == 0,
+                TT2_ERR_INVALID_ARG,
+                "mulaw-quantize: out_channels must equal quantize_channels (a multiple of 4, <= 1024)");
+    else
+      TT2_CHECK(cfg->out_channels == 2 || (cfg->out_channels % 3 == 0 && cfg->out_channels <= 30 && cfg->out_channels >= 3),
+                TT2_ERR_INVALID_ARG, "head needs out_channels = 2 (Gaussian) or 3*nr_mix <= 30 (MoL)");
     TT2_CHECK(cfg->layers >= 1 && cfg->stacks >= 1 && cfg->layers % cfg->stacks == 0, TT2_ERR_INVALID_ARG,
               "layers % stacks != 0");
-    TT2_CHECK(cfg->cin_channels >= 1 && cfg->cin_channels <= 128, TT2_ERR_INVALID_ARG, "cin_channels out of range");
-    TT2_CHECK(cfg->n_upsample >= 1 && cfg->n_upsample <= 8, TT2_ERR_INVALID_ARG, "n_upsample out of range");
+    TT2_CHECK(cfg->cin_channels <= 128, TT2_ERR_INVALID_ARG, "cin_channels out of range");
+    if (cfg->cin_channels > 0) {  // local conditioning: the upsampling network
+      TT2_CHECK(cfg->upsample_type >= WN_UP_2D && cfg->upsample_type <= WN_UP_NN, TT2_ERR_INVALID_ARG,
+                "upsample_type out of range");
+      TT2_CHECK(cfg->upsample_activation >= WN_ACT_NONE && cfg->upsample_activation <= WN_ACT_LEAKY,
+                TT2_ERR_INVALID_ARG, "upsample_activation out of range");
+      TT2_CHECK(cfg->n_upsample >= 1 && cfg->n_upsample <= 8, TT2_ERR_INVALID_ARG, "n_upsample out of range");
+    }
     TT2_CHECK(cfg->max_batch >= 1 && cfg->max_samples >= 1, TT2_ERR_INVALID_ARG, "capacities must be >= 1");
     auto c = std::make_unique<tt2_wn_ctx>();
     c->cfg = *cfg;
     c->dev = hip_device;
     c->R = cfg->residual_channels; c->G = cfg->gate_channels; c->S = cfg->skip_out_channels;
-    c->L = cfg->layers; c->C = cfg->out_channels; c->cin = cfg->cin_channels;
+    c->L = cfg->layers; c->C = cfg->out_channels; c->cin = std::max(cfg->cin_channels, 0);
     c->hop = 1;
-    for (int i = 0; i < cfg->n_upsample; ++i) c->hop *= cfg->upsample_scales[i];
+    for (int i = 0; c->cin > 0 && i < cfg->n_upsample; ++i) c->hop *= cfg->upsample_scales[i];
     TT2_HIP(hipSetDevice(hip_device));
     TT2_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
+    if (quant) {  // k_generate_q: one work-group per utterance, no co-residency requirement
+      c->quantize = true;
+      const size_t qshm = wq_lds_bytes(c->R, c->G, c->S, c->C);
+      TT2_CHECK(qshm <= 64 * 1024, TT2_ERR_INVALID_ARG, "mulaw-quantize generator LDS exceeds 64 KiB");
+      TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->status_host), sizeof(int), hipHostMallocDefault));
+      *c->status_host = 0;
+      *out = c.release();
+      return;
+    }
     int ncu = 0;
     TT2_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     if (Rc != 64) {  // k_generate_wide: NC work-groups per layer + a head, queues in global memory
@@ -1106,7 +1237,8 @@ tt2_status tt2_wn_set_global_condition(tt2_wn_ctx* c, const int32_t* ids, const 
       for (int b = 0; b < B; ++b)
         for (int q = 0; q < G / 4; ++q)
           for (int e = 0; e < 4; ++e) {
-            const int src = gate_col(R, q, e), dst = 4 * q + e;  // the conditioning's gate permutation
+            // the conditioning's gate permutation (natural order for k_generate_q)
+            const int src = c->quantize ? 4 * q + e : gate_col(R, q, e), dst = 4 * q + e;
             double v = bg.data[src];
             for (int i = 0; i < gin; ++i) v += (double)g[(size_t)b * gin + i] * kg.data[(size_t)i * G + src];
             gcv[((size_t)b * L + l) * G + dst] = (float)v;
@@ -1174,7 +1306,8 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* c, const float* cond, int B, int T_f, con
     hipStream_t s = c->stream;
     const long T = (long)T_f * c->hop;
     TT2_CHECK(T <= c->cfg.max_samples, TT2_ERR_SHAPE_MISMATCH, "synthesis length exceeds capacity");
-    const int F = c->cin, nr = c->C / 3;
+    const int F = c->cin, nr = c->quantize ? 0 : c->C / 3;
+    TT2_CHECK(F > 0, TT2_ERR_INVALID_ARG, "cin_channels <= 0: tt2_wn_generate_unconditional");
     // host layout [B][T_f][F] -> device channels-first [B][F][T_f]
     std::vector<float> cf((size_t)B * F * T_f);
     for (int b = 0; b < B; ++b)
@@ -1211,6 +1344,47 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* c, const float* cond, int B, int T_f, con
       TT2_HIP(hipMemcpyAsync(logits_out, c->logits.p, sizeof(float) * B * T * c->C, hipMemcpyDeviceToHost, s));
     if (upsampled_out)
       TT2_HIP(hipMemcpyAsync(upsampled_out, upl.p, sizeof(float) * B * F * T, hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipStreamSynchronize(s));
+    check_status(c);
+  });
+}
+
+tt2_status tt2_wn_generate_unconditional(tt2_wn_ctx* c, int B, int64_t T, const float* u_mix, const float* u_log,
+                                         uint64_t seed, const float* teacher, float* wav_out, int32_t* mix_idx_out,
+                                         float* logits_out) {
+  return guard([&] {
+    TT2_CHECK(c && wav_out, TT2_ERR_INVALID_ARG, "tt2_wn_generate_unconditional: null argument");
+    TT2_CHECK(c->cin == 0, TT2_ERR_INVALID_ARG, "tt2_wn_generate_unconditional: cin_channels > 0 needs a condition");
+    TT2_CHECK(B >= 1 && B <= c->cfg.max_batch && T >= 1 && T <= c->cfg.max_samples, TT2_ERR_SHAPE_MISMATCH,
+              "bad batch / length");
+    TT2_HIP(hipSetDevice(c->dev));
+    hipStream_t s = c->stream;
+    const int nr = c->quantize ? 0 : c->C / 3;
+    const float *um = nullptr, *ul = nullptr, *tg = nullptr;
+    if (u_mix && nr > 0) {
+      c->umix.alloc(sizeof(float) * T * B * nr);
+      TT2_HIP(hipMemcpyAsync(c->umix.p, u_mix, sizeof(float) * T * B * nr, hipMemcpyHostToDevice, s));
+      um = c->umix.as<float>();
+    }
+    if (u_log) {
+      c->ulog.alloc(sizeof(float) * T * B);
+      TT2_HIP(hipMemcpyAsync(c->ulog.p, u_log, sizeof(float) * T * B, hipMemcpyHostToDevice, s));
+      ul = c->ulog.as<float>();
+    }
+    if (teacher) {
+      c->teacher.alloc(sizeof(float) * T * B);
+      TT2_HIP(hipMemcpyAsync(c->teacher.p, teacher, sizeof(float) * T * B, hipMemcpyHostToDevice, s));
+      tg = c->teacher.as<float>();
+    }
+    c->wav.alloc(sizeof(float) * B * T);
+    c->kout.alloc(sizeof(int) * B * T);
+    if (logits_out) c->logits.alloc(sizeof(float) * B * T * c->C);
+    wn_generate_dev(c, nullptr, B, 0, um, ul, seed, tg, c->wav.as<float>(), c->kout.as<int>(),
+                    logits_out ? c->logits.as<float>() : nullptr, nullptr, s, (long)T);
+    TT2_HIP(hipMemcpyAsync(wav_out, c->wav.p, sizeof(float) * B * T, hipMemcpyDeviceToHost, s));
+    if (mix_idx_out) TT2_HIP(hipMemcpyAsync(mix_idx_out, c->kout.p, sizeof(int) * B * T, hipMemcpyDeviceToHost, s));
+    if (logits_out)
+      TT2_HIP(hipMemcpyAsync(logits_out, c->logits.p, sizeof(float) * B * T * c->C, hipMemcpyDeviceToHost, s));
     TT2_HIP(hipStreamSynchronize(s));
     check_status(c);
   });

@@ -59,7 +59,7 @@ class WnConfig(ctypes.Structure):
         ("upsample_type", ctypes.c_int), ("upsample_activation", ctypes.c_int),
         ("leaky_alpha", ctypes.c_float), ("NN_init", ctypes.c_int),
         ("log_scale_min_gauss", ctypes.c_float), ("gin_channels", ctypes.c_int),
-        ("n_speakers", ctypes.c_int)]
+        ("n_speakers", ctypes.c_int), ("input_type", ctypes.c_int), ("quantize_channels", ctypes.c_int)]
 
 
 class GlConfig(ctypes.Structure):
@@ -137,6 +137,7 @@ SIGNATURES = {
     "tt2_wn_finalize": (_I, [_P]),
     "tt2_wn_generate": (_I, [_P, _P, _I, _I, _P, _P, _U64, _P, _P, _P, _P, _P]),
     "tt2_wn_generate_dev": (_I, [_P, _P, _I, _I, _P, _P, _U64, _P, _P, _P, _P, _P]),
+    "tt2_wn_generate_unconditional": (_I, [_P, _I, ctypes.c_int64, _P, _P, _U64, _P, _P, _P, _P]),
     "tt2_wn_cond_from_mels_dev": (_I, [_P, _I, _P, _I, _I, _I, _F, _F, _I, _I, _P, _P]),
     "tt2_gl_default_config": (None, [ctypes.POINTER(GlConfig)]),
     "tt2_gl_create": (_I, [ctypes.POINTER(GlConfig), _I, ctypes.POINTER(_P)]),

@@ -395,6 +395,13 @@ def wavenet_config(hp, max_batch, max_samples, lib=None):
     cfg.log_scale_min_gauss = hp.log_scale_min_gauss
     cfg.gin_channels = hp.gin_channels if hp.gin_channels > 0 else -1       # wavenet.py:152-158
     cfg.n_speakers = hp.n_speakers if (hp.gin_channels > 0 and hp.use_speaker_embedding) else 0
+    itype = getattr(hp, "input_type", "raw")
+    cfg.input_type = ("raw", "mulaw", "mulaw-quantize").index(itype)
+    cfg.quantize_channels = hp.quantize_channels
+    if itype == "mulaw-quantize" and hp.out_channels != hp.quantize_channels:
+        raise ValueError("mulaw-quantize: out_channels must equal quantize_channels (hparams.py:222)")
+    if hp.cin_channels <= 0:   # unconditional: no upsampling network
+        return cfg
     cfg.n_upsample = len(hp.upsample_scales)
     for i, s in enumerate(hp.upsample_scales):
         cfg.upsample_scales[i] = s
@@ -414,7 +421,8 @@ class WaveNetEngine(object):
         self.hp = hp
         self.cfg = wavenet_config(hp, max_batch, max_samples, self.lib)
         self.caps = (max_batch, max_samples)
-        self.hop = int(np.prod(hp.upsample_scales))
+        self.hop = int(np.prod(hp.upsample_scales)) if hp.cin_channels > 0 else 1
+        self.quantize = getattr(hp, "input_type", "raw") == "mulaw-quantize"
         h = ctypes.c_void_p()
         self._ok(self.lib.tt2_wn_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
         self.h = h
@@ -466,8 +474,8 @@ class WaveNetEngine(object):
         T = T_f * self.hop
         nr = self.hp.out_channels // 3
         um, ul, tg = f32(u_mix), f32(u_log), f32(teacher)
-        if self.hp.out_channels == 2:
-            um = None  # Gaussian head: only the N(0,1) draws in u_log
+        if self.hp.out_channels == 2 or self.quantize:
+            um = None  # Gaussian head: the N(0,1) draws in u_log; mulaw-quantize: tf.multinomial's uniforms
         if um is not None and um.shape != (T, B, nr):
             raise ValueError("u_mix must be [T, B, nr_mix] = {}".format((T, B, nr)))
         if ul is not None and ul.shape != (T, B):
@@ -481,6 +489,31 @@ class WaveNetEngine(object):
         self._ok(self.lib.tt2_wn_generate(self.h, ptr(cond), B, T_f, ptr(um), ptr(ul), seed, ptr(tg),
                                        ptr(y), ptr(k), ptr(lg), ptr(up)))
         return dict(y=y, k=k, logits=lg, upsampled=up)
+
+    def generate_unconditional(self, B, T, u_mix=None, u_log=None, seed=0, teacher=None,
+                               want_logits=False, g=None):
+        """cin_channels <= 0: T samples per row without a local condition (wavenet.py:410-411,
+        synthesis_length); the sampler / teacher contract of generate()."""
+        if self.hp.gin_channels > 0:
+            if g is None:
+                raise ValueError("gin_channels > 0: a global condition g is required")
+            self.set_global_condition(g, B)
+        nr = self.hp.out_channels // 3
+        um, ul, tg = f32(u_mix), f32(u_log), f32(teacher)
+        if self.hp.out_channels == 2 or self.quantize:
+            um = None
+        if um is not None and um.shape != (T, B, nr):
+            raise ValueError("u_mix must be [T, B, nr_mix] = {}".format((T, B, nr)))
+        if ul is not None and ul.shape != (T, B):
+            raise ValueError("u_log must be [T, B]")
+        if tg is not None and tg.shape != (B, T):
+            raise ValueError("teacher (test_inputs) must be [B, T]")
+        y = np.zeros((B, T), np.float32)
+        k = np.zeros((B, T), np.int32)
+        lg = np.zeros((B, T, self.hp.out_channels), np.float32) if want_logits else None
+        self._ok(self.lib.tt2_wn_generate_unconditional(self.h, B, T, ptr(um), ptr(ul), seed, ptr(tg),
+                                                     ptr(y), ptr(k), ptr(lg)))
+        return dict(y=y, k=k, logits=lg)
 
 
 def mol_sample(logits, u_mix, u_log, log_scale_min):

@@ -312,12 +312,17 @@ def wavenet_weight_specs(hp):
     """(name, shape, init) of the WaveNet synthesis graph (wavenet.py:89-208)."""
     S = []
     R, G, Sk = hp.residual_channels, hp.gate_channels, hp.skip_out_channels
-    S.append((WP + "input_convolution/kernel", (1, 1, R), "glorot"))
+    # one-hot input of quantize_channels classes for 'mulaw-quantize' (Conv1D1x1 builds its kernel on
+    # the input's channels, wavenet.py:102-115), a scalar otherwise
+    qin = hp.quantize_channels if getattr(hp, "input_type", "raw") == "mulaw-quantize" else 1
+    S.append((WP + "input_convolution/kernel", (1, qin, R), "glorot"))
     S.append((WP + "input_convolution/bias", (R,), "bias"))
     for l in range(hp.layers):
         s = WP + "ResidualConv1DGLU_{}/".format(l)
         kinds = [("causal", (hp.kernel_size, R, G)), ("cin", (1, hp.cin_channels, G)),
                  ("skip", (1, G // 2, Sk)), ("out", (1, G // 2, R))]
+        if hp.cin_channels <= 0:  # local conditioning disabled: no conv1x1c (modules.py:421-426)
+            kinds.pop(1)
         if hp.gin_channels > 0:   # conv1x1g (modules.py:427-433)
             kinds.insert(2, ("gin", (1, hp.gin_channels, G)))
         for kind, shape in kinds:
@@ -331,8 +336,8 @@ def wavenet_weight_specs(hp):
     if hp.gin_channels > 0 and hp.use_speaker_embedding:   # Embedding, truncated normal std 0.1
         S.append(("WaveNet_model/gc_embedding", (hp.n_speakers, hp.gin_channels), "embed:0.1"))
     ut = hp.upsample_type
-    if ut == "NearestNeighbor":  # NearestNeighborUpsample: no variables (modules.py:524-536)
-        return S
+    if ut == "NearestNeighbor" or hp.cin_channels <= 0:  # NearestNeighborUpsample: no variables
+        return S                                          # (modules.py:524-536); no upsampler without c
     name = {"2D": "ConvTranspose2D", "1D": "ConvTranspose1D", "Resize": "ResizeConvolution",
             "SubPixel": "SubPixelConvolution"}[ut]
     kf, nl = hp.freq_axis_kernel_size, len(hp.upsample_scales)

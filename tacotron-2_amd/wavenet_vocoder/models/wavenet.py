@@ -87,11 +87,8 @@ class WaveNet():
 
     def _check_path(self):
         hp = self._hparams
-        if not is_scalar_input(hp.input_type):
-            raise NotImplementedError("input_type='mulaw-quantize' (one-hot input, softmax head) is "
-                                      "not on the MI355X path; 'raw' and 'mulaw' are")
-        if not self.local_conditioning_enabled():
-            raise NotImplementedError("unconditional synthesis (cin_channels <= 0) is not built")
+        if not is_scalar_input(hp.input_type) and hp.out_channels != hp.quantize_channels:
+            raise ValueError("mulaw-quantize: out_channels must equal quantize_channels (hparams.py:222)")
 
     def _get_engine(self, B, T):
         if self._weights is None:
@@ -110,7 +107,9 @@ class WaveNet():
                    split_infos=None, u_mix=None, u_log=None, seed=0):
         """wavenet.py:218-473 (synthesis branch :408-465).  c: [B, T_frames, cin] conditioning,
         already clipped + _interp'd by the caller (wavenet_vocoder/synthesizer.py:63-70).
-        u_mix [T,B,10] / u_log [T,B] inject the MoL sampler's uniforms (None = device RNG)."""
+        u_mix [T,B,10] / u_log [T,B] inject the MoL sampler's uniforms (None = device RNG);
+        'mulaw-quantize': u_log [T,B] the uniforms of tf.multinomial, y the drawn class through
+        inv_mulaw_quantize (wavenet.py:450-452), test_inputs class indices."""
         hp = self._hparams
         self.is_training = x is not None
         self.is_evaluating = not self.is_training and y is not None
@@ -118,8 +117,27 @@ class WaveNet():
             raise NotImplementedError("WaveNet training / eval-loss graphs are not on the synthesis "
                                       "path")
         self._check_path()
-        if c is None:
-            raise NotImplementedError("synthesis without local conditioning is not built")
+        if c is None:   # wavenet.py:410-411: synthesis_length samples without a local condition
+            if self.local_conditioning_enabled():
+                raise ValueError("cin_channels > 0: the local condition c is required")
+            if synthesis_length is None:
+                raise ValueError("unconditional synthesis needs synthesis_length")
+            B = 1 if test_inputs is None else np.asarray(test_inputs).reshape(
+                -1, int(synthesis_length)).shape[0]
+            if g is not None:
+                B = np.asarray(g).reshape(-1, max(hp.gin_channels, 1) if not np.issubdtype(
+                    np.asarray(g).dtype, np.integer) else 1).shape[0]
+            T = int(synthesis_length)
+            ti = None if test_inputs is None else np.asarray(test_inputs, np.float32).reshape(B, T)
+            out = self._get_engine(B, T).generate_unconditional(
+                B, T, u_mix, u_log, seed, ti, g=g if self.global_conditioning_enabled() else None)
+            y = out["y"]
+            if is_mulaw(hp.input_type):
+                y = inv_mulaw(y, hp.quantize_channels).astype(np.float32)
+            self.tower_y_hat = [y]
+            self.tower_synth_upsampled_local_features = [None]
+            self.tower_mix_indices = [out["k"]]
+            return
         c = np.asarray(c, np.float32)
         if c.ndim != 3 or c.shape[2] != hp.cin_channels:
             raise ValueError('Expected 3 dimension shape [batch_size(1), time_length, {}] for local '
@@ -159,9 +177,25 @@ class WaveNet():
         [batch_size, channels, time_length]).  c: [B, cin, T_frames] (channels first, as the
         reference passes it at wavenet.py:427) — upsampled inside, like the reference."""
         self._check_path()
-        if initial_input is not None and np.any(np.asarray(initial_input) != 0):
+        hp = self._hparams
+        if not is_scalar_input(hp.input_type):
+            # one_hot(mulaw_quantize(0)) = class 127 (wavenet.py:433-446)
+            if initial_input is not None:
+                ii = np.asarray(initial_input).reshape(-1, hp.quantize_channels)
+                if not np.all(np.argmax(ii, 1) == 127) or not np.all(ii.sum(1) == 1):
+                    raise NotImplementedError("initial_input must be one_hot(mulaw_quantize(0))")
+        elif initial_input is not None and np.any(np.asarray(initial_input) != 0):
             # the start silence of both scalar input types: 0.0 ('raw'), mulaw(0.0) = 0 ('mulaw')
             raise NotImplementedError("initial_input must be the silence value 0")
+        if c is None:
+            B = np.asarray(initial_input).shape[0] if initial_input is not None else 1
+            out = self._get_engine(B, int(time_length)).generate_unconditional(
+                B, int(time_length), u_mix, u_log, seed,
+                None if test_inputs is None else np.asarray(test_inputs, np.float32).reshape(B, -1),
+                want_logits=return_logits, g=g if self.global_conditioning_enabled() else None)
+            self.upsampled_local_features = None
+            y = self._incremental_outputs(out)
+            return (y, out["logits"]) if return_logits else y
         if abs(log_scale_min - self._hparams.log_scale_min) > 1e-6:
             raise ValueError("log_scale_min must equal hparams.log_scale_min on this build")
         c = np.asarray(c, np.float32).transpose(0, 2, 1)
@@ -171,5 +205,16 @@ class WaveNet():
             want_logits=return_logits, want_upsampled=True,
             g=g if self.global_conditioning_enabled() else None)
         self.upsampled_local_features = out["upsampled"]
-        y = out["y"][:, None, :]
+        y = self._incremental_outputs(out)
         return (y, out["logits"]) if return_logits else y
+
+    def _incremental_outputs(self, out):
+        """[B, channels, T]: the samples ([B, 1, T]) or, for 'mulaw-quantize', the one-hot draws
+        [B, quantize_channels, T] (wavenet.py:866-874, 911)"""
+        hp = self._hparams
+        if is_scalar_input(hp.input_type):
+            return out["y"][:, None, :]
+        k = out["k"]
+        oh = np.zeros((k.shape[0], hp.quantize_channels, k.shape[1]), np.float32)
+        np.put_along_axis(oh, k[:, None, :].astype(np.int64), 1.0, axis=1)
+        return oh
