@@ -18,7 +18,8 @@ constexpr int PD_NPJ = 96;    // frame (80) + stop (1) columns, padded to 16
 constexpr int PD_NPF = 352;   // + the prenet-L1 columns folded into the projection
 constexpr int PD_NTILE = 22;  // projection column tiles
 constexpr int PD_KSP = 8;     // projection K split (128 h2 rows + 64 context rows per split)
-constexpr int PD_TMAX = 256;  // max encoder steps (T_in)
+constexpr int PD_TMAX = 256;  // encoder steps of the values slice held in registers (k_decode_persist<., 256>)
+constexpr int PD_TMAX_LONG = 512;  // max encoder steps: T_in > 256 runs k_decode_persist<false, 512>
 constexpr int PD_KLP = 32;    // location-conv taps padded to 16
 constexpr int PD_NREP = 8;    // replicas of the H1/H2 flag lines (32 pollers per line)
 // Hidden unit q (0..3) of LSTM tile g: the four units of a tile are the four components of one AF
@@ -59,14 +60,14 @@ struct PdArgs {
   const float* pre_w2t; // [256 out][256 in] prenet layer-2 kernel, transposed
   const float* pre_b2;  // [256]
   const float* TP1;     // GTA: [B][T_lim][256] targets·W1 + b1 (AF-group order), or null
-  const float* keysT;   // [B][128][256] keys (+ b_a + b_conv·W_loc), encoder step fastest
-  const float* valuesT; // [B][512][256] encoder half of the values, encoder step fastest, 0 past T_in
+  const float* keysT;   // [B][128][TM] keys (+ b_a + b_conv·W_loc), encoder step fastest (TM = 256 | 512)
+  const float* valuesT; // [B][512][TM] encoder half of the values, encoder step fastest, 0 past T_in
   const int* lengths;   // [B]
   const uint8_t* masks; // [max_iters][2][B][256] prenet keep bits
   // exchange buffers, two step parities each
   float* H1x;   // [2][32 x 1024] AF: h1_new
   float* H2x;   // [2][32 x 1024] AF: h2_new
-  unsigned long long* Eg;  // [2][32 rows][8 slices][256 t] {tag, partial energy} granules
+  unsigned long long* Eg;  // [2][32 rows][8 slices][TM t] {tag, partial energy} granules
   float* CTXx;  // [2][32 x 512] AF: context_enc
   float* SSx;   // [2][32]: Σ_{t<len} alignments (style-context scale)
   unsigned long long* PPg; // [2][8 splits][32 rows][352] {tag, projection partial} granules
@@ -98,6 +99,7 @@ struct PdArgs {
 size_t pd_lds_bytes();
 // True when this device can keep all PD_NB work-groups resident at once.
 bool pd_device_ok(int dev);
-void pd_launch(const PdArgs& a, hipStream_t s, bool emt = false);
+// tm: 256, or 512 for T_in > 256 (no emotion attention)
+void pd_launch(const PdArgs& a, hipStream_t s, bool emt = false, int tm = PD_TMAX);
 
 }  // namespace tt2

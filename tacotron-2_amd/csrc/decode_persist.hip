@@ -324,8 +324,16 @@ __device__ __forceinline__ void tail_bar(int* ctr, unsigned& gen, int lane) {
     if (stp && tid == 0) stp[g * 32 + (i)] = __builtin_amdgcn_s_memrealtime();        \
   } while (0)
 
-template <bool EMT>
+// TM: encoder steps covered (256, or 512 for T_in > 256).  TM = 512 keeps the values of positions
+// [0, 256) resident like TM = 256 and streams those of [256, 512) from L2 / MALL every step (issued
+// ahead of the energy take); its alignments live in the stage scratch (red + 2048: free during the
+// softmax / context stage) so the cumulative alignments can take their place (15 + 512 + 17 floats).
+template <bool EMT, int TM>
 __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
+  static_assert(TM == PD_TMAX || (TM == PD_TMAX_LONG && !EMT), "k_decode_persist geometry");
+  constexpr int NI = TM / 128;          // 16-position key / location tiles per wave
+  constexpr int NWE = TM / 64;          // waves holding one energy per lane in the softmax
+  constexpr int CWN = TM == PD_TMAX ? 288 : 544;  // cumulative-alignment floats (zero padded)
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* const sW1h = sm;              // [64 kg][64 lanes] f32x4: W1 recurrent rows of this tile
   float* const sW2h = sm + 16384;      // same for W2
@@ -336,8 +344,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   float* const RGc = RG2 + 512;        // [32][16] context rows of the next L1
   float* const PPh = RGc + 512;        // [32][16] projection partial, h2 rows (proj blocks)
   float* const cw = PPh + 512;         // [15 + T + 16] cumulative alignments, zero padded (location conv)
-  float* const al = cw + 288;          // [256] alignments of the step
-  float* const x1 = al + 256;          // [256] prenet layer-1 output of the row
+  float* const al = TM == PD_TMAX ? cw + 288 : red + 2048;  // [TM] alignments of the step
+  float* const x1 = cw + 544;          // [256] prenet layer-1 output of the row
   float* const ssa = x1 + 256;         // [32] Σ_{t<len} align of every row (last step)
   float* const qv = ssa + 32;          // [16] query slice
   float* const sc = qv + 16;           // softmax max / sum, Σ_{t<len} align of this row
@@ -419,8 +427,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   const int len = rowv ? a.lengths[b] : 0;
   const float va_k = a.va[16 * j + (lane & 15)];
   const float b2p = a.pre_b2[32 * j + (tid & 31)];
-  for (int e = tid; e < 288; e += PD_NT) cw[e] = 0.f;
-  if (tid < 256) al[tid] = 0.f;
+  for (int e = tid; e < CWN; e += PD_NT) cw[e] = 0.f;
+  if (tid < TM) al[tid] = 0.f;
   if (tid < 32) ssa[tid] = 0.f;
   if (tid == 0) {
     si[0] = 0;
@@ -428,14 +436,16 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     si[8] = 0;
     sc[2] = 0.f;
   }
-  f32x4 vals[8];  // values[b][32*(tid/64) + 4i + e][64j + tid%64]: valuesT is [B][E2][256], 0 past T_in
+  f32x4 vals[8];  // values[b][32*(tid/64) + 4i + e][64j + tid%64]: valuesT is [B][E2][TM], 0 past T_in
   {
-    const f32x4* V = reinterpret_cast<const f32x4*>(a.valuesT + ((long)(rowv ? b : 0) * PD_E2 + 64 * j + (tid & 63)) * PD_TMAX +
+    const f32x4* V = reinterpret_cast<const f32x4*>(a.valuesT + ((long)(rowv ? b : 0) * PD_E2 + 64 * j + (tid & 63)) * TM +
                                                     32 * (tid >> 6));
 #pragma unroll
     for (int i = 0; i < 8; ++i) vals[i] = V[i];
   }
-  f32x4 loc[2] = {zero4, zero4};  // location features of the next step (cum = 0)
+  f32x4 loc[NI];  // location features of the next step (cum = 0)
+#pragma unroll
+  for (int i = 0; i < NI; ++i) loc[i] = zero4;
   f32x4 accC0 = zero4, accC1 = zero4;  // L1 context rows of the next step (context(-1) = 0)
   if constexpr (EMT) {  // the emotion block of step 0 (zero_state: refnet_spk alone), host-written at parity 1
     const float* XE = a.EMTx + 32 * PD_EQ;
@@ -693,11 +703,11 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) wq[i] = Q[i];
     }
-    f32x4 kv[2];  // keys[b][t0 + r][16j + lane%16], t0 = 16(w + 8i) + 4(lane/16): keysT is [B][A][256]
+    f32x4 kv[NI];  // keys[b][t0 + r][16j + lane%16], t0 = 16(w + 8i) + 4(lane/16): keysT is [B][A][TM]
     {
-      const f32x4* K = reinterpret_cast<const f32x4*>(a.keysT + ((long)(rowv ? b : 0) * PD_A + 16 * j + (lane & 15)) * PD_TMAX);
+      const f32x4* K = reinterpret_cast<const f32x4*>(a.keysT + ((long)(rowv ? b : 0) * PD_A + 16 * j + (lane & 15)) * TM);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) kv[i] = K[(w + 8 * i) * 4 + (lane >> 4)];
+      for (int i = 0; i < NI; ++i) kv[i] = K[(w + 8 * i) * 4 + (lane >> 4)];
     }
     rec_half(PD_F_H1, a.H1x + p * 32 * PD_H, tb, sW1h, 0, q1a, q1b, w, lane, false);  // RG1(t+1) from h1_new(t), 1st half
     PD_STAMP(6);
@@ -729,14 +739,14 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       float qk = 0.f;
 #pragma unroll
       for (int ww = 0; ww < 8; ++ww) qk += red[1024 + ww * 16 + (lane & 15)];
-      unsigned long long* E = a.Eg + (((long)p * 32 + b) * 8 + j) * PD_TMAX;
+      unsigned long long* E = a.Eg + (((long)p * 32 + b) * 8 + j) * TM;
       // after sum16 every lane of group q = lane/16 holds the energies of positions 4q + r; one
-      // shuffle gathers position l (l < 16) of i = 0 on lane l and of i = 1 on lane 16 + l, so the
-      // 32 granules leave as ONE store instruction of two whole 128-B lines (not 8 stores of 4
-      // lanes at a 32-B stride, each its own fabric write)
-      float sel[2];
+      // shuffle gathers position l (l < 16) of tile i on lane 16 i + l, so the 16 NI granules leave
+      // as ONE store instruction of whole 128-B lines (not 4 NI stores of 4 lanes at a 32-B stride,
+      // each its own fabric write)
+      float sel[NI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NI; ++i) {
         float e4[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) e4[r] = sum16(va_k * tanh_fast(kv[i][r] + qk + loc[i][r]));
@@ -744,8 +754,13 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         sel[i] = rr == 0 ? e4[0] : rr == 1 ? e4[1] : rr == 2 ? e4[2] : e4[3];
       }
       const int src = ((lane >> 2) & 3) * 16 + (lane & 3);
-      const float v0 = __shfl(sel[0], src), v1 = __shfl(sel[1], src);
-      if (lane < 32) pd_put(E + (w + 8 * (lane >> 4)) * 16 + (lane & 15), tg, lane < 16 ? v0 : v1);
+      float vi[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) vi[i] = __shfl(sel[i], src);
+      float vo = vi[0];
+#pragma unroll
+      for (int i = 1; i < NI; ++i) vo = (lane >> 4) == i ? vi[i] : vo;
+      if (lane < 16 * NI) pd_put(E + (w + 8 * (lane >> 4)) * 16 + (lane & 15), tg, vo);
     }
     __syncthreads();  // red / qv reuse below
     if (si[8]) return;
@@ -769,15 +784,24 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     // ================= D: softmax, cumulative alignments, context (attention.py:10-35, 202-227) ==========
     PD_STAMP(9);
     if (rowv) {
-      const unsigned long long* E = a.Eg + ((long)p * 32 + b) * 8 * PD_TMAX;
+      const unsigned long long* E = a.Eg + ((long)p * 32 + b) * 8 * TM;
+      // TM = 512: the values of positions [256 + 32 (tid/64), +32) of channel 64j + tid%64 for the
+      // context below, in flight across the energy take and the softmax
+      f32x4 vhi[TM == PD_TMAX ? 1 : 8];
+      if constexpr (TM != PD_TMAX) {
+        const f32x4* V = reinterpret_cast<const f32x4*>(a.valuesT + ((long)(rowv ? b : 0) * PD_E2 + 64 * j + (tid & 63)) * TM +
+                                                        PD_TMAX + 32 * (tid >> 6));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vhi[i] = V[i];
+      }
       if (tid == 0) si[5] = 1;
       __syncthreads();
-      // waves 0..3 hold one energy per lane; max and sum as wave shuffles + one LDS exchange of the
-      // four wave results each
+      // waves 0..NWE-1 hold one energy per lane; max and sum as wave shuffles + one LDS exchange of
+      // the wave results each
       float e = -INFINITY;
-      if (tid < PD_TMAX) {
+      if (tid < TM) {
         float ev[8];
-        if (!pd_take<8>(a, PD_F_E, E, tid, PD_TMAX, tg, tid < T, ev)) si[5] = 0;
+        if (!pd_take<8>(a, PD_F_E, E, tid, TM, tg, tid < T, ev)) si[5] = 0;
         if (tid < T) {
           e = 0.f;
 #pragma unroll
@@ -798,8 +822,9 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       __syncthreads();
       if (!si[5]) return;
       float ex = 0.f;
-      if (tid < PD_TMAX) {
-        const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      if (tid < TM) {
+        float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        if constexpr (NWE == 8) mx = fmaxf(mx, fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7])));
         ex = tid < T ? expf(e - mx) : 0.f;
         float sum = ex;
         for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
@@ -807,7 +832,11 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       }
       __syncthreads();
       PD_STAMP(21);
-      if (tid < PD_TMAX) al[tid] = tid < T ? ex / ((red[8] + red[9]) + (red[10] + red[11])) : 0.f;
+      if (tid < TM) {
+        float den = (red[8] + red[9]) + (red[10] + red[11]);
+        if constexpr (NWE == 8) den += (red[12] + red[13]) + (red[14] + red[15]);
+        al[tid] = tid < T ? ex / den : 0.f;
+      }
       __syncthreads();
       if (tid < T) {
         const float cp = cw[15 + tid];
@@ -843,6 +872,10 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < 32; ++i) s += al[ts * 32 + i] * vals[i >> 2][i & 3];
+        if constexpr (TM != PD_TMAX) {
+#pragma unroll
+          for (int i = 0; i < 32; ++i) s += al[PD_TMAX + ts * 32 + i] * vhi[i >> 2][i & 3];
+        }
         red[ts * 64 + c] = s;
       }
       __syncthreads();
@@ -865,7 +898,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     rec_half(PD_F_H1, a.H1x + p * 32 * PD_H, tb, sW1h, 1, q1a, q1b, w, lane, false);  // RG1(t+1), 2nd half
     // location features of step t+1: im2col(cum) · (W_conv·W_loc) on MFMA (attention.py:59-62)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int t0 = (w + 8 * i) * 16 + (lane & 15) + (lane >> 4);
       f32x4 l = zero4;
 #pragma unroll
@@ -1131,25 +1164,31 @@ bool pd_device_ok(int dev) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   if (prop.multiProcessorCount < PD_NB) return false;
-  for (const void* k : {reinterpret_cast<const void*>(k_decode_persist<false>),
-                        reinterpret_cast<const void*>(k_decode_persist<true>)})
+  for (const void* k : {reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX>),
+                        reinterpret_cast<const void*>(k_decode_persist<true, PD_TMAX>),
+                        reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX_LONG>)})
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pd_lds_bytes()) != hipSuccess)
       return false;
-  int nb = 0, ne = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_persist<false>, PD_NT, pd_lds_bytes()) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&ne, k_decode_persist<true>, PD_NT, pd_lds_bytes()) != hipSuccess)
+  int nb = 0, ne = 0, nl = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_persist<false, PD_TMAX>, PD_NT, pd_lds_bytes()) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&ne, k_decode_persist<true, PD_TMAX>, PD_NT, pd_lds_bytes()) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nl, k_decode_persist<false, PD_TMAX_LONG>, PD_NT, pd_lds_bytes()) !=
+          hipSuccess)
     return false;
-  return nb >= 1 && ne >= 1;
+  return nb >= 1 && ne >= 1 && nl >= 1;
 }
 
 // Cooperative launch: the runtime guarantees every one of the PD_NB work-groups is resident at
 // once (or fails the launch) -- the spin-waits of the hand-offs depend on it, and a plain launch
 // could be starved of CUs by a concurrent kernel on another stream or context.
-void pd_launch(const PdArgs& a, hipStream_t s, bool emt) {
+void pd_launch(const PdArgs& a, hipStream_t s, bool emt, int tm) {
+  TT2_CHECK(tm == PD_TMAX || (tm == PD_TMAX_LONG && !emt), TT2_ERR_INVALID_ARG, "persistent decoder: unsupported geometry");
+  TT2_CHECK(a.T_in >= 1 && a.T_in <= tm, TT2_ERR_INVALID_ARG, "persistent decoder: T_in outside the kernel's range");
   PdArgs arg = a;
   void* params[] = {&arg};
-  const void* k = emt ? reinterpret_cast<const void*>(k_decode_persist<true>)
-                      : reinterpret_cast<const void*>(k_decode_persist<false>);
+  const void* k = emt ? reinterpret_cast<const void*>(k_decode_persist<true, PD_TMAX>)
+                  : tm == PD_TMAX ? reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX>)
+                                  : reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX_LONG>);
   TT2_HIP(launch_persistent(k, dim3(PD_NB), dim3(PD_NT), params, (unsigned)pd_lds_bytes(), s));
 }
 

@@ -1227,7 +1227,7 @@ __global__ void k_af_rows(const float* __restrict__ src, int C, float* __restric
   for (int n = threadIdx.x; n < C; n += blockDim.x) dst[af_idx(b, n)] = src[(long)b * C + n];
 }
 
-__global__ void k_transpose_bt(const float* __restrict__ src, long ld, float* __restrict__ dst, int T, int C) {
+__global__ void k_transpose_bt(const float* __restrict__ src, long ld, float* __restrict__ dst, int T, int C, int ldt) {
   __shared__ float tile[32][33];
   const int b = blockIdx.z, c0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
@@ -1236,7 +1236,7 @@ __global__ void k_transpose_bt(const float* __restrict__ src, long ld, float* __
     tile[r][tx] = t < T ? src[((long)b * T + t) * ld + c0 + tx] : 0.f;
   }
   __syncthreads();
-  for (int r = ty; r < 32; r += 8) dst[((long)b * C + c0 + r) * 256 + t0 + tx] = tile[tx][r];
+  for (int r = ty; r < 32; r += 8) dst[((long)b * C + c0 + r) * ldt + t0 + tx] = tile[tx][r];
 }
 
 // step-major alignments [B][n][T] -> the reference layout [B][T][ldt] (tower_alignments), columns < n
@@ -2262,7 +2262,7 @@ static bool pd_emt(const tt2_ctx* c) {
 
 static bool pd_fits(tt2_ctx* c) {
   return (!c->emt.on() || pd_emt(c)) && c->pd_mode == 1 && c->pd_dev_ok && c->kg_wmax_dec < KG_BMAX && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
-         c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= PD_TMAX && c->B <= 32 &&
+         c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= (c->emt.on() ? PD_TMAX : PD_TMAX_LONG) && c->B <= 32 &&
          !c->cfg.smoothing;
 }
 
@@ -2272,7 +2272,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     c->pd_ctl.alloc(sizeof(unsigned) * (2 * PD_NPH * PD_NB + 32 + 3 * PD_NREP * PD_NB));
     c->H1x.alloc(2L * 32 * PD_H * 4);
     c->H2x.alloc(2L * 32 * PD_H * 4);
-    c->Ex.alloc(2L * 32 * 8 * PD_TMAX * 8);
+    c->Ex.alloc(2L * 32 * 8 * PD_TMAX_LONG * 8);
     c->CTXx.alloc(2L * 32 * PD_E2 * 4);
     c->SSx.alloc(2L * 32 * 4);
     c->PPx.alloc(2L * PD_KSP * 32 * PD_NPF * 8);
@@ -2287,17 +2287,20 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     c->EMTx.alloc(2L * 32 * PD_EQ * 4);
   }
   const auto& cfg = c->cfg;
-  c->keysT.alloc(sizeof(float) * (size_t)cfg.max_batch * PD_A * PD_TMAX);
-  c->valuesT.alloc(sizeof(float) * (size_t)cfg.max_batch * PD_E2 * PD_TMAX);
-  hipLaunchKernelGGL(k_transpose_bt, dim3(PD_TMAX / 32, PD_A / 32, c->B), dim3(256), 0, s, c->keys.as<float>(),
-                     (long)PD_A, c->keysT.as<float>(), c->T_in, PD_A);
-  hipLaunchKernelGGL(k_transpose_bt, dim3(PD_TMAX / 32, PD_E2 / 32, c->B), dim3(256), 0, s, c->values.as<float>(),
-                     (long)c->Dm, c->valuesT.as<float>(), c->T_in, PD_E2);
+  // encoder steps the kernel covers: the values slice of 256 positions lives in registers; longer
+  // inputs run the TM = 512 instance (the upper 256 positions streamed per step)
+  const int tm = c->T_in > PD_TMAX ? PD_TMAX_LONG : PD_TMAX;
+  c->keysT.alloc(sizeof(float) * (size_t)cfg.max_batch * PD_A * PD_TMAX_LONG);
+  c->valuesT.alloc(sizeof(float) * (size_t)cfg.max_batch * PD_E2 * PD_TMAX_LONG);
+  hipLaunchKernelGGL(k_transpose_bt, dim3(tm / 32, PD_A / 32, c->B), dim3(256), 0, s, c->keys.as<float>(),
+                     (long)PD_A, c->keysT.as<float>(), c->T_in, PD_A, tm);
+  hipLaunchKernelGGL(k_transpose_bt, dim3(tm / 32, PD_E2 / 32, c->B), dim3(256), 0, s, c->values.as<float>(),
+                     (long)c->Dm, c->valuesT.as<float>(), c->T_in, PD_E2, tm);
   TT2_HIP(hipGetLastError());
   // flags + ctl words, every launch; granule tags restart at 1 every launch: a stale tag of an
   // earlier decode must never match.  The self-tagged h1 / h2 / context / Σ-align buffers are zeroed
   // too (tag bit 0, which steps 0 and 1 never expect: decode_persist.hip pd_tb)
-  zero_many({{c->pd_ctl.p, c->pd_ctl.bytes}, {c->Ex.p, c->Ex.bytes}, {c->PPx.p, c->PPx.bytes},
+  zero_many({{c->pd_ctl.p, c->pd_ctl.bytes}, {c->Ex.p, 2ul * 32 * 8 * tm * 8}, {c->PPx.p, c->PPx.bytes},
              {c->PREx.p, c->PREx.bytes}, {c->H1x.p, c->H1x.bytes}, {c->H2x.p, c->H2x.bytes},
              {c->CTXx.p, c->CTXx.bytes}, {c->SSx.p, c->SSx.bytes}}, s);
   if (emt) {
@@ -2356,7 +2359,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     a.stamp_step = atoi(st);
   }
   TT2_HIP(hipEventRecord(c->pd_ev[0], s));
-  pd_launch(a, s, emt);
+  pd_launch(a, s, emt, tm);
   TT2_HIP(hipEventRecord(c->pd_ev[1], s));
   int h[4];
   TT2_HIP(hipMemcpyAsync(h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));

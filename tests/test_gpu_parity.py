@@ -299,6 +299,56 @@ def test_persistent_repeat_calls_after_early_stop(full_setup):
     np.testing.assert_allclose(again["alignments"], ref["alignments"], atol=MEL_TOL)
 
 
+@pytest.mark.parametrize("B,T,n,constraint", [(8, 300, 30, False), (3, 512, 20, True), (32, 257, 12, False)])
+def test_persistent_long_inputs_match_oracle(full_setup, B, T, n, constraint):
+    """T_in > 256 on the persistent decoder (k_decode_persist<false, 512>: values of positions
+    [256, T_in) streamed per step, cumulative alignments over 512 + 31 taps): ragged rows, the
+    window constraint at T_in = 512, and the 257 boundary with a full 32-row batch, against the
+    oracle (attention.py:170-227 has no length cliff)."""
+    hp, W = full_setup
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=T)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=T)
+    eng = _engine(hp, W, B, T, 64, n, constraint)
+    out = eng.synthesize(ids, lens, re, rs, n, masks)
+    assert _persistent(eng), "k_decode_persist not used at T_in = %d" % T
+    eng.close()
+    ref = TR.synthesize(ids, lens, re, rs, W, oracle_hp(hp, constraint), masks, n)
+    assert int(lens.max()) > 256
+    assert out["frames"].shape == ref["decoder_output"].shape
+    np.testing.assert_allclose(out["stop_token_prediction"], ref["stop_token_prediction"], atol=MEL_TOL)
+    np.testing.assert_allclose(out["alignments"], ref["alignments"], atol=MEL_TOL)
+    np.testing.assert_allclose(out["decoder_output"], ref["decoder_output"], atol=MEL_TOL)
+    np.testing.assert_allclose(out["mel_outputs"], ref["mel_outputs"], atol=MEL_TOL)
+
+
+def test_persistent_long_inputs_match_launch_path(full_setup):
+    """T_in = 300 over 400 steps: the long-input persistent decoder against the per-step launch
+    path (the attention walks past position 256 within the horizon)."""
+    import os
+    hp, W = full_setup
+    B, T, n = 32, 300, 400
+    ids, lens, re, rs = tacotron_inputs(B, T, 64, seed=77)
+    masks = prenet_masks(n, B, hp.prenet_layers[0], seed=77)
+    eng = _engine(hp, W, B, T, 64, n)
+    a = eng.synthesize(ids, lens, re, rs, n, masks)
+    assert _persistent(eng)
+    a = eng.synthesize(ids, lens, re, rs, n, masks)  # timed second launch
+    print("T_in=%d persistent decoder: %.2f us/step" % (T, 1e3 * eng.decoder_path()[1] / a["frames"].shape[1]))
+    eng.close()
+    os.environ["TT2_DECODER"] = "launch"
+    try:
+        eng2 = _engine(hp, W, B, T, 64, n)
+    finally:
+        del os.environ["TT2_DECODER"]
+    b = eng2.synthesize(ids, lens, re, rs, n, masks)
+    assert not _persistent(eng2)
+    eng2.close()
+    assert a["frames"].shape == b["frames"].shape
+    np.testing.assert_allclose(a["stop_token_prediction"], b["stop_token_prediction"], atol=1e-4)
+    np.testing.assert_allclose(a["alignments"], b["alignments"], atol=1e-4)
+    np.testing.assert_allclose(a["decoder_output"], b["decoder_output"], atol=1e-4)
+
+
 def test_persistent_matches_launch_path_long(full_setup):
     """1000-step horizon at configs[1] shapes: persistent decoder vs the per-step launch path
     (both HIP; the oracle is too slow for 1000 steps x 32 rows in a unit test)."""
