@@ -473,6 +473,13 @@ typedef struct tt2_train_config {
    * are the style embeddings (no style tokens / attention variables; memory_dim = 2*U + (emt_only ?
    * 1 : 2) * 128) */
   int use_gst;
+  /* args.adain (tacotron.py:236-242, 266-268; modules.py:66-107): ReferenceEncoderAdaIn 'refnet' in
+   * training mode -- the speaker and emotion mels through two conv2d + ReLU stacks without batch
+   * norm (strides (2,2),(2,2),(1,1)x4; variables refnet/conv2d_i/conv2d/* speaker, conv2d_1/*
+   * emotion), the speaker map restyled by the emotion map's per-channel moments, one GRU + dense
+   * tanh; its 128-wide output is the style embedding (memory_dim = 2*encoder_lstm_units + 128).
+   * Needs both references, no style classifiers / orthogonality loss (the reference builds none). */
+  int adain;
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;

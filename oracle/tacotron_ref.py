@@ -227,16 +227,19 @@ def gst_attention(ref, W, tag, num_heads=4, dt=np.float32):
 
 def reference_encoder_adain(mel_spk, mel_emt, W, dt=np.float32, scope="refnet/"):
     """ReferenceEncoderAdaIn.__call__ (modules.py:75-107) with strides (2,2),(2,2),(1,1)x4
-    (tacotron.py:237): shared conv2d + ReLU stack without batch norm on both mels; per sample and
+    (tacotron.py:237): conv2d + ReLU stacks without batch norm on both mels; per sample and
     channel moments over (time, freq); spk_norm = tf.nn.batch_normalization(spk, mean_spk, var_spk,
     offset=mean_emt, scale=var_emt, 1e-9); spk = 0.9·spk + 0.1·spk_norm; GRU over every frame;
-    last output -> Dense(128, tanh)."""
+    last output -> Dense(128, tanh).  Both stacks call conv2d(..., 'conv2d_%d' % i) in the same
+    variable scope, speaker first (modules.py:84-87): tf.layers.conv2d's default layer name is
+    uniquified inside the re-entered scope, so the speaker stack owns conv2d_i/conv2d/* and the
+    emotion stack conv2d_i/conv2d_1/* (two weight sets, not one shared)."""
     strides = [(2, 2), (2, 2), (1, 1), (1, 1), (1, 1), (1, 1)]
     xs = [np.asarray(m, dt)[..., None] for m in (mel_spk, mel_emt)]
     for i in range(6):
         s = scope + "conv2d_{}/".format(i)
-        k, b = _w(W, s + "conv2d/kernel", dt), _w(W, s + "conv2d/bias", dt)
-        xs = [np.maximum(conv2d_same(x, k, b, strides[i]), dt(0)) for x in xs]
+        xs = [np.maximum(conv2d_same(x, _w(W, s + ly + "/kernel", dt), _w(W, s + ly + "/bias", dt), strides[i]),
+                         dt(0)) for x, ly in zip(xs, ("conv2d", "conv2d_1"))]
     spk, emt = xs
     m_s = spk.mean(axis=(1, 2), keepdims=True)
     v_s = np.square(spk - m_s).mean(axis=(1, 2), keepdims=True)

@@ -218,10 +218,12 @@ RN = P + "refnet_{}/"
 MH = P + "Multihead-attention-{}/"
 
 
-def frontend_var_names(emt_only=False, conv_layers=3, ref_layers=6, use_gst=True):
+def frontend_var_names(emt_only=False, conv_layers=3, ref_layers=6, use_gst=True, adain=False):
     """Trainable front-end variables (tacotron.py:215-308, modules.py:9-64,251-323,
     multihead_attention.py:35-132), in the library's flat-buffer order.  use_gst=False: no style
-    tokens / style attention (tacotron.py:284-291)."""
+    tokens / style attention (tacotron.py:284-291).  adain: ReferenceEncoderAdaIn's 'refnet'
+    (modules.py:66-107): per layer the speaker conv (conv2d_i/conv2d) and the emotion conv
+    (conv2d_i/conv2d_1, tf.layers' uniquified default name), no batch norm, one GRU + dense."""
     names = [P + "inputs_embedding"]
     for i in range(1, conv_layers + 1):
         s = EC.format(i)
@@ -229,6 +231,14 @@ def frontend_var_names(emt_only=False, conv_layers=3, ref_layers=6, use_gst=True
                   s + "batch_normalization/beta"]
     for d in ("fw", "bw"):
         names += [EL.format(d) + "kernel", EL.format(d) + "bias"]
+    if adain:
+        r = P + "refnet/"
+        for i in range(ref_layers):
+            for ly in ("conv2d", "conv2d_1"):
+                names += [r + "conv2d_{}/{}/kernel".format(i, ly), r + "conv2d_{}/{}/bias".format(i, ly)]
+        return names + [r + "rnn/gru_cell/gates/kernel", r + "rnn/gru_cell/gates/bias",
+                        r + "rnn/gru_cell/candidate/kernel", r + "rnn/gru_cell/candidate/bias",
+                        r + "dense/kernel", r + "dense/bias"]
     for tag in (("emt",) if emt_only else ("emt", "spk")):
         r = RN.format(tag)
         for i in range(ref_layers):
@@ -258,21 +268,21 @@ def _bn_train(a, gamma, beta, dims, eps=1e-3, moving=None):
     return gamma * (a - mean) / torch.sqrt(var + eps) + beta, (mean, var)
 
 
-def _conv2d_same_s2(x, k, b):
-    """tf.layers.conv2d 3x3 stride 2 padding='same' NHWC (odd pad bottom/right)."""
+def _conv2d_same_s2(x, k, b, st=2):
+    """tf.layers.conv2d 3x3 stride st (2 by default) padding='same' NHWC (odd pad bottom/right)."""
     N, H, Wd, C = x.shape
     outs = []
     pads = []
     for n, kk in ((H, k.shape[0]), (Wd, k.shape[1])):
-        o = -(-n // 2)
-        tot = max((o - 1) * 2 + kk - n, 0)
+        o = -(-n // st)
+        tot = max((o - 1) * st + kk - n, 0)
         pads.append((tot // 2, tot - tot // 2))
     xp = torch.nn.functional.pad(x, (0, 0, pads[1][0], pads[1][1], pads[0][0], pads[0][1]))
-    Ho, Wo = -(-H // 2), -(-Wd // 2)
+    Ho, Wo = -(-H // st), -(-Wd // st)
     cols = []
     for i in range(k.shape[0]):
         for j in range(k.shape[1]):
-            cols.append(xp[:, i:i + (Ho - 1) * 2 + 1:2, j:j + (Wo - 1) * 2 + 1:2, :])
+            cols.append(xp[:, i:i + (Ho - 1) * st + 1:st, j:j + (Wo - 1) * st + 1:st, :])
     cols = torch.cat(cols, -1)
     return cols @ k.reshape(-1, k.shape[3]) + b
 
@@ -346,8 +356,33 @@ def _gst(ref, W, tag, heads=4):
     return (w @ tok).reshape(N, -1)
 
 
+def _adain_refnet(W, ref_spk, ref_emt, dt):
+    """ReferenceEncoderAdaIn (modules.py:75-107) with strides (2,2),(2,2),(1,1)x4 (tacotron.py:237):
+    speaker and emotion stacks of conv2d + ReLU without batch norm (conv2d_i/conv2d, conv2d_i/conv2d_1),
+    per (row, channel) moments over (time, freq) (tf.nn.moments: biased variance), speaker map
+    0.9 x + 0.1 tf.nn.batch_normalization(x, m_s, v_s, offset=m_e, scale=v_e, 1e-9), GRU over every
+    frame, last output -> Dense(128, tanh)."""
+    r = P + "refnet/"
+    strides = (2, 2, 1, 1, 1, 1)
+    hs = [torch.as_tensor(np.asarray(m), dtype=dt)[..., None] for m in (ref_spk, ref_emt)]
+    for i in range(6):
+        s = r + "conv2d_{}/".format(i)
+        hs = [torch.relu(_conv2d_same_s2(h, W[s + ly + "/kernel"], W[s + ly + "/bias"], strides[i]))
+              for h, ly in zip(hs, ("conv2d", "conv2d_1"))]
+    spk, emt = hs
+    m_s = spk.mean(dim=(1, 2), keepdim=True)
+    v_s = ((spk - m_s) ** 2).mean(dim=(1, 2), keepdim=True)
+    m_e = emt.mean(dim=(1, 2), keepdim=True)
+    v_e = ((emt - m_e) ** 2).mean(dim=(1, 2), keepdim=True)
+    inv = v_e / torch.sqrt(v_s + 1e-9)
+    x = spk * 0.9 + (spk * inv + (m_e - m_s * inv)) * 0.1
+    N, T2, F2, C = x.shape
+    hl = _gru_last(x.reshape(N, T2, F2 * C), W, r)
+    return torch.tanh(hl @ W[r + "dense/kernel"] + W[r + "dense/bias"])
+
+
 def frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks=None, enc_zm=None, emt_only=False,
-                     eps=1e-3, moving=None, refs_out=None, use_gst=True):
+                     eps=1e-3, moving=None, refs_out=None, use_gst=True, adain=False):
     """Training-mode front end -> memory [B,T_in,D] (unmasked: the decoder masks it) and the batch
     statistics [(mean, var)] of every batch norm (encoder convs, then refnet convs).
     enc_masks [3, B, T_in, C] conv dropout keep bits (rate 0.5) or None; enc_zm [T_in, 2 (fw, bw),
@@ -382,6 +417,12 @@ def frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks=None, enc_zm=N
                    None if zm is None else zm[:, 1], True)
     parts = [fw, bw]
     B, T = x.shape[:2]
+    if adain:  # the speaker embedding of the AdaIN encoder is the style embedding (tacotron.py:266-268)
+        refo = _adain_refnet(W, ref_spk, ref_emt, dt)
+        if refs_out is not None:
+            refs_out.append(refo)
+        parts.append(refo[:, None, :].expand(B, T, refo.shape[1]))
+        return torch.cat(parts, -1), stats
     for tag, ref in (("emt", ref_emt),) + ((() if emt_only else (("spk", ref_spk),))):
         r = RN.format(tag)
         h = torch.as_tensor(np.asarray(ref), dtype=dt)[..., None]
@@ -439,19 +480,20 @@ def style_emb_losses(W, refs, emt_labels, spk_labels, n_emt=0, n_spk=0, orthog_w
 
 def train_grads_frontend(Wnp, ids, lengths, ref_emt, ref_spk, targets, stop_targets, prenet_masks,
                          zoneout_masks, enc_masks, enc_zm, reg_weight=1e-6, dtype=torch.float64,
-                         clip=(-4.1, 4.0), postnet_masks=None, emt_only=False, style=None, use_gst=True):
+                         clip=(-4.1, 4.0), postnet_masks=None, emt_only=False, style=None, use_gst=True,
+                         adain=False):
     """The whole configs[4] step: front end (training mode) -> memory -> decoder + Postnet; returns
     (losses, grads of every front-end, decoder and Postnet variable, [(mean, var)] batch stats of
     the front end's batch norms).  ``style`` = dict(emt_labels, spk_labels, n_emt, n_spk,
     orthog_weight) adds the style-embedding losses (style_emb_losses); the losses tuple then
     gains (loss_emt, loss_spk, loss_orthog)."""
     st_kw = dict(style or {})
-    names = (frontend_var_names(emt_only, use_gst=use_gst) + style_disc_var_names(emt_only, st_kw.get("n_emt", 0), st_kw.get("n_spk", 0))
+    names = (frontend_var_names(emt_only, use_gst=use_gst, adain=adain) + style_disc_var_names(emt_only, st_kw.get("n_emt", 0), st_kw.get("n_spk", 0))
              + train_var_names() + postnet_var_names())
     W = {n: torch.tensor(np.asarray(Wnp[n]), dtype=dtype, requires_grad=True) for n in names}
     refs = []
     mem, stats = frontend_forward(W, ids, lengths, ref_emt, ref_spk, enc_masks, enc_zm, emt_only, refs_out=refs,
-                                  use_gst=use_gst)
+                                  use_gst=use_gst, adain=adain)
     tg = torch.tensor(np.asarray(targets), dtype=dtype)
     st = torch.tensor(np.asarray(stop_targets), dtype=dtype)
     pm = torch.tensor(np.asarray(prenet_masks), dtype=dtype)

@@ -274,15 +274,15 @@ void bilstm(tt2_ctx* c, const float* x, int B, int T, int C, float* out) {
 // ReferenceEncoderAdaIn's (modules.py:75-87: conv + ReLU, no BN, strides (2,2),(2,2),(1,1)x4):
 // mel [B][TR][nm] -> NHWC [B][H][W][C]
 std::vector<float> conv_stack(tt2_ctx* c, const std::string& s, const float* mel, int B, int TR, bool adain, int& H,
-                              int& Wd, int& C) {
+                              int& Wd, int& C, const char* layer = "conv2d") {
   const auto& cfg = c->cfg;
   std::vector<float> x(mel, mel + (size_t)B * TR * c->nm), y;
   H = TR; Wd = c->nm; C = 1;
   for (int i = 0; i < 6; ++i) {
     const std::string s2 = s + "conv2d_" + std::to_string(i) + "/";
     const int f = cfg.reference_filters[i], st = adain && i >= 2 ? 1 : 2;
-    const auto& k = W(c, s2 + "conv2d/kernel", {3, 3, C, f});
-    const auto& bi = W(c, s2 + "conv2d/bias", {f});
+    const auto& k = W(c, s2 + layer + "/kernel", {3, 3, C, f});
+    const auto& bi = W(c, s2 + layer + "/bias", {f});
     BN bn;
     if (!adain) bn = bn_consts(c->wm, TP + s2, f);
     const int Ho = (H + st - 1) / st, Wo = (Wd + st - 1) / st;
@@ -456,7 +456,8 @@ void encode(tt2_ctx* c, const int* ids, const int* lengths, int B, int T, const 
   int H, Wd, C;
   if (c->style_mode == 2) {
     int He, We, Ce;
-    const std::vector<float> xe = conv_stack(c, "refnet/", ref[0], B, TR[0], true, He, We, Ce);
+    // the emotion stack's convs are conv2d_i/conv2d_1/* (weights.py _adain_refnet_specs)
+    const std::vector<float> xe = conv_stack(c, "refnet/", ref[0], B, TR[0], true, He, We, Ce, "conv2d_1");
     std::vector<float> xs = conv_stack(c, "refnet/", ref[1], B, TR[1], true, H, Wd, C);
     adain_mix(xs, xe, B, H * Wd, He * We, C);
     const auto r = gru_dense(c, "refnet/", xs.data(), B, H, Wd * C);

@@ -1528,6 +1528,17 @@ static void finalize(tt2_ctx* c) {
     }
     const int gin = F * ci, D = cfg.reference_depth;
     R.gin = gin;
+    if (adain) {  // the emotion stack's own convs: conv2d_i/conv2d_1/* (tf.layers default-name
+                  // uniquification in the re-entered scope, modules.py:84-87) -> ref[1]
+      int ce = 1;
+      for (int i = 0; i < 6; ++i) {
+        const std::string s2 = s + "conv2d_" + std::to_string(i) + "/";
+        const int f = cfg.reference_filters[i];
+        upload(c->ref[1].cw[i], need(wm, s2 + "conv2d_1/kernel", {3, 3, ce, f}));
+        upload(c->ref[1].cb[i], need(wm, s2 + "conv2d_1/bias", {f}));
+        ce = f;
+      }
+    }
     if (emt_model && r == 0) continue;
     {
       const auto& kg = need(wm, s + "rnn/gru_cell/gates/kernel", {gin + D, 2 * D});
@@ -2030,7 +2041,7 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
       const RefNetDev& R = c->ref[0];
       float* mv_e = c->adain_mv.as<float>();
       float* mv_s = mv_e + (size_t)cfg.max_batch * cfg.reference_filters[5] * 2;
-      float* xe = conv_stack(R, ref_d[0], T_ref[0], H, Wd, C);
+      float* xe = conv_stack(c->ref[1], ref_d[0], T_ref[0], H, Wd, C);  // emotion stack (conv2d_1 weights)
       hipLaunchKernelGGL(k_adain_moments, dim3(B, C), dim3(256), 0, sr, xe, H * Wd, C, mv_e);
       float* xs = conv_stack(R, ref_d[1], T_ref[1], H, Wd, C);
       hipLaunchKernelGGL(k_adain_moments, dim3(B, C), dim3(256), 0, sr, xs, H * Wd, C, mv_s);

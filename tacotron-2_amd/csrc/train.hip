@@ -98,6 +98,12 @@ struct tt2_train_ctx {
   // front end (cfg.frontend: encoder + reference encoders + GST, train_front.hip)
   int f_nref = 0, f_gin = 0, f_T2 = 0, f_T2max = 0;
   bool f_ran = false;
+  // cfg.adain (ReferenceEncoderAdaIn, modules.py:66-107): stacks r = 0 (emotion mel) and r = 1 (speaker
+  // mel) without batch norm, the speaker map restyled by the emotion map's moments, one GRU + dense
+  // (r = 1 buffers): fADX the restyled map (GRU input), fADM moments [2 (emt, spk)][B][C][2], fADS the
+  // backward's per-channel sums, fDYE the emotion stack's map gradient
+  bool f_adain = false;
+  DevBuf fADX, fADM, fADS, fDYE;
   DevBuf fTWf, fTWb, fHSh, fDZh;  // encoder BiLSTM fused steps: TF-layout weights and state / dZ shadows
   DevBuf fEX, fEA[8], fEY[9], fXP, fGZ, fGA, fCN, fCS, fHS, fENC, fMEM, fSTY, fDSTY, fDZ, fDHC, fDCC, fDHP, fdXP, fdA,
       fdB, fLWxT, fLWhT;
@@ -3295,7 +3301,14 @@ static void tr_regularize(tt2_train_ctx* c, hipStream_t s) {
 static std::string fe_conv_scope(int i) {
   return vn("encoder_convolutions/conv_layer_") + std::to_string(i) + "_encoder_convolutions/";
 }
-static std::string fe_ref_scope(int r) { return vn(r == 0 ? "refnet_emt/" : "refnet_spk/"); }
+static std::string fe_ref_scope(const tt2_train_ctx* c, int r) {
+  return vn(c->f_adain ? "refnet/" : r == 0 ? "refnet_emt/" : "refnet_spk/");
+}
+// conv layer scope of stack r in conv2d_i/: AdaIN's two stacks share 'refnet/conv2d_i' and
+// tf.layers uniquifies the second (emotion) layer's default name (modules.py:84-87)
+static std::string fe_ref_conv(const tt2_train_ctx* c, int r) { return c->f_adain && r == 0 ? "conv2d_1/" : "conv2d/"; }
+// stride of refnet layer i: (2, 2) everywhere, AdaIN (2,2),(2,2),(1,1)x4 (tacotron.py:237)
+static int fe_ref_stride(const tt2_train_ctx* c, int i) { return c->f_adain && i >= 2 ? 1 : 2; }
 static std::string fe_mh_scope(int r) { return vn(r == 0 ? "Multihead-attention-emt/" : "Multihead-attention-spk/"); }
 static std::string fe_lstm_scope(int d) {
   return vn(d == 0 ? "encoder_LSTM/bidirectional_rnn/fw/lstm_cell/" : "encoder_LSTM/bidirectional_rnn/bw/lstm_cell/");
@@ -3325,8 +3338,27 @@ static void tr_front_build_vars(tt2_train_ctx* c, const std::function<void(const
     addr(fe_lstm_scope(d) + "bias", {4 * U});
   }
   const int RD = f.reference_depth, tokd = f.style_embed_depth / f.num_heads, A = f.style_att_dim, dh = A / f.num_heads;
+  if (c->f_adain) {  // 'refnet' (modules.py:66-107): both conv stacks per layer, then GRU + dense
+    const std::string rs = fe_ref_scope(c, 1);
+    int ci = 1;
+    for (int i = 0; i < 6; ++i) {
+      const std::string s = rs + "conv2d_" + std::to_string(i) + "/";
+      for (int r = 1; r >= 0; --r) {  // speaker stack first (conv2d/), then emotion (conv2d_1/)
+        addr(s + fe_ref_conv(c, r) + "kernel", {3, 3, ci, f.reference_filters[i]});
+        addr(s + fe_ref_conv(c, r) + "bias", {f.reference_filters[i]});
+      }
+      ci = f.reference_filters[i];
+    }
+    addr(rs + "rnn/gru_cell/gates/kernel", {c->f_gin + RD, 2 * RD});
+    addr(rs + "rnn/gru_cell/gates/bias", {2 * RD});
+    addr(rs + "rnn/gru_cell/candidate/kernel", {c->f_gin + RD, RD});
+    addr(rs + "rnn/gru_cell/candidate/bias", {RD});
+    addr(rs + "dense/kernel", {RD, 128});
+    addr(rs + "dense/bias", {128});
+    return;
+  }
   for (int r = 0; r < c->f_nref; ++r) {
-    const std::string rs = fe_ref_scope(r);
+    const std::string rs = fe_ref_scope(c, r);
     int ci = 1;
     for (int i = 0; i < 6; ++i) {
       const std::string s = rs + "conv2d_" + std::to_string(i) + "/";
@@ -3413,10 +3445,10 @@ static void tr_front_alloc(tt2_train_ctx* c) {
   long wt_conv2d = 1;  // largest 3x3 conv2d kernel transpose [fo][9·ci]
   int H = f.max_T_ref, W = nm, ci = 1;
   for (int i = 0; i < 6; ++i) {
-    const int Ho = (H + 1) / 2, Wo = (W + 1) / 2, fo = f.reference_filters[i];
+    const int st = fe_ref_stride(c, i), Ho = (H + st - 1) / st, Wo = (W + st - 1) / st, fo = f.reference_filters[i];
     const long M = B * Ho * Wo;
     for (int r = 0; r < c->f_nref; ++r) {
-      a(c->fRA[r][i], M * fo);
+      a(c->fRA[r][i], c->f_adain ? 1 : M * fo);  // pre-BN activations (AdaIN: no batch norm)
       a(c->fRY[r][i], M * fo);
     }
     fbuf = std::max(fbuf, 9L * ci * M);
@@ -3433,6 +3465,12 @@ static void tr_front_alloc(tt2_train_ctx* c) {
     a(c->fGRH[r], T2 * B * RD); a(c->fHG[r], (T2 + 1) * B * RD); a(c->fREF[r], B * 128);
   }
   a(c->fGG, B * 2 * RD); a(c->fGC, B * RD);
+  if (c->f_adain) {
+    const long nmap = T2 * B * (long)W * ci;
+    a(c->fADX, nmap); a(c->fDYE, std::max(mmax, nmap));
+    a(c->fADM, 2L * B * ci * 2); a(c->fADS, (long)B * ci * 2);
+    mmax = std::max(mmax, nmap);
+  }
   a(c->fFBUF, fbuf); a(c->fDY, mmax); a(c->fDY2, mmax); a(c->fDZc, mmax);
   const int ntok = f.num_gst, tokd = f.style_embed_depth / f.num_heads, A = f.style_att_dim, dh = A / f.num_heads;
   a(c->fGq, B * A); a(c->fGkk, B * ntok * A); a(c->fGv, B * ntok * tokd); a(c->fGnv, B * dh); a(c->fGbb, B * dh);
@@ -3589,29 +3627,47 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
   const int RD = f.reference_depth;
   int nbn = f.enc_conv_layers;
   for (int r = 0; r < c->f_nref; ++r) {
-    const std::string rs = fe_ref_scope(r);
+    const std::string rs = fe_ref_scope(c, r);
     int H = T_ref, W = c->NM, ci = 1;
     const float* x = refs[r];
-    for (int i = 0; i < 6; ++i, ++nbn) {
+    for (int i = 0; i < 6; ++i) {
       const std::string sc = rs + "conv2d_" + std::to_string(i) + "/";
-      const int fo = f.reference_filters[i], Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+      const int st = fe_ref_stride(c, i);
+      const int fo = f.reference_filters[i], Ho = (H + st - 1) / st, Wo = (W + st - 1) / st;
       GemmArgs g;
       g.M = B * Ho * Wo; g.N = fo; g.K = 9 * ci; g.a_mode = A_CONV2D; g.A = x;
-      g.H = H; g.Wd = W; g.C = ci; g.Ho = Ho; g.Wo = Wo; g.kh = 3; g.kw2 = 3; g.sh = 2; g.sw = 2;
-      g.pt = std::max((Ho - 1) * 2 + 3 - H, 0) / 2; g.pl = std::max((Wo - 1) * 2 + 3 - W, 0) / 2;
-      g.Bw = pvar(c, sc + "conv2d/kernel"); g.ldb = fo; g.Cout = c->fRA[r][i].as<float>(); g.ldc = fo;
-      g.bias = pvar(c, sc + "conv2d/bias");
-      tr_gemm_run(g, s);
-      float* mean = BN + (long)nbn * 2 * 512;
-      float* var = mean + 512;
-      fe_stats(c, c->fRA[r][i].as<float>(), g.M, fo, mean, var, s);
-      fe_bn_relu_fwd(c->fRA[r][i].as<float>(), g.M, fo, mean, var, pvar(c, sc + "batch_normalization/gamma"),
-                     pvar(c, sc + "batch_normalization/beta"), eps, c->fRY[r][i].as<float>(), s);
+      g.H = H; g.Wd = W; g.C = ci; g.Ho = Ho; g.Wo = Wo; g.kh = 3; g.kw2 = 3; g.sh = st; g.sw = st;
+      g.pt = std::max((Ho - 1) * st + 3 - H, 0) / 2; g.pl = std::max((Wo - 1) * st + 3 - W, 0) / 2;
+      g.Bw = pvar(c, sc + fe_ref_conv(c, r) + "kernel"); g.ldb = fo; g.ldc = fo;
+      g.bias = pvar(c, sc + fe_ref_conv(c, r) + "bias");
+      if (c->f_adain) {  // conv2d(..., batch_norm=False): conv + ReLU (modules.py:84-87)
+        g.Cout = c->fRY[r][i].as<float>();
+        g.act = ACT_RELU;
+        tr_gemm_run(g, s);
+      } else {
+        g.Cout = c->fRA[r][i].as<float>();
+        tr_gemm_run(g, s);
+        float* mean = BN + (long)nbn * 2 * 512;
+        float* var = mean + 512;
+        fe_stats(c, c->fRA[r][i].as<float>(), g.M, fo, mean, var, s);
+        fe_bn_relu_fwd(c->fRA[r][i].as<float>(), g.M, fo, mean, var, pvar(c, sc + "batch_normalization/gamma"),
+                       pvar(c, sc + "batch_normalization/beta"), eps, c->fRY[r][i].as<float>(), s);
+        ++nbn;
+      }
       x = c->fRY[r][i].as<float>();
       H = Ho; W = Wo; ci = fo;
     }
     const int T2 = H, gin = W * ci;
     c->f_T2 = T2;
+    if (c->f_adain) {
+      // moments over (time, freq) per row and channel (modules.py:90-91); the speaker map (r = 1,
+      // after the emotion stack r = 0) restyled into fADX, which alone feeds the GRU (:94-104)
+      float* mv = c->fADM.as<float>() + (long)r * B * ci * 2;
+      fe_ad_moments(x, B, T2 * W, ci, mv, s);
+      if (r == 0) continue;
+      fe_ad_mix(x, B, T2 * W, ci, mv, c->fADM.as<float>(), c->fADX.as<float>(), s);
+      x = c->fADX.as<float>();
+    }
     const float* kg = pvar(c, rs + "rnn/gru_cell/gates/kernel");
     const float* kcn = pvar(c, rs + "rnn/gru_cell/candidate/kernel");
     float* XG = c->fXG[r].as<float>();
@@ -3630,7 +3686,11 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
     }
     tr_gemm(B, 128, RD, c->fHG[r].as<float>() + (long)T2 * B * RD, RD, pvar(c, rs + "dense/kernel"), 128,
             c->fREF[r].as<float>(), 128, s, pvar(c, rs + "dense/bias"), nullptr, 0, ACT_TANH);
-    if (f.use_gst) {
+    if (c->f_adain) {  // the speaker reference embedding is the style embedding (tacotron.py:269-272)
+      hipLaunchKernelGGL(k_tr_rows_copy, dim3(nblk((long)B * 128)), dim3(256), 0, s, c->fREF[r].as<float>(), 128L,
+                         (long)B, 128, c->fSTY.as<float>(), (long)(c->D - 2 * f.encoder_lstm_units),
+                         (const float*)nullptr, 0L);
+    } else if (f.use_gst) {
       fe_gst_fwd(fe_gst_args(c, r, B), s);
     } else {  // the reference embedding is the style embedding (tacotron.py:284-291)
       const int SW = c->D - 2 * f.encoder_lstm_units;
@@ -3788,10 +3848,54 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
   fe_style_grad(c->DMEM.as<float>(), B, T, D, 2 * U, c->fDSTY.as<float>(), s);
   const bool style_on = tr_style_on(c);
   if (style_on) tr_style_losses(c, s);
-  for (int r = 0; r < c->f_nref; ++r) {
-    const std::string rs = fe_ref_scope(r), m = fe_mh_scope(r);
-    if (!f.use_gst) {  // d ref = d style slice (+ style-loss terms)
-      hipLaunchKernelGGL(k_tr_rows_copy, dim3(nblk((long)B * 128)), dim3(256), 0, s, c->fDSTY.as<float>() + r * 128,
+  // conv2d stack r backward from d map `din` (conv -> BN -> ReLU per layer; AdaIN: conv -> ReLU)
+  auto conv_bwd = [&](int r, const float* din) {
+    const std::string rs = fe_ref_scope(c, r);
+    float* dY = c->fDY.as<float>();
+    int dims[7][3];
+    {
+      int H = T_ref, W = c->NM, ci = 1;
+      for (int i = 0; i < 6; ++i) {
+        dims[i][0] = H; dims[i][1] = W; dims[i][2] = ci;
+        const int st = fe_ref_stride(c, i);
+        H = (H + st - 1) / st; W = (W + st - 1) / st; ci = f.reference_filters[i];
+      }
+      dims[6][0] = H; dims[6][1] = W; dims[6][2] = ci;
+    }
+    for (int i = 5; i >= 0; --i) {
+      const int nbn = f.enc_conv_layers + 6 * r + i;  // forward order: encoder convs, then refnet r's layers
+      const std::string sc = rs + "conv2d_" + std::to_string(i) + "/", ly = fe_ref_conv(c, r);
+      const int H = dims[i][0], W = dims[i][1], ci = dims[i][2], Ho = dims[i + 1][0], Wo = dims[i + 1][1];
+      const int fo = f.reference_filters[i], st = fe_ref_stride(c, i);
+      const long Mi = (long)B * Ho * Wo;
+      float* dYr = c->fDY2.as<float>();
+      fe_relu_mask(i == 5 ? din : dY, c->fRY[r][i].as<float>(), Mi * fo, dYr, s);
+      float* dz = dYr;
+      if (!c->f_adain) {
+        const float* mean = BN + (long)nbn * 2 * 512;
+        const float* var = mean + 512;
+        dz = c->fDZc.as<float>();
+        fe_bn_bwd(c, dYr, nullptr, c->fRA[r][i].as<float>(), Mi, fo, mean, var, sc, 0, dYr, dz, s);
+      }
+      tr_colsum(c, dz, Mi, fo, fo, gvar(c, sc + ly + "bias"), s);
+      const int pt = std::max((Ho - 1) * st + 3 - H, 0) / 2, pl = std::max((Wo - 1) * st + 3 - W, 0) / 2;
+      const float* xin = i == 0 ? refs[r] : c->fRY[r][i - 1].as<float>();
+      // (gemm_bf16_kc with the im2colᵀ gathered into bf16 measured 458 us per layer here against
+      // 525 + ~60 for the fp32 columns + gemm_x3_kernel: its 256-wide N tile is 8x idle at fo = 32)
+      fe_im2col2d_t(xin, B, H, W, ci, Ho, Wo, pt, pl, FB, Mi, s, st);
+      tr_gemm(9 * ci, fo, (int)Mi, FB, Mi, dz, fo, gvar(c, sc + ly + "kernel"), fo, s);
+      if (i > 0) {
+        tr_transpose(pvar(c, sc + ly + "kernel"), 9L * ci, fo, fo, WT, 9L * ci, s);  // [fo][9ci]
+        tr_gemm((int)Mi, 9 * ci, fo, dz, fo, WT, 9 * ci, FB, 9 * ci, s);
+        fe_col2im2d(FB, B, H, W, ci, Ho, Wo, pt, pl, dY, s, st);
+      }
+    }
+  };
+  for (int r = c->f_adain ? 1 : 0; r < c->f_nref; ++r) {
+    const std::string rs = fe_ref_scope(c, r), m = fe_mh_scope(r);
+    if (!f.use_gst || c->f_adain) {  // d ref = d style slice (+ style-loss terms)
+      hipLaunchKernelGGL(k_tr_rows_copy, dim3(nblk((long)B * 128)), dim3(256), 0, s,
+                         c->fDSTY.as<float>() + (c->f_adain ? 0 : r * 128),
                          (long)SW, (long)B, 128, c->fdREF.as<float>(), 128L,
                          style_on ? (const float*)(c->sXREF.as<float>() + (long)r * B * 128) : (const float*)nullptr,
                          128L);
@@ -3852,7 +3956,7 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
             (long)gin * RD, RD, s);
     // input side over all (n, t) rows: DXG = [dGP | dCP] in (n, t) order
     fe_gru_dxg(c->fDGP.as<float>(), c->fDCP.as<float>(), B, T2, RD, c->fDXG.as<float>(), s);
-    const float* x6 = c->fRY[r][5].as<float>();
+    const float* x6 = c->f_adain ? c->fADX.as<float>() : c->fRY[r][5].as<float>();
     tr_transpose(x6, R2, gin, gin, FB, R2, s);
     tr_gemm(gin, 2 * RD, (int)R2, FB, R2, c->fDXG.as<float>(), 3 * RD, gvar(c, rs + "rnn/gru_cell/gates/kernel"),
             2 * RD, s);
@@ -3865,41 +3969,17 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
     tr_gemm((int)R2, gin, 2 * RD, c->fDXG.as<float>(), 3 * RD, WT, gin, dY, gin, s);
     tr_transpose(kcn, gin, RD, RD, WT, gin, s);
     tr_gemm((int)R2, gin, RD, c->fDXG.as<float>() + 2 * RD, 3 * RD, WT, gin, dY, gin, s, nullptr, dY, gin);
-    // conv2d stack backward (conv -> BN -> ReLU per layer)
-    int dims[7][3];
-    {
-      int H = T_ref, W = c->NM, ci = 1;
-      for (int i = 0; i < 6; ++i) {
-        dims[i][0] = H; dims[i][1] = W; dims[i][2] = ci;
-        H = (H + 1) / 2; W = (W + 1) / 2; ci = f.reference_filters[i];
-      }
-      dims[6][0] = H; dims[6][1] = W; dims[6][2] = ci;
+    if (!c->f_adain) {
+      conv_bwd(r, dY);
+      continue;
     }
-    for (int i = 5; i >= 0; --i) {
-      const int nbn = f.enc_conv_layers + 6 * r + i;  // forward order: encoder convs, then refnet r's layers
-      const std::string sc = rs + "conv2d_" + std::to_string(i) + "/";
-      const int H = dims[i][0], W = dims[i][1], ci = dims[i][2], Ho = dims[i + 1][0], Wo = dims[i + 1][1];
-      const int fo = f.reference_filters[i];
-      const long Mi = (long)B * Ho * Wo;
-      const float* mean = BN + (long)nbn * 2 * 512;
-      const float* var = mean + 512;
-      float* dYr = c->fDY2.as<float>();
-      fe_relu_mask(dY, c->fRY[r][i].as<float>(), Mi * fo, dYr, s);
-      float* dz = c->fDZc.as<float>();
-      fe_bn_bwd(c, dYr, nullptr, c->fRA[r][i].as<float>(), Mi, fo, mean, var, sc, 0, dYr, dz, s);
-      tr_colsum(c, dz, Mi, fo, fo, gvar(c, sc + "conv2d/bias"), s);
-      const int pt = std::max((Ho - 1) * 2 + 3 - H, 0) / 2, pl = std::max((Wo - 1) * 2 + 3 - W, 0) / 2;
-      const float* xin = i == 0 ? refs[r] : c->fRY[r][i - 1].as<float>();
-      // (gemm_bf16_kc with the im2colᵀ gathered into bf16 measured 458 us per layer here against
-      // 525 + ~60 for the fp32 columns + gemm_x3_kernel: its 256-wide N tile is 8x idle at fo = 32)
-      fe_im2col2d_t(xin, B, H, W, ci, Ho, Wo, pt, pl, FB, Mi, s);
-      tr_gemm(9 * ci, fo, (int)Mi, FB, Mi, dz, fo, gvar(c, sc + "conv2d/kernel"), fo, s);
-      if (i > 0) {
-        tr_transpose(pvar(c, sc + "conv2d/kernel"), 9L * ci, fo, fo, WT, 9L * ci, s);  // [fo][9ci]
-        tr_gemm((int)Mi, 9 * ci, fo, dz, fo, WT, 9 * ci, FB, 9 * ci, s);
-        fe_col2im2d(FB, B, H, W, ci, Ho, Wo, pt, pl, dY, s);
-      }
-    }
+    // AdaIN: the restyle's backward splits d map into the speaker map's gradient (in place) and the
+    // emotion map's (through its moments), then both stacks run backward
+    const int C6 = f.reference_filters[5], HW = T2 * (gin / C6);
+    fe_ad_mix_bwd(dY, c->fRY[1][5].as<float>(), c->fRY[0][5].as<float>(), B, HW, C6, c->fADM.as<float>() + (long)B * C6 * 2,
+                  c->fADM.as<float>(), c->fADS.as<float>(), dY, c->fDYE.as<float>(), s);
+    conv_bwd(1, dY);  // (din is read by the top layer's ReLU mask before any col2im writes dY)
+    conv_bwd(0, c->fDYE.as<float>());
   }
   // BiLSTM BPTT (the decoder's DMEM rows carry d enc_out in columns [0, 2U))
   for (int d = 0; d < 2; ++d) {
@@ -4022,8 +4102,8 @@ static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s)
       ++nbn;
     };
     for (int i = 0; i < c->cfg.enc_conv_layers; ++i) upd(fe_conv_scope(i + 1), c->cfg.enc_conv_channels);
-    for (int r = 0; r < c->f_nref; ++r)
-      for (int i = 0; i < 6; ++i) upd(fe_ref_scope(r) + "conv2d_" + std::to_string(i) + "/", c->cfg.reference_filters[i]);
+    for (int r = 0; r < c->f_nref && !c->f_adain; ++r)  // (AdaIN's refnet has no batch norm)
+      for (int i = 0; i < 6; ++i) upd(fe_ref_scope(c, r) + "conv2d_" + std::to_string(i) + "/", c->cfg.reference_filters[i]);
     c->f_ran = false;
   }
   hipLaunchKernelGGL(k_tr_sumsq, dim3(256), dim3(256), 0, s, c->grads, c->total, c->part.as<float>());
@@ -4101,6 +4181,7 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   c->max_T_ref = max_T_out;
   c->mask_decoder = 0;
   c->pos_weight = 1.0f;
+  c->adain = 0;
 }
 
 tt2_status tt2_train_set_target_lengths(tt2_train_ctx* c, const int32_t* lengths) {
@@ -4214,16 +4295,22 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
                 "bad postnet shape");
       if (cfg->frontend) {
         c->f_nref = cfg->emt_only ? 1 : 2;
+        c->f_adain = cfg->adain != 0;
         TT2_CHECK(cfg->n_emt >= 0 && cfg->n_spk >= 0 && cfg->orthog_weight >= 0.f, TT2_ERR_INVALID_ARG,
                   "n_emt / n_spk / orthog_weight must be >= 0");
+        // tacotron.py:68-69; the AdaIN graph builds no style classifiers / orthogonality loss (:485-495, :841)
+        TT2_CHECK(!c->f_adain || !cfg->emt_only, TT2_ERR_INVALID_ARG, "must provide speaker reference to use AdaIn");
+        TT2_CHECK(!c->f_adain || (cfg->n_emt == 0 && cfg->n_spk == 0 && cfg->orthog_weight == 0.f), TT2_ERR_INVALID_ARG,
+                  "adain: no style-embedding classifiers or orthogonality loss (n_emt = n_spk = 0, orthog_weight = 0)");
         int W = cfg->num_mels;
-        for (int i = 0; i < 6; ++i) W = (W + 1) / 2;
+        for (int i = 0; i < 6; ++i) W = (c->f_adain && i >= 2) ? W : (W + 1) / 2;
         c->f_gin = W * cfg->reference_filters[5];
         const int tokd = cfg->num_heads > 0 ? cfg->style_embed_depth / cfg->num_heads : 0;
-        const int sw = cfg->use_gst ? cfg->num_heads * tokd : 128;  // style embedding width
-        TT2_CHECK(cfg->memory_dim == 2 * cfg->encoder_lstm_units + c->f_nref * sw, TT2_ERR_INVALID_ARG,
-                  cfg->use_gst ? "memory_dim must be 2*encoder_lstm_units + (emt_only ? 1 : 2) * style_embed_depth"
-                               : "use_gst = 0: memory_dim must be 2*encoder_lstm_units + (emt_only ? 1 : 2) * 128");
+        const int sw = cfg->use_gst && !c->f_adain ? cfg->num_heads * tokd : 128;  // style embedding width
+        TT2_CHECK(cfg->memory_dim == 2 * cfg->encoder_lstm_units + (c->f_adain ? 1 : c->f_nref) * sw, TT2_ERR_INVALID_ARG,
+                  c->f_adain    ? "adain: memory_dim must be 2*encoder_lstm_units + 128"
+                  : cfg->use_gst ? "memory_dim must be 2*encoder_lstm_units + (emt_only ? 1 : 2) * style_embed_depth"
+                                 : "use_gst = 0: memory_dim must be 2*encoder_lstm_units + (emt_only ? 1 : 2) * 128");
         TT2_CHECK(cfg->enc_conv_layers >= 1 && cfg->enc_conv_layers <= 8 && cfg->enc_conv_channels <= 512 &&
                       cfg->n_symbols >= 1 && cfg->embedding_dim >= 1 && cfg->max_T_ref >= 1,
                   TT2_ERR_INVALID_ARG, "bad front-end shape");

@@ -39,11 +39,19 @@ void fe_lstm_dxp(const float* DZ, const int* lens, int B, int T, int U, float* d
 void fe_bn_relu_fwd(const float* a, long M, int C, const float* mean, const float* var, const float* gamma,
                     const float* beta, float eps, float* y, hipStream_t s);
 void fe_relu_mask(const float* dy, const float* y, long n, float* out, hipStream_t s);
-// conv2d 3x3 stride 2 'same' (TF: odd pad bottom/right) on NHWC x [N][H][W][C]
+// conv2d 3x3 stride st (2, or 1 for ReferenceEncoderAdaIn's deeper layers) 'same' (TF: odd pad
+// bottom/right) on NHWC x [N][H][W][C]
 void fe_im2col2d_t(const float* x, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* out, long ldo,
-                   hipStream_t s);
+                   hipStream_t s, int st = 2);
 void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* dx,
-                 hipStream_t s);
+                 hipStream_t s, int st = 2);
+// ReferenceEncoderAdaIn (modules.py:89-98): per (row, channel) moments of NHWC x over HW -> mv [N][C][2]
+// (mean, biased variance); the 0.9 / 0.1 restyle of the speaker map by the emotion map's moments and
+// its backward (S: [N][C][2] scratch; dxe: the emotion map's gradient through m_e, v_e)
+void fe_ad_moments(const float* x, int N, int HW, int C, float* mv, hipStream_t s);
+void fe_ad_mix(const float* xs, int N, int HW, int C, const float* mv_s, const float* mv_e, float* y, hipStream_t s);
+void fe_ad_mix_bwd(const float* dy, const float* xs, const float* xe, int N, int HW, int C, const float* mv_s,
+                   const float* mv_e, float* S, float* dxs, float* dxe, hipStream_t s);
 // GRU (TF1 GRUCell, modules.py:59): XG [N][T2][3D] = x·[Wg_x | Wc_x] + [bg | bc]; per step
 // GG = h·Wg_h [N][2D], GC = (r·h)·Wc_h [N][D]; stored step-major R, U, CC [T2][N][D], RH [T2][N][D],
 // HG [T2+1][N][D]

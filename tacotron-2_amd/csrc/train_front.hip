@@ -206,26 +206,26 @@ __global__ void k_fe_relu_mask(const float* __restrict__ dy, const float* __rest
 void fe_relu_mask(const float* dy, const float* y, long n, float* out, hipStream_t s) {
   hipLaunchKernelGGL(k_fe_relu_mask, dim3(fe_blk(n)), dim3(256), 0, s, dy, y, n, out);
 }
-// out[((i*3 + j)*C + c) * ldo + m] = x(n, 2ho + i - pt, 2wo + j - pl, c), m = (n*Ho + ho)*Wo + wo
+// out[((i*3 + j)*C + c) * ldo + m] = x(n, st ho + i - pt, st wo + j - pl, c), m = (n*Ho + ho)*Wo + wo
 __global__ void k_fe_im2col2d_t(const float* __restrict__ x, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl,
-                                float* __restrict__ out, long ldo) {
+                                float* __restrict__ out, long ldo, int st) {
   const long M = (long)N * Ho * Wo;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 9L * C * M) return;
   const long m = i % M, k = i / M;
   const int c = (int)(k % C), ij = (int)(k / C), ii = ij / 3, jj = ij % 3;
   const int wo = (int)(m % Wo), ho = (int)((m / Wo) % Ho), n = (int)(m / ((long)Wo * Ho));
-  const int h = 2 * ho + ii - pt, w = 2 * wo + jj - pl;
+  const int h = st * ho + ii - pt, w = st * wo + jj - pl;
   out[k * ldo + m] = (h >= 0 && h < H && w >= 0 && w < W) ? x[(((long)n * H + h) * W + w) * C + c] : 0.f;
 }
 void fe_im2col2d_t(const float* x, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* out, long ldo,
-                   hipStream_t s) {
+                   hipStream_t s, int st) {
   hipLaunchKernelGGL(k_fe_im2col2d_t, dim3(fe_blk(9L * C * N * Ho * Wo)), dim3(256), 0, s, x, N, H, W, C, Ho, Wo, pt,
-                     pl, out, ldo);
+                     pl, out, ldo, st);
 }
 // dx(n, h, w, c) = Σ_{i,j} dcols[(n, ho, wo)][(i*3+j)*C + c] over the outputs whose taps read it
 __global__ void k_fe_col2im2d(const float* __restrict__ dcols, int N, int H, int W, int C, int Ho, int Wo, int pt,
-                              int pl, float* __restrict__ dx) {
+                              int pl, float* __restrict__ dx, int st) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)N * H * W * C) return;
   const int c = (int)(i % C), w = (int)((i / C) % W), h = (int)((i / ((long)C * W)) % H);
@@ -233,20 +233,121 @@ __global__ void k_fe_col2im2d(const float* __restrict__ dcols, int N, int H, int
   float acc = 0.f;
   for (int ii = 0; ii < 3; ++ii) {
     const int hh = h + pt - ii;
-    if (hh < 0 || (hh & 1) || (hh >> 1) >= Ho) continue;
+    if (hh < 0 || hh % st || hh / st >= Ho) continue;
     for (int jj = 0; jj < 3; ++jj) {
       const int ww = w + pl - jj;
-      if (ww < 0 || (ww & 1) || (ww >> 1) >= Wo) continue;
-      const long m = ((long)n * Ho + (hh >> 1)) * Wo + (ww >> 1);
+      if (ww < 0 || ww % st || ww / st >= Wo) continue;
+      const long m = ((long)n * Ho + hh / st) * Wo + ww / st;
       acc += dcols[m * 9 * C + (ii * 3 + jj) * C + c];
     }
   }
   dx[i] = acc;
 }
 void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* dx,
-                 hipStream_t s) {
+                 hipStream_t s, int st) {
   hipLaunchKernelGGL(k_fe_col2im2d, dim3(fe_blk((long)N * H * W * C)), dim3(256), 0, s, dcols, N, H, W, C, Ho, Wo, pt,
-                     pl, dx);
+                     pl, dx, st);
+}
+
+// ---- ReferenceEncoderAdaIn (modules.py:89-98) ------------------------------------------------------
+// per (row, channel) moments over the HW positions of NHWC x [N][HW][C] (tf.nn.moments axes [1, 2]:
+// biased variance): mv[(n*C + c)*2 + {0: mean, 1: var}].  Work-group (n, 64-channel block): 4 row
+// groups of 64 lanes, two passes (mean, then Σ (x - mean)²)
+__global__ __launch_bounds__(256) void k_fe_ad_moments(const float* __restrict__ x, int HW, int C,
+                                                       float* __restrict__ mv) {
+  __shared__ float red[4][64];
+  const int n = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  const bool ok = c < C;
+  const float* xr = x + (long)n * HW * C;
+  float s = 0.f;
+  if (ok)
+    for (int p = g; p < HW; p += 4) s += xr[(long)p * C + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  const float mean = ((red[0][threadIdx.x & 63] + red[1][threadIdx.x & 63]) +
+                      (red[2][threadIdx.x & 63] + red[3][threadIdx.x & 63])) / (float)HW;
+  __syncthreads();
+  float q = 0.f;
+  if (ok)
+    for (int p = g; p < HW; p += 4) {
+      const float d = xr[(long)p * C + c] - mean;
+      q += d * d;
+    }
+  red[g][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (ok && g == 0) {
+    const int l = threadIdx.x;
+    mv[((long)n * C + c) * 2] = mean;
+    mv[((long)n * C + c) * 2 + 1] = ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l])) / (float)HW;
+  }
+}
+void fe_ad_moments(const float* x, int N, int HW, int C, float* mv, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_ad_moments, dim3(N, (C + 63) / 64), dim3(256), 0, s, x, HW, C, mv);
+}
+// y = 0.9 xs + 0.1 tf.nn.batch_normalization(xs, m_s, v_s, offset = m_e, scale = v_e, 1e-9)
+//   = 0.9 xs + 0.1 (xs inv + (m_e - m_s inv)), inv = v_e / sqrt(v_s + 1e-9)
+__global__ void k_fe_ad_mix(const float* __restrict__ xs, long n, int HW, int C, const float* __restrict__ mv_s,
+                            const float* __restrict__ mv_e, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long r = i / ((long)HW * C);
+  const int c = (int)(i % C);
+  const long q = (r * C + c) * 2;
+  const float inv = mv_e[q + 1] / sqrtf(mv_s[q + 1] + 1e-9f);
+  y[i] = xs[i] * 0.9f + (xs[i] * inv + (mv_e[q] - mv_s[q] * inv)) * 0.1f;
+}
+void fe_ad_mix(const float* xs, int N, int HW, int C, const float* mv_s, const float* mv_e, float* y, hipStream_t s) {
+  const long n = (long)N * HW * C;
+  hipLaunchKernelGGL(k_fe_ad_mix, dim3(fe_blk(n)), dim3(256), 0, s, xs, n, HW, C, mv_s, mv_e, y);
+}
+// backward of the mix, g = 0.1 dy, x̂ = (xs - m_s) / sqrt(v_s + 1e-9), per (row, channel) over N = HW:
+//   S1 = Σ g, S2 = Σ g x̂
+//   d xs = 0.9 dy + inv (g - S1 / N - x̂ S2 / N)          (m_s, v_s are functions of xs)
+//   d xe = S1 / N + S2 · 2 (xe - m_e) / N                  (offset m_e, scale v_e: d m_e = S1, d v_e = S2)
+__global__ __launch_bounds__(256) void k_fe_ad_mix_sums(const float* __restrict__ dy, const float* __restrict__ xs,
+                                                        int HW, int C, const float* __restrict__ mv_s,
+                                                        float* __restrict__ S) {
+  __shared__ float r1[4][64], r2[4][64];
+  const int n = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const bool ok = c < C;
+  float s1 = 0.f, s2 = 0.f;
+  if (ok) {
+    const long q = ((long)n * C + c) * 2;
+    const float m = mv_s[q], rs = 1.0f / sqrtf(mv_s[q + 1] + 1e-9f);
+    const long base = (long)n * HW * C + c;
+    for (int p = g; p < HW; p += 4) {
+      const float gg = 0.1f * dy[base + (long)p * C];
+      s1 += gg;
+      s2 += gg * ((xs[base + (long)p * C] - m) * rs);
+    }
+  }
+  r1[g][l] = s1;
+  r2[g][l] = s2;
+  __syncthreads();
+  if (ok && g == 0) {
+    S[((long)n * C + c) * 2] = (r1[0][l] + r1[1][l]) + (r1[2][l] + r1[3][l]);
+    S[((long)n * C + c) * 2 + 1] = (r2[0][l] + r2[1][l]) + (r2[2][l] + r2[3][l]);
+  }
+}
+__global__ void k_fe_ad_mix_bwd(const float* __restrict__ dy, const float* __restrict__ xs,
+                                const float* __restrict__ xe, long n, int HW, int C, const float* __restrict__ mv_s,
+                                const float* __restrict__ mv_e, const float* __restrict__ S, float* __restrict__ dxs,
+                                float* __restrict__ dxe) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long r = i / ((long)HW * C);
+  const int c = (int)(i % C);
+  const long q = (r * C + c) * 2;
+  const float rs = 1.0f / sqrtf(mv_s[q + 1] + 1e-9f), inv = mv_e[q + 1] * rs, N = (float)HW;
+  const float xh = (xs[i] - mv_s[q]) * rs, g = 0.1f * dy[i];
+  dxs[i] = 0.9f * dy[i] + inv * (g - S[q] / N - xh * S[q + 1] / N);
+  dxe[i] = S[q] / N + S[q + 1] * 2.f * (xe[i] - mv_e[q]) / N;
+}
+void fe_ad_mix_bwd(const float* dy, const float* xs, const float* xe, int N, int HW, int C, const float* mv_s,
+                   const float* mv_e, float* S, float* dxs, float* dxe, hipStream_t s) {
+  hipLaunchKernelGGL(k_fe_ad_mix_sums, dim3(N, (C + 63) / 64), dim3(256), 0, s, dy, xs, HW, C, mv_s, S);
+  const long n = (long)N * HW * C;
+  hipLaunchKernelGGL(k_fe_ad_mix_bwd, dim3(fe_blk(n)), dim3(256), 0, s, dy, xs, xe, n, HW, C, mv_s, mv_e, S, dxs, dxe);
 }
 
 // GRU step t, part a: [r, u] = σ(XG_g + h·Wg_h); RH = r·h

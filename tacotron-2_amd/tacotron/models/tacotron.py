@@ -267,10 +267,10 @@ class Tacotron():
         hp = self._hparams
         if mel_targets is None or stop_token_targets is None:
             raise ValueError("training needs mel_targets and stop_token_targets")
-        if style != "gst":
-            raise NotImplementedError("training builds the GST and hp.use_gst = False style paths (the "
-                                      "adain / pretrained_emb_disc_all front ends are synthesis-only on "
-                                      "this build)")
+        # style paths in training (tacotron.py:236-308): GST (or hp.use_gst = False), AdaIN, and the
+        # reference embeddings themselves for pretrained_emb_disc_all (whose add_loss the reference
+        # can only run with the unpaired towers, see add_loss)
+        self._train_style = style
         # use_emt_disc / use_spk_disc / use_intercross are stored and never read by the reference
         # graph (tacotron.py:74-76): accepted and ignored alike
         if hp.outputs_per_step != 1:
@@ -307,7 +307,9 @@ class Tacotron():
         cap = dict(max_T_in=T_in, max_T_out=T_out, max_T_ref=T_ref)
         cap.update(train_capacity or {})
         n_emt, n_spk = (int(n_emt or 0), int(n_spk or 0)) if hp.tacotron_use_style_emb_disc else (0, 0)
-        key = (B, emt_only, precision, n_emt, n_spk)
+        if style != "gst":  # the AdaIN / pretrained_emb_disc_all graphs build no Style_Emb_Disc (:485-495)
+            n_emt = n_spk = 0
+        key = (B, emt_only, precision, n_emt, n_spk, style)
         tr = self._trainer
         if tr is not None and (self._train_key != key or T_in > self._train_cap["max_T_in"]
                                or T_out > self._train_cap["max_T_out"] or T_ref > self._train_cap["max_T_ref"]):
@@ -317,7 +319,7 @@ class Tacotron():
         if tr is None:
             tr = TacotronTrainer(hp, self._weights, B, cap["max_T_in"], cap["max_T_out"], self.device,
                                  emt_only=emt_only, precision=precision, postnet=True, frontend=True,
-                                 max_T_ref=cap["max_T_ref"], tf_seed=seed, n_emt=n_emt, n_spk=n_spk)
+                                 max_T_ref=cap["max_T_ref"], tf_seed=seed, n_emt=n_emt, n_spk=n_spk, style=style)
             self._trainer, self._train_key, self._train_cap = tr, key, cap
             # the classifiers' variables are trained and saved like the rest (tf.train.Saver)
             for k, v in tr.style_disc_weights.items():
@@ -365,6 +367,13 @@ class Tacotron():
         tr = self._trainer
         if tr is None:
             raise RuntimeError("add_loss: call initialize(..., is_training=True) first")
+        if getattr(self, "_train_style", "gst") == "embed":
+            # tacotron.py:808-811: with pretrained_emb_disc_all the loss reads the unpaired towers'
+            # reference embeddings (tower_refnet_out_up_emt[i]), appended only when use_unpaired
+            # (:603-607); without them the reference's add_loss fails indexing the empty list, and the
+            # unpaired decode itself is out of scope here
+            raise IndexError("list index out of range: pretrained_emb_disc_all's add_loss needs the unpaired "
+                             "towers (tacotron.py:808-811), which this build does not construct")
         L = tr.losses()
         self._losses = L
         self.before_loss, self.after_loss = L["before"], L["after"]

@@ -58,7 +58,7 @@ _UNSET = object()
 
 
 def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32", postnet=True,
-                 frontend=False, max_T_ref=None, n_emt=0, n_spk=0):
+                 frontend=False, max_T_ref=None, n_emt=0, n_spk=0, style="gst"):
     lib = _lib.load_library()
     cfg = _lib.TrainConfig()
     lib.tt2_train_default_config(ctypes.byref(cfg), batch, max_T_in, max_T_out)
@@ -72,7 +72,13 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
         raise NotImplementedError("predict_linear (CBHG linear loss) is not built in the training step")
     if hp.smoothing:
         raise NotImplementedError("smoothing attention normalisation is built for synthesis only")
-    cfg.memory_dim = memory_width(hp, emt_only)
+    # style path of the front end (tacotron.py:236-308): 'gst' (hp.use_gst; False = the embeddings),
+    # 'embed' (args.pretrained_emb_disc_all: the reference embeddings themselves), 'adain'
+    if style not in ("gst", "embed", "adain"):
+        raise ValueError("style must be 'gst', 'embed' or 'adain'")
+    if style != "gst" and not frontend:
+        raise ValueError("style paths other than GST live in the front end (frontend=True)")
+    cfg.memory_dim = memory_width(hp, emt_only, style)
     cfg.num_mels = hp.num_mels
     cfg.prenet_units = hp.prenet_layers[0]
     cfg.decoder_lstm_units = hp.decoder_lstm_units
@@ -116,7 +122,8 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
         cfg.encoder_lstm_units = hp.encoder_lstm_units
         cfg.emt_only = 1 if emt_only else 0
         # hp.use_gst = False: the reference embeddings are the style embeddings (tacotron.py:284-291)
-        cfg.use_gst = 1 if hp.use_gst else 0
+        cfg.use_gst = 1 if hp.use_gst and style == "gst" else 0
+        cfg.adain = 1 if style == "adain" else 0
         cfg.num_gst = hp.num_gst
         cfg.num_heads = hp.num_heads
         cfg.style_embed_depth = hp.style_embed_depth
@@ -128,10 +135,11 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
         # style-embedding losses of the default training graph (tacotron.py:486-495, 812-846): the
         # classifiers need the class counts (feeder.total_emt / total_spk); the orthogonality loss
         # needs both reference encoders
-        if hp.tacotron_use_style_emb_disc:
+        # (neither is part of the adain / pretrained_emb_disc_all graphs: tacotron.py:485-495, 581, 841)
+        if hp.tacotron_use_style_emb_disc and style == "gst":
             cfg.n_emt = int(n_emt)
             cfg.n_spk = 0 if emt_only else int(n_spk)
-        if hp.tacotron_use_orthog_loss and not emt_only:
+        if hp.tacotron_use_orthog_loss and not emt_only and style == "gst":
             cfg.orthog_weight = 0.02
     return cfg
 
@@ -156,7 +164,7 @@ class TacotronTrainer(object):
 
     def __init__(self, hp, weights, batch, max_T_in, max_T_out, device=0, emt_only=False,
                  precision="fp32", postnet=True, frontend=False, max_T_ref=None, tf_seed=None,
-                 n_emt=0, n_spk=0):
+                 n_emt=0, n_spk=0, style="gst"):
         """n_emt / n_spk: classes of the style-embedding classifiers (frontend, when
         hp.tacotron_use_style_emb_disc); their variables are taken from ``weights`` or freshly
         initialised (init_style_disc_weights), and set_style_labels() feeds the labels."""
@@ -166,7 +174,8 @@ class TacotronTrainer(object):
         self.hp = hp
         self.device = torch.device("cuda", device)
         self.cfg = train_config(hp, batch, max_T_in, max_T_out, emt_only, precision, postnet, frontend,
-                                max_T_ref, n_emt if frontend else 0, n_spk if frontend else 0)
+                                max_T_ref, n_emt if frontend else 0, n_spk if frontend else 0, style)
+        self.style = style
         # the Style_Emb_Disc variables this context trains, with the values it starts from (the
         # caller's, else a fresh draw): callers that save checkpoints merge them into their weights
         self.style_disc_weights = {}

@@ -140,13 +140,17 @@ def style_mode(hp, style="gst"):
 
 def _adain_refnet_specs(hp, sc):
     """ReferenceEncoderAdaIn (modules.py:66-107): conv2d without batch norm, strides
-    (2,2),(2,2),(1,1)x4 (tacotron.py:237), one GRU + dense(128, tanh) over the mixed speaker map."""
+    (2,2),(2,2),(1,1)x4 (tacotron.py:237), one GRU + dense(128, tanh) over the mixed speaker map.
+    The speaker and emotion stacks each call conv2d(..., 'conv2d_%d') in scope 'refnet' (speaker
+    first): tf.layers.conv2d uniquifies its default layer name in the re-entered scope, so the
+    speaker convs are conv2d_i/conv2d/* and the emotion convs conv2d_i/conv2d_1/*."""
     S = []
     c_in, F = 1, hp.num_mels
     for i, f in enumerate(hp.reference_filters):
         s2 = sc + "conv2d_{}/".format(i)
-        S.append((s2 + "conv2d/kernel", (3, 3, c_in, f), "glorot"))
-        S.append((s2 + "conv2d/bias", (f,), "bias"))
+        for ly in ("conv2d", "conv2d_1"):
+            S.append((s2 + ly + "/kernel", (3, 3, c_in, f), "glorot"))
+            S.append((s2 + ly + "/bias", (f,), "bias"))
         c_in = f
         if i < 2:
             F = -(-F // 2)

@@ -51,8 +51,8 @@ def test_training_api_validation():
         model.initialize(ARGS, ids, lens, tg, st, is_evaluating=True, ref_mel_emt=re, ref_mel_spk=rs)
     with pytest.raises(ValueError, match="without corresponding token_targets"):
         model.initialize(ARGS, ids, lens, tg, None, is_training=True, ref_mel_emt=re, ref_mel_spk=rs)
-    with pytest.raises(NotImplementedError, match="GST"):
-        model.initialize(types.SimpleNamespace(**dict(vars(ARGS), pretrained_emb_disc_all=True)), ids, lens, tg, st,
+    with pytest.raises(ValueError, match="AdaIn"):  # tacotron.py:68-69
+        model.initialize(types.SimpleNamespace(**dict(vars(ARGS), adain=True, emt_only=True)), ids, lens, tg, st,
                          is_training=True, ref_mel_emt=re, ref_mel_spk=rs)
     hp3 = small_hparams()   # the default graph's style classifiers need the classes and labels
     with pytest.raises(ValueError, match="number of emotions"):
@@ -195,3 +195,53 @@ def test_style_classifier_variables_saved_and_restored():
             np.testing.assert_array_equal(resumed._trainer.get(n, 0, saved[n].shape), saved[n])
     finally:
         resumed._trainer.close()
+
+
+@pytest.mark.gpu
+def test_reference_calls_adain_and_pretrained_emb_disc_all():
+    """args.adain trains through the reference's calls (initialize / add_loss / add_optimizer) like
+    TacotronTrainer(style='adain').step_text, bit for bit; args.pretrained_emb_disc_all builds the
+    training forward on the reference embeddings themselves, and its add_loss fails like the
+    reference's without the unpaired towers (tacotron.py:808-811 index tower_refnet_out_up_emt)."""
+    from oracle import train_ref as TRN
+    from tt2.train import TacotronTrainer
+    hp = _hp()
+    W = init_tacotron_weights(hp, seed=5339, style="adain")
+    ids, lens, re, rs, _, st, m = _batch(hp, T_ref=40)
+    _, _, tg, _ = train_batch(ids.shape[0], ids.shape[1], 6, memory_width(hp, style="adain"), seed=32)
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    args = types.SimpleNamespace(**dict(vars(ARGS), adain=True))
+    model = _model(hp, W)
+    got = []
+    for step in range(2):
+        model.initialize(args, ids, lens, tg, st, is_training=True, ref_mel_emt=re, ref_mel_spk=rs, train_masks=m)
+        got.append(model.add_loss())
+        assert model.add_optimizer(step) == step + 1
+    names = TRN.frontend_var_names(adain=True) + TRN.train_var_names() + TRN.postnet_var_names()
+    params = {n: model._trainer.get(n, 0, np.asarray(W[n]).shape) for n in names}
+    model._trainer.close()
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1], style="adain")
+    try:
+        for step in range(2):
+            L = tr.step_text(ids, lens, re, rs, tg, st, m["prenet"], m["zoneout"], m["postnet"], m["enc_conv"],
+                             m["enc_zoneout"])
+            assert got[step] == L["loss"]
+        for n in names:
+            assert np.array_equal(params[n], tr.get(n, 0, params[n].shape)), n
+        moved = [n for n in names if "refnet/" in n and not np.array_equal(params[n], np.asarray(W[n], np.float32))]
+        assert len(moved) >= 8, moved   # both conv stacks, the GRU and the dense were updated
+    finally:
+        tr.close()
+    # pretrained_emb_disc_all: forward on refnet_emt / refnet_spk's embeddings, add_loss as the reference's
+    W2 = init_tacotron_weights(hp, seed=5339, style="embed")   # memory width 2U + 2 x 128 (tacotron.py:284-291)
+    ids, lens, re, rs, tg, st, m = _batch(hp, T_ref=40)
+    model = _model(hp, W2)
+    model.initialize(types.SimpleNamespace(**dict(vars(ARGS), pretrained_emb_disc_all=True)), ids, lens, tg, st,
+                     is_training=True, ref_mel_emt=re, ref_mel_spk=rs, train_masks=m)
+    try:
+        assert np.isfinite(model.tower_decoder_output[0]).all()
+        assert model._trainer.cfg.use_gst == 0 and model._trainer.cfg.n_emt == 0
+        with pytest.raises(IndexError):
+            model.add_loss()
+    finally:
+        model._trainer.close()

@@ -710,6 +710,114 @@ def test_gpu_train_frontend_without_gst_matches_oracle():
         tr.close()
 
 
+def _adain_case(hp, B=3, T_in=9, T_out=6, T_ref=40, seed=33):
+    from tt2.synthetic import enc_conv_masks, enc_zoneout_masks, tacotron_inputs
+    W = init_tacotron_weights(hp, seed=5339, style="adain")
+    ids, lens, re, rs = tacotron_inputs(B, T_in, T_ref, seed=seed)
+    _, _, tg, st = train_batch(B, T_in, T_out, memory_width(hp, style="adain"), seed=seed)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=seed)
+    zm = zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=seed)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=seed)
+    em = enc_conv_masks(hp.enc_conv_num_layers, B, T_in, hp.enc_conv_channels, seed=seed)
+    ezm = enc_zoneout_masks(T_in, B, hp.encoder_lstm_units, seed=seed)
+    return W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm
+
+
+def test_adain_oracle_gradients_match_finite_differences():
+    """The AdaIN front end of the training oracle (ReferenceEncoderAdaIn, modules.py:66-107: two conv
+    stacks without BN, the moments restyle, GRU + dense) against central differences on the refnet
+    variables of both stacks, the GRU and the dense."""
+    hp = small_hparams()
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _adain_case(hp, B=2, T_in=6, T_out=3, T_ref=24)
+    _, g, _ = TRN.train_grads_frontend(W, ids, lens, re, rs, tg, st, pm, zm, em, ezm, reg_weight=1e-3,
+                                       postnet_masks=pnm, adain=True)
+    names = TRN.frontend_var_names(adain=True) + TRN.train_var_names() + TRN.postnet_var_names()
+    assert "Tacotron_model/inference/refnet/conv2d_3/conv2d_1/kernel" in names
+
+    def loss_of(W2):
+        Wt = {n: torch.tensor(np.asarray(W2[n]), dtype=torch.float64) for n in names}
+        mem, _ = TRN.frontend_forward(Wt, ids, lens, re, rs, em, ezm, adain=True)
+        tg_t = torch.tensor(tg, dtype=torch.float64)
+        fr, sl, _ = TRN.forward(Wt, mem, lens, tg_t, torch.tensor(pm, dtype=torch.float64),
+                                torch.tensor(zm, dtype=torch.float64))
+        b, s, r = TRN.losses(fr, sl, tg_t, torch.tensor(st, dtype=torch.float64), Wt, 1e-3)
+        dec = TRN.clip_decoder_output(fr)
+        proj, _ = TRN.postnet_train(Wt, dec, torch.tensor(pnm, dtype=torch.float64))
+        mel = TRN.clip_decoder_output(dec + proj)
+        return float(b + s + r + ((mel - tg_t) ** 2).mean())
+
+    rng = np.random.default_rng(3)
+    P = "Tacotron_model/inference/refnet/"
+    for n in (P + "conv2d_0/conv2d/kernel", P + "conv2d_3/conv2d_1/kernel", P + "conv2d_5/conv2d_1/bias",
+              P + "conv2d_4/conv2d/bias", P + "rnn/gru_cell/gates/kernel", P + "dense/kernel"):
+        W64 = {k: np.asarray(v, np.float64) for k, v in W.items()}
+        idx = np.unravel_index(np.argmax(np.abs(g[n])), np.shape(W64[n]))
+        h = 1e-6
+        Wp, Wm = dict(W64), dict(W64)
+        Wp[n] = W64[n].copy(); Wp[n][idx] += h
+        Wm[n] = W64[n].copy(); Wm[n][idx] -= h
+        fd = (loss_of(Wp) - loss_of(Wm)) / (2 * h)
+        assert abs(fd - g[n][idx]) <= 1e-6 + 1e-4 * abs(fd), (n, fd, g[n][idx])
+
+
+@pytest.mark.gpu
+def test_gpu_train_frontend_adain_matches_oracle():
+    """args.adain (tacotron.py:236-242, 266-268; modules.py:66-107) in training: speaker and emotion
+    conv stacks without batch norm (strides (2,2),(2,2),(1,1)x4), the speaker map restyled by the
+    emotion map's moments, GRU + dense tanh as the 128-wide style embedding, backward through the
+    restyle into both stacks.  fp32: the whole step from ids + reference mels against the torch
+    float64 oracle, losses and every gradient within 2e-4.  bf16 GEMM operands (configs[4]'s mode):
+    losses within 1e-2 of fp32 and the front-end gradient direction (cosine) above 0.97 -- single
+    gradients of a bf16 step move by ReLU / dropout-boundary flips, as in the other bf16 tests."""
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _adain_case(hp)
+    B, T_in, T_out = ids.shape[0], ids.shape[1], tg.shape[1]
+    names = TRN.frontend_var_names(adain=True) + TRN.train_var_names() + TRN.postnet_var_names()
+    fe = TRN.frontend_var_names(adain=True)
+    res = {}
+    for precision in ("fp32", "bf16"):
+        tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, frontend=True, max_T_ref=re.shape[1], precision=precision,
+                             style="adain")
+        try:
+            tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+            res[precision] = (tr.losses(), {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names})
+        finally:
+            tr.close()
+    L, got = res["fp32"]
+    (b, s_, r, a), g, _ = TRN.train_grads_frontend(
+        W, ids, lens, re, rs, tg, st, pm, zm, em, ezm, hp.tacotron_reg_weight, postnet_masks=pnm, adain=True)
+    assert abs(L["before"] - b) < 2e-4 * b and abs(L["after"] - a) < 2e-4 * a
+    for n in names:
+        if np.abs(g[n]).max() < 1e-12:   # a conv bias feeding batch-statistics BN: exactly 0
+            assert np.abs(got[n]).max() < 1e-6, (n, np.abs(got[n]).max())
+            continue
+        assert _rel(got[n], g[n]) < 2e-4, (n, _rel(got[n], g[n]))
+    Lb, gb = res["bf16"]
+    for k in ("before", "after", "stop_token"):
+        assert abs(Lb[k] - L[k]) < 1e-2 * abs(L[k]), (k, Lb[k], L[k])
+    def cos(sel):
+        u = np.concatenate([got[n].ravel() for n in sel])
+        v = np.concatenate([gb[n].ravel() for n in sel])
+        return float(u @ v / (np.linalg.norm(u) * np.linalg.norm(v)))
+    ref = [n for n in fe if "/refnet/" in n]
+    c_all, c_ref = cos(fe), cos(ref)
+    print("adain bf16 vs fp32 gradient cosine: front end {:.5f}, refnet {:.5f}".format(c_all, c_ref))
+    assert c_all > 0.97 and c_ref > 0.97
+
+
+def test_train_config_adain_without_gpu():
+    """train_config for args.adain: one 128-wide style embedding, no style classifiers / orthogonality
+    loss (the AdaIN graph builds none, tacotron.py:485-495, 841)."""
+    from tt2.train import train_config
+    hp = small_hparams()
+    cfg = train_config(hp, 4, 9, 6, frontend=True, n_emt=4, n_spk=2, style="adain")
+    assert cfg.adain == 1 and cfg.use_gst == 0 and cfg.n_emt == 0 and cfg.n_spk == 0 and cfg.orthog_weight == 0
+    assert cfg.memory_dim == 2 * hp.encoder_lstm_units + 128
+    with pytest.raises(ValueError):
+        train_config(hp, 4, 9, 6, frontend=False, style="adain")
+
+
 def test_train_config_use_gst_without_gpu():
     """train_config carries hp.use_gst and the matching memory width (tacotron.py:284-291)."""
     from tt2.train import train_config
