@@ -64,6 +64,7 @@ struct tt2_train_ctx {
   DevBuf dFR, dST, dPIN, dX1, dX2, dG1, dG2, DC1, DC2, R1, R2, DQ, DCTX, DKEYS, DCUM;
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
   DevBuf DF2, DCUM2, PQ2, SC2;
+  DevBuf DWGP;  // [B][NT][32][A] k_tr_att_bwd_q's d W_loc accumulators (TrAtt::DWGP)
   DevBuf DWG;  // [32][A] k_tr_dwloc_cum: Σ cum_{t-1}·du per tap (+ the Σ du row)  // k_tr_att_bwd_q: df / d cum / d query / Σ a·d cum partials by step parity
   DevBuf TH, E, DF, PQ, FALL, ALN;
   // the large plain products (tr_gemm_big)
@@ -841,6 +842,7 @@ struct TrAtt {
   float* dBC;    // [B][nt][F]
   long long* stamps;  // diagnostic: k_tr_att_bwd_q stage stamps of step stamp_t ([B][4][16]) or null
   int stamp_t;
+  float* DWGP;   // [B][nt][32][A] k_tr_att_bwd_q: Σ_t G[tap][a] = Σ_j cum_{t-1}[j + tap - pad]·du[j][a] (d W_loc)
 };
 
 // Location features of rows j0..j0+TR_JT-1 of utterance b (attention.py:193-195):
@@ -1689,6 +1691,17 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
   float okc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) okc[i] = a.dKC[pt * KW * F + min(kt0 + i, KW - 1) * F + kcc];
+  // the d W_loc accumulator entries of this lane: wave w owns the G tiles w + 4u (tap tile tl >> 3,
+  // column tile tl & 7), MFMA D rows 4 g4 + i, column jl
+  float* const dwg = a.DWGP + pt * 32 * A;
+  float odw[16];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int tl = w + 4 * u;
+      odw[4 * u + i] = dwg[(16 * (tl >> 3) + 4 * g4 + i) * A + 16 * (tl & 7) + jl];
+    }
   // d query of step t + 1 = the sum of that launch's partials (in range order), written by q == 0
   const bool dq_prev = q == 0 && tid < A && a.t + 1 < a.T;
   float pqv[4];
@@ -1858,8 +1871,6 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
     dq1 += du1;
     a.DKEYS[krow + k0] = e0[u] + du0;
     a.DKEYS[krow + k1] = e1[u] + du1;
-    a.TH[hrow + k0] = du0;  // d W_loc = FALL^T · du after the loop
-    a.TH[hrow + k1] = du1;
     dus[jr * (A + 1) + k0] = du0;
     dus[jr * (A + 1) + k1] = du1;
   }
@@ -1876,6 +1887,30 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
     a.dV[pt * A + tid] = odv + sv;
     a.dBA[pt * A + tid] = odb + sq;
     z.pq_out[pt * A + tid] = sq;
+  }
+  // ---- d W_loc through the cumulative alignments, accumulated over the steps in this work-group's
+  // slot (no du stream to HBM, no pass after the loop): G[tap][a] += Σ_jr cseg[jr + tap]·du[jr][a] on
+  // fp32 MFMA; A [tap = 16 mt + jl][jr = 4 ks + g4] from cseg, B [jr][a = 16 nt + jl] from dus (zero past
+  // nown).  Row 31 (no tap) is Σ du = d b_a, filled after the loop.
+  {
+    const int nk = (nown + 3) >> 2;
+    trq_f4 gacc[4] = {};
+    for (int ks = 0; ks < nk; ++ks) {
+      const int jr = 4 * ks + g4;
+      const float* dr = dus + jr * (A + 1) + jl;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int tl = w + 4 * u;
+        gacc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(cseg[jr + 16 * (tl >> 3) + jl], dr[16 * (tl & 7)], gacc[u], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int tl = w + 4 * u;
+        dwg[(16 * (tl >> 3) + 4 * g4 + i) * A + 16 * (tl & 7) + jl] = odw[4 * u + i] + gacc[u][i];
+      }
   }
   // ---- df^T[c][j] = Σ_k W_loc[c][k] du[j][k]: wave w owns the position tile 16 w (16 rows), both
   // filter tiles; A [c = 16 mt + jl][k = 4 ks + g4] from wls, B [k][j = 16 w + jl] from dus
@@ -2561,6 +2596,7 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->TH, TB * Tin * A); f(c->E, B * Tin); f(c->DF, B * Tin * F); f(c->PQ, B * NT * A); f(c->DVAL, B * Tin * D); f(c->DMEM, B * Tin * D);
   f(c->dZ, TB * P); f(c->dPre, TB * P);
   f(c->DF2, 2 * B * Tin * F); f(c->DCUM2, 2 * B * Tin); f(c->PQ2, 2 * B * NT * A); f(c->SC2, 2 * B * 4); f(c->DWG, 32 * A);
+  f(c->DWGP, B * NT * 32 * A);
   f(c->W1T, P * NM); f(c->sDZ, B * P); f(c->sDP, B * P); f(c->sDX, B * NM); c->TLEN.alloc(sizeof(int) * (size_t)B);
   const long tmax = std::max({TB * LX1, TB * (H + D), TB * 2 * H, B * Tin * D, TB * P, TB * NM, TB * Tin * F,
                               // Postnet im2col^T: K·cin rows per position, cin = num_mels for layer 1
@@ -3084,7 +3120,8 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   const bool att_q = att_q_env && fused && A == 128 && F == 32 && KW == 31 && D % 4 == 0 && D <= 1024 && Tin <= 256;
   const int nq = std::min(4, NT);
   if (att_q)
-    for (DevBuf* d : {&c->DF2, &c->DCUM2, &c->SC2}) TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+    for (DevBuf* d : {&c->DF2, &c->DCUM2, &c->SC2, &c->DWGP}) TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+  at.DWGP = c->DWGP.as<float>();
   // TT2_ATTQ_STAMP=<step>: k_tr_att_bwd_q stage stamps of that step -> TT2_ATTQ_STAMP_FILE (diagnostic)
   const char* aqs = std::getenv("TT2_ATTQ_STAMP");
   at.stamps = nullptr;
@@ -3238,7 +3275,15 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     // and never more than TBUF holds (small T·B configurations have a small TBUF)
     const long cap = (long)(c->TBUF.bytes / sizeof(float)) / ((long)F * A);
     const long cap32 = (long)(c->TBUF.bytes / sizeof(float)) / (32L * A);
-    if (tr_dwloc_cum_ok(c) && cap32 >= 1) {
+    if (att_q) {  // k_tr_att_bwd_q accumulated G per (row, range) slot; row 31 = Σ du = d b_a (just summed)
+      tr_colsum(c, c->DWGP.as<float>(), BNT, 32 * A, 32L * A, c->DWG.as<float>(), s);
+      TT2_HIP(hipMemcpyAsync(c->DWG.as<float>() + 31L * A, gvar(c, LAV("attention_bias")), sizeof(float) * (size_t)A,
+                             hipMemcpyDeviceToDevice, s));
+      hipLaunchKernelGGL(k_tr_dwloc_fin, dim3((F * A + 255) / 256), dim3(256), 0, s, c->DWG.as<float>(),
+                         pvar(c, LAV("location_features_convolution/kernel")),
+                         pvar(c, LAV("location_features_convolution/bias")), F, A, KW,
+                         gvar(c, LAV("location_features_layer/kernel")));
+    } else if (tr_dwloc_cum_ok(c) && cap32 >= 1) {
       const long nb = std::min<long>(512, cap32);
       const long rpb = ((R + nb - 1) / nb + 31) / 32 * 32;
       const int nbk = (int)((R + rpb - 1) / rpb);
