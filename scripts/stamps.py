@@ -19,3 +19,18 @@ for i in ORDER:
         if len(v):
             line += f"  {k}: {np.median(v):6.2f} / {v.max():6.2f}"
     print(line)
+
+# per-XCD view (slot 31 = HW_REG_XCC_ID of the work-group, slots 22..29 = wave w's context-load miss)
+if s[:, 31].any() or (s[:, 31] == 0).all():
+    xcc = s[:, 31]
+    print("XCD of work-group g: g % 8 ->", [int(np.bincount(xcc[g % 8 == k]).argmax()) for k in range(8)])
+    for i in (13, 20, 14, 15, 0, 1, 4):
+        line = f"{i:2d} {NAMES[i]:16s}"
+        for x in range(8):
+            v = r[xcc == x, i][s[xcc == x, i] != 0]
+            line += f" x{x}:{np.median(v):6.2f}" if len(v) else ""
+        print(line)
+    miss = (s[:, 22:30] != 0)
+    print("context-load misses per XCD (waves):", [int(miss[xcc == x].sum()) for x in range(8)])
+    tail = r[:, 15] - r[:, 14]
+    print("L1 context-row tail (15 - 14) median per XCD:", [round(float(np.median(tail[xcc == x])), 2) for x in range(8)])

@@ -26,9 +26,9 @@ constexpr int PD_NREP = 8;    // replicas of the H1/H2 flag lines (32 pollers pe
 // float4 (common.h af_idx), 16(g/4) + g%4 + 4q.  Tiles [32w, 32w+32) own units [128w, 128w+128).
 __host__ __device__ inline int pd_unit(int g, int q) { return 16 * (g >> 2) + (g & 3) + 4 * q; }
 enum { PD_F_PRE = 0, PD_F_H1, PD_F_H2, PD_F_E, PD_F_CTX, PD_F_PP, PD_F_QE, PD_F_CMB, PD_F_EO, PD_F_EMT, PD_NPH };
-// Tacotron_emt_attn 'multihead' in the persistent decoder (k_decode_persist<true>): the emotion query
-// (128) rides as 8 more projection tiles; 16 emotion work-groups own 2 rows each; the attn_emt dense
-// (KC -> 128) runs on the 64 emotion-query projection work-groups.
+// Tacotron_emt_attn 'multihead' / 'style_tokens' in the persistent decoder (k_decode_persist<true>): the
+// emotion query (128) rides as 8 more projection tiles; 16 emotion work-groups own 2 rows each; the
+// attn_emt dense (KC -> 128, 'multihead' only) runs on the 64 emotion-query projection work-groups.
 constexpr int PD_ENT = 8;        // emotion-query projection tiles (128 = style_att_dim)
 constexpr int PD_EG0 = 240;      // first emotion work-group (rows 2(g-240), +1)
 constexpr int PD_EQ = 128;       // emotion query width = attn_emt dense output width
@@ -81,6 +81,10 @@ struct PdArgs {
   // Tacotron_emt_attn 'multihead' (k_decode_persist<true> only)
   int K1;               // LSTM-1 critical rows per tile: P + E2 (+ 128 emotion block)
   int e_Tv, e_Dv, e_KC, e_heads, e_dh;  // attended rows, value width, heads x Dv, heads, dims per head
+  int e_dense;          // 1 'multihead': contexts -> attn_emt dense (+ refnet_spk) = the block; 0 'style_tokens':
+                        // the heads-concatenated contexts are the block
+  int e_XW;             // block width joining LSTM-1 (128 'multihead', 64 'style_tokens')
+  long e_vbs, e_kbs;    // batch strides of e_val / e_ke (0: style tokens shared by every row)
   const float* e_ke;    // [B][Tv][128] keys of the attended values (conv1d_1 + bias)
   const float* e_val;   // [B][Tv][Dv] attended values
   const float* e_qrow;  // [32][128] query bias per row

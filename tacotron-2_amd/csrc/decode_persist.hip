@@ -402,8 +402,9 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   }
   f32x4 w1e = zero4, wdf = zero4;  // EMT: L1 emotion-block rows (k-group 48 + w); dense fragment (q blocks)
   if constexpr (EMT) {
-    w1e = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * K1S * 16)[((PD_P + PD_E2) / 16 + w) * 64 + lane];
-    if (isq && w < a.e_KC / 128)
+    if (w < a.e_XW / 16)  // the block's k-groups ('style_tokens': 4 of the 8 waves)
+      w1e = reinterpret_cast<const f32x4*>(a.l1_w + (long)g * K1S * 16)[((PD_P + PD_E2) / 16 + w) * 64 + lane];
+    if (a.e_dense && isq && w < a.e_KC / 128)
       wdf = reinterpret_cast<const f32x4*>(a.e_wd + (long)(pn - PD_NTILE) * a.e_KC * 16)[(pks * (a.e_KC / 128) + w) * 64 + lane];
   }
   // location-conv WF fragments of this slice in LDS (2 KB after si: the same for every wave)
@@ -560,6 +561,9 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     em = (tid >> 2) & 31;
     eu = tid & 3;
     PD_STAMP(0);
+    if constexpr (!EMT) {  // diagnostic: the hardware XCD of this work-group (HW_REG_XCC_ID bits 3:0)
+      if (stp && tid == 0) stp[g * 32 + 31] = __builtin_amdgcn_s_getreg(0x1814) & 15;
+    }
     float keep1n, keep2n;  // prenet keep bits of step t+1, in flight during the whole step
     prenet_keep(t + 1, tid, keep1n, keep2n);
     // ================= A: LSTM layer 1 =================
@@ -923,7 +927,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int e = tid + PD_NT * u, rr = e >= nv, b2 = r0 + rr;
-          vt[u] = (vl && e < 2 * nv && b2 < a.B) ? a.e_val[(long)b2 * nv + (e - rr * nv)] : 0.f;
+          vt[u] = (vl && e < 2 * nv && b2 < a.B) ? a.e_val[b2 * a.e_vbs + (e - rr * nv)] : 0.f;
         }
         {  // 4 of the 8 K-split partials per thread (threads 256.. take splits 4..7): few registers
           const int row = r0 + ((tid >> 7) & 1), col = tid & 127, hs = tid >> 8;
@@ -953,7 +957,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
             for (int u = 0; u < 4; ++u) {
               const int sidx = s0 + (tid >> 5) + 16 * u;
               const int rr = sidx / HT, hh = (sidx % HT) / a.e_Tv, tv = sidx % a.e_Tv, b2 = r0 + rr;
-              kx[u] = (sidx < 2 * HT && b2 < a.B && d < dh) ? a.e_ke[((long)b2 * a.e_Tv + tv) * PD_EQ + hh * dh + d] : 0.f;
+              kx[u] = (sidx < 2 * HT && b2 < a.B && d < dh) ? a.e_ke[b2 * a.e_kbs + (long)tv * PD_EQ + hh * dh + d] : 0.f;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -984,12 +988,14 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         {  // contexts, heads concatenated (_combine_heads): one AF float4 = k = i0 + 4c (c < 4, one head) of
            // one row per thread, stored as ONE 16-byte write-through store
           const int nq = a.e_KC / 4;
-          const auto rc = __builtin_amdgcn_make_buffer_rsrc(a.CMBx + (long)p * 32 * a.e_KC, (short)0, 0x7fffffff, 0x00020000);
+          // 'multihead': the contexts go to the dense blocks (CMB); 'style_tokens': they are the block (EMT)
+          float* const cdst = a.e_dense ? a.CMBx + (long)p * 32 * a.e_KC : a.EMTx + (long)p * 32 * PD_EQ;
+          const auto rc = __builtin_amdgcn_make_buffer_rsrc(cdst, (short)0, 0x7fffffff, 0x00020000);
           for (int e = tid; e < 2 * nq; e += PD_NT) {
             const int rr = e >= nq, q = e - rr * nq, b2 = r0 + rr;
             const int i0 = 16 * (q >> 2) + (q & 3), hh = i0 / a.e_Dv, d0 = i0 - hh * a.e_Dv;
             const float* al = sco + (rr * a.e_heads + hh) * a.e_Tv;
-            const float* v = vl ? vls + rr * nv + d0 : a.e_val + (long)min(b2, a.B - 1) * nv + d0;
+            const float* v = vl ? vls + rr * nv + d0 : a.e_val + min(b2, a.B - 1) * a.e_vbs + d0;
             float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
             for (int tv = 0; tv < a.e_Tv; ++tv) {
               const float wt = al[tv];
@@ -1006,13 +1012,14 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           }
         }
         PD_STAMP(31);
-        pd_publish(a, PD_F_CMB, tg, tid);
+        if (a.e_dense) pd_publish(a, PD_F_CMB, tg, tid);
+        else pd_publish_rep(a, 2, tg, tid);
         PD_STAMP(24);
         for (int e = tid; e < 2 * HT; e += PD_NT) {  // emotion alignments (output only: after the publish)
           const int rr = e / HT, b2 = r0 + rr;
           if (b2 < a.B) a.e_hist[((long)t * a.B + b2) * HT + (e - rr * HT)] = sco[e];
         }
-      } else if (isq) {  // attn_emt dense (Architecture_wrappers.py:233-234): tile pn - PD_NTILE, K split pks
+      } else if (isq && a.e_dense) {  // attn_emt dense (Architecture_wrappers.py:233-234): tile pn - PD_NTILE, K split pks
         if (!pd_block_wait(si + 6, [&] { return pd_poll(a, PD_F_CMB, PD_EG0, 1, 16, tg, 0, lane); })) return;
         PD_STAMP(25);
         const int nkg = a.e_KC / 128;  // k-groups per split
@@ -1101,7 +1108,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     __syncthreads();  // red reuse by stage A
     PD_STAMP(14);
     if constexpr (EMT) {
-      if (g >= PD_EG0) {  // dense partials of rows r0, r0+1 -> the next step's emotion block (+ refnet_spk),
+      if (g >= PD_EG0 && a.e_dense) {  // dense partials of rows r0, r0+1 -> the next step's emotion block (+ refnet_spk),
                           // after this work-group's own prenet hand-off
         const int r0 = 2 * (g - PD_EG0);
         {
@@ -1132,7 +1139,12 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       accC1 = zero4;
       f32x4 xv[8];  // wave w: channels [64w, 64w + 64) = slice j = w, producers [32w, 32w + 32)
       if (!pd_take4<8>(a, PD_F_CTX, XC, [&](int i) { return ((4 * w + (i >> 1)) * 2 + (i & 1)) * 64 + lane; }, tb, xv,
-                       [&] { return pd_poll(a, PD_F_CTX, 32 * w, 1, 32, tg, 0, lane); }))
+                       [&] {
+                         if constexpr (!EMT) {  // diagnostic: when wave w's optimistic context load missed
+                           if (stp && lane == 0) stp[g * 32 + 22 + w] = __builtin_amdgcn_s_memrealtime();
+                         }
+                         return pd_poll(a, PD_F_CTX, 32 * w, 1, 32, tg, 0, lane);
+                       }))
         si[8] = 1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) kg_mfma(xv[2 * i], xv[2 * i + 1], w1c[i], accC0, accC1);

@@ -1706,10 +1706,13 @@ static void finalize(tt2_ctx* c) {
       const auto pw = pack_wf(W.data(), c->Kp, NPF, cols, c->Kp);  // rows [h2 | context_enc]
       c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pw));
       upload(c->proj_w, pw);
-      if (c->emt.attn == EMT_MULTIHEAD && c->emt.Aq == PD_EQ) {
-        // persistent decoder: 8 more tiles = the emotion query h2·W_q (multihead conv1d, first H rows;
-        // zero context rows), Architecture_wrappers.py:228-232 / multihead_attention.py:71
-        const auto& kq = need(wm, P + "decoder/Multihead-attention-attn_emt/conv1d/kernel", {1, c->H, PD_EQ});
+      const bool emt_mh = c->emt.attn == EMT_MULTIHEAD || c->emt.attn == EMT_STYLE_TOKENS;
+      if (emt_mh && c->emt.Aq == PD_EQ) {
+        // persistent decoder: 8 more tiles = the emotion query h2·W_q (multihead conv1d, first H rows --
+        // 'style_tokens' appends the one-hot label rows, folded into the per-row query bias; zero context
+        // rows), Architecture_wrappers.py:228-232 / multihead_attention.py:71
+        const int qin = c->H + (c->emt.attn == EMT_STYLE_TOKENS ? c->emt.n_emt : 0);
+        const auto& kq = need(wm, P + "decoder/Multihead-attention-attn_emt/conv1d/kernel", {1, qin, PD_EQ});
         const int NX = NPF + PD_EQ;
         std::vector<float> Wx((size_t)c->Kp * NX, 0.f);
         std::vector<int> colx;
@@ -1722,13 +1725,15 @@ static void finalize(tt2_ctx* c) {
         const auto pwx = pack_wf(Wx.data(), c->Kp, NX, colx, c->Kp);
         c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pwx));
         upload_scaled(c->pd_proj_w, pwx, KG_SB);
-        const int KC = c->emt.heads * c->emt.Dv;
-        const auto& kd = need(wm, P + "decoder/attn_emt/dense/kernel", {KC, EMT_OUT});
-        std::vector<int> ocols;
-        for (int j = 0; j < EMT_OUT; ++j) ocols.push_back(j);
-        const auto pwd = pack_wf(kd.data.data(), KC, EMT_OUT, ocols, KC);
-        c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pwd));
-        upload_scaled(c->pd_e_wd, pwd, KG_SB);
+        if (c->emt.attn == EMT_MULTIHEAD) {  // the attn_emt dense as WF tiles ('style_tokens' has none)
+          const int KC = c->emt.heads * c->emt.Dv;
+          const auto& kd = need(wm, P + "decoder/attn_emt/dense/kernel", {KC, EMT_OUT});
+          std::vector<int> ocols;
+          for (int j = 0; j < EMT_OUT; ++j) ocols.push_back(j);
+          const auto pwd = pack_wf(kd.data.data(), KC, EMT_OUT, ocols, KC);
+          c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pwd));
+          upload_scaled(c->pd_e_wd, pwd, KG_SB);
+        }
       } else {
         upload_scaled(c->pd_proj_w, pw, KG_SB);
       }
@@ -2266,9 +2271,12 @@ static void check_encoder(tt2_ctx* c) {
 static bool pd_emt(const tt2_ctx* c) {
   const auto& m = c->emt;
   const int KC = m.heads * m.Dv;
-  return m.attn == EMT_MULTIHEAD && m.Aq == PD_EQ && m.XW == PD_EQ && (KC == 512 || KC == 1024) && m.Tv >= 1 &&
-         m.Tv <= 64 && 2 * m.heads * m.Tv <= 128 && m.dh <= 32 && c->K1 == PD_P + PD_E2 + PD_EQ &&
-         c->pd_e_wd.p;
+  // 'multihead': contexts (KC = heads x Dv) -> attn_emt dense (128) = the block; 'style_tokens': 4 x 16
+  // contexts over the 24 tokens = the 64-wide block (no dense, no refnet_spk term)
+  const bool mh = m.attn == EMT_MULTIHEAD && m.XW == PD_EQ && (KC == 512 || KC == 1024) && c->pd_e_wd.p;
+  const bool st = m.attn == EMT_STYLE_TOKENS && m.XW == 64 && KC == 64 && m.Dv == 16;
+  return (mh || st) && m.Aq == PD_EQ && m.Tv >= 1 && m.Tv <= 64 && 2 * m.heads * m.Tv <= 192 && m.dh <= 32 &&
+         c->K1 == PD_P + PD_E2 + m.XW;
 }
 
 static bool pd_fits(tt2_ctx* c) {
@@ -2355,6 +2363,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   if (emt) {
     const auto& m = c->emt;
     a.e_Tv = m.Tv; a.e_Dv = m.Dv; a.e_KC = m.heads * m.Dv; a.e_heads = m.heads; a.e_dh = m.dh;
+    a.e_dense = m.attn == EMT_MULTIHEAD; a.e_XW = m.XW; a.e_vbs = m.val_bstride(); a.e_kbs = m.ke_bstride();
     a.e_ke = m.ke.as<float>(); a.e_val = m.val.as<float>(); a.e_qrow = m.qrow.as<float>();
     a.e_vv = m.vv.as<float>(); a.e_ab = m.ab.as<float>(); a.e_wd = c->pd_e_wd.as<float>(); a.e_bd = m.bd.as<float>();
     a.e_spk = emt_spk(c); a.e_hist = m.hist.as<float>();

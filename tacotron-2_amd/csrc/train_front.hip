@@ -206,38 +206,46 @@ __global__ void k_fe_relu_mask(const float* __restrict__ dy, const float* __rest
 void fe_relu_mask(const float* dy, const float* y, long n, float* out, hipStream_t s) {
   hipLaunchKernelGGL(k_fe_relu_mask, dim3(fe_blk(n)), dim3(256), 0, s, dy, y, n, out);
 }
-// out[((i*3 + j)*C + c) * ldo + m] = x(n, st ho + i - pt, st wo + j - pl, c), m = (n*Ho + ho)*Wo + wo
-__global__ void k_fe_im2col2d_t(const float* __restrict__ x, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl,
-                                float* __restrict__ out, long ldo, int st) {
-  const long M = (long)N * Ho * Wo;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 9L * C * M) return;
-  const long m = i % M, k = i / M;
-  const int c = (int)(k % C), ij = (int)(k / C), ii = ij / 3, jj = ij % 3;
-  const int wo = (int)(m % Wo), ho = (int)((m / Wo) % Ho), n = (int)(m / ((long)Wo * Ho));
+// out[((i*3 + j)*C + c) * ldo + m] = x(n, st ho + i - pt, st wo + j - pl, c), m = (n*Ho + ho)*Wo + wo.
+// Grid (M / 256, 9 C): the column k = (i*3 + j)*C + c is the block's y (uniform), m the thread's x, so
+// the stores of a wave are one contiguous run and the index arithmetic is 32-bit (the 1-D form's
+// 64-bit i / M, i % M per element bound it at 0.5 TB/s)
+__global__ __launch_bounds__(256) void k_fe_im2col2d_t(const float* __restrict__ x, int N, int H, int W, int C, int Ho,
+                                                       int Wo, int pt, int pl, float* __restrict__ out, long ldo, int st) {
+  const int M = N * Ho * Wo;
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const int k = blockIdx.y, c = k % C, ij = k / C, ii = ij / 3, jj = ij - 3 * ii;
+  const int wo = m % Wo, r = m / Wo, ho = r % Ho, n = r / Ho;
   const int h = st * ho + ii - pt, w = st * wo + jj - pl;
-  out[k * ldo + m] = (h >= 0 && h < H && w >= 0 && w < W) ? x[(((long)n * H + h) * W + w) * C + c] : 0.f;
+  out[(long)k * ldo + m] = (h >= 0 && h < H && w >= 0 && w < W) ? x[((long)(n * H + h) * W + w) * C + c] : 0.f;
 }
 void fe_im2col2d_t(const float* x, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* out, long ldo,
                    hipStream_t s, int st) {
-  hipLaunchKernelGGL(k_fe_im2col2d_t, dim3(fe_blk(9L * C * N * Ho * Wo)), dim3(256), 0, s, x, N, H, W, C, Ho, Wo, pt,
-                     pl, out, ldo, st);
+  const long M = (long)N * Ho * Wo;
+  TT2_CHECK(M < (1L << 31) && 9L * C <= 65535, TT2_ERR_SHAPE_MISMATCH, "im2col2d: shape exceeds the 32-bit grid");
+  hipLaunchKernelGGL(k_fe_im2col2d_t, dim3((unsigned)((M + 255) / 256), 9 * C), dim3(256), 0, s, x, N, H, W, C, Ho, Wo,
+                     pt, pl, out, ldo, st);
 }
 // dx(n, h, w, c) = Σ_{i,j} dcols[(n, ho, wo)][(i*3+j)*C + c] over the outputs whose taps read it
-__global__ void k_fe_col2im2d(const float* __restrict__ dcols, int N, int H, int W, int C, int Ho, int Wo, int pt,
-                              int pl, float* __restrict__ dx, int st) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)N * H * W * C) return;
-  const int c = (int)(i % C), w = (int)((i / C) % W), h = (int)((i / ((long)C * W)) % H);
-  const int n = (int)(i / ((long)C * W * H));
+// (32-bit index arithmetic; stride 1 / 2 as a uniform branch)
+__global__ __launch_bounds__(256) void k_fe_col2im2d(const float* __restrict__ dcols, int N, int H, int W, int C, int Ho,
+                                                     int Wo, int pt, int pl, float* __restrict__ dx, int st) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * H * W * C) return;
+  const int c = i % C, r0 = i / C, w = r0 % W, r1 = r0 / W, h = r1 % H, n = r1 / H;
   float acc = 0.f;
+#pragma unroll
   for (int ii = 0; ii < 3; ++ii) {
     const int hh = h + pt - ii;
-    if (hh < 0 || hh % st || hh / st >= Ho) continue;
+    const int ho = st == 1 ? hh : hh >> 1;
+    if (hh < 0 || (st != 1 && (hh & 1)) || ho >= Ho) continue;
+#pragma unroll
     for (int jj = 0; jj < 3; ++jj) {
       const int ww = w + pl - jj;
-      if (ww < 0 || ww % st || ww / st >= Wo) continue;
-      const long m = ((long)n * Ho + hh / st) * Wo + ww / st;
+      const int wo = st == 1 ? ww : ww >> 1;
+      if (ww < 0 || (st != 1 && (ww & 1)) || wo >= Wo) continue;
+      const long m = (long)(n * Ho + ho) * Wo + wo;
       acc += dcols[m * 9 * C + (ii * 3 + jj) * C + c];
     }
   }
@@ -245,7 +253,9 @@ __global__ void k_fe_col2im2d(const float* __restrict__ dcols, int N, int H, int
 }
 void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* dx,
                  hipStream_t s, int st) {
-  hipLaunchKernelGGL(k_fe_col2im2d, dim3(fe_blk((long)N * H * W * C)), dim3(256), 0, s, dcols, N, H, W, C, Ho, Wo, pt,
+  const long n = (long)N * H * W * C;
+  TT2_CHECK(n < (1L << 31) && (st == 1 || st == 2), TT2_ERR_SHAPE_MISMATCH, "col2im2d: shape / stride unsupported");
+  hipLaunchKernelGGL(k_fe_col2im2d, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dcols, N, H, W, C, Ho, Wo, pt,
                      pl, dx, st);
 }
 

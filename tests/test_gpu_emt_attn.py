@@ -183,3 +183,25 @@ def test_multihead_persistent_matches_launch_path_b32():
     assert steps >= 20
     np.testing.assert_allclose(a["frames"][:, :steps], b["frames"][:, :steps], atol=1e-3)
     np.testing.assert_allclose(ea[..., :steps], eb[..., :steps], atol=1e-3)
+
+
+def test_style_tokens_full_width_persistent():
+    """'style_tokens' at the fork widths runs in k_decode_persist<true> (round 5): the emotion query
+    [h2 | one-hot label] as 8 more projection tiles (label rows in the per-row query bias), the 16
+    emotion work-groups attend over the 24 shared tanh(style tokens) (4 heads x 16), and the
+    heads-concatenated contexts are the 64-wide LSTM-1 block themselves (no dense, no speaker term).
+    Ragged rows with an out-of-range label (tf.one_hot's zero row), against the oracle at 1e-4."""
+    _case(full_hparams(), "style_tokens", "none", B=4, T=9, T_ref=80, n=14, labels=[0, 3, 1, 7],
+          persistent_expected=1)
+
+
+def test_style_tokens_persistent_configs1_gta_vs_oracle():
+    """configs[1] shape (B = 32 ragged rows x 201 chars) through the persistent 'style_tokens'
+    decoder, 200 teacher-forced steps against the oracle at 1e-4, every step's emotion weights too."""
+    hp = full_hparams()
+    B, T, n = 32, 201, 200
+    tg = np.random.default_rng(5).normal(0, 1, (B, n, hp.num_mels)).astype(np.float32)
+    labels = [i % 5 for i in range(B)]
+    out, _ = _case(hp, "style_tokens", "none", B=B, T=T, T_ref=80, n=n, seed=9, targets=tg, labels=labels,
+                   persistent_expected=1)
+    assert out["frames"].shape[1] == n
