@@ -464,8 +464,7 @@ def bench_e2e(a, rank, world, local, barrier, max_over_ranks):
 
 def bench_variants(a, local):
     """Model variants on the configs[1] shape (B=32 x 201 chars, T_ref 400, T_out 1000; rank 0):
-    Tacotron_emt_attn (args.attn 'multihead': persistent decoder, k_decode_persist<true>; 'style_tokens':
-    per-step launch path + k_emt_step),
+    Tacotron_emt_attn (args.attn 'multihead' and 'style_tokens': persistent decoder, k_decode_persist<true>),
     the AdaIN and reference-embedding style paths (persistent decoder), and the CBHG linear post-net
     over the 32 x 1000 mel frames.  Device-resident inputs, tt2_synthesize_dev, HIP-event phases."""
     import torch

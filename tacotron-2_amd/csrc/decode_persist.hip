@@ -328,9 +328,19 @@ __device__ __forceinline__ void tail_bar(int* ctr, unsigned& gen, int lane) {
 // [0, 256) resident like TM = 256 and streams those of [256, 512) from L2 / MALL every step (issued
 // ahead of the energy take); its alignments live in the stage scratch (red + 2048: free during the
 // softmax / context stage) so the cumulative alignments can take their place (15 + 512 + 17 floats).
-template <bool EMT, int TM>
+// FL (diagnostic, TT2_PD_FLOOR=1): the "floor" instance -- every exchange, poll, barrier and load of the
+// production kernel, with the arithmetic of the stage bodies removed (the MFMA products, the query /
+// prenet / context dot products and the energies' tanh reductions consume their operands through an
+// empty asm sink instead): the step time that is hand-offs + memory round trips alone.  Results garbage.
+template <bool EMT, int TM, bool FL>
 __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   static_assert(TM == PD_TMAX || (TM == PD_TMAX_LONG && !EMT), "k_decode_persist geometry");
+  static_assert(!FL || (!EMT && TM == PD_TMAX), "floor instance: the Tacotron decoder only");
+  // split fp16x3 product, or (FL) its operands sunk
+  const auto mm = [](const f32x4& a0, const f32x4& a1, const f32x4& bw, f32x4& c0, f32x4& c1) {
+    if constexpr (FL) asm volatile("" ::"v"(a0), "v"(a1), "v"(bw));
+    else kg_mfma(a0, a1, bw, c0, c1);
+  };
   constexpr int NI = TM / 128;          // 16-position key / location tiles per wave
   constexpr int NWE = TM / 64;          // waves holding one energy per lane in the softmax
   constexpr int CWN = TM == PD_TMAX ? 288 : 544;  // cumulative-alignment floats (zero padded)
@@ -450,7 +460,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
   f32x4 accC0 = zero4, accC1 = zero4;  // L1 context rows of the next step (context(-1) = 0)
   if constexpr (EMT) {  // the emotion block of step 0 (zero_state: refnet_spk alone), host-written at parity 1
     const float* XE = a.EMTx + 32 * PD_EQ;
-    kg_mfma(pd_ld4(XE, (w * 2) * 64 + lane), pd_ld4(XE, (w * 2 + 1) * 64 + lane), w1e, accC0, accC1);
+    mm(pd_ld4(XE, (w * 2) * 64 + lane), pd_ld4(XE, (w * 2 + 1) * 64 + lane), w1e, accC0, accC1);
   }
   f32x4 q1a = zero4, q1b = zero4, q2a = zero4, q2b = zero4;  // this wave's Q partials of RG1, RG2
   const long BP = (long)a.B * PD_P;
@@ -492,7 +502,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       const int k16 = tid >> 5;  // wave w: k16 = 2w (lanes 0..31), 2w + 1 (lanes 32..63)
       float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s += x1[16 * k16 + i] * o.w2p[i >> 2][i & 3];
+      for (int i = 0; i < 16; ++i)
+        if (!FL || i == 0) s += x1[16 * k16 + i] * o.w2p[i >> 2][i & 3];
       s += __shfl_xor(s, 32);
       if ((tid & 63) < 32) red[(tid >> 6) * 32 + (tid & 31)] = s;
     }
@@ -534,7 +545,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int sg = 8 * w + 4 * h + i;
-      kg_mfma(xv[2 * i], xv[2 * i + 1], Wv[sg * 64 + lane], Qa, Qb);
+      mm(xv[2 * i], xv[2 * i + 1], Wv[sg * 64 + lane], Qa, Qb);
     }
   };
   __syncthreads();
@@ -626,7 +637,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       // L1 context rows of t-1 (accumulated during the prenet hand-off) + this wave's RG1 partial
       f32x4 s0 = accC0 + a.one_m_zo * q1a, s1 = accC1 + a.one_m_zo * q1b;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) kg_mfma(a0[i], a1[i], w1p[i], s0, s1);
+      for (int i = 0; i < 2; ++i) mm(a0[i], a1[i], w1p[i], s0, s1);
       PD_STAMP(18);
       put_partials(s0, s1, red, w, lane);
       __syncthreads();
@@ -678,7 +689,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           if (!pd_take4<8>(a, PD_F_H1, X, ix, tb, xv, [] { return true; })) si[8] = 1;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) kg_mfma(xv[2 * i], xv[2 * i + 1], w2i[4 * h + i], s0, s1);
+        for (int i = 0; i < 4; ++i) mm(xv[2 * i], xv[2 * i + 1], w2i[4 * h + i], s0, s1);
       }
       PD_STAMP(16);
       put_partials(s0, s1, red, w, lane);
@@ -733,10 +744,15 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       {
         const int seg = tid >> 4;
         float s = 0.f;
+        if constexpr (FL) {
+          s = red[seg * 32];
+          asm volatile("" ::"v"(wq[0]), "v"(wq[1]), "v"(wq[2]), "v"(wq[3]), "v"(wq[4]), "v"(wq[5]), "v"(wq[6]), "v"(wq[7]));
+        } else {
 #pragma unroll
-        for (int ii = 0; ii < 32; ++ii) s += red[seg * 32 + ii] * wq[ii >> 2][ii & 3];
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
+          for (int ii = 0; ii < 32; ++ii) s += red[seg * 32 + ii] * wq[ii >> 2][ii & 3];
+          s += __shfl_xor(s, 16);
+          s += __shfl_xor(s, 32);
+        }
         if (lane < 16) red[1024 + w * 16 + lane] = s;
       }
       __syncthreads();
@@ -753,7 +769,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       for (int i = 0; i < NI; ++i) {
         float e4[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) e4[r] = sum16(va_k * tanh_fast(kv[i][r] + qk + loc[i][r]));
+        for (int r = 0; r < 4; ++r)
+          e4[r] = FL ? kv[i][r] + qk + loc[i][r] : sum16(va_k * tanh_fast(kv[i][r] + qk + loc[i][r]));
         const int rr = lane & 3;
         sel[i] = rr == 0 ? e4[0] : rr == 1 ? e4[1] : rr == 2 ? e4[2] : e4[3];
       }
@@ -776,7 +793,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       if (!pd_take4<2>(a, PD_F_H2, X, [&](int i) { return (sg * 2 + i) * 64 + lane; }, tb, xv,
                        [&] { return pd_poll_rep(a, PD_F_H2, 1, 32 * pks, tg, lane); }))
         si[8] = 1;
-      kg_mfma(xv[0], xv[1], WPH[w * 64 + lane], s0, s1);
+      mm(xv[0], xv[1], WPH[w * 64 + lane], s0, s1);
       reduce_waves_32x16<8>(s0, s1, red, G, w, lane, tid);
       if (isq) {  // emotion query: h2 rows are all of it -> granules for the emotion work-groups
         const int m = tid >> 4, col = tid & 15;
@@ -875,7 +892,9 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         const int c = tid & 63, ts = tid >> 6;
         float s = 0.f;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) s += al[ts * 32 + i] * vals[i >> 2][i & 3];
+        for (int i = 0; i < 32; ++i)
+          if (!FL || i == 0) s += al[ts * 32 + i] * vals[i >> 2][i & 3];
+        if constexpr (FL) asm volatile("" ::"v"(vals[1]), "v"(vals[2]), "v"(vals[3]), "v"(vals[4]), "v"(vals[5]), "v"(vals[6]), "v"(vals[7]));
         if constexpr (TM != PD_TMAX) {
 #pragma unroll
           for (int i = 0; i < 32; ++i) s += al[PD_TMAX + ts * 32 + i] * vhi[i >> 2][i & 3];
@@ -909,7 +928,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          l = __builtin_amdgcn_mfma_f32_16x16x4f32(cw[t0 + 16 * sg + 4 * e], swl[64 * sg + lane][e], l, 0, 0, 0);
+          if constexpr (FL) asm volatile("" ::"v"(cw[t0 + 16 * sg + 4 * e]), "v"(swl[64 * sg + lane][e]));
+          else l = __builtin_amdgcn_mfma_f32_16x16x4f32(cw[t0 + 16 * sg + 4 * e], swl[64 * sg + lane][e], l, 0, 0, 0);
       loc[i] = l;
     }
     // ================= E: projection partial, context rows =================
@@ -1027,7 +1047,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           const float* X = a.CMBx + (long)p * 32 * a.e_KC;
           const int sg = pks * nkg + w;
           f32x4 s0 = zero4, s1 = zero4;
-          kg_mfma(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wdf, s0, s1);
+          mm(pd_ld4(X, (sg * 2) * 64 + lane), pd_ld4(X, (sg * 2 + 1) * 64 + lane), wdf, s0, s1);
           put_partials(s0, s1, red, w, lane);
         }
         __syncthreads();
@@ -1050,7 +1070,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         if (!pd_take4<2>(a, PD_F_CTX, X, [&](int i) { return (sg * 2 + i) * 64 + lane; }, tb, xv,
                          [&] { return pd_poll(a, PD_F_CTX, 32 * pks, 1, 32, tg, 0, lane); }))
           si[8] = 1;
-        kg_mfma(xv[0], xv[1], wpc, s0, s1);
+        mm(xv[0], xv[1], wpc, s0, s1);
         put_partials(s0, s1, red, w, lane);
       }
       __syncthreads();
@@ -1147,7 +1167,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
                        }))
         si[8] = 1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) kg_mfma(xv[2 * i], xv[2 * i + 1], w1c[i], accC0, accC1);
+      for (int i = 0; i < 4; ++i) mm(xv[2 * i], xv[2 * i + 1], w1c[i], accC0, accC1);
       if (w == 0) {  // Σ_{t<len} align of every row (written by the j = 0 work-groups, producers [0, 32))
         float sv[1];
         if (!pd_take1<1>(a, PD_F_CTX, a.SSx + p * 32, [&](int) { return lane & 31; }, tb, sv,
@@ -1160,7 +1180,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       if (!pd_block_wait(si + 6, [&] { return pd_poll_rep(a, PD_F_EMT, 2, PD_EG0, tg, lane, 16); })) return;
       PD_STAMP(29);
       const float* XE = a.EMTx + p * 32 * PD_EQ;
-      kg_mfma(pd_ld4(XE, (w * 2) * 64 + lane), pd_ld4(XE, (w * 2 + 1) * 64 + lane), w1e, accC0, accC1);
+      mm(pd_ld4(XE, (w * 2) * 64 + lane), pd_ld4(XE, (w * 2 + 1) * 64 + lane), w1e, accC0, accC1);
     }
     PD_STAMP(15);
   }
@@ -1176,15 +1196,16 @@ bool pd_device_ok(int dev) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   if (prop.multiProcessorCount < PD_NB) return false;
-  for (const void* k : {reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX>),
-                        reinterpret_cast<const void*>(k_decode_persist<true, PD_TMAX>),
-                        reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX_LONG>)})
+  for (const void* k : {reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX, false>),
+                        reinterpret_cast<const void*>(k_decode_persist<true, PD_TMAX, false>),
+                        reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX_LONG, false>),
+                        reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX, true>)})
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pd_lds_bytes()) != hipSuccess)
       return false;
   int nb = 0, ne = 0, nl = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_persist<false, PD_TMAX>, PD_NT, pd_lds_bytes()) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&ne, k_decode_persist<true, PD_TMAX>, PD_NT, pd_lds_bytes()) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nl, k_decode_persist<false, PD_TMAX_LONG>, PD_NT, pd_lds_bytes()) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_persist<false, PD_TMAX, false>, PD_NT, pd_lds_bytes()) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&ne, k_decode_persist<true, PD_TMAX, false>, PD_NT, pd_lds_bytes()) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nl, k_decode_persist<false, PD_TMAX_LONG, false>, PD_NT, pd_lds_bytes()) !=
           hipSuccess)
     return false;
   return nb >= 1 && ne >= 1 && nl >= 1;
@@ -1198,9 +1219,14 @@ void pd_launch(const PdArgs& a, hipStream_t s, bool emt, int tm) {
   TT2_CHECK(a.T_in >= 1 && a.T_in <= tm, TT2_ERR_INVALID_ARG, "persistent decoder: T_in outside the kernel's range");
   PdArgs arg = a;
   void* params[] = {&arg};
-  const void* k = emt ? reinterpret_cast<const void*>(k_decode_persist<true, PD_TMAX>)
-                  : tm == PD_TMAX ? reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX>)
-                                  : reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX_LONG>);
+  static const bool floor_env = [] {  // diagnostic: the arithmetic-free floor instance (see FL)
+    const char* e = std::getenv("TT2_PD_FLOOR");
+    return e && e[0] == '1';
+  }();
+  const void* k = emt ? reinterpret_cast<const void*>(k_decode_persist<true, PD_TMAX, false>)
+                  : tm != PD_TMAX ? reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX_LONG, false>)
+                  : floor_env     ? reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX, true>)
+                                  : reinterpret_cast<const void*>(k_decode_persist<false, PD_TMAX, false>);
   TT2_HIP(launch_persistent(k, dim3(PD_NB), dim3(PD_NT), params, (unsigned)pd_lds_bytes(), s));
 }
 
