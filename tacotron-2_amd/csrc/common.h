@@ -341,6 +341,27 @@ __device__ __forceinline__ void sum16x4(f32x4& a) {
   TT2_STEP(DPP_XOR1) TT2_STEP(DPP_XOR2) TT2_STEP(DPP_HALF_MIRROR) TT2_STEP(DPP_MIRROR)
 #undef TT2_STEP
 }
+// wave-uniform max / sum of 64 lanes from DPP row operations + the two row broadcasts (no LDS
+// round trip as __shfl_xor's ds_bpermute): the masked-off rows keep their own value
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float dpp_keep(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, RMASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_f<DPP_XOR1>(v));
+  v = fmaxf(v, dpp_f<DPP_XOR2>(v));
+  v = fmaxf(v, dpp_f<DPP_HALF_MIRROR>(v));
+  v = fmaxf(v, dpp_f<DPP_MIRROR>(v));
+  v = fmaxf(v, dpp_keep<0x142, 0xA>(v));  // row_bcast:15
+  v = fmaxf(v, dpp_keep<0x143, 0xC>(v));  // row_bcast:31
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = sum16(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 // after sum16: lane 31 of each 32-lane half holds that half's sum (rows 0+1, rows 2+3)
 __device__ __forceinline__ float sum32_to_lane31(float v) {
   v = sum16(v);

@@ -770,7 +770,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         float e4[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          e4[r] = FL ? kv[i][r] + qk + loc[i][r] : sum16(va_k * tanh_fast(kv[i][r] + qk + loc[i][r]));
+          e4[r] = FL ? kv[i][r] + qk + loc[i][r] : sum16(va_k * tanh_rcp(kv[i][r] + qk + loc[i][r]));
         const int rr = lane & 3;
         sel[i] = rr == 0 ? e4[0] : rr == 1 ? e4[1] : rr == 2 ? e4[2] : e4[3];
       }
@@ -836,8 +836,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           }
           if (a.mask_encoder && tid >= len) e = -INFINITY;
         }
-        float mx = e;
-        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        const float mx = wave_max_dpp(e);
         if (lane == 0) red[w] = mx;
       }
       __syncthreads();
@@ -846,9 +845,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       if (tid < TM) {
         float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
         if constexpr (NWE == 8) mx = fmaxf(mx, fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7])));
-        ex = tid < T ? expf(e - mx) : 0.f;
-        float sum = ex;
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        ex = tid < T ? __expf(e - mx) : 0.f;
+        const float sum = wave_sum_dpp(ex);
         if (lane == 0) red[8 + w] = sum;
       }
       __syncthreads();
@@ -856,7 +854,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       if (tid < TM) {
         float den = (red[8] + red[9]) + (red[10] + red[11]);
         if constexpr (NWE == 8) den += (red[12] + red[13]) + (red[14] + red[15]);
-        al[tid] = tid < T ? ex / den : 0.f;
+        al[tid] = tid < T ? ex * __builtin_amdgcn_rcpf(den) : 0.f;
       }
       __syncthreads();
       if (tid < T) {
@@ -984,7 +982,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
               const int sidx = s0 + (tid >> 5) + 16 * u;
               const int rr = sidx / HT, hh = (sidx % HT) / a.e_Tv;
               float x = 0.f;
-              if (sidx < 2 * HT && d < dh) x = vvd * tanh_fast(kx[u] + qe[rr * PD_EQ + hh * dh + d] + abd);
+              if (sidx < 2 * HT && d < dh) x = vvd * tanh_rcp(kx[u] + qe[rr * PD_EQ + hh * dh + d] + abd);
 #pragma unroll
               for (int o = 16; o >= 1; o >>= 1) x += __shfl_xor(x, o, 32);
               if (d == 0 && sidx < 2 * HT) sco[sidx] = x;
