@@ -464,7 +464,7 @@ def bench_e2e(a, rank, world, local, barrier, max_over_ranks):
 
 def bench_variants(a, local):
     """Model variants on the configs[1] shape (B=32 x 201 chars, T_ref 400, T_out 1000; rank 0):
-    Tacotron_emt_attn (args.attn 'multihead' and 'style_tokens': persistent decoder, k_decode_persist<true>),
+    Tacotron_emt_attn (args.attn 'multihead', 'style_tokens' and 'simple': persistent decoder, k_decode_persist<true>),
     the AdaIN and reference-embedding style paths (persistent decoder), and the CBHG linear post-net
     over the 32 x 1000 mel frames.  Device-resident inputs, tt2_synthesize_dev, HIP-event phases."""
     import torch
@@ -509,7 +509,7 @@ def bench_variants(a, local):
 
     hp = hparams.copy()
     hp.override_from_dict(dict(tacotron_num_gpus=1, max_iters=n))
-    for attn, rg in (("multihead", "gru"), ("style_tokens", "none")):
+    for attn, rg in (("multihead", "gru"), ("style_tokens", "none"), ("simple", "gru_multi")):
         W = init_tacotron_emt_weights(hp, attn, rg, seed=hp.tacotron_random_seed)
         eng = TacotronEngine(hp, W, B, T, TR, n, local, emt_attn=attn, emt_ref_gru=rg)
         if attn == "style_tokens":

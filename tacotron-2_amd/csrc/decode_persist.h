@@ -85,6 +85,10 @@ struct PdArgs {
                         // the heads-concatenated contexts are the block
   int e_XW;             // block width joining LSTM-1 (128 'multihead', 64 'style_tokens')
   long e_vbs, e_kbs;    // batch strides of e_val / e_ke (0: style tokens shared by every row)
+  int e_simple;         // 'simple' (SimpleBahdanauAttention): one softmax per row over V(tanh(W1 v + W2 q))
+                        // computed as e_heads unit-slice partials; the context (Dv = 128) is the block
+  const float* e_spk1;  // [32][4096] refnet_spk·W1[speaker rows] in lstm-column order ('simple': the
+                        // speaker half of the concatenated block, constant per row -> LSTM-1 bias), or null
   const float* e_ke;    // [B][Tv][128] keys of the attended values (conv1d_1 + bias)
   const float* e_val;   // [B][Tv][Dv] attended values
   const float* e_qrow;  // [32][128] query bias per row

@@ -429,7 +429,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     for (int q = 0; q < 4; ++q) {
       const int u = pd_unit(g, eu);
       const int col = (u >> 2) * 16 + 4 * q + (u & 3);  // biases / style terms come in lstm_cols order
-      cst[q * 128 + tid] = a.l1_b[col];
+      cst[q * 128 + tid] = a.l1_b[col] + (EMT && a.e_spk1 ? a.e_spk1[(long)em * 4 * PD_H + col] : 0.f);
       cst[(4 + q) * 128 + tid] = a.l2_b[col];
       cst[(8 + q) * 128 + tid] = a.GS[(long)em * 4 * PD_H + col];
     }
@@ -967,8 +967,10 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         const int HT = a.e_heads * a.e_Tv;
         {  // s = Σ_d normed_v·tanh(keys + q + attention_b): lane d of a 32-lane group per dim (dh <= 32),
            // 16 scores per pass of 512 threads, the keys of 4 passes loaded before their arithmetic
+          // ('simple': V(tanh(W1 v + W2 q)) over 128 units, split into 4 x 32-unit partials with each
+          // part's own V slice and no attention_b; the partials are summed below)
           const int dh = a.e_dh, d = tid & 31;
-          const float vvd = d < dh ? a.e_vv[d] : 0.f, abd = d < dh ? a.e_ab[d] : 0.f;
+          const float vvd = d < dh && !a.e_simple ? a.e_vv[d] : 0.f, abd = d < dh && !a.e_simple ? a.e_ab[d] : 0.f;
           for (int s0 = 0; s0 < 2 * HT; s0 += 64) {
             float kx[4];
 #pragma unroll
@@ -982,7 +984,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
               const int sidx = s0 + (tid >> 5) + 16 * u;
               const int rr = sidx / HT, hh = (sidx % HT) / a.e_Tv;
               float x = 0.f;
-              if (sidx < 2 * HT && d < dh) x = vvd * tanh_rcp(kx[u] + qe[rr * PD_EQ + hh * dh + d] + abd);
+              const float vv = a.e_simple ? a.e_vv[min(hh * dh + d, PD_EQ - 1)] : vvd;
+              if (sidx < 2 * HT && d < dh) x = vv * tanh_rcp(kx[u] + qe[rr * PD_EQ + hh * dh + d] + abd);
 #pragma unroll
               for (int o = 16; o >= 1; o >>= 1) x += __shfl_xor(x, o, 32);
               if (d == 0 && sidx < 2 * HT) sco[sidx] = x;
@@ -990,9 +993,19 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           }
         }
         __syncthreads();
+        if (a.e_simple) {  // one score per (row, t): the sum of the 4 unit-slice partials (in the head-0 slot)
+          if (tid < 2 * a.e_Tv) {
+            const int rr = tid / a.e_Tv, tv = tid - rr * a.e_Tv;
+            float v = 0.f;
+            for (int h = 0; h < a.e_heads; ++h) v += sco[(rr * a.e_heads + h) * a.e_Tv + tv];
+            sco[rr * HT + tv] = v;
+          }
+          __syncthreads();
+        }
         PD_STAMP(23);
-        for (int pr = w; pr < 2 * a.e_heads; pr += PD_NT / 64) {  // softmax over the attended rows, one
-          float* r = sco + pr * a.e_Tv;                            // (row, head) per wave, lanes over t
+        const int nsm = a.e_simple ? 2 : 2 * a.e_heads;  // softmax rows: (row, head), or one per row
+        for (int pr = w; pr < nsm; pr += PD_NT / 64) {   // softmax over the attended rows, one
+          float* r = sco + (a.e_simple ? pr * HT : pr * a.e_Tv);  // (row, head) per wave, lanes over t
           const float x = lane < a.e_Tv ? r[lane] : -INFINITY;     // (no mask: padded frames count)
           float mx = x;
           for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
@@ -1033,9 +1046,16 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         if (a.e_dense) pd_publish(a, PD_F_CMB, tg, tid);
         else pd_publish_rep(a, 2, tg, tid);
         PD_STAMP(24);
-        for (int e = tid; e < 2 * HT; e += PD_NT) {  // emotion alignments (output only: after the publish)
-          const int rr = e / HT, b2 = r0 + rr;
-          if (b2 < a.B) a.e_hist[((long)t * a.B + b2) * HT + (e - rr * HT)] = sco[e];
+        if (a.e_simple) {  // [max_iters][B][1][T_v]
+          for (int e = tid; e < 2 * a.e_Tv; e += PD_NT) {
+            const int rr = e / a.e_Tv, b2 = r0 + rr;
+            if (b2 < a.B) a.e_hist[((long)t * a.B + b2) * a.e_Tv + (e - rr * a.e_Tv)] = sco[rr * HT + e - rr * a.e_Tv];
+          }
+        } else {
+          for (int e = tid; e < 2 * HT; e += PD_NT) {  // emotion alignments (output only: after the publish)
+            const int rr = e / HT, b2 = r0 + rr;
+            if (b2 < a.B) a.e_hist[((long)t * a.B + b2) * HT + (e - rr * HT)] = sco[e];
+          }
         }
       } else if (isq && a.e_dense) {  // attn_emt dense (Architecture_wrappers.py:233-234): tile pn - PD_NTILE, K split pks
         if (!pd_block_wait(si + 6, [&] { return pd_poll(a, PD_F_CMB, PD_EG0, 1, 16, tg, 0, lane); })) return;

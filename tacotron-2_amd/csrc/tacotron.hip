@@ -1350,6 +1350,9 @@ struct tt2_ctx {
   // the persistent decoder's copies of l1_w, l1_wh, l2_w, l2_wh, proj_w, pre-scaled by KG_SB
   tt2::DevBuf pd_l1_w, pd_l1_wh, pd_l2_w, pd_l2_wh, pd_proj_w;
   tt2::DevBuf pd_e_wd;  // emt 'multihead' in the persistent decoder: attn_emt dense as WF tiles (x KG_SB)
+  // emt 'simple' in the persistent decoder: the speaker rows of the LSTM-1 kernel ([128][4H], lstm column
+  // order) and per utterance refnet_spk·those rows ([32][4H]): the block's constant speaker half as a bias
+  tt2::DevBuf l1_wspk, SPK1;
   tt2::DevBuf pre_w1r, pre_b1, pre_w2, pre_b2, q_w;  // pre_w1r: row-major [nm][P] (GTA TP1 GEMM)
   tt2::DevBuf l1_w, l1_wh, l1_ws, l1_b, l2_w, l2_wh, l2_b;  // critical rows / recurrent rows / style rows
   tt2::DevBuf loc_cw, keys_b, va, proj_w, proj_ws, proj_b;
@@ -1634,6 +1637,12 @@ static void finalize(tt2_ctx* c) {
       }
     }
     upload(l == 0 ? c->l1_b : c->l2_b, bt);
+    if (l == 0 && c->emt.attn == EMT_SIMPLE && c->emt.spk) {  // 'simple': [ctx_emt | spk] block, speaker rows
+      std::vector<float> wsp((size_t)EMT_OUT * N);
+      for (int r = 0; r < EMT_OUT; ++r)
+        for (int i = 0; i < N; ++i) wsp[(size_t)r * N + i] = k.data[(size_t)(c->P + c->E2 + c->emt.Aq + r) * N + cols[i]];
+      upload(c->l1_wspk, wsp);
+    }
     if (l == 0 && c->SW) {  // style rows, lstm column order, row-major [SW][4H] (B operand of the GS GEMM)
       std::vector<float> ws((size_t)c->SW * N);
       for (int r = 0; r < c->SW; ++r)
@@ -1706,13 +1715,15 @@ static void finalize(tt2_ctx* c) {
       const auto pw = pack_wf(W.data(), c->Kp, NPF, cols, c->Kp);  // rows [h2 | context_enc]
       c->kg_wmax_dec = std::max(c->kg_wmax_dec, absmax(pw));
       upload(c->proj_w, pw);
-      const bool emt_mh = c->emt.attn == EMT_MULTIHEAD || c->emt.attn == EMT_STYLE_TOKENS;
+      const bool emt_mh = c->emt.on();
       if (emt_mh && c->emt.Aq == PD_EQ) {
         // persistent decoder: 8 more tiles = the emotion query h2·W_q (multihead conv1d, first H rows --
         // 'style_tokens' appends the one-hot label rows, folded into the per-row query bias; zero context
         // rows), Architecture_wrappers.py:228-232 / multihead_attention.py:71
         const int qin = c->H + (c->emt.attn == EMT_STYLE_TOKENS ? c->emt.n_emt : 0);
-        const auto& kq = need(wm, P + "decoder/Multihead-attention-attn_emt/conv1d/kernel", {1, qin, PD_EQ});
+        // 'simple': the query is W2(h2) (attention.py:241-250)
+        const auto& kq = c->emt.attn == EMT_SIMPLE ? need(wm, P + "decoder/W2/kernel", {c->H, PD_EQ})
+                                                    : need(wm, P + "decoder/Multihead-attention-attn_emt/conv1d/kernel", {1, qin, PD_EQ});
         const int NX = NPF + PD_EQ;
         std::vector<float> Wx((size_t)c->Kp * NX, 0.f);
         std::vector<int> colx;
@@ -2103,6 +2114,18 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     p.kpart = c->kpart.as<float>(); p.kpart_floats = (long)(c->kpart.bytes / sizeof(float));
     gemm(p, s);
   }
+  if (c->l1_wspk.p && c->emt.spk) {  // emt 'simple': refnet_spk·W_lstm1[speaker rows] per utterance
+    if (!c->SPK1.p) {
+      c->SPK1.alloc(32L * 4 * c->H * 4);
+      TT2_HIP(hipMemsetAsync(c->SPK1.p, 0, c->SPK1.bytes, s));  // rows >= B stay zero
+    }
+    GemmArgs g;
+    g.M = B; g.N = 4 * c->H; g.K = EMT_OUT; g.A = c->ref_out.as<float>() + (size_t)c->cfg.max_batch * 128; g.lda = EMT_OUT;
+    g.Bw = c->l1_wspk.as<float>(); g.ldb = 4 * c->H; g.Cout = c->SPK1.as<float>(); g.ldc = 4 * c->H;
+    g.split16 = 1;  // fp16x3 split MFMA (gemm.h): operands bounded, error ~1e-7 relative
+    g.kpart = c->kpart.as<float>(); g.kpart_floats = (long)(c->kpart.bytes / sizeof(float));
+    gemm(g, s);
+  }
   c->B = B;
   c->T_in = T;
   c->encoded = true;
@@ -2274,9 +2297,13 @@ static bool pd_emt(const tt2_ctx* c) {
   // 'multihead': contexts (KC = heads x Dv) -> attn_emt dense (128) = the block; 'style_tokens': 4 x 16
   // contexts over the 24 tokens = the 64-wide block (no dense, no refnet_spk term)
   const bool mh = m.attn == EMT_MULTIHEAD && m.XW == PD_EQ && (KC == 512 || KC == 1024) && c->pd_e_wd.p;
-  const bool st = m.attn == EMT_STYLE_TOKENS && m.XW == 64 && KC == 64 && m.Dv == 16;
-  return (mh || st) && m.Aq == PD_EQ && m.Tv >= 1 && m.Tv <= 64 && 2 * m.heads * m.Tv <= 192 && m.dh <= 32 &&
-         c->K1 == PD_P + PD_E2 + m.XW;
+  const bool st = m.attn == EMT_STYLE_TOKENS && m.XW == 64 && KC == 64 && m.Dv == 16 && 2 * m.heads * m.Tv <= 192 &&
+                  m.dh <= 32;
+  // 'simple' (gru_multi at the fork widths): 128 units scored as 4 x 32-unit partials, one softmax per
+  // row, the 128-wide context is the block's first half; the speaker half folds into the LSTM-1 bias
+  const bool sp = m.attn == EMT_SIMPLE && m.Dv == PD_EQ && m.Tv <= 16 && (m.spk ? c->l1_wspk.p != nullptr : true) &&
+                  m.XW == PD_EQ + (m.spk ? EMT_OUT : 0);
+  return (mh || st || sp) && m.Aq == PD_EQ && m.Tv >= 1 && m.Tv <= 64 && c->K1 == PD_P + PD_E2 + m.XW;
 }
 
 static bool pd_fits(tt2_ctx* c) {
@@ -2325,7 +2352,7 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
   if (emt) {
     zero_many({{c->QEx.p, c->QEx.bytes}, {c->EOx.p, c->EOx.bytes}, {c->EMTx.p, c->EMTx.bytes}}, s);
     // zero_state (Architecture_wrappers.py:182): the step-0 emotion block is refnet_spk alone
-    const float* spk = emt_spk(c);
+    const float* spk = c->emt.attn == EMT_MULTIHEAD ? emt_spk(c) : nullptr;  // 'multihead': spk is IN the block
     if (spk)
       hipLaunchKernelGGL(k_af_rows, dim3(c->B), dim3(PD_EQ), 0, s, spk, PD_EQ, c->EMTx.as<float>() + 32 * PD_EQ);
   }
@@ -2364,6 +2391,13 @@ static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d
     const auto& m = c->emt;
     a.e_Tv = m.Tv; a.e_Dv = m.Dv; a.e_KC = m.heads * m.Dv; a.e_heads = m.heads; a.e_dh = m.dh;
     a.e_dense = m.attn == EMT_MULTIHEAD; a.e_XW = m.XW; a.e_vbs = m.val_bstride(); a.e_kbs = m.ke_bstride();
+    a.e_simple = m.attn == EMT_SIMPLE;
+    a.e_spk1 = nullptr;
+    if (a.e_simple) {  // 4 unit-slice partials of 32 per score, context = the block's ctx half (128)
+      a.e_heads = 4; a.e_dh = PD_EQ / 4; a.e_KC = PD_EQ; a.e_XW = PD_EQ;
+      a.e_ab = m.vv.as<float>();  // unused ('simple' has no attention_b)
+      if (m.spk) a.e_spk1 = c->SPK1.as<float>();
+    }
     a.e_ke = m.ke.as<float>(); a.e_val = m.val.as<float>(); a.e_qrow = m.qrow.as<float>();
     a.e_vv = m.vv.as<float>(); a.e_ab = m.ab.as<float>(); a.e_wd = c->pd_e_wd.as<float>(); a.e_bd = m.bd.as<float>();
     a.e_spk = emt_spk(c); a.e_hist = m.hist.as<float>();

@@ -63,8 +63,9 @@ def test_simple_gru():
 
 
 def test_simple_gru_multi_full_width():
-    """The only 'simple' combination at the fork's own widths: 8 x dense(128) = attention_dim."""
-    _case(full_hparams(), "simple", "gru_multi", B=2, T=9, T_ref=80, n=12)
+    """The only 'simple' combination at the fork's own widths: 8 x dense(128) = attention_dim; it
+    decodes in the persistent decoder (round 5)."""
+    _case(full_hparams(), "simple", "gru_multi", B=2, T=9, T_ref=80, n=12, persistent_expected=1)
 
 
 @pytest.mark.parametrize("ref_gru", ["none", "gru", "gru_multi"])
@@ -204,4 +205,28 @@ def test_style_tokens_persistent_configs1_gta_vs_oracle():
     labels = [i % 5 for i in range(B)]
     out, _ = _case(hp, "style_tokens", "none", B=B, T=T, T_ref=80, n=n, seed=9, targets=tg, labels=labels,
                    persistent_expected=1)
+    assert out["frames"].shape[1] == n
+
+
+def test_simple_full_width_persistent_emt_only_and_launch_path():
+    """'simple' in k_decode_persist<true> (round 5): V(tanh(W1 v + W2 q)) over the 128 units as four
+    32-unit partials summed into one softmax per row over the 8 'gru_multi' heads, the 128-wide context
+    as the block's first half, refnet_spk's half folded into a per-row LSTM-1 bias; emt_only (no
+    speaker half) too, and the launch path (TT2_DECODER=launch) on the same case."""
+    import os
+    _case(full_hparams(), "simple", "gru_multi", emt_only=True, B=3, T=9, T_ref=80, n=12, persistent_expected=1)
+    os.environ["TT2_DECODER"] = "launch"
+    try:
+        _case(full_hparams(), "simple", "gru_multi", B=3, T=9, T_ref=80, n=12, persistent_expected=0)
+    finally:
+        del os.environ["TT2_DECODER"]
+
+
+def test_simple_persistent_configs1_gta_vs_oracle():
+    """configs[1] shape (B = 32 ragged rows x 201 chars, T_ref 400) through the persistent 'simple'
+    decoder, 200 teacher-forced steps against the oracle at 1e-4, every step's emotion weights too."""
+    hp = full_hparams()
+    B, T, TR, n = 32, 201, 400, 200
+    tg = np.random.default_rng(8).normal(0, 1, (B, n, hp.num_mels)).astype(np.float32)
+    out, _ = _case(hp, "simple", "gru_multi", B=B, T=T, T_ref=TR, n=n, seed=11, targets=tg, persistent_expected=1)
     assert out["frames"].shape[1] == n
