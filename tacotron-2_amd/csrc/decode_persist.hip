@@ -986,9 +986,8 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
               float x = 0.f;
               const float vv = a.e_simple ? a.e_vv[min(hh * dh + d, PD_EQ - 1)] : vvd;
               if (sidx < 2 * HT && d < dh) x = vv * tanh_rcp(kx[u] + qe[rr * PD_EQ + hh * dh + d] + abd);
-#pragma unroll
-              for (int o = 16; o >= 1; o >>= 1) x += __shfl_xor(x, o, 32);
-              if (d == 0 && sidx < 2 * HT) sco[sidx] = x;
+              x = sum32_to_lane31(x);  // DPP: the 32-lane group's sum in its lane 31
+              if (d == 31 && sidx < 2 * HT) sco[sidx] = x;
             }
           }
         }
@@ -1007,12 +1006,10 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
         for (int pr = w; pr < nsm; pr += PD_NT / 64) {   // softmax over the attended rows, one
           float* r = sco + (a.e_simple ? pr * HT : pr * a.e_Tv);  // (row, head) per wave, lanes over t
           const float x = lane < a.e_Tv ? r[lane] : -INFINITY;     // (no mask: padded frames count)
-          float mx = x;
-          for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-          const float ex = lane < a.e_Tv ? expf(x - mx) : 0.f;
-          float sum = ex;
-          for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-          if (lane < a.e_Tv) r[lane] = ex / sum;
+          const float mx = wave_max_dpp(x);
+          const float ex = lane < a.e_Tv ? __expf(x - mx) : 0.f;
+          const float sum = wave_sum_dpp(ex);
+          if (lane < a.e_Tv) r[lane] = ex * __builtin_amdgcn_rcpf(sum);
         }
         __syncthreads();
         PD_STAMP(30);

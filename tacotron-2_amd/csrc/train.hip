@@ -1634,6 +1634,8 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
   __shared__ float dus[RQX * (A + 1)];                        // du of the own rows (stride A + 1)
   __shared__ float dfo[RQX * F];                              // this launch's df of the own rows (zero past nown)
   __shared__ float cseg[RQX + 32];                            // cum_{t-1}[j0 + i - pad]
+  constexpr int MSS = 33;                                     // stride of ms: conflict-free diagonal reads
+  __shared__ float ms[HR * MSS];                              // M[r][tap] = Σ_c df_{t+1}[r][c]·Kc[tap][c]
   __shared__ float red[2][NW][A];
   __shared__ float s16[16];
   const int q = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1773,17 +1775,36 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
   float kcr[KW];
 #pragma unroll
   for (int tp = 0; tp < KW; ++tp) kcr[tp] = kcs[tp * F + (tid & 31)];
-  for (int p0 = 0; p0 < nown; p0 += TRQ_NT / 32) {
-    const int ir = p0 + (tid >> 5), c = tid & 31;  // own row
+  // d cum_t[ir] = d cum_{t+1}[ir] + Σ_tap M[ir - tap + 2 pad + 1][tap]: M = dfin·Kcᵀ on fp32 MFMA
+  // (v_mfma_f32_16x16x4f32, tile = 16 halo rows x 16 taps, K = the 32 filters), then the diagonal sums
+  // from LDS, a quad of lanes per own row (8 taps each)
+  {
+    const int nrt = min(HR / 16, (nown + 2 * PAD + 1 + 15) / 16);
+    for (int tl = w; tl < 2 * nrt; tl += NW) {
+      const int rt = tl >> 1, tt = tl & 1;
+      trq_f4 acc = {};
+#pragma unroll
+      for (int ks = 0; ks < F / 4; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dfin[(16 * rt + jl) * F + 4 * ks + g4], kcs[(16 * tt + jl) * F + 4 * ks + g4],
+                                                   acc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ms[(16 * rt + 4 * g4 + i) * MSS + 16 * tt + jl] = acc[i];
+    }
+  }
+  __syncthreads();
+  for (int p0 = 0; p0 < nown; p0 += TRQ_NT / 4) {
+    const int ir = p0 + (tid >> 2), qq = tid & 3;  // own row, taps [8 qq, 8 qq + 8)
     float acc = 0.f;
     if (ir < nown) {
-      const float* dr = dfin + (ir + 2 * PAD + 1) * F + c;  // row of position (j0 + ir) - tap + pad at -tap
 #pragma unroll
-      for (int tp = 0; tp < KW; ++tp) acc += dr[-tp * F] * kcr[tp];
+      for (int k = 0; k < 8; ++k) {
+        const int tp = 8 * qq + k;
+        if (tp < KW) acc += ms[(ir - tp + 2 * PAD + 1) * MSS + tp];
+      }
     }
-    acc = trq_row_sum(acc);
-    acc += trq_dpp<0x142, 0xa>(acc);
-    if ((lane & 31) == 31 && ir < nown) {
+    acc += trq_dpp<0xB1, 0xf>(acc);
+    acc += trq_dpp<0x4E, 0xf>(acc);
+    if (qq == 0 && ir < nown) {
       const float v = dcin[j0 + ir] + acc;
       dcum[ir] = v;
       z.dcum_out[(long)b * Tin + j0 + ir] = v;
