@@ -93,7 +93,8 @@ __device__ __forceinline__ float tp_tanh(float x) {
   return ax < 0.0625f ? p : r;
 }
 
-__device__ __forceinline__ float tp_sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// v_exp_f32 + v_rcp_f32 (relative error < 4e-7, no IEEE division on the per-step chain)
+__device__ __forceinline__ float tp_sigm(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float tp_lo(unsigned v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float tp_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
 __device__ __forceinline__ unsigned tp_pack(float lo, float hi) {
@@ -690,10 +691,10 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
       // masked softmax over j < len (attention.py:218, TF _maybe_mask_score), cumulative alignments
       const float ev = tid < len ? al[tid] : -INFINITY;
       const float mx = tp_block_max(ev, scr);
-      const float x = tid < len ? expf(ev - mx) : 0.f;
+      const float x = tid < len ? __expf(ev - mx) : 0.f;
       const float ssum = tp_block_sum(x, scr);
       if (tid < Tin) {
-        const float alv = x / ssum;
+        const float alv = x * __builtin_amdgcn_rcpf(ssum);
         al[tid] = alv;
         const float cn = cw[15 + tid] + alv;
         cw[15 + tid] = cn;

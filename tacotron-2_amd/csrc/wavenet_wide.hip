@@ -73,9 +73,10 @@ __device__ __forceinline__ void ww_reduce(f32x4& a) {
 #undef TT2_STEP
 }
 
-// gate nonlinearities of the one-hop form on v_exp_f32 + one division (|abs err| < 3e-7)
-__device__ __forceinline__ float ww_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
-__device__ __forceinline__ float ww_sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+// gate nonlinearities on v_exp_f32 + v_rcp_f32 (common.h tanh_rcp / sigm_fast: abs error < 3e-7,
+// no IEEE division on the per-layer chain)
+__device__ __forceinline__ float ww_tanh(float x) { return tanh_rcp(x); }
+__device__ __forceinline__ float ww_sigm(float x) { return sigm_fast(x); }
 
 __device__ __forceinline__ void ww_fma4(f32x4& acc, float x, const f32x4& w) {
   acc[0] += x * w[0]; acc[1] += x * w[1]; acc[2] += x * w[2]; acc[3] += x * w[3];
@@ -376,8 +377,8 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
     ww_reduce<NKS>(acc);
     if (ks == 0) {
       float2 zz;
-      zz.x = tanhf(acc[0]) * sigm(acc[2]);
-      zz.y = tanhf(acc[1]) * sigm(acc[3]);
+      zz.x = ww_tanh(acc[0]) * ww_sigm(acc[2]);
+      zz.y = ww_tanh(acc[1]) * ww_sigm(acc[3]);
       reinterpret_cast<float2*>(z)[q] = zz;
     }
     __syncthreads();
