@@ -475,7 +475,7 @@ typedef struct tt2_train_config {
   int use_gst;
   /* args.adain (tacotron.py:236-242, 266-268; modules.py:66-107): ReferenceEncoderAdaIn 'refnet' in
    * training mode -- the speaker and emotion mels through two conv2d + ReLU stacks without batch
-   * norm (strides (2,2),(2,2),(1,1)x4; variables refnet/conv2d_i/conv2d/* speaker, conv2d_1/*
+   * norm (strides (2,2),(2,2),(1,1)x4; variables refnet/conv2d_i/conv2d/{kernel,bias} speaker, conv2d_1/{kernel,bias}
    * emotion), the speaker map restyled by the emotion map's per-channel moments, one GRU + dense
    * tanh; its 128-wide output is the style embedding (memory_dim = 2*encoder_lstm_units + 128).
    * Needs both references, no style classifiers / orthogonality loss (the reference builds none). */

@@ -78,8 +78,27 @@ __device__ __forceinline__ void ww_reduce(f32x4& a) {
 __device__ __forceinline__ float ww_tanh(float x) { return tanh_rcp(x); }
 __device__ __forceinline__ float ww_sigm(float x) { return sigm_fast(x); }
 
+// two v_pk_fma_f32 (x broadcast through op_sel_hi) instead of four v_fma_f32: the per-layer
+// gate and [out | skip] products sit on the sample chain, so halving their issue count counts
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+#ifndef WW_PK
+#define WW_PK 1
+#endif
 __device__ __forceinline__ void ww_fma4(f32x4& acc, float x, const f32x4& w) {
+  if (!WW_PK) { acc[0] += x * w[0]; acc[1] += x * w[1]; acc[2] += x * w[2]; acc[3] += x * w[3]; return; }
+  const f32x2 xx = {x, x};
+  const f32x2 lo = __builtin_elementwise_fma(xx, f32x2{w[0], w[1]}, f32x2{acc[0], acc[1]});
+  const f32x2 hi = __builtin_elementwise_fma(xx, f32x2{w[2], w[3]}, f32x2{acc[2], acc[3]});
+  acc = f32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+__device__ __forceinline__ void ww_fma4s(f32x4& acc, float x, const f32x4& w) {
   acc[0] += x * w[0]; acc[1] += x * w[1]; acc[2] += x * w[2]; acc[3] += x * w[3];
+}
+#ifndef WW1_PK
+#define WW1_PK 0
+#endif
+__device__ __forceinline__ void ww1_fma4(f32x4& acc, float x, const f32x4& w) {
+  if (WW1_PK) ww_fma4(acc, x, w); else ww_fma4s(acc, x, w);
 }
 
 template <bool GAUSS>
@@ -113,18 +132,27 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
     float* h1 = skv + S;           // [S]
     float* lg = h1 + S;            // [32]
     float* gum = lg + 32;          // [2][16] Gumbel terms (+ [15] logistic / normal draw) by t&1
-    float* f2 = gum + 32;          // [S][32]
-    float* red = f2 + S * 32;      // [32][32] f2 partials
     const int qh = tid / NKSH, kh = tid % NKSH;
+    // f2 in registers: column quad cq = tid / 32, rows k = i * 32 + ks (ks = tid % 32) -- the
+    // 32 row slices of one quad sit in one half-wave and reduce on DPP
+    constexpr int RK = S / 32;
+    static_assert(S % 32 == 0 && WW_THREADS == 256, "head f2 geometry");
+    const int cq = tid >> 5, ks = tid & 31;
+    f32x4 w2[RK];
+#pragma unroll
+    for (int i = 0; i < RK; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cc = cq * 4 + e;
+        w2[i][e] = cc < a.C ? a.f2_w[(i * 32 + ks) * a.C + cc] : 0.f;
+      }
     f32x4 w1[HK];
 #pragma unroll
     for (int i = 0; i < HK; ++i) w1[i] = reinterpret_cast<const f32x4*>(a.f1_w + (long)(kh * HK + i) * S)[qh];
     const f32x4 b1 = reinterpret_cast<const f32x4*>(a.f1_b)[qh];
-    for (int i = tid; i < S * 32; i += WW_THREADS) {
-      const int k = i >> 5, cc = i & 31;
-      f2[i] = cc < a.C ? a.f2_w[k * a.C + cc] : 0.f;
-    }
-    const float b2 = tid < a.C ? a.f2_b[tid] : 0.f;
+    f32x4 b2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b2[e] = cq * 4 + e < a.C ? a.f2_b[cq * 4 + e] : 0.f;
     const int nr = a.C / 3;
     // one-hop: the tail's skip block, read at [256 + tid] like the two-hop layer's x granules
     const unsigned long long* gin = ONEHOP ? a.gran + (long)L * W1_GB + 2 * R - 256 : a.gran + (long)(L - 1) * NG;
@@ -199,23 +227,14 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
         }
       }
       __syncthreads();
-      {  // f2 (wavenet.py:843-844): 8 column quads x 32 row slices of S/32, partials through LDS
-        constexpr int RK = S / 32;
-        const int cq = tid & 7, ksl = tid >> 3;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      {  // f2 (wavenet.py:843-844): 8 column quads x 32 row slices, summed on DPP to lane ks = 31
+        f32x4 acc = b2;
+        if (ks != 0) acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < RK; ++i) {
-          const int k = ksl * RK + i;
-          ww_fma4(acc, h1[k], reinterpret_cast<const f32x4*>(f2 + k * 32)[cq]);
-        }
-        reinterpret_cast<f32x4*>(red + ksl * 32)[cq] = acc;
-      }
-      __syncthreads();
-      if (tid < 32) {
-        float s = b2;
-        for (int k = 0; k < 32; ++k) s += red[k * 32 + tid];
-        lg[tid] = s;
-        if (a.logits && tid < a.C) a.logits[((long)a.b * a.T + t) * a.C + tid] = s;
+        for (int i = 0; i < RK; ++i) ww_fma4(acc, h1[i * 32 + ks], w2[i]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = sum32_to_lane31(acc[e]);
+        if (ks == 31) reinterpret_cast<f32x4*>(lg)[cq] = acc;
       }
       __syncthreads();
       if (wave == 0) {  // sampler (mixture.py:76-107 / gaussian.py:39-52), as k_generate_pipe
@@ -223,11 +242,12 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
         int idx = lane;
         if (!GAUSS && lane < nr) temp = lg[lane] - gum[cb * 16 + lane];
         argmax16(temp, idx);  // nr <= 10: the mixture logits sit in lanes 0..15
+        if (a.logits && lane < a.C) a.logits[((long)a.b * a.T + t) * a.C + lane] = lg[lane];
         if (lane == 0) {
           if (GAUSS) idx = 0;
           const float mean = GAUSS ? lg[0] : lg[nr + idx];
           const float ls = GAUSS ? fmaxf(lg[1], a.log_scale_min_gauss) : fmaxf(lg[2 * nr + idx], a.log_scale_min);
-          float x = mean + expf(ls) * gum[cb * 16 + 15];
+          float x = mean + __expf(ls) * gum[cb * 16 + 15];
           x = fminf(fmaxf(x, -1.f), 1.f);
           const float xn = a.teacher ? a.teacher[(long)a.b * a.T + t] : x;  // wavenet.py:876-878
           ww_put(sample_gran, (unsigned)(t + 1), xn);
@@ -235,7 +255,8 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
           if (a.kout) a.kout[(long)a.b * a.T + t] = idx;
         }
       }
-      __syncthreads();
+      // no barrier here: the next sample's LDS writes (gum[t+1 & 1], skv, h1, lg) each sit
+      // behind at least one barrier that wave 0 reaches only after this sampler
     }
     return;
   }
@@ -545,7 +566,7 @@ __device__ void ww1_layer(const WideArgs& a, float* sm, const unsigned long long
       for (int i4 = 0; i4 < 8; ++i4) {
         const f32x4 xv = ww_ld4(row, i4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ww_fma4(acc, xv[e], tapw[(4 * i4 + e) * WW_THREADS + tid]);
+        for (int e = 0; e < 4; ++e) ww1_fma4(acc, xv[e], tapw[(4 * i4 + e) * WW_THREADS + tid]);
       }
       if (ks == 0) {
         const f32x4 cd = reinterpret_cast<const f32x4*>(condp + (long)t * L * G)[q];
@@ -597,7 +618,7 @@ __device__ void ww1_layer(const WideArgs& a, float* sm, const unsigned long long
       for (int i4 = 0; i4 < 4; ++i4) {
         const f32x4 z4 = zv4[i4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ww_fma4(acc2, z4[e], wso[4 * i4 + e]);
+        for (int e = 0; e < 4; ++e) ww1_fma4(acc2, z4[e], wso[4 * i4 + e]);
       }
       ww_reduce<16>(acc2);
       if (ks == 0) {
@@ -626,7 +647,7 @@ __device__ void ww1_layer(const WideArgs& a, float* sm, const unsigned long long
       for (int i4 = 0; i4 < 4; ++i4) {
         const f32x4 x4 = xv4[i4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ww_fma4(acc, x4[e], wx[4 * i4 + e]);
+        for (int e = 0; e < 4; ++e) ww1_fma4(acc, x4[e], wx[4 * i4 + e]);
       }
       if (l > 0) {
         const f32x4* zv4 = reinterpret_cast<const f32x4*>(zin + ks * 16);
@@ -634,7 +655,7 @@ __device__ void ww1_layer(const WideArgs& a, float* sm, const unsigned long long
         for (int i4 = 0; i4 < 4; ++i4) {
           const f32x4 z4 = zv4[i4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) ww_fma4(acc, z4[e], wm[4 * i4 + e]);
+          for (int e = 0; e < 4; ++e) ww1_fma4(acc, z4[e], wm[4 * i4 + e]);
         }
       }
       ww_reduce<16>(acc);
