@@ -635,7 +635,7 @@ struct tt2_wn_ctx {
   int R, G, S, L, C, cin;
   long hop;
   tt2::DevBuf first_w, first_b, conv_w, conv_b, cond_w, cond_b, so_w, so_b, f1_w, f1_b, f2_w, f2_b;
-  tt2::DevBuf w1, gb1;  // R = 256 one-hop form (wavenet_wide.h WideArgs::w1 / gb1)
+  tt2::DevBuf w1, gb1, l0;  // R = 256 one-hop form (wavenet_wide.h WideArgs::w1 / gb1 / l0)
   tt2::DevBuf up_k[8], up_b[8];
   tt2::DevBuf cin_d, up_a, up_b_buf, c_up_t, cond, umix, ulog, teacher, wav, kout, logits, gran, stamps;
   int chunk = 1;                 // utterances per generation launch
@@ -869,6 +869,30 @@ static void wn_finalize(tt2_wn_ctx* c) {
     }
     wupload(c->w1, w1);
     wupload(c->gb1, gb1);
+    {  // layer 0 folded into the head (WideArgs::l0): U_k = W_k·fw, V_k = W_k·fb per gate column
+      const std::string s = P + "ResidualConv1DGLU_0/";
+      const float* conv = need(wm, s + "residual_block_causal_conv_ResidualConv1DGLU_0/kernel", {kw, R, G}).data.data();
+      const float* fw = need(wm, P + "input_convolution/kernel", {1, 1, R}).data.data();
+      const float* fb = need(wm, P + "input_convolution/bias", {R}).data.data();
+      std::vector<float> l0((size_t)R * 16, 0.f);
+      for (int j = 0; j < R; ++j)
+        for (int h = 0; h < 2; ++h) {
+          const int col = h ? R + j : j;
+          float* o = l0.data() + (size_t)j * 16 + h * 8;
+          for (int k = 0; k < 3; ++k) {
+            double u = 0.0, v = 0.0;
+            for (int x = 0; x < R; ++x) {
+              const double w = conv[(size_t)(k * R + x) * G + col];
+              u += w * fw[x];
+              v += w * fb[x];
+            }
+            o[k] = (float)u;
+            o[4 + k] = (float)v;
+          }
+          o[3] = gb1[4 * (j >> 1) + (j & 1) + 2 * h];  // gate bias, gate-permuted column
+        }
+      wupload(c->l0, l0);
+    }
   }
   if (c->cfg.gin_channels > 0) {  // conv1x1g of every layer (modules.py:427-433) and the embedding
     for (int l = 0; l < L; ++l) {
@@ -1045,6 +1069,11 @@ static void wn_generate_dev(tt2_wn_ctx* c, const float* cond_in, int B, int T_f,
     w.gran = reinterpret_cast<unsigned long long*>(c->gran.as<char>() + 16);
     w.w1 = c->w1.p ? c->w1.as<f32x4>() : nullptr;
     w.gb1 = c->gb1.p ? c->gb1.as<float>() : nullptr;
+    static const bool fuse0 = [] {
+      const char* e = std::getenv("TT2_WW_L0HEAD");  // 0: layer 0 on its own work-groups (A/B)
+      return !e || std::atoi(e) != 0;
+    }();
+    w.l0 = fuse0 && c->l0.p ? c->l0.as<float>() : nullptr;
     const void* kern = ww_kernel(R, c->C == 2);
     const unsigned shm = (unsigned)ww_lds_bytes(R, c->C);
     for (int b = 0; b < B; ++b) {  // one utterance per launch: its layers fill NC x L CUs

@@ -41,6 +41,11 @@ struct WideArgs {
   // previous layer's out bias folded in [L][G] (gate-permuted)
   const f32x4* w1;
   const float* gb1;
+  // layer 0 folded into the head (null: layer 0 runs on its own work-groups).  Layer 0's input is
+  // the affine x_0(s) = y_{s-1}·fw + fb of the scalar sample, so each of its gate columns is
+  // g + cond + Σ_k [tap k live] (y·U_k + V_k), U_k = W_k·fw, V_k = W_k·fb (k: x(s-2), x(s-1), x(s)).
+  // Per z channel j: [a column | b column] x {U_0, U_1, U_2, g, V_0, V_1, V_2, 0}, float64-formed
+  const float* l0;
 };
 constexpr int W1_NW = 80;         // float4 weights per thread and (layer, WG) in the one-hop form
 constexpr int W1_GB = 3 * 256;    // granules per layer block: [z | x | skip]

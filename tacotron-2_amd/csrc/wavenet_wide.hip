@@ -156,9 +156,34 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
     const int nr = a.C / 3;
     // one-hop: the tail's skip block, read at [256 + tid] like the two-hop layer's x granules
     const unsigned long long* gin = ONEHOP ? a.gran + (long)L * W1_GB + 2 * R - 256 : a.gran + (long)(L - 1) * NG;
+    // layer 0 in the head (ONEHOP, a.l0): thread j owns z channel j; its a / b gate columns sit at
+    // gate-permuted pa, pa + 2 of the conditioning; it publishes z_0(s) and x_0(s) with tag s + 1
+    const bool fuse0 = ONEHOP && a.l0 != nullptr;
+    f32x4 u0a = {0.f, 0.f, 0.f, 0.f}, v0a = u0a, u0b = u0a, v0b = u0a;
+    float fwj = 0.f, fbj = 0.f, in1 = 0.f, in2 = 0.f, base_a = 0.f, base_b = 0.f;
+    const int pa = 4 * (tid >> 1) + (tid & 1);
+    const float* cond0 = a.cond + (long)a.b * a.T * L * (2 * R) + pa;
+    if (fuse0) {
+      const f32x4* l0 = reinterpret_cast<const f32x4*>(a.l0) + tid * 4;
+      u0a = l0[0]; v0a = l0[1]; u0b = l0[2]; v0b = l0[3];
+      fwj = a.first_w[tid]; fbj = a.first_b[tid];
+      // s = 0: no live taps, x_0(0) = fb
+      const float za = u0a[3] + cond0[0] + v0a[2], zb = u0b[3] + cond0[2] + v0b[2];
+      ww_put(a.gran + tid, 1u, ww_tanh(za) * ww_sigm(zb));
+      ww_put(a.gran + R + tid, 1u, fbj);
+    }
     __syncthreads();
     for (int t = 0; t < a.T; ++t) {
       const int cb = t & 1;
+      if (fuse0 && t + 1 < a.T) {  // layer 0 at s = t + 1 up to the y_t term, before the skips arrive
+        const float* cs = cond0 + (long)(t + 1) * L * (2 * R);
+        base_a = u0a[3] + cs[0] + in1 * u0a[1] + v0a[1] + v0a[2];
+        base_b = u0b[3] + cs[2] + in1 * u0b[1] + v0b[1] + v0b[2];
+        if (t >= 1) {
+          base_a += in2 * u0a[0] + v0a[0];
+          base_b += in2 * u0b[0] + v0b[0];
+        }
+      }
       if (wave == 1) {  // this sample's noise (injected, or the device RNG of common.h)
         if (GAUSS) {
           if (lane == 15) gum[cb * 16 + 15] = a.u_log ? a.u_log[(long)t * a.Bg + a.b] : wn_gauss(a.seed, t, a.Bg, a.b);
@@ -250,13 +275,25 @@ __global__ __launch_bounds__(WW_THREADS, 1) void k_generate_wide(WideArgs a) {
           float x = mean + __expf(ls) * gum[cb * 16 + 15];
           x = fminf(fmaxf(x, -1.f), 1.f);
           const float xn = a.teacher ? a.teacher[(long)a.b * a.T + t] : x;  // wavenet.py:876-878
-          ww_put(sample_gran, (unsigned)(t + 1), xn);
+          if (fuse0) sm[4] = xn;
+          else ww_put(sample_gran, (unsigned)(t + 1), xn);
           a.wav[(long)a.b * a.T + t] = x;
           if (a.kout) a.kout[(long)a.b * a.T + t] = idx;
         }
       }
-      // no barrier here: the next sample's LDS writes (gum[t+1 & 1], skv, h1, lg) each sit
-      // behind at least one barrier that wave 0 reaches only after this sampler
+      // unfused: no barrier here -- the next sample's LDS writes (gum[t+1 & 1], skv, h1, lg) each
+      // sit behind at least one barrier that wave 0 reaches only after this sampler
+      if (fuse0) {
+        __syncthreads();
+        const float xn = sm[4];
+        if (t + 1 < a.T) {
+          const float za = base_a + xn * u0a[2], zb = base_b + xn * u0b[2];
+          ww_put(a.gran + tid, (unsigned)(t + 2), ww_tanh(za) * ww_sigm(zb));
+          ww_put(a.gran + R + tid, (unsigned)(t + 2), xn * fwj + fbj);
+        }
+        in2 = in1;
+        in1 = xn;
+      }
     }
     return;
   }
@@ -499,6 +536,7 @@ __device__ void ww1_layer(const WideArgs& a, float* sm, const unsigned long long
   int* flag = reinterpret_cast<int*>(sm);
   const int L = a.L;
   const int l = blockIdx.x / NC, c = blockIdx.x % NC;
+  if (l == 0 && a.l0) return;  // layer 0 runs in the head
   const bool tail = l == L;
   f32x4* tapw = reinterpret_cast<f32x4*>(sm + 16);  // [32][256] tap weights
   float* xprev = sm + 16 + 32 * WW_THREADS * 4;      // [R] x_{l-1}(t) (layer 0: x_0(t))
