@@ -243,6 +243,23 @@ __device__ __forceinline__ void sum8x4(f32x4& a) {
 #undef TT2_STEP
 }
 
+// acc += x·w on four columns: WN_PK = 1 issues two v_pk_fma_f32 (x broadcast by op_sel_hi) instead
+// of four v_fma_f32 (A/B switch for the per-layer chain products)
+#ifndef WN_PK
+#define WN_PK 0
+#endif
+typedef float wn_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void wn_fma4(f32x4& acc, float x, const f32x4& w) {
+  if (WN_PK) {
+    const wn_f32x2 xx = {x, x};
+    const wn_f32x2 lo = __builtin_elementwise_fma(xx, wn_f32x2{w[0], w[1]}, wn_f32x2{acc[0], acc[1]});
+    const wn_f32x2 hi = __builtin_elementwise_fma(xx, wn_f32x2{w[2], w[3]}, wn_f32x2{acc[2], acc[3]});
+    acc = f32x4{lo[0], lo[1], hi[0], hi[1]};
+  } else {
+    acc[0] += x * w[0]; acc[1] += x * w[1]; acc[2] += x * w[2]; acc[3] += x * w[3];
+  }
+}
+
 // Explicit AGPR residency for the off-critical-path tap weights (the allocator otherwise parks the
 // critical-path weights there and pays a v_accvgpr_read per use inside the serial chain).
 __device__ __forceinline__ float agpr_put(float v) {
@@ -450,8 +467,7 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const f32x4 w = wx[j][i];
-          acc[0] += xv[i] * w[0]; acc[1] += xv[i] * w[1]; acc[2] += xv[i] * w[2]; acc[3] += xv[i] * w[3];
+          wn_fma4(acc, xv[i], wx[j][i]);
         }
       }
       const f32x4 sb = reinterpret_cast<const f32x4*>(sbias + j * G)[q];  // for the skip/out phase
@@ -475,8 +491,7 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_generate_pipe(GenArgs a) {
           const f32x4 zv = zv4[k4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const f32x4 w = wsr[j][4 * k4 + e];
-            acc2[0] += zv[e] * w[0]; acc2[1] += zv[e] * w[1]; acc2[2] += zv[e] * w[2]; acc2[3] += zv[e] * w[3];
+            wn_fma4(acc2, zv[e], wsr[j][4 * k4 + e]);
           }
         }
       }
