@@ -24,7 +24,8 @@ for i in ORDER:
 if s[:, 31].any() or (s[:, 31] == 0).all():
     xcc = s[:, 31]
     print("XCD of work-group g: g % 8 ->", [int(np.bincount(xcc[g % 8 == k]).argmax()) for k in range(8)])
-    for i in (13, 20, 14, 15, 0, 1, 4):
+    NAMES[30] = "14 + vmcnt(0)"
+    for i in (13, 20, 14, 30, 15, 0, 1, 4):
         line = f"{i:2d} {NAMES[i]:16s}"
         for x in range(8):
             v = r[xcc == x, i][s[xcc == x, i] != 0]

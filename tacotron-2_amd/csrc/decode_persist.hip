@@ -1142,6 +1142,14 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
     }
     __syncthreads();  // red reuse by stage A
     PD_STAMP(14);
+#ifdef PD_XSTAMP
+    if constexpr (!EMT) {  // diagnostic build: how long the stores still in flight at 14 take to drain
+      if (stp) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PD_STAMP(30);
+      }
+    }
+#endif
     if constexpr (EMT) {
       if (g >= PD_EG0 && a.e_dense) {  // dense partials of rows r0, r0+1 -> the next step's emotion block (+ refnet_spk),
                           // after this work-group's own prenet hand-off
