@@ -695,6 +695,33 @@ __global__ __launch_bounds__(TLG_NT, 1) void k_tr_fused(TrFused a) {
   const bool rok = r0 + c < a.B;
   const bf8 z8 = {};
   tlg_f32x16 acc = {};
+  if (MODE != TF_BWD_H && ks == 2 * TLG_KSMAX) {
+    // K = 4096 (the LSTM backward products, d X1): a rolling pipeline over the wave's 32 k-steps, fully
+    // unrolled and branch-free (rows past B load row 0 and are zeroed by a select; the second row half
+    // of a B <= 32 launch lies past the Bp-row shadow),
+    // so the slot a k-step's MFMA frees is refilled with the k-step 16 ahead while the first loads
+    // are still landing: the K range costs one memory round trip instead of two batches back to back
+    bf8 va[TLG_KSMAX], vb[TLG_KSMAX];
+    const __bf16* const wrow = Wb + tf_sw(32 * cgl + c, k0 + kh, a.K);
+    const __bf16* const arow = Ab + tf_sw(rok ? r0 + c : 0, k0 + kh, a.K);  // row 0: always allocated
+    // tf_sw(r, k + 16 j, K) = tf_sw(r, k, K) + 512 j for k % 16 == kh (16-deep k-steps of 32 x 16)
+#pragma unroll
+    for (int s = 0; s < TLG_KSMAX; ++s) {
+      vb[s] = *reinterpret_cast<const bf8*>(wrow + 512 * s);
+      const bf8 x = *reinterpret_cast<const bf8*>(arow + 512 * s);
+      va[s] = rok ? x : z8;
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2 * TLG_KSMAX; ++ss) {
+      const int s = ss % TLG_KSMAX;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s], vb[s], acc, 0, 0, 0);
+      if (ss + TLG_KSMAX < 2 * TLG_KSMAX) {
+        vb[s] = *reinterpret_cast<const bf8*>(wrow + 512 * (ss + TLG_KSMAX));
+        const bf8 x = *reinterpret_cast<const bf8*>(arow + 512 * (ss + TLG_KSMAX));
+        va[s] = rok ? x : z8;
+      }
+    }
+  } else
   for (int s0 = 0; s0 < ks; s0 += TLG_KSMAX) {
     bf8 va[TLG_KSMAX], vb[TLG_KSMAX];
 #pragma unroll
