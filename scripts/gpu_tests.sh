@@ -1,9 +1,10 @@
-# GPU parity tests only (tag = $1, optional -k expression = $2)
+# the whole -m gpu suite + smoke on the in-tree build (tag = $1)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${1:-x}
-K=${2:+-k "$2"}
-timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread $K > gpurun_out/tests_$TAG.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|error" gpurun_out/tests_$TAG.log | head -30; tail -40 gpurun_out/tests_$TAG.log; exit 1; }
-tail -3 gpurun_out/tests_$TAG.log
+TAG=${1:-t}
+timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/tests_$TAG.log; exit 1; }
+tail -2 gpurun_out/tests_$TAG.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
+tail -1 gpurun_out/smoke_$TAG.log
