@@ -238,6 +238,19 @@ def load_traffic(kernel):
     except Exception:
         return None
 
+
+def traffic_source():
+    """Where load_traffic's bytes come from: the committed PMC passes named in
+    profiles/pmc_traffic.json (counted in a separate rocprofv3 --pmc run of the same build, not
+    in this bench run)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            d = json.load(f)
+        return ("profiles/pmc_traffic.json ({} PMC passes: {}); counted in a separate rocprofv3 --pmc "
+                "run, not in this bench run".format(d.get("source"), d.get("method")))
+    except Exception:
+        return None
+
 def bench_griffin_lim(local, frames=1000):
     """tt2_gl_synthesize_dev on a synthetic normalised mel [1000, 80] (paper_hparams audio: n_fft
     2048, win 1100, hop 275; 60 iterations), HIP-event timed; audio-samples/s of the output."""
@@ -309,6 +322,10 @@ def front_end_flops(B, Ti, T_ref, hp, emt_only=False):
     D = hp.reference_depth
     ref += 2.0 * B * H * (W * ci + D) * 3 * D + 2.0 * B * D * 128
     return fl + ref * (1 if emt_only else 2)
+
+
+LOSS_PARTS = ("before", "after", "stop_token", "regularization", "style_emb_loss_emt", "style_emb_loss_spk",
+              "style_emb_orthog_loss")
 
 
 def bench_train(a, rank, world, local, barrier, max_over_ranks):
@@ -384,6 +401,12 @@ def bench_train(a, rank, world, local, barrier, max_over_ranks):
                 ms_per_step=round(ms, 2), steps=a.train_steps, warmup=1,
                 forward_backward_ms=round(L["forward_backward_ms"], 2),
                 loss_first=round(losses[0]["loss"], 5), loss_last=round(L["loss"], 5),
+                # every component of the first step's and the last timed step's forward loss (the
+                # total's rise over the first clipped-Adam updates is the orthogonality loss at
+                # lr 1e-3: DESIGN.md §5.6h, scripts/diag_train_loss.py)
+                losses_first={k: round(v, 5) for k, v in losses[0].items() if k in LOSS_PARTS},
+                losses_last={k: round(v, 5) for k, v in L.items() if k in LOSS_PARTS},
+                updates_before_last=a.train_steps,
                 grad_norm=round(L["grad_norm"], 5), dtype=a.train_precision,
                 config=dict(workload=("configs[4]: whole Tacotron-2 training step from ids + reference mels "
                                       "(encoder, 2 reference encoders + GST, teacher-forced decoder, Postnet; "
@@ -653,6 +676,7 @@ def main():
                         bound="latency (chip-wide hand-offs; weights on-chip)", roofline="hbm",
                         achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        traffic_source=traffic_source() if traffic else None,
                         algorithmic_bytes_per_launch=int(step_bytes * n),
                         algorithmic_bytes_per_step=int(step_bytes), steps_per_launch=n,
                         avg_launch_us=round(pd_ms * 1000.0, 1),
@@ -686,6 +710,7 @@ def main():
         roofline = dict(kernel="k_lstm (decoder Zoneout-LSTM, layers 1/2 alternating)", bound="hbm",
                         achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        traffic_source=traffic_source() if traffic else None,
                         algorithmic_bytes_per_launch=int(by), avg_launch_us=round(lstm_us, 3),
                         per_kernel_us=dict(zip(["prenet", "lstm_avg", "query", "energy",
                                                 "softmax_context", "projection", "lstm2", "side_job_only",

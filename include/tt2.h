@@ -480,6 +480,11 @@ typedef struct tt2_train_config {
    * tanh; its 128-wide output is the style embedding (memory_dim = 2*encoder_lstm_units + 128).
    * Needs both references, no style classifiers / orthogonality loss (the reference builds none). */
   int adain;
+  /* hp.smoothing (attention.py:71-91,150): the attention's probability_fn is the smoothing
+   * normalisation a_j = sigmoid(e_j) / sum_k sigmoid(e_k) over the unmasked positions instead of the
+   * softmax; the backward multiplies the softmax form by (1 - sigmoid(e_j)).  Runs the per-step
+   * attention launches (the persistent forward keeps the softmax). */
+  int smoothing;
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;
@@ -493,7 +498,11 @@ tt2_status tt2_train_load_tensor(tt2_train_ctx* ctx, const char* tf_name, const 
 /* All slice variables loaded -> zero the Adam moments. */
 tt2_status tt2_train_finalize(tt2_train_ctx* ctx);
 /* Use a caller-owned device buffer (e.g. a torch tensor RCCL all-reduces) as the flat gradient
- * buffer; NULL restores the internal one.  *n_out = its length in floats. */
+ * buffer; NULL restores the internal one.  *n_out = its length in floats: every variable's gradient
+ * followed by ONE status word that each forward_backward writes (0 = ok, 1 = the persistent forward
+ * timed out in a hand-off or stopped early).  The word travels in the tower mean with the gradients,
+ * and tt2_train_apply_dev skips the Adam and BN moving-average updates while it is nonzero, so a
+ * failed forward on any rank leaves every rank's weights unchanged; tt2_train_losses reports it. */
 tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* ctx, float* grads_d, int64_t* n_out);
 /* Every batch-norm moving_mean / moving_variance (Postnet, encoder convs, reference-encoder
  * convs) packed in variable order into a caller-owned device buffer (unpack = 0) or written back

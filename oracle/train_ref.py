@@ -80,13 +80,16 @@ def _conv_same(cum, k, b):
     return cols @ k[:, 0, :] + b                       # [B,T,F]
 
 
-def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneout=0.1, feed_target=None):
+def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneout=0.1, feed_target=None,
+            smoothing=False):
     """Teacher-forced decoder forward.  W: dict name -> torch tensor (requires_grad as wanted);
     memory [B,T_in,D]; lengths [B]; targets [B,T,80]; prenet_masks [T,2,B,P] keep bits;
     zoneout_masks [T,4,B,H] keep bits (c1,h1,c2,h2; training zoneout) or None (inference mix);
     feed_target [T] (None = all 1): the outcome of TacoTrainingHelper.next_inputs' per-step draw
     u < ratio (helpers.py:122-133) -- step t (t >= 1) gets the target frame t-1 when 1, else the
     decoder's own unclipped frame t-1 (outputs[:, -output_dim:]), through which gradients flow.
+    smoothing: hp.smoothing (attention.py:71-91,150), a = sigmoid(e) / sum sigmoid(e) over the
+    unmasked positions (sigmoid(-inf) = 0) instead of the softmax.
     Returns frames [B,T,80], stop logits [B,T], alignments [B,T_in,T]."""
     B, T_in, D = memory.shape
     T = targets.shape[1]
@@ -127,7 +130,11 @@ def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneo
         e = (W[LA + "attention_variable_projection"]
              * torch.tanh(keys + q[:, None, :] + loc + W[LA + "attention_bias"])).sum(2)
         e = torch.where(mask > 0, e, big_neg)
-        a = torch.softmax(e, 1)
+        if smoothing:
+            sg = torch.sigmoid(e)
+            a = sg / sg.sum(1, keepdim=True)
+        else:
+            a = torch.softmax(e, 1)
         cum = cum + a
         ctx = (a[:, :, None] * values).sum(1)
         pin = torch.cat([o2, ctx], 1)
@@ -520,7 +527,7 @@ def train_grads_frontend(Wnp, ids, lengths, ref_emt, ref_spk, targets, stop_targ
 
 def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneout_masks,
                 reg_weight=1e-6, dtype=torch.float64, clip=(-4.1, 4.0), postnet=False,
-                postnet_masks=None, feed_target=None, target_lengths=None, pos_weight=1.0):
+                postnet_masks=None, feed_target=None, target_lengths=None, pos_weight=1.0, smoothing=False):
     """One forward + backward; returns (outputs dict, losses tuple, grads dict incl. 'memory').
     postnet=True adds the Postnet and the ``after`` loss (tacotron.py:362-381, 775-776): losses
     become (before, stop, reg, after) and outputs gain 'mel_outputs' and 'bn_stats'.
@@ -532,7 +539,7 @@ def train_grads(Wnp, memory, lengths, targets, stop_targets, prenet_masks, zoneo
     st = torch.tensor(np.asarray(stop_targets), dtype=dtype)
     pm = torch.tensor(np.asarray(prenet_masks), dtype=dtype)
     zm = None if zoneout_masks is None else torch.tensor(np.asarray(zoneout_masks), dtype=dtype)
-    fr, sl, al = forward(W, mem, lengths, tg, pm, zm, feed_target=feed_target)
+    fr, sl, al = forward(W, mem, lengths, tg, pm, zm, feed_target=feed_target, smoothing=smoothing)
     b, s, r = losses(fr, sl, tg, st, W, reg_weight, clip, target_lengths, pos_weight)
     total = b + s + r
     out = dict(frames=clip_decoder_output(fr, clip).detach().numpy(), stop_logits=sl.detach().numpy(),

@@ -65,6 +65,7 @@ struct tt2_train_ctx {
   DevBuf dV, dBA, dKC, dBC, DVAL, DMEM, dZ, dPre, TBUF, part, red, kpart;
   DevBuf DF2, DCUM2, PQ2, SC2;
   DevBuf DWGP;  // [B][NT][32][A] k_tr_att_bwd_q's d W_loc accumulators (TrAtt::DWGP)
+  DevBuf SS;   // [T][B] smoothing: Σ sigmoid(e) per step (TrAtt::SS)
   DevBuf DWG;  // [32][A] k_tr_dwloc_cum: Σ cum_{t-1}·du per tap (+ the Σ du row)  // k_tr_att_bwd_q: df / d cum / d query / Σ a·d cum partials by step parity
   DevBuf TH, E, DF, PQ, FALL, ALN;
   // the large plain products (tr_gemm_big)
@@ -128,6 +129,7 @@ struct tt2_train_ctx {
   // buffers, energy granules, flags + control words, the prenet rows in bf16 fragment layout
   DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps, tpKWT;
   bool tp_on = false, tp_last = false, tp_check = false;
+  int* tp_ctl_dev = nullptr;  // control words of the last persistent forward (device)
   int* tp_ctl_host = nullptr;  // pinned [2]: the launch's control words, checked at the next read-back
 };
 
@@ -831,6 +833,8 @@ __global__ void k_tr_rows_bf16(const float* __restrict__ src, long lds, long row
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 struct TrAtt {
   int B, Tin, T, A, F, KW, D, H, P, t, nt;  // nt = j-tiles per row (TR_JT rows each)
+  int smooth;           // hp.smoothing: a = sigmoid(e) / Σ sigmoid(e) (attention.py:71-91) instead of softmax
+  float* SS;            // [T][B] Σ_j sigmoid(e_j) of each step (smooth): sigmoid(e_j) = a_j·SS for the backward
   const int* lens;
   const float* keys;    // [B,Tin,A]
   const float* values;  // [B,Tin,D]
@@ -1045,16 +1049,20 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
   const int len = a.lens[b];
   const float* e = a.E + (long)b * a.Tin;
   float mx = -INFINITY;
-  for (int j = threadIdx.x; j < len; j += blockDim.x) mx = fmaxf(mx, e[j]);
-  mx = block_max(mx, s16);
+  if (!a.smooth) {
+    for (int j = threadIdx.x; j < len; j += blockDim.x) mx = fmaxf(mx, e[j]);
+    mx = block_max(mx, s16);
+  }
   float sm = 0.f;
   for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) {
-    const float x = j < len ? expf(e[j] - mx) : 0.f;
+    // masked positions score -inf: exp -> 0, and sigmoid(-inf) = 0 under the smoothing normalisation
+    const float x = j < len ? (a.smooth ? 1.f / (1.f + expf(-e[j])) : expf(e[j] - mx)) : 0.f;
     al[j] = x;
     sm += x;
   }
   sm = block_sum(sm, s16);
   const long tb = (long)a.t * a.B + b;
+  if (a.smooth && blockIdx.x == 0 && threadIdx.x == 0) a.SS[tb] = sm;
   for (int j = threadIdx.x; j < a.Tin; j += blockDim.x) {
     const float x = al[j] / sm;
     al[j] = x;
@@ -1358,7 +1366,9 @@ __global__ __launch_bounds__(TR_AT) void k_tr_att_energy_bwd(TrAtt a) {
   __syncthreads();
   if (tid < TR_JT) {
     const int j = j0 + tid;
-    de[tid] = j < len ? a.ALN[tb * a.Tin + j] * (dat[tid] - s) : 0.f;
+    const float aj = j < len ? a.ALN[tb * a.Tin + j] : 0.f;
+    // smoothing: d e_j = a_j (d a_j - s)·(1 - sigmoid(e_j)), sigmoid(e_j) = a_j·Σ sigmoid
+    de[tid] = j < len ? aj * (dat[tid] - s) * (a.smooth ? 1.f - aj * a.SS[tb] : 1.f) : 0.f;
   }
   for (int i = tid; i < a.F * a.A; i += blockDim.x) WlT[(i % a.A) * 33 + i / a.A] = a.Wl[i];
   __syncthreads();
@@ -1489,7 +1499,7 @@ __global__ __launch_bounds__(TR_E2T) void k_tr_att_energy_bwd2(TrAtt a) {
       }
     }
     acc = wave_sum(acc);
-    const float de = j < len ? aln * ((acc + dcum) - s) : 0.f;
+    const float de = j < len ? aln * ((acc + dcum) - s) * (a.smooth ? 1.f - aln * a.SS[tb] : 1.f) : 0.f;
     const float du0 = de * va0 * (1.f - th0 * th0), du1 = de * va1 * (1.f - th1 * th1);
     dv0 += de * th0;
     dv1 += de * th1;
@@ -1840,6 +1850,7 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
   TRQ_STAMP(2);
   // s = Σ_j a_j da_j = dctx·ctx_t + Σ_j a_j d cum_t[j]   (block_sum's barriers also publish dcum)
   const float s = block_sum(sp, s16) + scv;
+  const float ssum = a.smooth ? a.SS[tb] : 0.f;  // smoothing: Σ sigmoid(e) of this step
   TRQ_STAMP(3);
   // ---- d align of the own rows (jr = w + NW u): every row's values in flight before the dot products
   const trq_f4* d4 = reinterpret_cast<const trq_f4*>(dctx);
@@ -1868,7 +1879,7 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
       acc = trq_wave_sum(acc);
       if (lane == 0) {
         const int j = j0 + jr;
-        de[jr] = j < len ? alns[j] * ((acc + dcum[jr]) - s) : 0.f;
+        de[jr] = j < len ? alns[j] * ((acc + dcum[jr]) - s) * (a.smooth ? 1.f - alns[j] * ssum : 1.f) : 0.f;
       }
     }
   } else {
@@ -1896,7 +1907,7 @@ __global__ __launch_bounds__(TRQ_NT, 1) void k_tr_att_bwd_q(TrAtt a, TrQ z) {
         acc = trq_wave_sum(acc);
         if (lane == 0) {
           const int j = j0 + jr;
-          de[jr] = j < len ? alns[j] * ((acc + dcum[jr]) - s) : 0.f;
+          de[jr] = j < len ? alns[j] * ((acc + dcum[jr]) - s) * (a.smooth ? 1.f - alns[j] * ssum : 1.f) : 0.f;
         }
       }
     }
@@ -2187,11 +2198,13 @@ __global__ __launch_bounds__(256) void k_tr_sum_final(const float* __restrict__ 
 }
 
 // clip_by_global_norm(clip) + TF Adam (lr_t folded on the host)
+// g[n] is the step's status word (k_tr_status; averaged over ranks with the gradients): nonzero when
+// any rank's persistent forward failed, and then no rank applies the update
 __global__ void k_tr_adam(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
                           float* __restrict__ v, long n, const float* __restrict__ norm, float clip, float b1, float b2,
                           float eps, float lr_t) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || g[n] != 0.f) return;
   const float scale = clip > 0.f ? clip / fmaxf(norm[0], clip) : 1.f;
   const float gi = g[i] * scale;
   const float mi = b1 * m[i] + (1.f - b1) * gi;
@@ -2380,11 +2393,19 @@ __global__ void k_pn_add_ddec(const float* __restrict__ dprj, const float* __res
   if (clipm[j]) dFR[j] += dprj[i] + dx0[i];
 }
 __global__ void k_pn_moving(float* __restrict__ mm, float* __restrict__ mv, const float* __restrict__ mean,
-                            const float* __restrict__ var, int C, float momentum) {
+                            const float* __restrict__ var, int C, float momentum, const float* __restrict__ status) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  if (c >= C || status[0] != 0.f) return;
   mm[c] -= (mm[c] - mean[c]) * (1.f - momentum);
   mv[c] -= (mv[c] - var[c]) * (1.f - momentum);
+}
+
+// The step's status word behind the gradients (g[total]): 1 when the persistent forward of this step
+// timed out in a hand-off or did not run every step (its control words), else 0.  It rides in the
+// data-parallel tower mean with the gradients, so k_tr_adam / k_pn_moving on every rank skip an
+// update that any rank's failed forward would have corrupted; tt2_train_losses then reports it.
+__global__ void k_tr_status(const int* __restrict__ ctl, int T, float* __restrict__ status) {
+  if (threadIdx.x == 0) status[0] = (ctl && (ctl[0] != 0 || ctl[1] != T)) ? 1.f : 0.f;
 }
 
 // ---- host orchestration ----------------------------------------------------------------------
@@ -2626,7 +2647,8 @@ static void tr_alloc(tt2_train_ctx* c) {
              NM = c->NM, LX1 = c->LX1;
   const long TB = T * B;
   auto f = [](DevBuf& d, long n) { d.alloc(sizeof(float) * (size_t)std::max<long>(n, 1)); };
-  f(c->params, c->total); f(c->grads_own, c->total); f(c->adam_m, c->total); f(c->adam_v, c->total);
+  f(c->params, c->total); f(c->grads_own, c->total + 1);  // + the status word (k_tr_status)
+  f(c->adam_m, c->total); f(c->adam_v, c->total);
   c->grads = c->grads_own.as<float>();
   f(c->K1T, 4 * H * LX1); f(c->K2T, 4 * H * 2 * H); f(c->WqT, A * H); f(c->WfT, NM * (H + D)); f(c->WsT, H + D);
   f(c->WmT, A * D); f(c->Wp2T, P * P);
@@ -2855,7 +2877,7 @@ static bool tr_dwloc_cum_ok(const tt2_train_ctx* c) {
 // x 32 filters), B <= 64, T_in <= TP_TMAX, bf16 operands with the bf16 values copy, every step
 // teacher-forced (a step fed its own frame needs the frame projection inside the loop).
 static bool tr_persist_fits(const tt2_train_ctx* c, int Tin, bool free_run, bool values16) {
-  return c->tp_on && !free_run && values16 && c->B <= 64 && Tin <= TP_TMAX && c->H == TP_H && c->P == TP_P &&
+  return c->tp_on && !free_run && values16 && !c->cfg.smoothing && c->B <= 64 && Tin <= TP_TMAX && c->H == TP_H && c->P == TP_P &&
          c->D == TP_D && c->A == TP_A && c->F == TP_F && c->KW == TP_KWMAX && c->LX1 == TP_LX1;
 }
 
@@ -2901,6 +2923,11 @@ static void tr_persist_forward(tt2_train_ctx* c, const TrAtt& at, const uint8_t*
     a.stamps = c->tpStamps.as<long long>();
   }
   tp_launch(a, s);
+  c->tp_ctl_dev = a.ctl;
+  // TT2_TP_FORCE_FAIL=1 (test hook): mark this launch's control word as a timed-out hand-off in phase
+  // 0, as a stalled launch would, to exercise the status word and the skipped update
+  if (const char* ff = std::getenv("TT2_TP_FORCE_FAIL"))
+    if (ff[0] == '1') TT2_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.ctl), 1, 1, s));
   if (!tr_dwloc_cum_ok(c)) tp_location_features(at.CUM, at.Kc, at.bc, c->B, T, Tin, at.FALL, s);
   if (st) {
     std::vector<long long> h((size_t)TP_NB * 32);
@@ -2927,6 +2954,11 @@ static void tr_persist_check(tt2_train_ctx* c) {
             "persistent training forward: a hand-off wait timed out (phase " + std::to_string(ph - 1) +
                 "); TT2_TR_PERSIST=0 runs the per-step launches");
   TT2_CHECK(steps == c->T_last, TT2_ERR_STATE, "persistent training forward did not complete every step");
+}
+
+static void tr_write_status(tt2_train_ctx* c, hipStream_t s) {
+  hipLaunchKernelGGL(k_tr_status, dim3(1), dim3(64), 0, s, c->tp_last ? c->tp_ctl_dev : nullptr, c->T_last,
+                     c->grads + c->total);
 }
 
 static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* lens, const float* tg, const float* stg,
@@ -2966,7 +2998,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     cv(pvar(c, vn("decoder/query_layer/kernel")), (long)H * A, c->hWq);
     cv(c->WqT.as<float>(), (long)H * A, c->hWqT);
   }
-  TT2_HIP(hipMemsetAsync(c->grads, 0, sizeof(float) * c->total, s));
+  TT2_HIP(hipMemsetAsync(c->grads, 0, sizeof(float) * (c->total + 1), s));
   TT2_HIP(hipMemsetAsync(c->red.p, 0xFF, 4 * sizeof(float), s));  // NaN until this call's losses land
 
   // ---- forward ----
@@ -3041,6 +3073,11 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   at.FALL = c->FALL.as<float>(); at.ALN = c->ALN.as<float>();
   at.TH = c->TH.as<float>(); at.E = c->E.as<float>(); at.DF = c->DF.as<float>();
   at.PQ = c->PQ.as<float>();
+  at.smooth = c->cfg.smoothing ? 1 : 0;
+  if (at.smooth) {
+    if (c->SS.bytes < sizeof(float) * (size_t)T * B) c->SS.alloc(sizeof(float) * (size_t)T * B);
+    at.SS = c->SS.as<float>();
+  }
   const int NT = (Tin + TR_JT - 1) / TR_JT;
   at.nt = NT;
   const dim3 att_grid(NT, B);
@@ -4182,7 +4219,7 @@ static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s)
       const std::string sc = pn_scope(i + 1) + "batch_normalization/";
       hipLaunchKernelGGL(k_pn_moving, dim3((c->PC + 255) / 256), dim3(256), 0, s, pvar(c, sc + "moving_mean"),
                          pvar(c, sc + "moving_variance"), c->BNM.as<float>() + (long)i * c->PC,
-                         c->BNV.as<float>() + (long)i * c->PC, c->PC, c->cfg.bn_momentum);
+                         c->BNV.as<float>() + (long)i * c->PC, c->PC, c->cfg.bn_momentum, c->grads + c->total);
     }
     c->pn_ran = false;
   }
@@ -4191,7 +4228,8 @@ static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s)
     auto upd = [&](const std::string& sc, int C) {
       const float* st = c->fBN.as<float>() + (long)nbn * 2 * 512;
       hipLaunchKernelGGL(k_pn_moving, dim3((C + 255) / 256), dim3(256), 0, s, pvar(c, sc + "batch_normalization/moving_mean"),
-                         pvar(c, sc + "batch_normalization/moving_variance"), st, st + 512, C, c->cfg.bn_momentum);
+                         pvar(c, sc + "batch_normalization/moving_variance"), st, st + 512, C, c->cfg.bn_momentum,
+                         c->grads + c->total);
       ++nbn;
     };
     for (int i = 0; i < c->cfg.enc_conv_layers; ++i) upd(fe_conv_scope(i + 1), c->cfg.enc_conv_channels);
@@ -4470,7 +4508,7 @@ tt2_status tt2_train_finalize(tt2_train_ctx* c) {
 tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* c, float* grads_d, int64_t* n_out) {
   return guard([&] {
     TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
-    if (n_out) *n_out = c->total;
+    if (n_out) *n_out = c->total + 1;  // the gradients + the step's status word (k_tr_status)
     c->grads = grads_d ? grads_d : c->grads_own.as<float>();
   });
 }
@@ -4526,6 +4564,7 @@ tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* c, const float* memory_
                         postnet_masks_d, T_in, T_out, s);
     tr_redzones(c, "decoder + postnet");
     tr_regularize(c, s);
+    tr_write_status(c, s);
     TT2_HIP(hipEventRecord(c->ev1, s));
     TT2_HIP(hipGetLastError());
   });
@@ -4570,6 +4609,7 @@ tt2_status tt2_train_forward_backward_text_dev(tt2_train_ctx* c, const int32_t* 
     g_tr_prec = 0;
     g_tr_ctx = nullptr;
     tr_regularize(c, s);
+    tr_write_status(c, s);
     TT2_HIP(hipEventRecord(c->ev1, s));
     TT2_HIP(hipGetLastError());
   });

@@ -140,6 +140,8 @@ _FORK = dict(
     leaky_alpha=0.4, NN_init=True, NN_scaler=0.3, gin_channels=-1, use_speaker_embedding=False,
     n_speakers=5, wavenet_random_seed=5339, wavenet_synthesis_batch_size=20, wavenet_dropout=0.05,
     wavenet_weight_normalization=False, wavenet_synth_debug=False,
+    wavenet_debug_wavs=['training_data/audio/audio-LJ001-0008.npy'],
+    wavenet_debug_mels=['training_data/mels/mel-LJ001-0008.npy'],
 )
 
 #: fork default hyper-parameters (code/hparams.py)

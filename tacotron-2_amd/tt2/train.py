@@ -70,8 +70,7 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
         raise ValueError("tacotron_teacher_forcing_mode must be 'constant' or 'scheduled'")
     if hp.predict_linear:
         raise NotImplementedError("predict_linear (CBHG linear loss) is not built in the training step")
-    if hp.smoothing:
-        raise NotImplementedError("smoothing attention normalisation is built for synthesis only")
+    cfg.smoothing = 1 if hp.smoothing else 0        # attention.py:71-91,150 (training graph too)
     # style path of the front end (tacotron.py:236-308): 'gst' (hp.use_gst; False = the embeddings),
     # 'embed' (args.pretrained_emb_disc_all: the reference embeddings themselves), 'adain'
     if style not in ("gst", "embed", "adain"):

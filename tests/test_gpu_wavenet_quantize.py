@@ -135,3 +135,63 @@ def test_quantize_fork_widths_teacher_forced():
     np.testing.assert_allclose(out["logits"], lg, atol=1e-4, rtol=1e-4)
     safe = _margin_ok(lg, ul.T, k)
     np.testing.assert_array_equal(out["k"][safe], k[safe])
+
+
+@pytest.mark.parametrize("quant", [False, True])
+def test_synthesizer_unconditional_path(quant):
+    """wavenet_vocoder.synthesizer.Synthesizer without local conditioning (synthesizer.py:51-53,
+    75-78): synthesis_length = 100 samples per row, trimmed to len(mel) * hop like the reference's
+    audio_lengths; the generated row equals the engine's own unconditional run on the same uniforms,
+    and its logits (teacher-forced on the produced samples) match the oracle within 1e-4."""
+    from wavenet_vocoder.synthesizer import SYNTHESIS_LENGTH, Synthesizer
+    hp = _quant_hp(6, 2, cin=-1) if quant else small_wavenet_hparams(6, 2)
+    if not quant:
+        hp.override_from_dict(dict(cin_channels=-1))
+    T = SYNTHESIS_LENGTH
+    um, ul = mol_uniforms(T, 1, seed=13)
+    syn = Synthesizer()
+    syn.load(None, hp)
+    wavs = syn.synthesize(None, None, None, None, None, u_mix=None if quant else um, u_log=ul)
+    assert len(wavs) == 1 and wavs[0].shape == (T,)
+    W = syn.model._weights
+    eng = _eng(hp, W, 1, T)
+    out = eng.generate_unconditional(1, T, None if quant else um, ul, 0, None)
+    eng.close()
+    np.testing.assert_array_equal(wavs[0], out["y"][0])
+    # with mels given, the rows are trimmed to len(mel) * hop (here shorter than 100 samples)
+    short = syn.synthesize([np.zeros((0, 80), np.float32)], None, None, None, None,
+                           u_mix=None if quant else um, u_log=ul)
+    assert short[0].shape == (0,)
+    teacher = (out["k"] if quant else out["y"]).astype(np.float32)
+    eng = _eng(hp, W, 1, T)
+    tf = eng.generate_unconditional(1, T, None if quant else um, ul, 0, teacher, want_logits=True)
+    eng.close()
+    _, _, lg = WR.incremental(None, W, wavenet_oracle_hp(hp), None if quant else um, ul, teacher,
+                              return_logits=True, T=T)
+    np.testing.assert_allclose(tf["logits"], lg, atol=1e-4, rtol=1e-4)
+
+
+def test_synthesizer_debug_wavs_teacher_force(tmp_path):
+    """hparams.wavenet_synth_debug (synthesizer.py:56-58, 83-95): the mels come from
+    wavenet_debug_mels and the debug wavs teacher-force the generator; the result equals the
+    engine's teacher-forced generation on the same condition and uniforms."""
+    from wavenet_vocoder.synthesizer import Synthesizer, _interp
+    hp = small_wavenet_hparams(6, 2)
+    rng = np.random.default_rng(5)
+    hop = int(np.prod(hp.upsample_scales))
+    mel = rng.uniform(-4, 4, (2, 80)).astype(np.float32)
+    wav = rng.uniform(-0.5, 0.5, (2 * hop,)).astype(np.float32)
+    np.save(tmp_path / "mel.npy", mel)
+    np.save(tmp_path / "audio.npy", wav)
+    hp.override_from_dict(dict(wavenet_synth_debug=True, wavenet_debug_mels=[str(tmp_path / "mel.npy")],
+                               wavenet_debug_wavs=[str(tmp_path / "audio.npy")]))
+    um, ul = mol_uniforms(2 * hop, 1, seed=3)
+    syn = Synthesizer()
+    syn.load(None, hp)
+    got = syn.synthesize([np.zeros((7, 80), np.float32)], None, None, None, None, u_mix=um, u_log=ul)
+    assert len(got) == 1 and got[0].shape == (2 * hop,)
+    cond = _interp(np.clip(mel, -4, 4), (-4, 4))[None].astype(np.float32)
+    eng = _eng(hp, syn.model._weights, 1, 2 * hop)
+    out = eng.generate(cond, um, ul, 0, wav[None])
+    eng.close()
+    np.testing.assert_array_equal(got[0], out["y"][0])

@@ -292,13 +292,24 @@ def test_synthesizer_filenames_to_inputs_pads_per_tower(tmp_path):
     assert get_output_lengths(np.array([[0.2, 0.7], [0.1, 0.1]])) == [1, 2]
 
 
-def test_wavenet_synthesizer_host_prep_rejects_unconditional():
-    from wavenet_vocoder.synthesizer import Synthesizer, _interp
+def test_wavenet_synthesizer_host_prep_and_conditions():
+    """The Synthesizer's host prep (_interp) and its condition switches: cin_channels <= 0 builds the
+    unconditional synthesis_length path (synthesizer.py:51-53,75-78), wavenet_synth_debug needs the
+    debug mels and wavs to pair up (synthesizer.py:56-58)."""
+    from wavenet_vocoder.synthesizer import SYNTHESIS_LENGTH, Synthesizer, _interp
     np.testing.assert_allclose(_interp(np.array([-4.0, 0.0, 4.0]), (-4, 4)), [0, 0.5, 1])
     hp = bench_wavenet_hparams()
     hp.cin_channels = -1
-    with pytest.raises(NotImplementedError):
-        Synthesizer().load(None, hp)
+    syn = Synthesizer()
+    syn.load(None, hp)
+    assert syn._check_conditions() == (False, False) and SYNTHESIS_LENGTH == 100
+    hp = bench_wavenet_hparams()
+    hp.override_from_dict(dict(wavenet_synth_debug=True, wavenet_debug_mels=["a.npy", "b.npy"],
+                               wavenet_debug_wavs=["a.npy"]))
+    syn = Synthesizer()
+    syn.load(None, hp)
+    with pytest.raises(ValueError, match="pair up"):
+        syn.synthesize([np.zeros((2, 80), np.float32)], None, ["x"], None, None)
 
 
 def test_wavenet_gc_weight_specs():

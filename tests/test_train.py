@@ -1088,3 +1088,150 @@ def test_gpu_train_persistent_forward_close_to_oracle():
         frob = float(np.linalg.norm(r["g"][n] - g[n]) / max(np.linalg.norm(g[n]), 1e-30))
         print("  {:90s} frob {:.3e}".format(n, frob))
         assert frob < (0.1 if "prenet" in n else 1e-2), (n, frob)
+
+
+@pytest.mark.gpu
+def test_gpu_train_failed_persistent_forward_skips_update():
+    """a persistent forward whose hand-off timed out (forced with the TT2_TP_FORCE_FAIL
+    test hook, which writes the control word a stalled launch leaves) must not reach the weights.
+    The step's status word behind the gradients (k_tr_status) makes clipped Adam and the BN moving
+    averages skip the update -- on every rank, since the word rides in the tower mean -- and the
+    read-back after the step reports the failure; the next good step updates normally."""
+    import os
+    from tt2._lib import TT2Error
+    from tt2.hparams import hparams
+    from tt2.train import TacotronTrainer
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    B, T_in, T_out = 5, 7, 3
+    W = init_tacotron_weights(hp, seed=5339)
+    mem, lens, tg, st = train_batch(B, T_in, T_out, memory_width(hp), seed=7)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=7)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=7)
+    name = TRN.L1 + "kernel"
+    shape = np.asarray(W[name]).shape
+    mm = "Tacotron_model/inference/postnet_convolutions/conv_layer_1_postnet_convolutions/batch_normalization/moving_mean"
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, precision="bf16", postnet=True)
+    try:
+        w0, m0 = tr.get(name, 0, shape), tr.get(mm, 0, (hp.postnet_channels,))
+        os.environ["TT2_TP_FORCE_FAIL"] = "1"
+        try:
+            tr.forward_backward(mem, lens, tg, st, pm, None, pnm)
+            tr.apply(1)
+        finally:
+            os.environ.pop("TT2_TP_FORCE_FAIL", None)
+        with pytest.raises(TT2Error, match="timed out"):
+            tr.losses()
+        assert float(tr.get("diag:persist", 0, (1,))[0]) == 1.0
+        assert float(tr.grad_buf[-1].item()) == 1.0          # the status word
+        np.testing.assert_array_equal(tr.get(name, 0, shape), w0)
+        np.testing.assert_array_equal(tr.get(mm, 0, (hp.postnet_channels,)), m0)
+        np.testing.assert_array_equal(tr.get(name, 2, shape), 0.0)   # Adam m untouched
+        tr.forward_backward(mem, lens, tg, st, pm, None, pnm)
+        tr.apply(1)
+        L = tr.losses()
+        assert np.isfinite(L["loss"]) and float(tr.grad_buf[-1].item()) == 0.0
+        assert np.abs(tr.get(name, 0, shape) - w0).max() > 0
+    finally:
+        tr.close()
+
+
+_LOSS_KEYS = ("before", "after", "stop_token", "regularization", "style_emb_loss_emt", "style_emb_loss_spk",
+              "style_emb_orthog_loss")
+
+
+def _configs4_case(T_out, T_ref=800, B=64, T_in=150):
+    """The bench's configs[4] batch (bench.py bench_train: seeds, 4 + 4 style classes, synthetic
+    labels) at a chosen T_out."""
+    from tt2.hparams import hparams
+    from tt2.synthetic import enc_conv_masks, enc_zoneout_masks, tacotron_inputs
+    from tt2.train import init_style_disc_weights
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    W = init_tacotron_weights(hp, seed=hp.tacotron_random_seed)
+    W.update(init_style_disc_weights(hp, 4, 4))
+    _, _, tg, st = train_batch(B, T_in, T_out, memory_width(hp), seed=1234)
+    ids, tl, re, rs = tacotron_inputs(B, T_in, T_ref, seed=1234)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=7)
+    zm = zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=7)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=7)
+    em = enc_conv_masks(hp.enc_conv_num_layers, B, T_in, hp.enc_conv_channels, seed=7)
+    ezm = enc_zoneout_masks(T_in, B, hp.encoder_lstm_units, seed=7)
+    lab = np.random.default_rng(99).integers(0, 4, (2, B)).astype(np.int32)
+    return hp, W, (ids, tl, re, rs, tg, st, pm, zm, pnm, em, ezm), lab
+
+
+@pytest.mark.gpu
+def test_gpu_train_configs4_whole_step_fp32_bf16_agree():
+    """the whole configs[4] step at full size (B = 64, T_in = 150, T_ref = 800,
+    T_out = 800, from ids with the front end, 4 + 4 class style classifiers and the orthogonality
+    loss): fp32 and bf16 agree on every loss component -- the decoder / Postnet losses within 1e-3,
+    the style losses within 5e-3 (both reference encoders' conv and GRU products take bf16 operands,
+    2^-9 relative rounding, and the orthogonality loss multiplies two of their outputs) -- and on the
+    global gradient norm within 2 %; everything finite."""
+    from tt2.train import TacotronTrainer
+    hp, W, batch, lab = _configs4_case(800)
+    res = {}
+    for prec in ("fp32", "bf16"):
+        tr = TacotronTrainer(hp, W, 64, 150, 800, 0, precision=prec, frontend=True, max_T_ref=800, n_emt=4, n_spk=4)
+        try:
+            tr.set_style_labels(lab[0], lab[1])
+            tr.forward_backward_text(*batch)
+            tr.apply(1)
+            res[prec] = tr.losses()
+        finally:
+            tr.close()
+        print(prec, {k: round(v, 5) for k, v in res[prec].items()})
+        assert all(np.isfinite(v) for v in res[prec].values())
+    for k in _LOSS_KEYS:
+        a, b = res["fp32"][k], res["bf16"][k]
+        tol = 5e-3 if k.startswith("style") else 1e-3
+        assert abs(a - b) <= tol * abs(a), (k, a, b)
+    a, b = res["fp32"]["grad_norm"], res["bf16"]["grad_norm"]
+    assert abs(a - b) < 2e-2 * a, (a, b)
+
+
+@pytest.mark.gpu
+def test_gpu_train_configs4_trajectory_matches_oracle():
+    """the whole configs[4] step at its full widths and shapes -- B = 64 (two
+    32-row blocks), T_in = 150, both reference encoders over T_ref = 800 (6 stride-2 convs with
+    batch-statistics BN, the GRU), 4 + 4 class style classifiers, orthogonality loss, Postnet --
+    with T_out reduced to 6 so the float64 oracle (oracle/train_ref.py) runs in seconds: the fp32
+    device's per-component losses over three clipped-Adam updates at lr 1e-3 follow the oracle's
+    (losses before update 1 within 1e-4 relative, before updates 2 and 3 within 2e-3; the global
+    gradient norm of each update within 1e-3).  This is the trajectory the bench reports at T_out =
+    800 (the orthogonality loss jumps after the first sign-sized Adam step)."""
+    from tt2.train import TacotronTrainer
+    T = 6
+    hp, W, batch, lab = _configs4_case(T)
+    ids, tl, re, rs, tg, st, pm, zm, pnm, em, ezm = batch
+    style = dict(emt_labels=lab[0], spk_labels=lab[1], n_emt=4, n_spk=4, orthog_weight=0.02)
+    names = (TRN.frontend_var_names() + TRN.style_disc_var_names(False, 4, 4) + TRN.train_var_names()
+             + TRN.postnet_var_names())
+    tr = TacotronTrainer(hp, W, 64, 150, T, 0, precision="fp32", frontend=True, max_T_ref=800, n_emt=4, n_spk=4)
+    dev = []
+    try:
+        tr.set_style_labels(lab[0], lab[1])
+        for step in (1, 2, 3):
+            tr.forward_backward_text(*batch)
+            tr.apply(step, lr=1e-3)
+            dev.append(tr.losses())
+    finally:
+        tr.close()
+    params = {n: np.asarray(W[n], np.float64) for n in names}
+    m = {n: np.zeros_like(p) for n, p in params.items()}
+    v = {n: np.zeros_like(p) for n, p in params.items()}
+    for step in (1, 2, 3):
+        Wc = dict(W)
+        Wc.update(params)
+        L, g, _ = TRN.train_grads_frontend(Wc, ids, tl, re, rs, tg, st, pm, zm, em, ezm, hp.tacotron_reg_weight,
+                                           postnet_masks=pnm, style=style)
+        ref = dict(zip(("before", "stop_token", "regularization", "after", "style_emb_loss_emt",
+                        "style_emb_loss_spk", "style_emb_orthog_loss"), L))
+        gn = TRN.clip_and_adam(params, {n: g[n] for n in names}, m, v, step, 1e-3, eps=hp.tacotron_adam_epsilon)
+        got = dev[step - 1]
+        print(step, {k: (round(got[k], 5), round(ref[k], 5)) for k in ref}, "gnorm", got["grad_norm"], gn)
+        tol = 1e-4 if step == 1 else 2e-3
+        for k, want in ref.items():
+            assert abs(got[k] - want) <= tol * abs(want) + 1e-7, (step, k, got[k], want)
+        assert abs(got["grad_norm"] - gn) < 1e-3 * gn, (step, got["grad_norm"], gn)

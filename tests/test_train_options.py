@@ -200,3 +200,106 @@ def test_gpu_train_mask_decoder_requires_target_lengths():
             tr.set_step_inputs(targets_lengths=np.array([4, 9]))        # > max_T_out
     finally:
         tr.close()
+
+
+def test_oracle_smoothing_gradients_match_finite_differences():
+    """hp.smoothing in the training graph (attention.py:71-91,150: a = sigmoid(e) / Σ sigmoid(e)
+    over the unmasked positions): the restatement's autograd against central differences on the
+    attention variables, ragged input lengths."""
+    hp = small_hparams()
+    W, mem, lens, tg, st, pm, zm = _case(hp, B=2, T_in=6, T_out=4)
+    out, _, g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, reg_weight=1e-3, smoothing=True)
+    al = out["alignments"]
+    np.testing.assert_allclose(al.sum(1), 1.0, atol=1e-12)
+    assert np.all(al[1, lens[1]:] == 0)
+
+    def loss_of(W2):
+        Wt = {n: torch.tensor(np.asarray(W2[n]), dtype=torch.float64) for n in TRN.train_var_names()}
+        fr, sl, _ = TRN.forward(Wt, torch.tensor(mem, dtype=torch.float64), lens, torch.tensor(tg, dtype=torch.float64),
+                                torch.tensor(pm, dtype=torch.float64), torch.tensor(zm, dtype=torch.float64),
+                                smoothing=True)
+        b, s, r = TRN.losses(fr, sl, torch.tensor(tg, dtype=torch.float64), torch.tensor(st, dtype=torch.float64),
+                             Wt, 1e-3)
+        return float(b + s + r)
+
+    rng = np.random.default_rng(2)
+    for name in [TRN.LA + "attention_variable_projection", TRN.LA + "attention_bias",
+                 TRN.LA + "location_features_convolution/kernel", TRN.P + "decoder/query_layer/kernel"]:
+        arr = np.asarray(W[name], np.float64)
+        for _ in range(2):
+            idx = tuple(rng.integers(0, s) for s in arr.shape)
+            eps = 1e-6
+            Wp, Wm = dict(W), dict(W)
+            ap, am = arr.copy(), arr.copy()
+            ap[idx] += eps
+            am[idx] -= eps
+            Wp[name], Wm[name] = ap, am
+            fd = (loss_of(Wp) - loss_of(Wm)) / (2 * eps)
+            assert abs(fd - g[name][idx]) < 1e-7 + 1e-4 * abs(fd), (name, idx, fd, g[name][idx])
+
+
+def test_train_config_smoothing():
+    hp = small_hparams()
+    hp.override_from_dict(dict(smoothing=True))
+    assert train_config(hp, 2, 8, 4).smoothing == 1
+
+
+@pytest.mark.gpu
+def test_gpu_train_smoothing_matches_oracle():
+    """hp.smoothing in the training step: the sigmoid normalisation forward (k_tr_ctx) and the
+    softmax backward times (1 - sigmoid(e_j)) in the attention backward: fp32 frames / alignments
+    within 1e-4 and every gradient (incl. d memory) within 2e-4 of the float64 oracle, with the
+    Postnet and ragged lengths; the alignments are not the softmax ones."""
+    from tt2.train import TacotronTrainer
+    hp = small_hparams()
+    hp.override_from_dict(dict(smoothing=True))
+    B, T_in, T_out = 3, 9, 7
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out, seed=31)
+    pnm = postnet_masks(hp.postnet_num_layers, B, T_out, hp.postnet_channels, seed=31)
+    names = TRN.train_var_names() + TRN.postnet_var_names()
+    tr = TacotronTrainer(hp, W, B, T_in, T_out, 0, postnet=True)
+    try:
+        tr.forward_backward(mem, lens, tg, st, pm, zm, pnm)
+        L = tr.losses()
+        fr, sl, al = tr.outputs(T_in, T_out)
+        grads = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}
+        gmem = tr.get("memory", 1, mem.shape)
+    finally:
+        tr.close()
+    out, Lr, g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight, clip=_clip(hp),
+                                 postnet=True, postnet_masks=pnm, smoothing=True)
+    soft, _, _ = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight, clip=_clip(hp))
+    assert np.abs(al - soft["alignments"]).max() > 1e-3
+    assert np.abs(al - out["alignments"]).max() < 1e-4
+    assert np.abs(fr - out["frames"]).max() < 1e-4
+    assert abs(L["before"] - Lr[0]) < 1e-5 * Lr[0] and abs(L["after"] - Lr[3]) < 1e-5 * Lr[3]
+    for n in names:
+        if np.abs(g[n]).max() < 1e-12:
+            assert np.abs(grads[n]).max() < 1e-6, n
+            continue
+        assert _rel(grads[n], g[n]) < 2e-4, (n, _rel(grads[n], g[n]))
+    assert _rel(gmem, g["memory"]) < 2e-4
+
+
+@pytest.mark.gpu
+def test_gpu_train_smoothing_fork_widths_bf16():
+    """hp.smoothing at the fork widths in the bf16 step: the one-launch attention backward
+    (k_tr_att_bwd_q) with the smoothing factor, the persistent forward left out (it keeps the
+    softmax): against the float64 oracle at the mixed-precision tolerance of
+    test_gpu_train_persistent_forward_close_to_oracle."""
+    from tt2.hparams import hparams
+    from test_train import _trainer_run
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1, smoothing=True))
+    B, T_in, T_out = 4, 37, 10
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
+    r = _trainer_run(hp, W, (mem, lens, tg, st, pm, zm), {"TT2_TR_PERSIST": "1"})
+    assert r["persist"] == 0.0
+    out, (b, s, _), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight, clip=_clip(hp),
+                                        smoothing=True)
+    assert np.abs(r["al"] - out["alignments"]).max() < 1e-3
+    assert np.abs(r["fr"] - out["frames"]).max() < 1e-2
+    assert abs(r["L"]["before"] - b) < 1e-3 * b
+    for n in TRN.train_var_names():
+        frob = float(np.linalg.norm(r["g"][n] - g[n]) / max(np.linalg.norm(g[n]), 1e-30))
+        assert frob < (0.1 if "prenet" in n else 1e-2), (n, frob)
