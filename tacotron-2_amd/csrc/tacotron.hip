@@ -2115,10 +2115,10 @@ static void encode_dev(tt2_ctx* c, const int* ids_d, const int* lens_d, const in
     gemm(p, s);
   }
   if (c->l1_wspk.p && c->emt.spk) {  // emt 'simple': refnet_spk·W_lstm1[speaker rows] per utterance
-    if (!c->SPK1.p) {
-      c->SPK1.alloc(32L * 4 * c->H * 4);
-      TT2_HIP(hipMemsetAsync(c->SPK1.p, 0, c->SPK1.bytes, s));  // rows >= B stay zero
-    }
+    if (!c->SPK1.p) c->SPK1.alloc(32L * 4 * c->H * 4);
+    // every encode: rows >= B must be zero (the persistent decoder folds all 32 rows into its
+    // constants), also after an earlier encode of a larger batch
+    TT2_HIP(hipMemsetAsync(c->SPK1.p, 0, c->SPK1.bytes, s));
     GemmArgs g;
     g.M = B; g.N = 4 * c->H; g.K = EMT_OUT; g.A = c->ref_out.as<float>() + (size_t)c->cfg.max_batch * 128; g.lda = EMT_OUT;
     g.Bw = c->l1_wspk.as<float>(); g.ldb = 4 * c->H; g.Cout = c->SPK1.as<float>(); g.ldc = 4 * c->H;

@@ -1340,6 +1340,17 @@ tt2_status tt2_wn_finalize(tt2_wn_ctx* c) {
   });
 }
 
+// 'mulaw-quantize' teacher inputs are class indices: integers in [0, quantize_channels) (host check
+// of the tt2_wn_generate* host-buffer entry points; the device-pointer variant clamps in the kernel)
+static void wn_check_teacher(const tt2_wn_ctx* c, const float* teacher, long n) {
+  if (!c->quantize || !teacher) return;
+  for (long i = 0; i < n; ++i) {
+    const float v = teacher[i];
+    TT2_CHECK(v >= 0.f && v < (float)c->C && v == std::floor(v), TT2_ERR_INVALID_ARG,
+              "mulaw-quantize teacher inputs must be integer classes in [0, quantize_channels)");
+  }
+}
+
 tt2_status tt2_wn_generate(tt2_wn_ctx* c, const float* cond, int B, int T_f, const float* u_mix, const float* u_log,
                            uint64_t seed, const float* teacher, float* wav_out, int32_t* mix_idx_out,
                            float* logits_out, float* upsampled_out) {
@@ -1370,6 +1381,7 @@ tt2_status tt2_wn_generate(tt2_wn_ctx* c, const float* cond, int B, int T_f, con
       TT2_HIP(hipMemcpyAsync(c->ulog.p, u_log, sizeof(float) * T * B, hipMemcpyHostToDevice, s));
       ul = c->ulog.as<float>();
     }
+    wn_check_teacher(c, teacher, (long)T * B);
     if (teacher) {
       c->teacher.alloc(sizeof(float) * T * B);
       TT2_HIP(hipMemcpyAsync(c->teacher.p, teacher, sizeof(float) * T * B, hipMemcpyHostToDevice, s));
@@ -1415,6 +1427,7 @@ tt2_status tt2_wn_generate_unconditional(tt2_wn_ctx* c, int B, int64_t T, const 
       TT2_HIP(hipMemcpyAsync(c->ulog.p, u_log, sizeof(float) * T * B, hipMemcpyHostToDevice, s));
       ul = c->ulog.as<float>();
     }
+    wn_check_teacher(c, teacher, (long)T * B);
     if (teacher) {
       c->teacher.alloc(sizeof(float) * T * B);
       TT2_HIP(hipMemcpyAsync(c->teacher.p, teacher, sizeof(float) * T * B, hipMemcpyHostToDevice, s));

@@ -175,7 +175,9 @@ __global__ __launch_bounds__(WQ_THREADS, 1) void k_generate_q(QGenArgs a) {
       a.wav[(long)b * a.T + t] = w;
       if (a.kout) a.kout[(long)b * a.T + t] = k;
     }
-    kprev = a.teacher ? (int)a.teacher[(long)b * a.T + t] : k;
+    // teacher classes are validated on the host for tt2_wn_generate*; device-side teachers
+    // (tt2_wn_generate_dev) are clamped so a bad class cannot index past the first conv's rows
+    kprev = a.teacher ? min(max((int)a.teacher[(long)b * a.T + t], 0), a.Q - 1) : k;
     __syncthreads();
   }
 }

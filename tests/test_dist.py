@@ -118,7 +118,7 @@ class _StubTTS(object):
         return dict(wav=wav, audio_lengths=np.array([w.shape[0] for w in wavs], np.int64))
 
 
-def _e2e_worker(rank, world, port, out_dir):
+def _e2e_worker(rank, world, port, out_dir, B=5):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "tacotron-2_amd"), root, os.path.join(root, "tests")):
@@ -131,26 +131,27 @@ def _e2e_worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        ids, lens, re, rs = tacotron_inputs(5, 9, 4, seed=21)
+        ids, lens, re, rs = tacotron_inputs(B, 9, 4, seed=21)
         got = synthesize_sharded(_StubTTS(), ids, lens, re, rs)
         np.savez(os.path.join(out_dir, "r{}.npz".format(rank)), *got)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_sharded_e2e_gathers_in_global_order(tmp_path, world):
+@pytest.mark.parametrize("world,B", [(2, 5), (3, 5), (8, 8)])
+def test_gloo_sharded_e2e_gathers_in_global_order(tmp_path, world, B):
     """tt2.e2e.synthesize_sharded: every rank ends with the trimmed waveforms of ALL utterances in
-    global order (ragged lengths, uneven shards: 5 utterances over 2 or 3 ranks)."""
+    global order (ragged lengths, uneven shards: 5 utterances over 2 or 3 ranks; configs[3]'s shape,
+    8 utterances over 8 ranks, one per rank)."""
     from tt2.synthetic import tacotron_inputs
-    mp.start_processes(_e2e_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+    mp.start_processes(_e2e_worker, args=(world, _free_port(), str(tmp_path), B), nprocs=world,
                        join=True, start_method="spawn")
-    ids, lens, re, rs = tacotron_inputs(5, 9, 4, seed=21)
+    ids, lens, re, rs = tacotron_inputs(B, 9, 4, seed=21)
     ref = _StubTTS().synthesize(ids, lens, re, rs)["wavs"]
     for r in range(world):
         with np.load(str(tmp_path / "r{}.npz".format(r)), allow_pickle=False) as z:
             got = [z["arr_{}".format(i)] for i in range(len(z.files))]
-        assert len(got) == 5
+        assert len(got) == B
         for g, w in zip(got, ref):
             np.testing.assert_array_equal(g, w)
 

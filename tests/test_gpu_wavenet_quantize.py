@@ -195,3 +195,26 @@ def test_synthesizer_debug_wavs_teacher_force(tmp_path):
     out = eng.generate(cond, um, ul, 0, wav[None])
     eng.close()
     np.testing.assert_array_equal(got[0], out["y"][0])
+
+
+def test_quantize_teacher_classes_validated():
+    """a 'mulaw-quantize' teacher class outside [0, Q) (or not an integer) is refused on
+    the host instead of indexing past the first conv's rows on the next sample."""
+    from tt2._lib import TT2Error
+    from tt2.weights import init_wavenet_weights
+    hp = _quant_hp(6, 2)
+    W = init_wavenet_weights(hp, seed=5339)
+    B, T = 1, 275
+    cond = WR.interp_condition(np.zeros((B, 1, 80), np.float32))
+    _, ul = mol_uniforms(T, B, seed=4)
+    eng = _eng(hp, W, B, T)
+    try:
+        for bad in (256.0, -1.0, 3.5):
+            teacher = np.full((B, T), 7.0, np.float32)
+            teacher[0, 100] = bad
+            with pytest.raises(TT2Error, match="integer classes"):
+                eng.generate(cond, None, ul, 0, teacher)
+        out = eng.generate(cond, None, ul, 0, np.full((B, T), 255.0, np.float32))
+        assert out["k"].shape == (B, T)
+    finally:
+        eng.close()
