@@ -26,6 +26,7 @@
 #include "common.h"
 #include "gemm.h"
 #include "train_front.h"
+#include "train_bwd_persist.h"
 #include "train_persist.h"
 
 namespace tt2 {
@@ -129,6 +130,10 @@ struct tt2_train_ctx {
   // buffers, energy granules, flags + control words, the prenet rows in bf16 fragment layout
   DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps, tpKWT;
   bool tp_on = false, tp_last = false, tp_check = false;
+  // persistent backward (train_bwd_persist.hip): exchange buffers, flags + control words
+  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl;
+  bool tb_on = false, tb_last = false, tb_check = false;
+  int* tb_ctl_dev = nullptr;
   int* tp_ctl_dev = nullptr;  // control words of the last persistent forward (device)
   int* tp_ctl_host = nullptr;  // pinned [2]: the launch's control words, checked at the next read-back
 };
@@ -2404,8 +2409,10 @@ __global__ void k_pn_moving(float* __restrict__ mm, float* __restrict__ mv, cons
 // timed out in a hand-off or did not run every step (its control words), else 0.  It rides in the
 // data-parallel tower mean with the gradients, so k_tr_adam / k_pn_moving on every rank skip an
 // update that any rank's failed forward would have corrupted; tt2_train_losses then reports it.
-__global__ void k_tr_status(const int* __restrict__ ctl, int T, float* __restrict__ status) {
-  if (threadIdx.x == 0) status[0] = (ctl && (ctl[0] != 0 || ctl[1] != T)) ? 1.f : 0.f;
+__global__ void k_tr_status(const int* __restrict__ ctl, const int* __restrict__ ctl_bwd, int T,
+                            float* __restrict__ status) {
+  if (threadIdx.x == 0)
+    status[0] = ((ctl && (ctl[0] != 0 || ctl[1] != T)) || (ctl_bwd && (ctl_bwd[0] != 0 || ctl_bwd[1] != T))) ? 1.f : 0.f;
 }
 
 // ---- host orchestration ----------------------------------------------------------------------
@@ -2946,18 +2953,87 @@ static void tr_persist_forward(tt2_train_ctx* c, const TrAtt& at, const uint8_t*
 // Control words of the last persistent forward (after the stream has passed it): a timed-out
 // hand-off or a launch that did not run every step fails the read-back that follows the step.
 static void tr_persist_check(tt2_train_ctx* c) {
-  if (!c->tp_check) return;
+  if (!c->tp_check && !c->tb_check) return;
   TT2_HIP(hipStreamSynchronize(c->last_stream));
-  c->tp_check = false;
-  const int ph = c->tp_ctl_host[0], steps = c->tp_ctl_host[1];
-  TT2_CHECK(ph == 0, TT2_ERR_HIP,
-            "persistent training forward: a hand-off wait timed out (phase " + std::to_string(ph - 1) +
-                "); TT2_TR_PERSIST=0 runs the per-step launches");
-  TT2_CHECK(steps == c->T_last, TT2_ERR_STATE, "persistent training forward did not complete every step");
+  const bool fwd = c->tp_check, bwd = c->tb_check;
+  c->tp_check = c->tb_check = false;
+  if (fwd) {
+    const int ph = c->tp_ctl_host[0], steps = c->tp_ctl_host[1];
+    TT2_CHECK(ph == 0, TT2_ERR_HIP,
+              "persistent training forward: a hand-off wait timed out (phase " + std::to_string(ph - 1) +
+                  "); TT2_TR_PERSIST=0 runs the per-step launches");
+    TT2_CHECK(steps == c->T_last, TT2_ERR_STATE, "persistent training forward did not complete every step");
+  }
+  if (bwd) {
+    const int ph = c->tp_ctl_host[2], steps = c->tp_ctl_host[3];
+    TT2_CHECK(ph == 0, TT2_ERR_HIP,
+              "persistent training backward: a hand-off wait timed out (phase " + std::to_string(ph - 1) +
+                  "); TT2_TR_PERSIST_BWD=0 runs the per-step launches");
+    TT2_CHECK(steps == c->T_last, TT2_ERR_STATE, "persistent training backward did not complete every step");
+  }
+}
+
+// Persistent backward of the decoder loop (train_bwd_persist.hip): the fork geometry of the
+// persistent forward, bf16 fused step, every step teacher-forced, softmax attention
+static void tr_persist_backward(tt2_train_ctx* c, const TrAtt& at, const uint8_t* zm, int Tin, int T, int NT,
+                                hipStream_t s) {
+  const int B = c->B;
+  auto grow = [](DevBuf& d, size_t n) {
+    if (d.bytes < n) d.alloc(n);
+  };
+  const size_t xg = 2ul * 64 * 4 * TP_H * sizeof(__bf16);
+  grow(c->tbG1X, xg);
+  grow(c->tbG2X, xg);
+  grow(c->tbP1X, 2ul * TB_NKB * 64 * TB_NOUT * sizeof(float));
+  grow(c->tbP2X, 2ul * TB_NKB * 64 * TB_NOUT * sizeof(float));
+  grow(c->tbQX, 2ul * 4 * 64 * TP_H * sizeof(float));
+  grow(c->tpEX, 2ul * 64 * 4 * TP_TMAX * sizeof(unsigned long long));
+  grow(c->tbCtl, sizeof(unsigned) * ((size_t)TB_NPH * TP_NREP * TP_NB + 16));
+  if (!c->tp_ctl_host) TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->tp_ctl_host), 4 * sizeof(int)));
+  // rows >= B of the dG exchange rows stay zero (A-operand padding); tags restart at 1 every launch
+  for (DevBuf* d : {&c->tbG1X, &c->tbG2X, &c->tpEX, &c->tbCtl}) TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+  TT2_HIP(hipMemsetAsync(c->DWGP.p, 0, c->DWGP.bytes, s));
+  TbArgs a{};
+  a.B = B; a.T = T; a.Tin = Tin; a.NT = NT; a.z = c->cfg.zoneout;
+  a.K1T = c->hK1T.as<__bf16>(); a.K2T = c->hK2T.as<__bf16>(); a.Wq = c->hWq.as<__bf16>();
+  a.va = at.va; a.KWT = c->tpKWT.as<float>(); a.values16 = at.values16; a.lens = at.lens; a.zm = zm;
+  a.ALN = at.ALN; a.CUM = at.CUM; a.TH = at.TH;
+  a.G1 = c->G1.as<float>(); a.G2 = c->G2.as<float>(); a.CN1 = c->CN1.as<float>(); a.CN2 = c->CN2.as<float>();
+  a.C1 = c->C1.as<float>(); a.C2 = c->C2.as<float>(); a.dPIN = c->dPIN.as<float>();
+  a.dG1 = c->dG1.as<float>(); a.dG2 = c->dG2.as<float>(); a.DQ = c->DQ.as<float>(); a.DCTX = c->DCTX.as<float>();
+  a.DKEYS = c->DKEYS.as<float>(); a.dV = c->dV.as<float>(); a.dBA = c->dBA.as<float>(); a.DWGP = c->DWGP.as<float>();
+  a.G1X = c->tbG1X.as<__bf16>(); a.G2X = c->tbG2X.as<__bf16>(); a.P1X = c->tbP1X.as<float>();
+  a.P2X = c->tbP2X.as<float>(); a.QX = c->tbQX.as<float>(); a.EX = c->tpEX.as<unsigned long long>();
+  a.flags = c->tbCtl.as<unsigned>();
+  a.ctl = reinterpret_cast<int*>(a.flags + (size_t)TB_NPH * TP_NREP * TP_NB);
+  // TT2_TB_STAMP=<step>: stage stamps of that step -> TT2_TB_STAMP_FILE (int64 [256][32], diagnostic)
+  const char* st = std::getenv("TT2_TB_STAMP");
+  a.stamp_step = st ? std::atoi(st) : -1;
+  a.stamps = nullptr;
+  if (st) {
+    grow(c->tpStamps, sizeof(long long) * TP_NB * 32);
+    TT2_HIP(hipMemsetAsync(c->tpStamps.p, 0, c->tpStamps.bytes, s));
+    a.stamps = c->tpStamps.as<long long>();
+  }
+  tb_launch(a, s);
+  c->tb_ctl_dev = a.ctl;
+  if (st) {
+    std::vector<long long> h((size_t)TP_NB * 32);
+    TT2_HIP(hipMemcpyAsync(h.data(), a.stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, s));
+    TT2_HIP(hipStreamSynchronize(s));
+    const char* fn = std::getenv("TT2_TB_STAMP_FILE");
+    if (FILE* f = std::fopen(fn ? fn : "tb_stamps.bin", "wb")) {
+      std::fwrite(h.data(), sizeof(long long), h.size(), f);
+      std::fclose(f);
+    }
+  }
+  TT2_HIP(hipMemcpyAsync(c->tp_ctl_host + 2, a.ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+  c->tb_check = true;
 }
 
 static void tr_write_status(tt2_train_ctx* c, hipStream_t s) {
-  hipLaunchKernelGGL(k_tr_status, dim3(1), dim3(64), 0, s, c->tp_last ? c->tp_ctl_dev : nullptr, c->T_last,
+  hipLaunchKernelGGL(k_tr_status, dim3(1), dim3(64), 0, s, c->tp_last ? c->tp_ctl_dev : nullptr,
+                     c->tb_last ? c->tb_ctl_dev : nullptr, c->T_last,
                      c->grads + c->total);
 }
 
@@ -3216,7 +3292,15 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     TT2_HIP(hipMemsetAsync(c->tpStamps.p, 0, c->tpStamps.bytes, s));
     at.stamps = c->tpStamps.as<long long>();
   }
-  for (int t = T - 1; t >= 0; --t) {
+  // the whole reverse loop as one persistent launch when the forward ran persistent (same geometry)
+  const bool tb_run = c->tb_on && fused && tr_persist_fits(c, Tin, free_run, at.values16 != nullptr);
+  c->tb_last = tb_run;
+  if (tb_run) {
+    tr_persist_backward(c, at, zm, Tin, T, NT, s);
+    // the prenet columns of d X1 (off the recurrence): one product over all T·B rows
+    tr_gemm((int)TB, P, 4 * H, c->dG1.as<float>(), 4 * H, c->K1T.as<float>(), LX1, dX1, LX1, s);
+  }
+  for (int t = tb_run ? -1 : T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
     at.t = t;
     // (d align from the bf16 values copy measured 28.3 against 18.7 us per launch: hipcc waits
@@ -3312,7 +3396,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     }
   }
 
-  if (att_q)  // d query of step 0 (the later steps' sums were written by the launch after them)
+  if (att_q && !tb_run)  // d query of step 0 (the later steps' sums were written by the launch after them)
     hipLaunchKernelGGL(k_tr_dq_sum, dim3(B), dim3(128), 0, s, c->PQ2.as<float>(), NT, nq, A, c->DQ.as<float>());
   if (at.stamps) {
     std::vector<long long> h((size_t)B * 64);
@@ -3360,7 +3444,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     // and never more than TBUF holds (small T·B configurations have a small TBUF)
     const long cap = (long)(c->TBUF.bytes / sizeof(float)) / ((long)F * A);
     const long cap32 = (long)(c->TBUF.bytes / sizeof(float)) / (32L * A);
-    if (att_q) {  // k_tr_att_bwd_q accumulated G per (row, range) slot; row 31 = Σ du = d b_a (just summed)
+    if (att_q || tb_run) {  // G per (row, range) slot (k_tr_att_bwd_q / the persistent backward); row 31 = Σ du = d b_a
       tr_colsum(c, c->DWGP.as<float>(), BNT, 32 * A, 32L * A, c->DWG.as<float>(), s);
       TT2_HIP(hipMemcpyAsync(c->DWG.as<float>() + 31L * A, gvar(c, LAV("attention_bias")), sizeof(float) * (size_t)A,
                              hipMemcpyDeviceToDevice, s));
@@ -3393,9 +3477,15 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
       tr_gemm(F, A, (int)R, TBUF, R, c->TH.as<float>(), A, gvar(c, LAV("location_features_layer/kernel")), A, s);
     }
   }
-  tr_colsum(c, c->dKC.as<float>(), BNT, KW * F, (long)KW * F,
-            gvar(c, LAV("location_features_convolution/kernel")), s);
-  tr_colsum(c, c->dBC.as<float>(), BNT, F, F, gvar(c, LAV("location_features_convolution/bias")), s);
+  if (tb_run) {  // d Kc, d bc from the summed G (train_bwd_persist.h)
+    tb_loc_grads(c->DWG.as<float>(), pvar(c, LAV("location_features_layer/kernel")), F, A, KW,
+                 gvar(c, LAV("location_features_convolution/kernel")), gvar(c, LAV("location_features_convolution/bias")),
+                 s);
+  } else {
+    tr_colsum(c, c->dKC.as<float>(), BNT, KW * F, (long)KW * F,
+              gvar(c, LAV("location_features_convolution/kernel")), s);
+    tr_colsum(c, c->dBC.as<float>(), BNT, F, F, gvar(c, LAV("location_features_convolution/bias")), s);
+  }
   // memory: d values = Σ_t align_t^T · dctx_t (+ keys path), memory_layer kernel
   for (int b = 0; b < B; ++b)
     tr_gemm(Tin, D, T, c->ALIGN.as<float>() + (long)b * Tin * T, T, c->DCTX.as<float>() + (long)b * D, (long)B * D,
@@ -4413,6 +4503,9 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
     {
       const char* e = std::getenv("TT2_TR_PERSIST");
       c->tp_on = !(e && e[0] == '0') && tp_device_ok(hip_device);
+      // TT2_TR_PERSIST_BWD=1 runs the persistent backward (default off until it beats the launches)
+      const char* eb = std::getenv("TT2_TR_PERSIST_BWD");
+      c->tb_on = eb && eb[0] == '1' && tb_device_ok(hip_device);
     }
     try {
       c->dev = hip_device;
@@ -4654,6 +4747,10 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
     }
     if (std::string(name) == "diag:persist") {  // 1 when the last forward ran the persistent launch
       host[0] = c->tp_last ? 1.f : 0.f;
+      return;
+    }
+    if (std::string(name) == "diag:persist_bwd") {  // 1 when the last backward ran the persistent launch
+      host[0] = c->tb_last ? 1.f : 0.f;
       return;
     }
     if (std::string(name) == "memory") {  // d loss / d memory of the last forward_backward

@@ -1,0 +1,67 @@
+// Persistent BPTT backward of the teacher-forced decoder in the training step (configs[4]; VERDICT
+// r05 item 2): the reverse walk over the decoder steps that train.hip otherwise runs as four launches
+// per step (k_tr_att_bwd_q + k_tr_fused<TF_BWD_H / TF_BWD_S / TF_PLAIN>) as ONE cooperative launch of
+// 256 work-groups with the bf16 LSTM weights, the row's bf16 values quarter and the query columns
+// resident on chip (helpers.py:62-133 and Architecture_wrappers.py:197-267 differentiated; the
+// gradients tacotron.py:1194-1225 feeds to the optimizer).  It writes exactly what the per-step loop
+// leaves for the weight-gradient products after the loop: dG1 / dG2 [T][B][4H], DQ [T][B][A],
+// DCTX [T][B][D], DKEYS, the d v_a / d b_a partials and the d W_loc accumulators (DWGP); the prenet
+// columns of d X1 come from one product after the launch.
+#pragma once
+#include <cstdint>
+
+#include "train_persist.h"
+
+namespace tt2 {
+
+constexpr int TB_NKB = 16;  // K-blocks of the gate columns: units [64 kb, 64 kb + 64) x 4 gates
+constexpr int TB_NNB = 16;  // N-blocks of the 2048 outputs of each backward product (128 each)
+constexpr int TB_NPH = 5;   // flag phases (P1, Q, G2, P2, G1)
+constexpr int TB_NOUT = 2 * TP_H;  // outputs of each product: [d h1 | d hz2] and [d ctx | d hz1]
+
+struct TbArgs {
+  int B, T, Tin, NT;         // NT: the per-row slot stride of dV / dBA / DWGP (train.hip's j-tiles)
+  float z;                   // zoneout rate (only without keep masks)
+  const __bf16* K1T;         // [4H][LX1] bf16 W1^T (hK1T)
+  const __bf16* K2T;         // [4H][2H]  bf16 W2^T (hK2T)
+  const __bf16* Wq;          // [H][A]    bf16 query_layer kernel (hWq)
+  const float* va;           // [A]
+  const float* KWT;          // [A][32] (tp_prepare): [a][tap] = (Kc·W_loc)[tap][a] for tap < KW
+  const __bf16* values16;    // [B][Tin][D] bf16
+  const int* lens;           // [B]
+  const uint8_t* zm;         // [T][4][B][H] zoneout keep bits or null
+  // forward slots (train.hip layout)
+  const float *ALN, *CUM, *TH, *G1, *G2, *CN1, *CN2, *C1, *C2;
+  const float* dPIN;         // [T][B][H + D] d [h2 | ctx] from the frame / stop projections
+  // outputs
+  float *dG1, *dG2;          // [T][B][4H]
+  float *DQ, *DCTX;          // [T][B][A], [T][B][D]
+  float* DKEYS;              // [B][Tin][A]
+  float *dV, *dBA;           // [B][NT][A]: slot b·NT holds row b's sums over steps and positions
+  float* DWGP;               // [B][NT][32][A]: slot b·NT, G[tap][a] = Σ_t,j cum_t[j + tap - 15]·du[j][a]
+  // exchange buffers
+  __bf16 *G1X, *G2X;         // [2 parities][64 x 4H] bf16 A-fragment layout in the tb_kperm column order
+  float *P1X, *P2X;          // [2][TB_NKB][64][TB_NOUT] per-K-block product partials
+  float* QX;                 // [2][4 quarters][64][H] d h2 partials through the quarter's query columns
+  unsigned long long* EX;    // [2][64][4][TP_TMAX] data-tagged d align partials
+  unsigned* flags;           // [TB_NPH][TP_NREP][TP_NB] step tags (zeroed before the launch)
+  int* ctl;                  // [0] = 1 + phase of a timed-out wait, [1] = steps completed
+  long long* stamps;         // [TP_NB][32] s_memrealtime stage stamps of step stamp_step (diagnostic) or null
+  int stamp_step;
+};
+
+// exchange column order of the dG rows: gate column q·H + u -> K-block u / 64 holds its 4 gates x 64
+// units contiguously, so one product work-group reads one contiguous K range
+__host__ __device__ inline int tb_kperm(int c) {
+  const int q = c / TP_H, u = c % TP_H;
+  return (u >> 6) * 256 + q * 64 + (u & 63);
+}
+
+size_t tb_lds_bytes();
+bool tb_device_ok(int dev);
+void tb_launch(const TbArgs& a, hipStream_t s);
+// d Kc / d bc from the summed d W_loc accumulators G [32][A] (row 31 = Σ du = d b_a):
+// dKc[tap][c] = Σ_a G[tap][a]·W_loc[c][a], dbc[c] = Σ_a G[31][a]·W_loc[c][a]
+void tb_loc_grads(const float* G, const float* Wl, int F, int A, int KW, float* dKc, float* dbc, hipStream_t s);
+
+}  // namespace tt2

@@ -1021,6 +1021,7 @@ def _trainer_run(hp, W, case, env, postnet=False):
             g = {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in TRN.train_var_names()}
             gmem = tr.get("memory", 1, mem.shape)
             persist = float(tr.get("diag:persist", 0, (1,))[0])
+            persist_bwd = float(tr.get("diag:persist_bwd", 0, (1,))[0])
         finally:
             tr.close()
     finally:
@@ -1029,7 +1030,7 @@ def _trainer_run(hp, W, case, env, postnet=False):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    return dict(L=L, fr=fr, sl=sl, al=al, g=g, gmem=gmem, persist=persist)
+    return dict(L=L, fr=fr, sl=sl, al=al, g=g, gmem=gmem, persist=persist, persist_bwd=persist_bwd)
 
 
 @pytest.mark.gpu
@@ -1235,3 +1236,55 @@ def test_gpu_train_configs4_trajectory_matches_oracle():
         for k, want in ref.items():
             assert abs(got[k] - want) <= tol * abs(want) + 1e-7, (step, k, got[k], want)
         assert abs(got["grad_norm"] - gn) < 1e-3 * gn, (step, got["grad_norm"], gn)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T_in,T_out,zmask", [(5, 7, 3, False), (16, 40, 24, True), (64, 150, 12, True),
+                                                 (64, 192, 6, True), (33, 129, 17, False)])
+def test_gpu_train_persistent_backward_matches_launch_loop(B, T_in, T_out, zmask):
+    """The persistent BPTT backward (train_bwd_persist.hip: one launch for the whole reverse decoder loop,
+    LSTM weight blocks and the values quarter resident) against the per-step backward launches
+    (TT2_TR_PERSIST_BWD=0), both after the persistent forward, fork widths, bf16 step, ragged lengths:
+    the same bf16 operand rounding, different fp32 summation orders (K-block partials, the d align
+    quarters, the location-conv backward folded through KW).  Every gradient within 1e-2 (Frobenius,
+    relative: the tolerance of the fused and persistent-forward A/B tests), losses identical."""
+    from tt2.hparams import hparams
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    W = init_tacotron_weights(hp, seed=5339)
+    mem, lens, tg, st = train_batch(B, T_in, T_out, memory_width(hp), seed=7)
+    pm = prenet_masks(T_out, B, hp.prenet_layers[0], seed=7)
+    zm = zoneout_masks(T_out, B, hp.decoder_lstm_units, seed=7) if zmask else None
+    case = (mem, lens, tg, st, pm, zm)
+    p = _trainer_run(hp, W, case, {"TT2_TR_PERSIST_BWD": "1"})
+    q = _trainer_run(hp, W, case, {"TT2_TR_PERSIST_BWD": "0"})
+    assert p["persist"] == 1.0 and q["persist"] == 1.0
+    assert p["persist_bwd"] == 1.0 and q["persist_bwd"] == 0.0
+    for k in ("before", "stop_token"):
+        assert p["L"][k] == q["L"][k], (k, p["L"][k], q["L"][k])
+    for n in list(p["g"]) + ["memory"]:
+        a, b = (p["gmem"], q["gmem"]) if n == "memory" else (p["g"][n], q["g"][n])
+        rel = float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+        print("  {:90s} rel {:.3e}".format(n, rel))
+        assert np.isfinite(a).all()
+        assert rel < 1e-2, (n, rel)
+
+
+@pytest.mark.gpu
+def test_gpu_train_persistent_backward_close_to_oracle():
+    """The persistent backward's bf16 step at the fork widths against the float64 oracle: the
+    mixed-precision tolerance of test_gpu_train_persistent_forward_close_to_oracle."""
+    from tt2.hparams import hparams
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    B, T_in, T_out = 4, 37, 10
+    W, mem, lens, tg, st, pm, zm = _case(hp, B, T_in, T_out)
+    r = _trainer_run(hp, W, (mem, lens, tg, st, pm, zm), {"TT2_TR_PERSIST": "1", "TT2_TR_PERSIST_BWD": "1"})
+    assert r["persist"] == 1.0 and r["persist_bwd"] == 1.0
+    out, (b, s, _), g = TRN.train_grads(W, mem, lens, tg, st, pm, zm, hp.tacotron_reg_weight, clip=_clip(hp))
+    assert abs(r["L"]["before"] - b) < 1e-3 * b
+    for n in TRN.train_var_names() + ["memory"]:
+        got, want = (r["gmem"], g["memory"]) if n == "memory" else (r["g"][n], g[n])
+        frob = float(np.linalg.norm(got - want) / max(np.linalg.norm(want), 1e-30))
+        print("  {:90s} frob {:.3e}".format(n, frob))
+        assert frob < (0.1 if "prenet" in n else 1e-2), (n, frob)
