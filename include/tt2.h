@@ -82,8 +82,10 @@ typedef struct tt2_config {
   float lower_bound_decay; /* 0.1 */
   int symmetric_mels;      /* 1 */
   int clip_outputs;        /* 1 */
-  int stop_at_any;         /* 0 (fork) / 1 (paper); 2 = never stop before max_iters (the row chunks of a
-                            * batch > 32, whose one stop step the host takes over all chunks) */
+  int stop_at_any;         /* 0 (fork) / 1 (paper): identical at r = 1 -- every row's round(stop) == 1
+                            * (helpers.py:40-54 reduce the batch axis of the [B, r] flags first, then
+                            * any / all over the r frames); 2 = never stop before max_iters (the row
+                            * chunks of a batch > 32, whose one stop step the host takes over all chunks) */
   int mask_encoder;        /* 1 */
   int cumulative_weights;  /* 1 */
   int synthesis_constraint;/* args.synth_constraint (attention.py:166, tacotron.py:315) */

@@ -187,7 +187,7 @@ def synthesize(ids, lengths, ref_emt, ref_spk, W, hp, attn, emt_ref_gru, prenet_
             frame_in = np.asarray(targets[:, t], dt)
             continue
         fin = np.round(stop) == 1.0
-        if bool(np.any(fin)) if hp.get("stop_at_any", False) else bool(np.all(fin)):
+        if bool(np.all(fin)):  # helpers.py:40-54: batch axis reduced first (stop_at_any: r frames, r = 1)
             break
         frame_in = frame
     frames = np.stack(frames, 1)

@@ -382,8 +382,9 @@ def dynamic_decode(keys, values, lengths, W, hp, prenet_masks, max_iters, target
     when ``targets`` is given, the GTA TacoTrainingHelper with ratio 1 (helpers.py:62-133).
 
     The loop emits every step including the stopping one; it ends when every batch row's
-    round(stop) == 1 at the same step (stop_at_any=False → reduce_all; r=1) or time+1 ≥ max_iters
-    (or, GTA, time+1 ≥ T_targets).  Returns frames [B,T,80], stop [B,T], alignments [B,T_in,T]."""
+    round(stop) == 1 at the same step or time+1 ≥ max_iters (or, GTA, time+1 ≥ T_targets).
+    stop_at_any has no effect at r = 1: helpers.py:40-54 reduce_all over the batch axis of the
+    [B, r] finished flags first, then any (stop_at_any) / all over the r frames.  Returns frames [B,T,80], stop [B,T], alignments [B,T_in,T]."""
     B, T_in, D = values.shape
     units = W[P + "decoder/decoder_LSTM/multi_rnn_cell/cell_0/lstm_cell/bias"].shape[0] // 4
     st = DecoderState(B, T_in, D, units, dt)
@@ -401,7 +402,7 @@ def dynamic_decode(keys, values, lengths, W, hp, prenet_masks, max_iters, target
             frame_in = np.asarray(targets[:, t], dt)                    # helpers.py:126-129
             continue
         fin = np.round(stop) == 1.0                                      # helpers.py:40
-        done = bool(np.any(fin)) if hp.get("stop_at_any", False) else bool(np.all(fin))
+        done = bool(np.all(fin))                                         # reduce_all(axis=0), r = 1
         if done:
             break
         frame_in = frame                                                 # helpers.py:57

@@ -769,10 +769,11 @@ tt2_status tt2_decode(tt2_ctx* c, int max_iters, const uint8_t* prenet_masks, ui
           std::memcpy(&fin[(size_t)b * nm], &targets[((size_t)b * T_targets + t) * nm], sizeof(float) * nm);
         continue;
       }
-      // TacoTestHelper stop rule (helpers.py:36-59): round(stop) == 1 for all (or any) rows
+      // TacoTestHelper stop rule (helpers.py:36-59): round(stop) == 1 for every row.  stop_at_any picks
+      // any / all over the r frames of a step AFTER reduce_all over the batch axis: no effect at r = 1
       int fin_rows = 0;
       for (int b = 0; b < B; ++b) fin_rows += std::nearbyint(sp[b]) == 1.f;
-      if (c->cfg.stop_at_any == 2 ? false : c->cfg.stop_at_any ? fin_rows > 0 : fin_rows == B) {
+      if (c->cfg.stop_at_any == 2 ? false : fin_rows == B) {
         ++t;
         break;
       }

@@ -618,7 +618,9 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
       }
       if (t > 0 && w == 0) {
         // stop rule of step t-1 (TacoTestHelper.next_inputs, helpers.py:40-59 + dynamic_decode):
-        // every valid row rounds to 1 (stop_at_any: any row); GTA stops at T_targets instead
+        // every valid row rounds to 1; GTA stops at T_targets instead.  stop_at_any does not change it at
+        // r = 1: TacoTestHelper reduces the batch axis first (reduce_all(finished, axis=0) over [B, r],
+        // helpers.py:40-54), then any / all over the r frames of the step
         int dn;
         if (a.T_lim > 0) {
           dn = t >= a.T_lim;
@@ -627,7 +629,7 @@ __global__ __launch_bounds__(PD_NT) void k_decode_persist(PdArgs a) {
           const bool v0 = lane < 16 && r0 < a.B, v1 = lane < 16 && r0 + 16 < a.B;
           const unsigned long long f0 = __ballot(v0 && sb[0]), f1 = __ballot(v1 && sb[1]);
           const unsigned long long m0 = __ballot(v0), m1 = __ballot(v1);
-          dn = a.stop_at_any == 2 ? 0 : a.stop_at_any ? ((f0 | f1) != 0ull) : (f0 == m0 && f1 == m1);
+          dn = a.stop_at_any == 2 ? 0 : (f0 == m0 && f1 == m1);
         }
         if (lane == 0 && dn) atomicMax(si + 1, 1);
       }

@@ -982,7 +982,9 @@ __global__ __launch_bounds__(256) void k_proj(ProjArgs a, SideJob sj, int t) {
     const bool f = valid && rintf(sv) == 1.0f;
     const unsigned long long fb = __ballot(f), vb = __ballot(valid);
     if (valid) a.stop[(long)lane * a.max_iters + t] = sv;
-    int dn = a.stop_at_any == 2 ? 0 : a.stop_at_any ? (fb != 0ull) : (fb == vb);
+    // every valid row rounds to 1, whatever stop_at_any: at r = 1 TacoTestHelper's reduce_all over the
+    // batch axis (helpers.py:40-54) comes before the any / all over the step's r frames
+    int dn = a.stop_at_any == 2 ? 0 : (fb == vb);
     if (a.T_lim > 0) dn = t + 1 >= a.T_lim;  // TacoTrainingHelper: time + 1 >= T_targets
     if (t + 1 >= a.max_iters) dn = 1;         // dynamic_decode maximum_iterations
     if (lane == 0 && dn) {

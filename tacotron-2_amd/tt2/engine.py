@@ -99,11 +99,13 @@ def chunk_ranges(B, cap=MAX_CONTEXT_BATCH):
 
 def global_stop_steps(stop, stop_at_any):
     """dynamic_decode's batch-level stop over the whole tower (TacoTestHelper, helpers.py:40-54):
-    the first step at which every row's stop probability rounds to 1 (stop_at_any: any row),
-    round half to even as tf.round; the step is emitted, so the decode keeps step + 1 frames.
-    stop [B, n] -> n_steps (n when the rule never fires)."""
+    the first step at which every row's stop probability rounds to 1 (round half to even as
+    tf.round); the step is emitted, so the decode keeps step + 1 frames.  stop_at_any has no effect
+    at r = 1: the helper's reduce_all over the batch axis of the [B, r] flags comes first, then
+    any (stop_at_any) / all over the step's r frames.  stop [B, n] -> n_steps (n when the rule never
+    fires)."""
     fin = np.rint(np.asarray(stop, np.float32)) == 1.0
-    cond = fin.any(axis=0) if stop_at_any else fin.all(axis=0)
+    cond = fin.all(axis=0)
     return int(np.argmax(cond)) + 1 if cond.any() else fin.shape[1]
 
 

@@ -282,7 +282,8 @@ def test_smoothing_normalization_matches_oracle(cpu, constraint):
 
 def test_chunk_ranges_and_global_stop():
     """Row chunks of a tower above one context's 32 rows, and the tower-level stop step
-    (TacoTestHelper, helpers.py:40-54: all rows' rounded stop tokens, or any with stop_at_any)."""
+    (TacoTestHelper, helpers.py:40-54: every row's rounded stop token; stop_at_any reduces over the r
+    frames of a step AFTER the batch axis, so at r = 1 it changes nothing)."""
     from tt2.engine import chunk_ranges, global_stop_steps
     assert chunk_ranges(32) == [(0, 32)]
     assert chunk_ranges(33) == [(0, 17), (17, 33)]
@@ -290,21 +291,22 @@ def test_chunk_ranges_and_global_stop():
     assert chunk_ranges(65) == [(0, 22), (22, 44), (44, 65)]
     st = np.full((4, 9), 0.2, np.float32)
     assert global_stop_steps(st, False) == 9 and global_stop_steps(st, True) == 9
-    st[1, 3] = 0.9                       # one row only: the any-rule fires at step 3
-    assert global_stop_steps(st, True) == 4 and global_stop_steps(st, False) == 9
+    st[1, 3] = 0.9                       # one row only: no stop, with or without stop_at_any
+    assert global_stop_steps(st, True) == 9 and global_stop_steps(st, False) == 9
     st[:, 6] = 0.75
-    assert global_stop_steps(st, False) == 7
+    assert global_stop_steps(st, False) == 7 and global_stop_steps(st, True) == 7
     st[:, 5] = 0.5                       # tf.round: half to even -> 0, no stop at step 5
     assert global_stop_steps(st, False) == 7
 
 
-@pytest.mark.parametrize("stop_at_any,bias,scale,steps", [(False, -6.0, 1, 12), (True, -3.0, 30, 3),
-                                                         (False, 4.0, 1, 1)])
+@pytest.mark.parametrize("stop_at_any,bias,scale,steps", [(False, -6.0, 1, 12), (True, -3.0, 30, 12),
+                                                         (False, 4.0, 1, 1), (True, 4.0, 1, 1)])
 def test_chunked_tower_matches_oracle(cpu, stop_at_any, bias, scale, steps):
     """A 40-row tower (two 20-row contexts, no stop rule of their own) against one oracle decode
     of all 40 rows: frames, alignments and the tower's stop step.  The stop
-    projection is biased / scaled so the rule never fires, fires mid-run on a few rows (any), or
-    fires on every row at the first step (all)."""
+    projection is biased / scaled so the rule never fires, fires mid-run on a few rows only (no stop:
+    every row must round to 1, stop_at_any or not -- helpers.py:40-54 at r = 1), or fires on every
+    row at the first step."""
     from tt2.engine import TacotronEngine
     from _common import STOP_BIAS
     hp = small_hparams()

@@ -589,7 +589,8 @@ def test_smoothing_normalization(widths):
     eng.close()
 
 
-@pytest.mark.parametrize("stop_at_any,bias,scale,steps", [(False, -6.0, 1, 14), (True, -3.0, 30, None)])
+@pytest.mark.parametrize("stop_at_any,bias,scale,steps", [(False, -6.0, 1, 14), (True, -3.0, 30, 14),
+                                                         (True, 4.0, 1, 1)])
 def test_chunked_tower_b48_matches_oracle(stop_at_any, bias, scale, steps):
     """A 48-row tower (two 24-row contexts decoding without their own stop rule, the tower's stop
     step taken over all rows afterwards) against one oracle decode of all 48 rows (VERDICT r04
