@@ -131,7 +131,7 @@ struct tt2_train_ctx {
   DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps, tpKWT;
   bool tp_on = false, tp_last = false, tp_check = false;
   // persistent backward (train_bwd_persist.hip): exchange buffers, flags + control words
-  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl;
+  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl, tbW1F;
   bool tb_on = false, tb_last = false, tb_check = false;
   int* tb_ctl_dev = nullptr;
   int* tp_ctl_dev = nullptr;  // control words of the last persistent forward (device)
@@ -2986,12 +2986,13 @@ static void tr_persist_backward(tt2_train_ctx* c, const TrAtt& at, const uint8_t
   grow(c->tbG2X, xg);
   grow(c->tbP1X, 2ul * TB_NKB * 64 * TB_NOUT * sizeof(float));
   grow(c->tbP2X, 2ul * TB_NKB * 64 * TB_NOUT * sizeof(float));
-  grow(c->tbQX, 2ul * 4 * 64 * TP_H * sizeof(float));
+  grow(c->tbQX, 2ul * 64 * TP_A * sizeof(__bf16));
+  grow(c->tbW1F, (size_t)TP_NB * 4 * 16 * 64 * 8 * sizeof(__bf16));
   grow(c->tpEX, 2ul * 64 * 4 * TP_TMAX * sizeof(unsigned long long));
   grow(c->tbCtl, sizeof(unsigned) * ((size_t)TB_NPH * TP_NREP * TP_NB + 16));
   if (!c->tp_ctl_host) TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->tp_ctl_host), 4 * sizeof(int)));
   // rows >= B of the dG exchange rows stay zero (A-operand padding); tags restart at 1 every launch
-  for (DevBuf* d : {&c->tbG1X, &c->tbG2X, &c->tpEX, &c->tbCtl}) TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+  for (DevBuf* d : {&c->tbG1X, &c->tbG2X, &c->tbQX, &c->tpEX, &c->tbCtl}) TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
   TT2_HIP(hipMemsetAsync(c->DWGP.p, 0, c->DWGP.bytes, s));
   TbArgs a{};
   a.B = B; a.T = T; a.Tin = Tin; a.NT = NT; a.z = c->cfg.zoneout;
@@ -3003,7 +3004,8 @@ static void tr_persist_backward(tt2_train_ctx* c, const TrAtt& at, const uint8_t
   a.dG1 = c->dG1.as<float>(); a.dG2 = c->dG2.as<float>(); a.DQ = c->DQ.as<float>(); a.DCTX = c->DCTX.as<float>();
   a.DKEYS = c->DKEYS.as<float>(); a.dV = c->dV.as<float>(); a.dBA = c->dBA.as<float>(); a.DWGP = c->DWGP.as<float>();
   a.G1X = c->tbG1X.as<__bf16>(); a.G2X = c->tbG2X.as<__bf16>(); a.P1X = c->tbP1X.as<float>();
-  a.P2X = c->tbP2X.as<float>(); a.QX = c->tbQX.as<float>(); a.EX = c->tpEX.as<unsigned long long>();
+  a.P2X = c->tbP2X.as<float>(); a.DQX = c->tbQX.as<__bf16>(); a.EX = c->tpEX.as<unsigned long long>();
+  a.W1F = c->tbW1F.as<__bf16>();
   a.flags = c->tbCtl.as<unsigned>();
   a.ctl = reinterpret_cast<int*>(a.flags + (size_t)TB_NPH * TP_NREP * TP_NB);
   // TT2_TB_STAMP=<step>: stage stamps of that step -> TT2_TB_STAMP_FILE (int64 [256][32], diagnostic)
@@ -3293,7 +3295,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     at.stamps = c->tpStamps.as<long long>();
   }
   // the whole reverse loop as one persistent launch when the forward ran persistent (same geometry)
-  const bool tb_run = c->tb_on && fused && tr_persist_fits(c, Tin, free_run, at.values16 != nullptr);
+  const bool tb_run = c->tb_on && fused && Tin <= TB_TMAX && tr_persist_fits(c, Tin, free_run, at.values16 != nullptr);
   c->tb_last = tb_run;
   if (tb_run) {
     tr_persist_backward(c, at, zm, Tin, T, NT, s);
@@ -4503,9 +4505,9 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
     {
       const char* e = std::getenv("TT2_TR_PERSIST");
       c->tp_on = !(e && e[0] == '0') && tp_device_ok(hip_device);
-      // TT2_TR_PERSIST_BWD=1 runs the persistent backward (default off until it beats the launches)
+      // TT2_TR_PERSIST_BWD=0 runs the per-step backward launches instead of the persistent backward
       const char* eb = std::getenv("TT2_TR_PERSIST_BWD");
-      c->tb_on = eb && eb[0] == '1' && tb_device_ok(hip_device);
+      c->tb_on = !(eb && eb[0] == '0') && tb_device_ok(hip_device);
     }
     try {
       c->dev = hip_device;

@@ -18,6 +18,7 @@ constexpr int TB_NKB = 16;  // K-blocks of the gate columns: units [64 kb, 64 kb
 constexpr int TB_NNB = 16;  // N-blocks of the 2048 outputs of each backward product (128 each)
 constexpr int TB_NPH = 5;   // flag phases (P1, Q, G2, P2, G1)
 constexpr int TB_NOUT = 2 * TP_H;  // outputs of each product: [d h1 | d hz2] and [d ctx | d hz1]
+constexpr int TB_TMAX = 160;       // encoder positions: the row's bf16 values quarter lives in LDS (80 KB)
 
 struct TbArgs {
   int B, T, Tin, NT;         // NT: the per-row slot stride of dV / dBA / DWGP (train.hip's j-tiles)
@@ -41,8 +42,14 @@ struct TbArgs {
   float* DWGP;               // [B][NT][32][A]: slot b·NT, G[tap][a] = Σ_t,j cum_t[j + tap - 15]·du[j][a]
   // exchange buffers
   __bf16 *G1X, *G2X;         // [2 parities][64 x 4H] bf16 A-fragment layout in the tb_kperm column order
-  float *P1X, *P2X;          // [2][TB_NKB][64][TB_NOUT] per-K-block product partials
-  float* QX;                 // [2][4 quarters][64][H] d h2 partials through the quarter's query columns
+  float *P1X, *P2X;          // per-K-block product partials, 2 parities of 16 MB: the d ctx block of P1
+                             // (N-blocks < 8) row-major [kb][64][1024] in the first half (its reader takes
+                             // one row), every unit-consumed block unit-major [nb][32][kb][64][4] (tb_uoff)
+  __bf16* DQX;               // [2][64 x A] d query rows (bf16 A-fragment layout, K = A): each (row, quarter)
+                             // writes its 32 dims, the unit role forms d h2 = dq·Wq^T
+  __bf16* W1F;               // [TP_NB][4 waves][16 fragments][64 lanes][8] the W1 blocks, fragment-major
+                             // (written at the start of the launch, streamed from L2 by each step's d X1
+                             // product: one resident weight block per work-group fits the registers)
   unsigned long long* EX;    // [2][64][4][TP_TMAX] data-tagged d align partials
   unsigned* flags;           // [TB_NPH][TP_NREP][TP_NB] step tags (zeroed before the launch)
   int* ctl;                  // [0] = 1 + phase of a timed-out wait, [1] = steps completed

@@ -7,8 +7,8 @@
 //
 // Roles of work-group g (all 256 have all three):
 //   attention  row rb = g & 63, quarter s = g >> 6: context channels [256 s, 256 s + 256) (the bf16
-//              values quarter as MFMA A fragments in AGPRs) and attention dims [32 s, 32 s + 32)
-//              (th, du, d keys, the query columns of the d h2 product, the location-conv backward)
+//              values quarter as MFMA A fragments in LDS, 80 KB at TB_TMAX = 160 positions) and
+//              attention dims [32 s, 32 s + 32) (th, du, d keys, d query, the location-conv backward)
 //   unit       hidden units [4g, 4g + 4) of both layers, all 64 rows: the LSTM cell backward
 //              (k_tr_lstm_bwd's arithmetic), the carried d c and the zoneout residuals in registers
 //   product    K-block kb = g >> 4 (units [64 kb, 64 kb + 64) x 4 gates = 256 gate columns, the
@@ -21,14 +21,15 @@
 //        d align partial = values quarter · d ctx (hi / lo bf16 halves of d ctx: ~fp32 products) +
 //        this quarter's running d cum partial -> granules to the other 3 quarters; take and sum them in
 //        quarter order (identical in all four); softmax backward; du = de·v_a·(1 - th²) of the own dims;
-//        d query of the own dims (complete) -> DQ and d h2 partial = dq·Wq[:, own dims]^T -> QX
-//   CELL2  wait QX of every (row, quarter), d h2 = d PIN + Σ_s QX; d hz2 = Σ_kb P2_{t+1} + residual;
+//        d query of the own dims (complete) -> DQ and the bf16 dq exchange rows DQX
+//   CELL2  wait DQX of every (row, quarter), d h2 = d PIN + dq·Wq[own units]^T (one MFMA chain per
+//        wave); d hz2 = Σ_kb P2_{t+1} + residual;
 //        cell backward -> dG2 (fp32 slot + bf16 exchange)
 //   PROD2  wait the K-block's 16 unit producers, dG2 block · W2 block -> P2
 //   CELL1  wait P2 of the own N-block, d h1 = Σ_kb P2; d hz1 = Σ_kb P1_{t+1} + residual; cell
 //        backward -> dG1
 //   PROD1  wait the K-block's dG1, dG1 block · W1 block -> P1 (consumed at step t-1)
-// Off the chain, after QX is published: G[tap][a] += Σ_j cum_t[j + tap - 15]·du[j][a] (d W_loc, d Kc,
+// Off the chain, after DQX is published: G[tap][a] += Σ_j cum_t[j + tap - 15]·du[j][a] (d W_loc, d Kc,
 // d bc after the launch) and the location-conv backward into this quarter's d cum partial
 // (M = du·KW^T over the own dims, then the tap diagonals).
 // Exchange protocol as train_persist.hip: sc1 write-through stores, drained before one barrier and the
@@ -42,26 +43,35 @@ namespace tt2 {
 
 enum { TB_PH_P1 = 0, TB_PH_Q = 1, TB_PH_G2 = 2, TB_PH_P2 = 3, TB_PH_G1 = 4, TB_PH_E = 5 };
 constexpr int TB_NW = TP_NT / 64;        // waves
-constexpr int TB_TM = TP_TMAX;           // encoder positions (capacity)
+constexpr int TB_TM = TB_TMAX;           // encoder positions (capacity: the values quarter lives in LDS)
 constexpr int TB_NPT = TB_TM / 16;       // position tiles
-constexpr int TB_PTW = TB_NPT / TB_NW;   // position tiles per wave
+constexpr int TB_PTW = (TB_NPT + TB_NW - 1) / TB_NW;  // position tiles per wave (w + 4 r)
 constexpr int TB_K4 = 4 * TP_H;          // gate columns
-static_assert(TB_NPT % TB_NW == 0 && TP_NT == 256 && TP_A == 128 && TP_D == 1024 && TP_H == 1024,
+constexpr long TB_PSTRIDE = (long)TB_NNB * 32 * TB_NKB * 64 * 4;  // floats per parity of P1X / P2X
+static_assert(TB_TM % 16 == 0 && TB_TM <= TP_TMAX && TP_NT == 256 && TP_A == 128 && TP_D == 1024 && TP_H == 1024,
               "train_bwd_persist geometry");
 
-// LDS layout (floats)
-constexpr int TBL_DCTX = 0;                   // [256] d ctx of this quarter
-constexpr int TBL_EP = TBL_DCTX + 256;        // [TM] own d align partial
-constexpr int TBL_DA = TBL_EP + TB_TM;        // [TM] d align, then de
-constexpr int TBL_DS = TBL_DA + TB_TM;        // [TM] running d cum partial of the own dims
-constexpr int TBL_CUM = TBL_DS + TB_TM;       // [TM + 48] cum_t at +15, zero padded
-constexpr int TBL_DU = TBL_CUM + TB_TM + 48;  // [TM][33] du of the own dims
-constexpr int TBL_M = TBL_DU + TB_TM * 33;    // [TM][33] M[j][tap] = Σ_d du[j][d]·KW[d][tap]
-constexpr int TBL_RED = TBL_M + TB_TM * 33;   // [2][TB_NW][32] wave partials of dq / d v_a
+// LDS layout (floats).  The attention phase's du / M tiles and the products' staging share one
+// region (different phases of a step, separated by barriers).
+constexpr int TB_DUS = 34;                      // row stride of du (the G operand's column reads: 2 banks apart
+                                                // per 8 positions, conflict-free per half wave)
+constexpr int TB_OS = 132;                      // row stride of the staged product outputs
+constexpr int TBL_DCH = 0;                      // [512] bf16: split halves of d ctx, hi [0, 256) | lo [256, 512)
+constexpr int TBL_EP = TBL_DCH + 256;           // [TM] own d align partial
+constexpr int TBL_DA = TBL_EP + TB_TM;          // [TM] d align, then de
+constexpr int TBL_DS = TBL_DA + TB_TM;          // [TM] running d cum partial of the own dims
+constexpr int TBL_CUM = TBL_DS + TB_TM;         // [TM + 64] cum_t at +15, zero padded
+constexpr int TBL_RED = TBL_CUM + TB_TM + 64;   // [2][TB_NW][32] wave partials of dq / d v_a
 constexpr int TBL_DQ = TBL_RED + 2 * TB_NW * 32;  // [32] dq
-constexpr int TBL_SC = TBL_DQ + 32;           // [16] reduction scratch, then ints
-constexpr int TBL_WQ = TBL_SC + 32;           // [64 M-tiles][64 lanes] bf16 x 8: the own query columns
-constexpr int TBL_END = TBL_WQ + 64 * 64 * 4;
+constexpr int TBL_SC = TBL_DQ + 32;             // [16] reduction scratch, then ints
+constexpr int TBL_CELL = TBL_SC + 32;           // [17][256] the unit role's cell operands of the step
+constexpr int TBL_DU = TBL_CELL + 17 * 256;     // [TM][34] du of the own dims (kept to the end of the step)
+constexpr int TBL_U = TBL_DU + TB_TM * TB_DUS;  // union: M [TM][33] / PROD {A 32 KB, then out [64][132]}
+constexpr int TBL_U_SZ = (TB_TM * 33 > 64 * TB_OS) ? TB_TM * 33 : 64 * TB_OS;
+constexpr int TBL_VAL = TBL_U + TBL_U_SZ;       // [NPT tiles][8 k-steps][64 lanes] bf16 x 8: the values quarter
+constexpr int TBL_END = TBL_VAL + TB_NPT * 8 * 64 * 4;
+static_assert(TBL_U % 4 == 0 && TBL_VAL % 4 == 0 && TBL_DCH % 4 == 0 && 64 * TB_OS >= 8192,
+              "16-byte aligned LDS regions; the product staging fits the union");
 
 size_t tb_lds_bytes() { return sizeof(float) * (size_t)TBL_END; }
 
@@ -97,46 +107,71 @@ __device__ __forceinline__ tp_bf8 tb_bf8(const float (&x)[8]) {
   for (int e = 0; e < 8; ++e) v[e] = (__bf16)x[e];
   return v;
 }
+// split-bf16 halves of 8 floats: hi = bf16(x), lo = bf16(x - hi) (hi + lo within ~2^-17 of x)
+__device__ __forceinline__ void tb_split8(const float (&x)[8], tp_bf8& hi, tp_bf8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    hi[e] = (__bf16)x[e];
+    lo[e] = (__bf16)(x[e] - (float)hi[e]);
+  }
+}
+// a ≈ A·B in fp32 from split-bf16 operands: Ah·Bh + Ah·Bl + Al·Bh (the Al·Bl term is below 2^-16)
+__device__ __forceinline__ tp_f4 tb_mfma3(const tp_bf8& ah, const tp_bf8& al, const tp_bf8& bh, const tp_bf8& bl,
+                                          tp_f4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+}
+// byte offset of (N-block nb, unit group m4 = 4-output group inside the block, K-block kb, row, e) in the
+// unit-major partial layout [nb][m4][kb][row][4] (one parity): a unit work-group's 16 K-block partials of
+// its 4 units are one contiguous 16 KB run
+__device__ __forceinline__ int tb_uoff(int nb, int m4, int kb, int row, int e) {
+  return ((((nb * 32 + m4) * TB_NKB + kb) * 64 + row) * 4 + e) * 4;
+}
 __device__ __forceinline__ float tb_ld(const __amdgpu_buffer_rsrc_t rs, int byte_off) {  // sc1 dword load
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, byte_off, 0, 16));
 }
-__device__ __forceinline__ void tb_st(void* base, int byte_off, float v) {  // sc1 write-through dword store
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), tp_rsrc(base), byte_off, 0, 16);
+// plain dword load of a read-only slot: wave-uniform base + per-lane byte offset (buffer addressing
+// keeps the step loop free of per-lane 64-bit addresses, as train_persist.hip)
+__device__ __forceinline__ float tb_lg(const float* base, int byte_off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(tp_rsrc(base), byte_off, 0, 0));
 }
 
-// LSTM cell backward of one (row, unit) (k_tr_lstm_bwd / tf_cell_bwd): returns the 4 gate gradients,
-// updates the carried d(zoned c) and returns the zoneout residual (1 - kh)·dhz in *res
-struct TbCell {
-  float g[4];  // activated gates i, j, f, o
-  float cn, cp, kc, kh;
-};
-__device__ __forceinline__ void tb_cell_bwd(const TbCell& v, float dext, float dhz, float& dc, float& res, float (&d)[4]) {
-  const float si = v.g[0], tj = v.g[1], sf = v.g[2], so = v.g[3];
-  const float dhn = dext + v.kh * dhz;
-  const float tc = tanhf(v.cn);
-  const float dcn = v.kc * dc + dhn * so * (1.f - tc * tc);
-  const float dso = dhn * tc, dsf = dcn * v.cp, dsi = dcn * tj, dtj = dcn * si;
+// LSTM cell backward of one (row, unit) (k_tr_lstm_bwd / tf_cell_bwd): the 4 gate gradients, the
+// carried d(zoned c) updated, the zoneout residual (1 - kh)·dhz returned in res.  Operands: activated
+// gates i j f o, c_new, c_prev (zoned), keep bits kc / kh (or 1 - z)
+__device__ __forceinline__ void tb_cell_bwd(const float (&v)[8], float dext, float dhz, float& dc, float& res,
+                                            float (&d)[4]) {
+  const float si = v[0], tj = v[1], sf = v[2], so = v[3], cn = v[4], cp = v[5], kc = v[6], kh = v[7];
+  const float dhn = dext + kh * dhz;
+  const float tc = tanhf(cn);
+  const float dcn = kc * dc + dhn * so * (1.f - tc * tc);
+  const float dso = dhn * tc, dsf = dcn * cp, dsi = dcn * tj, dtj = dcn * si;
   d[0] = dsi * si * (1.f - si);
   d[1] = dtj * (1.f - tj * tj);
   d[2] = dsf * sf * (1.f - sf);
   d[3] = dso * so * (1.f - so);
-  dc = (1.f - v.kc) * dc + dcn * sf;
-  res = (1.f - v.kh) * dhz;
+  dc = (1.f - kc) * dc + dcn * sf;
+  res = (1.f - kh) * dhz;
 }
 
 __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* const dctx_s = sm + TBL_DCTX;
+  __bf16* const dch = reinterpret_cast<__bf16*>(sm + TBL_DCH);  // [0, 256) hi, [256, 512) lo
   float* const ep = sm + TBL_EP;
   float* const da_s = sm + TBL_DA;
   float* const ds = sm + TBL_DS;
   float* const cum_s = sm + TBL_CUM;
-  float* const dus = sm + TBL_DU;
-  float* const ms = sm + TBL_M;
   float* const red = sm + TBL_RED;
   float* const dq_s = sm + TBL_DQ;
   float* const scr = sm + TBL_SC;
   int* const sfail = reinterpret_cast<int*>(sm + TBL_SC + 16);
+  float* const cel = sm + TBL_CELL;
+  float* const dus = sm + TBL_DU;                    // ATT phase .. end of the step
+  float* const ms = sm + TBL_U;                      // end of the step
+  float* const stA = sm + TBL_U;                     // PROD phase: 32 A blocks of 1 KB
+  float* const stO = sm + TBL_U;                     // PROD phase, after the products: [64][TB_OS] outputs
+  tp_bf8* const valf = reinterpret_cast<tp_bf8*>(sm + TBL_VAL);
   constexpr int H = TP_H, D = TP_D, A = TP_A, P = TP_P, LX1 = TP_LX1, K4 = TB_K4, TM = TB_TM;
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -149,7 +184,10 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
   // ---- product weights, B fragments of v_mfma_f32_16x16x32_bf16: wave w owns the output columns
   // m = 128 nb + 32 w + 16 nt + jl; k-step ks of the K-block covers its exchange positions
   // 32 ks + 8 g4 + e -> gate column c = (p >> 6)·H + 64 kb + (p & 63)
-  tp_bf8 w2f[2][8], w1f[2][8];
+  // W2's block stays in registers; W1's goes to the fragment-major copy W1F that the d X1 product
+  // streams from L2 every step (2 x 64 regs of resident weights do not fit beside the values quarter)
+  tp_bf8 w2f[2][8];
+  tp_bf8* const w1g = reinterpret_cast<tp_bf8*>(a.W1F) + ((long)g * TB_NW + w) * 16 * 64;
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
     const int m = 128 * nb + 32 * w + 16 * nt + jl;
@@ -157,47 +195,47 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
     for (int ks = 0; ks < 8; ++ks) {
       const int p0 = 32 * ks + 8 * g4;
       const int c0 = (p0 >> 6) * H + 64 * kb + (p0 & 63);
+      tp_bf8 f1;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        w2f[nt][ks][e] = a.K2T[(long)(c0 + e) * 2 * H + m];       // W2[m][c]: m < H h1 rows, then hz2
-        w1f[nt][ks][e] = a.K1T[(long)(c0 + e) * LX1 + P + m];     // W1[P + m][c]: ctx rows, then hz1
+        w2f[nt][ks][e] = a.K2T[(long)(c0 + e) * 2 * H + m];  // W2[m][c]: m < H h1 rows, then hz2
+        f1[e] = a.K1T[(long)(c0 + e) * LX1 + P + m];         // W1[P + m][c]: ctx rows, then hz1
       }
+      w1g[(nt * 8 + ks) * 64 + lane] = f1;
     }
   }
   // ---- attention row constants
-  // values quarter as A fragments (AGPRs): tile pt = w + 4 r, k-step ks: lane holds
-  // values16[rb][16 pt + jl][256 sq + 32 ks + 8 g4 .. + 8]
-  float vfr[TB_PTW][8][4];
+  // values quarter as A fragments in LDS (fragment-major, conflict-free reads): tile pt, k-step ks: lane
+  // holds values16[rb][16 pt + jl][256 sq + 32 ks + 8 g4 .. + 8]
 #pragma unroll
   for (int r = 0; r < TB_PTW; ++r) {
-    const int j = 16 * (w + 4 * r) + jl;
+    const int pt = w + 4 * r;
+    if (pt >= TB_NPT) break;  // wave-uniform
+    const int j = 16 * pt + jl;
     const bool ok = arow && j < Tin;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const tp_u4 v = ok ? *reinterpret_cast<const tp_u4*>(a.values16 + ((long)rb * Tin + j) * D + 256 * sq + 32 * ks + 8 * g4)
-                         : tp_u4{0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) vfr[r][ks][i] = tp_aput(__uint_as_float(v[i]));
-    }
+    for (int ks = 0; ks < 8; ++ks)
+      valf[(pt * 8 + ks) * 64 + lane] =
+          ok ? *reinterpret_cast<const tp_bf8*>(a.values16 + ((long)rb * Tin + j) * D + 256 * sq + 32 * ks + 8 * g4) : tp_bf8{};
   }
-  // query columns of the own dims as A fragments of the d h2 product, in LDS: M-tile mt = 16 w + i
-  // (rows u = 16 mt + jl), lane holds Wq[u][32 sq + 8 g4 .. + 8]
-  tp_bf8* const wqf = reinterpret_cast<tp_bf8*>(sm + TBL_WQ);
+  // the own 4 units' query rows as B fragments of the unit role's d h2 product (columns jl < 4 = units
+  // 4g + jl, the others zero): k-step ks, lane holds Wq[4g + jl][32 ks + 8 g4 .. + 8]
+  tp_bf8 wqb[4];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int u = 16 * (16 * w + i) + jl;
-    wqf[(16 * w + i) * 64 + lane] = arow ? *reinterpret_cast<const tp_bf8*>(a.Wq + (long)u * A + 32 * sq + 8 * g4) : tp_bf8{};
+  for (int ks = 0; ks < 4; ++ks)
+    wqb[ks] = jl < 4 ? *reinterpret_cast<const tp_bf8*>(a.Wq + (long)(4 * g + jl) * A + 32 * ks + 8 * g4) : tp_bf8{};
+  // KW (the location conv folded through W_loc) as split-bf16 B fragments of the location-conv
+  // backward M = du·KW over the own 32 dims: tap tile nt, lane holds KW[dim 32 sq + 8 g4 + e][tap 16 nt + jl]
+  // (tap 31, the bias column, zero)
+  tp_bf8 kwh[2], kwl[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int tap = 16 * nt + jl;
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = (arow && tap < 31) ? a.KWT[(32 * sq + 8 * g4 + e) * 32 + tap] : 0.f;
+    tb_split8(x, kwh[nt], kwl[nt]);
   }
-  // KW^T as B fragments of the location-conv backward (v_mfma_f32_16x16x4f32): tap tile nt, k-step ks:
-  // lane holds KW[dim 32 sq + 4 ks + g4][tap 16 nt + jl] (tap 31, the bias column, zero)
-  float kwb[2][8];
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const int tap = 16 * nt + jl;
-      kwb[nt][ks] = (arow && tap < 31) ? a.KWT[(32 * sq + 4 * ks + g4) * 32 + tap] : 0.f;
-    }
   // v_a of the lane's dims 16 mt + 4 g4 + i (energy-tile layout, as the forward)
   float vav[8];
 #pragma unroll
@@ -213,7 +251,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
   float dva = 0.f, dba = 0.f;
   tp_f4 gacc = {0.f, 0.f, 0.f, 0.f};
   const int len = arow ? a.lens[rb] : 0;
-  for (int e = tid; e < TM + 48; e += TP_NT) cum_s[e] = 0.f;
+  for (int e = tid; e < TM + 64; e += TP_NT) cum_s[e] = 0.f;
   for (int e = tid; e < TM; e += TP_NT) ds[e] = 0.f;
   if (tid == 0) sfail[0] = 0;
 
@@ -223,6 +261,87 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
   const int evo = er * H + en;
   float dc1 = 0.f, dc2 = 0.f, rr1 = 0.f, rr2 = 0.f;
   __syncthreads();
+
+  // product partial of (kb, nb): the K-block of dG (bf16 exchange rows X, parity par) staged in LDS in
+  // one round trip (thread: 8 of its 32 one-KB (row tile, k-step) blocks; stored lane-major, each
+  // fragment's 64 lanes contiguous, so the MFMA-side reads are conflict-free), then wave w's 2 x 4
+  // tiles against its B fragments (resident, or streamed from the fragment-major copy wst in the same
+  // round trip); the [64][128] fp32 partial staged in LDS and stored as 16-byte rows to
+  // out[par][kb][row][128 nb ..)
+  auto product = [&](const __bf16* X, const tp_bf8 (*wres)[8], const tp_bf8* wst, float* out, bool rowmajor, int ph,
+                     int par, unsigned tag, long long* stp, int sb) {
+    auto pst = [&](int i) {
+      if (stp && tid == 0) stp[g * 32 + sb + i] = __builtin_amdgcn_s_memrealtime();
+    };
+    // the streamed weight fragments (independent of the step) go out before the wait on the dG block
+    tp_bf8 ws[16];
+    if (wst) {
+      const auto rw = tp_rsrc(wst);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ws[i] = tp_ldx4<false>(rw, lane * 16, i * 1024);
+    }
+    if (!tb_poll(a, ph, 16, tag, [&](int l) { return 16 * kb + l; })) sfail[0] = 1;
+    pst(0);
+    {
+      if (wst) tp_wait(ws);
+      const auto rs = tp_rsrc(X + (long)par * 64 * K4);
+      tp_bf8 f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // block b = w + 4 k: row tile b >> 3, k-step b & 7
+        const int b = w + 4 * k;
+        f[k] = tp_ldx4<true>(rs, lane * 16, ((b >> 3) * (K4 >> 5) + 8 * kb + (b & 7)) * 1024);
+      }
+      tp_wait(f);
+      pst(1);
+      // the 16-byte chunk at lane * 16 of a block is row lane >> 2, k-chunk lane & 3 = fragment lane
+      // (lane >> 2) + 16 (lane & 3)
+      const int dl = (lane >> 2) + 16 * (lane & 3);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) *reinterpret_cast<tp_bf8*>(stA + (w + 4 * k) * 256 + dl * 4) = f[k];
+    }
+    __syncthreads();
+    pst(2);
+    tp_f4 acc[2][4] = {};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      tp_bf8 af[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) af[mt] = *reinterpret_cast<const tp_bf8*>(stA + (mt * 8 + ks) * 256 + lane * 4);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], wst ? ws[nt * 8 + ks] : wres[nt][ks], acc[nt][mt],
+                                                                0, 0, 0);
+    }
+    __syncthreads();  // every wave's last A read before the outputs overwrite the staging area
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) stO[(16 * mt + 4 * g4 + i) * TB_OS + 32 * w + 16 * nt + jl] = acc[nt][mt][i];
+    __syncthreads();
+    pst(3);
+    if (rowmajor) {  // d ctx block (nb < 8): [kb][row][1024]; store k: rows 8 k + (tid >> 5), 32 lanes per
+                     // 512-byte row segment
+      float* const ob = out + (long)par * TB_PSTRIDE + (long)kb * 64 * 1024;
+      const int c4 = 4 * (tid & 31);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = 8 * k + (tid >> 5);
+        tp_st16(ob, (r * 1024 + 128 * nb + c4) * 4, *reinterpret_cast<const tp_u4*>(stO + r * TB_OS + c4));
+      }
+    } else {  // unit-major [par][nb][m4][kb][row][4]: wave-instruction k = one 1-KB (m4, kb) run of 64 rows
+      float* const ob = out + (long)par * TB_PSTRIDE;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int m4 = w + 4 * k;
+        tp_st16(ob, ((((nb * 32 + m4) * TB_NKB + kb) * 64 + lane) * 4) * 4,
+                *reinterpret_cast<const tp_u4*>(stO + lane * TB_OS + 4 * m4));
+      }
+    }
+  };
 
 #define TB_STAMP(i)                                                         \
   do {                                                                      \
@@ -236,69 +355,78 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
     long long* const stp = t == a.stamp_step ? a.stamps : nullptr;
     asm volatile("" ::: "memory");
     TB_STAMP(0);
-    // unit-role operands of one cell (layer 0 / 1), loaded ahead of that cell's waits
-    auto cell_load = [&](int layer, TbCell& c, float& dpin) {
-      if (!erow) return;
-      const float* gg = (layer ? a.G2 : a.G1) + (tb + er) * K4 + en;
+    // ---- the unit role's operands of both cells (HBM), loaded at the start of the step and parked in
+    // LDS ([17][256], thread-private columns) once they land: no load of them waits behind a poll later
+    float cv[17];
+    if (erow) {
+      const int go = (er * K4 + en) * 4;
+      const float* g2 = a.G2 + tb * K4;
+      const float* g1 = a.G1 + tb * K4;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) c.g[q] = gg[q * H];
-      c.cn = (layer ? a.CN2 : a.CN1)[tb * H + evo];
-      c.cp = (layer ? a.C2 : a.C1)[tb * H + evo];
-      if (layer) dpin = a.dPIN[(tb + er) * (H + D) + en];
-      if (a.zm) {
-        const uint8_t* z = a.zm + (long)t * 4 * B * H + evo + (long)(2 * layer) * B * H;
-        c.kc = (float)z[0];
-        c.kh = (float)z[(long)B * H];
-      } else {
-        c.kc = c.kh = 1.f - a.z;
+      for (int q = 0; q < 4; ++q) {
+        cv[q] = tb_lg(g2, go + q * H * 4);
+        cv[8 + q] = tb_lg(g1, go + q * H * 4);
       }
+      cv[4] = tb_lg(a.CN2 + tb * H, evo * 4);
+      cv[5] = tb_lg(a.C2 + tb * H, evo * 4);
+      cv[12] = tb_lg(a.CN1 + tb * H, evo * 4);
+      cv[13] = tb_lg(a.C1 + tb * H, evo * 4);
+      cv[16] = tb_lg(a.dPIN + tb * (H + D), (er * (H + D) + en) * 4);
+      if (a.zm) {
+        const auto rz = tp_rsrc(a.zm + (long)t * 4 * B * H);
+        const int zs = B * H;
+        cv[14] = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 0, 0);
+        cv[15] = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, zs, 0);
+        cv[6] = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 2 * zs, 0);
+        cv[7] = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 3 * zs, 0);
+      } else {
+        cv[6] = cv[7] = cv[14] = cv[15] = 1.f - a.z;
+      }
+    }
+    auto park = [&] {
+      if (erow)
+#pragma unroll
+        for (int k = 0; k < 17; ++k) cel[k * 256 + tid] = cv[k];
     };
     // ================= ATT
+    if (!arow) park();
     if (arow) {
       const long rt = (tb + rb) * Tin;  // this row's [Tin] block of step t
-      const float aj = tid < Tin ? a.ALN[rt + tid] : 0.f;
-      const float cumv = tid < Tin ? a.CUM[rt + tid] : 0.f;
-      tp_f4 th[TB_PTW][2];
-#pragma unroll
-      for (int r = 0; r < TB_PTW; ++r) {
-        const int j = 16 * (w + 4 * r) + jl;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-          th[r][mt] = j < Tin ? *reinterpret_cast<const tp_f4*>(a.TH + (rt + j) * A + 32 * sq + 16 * mt + 4 * g4)
-                              : tp_f4{0.f, 0.f, 0.f, 0.f};
-      }
+      const int tc = min(tid, Tin - 1);  // clamped: unconditional loads (no vmcnt(0) at a branch join)
+      float aj = tb_lg(a.ALN + rt, tc * 4);
+      float cumv = tb_lg(a.CUM + rt, tc * 4);
       // d ctx of channel 256 sq + tid = d PIN + Σ_kb P1_{t+1} (wave w: the N-block 2 sq + (w >> 1))
-      float dctx = a.dPIN[(tb + rb) * (H + D) + H + 256 * sq + tid];
+      float dctx = tb_lg(a.dPIN + (tb + rb) * (H + D) + H + 256 * sq, tid * 4);
       if (!first) {
         const int nbw = 2 * sq + (w >> 1);
         if (!tb_poll(a, TB_PH_P1, TB_NKB, tagn, [&](int l) { return 16 * l + nbw; })) sfail[0] = 1;
         TB_STAMP(1);
-        const auto rs = tp_rsrc(a.P1X + (long)parn * TB_NKB * 64 * TB_NOUT);
+        const auto rs = tp_rsrc(a.P1X + (long)parn * TB_PSTRIDE);
         float pv[TB_NKB];
 #pragma unroll
-        for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rs, (int)((((long)k * 64 + rb) * TB_NOUT + 256 * sq + tid) * 4));
+        for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rs, ((k * 64 + rb) * 1024 + 256 * sq + tid) * 4);
 #pragma unroll
         for (int k = 0; k < TB_NKB; ++k) dctx += pv[k];
       }
-      a.DCTX[(tb + rb) * D + 256 * sq + tid] = dctx;
-      dctx_s[tid] = dctx;
+      park();
+      if (tid >= Tin) aj = cumv = 0.f;
+      tp_bst(a.DCTX + (tb + rb) * D + 256 * sq, tid * 4, 0, dctx);
+      {  // split-bf16 halves of d ctx: the B columns 0 (hi) and 1 (lo) of the d align product
+        const __bf16 hi = (__bf16)dctx;
+        dch[tid] = hi;
+        dch[256 + tid] = (__bf16)(dctx - (float)hi);
+      }
+      if (tid < Tin) cum_s[15 + tid] = cumv;
       __syncthreads();
       TB_STAMP(2);
       if (sfail[0]) return;
-      // d align partial of the own channels: values quarter · (hi, lo) bf16 halves of d ctx in the B
-      // columns 0 / 1 of v_mfma_f32_16x16x32_bf16 (the other columns zero)
+      // d align partial of the own channels: values quarter · (hi, lo) of d ctx on v_mfma_f32_16x16x32_bf16
       {
         tp_bf8 bfr[8];
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
-          float x[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = dctx_s[32 * ks + 8 * g4 + e];
-            const float hi = (float)(__bf16)v;
-            x[e] = jl == 0 ? hi : jl == 1 ? v - hi : 0.f;
-          }
-          bfr[ks] = tb_bf8(x);
+          const tp_bf8 v = *reinterpret_cast<const tp_bf8*>(dch + (jl == 1 ? 256 : 0) + 32 * ks + 8 * g4);
+          bfr[ks] = jl < 2 ? v : tp_bf8{};
         }
 #pragma unroll
         for (int r = 0; r < TB_PTW; ++r) {
@@ -306,11 +434,8 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
           if (16 * pt >= Tin) break;  // wave-uniform
           tp_f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int ks = 0; ks < 8; ++ks) {
-            const tp_u4 u = {__float_as_uint(tp_aget(vfr[r][ks][0])), __float_as_uint(tp_aget(vfr[r][ks][1])),
-                             __float_as_uint(tp_aget(vfr[r][ks][2])), __float_as_uint(tp_aget(vfr[r][ks][3]))};
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(tp_bf8, u), bfr[ks], acc, 0, 0, 0);
-          }
+          for (int ks = 0; ks < 8; ++ks)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(valf[(pt * 8 + ks) * 64 + lane], bfr[ks], acc, 0, 0, 0);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float lo = __shfl(acc[i], lane + 1, 64);
@@ -354,11 +479,23 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
       __syncthreads();
       TB_STAMP(4);
       if (sfail[0]) return;
+      // tanh of the own dims (loaded here: they would hold 24 registers across the whole phase)
+      tp_f4 th[TB_PTW][2];
+      {
+        const auto rth = tp_rsrc(a.TH + rt * A);
+#pragma unroll
+        for (int r = 0; r < TB_PTW; ++r) {
+          const int j = min(16 * (w + 4 * r) + jl, Tin - 1);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+            th[r][mt] = __builtin_bit_cast(tp_f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rth, (j * A + 32 * sq + 16 * mt + 4 * g4) * 4, 0, 0));
+        }
+      }
       // softmax backward (attention.py:218): de_j = a_j (d a_j - Σ_k a_k d a_k), 0 past the length
       const float dav = tid < Tin ? da_s[tid] : 0.f;
       const float ssum = tb_block_sum(aj * dav, scr);
       if (tid < Tin) da_s[tid] = tid < len ? aj * (dav - ssum) : 0.f;
-      if (tid < Tin) cum_s[15 + tid] = cumv;
       __syncthreads();
       // du of the own dims (energy-tile layout): d keys, d query, d v_a; du -> LDS
       float dqp[8], dvp[8];
@@ -370,8 +507,10 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         if (16 * pt >= Tin) break;  // wave-uniform
         const int j = 16 * pt + jl;
         const float dej = j < Tin ? da_s[j] : 0.f;
+        if (j >= Tin) th[r][0] = th[r][1] = tp_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < 2; ++mt) {
+          tp_f4 dv4;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float thv = th[r][mt][i];
@@ -379,8 +518,11 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
             dkey[r][4 * mt + i] = tp_aput(tp_aget(dkey[r][4 * mt + i]) + du);
             dqp[4 * mt + i] += du;
             dvp[4 * mt + i] += dej * thv;
-            dus[j * 33 + 16 * mt + 4 * g4 + i] = du;
+            dv4[i] = du;
           }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dus[j * TB_DUS + 16 * mt + 4 * g4 + i] = dv4[i];
+        }
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -407,94 +549,70 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         dq_s[tid] = q;
         dba += q;
         dva += v;
-        a.DQ[(tb + rb) * A + 32 * sq + tid] = q;
+        tp_bst(a.DQ + (tb + rb) * A + 32 * sq, tid * 4, 0, q);
       }
       __syncthreads();
       TB_STAMP(5);
-      // d h2 partial of this quarter: Σ_{own dims} Wq[u][a]·dq[a] for all u (bf16 operands as the
-      // per-step product k_tr_fused<TF_BWD_H>), B column 0 = dq
-      {
-        float x[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = jl == 0 ? dq_s[8 * g4 + e] : 0.f;
-        const tp_bf8 bq = tb_bf8(x);
-        float* const qrow = a.QX + (((long)par * 4 + sq) * 64 + rb) * H;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const tp_f4 acc =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wqf[(16 * w + i) * 64 + lane], bq, tp_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          if (jl == 0) tp_st16(qrow, (16 * (16 * w + i) + 4 * g4) * 4, __builtin_bit_cast(tp_u4, acc));
-        }
+      // d query of the own dims -> the dq exchange rows (bf16, A-fragment layout, K = 128): the unit
+      // role forms d h2 = dq·Wq^T itself (bf16 operands, as k_tr_fused<TF_BWD_H>)
+      if (tid < 4) {
+        const float* q8 = dq_s + 8 * tid;
+        const tp_u4 v = {tp_pack(q8[0], q8[1]), tp_pack(q8[2], q8[3]), tp_pack(q8[4], q8[5]), tp_pack(q8[6], q8[7])};
+        tp_st16(a.DQX, (int)(((long)par * 64 * A + tp_afl(rb, 32 * sq + 8 * tid, A)) * 2), v);
       }
       tp_publish(a, TB_PH_Q, tag);
       TB_STAMP(6);
-      // ---- off the chain: d W_loc accumulators and the location-conv backward of the own dims
-      {  // G^T[a][tap] += Σ_j du[j][a]·cum_t[j + tap - 15]: wave w -> dim tile w >> 1, tap tile w & 1
-        const int mt = w >> 1, nt = w & 1;
-        const int nks = (Tin + 3) >> 2;
-        for (int ks = 0; ks < nks; ++ks) {
-          const int j = 4 * ks + g4;
-          gacc = __builtin_amdgcn_mfma_f32_16x16x4f32(dus[j * 33 + 16 * mt + jl], cum_s[j + 16 * nt + jl], gacc, 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int q6 = 0; q6 < 2 * TB_PTW; ++q6) {  // M tiles (position tile, tap tile) = w + 4 q6
-        const int idx = w + 4 * q6, pt = idx >> 1, nt = idx & 1;
-        if (16 * pt >= Tin) continue;  // wave-uniform
-        tp_f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dus[(16 * pt + jl) * 33 + 4 * ks + g4], kwb[nt][ks], acc, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ms[(16 * pt + 4 * g4 + i) * 33 + 16 * nt + jl] = acc[i];
-      }
-      __syncthreads();
-      if (tid < Tin) {  // d cum_t[i] += Σ_tap M[i - tap + 15][tap]
-        float v = 0.f;
-        for (int tap = 0; tap < 31; ++tap) {
-          const int jj = tid - tap + 15;
-          if (jj >= 0 && jj < Tin) v += ms[jj * 33 + tap];
-        }
-        ds[tid] += v;
-      }
     }
-    TB_STAMP(7);
-    // ================= CELL2: d hz2 from step t+1's product, d h2 from the 4 quarters' QX
-    TbCell c2{};
-    float dpin_h = 0.f;
-    cell_load(1, c2, dpin_h);
-    float dhz2 = 0.f;
-    if (!first) {
-      if (!tb_poll(a, TB_PH_P2, TB_NKB, tagn, [&](int l) { return 16 * l + 8 + (g >> 5); })) sfail[0] = 1;
-      if (erow) {
-        const auto rs = tp_rsrc(a.P2X + (long)parn * TB_NKB * 64 * TB_NOUT);
-        float pv[TB_NKB];
-#pragma unroll
-        for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rs, (int)((((long)k * 64 + er) * TB_NOUT + H + en) * 4));
-#pragma unroll
-        for (int k = 0; k < TB_NKB; ++k) dhz2 += pv[k];
-      }
-      dhz2 += rr2;
-    }
+    // ================= CELL2: d hz2 from step t+1's product, d h2 from the dq rows of all quarters: both waits
+    // first, then every load of the cell in one round trip
+    if (!first && !tb_poll(a, TB_PH_P2, TB_NKB, tagn, [&](int l) { return 16 * l + 8 + (g >> 5); })) sfail[0] = 1;
     if (!tb_poll(a, TB_PH_Q, B, tag, [&](int l) { return 64 * w + l; })) sfail[0] = 1;  // wave w: quarter w
-    __syncthreads();  // every quarter's poll behind this barrier
+    __syncthreads();  // every quarter's poll behind this barrier; the parked operands visible
     TB_STAMP(8);
     if (sfail[0]) return;
     {
+      // d h2 of (row, own unit) = dq[row]·Wq[unit]^T: wave w's row tile (rows 16 w ..) on one MFMA chain,
+      // the 4 unit columns moved to the cell threads (row 16 w + (lane >> 2), unit lane & 3)
+      float dh2;
+      {
+        const auto rq = tp_rsrc(a.DQX + (long)par * 64 * A);
+        tp_bf8 af[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) af[ks] = tp_ldx4<true>(rq, ((lane & 15) * 32 + 8 * (lane >> 4)) * 2, (w * 4 + ks) * 1024);
+        tp_wait(af);
+        tp_f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], wqb[ks], acc, 0, 0, 0);
+        const int rl = lane >> 2, srcl = (lane & 3) + 16 * (rl >> 2);
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = __shfl(acc[i], srcl, 64);
+        const int ri = rl & 3;
+        dh2 = ri == 0 ? v[0] : ri == 1 ? v[1] : ri == 2 ? v[2] : v[3];
+      }
       float d[4] = {0.f, 0.f, 0.f, 0.f};
       if (erow) {
-        const auto rs = tp_rsrc(a.QX + (long)par * 4 * 64 * H);
-        float qv[4];
+        float pv[TB_NKB];
+        const auto rp = tp_rsrc(a.P2X + (long)parn * TB_PSTRIDE);
+        if (!first)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) qv[s] = tb_ld(rs, (int)((((long)s * 64 + er) * H + en) * 4));
-        const float dext = dpin_h + (((qv[0] + qv[1]) + qv[2]) + qv[3]);
-        tb_cell_bwd(c2, dext, dhz2, dc2, rr2, d);
-        float* const dg = a.dG2 + (tb + er) * K4 + en;
+          for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rp, tb_uoff(8 + (g >> 5), g & 31, k, er, eu));
+        float c[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dg[q * H] = d[q];
+        for (int k = 0; k < 8; ++k) c[k] = cel[k * 256 + tid];
+        float dhz2 = 0.f;
+        if (!first) {
+#pragma unroll
+          for (int k = 0; k < TB_NKB; ++k) dhz2 += pv[k];
+          dhz2 += rr2;
+        }
+        const float dext = cel[16 * 256 + tid] + dh2;
+        tb_cell_bwd(c, dext, dhz2, dc2, rr2, d);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tp_bst(a.dG2 + tb * K4, (er * K4 + en + q * H) * 4, 0, d[q]);
       }
-      // bf16 exchange row: the 4 units of (row er, gate q) are 4 adjacent tb_kperm positions (the
-      // quad of lanes of row er shares erow, so the shuffles stay inside active quads)
+      // bf16 exchange row: the 4 units of (row er, gate q) are 4 adjacent tb_kperm positions (the quad
+      // of lanes of row er shares erow, so the shuffles stay inside active quads)
       const int src = lane & ~3;
       float v[4][4];
 #pragma unroll
@@ -512,78 +630,47 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
     tp_publish(a, TB_PH_G2, tag);
     TB_STAMP(9);
     // ================= PROD2: [d h1 | d hz2_{t-1}] partial of (kb, nb)
-    auto product = [&](const __bf16* X, const tp_bf8 (&wf)[2][8], float* out, int ph) {
-      if (!tb_poll(a, ph, 16, tag, [&](int l) { return 16 * kb + l; })) sfail[0] = 1;
-      const auto rs = tp_rsrc(X + (long)par * 64 * K4);
-      const int vo = ((lane & 15) * 32 + 8 * (lane >> 4)) * 2;
-      tp_f4 acc[2][4] = {};
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {  // four batches of 2 k-steps, every load of a batch in flight
-        tp_bf8 af[8];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) af[4 * i + mt] = tp_ldx4<true>(rs, vo, (mt * (K4 >> 5) + 8 * kb + 2 * h + i) * 1024);
-        tp_wait(af);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-              acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[4 * i + mt], wf[nt][2 * h + i], acc[nt][mt], 0, 0, 0);
-      }
-      float* const ob = out + ((long)par * TB_NKB + kb) * 64 * TB_NOUT;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int m = 128 * nb + 32 * w + 16 * nt + jl;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) tb_st(ob, (int)(((16 * mt + 4 * g4 + i) * TB_NOUT + m) * 4), acc[nt][mt][i]);
-      }
-    };
-    product(a.G2X, w2f, a.P2X, TB_PH_G2);
+    product(a.G2X, w2f, nullptr, a.P2X, false, TB_PH_G2, par, tag, stp, 14);
     __syncthreads();
     if (sfail[0]) return;
     tp_publish(a, TB_PH_P2, tag);
     TB_STAMP(10);
     // ================= CELL1: d h1 = Σ_kb P2 of the own N-block; d hz1 from step t+1's product 1
-    TbCell c1{};
-    float unused = 0.f;
-    cell_load(0, c1, unused);
-    float dh1 = 0.f, dhz1 = 0.f;
-    if (!first) {
-      if (!tb_poll(a, TB_PH_P1, TB_NKB, tagn, [&](int l) { return 16 * l + 8 + (g >> 5); })) sfail[0] = 1;
-      if (erow) {
-        const auto rs = tp_rsrc(a.P1X + (long)parn * TB_NKB * 64 * TB_NOUT);
-        float pv[TB_NKB];
-#pragma unroll
-        for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rs, (int)((((long)k * 64 + er) * TB_NOUT + H + en) * 4));
-#pragma unroll
-        for (int k = 0; k < TB_NKB; ++k) dhz1 += pv[k];
-      }
-      dhz1 += rr1;
-    }
+    if (!first && !tb_poll(a, TB_PH_P1, TB_NKB, tagn, [&](int l) { return 16 * l + 8 + (g >> 5); })) sfail[0] = 1;
     if (!tb_poll(a, TB_PH_P2, TB_NKB, tag, [&](int l) { return 16 * l + (g >> 5); })) sfail[0] = 1;
-    if (erow) {
-      const auto rs = tp_rsrc(a.P2X + (long)par * TB_NKB * 64 * TB_NOUT);
-      float pv[TB_NKB];
-#pragma unroll
-      for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rs, (int)((((long)k * 64 + er) * TB_NOUT + en) * 4));
-#pragma unroll
-      for (int k = 0; k < TB_NKB; ++k) dh1 += pv[k];
-    }
     __syncthreads();
     TB_STAMP(11);
     if (sfail[0]) return;
     {
       float d[4] = {0.f, 0.f, 0.f, 0.f};
       if (erow) {
-        tb_cell_bwd(c1, dh1, dhz1, dc1, rr1, d);
-        float* const dg = a.dG1 + (tb + er) * K4 + en;
+        float pa[TB_NKB], pb[TB_NKB];
+        const auto r1 = tp_rsrc(a.P1X + (long)parn * TB_PSTRIDE);
+        const auto r2 = tp_rsrc(a.P2X + (long)par * TB_PSTRIDE);
+        if (!first)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dg[q * H] = d[q];
+          for (int k = 0; k < TB_NKB; ++k) pa[k] = tb_ld(r1, tb_uoff(8 + (g >> 5), g & 31, k, er, eu));
+#pragma unroll
+        for (int k = 0; k < TB_NKB; ++k) pb[k] = tb_ld(r2, tb_uoff(g >> 5, g & 31, k, er, eu));
+        if (stp && tid == 0) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          stp[g * 32 + 22] = __builtin_amdgcn_s_memrealtime();
+        }
+        float c[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = cel[(8 + k) * 256 + tid];
+        float dh1 = 0.f, dhz1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < TB_NKB; ++k) dh1 += pb[k];
+        if (!first) {
+#pragma unroll
+          for (int k = 0; k < TB_NKB; ++k) dhz1 += pa[k];
+          dhz1 += rr1;
+        }
+        tb_cell_bwd(c, dh1, dhz1, dc1, rr1, d);
+        if (stp && tid == 0) stp[g * 32 + 23] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tp_bst(a.dG1 + tb * K4, (er * K4 + en + q * H) * 4, 0, d[q]);
       }
       const int src = lane & ~3;
       float v[4][4];
@@ -602,11 +689,56 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
     tp_publish(a, TB_PH_G1, tag);
     TB_STAMP(12);
     // ================= PROD1: [d ctx_{t-1} | d hz1_{t-1}] partial of (kb, nb)
-    product(a.G1X, w1f, a.P1X, TB_PH_G1);
+    product(a.G1X, w2f, w1g, a.P1X, nb < TB_NNB / 2, TB_PH_G1, par, tag, stp, 18);
     __syncthreads();
     if (sfail[0]) return;
     tp_publish(a, TB_PH_P1, tag);
     TB_STAMP(13);
+    if (arow) {
+      // ---- off the chain (the step's wait for the next P1 is the idle slot): d W_loc accumulators and the location-conv backward of the own dims, both on
+      // split-bf16 v_mfma_f32_16x16x32_bf16 (three products: ~fp32)
+      {  // G^T[a][tap] += Σ_j du[j][a]·cum_t[j + tap - 15]: wave w -> dim tile w >> 1, tap tile w & 1
+        const int mt = w >> 1, nt = w & 1;
+        const int nks = (Tin + 31) >> 5;
+        for (int ks = 0; ks < nks; ++ks) {
+          float xa[8], xb[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int j = 32 * ks + 8 * g4 + e;
+            xa[e] = j < Tin ? dus[j * TB_DUS + 16 * mt + jl] : 0.f;
+            xb[e] = cum_s[j + 16 * nt + jl];
+          }
+          tp_bf8 ah, al, bh, bl;
+          tb_split8(xa, ah, al);
+          tb_split8(xb, bh, bl);
+          gacc = tb_mfma3(ah, al, bh, bl, gacc);
+        }
+      }
+#pragma unroll
+      for (int q6 = 0; q6 < 2 * TB_PTW; ++q6) {  // M tiles (position tile, tap tile) = w + 4 q6
+        const int idx = w + 4 * q6, pt = idx >> 1, nt = idx & 1;
+        if (16 * pt >= Tin) continue;  // wave-uniform
+        float xa[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xa[e] = dus[(16 * pt + jl) * TB_DUS + 8 * g4 + e];
+        tp_bf8 ah, al;
+        tb_split8(xa, ah, al);
+        const tp_f4 acc = tb_mfma3(ah, al, kwh[nt], kwl[nt], tp_f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ms[(16 * pt + 4 * g4 + i) * 33 + 16 * nt + jl] = acc[i];
+      }
+      __syncthreads();
+      if (tid < Tin) {  // d cum_t[i] += Σ_tap M[i - tap + 15][tap] (4 independent chains)
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tap = 0; tap < 32; ++tap) {
+          const int jj = tid - tap + 15;
+          if (tap < 31 && jj >= 0 && jj < Tin) v[tap & 3] += ms[jj * 33 + tap];
+        }
+        ds[tid] += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+    }
+    TB_STAMP(7);
   }
 #undef TB_STAMP
   // ---- the attention role's sums over the steps
