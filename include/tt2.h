@@ -123,6 +123,13 @@ typedef struct tt2_config {
    * (Chorowski et al. 2015); masked scores (-inf / -2^32+1) get sigmoid = 0.  Launch path only: a
    * context with it set never takes the persistent decoder. */
   int smoothing;                /* 0 */
+  /* hparams.outputs_per_step r (hparams.py:140; tacotron.py:322-324): each decoder step projects
+   * r frames and r stop tokens, feeds the last frame back (helpers.py:57) and, with GTA targets,
+   * takes every r-th target frame (helpers.py:78).  max_iters stays the decoder-STEP capacity:
+   * tt2_decode's frames are [B][max_iters * r][num_mels], stop [B][max_iters * r], alignments
+   * [B][T_in][max_iters] and *n_steps counts steps (n_steps * r frames are valid).  r > 1 decodes
+   * on the per-step launch path; tt2_decoder_step serves r = 1 only.  1 <= r <= 8. */
+  int outputs_per_step;         /* 1 */
 } tt2_config;
 
 typedef struct tt2_ctx tt2_ctx;
@@ -154,9 +161,10 @@ tt2_status tt2_encode(tt2_ctx* ctx, const int32_t* ids, const int32_t* lengths, 
  * with the GTA TacoTrainingHelper (helpers.py:62-133, ratio 1) when targets != NULL.
  *   prenet_masks [max_iters,2,B,prenet_units] uint8 keep bits of the always-on prenet dropout
  *                (modules.py:355-356); NULL = counter-based device RNG keyed by seed.
- *   targets      [B,T_targets,80] teacher frames (GTA) or NULL.
- *   frames [B,max_iters,80], stop [B,max_iters] (sigmoid probs), align [B,T_in,max_iters]
- *   (nullable) are written for steps [0, *n_steps). */
+ *   targets      [B,T_targets,80] teacher frames (GTA) or NULL; with r = outputs_per_step the
+ *                decode runs T_targets / r steps fed by frames r-1, 2r-1, ... (helpers.py:78).
+ *   frames [B,max_iters*r,80], stop [B,max_iters*r] (sigmoid probs), align [B,T_in,max_iters]
+ *   (nullable) are written for steps [0, *n_steps), i.e. frames [0, *n_steps * r). */
 tt2_status tt2_decode(tt2_ctx* ctx, int max_iters, const uint8_t* prenet_masks, uint64_t seed,
                       const float* targets, int T_targets, float* frames, float* stop,
                       float* align, int32_t* n_steps);
@@ -207,13 +215,14 @@ tt2_status tt2_set_emt_labels(tt2_ctx* ctx, const int32_t* labels, int B);
 tt2_status tt2_emt_alignments(tt2_ctx* ctx, float* out, int32_t* heads, int32_t* T_v);
 
 /* decoder clip + Postnet + postnet_projection + final clip (tacotron.py:362-381) on the frames of
- * the last tt2_decode (frames_in == NULL) or on caller frames [B,T,80].
- * decoder_output (nullable) and mel_out are [B,T,80]. */
+ * the last tt2_decode (frames_in == NULL: T = n_steps * outputs_per_step) or on caller frames
+ * [B,T,80] (T <= max_iters * outputs_per_step).  decoder_output (nullable) and mel_out are [B,T,80]. */
 tt2_status tt2_postnet(tt2_ctx* ctx, const float* frames_in, int B, int T, float* decoder_output,
                        float* mel_out);
 
 /* encode + decode + postnet on DEVICE pointers, enqueued on `stream` (hipStream_t as void*);
- * intermediates stay in HBM.  n_steps_host receives the decoded length. */
+ * intermediates stay in HBM.  n_steps_host receives the decoded length in steps; mel_d holds
+ * [B][n_steps * r][80] (row stride n_steps * r frames), stop_d [B][max_iters * r]. */
 tt2_status tt2_synthesize_dev(tt2_ctx* ctx, const int32_t* ids_d, const int32_t* lengths_d,
                               const int32_t* lengths_host, int B, int T_in,
                               const float* ref_emt_d, int T_ref_emt, const float* ref_spk_d,

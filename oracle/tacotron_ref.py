@@ -356,7 +356,9 @@ def attention_step(query, st, keys, values, lengths, W, hp, dt):
 
 def decoder_step(frame_in, masks, st, keys, values, lengths, W, hp, dt=np.float32):
     """TacotronDecoderCell.__call__ (Architecture_wrappers.py:197-267) for the default (no emt
-    attention) decoder.  Mutates ``st``; returns (frame [B,80], stop prob [B], alignments)."""
+    attention) decoder.  Mutates ``st``; returns (frames [B, num_mels * r], stop probs, alignments):
+    FrameProjection(num_mels * outputs_per_step) and StopProjection(shape=outputs_per_step)
+    (tacotron.py:322-324); the stop probs are [B] at r = 1, [B, r] above."""
     z = hp["zoneout"]
     pre = prenet(frame_in, masks, W, dt)                                               # :199
     x1 = np.concatenate([pre, st.ctx], axis=-1)                                        # :202
@@ -371,8 +373,8 @@ def decoder_step(frame_in, masks, st, keys, values, lengths, W, hp, dt=np.float3
     fs = "decoder/linear_transform_projection/projection_linear_transform_projection/"
     ss = "decoder/stop_token_projection/projection_stop_token_projection/"
     frame = dense(pin, _w(W, fs + "kernel", dt), _w(W, fs + "bias", dt))               # :246
-    stop = sigmoid(dense(pin, _w(W, ss + "kernel", dt), _w(W, ss + "bias", dt)))[:, 0]  # :247
-    return frame, stop, align
+    stop = sigmoid(dense(pin, _w(W, ss + "kernel", dt), _w(W, ss + "bias", dt)))       # :247
+    return frame, (stop[:, 0] if stop.shape[1] == 1 else stop), align
 
 
 def dynamic_decode(keys, values, lengths, W, hp, prenet_masks, max_iters, targets=None,
@@ -381,32 +383,40 @@ def dynamic_decode(keys, values, lengths, W, hp, prenet_masks, max_iters, target
     maximum_iterations=max_iters) (tacotron.py:349-354) with TacoTestHelper (helpers.py:6-59) or,
     when ``targets`` is given, the GTA TacoTrainingHelper with ratio 1 (helpers.py:62-133).
 
-    The loop emits every step including the stopping one; it ends when every batch row's
-    round(stop) == 1 at the same step or time+1 ≥ max_iters (or, GTA, time+1 ≥ T_targets).
-    stop_at_any has no effect at r = 1: helpers.py:40-54 reduce_all over the batch axis of the
-    [B, r] finished flags first, then any (stop_at_any) / all over the r frames.  Returns frames [B,T,80], stop [B,T], alignments [B,T_in,T]."""
+    The loop emits every step including the stopping one; it ends when time+1 ≥ max_iters (or,
+    GTA, time+1 ≥ T_targets / r) or on the helper's stop rule.  r = outputs_per_step is the stop
+    projection's width (tacotron.py:322-324): each step emits r frames, the last of which is the next
+    step's input (helpers.py:57), and GTA feeds every r-th target frame, targets[:, r-1::r]
+    (helpers.py:78).  Stop rule (helpers.py:40-54): finished = round(stop) [B, r]; reduce_all over the
+    batch axis first, then any (stop_at_any) / all over the r frames -- at r = 1 both are "every row
+    rounds to 1".  Returns frames [B, T*r, num_mels], stop [B, T*r], alignments [B, T_in, T] (the
+    reshapes of tacotron.py:357-360)."""
     B, T_in, D = values.shape
     units = W[P + "decoder/decoder_LSTM/multi_rnn_cell/cell_0/lstm_cell/bias"].shape[0] // 4
     st = DecoderState(B, T_in, D, units, dt)
     nm = hp.get("num_mels", 80)
+    r = W[P + "decoder/stop_token_projection/projection_stop_token_projection/bias"].shape[0]
     frame_in = np.zeros((B, nm), dt)                                    # _go_frames helpers.py:136
     frames, stops, aligns = [], [], []
-    n_limit = max_iters if targets is None else min(max_iters, targets.shape[1])
+    tin = None if targets is None else np.asarray(targets)[:, r - 1::r]  # helpers.py:78
+    n_limit = max_iters if targets is None else min(max_iters, tin.shape[1])
     for t in range(n_limit):
         frame, stop, align = decoder_step(frame_in, prenet_masks[t], st, keys, values, lengths, W,
                                           hp, dt)
-        frames.append(frame)
+        stop = stop.reshape(B, r)
+        frames.append(frame.reshape(B, r, nm))
         stops.append(stop)
         aligns.append(align)
         if targets is not None:
-            frame_in = np.asarray(targets[:, t], dt)                    # helpers.py:126-129
+            frame_in = np.asarray(tin[:, t], dt)                        # helpers.py:126-129
             continue
         fin = np.round(stop) == 1.0                                      # helpers.py:40
-        done = bool(np.all(fin))                                         # reduce_all(axis=0), r = 1
+        per_frame = np.all(fin, axis=0)                                  # reduce_all(axis=0) -> [r]
+        done = bool(np.any(per_frame) if hp.get("stop_at_any", False) else np.all(per_frame))
         if done:
             break
-        frame_in = frame                                                 # helpers.py:57
-    return (np.stack(frames, 1), np.stack(stops, 1), np.stack(aligns, 2))
+        frame_in = frame[:, -nm:]                                        # helpers.py:57
+    return (np.concatenate(frames, 1), np.concatenate(stops, 1), np.stack(aligns, 2))
 
 
 def postnet_and_clip(dec, W, hp, dt=np.float32):

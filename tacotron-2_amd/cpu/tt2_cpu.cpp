@@ -220,7 +220,7 @@ struct tt2_ctx {
   std::vector<float> values, keys, style;  // [B][T][Dm], [B][T][A], [B][SW]
   // last decode
   int n_steps = 0, max_iters_last = 0;
-  std::vector<float> frames;               // [B][max_iters][nm]
+  std::vector<float> frames;               // [B][max_iters * r][nm]
 };
 
 namespace {
@@ -615,7 +615,9 @@ void dec_step(tt2_ctx* c, const float* frame_in, const uint8_t* masks, DecState&
     st.max_att[b] = bi;
   }
   st.ctx.swap(ctx);
-  // frame / stop projections on [h2_new, context] (Architecture_wrappers.py:243-247)
+  // frame / stop projections on [h2_new, context] (Architecture_wrappers.py:243-247): r frames and r
+  // stop tokens per step (FrameProjection(num_mels * r), StopProjection(shape=r), tacotron.py:322-324)
+  const int r = cfg.outputs_per_step, NF = nm * r;
   std::vector<float> pin((size_t)B * (H + D));
   for (int b = 0; b < B; ++b) {
     std::memcpy(&pin[(size_t)b * (H + D)], &o2[(size_t)b * H], sizeof(float) * H);
@@ -623,10 +625,10 @@ void dec_step(tt2_ctx* c, const float* frame_in, const uint8_t* masks, DecState&
   }
   const std::string fp = "decoder/linear_transform_projection/projection_linear_transform_projection/";
   const std::string sp = "decoder/stop_token_projection/projection_stop_token_projection/";
-  gemm(pin.data(), B, H + D, H + D, W(c, fp + "kernel", {H + D, nm}).data(), nm, W(c, fp + "bias", {nm}).data(),
-       frame, nm);
-  gemm(pin.data(), B, H + D, H + D, W(c, sp + "kernel", {H + D, 1}).data(), 1, W(c, sp + "bias", {1}).data(), stop, 1);
-  for (int b = 0; b < B; ++b) stop[b] = sigm(stop[b]);
+  gemm(pin.data(), B, H + D, H + D, W(c, fp + "kernel", {H + D, NF}).data(), NF, W(c, fp + "bias", {NF}).data(),
+       frame, NF);
+  gemm(pin.data(), B, H + D, H + D, W(c, sp + "kernel", {H + D, r}).data(), r, W(c, sp + "bias", {r}).data(), stop, r);
+  for (int i = 0; i < B * r; ++i) stop[i] = sigm(stop[i]);
 }
 
 DecState zero_state(const tt2_ctx* c) {
@@ -672,7 +674,7 @@ void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_re
   c->synthesis_constraint = 0; c->constraint_monotonic = 0; c->attention_win_size = 7;
   c->max_batch = max_batch; c->max_T_in = max_T_in; c->max_T_ref = max_T_ref; c->max_iters = max_iters;
   c->emt_attn = 0; c->emt_ref_gru = 0; c->n_emt = 4; c->style_mode = 0;
-  c->smoothing = 0;
+  c->smoothing = 0; c->outputs_per_step = 1;
 }
 
 tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
@@ -684,6 +686,7 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     CK(cfg->emt_attn == 0, TT2_ERR_INVALID_ARG, "the CPU backend builds the Tacotron model only (emt_attn = 0)");
 
     CK(cfg->attention_filters <= 64, TT2_ERR_INVALID_ARG, "attention_filters must be <= 64");
+    CK(cfg->outputs_per_step >= 1 && cfg->outputs_per_step <= 8, TT2_ERR_INVALID_ARG, "outputs_per_step must be in [1, 8]");
     auto c = std::make_unique<tt2_ctx>();
     c->cfg = *cfg;
     c->nm = cfg->num_mels; c->E = cfg->embedding_dim; c->Cenc = cfg->enc_conv_channels; c->U = cfg->encoder_lstm_units;
@@ -742,8 +745,8 @@ tt2_status tt2_decode(tt2_ctx* c, int max_iters, const uint8_t* prenet_masks, ui
     CK(c && frames && stop && n_steps, TT2_ERR_INVALID_ARG, "tt2_decode: null argument");
     CK(c->encoded, TT2_ERR_STATE, "tt2_decode called before tt2_encode");
     CK(max_iters >= 1 && max_iters <= c->cfg.max_iters, TT2_ERR_SHAPE_MISMATCH, "max_iters exceeds capacity");
-    CK(!targets || T_targets >= 1, TT2_ERR_INVALID_ARG, "targets given with T_targets < 1");
-    const int B = c->B, T = c->T_in, nm = c->nm, P = c->P;
+    const int B = c->B, T = c->T_in, nm = c->nm, P = c->P, r = c->cfg.outputs_per_step;
+    CK(!targets || T_targets >= r, TT2_ERR_INVALID_ARG, "targets given with T_targets < outputs_per_step");
     std::vector<uint8_t> gm;
     if (!prenet_masks) {  // the device RNG's stream (rng.h), identical bits
       gm.resize((size_t)max_iters * 2 * B * P);
@@ -751,33 +754,42 @@ tt2_status tt2_decode(tt2_ctx* c, int max_iters, const uint8_t* prenet_masks, ui
       prenet_masks = gm.data();
     }
     DecState st = zero_state(c);
-    std::vector<float> fin((size_t)B * nm, 0.f), fr((size_t)B * nm), sp(B), al((size_t)B * T);
-    c->frames.assign((size_t)B * max_iters * nm, 0.f);
-    const int n_limit = targets ? std::min(max_iters, T_targets) : max_iters;
+    const size_t NF = (size_t)nm * r, fs = (size_t)max_iters * r;  // frames per step / per row
+    std::vector<float> fin((size_t)B * nm, 0.f), fr(B * NF), sp((size_t)B * r), al((size_t)B * T);
+    c->frames.assign(B * fs * nm, 0.f);
+    // GTA: len(targets[:, r-1::r]) = T_targets / r steps (helpers.py:78-81)
+    const int n_limit = targets ? std::min(max_iters, T_targets / r) : max_iters;
     int t = 0;
     for (; t < n_limit; ++t) {
       dec_step(c, fin.data(), prenet_masks + (size_t)t * 2 * B * P, st, fr.data(), sp.data(), al.data());
       for (int b = 0; b < B; ++b) {
-        std::memcpy(&frames[((size_t)b * max_iters + t) * nm], &fr[(size_t)b * nm], sizeof(float) * nm);
-        std::memcpy(&c->frames[((size_t)b * max_iters + t) * nm], &fr[(size_t)b * nm], sizeof(float) * nm);
-        stop[(size_t)b * max_iters + t] = sp[b];
+        std::memcpy(&frames[(b * fs + (size_t)t * r) * nm], &fr[b * NF], sizeof(float) * NF);
+        std::memcpy(&c->frames[(b * fs + (size_t)t * r) * nm], &fr[b * NF], sizeof(float) * NF);
+        for (int i = 0; i < r; ++i) stop[b * fs + (size_t)t * r + i] = sp[(size_t)b * r + i];
         if (align)
           for (int j = 0; j < T; ++j) align[((size_t)b * T + j) * max_iters + t] = al[(size_t)b * T + j];
       }
-      if (targets) {  // GTA TacoTrainingHelper, ratio 1 (helpers.py:126-129)
+      if (targets) {  // GTA TacoTrainingHelper, ratio 1: frame t·r + r - 1 (helpers.py:78, 126-129)
         for (int b = 0; b < B; ++b)
-          std::memcpy(&fin[(size_t)b * nm], &targets[((size_t)b * T_targets + t) * nm], sizeof(float) * nm);
+          std::memcpy(&fin[(size_t)b * nm], &targets[((size_t)b * T_targets + (size_t)t * r + r - 1) * nm],
+                      sizeof(float) * nm);
         continue;
       }
-      // TacoTestHelper stop rule (helpers.py:36-59): round(stop) == 1 for every row.  stop_at_any picks
-      // any / all over the r frames of a step AFTER reduce_all over the batch axis: no effect at r = 1
-      int fin_rows = 0;
-      for (int b = 0; b < B; ++b) fin_rows += std::nearbyint(sp[b]) == 1.f;
-      if (c->cfg.stop_at_any == 2 ? false : fin_rows == B) {
+      // TacoTestHelper stop rule (helpers.py:40-54): finished = round(stop) [B, r]; reduce_all over the
+      // batch axis first, then any (stop_at_any) / all over the step's r frames
+      bool any_f = false, all_f = true;
+      for (int i = 0; i < r; ++i) {
+        int fin_rows = 0;
+        for (int b = 0; b < B; ++b) fin_rows += std::nearbyint(sp[(size_t)b * r + i]) == 1.f;
+        any_f |= fin_rows == B;
+        all_f &= fin_rows == B;
+      }
+      if (c->cfg.stop_at_any == 2 ? false : (c->cfg.stop_at_any ? any_f : all_f)) {
         ++t;
         break;
       }
-      fin = fr;  // helpers.py:57
+      for (int b = 0; b < B; ++b)  // the step's last frame is the next input (helpers.py:57)
+        std::memcpy(&fin[(size_t)b * nm], &fr[b * NF + NF - nm], sizeof(float) * nm);
     }
     c->n_steps = t;
     c->max_iters_last = max_iters;
@@ -801,6 +813,7 @@ tt2_status tt2_decoder_step(tt2_ctx* c, const float* frame_in, const uint8_t* pr
     CK(c && frame_in && prenet_masks && in && out && frame_out && stop_out, TT2_ERR_INVALID_ARG,
        "tt2_decoder_step: null argument");
     CK(c->encoded, TT2_ERR_STATE, "tt2_decoder_step called before tt2_encode");
+    CK(c->cfg.outputs_per_step == 1, TT2_ERR_INVALID_ARG, "tt2_decoder_step: outputs_per_step > 1 decodes through tt2_decode");
     const size_t B = c->B, H = c->H, D = c->Dm, T = c->T_in;
     DecState st;
     st.h1.assign(in->h1, in->h1 + B * H); st.c1.assign(in->c1, in->c1 + B * H);
@@ -829,10 +842,11 @@ tt2_status tt2_postnet(tt2_ctx* c, const float* frames_in, int B, int T, float* 
     if (!frames_in) {
       CK(c->decoded, TT2_ERR_STATE, "tt2_postnet(NULL) called before tt2_decode");
       B = c->B;
-      T = c->n_steps;
+      const int r = cfg.outputs_per_step;
+      T = c->n_steps * r;
       dec.resize((size_t)B * T * nm);
       for (int b = 0; b < B; ++b)
-        std::memcpy(&dec[(size_t)b * T * nm], &c->frames[(size_t)b * c->max_iters_last * nm], sizeof(float) * T * nm);
+        std::memcpy(&dec[(size_t)b * T * nm], &c->frames[(size_t)b * c->max_iters_last * r * nm], sizeof(float) * T * nm);
     } else {
       CK(B >= 1 && T >= 1, TT2_ERR_INVALID_ARG, "tt2_postnet: B, T must be >= 1");
       dec.assign(frames_in, frames_in + (size_t)B * T * nm);

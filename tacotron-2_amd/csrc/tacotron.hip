@@ -599,8 +599,8 @@ struct DecArgs {
   const float* targets;  // [B][T_lim][nm] or null
   long long* stamps;  // diagnostic s_memtime stamps (profiling only; no output depends on them)
   // outputs
-  float* frames;  // [B][max_iters][nm]
-  float* stop;    // [B][max_iters]
+  float* frames;  // [B][max_iters * r][nm]
+  float* stop;    // [B][max_iters * r]
   float* align;   // [B][T_in][max_iters] or null
 };
 
@@ -916,15 +916,16 @@ struct ProjArgs {
   unsigned* cnt;                  // [ntile] arrival tickets (zeroed per decode, reset by the last arriver)
   const float* PS; const float* bias; const float* ssum;
   float* pre1;                    // [32][P] prenet-L1 pre-activations (AF-group column order)
-  float* frames; float* stop;
+  float* frames; float* stop;      // [B][max_iters * r][nm], [B][max_iters * r]
   int B, nm, NPJ, P, max_iters, T_lim, stop_at_any;
+  int r, sc;                      // frames per step; first stop column (sc / 16 = the stop tile)
 };
 
 template <int NPW>
 __global__ __launch_bounds__(256) void k_proj(ProjArgs a, SideJob sj, int t) {
   __shared__ float red[4 * 512];
   __shared__ float G[512];
-  __shared__ float stopv[32];
+  __shared__ float stopv[8 * 32];
   __shared__ int s_last;
   if ((int)blockIdx.x >= a.ntile * a.KS) {  // extra blocks: side job
     if (a.ctl->done) return;
@@ -968,23 +969,30 @@ __global__ __launch_bounds__(256) void k_proj(ProjArgs a, SideJob sj, int t) {
     v = (v + a.ssum[m] * a.PS[(long)m * a.ldo + c]) + a.bias[c];
     if (c >= a.NPJ) {
       a.pre1[(long)m * a.P + (c - a.NPJ)] = v;
-    } else if (c < a.nm) {
-      if (m < a.B) a.frames[((long)m * a.max_iters + t) * a.nm + c] = v;
-    } else if (c == a.nm) {
-      stopv[m] = sigm(v);
+    } else if (c < a.nm * a.r) {  // frame t·r + c / nm of the step's r (tacotron.py:357 reshape)
+      const int f = c / a.nm;
+      if (m < a.B) a.frames[((long)m * a.max_iters * a.r + (long)t * a.r + f) * a.nm + (c - f * a.nm)] = v;
+    } else if (c >= a.sc && c < a.sc + a.r) {
+      stopv[(c - a.sc) * 32 + m] = sigm(v);
     }
   }
-  if (a.nm / 16 != tile) return;  // the tile holding the stop column decides `done`
+  if (a.sc / 16 != tile) return;  // the tile holding the stop columns decides `done`
   __syncthreads();
   if (wave == 0) {
+    // TacoTestHelper (helpers.py:40-54): finished = round(stop) [B, r]; reduce_all over the batch
+    // axis first, then any (stop_at_any) / all over the step's r frames -- at r = 1 both are "every
+    // valid row rounds to 1"
     const bool valid = lane < a.B;
-    const float sv = valid ? stopv[lane] : 0.f;
-    const bool f = valid && rintf(sv) == 1.0f;
-    const unsigned long long fb = __ballot(f), vb = __ballot(valid);
-    if (valid) a.stop[(long)lane * a.max_iters + t] = sv;
-    // every valid row rounds to 1, whatever stop_at_any: at r = 1 TacoTestHelper's reduce_all over the
-    // batch axis (helpers.py:40-54) comes before the any / all over the step's r frames
-    int dn = a.stop_at_any == 2 ? 0 : (fb == vb);
+    int any_f = 0, all_f = 1;
+    for (int i = 0; i < a.r; ++i) {
+      const float sv = valid ? stopv[i * 32 + lane] : 0.f;
+      const bool f = valid && rintf(sv) == 1.0f;
+      const unsigned long long fb = __ballot(f), vb = __ballot(valid);
+      if (valid) a.stop[(long)lane * a.max_iters * a.r + (long)t * a.r + i] = sv;
+      any_f |= fb == vb;
+      all_f &= fb == vb;
+    }
+    int dn = a.stop_at_any == 2 ? 0 : (a.stop_at_any ? any_f : all_f);
     if (a.T_lim > 0) dn = t + 1 >= a.T_lim;  // TacoTrainingHelper: time + 1 >= T_targets
     if (t + 1 >= a.max_iters) dn = 1;         // dynamic_decode maximum_iterations
     if (lane == 0 && dn) {
@@ -1332,6 +1340,8 @@ struct tt2_ctx {
   tt2::WeightMap host;
   bool finalized = false;
   int nm, E, Cenc, U, Dm, E2, A, F, KL, P, H, PC, SW, K1, Kp, NPJ, NPF, KSQ = tt2::KSQ_C, KSP = tt2::KSP_C, KLp, Fp;
+  int R = 1;       // outputs_per_step: frames (and stop tokens) per decoder step
+  int SC = 0;      // first stop column of the projection (all R stop columns in one 16-column tile)
   int nref;        // reference encoders with their own weights
   int nmel = 0;    // reference mels the encode reads (AdaIN: one encoder, both mels)
   int style_mode = 0;  // 0 GST, 1 reference embeddings, 2 AdaIN (tt2_config.style_mode)
@@ -1691,23 +1701,26 @@ static void finalize(tt2_ctx* c) {
   {
     const std::string fp = P + "decoder/linear_transform_projection/projection_linear_transform_projection/";
     const std::string sp = P + "decoder/stop_token_projection/projection_stop_token_projection/";
-    const auto& fk = need(wm, fp + "kernel", {c->H + c->Dm, c->nm});
-    const auto& fb = need(wm, fp + "bias", {c->nm});
-    const auto& sk = need(wm, sp + "kernel", {c->H + c->Dm, 1});
-    const auto& sb = need(wm, sp + "bias", {1});
-    // columns [0, NPJ): frame (nm) | stop | 0-pad; [NPJ, NPF): prenet layer 1 folded through the
-    // frame projection, W_f·W1 (free-running decoding feeds the frame back: helpers.py:57)
-    const int N = c->nm + 1, Kfull = c->H + c->Dm, NPF = c->NPF, Pn = c->P;
+    // FrameProjection(num_mels * r) / StopProjection(shape=r) (tacotron.py:322-324)
+    const int r = c->R, NF = c->nm * r;
+    const auto& fk = need(wm, fp + "kernel", {c->H + c->Dm, NF});
+    const auto& fb = need(wm, fp + "bias", {NF});
+    const auto& sk = need(wm, sp + "kernel", {c->H + c->Dm, r});
+    const auto& sb = need(wm, sp + "bias", {r});
+    // columns [0, NPJ): frames (nm·r) | 0-pad | stop (r, from SC) | 0-pad; [NPJ, NPF): prenet layer 1
+    // folded through the LAST frame's projection columns, W_f[:, (r-1)·nm:]·W1 (free-running decoding
+    // feeds the step's last frame back: helpers.py:57)
+    const int N = NF + r, Kfull = c->H + c->Dm, NPF = c->NPF, Pn = c->P, l0 = (r - 1) * c->nm;
     const auto& w1 = need(wm, P + "decoder/decoder_prenet/dense_1/kernel", {c->nm, Pn});
     const auto& b1 = need(wm, P + "decoder/decoder_prenet/dense_1/bias", {Pn});
     std::vector<float> W((size_t)Kfull * NPF, 0.f);
     for (int k = 0; k < Kfull; ++k) {
-      for (int n = 0; n < c->nm; ++n) W[(size_t)k * NPF + n] = fk.data[(size_t)k * c->nm + n];
-      W[(size_t)k * NPF + c->nm] = sk.data[k];
+      for (int n = 0; n < NF; ++n) W[(size_t)k * NPF + n] = fk.data[(size_t)k * NF + n];
+      for (int i = 0; i < r; ++i) W[(size_t)k * NPF + c->SC + i] = sk.data[(size_t)k * r + i];
       for (int p = 0; p < Pn; ++p) {
         const int j = af_group_col(p);
         double acc = 0.0;
-        for (int n = 0; n < c->nm; ++n) acc += (double)fk.data[(size_t)k * c->nm + n] * w1.data[(size_t)n * Pn + j];
+        for (int n = 0; n < c->nm; ++n) acc += (double)fk.data[(size_t)k * NF + l0 + n] * w1.data[(size_t)n * Pn + j];
         W[(size_t)k * NPF + c->NPJ + p] = (float)acc;
       }
     }
@@ -1756,12 +1769,12 @@ static void finalize(tt2_ctx* c) {
       for (int n = 0; n < NPF; ++n) ws[(size_t)r * NPF + n] = W[(size_t)(c->Kp + r) * NPF + n];
     if (c->SW) upload(c->proj_ws, ws);
     std::vector<float> pb(NPF, 0.f);
-    for (int n = 0; n < c->nm; ++n) pb[n] = fb.data[n];
-    pb[c->nm] = sb.data[0];
-    for (int p = 0; p < Pn; ++p) {  // b_f·W1 + b1
+    for (int n = 0; n < NF; ++n) pb[n] = fb.data[n];
+    for (int i = 0; i < r; ++i) pb[c->SC + i] = sb.data[i];
+    for (int p = 0; p < Pn; ++p) {  // b_f[(r-1)·nm:]·W1 + b1
       const int j = af_group_col(p);
       double acc = 0.0;
-      for (int n = 0; n < c->nm; ++n) acc += (double)fb.data[n] * w1.data[(size_t)n * Pn + j];
+      for (int n = 0; n < c->nm; ++n) acc += (double)fb.data[l0 + n] * w1.data[(size_t)n * Pn + j];
       pb[c->NPJ + p] = (float)(acc + b1.data[j]);
     }
     upload(c->proj_b, pb);
@@ -1851,13 +1864,14 @@ static void alloc_acts(tt2_ctx* c) {
   c->max_att.alloc(64 * 4);
   c->PP.alloc((long)c->KSP * 32 * c->NPF * 4);
   c->ctl.alloc(sizeof(DecCtl));
-  c->frames.alloc(B * MI * c->nm * 4);
-  c->stop.alloc(B * MI * 4);
+  const long MF = MI * c->R;  // frame capacity: r frames per decoder step
+  c->frames.alloc(B * MF * c->nm * 4);
+  c->stop.alloc(B * MF * 4);
   c->align.alloc(B * T * MI * 4);
-  c->dec.alloc(B * MI * c->nm * 4);
-  c->post_a.alloc(B * MI * std::max(c->PC, c->nm) * 4);
-  c->post_b.alloc(B * MI * std::max(c->PC, c->nm) * 4);
-  c->mel.alloc(B * MI * c->nm * 4);
+  c->dec.alloc(B * MF * c->nm * 4);
+  c->post_a.alloc(B * MF * std::max(c->PC, c->nm) * 4);
+  c->post_b.alloc(B * MF * std::max(c->PC, c->nm) * 4);
+  c->mel.alloc(B * MF * c->nm * 4);
   {  // conv_x3 Postnet: TT2_POSTNET_CX=0 selects the im2col GEMMs
     const char* e = std::getenv("TT2_POSTNET_CX");
     c->post_cx = (!e || std::atoi(e) != 0) && c->PC % CX_BN == 0 && (cfg.postnet_kernel_size & 1) &&
@@ -1877,7 +1891,7 @@ static void alloc_acts(tt2_ctx* c) {
     c->ex_part.alloc((size_t)kEncSplitK * B * (T + 2 * CX_P) * c->Cenc * 4);
   }
   if (c->post_cx) {
-    const long rows = cx_rows((int)B, (int)MI), cp0 = (c->nm + 31) / 32 * 32;
+    const long rows = cx_rows((int)B, (int)MF), cp0 = (c->nm + 31) / 32 * 32;
     c->px_in_h.alloc(rows * cp0 * 2);
     c->px_in_l.alloc(rows * cp0 * 2);
     for (int i = 0; i < 2; ++i) {
@@ -2216,7 +2230,7 @@ static void launch_proj(tt2_ctx* c, const DecArgs& a, int t, const SideJob& sj, 
   p.PS = a.PS; p.bias = a.proj_b; p.ssum = a.ssum; p.pre1 = c->pre1.as<float>();
   p.frames = a.frames; p.stop = a.stop;
   p.B = a.B; p.nm = a.nm; p.NPJ = c->NPJ; p.P = c->P; p.max_iters = a.max_iters; p.T_lim = a.T_lim;
-  p.stop_at_any = a.stop_at_any;
+  p.stop_at_any = a.stop_at_any; p.r = c->R; p.sc = c->SC;
   const int nsg = p.K / 16;
   const dim3 grid(p.ntile * p.KS + sj.ntile), blk(256);
   const int npw = nsg % (p.KS * 4) == 0 ? nsg / (p.KS * 4) : 0;
@@ -2311,7 +2325,7 @@ static bool pd_emt(const tt2_ctx* c) {
 static bool pd_fits(tt2_ctx* c) {
   return (!c->emt.on() || pd_emt(c)) && c->pd_mode == 1 && c->pd_dev_ok && c->kg_wmax_dec < KG_BMAX && c->H == PD_H && c->P == PD_P && c->E2 == PD_E2 && c->A == PD_A &&
          c->NPJ == PD_NPJ && c->NPF == PD_NPF && c->KLp == PD_KLP && c->T_in <= (c->emt.on() ? PD_TMAX : PD_TMAX_LONG) && c->B <= 32 &&
-         !c->cfg.smoothing;
+         !c->cfg.smoothing && c->R == 1;
 }
 
 static void decode_persist_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, const float* targets_d, int T_lim,
@@ -2460,9 +2474,10 @@ static void decode_dev(tt2_ctx* c, int max_iters, const uint8_t* masks_d, uint64
     masks_d = c->gmasks.as<uint8_t>();
   }
   if (targets_d) {  // GTA: prenet layer-1 pre-activations of every teacher frame, TP1 = targets·W1 + b1
+    // targets_d is [B][T_lim·r][nm]: step t is fed frame t·r + r - 1 (targets[:, r-1::r], helpers.py:78)
     c->TP1.alloc(sizeof(float) * (size_t)c->B * T_lim * c->P);
     GemmArgs g;
-    g.M = c->B * T_lim; g.N = c->P; g.K = c->nm; g.A = targets_d; g.lda = c->nm;
+    g.M = c->B * T_lim; g.N = c->P; g.K = c->nm; g.A = targets_d + (size_t)(c->R - 1) * c->nm; g.lda = c->nm * c->R;
     g.Bw = c->pre_w1r.as<float>(); g.ldb = c->P; g.Cout = c->TP1.as<float>(); g.ldc = c->P;
     g.bias = c->pre_b1.as<float>();
     gemm(g, s);
@@ -2661,7 +2676,7 @@ void tt2_default_config(tt2_config* c, int max_batch, int max_T_in, int max_T_re
   c->predict_linear = 0; c->num_freq = 1025; c->cbhg_kernels = 8; c->cbhg_conv_channels = 128;
   c->cbhg_pool_size = 2; c->cbhg_projection = 256; c->cbhg_projection_kernel_size = 3;
   c->cbhg_highwaynet_layers = 4; c->cbhg_highway_units = 128; c->cbhg_rnn_units = 128;
-  c->smoothing = 0;
+  c->smoothing = 0; c->outputs_per_step = 1;
 }
 
 tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
@@ -2719,7 +2734,12 @@ tt2_status tt2_create(const tt2_config* cfg, int hip_device, tt2_ctx** out) {
     // LSTM-1 critical rows: [prenet | context_enc | emotion block (emt variant)]
     c->K1 = c->P + c->E2 + c->emt.XW; c->Kp = c->H + c->E2;
     TT2_CHECK(c->E2 % 64 == 0, TT2_ERR_INVALID_ARG, "2*encoder_lstm_units must be a multiple of 64");
-    c->NPJ = ((c->nm + 1 + 15) / 16) * 16;
+    // outputs_per_step r (tacotron.py:322-324): frame columns [0, nm·r), then the r stop columns from
+    // SC inside ONE 16-column tile (the tile whose last arriver applies the stop rule)
+    c->R = cfg->outputs_per_step;
+    TT2_CHECK(c->R >= 1 && c->R <= 8, TT2_ERR_INVALID_ARG, "outputs_per_step must be in [1, 8]");
+    c->SC = (c->nm * c->R) % 16 + c->R <= 16 ? c->nm * c->R : (c->nm * c->R + 15) / 16 * 16;
+    c->NPJ = ((c->SC + c->R + 15) / 16) * 16;
     c->NPF = c->NPJ + c->P;
     alloc_acts(c.get());
     for (auto& e : c->ev) TT2_HIP(hipEventCreate(&e));
@@ -2808,6 +2828,7 @@ static void decoder_step_dev(tt2_ctx* c, const float* frame_in, const uint8_t* m
   TT2_CHECK(c->encoded, TT2_ERR_STATE, "tt2_decoder_step called before tt2_encode");
   TT2_CHECK(!c->emt.on(), TT2_ERR_INVALID_ARG,
             "tt2_decoder_step: the Tacotron_emt_attn variant decodes through tt2_decode / tt2_synthesize_dev");
+  TT2_CHECK(c->R == 1, TT2_ERR_INVALID_ARG, "tt2_decoder_step: outputs_per_step > 1 decodes through tt2_decode");
   TT2_CHECK(frame_in && masks && in && out && frame_out && stop_out, TT2_ERR_INVALID_ARG,
             "tt2_decoder_step: null argument");
   TT2_CHECK(in->h1 && in->c1 && in->h2 && in->c2 && in->attention && in->alignments && in->max_attentions &&
@@ -2924,22 +2945,29 @@ tt2_status tt2_decode(tt2_ctx* c, int max_iters, const uint8_t* prenet_masks, ui
       masks_d = c->masks.as<uint8_t>();
     }
     const float* tg_d = nullptr;
+    const int r = c->R;
+    int T_lim = 0;
     if (targets) {
-      TT2_CHECK(T_targets >= 1, TT2_ERR_INVALID_ARG, "T_targets must be >= 1");
-      const size_t n = (size_t)B * T_targets * c->nm * sizeof(float);
-      c->targets.alloc(n);
-      TT2_HIP(hipMemcpyAsync(c->targets.p, targets, n, hipMemcpyHostToDevice, s));
+      TT2_CHECK(T_targets >= r, TT2_ERR_INVALID_ARG, "T_targets must be >= outputs_per_step");
+      // TacoTrainingHelper runs len(targets[:, r-1::r]) = T_targets / r steps (helpers.py:78-81); the
+      // device copy keeps the first T_lim·r frames of each row
+      T_lim = T_targets / r;
+      const size_t row = (size_t)T_lim * r * c->nm * sizeof(float);
+      c->targets.alloc(row * B);
+      TT2_HIP(hipMemcpy2DAsync(c->targets.p, row, targets, (size_t)T_targets * c->nm * sizeof(float), row, B,
+                               hipMemcpyHostToDevice, s));
       tg_d = c->targets.as<float>();
     }
-    decode_dev(c, max_iters, masks_d, seed, tg_d, T_targets, c->frames.as<float>(), c->stop.as<float>(),
+    decode_dev(c, max_iters, masks_d, seed, tg_d, T_lim, c->frames.as<float>(), c->stop.as<float>(),
                align ? c->align.as<float>() : nullptr, s);
     const int n = c->n_steps;
     *n_steps = n;
+    const size_t fs = (size_t)max_iters * r;  // frames per row in the caller's and the device layout
     for (int b = 0; b < B; ++b) {
-      TT2_HIP(hipMemcpyAsync(frames + (size_t)b * max_iters * c->nm, c->frames.as<float>() + (size_t)b * max_iters * c->nm,
-                             sizeof(float) * n * c->nm, hipMemcpyDeviceToHost, s));
-      TT2_HIP(hipMemcpyAsync(stop + (size_t)b * max_iters, c->stop.as<float>() + (size_t)b * max_iters,
-                             sizeof(float) * n, hipMemcpyDeviceToHost, s));
+      TT2_HIP(hipMemcpyAsync(frames + b * fs * c->nm, c->frames.as<float>() + b * fs * c->nm,
+                             sizeof(float) * n * r * c->nm, hipMemcpyDeviceToHost, s));
+      TT2_HIP(hipMemcpyAsync(stop + b * fs, c->stop.as<float>() + b * fs, sizeof(float) * n * r,
+                             hipMemcpyDeviceToHost, s));
     }
     if (align)
       TT2_HIP(hipMemcpyAsync(align, c->align.p, sizeof(float) * B * c->T_in * max_iters, hipMemcpyDeviceToHost, s));
@@ -2951,7 +2979,7 @@ tt2_status tt2_postnet(tt2_ctx* c, const float* frames_in, int B, int T, float* 
   return guard([&] {
     TT2_CHECK(c && mel_out, TT2_ERR_INVALID_ARG, "tt2_postnet: null argument");
     TT2_CHECK(c->finalized, TT2_ERR_NOT_LOADED, "tt2_finalize_weights not called");
-    TT2_CHECK(B >= 1 && B <= c->cfg.max_batch && T >= 1 && T <= c->cfg.max_iters, TT2_ERR_SHAPE_MISMATCH,
+    TT2_CHECK(B >= 1 && B <= c->cfg.max_batch && T >= 1 && T <= c->cfg.max_iters * c->R, TT2_ERR_SHAPE_MISMATCH,
               "postnet: shape exceeds capacity");
     TT2_HIP(hipSetDevice(c->dev));
     hipStream_t s = c->stream;
@@ -2965,9 +2993,9 @@ tt2_status tt2_postnet(tt2_ctx* c, const float* frames_in, int B, int T, float* 
       bstride = (long)T * c->nm;
     } else {
       TT2_CHECK(c->decoded, TT2_ERR_STATE, "tt2_postnet(NULL) called before tt2_decode");
-      TT2_CHECK(B == c->B && T == c->n_steps, TT2_ERR_SHAPE_MISMATCH, "postnet shape differs from last decode");
+      TT2_CHECK(B == c->B && T == c->n_steps * c->R, TT2_ERR_SHAPE_MISMATCH, "postnet shape differs from last decode");
       src = c->frames.as<float>();
-      bstride = (long)c->last_max_iters * c->nm;
+      bstride = (long)c->last_max_iters * c->R * c->nm;
     }
     postnet_dev(c, src, bstride, B, T, c->dec.as<float>(), c->mel.as<float>(), s);
     if (decoder_output)
@@ -2995,7 +3023,8 @@ tt2_status tt2_synthesize_dev(tt2_ctx* c, const int32_t* ids_d, const int32_t* l
     decode_dev(c, max_iters, prenet_masks_d, seed, nullptr, 0, c->frames.as<float>(),
                stop_d ? stop_d : c->stop.as<float>(), nullptr, s);
     TT2_HIP(hipEventRecord(c->ev[2], s));
-    postnet_dev(c, c->frames.as<float>(), (long)max_iters * c->nm, B, c->n_steps, c->dec.as<float>(), mel_d, s);
+    postnet_dev(c, c->frames.as<float>(), (long)max_iters * c->R * c->nm, B, c->n_steps * c->R, c->dec.as<float>(),
+                mel_d, s);
     TT2_HIP(hipEventRecord(c->ev[3], s));
     c->timed = true;
     *n_steps_host = c->n_steps;

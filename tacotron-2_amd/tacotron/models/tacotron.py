@@ -230,7 +230,8 @@ class Tacotron():
             T_ref = max(ref_e.shape[1], ref_s.shape[1] if ref_s is not None else 0)
             tg = None
             if gta and tower_targets[i] is not None:
-                tg = tower_targets[i].reshape(B, -1, hp.num_mels)[:, hp.outputs_per_step - 1::hp.outputs_per_step]
+                # every target frame: the decode feeds targets[:, r-1::r] itself (helpers.py:78)
+                tg = tower_targets[i].reshape(B, -1, hp.num_mels)
             eng = self._get_engine(B, T_in, T_ref, max_iters, emt_only, constraint, style)
             masks = tower_masks(prenet_masks, i, row0, B)
             row0 += B

@@ -124,7 +124,8 @@ class Tacotron_emt_attn(Tacotron):
             T_ref = max([r.shape[1] for r in (ref_e, ref_s) if r is not None] or [1])
             tg = None
             if gta and tower_targets[i] is not None:
-                tg = tower_targets[i].reshape(B, -1, hp.num_mels)[:, hp.outputs_per_step - 1::hp.outputs_per_step]
+                # every target frame: the decode feeds targets[:, r-1::r] itself (helpers.py:78)
+                tg = tower_targets[i].reshape(B, -1, hp.num_mels)
             eng = self._get_emt_engine(B, T_in, T_ref, max_iters, emt_only, constraint, attn,
                                        ref_gru, n_lab)
             if tower_labels[i] is not None:

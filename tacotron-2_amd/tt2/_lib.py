@@ -45,7 +45,7 @@ class Config(ctypes.Structure):
             "max_T_in", "max_T_ref", "max_iters", "emt_attn", "emt_ref_gru", "n_emt", "style_mode",
             "predict_linear", "num_freq", "cbhg_kernels", "cbhg_conv_channels", "cbhg_pool_size",
             "cbhg_projection", "cbhg_projection_kernel_size", "cbhg_highwaynet_layers",
-            "cbhg_highway_units", "cbhg_rnn_units", "smoothing")]
+            "cbhg_highway_units", "cbhg_rnn_units", "smoothing", "outputs_per_step")]
 
 
 class WnConfig(ctypes.Structure):

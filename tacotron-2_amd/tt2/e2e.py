@@ -60,7 +60,8 @@ class TextToSpeech(object):
         self.hop = get_hop_size(hp)
         if int(np.prod(hp.upsample_scales)) != self.hop:
             raise ValueError("prod(upsample_scales) != hop_size")
-        self.wn = WaveNetEngine(hp, wn_weights, max_batch, max_iters * self.hop, device)
+        self.wn = WaveNetEngine(hp, wn_weights, max_batch, max_iters * hp.outputs_per_step * self.hop,
+                                device)
         self.lib = _lib.load_library()
 
     @property
@@ -79,7 +80,8 @@ class TextToSpeech(object):
         """ids_d [B,T_in] int32, lens_d [B] int32 (device) + lens_h (host copy), reference mels
         [B,T_ref,80] (device).  Returns dict(wav [B, T_f*hop] device tensor, lengths (host int
         array of mel frames per row), audio_lengths = lengths*hop, mel [B,n,80], stop [B,max_iters],
-        n_steps).  Everything between the two models stays on the device.  Injected randomness
+        n_steps = decoded frames, steps x outputs_per_step).  Everything between the two models stays
+        on the device.  Injected randomness
         (parity runs): prenet_masks_d [max_iters,2,B,P] uint8 keep bits; u_mix_d [>=T,B,10] and
         u_log_d [>=T,B] MoL uniforms for T = max(lengths)*hop samples (t-major, so a buffer sized
         for max_iters*hop serves any decoded length).  None = the device RNGs keyed by ``seed``."""
@@ -101,10 +103,11 @@ class TextToSpeech(object):
         hp = self.hp
         B, T_in = ids_d.shape
         mi = self.max_iters if max_iters is None else max_iters
+        r = hp.outputs_per_step                   # r frames per decoder step (tacotron.py:322-324)
         st = ctypes.c_void_p(stream)
         lens_h = np.ascontiguousarray(lens_h, np.int32)
-        mel = torch.empty((B, mi, hp.num_mels), dtype=torch.float32, device=dev)
-        stop = torch.empty((B, mi), dtype=torch.float32, device=dev)
+        mel = torch.empty((B, mi * r, hp.num_mels), dtype=torch.float32, device=dev)
+        stop = torch.empty((B, mi * r), dtype=torch.float32, device=dev)
         n = ctypes.c_int32()
         check(self.lib.tt2_synthesize_dev(
             self.taco.h, ids_d.data_ptr(), lens_d.data_ptr(), _lib.ptr(lens_h), B, T_in,
@@ -113,9 +116,9 @@ class TextToSpeech(object):
             0 if ref_spk_d is None else ref_spk_d.shape[1], mi,
             None if prenet_masks_d is None else prenet_masks_d.data_ptr(), seed, mel.data_ptr(),
             stop.data_ptr(), ctypes.byref(n), st))
-        n = n.value
+        n = n.value * r                           # decoded frames
         lengths_d = torch.empty((B,), dtype=torch.int32, device=dev)
-        check(self.lib.tt2_output_lengths_dev(stop.data_ptr(), B, n, mi, lengths_d.data_ptr(), st))
+        check(self.lib.tt2_output_lengths_dev(stop.data_ptr(), B, n, mi * r, lengths_d.data_ptr(), st))
         lengths = lengths_d.cpu().numpy()  # the one host round trip (on this stream): sizes WaveNet
         T_f = int(lengths.max()) if B else 0
         wav = torch.zeros((B, max(T_f, 0) * self.hop), dtype=torch.float32, device=dev)

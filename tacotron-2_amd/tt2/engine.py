@@ -61,8 +61,7 @@ def tacotron_config(hp, max_batch, max_T_in, max_T_ref, max_iters, emt_only=Fals
     cfg.synthesis_constraint = 1 if synthesis_constraint else 0
     cfg.constraint_monotonic = 1 if hp.synthesis_constraint_type == "monotonic" else 0
     cfg.attention_win_size = hp.attention_win_size
-    if hp.outputs_per_step != 1:
-        raise NotImplementedError("outputs_per_step (r) must be 1 on this build (hparams.py:140)")
+    cfg.outputs_per_step = hp.outputs_per_step     # r frames per decoder step (tacotron.py:322-324)
     cfg.smoothing = 1 if hp.smoothing else 0        # attention.py:71-80,150
     cfg.style_mode = STYLE_MODES.index(style_mode(hp, style))
     cfg.predict_linear = 1 if hp.predict_linear else 0    # CBHG post-net (tacotron.py:466-481)
@@ -97,16 +96,17 @@ def chunk_ranges(B, cap=MAX_CONTEXT_BATCH):
     return out
 
 
-def global_stop_steps(stop, stop_at_any):
+def global_stop_steps(stop, stop_at_any, r=1):
     """dynamic_decode's batch-level stop over the whole tower (TacoTestHelper, helpers.py:40-54):
-    the first step at which every row's stop probability rounds to 1 (round half to even as
-    tf.round); the step is emitted, so the decode keeps step + 1 frames.  stop_at_any has no effect
-    at r = 1: the helper's reduce_all over the batch axis of the [B, r] flags comes first, then
-    any (stop_at_any) / all over the step's r frames.  stop [B, n] -> n_steps (n when the rule never
-    fires)."""
+    finished = round(stop) [B, r] per step (round half to even as tf.round); reduce_all over the
+    batch axis first, then any (stop_at_any) / all over the step's r frames -- at r = 1 both are
+    "every row rounds to 1".  The stopping step is emitted, so the decode keeps step + 1 steps.
+    stop [B, n * r] -> n_steps (n when the rule never fires)."""
     fin = np.rint(np.asarray(stop, np.float32)) == 1.0
-    cond = fin.all(axis=0)
-    return int(np.argmax(cond)) + 1 if cond.any() else fin.shape[1]
+    B, nr = fin.shape
+    per_frame = fin.reshape(B, nr // r, r).all(axis=0)
+    cond = per_frame.any(axis=1) if stop_at_any else per_frame.all(axis=1)
+    return int(np.argmax(cond)) + 1 if cond.any() else nr // r
 
 
 class TacotronEngine(object):
@@ -211,8 +211,9 @@ class TacotronEngine(object):
         if masks is not None:
             masks = np.ascontiguousarray(masks[:max_iters])
         tg = f32(targets)
-        frames = np.zeros((B, max_iters, self.hp.num_mels), np.float32)
-        stop = np.zeros((B, max_iters), np.float32)
+        r = self.hp.outputs_per_step
+        frames = np.zeros((B, max_iters * r, self.hp.num_mels), np.float32)
+        stop = np.zeros((B, max_iters * r), np.float32)
         align = np.zeros((B, self._T_in, max_iters), np.float32)
         n = ctypes.c_int32()
         self._ok(self.lib.tt2_decode(self.h, max_iters, ptr(masks), seed, ptr(tg),
@@ -220,7 +221,7 @@ class TacotronEngine(object):
                                   ptr(align), ctypes.byref(n)))
         n = n.value
         self._n_steps = n
-        return frames[:, :n], stop[:, :n], align[:, :, :n]
+        return frames[:, :n * r], stop[:, :n * r], align[:, :, :n]
 
     def _decode_chunked(self, max_iters, prenet_masks, seed, targets):
         """Every chunk decodes max_iters steps (T_targets under GTA) without its own stop rule; the
@@ -238,11 +239,13 @@ class TacotronEngine(object):
             st.append(so)
             al.append(a)
         frames, stop, align = np.concatenate(fr), np.concatenate(st), np.concatenate(al)
-        n = frames.shape[1] if targets is not None else global_stop_steps(stop, self.hp.stop_at_any)
+        r = self.hp.outputs_per_step
+        n = (frames.shape[1] // r if targets is not None else
+             global_stop_steps(stop, self.hp.stop_at_any, r))
         self._n_steps = n
-        # each chunk decoded past the tower's stop step: postnet(None) takes these n frames
-        self._frames = np.ascontiguousarray(frames[:, :n])
-        return self._frames, stop[:, :n], align[:, :, :n]
+        # each chunk decoded past the tower's stop step: postnet(None) takes these n·r frames
+        self._frames = np.ascontiguousarray(frames[:, :n * r])
+        return self._frames, stop[:, :n * r], align[:, :, :n]
 
     def zero_state(self):
         """TacotronDecoderCell.zero_state (Architecture_wrappers.py:158-195) for the batch of the last
@@ -256,7 +259,8 @@ class TacotronEngine(object):
     def decoder_step(self, frame_in, prenet_masks, state):
         """tt2_decoder_step: one TacotronDecoderCell.__call__ (Architecture_wrappers.py:197-267)
         on the memory of the last encode.  frame_in [B,80], prenet_masks [2,B,P] uint8, state as
-        zero_state() returns.  Returns (frame [B,80], stop [B], alignments [B,T_in], next_state)."""
+        zero_state() returns.  Returns (frame [B,80], stop [B], alignments [B,T_in], next_state).
+        outputs_per_step = 1 only (r > 1 decodes through decode())."""
         B, T = self._B, self._T_in
         P = self.hp.prenet_layers[0]
         fi = f32(frame_in)
