@@ -8,7 +8,8 @@ import numpy as np
 NAMES = ["start", "ATT P1 waited", "dctx", "granules out", "E taken", "dq", "Q published",
          "off-chain done (step end)", "CELL2 waited", "G2 published", "P2 published", "CELL1 waited",
          "G1 published", "P1 published", "PROD2 polled", "PROD2 loads", "PROD2 staged", "PROD2 mfma",
-         "PROD1 polled", "PROD1 loads", "PROD1 staged", "PROD1 mfma", "CELL1 loads", "CELL1 cell"]
+         "PROD1 polled", "PROD1 loads", "PROD1 staged", "PROD1 mfma", "CELL1 loads", "CELL1 cell",
+         "prefetch issued", "off-chain G", "off-chain M + barrier"]
 s = np.fromfile(sys.argv[1], dtype=np.int64).reshape(256, 32)
 r = (s - s[:, 0][s[:, 0] != 0].min()) * 0.01
 for i, n in enumerate(NAMES):

@@ -131,7 +131,7 @@ struct tt2_train_ctx {
   DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps, tpKWT;
   bool tp_on = false, tp_last = false, tp_check = false;
   // persistent backward (train_bwd_persist.hip): exchange buffers, flags + control words
-  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl, tbW1F;
+  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl, tbW1F, tbPK;
   bool tb_on = false, tb_last = false, tb_check = false;
   int* tb_ctl_dev = nullptr;
   int* tp_ctl_dev = nullptr;  // control words of the last persistent forward (device)
@@ -2915,6 +2915,12 @@ static void tr_persist_forward(tt2_train_ctx* c, const TrAtt& at, const uint8_t*
   a.G1 = c->G1.as<float>(); a.G2 = c->G2.as<float>(); a.CN1 = c->CN1.as<float>(); a.CN2 = c->CN2.as<float>();
   a.C1 = c->C1.as<float>(); a.C2 = c->C2.as<float>(); a.ALIGN = at.ALIGN; a.CUM = at.CUM; a.TH = at.TH;
   a.FALL = at.FALL; a.ALN = at.ALN;
+  // the persistent backward's packed unit operands (train_persist.h TpArgs::BPK), when it will run
+  a.BPK = nullptr;
+  if (c->tb_on && Tin <= TB_TMAX) {
+    grow(c->tbPK, (size_t)T * TP_NB * 4 * TP_NT * 4 * sizeof(float));
+    a.BPK = c->tbPK.as<float>();
+  }
   a.CX = c->tpCX.as<__bf16>(); a.H1X = c->tpH1X.as<__bf16>(); a.Z1X = c->tpZ1X.as<__bf16>();
   a.H2X = c->tpH2X.as<__bf16>(); a.Z2X = c->tpZ2X.as<__bf16>();
   a.EX = c->tpEX.as<unsigned long long>();
@@ -2997,10 +3003,11 @@ static void tr_persist_backward(tt2_train_ctx* c, const TrAtt& at, const uint8_t
   TbArgs a{};
   a.B = B; a.T = T; a.Tin = Tin; a.NT = NT; a.z = c->cfg.zoneout;
   a.K1T = c->hK1T.as<__bf16>(); a.K2T = c->hK2T.as<__bf16>(); a.Wq = c->hWq.as<__bf16>();
-  a.va = at.va; a.KWT = c->tpKWT.as<float>(); a.values16 = at.values16; a.lens = at.lens; a.zm = zm;
+  a.va = at.va; a.KWT = c->tpKWT.as<float>(); a.values16 = at.values16; a.lens = at.lens;
   a.ALN = at.ALN; a.CUM = at.CUM; a.TH = at.TH;
-  a.G1 = c->G1.as<float>(); a.G2 = c->G2.as<float>(); a.CN1 = c->CN1.as<float>(); a.CN2 = c->CN2.as<float>();
-  a.C1 = c->C1.as<float>(); a.C2 = c->C2.as<float>(); a.dPIN = c->dPIN.as<float>();
+  TT2_CHECK(c->tbPK.bytes >= (size_t)T * TP_NB * 4 * TP_NT * 4 * sizeof(float), TT2_ERR_STATE,
+            "persistent backward: the forward did not pack the unit operands");
+  a.BPK = c->tbPK.as<float>(); a.dPIN = c->dPIN.as<float>();
   a.dG1 = c->dG1.as<float>(); a.dG2 = c->dG2.as<float>(); a.DQ = c->DQ.as<float>(); a.DCTX = c->DCTX.as<float>();
   a.DKEYS = c->DKEYS.as<float>(); a.dV = c->dV.as<float>(); a.dBA = c->dBA.as<float>(); a.DWGP = c->DWGP.as<float>();
   a.G1X = c->tbG1X.as<__bf16>(); a.G2X = c->tbG2X.as<__bf16>(); a.P1X = c->tbP1X.as<float>();

@@ -30,9 +30,9 @@ struct TbArgs {
   const float* KWT;          // [A][32] (tp_prepare): [a][tap] = (Kc·W_loc)[tap][a] for tap < KW
   const __bf16* values16;    // [B][Tin][D] bf16
   const int* lens;           // [B]
-  const uint8_t* zm;         // [T][4][B][H] zoneout keep bits or null
+  const float* BPK;          // [T][TP_NB][4][TP_NT][4] the unit operands the persistent forward packed (TpArgs::BPK)
   // forward slots (train.hip layout)
-  const float *ALN, *CUM, *TH, *G1, *G2, *CN1, *CN2, *C1, *C2;
+  const float *ALN, *CUM, *TH;
   const float* dPIN;         // [T][B][H + D] d [h2 | ctx] from the frame / stop projections
   // outputs
   float *dG1, *dG2;          // [T][B][4H]

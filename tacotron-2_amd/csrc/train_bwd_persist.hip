@@ -67,7 +67,7 @@ constexpr int TBL_SC = TBL_DQ + 32;             // [16] reduction scratch, then 
 constexpr int TBL_CELL = TBL_SC + 32;           // [17][256] the unit role's cell operands of the step
 constexpr int TBL_DU = TBL_CELL + 17 * 256;     // [TM][34] du of the own dims (kept to the end of the step)
 constexpr int TBL_U = TBL_DU + TB_TM * TB_DUS;  // union: M [TM][33] / PROD {A 32 KB, then out [64][132]}
-constexpr int TBL_U_SZ = (TB_TM * 33 > 64 * TB_OS) ? TB_TM * 33 : 64 * TB_OS;
+constexpr int TBL_U_SZ = ((TB_TM + 32) * 33 > 64 * TB_OS) ? (TB_TM + 32) * 33 : 64 * TB_OS;
 constexpr int TBL_VAL = TBL_U + TBL_U_SZ;       // [NPT tiles][8 k-steps][64 lanes] bf16 x 8: the values quarter
 constexpr int TBL_END = TBL_VAL + TB_NPT * 8 * 64 * 4;
 static_assert(TBL_U % 4 == 0 && TBL_VAL % 4 == 0 && TBL_DCH % 4 == 0 && 64 * TB_OS >= 8192,
@@ -86,6 +86,10 @@ __device__ __forceinline__ float tb_block_sum(float v, float* scr) {
   for (int i = 1; i < TB_NW; ++i) r += scr[i];
   return r;
 }
+// work-group barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier, WITHOUT
+// the vmcnt(0) that __syncthreads()' release fence adds -- the HBM loads issued ahead (the next step's
+// operands, the tanh tiles) stay in flight across it
+__device__ __forceinline__ void tb_lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // sum over the 16 lanes of each lane row (xor within the low 4 lane bits)
 __device__ __forceinline__ float tb_row16_sum(float v) {
 #pragma unroll
@@ -106,21 +110,6 @@ __device__ __forceinline__ tp_bf8 tb_bf8(const float (&x)[8]) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = (__bf16)x[e];
   return v;
-}
-// split-bf16 halves of 8 floats: hi = bf16(x), lo = bf16(x - hi) (hi + lo within ~2^-17 of x)
-__device__ __forceinline__ void tb_split8(const float (&x)[8], tp_bf8& hi, tp_bf8& lo) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    hi[e] = (__bf16)x[e];
-    lo[e] = (__bf16)(x[e] - (float)hi[e]);
-  }
-}
-// a ≈ A·B in fp32 from split-bf16 operands: Ah·Bh + Ah·Bl + Al·Bh (the Al·Bl term is below 2^-16)
-__device__ __forceinline__ tp_f4 tb_mfma3(const tp_bf8& ah, const tp_bf8& al, const tp_bf8& bh, const tp_bf8& bl,
-                                          tp_f4 acc) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
 }
 // byte offset of (N-block nb, unit group m4 = 4-output group inside the block, K-block kb, row, e) in the
 // unit-major partial layout [nb][m4][kb][row][4] (one parity): a unit work-group's 16 K-block partials of
@@ -168,7 +157,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
   int* const sfail = reinterpret_cast<int*>(sm + TBL_SC + 16);
   float* const cel = sm + TBL_CELL;
   float* const dus = sm + TBL_DU;                    // ATT phase .. end of the step
-  float* const ms = sm + TBL_U;                      // end of the step
+  float* const ms = sm + TBL_U + 16 * 33;            // end of the step: M rows, 16 zero rows either side
   float* const stA = sm + TBL_U;                     // PROD phase: 32 A blocks of 1 KB
   float* const stO = sm + TBL_U;                     // PROD phase, after the products: [64][TB_OS] outputs
   tp_bf8* const valf = reinterpret_cast<tp_bf8*>(sm + TBL_VAL);
@@ -224,18 +213,17 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
     wqb[ks] = jl < 4 ? *reinterpret_cast<const tp_bf8*>(a.Wq + (long)(4 * g + jl) * A + 32 * ks + 8 * g4) : tp_bf8{};
-  // KW (the location conv folded through W_loc) as split-bf16 B fragments of the location-conv
-  // backward M = du·KW over the own 32 dims: tap tile nt, lane holds KW[dim 32 sq + 8 g4 + e][tap 16 nt + jl]
+  // KW (the location conv folded through W_loc) as fp32 B fragments of the location-conv backward M = du·KW over
+  // the own 32 dims (v_mfma_f32_16x16x4f32): tap tile nt, k-step k, lane holds KW[dim 32 sq + 4 k + g4][tap 16 nt + jl]
   // (tap 31, the bias column, zero)
-  tp_bf8 kwh[2], kwl[2];
+  float kwf[2][8];
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int tap = 16 * nt + jl;
-    float x[8];
+  for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] = (arow && tap < 31) ? a.KWT[(32 * sq + 8 * g4 + e) * 32 + tap] : 0.f;
-    tb_split8(x, kwh[nt], kwl[nt]);
-  }
+    for (int k = 0; k < 8; ++k) {
+      const int tap = 16 * nt + jl;
+      kwf[nt][k] = (arow && tap < 31) ? a.KWT[(32 * sq + 4 * k + g4) * 32 + tap] : 0.f;
+    }
   // v_a of the lane's dims 16 mt + 4 g4 + i (energy-tile layout, as the forward)
   float vav[8];
 #pragma unroll
@@ -260,6 +248,32 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
   const bool erow = er < B;
   const int evo = er * H + en;
   float dc1 = 0.f, dc2 = 0.f, rr1 = 0.f, rr2 = 0.f;
+  // The step's HBM operands (the unit role's cell operands of both layers, the attention row's align /
+  // cum / d PIN ctx) are loaded one step AHEAD, at the start of the previous step's off-chain window
+  // (LDS and MFMA work only, no global load waits there), and parked at the step's start: with vmcnt
+  // in order, an HBM load issued in the step would hold every later poll and exchange load behind it
+  // The cell operands come from the forward's packed copy (TpArgs::BPK: four coalesced 16-byte loads per
+  // thread instead of 16 scattered dwords, 4x fewer bytes than the [T][B][4H] slots would fetch).
+  tp_f4 cq[4];
+  float cvd = 0.f, paj = 0.f, pcum = 0.f, pdctx = 0.f;
+  auto prefetch = [&](int tt) {
+    const long tbb = (long)tt * B;
+    if (erow) {
+      const auto rp = tp_rsrc(a.BPK + ((long)tt * TP_NB + g) * 4 * TP_NT * 4);
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+        cq[k4] = __builtin_bit_cast(tp_f4, __builtin_amdgcn_raw_buffer_load_b128(rp, (k4 * TP_NT + tid) * 16, 0, 0));
+      cvd = tb_lg(a.dPIN + tbb * (H + D), (er * (H + D) + en) * 4);
+    }
+    if (arow) {
+      const long rt = (tbb + rb) * Tin;
+      const int tc = min(tid, Tin - 1);  // clamped: unconditional loads
+      paj = tb_lg(a.ALN + rt, tc * 4);
+      pcum = tb_lg(a.CUM + rt, tc * 4);
+      pdctx = tb_lg(a.dPIN + (tbb + rb) * (H + D) + H + 256 * sq, tid * 4);
+    }
+  };
+  prefetch(T - 1);
   __syncthreads();
 
   // product partial of (kb, nb): the K-block of dG (bf16 exchange rows X, parity par) staged in LDS in
@@ -355,48 +369,35 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
     long long* const stp = t == a.stamp_step ? a.stamps : nullptr;
     asm volatile("" ::: "memory");
     TB_STAMP(0);
-    // ---- the unit role's operands of both cells (HBM), loaded at the start of the step and parked in
-    // LDS ([17][256], thread-private columns) once they land: no load of them waits behind a poll later
-    float cv[17];
-    if (erow) {
-      const int go = (er * K4 + en) * 4;
-      const float* g2 = a.G2 + tb * K4;
-      const float* g1 = a.G1 + tb * K4;
+    // ---- park the prefetched operands of step t (landed during the previous step's off-chain work):
+    // the unit role's in LDS ([17][256], thread-private columns), the attention row's in registers
+    if (erow) {  // slots 0-7 layer 2 (i j f o c_new c_prev kc kh), 8-15 layer 1, 16 d PIN (h part)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        cv[q] = tb_lg(g2, go + q * H * 4);
-        cv[8 + q] = tb_lg(g1, go + q * H * 4);
-      }
-      cv[4] = tb_lg(a.CN2 + tb * H, evo * 4);
-      cv[5] = tb_lg(a.C2 + tb * H, evo * 4);
-      cv[12] = tb_lg(a.CN1 + tb * H, evo * 4);
-      cv[13] = tb_lg(a.C1 + tb * H, evo * 4);
-      cv[16] = tb_lg(a.dPIN + tb * (H + D), (er * (H + D) + en) * 4);
-      if (a.zm) {
-        const auto rz = tp_rsrc(a.zm + (long)t * 4 * B * H);
-        const int zs = B * H;
-        cv[14] = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 0, 0);
-        cv[15] = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, zs, 0);
-        cv[6] = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 2 * zs, 0);
-        cv[7] = (float)__builtin_amdgcn_raw_buffer_load_b8(rz, evo, 3 * zs, 0);
-      } else {
-        cv[6] = cv[7] = cv[14] = cv[15] = 1.f - a.z;
-      }
+      for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cel[(4 * k4 + e) * 256 + tid] = cq[k4][e];
+      cel[16 * 256 + tid] = cvd;
     }
-    auto park = [&] {
-      if (erow)
-#pragma unroll
-        for (int k = 0; k < 17; ++k) cel[k * 256 + tid] = cv[k];
-    };
     // ================= ATT
-    if (!arow) park();
     if (arow) {
       const long rt = (tb + rb) * Tin;  // this row's [Tin] block of step t
-      const int tc = min(tid, Tin - 1);  // clamped: unconditional loads (no vmcnt(0) at a branch join)
-      float aj = tb_lg(a.ALN + rt, tc * 4);
-      float cumv = tb_lg(a.CUM + rt, tc * 4);
+      float aj = paj, cumv = pcum;
       // d ctx of channel 256 sq + tid = d PIN + Σ_kb P1_{t+1} (wave w: the N-block 2 sq + (w >> 1))
-      float dctx = tb_lg(a.dPIN + (tb + rb) * (H + D) + H + 256 * sq, tid * 4);
+      float dctx = pdctx;
+      // tanh of the own dims for the softmax / du stage, issued with the d align granules: the HBM latency
+      // runs under the quarter exchange
+      tp_f4 th[TB_PTW][2];
+      auto load_th = [&] {
+        const auto rth = tp_rsrc(a.TH + rt * A);
+#pragma unroll
+        for (int r = 0; r < TB_PTW; ++r) {
+          const int j = min(16 * (w + 4 * r) + jl, Tin - 1);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+            th[r][mt] = __builtin_bit_cast(tp_f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rth, (j * A + 32 * sq + 16 * mt + 4 * g4) * 4, 0, 0));
+        }
+      };
       if (!first) {
         const int nbw = 2 * sq + (w >> 1);
         if (!tb_poll(a, TB_PH_P1, TB_NKB, tagn, [&](int l) { return 16 * l + nbw; })) sfail[0] = 1;
@@ -408,7 +409,6 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
 #pragma unroll
         for (int k = 0; k < TB_NKB; ++k) dctx += pv[k];
       }
-      park();
       if (tid >= Tin) aj = cumv = 0.f;
       tp_bst(a.DCTX + (tb + rb) * D + 256 * sq, tid * 4, 0, dctx);
       {  // split-bf16 halves of d ctx: the B columns 0 (hi) and 1 (lo) of the d align product
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         dch[256 + tid] = (__bf16)(dctx - (float)hi);
       }
       if (tid < Tin) cum_s[15 + tid] = cumv;
-      __syncthreads();
+      tb_lds_bar();
       TB_STAMP(2);
       if (sfail[0]) return;
       // d align partial of the own channels: values quarter · (hi, lo) of d ctx on v_mfma_f32_16x16x32_bf16
@@ -428,27 +428,39 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
           const tp_bf8 v = *reinterpret_cast<const tp_bf8*>(dch + (jl == 1 ? 256 : 0) + 32 * ks + 8 * g4);
           bfr[ks] = jl < 2 ? v : tp_bf8{};
         }
+        // the wave's position tiles interleaved k-step-major (each fragment read has the other tiles' MFMAs
+        // to hide behind); a wave without a third tile recomputes the last one (identical values, and rows
+        // past Tin are zero fragments: no branches)
+        tp_f4 acc[TB_PTW];
+#pragma unroll
+        for (int r = 0; r < TB_PTW; ++r) acc[r] = tp_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+          for (int r = 0; r < TB_PTW; ++r) {
+            const int pt = min(w + 4 * r, TB_NPT - 1);
+            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(valf[(pt * 8 + ks) * 64 + lane], bfr[ks], acc[r], 0, 0, 0);
+          }
+        // column 0 (hi) + column 1 (lo) of each row: DPP row_shl:1 brings lane jl + 1 to lane jl
 #pragma unroll
         for (int r = 0; r < TB_PTW; ++r) {
-          const int pt = w + 4 * r;
-          if (16 * pt >= Tin) break;  // wave-uniform
-          tp_f4 acc = {0.f, 0.f, 0.f, 0.f};
+          const int j0 = 16 * min(w + 4 * r, TB_NPT - 1) + 4 * g4;
+          tp_f4 lo;
 #pragma unroll
-          for (int ks = 0; ks < 8; ++ks)
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(valf[(pt * 8 + ks) * 64 + lane], bfr[ks], acc, 0, 0, 0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float lo = __shfl(acc[i], lane + 1, 64);
-            const int j = 16 * pt + 4 * g4 + i;
-            if (jl == 0 && j < Tin) ep[j] = acc[i] + lo + ds[j];
+          for (int i = 0; i < 4; ++i)
+            lo[i] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc[r][i]), 0x101, 0xf, 0xf, false));
+          if (jl == 0) {
+            const tp_f4 d4 = *reinterpret_cast<const tp_f4*>(ds + j0);
+            *reinterpret_cast<tp_f4*>(ep + j0) = acc[r] + lo + d4;
           }
         }
       }
-      __syncthreads();
+      tb_lds_bar();
       // granules of the own partial, then the other quarters' (summed in quarter order)
       if (tid < Tin)
         __builtin_amdgcn_raw_buffer_store_b64(tp_u2{__float_as_uint(ep[tid]), tag},
                                               tp_rsrc(a.EX + (((long)par * 64 + rb) * 4 + sq) * TM), tid * 8, 0, 16);
+      load_th();  // HBM latency under the quarter exchange
       TB_STAMP(3);
       if (w < (Tin + 63) / 64) {
         const bool act = tid < Tin;
@@ -479,19 +491,6 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
       __syncthreads();
       TB_STAMP(4);
       if (sfail[0]) return;
-      // tanh of the own dims (loaded here: they would hold 24 registers across the whole phase)
-      tp_f4 th[TB_PTW][2];
-      {
-        const auto rth = tp_rsrc(a.TH + rt * A);
-#pragma unroll
-        for (int r = 0; r < TB_PTW; ++r) {
-          const int j = min(16 * (w + 4 * r) + jl, Tin - 1);
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt)
-            th[r][mt] = __builtin_bit_cast(tp_f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      rth, (j * A + 32 * sq + 16 * mt + 4 * g4) * 4, 0, 0));
-        }
-      }
       // softmax backward (attention.py:218): de_j = a_j (d a_j - Σ_k a_k d a_k), 0 past the length
       const float dav = tid < Tin ? da_s[tid] : 0.f;
       const float ssum = tb_block_sum(aj * dav, scr);
@@ -549,7 +548,6 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         dq_s[tid] = q;
         dba += q;
         dva += v;
-        tp_bst(a.DQ + (tb + rb) * A + 32 * sq, tid * 4, 0, q);
       }
       __syncthreads();
       TB_STAMP(5);
@@ -561,6 +559,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         tp_st16(a.DQX, (int)(((long)par * 64 * A + tp_afl(rb, 32 * sq + 8 * tid, A)) * 2), v);
       }
       tp_publish(a, TB_PH_Q, tag);
+      if (tid < 32) tp_bst(a.DQ + (tb + rb) * A + 32 * sq, tid * 4, 0, dq_s[tid]);
       TB_STAMP(6);
     }
     // ================= CELL2: d hz2 from step t+1's product, d h2 from the dq rows of all quarters: both waits
@@ -573,12 +572,19 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
     {
       // d h2 of (row, own unit) = dq[row]·Wq[unit]^T: wave w's row tile (rows 16 w ..) on one MFMA chain,
       // the 4 unit columns moved to the cell threads (row 16 w + (lane >> 2), unit lane & 3)
+      // the P2_{t+1} partials of d hz2 go out with the dq rows: one round trip for both
       float dh2;
+      float pv[TB_NKB];
       {
         const auto rq = tp_rsrc(a.DQX + (long)par * 64 * A);
         tp_bf8 af[4];
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) af[ks] = tp_ldx4<true>(rq, ((lane & 15) * 32 + 8 * (lane >> 4)) * 2, (w * 4 + ks) * 1024);
+        if (erow && !first) {
+          const auto rp = tp_rsrc(a.P2X + (long)parn * TB_PSTRIDE);
+#pragma unroll
+          for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rp, tb_uoff(8 + (g >> 5), g & 31, k, er, eu));
+        }
         tp_wait(af);
         tp_f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -592,11 +598,6 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
       }
       float d[4] = {0.f, 0.f, 0.f, 0.f};
       if (erow) {
-        float pv[TB_NKB];
-        const auto rp = tp_rsrc(a.P2X + (long)parn * TB_PSTRIDE);
-        if (!first)
-#pragma unroll
-          for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rp, tb_uoff(8 + (g >> 5), g & 31, k, er, eu));
         float c[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) c[k] = cel[k * 256 + tid];
@@ -608,8 +609,6 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         }
         const float dext = cel[16 * 256 + tid] + dh2;
         tb_cell_bwd(c, dext, dhz2, dc2, rr2, d);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) tp_bst(a.dG2 + tb * K4, (er * K4 + en + q * H) * 4, 0, d[q]);
       }
       // bf16 exchange row: the 4 units of (row er, gate q) are 4 adjacent tb_kperm positions (the quad
       // of lanes of row er shares erow, so the shuffles stay inside active quads)
@@ -626,8 +625,13 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
           tp_st8(a.G2X, (int)(((long)par * 64 * K4 + tp_afl(er, p0 + 64 * q, K4)) * 2),
                  tp_u2{tp_pack(v[q][0], v[q][1]), tp_pack(v[q][2], v[q][3])});
       }
+      tp_publish(a, TB_PH_G2, tag);
+      // the fp32 dG2 slot (read after the launch) behind the publish: its scattered stores drain at the
+      // next publish instead of holding this one
+      if (erow)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tp_bst(a.dG2 + tb * K4, (er * K4 + en + q * H) * 4, 0, d[q]);
     }
-    tp_publish(a, TB_PH_G2, tag);
     TB_STAMP(9);
     // ================= PROD2: [d h1 | d hz2_{t-1}] partial of (kb, nb)
     product(a.G2X, w2f, nullptr, a.P2X, false, TB_PH_G2, par, tag, stp, 14);
@@ -669,8 +673,6 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         }
         tb_cell_bwd(c, dh1, dhz1, dc1, rr1, d);
         if (stp && tid == 0) stp[g * 32 + 23] = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-        for (int q = 0; q < 4; ++q) tp_bst(a.dG1 + tb * K4, (er * K4 + en + q * H) * 4, 0, d[q]);
       }
       const int src = lane & ~3;
       float v[4][4];
@@ -685,8 +687,11 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
           tp_st8(a.G1X, (int)(((long)par * 64 * K4 + tp_afl(er, p0 + 64 * q, K4)) * 2),
                  tp_u2{tp_pack(v[q][0], v[q][1]), tp_pack(v[q][2], v[q][3])});
       }
+      tp_publish(a, TB_PH_G1, tag);
+      if (erow)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tp_bst(a.dG1 + tb * K4, (er * K4 + en + q * H) * 4, 0, d[q]);
     }
-    tp_publish(a, TB_PH_G1, tag);
     TB_STAMP(12);
     // ================= PROD1: [d ctx_{t-1} | d hz1_{t-1}] partial of (kb, nb)
     product(a.G1X, w2f, w1g, a.P1X, nb < TB_NNB / 2, TB_PH_G1, par, tag, stp, 18);
@@ -694,47 +699,54 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
     if (sfail[0]) return;
     tp_publish(a, TB_PH_P1, tag);
     TB_STAMP(13);
+    if (t > 0) prefetch(t - 1);
+    TB_STAMP(24);
     if (arow) {
-      // ---- off the chain (the step's wait for the next P1 is the idle slot): d W_loc accumulators and the location-conv backward of the own dims, both on
-      // split-bf16 v_mfma_f32_16x16x32_bf16 (three products: ~fp32)
-      {  // G^T[a][tap] += Σ_j du[j][a]·cum_t[j + tap - 15]: wave w -> dim tile w >> 1, tap tile w & 1
+      // ---- off the chain: d W_loc accumulators and the location-conv backward of the own dims, both on
+      // fp32 v_mfma_f32_16x16x4f32 (exact products, operands straight from LDS)
+      {  // G^T[a][tap] += Σ_j du[j][a]·cum_t[j + tap - 15]: wave w -> dim tile w >> 1, tap tile w & 1; K = the
+         // positions, 4 per MFMA (rows past Tin of du and cum are zero), 4 accumulation chains
         const int mt = w >> 1, nt = w & 1;
-        const int nks = (Tin + 31) >> 5;
-        for (int ks = 0; ks < nks; ++ks) {
-          float xa[8], xb[8];
+        const int nk16 = (Tin + 15) >> 4;
+        tp_f4 gq[4] = {};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int j = 32 * ks + 8 * g4 + e;
-            xa[e] = j < Tin ? dus[j * TB_DUS + 16 * mt + jl] : 0.f;
-            xb[e] = cum_s[j + 16 * nt + jl];
+        for (int k16 = 0; k16 < TB_NPT; ++k16) {
+          if (k16 >= nk16) break;  // wave-uniform
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int j = 16 * k16 + 4 * q + g4;
+            gq[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(dus[j * TB_DUS + 16 * mt + jl], cum_s[j + 16 * nt + jl], gq[q],
+                                                         0, 0, 0);
           }
-          tp_bf8 ah, al, bh, bl;
-          tb_split8(xa, ah, al);
-          tb_split8(xb, bh, bl);
-          gacc = tb_mfma3(ah, al, bh, bl, gacc);
         }
+        gacc += (gq[0] + gq[1]) + (gq[2] + gq[3]);
       }
+      TB_STAMP(25);
 #pragma unroll
-      for (int q6 = 0; q6 < 2 * TB_PTW; ++q6) {  // M tiles (position tile, tap tile) = w + 4 q6
+      for (int q6 = 0; q6 < 2 * TB_PTW; ++q6) {  // M tiles (position tile, tap tile) = w + 4 q6, K = the 32 own dims
         const int idx = w + 4 * q6, pt = idx >> 1, nt = idx & 1;
         if (16 * pt >= Tin) continue;  // wave-uniform
-        float xa[8];
+        tp_f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) xa[e] = dus[(16 * pt + jl) * TB_DUS + 8 * g4 + e];
-        tp_bf8 ah, al;
-        tb_split8(xa, ah, al);
-        const tp_f4 acc = tb_mfma3(ah, al, kwh[nt], kwl[nt], tp_f4{0.f, 0.f, 0.f, 0.f});
+        for (int k = 0; k < 8; ++k)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dus[(16 * pt + jl) * TB_DUS + 4 * k + g4], kwf[nt][k], acc, 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) ms[(16 * pt + 4 * g4 + i) * 33 + 16 * nt + jl] = acc[i];
       }
-      __syncthreads();
-      if (tid < Tin) {  // d cum_t[i] += Σ_tap M[i - tap + 15][tap] (4 independent chains)
+      {  // the zero pad rows of the diagonal sum (the product staging shares the region)
+        const int r1 = 16 * ((Tin + 15) >> 4);
+        for (int e = tid; e < 32 * 33; e += TP_NT) {
+          const int r = e / 33, c = e - 33 * r;
+          ms[(r < 16 ? r - 16 : r1 + r - 16) * 33 + c] = 0.f;
+        }
+      }
+      tb_lds_bar();
+      TB_STAMP(26);
+      if (tid < Tin) {  // d cum_t[i] += Σ_tap M[i - tap + 15][tap] (4 independent chains; rows -16.. and
+                        // past the tiles are the zero pad, tap 31 the zero column: no conditions)
         float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int tap = 0; tap < 32; ++tap) {
-          const int jj = tid - tap + 15;
-          if (tap < 31 && jj >= 0 && jj < Tin) v[tap & 3] += ms[jj * 33 + tap];
-        }
+        for (int tap = 0; tap < 32; ++tap) v[tap & 3] += ms[(tid - tap + 15) * 33 + tap];
         ds[tid] += (v[0] + v[1]) + (v[2] + v[3]);
       }
     }

@@ -47,6 +47,10 @@ struct TpArgs {
   // exchange buffers, [2 parities][64 x K] bf16 in A-fragment layout; granules [2][64][4][TMAX]
   __bf16 *CX, *H1X, *Z1X, *H2X, *Z2X;
   unsigned long long* EX;
+  // the persistent backward's unit operands, or null: [T][TP_NB][4][TP_NT][4] floats, thread (row er, unit 4g + eu)
+  // of work-group g: [layer-2 i j f o | c_new c_prev kc kh | layer-1 i j f o | c_new c_prev kc kh] (activated
+  // gates, the carried c before the step, the zoneout keep factors) -- one coalesced 16-byte store per quad
+  float* BPK;
   long long* stamps;         // [TP_NB][32] s_memrealtime stage stamps of step stamp_step (diagnostic) or null
   int stamp_step;
   unsigned* flags;           // [3 phases][TP_NREP][TP_NB] step tags (zeroed before the launch)

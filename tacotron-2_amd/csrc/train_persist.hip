@@ -352,6 +352,16 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
     }
   };
 
+  // the backward's packed unit operands of one layer (TpArgs::BPK): quads k4, k4 + 1 of this thread
+  auto bpk_store = [&](int t, int k4, const Cell& o, float cp, float kc, float kh) {
+    const auto rp = tp_rsrc(a.BPK + ((long)t * TP_NB + g) * 4 * TP_NT * 4);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        tp_u4{__float_as_uint(o.si), __float_as_uint(o.tj), __float_as_uint(o.sf), __float_as_uint(o.so)}, rp,
+        (k4 * TP_NT + tid) * 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        tp_u4{__float_as_uint(o.cn), __float_as_uint(cp), __float_as_uint(kc), __float_as_uint(kh)}, rp,
+        ((k4 + 1) * TP_NT + tid) * 16, 0, 0);
+  };
 #define TP_STAMP(i)                                                         \
   do {                                                                      \
     if (stp && tid == 0) stp[g * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
@@ -406,6 +416,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
         tp_bst(a.C1 + (tb + B) * H, evo * 4, 0, o.cz);
         tp_bst(a.X2 + tb * 2 * H, (er * 2 * H + en) * 4, 0, o.hn);
         tp_bst(a.X1 + (tb + B) * LX1, (er * LX1 + P + D + en) * 4, 0, o.hz);
+        if (a.BPK) bpk_store(t, 2, o, c1, a.zm ? kc1 : 1.f - a.z, a.zm ? kh1 : 1.f - a.z);
         c1 = o.cz;
         hz1 = o.hz;
       }
@@ -439,6 +450,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
         tp_bst(a.C2 + (tb + B) * H, evo * 4, 0, o.cz);
         tp_bst(a.PIN + tb * (H + D), (er * (H + D) + en) * 4, 0, o.hn);
         tp_bst(a.X2 + (tb + B) * 2 * H, (er * 2 * H + H + en) * 4, 0, o.hz);
+        if (a.BPK) bpk_store(t, 0, o, c2, a.zm ? kc2 : 1.f - a.z, a.zm ? kh2 : 1.f - a.z);
         c2 = o.cz;
         hz2 = o.hz;
       }
