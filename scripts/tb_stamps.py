@@ -6,7 +6,7 @@ import sys
 import numpy as np
 
 NAMES = ["start", "ATT P1 waited", "dctx", "granules out", "E taken", "dq", "Q published",
-         "off-chain done (step end)", "CELL2 waited", "G2 published", "P2 published", "CELL1 waited",
+         "step end", "CELL2 waited", "G2 published", "P2 published", "CELL1 waited",
          "G1 published", "P1 published", "PROD2 polled", "PROD2 loads", "PROD2 staged", "PROD2 mfma",
          "PROD1 polled", "PROD1 loads", "PROD1 staged", "PROD1 mfma", "CELL1 loads", "CELL1 cell",
          "prefetch issued", "off-chain G", "off-chain M + barrier"]

@@ -62,9 +62,10 @@ constexpr int TBL_DA = TBL_EP + TB_TM;          // [TM] d align, then de
 constexpr int TBL_DS = TBL_DA + TB_TM;          // [TM] running d cum partial of the own dims
 constexpr int TBL_CUM = TBL_DS + TB_TM;         // [TM + 64] cum_t at +15, zero padded
 constexpr int TBL_RED = TBL_CUM + TB_TM + 64;   // [2][TB_NW][32] wave partials of dq / d v_a
-constexpr int TBL_DQ = TBL_RED + 2 * TB_NW * 32;  // [32] dq
-constexpr int TBL_SC = TBL_DQ + 32;             // [16] reduction scratch, then ints
-constexpr int TBL_CELL = TBL_SC + 32;           // [17][256] the unit role's cell operands of the step
+constexpr int TBL_SC = TBL_RED + 2 * TB_NW * 32;  // [32] flags (ints)
+constexpr int TBL_AL = TBL_SC + 32;             // [TM] the step's alignments a_j
+constexpr int TBL_PA = TBL_AL + TB_TM;          // [TM] a_j · d a_j (the softmax backward's sum)
+constexpr int TBL_CELL = TBL_PA + TB_TM;        // [17][256] the unit role's cell operands of the step
 constexpr int TBL_DU = TBL_CELL + 17 * 256;     // [TM][34] du of the own dims (kept to the end of the step)
 constexpr int TBL_U = TBL_DU + TB_TM * TB_DUS;  // union: M [TM][33] / PROD {A 32 KB, then out [64][132]}
 constexpr int TBL_U_SZ = ((TB_TM + 32) * 33 > 64 * TB_OS) ? (TB_TM + 32) * 33 : 64 * TB_OS;
@@ -75,25 +76,20 @@ static_assert(TBL_U % 4 == 0 && TBL_VAL % 4 == 0 && TBL_DCH % 4 == 0 && 64 * TB_
 
 size_t tb_lds_bytes() { return sizeof(float) * (size_t)TBL_END; }
 
-__device__ __forceinline__ float tb_block_sum(float v, float* scr) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) scr[threadIdx.x >> 6] = v;
-  __syncthreads();
-  float r = scr[0];
-#pragma unroll
-  for (int i = 1; i < TB_NW; ++i) r += scr[i];
-  return r;
-}
 // work-group barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier, WITHOUT
 // the vmcnt(0) that __syncthreads()' release fence adds -- the HBM loads issued ahead (the next step's
 // operands, the tanh tiles) stay in flight across it
 __device__ __forceinline__ void tb_lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-// sum over the 16 lanes of each lane row (xor within the low 4 lane bits)
+// sum over the 16 lanes of each lane row (xor within the low 4 lane bits; a butterfly reduce-scatter
+// over 16 sums takes fewer shuffles but its selects cost the registers this kernel does not have)
 __device__ __forceinline__ float tb_row16_sum(float v) {
 #pragma unroll
   for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float tb_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 // wave poll of n producers, producer(l) for lane l < n (this XCD group's flag replica)
@@ -152,8 +148,8 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
   float* const ds = sm + TBL_DS;
   float* const cum_s = sm + TBL_CUM;
   float* const red = sm + TBL_RED;
-  float* const dq_s = sm + TBL_DQ;
-  float* const scr = sm + TBL_SC;
+  float* const al_s = sm + TBL_AL;
+  float* const pa_s = sm + TBL_PA;
   int* const sfail = reinterpret_cast<int*>(sm + TBL_SC + 16);
   float* const cel = sm + TBL_CELL;
   float* const dus = sm + TBL_DU;                    // ATT phase .. end of the step
@@ -371,13 +367,18 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
     TB_STAMP(0);
     // ---- park the prefetched operands of step t (landed during the previous step's off-chain work):
     // the unit role's in LDS ([17][256], thread-private columns), the attention row's in registers
-    if (erow) {  // slots 0-7 layer 2 (i j f o c_new c_prev kc kh), 8-15 layer 1, 16 d PIN (h part)
+    // (slots 0-7 layer 2 (i j f o c_new c_prev kc kh), 8-15 layer 1, 16 d PIN (h part)); an attention row
+    // parks behind its P1 poll, whose flag loads then travel beside the prefetch instead of after it
+    auto park = [&] {
+      if (erow) {
 #pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4)
+        for (int k4 = 0; k4 < 4; ++k4)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) cel[(4 * k4 + e) * 256 + tid] = cq[k4][e];
-      cel[16 * 256 + tid] = cvd;
-    }
+          for (int e = 0; e < 4; ++e) cel[(4 * k4 + e) * 256 + tid] = cq[k4][e];
+        cel[16 * 256 + tid] = cvd;
+      }
+    };
+    if (!arow) park();
     // ================= ATT
     if (arow) {
       const long rt = (tb + rb) * Tin;  // this row's [Tin] block of step t
@@ -406,8 +407,11 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         float pv[TB_NKB];
 #pragma unroll
         for (int k = 0; k < TB_NKB; ++k) pv[k] = tb_ld(rs, ((k * 64 + rb) * 1024 + 256 * sq + tid) * 4);
+        park();
 #pragma unroll
         for (int k = 0; k < TB_NKB; ++k) dctx += pv[k];
+      } else {
+        park();
       }
       if (tid >= Tin) aj = cumv = 0.f;
       tp_bst(a.DCTX + (tb + rb) * D + 256 * sq, tid * 4, 0, dctx);
@@ -416,7 +420,10 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         dch[tid] = hi;
         dch[256 + tid] = (__bf16)(dctx - (float)hi);
       }
-      if (tid < Tin) cum_s[15 + tid] = cumv;
+      if (tid < Tin) {
+        cum_s[15 + tid] = cumv;
+        al_s[tid] = aj;
+      }
       tb_lds_bar();
       TB_STAMP(2);
       if (sfail[0]) return;
@@ -486,16 +493,27 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
           return good;
         });
         if (!ok) sfail[0] = 1;
-        if (act) da_s[tid] = ((e4[0] + e4[1]) + e4[2]) + e4[3];
+        if (act) {
+          const float dv = ((e4[0] + e4[1]) + e4[2]) + e4[3];
+          da_s[tid] = dv;
+          pa_s[tid] = aj * dv;
+        }
       }
       __syncthreads();
       TB_STAMP(4);
       if (sfail[0]) return;
-      // softmax backward (attention.py:218): de_j = a_j (d a_j - Σ_k a_k d a_k), 0 past the length
-      const float dav = tid < Tin ? da_s[tid] : 0.f;
-      const float ssum = tb_block_sum(aj * dav, scr);
-      if (tid < Tin) da_s[tid] = tid < len ? aj * (dav - ssum) : 0.f;
-      __syncthreads();
+      // softmax backward (attention.py:218): de_j = a_j (d a_j - Σ_k a_k d a_k), 0 past the length; every
+      // wave forms the sum itself (same order in all: no barrier)
+      float ssum;
+      {
+        float sp = 0.f;
+#pragma unroll
+        for (int k = 0; k < (TB_TM + 63) / 64; ++k) {
+          const int j = lane + 64 * k;
+          sp += j < Tin ? pa_s[j] : 0.f;
+        }
+        ssum = tb_wave_sum(sp);
+      }
       // du of the own dims (energy-tile layout): d keys, d query, d v_a; du -> LDS
       float dqp[8], dvp[8];
 #pragma unroll
@@ -505,7 +523,7 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         const int pt = w + 4 * r;
         if (16 * pt >= Tin) break;  // wave-uniform
         const int j = 16 * pt + jl;
-        const float dej = j < Tin ? da_s[j] : 0.f;
+        const float dej = j < len ? al_s[j] * (da_s[j] - ssum) : 0.f;
         if (j >= Tin) th[r][0] = th[r][1] = tp_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
@@ -523,43 +541,50 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
           for (int i = 0; i < 4; ++i) dus[j * TB_DUS + 16 * mt + 4 * g4 + i] = dv4[i];
         }
       }
+      {  // the wave's sums over its positions of d query / d v_a per dim
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        dqp[i] = tb_row16_sum(dqp[i]);
-        dvp[i] = tb_row16_sum(dvp[i]);
-      }
-      if (jl == 0) {
+        for (int i = 0; i < 8; ++i) {
+          dqp[i] = tb_row16_sum(dqp[i]);
+          dvp[i] = tb_row16_sum(dvp[i]);
+        }
+        if (jl == 0) {
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+          for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            red[w * 32 + 16 * mt + 4 * g4 + i] = dqp[4 * mt + i];
-            red[TB_NW * 32 + w * 32 + 16 * mt + 4 * g4 + i] = dvp[4 * mt + i];
-          }
+            for (int i = 0; i < 4; ++i) {
+              red[w * 32 + 16 * mt + 4 * g4 + i] = dqp[4 * mt + i];
+              red[TB_NW * 32 + w * 32 + 16 * mt + 4 * g4 + i] = dvp[4 * mt + i];
+            }
+        }
       }
       __syncthreads();
-      if (tid < 32) {
-        float q = 0.f, v = 0.f;
+      // wave 0: lanes < 32 sum the waves' d query / d v_a of dim lane; lanes < 4 pack the bf16 dq exchange row
+      // (A-fragment layout, K = 128: the unit role forms d h2 = dq·Wq^T itself, bf16 operands as
+      // k_tr_fused<TF_BWD_H>)
+      float q = 0.f;
+      if (w == 0) {
+        float v = 0.f;
+        const int dl = lane & 31;
 #pragma unroll
         for (int ww = 0; ww < TB_NW; ++ww) {
-          q += red[ww * 32 + tid];
-          v += red[TB_NW * 32 + ww * 32 + tid];
+          q += red[ww * 32 + dl];
+          v += red[TB_NW * 32 + ww * 32 + dl];
         }
-        dq_s[tid] = q;
-        dba += q;
-        dva += v;
+        if (lane < 32) {
+          dba += q;
+          dva += v;
+        }
+        float q8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q8[e] = __shfl(q, 8 * (lane & 3) + e, 64);
+        if (lane < 4) {
+          const tp_u4 pk = {tp_pack(q8[0], q8[1]), tp_pack(q8[2], q8[3]), tp_pack(q8[4], q8[5]), tp_pack(q8[6], q8[7])};
+          tp_st16(a.DQX, (int)(((long)par * 64 * A + tp_afl(rb, 32 * sq + 8 * lane, A)) * 2), pk);
+        }
       }
-      __syncthreads();
       TB_STAMP(5);
-      // d query of the own dims -> the dq exchange rows (bf16, A-fragment layout, K = 128): the unit
-      // role forms d h2 = dq·Wq^T itself (bf16 operands, as k_tr_fused<TF_BWD_H>)
-      if (tid < 4) {
-        const float* q8 = dq_s + 8 * tid;
-        const tp_u4 v = {tp_pack(q8[0], q8[1]), tp_pack(q8[2], q8[3]), tp_pack(q8[4], q8[5]), tp_pack(q8[6], q8[7])};
-        tp_st16(a.DQX, (int)(((long)par * 64 * A + tp_afl(rb, 32 * sq + 8 * tid, A)) * 2), v);
-      }
       tp_publish(a, TB_PH_Q, tag);
-      if (tid < 32) tp_bst(a.DQ + (tb + rb) * A + 32 * sq, tid * 4, 0, dq_s[tid]);
+      if (tid < 32) tp_bst(a.DQ + (tb + rb) * A + 32 * sq, tid * 4, 0, q);
       TB_STAMP(6);
     }
     // ================= CELL2: d hz2 from step t+1's product, d h2 from the dq rows of all quarters: both waits
@@ -735,9 +760,9 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
       }
       {  // the zero pad rows of the diagonal sum (the product staging shares the region)
         const int r1 = 16 * ((Tin + 15) >> 4);
-        for (int e = tid; e < 32 * 33; e += TP_NT) {
-          const int r = e / 33, c = e - 33 * r;
-          ms[(r < 16 ? r - 16 : r1 + r - 16) * 33 + c] = 0.f;
+        for (int e = tid; e < 16 * 33; e += TP_NT) {
+          ms[e - 16 * 33] = 0.f;
+          ms[r1 * 33 + e] = 0.f;
         }
       }
       tb_lds_bar();
