@@ -18,13 +18,14 @@ typedef __attribute__((address_space(1))) unsigned long long tp_gu64;
 #define TP_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 constexpr long long TP_TIMEOUT = 200000000LL;  // 2 s of s_memrealtime (100 MHz)
 // branch-free tanh (tanhf's two paths diverge per lane): odd Taylor polynomial below |x| = 1/16
-// (truncation < 2e-13), (1 - e) / (1 + e) with e = exp(-2|x|) above (the subtraction exact, the result
-// within ~1e-6 relative); the sign restored by copysign
+// (truncation < 2e-13), (1 - e)·rcp(1 + e) with e = exp(-2|x|) above (the subtraction exact; v_rcp_f32
+// instead of the IEEE division sequence __fdividef compiles to here: the result within ~1e-6 relative); the
+// sign restored by copysign
 __device__ __forceinline__ float tp_tanh(float x) {
   const float ax = fabsf(x), x2 = x * x;
   const float p = x * (1.f + x2 * (-1.f / 3.f + x2 * (2.f / 15.f + x2 * (-17.f / 315.f))));
   const float e = __expf(-2.f * ax);
-  const float r = copysignf(__fdividef(1.f - e, 1.f + e), x);
+  const float r = copysignf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e), x);
   return ax < 0.0625f ? p : r;
 }
 
