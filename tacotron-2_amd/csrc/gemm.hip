@@ -1478,9 +1478,8 @@ void kc_transpose_bf16(const float* B, int K, int N, long ldb, __bf16* out, int 
   TT2_HIP(hipGetLastError());
 }
 
-void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
-                  DevBuf& a16, DevBuf& b16, DevBuf& part, hipStream_t s, bool a_kmajor, const KcConvA* conv) {
-  TT2_CHECK(M > 0 && N > 0 && K > 0, TT2_ERR_SHAPE_MISMATCH, "gemm_bf16_kc: empty problem");
+// the K split of one gemm_bf16_kc product: ks work-groups per tile over per k-steps each
+static void kc_split(int M, int N, int K, int* ks_out, int* per_out) {
   const int n_mt = cdiv(M, KC_BM), n_nt = cdiv(N, KC_BN), tiles = n_mt * n_nt;
   const int nkt = cdiv(K, KC_BK);
   // K split: one work-group per CU, so the time is ~ rounds x k-steps per work-group, rounds =
@@ -1497,13 +1496,33 @@ void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B,
   }
   const int per = cdiv(nkt, ks);
   ks = cdiv(nkt, per);  // no empty slices
+  *ks_out = ks;
+  *per_out = per;
+}
+
+void gemm_bf16_kc_bt_dims(int M, int N, int K, long* Np, long* Kp) {
+  int ks, per;
+  kc_split(M, N, K, &ks, &per);
+  *Np = (long)cdiv(N, KC_BN) * KC_BN;
+  *Kp = (long)per * ks * KC_BK;
+}
+
+void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
+                  DevBuf& a16, DevBuf& b16, DevBuf& part, hipStream_t s, bool a_kmajor, const KcConvA* conv,
+                  const __bf16* bt_pre) {
+  TT2_CHECK(M > 0 && N > 0 && K > 0, TT2_ERR_SHAPE_MISMATCH, "gemm_bf16_kc: empty problem");
+  const int n_mt = cdiv(M, KC_BM), n_nt = cdiv(N, KC_BN);
+  const int nkt = cdiv(K, KC_BK);
+  int ks, per;
+  kc_split(M, N, K, &ks, &per);
+  (void)nkt;
   const int Kp = per * ks * KC_BK, Mp = n_mt * KC_BM, Np = n_nt * KC_BN;
-  const size_t na = (size_t)Mp * Kp * 2, nb = (size_t)Np * Kp * 2, np = ks > 1 ? (size_t)ks * M * N * 4 : 0;
+  const size_t na = (size_t)Mp * Kp * 2, nb = bt_pre ? 0 : (size_t)Np * Kp * 2, np = ks > 1 ? (size_t)ks * M * N * 4 : 0;
   if (a16.bytes < na) a16.alloc(na);  // growth frees the old buffer (device-synchronising hipFree)
   if (b16.bytes < nb) b16.alloc(nb);
   if (part.bytes < np) part.alloc(np);
   __bf16* a = reinterpret_cast<__bf16*>(a16.p);
-  __bf16* b = reinterpret_cast<__bf16*>(b16.p);
+  const __bf16* b = bt_pre ? bt_pre : reinterpret_cast<__bf16*>(b16.p);
   const long n4 = (long)Mp * Kp / 4;
   if (conv) {
     TT2_CHECK(conv->kw * conv->C == M && conv->B * conv->T == K, TT2_ERR_SHAPE_MISMATCH, "gemm_bf16_kc: conv shape");
@@ -1511,7 +1530,7 @@ void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B,
   } else if (a_kmajor) hipLaunchKernelGGL(k_kc_tr, dim3(Kp / 64, Mp / 64), dim3(256), 0, s, A, K, M, lda, a, Kp);
   else hipLaunchKernelGGL(k_kc_pad, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, A, M, K,
                           lda, a, Kp, n4);
-  hipLaunchKernelGGL(k_kc_tr, dim3(Kp / 64, Np / 64), dim3(256), 0, s, B, K, N, ldb, b, Kp);
+  if (!bt_pre) hipLaunchKernelGGL(k_kc_tr, dim3(Kp / 64, Np / 64), dim3(256), 0, s, B, K, N, ldb, const_cast<__bf16*>(b), Kp);
   TT2_HIP(hipGetLastError());
   float* pp = ks > 1 ? reinterpret_cast<float*>(part.p) : nullptr;
   hipLaunchKernelGGL(k_gemm_kc<ACT_NONE>, dim3((unsigned)(cdiv(n_mt, 8) * 8 * n_nt), (unsigned)ks), dim3(512), 0, s, a,

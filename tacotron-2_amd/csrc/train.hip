@@ -131,7 +131,8 @@ struct tt2_train_ctx {
   DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps, tpKWT;
   bool tp_on = false, tp_last = false, tp_check = false;
   // persistent backward (train_bwd_persist.hip): exchange buffers, flags + control words
-  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl, tbW1F, tbPK;
+  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl, tbW1F, tbPK, tbDGT1, tbDGT2;
+  bool tb_dgt = false;  // the last persistent backward wrote bf16(dG)^T for the weight-gradient GEMMs
   bool tb_on = false, tb_last = false, tb_check = false;
   int* tb_ctl_dev = nullptr;
   int* tp_ctl_dev = nullptr;  // control words of the last persistent forward (device)
@@ -2481,10 +2482,11 @@ static void tr_gemm(int M, int N, int K, const float* A, long lda, const float* 
 // ones straight from X on gemm_bf16_kc (its conversion pass transposes X), the rest through
 // tr_transpose into TBUF and tr_gemm
 static void tr_gemm_xtg(int M, int N, int K, const float* X, long ldx, const float* dG, long ldg, float* C, long ldc,
-                        float* TBUF, hipStream_t s) {
+                        float* TBUF, hipStream_t s, const __bf16* dgt = nullptr) {
   tt2_train_ctx* c = g_tr_ctx;
   if (c && c->blas_on && g_tr_prec == 2 && 2.0 * M * (double)N * K >= kTrBigMinFlops) {
-    gemm_bf16_kc(M, N, K, X, ldx, dG, ldg, C, ldc, c->blasA, c->blasB, c->blasP, s, true);
+    // dgt: bf16(dG)^T already staged by the persistent backward (gemm_bf16_kc bt_pre)
+    gemm_bf16_kc(M, N, K, X, ldx, dG, ldg, C, ldc, c->blasA, c->blasB, c->blasP, s, true, nullptr, dgt);
     ++c->blas_calls;
     return;
   }
@@ -3008,6 +3010,26 @@ static void tr_persist_backward(tt2_train_ctx* c, const TrAtt& at, const uint8_t
   TT2_CHECK(c->tbPK.bytes >= (size_t)T * TP_NB * 4 * TP_NT * 4 * sizeof(float), TT2_ERR_STATE,
             "persistent backward: the forward did not pack the unit operands");
   a.BPK = c->tbPK.as<float>(); a.dPIN = c->dPIN.as<float>();
+  // bf16(dG)^T in the layout the weight-gradient GEMMs stage (B = 64: the K index t·64 + row is t·B + b),
+  // when both products' K split keeps Kp = T·B (no padding columns to clear)
+  a.DGT1 = a.DGT2 = nullptr;
+  a.dgt_ld = 0;
+  c->tb_dgt = false;
+  {
+    long np1, kp1, np2, kp2;
+    gemm_bf16_kc_bt_dims(c->LX1, 4 * TP_H, T * B, &np1, &kp1);
+    gemm_bf16_kc_bt_dims(2 * TP_H, 4 * TP_H, T * B, &np2, &kp2);
+    const char* e = std::getenv("TT2_TB_DGT");
+    if (B == 64 && c->blas_on && g_tr_prec == 2 && np1 == 4 * TP_H && np2 == 4 * TP_H && kp1 == (long)T * B &&
+        kp2 == kp1 && !(e && e[0] == '0')) {
+      grow(c->tbDGT1, (size_t)4 * TP_H * kp1 * sizeof(__bf16));
+      grow(c->tbDGT2, (size_t)4 * TP_H * kp1 * sizeof(__bf16));
+      a.DGT1 = c->tbDGT1.as<__bf16>();
+      a.DGT2 = c->tbDGT2.as<__bf16>();
+      a.dgt_ld = kp1;
+      c->tb_dgt = true;
+    }
+  }
   a.dG1 = c->dG1.as<float>(); a.dG2 = c->dG2.as<float>(); a.DQ = c->DQ.as<float>(); a.DCTX = c->DCTX.as<float>();
   a.DKEYS = c->DKEYS.as<float>(); a.dV = c->dV.as<float>(); a.dBA = c->dBA.as<float>(); a.DWGP = c->DWGP.as<float>();
   a.G1X = c->tbG1X.as<__bf16>(); a.G2X = c->tbG2X.as<__bf16>(); a.P1X = c->tbP1X.as<float>();
@@ -3421,9 +3443,12 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   // ---- weight gradients over all T·B rows ----
   float* TBUF = c->TBUF.as<float>();
   const int TBi = (int)TB;
-  tr_gemm_xtg(LX1, 4 * H, TBi, X1, LX1, c->dG1.as<float>(), 4 * H, gvar(c, L1V("kernel")), 4 * H, TBUF, s);
+  const bool dgt = tb_run && c->tb_dgt;
+  tr_gemm_xtg(LX1, 4 * H, TBi, X1, LX1, c->dG1.as<float>(), 4 * H, gvar(c, L1V("kernel")), 4 * H, TBUF, s,
+              dgt ? c->tbDGT1.as<__bf16>() : nullptr);
   tr_colsum(c, c->dG1.as<float>(), TB, 4 * H, 4 * H, gvar(c, L1V("bias")), s);
-  tr_gemm_xtg(2 * H, 4 * H, TBi, X2, 2 * H, c->dG2.as<float>(), 4 * H, gvar(c, L2V("kernel")), 4 * H, TBUF, s);
+  tr_gemm_xtg(2 * H, 4 * H, TBi, X2, 2 * H, c->dG2.as<float>(), 4 * H, gvar(c, L2V("kernel")), 4 * H, TBUF, s,
+              dgt ? c->tbDGT2.as<__bf16>() : nullptr);
   tr_colsum(c, c->dG2.as<float>(), TB, 4 * H, 4 * H, gvar(c, L2V("bias")), s);
   tr_transpose(PIN, TB, H + D, H + D, TBUF, TB, s);
   tr_gemm(H, A, TBi, TBUF, TB, c->DQ.as<float>(), A, gvar(c, vn("decoder/query_layer/kernel")), A, s);

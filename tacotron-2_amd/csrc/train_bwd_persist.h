@@ -36,6 +36,9 @@ struct TbArgs {
   const float* dPIN;         // [T][B][H + D] d [h2 | ctx] from the frame / stop projections
   // outputs
   float *dG1, *dG2;          // [T][B][4H]
+  __bf16 *DGT1, *DGT2;       // or null: bf16(dG)^T [4H][dgt_ld] (column t·64 + row; B = 64), the B^T operand the
+                             // weight-gradient GEMMs stage (gemm_bf16_kc bt_pre), written beside the fp32 slots
+  long dgt_ld;
   float *DQ, *DCTX;          // [T][B][A], [T][B][D]
   float* DKEYS;              // [B][Tin][A]
   float *dV, *dBA;           // [B][NT][A]: slot b·NT holds row b's sums over steps and positions

@@ -116,6 +116,16 @@ __device__ __forceinline__ int tb_uoff(int nb, int m4, int kb, int row, int e) {
 __device__ __forceinline__ float tb_ld(const __amdgpu_buffer_rsrc_t rs, int byte_off) {  // sc1 dword load
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, byte_off, 0, 16));
 }
+// the 4 gate gradients of (row er, unit en) at step t into bf16(dG)^T [4H][ld], column t·64 + er: a wave's
+// store per gate writes 4 units x 16 consecutive rows (the work-group's 4 waves complete 128-byte runs)
+__device__ __forceinline__ void tb_dgt(__bf16* DGT, long ld, int t, int er, int en, const float (&d)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long col = (long)q * TP_H + en;
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)d[q]), tp_rsrc(DGT),
+                                          (int)((col * ld + (long)t * 64 + er) * 2), 0, 0);
+  }
+}
 // plain dword load of a read-only slot: wave-uniform base + per-lane byte offset (buffer addressing
 // keeps the step loop free of per-lane 64-bit addresses, as train_persist.hip)
 __device__ __forceinline__ float tb_lg(const float* base, int byte_off) {
@@ -653,9 +663,11 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
       tp_publish(a, TB_PH_G2, tag);
       // the fp32 dG2 slot (read after the launch) behind the publish: its scattered stores drain at the
       // next publish instead of holding this one
-      if (erow)
+      if (erow) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) tp_bst(a.dG2 + tb * K4, (er * K4 + en + q * H) * 4, 0, d[q]);
+        if (a.DGT2) tb_dgt(a.DGT2, a.dgt_ld, t, er, en, d);
+      }
     }
     TB_STAMP(9);
     // ================= PROD2: [d h1 | d hz2_{t-1}] partial of (kb, nb)
@@ -713,9 +725,11 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
                  tp_u2{tp_pack(v[q][0], v[q][1]), tp_pack(v[q][2], v[q][3])});
       }
       tp_publish(a, TB_PH_G1, tag);
-      if (erow)
+      if (erow) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) tp_bst(a.dG1 + tb * K4, (er * K4 + en + q * H) * 4, 0, d[q]);
+        if (a.DGT1) tb_dgt(a.DGT1, a.dgt_ld, t, er, en, d);
+      }
     }
     TB_STAMP(12);
     // ================= PROD1: [d ctx_{t-1} | d hz1_{t-1}] partial of (kb, nb)
