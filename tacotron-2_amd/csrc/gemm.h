@@ -124,7 +124,7 @@ struct KcConvA {
 };
 void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
                   DevBuf& a16, DevBuf& b16, DevBuf& part, hipStream_t s, bool a_kmajor = false,
-                  const KcConvA* conv = nullptr, const __bf16* bt_pre = nullptr);
+                  const KcConvA* conv = nullptr, const __bf16* bt_pre = nullptr, const __bf16* a_pre = nullptr);
 // the [Np][Kp] bf16 B^T layout gemm_bf16_kc stages (Np = N rounded to 256; Kp = K rounded to its k-step split),
 // for producers that write it themselves (gemm_bf16_kc(..., bt_pre) skips the conversion pass)
 void gemm_bf16_kc_bt_dims(int M, int N, int K, long* Np, long* Kp);

@@ -1509,7 +1509,7 @@ void gemm_bf16_kc_bt_dims(int M, int N, int K, long* Np, long* Kp) {
 
 void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
                   DevBuf& a16, DevBuf& b16, DevBuf& part, hipStream_t s, bool a_kmajor, const KcConvA* conv,
-                  const __bf16* bt_pre) {
+                  const __bf16* bt_pre, const __bf16* a_pre) {
   TT2_CHECK(M > 0 && N > 0 && K > 0, TT2_ERR_SHAPE_MISMATCH, "gemm_bf16_kc: empty problem");
   const int n_mt = cdiv(M, KC_BM), n_nt = cdiv(N, KC_BN);
   const int nkt = cdiv(K, KC_BK);
@@ -1517,14 +1517,16 @@ void gemm_bf16_kc(int M, int N, int K, const float* A, long lda, const float* B,
   kc_split(M, N, K, &ks, &per);
   (void)nkt;
   const int Kp = per * ks * KC_BK, Mp = n_mt * KC_BM, Np = n_nt * KC_BN;
-  const size_t na = (size_t)Mp * Kp * 2, nb = bt_pre ? 0 : (size_t)Np * Kp * 2, np = ks > 1 ? (size_t)ks * M * N * 4 : 0;
+  const size_t na = a_pre ? 0 : (size_t)Mp * Kp * 2, nb = bt_pre ? 0 : (size_t)Np * Kp * 2, np = ks > 1 ? (size_t)ks * M * N * 4 : 0;
   if (a16.bytes < na) a16.alloc(na);  // growth frees the old buffer (device-synchronising hipFree)
   if (b16.bytes < nb) b16.alloc(nb);
   if (part.bytes < np) part.alloc(np);
-  __bf16* a = reinterpret_cast<__bf16*>(a16.p);
+  __bf16* a = a_pre ? const_cast<__bf16*>(a_pre) : reinterpret_cast<__bf16*>(a16.p);
   const __bf16* b = bt_pre ? bt_pre : reinterpret_cast<__bf16*>(b16.p);
   const long n4 = (long)Mp * Kp / 4;
-  if (conv) {
+  if (a_pre) {
+    // the caller staged A as [Mp][Kp] bf16 itself
+  } else if (conv) {
     TT2_CHECK(conv->kw * conv->C == M && conv->B * conv->T == K, TT2_ERR_SHAPE_MISMATCH, "gemm_bf16_kc: conv shape");
     hipLaunchKernelGGL(k_kc_im2col, dim3(Kp / 64, Mp / 64), dim3(256), 0, s, *conv, a, Kp);
   } else if (a_kmajor) hipLaunchKernelGGL(k_kc_tr, dim3(Kp / 64, Mp / 64), dim3(256), 0, s, A, K, M, lda, a, Kp);

@@ -131,8 +131,11 @@ struct tt2_train_ctx {
   DevBuf tpCX, tpH1X, tpZ1X, tpH2X, tpZ2X, tpEX, tpCtl, tpPre, tpStamps, tpKWT;
   bool tp_on = false, tp_last = false, tp_check = false;
   // persistent backward (train_bwd_persist.hip): exchange buffers, flags + control words
-  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl, tbW1F, tbPK, tbDGT1, tbDGT2;
+  DevBuf tbG1X, tbG2X, tbP1X, tbP2X, tbQX, tbCtl, tbW1F, tbPK, tbDGT1, tbDGT2, tbDGR1;
+  DevBuf reg_segs;  // [nreg] (offset, size) of the regularised variables (tr_regularize)
+  int nreg = 0;
   bool tb_dgt = false;  // the last persistent backward wrote bf16(dG)^T for the weight-gradient GEMMs
+  bool tb_dgr = false;  // ... and bf16(dG1) row-major for the d X1 product
   bool tb_on = false, tb_last = false, tb_check = false;
   int* tb_ctl_dev = nullptr;
   int* tp_ctl_dev = nullptr;  // control words of the last persistent forward (device)
@@ -2172,18 +2175,20 @@ __global__ void k_tr_mask_rows(const float* __restrict__ x, const int* __restric
   y[i] = j < lens[b] ? x[i] : 0.f;
 }
 
-// L2 regularisation (tacotron.py:865-867): g += reg·w over [off, off+n); partial Σ w²/2
-__global__ __launch_bounds__(256) void k_tr_reg(const float* __restrict__ w, float* __restrict__ g, long n, float reg,
-                                                float* __restrict__ part) {
+// L2 regularisation (tacotron.py:865-867) of every regularised variable in ONE launch: block (x, y) takes
+// variable y's [off, off + n) = seg[y] with the grid's x-stride, g += reg·w, partial Σ w²/2 -> part[64 y + x]
+__global__ __launch_bounds__(256) void k_tr_reg(const float* __restrict__ w, float* __restrict__ g,
+                                                const long2* __restrict__ seg, float reg, float* __restrict__ part) {
   __shared__ float s4[16];
+  const long off = seg[blockIdx.y].x, n = seg[blockIdx.y].y;
   float acc = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const float v = w[i];
-    g[i] += reg * v;
+    const float v = w[off + i];
+    g[off + i] += reg * v;
     acc += 0.5f * v * v;
   }
   acc = block_sum(acc, s4);
-  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+  if (threadIdx.x == 0) part[64 * blockIdx.y + blockIdx.x] = acc;
 }
 
 __global__ __launch_bounds__(256) void k_tr_sumsq(const float* __restrict__ g, long n, float* __restrict__ part) {
@@ -3013,8 +3018,9 @@ static void tr_persist_backward(tt2_train_ctx* c, const TrAtt& at, const uint8_t
   // bf16(dG)^T in the layout the weight-gradient GEMMs stage (B = 64: the K index t·64 + row is t·B + b),
   // when both products' K split keeps Kp = T·B (no padding columns to clear)
   a.DGT1 = a.DGT2 = nullptr;
+  a.DGR1 = nullptr;
   a.dgt_ld = 0;
-  c->tb_dgt = false;
+  c->tb_dgt = c->tb_dgr = false;
   {
     long np1, kp1, np2, kp2;
     gemm_bf16_kc_bt_dims(c->LX1, 4 * TP_H, T * B, &np1, &kp1);
@@ -3028,6 +3034,14 @@ static void tr_persist_backward(tt2_train_ctx* c, const TrAtt& at, const uint8_t
       a.DGT2 = c->tbDGT2.as<__bf16>();
       a.dgt_ld = kp1;
       c->tb_dgt = true;
+      // the d X1 product's A staging is bf16(dG1) row-major when its K split keeps Kp = 4H
+      long np3, kp3;
+      gemm_bf16_kc_bt_dims(T * B, TP_P, 4 * TP_H, &np3, &kp3);
+      if (kp3 == 4 * TP_H) {
+        grow(c->tbDGR1, (size_t)T * B * 4 * TP_H * sizeof(__bf16));
+        a.DGR1 = c->tbDGR1.as<__bf16>();
+        c->tb_dgr = true;
+      }
     }
   }
   a.dG1 = c->dG1.as<float>(); a.dG2 = c->dG2.as<float>(); a.DQ = c->DQ.as<float>(); a.DCTX = c->DCTX.as<float>();
@@ -3328,8 +3342,15 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   c->tb_last = tb_run;
   if (tb_run) {
     tr_persist_backward(c, at, zm, Tin, T, NT, s);
-    // the prenet columns of d X1 (off the recurrence): one product over all T·B rows
-    tr_gemm((int)TB, P, 4 * H, c->dG1.as<float>(), 4 * H, c->K1T.as<float>(), LX1, dX1, LX1, s);
+    // the prenet columns of d X1 (off the recurrence): one product over all T·B rows (A = bf16(dG1) as the
+    // launch wrote it, when it did)
+    if (c->tb_dgr && c->blas_on && g_tr_prec == 2) {
+      gemm_bf16_kc((int)TB, P, 4 * H, c->dG1.as<float>(), 4 * H, c->K1T.as<float>(), LX1, dX1, LX1, c->blasA, c->blasB,
+                   c->blasP, s, false, nullptr, nullptr, c->tbDGR1.as<__bf16>());
+      ++c->blas_calls;
+    } else {
+      tr_gemm((int)TB, P, 4 * H, c->dG1.as<float>(), 4 * H, c->K1T.as<float>(), LX1, dX1, LX1, s);
+    }
   }
   for (int t = tb_run ? -1 : T - 1; t >= 0; --t) {
     const long s1 = (long)t * B;
@@ -3537,14 +3558,18 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
 
 // L2 regularisation of the regularised kernels (after every gradient of the step has landed)
 static void tr_regularize(tt2_train_ctx* c, hipStream_t s) {
-  int nreg = 0;
-  for (const auto& v : c->vars) {
-    if (!v.reg) continue;
-    hipLaunchKernelGGL(k_tr_reg, dim3(64), dim3(256), 0, s, c->params.as<float>() + v.off, c->grads + v.off, v.n,
-                       c->cfg.reg_weight, c->part.as<float>() + 64 * nreg);
-    ++nreg;
+  if (!c->reg_segs.p) {  // the regularised variables' (offset, size), fixed at create
+    std::vector<long2> seg;
+    for (const auto& v : c->vars)
+      if (v.reg) seg.push_back(make_long2((long)v.off, (long)v.n));
+    c->nreg = (int)seg.size();
+    c->reg_segs.alloc(sizeof(long2) * std::max<size_t>(seg.size(), 1));
+    if (!seg.empty()) TT2_HIP(hipMemcpy(c->reg_segs.p, seg.data(), sizeof(long2) * seg.size(), hipMemcpyHostToDevice));
   }
-  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 64 * nreg, c->cfg.reg_weight,
+  if (c->nreg)
+    hipLaunchKernelGGL(k_tr_reg, dim3(64, c->nreg), dim3(256), 0, s, c->params.as<float>(), c->grads,
+                       c->reg_segs.as<long2>(), c->cfg.reg_weight, c->part.as<float>());
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 64 * c->nreg, c->cfg.reg_weight,
                      c->red.as<float>() + 2, 0);
 }
 

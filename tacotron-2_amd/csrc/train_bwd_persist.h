@@ -39,6 +39,7 @@ struct TbArgs {
   __bf16 *DGT1, *DGT2;       // or null: bf16(dG)^T [4H][dgt_ld] (column t·64 + row; B = 64), the B^T operand the
                              // weight-gradient GEMMs stage (gemm_bf16_kc bt_pre), written beside the fp32 slots
   long dgt_ld;
+  __bf16* DGR1;              // or null (with DGT1): bf16(dG1) row-major [T·64][4H], the A operand of the d X1 product
   float *DQ, *DCTX;          // [T][B][A], [T][B][D]
   float* DKEYS;              // [B][Tin][A]
   float *dV, *dBA;           // [B][NT][A]: slot b·NT holds row b's sums over steps and positions

@@ -723,6 +723,11 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_bwd_persist(TbArgs a) {
         for (int q = 0; q < 4; ++q)
           tp_st8(a.G1X, (int)(((long)par * 64 * K4 + tp_afl(er, p0 + 64 * q, K4)) * 2),
                  tp_u2{tp_pack(v[q][0], v[q][1]), tp_pack(v[q][2], v[q][3])});
+        if (a.DGR1)  // the same 4 units of gate q, row-major (off the chain: drained by a later publish)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            __builtin_amdgcn_raw_buffer_store_b64(tp_u2{tp_pack(v[q][0], v[q][1]), tp_pack(v[q][2], v[q][3])},
+                                                  tp_rsrc(a.DGR1), (int)((((long)t * 64 + er) * K4 + q * H + 4 * g) * 2), 0, 0);
       }
       tp_publish(a, TB_PH_G1, tag);
       if (erow) {
