@@ -2191,10 +2191,66 @@ __global__ __launch_bounds__(256) void k_tr_reg(const float* __restrict__ w, flo
   if (threadIdx.x == 0) part[64 * blockIdx.y + blockIdx.x] = acc;
 }
 
-__global__ __launch_bounds__(256) void k_tr_sumsq(const float* __restrict__ g, long n, float* __restrict__ part) {
+// Zero-fill of up to TR_ZL_MAX device ranges in ONE launch (the step's state resets: a hipMemsetAsync costs
+// ~6 us of launch each); 16-byte stores when a range's base is 16-byte aligned, else dwords
+constexpr int TR_ZL_MAX = 16;
+struct TrZeroList {
+  void* p[TR_ZL_MAX];
+  unsigned long long n[TR_ZL_MAX];  // bytes (multiples of 4)
+  int count;
+};
+__global__ void k_tr_zero_many(TrZeroList z) {
+  const unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x,
+                           stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (int i = 0; i < z.count; ++i) {
+    if ((reinterpret_cast<uintptr_t>(z.p[i]) & 15) == 0) {
+      uint4* q = reinterpret_cast<uint4*>(z.p[i]);
+      const unsigned long long n16 = z.n[i] / 16;
+      for (unsigned long long k = t; k < n16; k += stride) q[k] = make_uint4(0u, 0u, 0u, 0u);
+      unsigned* w = reinterpret_cast<unsigned*>(z.p[i]);
+      for (unsigned long long k = n16 * 4 + t; k < z.n[i] / 4; k += stride) w[k] = 0u;
+    } else {
+      unsigned* w = reinterpret_cast<unsigned*>(z.p[i]);
+      for (unsigned long long k = t; k < z.n[i] / 4; k += stride) w[k] = 0u;
+    }
+  }
+}
+static void tr_zero_many(std::initializer_list<std::pair<void*, size_t>> l, hipStream_t s) {
+  TrZeroList z{};
+  unsigned long long tot = 0;
+  for (const auto& e : l) {
+    if (!e.first || !e.second) continue;
+    if (z.count == TR_ZL_MAX) {  // full: flush
+      hipLaunchKernelGGL(k_tr_zero_many, dim3((unsigned)std::min<unsigned long long>((tot / 16 + 255) / 256 + 1, 4096)),
+                         dim3(256), 0, s, z);
+      z.count = 0;
+      tot = 0;
+    }
+    TT2_CHECK(e.second % 4 == 0, TT2_ERR_INVALID_ARG, "tr_zero_many: byte count % 4 != 0");
+    z.p[z.count] = e.first;
+    z.n[z.count++] = e.second;
+    tot = std::max<unsigned long long>(tot, e.second);
+  }
+  if (z.count)
+    hipLaunchKernelGGL(k_tr_zero_many, dim3((unsigned)std::min<unsigned long long>((tot / 16 + 255) / 256 + 1, 4096)),
+                       dim3(256), 0, s, z);
+  TT2_HIP(hipGetLastError());
+}
+
+// Σ g² partials per block: 16-byte loads when the gradient buffer is 16-byte aligned (a caller-bound
+// buffer need not be), the tail by block 0
+constexpr int TR_SUMSQ_BLOCKS = 1024;
+__global__ __launch_bounds__(256) void k_tr_sumsq(const float* __restrict__ g, long n, float* __restrict__ part, int vec) {
   __shared__ float s4[16];
   float acc = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) acc += g[i] * g[i];
+  const long n4 = vec ? n / 4 : 0;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = g4[i];
+    acc += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+  }
+  for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    acc += g[i] * g[i];
   acc = block_sum(acc, s4);
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
@@ -3005,8 +3061,9 @@ static void tr_persist_backward(tt2_train_ctx* c, const TrAtt& at, const uint8_t
   grow(c->tbCtl, sizeof(unsigned) * ((size_t)TB_NPH * TP_NREP * TP_NB + 16));
   if (!c->tp_ctl_host) TT2_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->tp_ctl_host), 4 * sizeof(int)));
   // rows >= B of the dG exchange rows stay zero (A-operand padding); tags restart at 1 every launch
-  for (DevBuf* d : {&c->tbG1X, &c->tbG2X, &c->tbQX, &c->tpEX, &c->tbCtl}) TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
-  TT2_HIP(hipMemsetAsync(c->DWGP.p, 0, c->DWGP.bytes, s));
+  tr_zero_many({{c->tbG1X.p, c->tbG1X.bytes}, {c->tbG2X.p, c->tbG2X.bytes}, {c->tbQX.p, c->tbQX.bytes},
+                {c->tpEX.p, c->tpEX.bytes}, {c->tbCtl.p, c->tbCtl.bytes}, {c->DWGP.p, c->DWGP.bytes}},
+               s);
   TbArgs a{};
   a.B = B; a.T = T; a.Tin = Tin; a.NT = NT; a.z = c->cfg.zoneout;
   a.K1T = c->hK1T.as<__bf16>(); a.K2T = c->hK2T.as<__bf16>(); a.Wq = c->hWq.as<__bf16>();
@@ -3126,11 +3183,10 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   float* X1 = c->X1.as<float>();
   float* X2 = c->X2.as<float>();
   float* PIN = c->PIN.as<float>();
-  TT2_HIP(hipMemsetAsync(X1, 0, sizeof(float) * (size_t)B * LX1, s));  // slot 0: ctx_{-1} = h_{-1} = 0
-  TT2_HIP(hipMemsetAsync(X2, 0, sizeof(float) * (size_t)B * 2 * H, s));
-  TT2_HIP(hipMemsetAsync(c->C1.p, 0, sizeof(float) * (size_t)B * H, s));
-  TT2_HIP(hipMemsetAsync(c->C2.p, 0, sizeof(float) * (size_t)B * H, s));
-  TT2_HIP(hipMemsetAsync(c->CUM.p, 0, sizeof(float) * (size_t)B * Tin, s));
+  tr_zero_many({{X1, sizeof(float) * (size_t)B * LX1},  // slot 0: ctx_{-1} = h_{-1} = 0
+                {X2, sizeof(float) * (size_t)B * 2 * H}, {c->C1.p, sizeof(float) * (size_t)B * H},
+                {c->C2.p, sizeof(float) * (size_t)B * H}, {c->CUM.p, sizeof(float) * (size_t)B * Tin}},
+               s);
   hipLaunchKernelGGL(k_tr_inputs, dim3(nblk(TB * NM)), dim3(256), 0, s, tg, B, T, NM, c->XIN.as<float>());
   hipLaunchKernelGGL(k_tr_values, dim3(nblk((long)B * Tin * D)), dim3(256), 0, s, mem, lens, B, Tin, D,
                      c->values.as<float>());
@@ -3313,10 +3369,11 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
                        c->WsT.as<float>(), TB, H + D);
   else
     tr_gemm((int)TB, H + D, 1, c->dST.as<float>(), 1, c->WsT.as<float>(), H + D, dPIN, H + D, s, nullptr, dPIN, H + D);
-  TT2_HIP(hipMemsetAsync(dX1 + TB * LX1, 0, sizeof(float) * (size_t)B * LX1, s));
-  TT2_HIP(hipMemsetAsync(dX2 + TB * 2 * H, 0, sizeof(float) * (size_t)B * 2 * H, s));
-  for (DevBuf* d : {&c->DC1, &c->DC2, &c->R1, &c->R2, &c->DKEYS, &c->DCUM, &c->dV, &c->dBA, &c->dKC, &c->dBC})
-    TT2_HIP(hipMemsetAsync(d->p, 0, d->bytes, s));
+  tr_zero_many({{dX1 + TB * LX1, sizeof(float) * (size_t)B * LX1}, {dX2 + TB * 2 * H, sizeof(float) * (size_t)B * 2 * H},
+                {c->DC1.p, c->DC1.bytes}, {c->DC2.p, c->DC2.bytes}, {c->R1.p, c->R1.bytes}, {c->R2.p, c->R2.bytes},
+                {c->DKEYS.p, c->DKEYS.bytes}, {c->DCUM.p, c->DCUM.bytes}, {c->dV.p, c->dV.bytes}, {c->dBA.p, c->dBA.bytes},
+                {c->dKC.p, c->dKC.bytes}, {c->dBC.p, c->dBC.bytes}},
+               s);
   // the attention backward as one launch of nq work-groups per row (k_tr_att_bwd_q; TT2_TR_ATTQ=0: the
   // two per-tile launches)
   static const bool att_q_env = [] {
@@ -4386,8 +4443,9 @@ static void tr_apply(tt2_train_ctx* c, float lr, int global_step, hipStream_t s)
       for (int i = 0; i < 6; ++i) upd(fe_ref_scope(c, r) + "conv2d_" + std::to_string(i) + "/", c->cfg.reference_filters[i]);
     c->f_ran = false;
   }
-  hipLaunchKernelGGL(k_tr_sumsq, dim3(256), dim3(256), 0, s, c->grads, c->total, c->part.as<float>());
-  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 256, 1.f, red + 3, 1);
+  hipLaunchKernelGGL(k_tr_sumsq, dim3(TR_SUMSQ_BLOCKS), dim3(256), 0, s, c->grads, c->total, c->part.as<float>(),
+                     (int)(reinterpret_cast<uintptr_t>(c->grads) % 16 == 0));
+  hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), TR_SUMSQ_BLOCKS, 1.f, red + 3, 1);
   const double b1 = c->cfg.adam_beta1, b2 = c->cfg.adam_beta2;
   const int t = std::max(1, global_step);
   const float lr_t = (float)(lr * std::sqrt(1.0 - std::pow(b2, t)) / (1.0 - std::pow(b1, t)));
