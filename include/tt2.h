@@ -435,7 +435,7 @@ tt2_status tt2_gl_synthesize_dev(tt2_gl_ctx* ctx, const float* spec_d, int T, in
 typedef struct tt2_train_config {
   int batch;               /* rows per step on this device (configs[4]: 64) */
   int max_T_in;            /* <= 320 (attention-kernel LDS budget) */
-  int max_T_out;           /* decoder steps (r = 1) */
+  int max_T_out;           /* frames (decoder steps · outputs_per_step) */
   int memory_dim;          /* D_mem (1024 fork default) */
   int num_mels;            /* 80 */
   int prenet_units;        /* 256 (both prenet layers) */
@@ -496,6 +496,12 @@ typedef struct tt2_train_config {
    * softmax; the backward multiplies the softmax form by (1 - sigmoid(e_j)).  Runs the per-step
    * attention launches (the persistent forward keeps the softmax). */
   int smoothing;
+  /* hparams.outputs_per_step r (hparams.py:140; tacotron.py:322-324; helpers.py:78,129): each decoder
+   * step projects r frames (frame projection num_mels*r wide, stop projection r wide) and is fed the
+   * last of the r target frames of the previous step (targets[:, r-1::r]).  T_out (the frame count of
+   * targets / stop targets / postnet masks) must be a multiple of r; prenet and zoneout masks and the
+   * teacher-forcing draw are per decoder step (T_out / r); alignments are [B][T_in][T_out / r]. */
+  int outputs_per_step;
 } tt2_train_config;
 
 typedef struct tt2_train_ctx tt2_train_ctx;
@@ -524,8 +530,9 @@ tt2_status tt2_train_bind_grads_dev(tt2_train_ctx* ctx, float* grads_d, int64_t*
 tt2_status tt2_train_moving_stats_dev(tt2_train_ctx* ctx, float* buf_d, int64_t* n_out, int unpack,
                                       void* stream);
 /* Forward + losses + backward on DEVICE inputs: memory [B,T_in,D] (encoder outputs ⊕ style),
- * lengths int32 [B], mel targets [B,T_out,80], stop targets [B,T_out], prenet keep bits u8
- * [T_out,2,B,P], zoneout keep bits u8 [T_out,4,B,H] (c1,h1,c2,h2) or NULL (inference mix),
+ * lengths int32 [B], mel targets [B,T_out,80], stop targets [B,T_out] (T_out frames, a multiple of
+ * cfg.outputs_per_step r), prenet keep bits u8 [T_out/r,2,B,P] and zoneout keep bits u8
+ * [T_out/r,4,B,H] (c1,h1,c2,h2; one set per decoder step) or NULL (inference mix),
  * Postnet dropout keep bits u8 [layers,B,T_out,channels] or NULL (no dropout; cfg.postnet only).
  * Gradients (incl. L2) land in the flat gradient buffer; enqueued on `stream`. */
 tt2_status tt2_train_forward_backward_dev(tt2_train_ctx* ctx, const float* memory_d,
@@ -558,9 +565,10 @@ tt2_status tt2_train_forward_backward_text_dev(tt2_train_ctx* ctx, const int32_t
  * the reference's RuntimeError (tacotron.py:56-57). */
 tt2_status tt2_train_set_target_lengths(tt2_train_ctx* ctx, const int32_t* lengths);
 /* Teacher-forcing draw of the next forward_backward calls (TacoTrainingHelper.next_inputs,
- * helpers.py:122-133): feed_target[t] (host u8 [T_out], copied) = 1 feeds the target frame t-1 to
- * step t, 0 feeds the decoder's own (unclipped) frame t-1, whose gradient then flows back through
- * the prenet into frame t-1; feed_target[0] is ignored (go frame).  It is the outcome of the
+ * helpers.py:122-133): feed_target[t] (host u8, one per decoder step [T_out/r], copied) = 1 feeds
+ * the target frame t·r-1 to step t, 0 feeds the last of the decoder's own (unclipped) r frames of
+ * step t-1, whose gradient then flows back through the prenet into that frame; feed_target[0] is
+ * ignored (go frame).  It is the outcome of the
  * reference's per-step draw u < ratio (ratio: constant or _teacher_forcing_ratio_decay,
  * helpers.py:140-180), injected like the dropout keep bits.  NULL = every step teacher-forced. */
 tt2_status tt2_train_set_teacher_forcing(tt2_train_ctx* ctx, const uint8_t* feed_target, int T_out);

@@ -83,16 +83,22 @@ def _conv_same(cum, k, b):
 def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneout=0.1, feed_target=None,
             smoothing=False):
     """Teacher-forced decoder forward.  W: dict name -> torch tensor (requires_grad as wanted);
-    memory [B,T_in,D]; lengths [B]; targets [B,T,80]; prenet_masks [T,2,B,P] keep bits;
+    memory [B,T_in,D]; lengths [B]; targets [B,T·r,80] with r = outputs_per_step (the width of the
+    stop projection, tacotron.py:322-324); prenet_masks [T,2,B,P] keep bits per decoder step;
     zoneout_masks [T,4,B,H] keep bits (c1,h1,c2,h2; training zoneout) or None (inference mix);
     feed_target [T] (None = all 1): the outcome of TacoTrainingHelper.next_inputs' per-step draw
-    u < ratio (helpers.py:122-133) -- step t (t >= 1) gets the target frame t-1 when 1, else the
-    decoder's own unclipped frame t-1 (outputs[:, -output_dim:]), through which gradients flow.
+    u < ratio (helpers.py:122-133) -- step t (t >= 1) gets the target frame t·r-1 when 1
+    (targets[:, r-1::r], helpers.py:78), else the last of the decoder's own unclipped r frames of
+    step t-1 (outputs[:, -output_dim:], helpers.py:129), through which gradients flow.
     smoothing: hp.smoothing (attention.py:71-91,150), a = sigmoid(e) / sum sigmoid(e) over the
     unmasked positions (sigmoid(-inf) = 0) instead of the softmax.
-    Returns frames [B,T,80], stop logits [B,T], alignments [B,T_in,T]."""
+    Returns frames [B,T·r,80], stop logits [B,T·r] (the reshapes of tacotron.py:355-358),
+    alignments [B,T_in,T]."""
     B, T_in, D = memory.shape
-    T = targets.shape[1]
+    nm = targets.shape[2]
+    r = W[SP + "bias"].shape[0]
+    assert targets.shape[1] % r == 0, "targets must hold a multiple of outputs_per_step frames"
+    T = targets.shape[1] // r
     dt = memory.dtype
     mask = (torch.arange(T_in)[None, :] < torch.as_tensor(lengths)[:, None]).to(dt)
     values = memory * mask[:, :, None]                                  # BahdanauAttention memory
@@ -138,14 +144,15 @@ def forward(W, memory, lengths, targets, prenet_masks, zoneout_masks=None, zoneo
         cum = cum + a
         ctx = (a[:, :, None] * values).sum(1)
         pin = torch.cat([o2, ctx], 1)
-        frames.append(pin @ W[FP + "kernel"] + W[FP + "bias"])
-        stops.append((pin @ W[SP + "kernel"] + W[SP + "bias"])[:, 0])
+        frames.append(pin @ W[FP + "kernel"] + W[FP + "bias"])      # [B, nm·r]
+        stops.append(pin @ W[SP + "kernel"] + W[SP + "bias"])       # [B, r]
         aligns.append(a)
         if feed_target is None or t + 1 >= T or feed_target[t + 1]:
-            frame_in = targets[:, t]
+            frame_in = targets[:, t * r + r - 1]
         else:
-            frame_in = frames[-1]
-    return torch.stack(frames, 1), torch.stack(stops, 1), torch.stack(aligns, 2)
+            frame_in = frames[-1][:, -nm:]
+    return (torch.stack(frames, 1).reshape(B, T * r, nm), torch.stack(stops, 1).reshape(B, T * r),
+            torch.stack(aligns, 2))
 
 
 def clip_decoder_output(frames, clip=(-4.1, 4.0)):

@@ -48,6 +48,7 @@ struct tt2_train_ctx {
   tt2_train_config cfg{};
   int B = 0, Tm = 0, Tin = 0, D = 0, NM = 0, P = 0, H = 0, A = 0, F = 0, KW = 0;
   int LX1 = 0;  // P + D + H
+  int R = 1;    // outputs_per_step: frames per decoder step
   std::vector<TrVar> vars;
   std::map<std::string, int> index;
   long total = 0;
@@ -84,7 +85,9 @@ struct tt2_train_ctx {
   DevBuf BNM, BNV, PPRJ, dPP, DYb, DZb, dPXa, dPXb, WFLIP, PWT, CLIPM, pn_part;
   int PL = 0, PC = 0, PK = 0;
   bool pn_masks = false;
-  int T_last = 0, Tin_last = 0;
+  int T_last = 0, Tin_last = 0;  // decoder steps / encoder positions of the last forward_backward
+  int Tf_last = 0;               // its frame count T_last * R
+  DevBuf FRT;                    // R > 1: the clipped frames time-major [T_f][B][NM] (the Postnet's input)
   bool pn_ran = false;  // batch stats of the last forward are valid (moving averages in apply)
   // bf16 Postnet convolutions over padded planes (gemm.h conv_bf16_planes): the layer input / dz
   // planes (pad rows zeroed when the shape changes) and the transposed bf16 weights of one layer
@@ -274,15 +277,29 @@ __global__ void k_tr_to_bf16(const float* __restrict__ src, long n, __bf16* __re
 }
 
 // ---- forward -------------------------------------------------------------------------------
-// XIN[t][b] = t == 0 ? GO (zeros, helpers.py:136-138) : targets[b][t-1]  (helpers.py:126-129)
-__global__ void k_tr_inputs(const float* __restrict__ tg, int B, int T, int NM, float* __restrict__ xin) {
+// XIN[t][b] = t == 0 ? GO (zeros, helpers.py:136-138) : targets[b][t·r - 1], the last frame of step
+// t-1's r (targets[:, r-1::r], helpers.py:78,126-129); targets [B][T·r][NM]
+__global__ void k_tr_inputs(const float* __restrict__ tg, int B, int T, int NM, int r, float* __restrict__ xin) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long n = (long)T * B * NM;
   if (i >= n) return;
   const int c = (int)(i % NM);
   const int b = (int)((i / NM) % B);
   const int t = (int)(i / ((long)NM * B));
-  xin[i] = t == 0 ? 0.f : tg[((long)b * T + (t - 1)) * NM + c];
+  xin[i] = t == 0 ? 0.f : tg[((long)b * T * r + ((long)t * r - 1)) * NM + c];
+}
+// frame f of row b in the projection output [T][B][r·NM] (f = t·r + i -> row t·B + b, columns i·NM..)
+__device__ __forceinline__ long tr_frame_off(int f, int b, int B, int r, int NM) {
+  return (((long)(f / r) * B + b) * r + f % r) * NM;
+}
+// R > 1: dst[f][b][:] = FR frame (f, b): the clipped frames time-major for the Postnet's convolutions
+__global__ void k_tr_frames_tm(const float* __restrict__ FR, int B, int Tf, int NM, int r, float* __restrict__ dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)Tf * B * NM) return;
+  const int c = (int)(i % NM);
+  const int b = (int)((i / NM) % B);
+  const int f = (int)(i / ((long)NM * B));
+  dst[i] = FR[tr_frame_off(f, b, B, r, NM) + c];
 }
 // values = memory · seq_mask (BahdanauAttention memory masking)
 __global__ void k_tr_values(const float* __restrict__ mem, const int* __restrict__ lens, int B, int Tin, int D,
@@ -1159,18 +1176,22 @@ __global__ __launch_bounds__(256) void k_tr_ctx(TrAtt a) {
 // the reduction; k_tr_loss_final / k_tr_div finish it).  inv_f = 1 / (MSE normaliser).
 __global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const float* __restrict__ ST,
                                                  const float* __restrict__ tg, const float* __restrict__ stg, int B,
-                                                 int T, int NM, int clip, float lo, float hi, float* __restrict__ dFR,
+                                                 int T, int NM, int r, int clip, float lo, float hi,
+                                                 float* __restrict__ dFR,
                                                  float* __restrict__ dST, float* __restrict__ part,
                                                  uint8_t* __restrict__ clipm, const int* __restrict__ tlen, float inv_f,
                                                  float pos_weight) {
   __shared__ float s4[16];
+  // T = frames here (decoder steps · r); frame (t, b) of FR / dFR / clipm at tr_frame_off, stop (t, b)
+  // of ST / dST at [t / r][b][t % r] (the r-wide stop projection; r = 1: [t][b])
   const long nf = (long)T * B * NM;
   const float inv_s = 1.0f / (float)((long)T * B);
   float sq = 0.f, ce = 0.f, nz = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % NM);
-    const int b = (int)((i / NM) % B);
-    const int t = (int)(i / ((long)NM * B));
+  for (long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x; i0 < nf; i0 += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i0 % NM);
+    const int b = (int)((i0 / NM) % B);
+    const int t = (int)(i0 / ((long)NM * B));
+    const long i = r == 1 ? i0 : tr_frame_off(t, b, B, r, NM) + c;
     // decoder_output = clip(frames, lo, hi) when clip_outputs (tacotron.py:360-361); the clip's
     // gradient passes where lo <= x <= hi (TF maximum/minimum)
     const float x = FR[i];
@@ -1183,8 +1204,9 @@ __global__ __launch_bounds__(256) void k_tr_loss(float* __restrict__ FR, const f
     if (clipm) clipm[i] = pass ? 1 : 0;
     FR[i] = y;
   }
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < (long)T * B; i += (long)gridDim.x * blockDim.x) {
-    const int b = (int)(i % B), t = (int)(i / B);
+  for (long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x; i0 < (long)T * B; i0 += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i0 % B), t = (int)(i0 / B);
+    const long i = ((long)(t / r) * B + b) * r + t % r;
     const float x = ST[i], z = stg[(long)b * T + t];
     if (!tlen) {
       ce += fmaxf(x, 0.f) - x * z + log1pf(expf(-fabsf(x)));
@@ -2428,8 +2450,8 @@ __global__ void k_pn_flip(const float* __restrict__ w, int kw, int cin, int cout
 // after loss: mel = clip(dec[t][b] + proj[b][t]) (tacotron.py:375-378); MSE partials; d proj
 // inv = 1 / (MSE normaliser); tlen masks t >= lengths[b] (mask_decoder, MaskedMSE)
 __global__ __launch_bounds__(256) void k_pn_after_loss(const float* __restrict__ FR, const float* __restrict__ prj,
-                                                       const float* __restrict__ tg, int B, int T, int NM, int clip,
-                                                       float lo, float hi, float* __restrict__ dprj,
+                                                       const float* __restrict__ tg, int B, int T, int NM, int r,
+                                                       int clip, float lo, float hi, float* __restrict__ dprj,
                                                        float* __restrict__ part, const int* __restrict__ tlen,
                                                        float inv) {
   __shared__ float s16[16];
@@ -2439,7 +2461,7 @@ __global__ __launch_bounds__(256) void k_pn_after_loss(const float* __restrict__
     const int c = (int)(i % NM);
     const long bt = i / NM;
     const int t = (int)(bt % T), b = (int)(bt / T);
-    const float x = FR[((long)t * B + b) * NM + c] + prj[i];
+    const float x = FR[tr_frame_off(t, b, B, r, NM) + c] + prj[i];
     const float y = clip ? fminf(fmaxf(x, lo), hi) : x;
     const float d = (!tlen || t < tlen[b]) ? y - tg[i] : 0.f;
     sq += d * d;
@@ -2450,13 +2472,13 @@ __global__ __launch_bounds__(256) void k_pn_after_loss(const float* __restrict__
 }
 // dFR[t][b] += clipmask(frames) * (d mel + d postnet input)   (dec = clip(frames) feeds both)
 __global__ void k_pn_add_ddec(const float* __restrict__ dprj, const float* __restrict__ dx0, const uint8_t* clipm,
-                              int B, int T, int NM, float* __restrict__ dFR) {
+                              int B, int T, int NM, int r, float* __restrict__ dFR) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)B * T * NM) return;
   const int c = (int)(i % NM);
   const long bt = i / NM;
   const int t = (int)(bt % T), b = (int)(bt / T);
-  const long j = ((long)t * B + b) * NM + c;
+  const long j = tr_frame_off(t, b, B, r, NM) + c;
   if (clipm[j]) dFR[j] += dprj[i] + dx0[i];
 }
 __global__ void k_pn_moving(float* __restrict__ mm, float* __restrict__ mv, const float* __restrict__ mean,
@@ -2684,10 +2706,10 @@ static void tr_build_vars(tt2_train_ctx* c) {
   add(L1V("bias"), {4 * H}, false);
   add(L2V("kernel"), {2 * H, 4 * H}, false);
   add(L2V("bias"), {4 * H}, false);
-  add(FPV("kernel"), {H + D, NM}, false);
-  add(FPV("bias"), {NM}, false);
-  add(SPV("kernel"), {H + D, 1}, false);
-  add(SPV("bias"), {1}, false);
+  add(FPV("kernel"), {H + D, (int64_t)NM * c->R}, false);  // num_mels * r (tacotron.py:322)
+  add(FPV("bias"), {(int64_t)NM * c->R}, false);
+  add(SPV("kernel"), {H + D, c->R}, false);                   // shape = r (tacotron.py:324)
+  add(SPV("bias"), {c->R}, false);
   if (c->cfg.frontend) tr_front_build_vars(c, add);
   if (!c->cfg.postnet) return;
   // Postnet (oracle/train_ref.py postnet_var_names / postnet_stat_names); moving statistics are
@@ -2720,7 +2742,7 @@ static void tr_alloc(tt2_train_ctx* c) {
   f(c->params, c->total); f(c->grads_own, c->total + 1);  // + the status word (k_tr_status)
   f(c->adam_m, c->total); f(c->adam_v, c->total);
   c->grads = c->grads_own.as<float>();
-  f(c->K1T, 4 * H * LX1); f(c->K2T, 4 * H * 2 * H); f(c->WqT, A * H); f(c->WfT, NM * (H + D)); f(c->WsT, H + D);
+  f(c->K1T, 4 * H * LX1); f(c->K2T, 4 * H * 2 * H); f(c->WqT, A * H); f(c->WfT, NM * c->R * (H + D)); f(c->WsT, c->R * (H + D));
   f(c->WmT, A * D); f(c->Wp2T, P * P);
   f(c->values, B * Tin * D); f(c->keys, B * Tin * A);
   f(c->X1, (T + 1) * B * LX1); f(c->X2, (T + 1) * B * 2 * H); f(c->PIN, TB * (H + D));
@@ -2783,11 +2805,13 @@ static void tr_alloc(tt2_train_ctx* c) {
       c->pnWt.alloc((size_t)Wr * PK * W * 2);
     }
     c->CLIPM.alloc((size_t)TB * NM);
+    if (c->R > 1) f(c->FRT, TB * NM);
   }
 }
 
 // Postnet forward (training-mode BN + dropout) + after loss + backward; adds d decoder_output into
-// dFR (through the frame clip).  Runs between the decoder forward and the decoder backward.
+// dFR (through the frame clip).  Runs between the decoder forward and the decoder backward.  T = frames
+// (decoder steps · r).
 static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, int T, hipStream_t s) {
   const int B = c->B, NM = c->NM, C = c->PC, KW = c->PK, L = c->PL;
   const long M = (long)B * T;
@@ -2804,8 +2828,8 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
     hipLaunchKernelGGL(k_pn_colstat_final, dim3((C + 31) / 32), dim3(TR_FIN), 0, s, part, S, C, 1.0f / (float)M, out);
   };
   auto conv_in = [&](int i, GemmArgs& g) {  // layer i's input as an implicit-im2col conv1d operand
-    if (i == 0) {  // clipped decoder frames, time-major [T][B][NM]
-      g.A = c->FR.as<float>(); g.C = NM; g.xs_b = NM; g.xs_t = (long)B * NM;
+    if (i == 0) {  // clipped decoder frames, time-major [T][B][NM] (r > 1: the FRT copy)
+      g.A = c->R > 1 ? c->FRT.as<float>() : c->FR.as<float>(); g.C = NM; g.xs_b = NM; g.xs_t = (long)B * NM;
     } else {
       g.A = c->PX[i].as<float>(); g.C = C; g.xs_b = (long)T * C; g.xs_t = C;
     }
@@ -2819,6 +2843,9 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
     c->pn_pl_T = T;
   }
   const int Cr = (C + 255) / 256 * 256;
+  if (c->R > 1)
+    hipLaunchKernelGGL(k_tr_frames_tm, dim3(nblk(M * NM)), dim3(256), 0, s, c->FR.as<float>(), B, T, NM, c->R,
+                       c->FRT.as<float>());
   for (int i = 0; i < L; ++i) {
     const std::string sc = pn_scope(i + 1);
     if (planes && i > 0) {  // layer i's input planes were written by layer i-1's BN forward
@@ -2849,7 +2876,7 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
   const int* tlen = c->cfg.mask_decoder ? c->TLEN.as<int>() : nullptr;
   const double nmse = c->cfg.mask_decoder ? (double)c->tlen_sum * NM : (double)M * NM;
   hipLaunchKernelGGL(k_pn_after_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->PPRJ.as<float>(), tg, B, T,
-                     NM, c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dPP.as<float>(), c->part.as<float>(),
+                     NM, c->R, c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dPP.as<float>(), c->part.as<float>(),
                      tlen, (float)(1.0 / nmse));
   hipLaunchKernelGGL(k_tr_sum_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 256, (float)(1.0 / nmse),
                      red + 4, 0);
@@ -2905,7 +2932,7 @@ static void tr_postnet(tt2_train_ctx* c, const float* tg, const uint8_t* pnm, in
     std::swap(dxn, dxo);
   }
   hipLaunchKernelGGL(k_pn_add_ddec, dim3(nblk(M * NM)), dim3(256), 0, s, c->dPP.as<float>(), dxn,
-                     c->CLIPM.as<uint8_t>(), B, T, NM, c->dFR.as<float>());
+                     c->CLIPM.as<uint8_t>(), B, T, NM, c->R, c->dFR.as<float>());
   c->pn_ran = true;
 }
 
@@ -3140,9 +3167,15 @@ static void tr_write_status(tt2_train_ctx* c, hipStream_t s) {
 }
 
 static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* lens, const float* tg, const float* stg,
-                                const uint8_t* pm, const uint8_t* zm, const uint8_t* pnm, int Tin, int T,
+                                const uint8_t* pm, const uint8_t* zm, const uint8_t* pnm, int Tin, int Tf,
                                 hipStream_t s) {
   const int B = c->B, D = c->D, H = c->H, P = c->P, A = c->A, F = c->F, KW = c->KW, NM = c->NM, LX1 = c->LX1;
+  // Tf frames = T decoder steps of R frames each (outputs_per_step; the feeder pads targets to a
+  // multiple of r, feeder.py:283-310)
+  const int R = c->R;
+  TT2_CHECK(Tf % R == 0, TT2_ERR_SHAPE_MISMATCH, "T_out must be a multiple of outputs_per_step");
+  const int T = Tf / R;
+  const int NR = NM * R;  // frame projection width num_mels * r
   const long TB = (long)T * B;
   const float z = c->cfg.zoneout;
   // tacotron.py:56-57 (the reference raises RuntimeError) and the MaskedMSE shape assert
@@ -3150,9 +3183,11 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   TT2_CHECK(!c->cfg.mask_decoder || c->has_tlen, TT2_ERR_STATE,
             "Model set to mask paddings but no targets lengths provided for the mask! "
             "(tt2_train_set_target_lengths)");
-  TT2_CHECK(!c->cfg.mask_decoder || c->tlen_max == T, TT2_ERR_SHAPE_MISMATCH,
-            "mask_decoder: max(target lengths) must equal T_out");
+  // (sequence_mask rounds max(lengths) up to a multiple of r, modules.py:523-530)
+  TT2_CHECK(!c->cfg.mask_decoder || (c->tlen_max + R - 1) / R * R == Tf, TT2_ERR_SHAPE_MISMATCH,
+            "mask_decoder: max(target lengths) rounded up to outputs_per_step must equal T_out");
   c->T_last = T;
+  c->Tf_last = Tf;
   c->Tin_last = Tin;
   g_tr_kpart = &c->kpart;
   g_tr_prec = c->cfg.precision ? 2 : 0;
@@ -3161,8 +3196,8 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_transpose(pvar(c, L1V("kernel")), LX1, 4 * H, 4 * H, c->K1T.as<float>(), LX1, s);
   tr_transpose(pvar(c, L2V("kernel")), 2 * H, 4 * H, 4 * H, c->K2T.as<float>(), 2 * H, s);
   tr_transpose(pvar(c, vn("decoder/query_layer/kernel")), H, A, A, c->WqT.as<float>(), H, s);
-  tr_transpose(pvar(c, FPV("kernel")), H + D, NM, NM, c->WfT.as<float>(), H + D, s);
-  tr_transpose(pvar(c, SPV("kernel")), H + D, 1, 1, c->WsT.as<float>(), H + D, s);
+  tr_transpose(pvar(c, FPV("kernel")), H + D, NR, NR, c->WfT.as<float>(), H + D, s);
+  tr_transpose(pvar(c, SPV("kernel")), H + D, R, R, c->WsT.as<float>(), H + D, s);
   tr_transpose(pvar(c, vn("memory_layer/kernel")), D, A, A, c->WmT.as<float>(), D, s);
   tr_transpose(pvar(c, PRV(2, "kernel")), P, P, P, c->Wp2T.as<float>(), P, s);
   if (c->cfg.precision) {
@@ -3187,7 +3222,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
                 {X2, sizeof(float) * (size_t)B * 2 * H}, {c->C1.p, sizeof(float) * (size_t)B * H},
                 {c->C2.p, sizeof(float) * (size_t)B * H}, {c->CUM.p, sizeof(float) * (size_t)B * Tin}},
                s);
-  hipLaunchKernelGGL(k_tr_inputs, dim3(nblk(TB * NM)), dim3(256), 0, s, tg, B, T, NM, c->XIN.as<float>());
+  hipLaunchKernelGGL(k_tr_inputs, dim3(nblk(TB * NM)), dim3(256), 0, s, tg, B, T, NM, R, c->XIN.as<float>());
   hipLaunchKernelGGL(k_tr_values, dim3(nblk((long)B * Tin * D)), dim3(256), 0, s, mem, lens, B, Tin, D,
                      c->values.as<float>());
   tr_gemm(B * Tin, A, D, c->values.as<float>(), D, pvar(c, vn("memory_layer/kernel")), A, c->keys.as<float>(), A, s);
@@ -3277,8 +3312,9 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     if (free_run && t > 0 && !c->feed[t]) {
       float* xin = c->XIN.as<float>() + s1 * NM;
       float* p1 = c->P1.as<float>() + s1 * P;
-      tr_gemm(B, NM, H + D, PIN + (s1 - B) * (H + D), H + D, pvar(c, FPV("kernel")), NM, xin, NM, s,
-              pvar(c, FPV("bias")));
+      // the last of step t-1's r frames (outputs[:, -output_dim:], helpers.py:129)
+      tr_gemm(B, NM, H + D, PIN + (s1 - B) * (H + D), H + D, pvar(c, FPV("kernel")) + (R - 1) * NM, NR, xin, NM, s,
+              pvar(c, FPV("bias")) + (R - 1) * NM);
       tr_gemm(B, P, NM, xin, NM, pvar(c, PRV(1, "kernel")), P, p1, P, s, pvar(c, PRV(1, "bias")), nullptr, 0,
               ACT_RELU);
       hipLaunchKernelGGL(k_tr_prenet_mask, dim3(nblk((long)B * P)), dim3(256), 0, s, p1, (long)P,
@@ -3344,27 +3380,31 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     }
     hipLaunchKernelGGL(k_tr_ctx, dim3((D + 63) / 64, B), dim3(256), sizeof(float) * Tin, s, at);
   }
-  tr_gemm((int)TB, NM, H + D, PIN, H + D, pvar(c, FPV("kernel")), NM, c->FR.as<float>(), NM, s, pvar(c, FPV("bias")));
-  tr_gemm((int)TB, 1, H + D, PIN, H + D, pvar(c, SPV("kernel")), 1, c->ST.as<float>(), 1, s, pvar(c, SPV("bias")));
+  tr_gemm((int)TB, NR, H + D, PIN, H + D, pvar(c, FPV("kernel")), NR, c->FR.as<float>(), NR, s, pvar(c, FPV("bias")));
+  tr_gemm((int)TB, R, H + D, PIN, H + D, pvar(c, SPV("kernel")), R, c->ST.as<float>(), R, s, pvar(c, SPV("bias")));
   float* red = c->red.as<float>();
   const int* tlen = c->cfg.mask_decoder ? c->TLEN.as<int>() : nullptr;
-  const long nmse = c->cfg.mask_decoder ? c->tlen_sum * NM : TB * NM;
-  hipLaunchKernelGGL(k_tr_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->ST.as<float>(), tg, stg, B, T, NM,
-                     c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dFR.as<float>(), c->dST.as<float>(),
+  const long nmse = c->cfg.mask_decoder ? c->tlen_sum * NM : TB * NR;
+  hipLaunchKernelGGL(k_tr_loss, dim3(256), dim3(256), 0, s, c->FR.as<float>(), c->ST.as<float>(), tg, stg, B, Tf, NM,
+                     R, c->cfg.clip_outputs, c->cfg.clip_lo, c->cfg.clip_hi, c->dFR.as<float>(), c->dST.as<float>(),
                      c->part.as<float>(), c->cfg.postnet ? c->CLIPM.as<uint8_t>() : nullptr, tlen,
                      (float)(1.0 / (double)nmse), c->cfg.pos_weight);
-  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 256, nmse, tlen ? 0L : TB, red);
-  if (tlen) hipLaunchKernelGGL(k_tr_div, dim3(nblk(TB)), dim3(256), 0, s, c->dST.as<float>(), TB, red + 5);
+  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(256), 0, s, c->part.as<float>(), 256, nmse, tlen ? 0L : TB * R,
+                     red);
+  if (tlen) hipLaunchKernelGGL(k_tr_div, dim3(nblk(TB * R)), dim3(256), 0, s, c->dST.as<float>(), TB * R, red + 5);
   c->pn_ran = false;
-  if (c->cfg.postnet) tr_postnet(c, tg, pnm, T, s);
+  if (c->cfg.postnet) tr_postnet(c, tg, pnm, Tf, s);
 
   // ---- backward ----
   float* dPIN = c->dPIN.as<float>();
   float* dX1 = c->dX1.as<float>();
   float* dX2 = c->dX2.as<float>();
-  tr_gemm((int)TB, H + D, NM, c->dFR.as<float>(), NM, c->WfT.as<float>(), H + D, dPIN, H + D, s);
-  // + dST·W_s^T: a rank-1 update, streamed (as a K = 1 GEMM with the residual it took 0.69 ms)
-  if ((H + D) % 4 == 0)
+  tr_gemm((int)TB, H + D, NR, c->dFR.as<float>(), NR, c->WfT.as<float>(), H + D, dPIN, H + D, s);
+  // + dST·W_s^T: a rank-1 update, streamed (as a K = 1 GEMM with the residual it took 0.69 ms); rank r
+  // for r > 1
+  if (R > 1)
+    tr_gemm((int)TB, H + D, R, c->dST.as<float>(), R, c->WsT.as<float>(), H + D, dPIN, H + D, s, nullptr, dPIN, H + D);
+  else if ((H + D) % 4 == 0)
     hipLaunchKernelGGL(k_tr_rank1_add, dim3(2048), dim3(256), 0, s, dPIN, (long)(H + D), c->dST.as<float>(),
                        c->WsT.as<float>(), TB, H + D);
   else
@@ -3498,10 +3538,11 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
       hipLaunchKernelGGL(k_tr_prenet_bwd, dim3(nblk((long)B * P)), dim3(256), 0, s, dp, (long)P,
                          c->P1.as<float>() + s1 * P, (long)P, (long)B, P, dz);
       tr_gemm(B, NM, P, dz, P, c->W1T.as<float>(), NM, dx, NM, s);
-      float* dfr = c->dFR.as<float>() + (s1 - B) * NM;
-      tr_gemm(B, NM, P, dz, P, c->W1T.as<float>(), NM, dfr, NM, s, nullptr, dfr, NM);
+      float* dfr = c->dFR.as<float>() + (s1 - B) * NR + (R - 1) * NM;  // the last of step t-1's r frames
+      tr_gemm(B, NM, P, dz, P, c->W1T.as<float>(), NM, dfr, NR, s, nullptr, dfr, NR);
       float* dpin = dPIN + (s1 - B) * (H + D);
-      tr_gemm(B, H + D, NM, dx, NM, c->WfT.as<float>(), H + D, dpin, H + D, s, nullptr, dpin, H + D);
+      tr_gemm(B, H + D, NM, dx, NM, c->WfT.as<float>() + (long)(R - 1) * NM * (H + D), H + D, dpin, H + D, s, nullptr,
+              dpin, H + D);
     }
   }
 
@@ -3530,10 +3571,10 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   tr_colsum(c, c->dG2.as<float>(), TB, 4 * H, 4 * H, gvar(c, L2V("bias")), s);
   tr_transpose(PIN, TB, H + D, H + D, TBUF, TB, s);
   tr_gemm(H, A, TBi, TBUF, TB, c->DQ.as<float>(), A, gvar(c, vn("decoder/query_layer/kernel")), A, s);
-  tr_gemm(H + D, NM, TBi, TBUF, TB, c->dFR.as<float>(), NM, gvar(c, FPV("kernel")), NM, s);
-  tr_gemm(H + D, 1, TBi, TBUF, TB, c->dST.as<float>(), 1, gvar(c, SPV("kernel")), 1, s);
-  tr_colsum(c, c->dFR.as<float>(), TB, NM, NM, gvar(c, FPV("bias")), s);
-  tr_colsum(c, c->dST.as<float>(), TB, 1, 1, gvar(c, SPV("bias")), s);
+  tr_gemm(H + D, NR, TBi, TBUF, TB, c->dFR.as<float>(), NR, gvar(c, FPV("kernel")), NR, s);
+  tr_gemm(H + D, R, TBi, TBUF, TB, c->dST.as<float>(), R, gvar(c, SPV("kernel")), R, s);
+  tr_colsum(c, c->dFR.as<float>(), TB, NR, NR, gvar(c, FPV("bias")), s);
+  tr_colsum(c, c->dST.as<float>(), TB, R, R, gvar(c, SPV("bias")), s);
   // prenet
   hipLaunchKernelGGL(k_tr_prenet_bwd, dim3(nblk(TB * P)), dim3(256), 0, s, dX1, (long)LX1, X1, (long)LX1, TB, P,
                      c->dZ.as<float>());
@@ -4520,6 +4561,8 @@ void tt2_train_default_config(tt2_train_config* c, int batch, int max_T_in, int 
   c->mask_decoder = 0;
   c->pos_weight = 1.0f;
   c->adain = 0;
+  c->smoothing = 0;
+  c->outputs_per_step = 1;
 }
 
 tt2_status tt2_train_set_target_lengths(tt2_train_ctx* c, const int32_t* lengths) {
@@ -4630,6 +4673,8 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
       c->B = cfg->batch; c->Tm = cfg->max_T_out; c->Tin = cfg->max_T_in; c->D = cfg->memory_dim;
       c->NM = cfg->num_mels; c->P = cfg->prenet_units; c->H = cfg->decoder_lstm_units; c->A = cfg->attention_dim;
       c->F = cfg->attention_filters; c->KW = cfg->attention_kernel; c->LX1 = c->P + c->D + c->H;
+      c->R = cfg->outputs_per_step;
+      TT2_CHECK(c->R >= 1 && c->R <= c->Tm, TT2_ERR_INVALID_ARG, "outputs_per_step out of [1, max_T_out]");
       c->PL = cfg->postnet_layers; c->PC = cfg->postnet_channels; c->PK = cfg->postnet_kernel;
       TT2_CHECK(!cfg->postnet || (c->PL >= 1 && c->PL <= 8 && c->PC >= 1 && c->PK >= 1 && c->PK <= 64),
                 TT2_ERR_INVALID_ARG,
@@ -4875,7 +4920,7 @@ tt2_status tt2_train_get_tensor(tt2_train_ctx* c, const char* name, int which, f
       return;
     }
     if (c->cfg.postnet && std::string(name) == "postnet:projection") {  // Postnet residual [B,T,NM]
-      tr_d2h(c, host, c->PPRJ.p, sizeof(float) * (size_t)c->B * c->T_last * c->NM);
+      tr_d2h(c, host, c->PPRJ.p, sizeof(float) * (size_t)c->B * c->Tf_last * c->NM);
       return;
     }
     if (c->cfg.frontend && std::string(name) == "frontend:memory") {  // the front end's memory [B,T_in,D]
@@ -4913,20 +4958,22 @@ tt2_status tt2_train_outputs(tt2_train_ctx* c, float* frames, float* stop_logits
     TT2_CHECK(c, TT2_ERR_INVALID_ARG, "null ctx");
     TT2_HIP(hipSetDevice(c->dev));
     TT2_HIP(hipDeviceSynchronize());
-    const int B = c->B, T = c->T_last, NM = c->NM, Tin = c->Tin_last;
-    // device layouts are time-major [T][B][..]; the ABI returns [B][T][..] like tower_decoder_output
+    const int B = c->B, T = c->T_last, R = c->R, Tf = c->Tf_last, NM = c->NM, Tin = c->Tin_last;
+    // device layouts are step-major [T][B][r·..]; the ABI returns frames [B][T·r][..] like
+    // tower_decoder_output (tacotron.py:355-358: reshape [B, -1, num_mels])
     if (frames) {
-      std::vector<float> tmp((size_t)T * B * NM);
+      std::vector<float> tmp((size_t)Tf * B * NM);
       tr_d2h(c, tmp.data(), c->FR.p, sizeof(float) * tmp.size());
-      for (int t = 0; t < T; ++t)
+      for (int f = 0; f < Tf; ++f)
         for (int b = 0; b < B; ++b)
-          std::memcpy(frames + ((size_t)b * T + t) * NM, tmp.data() + ((size_t)t * B + b) * NM, sizeof(float) * NM);
+          std::memcpy(frames + ((size_t)b * Tf + f) * NM, tmp.data() + (((size_t)(f / R) * B + b) * R + f % R) * NM,
+                      sizeof(float) * NM);
     }
     if (stop_logits) {
-      std::vector<float> tmp((size_t)T * B);
+      std::vector<float> tmp((size_t)Tf * B);
       tr_d2h(c, tmp.data(), c->ST.p, sizeof(float) * tmp.size());
-      for (int t = 0; t < T; ++t)
-        for (int b = 0; b < B; ++b) stop_logits[(size_t)b * T + t] = tmp[(size_t)t * B + b];
+      for (int f = 0; f < Tf; ++f)
+        for (int b = 0; b < B; ++b) stop_logits[(size_t)b * Tf + f] = tmp[((size_t)(f / R) * B + b) * R + f % R];
     }
     if (alignments)  // [B][Tin][T] already
       tr_d2h(c, alignments, c->ALIGN.p, sizeof(float) * (size_t)B * Tin * T);

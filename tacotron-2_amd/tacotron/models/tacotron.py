@@ -274,8 +274,6 @@ class Tacotron():
         self._train_style = style
         # use_emt_disc / use_spk_disc / use_intercross are stored and never read by the reference
         # graph (tacotron.py:74-76): accepted and ignored alike
-        if hp.outputs_per_step != 1:
-            raise NotImplementedError("outputs_per_step = 1 on this build")
         n_emt, n_spk = (int(n_emt or 0), int(n_spk or 0)) if hp.tacotron_use_style_emb_disc else (0, 0)
         if n_emt and emt_labels is None or (n_spk and not emt_only and spk_labels is None):
             raise ValueError("the style-embedding classifiers (tacotron_use_style_emb_disc) need emt_labels "
@@ -336,9 +334,10 @@ class Tacotron():
         sub = lambda: int(r.integers(1 << 31))  # noqa: E731  (one fresh stream per mask per step)
         P, H, U = hp.prenet_layers[0], hp.decoder_lstm_units, hp.encoder_lstm_units
         zr, dr = hp.tacotron_zoneout_rate, hp.tacotron_dropout_rate
+        T_dec = T_out // hp.outputs_per_step  # decoder steps (r frames each)
         masks = dict(
-            prenet=m.get("prenet") if "prenet" in m else S.prenet_masks(T_out, B, P, seed=sub()),
-            zoneout=m.get("zoneout") if "zoneout" in m else S.zoneout_masks(T_out, B, H, zr, seed=sub()),
+            prenet=m.get("prenet") if "prenet" in m else S.prenet_masks(T_dec, B, P, seed=sub()),
+            zoneout=m.get("zoneout") if "zoneout" in m else S.zoneout_masks(T_dec, B, H, zr, seed=sub()),
             postnet=m.get("postnet") if "postnet" in m else S.postnet_masks(
                 hp.postnet_num_layers, B, T_out, hp.postnet_channels, dr, seed=sub()),
             enc_conv=m.get("enc_conv") if "enc_conv" in m else S.enc_conv_masks(

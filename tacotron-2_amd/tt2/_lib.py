@@ -89,7 +89,8 @@ class TrainConfig(ctypes.Structure):
         ("reference_filters", ctypes.c_int * 6), ("max_T_ref", ctypes.c_int),
         ("mask_decoder", ctypes.c_int), ("pos_weight", ctypes.c_float),
         ("n_emt", ctypes.c_int), ("n_spk", ctypes.c_int), ("orthog_weight", ctypes.c_float),
-        ("use_gst", ctypes.c_int), ("adain", ctypes.c_int), ("smoothing", ctypes.c_int)]
+        ("use_gst", ctypes.c_int), ("adain", ctypes.c_int), ("smoothing", ctypes.c_int),
+        ("outputs_per_step", ctypes.c_int)]
 
 
 class DecoderState(ctypes.Structure):

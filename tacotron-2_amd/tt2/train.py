@@ -64,8 +64,13 @@ def train_config(hp, batch, max_T_in, max_T_out, emt_only=False, precision="fp32
     lib.tt2_train_default_config(ctypes.byref(cfg), batch, max_T_in, max_T_out)
     if len(hp.prenet_layers) != 2 or hp.prenet_layers[0] != hp.prenet_layers[1]:
         raise NotImplementedError("prenet_layers must be two equal widths on this build")
-    if hp.decoder_layers != 2 or hp.outputs_per_step != 1:
-        raise NotImplementedError("decoder_layers = 2 and outputs_per_step = 1 on this build")
+    if hp.decoder_layers != 2:
+        raise NotImplementedError("decoder_layers = 2 on this build")
+    if hp.outputs_per_step < 1:
+        raise ValueError("outputs_per_step must be >= 1")
+    # r frames per decoder step (tacotron.py:322-324; helpers.py:78,129): T_out counts frames, the
+    # prenet / zoneout masks and the teacher-forcing draw count decoder steps T_out / r
+    cfg.outputs_per_step = int(hp.outputs_per_step)
     if hp.tacotron_teacher_forcing_mode not in ("constant", "scheduled"):
         raise ValueError("tacotron_teacher_forcing_mode must be 'constant' or 'scheduled'")
     if hp.predict_linear:
@@ -187,6 +192,7 @@ class TacotronTrainer(object):
         self.frontend = frontend
         self.postnet = postnet
         self.B = batch
+        self.r = int(hp.outputs_per_step)
         h = ctypes.c_void_p()
         check(self.lib.tt2_train_create(ctypes.byref(self.cfg), device, ctypes.byref(h)))
         self.h = h
@@ -247,7 +253,7 @@ class TacotronTrainer(object):
         """Per-step inputs of the reference's training graph beyond the tensors; an argument left
         out keeps its current setting.  targets_lengths [B] (mask_decoder's loss masks,
         tacotron.py:56,758-767; required when hp.mask_decoder; None clears them).  feed_target
-        [T_out] u8 injects the teacher-forcing draw (draw_teacher_forcing) for this and later
+        [T_out / r] u8 (one per decoder step) injects the teacher-forcing draw (draw_teacher_forcing) for this and later
         steps; None = every step teacher-forced; auto_teacher_forcing() returns to drawing from
         the ratio schedule, which is the default."""
         if targets_lengths is not _UNSET:
@@ -295,11 +301,21 @@ class TacotronTrainer(object):
         if self._feed_explicit:
             return
         self.ratio = teacher_forcing_ratio(self.global_step, self.hp)
-        self._set_feed(None if self.ratio >= 1.0 else draw_teacher_forcing(T_out, self.ratio, self._tf_rng))
+        self._set_feed(None if self.ratio >= 1.0 else
+                       draw_teacher_forcing(T_out // self.r, self.ratio, self._tf_rng))
+
+    def _steps(self, T_out):
+        """Decoder steps of a T_out-frame batch (the feeder pads targets to a multiple of r,
+        feeder.py:283-310)."""
+        if T_out % self.r:
+            raise ValueError("T_out = {} is not a multiple of outputs_per_step = {}".format(T_out, self.r))
+        return T_out // self.r
 
     def forward_backward(self, memory, lengths, targets, stop_targets, prenet_masks,
                          zoneout_masks=None, postnet_masks=None):
         """Teacher-forced forward + losses + backward; gradients land in the flat buffer.
+        targets [B, T_out, 80] / stop_targets [B, T_out] in frames; prenet_masks [T_dec, 2, B, P]
+        and zoneout_masks [T_dec, 4, B, H] per decoder step (T_dec = T_out / outputs_per_step).
         postnet_masks: Postnet dropout keep bits [layers, B, T_out, channels] (None = no
         dropout).  Target lengths / teacher-forcing draw: set_step_inputs."""
         t = self.torch
@@ -313,13 +329,14 @@ class TacotronTrainer(object):
             pnm = self._dev(postnet_masks, t.uint8) if self.postnet else None
             B, T_in, _ = mem.shape
             T_out = tg.shape[1]
+            T_dec = self._steps(T_out)
             if B != self.B:
                 raise ValueError("batch {} != trainer batch {}".format(B, self.B))
-            if tuple(pm.shape) != (T_out, 2, B, self.cfg.prenet_units):
-                raise ValueError("prenet_masks must be [T_out, 2, B, prenet_units]")
+            if tuple(pm.shape) != (T_dec, 2, B, self.cfg.prenet_units):
+                raise ValueError("prenet_masks must be [T_out / r, 2, B, prenet_units]")
             self._teacher_forcing(T_out)
-            if zm is not None and tuple(zm.shape) != (T_out, 4, B, self.cfg.decoder_lstm_units):
-                raise ValueError("zoneout_masks must be [T_out, 4, B, decoder_lstm_units]")
+            if zm is not None and tuple(zm.shape) != (T_dec, 4, B, self.cfg.decoder_lstm_units):
+                raise ValueError("zoneout_masks must be [T_out / r, 4, B, decoder_lstm_units]")
             if pnm is not None and tuple(pnm.shape) != (self.cfg.postnet_layers, B, T_out,
                                                         self.cfg.postnet_channels):
                 raise ValueError("postnet_masks must be [layers, B, T_out, channels]")
@@ -353,13 +370,16 @@ class TacotronTrainer(object):
             ezm = self._dev(enc_zoneout_masks, t.uint8)
             B, T_in = ids_d.shape
             T_out = tg.shape[1]
+            T_dec = self._steps(T_out)
             T_ref = re.shape[1]
             if B != self.B:
                 raise ValueError("batch {} != trainer batch {}".format(B, self.B))
             if rs is not None and tuple(rs.shape) != tuple(re.shape):
                 raise ValueError("ref_emt and ref_spk must have the same shape")
-            if tuple(pm.shape) != (T_out, 2, B, self.cfg.prenet_units):
-                raise ValueError("prenet_masks must be [T_out, 2, B, prenet_units]")
+            if tuple(pm.shape) != (T_dec, 2, B, self.cfg.prenet_units):
+                raise ValueError("prenet_masks must be [T_out / r, 2, B, prenet_units]")
+            if zm is not None and tuple(zm.shape) != (T_dec, 4, B, self.cfg.decoder_lstm_units):
+                raise ValueError("zoneout_masks must be [T_out / r, 4, B, decoder_lstm_units]")
             self._teacher_forcing(T_out)
             if em is not None and tuple(em.shape) != (self.cfg.enc_conv_layers, B, T_in,
                                                       self.cfg.enc_conv_channels):
@@ -503,9 +523,11 @@ class TacotronTrainer(object):
         return np.clip(x, self.cfg.clip_lo, self.cfg.clip_hi) if self.cfg.clip_outputs else x
 
     def outputs(self, T_in, T_out):
+        """The last forward's frames [B, T_out, 80], stop logits [B, T_out] and (T_in given)
+        alignments [B, T_in, T_out / r] (one per decoder step)."""
         fr = np.zeros((self.B, T_out, self.cfg.num_mels), np.float32)
         st = np.zeros((self.B, T_out), np.float32)
-        al = None if T_in is None else np.zeros((self.B, T_in, T_out), np.float32)
+        al = None if T_in is None else np.zeros((self.B, T_in, self._steps(T_out)), np.float32)
         check(self.lib.tt2_train_outputs(self.h, fr.ctypes.data_as(ctypes.c_void_p),
                                          st.ctypes.data_as(ctypes.c_void_p),
                                          None if al is None else al.ctypes.data_as(ctypes.c_void_p)))
