@@ -72,6 +72,7 @@ struct tt2_train_ctx {
   DevBuf TH, E, DF, PQ, FALL, ALN;
   // the large plain products (tr_gemm_big)
   DevBuf blasA, blasB, blasP;  // gemm_bf16_kc: bf16 operand copies, split-K partials
+  bool fe_direct = true;  // TT2_FE_CONV_DIRECT=0 at create: the refnet conv2d backward as im2col + GEMM + col2im
   bool blas_on = true;  // TT2_TRAIN_BLAS=0 at create: the large products on gemm_x3_kernel too
   long blas_calls = 0;
   // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
@@ -3019,6 +3020,10 @@ static void tr_persist_forward(tt2_train_ctx* c, const TrAtt& at, const uint8_t*
   // TT2_TP_STAMP=<step>: stage stamps of that step -> TT2_TP_STAMP_FILE (int64 [256][32], diagnostic)
   const char* st = std::getenv("TT2_TP_STAMP");
   a.stamp_step = st ? std::atoi(st) : -1;
+  {  // TT2_TP_OC: placement of the forward's off-chain products (A/B; k_tr_persist)
+    const char* e = std::getenv("TT2_TP_OC");
+    a.oc_mode = e ? std::atoi(e) : 1;  // mode 1 measured 69.9 against 70.45 ms/step (mode 0)
+  }
   a.stamps = nullptr;
   if (st) {
     grow(c->tpStamps, sizeof(long long) * TP_NB * 32);
@@ -4226,6 +4231,7 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
   const bool style_on = tr_style_on(c);
   if (style_on) tr_style_losses(c, s);
   // conv2d stack r backward from d map `din` (conv -> BN -> ReLU per layer; AdaIN: conv -> ReLU)
+  const bool fe_direct = c->fe_direct;
   auto conv_bwd = [&](int r, const float* din) {
     const std::string rs = fe_ref_scope(c, r);
     float* dY = c->fDY.as<float>();
@@ -4257,14 +4263,26 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
       tr_colsum(c, dz, Mi, fo, fo, gvar(c, sc + ly + "bias"), s);
       const int pt = std::max((Ho - 1) * st + 3 - H, 0) / 2, pl = std::max((Wo - 1) * st + 3 - W, 0) / 2;
       const float* xin = i == 0 ? refs[r] : c->fRY[r][i - 1].as<float>();
-      // (gemm_bf16_kc with the im2colᵀ gathered into bf16 measured 458 us per layer here against
-      // 525 + ~60 for the fp32 columns + gemm_x3_kernel: its 256-wide N tile is 8x idle at fo = 32)
-      fe_im2col2d_t(xin, B, H, W, ci, Ho, Wo, pt, pl, FB, Mi, s, st);
-      tr_gemm(9 * ci, fo, (int)Mi, FB, Mi, dz, fo, gvar(c, sc + ly + "kernel"), fo, s);
+      // kernel gradient: direct (k_fe_conv2d_dw: patches staged in LDS, fp32 FMA, partial rows summed
+      // by tr_colsum) where its register / LDS budget takes the channel counts, else the im2colᵀ
+      // columns + GEMM (gemm_bf16_kc with the im2colᵀ gathered into bf16 measured 458 us per layer
+      // against 525 + ~60 for the fp32 columns + gemm_x3_kernel: its 256-wide N tile is 8x idle at fo = 32)
+      if (fe_direct && fe_conv2d_dw_ok(ci, fo)) {
+        const int rows = fe_conv2d_dw(xin, dz, B, H, W, ci, Ho, Wo, fo, pt, pl, st, FB, (long)(c->fFBUF.bytes / sizeof(float)),
+                                      s);
+        tr_colsum(c, FB, rows, 9 * ci * fo, 9L * ci * fo, gvar(c, sc + ly + "kernel"), s);
+      } else {
+        fe_im2col2d_t(xin, B, H, W, ci, Ho, Wo, pt, pl, FB, Mi, s, st);
+        tr_gemm(9 * ci, fo, (int)Mi, FB, Mi, dz, fo, gvar(c, sc + ly + "kernel"), fo, s);
+      }
       if (i > 0) {
-        tr_transpose(pvar(c, sc + ly + "kernel"), 9L * ci, fo, fo, WT, 9L * ci, s);  // [fo][9ci]
-        tr_gemm((int)Mi, 9 * ci, fo, dz, fo, WT, 9 * ci, FB, 9 * ci, s);
-        fe_col2im2d(FB, B, H, W, ci, Ho, Wo, pt, pl, dY, s, st);
+        if (fe_direct && fe_conv2d_dx_ok(ci, fo)) {  // input gradient as a gather over the taps (k_fe_conv2d_dx)
+          fe_conv2d_dx(dz, pvar(c, sc + ly + "kernel"), B, H, W, ci, Ho, Wo, fo, pt, pl, st, dY, s);
+        } else {
+          tr_transpose(pvar(c, sc + ly + "kernel"), 9L * ci, fo, fo, WT, 9L * ci, s);  // [fo][9ci]
+          tr_gemm((int)Mi, 9 * ci, fo, dz, fo, WT, 9 * ci, FB, 9 * ci, s);
+          fe_col2im2d(FB, B, H, W, ci, Ho, Wo, pt, pl, dY, s, st);
+        }
       }
     }
   };
@@ -4660,6 +4678,7 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
     auto* c = new tt2_train_ctx();
     if (const char* e = std::getenv("TT2_TRAIN_BLAS")) c->blas_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("TT2_TR_VALUES16")) c->values16_on = std::atoi(e) != 0;
+    if (const char* e = std::getenv("TT2_FE_CONV_DIRECT")) c->fe_direct = std::atoi(e) != 0;
     {
       const char* e = std::getenv("TT2_TR_PERSIST");
       c->tp_on = !(e && e[0] == '0') && tp_device_ok(hip_device);

@@ -45,6 +45,15 @@ void fe_im2col2d_t(const float* x, int N, int H, int W, int C, int Ho, int Wo, i
                    hipStream_t s, int st = 2);
 void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl, float* dx,
                  hipStream_t s, int st = 2);
+// the same conv2d's backward without a materialised im2col (fp32 FMA): the kernel gradient as
+// partial rows [rows][9·C·F] into part (returns rows; the caller sums them), the input gradient as a
+// gather over the taps.  *_ok: the channel counts these kernels take (LDS / register budgets)
+bool fe_conv2d_dw_ok(int C, int F);
+int fe_conv2d_dw(const float* x, const float* dz, int N, int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
+                 int st, float* part, long part_floats, hipStream_t s);
+bool fe_conv2d_dx_ok(int C, int F);
+void fe_conv2d_dx(const float* dz, const float* Wk, int N, int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
+                  int st, float* dx, hipStream_t s);
 // ReferenceEncoderAdaIn (modules.py:89-98): per (row, channel) moments of NHWC x over HW -> mv [N][C][2]
 // (mean, biased variance); the 0.9 / 0.1 restyle of the speaker map by the emotion map's moments and
 // its backward (S: [N][C][2] scratch; dxe: the emotion map's gradient through m_e, v_e)

@@ -259,6 +259,214 @@ void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo,
                      pl, dx, st);
 }
 
+// ---- direct conv2d backward (no materialised im2col) ------------------------------------------------
+// d kernel of a 3x3 conv2d (stride st, 'same' pads pt / pl) over NHWC x [N][H][W][C] and dz [M][F]
+// (M = N·Ho·Wo): dW[(tap·C + c)·F + f] = Σ_m x(patch of m)[tap][c] · dz[m][f], fp32 FMA.  Work-group
+// = a run of output positions staged PC at a time in LDS ([PC][9C] patches, [PC][F] dz rows);
+// thread tile = channel c × 4 columns f over the 9 taps (R tiles when C·F/4 > 256; G position
+// groups when it is < 256); one partial row [9CF] per (work-group, group), summed by the caller.
+template <int R>
+__global__ __launch_bounds__(256) void k_fe_conv2d_dw(const float* __restrict__ x, const float* __restrict__ dz, int N,
+                                                      int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
+                                                      int st, int ppb, int PC, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  const int K9 = 9 * C, T = C * F / 4, Tt = T < 256 ? T : 256, G = 256 / Tt;
+  const int tid = threadIdx.x, pg = tid / Tt, q0 = tid % Tt;
+  float* const xs = fsm;             // [PC][9C]
+  float* const ds = fsm + PC * K9;   // [PC][F]
+  const int M = N * Ho * Wo;
+  const int m0 = blockIdx.x * ppb, m1 = min(M, m0 + ppb);
+  float acc[R][9][4];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[r][k][j] = 0.f;
+  for (int p0 = m0; p0 < m1; p0 += PC) {
+    const int np = min(PC, m1 - p0);
+    for (int e = tid; e < np * C; e += 256) {  // one position decomposition per (p, c), the 9 taps inside
+      const int p = e / C, c = e - p * C;
+      const int m = p0 + p, wo = m % Wo, rr = m / Wo, ho = rr % Ho, n = rr / Ho;
+      const int hb = st * ho - pt, wb = st * wo - pl;
+      const float* xb = x + (long)n * H * W * C + c;
+      float* xd = xs + p * K9 + c;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int h = hb + ky;
+        const bool hv = h >= 0 && h < H;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int w = wb + kx;
+          xd[(ky * 3 + kx) * C] = (hv && w >= 0 && w < W) ? xb[((long)h * W + w) * C] : 0.f;
+        }
+      }
+    }
+    for (int e = tid; e < np * F / 4; e += 256)
+      reinterpret_cast<float4*>(ds)[e] = reinterpret_cast<const float4*>(dz + (long)p0 * F)[e];
+    __syncthreads();
+    for (int p = pg; p < np; p += G) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int q = q0 + 256 * r, c = q / (F / 4), ng = q % (F / 4);
+        const float4 d4 = reinterpret_cast<const float4*>(ds + p * F)[ng];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const float xv = xs[p * K9 + k * C + c];
+          acc[r][k][0] += xv * d4.x;
+          acc[r][k][1] += xv * d4.y;
+          acc[r][k][2] += xv * d4.z;
+          acc[r][k][3] += xv * d4.w;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* const out = part + ((long)blockIdx.x * G + pg) * K9 * F;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = q0 + 256 * r, c = q / (F / 4), ng = q % (F / 4);
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+      reinterpret_cast<float4*>(out + (k * C + c) * F)[ng] = make_float4(acc[r][k][0], acc[r][k][1], acc[r][k][2], acc[r][k][3]);
+  }
+}
+bool fe_conv2d_dw_ok(int C, int F) {
+  const int T = C * F / 4;
+  return F % 4 == 0 && T >= 1 && (T <= 256 ? 256 % T == 0 : (T % 256 == 0 && T / 256 <= 4)) &&
+         9 * C + F <= 24576 / 8;
+}
+int fe_conv2d_dw(const float* x, const float* dz, int N, int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
+                 int st, float* part, long part_floats, hipStream_t s) {
+  TT2_CHECK(fe_conv2d_dw_ok(C, F), TT2_ERR_SHAPE_MISMATCH, "conv2d_dw: unsupported channel counts");
+  const long M = (long)N * Ho * Wo;
+  TT2_CHECK(M < (1L << 31) && (long)N * H * W * C < (1L << 31), TT2_ERR_SHAPE_MISMATCH, "conv2d_dw: shape exceeds 32 bits");
+  const int K9 = 9 * C, T = C * F / 4, G = T < 256 ? 256 / T : 1, R = T > 256 ? T / 256 : 1;
+  // chunks of PC positions (<= 40 KB of LDS: several work-groups per CU), ~1024 work-groups
+  const int PC = std::max(8, std::min(128, 10240 / (K9 + F)) / 8 * 8);
+  const long rows_cap = part_floats / ((long)K9 * F * G);
+  long nblk = std::min<long>({1024L, (M + PC - 1) / PC, rows_cap});
+  TT2_CHECK(nblk >= 1, TT2_ERR_SHAPE_MISMATCH, "conv2d_dw: partial buffer too small");
+  const int ppb = (int)(((M + nblk - 1) / nblk + PC - 1) / PC * PC);
+  nblk = (M + ppb - 1) / ppb;
+  const size_t lds = sizeof(float) * (size_t)PC * (K9 + F);
+  static bool attr = false;
+  if (!attr) {
+    for (const void* k : {reinterpret_cast<const void*>(k_fe_conv2d_dw<1>), reinterpret_cast<const void*>(k_fe_conv2d_dw<2>),
+                          reinterpret_cast<const void*>(k_fe_conv2d_dw<4>)})
+      TT2_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    attr = true;
+  }
+  const dim3 grid((unsigned)nblk);
+  if (R == 1) hipLaunchKernelGGL(k_fe_conv2d_dw<1>, grid, dim3(256), lds, s, x, dz, N, H, W, C, Ho, Wo, F, pt, pl, st, ppb, PC, part);
+  else if (R == 2) hipLaunchKernelGGL(k_fe_conv2d_dw<2>, grid, dim3(256), lds, s, x, dz, N, H, W, C, Ho, Wo, F, pt, pl, st, ppb, PC, part);
+  else hipLaunchKernelGGL(k_fe_conv2d_dw<4>, grid, dim3(256), lds, s, x, dz, N, H, W, C, Ho, Wo, F, pt, pl, st, ppb, PC, part);
+  TT2_HIP(hipGetLastError());
+  return (int)(nblk * G);  // partial rows of [9CF]
+}
+
+// d input of the same conv2d as a gather: dx[n][h][w][c] = Σ_{taps reading (h, w)} Σ_f dz[n][ho][wo][f] ·
+// Wk[tap][c][f] (Wk the HWIO kernel [3][3][C][F], staged in LDS as [tap][f][C]).  Thread = 4 channels
+// × DXW positions w0 + st·k of one row h (equal w parity: one tap pattern), so each LDS weight float4
+// feeds 4·DXW FMAs; grid-stride over (n, h, w block, parity, channel group).
+constexpr int DXW = 4;
+__global__ __launch_bounds__(256) void k_fe_conv2d_dx(const float* __restrict__ dz, const float* __restrict__ Wk, int N,
+                                                      int H, int W, int C, int Ho, int Wo, int F, int pt, int pl, int st,
+                                                      float* __restrict__ dx) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  for (int e = threadIdx.x; e < 9 * C * F; e += 256) {  // Wk[(tap·C + c)·F + f] -> [(tap·F + f)·C + c]
+    const int f = e % F, tc = e / F, c = tc % C, tap = tc / C;
+    fsm[(tap * F + f) * C + c] = Wk[e];
+  }
+  __syncthreads();
+  const int CG = C / 4, WB = (W + st * DXW - 1) / (st * DXW);
+  const long total = (long)N * H * WB * st * CG;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int cg = (int)(i % CG);
+    long r = i / CG;
+    const int par = (int)(r % st);
+    r /= st;
+    const int wb = (int)(r % WB);
+    r /= WB;
+    const int h = (int)(r % H), n = (int)(r / H);
+    const int w0 = wb * st * DXW + par;
+    float acc[DXW][4] = {};
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int hh = h + pt - ky;
+      if (hh < 0 || hh % st) continue;
+      const int ho = hh / st;
+      if (ho >= Ho) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ww0 = w0 + pl - kx;  // + st·k for position k
+        if (((ww0 % st) + st) % st) continue;
+        const int tap = ky * 3 + kx;
+        const float* wt = fsm + tap * F * C + 4 * cg;
+        const float* dzr[DXW];
+        bool ok[DXW];
+#pragma unroll
+        for (int k = 0; k < DXW; ++k) {
+          const int ww = ww0 + st * k, wo = ww >= 0 ? ww / st : -1;
+          ok[k] = w0 + st * k < W && ww >= 0 && wo < Wo;
+          dzr[k] = dz + ((long)(n * Ho + ho) * Wo + (ok[k] ? wo : 0)) * F;
+        }
+        for (int f = 0; f < F; f += 4) {
+          float4 dv[DXW];
+#pragma unroll
+          for (int k = 0; k < DXW; ++k)
+            dv[k] = ok[k] ? *reinterpret_cast<const float4*>(dzr[k] + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float4 w4 = *reinterpret_cast<const float4*>(wt + (f + j) * C);
+#pragma unroll
+            for (int k = 0; k < DXW; ++k) {
+              const float d = j == 0 ? dv[k].x : j == 1 ? dv[k].y : j == 2 ? dv[k].z : dv[k].w;
+              acc[k][0] += d * w4.x;
+              acc[k][1] += d * w4.y;
+              acc[k][2] += d * w4.z;
+              acc[k][3] += d * w4.w;
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DXW; ++k) {
+      const int w = w0 + st * k;
+      if (w < W)
+        *reinterpret_cast<float4*>(dx + ((long)(n * H + h) * W + w) * C + 4 * cg) =
+            make_float4(acc[k][0], acc[k][1], acc[k][2], acc[k][3]);
+    }
+  }
+}
+bool fe_conv2d_dx_ok(int C, int F) {
+  // measured 420-466 us against 186 + 235 for the GEMM + col2im form at refnet layer 1 (every lane of a
+  // channel group re-loads the same dz quads): opt-in (TT2_FE_CONV_DX=1) until it stages dz in LDS
+  static const bool on = [] {
+    const char* e = std::getenv("TT2_FE_CONV_DX");
+    return e && e[0] == '1';
+  }();
+  return on && C % 4 == 0 && F % 4 == 0 && 9 * C * F <= 24576;
+}
+void fe_conv2d_dx(const float* dz, const float* Wk, int N, int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
+                  int st, float* dx, hipStream_t s) {
+  TT2_CHECK(fe_conv2d_dx_ok(C, F) && (st == 1 || st == 2), TT2_ERR_SHAPE_MISMATCH, "conv2d_dx: unsupported shape");
+  TT2_CHECK((long)N * Ho * Wo * F < (1L << 31) && (long)N * H * W * C < (1L << 31), TT2_ERR_SHAPE_MISMATCH,
+            "conv2d_dx: shape exceeds 32 bits");
+  static bool attr = false;
+  if (!attr) {
+    TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_fe_conv2d_dx), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                96 * 1024));
+    attr = true;
+  }
+  const long total = (long)N * H * ((W + st * DXW - 1) / (st * DXW)) * st * (C / 4);
+  const unsigned nb = (unsigned)std::min<long>((total + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_fe_conv2d_dx, dim3(nb), dim3(256), sizeof(float) * 9 * C * F, s, dz, Wk, N, H, W, C, Ho, Wo, F,
+                     pt, pl, st, dx);
+  TT2_HIP(hipGetLastError());
+}
+
 // ---- ReferenceEncoderAdaIn (modules.py:89-98) ------------------------------------------------------
 // per (row, channel) moments over the HW positions of NHWC x [N][HW][C] (tf.nn.moments axes [1, 2]:
 // biased variance): mv[(n*C + c)*2 + {0: mean, 1: var}].  Work-group (n, 64-channel block): 4 row

@@ -53,6 +53,7 @@ struct TpArgs {
   float* BPK;
   long long* stamps;         // [TP_NB][32] s_memrealtime stage stamps of step stamp_step (diagnostic) or null
   int stamp_step;
+  int oc_mode;               // placement of the off-chain products (TT2_TP_OC, A/B): see k_tr_persist
   unsigned* flags;           // [3 phases][TP_NREP][TP_NB] step tags (zeroed before the launch)
   int* ctl;                  // [0] = 1 + phase of a timed-out wait, [1] = steps completed
 };

@@ -283,27 +283,38 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
   auto prenet_part = [&](int tn) {  // prenet_tn·W1p, k-steps [TP_PKW w, TP_PKW (w + 1)) of the prenet rows
     tp_mfma_rows<TP_PKW, false>(ao1, a.preh + (long)tn * 64 * P, P, TP_PKW * w, w1p, lane);
   };
-  auto hz1_part = [&](int t0) {  // hz1_t0·W1h, this wave's k-range (the producers its L2 wait covered)
-    tp_mfma_seg(ao1, a.Z1X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w, w1h, lane);
+  // hz·W over k-steps [c0, c1) of this wave's segment (4 at a time: register budget)
+  auto hz_seg = [&](tp_f4(&acc)[4], const __bf16* X, const tp_bf8(&wf)[TP_KSW], int c0, int c1) {
+#pragma unroll
+    for (int c = 0; c < TP_KSW; c += 4) {
+      if (c < c0 || c >= c1) continue;
+      const tp_bf8 part[4] = {wf[c], wf[c + 1], wf[c + 2], wf[c + 3]};
+      tp_mfma_rows<4, true>(acc, X, H, TP_KSW * w + c, part, lane);
+    }
   };
-  auto hz2_part = [&](int t0) {  // hz2_t0·W2h, this wave's k-range (the producers its H2 wait covered)
-    tp_mfma_seg(ao2, a.Z2X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w, w2h, lane);
+  auto hz1_part = [&](int t0, int c0 = 0, int c1 = TP_KSW) {  // hz1_t0·W1h (the producers its L2 wait covered)
+    hz_seg(ao1, a.Z1X + (long)(t0 & 1) * 64 * H, w1h, c0, c1);
+  };
+  auto hz2_part = [&](int t0, int c0 = 0, int c1 = TP_KSW) {  // hz2_t0·W2h (the producers its H2 wait covered)
+    hz_seg(ao2, a.Z2X + (long)(t0 & 1) * 64 * H, w2h, c0, c1);
   };
 #else
   auto prenet_part = [&](int tn) {  // prenet_tn·W1p, k-steps [TP_PKW w, TP_PKW (w + 1)) of the prenet rows
     tp_mfma_stream<TP_PKW, false>(ao1, a.preh + (long)tn * 64 * P, P, TP_PKW * w, a.K1T, wvo1, 32 * TP_PKW * w, lane);
   };
-  auto hz1_part = [&](int t0) {  // hz1_t0·W1h, this wave's k-range (the producers its L2 wait covered)
+  auto hz1_part = [&](int t0, int c0 = 0, int c1 = TP_KSW) {  // hz1_t0·W1h (the producers its L2 wait covered)
 #pragma unroll
     for (int c = 0; c < TP_KSW; c += 4)
-      tp_mfma_stream<4, true>(ao1, a.Z1X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w + c, a.K1T, wvo1, P + D + wk0 + 32 * c,
-                              lane);
+      if (c >= c0 && c < c1)
+        tp_mfma_stream<4, true>(ao1, a.Z1X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w + c, a.K1T, wvo1, P + D + wk0 + 32 * c,
+                                lane);
   };
-  auto hz2_part = [&](int t0) {  // hz2_t0·W2h, this wave's k-range (the producers its H2 wait covered)
+  auto hz2_part = [&](int t0, int c0 = 0, int c1 = TP_KSW) {  // hz2_t0·W2h (the producers its H2 wait covered)
 #pragma unroll
     for (int c = 0; c < TP_KSW; c += 4)
-      tp_mfma_stream<4, true>(ao2, a.Z2X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w + c, a.K2T, wvo2, H + wk0 + 32 * c,
-                              lane);
+      if (c >= c0 && c < c1)
+        tp_mfma_stream<4, true>(ao2, a.Z2X + (long)(t0 & 1) * 64 * H, H, TP_KSW * w + c, a.K2T, wvo2, H + wk0 + 32 * c,
+                                lane);
   };
 #endif
   prenet_part(0);  // hz1_{-1} = hz2_{-1} = 0
@@ -456,8 +467,21 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
       }
     }
     const bool more = t + 1 < T;
-    // off-chain LSTM-1 term hz1_t·W1h of step t+1 while the other work-groups' h2 travel
-    if (more) hz1_part(t);
+    // Off-chain products of step t+1 in the chain's three hand-off windows (H2, E, CTX): every one of
+    // them re-reads a 128 KB exchange buffer in each of the 256 work-groups (32 MB of MALL traffic per
+    // product and step), so where they sit moves the chain's own loads.  oc_mode 0:
+    // hz1_t·W1h in the H2 window, hz2_t·W2h in the E window, prenet_{t+1}·W1p in the CTX window;
+    // 1: hz1 split over the H2 and E windows, hz2 + prenet in the CTX window; 2: as 1 with the
+    // prenet term in the H2 window; 3: as 1 with hz2's first half in the E window
+    const int ocm = a.oc_mode;
+    if (more) {
+      if (ocm == 0) {
+        hz1_part(t);
+      } else {
+        hz1_part(t, 0, TP_KSW / 2);
+        if (ocm == 2) prenet_part(t + 1);
+      }
+    }
     TP_STAMP(9);
     // ================= H2 of every producer (wave w polls its 8 TP_KSW producers), then the attention row
     if (!tp_poll(a, TP_PH_H2, 8 * TP_KSW * w, 8 * TP_KSW, tag)) sfail[0] = 1;
@@ -547,8 +571,15 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
       }
     }
     TP_STAMP(12);
-    // off-chain LSTM-2 term hz2_t·W2h of step t+1 while the other quarters' energy partials travel
-    if (more) hz2_part(t);
+    // off-chain terms while the other quarters' energy partials travel
+    if (more) {
+      if (ocm == 0) {
+        hz2_part(t);
+      } else {
+        hz1_part(t, TP_KSW / 2, TP_KSW);
+        if (ocm == 3) hz2_part(t, 0, TP_KSW / 2);
+      }
+    }
     __syncthreads();  // the own partials in ep[]
     TP_STAMP(13);
     if (arow) {
@@ -634,8 +665,11 @@ __global__ __launch_bounds__(TP_NT, 1) void k_tr_persist(TpArgs a) {
         tp_bst(a.X1 + (i + B) * LX1, (P + 256 * sib + tid) * 4, 0, ctx);
       }
     }
-    // off-chain LSTM-1 term prenet_{t+1}·W1p while the contexts travel
-    if (more) prenet_part(t + 1);
+    // off-chain terms while the contexts travel
+    if (more) {
+      if (ocm != 0) hz2_part(t, ocm == 3 ? TP_KSW / 2 : 0, TP_KSW);
+      if (ocm != 2) prenet_part(t + 1);
+    }
     TP_STAMP(18);
   }
 #undef TP_STAMP

@@ -1289,3 +1289,51 @@ def test_gpu_train_persistent_backward_close_to_oracle():
         frob = float(np.linalg.norm(got - want) / max(np.linalg.norm(want), 1e-30))
         print("  {:90s} frob {:.3e}".format(n, frob))
         assert frob < (0.1 if "prenet" in n else 1e-2), (n, frob)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 1e-2)])
+def test_gpu_refnet_conv_backward_direct_matches_im2col(precision, tol):
+    """The refnet conv2d backward without a materialised im2col (k_fe_conv2d_dw: LDS-staged patches,
+    fp32 FMA, partial rows summed; k_fe_conv2d_dx: the input gradient as a gather over the taps)
+    against the im2colᵀ + GEMM + col2im form (TT2_FE_CONV_DIRECT=0) at the fork widths (filters
+    32, 32, 64, 64, 128, 128: the direct kernels take layers 0-3 / 1-2, the rest stay on the GEMM
+    form) with T_ref = 96 (odd pads on the way down): every gradient of the step, relative to its
+    max.  fp32: both forms are fp32-grade, so they agree to 2e-5; bf16: the GEMM form rounds its
+    operands to bf16 (1e-2; the direct kernels stay fp32 in both modes)."""
+    import os
+    from tt2.hparams import hparams
+    from tt2.train import TacotronTrainer
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, B=4, T_in=12, T_out=6, T_ref=96)
+    names = TRN.frontend_var_names() + TRN.train_var_names() + TRN.postnet_var_names()
+    out = []
+    for direct in ("1", "0"):
+        old = os.environ.get("TT2_FE_CONV_DIRECT")
+        os.environ["TT2_FE_CONV_DIRECT"] = direct
+        try:
+            tr = TacotronTrainer(hp, W, 4, 12, 6, 0, frontend=True, max_T_ref=96, precision=precision)
+        finally:
+            if old is None:
+                os.environ.pop("TT2_FE_CONV_DIRECT", None)
+            else:
+                os.environ["TT2_FE_CONV_DIRECT"] = old
+        try:
+            tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+            L = tr.losses()
+            out.append((L, {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}))
+        finally:
+            tr.close()
+    (La, ga), (Lb, gb) = out
+    assert abs(La["loss"] - Lb["loss"]) < 1e-6 * abs(Lb["loss"])
+    # (a conv bias ahead of batch norm has a zero gradient: rounding noise of ~1e-9 both ways)
+    live = [n for n in names if np.abs(gb[n]).max() > 1e-6]
+    worst = max(live, key=lambda n: _rel(ga[n], gb[n]))
+    for n in names:
+        if "refnet" in n and "conv2d/kernel" in n:
+            assert n in live, n
+        if n in live:
+            assert _rel(ga[n], gb[n]) < tol, (n, _rel(ga[n], gb[n]), worst)
+        else:
+            assert np.abs(ga[n]).max() < 1e-6, n
