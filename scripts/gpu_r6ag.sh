@@ -18,7 +18,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 tail -1 $O/tests.log
 B="--steps 1 --warmup 1 --no-wavenet --no-e2e --no-griffin-lim --no-cpu-baseline --no-variants --train-steps 3"
 for rep in 1 2; do
-  for d in 0 1; do
+  for d in 0 1; do :
     TT2_FE_CONV_DIRECT=$d timeout -k 10 300 python -u bench.py $B > $O/ab.json 2> $O/ab.err || { echo "train bench failed"; tail -5 $O/ab.err; exit 1; }
     python -c "import json;d=json.loads(open('$O/ab.json').read().strip().splitlines()[-1]);t=d['train'];print('direct=$d', t.get('ms_per_step'), t.get('forward_backward_ms'), t.get('grad_norm'))"
   done

@@ -4276,7 +4276,7 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
         tr_gemm(9 * ci, fo, (int)Mi, FB, Mi, dz, fo, gvar(c, sc + ly + "kernel"), fo, s);
       }
       if (i > 0) {
-        if (fe_direct && fe_conv2d_dx_ok(ci, fo)) {  // input gradient as a gather over the taps (k_fe_conv2d_dx)
+        if (fe_direct && fe_conv2d_dx_ok(ci, W, Ho, Wo, fo, st)) {  // input gradient as a gather over the taps (k_fe_conv2d_dx)
           fe_conv2d_dx(dz, pvar(c, sc + ly + "kernel"), B, H, W, ci, Ho, Wo, fo, pt, pl, st, dY, s);
         } else {
           tr_transpose(pvar(c, sc + ly + "kernel"), 9L * ci, fo, fo, WT, 9L * ci, s);  // [fo][9ci]

@@ -51,7 +51,7 @@ void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo,
 bool fe_conv2d_dw_ok(int C, int F);
 int fe_conv2d_dw(const float* x, const float* dz, int N, int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
                  int st, float* part, long part_floats, hipStream_t s);
-bool fe_conv2d_dx_ok(int C, int F);
+bool fe_conv2d_dx_ok(int C, int W, int Ho, int Wo, int F, int st);
 void fe_conv2d_dx(const float* dz, const float* Wk, int N, int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
                   int st, float* dx, hipStream_t s);
 // ReferenceEncoderAdaIn (modules.py:89-98): per (row, channel) moments of NHWC x over HW -> mv [N][C][2]

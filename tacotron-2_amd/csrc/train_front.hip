@@ -366,30 +366,46 @@ int fe_conv2d_dw(const float* x, const float* dz, int N, int H, int W, int C, in
 }
 
 // d input of the same conv2d as a gather: dx[n][h][w][c] = Σ_{taps reading (h, w)} Σ_f dz[n][ho][wo][f] ·
-// Wk[tap][c][f] (Wk the HWIO kernel [3][3][C][F], staged in LDS as [tap][f][C]).  Thread = 4 channels
-// × DXW positions w0 + st·k of one row h (equal w parity: one tap pattern), so each LDS weight float4
-// feeds 4·DXW FMAs; grid-stride over (n, h, w block, parity, channel group).
-constexpr int DXW = 4;
+// Wk[tap][c][f] (Wk the HWIO kernel [3][3][C][F]).  Work-group = DXR consecutive rows h of one image:
+// the kernel (as [tap][f][C]) and the dz rows those rows read are staged in LDS once; thread item =
+// 4 channels × DXW positions w0 + st·k of one row (equal w parity: one tap pattern), so each weight
+// float4 feeds 4·DXW FMAs and the dz quads are LDS broadcasts across the channel groups.
+constexpr int DXW = 4, DXR = 16;
+template <int st>
 __global__ __launch_bounds__(256) void k_fe_conv2d_dx(const float* __restrict__ dz, const float* __restrict__ Wk, int N,
-                                                      int H, int W, int C, int Ho, int Wo, int F, int pt, int pl, int st,
+                                                      int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
                                                       float* __restrict__ dx) {
   extern __shared__ __attribute__((aligned(16))) float fsm[];
+  const int bpi = (H + DXR - 1) / DXR, n = blockIdx.x / bpi, h0 = (blockIdx.x % bpi) * DXR, h1 = min(H, h0 + DXR);
+  // dz rows [r0, r1) feed rows [h0, h1): ho = (h + pt - ky) / st
+  const int r0 = max(0, (h0 + pt - 2 + st - 1) / st), r1 = min(Ho, (h1 - 1 + pt) / st + 1);
+  const int Fp = F + 4;                 // padded dz position stride: lanes of consecutive positions
+                                        // hit different LDS banks
+  float* const wt = fsm;                // [9][F][C]
+  float* const ds = fsm + 9 * C * F;    // [r1 - r0][Wo][Fp], then one zero position (taps off the map)
   for (int e = threadIdx.x; e < 9 * C * F; e += 256) {  // Wk[(tap·C + c)·F + f] -> [(tap·F + f)·C + c]
     const int f = e % F, tc = e / F, c = tc % C, tap = tc / C;
-    fsm[(tap * F + f) * C + c] = Wk[e];
+    wt[(tap * F + f) * C + c] = Wk[e];
   }
+  const int F4 = F / 4, nd = max(0, r1 - r0) * Wo * F4;
+  const float4* dsrc = reinterpret_cast<const float4*>(dz + ((long)n * Ho + r0) * Wo * F);
+  for (int e = threadIdx.x; e < nd; e += 256) {
+    const int pos = e / F4, f4 = e - pos * F4;
+    *reinterpret_cast<float4*>(ds + pos * Fp + 4 * f4) = dsrc[e];
+  }
+  float* const dzero = ds + max(0, r1 - r0) * Wo * Fp;
+  for (int e = threadIdx.x; e < F; e += 256) dzero[e] = 0.f;
   __syncthreads();
+  // wave item = (row h, w parity): its lanes are (channel group, w block), so the tap pattern is
+  // wave-uniform (no divergence on the stride-2 parity tests)
   const int CG = C / 4, WB = (W + st * DXW - 1) / (st * DXW);
-  const long total = (long)N * H * WB * st * CG;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int cg = (int)(i % CG);
-    long r = i / CG;
-    const int par = (int)(r % st);
-    r /= st;
-    const int wb = (int)(r % WB);
-    r /= WB;
-    const int h = (int)(r % H), n = (int)(r / H);
-    const int w0 = wb * st * DXW + par;
+  const int lane = threadIdx.x & 63, cg = lane % CG;
+  const bool act = lane / CG < WB;            // lanes past the row's w blocks compute block 0 and store nothing
+  const int wb = act ? lane / CG : 0;         // (no divergent region around the tap branches)
+  const int nwi = (h1 - h0) * st;
+  for (int wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); wi < nwi; wi += 4) {  // wave-uniform (SGPR)
+    const int par = wi % st, h = h0 + wi / st;
+    const int w0 = par + st * wb;  // position k: w0 + st·WB·k (consecutive lanes, consecutive positions)
     float acc[DXW][4] = {};
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
@@ -399,26 +415,22 @@ __global__ __launch_bounds__(256) void k_fe_conv2d_dx(const float* __restrict__ 
       if (ho >= Ho) continue;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        const int ww0 = w0 + pl - kx;  // + st·k for position k
-        if (((ww0 % st) + st) % st) continue;
-        const int tap = ky * 3 + kx;
-        const float* wt = fsm + tap * F * C + 4 * cg;
-        const float* dzr[DXW];
-        bool ok[DXW];
+        const int ww0 = w0 + pl - kx;  // + st·WB·k for position k
+        if ((((par + pl - kx) % st) + st) % st) continue;  // = ww0's parity, written wave-uniform
+        const float* wp = wt + (ky * 3 + kx) * F * C + 4 * cg;
+        const float* dr[DXW];  // positions off the map read the zero row: no branches in the f loop
 #pragma unroll
         for (int k = 0; k < DXW; ++k) {
-          const int ww = ww0 + st * k, wo = ww >= 0 ? ww / st : -1;
-          ok[k] = w0 + st * k < W && ww >= 0 && wo < Wo;
-          dzr[k] = dz + ((long)(n * Ho + ho) * Wo + (ok[k] ? wo : 0)) * F;
+          const int ww = ww0 + st * WB * k, wo = ww >= 0 ? ww / st : 0;
+          dr[k] = (ww >= 0 && wo < Wo) ? ds + ((ho - r0) * Wo + wo) * Fp : dzero;
         }
         for (int f = 0; f < F; f += 4) {
           float4 dv[DXW];
 #pragma unroll
-          for (int k = 0; k < DXW; ++k)
-            dv[k] = ok[k] ? *reinterpret_cast<const float4*>(dzr[k] + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int k = 0; k < DXW; ++k) dv[k] = *reinterpret_cast<const float4*>(dr[k] + f);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float4 w4 = *reinterpret_cast<const float4*>(wt + (f + j) * C);
+            const float4 w4 = *reinterpret_cast<const float4*>(wp + (f + j) * C);
 #pragma unroll
             for (int k = 0; k < DXW; ++k) {
               const float d = j == 0 ? dv[k].x : j == 1 ? dv[k].y : j == 2 ? dv[k].z : dv[k].w;
@@ -433,37 +445,38 @@ __global__ __launch_bounds__(256) void k_fe_conv2d_dx(const float* __restrict__ 
     }
 #pragma unroll
     for (int k = 0; k < DXW; ++k) {
-      const int w = w0 + st * k;
-      if (w < W)
+      const int w = w0 + st * WB * k;
+      if (act && w < W)
         *reinterpret_cast<float4*>(dx + ((long)(n * H + h) * W + w) * C + 4 * cg) =
             make_float4(acc[k][0], acc[k][1], acc[k][2], acc[k][3]);
     }
   }
 }
-bool fe_conv2d_dx_ok(int C, int F) {
-  // measured 420-466 us against 186 + 235 for the GEMM + col2im form at refnet layer 1 (every lane of a
-  // channel group re-loads the same dz quads): opt-in (TT2_FE_CONV_DX=1) until it stages dz in LDS
-  static const bool on = [] {
-    const char* e = std::getenv("TT2_FE_CONV_DX");
-    return e && e[0] == '1';
-  }();
-  return on && C % 4 == 0 && F % 4 == 0 && 9 * C * F <= 24576;
+static long fe_dx_lds_floats(int C, int Ho, int Wo, int F, int st) {
+  const int rows = std::min(Ho, (DXR + 2) / st + 2);
+  return 9L * C * F + (long)rows * Wo * (F + 4) + F;
+}
+// F <= 32: at refnet layer 2 (C 32, F 64: 102 KB of LDS, one work-group per CU) it measured 440 us against
+// the GEMM + col2im form's ~150; at layer 1 (C = F = 32) 266 against 421
+bool fe_conv2d_dx_ok(int C, int W, int Ho, int Wo, int F, int st) {  // LDS budget; one wave covers a row
+  return C % 4 == 0 && F % 4 == 0 && F <= 32 && (st == 1 || st == 2) && fe_dx_lds_floats(C, Ho, Wo, F, st) * 4 <= 120 * 1024 &&
+         (C / 4) * ((W + st * DXW - 1) / (st * DXW)) <= 64;
 }
 void fe_conv2d_dx(const float* dz, const float* Wk, int N, int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
                   int st, float* dx, hipStream_t s) {
-  TT2_CHECK(fe_conv2d_dx_ok(C, F) && (st == 1 || st == 2), TT2_ERR_SHAPE_MISMATCH, "conv2d_dx: unsupported shape");
+  TT2_CHECK(fe_conv2d_dx_ok(C, W, Ho, Wo, F, st), TT2_ERR_SHAPE_MISMATCH, "conv2d_dx: unsupported shape");
   TT2_CHECK((long)N * Ho * Wo * F < (1L << 31) && (long)N * H * W * C < (1L << 31), TT2_ERR_SHAPE_MISMATCH,
             "conv2d_dx: shape exceeds 32 bits");
+  const long lds = sizeof(float) * fe_dx_lds_floats(C, Ho, Wo, F, st);
   static bool attr = false;
   if (!attr) {
-    TT2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_fe_conv2d_dx), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                96 * 1024));
+    for (const void* k : {reinterpret_cast<const void*>(k_fe_conv2d_dx<1>), reinterpret_cast<const void*>(k_fe_conv2d_dx<2>)})
+      TT2_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024));
     attr = true;
   }
-  const long total = (long)N * H * ((W + st * DXW - 1) / (st * DXW)) * st * (C / 4);
-  const unsigned nb = (unsigned)std::min<long>((total + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_fe_conv2d_dx, dim3(nb), dim3(256), sizeof(float) * 9 * C * F, s, dz, Wk, N, H, W, C, Ho, Wo, F,
-                     pt, pl, st, dx);
+  const unsigned nb = (unsigned)((long)N * ((H + DXR - 1) / DXR));
+  if (st == 1) hipLaunchKernelGGL(k_fe_conv2d_dx<1>, dim3(nb), dim3(256), (size_t)lds, s, dz, Wk, N, H, W, C, Ho, Wo, F, pt, pl, dx);
+  else hipLaunchKernelGGL(k_fe_conv2d_dx<2>, dim3(nb), dim3(256), (size_t)lds, s, dz, Wk, N, H, W, C, Ho, Wo, F, pt, pl, dx);
   TT2_HIP(hipGetLastError());
 }
 
