@@ -2190,6 +2190,65 @@ __global__ void k_tr_prenet_bwd(const float* __restrict__ dp, long ld_dp, const 
   dz[i] = p[m * ld_p + n] > 0.f ? 2.f * dp[m * ld_dp + n] : 0.f;
 }
 
+// d values of the attention context (context_t = align_t · values, attention.py:155-160), all rows in
+// one launch: DVAL[b][j][d] = Σ_t ALIGN[b][j][t] · DCTX[t][b][d] (fp32 FMA).  Work-group = (128 columns d,
+// DV_JT rows j, row b); thread = 4 columns × DV_JT / 8 rows; t in LDS-staged chunks of DV_TC.
+constexpr int DV_JT = 160, DV_TC = 32;
+__global__ __launch_bounds__(256) void k_tr_dval(const float* __restrict__ align, const float* __restrict__ dctx, int B,
+                                                 int Tin, int T, int D, float* __restrict__ dval) {
+  __shared__ __attribute__((aligned(16))) float As[DV_TC][DV_JT + 1];  // +1: the t-strided staging stores spread over the banks
+  __shared__ __attribute__((aligned(16))) float Ds[DV_TC][128];
+  constexpr int JI = DV_JT / 8;
+  const int tid = threadIdx.x, dq = tid & 31, jg = tid >> 5;
+  const int d0 = blockIdx.x * 128, j0 = blockIdx.y * DV_JT, b = blockIdx.z;
+  const float* ab = align + (long)b * Tin * T;
+  f32x4 acc[JI];
+#pragma unroll
+  for (int i = 0; i < JI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t0 = 0; t0 < T; t0 += DV_TC) {
+    for (int e = tid; e < DV_JT * DV_TC; e += 256) {  // coalesced over t
+      const int j = e / DV_TC, tt = e - j * DV_TC;
+      As[tt][j] = (j0 + j < Tin && t0 + tt < T) ? ab[(long)(j0 + j) * T + t0 + tt] : 0.f;
+    }
+    for (int e = tid; e < DV_TC * 32; e += 256) {
+      const int tt = e >> 5, q = e & 31, d = d0 + 4 * q;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t0 + tt < T) {
+        const float* src = dctx + ((long)(t0 + tt) * B + b) * D + d;
+        if (d + 3 < D) {
+          v = *reinterpret_cast<const f32x4*>(src);
+        } else {
+          for (int u = 0; u < 4; ++u) v[u] = d + u < D ? src[u] : 0.f;
+        }
+      }
+      *reinterpret_cast<f32x4*>(&Ds[tt][4 * q]) = v;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int tt = 0; tt < DV_TC; ++tt) {
+      const f32x4 dv = *reinterpret_cast<const f32x4*>(&Ds[tt][4 * dq]);
+#pragma unroll
+      for (int i = 0; i < JI; ++i) {
+        const float a = As[tt][jg + 8 * i];
+        acc[i] += a * dv;
+      }
+    }
+    __syncthreads();
+  }
+  const int d = d0 + 4 * dq;
+#pragma unroll
+  for (int i = 0; i < JI; ++i) {
+    const int j = j0 + jg + 8 * i;
+    if (j >= Tin) continue;
+    float* o = dval + ((long)b * Tin + j) * D + d;
+    if (d + 3 < D) {
+      *reinterpret_cast<f32x4*>(o) = acc[i];
+    } else {
+      for (int u = 0; u < 4; ++u)
+        if (d + u < D) o[u] = acc[i][u];
+    }
+  }
+}
 __global__ void k_tr_mask_rows(const float* __restrict__ x, const int* __restrict__ lens, int B, int Tin, int D,
                                float* __restrict__ y) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2510,6 +2569,7 @@ static void tr_transpose(const float* src, long rows, long cols, long lds, float
 
 static void tr_colsum(tt2_train_ctx* c, const float* in, long M, int N, long ld, float* out, hipStream_t s) {
   const int S = tr_splits(M, N, 64 * std::max<long>(4L * c->H, c->LX1));
+  TT2_CHECK((size_t)S * N * sizeof(float) <= c->part.bytes, TT2_ERR_SHAPE_MISMATCH, "tr_colsum: partial buffer too small");
   hipLaunchKernelGGL(k_tr_colsum_part, dim3((N + tr_tw(N) - 1) / tr_tw(N), S), dim3(256), 0, s, in, M, N, ld,
                      c->part.as<float>());
   hipLaunchKernelGGL(k_tr_colsum_final, dim3((N + 31) / 32), dim3(TR_FIN), 0, s, c->part.as<float>(), S, N, out);
@@ -3645,9 +3705,10 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
     tr_colsum(c, c->dBC.as<float>(), BNT, F, F, gvar(c, LAV("location_features_convolution/bias")), s);
   }
   // memory: d values = Σ_t align_t^T · dctx_t (+ keys path), memory_layer kernel
-  for (int b = 0; b < B; ++b)
-    tr_gemm(Tin, D, T, c->ALIGN.as<float>() + (long)b * Tin * T, T, c->DCTX.as<float>() + (long)b * D, (long)B * D,
-            c->DVAL.as<float>() + (long)b * Tin * D, D, s);
+  // (one launch for all rows: the per-row GEMMs were 64 launches + split-K combines, 1.37 ms at configs[4])
+  hipLaunchKernelGGL(k_tr_dval, dim3((D + 127) / 128, (Tin + DV_JT - 1) / DV_JT, B), dim3(256), 0, s, c->ALIGN.as<float>(),
+                     c->DCTX.as<float>(), B, Tin, T, D, c->DVAL.as<float>());
+  TT2_HIP(hipGetLastError());
   tr_transpose(c->values.as<float>(), (long)B * Tin, D, D, TBUF, (long)B * Tin, s);
   tr_gemm(D, A, B * Tin, TBUF, (long)B * Tin, c->DKEYS.as<float>(), A, gvar(c, vn("memory_layer/kernel")), A, s);
   tr_gemm(B * Tin, D, A, c->DKEYS.as<float>(), A, c->WmT.as<float>(), D, c->DVAL.as<float>(), D, s, nullptr,
@@ -3854,6 +3915,8 @@ static void tr_front_alloc(tt2_train_ctx* c) {
     mmax = std::max(mmax, nmap);
   }
   a(c->fFBUF, fbuf); a(c->fDY, mmax); a(c->fDY2, mmax); a(c->fDZc, mmax);
+  // the direct conv2d kernel gradient sums its partial rows with tr_colsum over 9·ci·fo columns
+  if (c->part.bytes < sizeof(float) * (size_t)(wt_conv2d + 4096)) c->part.alloc(sizeof(float) * (size_t)(wt_conv2d + 4096));
   const int ntok = f.num_gst, tokd = f.style_embed_depth / f.num_heads, A = f.style_att_dim, dh = A / f.num_heads;
   a(c->fGq, B * A); a(c->fGkk, B * ntok * A); a(c->fGv, B * ntok * tokd); a(c->fGnv, B * dh); a(c->fGbb, B * dh);
   a(c->fGsum, ntok * A + ntok * tokd + 2 * dh);
