@@ -1,4 +1,4 @@
-# round 6: one-launch d values (k_tr_dval) -- training parity tests, kernel trace, bench
+# round 6: training parity tests (incl. the one-work-group refnet GRU), kernel trace, bench
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r6ah

@@ -73,6 +73,7 @@ struct tt2_train_ctx {
   // the large plain products (tr_gemm_big)
   DevBuf blasA, blasB, blasP;  // gemm_bf16_kc: bf16 operand copies, split-K partials
   bool fe_direct = true;  // TT2_FE_CONV_DIRECT=0 at create: the refnet conv2d backward as im2col + GEMM + col2im
+  bool fe_gru_seq = true;  // TT2_FE_GRU_SEQ=0 at create: the refnet GRU as per-step launches (4 per step)
   bool blas_on = true;  // TT2_TRAIN_BLAS=0 at create: the large products on gemm_x3_kernel too
   long blas_calls = 0;
   // bf16 copies of the recurrent weights in both layouts (precision = bf16), refreshed per step
@@ -2191,62 +2192,48 @@ __global__ void k_tr_prenet_bwd(const float* __restrict__ dp, long ld_dp, const 
 }
 
 // d values of the attention context (context_t = align_t · values, attention.py:155-160), all rows in
-// one launch: DVAL[b][j][d] = Σ_t ALIGN[b][j][t] · DCTX[t][b][d] (fp32 FMA).  Work-group = (128 columns d,
-// DV_JT rows j, row b); thread = 4 columns × DV_JT / 8 rows; t in LDS-staged chunks of DV_TC.
-constexpr int DV_JT = 160, DV_TC = 32;
-__global__ __launch_bounds__(256) void k_tr_dval(const float* __restrict__ align, const float* __restrict__ dctx, int B,
+// one launch: DVAL[b][j][d] = Σ_t ALIGN[b][j][t] · DCTX[t][b][d] on v_mfma_f32_16x16x4f32 (exact fp32
+// products).  Work-group = (128 columns d, 64 rows j, row b), 8 waves: wave w owns column tile w over
+// the 4 row tiles; t in LDS-staged chunks of 32 (8 k-steps).
+constexpr int DV_JT = 64, DV_TC = 32;
+__global__ __launch_bounds__(512) void k_tr_dval(const float* __restrict__ align, const float* __restrict__ dctx, int B,
                                                  int Tin, int T, int D, float* __restrict__ dval) {
-  __shared__ __attribute__((aligned(16))) float As[DV_TC][DV_JT + 1];  // +1: the t-strided staging stores spread over the banks
-  __shared__ __attribute__((aligned(16))) float Ds[DV_TC][128];
-  constexpr int JI = DV_JT / 8;
-  const int tid = threadIdx.x, dq = tid & 31, jg = tid >> 5;
+  __shared__ float As[DV_JT][DV_TC + 1];
+  __shared__ float Bs[DV_TC][128 + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g4 = lane >> 4;
   const int d0 = blockIdx.x * 128, j0 = blockIdx.y * DV_JT, b = blockIdx.z;
   const float* ab = align + (long)b * Tin * T;
-  f32x4 acc[JI];
+  f32x4 acc[4];
 #pragma unroll
-  for (int i = 0; i < JI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int t0 = 0; t0 < T; t0 += DV_TC) {
-    for (int e = tid; e < DV_JT * DV_TC; e += 256) {  // coalesced over t
+    for (int e = tid; e < DV_JT * DV_TC; e += 512) {  // coalesced over t
       const int j = e / DV_TC, tt = e - j * DV_TC;
-      As[tt][j] = (j0 + j < Tin && t0 + tt < T) ? ab[(long)(j0 + j) * T + t0 + tt] : 0.f;
+      As[j][tt] = (j0 + j < Tin && t0 + tt < T) ? ab[(long)(j0 + j) * T + t0 + tt] : 0.f;
     }
-    for (int e = tid; e < DV_TC * 32; e += 256) {
-      const int tt = e >> 5, q = e & 31, d = d0 + 4 * q;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t0 + tt < T) {
-        const float* src = dctx + ((long)(t0 + tt) * B + b) * D + d;
-        if (d + 3 < D) {
-          v = *reinterpret_cast<const f32x4*>(src);
-        } else {
-          for (int u = 0; u < 4; ++u) v[u] = d + u < D ? src[u] : 0.f;
-        }
-      }
-      *reinterpret_cast<f32x4*>(&Ds[tt][4 * q]) = v;
+    for (int e = tid; e < DV_TC * 128; e += 512) {  // coalesced over d
+      const int tt = e >> 7, dd = e & 127;
+      Bs[tt][dd] = (t0 + tt < T && d0 + dd < D) ? dctx[((long)(t0 + tt) * B + b) * D + d0 + dd] : 0.f;
     }
     __syncthreads();
-#pragma unroll 4
-    for (int tt = 0; tt < DV_TC; ++tt) {
-      const f32x4 dv = *reinterpret_cast<const f32x4*>(&Ds[tt][4 * dq]);
 #pragma unroll
-      for (int i = 0; i < JI; ++i) {
-        const float a = As[tt][jg + 8 * i];
-        acc[i] += a * dv;
-      }
+    for (int ks = 0; ks < DV_TC / 4; ++ks) {
+      const float bv = Bs[4 * ks + g4][16 * w + r16];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(As[16 * mt + r16][4 * ks + g4], bv, acc[mt], 0, 0, 0);
     }
     __syncthreads();
   }
-  const int d = d0 + 4 * dq;
+  const int d = d0 + 16 * w + r16;
+  if (d < D) {
 #pragma unroll
-  for (int i = 0; i < JI; ++i) {
-    const int j = j0 + jg + 8 * i;
-    if (j >= Tin) continue;
-    float* o = dval + ((long)b * Tin + j) * D + d;
-    if (d + 3 < D) {
-      *reinterpret_cast<f32x4*>(o) = acc[i];
-    } else {
-      for (int u = 0; u < 4; ++u)
-        if (d + u < D) o[u] = acc[i][u];
-    }
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = j0 + 16 * mt + 4 * g4 + i;
+        if (j < Tin) dval[((long)b * Tin + j) * D + d] = acc[mt][i];
+      }
   }
 }
 __global__ void k_tr_mask_rows(const float* __restrict__ x, const int* __restrict__ lens, int B, int Tin, int D,
@@ -3706,7 +3693,7 @@ static void tr_forward_backward(tt2_train_ctx* c, const float* mem, const int* l
   }
   // memory: d values = Σ_t align_t^T · dctx_t (+ keys path), memory_layer kernel
   // (one launch for all rows: the per-row GEMMs were 64 launches + split-K combines, 1.37 ms at configs[4])
-  hipLaunchKernelGGL(k_tr_dval, dim3((D + 127) / 128, (Tin + DV_JT - 1) / DV_JT, B), dim3(256), 0, s, c->ALIGN.as<float>(),
+  hipLaunchKernelGGL(k_tr_dval, dim3((D + 127) / 128, (Tin + DV_JT - 1) / DV_JT, B), dim3(512), 0, s, c->ALIGN.as<float>(),
                      c->DCTX.as<float>(), B, Tin, T, D, c->DVAL.as<float>());
   TT2_HIP(hipGetLastError());
   tr_transpose(c->values.as<float>(), (long)B * Tin, D, D, TBUF, (long)B * Tin, s);
@@ -4119,7 +4106,10 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
     tr_gemm(B * T2, 2 * RD, gin, x, gin, kg, 2 * RD, XG, 3 * RD, s, pvar(c, rs + "rnn/gru_cell/gates/bias"));
     tr_gemm(B * T2, RD, gin, x, gin, kcn, RD, XG + 2 * RD, 3 * RD, s, pvar(c, rs + "rnn/gru_cell/candidate/bias"));
     TT2_HIP(hipMemsetAsync(c->fHG[r].p, 0, sizeof(float) * (size_t)B * RD, s));
-    for (int t = 0; t < T2; ++t) {
+    if (c->fe_gru_seq && fe_gru_seq_ok(B, RD))  // the whole recurrence in one work-group (fp32 MFMA)
+      fe_gru_fwd_seq(XG, kg + (long)gin * 2 * RD, kcn + (long)gin * RD, B, T2, RD, c->fGR[r].as<float>(), c->fGU[r].as<float>(),
+                     c->fGRH[r].as<float>(), c->fGCC[r].as<float>(), c->fHG[r].as<float>(), s);
+    for (int t = 0; t < (c->fe_gru_seq && fe_gru_seq_ok(B, RD) ? 0 : T2); ++t) {
       float* h = c->fHG[r].as<float>() + (long)t * B * RD;
       tr_gemm(B, 2 * RD, RD, h, RD, kg + (long)gin * 2 * RD, 2 * RD, c->fGG.as<float>(), 2 * RD, s);
       fe_gru_a(XG, c->fGG.as<float>(), c->fHG[r].as<float>(), B, T2, RD, t, c->fGR[r].as<float>(),
@@ -4393,9 +4383,16 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
     const float* kcn = pvar(c, rs + "rnn/gru_cell/candidate/kernel");
     float* WghT = WT;                       // [2RD][RD]
     float* WchT = WT + 2L * RD * RD;        // [RD][RD]
-    tr_transpose(kg + (long)gin * 2 * RD, RD, 2 * RD, 2 * RD, WghT, RD, s);
-    tr_transpose(kcn + (long)gin * RD, RD, RD, RD, WchT, RD, s);
-    for (int t = T2 - 1; t >= 0; --t) {
+    const bool gseq = c->fe_gru_seq && fe_gru_seq_ok(B, RD);
+    if (gseq) {  // the whole reverse recurrence in one work-group (fp32 MFMA)
+      fe_gru_bwd_seq(kg + (long)gin * 2 * RD, kcn + (long)gin * RD, c->fGR[r].as<float>(), c->fGU[r].as<float>(),
+                     c->fGCC[r].as<float>(), c->fHG[r].as<float>(), B, T2, RD, c->fDH.as<float>(), c->fDCP.as<float>(),
+                     c->fDGP.as<float>(), s);
+    } else {
+      tr_transpose(kg + (long)gin * 2 * RD, RD, 2 * RD, 2 * RD, WghT, RD, s);
+      tr_transpose(kcn + (long)gin * RD, RD, RD, RD, WchT, RD, s);
+    }
+    for (int t = gseq ? -1 : T2 - 1; t >= 0; --t) {
       fe_gru_bwd_a(c->fDH.as<float>(), c->fGU[r].as<float>(), c->fGCC[r].as<float>(), c->fHG[r].as<float>(), B, RD, t,
                    c->fDCP.as<float>(), c->fDHA.as<float>(), s);
       tr_gemm(B, RD, RD, c->fDCP.as<float>() + (long)t * B * RD, RD, WchT, RD, c->fDRH.as<float>(), RD, s);
@@ -4742,6 +4739,7 @@ tt2_status tt2_train_create(const tt2_train_config* cfg, int hip_device, tt2_tra
     if (const char* e = std::getenv("TT2_TRAIN_BLAS")) c->blas_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("TT2_TR_VALUES16")) c->values16_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("TT2_FE_CONV_DIRECT")) c->fe_direct = std::atoi(e) != 0;
+    if (const char* e = std::getenv("TT2_FE_GRU_SEQ")) c->fe_gru_seq = std::atoi(e) != 0;
     {
       const char* e = std::getenv("TT2_TR_PERSIST");
       c->tp_on = !(e && e[0] == '0') && tp_device_ok(hip_device);

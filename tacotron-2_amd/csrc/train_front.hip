@@ -608,6 +608,253 @@ __global__ void k_fe_gru_b(const float* __restrict__ XG, const float* __restrict
   CC[o] = c;
   HG[o + (long)N * D] = u * HG[o] + (1.f - u) * c;
 }
+// ---- the whole GRU recurrence of one reference encoder in one work-group -----------------------------
+// (modules.py:59, TF1 GRUCell; the per-step form above is 4 launches + split-K combines per step).  1024
+// threads; the recurrent weights live in registers as v_mfma_f32_16x16x4f32 B fragments (exact fp32
+// products), the step's A operands (h, r·h forward; d candidate, d gates backward) in LDS with k
+// permuted so a lane's four consecutive k-steps are one 16-byte read.  Rows >= N are never consumed
+// (MFMA rows are independent).  Same outputs as the per-step kernels: R, U, RH, CC, HG[t+1] forward;
+// DCP, DGP and the running d h backward.
+template <int KS4>
+__device__ __forceinline__ void gru_mm(f32x4 (&acc)[4], const float* AL, int ld, int K4, int s0, const float (&bf)[KS4],
+                                       int lane) {
+  const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int c = 0; c < KS4; c += 4) {
+    f32x4 a[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) a[mt] = *reinterpret_cast<const f32x4*>(AL + (16 * mt + r) * ld + g * K4 + s0 + c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt][j], bf[c + j], acc[mt], 0, 0, 0);
+    asm volatile("" ::: "memory");  // keep the next group's LDS reads below: 16 operand registers live, not 128
+  }
+}
+// C fragment (rows 16 mt + 4 (lane >> 4) + i, column col0 + (lane & 15)) -> P[row][col] (row stride ldp)
+__device__ __forceinline__ void gru_put(const f32x4 (&acc)[4], float* P, int ldp, int col0, int lane) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) P[(16 * mt + 4 * (lane >> 4) + i) * ldp + col0 + (lane & 15)] = acc[mt][i];
+}
+// k -> its slot in a permuted A row of K columns (k = 4 s + g at g·K/4 + s)
+__device__ __forceinline__ int gru_perm(int k, int K) { return (k & 3) * (K >> 2) + (k >> 2); }
+
+constexpr int GRU_NT = 512, GRU_NW = GRU_NT / 64;  // 8 waves: 256 registers per lane for the weight fragments
+template <int RD>
+__global__ __launch_bounds__(GRU_NT) void k_fe_gru_fwd_seq(const float* __restrict__ XG, const float* __restrict__ Wgh,
+                                                          const float* __restrict__ Wch, int N, int T2,
+                                                          float* __restrict__ R, float* __restrict__ Uo,
+                                                          float* __restrict__ RHo, float* __restrict__ CC,
+                                                          float* __restrict__ HG) {
+  constexpr int KS = RD / 4, LD = RD + 4, NTG = 2 * RD / 16, NTC = RD / 16, EPT = 64 * RD / GRU_NT;
+  constexpr int UG = (NTG + GRU_NW - 1) / GRU_NW, UC = (2 * NTC + GRU_NW - 1) / GRU_NW;  // units per wave
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* const hL = fsm;            // h(t) rows, permuted k
+  float* const rL = hL + 64 * LD;   // r·h rows
+  float* const P = rL + 64 * LD;    // GG [64][2RD], then the GC halves [2][64][RD]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g4 = lane >> 4, cl = lane & 15;
+  float bg[UG][KS], bc[UC][KS / 2];  // GG unit j: column tile w + 8 j; GC unit j: u = w + 8 j -> tile u % NTC, k half u / NTC
+#pragma unroll
+  for (int j = 0; j < UG; ++j)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bg[j][s] = w + GRU_NW * j < NTG ? Wgh[(4 * s + g4) * 2 * RD + 16 * (w + GRU_NW * j) + cl] : 0.f;
+#pragma unroll
+  for (int j = 0; j < UC; ++j) {
+    const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+#pragma unroll
+    for (int s = 0; s < KS / 2; ++s) bc[j][s] = u < 2 * NTC ? Wch[(4 * (kh * KS / 2 + s) + g4) * RD + 16 * ct + cl] : 0.f;
+  }
+  for (int e = tid; e < 2 * 64 * LD; e += GRU_NT) fsm[e] = 0.f;  // h(0) = 0
+  float uu[EPT];
+  __syncthreads();
+  for (int t = 0; t < T2; ++t) {
+    int tq = tid;
+    asm volatile("" : "+v"(tq));  // per-step element addresses recomputed, not hoisted (and spilled) across the loop
+#pragma unroll
+    for (int j = 0; j < UG; ++j)
+      if (w + GRU_NW * j < NTG) {  // GG = h·Wg_h, column tile w + 8 j
+        f32x4 acc[4] = {};
+        gru_mm<KS>(acc, hL, LD, KS, 0, bg[j], lane);
+        gru_put(acc, P, 2 * RD, 16 * (w + GRU_NW * j), lane);
+      }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {  // [r, u] = σ(XG_g + GG); RH = r·h
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      if (n < N) {
+        const float* xg = XG + ((long)n * T2 + t) * 3 * RD;
+        const float r = fe_sig(xg[d] + P[n * 2 * RD + d]);
+        const float u = fe_sig(xg[RD + d] + P[n * 2 * RD + RD + d]);
+        const long o = ((long)t * N + n) * RD + d;
+        const float rh = r * hL[n * LD + gru_perm(d, RD)];
+        R[o] = r;
+        Uo[o] = u;
+        RHo[o] = rh;
+        rL[n * LD + gru_perm(d, RD)] = rh;
+        uu[i] = u;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < UC; ++j) {
+      const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+      if (u < 2 * NTC) {  // GC = (r·h)·Wc_h, column tile ct, k half kh
+        f32x4 acc[4] = {};
+        gru_mm<KS / 2>(acc, rL, LD, KS, kh * KS / 2, bc[j], lane);
+        gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {  // c = tanh(XG_c + GC); h(t+1) = u·h + (1 - u)·c
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      if (n < N) {
+        const float c = tanhf(XG[((long)n * T2 + t) * 3 * RD + 2 * RD + d] + (P[n * RD + d] + P[64 * RD + n * RD + d]));
+        const long o = ((long)t * N + n) * RD + d;
+        const int hi = n * LD + gru_perm(d, RD);
+        const float hn = uu[i] * hL[hi] + (1.f - uu[i]) * c;
+        CC[o] = c;
+        HG[o + (long)N * RD] = hn;
+        hL[hi] = hn;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int RD>
+__global__ __launch_bounds__(GRU_NT) void k_fe_gru_bwd_seq(const float* __restrict__ Wgh, const float* __restrict__ Wch,
+                                                          const float* __restrict__ R, const float* __restrict__ Uu,
+                                                          const float* __restrict__ CC, const float* __restrict__ HG,
+                                                          int N, int T2, float* __restrict__ dH, float* __restrict__ DCP,
+                                                          float* __restrict__ DGP) {
+  constexpr int KS = RD / 4, L1 = RD + 4, L2 = 2 * RD + 4, NTC = RD / 16, EPT = 64 * RD / GRU_NT;
+  constexpr int UC = (2 * NTC + GRU_NW - 1) / GRU_NW;
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* const AL = fsm;            // d candidate rows [64][L1], then d gate rows [64][L2]
+  float* const P = AL + 64 * L2;    // [2][64][RD] k-half partials
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g4 = lane >> 4, cl = lane & 15;
+  float b1[UC][KS / 2], b2[UC][KS];  // unit u = w + 8 j: Wc_hᵀ and Wg_hᵀ fragments of column tile u % NTC, k half u / NTC
+#pragma unroll
+  for (int j = 0; j < UC; ++j) {
+    const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+    const bool cu = u < 2 * NTC;
+#pragma unroll
+    for (int s = 0; s < KS / 2; ++s) b1[j][s] = cu ? Wch[(16 * ct + cl) * RD + 4 * (kh * KS / 2 + s) + g4] : 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) b2[j][s] = cu ? Wgh[(16 * ct + cl) * 2 * RD + 4 * (kh * KS + s) + g4] : 0.f;
+  }
+  float dh[EPT], dha[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + GRU_NT * i, n = e / RD;
+    dh[i] = n < N ? dH[e] : 0.f;
+  }
+  for (int t = T2 - 1; t >= 0; --t) {
+    int tq = tid;
+    asm volatile("" : "+v"(tq));  // per-step element addresses recomputed, not hoisted (and spilled) across the loop
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {  // DCP = dh (1 - u)(1 - c²); DHA = dh u
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      if (n < N) {
+        const long o = (long)t * N * RD + e;
+        const float u = Uu[o], c = CC[o];
+        const float dcp = dh[i] * (1.f - u) * (1.f - c * c);
+        DCP[o] = dcp;
+        AL[n * L1 + gru_perm(d, RD)] = dcp;
+        dha[i] = dh[i] * u;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < UC; ++j) {
+      const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+      if (u < 2 * NTC) {  // d(r·h) = DCP·Wc_hᵀ
+        f32x4 acc[4] = {};
+        gru_mm<KS / 2>(acc, AL, L1, KS, kh * KS / 2, b1[j], lane);
+        gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {  // DGP = [d(rh)·h·r(1-r), dh (h - c)·u(1-u)]; DHA += d(rh)·r
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      if (n < N) {
+        const long o = (long)t * N * RD + e;
+        const float h = HG[o], r = R[o], u = Uu[o], c = CC[o];
+        const float drh = P[n * RD + d] + P[64 * RD + n * RD + d];
+        const float gr = drh * h * r * (1.f - r), gu = dh[i] * (h - c) * u * (1.f - u);
+        float* dg = DGP + ((long)t * N + n) * 2 * RD;
+        dg[d] = gr;
+        dg[RD + d] = gu;
+        dha[i] += drh * r;
+        AL[n * L2 + gru_perm(d, 2 * RD)] = gr;
+        AL[n * L2 + gru_perm(RD + d, 2 * RD)] = gu;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < UC; ++j) {
+      const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+      if (u < 2 * NTC) {  // d h(t) = DGP·Wg_hᵀ + DHA
+        f32x4 acc[4] = {};
+        gru_mm<KS>(acc, AL, L2, 2 * KS, kh * KS, b2[j], lane);
+        gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      dh[i] = n < N ? (P[n * RD + d] + P[64 * RD + n * RD + d]) + dha[i] : 0.f;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + GRU_NT * i, n = e / RD;
+    if (n < N) dH[e] = dh[i];
+  }
+}
+bool fe_gru_seq_ok(int N, int RD) { return N >= 1 && N <= 64 && (RD == 32 || RD == 128); }
+static size_t fe_gru_lds(int RD, bool bwd) {
+  return sizeof(float) * (bwd ? (size_t)64 * (2 * RD + 4) + 2 * 64 * RD : (size_t)2 * 64 * (RD + 4) + 64 * 2 * RD);
+}
+void fe_gru_fwd_seq(const float* XG, const float* Wgh, const float* Wch, int N, int T2, int RD, float* R, float* Uu,
+                    float* RH, float* CC, float* HG, hipStream_t s) {
+  TT2_CHECK(fe_gru_seq_ok(N, RD), TT2_ERR_SHAPE_MISMATCH, "gru_fwd_seq: batch <= 64, reference_depth 32 or 128");
+  static bool attr = false;
+  if (!attr) {
+    for (const void* k : {reinterpret_cast<const void*>(k_fe_gru_fwd_seq<32>), reinterpret_cast<const void*>(k_fe_gru_fwd_seq<128>),
+                          reinterpret_cast<const void*>(k_fe_gru_bwd_seq<32>), reinterpret_cast<const void*>(k_fe_gru_bwd_seq<128>)})
+      TT2_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  if (RD == 128)
+    hipLaunchKernelGGL(k_fe_gru_fwd_seq<128>, dim3(1), dim3(GRU_NT), fe_gru_lds(128, false), s, XG, Wgh, Wch, N, T2, R, Uu, RH, CC, HG);
+  else
+    hipLaunchKernelGGL(k_fe_gru_fwd_seq<32>, dim3(1), dim3(GRU_NT), fe_gru_lds(32, false), s, XG, Wgh, Wch, N, T2, R, Uu, RH, CC, HG);
+  TT2_HIP(hipGetLastError());
+}
+void fe_gru_bwd_seq(const float* Wgh, const float* Wch, const float* R, const float* Uu, const float* CC, const float* HG,
+                    int N, int T2, int RD, float* dH, float* DCP, float* DGP, hipStream_t s) {
+  TT2_CHECK(fe_gru_seq_ok(N, RD), TT2_ERR_SHAPE_MISMATCH, "gru_bwd_seq: batch <= 64, reference_depth 32 or 128");
+  static bool attr = false;
+  if (!attr) {
+    for (const void* k : {reinterpret_cast<const void*>(k_fe_gru_fwd_seq<32>), reinterpret_cast<const void*>(k_fe_gru_fwd_seq<128>),
+                          reinterpret_cast<const void*>(k_fe_gru_bwd_seq<32>), reinterpret_cast<const void*>(k_fe_gru_bwd_seq<128>)})
+      TT2_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  if (RD == 128)
+    hipLaunchKernelGGL(k_fe_gru_bwd_seq<128>, dim3(1), dim3(GRU_NT), fe_gru_lds(128, true), s, Wgh, Wch, R, Uu, CC, HG, N, T2, dH, DCP, DGP);
+  else
+    hipLaunchKernelGGL(k_fe_gru_bwd_seq<32>, dim3(1), dim3(GRU_NT), fe_gru_lds(32, true), s, Wgh, Wch, R, Uu, CC, HG, N, T2, dH, DCP, DGP);
+  TT2_HIP(hipGetLastError());
+}
+
 void fe_gru_a(const float* XG, const float* GG, const float* HG, int N, int T2, int D, int t, float* R, float* Uu,
               float* RH, hipStream_t s) {
   hipLaunchKernelGGL(k_fe_gru_a, dim3(fe_blk((long)N * D)), dim3(256), 0, s, XG, GG, HG, N, T2, D, t, R, Uu, RH);

@@ -1337,3 +1337,56 @@ def test_gpu_refnet_conv_backward_direct_matches_im2col(precision, tol):
             assert _rel(ga[n], gb[n]) < tol, (n, _rel(ga[n], gb[n]), worst)
         else:
             assert np.abs(ga[n]).max() < 1e-6, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision,tol,ltol", [("fp32", 1e-4, 1e-5), ("bf16", 2e-2, 1e-3)])
+def test_gpu_refnet_gru_sequence_kernels_match_per_step(precision, tol, ltol):
+    """The refnet GRU recurrence in one work-group per direction (k_fe_gru_fwd_seq / k_fe_gru_bwd_seq:
+    recurrent weights register-resident as fp32 MFMA fragments) against the per-step launches
+    (TT2_FE_GRU_SEQ=0: the two recurrent products per step on the GEMM kernels + the cell kernels) at
+    the fork widths (reference_depth 128, T_ref = 400: 7 GRU steps): every gradient
+    of the step relative to its max and the losses.  fp32: both fp32-grade (1e-4 after the
+    recurrence; losses 1e-5); bf16: the per-step products round to bf16, the sequence kernels stay
+    fp32, and the moved style embedding re-rounds the whole bf16 step (losses 1e-3, global gradient
+    norm 2 %, the criteria of the configs[4] fp32-vs-bf16 test)."""
+    import os
+    from tt2.hparams import hparams
+    from tt2.train import TacotronTrainer
+    hp = hparams.copy()
+    hp.override_from_dict(dict(tacotron_num_gpus=1))
+    W, ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm = _front_case(hp, B=4, T_in=12, T_out=6, T_ref=400)
+    names = TRN.frontend_var_names() + TRN.train_var_names() + TRN.postnet_var_names()
+    out = []
+    for seq in ("1", "0"):
+        old = os.environ.get("TT2_FE_GRU_SEQ")
+        os.environ["TT2_FE_GRU_SEQ"] = seq
+        try:
+            tr = TacotronTrainer(hp, W, 4, 12, 6, 0, frontend=True, max_T_ref=400, precision=precision)
+        finally:
+            if old is None:
+                os.environ.pop("TT2_FE_GRU_SEQ", None)
+            else:
+                os.environ["TT2_FE_GRU_SEQ"] = old
+        try:
+            tr.forward_backward_text(ids, lens, re, rs, tg, st, pm, zm, pnm, em, ezm)
+            L = tr.losses()
+            out.append((L, {n: tr.get(n, 1, np.asarray(W[n]).shape) for n in names}))
+        finally:
+            tr.close()
+    (La, ga), (Lb, gb) = out
+    assert abs(La["loss"] - Lb["loss"]) < ltol * abs(Lb["loss"])
+    if precision == "bf16":  # the moved style embedding re-rounds the whole bf16 step: global norm only
+        na = np.sqrt(sum(float((ga[n].astype(np.float64) ** 2).sum()) for n in names))
+        nb = np.sqrt(sum(float((gb[n].astype(np.float64) ** 2).sum()) for n in names))
+        assert abs(na - nb) < tol * nb, (na, nb)
+        return
+    live = [n for n in names if np.abs(gb[n]).max() > 1e-6]
+    worst = max(live, key=lambda n: _rel(ga[n], gb[n]))
+    for n in names:
+        if "gru_cell" in n:
+            assert n in live, n
+        if n in live:
+            assert _rel(ga[n], gb[n]) < tol, (n, _rel(ga[n], gb[n]), worst)
+        else:
+            assert np.abs(ga[n]).max() < 1e-6, n
