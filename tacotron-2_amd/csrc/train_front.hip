@@ -641,6 +641,9 @@ __device__ __forceinline__ void gru_put(const f32x4 (&acc)[4], float* P, int ldp
 // k -> its slot in a permuted A row of K columns (k = 4 s + g at g·K/4 + s)
 __device__ __forceinline__ int gru_perm(int k, int K) { return (k & 3) * (K >> 2) + (k >> 2); }
 
+// LDS-only work-group barrier: every barrier in the recurrences orders LDS data only, while a
+// __syncthreads() would also wait for the step's global stores (R, U, ... read only after the launch)
+__device__ __forceinline__ void gru_lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 constexpr int GRU_NT = 512, GRU_NW = GRU_NT / 64;  // 8 waves: 256 registers per lane for the weight fragments
 template <int RD>
 __global__ __launch_bounds__(GRU_NT) void k_fe_gru_fwd_seq(const float* __restrict__ XG, const float* __restrict__ Wgh,
@@ -679,7 +682,7 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_fwd_seq(const float* __restri
         gru_mm<KS>(acc, hL, LD, KS, 0, bg[j], lane);
         gru_put(acc, P, 2 * RD, 16 * (w + GRU_NW * j), lane);
       }
-    __syncthreads();
+    gru_lds_bar();
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {  // [r, u] = σ(XG_g + GG); RH = r·h
       const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
@@ -696,7 +699,7 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_fwd_seq(const float* __restri
         uu[i] = u;
       }
     }
-    __syncthreads();
+    gru_lds_bar();
 #pragma unroll
     for (int j = 0; j < UC; ++j) {
       const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
@@ -706,7 +709,7 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_fwd_seq(const float* __restri
         gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
       }
     }
-    __syncthreads();
+    gru_lds_bar();
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {  // c = tanh(XG_c + GC); h(t+1) = u·h + (1 - u)·c
       const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
@@ -720,7 +723,7 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_fwd_seq(const float* __restri
         hL[hi] = hn;
       }
     }
-    __syncthreads();
+    gru_lds_bar();
   }
 }
 
@@ -767,7 +770,7 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_bwd_seq(const float* __restri
         dha[i] = dh[i] * u;
       }
     }
-    __syncthreads();
+    gru_lds_bar();
 #pragma unroll
     for (int j = 0; j < UC; ++j) {
       const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
@@ -777,7 +780,7 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_bwd_seq(const float* __restri
         gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
       }
     }
-    __syncthreads();
+    gru_lds_bar();
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {  // DGP = [d(rh)·h·r(1-r), dh (h - c)·u(1-u)]; DHA += d(rh)·r
       const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
@@ -794,7 +797,7 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_bwd_seq(const float* __restri
         AL[n * L2 + gru_perm(RD + d, 2 * RD)] = gu;
       }
     }
-    __syncthreads();
+    gru_lds_bar();
 #pragma unroll
     for (int j = 0; j < UC; ++j) {
       const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
@@ -804,13 +807,13 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_bwd_seq(const float* __restri
         gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
       }
     }
-    __syncthreads();
+    gru_lds_bar();
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
       const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
       dh[i] = n < N ? (P[n * RD + d] + P[64 * RD + n * RD + d]) + dha[i] : 0.f;
     }
-    __syncthreads();
+    gru_lds_bar();
   }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
