@@ -4108,7 +4108,7 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
     TT2_HIP(hipMemsetAsync(c->fHG[r].p, 0, sizeof(float) * (size_t)B * RD, s));
     if (c->fe_gru_seq && fe_gru_seq_ok(B, RD))  // the whole recurrence in one work-group (fp32 MFMA)
       fe_gru_fwd_seq(XG, kg + (long)gin * 2 * RD, kcn + (long)gin * RD, B, T2, RD, c->fGR[r].as<float>(), c->fGU[r].as<float>(),
-                     c->fGRH[r].as<float>(), c->fGCC[r].as<float>(), c->fHG[r].as<float>(), s);
+                     c->fGRH[r].as<float>(), c->fGCC[r].as<float>(), c->fHG[r].as<float>(), s, g_tr_prec == 2);
     for (int t = 0; t < (c->fe_gru_seq && fe_gru_seq_ok(B, RD) ? 0 : T2); ++t) {
       float* h = c->fHG[r].as<float>() + (long)t * B * RD;
       tr_gemm(B, 2 * RD, RD, h, RD, kg + (long)gin * 2 * RD, 2 * RD, c->fGG.as<float>(), 2 * RD, s);
@@ -4387,7 +4387,7 @@ static void tr_front_backward(tt2_train_ctx* c, const int* ids, const int* lens,
     if (gseq) {  // the whole reverse recurrence in one work-group (fp32 MFMA)
       fe_gru_bwd_seq(kg + (long)gin * 2 * RD, kcn + (long)gin * RD, c->fGR[r].as<float>(), c->fGU[r].as<float>(),
                      c->fGCC[r].as<float>(), c->fHG[r].as<float>(), B, T2, RD, c->fDH.as<float>(), c->fDCP.as<float>(),
-                     c->fDGP.as<float>(), s);
+                     c->fDGP.as<float>(), s, g_tr_prec == 2);
     } else {
       tr_transpose(kg + (long)gin * 2 * RD, RD, 2 * RD, 2 * RD, WghT, RD, s);
       tr_transpose(kcn + (long)gin * RD, RD, RD, RD, WchT, RD, s);

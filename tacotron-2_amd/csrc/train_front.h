@@ -73,12 +73,12 @@ void fe_gru_b(const float* XG, const float* GC, const float* Uu, int N, int T2, 
 // the whole recurrence of one reference encoder's GRU in one work-group (N <= 64, RD 32 / 128): the same
 // outputs as the per-step fe_gru_a / fe_gru_b (forward) and fe_gru_bwd_a / b + the two products
 // (backward; dH holds d h(T2) on entry and d h(0) on exit).  Wgh = the gates kernel's h rows [RD][2RD],
-// Wch = the candidate kernel's h rows [RD][RD]
+// Wch = the candidate kernel's h rows [RD][RD]; bf16: bf16 operands (the bf16 step), else fp32 MFMA
 bool fe_gru_seq_ok(int N, int RD);
 void fe_gru_fwd_seq(const float* XG, const float* Wgh, const float* Wch, int N, int T2, int RD, float* R, float* Uu,
-                    float* RH, float* CC, float* HG, hipStream_t s);
+                    float* RH, float* CC, float* HG, hipStream_t s, bool bf16 = false);
 void fe_gru_bwd_seq(const float* Wgh, const float* Wch, const float* R, const float* Uu, const float* CC, const float* HG,
-                    int N, int T2, int RD, float* dH, float* DCP, float* DGP, hipStream_t s);
+                    int N, int T2, int RD, float* dH, float* DCP, float* DGP, hipStream_t s, bool bf16 = false);
 void fe_gru_bwd_a(const float* dH, const float* Uu, const float* CC, const float* HG, int N, int D, int t, float* DCP,
                   float* DHA, hipStream_t s);
 void fe_gru_bwd_b(const float* DRH, const float* R, const float* Uu, const float* HG, const float* CC, const float* dH,

@@ -821,12 +821,252 @@ __global__ __launch_bounds__(GRU_NT) void k_fe_gru_bwd_seq(const float* __restri
     if (n < N) dH[e] = dh[i];
   }
 }
+// bf16-operand forms for the bf16 training step (the per-step GEMMs they replace round A and B to
+// bf16 too): v_mfma_f32_16x16x32_bf16, the A operands as bf16 rows in LDS (k contiguous: a lane's 8
+// k of a k-step are one 16-byte read), B fragments 8 bf16 per lane per 32-deep k-step (half the fp32
+// fragments' registers, which leaves room for the step's XG slice to be loaded before the products)
+typedef __bf16 gru_bf8 __attribute__((ext_vector_type(8)));
+template <int NKS>
+__device__ __forceinline__ void gru_mm_bf(f32x4 (&acc)[4], const __bf16* AL, int ld, int k0, const gru_bf8 (&bf)[NKS],
+                                          int lane) {
+  const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    gru_bf8 a[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) a[mt] = *reinterpret_cast<const gru_bf8*>(AL + (16 * mt + r) * ld + k0 + 32 * ks + 8 * g);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], bf[ks], acc[mt], 0, 0, 0);
+  }
+}
+// B fragment of a row-major fp32 W (row stride ldw): W[k0 + 32 ks + 8 g + e][col], e < 8, as bf16
+__device__ __forceinline__ gru_bf8 gru_bfrag(const float* W, long ldw, int k, int col, bool on) {
+  gru_bf8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (__bf16)(on ? W[(long)(k + e) * ldw + col] : 0.f);
+  return v;
+}
+
+template <int RD>
+__global__ __launch_bounds__(GRU_NT) void k_fe_gru_fwd_seq_bf(const float* __restrict__ XG, const float* __restrict__ Wgh,
+                                                             const float* __restrict__ Wch, int N, int T2,
+                                                             float* __restrict__ R, float* __restrict__ Uo,
+                                                             float* __restrict__ RHo, float* __restrict__ CC,
+                                                             float* __restrict__ HG) {
+  constexpr int NTG = 2 * RD / 16, NTC = RD / 16, EPT = 64 * RD / GRU_NT, LB = RD + 8;
+  constexpr int UG = (NTG + GRU_NW - 1) / GRU_NW, UC = (2 * NTC + GRU_NW - 1) / GRU_NW, KG = RD / 32, KC = RD / 64;
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* const h32 = fsm;                                           // h(t) [64][RD] fp32 (the state)
+  __bf16* const hB = reinterpret_cast<__bf16*>(h32 + 64 * RD);      // bf16(h) rows [64][LB]
+  __bf16* const rB = hB + 64 * LB;                                  // bf16(r·h) rows
+  float* const P = reinterpret_cast<float*>(rB + 64 * LB);          // GG [64][2RD], then GC halves [2][64][RD]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g4 = lane >> 4, cl = lane & 15;
+  gru_bf8 bg[UG][KG], bc[UC][KC];
+#pragma unroll
+  for (int j = 0; j < UG; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KG; ++ks)
+      bg[j][ks] = gru_bfrag(Wgh, 2 * RD, 32 * ks + 8 * g4, 16 * (w + GRU_NW * j) + cl, w + GRU_NW * j < NTG);
+#pragma unroll
+  for (int j = 0; j < UC; ++j) {
+    const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+#pragma unroll
+    for (int ks = 0; ks < KC; ++ks) bc[j][ks] = gru_bfrag(Wch, RD, kh * RD / 2 + 32 * ks + 8 * g4, 16 * ct + cl, u < 2 * NTC);
+  }
+  for (int e = tid; e < 64 * RD + 64 * LB; e += GRU_NT) fsm[e] = 0.f;  // h(0) = 0 (fp32 and the bf16 rows)
+  float uu[EPT];
+  __syncthreads();
+  for (int t = 0; t < T2; ++t) {
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    float xr[EPT];  // this step's r-gate inputs, loaded ahead of the products
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      xr[i] = XG[((long)(n < N ? n : 0) * T2 + t) * 3 * RD + d];
+    }
+#pragma unroll
+    for (int j = 0; j < UG; ++j)
+      if (w + GRU_NW * j < NTG) {
+        f32x4 acc[4] = {};
+        gru_mm_bf<KG>(acc, hB, LB, 0, bg[j], lane);
+        gru_put(acc, P, 2 * RD, 16 * (w + GRU_NW * j), lane);
+      }
+    gru_lds_bar();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      if (n < N) {
+        const float r = fe_sig(xr[i] + P[n * 2 * RD + d]);
+        const float u = fe_sig(XG[((long)n * T2 + t) * 3 * RD + RD + d] + P[n * 2 * RD + RD + d]);
+        const long o = ((long)t * N + n) * RD + d;
+        const float rh = r * h32[n * RD + d];
+        R[o] = r;
+        Uo[o] = u;
+        RHo[o] = rh;
+        rB[n * LB + d] = (__bf16)rh;
+        uu[i] = u;
+      }
+    }
+    gru_lds_bar();
+#pragma unroll
+    for (int j = 0; j < UC; ++j) {
+      const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+      if (u < 2 * NTC) {
+        f32x4 acc[4] = {};
+        gru_mm_bf<KC>(acc, rB, LB, kh * RD / 2, bc[j], lane);
+        gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
+      }
+    }
+    gru_lds_bar();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      if (n < N) {
+        const float c = tanhf(XG[((long)n * T2 + t) * 3 * RD + 2 * RD + d] + (P[n * RD + d] + P[64 * RD + n * RD + d]));
+        const long o = ((long)t * N + n) * RD + d;
+        const float hn = uu[i] * h32[n * RD + d] + (1.f - uu[i]) * c;
+        CC[o] = c;
+        HG[o + (long)N * RD] = hn;
+        h32[n * RD + d] = hn;
+        hB[n * LB + d] = (__bf16)hn;
+      }
+    }
+    gru_lds_bar();
+  }
+}
+
+template <int RD>
+__global__ __launch_bounds__(GRU_NT) void k_fe_gru_bwd_seq_bf(const float* __restrict__ Wgh, const float* __restrict__ Wch,
+                                                             const float* __restrict__ R, const float* __restrict__ Uu,
+                                                             const float* __restrict__ CC, const float* __restrict__ HG,
+                                                             int N, int T2, float* __restrict__ dH,
+                                                             float* __restrict__ DCP, float* __restrict__ DGP) {
+  constexpr int NTC = RD / 16, EPT = 64 * RD / GRU_NT, L1 = RD + 8, L2 = 2 * RD + 8;
+  constexpr int UC = (2 * NTC + GRU_NW - 1) / GRU_NW, K1 = RD / 64, K2 = RD / 32;
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  __bf16* const AB = reinterpret_cast<__bf16*>(fsm);                // bf16 d candidate rows [64][L1], then d gate rows [64][L2]
+  float* const P = fsm + 64 * L2 / 2;                               // [2][64][RD] k-half partials
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g4 = lane >> 4, cl = lane & 15;
+  gru_bf8 b1[UC][K1], b2[UC][K2];  // unit u: Wc_hᵀ / Wg_hᵀ fragments of column tile u % NTC, k half u / NTC
+#pragma unroll
+  for (int j = 0; j < UC; ++j) {
+    const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+    const bool on = u < 2 * NTC;
+#pragma unroll
+    for (int ks = 0; ks < K1; ++ks) {  // Wc_hᵀ[k][col] = Wc_h[col][k]: k contiguous in the source row
+      gru_bf8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (__bf16)(on ? Wch[(long)(16 * ct + cl) * RD + kh * RD / 2 + 32 * ks + 8 * g4 + e] : 0.f);
+      b1[j][ks] = v;
+    }
+#pragma unroll
+    for (int ks = 0; ks < K2; ++ks) {
+      gru_bf8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (__bf16)(on ? Wgh[(long)(16 * ct + cl) * 2 * RD + kh * RD + 32 * ks + 8 * g4 + e] : 0.f);
+      b2[j][ks] = v;
+    }
+  }
+  float dh[EPT], dha[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + GRU_NT * i, n = e / RD;
+    dh[i] = n < N ? dH[e] : 0.f;
+  }
+  for (int t = T2 - 1; t >= 0; --t) {
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      if (n < N) {
+        const long o = (long)t * N * RD + e;
+        const float u = Uu[o], c = CC[o];
+        const float dcp = dh[i] * (1.f - u) * (1.f - c * c);
+        DCP[o] = dcp;
+        AB[n * L1 + d] = (__bf16)dcp;
+        dha[i] = dh[i] * u;
+      }
+    }
+    gru_lds_bar();
+#pragma unroll
+    for (int j = 0; j < UC; ++j) {
+      const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+      if (u < 2 * NTC) {
+        f32x4 acc[4] = {};
+        gru_mm_bf<K1>(acc, AB, L1, kh * RD / 2, b1[j], lane);
+        gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
+      }
+    }
+    gru_lds_bar();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      if (n < N) {
+        const long o = (long)t * N * RD + e;
+        const float h = HG[o], r = R[o], u = Uu[o], c = CC[o];
+        const float drh = P[n * RD + d] + P[64 * RD + n * RD + d];
+        const float gr = drh * h * r * (1.f - r), gu = dh[i] * (h - c) * u * (1.f - u);
+        float* dg = DGP + ((long)t * N + n) * 2 * RD;
+        dg[d] = gr;
+        dg[RD + d] = gu;
+        dha[i] += drh * r;
+        AB[n * L2 + d] = (__bf16)gr;
+        AB[n * L2 + RD + d] = (__bf16)gu;
+      }
+    }
+    gru_lds_bar();
+#pragma unroll
+    for (int j = 0; j < UC; ++j) {
+      const int u = w + GRU_NW * j, ct = u % NTC, kh = u / NTC;
+      if (u < 2 * NTC) {
+        f32x4 acc[4] = {};
+        gru_mm_bf<K2>(acc, AB, L2, kh * RD, b2[j], lane);
+        gru_put(acc, P + kh * 64 * RD, RD, 16 * ct, lane);
+      }
+    }
+    gru_lds_bar();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tq + GRU_NT * i, n = e / RD, d = e % RD;
+      dh[i] = n < N ? (P[n * RD + d] + P[64 * RD + n * RD + d]) + dha[i] : 0.f;
+    }
+    gru_lds_bar();
+  }
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + GRU_NT * i, n = e / RD;
+    if (n < N) dH[e] = dh[i];
+  }
+}
+
 bool fe_gru_seq_ok(int N, int RD) { return N >= 1 && N <= 64 && (RD == 32 || RD == 128); }
 static size_t fe_gru_lds(int RD, bool bwd) {
   return sizeof(float) * (bwd ? (size_t)64 * (2 * RD + 4) + 2 * 64 * RD : (size_t)2 * 64 * (RD + 4) + 64 * 2 * RD);
 }
+static size_t fe_gru_lds_bf(int RD, bool bwd) {
+  return bwd ? (size_t)64 * (2 * RD + 8) * 2 + sizeof(float) * 2 * 64 * RD
+             : sizeof(float) * (size_t)64 * RD + (size_t)2 * 64 * (RD + 8) * 2 + sizeof(float) * 64 * 2 * RD;
+}
+static void fe_gru_attrs() {
+  static bool attr = false;
+  if (attr) return;
+  for (const void* k : {reinterpret_cast<const void*>(k_fe_gru_fwd_seq<32>), reinterpret_cast<const void*>(k_fe_gru_fwd_seq<128>),
+                        reinterpret_cast<const void*>(k_fe_gru_bwd_seq<32>), reinterpret_cast<const void*>(k_fe_gru_bwd_seq<128>),
+                        reinterpret_cast<const void*>(k_fe_gru_fwd_seq_bf<128>), reinterpret_cast<const void*>(k_fe_gru_bwd_seq_bf<128>)})
+    TT2_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  attr = true;
+}
 void fe_gru_fwd_seq(const float* XG, const float* Wgh, const float* Wch, int N, int T2, int RD, float* R, float* Uu,
-                    float* RH, float* CC, float* HG, hipStream_t s) {
+                    float* RH, float* CC, float* HG, hipStream_t s, bool bf16) {
+  if (bf16 && RD == 128) {  // (a 32-deep bf16 k-step is deeper than RD = 32's k halves: fp32 form there)
+    TT2_CHECK(fe_gru_seq_ok(N, RD), TT2_ERR_SHAPE_MISMATCH, "gru_fwd_seq: batch <= 64");
+    fe_gru_attrs();
+    hipLaunchKernelGGL(k_fe_gru_fwd_seq_bf<128>, dim3(1), dim3(GRU_NT), fe_gru_lds_bf(128, false), s, XG, Wgh, Wch, N, T2, R, Uu, RH, CC, HG);
+    TT2_HIP(hipGetLastError());
+    return;
+  }
   TT2_CHECK(fe_gru_seq_ok(N, RD), TT2_ERR_SHAPE_MISMATCH, "gru_fwd_seq: batch <= 64, reference_depth 32 or 128");
   static bool attr = false;
   if (!attr) {
@@ -842,7 +1082,14 @@ void fe_gru_fwd_seq(const float* XG, const float* Wgh, const float* Wch, int N, 
   TT2_HIP(hipGetLastError());
 }
 void fe_gru_bwd_seq(const float* Wgh, const float* Wch, const float* R, const float* Uu, const float* CC, const float* HG,
-                    int N, int T2, int RD, float* dH, float* DCP, float* DGP, hipStream_t s) {
+                    int N, int T2, int RD, float* dH, float* DCP, float* DGP, hipStream_t s, bool bf16) {
+  if (bf16 && RD == 128) {
+    TT2_CHECK(fe_gru_seq_ok(N, RD), TT2_ERR_SHAPE_MISMATCH, "gru_bwd_seq: batch <= 64");
+    fe_gru_attrs();
+    hipLaunchKernelGGL(k_fe_gru_bwd_seq_bf<128>, dim3(1), dim3(GRU_NT), fe_gru_lds_bf(128, true), s, Wgh, Wch, R, Uu, CC, HG, N, T2, dH, DCP, DGP);
+    TT2_HIP(hipGetLastError());
+    return;
+  }
   TT2_CHECK(fe_gru_seq_ok(N, RD), TT2_ERR_SHAPE_MISMATCH, "gru_bwd_seq: batch <= 64, reference_depth 32 or 128");
   static bool attr = false;
   if (!attr) {
