@@ -4072,13 +4072,20 @@ static void tr_front_forward(tt2_train_ctx* c, const int* ids, const int* lens, 
       g.pt = std::max((Ho - 1) * st + 3 - H, 0) / 2; g.pl = std::max((Wo - 1) * st + 3 - W, 0) / 2;
       g.Bw = pvar(c, sc + fe_ref_conv(c, r) + "kernel"); g.ldb = fo; g.ldc = fo;
       g.bias = pvar(c, sc + fe_ref_conv(c, r) + "bias");
+      const bool small = c->fe_direct && fe_conv2d_fwd_small_ok(ci, fo);  // first layer: direct kernel
       if (c->f_adain) {  // conv2d(..., batch_norm=False): conv + ReLU (modules.py:84-87)
         g.Cout = c->fRY[r][i].as<float>();
         g.act = ACT_RELU;
-        tr_gemm_run(g, s);
+        if (small)
+          fe_conv2d_fwd_small(x, g.Bw, g.bias, B, H, W, ci, Ho, Wo, fo, g.pt, g.pl, st, true, g.Cout, s, g_tr_prec == 2);
+        else
+          tr_gemm_run(g, s);
       } else {
         g.Cout = c->fRA[r][i].as<float>();
-        tr_gemm_run(g, s);
+        if (small)
+          fe_conv2d_fwd_small(x, g.Bw, g.bias, B, H, W, ci, Ho, Wo, fo, g.pt, g.pl, st, false, g.Cout, s, g_tr_prec == 2);
+        else
+          tr_gemm_run(g, s);
         float* mean = BN + (long)nbn * 2 * 512;
         float* var = mean + 512;
         fe_stats(c, c->fRA[r][i].as<float>(), g.M, fo, mean, var, s);

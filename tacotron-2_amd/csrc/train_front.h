@@ -48,6 +48,11 @@ void fe_col2im2d(const float* dcols, int N, int H, int W, int C, int Ho, int Wo,
 // the same conv2d's backward without a materialised im2col (fp32 FMA): the kernel gradient as
 // partial rows [rows][9·C·F] into part (returns rows; the caller sums them), the input gradient as a
 // gather over the taps.  *_ok: the channel counts these kernels take (LDS / register budgets)
+// forward of the same conv2d for C <= 4 input channels (the refnets' first layer): + bias, optional ReLU;
+// bf16: operands rounded to bf16 as the bf16 step's GEMM form rounds them
+bool fe_conv2d_fwd_small_ok(int C, int F);
+void fe_conv2d_fwd_small(const float* x, const float* Wk, const float* bias, int N, int H, int W, int C, int Ho, int Wo,
+                         int F, int pt, int pl, int st, bool relu, float* out, hipStream_t s, bool bf16);
 bool fe_conv2d_dw_ok(int C, int F);
 int fe_conv2d_dw(const float* x, const float* dz, int N, int H, int W, int C, int Ho, int Wo, int F, int pt, int pl,
                  int st, float* part, long part_floats, hipStream_t s);

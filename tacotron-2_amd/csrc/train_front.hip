@@ -365,6 +365,55 @@ int fe_conv2d_dw(const float* x, const float* dz, int N, int H, int W, int C, in
   return (int)(nblk * G);  // partial rows of [9CF]
 }
 
+// forward of a 3x3 conv2d with few input channels (the refnets' first layer reads the 1-channel mel):
+// out[m][f] = bias[f] + Σ_{tap, c} x(patch of m)[tap][c] · Wk[tap][c][f] (+ ReLU), fp32 products and
+// sums.  Thread = (output position, 4 columns); the kernel and bias staged in LDS.  bf: operands
+// rounded to bf16 first, as the bf16 step's GEMM form rounds them.  The implicit-GEMM form padded K = 9
+// to its 32-deep tile and used 32 of its 128 columns (184 us per refnet at configs[4])
+__global__ __launch_bounds__(256) void k_fe_conv2d_fwd_small(const float* __restrict__ x, const float* __restrict__ Wk,
+                                                             const float* __restrict__ bias, int N, int H, int W, int C,
+                                                             int Ho, int Wo, int F, int pt, int pl, int st, int relu,
+                                                             int bf, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  for (int e = threadIdx.x; e < 9 * C * F; e += 256) fsm[e] = bf ? (float)(__bf16)Wk[e] : Wk[e];
+  for (int e = threadIdx.x; e < F; e += 256) fsm[9 * C * F + e] = bias[e];
+  __syncthreads();
+  const int FQ = F / 4;
+  const long total = (long)N * Ho * Wo * FQ;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int fq = (int)(i % FQ);
+    const long m = i / FQ;
+    const int wo = (int)(m % Wo), r = (int)(m / Wo), ho = r % Ho, n = r / Ho;
+    f32x4 acc = *reinterpret_cast<const f32x4*>(fsm + 9 * C * F + 4 * fq);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int h = st * ho + ky - pt;
+      if (h < 0 || h >= H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int w = st * wo + kx - pl;
+        if (w < 0 || w >= W) continue;
+        const float* xp = x + ((long)(n * H + h) * W + w) * C;
+        const float* wp = fsm + (ky * 3 + kx) * C * F + 4 * fq;
+        for (int c = 0; c < C; ++c) acc += (bf ? (float)(__bf16)xp[c] : xp[c]) * *reinterpret_cast<const f32x4*>(wp + c * F);
+      }
+    }
+    if (relu)
+      for (int u = 0; u < 4; ++u) acc[u] = fmaxf(acc[u], 0.f);
+    *reinterpret_cast<f32x4*>(out + m * F + 4 * fq) = acc;
+  }
+}
+bool fe_conv2d_fwd_small_ok(int C, int F) { return C >= 1 && C <= 4 && F % 4 == 0 && 9 * C * F + F <= 8192; }
+void fe_conv2d_fwd_small(const float* x, const float* Wk, const float* bias, int N, int H, int W, int C, int Ho, int Wo,
+                         int F, int pt, int pl, int st, bool relu, float* out, hipStream_t s, bool bf16) {
+  TT2_CHECK(fe_conv2d_fwd_small_ok(C, F), TT2_ERR_SHAPE_MISMATCH, "conv2d_fwd_small: unsupported channel counts");
+  const long total = (long)N * Ho * Wo * (F / 4);
+  const unsigned nb = (unsigned)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_fe_conv2d_fwd_small, dim3(nb), dim3(256), sizeof(float) * (size_t)(9 * C * F + F), s, x, Wk, bias,
+                     N, H, W, C, Ho, Wo, F, pt, pl, st, relu ? 1 : 0, bf16 ? 1 : 0, out);
+  TT2_HIP(hipGetLastError());
+}
+
 // d input of the same conv2d as a gather: dx[n][h][w][c] = Σ_{taps reading (h, w)} Σ_f dz[n][ho][wo][f] ·
 // Wk[tap][c][f] (Wk the HWIO kernel [3][3][C][F]).  Work-group = DXR consecutive rows h of one image:
 // the kernel (as [tap][f][C]) and the dz rows those rows read are staged in LDS once; thread item =

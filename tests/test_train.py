@@ -1292,15 +1292,17 @@ def test_gpu_train_persistent_backward_close_to_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 1e-2)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 2e-2)])
 def test_gpu_refnet_conv_backward_direct_matches_im2col(precision, tol):
     """The refnet conv2d backward without a materialised im2col (k_fe_conv2d_dw: LDS-staged patches,
     fp32 FMA, partial rows summed; k_fe_conv2d_dx: the input gradient as a gather over the taps)
     against the im2colᵀ + GEMM + col2im form (TT2_FE_CONV_DIRECT=0) at the fork widths (filters
     32, 32, 64, 64, 128, 128: the direct kernels take layers 0-3 / 1-2, the rest stay on the GEMM
-    form) with T_ref = 96 (odd pads on the way down): every gradient of the step, relative to its
-    max.  fp32: both forms are fp32-grade, so they agree to 2e-5; bf16: the GEMM form rounds its
-    operands to bf16 (1e-2; the direct kernels stay fp32 in both modes)."""
+    form) with T_ref = 96 (odd pads on the way down), and the first layer's forward conv
+    (k_fe_conv2d_fwd_small) against the implicit GEMM.  fp32: both forms are fp32-grade (the
+    forward's fp32 FMA against split fp16x3 moves every later gradient by ~2e-5): every gradient
+    within 1e-4 of its max; bf16: the moved forward re-rounds the whole bf16 step, so losses within
+    1e-5 and the global gradient norm within 2 % (the criteria of the configs[4] fp32-vs-bf16 test)."""
     import os
     from tt2.hparams import hparams
     from tt2.train import TacotronTrainer
@@ -1326,7 +1328,12 @@ def test_gpu_refnet_conv_backward_direct_matches_im2col(precision, tol):
         finally:
             tr.close()
     (La, ga), (Lb, gb) = out
-    assert abs(La["loss"] - Lb["loss"]) < 1e-6 * abs(Lb["loss"])
+    assert abs(La["loss"] - Lb["loss"]) < 1e-5 * abs(Lb["loss"])
+    if precision == "bf16":
+        na = np.sqrt(sum(float((ga[n].astype(np.float64) ** 2).sum()) for n in names))
+        nb = np.sqrt(sum(float((gb[n].astype(np.float64) ** 2).sum()) for n in names))
+        assert abs(na - nb) < tol * nb, (na, nb)
+        return
     # (a conv bias ahead of batch norm has a zero gradient: rounding noise of ~1e-9 both ways)
     live = [n for n in names if np.abs(gb[n]).max() > 1e-6]
     worst = max(live, key=lambda n: _rel(ga[n], gb[n]))
