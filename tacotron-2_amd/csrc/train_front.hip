@@ -379,11 +379,10 @@ __global__ __launch_bounds__(256) void k_fe_conv2d_fwd_small(const float* __rest
   for (int e = threadIdx.x; e < F; e += 256) fsm[9 * C * F + e] = bias[e];
   __syncthreads();
   const int FQ = F / 4;
-  const long total = (long)N * Ho * Wo * FQ;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int fq = (int)(i % FQ);
-    const long m = i / FQ;
-    const int wo = (int)(m % Wo), r = (int)(m / Wo), ho = r % Ho, n = r / Ho;
+  const int total = N * Ho * Wo * FQ;  // < 2^31 (host check): 32-bit index arithmetic
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int fq = i % FQ, m = i / FQ;
+    const int wo = m % Wo, r = m / Wo, ho = r % Ho, n = r / Ho;
     f32x4 acc = *reinterpret_cast<const f32x4*>(fsm + 9 * C * F + 4 * fq);
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
@@ -400,7 +399,7 @@ __global__ __launch_bounds__(256) void k_fe_conv2d_fwd_small(const float* __rest
     }
     if (relu)
       for (int u = 0; u < 4; ++u) acc[u] = fmaxf(acc[u], 0.f);
-    *reinterpret_cast<f32x4*>(out + m * F + 4 * fq) = acc;
+    *reinterpret_cast<f32x4*>(out + (long)m * F + 4 * fq) = acc;
   }
 }
 bool fe_conv2d_fwd_small_ok(int C, int F) { return C >= 1 && C <= 4 && F % 4 == 0 && 9 * C * F + F <= 8192; }
@@ -408,6 +407,8 @@ void fe_conv2d_fwd_small(const float* x, const float* Wk, const float* bias, int
                          int F, int pt, int pl, int st, bool relu, float* out, hipStream_t s, bool bf16) {
   TT2_CHECK(fe_conv2d_fwd_small_ok(C, F), TT2_ERR_SHAPE_MISMATCH, "conv2d_fwd_small: unsupported channel counts");
   const long total = (long)N * Ho * Wo * (F / 4);
+  TT2_CHECK(total < (1L << 31) && (long)N * H * W * C < (1L << 31), TT2_ERR_SHAPE_MISMATCH,
+            "conv2d_fwd_small: shape exceeds 32 bits");
   const unsigned nb = (unsigned)std::min<long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(k_fe_conv2d_fwd_small, dim3(nb), dim3(256), sizeof(float) * (size_t)(9 * C * F + F), s, x, Wk, bias,
                      N, H, W, C, Ho, Wo, F, pt, pl, st, relu ? 1 : 0, bf16 ? 1 : 0, out);
