@@ -2206,16 +2206,35 @@ __global__ __launch_bounds__(512) void k_tr_dval(const float* __restrict__ align
   f32x4 acc[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int t0 = 0; t0 < T; t0 += DV_TC) {
-    for (int e = tid; e < DV_JT * DV_TC; e += 512) {  // coalesced over t
-      const int j = e / DV_TC, tt = e - j * DV_TC;
-      As[j][tt] = (j0 + j < Tin && t0 + tt < T) ? ab[(long)(j0 + j) * T + t0 + tt] : 0.f;
+  // the next chunk's operands are loaded into registers while the current chunk's products run
+  constexpr int NA = DV_JT * DV_TC / 512, NB = DV_TC * 128 / 512;
+  float pa[NA], pb[NB];
+  auto load = [&](int t0) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {  // coalesced over t
+      const int e = tid + 512 * u, j = e / DV_TC, tt = e - j * DV_TC;
+      pa[u] = (j0 + j < Tin && t0 + tt < T) ? ab[(long)(j0 + j) * T + t0 + tt] : 0.f;
     }
-    for (int e = tid; e < DV_TC * 128; e += 512) {  // coalesced over d
-      const int tt = e >> 7, dd = e & 127;
-      Bs[tt][dd] = (t0 + tt < T && d0 + dd < D) ? dctx[((long)(t0 + tt) * B + b) * D + d0 + dd] : 0.f;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {  // coalesced over d
+      const int e = tid + 512 * u, tt = e >> 7, dd = e & 127;
+      pb[u] = (t0 + tt < T && d0 + dd < D) ? dctx[((long)(t0 + tt) * B + b) * D + d0 + dd] : 0.f;
+    }
+  };
+  load(0);
+  for (int t0 = 0; t0 < T; t0 += DV_TC) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int e = tid + 512 * u, j = e / DV_TC;
+      As[j][e - j * DV_TC] = pa[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int e = tid + 512 * u;
+      Bs[e >> 7][e & 127] = pb[u];
     }
     __syncthreads();
+    if (t0 + DV_TC < T) load(t0 + DV_TC);
 #pragma unroll
     for (int ks = 0; ks < DV_TC / 4; ++ks) {
       const float bv = Bs[4 * ks + g4][16 * w + r16];
